@@ -1,0 +1,319 @@
+#!/usr/bin/env python3
+"""Headline benchmark: counter samples/s per GPU, p50 /metrics scrape latency and
+GPU-time overhead %, under synthetic gfx950 load (BASELINE.json "metric").
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One rank per GPU.  A *step* is one fixed block of synthetic load on every GPU
+(an MFMA-bound bf16 kernel + HBM triads, ops/hip/load_kernels.hip).  Phases:
+
+  A  K steps, no exporter running                       (baseline, untimed for the result line)
+  B  K steps with the node exporter sampling every used GPU at --hz (PMFW table,
+     HBM, per-process list, xGMI, and hardware counters through rocprofiler-sdk)
+     while rank 0 scrapes /metrics at --scrape-hz      (THE timed region)
+  C  K steps, exporter stopped again                    (second baseline)
+
+``value`` = counter samples/s summed over the N GPUs (weak scaling: per-GPU work
+and sampling rate are fixed).  A counter sample is one hardware-counter drain
+(GRBM/SQ/TCC values advance on every drain) when rocprofiler-sdk counting is
+available, else one distinct PMFW table (new firmware timestamp).  Overhead % =
+100 · (t_B / mean(t_A, t_C) − 1), same device, same process.
+
+The exporter runs as its own process (as in production: DaemonSet vs workload),
+launched by local rank 0 over the PCI addresses of every local rank's GPU.
+``--mock`` runs the same flow on CPU with the mock provider (tests only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import select
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from kube_gpu_stats_amd.parallel import dist as D  # noqa: E402
+from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text  # noqa: E402
+
+METRIC = "counter samples/sec/GPU + p50 scrape latency at 8×MI355X; GPU-time overhead %"
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--hz", type=float, default=100.0, help="sampler rate per GPU")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "rocprofiler", "none"])
+    ap.add_argument("--scrape-hz", type=float, default=10.0)
+    ap.add_argument("--mfma-iters", type=int, default=60000)
+    ap.add_argument("--mfma-blocks", type=int, default=2048)
+    ap.add_argument("--stream-gib", type=float, default=6.0)
+    ap.add_argument("--triads", type=int, default=2)
+    ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
+    ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
+    ap.add_argument("--mock-step-ms", type=float, default=20.0)
+    ap.add_argument("--out", default="", help="also write the result JSON here")
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------- load
+class GpuLoad:
+    def __init__(self, a, device: int):
+        import torch
+
+        from kube_gpu_stats_amd.ops.load import LoadStep
+
+        self.torch = torch
+        self.ls = LoadStep(device=device, mfma_blocks=a.mfma_blocks, mfma_iters=a.mfma_iters,
+                           stream_bytes=int(a.stream_gib * (1 << 30)))
+        self.triads = a.triads
+
+    def step(self):
+        self.ls.run_mfma()
+        for _ in range(self.triads):
+            self.ls.run_stream()
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def calibrate(self) -> dict:
+        """Per-kernel throughput (events), outside every timed region."""
+        torch = self.torch
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        e[0].record()
+        self.ls.run_mfma()
+        e[1].record()
+        self.ls.run_stream()
+        e[2].record()
+        torch.cuda.synchronize()
+        mfma_s = e[0].elapsed_time(e[1]) * 1e-3
+        tri_s = e[1].elapsed_time(e[2]) * 1e-3
+        return {"mfma_ms": mfma_s * 1e3, "mfma_tflops": self.ls.flops / mfma_s / 1e12,
+                "triad_ms": tri_s * 1e3, "triad_tbps": self.ls.bytes / tri_s / 1e12}
+
+    def pci_bdf(self, device: int) -> str:
+        p = self.torch.cuda.get_device_properties(device)
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+
+class MockLoad:
+    def __init__(self, a, device: int):
+        self.dt = a.mock_step_ms * 1e-3
+
+    def step(self):
+        time.sleep(self.dt)  # releases the GIL like a GPU sync would
+
+    def sync(self):
+        pass
+
+    def calibrate(self) -> dict:
+        return {"mock_step_ms": self.dt * 1e3}
+
+    def pci_bdf(self, device: int) -> str:
+        return f"0000:{0x11 + 0x10 * device:02x}:00.0"  # mock provider's BDF scheme
+
+
+def timed(ctx, load, k: int) -> float:
+    """Barrier + sync on both sides; returns the MAX over ranks of the wall time."""
+    D.barrier(ctx)
+    load.sync()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        load.step()
+    load.sync()
+    D.barrier(ctx)
+    dt = time.perf_counter() - t0
+    return D.all_reduce(ctx, [dt], "max")[0]
+
+
+# ----------------------------------------------------------------------------- exporter
+class ExporterProc:
+    def __init__(self, a, bdfs: list[str], log_path: str):
+        cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
+               "--hz", str(a.hz), "--proc-every", str(max(1, int(a.hz // 10))),
+               "--link-every", str(max(1, int(a.hz))), "--control-stdin", "--node-name", "bench-node",
+               "--bdfs", ",".join(bdfs)]
+        if a.mock:
+            cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock"]
+        else:
+            cmd += ["--pmc", "rocprofiler" if a.pmc in ("auto", "rocprofiler") else "none"]
+        env = dict(os.environ)
+        env.setdefault("KGS_NO_BUILD", "1")
+        self.log = open(log_path, "w")
+        self.p = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.log,
+                                  text=True, env=env)
+        self.ready = self._wait_ready(120.0)
+        self.port = int(self.ready["port"])
+
+    def _wait_ready(self, timeout: float) -> dict:
+        end = time.time() + timeout
+        while time.time() < end:
+            r, _, _ = select.select([self.p.stdout], [], [], 1.0)
+            if r:
+                line = self.p.stdout.readline()
+                if not line:
+                    break
+                try:
+                    msg = json.loads(line)
+                except ValueError:
+                    continue
+                if msg.get("event") == "ready":
+                    return msg
+                if msg.get("event") == "error":
+                    raise RuntimeError("exporter failed: " + msg.get("error", ""))
+            if self.p.poll() is not None:
+                break
+        raise RuntimeError(f"exporter did not become ready (rc={self.p.poll()}); see {self.log.name}")
+
+    def stop(self) -> dict:
+        try:
+            self.p.stdin.write("quit\n")
+            self.p.stdin.flush()
+        except OSError:
+            pass
+        try:
+            out, _ = self.p.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            self.p.kill()
+            out, _ = self.p.communicate()
+        self.log.close()
+        for line in out.splitlines():
+            try:
+                msg = json.loads(line)
+                if msg.get("event") == "stopped":
+                    return msg
+            except ValueError:
+                pass
+        return {}
+
+
+def sample_counts(m: dict) -> tuple[dict, dict]:
+    pmfw = {lb["gpu"]: v for lb, v in m.get("kgs_samples_total", [])}
+    pmc = {lb["gpu"]: v for lb, v in m.get("kgs_pmc_samples_total", [])}
+    return pmfw, pmc
+
+
+# ----------------------------------------------------------------------------- main
+def main(argv=None) -> int:
+    a = parse_args(argv)
+    use_cuda = not a.mock
+    ctx = D.init_from_env(use_cuda)
+    if ctx.world != a.gpus:
+        if ctx.rank == 0:
+            print(f"warning: --gpus {a.gpus} but WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
+    n = ctx.world
+    load = (MockLoad if a.mock else GpuLoad)(a, ctx.local_rank)
+
+    for _ in range(a.warmup):
+        load.step()
+    load.sync()
+    calib = load.calibrate()
+
+    # phase A: no exporter
+    t_a = timed(ctx, load, a.steps)
+
+    # start the node exporter over every local rank's GPU
+    bdfs = D.all_gather_object(ctx, (ctx.local_rank, load.pci_bdf(ctx.local_rank)))
+    bdfs = [b for _, b in sorted(set(bdfs))]
+    exp = None
+    err = ""
+    if ctx.local_rank == 0:
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        try:
+            exp = ExporterProc(a, bdfs, os.path.join(REPO, "gpurun_out", f"bench_exporter_r{ctx.rank}.log"))
+        except Exception as e:  # noqa: BLE001
+            err = str(e)
+    err = D.broadcast_object(ctx, err)
+    if err:
+        if ctx.rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "error": err}))
+        D.destroy(ctx)
+        return 1
+    time.sleep(a.settle)
+
+    scraper = None
+    before = after = {}
+    t_w0 = t_w1 = 0.0
+    if exp is not None:
+        scraper = Scraper("127.0.0.1", exp.port)
+        before = parse_text(scraper.get())
+        t_w0 = time.perf_counter()
+        scraper.start(a.scrape_hz)
+    # phase B: exporter on (timed)
+    t_b = timed(ctx, load, a.steps)
+    if exp is not None:
+        scraper.stop()
+        after = parse_text(scraper.get())
+        t_w1 = time.perf_counter()
+    stopped = exp.stop() if exp is not None else {}
+
+    # phase C: exporter off again
+    t_c = timed(ctx, load, a.steps)
+
+    result = None
+    if exp is not None:
+        b_pmfw, b_pmc = sample_counts(before)
+        a_pmfw, a_pmc = sample_counts(after)
+        win = t_w1 - t_w0
+        gpus = sorted(a_pmfw, key=int)
+        pmfw_rate = {g: (a_pmfw[g] - b_pmfw.get(g, 0)) / win for g in gpus}
+        pmc_rate = {g: (a_pmc.get(g, 0) - b_pmc.get(g, 0)) / win for g in gpus}
+        pmc_on = exp.ready.get("pmc", "none") != "none" and sum(pmc_rate.values()) > 0
+        per_gpu = pmc_rate if pmc_on else pmfw_rate
+        total = sum(per_gpu.values())
+        t_off = 0.5 * (t_a + t_c)
+        result = {
+            "metric": METRIC,
+            "value": total,
+            "unit": "samples/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": t_b * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (gfx950 MFMA bf16 + HBM triad load; random-init operands)" if not a.mock
+            else "synthetic mock provider (CPU plumbing)",
+            "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + rocprofiler PMC, "
+                                f"{a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",
+                       "global_batch": n, "seq_len": a.steps, "parallelism": f"dp{n}",
+                       "hz": a.hz, "sample_source": "pmc" if pmc_on else "pmfw"},
+            "samples_per_sec_per_gpu": total / max(1, len(per_gpu)),
+            "pmc_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmc_rate.items()},
+            "pmfw_distinct_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmfw_rate.items()},
+            "p50_scrape_ms": scraper.percentile(0.5) * 1e3,
+            "p99_scrape_ms": scraper.percentile(0.99) * 1e3,
+            "scrapes": len(scraper.latencies_s),
+            "scrape_errors": scraper.errors,
+            "scrape_bytes_avg": scraper.bytes / max(1, len(scraper.latencies_s)),
+            "overhead_pct": 100.0 * (t_b / t_off - 1.0),
+            "t_off_a_s": t_a,
+            "t_on_s": t_b,
+            "t_off_c_s": t_c,
+            "pmc_source": exp.ready.get("pmc"),
+            "pmc_error": exp.ready.get("pmc_error"),
+            "load": calib,
+            "exporter_integrals": stopped.get("integrals"),
+        }
+    # make the result visible to rank 0 if the exporter lived elsewhere (single node: it is rank 0)
+    result = D.broadcast_object(ctx, result)
+    if ctx.rank == 0 and result is not None:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(line + "\n")
+    D.destroy(ctx)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,129 @@
+"""``kgs exporter`` — the per-node DaemonSet exporter process.
+
+Native data plane (C++ sampler threads + epoll HTTP, see native/include/kgs/*.h)
+plus the Python control plane (flags/env, attribution loop, lifecycle).  Prints
+one ``{"event": "ready", ...}`` JSON line on stdout once ``/metrics`` is being
+served, then runs until SIGTERM/SIGINT (or ``quit`` on stdin with
+``--control-stdin``).
+
+Run it in its own process: with ``--pmc rocprofiler`` it registers a
+rocprofiler-sdk tool and initialises HSA itself, which must happen before any
+HIP runtime in the same process.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import sys
+import threading
+
+from ..native import load as load_native
+from ..native import pmc_lib_path
+from ..utils import log
+from ..utils.config import add_flag
+
+L = log.get("exporter")
+
+
+def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.ArgumentParser:
+    ap = ap or argparse.ArgumentParser(prog="kgs exporter", description=__doc__.splitlines()[0])
+    add_flag(ap, "backend", "amdsmi", "device provider: amdsmi (MI355X) or mock")
+    add_flag(ap, "mock-gpus", 8, "mock provider: number of GPUs")
+    add_flag(ap, "mock-fail-rate", 0.0, "mock provider: injected read-failure probability")
+    add_flag(ap, "hz", 10.0, "fast-tier sampling rate per GPU (1/10/100 Hz tiers)")
+    add_flag(ap, "proc-every", 10, "per-process tier every N fast ticks (0 = off)")
+    add_flag(ap, "link-every", 100, "xGMI link tier every N fast ticks (0 = off)")
+    add_flag(ap, "pmc", "none", "hardware counters: none | rocprofiler | mock")
+    add_flag(ap, "pmc-lib", "", "path of libkgs_pmc.so (default: in-tree build)")
+    add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
+    add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
+    add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
+    add_flag(ap, "window", 1.0, "gauge averaging window in seconds")
+    add_flag(ap, "bdfs", "", "comma-separated PCI addresses to sample (default all)")
+    add_flag(ap, "pin-numa", True, "pin each sampler thread to its GPU's NUMA node")
+    add_flag(ap, "per-process", True, "export per-process HBM/CU metrics")
+    add_flag(ap, "compat-unallocated", False, "emit container_gpu_sm_util for GPUs no pod holds")
+    add_flag(ap, "pod-resources-socket", "/var/lib/kubelet/pod-resources/kubelet.sock", "kubelet pod-resources socket")
+    add_flag(ap, "static-owners", "", "JSON file mapping device id -> {pod,namespace,container}")
+    add_flag(ap, "attribution-interval", 1.0, "attribution refresh period (s)")
+    add_flag(ap, "control-stdin", False, "accept 'quit' on stdin")
+    return ap
+
+
+def config_from_args(a) -> dict:
+    host, _, port = a.listen.rpartition(":")
+    cfg = {
+        "backend": a.backend,
+        "mock": {"n_gpus": a.mock_gpus, "fail_rate": a.mock_fail_rate},
+        "hz": a.hz,
+        "proc_every": a.proc_every,
+        "link_every": a.link_every,
+        "pin_numa": a.pin_numa,
+        "pmc_source": a.pmc,
+        "pmc_lib": a.pmc_lib or pmc_lib_path(),
+        "listen_addr": host or "0.0.0.0",
+        "port": int(port),
+        "node_name": a.node_name,
+        "gpu_type_override": a.gpu_type,
+        "window_s": a.window,
+        "per_process": a.per_process,
+        "compat_unallocated": a.compat_unallocated,
+        "bdfs": [b for b in (a.bdfs.split(",") if isinstance(a.bdfs, str) else a.bdfs) if b],
+    }
+    return cfg
+
+
+def run(a) -> int:
+    N = load_native()
+    cfg = config_from_args(a)
+    try:
+        ex = N.Exporter(cfg)
+    except RuntimeError as e:
+        L.error("%s", e)
+        print(json.dumps({"event": "error", "error": str(e)}), flush=True)
+        return 2
+    if a.pmc != "none" and ex.pmc_name == "none":
+        L.warning("hardware counters unavailable (%s); continuing without the PMC tier", ex.pmc_error)
+    ex.start()
+    if ex.port < 0 and cfg["port"] >= 0:
+        L.error("HTTP server failed: %s", ex.error)
+        ex.stop()
+        return 2
+    from ..attribution.attributor import Attributor
+
+    attr = Attributor(ex, a.pod_resources_socket, a.static_owners or None,
+                      interval_s=a.attribution_interval).start()
+    print(json.dumps({"event": "ready", "port": ex.port, "pid": os.getpid(), "backend": ex.backend_name,
+                      "pmc": ex.pmc_name, "pmc_error": ex.pmc_error, "devices": ex.devices(),
+                      "hz": a.hz}), flush=True)
+    done = threading.Event()
+
+    def _sig(*_):
+        done.set()
+
+    signal.signal(signal.SIGTERM, _sig)
+    signal.signal(signal.SIGINT, _sig)
+    if a.control_stdin:
+        def _stdin():
+            for line in sys.stdin:
+                if line.strip().lower() in ("quit", "exit", "stop"):
+                    break
+            done.set()
+        threading.Thread(target=_stdin, daemon=True).start()
+    while not done.wait(0.5):
+        pass
+    attr.stop()
+    ex.stop()
+    print(json.dumps({"event": "stopped", "integrals": [ex.integrals(i) for i in range(ex.device_count)]}),
+          flush=True)
+    return 0
+
+
+def main(argv=None) -> int:
+    return run(build_parser().parse_args(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,99 @@
+// Device backends.  Exactly one real provider exists — AMD SMI + the PMFW
+// metrics table on sysfs (backend_amdsmi.cpp) — plus a deterministic mock used
+// by tests and the CPU-only plumbing config (BASELINE.json config 1).  There is
+// no NVML/DCGM path and no runtime multi-vendor dispatch.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kgs/sample.h"
+
+namespace kgs {
+
+struct DeviceInfo {
+  int index = 0;               // exporter-local index (label gpu="N")
+  std::string bdf;             // 0000:72:00.0
+  std::string uuid;            // amdsmi UUID
+  std::string serial;
+  std::string market_name;     // "AMD Instinct MI355 OAM"
+  std::string gpu_type;        // short label value, e.g. "MI355X"
+  std::string gfx_target;      // "gfx950"
+  int numa_node = -1;
+  int num_cu = 0;
+  uint32_t num_xcc = 0;
+  uint64_t vram_total_bytes = 0;
+  uint64_t kfd_gpu_id = 0;     // KFD gpu_id (matches rocprofiler agent gpu_id)
+  int kfd_node = -1;
+  int drm_card = -1;
+  int hip_id = -1;
+  std::string sysfs_dir;       // /sys/class/drm/cardN/device
+};
+
+struct ProcInfo {
+  uint32_t pid = 0;
+  std::string name;
+  uint64_t vram_bytes = 0, gtt_bytes = 0, cpu_bytes = 0;
+  uint64_t gfx_ns = 0;         // cumulative engine time (if the driver reports it)
+  uint32_t cu_occupancy = 0;   // CUs in use by the process' waves
+  uint32_t evicted_ms = 0;
+};
+
+struct LinkInfo {
+  int link = 0;
+  std::string peer_bdf;
+  int link_type = 0;            // amdsmi_link_type_t (2 = xGMI)
+  uint32_t bit_rate_gbps = 0;
+  uint32_t max_bw_gbps = 0;
+  uint64_t read_kb = 0, write_kb = 0;
+};
+
+struct TopoEdge {
+  int src = 0, dst = 0;
+  int link_type = 0;            // 2 = xGMI, 1 = PCIe
+  uint64_t hops = 0;
+  uint64_t weight = 0;
+};
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual std::string name() const = 0;
+  virtual int device_count() const = 0;
+  virtual const DeviceInfo& info(int dev) const = 0;
+  // Fast tier: fill everything the PMFW table + HBM occupancy give.  Must be
+  // callable concurrently for *different* devices.  0 on success.
+  virtual int read_metrics(int dev, GpuSample& out) = 0;
+  // Mid tier: per-process compute/HBM.  0 on success.
+  virtual int read_procs(int dev, std::vector<ProcInfo>& out) = 0;
+  // Slow tier: per-link xGMI metrics with peer BDFs.
+  virtual int read_links(int dev, std::vector<LinkInfo>& out) = 0;
+  // Pairwise topology among the visible devices.
+  virtual int topology(std::vector<TopoEdge>& out) = 0;
+};
+
+// Mock provider configuration (tests, plumbing benchmark).
+struct MockConfig {
+  int n_gpus = 8;
+  double fw_period_s = 0.020;   // PMFW cadence measured on MI355X (≈20 ms)
+  double util_base = 50, util_amp = 40, util_period_s = 10;
+  uint64_t vram_total_bytes = 309220868096ull;  // 288 GiB HBM3E as reported by sysfs
+  double fail_rate = 0;         // probability a read returns an error
+  double stall_s = 0;           // extra latency injected into every read
+  int vanish_dev = -1;          // device that starts failing after vanish_after_s
+  double vanish_after_s = 0;
+  uint64_t energy_wrap_at = 0;  // if >0 the energy accumulator wraps at this value
+  uint64_t seed = 1;
+  std::string hostname_seed;    // reserved
+};
+
+std::unique_ptr<Backend> make_mock_backend(const MockConfig& cfg);
+// Returns nullptr and fills `err` if AMD SMI cannot be initialised.
+std::unique_ptr<Backend> make_amdsmi_backend(std::string& err, const std::string& sysfs_root = "/sys");
+
+// Shorten an amdsmi market name to a gpu_type label ("AMD Instinct MI355 OAM" → "MI355X").
+std::string gpu_type_from_market_name(const std::string& market);
+
+}  // namespace kgs

@@ -1,0 +1,110 @@
+// The node exporter: backend + counter source + sampler + attribution labels +
+// Prometheus renderer + HTTP server (SURVEY.md §3.4 target call stack).
+//
+// Attribution (GPU → pod/namespace/container from the kubelet pod-resources
+// API, PID → pod from cgroups) is computed by the Python control plane at 1 Hz
+// and pushed in through set_device_owners()/set_pid_owners(); the scrape path
+// only reads immutable snapshots of those tables.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "kgs/backend.h"
+#include "kgs/pmc.h"
+#include "kgs/sampler.h"
+
+namespace kgs {
+
+struct Owner {
+  std::string pod, ns, container;
+};
+struct PidOwner {
+  std::string pod, ns, container, pod_uid;
+};
+
+struct ExporterConfig {
+  std::string backend = "amdsmi";   // "amdsmi" | "mock"
+  std::string sysfs_root = "/sys";
+  MockConfig mock;
+  MockPmcConfig mock_pmc;
+  SamplerConfig sampler;
+  std::vector<std::string> bdfs;    // restrict sampling to these PCI addresses (empty = all)
+  std::string pmc_source = "none";  // "none" | "rocprofiler" | "mock"
+  std::string pmc_lib;              // path of libkgs_pmc.so
+  std::string listen_addr = "0.0.0.0";
+  int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
+  std::string node_name;
+  std::string gpu_type_override;
+  double window_s = 1.0;            // gauge averaging window
+  bool per_process = true;
+  bool compat_series = true;        // container_gpu_sm_util (reference contract)
+  bool compat_unallocated = false;  // also emit it for GPUs with no pod (pod_name="")
+};
+
+class HttpServer;
+
+class Exporter {
+ public:
+  explicit Exporter(ExporterConfig cfg);
+  ~Exporter();
+
+  // Build the backend and counter source; returns false + error() on failure.
+  bool init();
+  void start();
+  void stop();
+
+  const std::string& error() const { return err_; }
+  const std::string& pmc_error() const { return pmc_err_; }
+  const ExporterConfig& config() const { return cfg_; }
+  Backend* backend() const { return be_.get(); }
+  Sampler* sampler() const { return sampler_.get(); }
+  CounterSource* counters() const { return pmc_.get(); }
+  int port() const;
+
+  void set_device_owners(int dev, std::vector<Owner> owners);
+  void set_pid_owners(std::unordered_map<uint32_t, PidOwner> m);
+  void set_node_name(const std::string& n);
+
+  // Prometheus text exposition of everything (the /metrics body).
+  void render(std::string& out);
+  std::string topology_json();
+  std::string devices_json();
+  std::string samples_json(int dev, int n);
+  bool healthy() const;
+
+  // self metrics
+  std::atomic<uint64_t> scrapes{0};
+  std::atomic<uint64_t> render_ns_total{0};
+  std::atomic<uint64_t> render_ns_last{0};
+  std::atomic<uint64_t> http_requests{0};
+
+ private:
+  void build_static_labels();
+  std::shared_ptr<const std::map<int, std::vector<Owner>>> owners() const;
+  std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> pid_owners() const;
+
+  ExporterConfig cfg_;
+  std::string err_, pmc_err_;
+  std::unique_ptr<Backend> be_;
+  std::unique_ptr<CounterSource> pmc_;
+  std::unique_ptr<Sampler> sampler_;
+  std::unique_ptr<HttpServer> http_;
+  std::vector<std::string> dev_labels_;   // pre-rendered `gpu="0",uuid=...,...`
+  std::vector<TopoEdge> topo_;
+  mutable std::mutex mu_;
+  std::shared_ptr<const std::map<int, std::vector<Owner>>> owners_;
+  std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> pid_owners_;
+  std::string node_name_;
+};
+
+// Escape a Prometheus label value.
+void append_label_value(std::string& out, const std::string& v);
+
+}  // namespace kgs

@@ -1,0 +1,27 @@
+// Direct reader of the PMFW metrics table (`/sys/class/drm/cardN/device/gpu_metrics`).
+//
+// On MI355X (gfx950) the kernel exposes format 1 / content 8 (3872 bytes).  One
+// pread of the table costs ≈46 µs on the box versus ≈270 µs through
+// amdsmi_get_gpu_metrics_info (measured, profiles/probe_summary.md), so the fast
+// tier parses the table itself.  Field offsets were verified against a live
+// table (tests/test_gpu_metrics.py pins them with a captured MI355X blob).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "kgs/sample.h"
+
+namespace kgs {
+
+constexpr size_t kGpuMetricsV18Size = 3872;
+constexpr int kV18NumXcp = 8;
+
+// Parse a v1.8 table into `out` (fields not in the table are left untouched).
+// Returns 0 on success, -1 on bad header / size.
+int parse_gpu_metrics_v1_8(const uint8_t* buf, size_t len, GpuSample& out);
+
+// Header peek: returns (format << 8) | content, or -1.
+int gpu_metrics_revision(const uint8_t* buf, size_t len);
+
+}  // namespace kgs

@@ -1,0 +1,118 @@
+// Fixed-size sample records produced by the per-GPU sampler threads.
+//
+// The reference consumes exactly one GPU series, `container_gpu_sm_util`
+// (reference gpu_util_stats/gpu_util_stats.py:159), produced by an exporter that
+// lives outside that repository.  These records are the MI355X-native source of
+// that series and of the wider amdgpu_* families.
+//
+// Everything here is trivially copyable so it can travel through the seqlock
+// slots in seqlock.h without locks or allocation on the hot path.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <type_traits>
+
+namespace kgs {
+
+constexpr int kMaxXcc = 8;       // MI355X: 8 XCDs, one XCC each (SPX mode)
+constexpr int kMaxXgmi = 8;      // gpu_metrics v1.8 NUM_XGMI_LINKS
+constexpr int kMaxPmc = 8;       // hardware counters drained per tick
+
+// Bits of GpuSample::valid.  A field whose bit is clear is "N/A" on this
+// device / driver (PMFW reports 0xFFFF / 0xFFFFFFFF for those).
+enum SampleField : uint64_t {
+  kFGfxBusy = 1ull << 0,
+  kFUmcBusy = 1ull << 1,
+  kFGfxBusyXcc = 1ull << 2,
+  kFTempHotspot = 1ull << 3,
+  kFTempMem = 1ull << 4,
+  kFTempVrSoc = 1ull << 5,
+  kFPower = 1ull << 6,
+  kFEnergy = 1ull << 7,
+  kFGfxClk = 1ull << 8,
+  kFUclk = 1ull << 9,
+  kFSocClk = 1ull << 10,
+  kFXgmi = 1ull << 11,
+  kFPcie = 1ull << 12,
+  kFVram = 1ull << 13,
+  kFAcc = 1ull << 14,        // gfx/mem activity accumulators present
+  kFThrottle = 1ull << 15,
+  kFFwTs = 1ull << 16,
+};
+
+// One hardware reading of one GPU (the PMFW metrics table + HBM occupancy).
+struct GpuSample {
+  uint64_t seq = 0;            // per-device sequence number of distinct samples
+  int64_t mono_ns = 0;         // host CLOCK_MONOTONIC when the read completed
+  int64_t wall_ns = 0;         // host CLOCK_REALTIME (for /samples consumers)
+  uint64_t fw_ts = 0;          // PMFW timestamp, 10 ns units (distinctness key)
+  uint64_t valid = 0;          // SampleField bits
+  uint32_t read_ns = 0;        // duration of the backend read
+  uint32_t num_xcc = 0;
+
+  float gfx_busy_pct = 0;      // instantaneous, average over XCCs
+  float umc_busy_pct = 0;      // memory-controller (HBM) activity
+  float gfx_busy_xcc[kMaxXcc] = {};
+  // Exact means over the interval since the previous distinct sample, derived
+  // from the PMFW activity accumulators (no aliasing: every PMFW tick counts).
+  float gfx_busy_window_pct = -1;
+  float umc_busy_window_pct = -1;
+  float dt_s = 0;              // firmware time since the previous distinct sample
+
+  float temp_hotspot_c = 0, temp_mem_c = 0, temp_vrsoc_c = 0;
+  float power_w = 0;
+  uint32_t gfxclk_mhz[kMaxXcc] = {};
+  uint32_t uclk_mhz = 0, socclk_mhz = 0;
+
+  uint64_t energy_acc = 0;             // raw, 15.259 uJ units (2^-16 J)
+  uint64_t gfx_activity_acc = 0;       // PMFW accumulators
+  uint64_t mem_activity_acc = 0;
+  uint64_t accumulation_counter = 0;
+  uint64_t ppt_residency_acc = 0, thm_residency_acc = 0;
+  uint64_t xgmi_read_kb[kMaxXgmi] = {};
+  uint64_t xgmi_write_kb[kMaxXgmi] = {};
+  uint16_t xgmi_link_up[kMaxXgmi] = {};
+  uint32_t xgmi_link_speed_gbps = 0, xgmi_link_width = 0;
+  uint64_t pcie_bw_acc_gb = 0, pcie_bw_inst_gbps = 0;
+  uint64_t pcie_replay_acc = 0;
+  uint32_t pcie_link_width = 0, pcie_link_speed_01gts = 0;
+
+  uint64_t vram_used_bytes = 0;
+  uint64_t vram_total_bytes = 0;
+};
+static_assert(std::is_trivially_copyable<GpuSample>::value, "seqlock payload");
+
+// One drain of the hardware performance counters (rocprofiler-sdk device
+// counting service).  Values are cumulative since the counter source opened.
+struct PmcSample {
+  uint64_t seq = 0;
+  int64_t mono_ns = 0;
+  uint32_t read_ns = 0;
+  uint32_t n = 0;
+  uint64_t value[kMaxPmc] = {};
+};
+static_assert(std::is_trivially_copyable<PmcSample>::value, "seqlock payload");
+
+// Running integrals maintained by the sampler so that Prometheus `rate()` over
+// any window gives exact averages regardless of scrape interval.
+struct Integrals {
+  double gfx_busy_seconds = 0;   // ∫ gfx busy fraction dt
+  double umc_busy_seconds = 0;
+  double energy_joules = 0;      // wrap-safe accumulation of energy_acc deltas
+  double sampled_seconds = 0;    // ∫ dt over distinct samples (firmware time)
+  uint64_t distinct_samples = 0; // samples with a new firmware timestamp
+  uint64_t reads = 0;            // backend reads attempted
+  uint64_t read_errors = 0;
+  uint64_t overruns = 0;         // ticks where the read exceeded the period
+  uint64_t pmc_samples = 0;
+  uint64_t pmc_errors = 0;
+  double read_seconds = 0;       // total time spent in backend reads
+};
+static_assert(std::is_trivially_copyable<Integrals>::value, "seqlock payload");
+
+inline double energy_units_to_joules(uint64_t units) {
+  return static_cast<double>(units) * (1.0 / 65536.0);  // 15.259 uJ = 2^-16 J
+}
+
+}  // namespace kgs

@@ -1,0 +1,111 @@
+// Per-GPU sampler threads (SURVEY.md §3.4 "HOT LOOP", §2.3 device fan-out).
+//
+// One std::thread per device, pinned to the CPUs of the GPU's NUMA node, wakes
+// on an absolute CLOCK_MONOTONIC deadline and
+//   * every tick   : reads the PMFW table + HBM occupancy (fast tier) and, if
+//                    enabled, drains the hardware counters (PMC tier);
+//   * every Nth    : reads the per-process list (mid tier);
+//   * every Mth    : reads per-link xGMI metrics (slow tier).
+// A sample counts as *distinct* only when the firmware timestamp moved
+// (BASELINE.md measurement rule).  Results are published through seqlocks; the
+// scrape path never calls into the driver.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kgs/backend.h"
+#include "kgs/pmc.h"
+#include "kgs/sample.h"
+#include "kgs/seqlock.h"
+
+namespace kgs {
+
+struct SamplerConfig {
+  double hz = 10.0;            // fast tier rate
+  int proc_every = 10;         // mid tier every N ticks (0 disables)
+  int link_every = 100;        // slow tier every N ticks (0 disables)
+  bool pin_numa = true;
+  bool pmc = false;            // drain hardware counters every tick
+  int max_backoff_ms = 1000;   // while a device keeps failing
+  std::vector<int> devices;    // subset to sample (empty = all)
+};
+
+constexpr size_t kRing = 1024;          // ≥10 s of history at 100 Hz
+constexpr int kReadHistBuckets = 12;    // backend read latency histogram
+extern const double kReadHistBoundsUs[kReadHistBuckets];
+
+struct DeviceState {
+  Seqlock<GpuSample> latest;
+  SampleRing<GpuSample, kRing> ring;
+  Seqlock<Integrals> integ;
+  Seqlock<PmcSample> pmc_latest;
+  SampleRing<PmcSample, kRing> pmc_ring;
+
+  mutable std::mutex slow_mu;  // guards the two shared_ptrs below
+  std::shared_ptr<const std::vector<ProcInfo>> procs;
+  std::shared_ptr<const std::vector<LinkInfo>> links;
+  int64_t procs_mono_ns = 0;
+
+  std::atomic<int> up{0};
+  std::atomic<int64_t> last_ok_mono_ns{0};
+  std::atomic<uint64_t> consecutive_errors{0};
+  std::atomic<uint64_t> read_hist[kReadHistBuckets + 1] = {};
+  std::atomic<int> cpu_pinned{-1};
+
+  std::shared_ptr<const std::vector<ProcInfo>> get_procs() const {
+    std::lock_guard<std::mutex> g(slow_mu);
+    return procs;
+  }
+  std::shared_ptr<const std::vector<LinkInfo>> get_links() const {
+    std::lock_guard<std::mutex> g(slow_mu);
+    return links;
+  }
+};
+
+class Sampler {
+ public:
+  Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg);
+  ~Sampler();
+  void start();
+  void stop();
+  bool running() const { return running_.load(); }
+
+  int device_count() const { return static_cast<int>(states_.size()); }
+  const DeviceState& state(int dev) const { return *states_[dev]; }
+  const SamplerConfig& config() const { return cfg_; }
+  const std::vector<int>& sampled_devices() const { return dev_ids_; }
+  Backend* backend() const { return be_; }
+
+  // Mean of gfx/umc busy over the trailing `window_s` of firmware time
+  // (time-weighted by each sample's dt).  Returns false if no data.
+  bool window_busy(int dev, double window_s, double& gfx_pct, double& umc_pct, int& n) const;
+  // Counter-derived rates over the trailing window.
+  bool window_pmc(int dev, double window_s, PmcRates& out) const;
+
+ private:
+  void run(int dev);
+  void integrate(int dev, const GpuSample* prev, GpuSample& cur, Integrals& I);
+
+  Backend* be_;
+  CounterSource* pmc_;
+  SamplerConfig cfg_;
+  std::vector<std::unique_ptr<DeviceState>> states_;
+  std::vector<int> dev_ids_;
+  std::vector<std::thread> threads_;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> stop_{false};
+  std::mutex cv_mu_;
+  std::condition_variable cv_;
+};
+
+// CPU list of a NUMA node ("0-31,64-95" parsed); empty if unknown.
+std::vector<int> numa_cpus(int node);
+
+}  // namespace kgs

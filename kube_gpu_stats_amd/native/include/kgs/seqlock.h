@@ -1,0 +1,102 @@
+// Single-writer / multi-reader publication primitives for the sampler → scrape
+// hand-off (SURVEY.md §2.3 "producer/consumer pipeline", §5.2).
+//
+// The writer (one sampler thread per GPU) never blocks and never allocates.
+// Readers (the HTTP renderer, Python snapshot calls) retry on a torn read.
+// The payload is copied word-by-word through relaxed atomics so the protocol is
+// data-race-free under the C++ memory model (and therefore TSAN-clean), not just
+// "works on x86".
+#pragma once
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <type_traits>
+
+namespace kgs {
+
+namespace detail {
+template <class T>
+constexpr size_t words_of() { return (sizeof(T) + sizeof(uint64_t) - 1) / sizeof(uint64_t); }
+}  // namespace detail
+
+template <class T>
+class Seqlock {
+  static_assert(std::is_trivially_copyable<T>::value, "Seqlock payload must be POD");
+  static constexpr size_t kWords = detail::words_of<T>();
+
+ public:
+  Seqlock() {
+    for (auto& w : data_) w.store(0, std::memory_order_relaxed);
+  }
+
+  // Writer side: exactly one thread.
+  void store(const T& v) {
+    uint64_t buf[kWords] = {};
+    std::memcpy(buf, &v, sizeof(T));
+    const uint64_t s = seq_.load(std::memory_order_relaxed);
+    seq_.store(s + 1, std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_release);
+    for (size_t i = 0; i < kWords; ++i) data_[i].store(buf[i], std::memory_order_relaxed);
+    seq_.store(s + 2, std::memory_order_release);
+  }
+
+  // Reader side: any number of threads.  Returns false if never written.
+  bool load(T& out, int max_spins = 1 << 20) const {
+    uint64_t buf[kWords];
+    for (int spin = 0; spin < max_spins; ++spin) {
+      const uint64_t s0 = seq_.load(std::memory_order_acquire);
+      if (s0 & 1) continue;
+      for (size_t i = 0; i < kWords; ++i) buf[i] = data_[i].load(std::memory_order_relaxed);
+      std::atomic_thread_fence(std::memory_order_acquire);
+      const uint64_t s1 = seq_.load(std::memory_order_relaxed);
+      if (s0 == s1) {
+        if (s0 == 0) return false;
+        std::memcpy(&out, buf, sizeof(T));
+        return true;
+      }
+    }
+    return false;
+  }
+
+  uint64_t version() const { return seq_.load(std::memory_order_acquire) >> 1; }
+
+ private:
+  alignas(64) std::atomic<uint64_t> seq_{0};
+  std::atomic<uint64_t> data_[kWords];
+};
+
+// Fixed-capacity history ring of seqlocked slots.  The writer publishes slot
+// `head % N` and then advances `head`; a reader walking back from `head` gets
+// every slot that was not overwritten while it read (torn slots are skipped).
+template <class T, size_t N>
+class SampleRing {
+  static_assert((N & (N - 1)) == 0, "capacity must be a power of two");
+
+ public:
+  void push(const T& v) {
+    const uint64_t h = head_.load(std::memory_order_relaxed);
+    slots_[h & (N - 1)].store(v);
+    head_.store(h + 1, std::memory_order_release);
+  }
+
+  uint64_t head() const { return head_.load(std::memory_order_acquire); }
+  static constexpr size_t capacity() { return N; }
+
+  // Copy up to `max` most recent entries (newest first) into out[]; returns count.
+  size_t recent(T* out, size_t max) const {
+    const uint64_t h = head();
+    size_t n = 0;
+    for (uint64_t i = 0; i < max && i < h && i < N - 1; ++i) {
+      if (slots_[(h - 1 - i) & (N - 1)].load(out[n], 4)) ++n;
+    }
+    return n;
+  }
+
+ private:
+  alignas(64) std::atomic<uint64_t> head_{0};
+  Seqlock<T> slots_[N];
+};
+
+}  // namespace kgs

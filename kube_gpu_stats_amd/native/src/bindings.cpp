@@ -1,0 +1,349 @@
+// pybind11 module `_kgs_native`: the Python control plane's handle on the
+// native data plane.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "kgs/exporter.h"
+#include "kgs/gpu_metrics.h"
+
+namespace py = pybind11;
+using namespace kgs;
+
+namespace {
+
+template <class T>
+T get(const py::dict& d, const char* k, T dflt) {
+  if (d.contains(k) && !d[k].is_none()) return d[k].cast<T>();
+  return dflt;
+}
+
+ExporterConfig parse_config(const py::dict& d) {
+  ExporterConfig c;
+  c.backend = get<std::string>(d, "backend", c.backend);
+  c.sysfs_root = get<std::string>(d, "sysfs_root", c.sysfs_root);
+  if (d.contains("mock")) {
+    py::dict m = d["mock"].cast<py::dict>();
+    c.mock.n_gpus = get<int>(m, "n_gpus", c.mock.n_gpus);
+    c.mock.fw_period_s = get<double>(m, "fw_period_s", c.mock.fw_period_s);
+    c.mock.util_base = get<double>(m, "util_base", c.mock.util_base);
+    c.mock.util_amp = get<double>(m, "util_amp", c.mock.util_amp);
+    c.mock.util_period_s = get<double>(m, "util_period_s", c.mock.util_period_s);
+    c.mock.fail_rate = get<double>(m, "fail_rate", c.mock.fail_rate);
+    c.mock.stall_s = get<double>(m, "stall_s", c.mock.stall_s);
+    c.mock.vanish_dev = get<int>(m, "vanish_dev", c.mock.vanish_dev);
+    c.mock.vanish_after_s = get<double>(m, "vanish_after_s", c.mock.vanish_after_s);
+    c.mock.energy_wrap_at = get<uint64_t>(m, "energy_wrap_at", c.mock.energy_wrap_at);
+    c.mock.seed = get<uint64_t>(m, "seed", c.mock.seed);
+  }
+  if (d.contains("mock_pmc")) {
+    py::dict m = d["mock_pmc"].cast<py::dict>();
+    c.mock_pmc.clock_mhz = get<double>(m, "clock_mhz", c.mock_pmc.clock_mhz);
+    c.mock_pmc.mfma_frac = get<double>(m, "mfma_frac", c.mock_pmc.mfma_frac);
+    c.mock_pmc.read_Bps = get<double>(m, "read_Bps", c.mock_pmc.read_Bps);
+    c.mock_pmc.write_Bps = get<double>(m, "write_Bps", c.mock_pmc.write_Bps);
+  }
+  c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
+  c.sampler.proc_every = get<int>(d, "proc_every", c.sampler.proc_every);
+  c.sampler.link_every = get<int>(d, "link_every", c.sampler.link_every);
+  c.sampler.pin_numa = get<bool>(d, "pin_numa", c.sampler.pin_numa);
+  c.sampler.max_backoff_ms = get<int>(d, "max_backoff_ms", c.sampler.max_backoff_ms);
+  c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
+  c.bdfs = get<std::vector<std::string>>(d, "bdfs", c.bdfs);
+  c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);
+  c.pmc_lib = get<std::string>(d, "pmc_lib", c.pmc_lib);
+  c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
+  c.port = get<int>(d, "port", c.port);
+  c.node_name = get<std::string>(d, "node_name", c.node_name);
+  c.gpu_type_override = get<std::string>(d, "gpu_type_override", c.gpu_type_override);
+  c.window_s = get<double>(d, "window_s", c.window_s);
+  c.per_process = get<bool>(d, "per_process", c.per_process);
+  c.compat_series = get<bool>(d, "compat_series", c.compat_series);
+  c.compat_unallocated = get<bool>(d, "compat_unallocated", c.compat_unallocated);
+  return c;
+}
+
+py::dict sample_dict(const GpuSample& s) {
+  py::dict o;
+  o["seq"] = s.seq;
+  o["mono_ns"] = s.mono_ns;
+  o["wall_ns"] = s.wall_ns;
+  o["fw_ts"] = s.fw_ts;
+  o["valid"] = s.valid;
+  o["read_ns"] = s.read_ns;
+  o["num_xcc"] = s.num_xcc;
+  o["gfx_busy_pct"] = s.gfx_busy_pct;
+  o["umc_busy_pct"] = s.umc_busy_pct;
+  o["gfx_busy_xcc"] = std::vector<float>(s.gfx_busy_xcc, s.gfx_busy_xcc + s.num_xcc);
+  o["gfx_busy_window_pct"] = s.gfx_busy_window_pct;
+  o["umc_busy_window_pct"] = s.umc_busy_window_pct;
+  o["dt_s"] = s.dt_s;
+  o["temp_hotspot_c"] = s.temp_hotspot_c;
+  o["temp_mem_c"] = s.temp_mem_c;
+  o["temp_vrsoc_c"] = s.temp_vrsoc_c;
+  o["power_w"] = s.power_w;
+  o["gfxclk_mhz"] = std::vector<uint32_t>(s.gfxclk_mhz, s.gfxclk_mhz + kMaxXcc);
+  o["uclk_mhz"] = s.uclk_mhz;
+  o["socclk_mhz"] = s.socclk_mhz;
+  o["energy_acc"] = s.energy_acc;
+  o["gfx_activity_acc"] = s.gfx_activity_acc;
+  o["mem_activity_acc"] = s.mem_activity_acc;
+  o["accumulation_counter"] = s.accumulation_counter;
+  o["ppt_residency_acc"] = s.ppt_residency_acc;
+  o["xgmi_read_kb"] = std::vector<uint64_t>(s.xgmi_read_kb, s.xgmi_read_kb + kMaxXgmi);
+  o["xgmi_write_kb"] = std::vector<uint64_t>(s.xgmi_write_kb, s.xgmi_write_kb + kMaxXgmi);
+  o["xgmi_link_up"] = std::vector<uint16_t>(s.xgmi_link_up, s.xgmi_link_up + kMaxXgmi);
+  o["xgmi_link_speed_gbps"] = s.xgmi_link_speed_gbps;
+  o["pcie_bw_acc_gb"] = s.pcie_bw_acc_gb;
+  o["pcie_link_width"] = s.pcie_link_width;
+  o["pcie_link_speed_01gts"] = s.pcie_link_speed_01gts;
+  o["vram_used_bytes"] = s.vram_used_bytes;
+  o["vram_total_bytes"] = s.vram_total_bytes;
+  return o;
+}
+
+py::dict info_dict(const DeviceInfo& in) {
+  py::dict o;
+  o["index"] = in.index;
+  o["bdf"] = in.bdf;
+  o["uuid"] = in.uuid;
+  o["serial"] = in.serial;
+  o["market_name"] = in.market_name;
+  o["gpu_type"] = in.gpu_type;
+  o["gfx_target"] = in.gfx_target;
+  o["numa_node"] = in.numa_node;
+  o["num_cu"] = in.num_cu;
+  o["num_xcc"] = in.num_xcc;
+  o["vram_total_bytes"] = in.vram_total_bytes;
+  o["kfd_gpu_id"] = in.kfd_gpu_id;
+  o["kfd_node"] = in.kfd_node;
+  o["drm_card"] = in.drm_card;
+  o["hip_id"] = in.hip_id;
+  o["sysfs_dir"] = in.sysfs_dir;
+  return o;
+}
+
+class PyExporter {
+ public:
+  explicit PyExporter(const py::dict& cfg) : ex_(parse_config(cfg)) {
+    if (!ex_.init()) throw std::runtime_error("exporter init failed: " + ex_.error());
+  }
+  void start() {
+    py::gil_scoped_release r;
+    ex_.start();
+  }
+  void stop() {
+    py::gil_scoped_release r;
+    ex_.stop();
+  }
+  std::string render() {
+    std::string out;
+    {
+      py::gil_scoped_release r;
+      ex_.render(out);
+    }
+    return out;
+  }
+  int port() const { return ex_.port(); }
+  int device_count() const { return ex_.backend()->device_count(); }
+  std::string backend_name() const { return ex_.backend()->name(); }
+  std::string pmc_name() const { return ex_.counters() ? ex_.counters()->name() : std::string("none"); }
+  std::string pmc_error() const { return ex_.pmc_error(); }
+  std::string error() const { return ex_.error(); }
+  py::list devices() const {
+    py::list l;
+    for (int d = 0; d < device_count(); ++d) l.append(info_dict(ex_.backend()->info(d)));
+    return l;
+  }
+  py::object snapshot(int d) const {
+    check(d);
+    GpuSample s;
+    if (!ex_.sampler()->state(d).latest.load(s)) return py::none();
+    return sample_dict(s);
+  }
+  py::list samples(int d, int n) const {
+    check(d);
+    if (n < 1) n = 1;
+    if (n > static_cast<int>(kRing) - 1) n = static_cast<int>(kRing) - 1;
+    std::vector<GpuSample> buf(static_cast<size_t>(n));
+    const size_t got = ex_.sampler()->state(d).ring.recent(buf.data(), static_cast<size_t>(n));
+    py::list l;
+    for (size_t i = got; i-- > 0;) l.append(sample_dict(buf[i]));
+    return l;
+  }
+  py::dict integrals(int d) const {
+    check(d);
+    Integrals I;
+    ex_.sampler()->state(d).integ.load(I);
+    py::dict o;
+    o["gfx_busy_seconds"] = I.gfx_busy_seconds;
+    o["umc_busy_seconds"] = I.umc_busy_seconds;
+    o["energy_joules"] = I.energy_joules;
+    o["sampled_seconds"] = I.sampled_seconds;
+    o["distinct_samples"] = I.distinct_samples;
+    o["reads"] = I.reads;
+    o["read_errors"] = I.read_errors;
+    o["overruns"] = I.overruns;
+    o["pmc_samples"] = I.pmc_samples;
+    o["pmc_errors"] = I.pmc_errors;
+    o["read_seconds"] = I.read_seconds;
+    o["up"] = ex_.sampler()->state(d).up.load();
+    o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
+    return o;
+  }
+  py::object pmc(int d) const {
+    check(d);
+    PmcSample p;
+    if (!ex_.sampler()->state(d).pmc_latest.load(p)) return py::none();
+    py::dict o;
+    o["seq"] = p.seq;
+    o["mono_ns"] = p.mono_ns;
+    o["read_ns"] = p.read_ns;
+    py::dict v;
+    for (int i = 0; i < kPmcCount; ++i) v[pmc_counter_name(i)] = p.value[i];
+    o["values"] = v;
+    o["read_bytes"] = pmc_read_bytes(p);
+    o["write_bytes"] = pmc_write_bytes(p);
+    return o;
+  }
+  py::dict window(int d, double window_s) const {
+    check(d);
+    py::dict o;
+    double g = 0, u = 0;
+    int n = 0;
+    if (ex_.sampler()->window_busy(d, window_s, g, u, n)) {
+      o["gfx_busy_pct"] = g;
+      o["umc_busy_pct"] = u;
+      o["n"] = n;
+    }
+    PmcRates r;
+    if (ex_.sampler()->window_pmc(d, window_s, r)) {
+      o["gpu_active_pct"] = r.gpu_active_pct;
+      o["mfma_util_pct"] = r.mfma_util_pct;
+      o["cu_busy_pct"] = r.cu_busy_pct;
+      o["hbm_read_Bps"] = r.hbm_read_Bps;
+      o["hbm_write_Bps"] = r.hbm_write_Bps;
+      o["gpu_clock_mhz"] = r.gpu_clock_mhz;
+      o["pmc_dt_s"] = r.dt_s;
+    }
+    return o;
+  }
+  py::list procs(int d) const {
+    check(d);
+    py::list l;
+    auto p = ex_.sampler()->state(d).get_procs();
+    if (!p) return l;
+    for (const ProcInfo& x : *p) {
+      py::dict o;
+      o["pid"] = x.pid;
+      o["name"] = x.name;
+      o["vram_bytes"] = x.vram_bytes;
+      o["gtt_bytes"] = x.gtt_bytes;
+      o["cpu_bytes"] = x.cpu_bytes;
+      o["gfx_ns"] = x.gfx_ns;
+      o["cu_occupancy"] = x.cu_occupancy;
+      o["evicted_ms"] = x.evicted_ms;
+      l.append(o);
+    }
+    return l;
+  }
+  py::list links(int d) const {
+    check(d);
+    py::list l;
+    auto p = ex_.sampler()->state(d).get_links();
+    if (!p) return l;
+    for (const LinkInfo& x : *p) {
+      py::dict o;
+      o["link"] = x.link;
+      o["peer_bdf"] = x.peer_bdf;
+      o["link_type"] = x.link_type;
+      o["bit_rate_gbps"] = x.bit_rate_gbps;
+      o["max_bw_gbps"] = x.max_bw_gbps;
+      o["read_kb"] = x.read_kb;
+      o["write_kb"] = x.write_kb;
+      l.append(o);
+    }
+    return l;
+  }
+  std::string topology_json() { return ex_.topology_json(); }
+  void set_device_owners(int d, const py::list& owners) {
+    check(d);
+    std::vector<Owner> v;
+    for (auto h : owners) {
+      py::dict o = h.cast<py::dict>();
+      v.push_back(Owner{get<std::string>(o, "pod", ""), get<std::string>(o, "namespace", ""),
+                        get<std::string>(o, "container", "")});
+    }
+    ex_.set_device_owners(d, std::move(v));
+  }
+  void set_pid_owners(const py::dict& m) {
+    std::unordered_map<uint32_t, PidOwner> mm;
+    for (auto kvp : m) {
+      py::dict o = kvp.second.cast<py::dict>();
+      mm[kvp.first.cast<uint32_t>()] = PidOwner{get<std::string>(o, "pod", ""), get<std::string>(o, "namespace", ""),
+                                                get<std::string>(o, "container", ""), get<std::string>(o, "pod_uid", "")};
+    }
+    ex_.set_pid_owners(std::move(mm));
+  }
+  void set_node_name(const std::string& n) { ex_.set_node_name(n); }
+  py::dict stats() const {
+    py::dict o;
+    o["scrapes"] = ex_.scrapes.load();
+    o["render_ns_total"] = ex_.render_ns_total.load();
+    o["render_ns_last"] = ex_.render_ns_last.load();
+    o["http_requests"] = ex_.http_requests.load();
+    return o;
+  }
+  bool healthy() const { return ex_.healthy(); }
+
+ private:
+  void check(int d) const {
+    if (d < 0 || d >= device_count()) throw py::index_error("gpu index out of range");
+  }
+  Exporter ex_;
+};
+
+py::dict parse_metrics_blob(const py::bytes& b) {
+  std::string s = b;
+  GpuSample g;
+  if (parse_gpu_metrics_v1_8(reinterpret_cast<const uint8_t*>(s.data()), s.size(), g) != 0)
+    throw std::runtime_error("not a gpu_metrics v1.8 table");
+  return sample_dict(g);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_kgs_native, m) {
+  m.doc() = "kube_gpu_stats_amd native data plane (C++17: sampler threads, seqlocks, renderer, HTTP)";
+  py::class_<PyExporter>(m, "Exporter")
+      .def(py::init<const py::dict&>())
+      .def("start", &PyExporter::start)
+      .def("stop", &PyExporter::stop)
+      .def("render", &PyExporter::render)
+      .def_property_readonly("port", &PyExporter::port)
+      .def_property_readonly("device_count", &PyExporter::device_count)
+      .def_property_readonly("backend_name", &PyExporter::backend_name)
+      .def_property_readonly("pmc_name", &PyExporter::pmc_name)
+      .def_property_readonly("pmc_error", &PyExporter::pmc_error)
+      .def_property_readonly("error", &PyExporter::error)
+      .def("devices", &PyExporter::devices)
+      .def("snapshot", &PyExporter::snapshot)
+      .def("samples", &PyExporter::samples, py::arg("gpu"), py::arg("n") = 100)
+      .def("integrals", &PyExporter::integrals)
+      .def("pmc", &PyExporter::pmc)
+      .def("window", &PyExporter::window, py::arg("gpu"), py::arg("window_s") = 1.0)
+      .def("procs", &PyExporter::procs)
+      .def("links", &PyExporter::links)
+      .def("topology_json", &PyExporter::topology_json)
+      .def("set_device_owners", &PyExporter::set_device_owners)
+      .def("set_pid_owners", &PyExporter::set_pid_owners)
+      .def("set_node_name", &PyExporter::set_node_name)
+      .def("stats", &PyExporter::stats)
+      .def("healthy", &PyExporter::healthy);
+  m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
+  m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
+  m.def("pmc_counter_names", [] {
+    std::vector<std::string> v;
+    for (int i = 0; i < kPmcCount; ++i) v.push_back(pmc_counter_name(i));
+    return v;
+  });
+}

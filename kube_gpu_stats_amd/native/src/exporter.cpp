@@ -1,0 +1,253 @@
+// Exporter lifecycle, attribution tables and JSON endpoints.  See exporter.h.
+#include "kgs/exporter.h"
+
+#include <unistd.h>
+
+#include <cstdio>
+#include <ctime>
+
+#include "kgs/http.h"
+
+namespace kgs {
+
+namespace {
+void jstr(std::string& o, const std::string& s) {
+  o += '"';
+  for (char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      default:
+        if (static_cast<unsigned char>(c) < 0x20) {
+          char b[8];
+          std::snprintf(b, sizeof b, "\\u%04x", c);
+          o += b;
+        } else {
+          o += c;
+        }
+    }
+  }
+  o += '"';
+}
+void jnum(std::string& o, double v) {
+  char b[40];
+  std::snprintf(b, sizeof b, "%.17g", v);
+  o += b;
+}
+}  // namespace
+
+Exporter::Exporter(ExporterConfig cfg) : cfg_(std::move(cfg)) {
+  node_name_ = cfg_.node_name;
+  if (node_name_.empty()) {
+    char h[256] = {};
+    if (gethostname(h, sizeof h - 1) == 0) node_name_ = h;
+  }
+}
+
+Exporter::~Exporter() { stop(); }
+
+bool Exporter::init() {
+  if (cfg_.backend == "mock") {
+    be_ = make_mock_backend(cfg_.mock);
+  } else if (cfg_.backend == "amdsmi") {
+    be_ = make_amdsmi_backend(err_, cfg_.sysfs_root);
+    if (!be_) return false;
+  } else {
+    err_ = "unknown backend '" + cfg_.backend + "' (expected amdsmi or mock)";
+    return false;
+  }
+  SamplerConfig sc = cfg_.sampler;
+  for (const std::string& want : cfg_.bdfs) {
+    int found = -1;
+    for (int d = 0; d < be_->device_count(); ++d)
+      if (be_->info(d).bdf == want) found = d;
+    if (found < 0) {
+      err_ = "no GPU with PCI address " + want;
+      return false;
+    }
+    sc.devices.push_back(found);
+  }
+  std::vector<int> devs = sc.devices;
+  if (devs.empty())
+    for (int d = 0; d < be_->device_count(); ++d) devs.push_back(d);
+  if (cfg_.pmc_source == "mock") {
+    pmc_ = make_mock_counter_source(*be_, cfg_.mock, cfg_.mock_pmc);
+  } else if (cfg_.pmc_source == "rocprofiler") {
+    pmc_ = make_rocprofiler_counter_source(cfg_.pmc_lib, *be_, devs, pmc_err_);
+  } else if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
+    err_ = "unknown pmc_source '" + cfg_.pmc_source + "'";
+    return false;
+  }
+  sc.pmc = pmc_ != nullptr;
+  sampler_ = std::make_unique<Sampler>(be_.get(), pmc_.get(), sc);
+  be_->topology(topo_);
+  build_static_labels();
+  return true;
+}
+
+void Exporter::build_static_labels() {
+  dev_labels_.clear();
+  for (int d = 0; d < be_->device_count(); ++d) {
+    const DeviceInfo& in = be_->info(d);
+    std::string lb;
+    lb += "gpu=\"" + std::to_string(d) + "\"";
+    lb += ",uuid=\"";
+    append_label_value(lb, in.uuid);
+    lb += "\",bdf=\"";
+    append_label_value(lb, in.bdf);
+    lb += "\",gpu_type=\"";
+    append_label_value(lb, cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override);
+    lb += '"';
+    dev_labels_.push_back(std::move(lb));
+  }
+}
+
+void Exporter::start() {
+  if (!sampler_) return;
+  sampler_->start();
+  if (cfg_.port >= 0 && !http_) {
+    http_ = std::make_unique<HttpServer>(this, cfg_.listen_addr, cfg_.port);
+    if (!http_->start(err_)) http_.reset();
+  }
+}
+
+void Exporter::stop() {
+  if (http_) {
+    http_->stop();
+    http_.reset();
+  }
+  if (sampler_) sampler_->stop();
+}
+
+int Exporter::port() const { return http_ ? http_->port() : -1; }
+
+void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto m = owners_ ? std::make_shared<std::map<int, std::vector<Owner>>>(*owners_)
+                   : std::make_shared<std::map<int, std::vector<Owner>>>();
+  if (o.empty()) m->erase(dev);
+  else (*m)[dev] = std::move(o);
+  owners_ = std::move(m);
+}
+
+void Exporter::set_pid_owners(std::unordered_map<uint32_t, PidOwner> m) {
+  auto p = std::make_shared<const std::unordered_map<uint32_t, PidOwner>>(std::move(m));
+  std::lock_guard<std::mutex> g(mu_);
+  pid_owners_ = std::move(p);
+}
+
+void Exporter::set_node_name(const std::string& n) {
+  std::lock_guard<std::mutex> g(mu_);
+  node_name_ = n;
+}
+
+std::shared_ptr<const std::map<int, std::vector<Owner>>> Exporter::owners() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return owners_;
+}
+std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> Exporter::pid_owners() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return pid_owners_;
+}
+
+bool Exporter::healthy() const {
+  if (!sampler_) return false;
+  for (int d = 0; d < sampler_->device_count(); ++d)
+    if (sampler_->state(d).up.load()) return true;
+  return false;
+}
+
+std::string Exporter::devices_json() {
+  std::string o = "[";
+  for (int d = 0; d < be_->device_count(); ++d) {
+    const DeviceInfo& in = be_->info(d);
+    if (d) o += ',';
+    o += "{\"gpu\":" + std::to_string(d) + ",\"bdf\":";
+    jstr(o, in.bdf);
+    o += ",\"uuid\":";
+    jstr(o, in.uuid);
+    o += ",\"serial\":";
+    jstr(o, in.serial);
+    o += ",\"market_name\":";
+    jstr(o, in.market_name);
+    o += ",\"gpu_type\":";
+    jstr(o, in.gpu_type);
+    o += ",\"gfx_target\":";
+    jstr(o, in.gfx_target);
+    o += ",\"numa_node\":" + std::to_string(in.numa_node) + ",\"num_cu\":" + std::to_string(in.num_cu) +
+         ",\"num_xcc\":" + std::to_string(in.num_xcc) + ",\"vram_total_bytes\":" + std::to_string(in.vram_total_bytes) +
+         ",\"kfd_gpu_id\":" + std::to_string(in.kfd_gpu_id) + ",\"kfd_node\":" + std::to_string(in.kfd_node) +
+         ",\"drm_card\":" + std::to_string(in.drm_card) + ",\"hip_id\":" + std::to_string(in.hip_id) +
+         ",\"sysfs_dir\":";
+    jstr(o, in.sysfs_dir);
+    o += ",\"cpu_pinned\":" + std::to_string(sampler_ ? sampler_->state(d).cpu_pinned.load() : -1);
+    o += '}';
+  }
+  o += ']';
+  return o;
+}
+
+std::string Exporter::topology_json() {
+  std::string o = "{\"node\":";
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    jstr(o, node_name_);
+  }
+  o += ",\"devices\":" + devices_json() + ",\"edges\":[";
+  for (size_t i = 0; i < topo_.size(); ++i) {
+    const TopoEdge& e = topo_[i];
+    if (i) o += ',';
+    o += "{\"src\":" + std::to_string(e.src) + ",\"dst\":" + std::to_string(e.dst) +
+         ",\"link_type\":" + std::to_string(e.link_type) + ",\"hops\":" + std::to_string(e.hops) +
+         ",\"weight\":" + std::to_string(e.weight) + '}';
+  }
+  o += "],\"links\":[";
+  bool first = true;
+  for (int d = 0; sampler_ && d < sampler_->device_count(); ++d) {
+    auto links = sampler_->state(d).get_links();
+    if (!links) continue;
+    for (const LinkInfo& l : *links) {
+      if (!first) o += ',';
+      first = false;
+      o += "{\"gpu\":" + std::to_string(d) + ",\"link\":" + std::to_string(l.link) + ",\"peer_bdf\":";
+      jstr(o, l.peer_bdf);
+      o += ",\"link_type\":" + std::to_string(l.link_type) + ",\"bit_rate_gbps\":" + std::to_string(l.bit_rate_gbps) +
+           ",\"max_bandwidth_gbps\":" + std::to_string(l.max_bw_gbps) + ",\"read_kb\":" + std::to_string(l.read_kb) +
+           ",\"write_kb\":" + std::to_string(l.write_kb) + '}';
+    }
+  }
+  o += "]}";
+  return o;
+}
+
+std::string Exporter::samples_json(int dev, int n) {
+  if (!sampler_ || dev < 0 || dev >= sampler_->device_count()) return "[]";
+  if (n <= 0) n = 1;
+  if (n > static_cast<int>(kRing) - 1) n = static_cast<int>(kRing) - 1;
+  std::vector<GpuSample> buf(static_cast<size_t>(n));
+  const size_t got = sampler_->state(dev).ring.recent(buf.data(), static_cast<size_t>(n));
+  std::string o = "[";
+  for (size_t i = got; i-- > 0;) {  // oldest first
+    const GpuSample& s = buf[i];
+    if (o.size() > 1) o += ',';
+    o += "{\"seq\":" + std::to_string(s.seq) + ",\"fw_ts\":" + std::to_string(s.fw_ts) +
+         ",\"wall_ns\":" + std::to_string(s.wall_ns) + ",\"gfx_busy_pct\":";
+    jnum(o, s.gfx_busy_pct);
+    o += ",\"gfx_busy_window_pct\":";
+    jnum(o, s.gfx_busy_window_pct);
+    o += ",\"umc_busy_window_pct\":";
+    jnum(o, s.umc_busy_window_pct);
+    o += ",\"dt_s\":";
+    jnum(o, s.dt_s);
+    o += ",\"power_w\":";
+    jnum(o, s.power_w);
+    o += ",\"temp_hotspot_c\":";
+    jnum(o, s.temp_hotspot_c);
+    o += ",\"vram_used_bytes\":" + std::to_string(s.vram_used_bytes) + ",\"read_ns\":" + std::to_string(s.read_ns) + '}';
+  }
+  o += ']';
+  return o;
+}
+
+}  // namespace kgs

@@ -1,0 +1,231 @@
+// epoll HTTP server.  See http.h.
+#include "kgs/http.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <unordered_map>
+
+#include "kgs/exporter.h"
+
+namespace kgs {
+
+namespace {
+
+struct Conn {
+  std::string in;
+  std::string out;
+  size_t out_off = 0;
+  bool close_after = false;
+};
+
+void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
+
+int query_int(const std::string& q, const char* key, int dflt) {
+  const std::string k = std::string(key) + "=";
+  size_t p = 0;
+  while ((p = q.find(k, p)) != std::string::npos) {
+    if (p == 0 || q[p - 1] == '&' || q[p - 1] == '?') return std::atoi(q.c_str() + p + k.size());
+    p += k.size();
+  }
+  return dflt;
+}
+
+void respond(Conn& c, int code, const char* reason, const char* ctype, const std::string& body) {
+  c.out.clear();
+  c.out_off = 0;
+  c.out.reserve(body.size() + 256);
+  c.out += "HTTP/1.1 ";
+  c.out += std::to_string(code);
+  c.out += ' ';
+  c.out += reason;
+  c.out += "\r\nContent-Type: ";
+  c.out += ctype;
+  c.out += "\r\nContent-Length: ";
+  c.out += std::to_string(body.size());
+  c.out += c.close_after ? "\r\nConnection: close\r\n\r\n" : "\r\nConnection: keep-alive\r\n\r\n";
+  c.out += body;
+}
+
+}  // namespace
+
+HttpServer::HttpServer(Exporter* ex, std::string addr, int port) : ex_(ex), addr_(std::move(addr)), port_(port) {}
+HttpServer::~HttpServer() { stop(); }
+
+bool HttpServer::start(std::string& err) {
+  lfd_ = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (lfd_ < 0) { err = "socket: " + std::string(strerror(errno)); return false; }
+  int one = 1;
+  setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons(static_cast<uint16_t>(port_));
+  if (inet_pton(AF_INET, addr_.c_str(), &sa.sin_addr) != 1) sa.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (bind(lfd_, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
+    err = "bind " + addr_ + ":" + std::to_string(port_) + ": " + strerror(errno);
+    close(lfd_);
+    lfd_ = -1;
+    return false;
+  }
+  socklen_t sl = sizeof sa;
+  getsockname(lfd_, reinterpret_cast<sockaddr*>(&sa), &sl);
+  port_ = ntohs(sa.sin_port);
+  listen(lfd_, 128);
+  set_nonblock(lfd_);
+  efd_ = epoll_create1(EPOLL_CLOEXEC);
+  wake_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.fd = lfd_;
+  epoll_ctl(efd_, EPOLL_CTL_ADD, lfd_, &ev);
+  ev.data.fd = wake_fd_;
+  epoll_ctl(efd_, EPOLL_CTL_ADD, wake_fd_, &ev);
+  stop_.store(false);
+  th_ = std::thread([this] { loop(); });
+  return true;
+}
+
+void HttpServer::stop() {
+  if (!th_.joinable()) return;
+  stop_.store(true);
+  uint64_t one = 1;
+  if (write(wake_fd_, &one, sizeof one) < 0) {}
+  th_.join();
+  if (lfd_ >= 0) close(lfd_);
+  if (efd_ >= 0) close(efd_);
+  if (wake_fd_ >= 0) close(wake_fd_);
+  lfd_ = efd_ = wake_fd_ = -1;
+}
+
+void HttpServer::loop() {
+  pthread_setname_np(pthread_self(), "kgs-http");
+  std::unordered_map<int, Conn> conns;
+  std::string body;
+  epoll_event evs[64];
+  auto drop = [&](int fd) {
+    epoll_ctl(efd_, EPOLL_CTL_DEL, fd, nullptr);
+    close(fd);
+    conns.erase(fd);
+  };
+  auto flush = [&](int fd, Conn& c) -> bool {  // false = connection gone
+    while (c.out_off < c.out.size()) {
+      const ssize_t n = send(fd, c.out.data() + c.out_off, c.out.size() - c.out_off, MSG_NOSIGNAL);
+      if (n > 0) { c.out_off += static_cast<size_t>(n); continue; }
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        epoll_event ev{};
+        ev.events = EPOLLIN | EPOLLOUT;
+        ev.data.fd = fd;
+        epoll_ctl(efd_, EPOLL_CTL_MOD, fd, &ev);
+        return true;
+      }
+      drop(fd);
+      return false;
+    }
+    c.out.clear();
+    c.out_off = 0;
+    if (c.close_after) { drop(fd); return false; }
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = fd;
+    epoll_ctl(efd_, EPOLL_CTL_MOD, fd, &ev);
+    return true;
+  };
+
+  while (!stop_.load()) {
+    const int n = epoll_wait(efd_, evs, 64, 500);
+    for (int i = 0; i < n; ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == wake_fd_) continue;
+      if (fd == lfd_) {
+        for (;;) {
+          const int c = accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (c < 0) break;
+          int one = 1;
+          setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          epoll_event ev{};
+          ev.events = EPOLLIN;
+          ev.data.fd = c;
+          epoll_ctl(efd_, EPOLL_CTL_ADD, c, &ev);
+          conns[c];
+        }
+        continue;
+      }
+      auto it = conns.find(fd);
+      if (it == conns.end()) { close(fd); continue; }
+      Conn& c = it->second;
+      if (evs[i].events & EPOLLOUT) {
+        if (!flush(fd, c)) continue;
+        if (!c.out.empty()) continue;
+      }
+      if (!(evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR))) continue;
+      char buf[4096];
+      bool gone = false;
+      for (;;) {
+        const ssize_t r = recv(fd, buf, sizeof buf, 0);
+        if (r > 0) { c.in.append(buf, static_cast<size_t>(r)); if (c.in.size() > (1u << 16)) { gone = true; break; } continue; }
+        if (r == 0) { gone = true; break; }
+        if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+        gone = true;
+        break;
+      }
+      // Serve every complete request in the buffer (pipelining-safe).
+      size_t hdr_end;
+      while (!gone && c.out.empty() && (hdr_end = c.in.find("\r\n\r\n")) != std::string::npos) {
+        const std::string req = c.in.substr(0, hdr_end);
+        c.in.erase(0, hdr_end + 4);
+        ex_->http_requests.fetch_add(1);
+        const size_t sp1 = req.find(' ');
+        const size_t sp2 = sp1 == std::string::npos ? std::string::npos : req.find(' ', sp1 + 1);
+        const std::string method = req.substr(0, sp1);
+        std::string target = sp1 == std::string::npos ? "/" : req.substr(sp1 + 1, sp2 - sp1 - 1);
+        std::string query;
+        const size_t q = target.find('?');
+        if (q != std::string::npos) { query = target.substr(q + 1); target.resize(q); }
+        const bool http10 = req.find("HTTP/1.0") != std::string::npos;
+        const bool conn_close = req.find("Connection: close") != std::string::npos ||
+                                req.find("connection: close") != std::string::npos;
+        c.close_after = conn_close || (http10 && req.find("eep-Alive") == std::string::npos);
+        if (method != "GET" && method != "HEAD") {
+          respond(c, 405, "Method Not Allowed", "text/plain", "only GET\n");
+        } else if (target == "/metrics") {
+          ex_->render(body);
+          respond(c, 200, "OK", "text/plain; version=0.0.4; charset=utf-8", body);
+        } else if (target == "/healthz") {
+          const bool ok = ex_->healthy();
+          respond(c, ok ? 200 : 503, ok ? "OK" : "Service Unavailable", "text/plain", ok ? "ok\n" : "no device sampled\n");
+        } else if (target == "/topology") {
+          respond(c, 200, "OK", "application/json", ex_->topology_json());
+        } else if (target == "/devices") {
+          respond(c, 200, "OK", "application/json", ex_->devices_json());
+        } else if (target == "/samples") {
+          respond(c, 200, "OK", "application/json",
+                  ex_->samples_json(query_int(query, "gpu", 0), query_int(query, "n", 100)));
+        } else if (target == "/") {
+          respond(c, 200, "OK", "text/html",
+                  "<html><body><h1>kube_gpu_stats_amd exporter</h1><a href=\"/metrics\">/metrics</a> "
+                  "<a href=\"/topology\">/topology</a> <a href=\"/devices\">/devices</a></body></html>\n");
+        } else {
+          respond(c, 404, "Not Found", "text/plain", "not found\n");
+        }
+        if (method == "HEAD") {
+          const size_t he = c.out.find("\r\n\r\n");
+          if (he != std::string::npos) c.out.resize(he + 4);
+        }
+        if (!flush(fd, c)) { gone = true; break; }
+      }
+      if (gone && conns.count(fd)) drop(fd);
+    }
+  }
+  for (auto& kvp : conns) close(kvp.first);
+}
+
+}  // namespace kgs

@@ -1,0 +1,185 @@
+// Counter-source plumbing: counter catalogue, derived rates, the mock source and
+// the dlopen bridge to libkgs_pmc.so (rocprofiler-sdk device counting).
+#include "kgs/pmc.h"
+
+#include <dlfcn.h>
+
+#include <cmath>
+#include <ctime>
+#include <mutex>
+
+namespace kgs {
+
+namespace {
+const char* const kNames[kPmcCount] = {
+    "GRBM_COUNT",     "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES",
+    "TCC_EA0_RDREQ",  "TCC_BUBBLE",      "TCC_EA0_WRREQ",            "TCC_EA0_WRREQ_64B",
+};
+
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+}  // namespace
+
+const char* pmc_counter_name(int idx) { return (idx >= 0 && idx < kPmcCount) ? kNames[idx] : "?"; }
+bool pmc_counter_is_max(int idx) { return idx == kPmcGrbmCount || idx == kPmcGrbmGuiActive; }
+
+double pmc_read_bytes(const PmcSample& s) {
+  // FETCH_SIZE expression for gfx950 (rocprofv3 -L), 32-byte requests folded
+  // into the 64-byte class: 128 B per TCC_BUBBLE, 64 B per other request.
+  const double rd = static_cast<double>(s.value[kPmcTccRdReq]);
+  const double bub = static_cast<double>(s.value[kPmcTccBubble]);
+  return bub * 128.0 + (rd > bub ? rd - bub : 0.0) * 64.0;
+}
+double pmc_write_bytes(const PmcSample& s) {
+  const double wr = static_cast<double>(s.value[kPmcTccWrReq]);
+  const double w64 = static_cast<double>(s.value[kPmcTccWrReq64]);
+  return w64 * 64.0 + (wr > w64 ? wr - w64 : 0.0) * 32.0;
+}
+
+PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
+  PmcRates r;
+  const double dt = (b.mono_ns - a.mono_ns) * 1e-9;
+  if (dt <= 0) return r;
+  r.dt_s = dt;
+  auto d = [&](int i) {
+    return b.value[i] >= a.value[i] ? static_cast<double>(b.value[i] - a.value[i]) : 0.0;
+  };
+  const double cnt = d(kPmcGrbmCount), act = d(kPmcGrbmGuiActive);
+  const double cu = num_cu > 0 ? num_cu : 256;
+  if (cnt > 0) r.gpu_active_pct = 100.0 * act / cnt;
+  if (act > 0) {
+    r.mfma_util_pct = 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0);
+    r.cu_busy_pct = 100.0 * 4.0 * d(kPmcSqBusyCu) / (act * cu);
+  }
+  r.hbm_read_Bps = (pmc_read_bytes(b) - pmc_read_bytes(a)) / dt;
+  r.hbm_write_Bps = (pmc_write_bytes(b) - pmc_write_bytes(a)) / dt;
+  if (r.hbm_read_Bps < 0) r.hbm_read_Bps = 0;
+  if (r.hbm_write_Bps < 0) r.hbm_write_Bps = 0;
+  r.gpu_clock_mhz = cnt / dt * 1e-6;
+  return r;
+}
+
+namespace {
+
+class MockCounterSource final : public CounterSource {
+ public:
+  MockCounterSource(const MockConfig& b, const MockPmcConfig& c) : b_(b), c_(c), t0_(mono_ns()) {}
+  std::string name() const override { return "mock"; }
+  int sample(int dev, PmcSample& s) override {
+    const int64_t now = mono_ns();
+    const double t = (now - t0_) * 1e-9;
+    const double w = 6.283185307179586 / b_.util_period_s, ph = 0.7 * dev;
+    // ∫ util/100 dt  (fraction-seconds)
+    const double busy_s = (b_.util_base * t + b_.util_amp / w * (std::cos(ph) - std::cos(w * t + ph))) / 100.0;
+    const double clk = c_.clock_mhz * 1e6;
+    s.n = kPmcCount;
+    s.value[kPmcGrbmCount] = static_cast<uint64_t>(clk * t);
+    s.value[kPmcGrbmGuiActive] = static_cast<uint64_t>(clk * busy_s);
+    s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
+    s.value[kPmcSqBusyCu] = static_cast<uint64_t>(clk * busy_s * 256.0 / 4.0);
+    s.value[kPmcTccBubble] = static_cast<uint64_t>(c_.read_Bps * busy_s / 128.0);
+    s.value[kPmcTccRdReq] = s.value[kPmcTccBubble];
+    s.value[kPmcTccWrReq64] = static_cast<uint64_t>(c_.write_Bps * busy_s / 64.0);
+    s.value[kPmcTccWrReq] = s.value[kPmcTccWrReq64];
+    s.mono_ns = now;
+    s.read_ns = 1000;
+    return 0;
+  }
+
+ private:
+  MockConfig b_;
+  MockPmcConfig c_;
+  int64_t t0_;
+};
+
+// --- dlopen bridge -------------------------------------------------------
+using init_fn = int (*)(char*, int);
+using open_fn = int (*)(uint64_t, const char* const*, const int*, int, char*, int);
+using sample_fn = int (*)(int, uint64_t*, int, uint32_t*);
+using close_fn = void (*)(int);
+
+class DlCounterSource final : public CounterSource {
+ public:
+  ~DlCounterSource() override {
+    if (close_)
+      for (int h : handles_)
+        if (h >= 0) close_(h);
+    // The library stays loaded: HSA/rocprofiler must not be unloaded mid-process.
+  }
+
+  bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, std::string& err) {
+    lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!lib_) {
+      err = std::string("dlopen failed: ") + dlerror();
+      return false;
+    }
+    auto init = reinterpret_cast<init_fn>(dlsym(lib_, "kgs_pmc_init"));
+    open_ = reinterpret_cast<open_fn>(dlsym(lib_, "kgs_pmc_open"));
+    sample_ = reinterpret_cast<sample_fn>(dlsym(lib_, "kgs_pmc_sample"));
+    close_ = reinterpret_cast<close_fn>(dlsym(lib_, "kgs_pmc_close"));
+    if (!init || !open_ || !sample_ || !close_) {
+      err = "libkgs_pmc.so: missing symbols";
+      return false;
+    }
+    char ebuf[512] = {};
+    if (init(ebuf, sizeof ebuf) != 0) {
+      err = std::string("kgs_pmc_init: ") + ebuf;
+      return false;
+    }
+    const char* names[kPmcCount];
+    int is_max[kPmcCount];
+    for (int i = 0; i < kPmcCount; ++i) {
+      names[i] = kNames[i];
+      is_max[i] = pmc_counter_is_max(i) ? 1 : 0;
+    }
+    int opened = 0;
+    handles_.assign(static_cast<size_t>(be.device_count()), -1);
+    for (int d : devices) {
+      ebuf[0] = 0;
+      const int h = open_(be.info(d).kfd_gpu_id, names, is_max, kPmcCount, ebuf, sizeof ebuf);
+      handles_[static_cast<size_t>(d)] = h;
+      if (h >= 0) ++opened;
+      else err += "dev" + std::to_string(d) + ": " + ebuf + "; ";
+    }
+    return opened > 0;
+  }
+
+  std::string name() const override { return "rocprofiler"; }
+
+  int sample(int dev, PmcSample& s) override {
+    if (dev < 0 || dev >= static_cast<int>(handles_.size()) || handles_[dev] < 0) return -1;
+    uint32_t rns = 0;
+    const int rc = sample_(handles_[dev], s.value, kPmcCount, &rns);
+    if (rc != 0) return rc;
+    s.n = kPmcCount;
+    s.read_ns = rns;
+    s.mono_ns = mono_ns();
+    return 0;
+  }
+
+ private:
+  void* lib_ = nullptr;
+  open_fn open_ = nullptr;
+  sample_fn sample_ = nullptr;
+  close_fn close_ = nullptr;
+  std::vector<int> handles_;
+};
+
+}  // namespace
+
+std::unique_ptr<CounterSource> make_mock_counter_source(const Backend&, const MockConfig& bcfg,
+                                                        const MockPmcConfig& cfg) {
+  return std::make_unique<MockCounterSource>(bcfg, cfg);
+}
+
+std::unique_ptr<CounterSource> make_rocprofiler_counter_source(const std::string& lib_path, const Backend& be,
+                                                               const std::vector<int>& devices, std::string& err) {
+  auto s = std::make_unique<DlCounterSource>();
+  if (!s->load(lib_path, be, devices, err)) return nullptr;
+  return s;
+}
+
+}  // namespace kgs

@@ -1,0 +1,417 @@
+// Prometheus text-format (0.0.4) renderer for the node exporter.
+//
+// The reference's report consumes `container_gpu_sm_util` grouped by
+// (kubernetes_io_hostname, nvidia_gpu_type, pod_name)
+// (reference gpu_util_stats/gpu_util_stats.py:159); that series is emitted with
+// exactly those label keys plus namespace/container/gpu/uuid, which the
+// reference's `avg ... by` averages away.  Everything else is
+// the amdgpu_* / kgs_* families documented in models/schema.py.
+#include <charconv>
+#include <cmath>
+#include <cstring>
+#include <ctime>
+
+#include "kgs/exporter.h"
+
+namespace kgs {
+
+void append_label_value(std::string& out, const std::string& v) {
+  for (char c : v) {
+    switch (c) {
+      case '\\': out += "\\\\"; break;
+      case '"': out += "\\\""; break;
+      case '\n': out += "\\n"; break;
+      default: out += c;
+    }
+  }
+}
+
+namespace {
+
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+// Small append-only writer; numbers go through std::to_chars (shortest
+// round-trip form) so the hot path never touches locale-dependent printf.
+struct W {
+  std::string& o;
+  void num(double v) {
+    if (std::isnan(v)) { o += "NaN"; return; }
+    if (std::isinf(v)) { o += v > 0 ? "+Inf" : "-Inf"; return; }
+    char b[40];
+    auto r = std::to_chars(b, b + sizeof b, v);
+    o.append(b, r.ptr);
+  }
+  void u64(uint64_t v) {
+    char b[24];
+    auto r = std::to_chars(b, b + sizeof b, v);
+    o.append(b, r.ptr);
+  }
+  void head(const char* name, const char* type, const char* help) {
+    o += "# HELP "; o += name; o += ' '; o += help; o += "\n# TYPE "; o += name; o += ' '; o += type; o += '\n';
+  }
+  // name{base,extra} value
+  void line(const char* name, const std::string& base, const char* extra, double v) {
+    o += name; o += '{'; o += base;
+    if (extra && *extra) { o += ','; o += extra; }
+    o += "} "; num(v); o += '\n';
+  }
+  void line_u(const char* name, const std::string& base, const char* extra, uint64_t v) {
+    o += name; o += '{'; o += base;
+    if (extra && *extra) { o += ','; o += extra; }
+    o += "} "; u64(v); o += '\n';
+  }
+};
+
+void kv(std::string& o, const char* k, const std::string& v, bool comma = true) {
+  if (comma) o += ',';
+  o += k; o += "=\""; append_label_value(o, v); o += '"';
+}
+
+}  // namespace
+
+void Exporter::render(std::string& out) {
+  const int64_t t0 = mono_ns();
+  out.clear();
+  out.reserve(64 * 1024);
+  W w{out};
+  Sampler& S = *sampler_;
+  const int nd = S.device_count();
+  const std::vector<int>& ids = S.sampled_devices();
+  std::vector<char> sampled(static_cast<size_t>(nd), 0);
+  for (int d : ids) sampled[static_cast<size_t>(d)] = 1;
+  std::string node;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    node = node_name_;
+  }
+  const auto own = owners();
+  const auto pown = pid_owners();
+  const int64_t now = mono_ns();
+
+  // Snapshot all devices once.
+  struct Snap {
+    bool have = false, busy = false, pmc_have = false, pmc_rates = false;
+    GpuSample s;
+    Integrals I;
+    PmcSample p;
+    PmcRates r;
+    double g = 0, u = 0;
+    int n = 0;
+  };
+  static thread_local std::vector<Snap> snaps;
+  snaps.assign(static_cast<size_t>(nd), Snap{});
+  for (int d : ids) {
+    Snap& x = snaps[static_cast<size_t>(d)];
+    const DeviceState& st = S.state(d);
+    x.have = st.latest.load(x.s);
+    st.integ.load(x.I);
+    x.busy = x.have && S.window_busy(d, cfg_.window_s, x.g, x.u, x.n);
+    x.pmc_have = st.pmc_latest.load(x.p);
+    x.pmc_rates = x.pmc_have && S.window_pmc(d, cfg_.window_s, x.r);
+  }
+
+  // ---- reference-compatible series (F5) ---------------------------------
+  if (cfg_.compat_series) {
+    w.head("container_gpu_sm_util", "gauge",
+           "GFX-engine (compute) busy percent of the GPU allocated to the pod, averaged over the exporter window "
+           "(reference metric contract; label nvidia_gpu_type kept for compatibility)");
+    for (int d : ids) {
+      const Snap& x = snaps[static_cast<size_t>(d)];
+      if (!x.busy) continue;
+      const DeviceInfo& in = be_->info(d);
+      const std::string type = cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override;
+      auto emit = [&](const Owner* o) {
+        std::string lb;
+        lb.reserve(256);
+        kv(lb, "kubernetes_io_hostname", node, false);
+        kv(lb, "nvidia_gpu_type", type);
+        kv(lb, "pod_name", o ? o->pod : std::string());
+        kv(lb, "namespace", o ? o->ns : std::string());
+        kv(lb, "container_name", o ? o->container : std::string());
+        kv(lb, "gpu", std::to_string(d));
+        kv(lb, "uuid", in.uuid);
+        w.line("container_gpu_sm_util", lb, nullptr, x.g);
+      };
+      auto it = own ? own->find(d) : decltype(own->end()){};
+      if (own && it != own->end() && !it->second.empty()) {
+        for (const Owner& o : it->second) emit(&o);
+      } else if (cfg_.compat_unallocated) {
+        emit(nullptr);
+      }
+    }
+  }
+
+  // ---- device info / topology -------------------------------------------
+  w.head("amdgpu_device_info", "gauge", "Static device information (value is always 1)");
+  for (int d : ids) {
+    const DeviceInfo& in = be_->info(d);
+    std::string lb = dev_labels_[static_cast<size_t>(d)];
+    kv(lb, "serial", in.serial);
+    kv(lb, "market_name", in.market_name);
+    kv(lb, "gfx_target", in.gfx_target);
+    kv(lb, "numa_node", std::to_string(in.numa_node));
+    kv(lb, "num_cu", std::to_string(in.num_cu));
+    kv(lb, "num_xcc", std::to_string(in.num_xcc));
+    kv(lb, "kfd_gpu_id", std::to_string(in.kfd_gpu_id));
+    kv(lb, "hip_id", std::to_string(in.hip_id));
+    w.line("amdgpu_device_info", lb, nullptr, 1);
+  }
+  if (!topo_.empty()) {
+    w.head("amdgpu_topology_link", "gauge", "Pairwise link between visible GPUs (1); labels carry type/hops/weight");
+    for (const TopoEdge& e : topo_) {
+      if (!sampled[static_cast<size_t>(e.src)]) continue;
+      std::string lb = dev_labels_[static_cast<size_t>(e.src)];
+      kv(lb, "peer_gpu", std::to_string(e.dst));
+      kv(lb, "peer_bdf", be_->info(e.dst).bdf);
+      kv(lb, "link_type", e.link_type == 2 ? "xgmi" : (e.link_type == 1 ? "pcie" : "other"));
+      kv(lb, "hops", std::to_string(e.hops));
+      kv(lb, "weight", std::to_string(e.weight));
+      w.line("amdgpu_topology_link", lb, nullptr, 1);
+    }
+  }
+
+  // ---- utilisation -------------------------------------------------------
+  w.head("amdgpu_gfx_busy_percent", "gauge", "GFX-engine busy percent, time-weighted mean over the exporter window (PMFW accumulators)");
+  for (int d : ids) if (snaps[d].busy) w.line("amdgpu_gfx_busy_percent", dev_labels_[d], nullptr, snaps[d].g);
+  w.head("amdgpu_gfx_busy_instant_percent", "gauge", "GFX-engine busy percent in the latest PMFW table");
+  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFGfxBusy)) w.line("amdgpu_gfx_busy_instant_percent", dev_labels_[d], nullptr, snaps[d].s.gfx_busy_pct);
+  w.head("amdgpu_gfx_busy_xcc_percent", "gauge", "Instantaneous busy percent per XCC (accelerator complex die)");
+  for (int d : ids) {
+    const Snap& x = snaps[d];
+    if (!x.have || !(x.s.valid & kFGfxBusyXcc)) continue;
+    for (uint32_t c = 0; c < x.s.num_xcc && c < static_cast<uint32_t>(kMaxXcc); ++c) {
+      char e[24];
+      std::snprintf(e, sizeof e, "xcc=\"%u\"", c);
+      w.line("amdgpu_gfx_busy_xcc_percent", dev_labels_[d], e, x.s.gfx_busy_xcc[c]);
+    }
+  }
+  w.head("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller (UMC) activity percent, mean over the exporter window");
+  for (int d : ids) if (snaps[d].busy) w.line("amdgpu_umc_busy_percent", dev_labels_[d], nullptr, snaps[d].u);
+  w.head("amdgpu_gfx_busy_seconds_total", "counter", "Integral of GFX busy fraction over firmware time; rate() gives exact mean utilisation");
+  for (int d : ids) if (snaps[d].have) w.line("amdgpu_gfx_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.gfx_busy_seconds);
+  w.head("amdgpu_umc_busy_seconds_total", "counter", "Integral of UMC busy fraction over firmware time");
+  for (int d : ids) if (snaps[d].have) w.line("amdgpu_umc_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds);
+
+  // ---- memory ------------------------------------------------------------
+  w.head("amdgpu_hbm_used_bytes", "gauge", "HBM3E bytes in use");
+  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFVram)) w.line_u("amdgpu_hbm_used_bytes", dev_labels_[d], nullptr, snaps[d].s.vram_used_bytes);
+  w.head("amdgpu_hbm_total_bytes", "gauge", "HBM3E capacity in bytes");
+  for (int d : ids) w.line_u("amdgpu_hbm_total_bytes", dev_labels_[d], nullptr, be_->info(d).vram_total_bytes);
+
+  // ---- thermals / power / clocks ----------------------------------------
+  w.head("amdgpu_temperature_celsius", "gauge", "Temperature by sensor");
+  for (int d : ids) {
+    const Snap& x = snaps[d];
+    if (!x.have) continue;
+    if (x.s.valid & kFTempHotspot) w.line("amdgpu_temperature_celsius", dev_labels_[d], "sensor=\"hotspot\"", x.s.temp_hotspot_c);
+    if (x.s.valid & kFTempMem) w.line("amdgpu_temperature_celsius", dev_labels_[d], "sensor=\"hbm\"", x.s.temp_mem_c);
+    if (x.s.valid & kFTempVrSoc) w.line("amdgpu_temperature_celsius", dev_labels_[d], "sensor=\"vrsoc\"", x.s.temp_vrsoc_c);
+  }
+  w.head("amdgpu_power_watts", "gauge", "Socket power in watts");
+  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPower)) w.line("amdgpu_power_watts", dev_labels_[d], nullptr, snaps[d].s.power_w);
+  w.head("amdgpu_energy_joules_total", "counter", "Energy consumed since the exporter started (wrap-safe integration of the PMFW accumulator)");
+  for (int d : ids) if (snaps[d].have) w.line("amdgpu_energy_joules_total", dev_labels_[d], nullptr, snaps[d].I.energy_joules);
+  w.head("amdgpu_clock_mhz", "gauge", "Current clock frequency (gfx = mean over XCCs)");
+  for (int d : ids) {
+    const Snap& x = snaps[d];
+    if (!x.have) continue;
+    if (x.s.valid & kFGfxClk) {
+      double sum = 0;
+      int n = 0;
+      for (int c = 0; c < kMaxXcc; ++c)
+        if (x.s.gfxclk_mhz[c]) { sum += x.s.gfxclk_mhz[c]; ++n; }
+      if (n) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"gfx\"", sum / n);
+    }
+    if (x.s.valid & kFUclk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"mem\"", x.s.uclk_mhz);
+    if (x.s.valid & kFSocClk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"soc\"", x.s.socclk_mhz);
+  }
+  w.head("amdgpu_power_throttle_residency_total", "counter", "PMFW package-power-tracking throttle residency accumulator (raw)");
+  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFThrottle)) w.line_u("amdgpu_power_throttle_residency_total", dev_labels_[d], nullptr, snaps[d].s.ppt_residency_acc);
+
+  // ---- interconnect ------------------------------------------------------
+  w.head("amdgpu_xgmi_read_bytes_total", "counter", "Bytes received per xGMI link (PMFW accumulator)");
+  for (int d : ids) {
+    const Snap& x = snaps[d];
+    if (!x.have || !(x.s.valid & kFXgmi)) continue;
+    for (int l = 0; l < kMaxXgmi; ++l) {
+      if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
+      char e[24];
+      std::snprintf(e, sizeof e, "link=\"%d\"", l);
+      w.line_u("amdgpu_xgmi_read_bytes_total", dev_labels_[d], e, x.s.xgmi_read_kb[l] * 1024ull);
+    }
+  }
+  w.head("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link (PMFW accumulator)");
+  for (int d : ids) {
+    const Snap& x = snaps[d];
+    if (!x.have || !(x.s.valid & kFXgmi)) continue;
+    for (int l = 0; l < kMaxXgmi; ++l) {
+      if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
+      char e[24];
+      std::snprintf(e, sizeof e, "link=\"%d\"", l);
+      w.line_u("amdgpu_xgmi_write_bytes_total", dev_labels_[d], e, x.s.xgmi_write_kb[l] * 1024ull);
+    }
+  }
+  w.head("amdgpu_xgmi_link_up", "gauge", "xGMI link status per port (1 up, 0 down)");
+  for (int d : ids) {
+    const Snap& x = snaps[d];
+    if (!x.have || !(x.s.valid & kFXgmi)) continue;
+    for (int l = 0; l < kMaxXgmi; ++l) {
+      if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
+      char e[24];
+      std::snprintf(e, sizeof e, "link=\"%d\"", l);
+      w.line("amdgpu_xgmi_link_up", dev_labels_[d], e, x.s.xgmi_link_up[l] ? 1 : 0);
+    }
+  }
+  w.head("amdgpu_xgmi_link_info", "gauge", "Per-link peer and speed (slow tier, value 1)");
+  for (int d : ids) {
+    auto links = S.state(d).get_links();
+    if (!links) continue;
+    for (const LinkInfo& li : *links) {
+      std::string lb = dev_labels_[d];
+      kv(lb, "link", std::to_string(li.link));
+      kv(lb, "peer_bdf", li.peer_bdf);
+      kv(lb, "link_type", li.link_type == 2 ? "xgmi" : (li.link_type == 1 ? "pcie" : "other"));
+      kv(lb, "bit_rate_gbps", std::to_string(li.bit_rate_gbps));
+      kv(lb, "max_bandwidth_gbps", std::to_string(li.max_bw_gbps));
+      w.line("amdgpu_xgmi_link_info", lb, nullptr, 1);
+    }
+  }
+  w.head("amdgpu_pcie_bandwidth_bytes_total", "counter", "PCIe accumulated bandwidth from the PMFW table (GB granularity)");
+  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPcie)) w.line_u("amdgpu_pcie_bandwidth_bytes_total", dev_labels_[d], nullptr, snaps[d].s.pcie_bw_acc_gb * 1000000000ull);
+
+  // ---- hardware counters (PMC tier) ----------------------------------------
+  bool any_pmc = false;
+  for (int d : ids) any_pmc |= snaps[d].pmc_have;
+  if (any_pmc) {
+    w.head("amdgpu_pmc_total", "counter", "Raw hardware counter (rocprofiler-sdk device counting), cumulative since exporter start");
+    for (int d : ids) {
+      const Snap& x = snaps[d];
+      if (!x.pmc_have) continue;
+      for (int i = 0; i < kPmcCount; ++i) {
+        std::string e = "counter=\"";
+        e += pmc_counter_name(i);
+        e += '"';
+        w.line_u("amdgpu_pmc_total", dev_labels_[d], e.c_str(), x.p.value[i]);
+      }
+    }
+    w.head("amdgpu_hbm_read_bytes_total", "counter", "HBM bytes read (TCC→EA requests)");
+    for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_hbm_read_bytes_total", dev_labels_[d], nullptr, pmc_read_bytes(snaps[d].p));
+    w.head("amdgpu_hbm_write_bytes_total", "counter", "HBM bytes written (TCC→EA requests)");
+    for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_hbm_write_bytes_total", dev_labels_[d], nullptr, pmc_write_bytes(snaps[d].p));
+    w.head("amdgpu_mfma_util_percent", "gauge", "Matrix-core (MFMA) busy percent of active cycles over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
+    w.head("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active percent of clocks over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
+    w.head("amdgpu_cu_busy_percent", "gauge", "CU busy percent of active cycles over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_cu_busy_percent", dev_labels_[d], nullptr, snaps[d].r.cu_busy_pct);
+    w.head("amdgpu_hbm_read_bytes_per_second", "gauge", "HBM read bandwidth over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_hbm_read_bytes_per_second", dev_labels_[d], nullptr, snaps[d].r.hbm_read_Bps);
+    w.head("amdgpu_hbm_write_bytes_per_second", "gauge", "HBM write bandwidth over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_hbm_write_bytes_per_second", dev_labels_[d], nullptr, snaps[d].r.hbm_write_Bps);
+  }
+
+  // ---- per-process attribution ------------------------------------------
+  if (cfg_.per_process) {
+    w.head("amdgpu_process_hbm_bytes", "gauge", "HBM bytes held by a process, attributed to its pod when known");
+    std::string tmp;
+    auto proc_labels = [&](int d, const ProcInfo& p) {
+      std::string lb = dev_labels_[d];
+      kv(lb, "pid", std::to_string(p.pid));
+      kv(lb, "process", p.name);
+      const PidOwner* po = nullptr;
+      if (pown) {
+        auto it = pown->find(p.pid);
+        if (it != pown->end()) po = &it->second;
+      }
+      kv(lb, "pod", po ? po->pod : std::string());
+      kv(lb, "namespace", po ? po->ns : std::string());
+      kv(lb, "container", po ? po->container : std::string());
+      kv(lb, "pod_uid", po ? po->pod_uid : std::string());
+      return lb;
+    };
+    std::vector<std::shared_ptr<const std::vector<ProcInfo>>> procs(static_cast<size_t>(nd));
+    for (int d : ids) procs[d] = S.state(d).get_procs();
+    for (int d : ids)
+      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line_u("amdgpu_process_hbm_bytes", proc_labels(d, p), nullptr, p.vram_bytes);
+    w.head("amdgpu_process_gtt_bytes", "gauge", "GTT (host-mapped) bytes held by a process");
+    for (int d : ids)
+      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line_u("amdgpu_process_gtt_bytes", proc_labels(d, p), nullptr, p.gtt_bytes);
+    w.head("amdgpu_process_cu_occupancy", "gauge", "Compute units occupied by the process' waves");
+    for (int d : ids)
+      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line_u("amdgpu_process_cu_occupancy", proc_labels(d, p), nullptr, p.cu_occupancy);
+    w.head("amdgpu_process_gfx_seconds_total", "counter", "GFX engine time consumed by the process (driver-reported; 0 where unsupported)");
+    for (int d : ids)
+      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line("amdgpu_process_gfx_seconds_total", proc_labels(d, p), nullptr, p.gfx_ns * 1e-9);
+  }
+
+  // ---- self metrics ------------------------------------------------------
+  w.head("kgs_up", "gauge", "1 if the device's last sampler read succeeded");
+  for (int d : ids) w.line("kgs_up", dev_labels_[d], nullptr, S.state(d).up.load());
+  w.head("kgs_last_sample_age_seconds", "gauge", "Seconds since the last successful read");
+  for (int d : ids) {
+    const int64_t t = S.state(d).last_ok_mono_ns.load();
+    w.line("kgs_last_sample_age_seconds", dev_labels_[d], nullptr, t ? (now - t) * 1e-9 : -1.0);
+  }
+  w.head("kgs_samples_total", "counter", "Distinct hardware samples (new PMFW firmware timestamp)");
+  for (int d : ids) w.line_u("kgs_samples_total", dev_labels_[d], nullptr, snaps[d].I.distinct_samples);
+  w.head("kgs_reads_total", "counter", "Sampler reads attempted");
+  for (int d : ids) w.line_u("kgs_reads_total", dev_labels_[d], nullptr, snaps[d].I.reads);
+  w.head("kgs_read_errors_total", "counter", "Sampler reads that failed");
+  for (int d : ids) w.line_u("kgs_read_errors_total", dev_labels_[d], nullptr, snaps[d].I.read_errors);
+  w.head("kgs_sampler_overruns_total", "counter", "Ticks whose work overran the sampling period");
+  for (int d : ids) w.line_u("kgs_sampler_overruns_total", dev_labels_[d], nullptr, snaps[d].I.overruns);
+  w.head("kgs_pmc_samples_total", "counter", "Hardware-counter drains completed");
+  for (int d : ids) w.line_u("kgs_pmc_samples_total", dev_labels_[d], nullptr, snaps[d].I.pmc_samples);
+  w.head("kgs_pmc_errors_total", "counter", "Hardware-counter drains that failed");
+  for (int d : ids) w.line_u("kgs_pmc_errors_total", dev_labels_[d], nullptr, snaps[d].I.pmc_errors);
+  w.head("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples");
+  for (int d : ids) w.line("kgs_sampled_seconds_total", dev_labels_[d], nullptr, snaps[d].I.sampled_seconds);
+  w.head("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read");
+  for (int d : ids) {
+    const DeviceState& st = S.state(d);
+    uint64_t cum = 0;
+    for (int b = 0; b <= kReadHistBuckets; ++b) {
+      cum += st.read_hist[b].load(std::memory_order_relaxed);
+      std::string e = "le=\"";
+      if (b < kReadHistBuckets) {
+        char nb[32];
+        auto r = std::to_chars(nb, nb + sizeof nb, kReadHistBoundsUs[b] * 1e-6);
+        e.append(nb, r.ptr);
+      } else {
+        e += "+Inf";
+      }
+      e += '"';
+      w.line_u("kgs_sample_read_seconds_bucket", dev_labels_[d], e.c_str(), cum);
+    }
+    w.line("kgs_sample_read_seconds_sum", dev_labels_[d], nullptr, snaps[d].I.read_seconds);
+    w.line_u("kgs_sample_read_seconds_count", dev_labels_[d], nullptr, cum);
+  }
+  std::string nl;
+  kv(nl, "kubernetes_io_hostname", node, false);
+  w.head("kgs_scrapes_total", "counter", "Scrapes rendered");
+  w.line_u("kgs_scrapes_total", nl, nullptr, scrapes.load() + 1);
+  w.head("kgs_scrape_render_seconds_total", "counter", "Total time spent rendering /metrics");
+  w.line("kgs_scrape_render_seconds_total", nl, nullptr, render_ns_total.load() * 1e-9);
+  w.head("kgs_scrape_render_last_seconds", "gauge", "Render time of the previous scrape");
+  w.line("kgs_scrape_render_last_seconds", nl, nullptr, render_ns_last.load() * 1e-9);
+  w.head("kgs_build_info", "gauge", "Exporter build / configuration (value 1)");
+  {
+    std::string lb = nl;
+    kv(lb, "version", "0.1.0");
+    kv(lb, "backend", be_->name());
+    kv(lb, "pmc_source", pmc_ ? pmc_->name() : std::string("none"));
+    kv(lb, "sample_hz", std::to_string(S.config().hz));
+    w.line("kgs_build_info", lb, nullptr, 1);
+  }
+
+  const int64_t dt = mono_ns() - t0;
+  scrapes.fetch_add(1);
+  render_ns_total.fetch_add(static_cast<uint64_t>(dt));
+  render_ns_last.store(static_cast<uint64_t>(dt));
+}
+
+}  // namespace kgs

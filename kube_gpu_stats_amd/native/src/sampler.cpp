@@ -1,0 +1,295 @@
+// Per-GPU sampler threads.  See sampler.h.
+#include "kgs/sampler.h"
+
+#include <pthread.h>
+#include <sched.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+
+namespace kgs {
+
+const double kReadHistBoundsUs[kReadHistBuckets] = {10, 25, 50, 100, 250, 500, 1000, 2500, 5000, 10000, 25000, 100000};
+
+namespace {
+
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+// Delta of a PMFW accumulator that the v1.8 table stores in 32 bits.
+bool acc_delta(uint64_t prev, uint64_t cur, uint64_t& d) {
+  if (cur >= prev) {
+    d = cur - prev;
+    return true;
+  }
+  if (prev <= 0xFFFFFFFFull && cur <= 0xFFFFFFFFull) {
+    d = cur + 0x100000000ull - prev;
+    return true;
+  }
+  return false;  // counter reset
+}
+
+}  // namespace
+
+std::vector<int> numa_cpus(int node) {
+  std::vector<int> cpus;
+  if (node < 0) return cpus;
+  char path[128];
+  std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return cpus;
+  char buf[4096];
+  size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  char* p = buf;
+  while (*p) {
+    char* end;
+    long a = std::strtol(p, &end, 10);
+    if (end == p) break;
+    long b = a;
+    p = end;
+    if (*p == '-') {
+      b = std::strtol(p + 1, &end, 10);
+      p = end;
+    }
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) cpus.push_back(static_cast<int>(c));
+    while (*p == ',' || *p == '\n' || *p == ' ') ++p;
+  }
+  return cpus;
+}
+
+Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), pmc_(pmc), cfg_(std::move(cfg)) {
+  const int n = be_->device_count();
+  for (int d = 0; d < n; ++d) states_.push_back(std::make_unique<DeviceState>());
+  if (cfg_.devices.empty()) {
+    for (int d = 0; d < n; ++d) dev_ids_.push_back(d);
+  } else {
+    for (int d : cfg_.devices)
+      if (d >= 0 && d < n) dev_ids_.push_back(d);
+  }
+  if (cfg_.hz <= 0) cfg_.hz = 1;
+}
+
+Sampler::~Sampler() { stop(); }
+
+void Sampler::start() {
+  if (running_.exchange(true)) return;
+  stop_.store(false);
+  for (int d : dev_ids_) threads_.emplace_back([this, d] { run(d); });
+}
+
+void Sampler::stop() {
+  if (!running_.load()) return;
+  {
+    std::lock_guard<std::mutex> g(cv_mu_);
+    stop_.store(true);
+  }
+  cv_.notify_all();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+  running_.store(false);
+}
+
+void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integrals& I) {
+  (void)dev;
+  if (!prev) return;
+  double dt;
+  if ((cur.valid & kFFwTs) && (prev->valid & kFFwTs) && cur.fw_ts > prev->fw_ts)
+    dt = static_cast<double>(cur.fw_ts - prev->fw_ts) * 1e-8;
+  else
+    dt = static_cast<double>(cur.mono_ns - prev->mono_ns) * 1e-9;
+  if (dt <= 0 || dt > 3600) return;
+  cur.dt_s = static_cast<float>(dt);
+
+  double g = cur.gfx_busy_pct, u = cur.umc_busy_pct;
+  uint64_t dc, dg, du;
+  if ((cur.valid & kFAcc) && (prev->valid & kFAcc) &&
+      acc_delta(prev->accumulation_counter, cur.accumulation_counter, dc) && dc > 0 &&
+      acc_delta(prev->gfx_activity_acc, cur.gfx_activity_acc, dg) &&
+      acc_delta(prev->mem_activity_acc, cur.mem_activity_acc, du)) {
+    g = static_cast<double>(dg) / static_cast<double>(dc);
+    u = static_cast<double>(du) / static_cast<double>(dc);
+  }
+  g = g < 0 ? 0 : (g > 100 ? 100 : g);
+  u = u < 0 ? 0 : (u > 100 ? 100 : u);
+  cur.gfx_busy_window_pct = static_cast<float>(g);
+  cur.umc_busy_window_pct = static_cast<float>(u);
+  I.gfx_busy_seconds += g * 0.01 * dt;
+  I.umc_busy_seconds += u * 0.01 * dt;
+  I.sampled_seconds += dt;
+  if ((cur.valid & kFEnergy) && (prev->valid & kFEnergy) && cur.energy_acc >= prev->energy_acc)
+    I.energy_joules += energy_units_to_joules(cur.energy_acc - prev->energy_acc);
+}
+
+void Sampler::run(int dev) {
+  DeviceState& st = *states_[dev];
+  const DeviceInfo& info = be_->info(dev);
+  if (cfg_.pin_numa) {
+    const std::vector<int> cpus = numa_cpus(info.numa_node);
+    if (!cpus.empty()) {
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      for (int c : cpus) CPU_SET(c, &set);
+      if (pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0) st.cpu_pinned.store(static_cast<int>(cpus.size()));
+    }
+  }
+  char tname[16];
+  std::snprintf(tname, sizeof tname, "kgs-gpu%d", dev);
+  pthread_setname_np(pthread_self(), tname);
+
+  const int64_t period_ns = static_cast<int64_t>(1e9 / cfg_.hz);
+  Integrals I;
+  GpuSample prev;
+  bool have_prev = false;
+  uint64_t seq = 0, pmc_seq = 0, tick = 0;
+  int64_t next = mono_ns();
+  std::vector<ProcInfo> procs;
+  std::vector<LinkInfo> links;
+
+  while (!stop_.load(std::memory_order_relaxed)) {
+    // ---- fast tier -----------------------------------------------------
+    GpuSample s;
+    const int64_t t0 = mono_ns();
+    const int rc = be_->read_metrics(dev, s);
+    const int64_t t1 = mono_ns();
+    const double us = (t1 - t0) * 1e-3;
+    int b = 0;
+    while (b < kReadHistBuckets && us > kReadHistBoundsUs[b]) ++b;
+    st.read_hist[b].fetch_add(1, std::memory_order_relaxed);
+    ++I.reads;
+    I.read_seconds += (t1 - t0) * 1e-9;
+    int backoff_shift = 0;
+    if (rc == 0) {
+      s.read_ns = static_cast<uint32_t>(t1 - t0);
+      if (s.mono_ns == 0) s.mono_ns = t1;
+      st.up.store(1, std::memory_order_relaxed);
+      st.consecutive_errors.store(0, std::memory_order_relaxed);
+      st.last_ok_mono_ns.store(t1, std::memory_order_relaxed);
+      const bool distinct = !have_prev || !(s.valid & kFFwTs) || s.fw_ts != prev.fw_ts;
+      if (distinct) {
+        integrate(dev, have_prev ? &prev : nullptr, s, I);
+        s.seq = ++seq;
+        ++I.distinct_samples;
+        st.ring.push(s);
+        st.latest.store(s);
+        prev = s;
+        have_prev = true;
+      } else {
+        // Same PMFW table: refresh host-side fields only (HBM occupancy).
+        prev.vram_used_bytes = s.vram_used_bytes;
+        prev.mono_ns = s.mono_ns;
+        prev.wall_ns = s.wall_ns;
+        st.latest.store(prev);
+      }
+    } else {
+      ++I.read_errors;
+      const uint64_t ce = st.consecutive_errors.fetch_add(1, std::memory_order_relaxed) + 1;
+      if (ce >= 3) st.up.store(0, std::memory_order_relaxed);
+      backoff_shift = ce > 10 ? 10 : static_cast<int>(ce);
+    }
+
+    // ---- PMC tier ------------------------------------------------------
+    if (cfg_.pmc && pmc_) {
+      PmcSample ps;
+      if (pmc_->sample(dev, ps) == 0) {
+        ps.seq = ++pmc_seq;
+        st.pmc_ring.push(ps);
+        st.pmc_latest.store(ps);
+        ++I.pmc_samples;
+      } else {
+        ++I.pmc_errors;
+      }
+    }
+
+    // ---- mid / slow tiers -----------------------------------------------
+    if (cfg_.proc_every > 0 && tick % static_cast<uint64_t>(cfg_.proc_every) == 0) {
+      if (be_->read_procs(dev, procs) == 0) {
+        auto p = std::make_shared<const std::vector<ProcInfo>>(procs);
+        std::lock_guard<std::mutex> g(st.slow_mu);
+        st.procs = std::move(p);
+        st.procs_mono_ns = mono_ns();
+      }
+    }
+    if (cfg_.link_every > 0 && tick % static_cast<uint64_t>(cfg_.link_every) == 0) {
+      if (be_->read_links(dev, links) == 0) {
+        auto l = std::make_shared<const std::vector<LinkInfo>>(links);
+        std::lock_guard<std::mutex> g(st.slow_mu);
+        st.links = std::move(l);
+      }
+    }
+    ++tick;
+
+    // ---- schedule --------------------------------------------------------
+    int64_t step = period_ns;
+    if (backoff_shift > 0) {
+      step = period_ns << backoff_shift;
+      const int64_t cap = static_cast<int64_t>(cfg_.max_backoff_ms) * 1000000LL;
+      if (step > cap) step = cap > period_ns ? cap : period_ns;
+    }
+    next += step;
+    const int64_t now = mono_ns();
+    if (next <= now) {
+      ++I.overruns;
+      next = now + (backoff_shift ? step : 0);
+      if (next <= now) next = now + period_ns / 4;  // never spin
+    }
+    st.integ.store(I);
+    std::unique_lock<std::mutex> lk(cv_mu_);
+    cv_.wait_for(lk, std::chrono::nanoseconds(next - now), [this] { return stop_.load(); });
+  }
+  st.integ.store(I);
+}
+
+bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, int& n) const {
+  static thread_local std::vector<GpuSample> buf(kRing);
+  const DeviceState& st = *states_[dev];
+  const size_t got = st.ring.recent(buf.data(), kRing);
+  double wsum = 0, g = 0, u = 0;
+  n = 0;
+  for (size_t i = 0; i < got; ++i) {
+    const GpuSample& s = buf[i];
+    if (s.dt_s <= 0 || s.gfx_busy_window_pct < 0) continue;
+    g += s.gfx_busy_window_pct * s.dt_s;
+    u += s.umc_busy_window_pct * s.dt_s;
+    wsum += s.dt_s;
+    ++n;
+    if (wsum >= window_s) break;
+  }
+  if (wsum <= 0) {
+    GpuSample s;
+    if (!st.latest.load(s)) return false;
+    gfx = s.gfx_busy_pct;
+    umc = s.umc_busy_pct;
+    n = 1;
+    return true;
+  }
+  gfx = g / wsum;
+  umc = u / wsum;
+  return true;
+}
+
+bool Sampler::window_pmc(int dev, double window_s, PmcRates& out) const {
+  static thread_local std::vector<PmcSample> buf(kRing);
+  const DeviceState& st = *states_[dev];
+  const size_t got = st.pmc_ring.recent(buf.data(), kRing);
+  if (got < 2) return false;
+  const PmcSample& b = buf[0];
+  size_t ai = 1;
+  for (size_t i = 1; i < got; ++i) {
+    ai = i;
+    if ((b.mono_ns - buf[i].mono_ns) * 1e-9 >= window_s) break;
+  }
+  out = pmc_rates(buf[ai], b, be_->info(dev).num_cu);
+  return out.dt_s > 0;
+}
+
+}  // namespace kgs

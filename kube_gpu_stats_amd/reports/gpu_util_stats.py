@@ -1,0 +1,248 @@
+"""``kgs gpu-util-stats`` — daily GPU utilisation accounting (capabilities F2-F4).
+
+Reference: gpu_util_stats/gpu_util_stats.py.
+
+* F2 node inventory (``get_gpu_servers`` :96-127): allocatable cards ⋈ node GPU
+  type label, and cards requested by Running pods, per node.
+* F3 per-pod report (``stats_pod_results`` :62-94 + ``get_pod_by_servers``
+  :129-151 + ``main`` :154-163): mean ``container_gpu_sm_util`` per (node, pod)
+  over the window joined with the pod's card count, for live (Running/Pending)
+  pods of one namespace.
+* F4 per-node report (``stats_server_results`` :36-60, dead code in the
+  reference): time-weighted node utilisation + type + used + total.
+
+``--compat`` issues the reference's five PromQL queries verbatim (M1-M5, in the
+order M1 → M2 → M3 → M4 → M5) and reproduces its arithmetic and
+output exactly, quirks included (Q1 overwrite, Q2 divide-by-range, Q5 first
+sample, Q6 string counts, Q7 finished pods dropped, Q8 JSON dump on stdout).
+The default mode keeps the join semantics but fixes the quirks: server-side
+``avg_over_time`` per step (Q4), max card count (Q5), ints (Q6), series of one
+node combined card-weighted (Q1), time-weighted means with ``--missing`` (Q2/Q3),
+AMD resource/label names, debug output on stderr (Q8).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from dataclasses import dataclass
+from datetime import datetime, timedelta
+
+from ..utils import log
+from ..utils.config import (REF_NAMESPACE, REF_PROM_URL, REF_PROXY, REF_STEP_S, REF_TIMEOUT_S, REF_WINDOW_S,
+                            add_flag)
+from .promql import PromClient, result
+from .table import render, render_csv
+
+L = log.get("gpu_util_stats")
+
+# --------------------------------------------------------------------------- queries
+REF_Q_UTIL = "avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)"  # :159
+REF_Q_TOTAL = ("max(kube_node_status_allocatable_nvidia_gpu_cards * on (instance, node) "
+               "group_left(label_nvidia_gpu_type) kube_node_labels) by (node,label_nvidia_gpu_type)")  # :105
+REF_Q_USED = ('(sum(max(kube_pod_container_resource_requests_nvidia_gpu_devices{node!=""} * on (instance,pod)  '
+              'group_right(node) kube_pod_status_phase{phase="Running"}) by (node,pod)) by (node) > 0) '
+              '* on (node) group_right kube_node_labels')  # :117
+REF_Q_LIVE = 'max(kube_pod_status_phase{namespace="%s",phase=~"Running|Pending"}) by (pod) > 0'  # :133
+REF_Q_REQ = "max(kube_pod_container_resource_requests_nvidia_gpu_devices) by (node, pod)"  # :137
+
+
+@dataclass
+class Queries:
+    util: str
+    total: str
+    used: str
+    live: str
+    req: str
+    type_label: str
+    util_host: str = "kubernetes_io_hostname"
+    util_pod: str = "pod_name"
+
+    @classmethod
+    def compat(cls, namespace: str = REF_NAMESPACE) -> "Queries":
+        return cls(REF_Q_UTIL, REF_Q_TOTAL, REF_Q_USED, REF_Q_LIVE % namespace, REF_Q_REQ, "label_nvidia_gpu_type")
+
+    @classmethod
+    def amd(cls, namespace: str, step_s: int, resource: str = "amd_com_gpu",
+            type_label: str = "label_amd_com_gpu_product_name", util_metric: str = "container_gpu_sm_util") -> "Queries":
+        ns = f'namespace="{namespace}",' if namespace else ""
+        return cls(
+            util=(f"avg(avg_over_time({util_metric}[{step_s}s])) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)"),
+            total=(f'max(kube_node_status_allocatable{{resource="{resource}"}} * on (node) '
+                   f"group_left({type_label}) max(kube_node_labels) by (node, {type_label})) by (node, {type_label})"),
+            used=(f'sum(max(kube_pod_container_resource_requests{{resource="{resource}",node!=""}} '
+                  f'* on (namespace, pod) group_left() max(kube_pod_status_phase{{phase="Running"}}) '
+                  f"by (namespace, pod)) by (node, namespace, pod)) by (node) > 0"),
+            live=f'max(kube_pod_status_phase{{{ns}phase=~"Running|Pending"}}) by (pod) > 0',
+            req=f'max(kube_pod_container_resource_requests{{resource="{resource}"}}) by (node, pod)',
+            type_label=type_label,
+        )
+
+
+# --------------------------------------------------------------------------- collectors (L2)
+def get_gpu_servers(c: PromClient, q: Queries, compat: bool) -> dict[str, tuple]:
+    """{node: (total, used, type)} — reference get_gpu_servers :96-127 (M2, M3)."""
+    server_card, server_total, server_used = {}, {}, {}
+    for res in result(c.query(q.total)):
+        node = res["metric"]["node"]
+        server_card[node] = res["metric"].get(q.type_label, "")
+        server_total[node] = res["value"][1]
+    for res in result(c.query(q.used)):
+        server_used[res["metric"]["node"]] = res["value"][1]
+    out = {}
+    for node in server_total:
+        if compat:  # strings, used defaults to int 0 (:126, Q6)
+            out[node] = (server_total[node], server_used.get(node, 0), server_card.get(node, ""))
+        else:
+            out[node] = (int(float(server_total[node])), int(float(server_used.get(node, 0))),
+                         server_card.get(node, ""))
+    return out
+
+
+def get_pod_by_servers(c: PromClient, q: Queries, start, end, step_s: int, compat: bool,
+                       out=sys.stdout) -> dict[str, dict[str, object]]:
+    """{node: {pod: cards}} for live pods — reference get_pod_by_servers :129-151 (M4, M5)."""
+    live = {m["metric"]["pod"] for m in result(c.query(q.live))}
+    res = {}
+    for m in result(c.query_range(q.req, start, end, step_s)):
+        node = m["metric"].get("node", "<unknown>")
+        pod = m["metric"].get("pod", "<unknown>")
+        if not m.get("values"):
+            continue
+        if compat:
+            val = m["values"][0][1]  # first sample, string (Q5, Q6)
+        else:
+            val = int(max(float(v[1]) for v in m["values"]))
+        if pod not in live:
+            continue
+        res.setdefault(node, {})[pod] = val
+    if compat:
+        print(json.dumps(res, indent=2), file=out)  # :150 (Q8)
+    else:
+        L.debug("live GPU pods: %s", json.dumps(res))
+    return res
+
+
+# --------------------------------------------------------------------------- aggregation (L3)
+def stats_pod_results(util_body: dict, servers: dict, server_pods: dict, compat: bool) -> list[list]:
+    """Reference stats_pod_results :62-94 (F3)."""
+    vals: dict[str, dict[str, float]] = {}
+    for res in result(util_body):
+        server = res["metric"].get("kubernetes_io_hostname", "")
+        pod = res["metric"].get("pod_name", "")
+        v = [float(x[1]) for x in res.get("values", [])]
+        vals.setdefault(server, {})[pod] = sum(v) / len(v) if v else 0.0
+    lines = []
+    for server in sorted(servers):
+        if server not in server_pods and server not in vals:
+            continue
+        pods = set(server_pods.get(server, {})) | set(vals.get(server, {}))
+        for pod in sorted(pods):  # the reference iterates a set (unspecified order); sorted is stable
+            cards = server_pods.get(server, {}).get(pod)
+            if cards is None:  # finished pod with util but no allocation (:87-90, Q7)
+                continue
+            lines.append([server, pod, cards, vals.get(server, {}).get(pod, 0.0)])
+    return lines
+
+
+def stats_server_results(util_body: dict, servers: dict, time_range_s: float, step_s: int, compat: bool,
+                         missing: str = "skip", weights: dict | None = None) -> list[list]:
+    """Per-node report (F4).  Reference stats_server_results :36-60 in compat mode."""
+    if compat:
+        sv = {}
+        for res in result(util_body):
+            sv[res["metric"]["kubernetes_io_hostname"]] = [float(x[1]) for x in res.get("values", [])]  # Q1
+        avg = {s: sum(v) * step_s / time_range_s for s, v in sv.items()}  # Q2/Q3
+        lines = []
+        for server in sorted(servers):
+            total, used, card = servers[server]
+            lines.append([server, card, avg.get(server, 0), used, total])
+        return lines
+    # fixed: combine every series of a node card-weighted per timestamp, then average over time
+    per_node: dict[str, dict[float, list[tuple[float, float]]]] = {}
+    for res in result(util_body):
+        node = res["metric"].get("kubernetes_io_hostname", "")
+        pod = res["metric"].get("pod_name", "")
+        w = float((weights or {}).get(node, {}).get(pod, 1) or 1)
+        for ts, v in res.get("values", []):
+            per_node.setdefault(node, {}).setdefault(float(ts), []).append((float(v), w))
+    n_steps = max(1, int(round(time_range_s / step_s)))
+    lines = []
+    for server in sorted(servers):
+        total, used, card = servers[server]
+        pts = per_node.get(server, {})
+        series = [sum(v * w for v, w in vs) / sum(w for _, w in vs) for vs in pts.values()]
+        if not series:
+            u = 0.0
+        elif missing == "zero":
+            u = sum(series) / max(n_steps, len(series))
+        else:
+            u = sum(series) / len(series)
+        lines.append([server, card, u, used, total])
+    return lines
+
+
+# --------------------------------------------------------------------------- report (L4)
+def run_report(c: PromClient, q: Queries, end: datetime | float, window_s: float, step_s: int, compat: bool,
+               mode: str = "pod", missing: str = "skip", out=sys.stdout) -> list[list]:
+    if isinstance(end, (int, float)):
+        end = datetime.fromtimestamp(end)
+    start = end - timedelta(seconds=window_s)
+    util = c.query_range(q.util, start, end, step_s)                     # M1
+    servers = get_gpu_servers(c, q, compat)                              # M2, M3
+    if mode == "node":
+        pods = None if compat else get_pod_by_servers(c, q, start, end, step_s, compat, out)
+        return stats_server_results(util, servers, window_s, step_s, compat, missing, pods)
+    pods = get_pod_by_servers(c, q, start, end, step_s, compat, out)     # M4, M5
+    return stats_pod_results(util, servers, pods, compat)
+
+
+def format_rows(rows: list[list], mode: str, fmt: str, compat: bool) -> str:
+    if compat:
+        return "\n".join(str(r) for r in rows)  # :162-163 prints each row's repr
+    header = ["Node", "Pod", "GPUs", "Util %"] if mode == "pod" else ["Node", "GPU Type", "Util %", "Used", "Total"]
+    disp = [[*r[:-1], f"{r[-1]:.2f}"] if mode == "pod" else [r[0], r[1], f"{r[2]:.2f}", r[3], r[4]] for r in rows]
+    if fmt == "json":
+        return json.dumps([dict(zip(header, r)) for r in rows], indent=2)
+    if fmt == "csv":
+        return render_csv(header, disp)
+    return render(header, disp)
+
+
+def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.ArgumentParser:
+    ap = ap or argparse.ArgumentParser(prog="kgs gpu-util-stats", description=__doc__.splitlines()[0])
+    add_flag(ap, "compat", False, "reference queries, arithmetic and output, quirks included")
+    add_flag(ap, "prom-url", REF_PROM_URL, "Prometheus HTTP API base URL (…/api/v1)")
+    add_flag(ap, "proxy", "", f"HTTP proxy for every call (reference used {REF_PROXY})")
+    add_flag(ap, "timeout", REF_TIMEOUT_S, "per-request timeout seconds")
+    add_flag(ap, "retries", 0, "retries per request")
+    add_flag(ap, "namespace", REF_NAMESPACE, "namespace of the live-pod filter ('' = all)")
+    add_flag(ap, "window", float(REF_WINDOW_S), "report window seconds (reference: 1 day)")
+    add_flag(ap, "step", REF_STEP_S, "query_range step seconds (reference: 3600)")
+    add_flag(ap, "end", 0.0, "window end as unix seconds (default now)")
+    add_flag(ap, "mode", "pod", "pod (F3) | node (F4)")
+    add_flag(ap, "missing", "skip", "node mode: treat missing samples as skip | zero")
+    add_flag(ap, "resource", "amd_com_gpu", "KSM resource label value of the GPU resource")
+    add_flag(ap, "type-label", "label_amd_com_gpu_product_name", "kube_node_labels label holding the GPU type")
+    add_flag(ap, "util-metric", "container_gpu_sm_util", "utilisation series")
+    add_flag(ap, "format", "table", "table | json | csv")
+    return ap
+
+
+def run(a) -> int:
+    c = PromClient(a.prom_url, a.proxy, a.timeout, a.retries)
+    q = (Queries.compat(a.namespace) if a.compat else
+         Queries.amd(a.namespace, a.step, a.resource, a.type_label, a.util_metric))
+    end = a.end if a.end else (datetime.now() if a.compat else time.time())
+    rows = run_report(c, q, end, a.window, a.step, a.compat, a.mode, a.missing)
+    print(format_rows(rows, a.mode, a.format, a.compat))
+    return 0
+
+
+def main(argv=None) -> int:
+    return run(build_parser().parse_args(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,81 @@
+"""Prometheus HTTP API client (reference transport layer L1).
+
+Reference: ``query_prom`` (gpu_util_stats.py:14-27, ``/query_range``) and
+``query_prom_instant`` (:29-34, ``/query``), plus the two inline instant GETs of
+``get_gpu_servers`` (:103-108, :115-120).  Differences, all deliberate:
+
+* one configured session — the proxy applies to every call (the reference skips
+  it for the instant client, :32 vs :24 — Q9);
+* HTTP and Prometheus-level errors raise ``PromError`` (the reference KeyErrors
+  on ``['data']`` — Q10);
+* optional retries with backoff; the 5 s timeout stays the default (:24).
+"""
+from __future__ import annotations
+
+import time
+from datetime import datetime
+from time import mktime
+
+from ..utils.config import REF_TIMEOUT_S
+
+
+class PromError(RuntimeError):
+    pass
+
+
+def to_unix(t) -> int:
+    """datetime → int seconds the way the reference does it (local-time mktime, :16-17)."""
+    if isinstance(t, datetime):
+        return int(mktime(t.timetuple()))
+    return int(t)
+
+
+class PromClient:
+    def __init__(self, base_url: str, proxy: str = "", timeout_s: float = REF_TIMEOUT_S, retries: int = 0,
+                 session=None):
+        import requests
+
+        self.base_url = base_url.rstrip("/")
+        self.timeout_s = timeout_s
+        self.retries = retries
+        self.s = session or requests.Session()
+        if proxy:
+            self.s.proxies = {"http": proxy, "https": proxy}
+        self.calls: list[tuple[str, dict]] = []
+
+    def _get(self, path: str, params: dict) -> dict:
+        import requests
+
+        url = self.base_url + path
+        last = None
+        for attempt in range(self.retries + 1):
+            try:
+                self.calls.append((path, dict(params)))
+                r = self.s.get(url, params=params, timeout=self.timeout_s)
+                try:
+                    body = r.json()
+                except ValueError as e:
+                    raise PromError(f"{url}: HTTP {r.status_code}, non-JSON body") from e
+                if r.status_code != 200 or body.get("status") != "success":
+                    raise PromError(f"{url}: HTTP {r.status_code} {body.get('errorType', '')}: {body.get('error', '')}")
+                if "data" not in body:
+                    raise PromError(f"{url}: response without data")
+                return body
+            except (requests.RequestException, PromError) as e:
+                last = e
+                if attempt < self.retries:
+                    time.sleep(min(2.0, 0.2 * (2 ** attempt)))
+        raise last if isinstance(last, PromError) else PromError(str(last))
+
+    def query(self, q: str, at=None) -> dict:
+        p = {"query": q}
+        if at is not None:
+            p["time"] = to_unix(at)
+        return self._get("/query", p)
+
+    def query_range(self, q: str, start, end, step_s: int) -> dict:
+        return self._get("/query_range", {"query": q, "start": to_unix(start), "end": to_unix(end), "step": step_s})
+
+
+def result(body: dict) -> list[dict]:
+    return body["data"]["result"]

@@ -1,0 +1,40 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on a GPU box)")
+    config.addinivalue_line("markers", "slow: takes more than a few seconds")
+
+
+@pytest.fixture(scope="session")
+def N():
+    """The compiled native data plane (built in-tree on first use)."""
+    from kube_gpu_stats_amd import load_native
+
+    return load_native()
+
+
+@pytest.fixture
+def mock_exporter(N):
+    made = []
+
+    def make(**kw):
+        cfg = {"backend": "mock", "mock": {"n_gpus": kw.pop("n_gpus", 4)}, "hz": kw.pop("hz", 100), "port": 0,
+               "node_name": "node-a", "pin_numa": False}
+        if "mock" in kw:
+            cfg["mock"].update(kw.pop("mock"))
+        cfg.update(kw)
+        ex = N.Exporter(cfg)
+        ex.start()
+        made.append(ex)
+        return ex
+
+    yield make
+    for ex in made:
+        ex.stop()

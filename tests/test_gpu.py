@@ -1,0 +1,210 @@
+"""Real-hardware tests (MI355X).  Run on a GPU box: ``pytest -m gpu``.
+
+Every test here exercises native code: the C++ amdsmi/PMFW backend, the gfx950
+HIP load kernels (numerics vs a torch fp32 reference), and the rocprofiler-sdk
+counter reader (in its own exporter process — HSA must come up under the tool
+before any HIP runtime, and this pytest process initialises HIP).
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda", 0)
+
+
+def test_amdsmi_backend_inventory(N):
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 50, "pin_numa": True})
+    devs = ex.devices()
+    assert len(devs) >= 1
+    d = devs[0]
+    assert d["gfx_target"] == "gfx950", d
+    assert d["gpu_type"].startswith("MI3"), d
+    assert d["num_cu"] == 256 and d["num_xcc"] == 8, d
+    assert d["vram_total_bytes"] > 250e9, d  # 288 GB HBM3E
+    assert d["sysfs_dir"].endswith("/device"), d
+    ex.start()
+    time.sleep(0.5)
+    s = ex.snapshot(0)
+    ex.stop()
+    assert s is not None and s["fw_ts"] > 0
+    assert 0 <= s["gfx_busy_pct"] <= 100
+    assert s["vram_used_bytes"] > 0 and s["power_w"] > 50
+    assert s["temp_hotspot_c"] > 10
+    assert len(s["gfx_busy_xcc"]) == 8
+
+
+def test_pmfw_table_parser_matches_amdsmi(N):
+    """Our direct v1.8 table parse equals amdsmi's parse of the same firmware tick."""
+    import amdsmi as A
+
+    ex = N.Exporter({"backend": "amdsmi", "port": -1})
+    sysfs = ex.devices()[0]["sysfs_dir"]
+    A.amdsmi_init(A.AmdSmiInitFlags.INIT_AMD_GPUS)
+    try:
+        h = A.amdsmi_get_processor_handles()[0]
+        for _ in range(20):
+            with open(os.path.join(sysfs, "gpu_metrics"), "rb") as f:
+                raw0 = f.read()
+            m = A.amdsmi_get_gpu_metrics_info(h)
+            with open(os.path.join(sysfs, "gpu_metrics"), "rb") as f:
+                raw1 = f.read()
+            p0, p1 = N.parse_gpu_metrics_v1_8(raw0), N.parse_gpu_metrics_v1_8(raw1)
+            if p0["fw_ts"] == p1["fw_ts"] == m["firmware_timestamp"]:
+                break
+        else:
+            pytest.fail("could not catch one firmware tick in 20 tries")
+    finally:
+        A.amdsmi_shut_down()
+    assert p0["energy_acc"] == m["energy_accumulator"]
+    assert p0["temp_hotspot_c"] == m["temperature_hotspot"]
+    assert p0["gfx_busy_pct"] == m["average_gfx_activity"]
+    assert p0["gfx_activity_acc"] == m["gfx_activity_acc"]
+    assert p0["xgmi_read_kb"][1] == m["xgmi_read_data_acc"][1]
+    assert p0["pcie_bw_acc_gb"] == m["pcie_bandwidth_acc"]
+    assert p0["uclk_mhz"] == m["current_uclk"]
+
+
+def test_mfma_kernel_numerics(torch_dev):
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+
+    g = torch.Generator().manual_seed(7)
+    # exact small integers: bf16-exact inputs, fp32-exact accumulation
+    A = torch.randint(-3, 4, (16, 32), generator=g).to(torch.bfloat16).to(torch_dev)
+    B = torch.randint(-3, 4, (32, 64), generator=g).float()
+    B[0, 5] = 3.0  # asymmetric B (guide: catch row/col swaps)
+    B = B.to(torch.bfloat16).to(torch_dev)
+    blocks, iters = 8, 5
+    C = torch.full((blocks * 4 * 16 * 64,), float("nan"), device=torch_dev)
+    load.mfma_bf16(A, B, C, blocks, iters)
+    torch.cuda.synchronize()
+    ref = (A.float() @ B.float()) * iters
+    got = C.view(blocks * 4, 16, 64)
+    assert torch.equal(got, ref.expand_as(got)), (got[0] - ref).abs().max()
+
+    Ar = torch.randn(16, 32, generator=g).to(torch.bfloat16).to(torch_dev)
+    Br = torch.randn(32, 64, generator=g).to(torch.bfloat16).to(torch_dev)
+    load.mfma_bf16(Ar, Br, C, blocks, 3)
+    torch.cuda.synchronize()
+    ref = (Ar.float() @ Br.float()) * 3
+    torch.testing.assert_close(C.view(-1, 16, 64)[-1], ref, rtol=1e-5, atol=1e-4)
+
+
+def test_stream_kernels_numerics(torch_dev):
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+
+    n = (1 << 22) + 4
+    a = torch.rand(n, device=torch_dev)
+    b = torch.rand(n, device=torch_dev)
+    c = torch.empty(n, device=torch_dev)
+    load.triad_f32(a, b, c, 2.5)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(c, a + 2.5 * b, rtol=1e-6, atol=1e-6)
+    d = torch.empty(n, device=torch_dev)
+    load.copy_f32(a, d)
+    torch.cuda.synchronize()
+    assert torch.equal(a, d)
+
+
+def test_load_throughput_and_util_accumulators(N, torch_dev):
+    """Under a saturating MFMA load the PMFW-accumulator window mean reads ~100 %."""
+    import torch
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=3 << 30)
+    ls()
+    torch.cuda.synchronize()
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record()
+    ls.run_mfma()
+    e1.record()
+    ls.run_stream()
+    e2.record()
+    torch.cuda.synchronize()
+    tflops = ls.flops / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    tbps = ls.bytes / (e1.elapsed_time(e2) * 1e-3) / 1e12
+    print(json.dumps({"mfma_tflops": tflops, "triad_tbps": tbps}))
+    assert tflops > 500, tflops      # dense bf16 MFMA peak ≈2500
+    assert tbps > 3.0, tbps          # HBM3E ≈6.3 measured achievable
+
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 100})
+    ex.start()
+    t0 = time.time()
+    while time.time() - t0 < 2.0:
+        ls.run_mfma()
+    torch.cuda.synchronize()
+    w = ex.window(0, 1.0)
+    integ = ex.integrals(0)
+    ex.stop()
+    print(json.dumps({"window": w, "integrals": integ}))
+    assert w["gfx_busy_pct"] > 90, w
+    # PMFW cadence ≈ 50 Hz of distinct tables
+    assert 30 <= integ["distinct_samples"] / 2.0 <= 120, integ
+
+
+def test_rocprofiler_counters_exporter_process(torch_dev):
+    """Exporter process with --pmc rocprofiler sees MFMA busy + HBM traffic of *this* process' kernels."""
+    import torch
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz", "100",
+           "--pmc", "rocprofiler", "--control-stdin", "--bdfs", bdf]
+    proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True)
+    try:
+        ready = json.loads(proc.stdout.readline())
+        print(json.dumps(ready)[:2000])
+        assert ready["event"] == "ready", ready
+        if ready["pmc"] != "rocprofiler":
+            pytest.fail("rocprofiler counters unavailable: " + ready.get("pmc_error", ""))
+        sc = Scraper("127.0.0.1", ready["port"])
+        ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=3 << 30)
+        t0 = time.time()
+        while time.time() - t0 < 2.0:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+        m1 = parse_text(sc.get())
+        mfma = [v for lb, v in m1["amdgpu_mfma_util_percent"]]
+        t0 = time.time()
+        while time.time() - t0 < 2.0:
+            ls.run_stream()
+            torch.cuda.synchronize()
+        m2 = parse_text(sc.get())
+        rd = [v for lb, v in m2["amdgpu_hbm_read_bytes_per_second"]]
+        pmc_n = [v for lb, v in m2["kgs_pmc_samples_total"]]
+        print(json.dumps({"mfma_util": mfma, "hbm_read_Bps": rd, "pmc_samples": pmc_n}))
+        assert mfma[0] > 50, mfma
+        assert rd[0] > 1e12, rd
+        assert pmc_n[0] > 200
+    finally:
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            proc.wait(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+        err = proc.stderr.read()
+        if err:
+            print(err[-4000:])
