@@ -97,6 +97,7 @@ def run(a) -> int:
                       interval_s=a.attribution_interval).start()
     print(json.dumps({"event": "ready", "port": ex.port, "pid": os.getpid(), "backend": ex.backend_name,
                       "pmc": ex.pmc_name, "pmc_error": ex.pmc_error, "devices": ex.devices(),
+                      "pmc_info": [ex.pmc_info(i) for i in range(ex.device_count)],
                       "hz": a.hz}), flush=True)
     done = threading.Event()
 

@@ -49,6 +49,8 @@ struct Agent {
   std::vector<double> acc;            // running totals (delta mode)
   int mode = 0;                       // 1 cumulative, 2 delta
   std::string err;
+  std::vector<int> instances;         // records seen per counter in the last read
+  size_t last_records = 0;
 };
 
 std::mutex g_mu;
@@ -171,6 +173,8 @@ int read_raw(Agent* a, std::vector<double>& vals) {
       rocprofiler_sample_device_counting_service(a->ctx, ud, ROCPROFILER_COUNTER_FLAG_NONE, a->recs.data(), &n);
   if (s != ROCPROFILER_STATUS_SUCCESS) return -static_cast<int>(s) - 1;
   vals.assign(a->names.size(), 0.0);
+  a->instances.assign(a->names.size(), 0);
+  a->last_records = n;
   for (size_t i = 0; i < n && i < a->recs.size(); ++i) {
     rocprofiler_counter_id_t cid{};
     if (rocprofiler_query_record_counter_id(a->recs[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
@@ -179,6 +183,7 @@ int read_raw(Agent* a, std::vector<double>& vals) {
       const double v = a->recs[i].counter_value;
       if (a->is_max[k]) vals[k] = std::max(vals[k], v);
       else vals[k] += v;
+      a->instances[k]++;
       break;
     }
   }
@@ -262,7 +267,13 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     const char* force = std::getenv("KGS_PMC_MODE");
     if (force && std::strcmp(force, "cumulative") == 0) a->mode = 1;
     else if (force && std::strcmp(force, "delta") == 0) a->mode = 2;
-    else a->mode = (v2[0] >= 1.5 * v1[0] && v2[0] > 0) ? 1 : 2;
+    else {
+      // Cumulative: equal increments over equal sleeps (v0 < v1 < v2, d2 ≈ d1).
+      // Per-read deltas: v1 ≈ v2 (each ≈ one sleep's worth), so d2 ≈ 0.
+      // (A ratio test like v2/v1 ≈ 2 fails when counting began well before v0.)
+      const double d1 = v1[0] - v0[0], d2 = v2[0] - v1[0];
+      a->mode = (d1 > 0 && d2 > 0.5 * d1) ? 1 : 2;
+    }
     if (a->mode == 2)
       for (size_t k = 0; k < a->acc.size(); ++k) a->acc[k] = v0[k] + v1[k] + v2[k];
     return static_cast<int>(h);
@@ -288,6 +299,22 @@ int kgs_pmc_sample(int handle, uint64_t* out, int n, uint32_t* read_ns) {
       out[k] = static_cast<uint64_t>(v[static_cast<size_t>(k)]);
     }
   }
+  return 0;
+}
+
+// "mode=cumulative;records=N;NAME=instances,...;missing=A,B"
+int kgs_pmc_info(int handle, char* buf, int len) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  std::string o = std::string("mode=") + (a->mode == 1 ? "cumulative" : a->mode == 2 ? "delta" : "unknown") +
+                  ";records=" + std::to_string(a->last_records);
+  std::string missing;
+  for (size_t k = 0; k < a->names.size(); ++k) {
+    if (!a->ids.empty() && a->ids[k] == 0) missing += (missing.empty() ? "" : ",") + a->names[k];
+    o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
+  }
+  if (!missing.empty()) o += ";missing=" + missing;
+  set_err(buf, len, o);
   return 0;
 }
 

@@ -57,6 +57,8 @@ class CounterSource {
   virtual std::string name() const = 0;
   // Fill `out.value[0..kPmcCount)` with cumulative counts for device `dev`.
   virtual int sample(int dev, PmcSample& out) = 0;
+  // Human-readable diagnostics (mode, per-counter instance counts, missing counters).
+  virtual std::string info(int dev) const { return name(); }
 };
 
 struct MockPmcConfig {

@@ -12,7 +12,6 @@
 #pragma once
 
 #include <atomic>
-#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -101,8 +100,7 @@ class Sampler {
   std::vector<std::thread> threads_;
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
-  std::mutex cv_mu_;
-  std::condition_variable cv_;
+  int stop_fd_ = -1;  // eventfd: readable once stop() was called; sampler threads ppoll() on it
 };
 
 // CPU list of a NUMA node ("0-31,64-95" parsed); empty if unknown.

@@ -265,6 +265,10 @@ class PyExporter {
     return l;
   }
   std::string topology_json() { return ex_.topology_json(); }
+  std::string pmc_info(int d) const {
+    check(d);
+    return ex_.counters() ? ex_.counters()->info(d) : std::string("none");
+  }
   void set_device_owners(int d, const py::list& owners) {
     check(d);
     std::vector<Owner> v;
@@ -334,6 +338,7 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("procs", &PyExporter::procs)
       .def("links", &PyExporter::links)
       .def("topology_json", &PyExporter::topology_json)
+      .def("pmc_info", &PyExporter::pmc_info)
       .def("set_device_owners", &PyExporter::set_device_owners)
       .def("set_pid_owners", &PyExporter::set_pid_owners)
       .def("set_node_name", &PyExporter::set_node_name)

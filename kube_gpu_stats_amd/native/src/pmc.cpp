@@ -100,6 +100,7 @@ using init_fn = int (*)(char*, int);
 using open_fn = int (*)(uint64_t, const char* const*, const int*, int, char*, int);
 using sample_fn = int (*)(int, uint64_t*, int, uint32_t*);
 using close_fn = void (*)(int);
+using info_fn = int (*)(int, char*, int);
 
 class DlCounterSource final : public CounterSource {
  public:
@@ -120,6 +121,7 @@ class DlCounterSource final : public CounterSource {
     open_ = reinterpret_cast<open_fn>(dlsym(lib_, "kgs_pmc_open"));
     sample_ = reinterpret_cast<sample_fn>(dlsym(lib_, "kgs_pmc_sample"));
     close_ = reinterpret_cast<close_fn>(dlsym(lib_, "kgs_pmc_close"));
+    info_ = reinterpret_cast<info_fn>(dlsym(lib_, "kgs_pmc_info"));
     if (!init || !open_ || !sample_ || !close_) {
       err = "libkgs_pmc.so: missing symbols";
       return false;
@@ -149,6 +151,13 @@ class DlCounterSource final : public CounterSource {
 
   std::string name() const override { return "rocprofiler"; }
 
+  std::string info(int dev) const override {
+    if (!info_ || dev < 0 || dev >= static_cast<int>(handles_.size()) || handles_[dev] < 0) return "closed";
+    char buf[1024] = {};
+    info_(handles_[dev], buf, sizeof buf);
+    return buf;
+  }
+
   int sample(int dev, PmcSample& s) override {
     if (dev < 0 || dev >= static_cast<int>(handles_.size()) || handles_[dev] < 0) return -1;
     uint32_t rns = 0;
@@ -165,6 +174,7 @@ class DlCounterSource final : public CounterSource {
   open_fn open_ = nullptr;
   sample_fn sample_ = nullptr;
   close_fn close_ = nullptr;
+  info_fn info_ = nullptr;
   std::vector<int> handles_;
 };
 

@@ -1,11 +1,13 @@
 // Per-GPU sampler threads.  See sampler.h.
 #include "kgs/sampler.h"
 
+#include <poll.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
 
 #include <chrono>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -76,23 +78,29 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
       if (d >= 0 && d < n) dev_ids_.push_back(d);
   }
   if (cfg_.hz <= 0) cfg_.hz = 1;
+  stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
 }
 
-Sampler::~Sampler() { stop(); }
+Sampler::~Sampler() {
+  stop();
+  if (stop_fd_ >= 0) close(stop_fd_);
+}
 
 void Sampler::start() {
   if (running_.exchange(true)) return;
   stop_.store(false);
+  uint64_t drain;
+  while (read(stop_fd_, &drain, sizeof drain) > 0) {
+  }
   for (int d : dev_ids_) threads_.emplace_back([this, d] { run(d); });
 }
 
 void Sampler::stop() {
   if (!running_.load()) return;
-  {
-    std::lock_guard<std::mutex> g(cv_mu_);
-    stop_.store(true);
+  stop_.store(true);
+  const uint64_t one = 1;
+  if (write(stop_fd_, &one, sizeof one) < 0) {
   }
-  cv_.notify_all();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   threads_.clear();
@@ -243,8 +251,11 @@ void Sampler::run(int dev) {
       if (next <= now) next = now + period_ns / 4;  // never spin
     }
     st.integ.store(I);
-    std::unique_lock<std::mutex> lk(cv_mu_);
-    cv_.wait_for(lk, std::chrono::nanoseconds(next - now), [this] { return stop_.load(); });
+    // Sleep until the absolute deadline or until stop() signals the eventfd.
+    const int64_t wait = next - now;
+    timespec ts{static_cast<time_t>(wait / 1000000000LL), static_cast<long>(wait % 1000000000LL)};
+    pollfd pfd{stop_fd_, POLLIN, 0};
+    ppoll(&pfd, 1, &ts, nullptr);
   }
   st.integ.store(I);
 }

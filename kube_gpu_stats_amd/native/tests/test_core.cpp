@@ -1,0 +1,157 @@
+// Host-only concurrency tests of the data plane, built with -fsanitize=thread
+// (SURVEY.md §5.2).  Run by tests/test_native_tsan.py.
+//
+//  1. Seqlock: one writer publishing self-consistent payloads (every word equal
+//     to the sequence), many readers; a torn read would show mixed words.
+//  2. SampleRing: readers walking back from head never see a slot out of order
+//     by more than the ring can explain, and never a torn slot.
+//  3. Sampler over the mock backend with fault injection, readers calling
+//     window_busy / window_pmc / integ concurrently, then stop().
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "kgs/backend.h"
+#include "kgs/pmc.h"
+#include "kgs/sampler.h"
+#include "kgs/seqlock.h"
+
+using namespace kgs;
+
+#define CHECK(c)                                                     \
+  do {                                                               \
+    if (!(c)) {                                                      \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      std::exit(1);                                                  \
+    }                                                                \
+  } while (0)
+
+struct Payload {
+  uint64_t w[24];
+};
+
+static void test_seqlock() {
+  Seqlock<Payload> sl;
+  std::atomic<bool> done{false};
+  std::thread wr([&] {
+    Payload p;
+    for (uint64_t s = 1; s <= 200000; ++s) {
+      for (auto& x : p.w) x = s;
+      sl.store(p);
+    }
+    done = true;
+  });
+  std::vector<std::thread> rd;
+  std::atomic<uint64_t> reads{0};
+  for (int t = 0; t < 3; ++t)
+    rd.emplace_back([&] {
+      Payload p;
+      uint64_t last = 0;
+      while (!done) {
+        if (sl.load(p)) {
+          for (auto x : p.w) CHECK(x == p.w[0]);
+          CHECK(p.w[0] >= last);
+          last = p.w[0];
+          reads++;
+        }
+      }
+    });
+  wr.join();
+  for (auto& t : rd) t.join();
+  CHECK(reads > 0);
+  std::printf("seqlock ok (%llu reads)\n", static_cast<unsigned long long>(reads.load()));
+}
+
+static void test_ring() {
+  SampleRing<Payload, 64> ring;
+  std::atomic<bool> done{false};
+  std::thread wr([&] {
+    Payload p;
+    for (uint64_t s = 1; s <= 100000; ++s) {
+      for (auto& x : p.w) x = s;
+      ring.push(p);
+    }
+    done = true;
+  });
+  std::thread rd([&] {
+    std::vector<Payload> buf(64);
+    while (!done) {
+      const size_t n = ring.recent(buf.data(), 64);
+      for (size_t i = 0; i < n; ++i) {
+        for (auto x : buf[i].w) CHECK(x == buf[i].w[0]);
+      }
+    }
+  });
+  wr.join();
+  rd.join();
+  std::vector<Payload> buf(64);
+  const size_t n = ring.recent(buf.data(), 64);
+  CHECK(n == 63);
+  for (size_t i = 0; i < n; ++i) CHECK(buf[i].w[0] == 100000 - i);
+  std::printf("ring ok\n");
+}
+
+static void test_sampler() {
+  MockConfig mc;
+  mc.n_gpus = 4;
+  mc.fw_period_s = 0.002;
+  mc.fail_rate = 0.1;
+  mc.vanish_dev = 3;
+  mc.vanish_after_s = 0.2;
+  auto be = make_mock_backend(mc);
+  auto pmc = make_mock_counter_source(*be, mc, MockPmcConfig{});
+  SamplerConfig sc;
+  sc.hz = 1000;
+  sc.proc_every = 5;
+  sc.link_every = 7;
+  sc.pin_numa = false;
+  sc.pmc = true;
+  sc.max_backoff_ms = 20;
+  Sampler s(be.get(), pmc.get(), sc);
+  s.start();
+  std::atomic<bool> done{false};
+  std::vector<std::thread> rd;
+  for (int t = 0; t < 2; ++t)
+    rd.emplace_back([&] {
+      while (!done) {
+        for (int d = 0; d < 4; ++d) {
+          double g, u;
+          int n;
+          PmcRates r;
+          s.window_busy(d, 0.05, g, u, n);
+          s.window_pmc(d, 0.05, r);
+          Integrals I;
+          s.state(d).integ.load(I);
+          auto p = s.state(d).get_procs();
+          auto l = s.state(d).get_links();
+          (void)p;
+          (void)l;
+        }
+      }
+    });
+  std::this_thread::sleep_for(std::chrono::milliseconds(600));
+  done = true;
+  for (auto& t : rd) t.join();
+  s.stop();
+  Integrals I0, I3;
+  s.state(0).integ.load(I0);
+  s.state(3).integ.load(I3);
+  CHECK(I0.distinct_samples > 50);
+  CHECK(I0.read_errors > 0);             // 10 % injected failures
+  CHECK(s.state(0).up.load() == 1);
+  CHECK(s.state(3).up.load() == 0);      // vanished device marked down
+  CHECK(I3.read_errors > 3);
+  CHECK(I0.pmc_samples > 50);
+  std::printf("sampler ok (dev0 %llu samples, %llu errors)\n", static_cast<unsigned long long>(I0.distinct_samples),
+              static_cast<unsigned long long>(I0.read_errors));
+}
+
+int main() {
+  test_seqlock();
+  test_ring();
+  test_sampler();
+  std::printf("ALL OK\n");
+  return 0;
+}

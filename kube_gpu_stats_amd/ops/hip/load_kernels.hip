@@ -30,6 +30,14 @@ constexpr int kBlock = 256;  // 4 waves, one per SIMD of the CU
 thread_local char g_err[256];
 
 // A: [16][32] bf16 row-major, B: [32][64] bf16 row-major, C: [nwaves][16][64] f32.
+//
+// The iteration loop is one inline-asm block: with the builtin, hipcc rotates
+// the four accumulators through AGPR copies every trip (≈20 v_accvgpr moves per
+// 4 MFMAs, half of peak measured on MI355X).  Here each accumulator is pinned
+// ("+a"), MFMA→MFMA accumulate chains need no wait states, the loop counter is
+// SALU work that issues beside the matrix pipe, and the block ends with 20 wait
+// states before the compiler's first read of the accumulators
+// (cdna_hip_programming.md §5.7 item 2).
 __global__ __launch_bounds__(kBlock) void mfma_bf16_kernel(const unsigned short* __restrict__ A,
                                                            const unsigned short* __restrict__ B,
                                                            float* __restrict__ C, int iters) {
@@ -38,46 +46,85 @@ __global__ __launch_bounds__(kBlock) void mfma_bf16_kernel(const unsigned short*
   const int r = lane & 15;          // A row / B column within a 16-wide tile
   const int kb = (lane >> 4) * 8;   // k base of this lane's 8 elements
 
-  bf16x8 a, b[4];
+  bf16x8 a, b0, b1, b2, b3;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) a[j] = static_cast<short>(A[r * 32 + kb + j]);
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[t][j] = static_cast<short>(B[(kb + j) * 64 + t * 16 + r]);
-
-  f32x4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int it = 0; it < iters; ++it) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[t], acc[t], 0, 0, 0);
+  for (int j = 0; j < 8; ++j) {
+    a[j] = static_cast<short>(A[r * 32 + kb + j]);
+    b0[j] = static_cast<short>(B[(kb + j) * 64 + r]);
+    b1[j] = static_cast<short>(B[(kb + j) * 64 + 16 + r]);
+    b2[j] = static_cast<short>(B[(kb + j) * 64 + 32 + r]);
+    b3[j] = static_cast<short>(B[(kb + j) * 64 + 48 + r]);
+  }
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+  int n = iters;
+  if (n > 0) {
+    asm volatile(
+        "s_nop 4\n"
+        "1:\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %5, %6, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %1, %5, %7, %1\n\t"
+        "v_mfma_f32_16x16x32_bf16 %2, %5, %8, %2\n\t"
+        "v_mfma_f32_16x16x32_bf16 %3, %5, %9, %3\n\t"
+        "s_sub_u32 %4, %4, 1\n\t"
+        "s_cmp_lg_u32 %4, 0\n\t"
+        "s_cbranch_scc1 1b\n\t"
+        "s_nop 15\n\t"
+        "s_nop 3"
+        : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3), "+s"(n)
+        : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+        : "scc");
   }
 
   // C/D map for 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg.
   float* out = C + static_cast<size_t>(wave) * 16 * 64;
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[((lane >> 4) * 4 + i) * 64 + t * 16 + (lane & 15)] = acc[t][i];
+  for (int i = 0; i < 4; ++i) {
+    float* row = out + ((lane >> 4) * 4 + i) * 64 + (lane & 15);
+    row[0] = c0[i];
+    row[16] = c1[i];
+    row[32] = c2[i];
+    row[48] = c3[i];
+  }
 }
 
+// Four independent 16-byte loads per operand in flight per lane per trip.
+// NT: nontemporal loads (once-read stream) vs default cache policy.
+template <bool NT>
+__device__ inline f32x4 ld(const f32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(kBlock) void triad_f32_kernel(const f32x4* __restrict__ a, const f32x4* __restrict__ b,
                                                            f32x4* __restrict__ c, float s, size_t n4) {
   const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n4; i += stride) {
-    const f32x4 x = __builtin_nontemporal_load(a + i);
-    const f32x4 y = __builtin_nontemporal_load(b + i);
-    c[i] = x + s * y;
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    f32x4 x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      x[u] = ld<NT>(a + i + u * stride);
+      y[u] = ld<NT>(b + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c[i + u * stride] = x[u] + s * y[u];
   }
+  for (; i < n4; i += stride) c[i] = ld<NT>(a + i) + s * ld<NT>(b + i);
 }
 
 __global__ __launch_bounds__(kBlock) void copy_f32_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
                                                           size_t n4) {
   const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n4; i += stride)
-    dst[i] = __builtin_nontemporal_load(src + i);
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    f32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dst[i + u * stride] = x[u];
+  }
+  for (; i < n4; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
 }
 
 int check(hipError_t e, const char* what) {
@@ -103,12 +150,22 @@ int kgs_load_mfma_bf16(const void* A, const void* B, float* C, int nblocks, int 
 }
 
 // n must be a multiple of 4 and pointers 16-byte aligned.
-int kgs_load_triad_f32(const float* a, const float* b, float* c, float s, size_t n, int nblocks, void* stream) {
+int kgs_load_triad_f32_ex(const float* a, const float* b, float* c, float s, size_t n, int nblocks, int nt,
+                          void* stream) {
   if ((n & 3) || nblocks <= 0) return check(hipErrorInvalidValue, "triad_f32 args");
-  hipLaunchKernelGGL(triad_f32_kernel, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
-                     reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b),
-                     reinterpret_cast<f32x4*>(c), s, n / 4);
+  if (nt)
+    hipLaunchKernelGGL(triad_f32_kernel<true>, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b),
+                       reinterpret_cast<f32x4*>(c), s, n / 4);
+  else
+    hipLaunchKernelGGL(triad_f32_kernel<false>, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b),
+                       reinterpret_cast<f32x4*>(c), s, n / 4);
   return check(hipGetLastError(), "triad_f32 launch");
+}
+
+int kgs_load_triad_f32(const float* a, const float* b, float* c, float s, size_t n, int nblocks, void* stream) {
+  return kgs_load_triad_f32_ex(a, b, c, s, n, nblocks, 1, stream);
 }
 
 int kgs_load_copy_f32(const float* src, float* dst, size_t n, int nblocks, void* stream) {

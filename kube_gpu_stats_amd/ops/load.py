@@ -35,6 +35,8 @@ def lib() -> ctypes.CDLL:
                                          ctypes.c_int, ctypes.c_void_p]
         L.kgs_load_triad_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
                                          ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.kgs_load_triad_f32_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                            ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.kgs_load_copy_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                         ctypes.c_void_p]
         L.kgs_load_enable_peer.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -67,7 +69,7 @@ def mfma_bf16(A, B, C, nblocks: int, iters: int, stream=None) -> None:
                                     _stream_ptr(stream)))
 
 
-def triad_f32(a, b, c, s: float, nblocks: int = 0, stream=None) -> None:
+def triad_f32(a, b, c, s: float, nblocks: int = 0, stream=None, nt: bool = True) -> None:
     """c = a + s·b over float32 vectors (length multiple of 4)."""
     import torch
 
@@ -78,8 +80,8 @@ def triad_f32(a, b, c, s: float, nblocks: int = 0, stream=None) -> None:
         assert t.data_ptr() % 16 == 0
     if nblocks <= 0:
         nblocks = default_stream_blocks(n)
-    _check(lib().kgs_load_triad_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), float(s), n, int(nblocks),
-                                    _stream_ptr(stream)))
+    _check(lib().kgs_load_triad_f32_ex(a.data_ptr(), b.data_ptr(), c.data_ptr(), float(s), n, int(nblocks),
+                                       int(bool(nt)), _stream_ptr(stream)))
 
 
 def copy_f32(src, dst, nblocks: int = 0, stream=None) -> None:

@@ -150,14 +150,15 @@ def test_load_throughput_and_util_accumulators(N, torch_dev):
     t0 = time.time()
     while time.time() - t0 < 2.0:
         ls.run_mfma()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()  # keep the queue short: the window below must see *this* load
     w = ex.window(0, 1.0)
     integ = ex.integrals(0)
+    wall = time.time() - t0
     ex.stop()
-    print(json.dumps({"window": w, "integrals": integ}))
+    print(json.dumps({"window": w, "integrals": integ, "wall_s": wall}))
     assert w["gfx_busy_pct"] > 90, w
     # PMFW cadence ≈ 50 Hz of distinct tables
-    assert 30 <= integ["distinct_samples"] / 2.0 <= 120, integ
+    assert 30 <= integ["distinct_samples"] / wall <= 120, integ
 
 
 def test_rocprofiler_counters_exporter_process(torch_dev):

@@ -1,0 +1,143 @@
+"""Report layer (capabilities F1-F4): golden --compat outputs of SURVEY.md §2.8 and
+the fixed default mode.  Reference: gpu_util_stats/gpu_util_stats.py,
+who_use_gpu/who_use_gpu.py."""
+import io
+import json
+from datetime import datetime
+
+import pytest
+
+from kube_gpu_stats_amd.reports import gpu_util_stats as G
+from kube_gpu_stats_amd.reports import who_use_gpu as W
+from kube_gpu_stats_amd.reports.fakeprom import FakeProm
+from kube_gpu_stats_amd.reports.promql import PromClient, PromError
+from kube_gpu_stats_amd.reports.table import render
+
+from fixtures import STEP, T_END, WINDOW, install_reference_scenario, reference_podlist
+
+
+@pytest.fixture
+def prom():
+    fp = FakeProm()
+    url = fp.start()
+    yield fp, url
+    fp.stop()
+
+
+def test_gpu_util_stats_compat_golden(prom):
+    fp, url = prom
+    q = install_reference_scenario(fp)
+    out = io.StringIO()
+    c = PromClient(url)
+    rows = G.run_report(c, q, datetime.fromtimestamp(T_END), WINDOW, STEP, compat=True, out=out)
+    text = out.getvalue() + G.format_rows(rows, "pod", "table", compat=True) + "\n"
+    assert text == ('{\n  "node-a": {\n    "pod1": "4",\n    "pod2": "2"\n  }\n}\n'
+                    "['node-a', 'pod1', '4', 50.0]\n['node-a', 'pod2', '2', 0.0]\n")
+    # call order M1 → M2 → M3 → M4 → M5, both range queries step 3600 over one day
+    paths = [p for p, _ in c.calls]
+    assert paths == ["/query_range", "/query", "/query", "/query", "/query_range"]
+    assert [c.calls[i][1]["query"] for i in range(5)] == [q.util, q.total, q.used, q.live, q.req]
+    for i in (0, 4):
+        prm = c.calls[i][1]
+        assert prm["step"] == 3600 and prm["end"] - prm["start"] == 86400
+
+
+def test_node_report_compat_golden(prom):
+    fp, url = prom
+    q = install_reference_scenario(fp)
+    c = PromClient(url)
+    rows = G.run_report(c, q, datetime.fromtimestamp(T_END), WINDOW, STEP, compat=True, mode="node")
+    assert rows == [["node-a", "v100", 11.25, "6", "8"], ["node-b", "p4", 10.416666666666666, 0, "4"]]
+
+
+def test_node_report_fixed_mode_fixes_q1_q2():
+    util = {"data": {"result": [
+        {"metric": {"kubernetes_io_hostname": "n", "pod_name": "a"}, "values": [[0, "50"], [3600, "50"]]},
+        {"metric": {"kubernetes_io_hostname": "n", "pod_name": "b"}, "values": [[0, "90"], [3600, "90"]]},
+    ]}}
+    servers = {"n": (8, 6, "MI355X")}
+    # card-weighted: a holds 6 cards, b holds 2 → (6*50 + 2*90)/8 = 60
+    rows = G.stats_server_results(util, servers, 7200, 3600, compat=False, weights={"n": {"a": 6, "b": 2}})
+    assert rows == [["n", "MI355X", 60.0, 6, 8]]
+    rows = G.stats_server_results(util, servers, 4 * 3600, 3600, compat=False, missing="zero",
+                                  weights={"n": {"a": 1, "b": 1}})
+    assert rows[0][2] == pytest.approx(70.0 * 2 / 4)
+
+
+def test_pod_report_fixed_mode_ints_and_max_cards(prom):
+    fp, url = prom
+    q = G.Queries.amd("ml", STEP)
+    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "pod_name": "p"},
+                           "values": [[T_END - 3600, "40"], [T_END, "60"]]}])
+    fp.add_instant(q.total, [{"metric": {"node": "n1", q.type_label: "MI355X"}, "value": [T_END, "8"]}])
+    fp.add_instant(q.used, [{"metric": {"node": "n1"}, "value": [T_END, "4"]}])
+    fp.add_instant(q.live, [{"metric": {"pod": "p"}, "value": [T_END, "1"]}])
+    fp.add_range(q.req, [{"metric": {"node": "n1", "pod": "p"}, "values": [[T_END - 3600, "2"], [T_END, "4"]]}])
+    out = io.StringIO()
+    rows = G.run_report(PromClient(url), q, T_END, 7200, STEP, compat=False, out=out)
+    assert rows == [["n1", "p", 4, 50.0]]
+    assert out.getvalue() == ""  # no debug dump on stdout (Q8)
+    table = G.format_rows(rows, "pod", "table", compat=False)
+    assert "| n1   | p   |  4   | 50.00  |" in table or "50.00" in table
+    assert json.loads(G.format_rows(rows, "pod", "json", False))[0]["GPUs"] == 4
+
+
+def test_amd_queries_mention_amd_resource():
+    q = G.Queries.amd("ml", 3600)
+    assert 'resource="amd_com_gpu"' in q.total and 'resource="amd_com_gpu"' in q.req
+    assert "avg_over_time(container_gpu_sm_util[3600s])" in q.util
+    assert 'namespace="ml"' in q.live
+    assert 'namespace=' not in G.Queries.amd("", 60).live
+
+
+def test_prom_errors_are_typed(prom):
+    fp, url = prom
+    c = PromClient(url)
+    with pytest.raises(PromError):
+        c.query("rate(nonsense[5m])")  # fake answers 400 bad_data
+    with pytest.raises(PromError):
+        PromClient("http://127.0.0.1:9/api/v1", timeout_s=0.5).query("up")
+
+
+def test_who_use_gpu_compat_golden():
+    out = io.StringIO()
+    rows, total, per_type = W.census(reference_podlist(), compat=True, resources=(W.REF_GPU_RESOURCE,), out=out)
+    assert out.getvalue() == "'nodeName'\n"
+    assert [r.as_list() for r in rows] == [["ava", "node-a", "train-1", "tesla-v100", 6],
+                                            ["dev", "node-b", "no-aff", "<unspecified>", 1]]
+    assert total == 7 and per_type == {"tesla-v100": 6, "<unspecified>": 1}
+    text = W.format_report(rows, total, per_type)
+    assert text.splitlines()[-3:] == ["Total GPU: 7", "tesla-v100\t6", "<unspecified>\t1"]
+    assert "| Namespace |  Node  |   Pod   |    GPU Type   | GPU Cores |" in text
+
+
+def test_who_use_gpu_fixed_mode():
+    from fixtures import ctr, pod
+
+    R = "amd.com/gpu"
+    pods = {"items": [
+        pod("a", "ml", "n1", [ctr("x", {R: "2"}), ctr("y", requests={R: "1"})]),
+        pod("init-heavy", "ml", "n1", [ctr("x", {R: "1"})], init=[ctr("i", {R: "4"})]),
+        pod("done", "ml", "n1", [ctr("x", {R: "8"})], phase="Succeeded"),
+        pod("queued", "ml", None, [ctr("x", {R: "1"})], phase="Pending"),
+    ]}
+    nodes = {"n1": {"metadata": {"name": "n1", "labels": {"amd.com/gpu.product-name": "MI355X"}}}}
+    rows, total, per_type = W.census(pods, compat=False, resources=(R,), nodes=nodes)
+    got = {r.pod: (r.node, r.gpu_type, r.gpus) for r in rows}
+    assert got == {"a": ("n1", "MI355X", 3), "init-heavy": ("n1", "MI355X", 4),
+                   "queued": ("<unscheduled>", "<unspecified>", 1)}
+    assert total == 8
+    rows2, total2, _ = W.census(pods, compat=False, resources=(R,), nodes=nodes, include_finished=True)
+    assert total2 == 16
+
+
+def test_table_matches_prettytable_centering():
+    t = render(["A", "Long header"], [["xy", 1], ["odd", 22]])
+    assert t.splitlines() == [
+        "+-----+-------------+",
+        "|  A  | Long header |",
+        "+-----+-------------+",
+        "|  xy |      1      |",
+        "| odd |      22     |",
+        "+-----+-------------+",
+    ]

@@ -1,0 +1,75 @@
+"""GPU diagnostic: which hardware counters count under device counting, and what a
+read costs.  Launches native pmc_probe (its own HSA process) over candidate
+counter sets, runs idle / MFMA / triad / copy phases here, and attributes each
+probe interval to a phase.  Writes gpurun_out/pmc_probe.json."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+PROBE = os.path.join(REPO, "kube_gpu_stats_amd", "native", "build", "pmc_probe")
+LIB = os.path.join(REPO, "kube_gpu_stats_amd", "lib", "libkgs_pmc.so")
+
+SETS = {
+    "tcc": ["GRBM_COUNT:max", "GRBM_GUI_ACTIVE:max", "TCC_EA0_RDREQ", "TCC_EA0_WRREQ", "TCC_REQ", "TCC_HIT",
+            "TCC_MISS", "TCC_EA0_RDREQ_DRAM"],
+    "sq": ["GRBM_COUNT:max", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES",
+           "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_VALU_MFMA_BUSY_CYCLES"],
+    "grbm_ta": ["GRBM_COUNT:max", "GRBM_GUI_ACTIVE:max", "GRBM_TC_BUSY:max", "GRBM_EA_BUSY:max",
+                "TA_BUSY_cycles", "TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TA_FLAT_READ_WAVEFRONTS_sum"],
+}
+
+
+def main():
+    from kube_gpu_stats_amd import load_native
+
+    N = load_native()
+    ex = N.Exporter({"backend": "amdsmi", "port": -1})
+    gpu_id = ex.devices()[0]["kfd_gpu_id"]
+    del ex
+    out = {"gpu_id": gpu_id, "sets": {}}
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+    from kube_gpu_stats_amd.ops.load import LoadStep
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=6 << 30)
+    ls()
+    torch.cuda.synchronize()
+    for name, counters in SETS.items():
+        period = "50"
+        p = subprocess.Popen([PROBE, LIB, str(gpu_id), "9", period, *counters], stdout=subprocess.PIPE, text=True)
+        first = p.stdout.readline()
+        phases = []
+
+        def run(ph, fn, secs=1.5):
+            t0 = time.time()
+            while time.time() - t0 < secs:
+                fn()
+                torch.cuda.synchronize()
+            phases.append((ph, t0 + 0.2, time.time()))
+
+        time.sleep(0.3)
+        run("idle", lambda: time.sleep(0.02))
+        run("mfma", ls.run_mfma)
+        run("triad", lambda: load.triad_f32(ls.a, ls.b, ls.c, 1.5, nt=False))
+        run("copy", lambda: load.copy_f32(ls.a, ls.c))
+        rest, _ = p.communicate(timeout=60)
+        lines = [json.loads(x) for x in (first + rest).splitlines() if x.startswith("{")]
+        res = {"info": lines[0], "summary": lines[-1], "phases": {}}
+        for ph, a, b in phases:
+            iv = [x for x in lines if "t" in x and a <= x["t"] <= b]
+            if iv:
+                res["phases"][ph] = {k: sum(x[k] for x in iv) / len(iv) for k in iv[0] if k not in ("t",)}
+        out["sets"][name] = res
+        print(name, json.dumps(res), flush=True)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "pmc_probe.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
