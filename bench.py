@@ -51,7 +51,7 @@ def parse_args(argv=None):
     ap.add_argument("--hz", type=float, default=100.0, help="sampler rate per GPU")
     ap.add_argument("--pmc", default="auto", choices=["auto", "rocprofiler", "none"])
     ap.add_argument("--scrape-hz", type=float, default=10.0)
-    ap.add_argument("--mfma-iters", type=int, default=60000)
+    ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per step on MI355X")
     ap.add_argument("--mfma-blocks", type=int, default=2048)
     ap.add_argument("--stream-gib", type=float, default=6.0)
     ap.add_argument("--triads", type=int, default=2)
@@ -199,6 +199,17 @@ def sample_counts(m: dict) -> tuple[dict, dict]:
     return pmfw, pmc
 
 
+def observed(m: dict) -> dict:
+    """What the exporter saw of the load (window gauges of the last scrape), per GPU."""
+    out: dict = {}
+    for fam, key in (("amdgpu_gfx_busy_percent", "gfx_busy_pct"), ("amdgpu_umc_busy_percent", "umc_busy_pct"),
+                     ("amdgpu_mfma_util_percent", "mfma_util_pct"), ("amdgpu_vmem_busy_percent", "vmem_busy_pct"),
+                     ("amdgpu_power_watts", "power_w"), ("amdgpu_gpu_clock_effective_mhz", "clock_mhz")):
+        for lb, v in m.get(fam, []):
+            out.setdefault(lb["gpu"], {})[key] = round(v, 2)
+    return out
+
+
 # ----------------------------------------------------------------------------- main
 def main(argv=None) -> int:
     a = parse_args(argv)
@@ -301,6 +312,11 @@ def main(argv=None) -> int:
             "pmc_source": exp.ready.get("pmc"),
             "pmc_error": exp.ready.get("pmc_error"),
             "load": calib,
+            "observed_during_load": observed(after),
+            "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in stopped.get("integrals") or [])
+            / max(1, sum(i.get("pmc_samples", 0) for i in stopped.get("integrals") or [])),
+            "pmfw_read_us_mean": 1e6 * sum(i.get("read_seconds", 0) for i in stopped.get("integrals") or [])
+            / max(1, sum(i.get("reads", 0) for i in stopped.get("integrals") or [])),
             "exporter_integrals": stopped.get("integrals"),
         }
     # make the result visible to rank 0 if the exporter lived elsewhere (single node: it is rank 0)

@@ -1,0 +1,119 @@
+"""Metric catalogue: every family the exporter emits, with type, labels and meaning.
+
+The reference consumes one GPU series and four kube-state-metrics series
+(SURVEY.md §2.6).  The first entry below is that GPU series, kept label-compatible
+so the reference's PromQL (gpu_util_stats.py:159) runs unchanged; the rest are the
+MI355X-native families.  ``tests/test_schema.py`` checks the renderer against this
+table, and ``docs/METRICS.md`` is generated from it (``python -m
+kube_gpu_stats_amd.models.schema``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+DEVICE_LABELS = ("gpu", "uuid", "bdf", "gpu_type")
+
+
+@dataclass(frozen=True)
+class Family:
+    name: str
+    type: str
+    help: str
+    labels: tuple[str, ...] = DEVICE_LABELS
+    source: str = "pmfw"
+    tier: str = "fast"
+    extra: tuple[str, ...] = field(default=())
+
+
+F = Family
+CATALOG: tuple[Family, ...] = (
+    # ---- reference contract ------------------------------------------------------------
+    F("container_gpu_sm_util", "gauge",
+      "GFX-engine busy % of the GPU allocated to the pod (mean over the exporter window). Reference contract: "
+      "consumed by `avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)`.",
+      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      "pmfw+kubelet", "fast"),
+    # ---- inventory / topology -------------------------------------------------------------
+    F("amdgpu_device_info", "gauge", "Static device information (1).", extra=(
+        "serial", "market_name", "gfx_target", "numa_node", "num_cu", "num_xcc", "kfd_gpu_id", "hip_id"),
+      source="amdsmi", tier="init"),
+    F("amdgpu_topology_link", "gauge", "Pairwise link between visible GPUs (1).",
+      extra=("peer_gpu", "peer_bdf", "link_type", "hops", "weight"), source="amdsmi", tier="init"),
+    F("amdgpu_xgmi_link_info", "gauge", "Per-link peer PCI address and speed (1).",
+      extra=("link", "peer_bdf", "link_type", "bit_rate_gbps", "max_bandwidth_gbps"), source="amdsmi", tier="slow"),
+    # ---- utilisation ------------------------------------------------------------------------
+    F("amdgpu_gfx_busy_percent", "gauge", "GFX busy %, time-weighted mean over the window from PMFW accumulators."),
+    F("amdgpu_gfx_busy_instant_percent", "gauge", "GFX busy % in the latest PMFW table."),
+    F("amdgpu_gfx_busy_xcc_percent", "gauge", "Instantaneous busy % per XCC.", extra=("xcc",)),
+    F("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller activity %, window mean."),
+    F("amdgpu_gfx_busy_seconds_total", "counter", "∫ GFX busy fraction dt; rate() = exact mean utilisation."),
+    F("amdgpu_umc_busy_seconds_total", "counter", "∫ UMC busy fraction dt."),
+    # ---- memory ------------------------------------------------------------------------------
+    F("amdgpu_hbm_used_bytes", "gauge", "HBM3E bytes in use.", source="sysfs"),
+    F("amdgpu_hbm_total_bytes", "gauge", "HBM3E capacity (288 GB on MI355X).", source="sysfs", tier="init"),
+    # ---- thermals / power / clocks -----------------------------------------------------------
+    F("amdgpu_temperature_celsius", "gauge", "Temperature by sensor (hotspot, hbm, vrsoc).", extra=("sensor",)),
+    F("amdgpu_power_watts", "gauge", "Socket power."),
+    F("amdgpu_energy_joules_total", "counter", "Energy since exporter start (wrap-safe)."),
+    F("amdgpu_clock_mhz", "gauge", "Current clock (gfx = mean over XCCs, mem, soc).", extra=("clock",)),
+    F("amdgpu_power_throttle_residency_total", "counter", "PMFW PPT throttle residency accumulator (raw)."),
+    # ---- interconnect ------------------------------------------------------------------------
+    F("amdgpu_xgmi_read_bytes_total", "counter", "Bytes received per xGMI link.", extra=("link",)),
+    F("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link.", extra=("link",)),
+    F("amdgpu_xgmi_link_up", "gauge", "xGMI link status per port.", extra=("link",)),
+    F("amdgpu_pcie_bandwidth_bytes_total", "counter", "PCIe accumulated bandwidth (GB granularity)."),
+    # ---- hardware counters (rocprofiler-sdk device counting) -----------------------------------
+    F("amdgpu_pmc_total", "counter", "Raw hardware counter since exporter start.", extra=("counter",),
+      source="rocprofiler", tier="pmc"),
+    F("amdgpu_mfma_util_percent", "gauge", "Matrix-core busy % of active cycles (window).", source="rocprofiler",
+      tier="pmc"),
+    F("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active % of clocks (window).", source="rocprofiler", tier="pmc"),
+    F("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy % of active cycles (window).",
+      source="rocprofiler", tier="pmc"),
+    F("amdgpu_vmem_data_busy_percent", "gauge", "Vector-memory data unit (TD) busy % of active cycles (window).",
+      source="rocprofiler", tier="pmc"),
+    F("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT (window).",
+      source="rocprofiler", tier="pmc"),
+    # ---- per process -------------------------------------------------------------------------
+    F("amdgpu_process_hbm_bytes", "gauge", "HBM bytes held by a process.",
+      extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
+    F("amdgpu_process_gtt_bytes", "gauge", "GTT bytes held by a process.",
+      extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
+    F("amdgpu_process_cu_occupancy", "gauge", "CUs occupied by the process' waves.",
+      extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
+    F("amdgpu_process_gfx_seconds_total", "counter", "GFX engine time of the process (driver-reported).",
+      extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
+    # ---- exporter self-metrics ---------------------------------------------------------------
+    F("kgs_up", "gauge", "1 if the device's last read succeeded.", source="self"),
+    F("kgs_last_sample_age_seconds", "gauge", "Seconds since the last successful read.", source="self"),
+    F("kgs_samples_total", "counter", "Distinct hardware samples (new PMFW firmware timestamp).", source="self"),
+    F("kgs_reads_total", "counter", "Sampler reads attempted.", source="self"),
+    F("kgs_read_errors_total", "counter", "Sampler reads that failed.", source="self"),
+    F("kgs_sampler_overruns_total", "counter", "Ticks that overran the period.", source="self"),
+    F("kgs_pmc_samples_total", "counter", "Hardware-counter drains completed.", source="self"),
+    F("kgs_pmc_errors_total", "counter", "Hardware-counter drains that failed.", source="self"),
+    F("kgs_pmc_read_seconds_total", "counter", "Time spent draining hardware counters.", source="self"),
+    F("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples.", source="self"),
+    F("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read.", extra=("le",), source="self"),
+    F("kgs_scrapes_total", "counter", "Scrapes rendered.", ("kubernetes_io_hostname",), "self"),
+    F("kgs_scrape_render_seconds_total", "counter", "Time spent rendering /metrics.", ("kubernetes_io_hostname",),
+      "self"),
+    F("kgs_scrape_render_last_seconds", "gauge", "Render time of the previous scrape.", ("kubernetes_io_hostname",),
+      "self"),
+    F("kgs_build_info", "gauge", "Build / configuration (1).",
+      ("kubernetes_io_hostname", "version", "backend", "pmc_source", "sample_hz"), "self"),
+)
+
+BY_NAME = {f.name: f for f in CATALOG}
+
+
+def markdown() -> str:
+    rows = ["| metric | type | labels | source / tier | meaning |", "|---|---|---|---|---|"]
+    for f in CATALOG:
+        labels = ", ".join(f.labels + f.extra)
+        rows.append(f"| `{f.name}` | {f.type} | {labels} | {f.source} / {f.tier} | {f.help} |")
+    return "\n".join(rows)
+
+
+if __name__ == "__main__":
+    print(markdown())

@@ -181,12 +181,14 @@ int read_raw(Agent* a, std::vector<double>& vals) {
     for (size_t k = 0; k < a->ids.size(); ++k) {
       if (a->ids[k] != cid.handle) continue;
       const double v = a->recs[i].counter_value;
-      if (a->is_max[k]) vals[k] = std::max(vals[k], v);
-      else vals[k] += v;
+      if (a->is_max[k] == 1) vals[k] = std::max(vals[k], v);
+      else vals[k] += v;  // sum, or sum then mean below
       a->instances[k]++;
       break;
     }
   }
+  for (size_t k = 0; k < vals.size(); ++k)
+    if (a->is_max[k] == 2 && a->instances[k] > 0) vals[k] /= a->instances[k];
   return 0;
 }
 
@@ -268,11 +270,11 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     if (force && std::strcmp(force, "cumulative") == 0) a->mode = 1;
     else if (force && std::strcmp(force, "delta") == 0) a->mode = 2;
     else {
-      // Cumulative: equal increments over equal sleeps (v0 < v1 < v2, d2 ≈ d1).
-      // Per-read deltas: v1 ≈ v2 (each ≈ one sleep's worth), so d2 ≈ 0.
-      // (A ratio test like v2/v1 ≈ 2 fails when counting began well before v0.)
-      const double d1 = v1[0] - v0[0], d2 = v2[0] - v1[0];
-      a->mode = (d1 > 0 && d2 > 0.5 * d1) ? 1 : 2;
+      // Measured on MI355X / ROCm 7.2: the device counting service returns values
+      // accumulated since the context started (a stopped MFMA load leaves
+      // SQ_VALU_MFMA_BUSY_CYCLES constant across reads).  The first reads after
+      // start can all be 0, so the warm-up reads only prime the agent.
+      a->mode = 1;
     }
     if (a->mode == 2)
       for (size_t k = 0; k < a->acc.size(); ++k) a->acc[k] = v0[k] + v1[k] + v2[k];

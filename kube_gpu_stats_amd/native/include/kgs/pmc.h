@@ -1,5 +1,5 @@
 // Hardware performance-counter sources for the high-rate tier (BASELINE.json
-// config 4: MFMA-busy + HBM-BW + xGMI at 100 Hz).
+// config 4: MFMA-busy + memory-pipe busy at 100 Hz and beyond).
 //
 // The real source is the rocprofiler-sdk *device counting service* driven from
 // our own HSA client (native/counters/pmc_rocprofiler.cpp, built as a separate
@@ -7,6 +7,11 @@
 // the exporter never pulls HSA into a process that does not want it).  Reads
 // are agent-wide: every wave on the GPU is counted regardless of which process
 // launched it, and no kernel is dispatched by the reader.
+//
+// Counter set — chosen by measurement on MI355X / ROCm 7.2 (profiles/pmc_probe.md):
+// under device counting GRBM, SQ_VALU_MFMA_BUSY_CYCLES, TA and TD count; the
+// other SQ counters and every TCC counter read (near) zero, so HBM bandwidth
+// comes from the PMFW UMC-activity accumulators instead.  GRBM has 2 slots.
 #pragma once
 
 #include <cstdint>
@@ -24,32 +29,28 @@ enum PmcIndex : int {
   kPmcGrbmCount = 0,      // GRBM_COUNT (max over XCC): free-running GPU clocks
   kPmcGrbmGuiActive = 1,  // GRBM_GUI_ACTIVE (max over XCC): clocks the GPU had work
   kPmcMfmaBusy = 2,       // SQ_VALU_MFMA_BUSY_CYCLES (sum over SIMDs)
-  kPmcSqBusyCu = 3,       // SQ_BUSY_CU_CYCLES (sum, quad-cycles)
-  kPmcTccRdReq = 4,       // TCC_EA0_RDREQ (sum)
-  kPmcTccBubble = 5,      // TCC_BUBBLE (sum): 128-byte read requests
-  kPmcTccWrReq = 6,       // TCC_EA0_WRREQ (sum)
-  kPmcTccWrReq64 = 7,     // TCC_EA0_WRREQ_64B (sum)
-  kPmcCount = 8,
+  kPmcTaBusy = 3,         // TA_TA_BUSY (mean over TA instances): vector-memory address unit busy cycles
+  kPmcTdBusy = 4,         // TD_TD_BUSY (mean over TD instances): vector-memory data return busy cycles
+  kPmcCount = 5,
 };
 static_assert(kPmcCount <= kMaxPmc, "PmcSample too small");
 
+// How a counter's dimension instances (XCC × SE × unit) reduce to one value.
+enum PmcReduce : int { kReduceSum = 0, kReduceMax = 1, kReduceAvg = 2 };
+
 const char* pmc_counter_name(int idx);
-bool pmc_counter_is_max(int idx);  // reduce over dimensions with max (GRBM) vs sum
+int pmc_counter_reduce(int idx);
 
 // Derived quantities over an interval between two cumulative samples.
 struct PmcRates {
   double gpu_active_pct = 0;     // 100 * ΔGUI_ACTIVE / ΔGRBM_COUNT
-  double mfma_util_pct = 0;      // 100 * ΔMFMA_BUSY / (ΔGUI_ACTIVE * SIMD_NUM)
-  double cu_busy_pct = 0;        // 100 * 4*ΔSQ_BUSY_CU / (ΔGUI_ACTIVE * CU_NUM)
-  double hbm_read_Bps = 0;       // bytes/s from TCC→EA read requests
-  double hbm_write_Bps = 0;
+  double mfma_util_pct = 0;      // 100 * ΔMFMA_BUSY / (ΔGUI_ACTIVE * SIMD_NUM)  (rocprofv3 MfmaUtil)
+  double vmem_busy_pct = 0;      // 100 * ΔTA_BUSY(avg) / ΔGUI_ACTIVE
+  double vmem_data_busy_pct = 0; // 100 * ΔTD_BUSY(avg) / ΔGUI_ACTIVE
   double gpu_clock_mhz = 0;      // ΔGRBM_COUNT / Δt
   double dt_s = 0;
 };
 PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu);
-// Cumulative HBM bytes implied by one sample's request counts.
-double pmc_read_bytes(const PmcSample& s);
-double pmc_write_bytes(const PmcSample& s);
 
 class CounterSource {
  public:
@@ -64,7 +65,7 @@ class CounterSource {
 struct MockPmcConfig {
   double clock_mhz = 2100;
   double mfma_frac = 0.6;       // fraction of active time the MFMA pipes are busy
-  double read_Bps = 2e12, write_Bps = 1e12;
+  double vmem_frac = 0.3;       // fraction of active time the TA units are busy
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,

@@ -108,6 +108,7 @@ struct Integrals {
   uint64_t pmc_samples = 0;
   uint64_t pmc_errors = 0;
   double read_seconds = 0;       // total time spent in backend reads
+  double pmc_read_seconds = 0;   // total time spent in counter drains
 };
 static_assert(std::is_trivially_copyable<Integrals>::value, "seqlock payload");
 

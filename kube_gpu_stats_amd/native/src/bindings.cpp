@@ -39,8 +39,7 @@ ExporterConfig parse_config(const py::dict& d) {
     py::dict m = d["mock_pmc"].cast<py::dict>();
     c.mock_pmc.clock_mhz = get<double>(m, "clock_mhz", c.mock_pmc.clock_mhz);
     c.mock_pmc.mfma_frac = get<double>(m, "mfma_frac", c.mock_pmc.mfma_frac);
-    c.mock_pmc.read_Bps = get<double>(m, "read_Bps", c.mock_pmc.read_Bps);
-    c.mock_pmc.write_Bps = get<double>(m, "write_Bps", c.mock_pmc.write_Bps);
+    c.mock_pmc.vmem_frac = get<double>(m, "vmem_frac", c.mock_pmc.vmem_frac);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.proc_every = get<int>(d, "proc_every", c.sampler.proc_every);
@@ -186,6 +185,7 @@ class PyExporter {
     o["pmc_samples"] = I.pmc_samples;
     o["pmc_errors"] = I.pmc_errors;
     o["read_seconds"] = I.read_seconds;
+    o["pmc_read_seconds"] = I.pmc_read_seconds;
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
     return o;
@@ -201,8 +201,6 @@ class PyExporter {
     py::dict v;
     for (int i = 0; i < kPmcCount; ++i) v[pmc_counter_name(i)] = p.value[i];
     o["values"] = v;
-    o["read_bytes"] = pmc_read_bytes(p);
-    o["write_bytes"] = pmc_write_bytes(p);
     return o;
   }
   py::dict window(int d, double window_s) const {
@@ -219,9 +217,8 @@ class PyExporter {
     if (ex_.sampler()->window_pmc(d, window_s, r)) {
       o["gpu_active_pct"] = r.gpu_active_pct;
       o["mfma_util_pct"] = r.mfma_util_pct;
-      o["cu_busy_pct"] = r.cu_busy_pct;
-      o["hbm_read_Bps"] = r.hbm_read_Bps;
-      o["hbm_write_Bps"] = r.hbm_write_Bps;
+      o["vmem_busy_pct"] = r.vmem_busy_pct;
+      o["vmem_data_busy_pct"] = r.vmem_data_busy_pct;
       o["gpu_clock_mhz"] = r.gpu_clock_mhz;
       o["pmc_dt_s"] = r.dt_s;
     }

@@ -12,9 +12,9 @@ namespace kgs {
 
 namespace {
 const char* const kNames[kPmcCount] = {
-    "GRBM_COUNT",     "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES",
-    "TCC_EA0_RDREQ",  "TCC_BUBBLE",      "TCC_EA0_WRREQ",            "TCC_EA0_WRREQ_64B",
+    "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY", "TD_TD_BUSY",
 };
+const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg, kReduceAvg};
 
 int64_t mono_ns() {
   timespec ts;
@@ -24,20 +24,7 @@ int64_t mono_ns() {
 }  // namespace
 
 const char* pmc_counter_name(int idx) { return (idx >= 0 && idx < kPmcCount) ? kNames[idx] : "?"; }
-bool pmc_counter_is_max(int idx) { return idx == kPmcGrbmCount || idx == kPmcGrbmGuiActive; }
-
-double pmc_read_bytes(const PmcSample& s) {
-  // FETCH_SIZE expression for gfx950 (rocprofv3 -L), 32-byte requests folded
-  // into the 64-byte class: 128 B per TCC_BUBBLE, 64 B per other request.
-  const double rd = static_cast<double>(s.value[kPmcTccRdReq]);
-  const double bub = static_cast<double>(s.value[kPmcTccBubble]);
-  return bub * 128.0 + (rd > bub ? rd - bub : 0.0) * 64.0;
-}
-double pmc_write_bytes(const PmcSample& s) {
-  const double wr = static_cast<double>(s.value[kPmcTccWrReq]);
-  const double w64 = static_cast<double>(s.value[kPmcTccWrReq64]);
-  return w64 * 64.0 + (wr > w64 ? wr - w64 : 0.0) * 32.0;
-}
+int pmc_counter_reduce(int idx) { return (idx >= 0 && idx < kPmcCount) ? kReduce[idx] : kReduceSum; }
 
 PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
   PmcRates r;
@@ -52,12 +39,9 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
   if (cnt > 0) r.gpu_active_pct = 100.0 * act / cnt;
   if (act > 0) {
     r.mfma_util_pct = 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0);
-    r.cu_busy_pct = 100.0 * 4.0 * d(kPmcSqBusyCu) / (act * cu);
+    r.vmem_busy_pct = 100.0 * d(kPmcTaBusy) / act;
+    r.vmem_data_busy_pct = 100.0 * d(kPmcTdBusy) / act;
   }
-  r.hbm_read_Bps = (pmc_read_bytes(b) - pmc_read_bytes(a)) / dt;
-  r.hbm_write_Bps = (pmc_write_bytes(b) - pmc_write_bytes(a)) / dt;
-  if (r.hbm_read_Bps < 0) r.hbm_read_Bps = 0;
-  if (r.hbm_write_Bps < 0) r.hbm_write_Bps = 0;
   r.gpu_clock_mhz = cnt / dt * 1e-6;
   return r;
 }
@@ -79,11 +63,8 @@ class MockCounterSource final : public CounterSource {
     s.value[kPmcGrbmCount] = static_cast<uint64_t>(clk * t);
     s.value[kPmcGrbmGuiActive] = static_cast<uint64_t>(clk * busy_s);
     s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
-    s.value[kPmcSqBusyCu] = static_cast<uint64_t>(clk * busy_s * 256.0 / 4.0);
-    s.value[kPmcTccBubble] = static_cast<uint64_t>(c_.read_Bps * busy_s / 128.0);
-    s.value[kPmcTccRdReq] = s.value[kPmcTccBubble];
-    s.value[kPmcTccWrReq64] = static_cast<uint64_t>(c_.write_Bps * busy_s / 64.0);
-    s.value[kPmcTccWrReq] = s.value[kPmcTccWrReq64];
+    s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac);
+    s.value[kPmcTdBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac * 0.8);
     s.mono_ns = now;
     s.read_ns = 1000;
     return 0;
@@ -135,7 +116,7 @@ class DlCounterSource final : public CounterSource {
     int is_max[kPmcCount];
     for (int i = 0; i < kPmcCount; ++i) {
       names[i] = kNames[i];
-      is_max[i] = pmc_counter_is_max(i) ? 1 : 0;
+      is_max[i] = kReduce[i];
     }
     int opened = 0;
     handles_.assign(static_cast<size_t>(be.device_count()), -1);

@@ -298,20 +298,16 @@ void Exporter::render(std::string& out) {
         w.line_u("amdgpu_pmc_total", dev_labels_[d], e.c_str(), x.p.value[i]);
       }
     }
-    w.head("amdgpu_hbm_read_bytes_total", "counter", "HBM bytes read (TCC→EA requests)");
-    for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_hbm_read_bytes_total", dev_labels_[d], nullptr, pmc_read_bytes(snaps[d].p));
-    w.head("amdgpu_hbm_write_bytes_total", "counter", "HBM bytes written (TCC→EA requests)");
-    for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_hbm_write_bytes_total", dev_labels_[d], nullptr, pmc_write_bytes(snaps[d].p));
     w.head("amdgpu_mfma_util_percent", "gauge", "Matrix-core (MFMA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
     w.head("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active percent of clocks over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
-    w.head("amdgpu_cu_busy_percent", "gauge", "CU busy percent of active cycles over the window");
-    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_cu_busy_percent", dev_labels_[d], nullptr, snaps[d].r.cu_busy_pct);
-    w.head("amdgpu_hbm_read_bytes_per_second", "gauge", "HBM read bandwidth over the window");
-    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_hbm_read_bytes_per_second", dev_labels_[d], nullptr, snaps[d].r.hbm_read_Bps);
-    w.head("amdgpu_hbm_write_bytes_per_second", "gauge", "HBM write bandwidth over the window");
-    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_hbm_write_bytes_per_second", dev_labels_[d], nullptr, snaps[d].r.hbm_write_Bps);
+    w.head("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy percent of active cycles over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
+    w.head("amdgpu_vmem_data_busy_percent", "gauge", "Vector-memory data unit (TD) busy percent of active cycles over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_vmem_data_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_data_busy_pct);
+    w.head("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT over the window");
+    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_clock_effective_mhz", dev_labels_[d], nullptr, snaps[d].r.gpu_clock_mhz);
   }
 
   // ---- per-process attribution ------------------------------------------
@@ -366,6 +362,8 @@ void Exporter::render(std::string& out) {
   for (int d : ids) w.line_u("kgs_sampler_overruns_total", dev_labels_[d], nullptr, snaps[d].I.overruns);
   w.head("kgs_pmc_samples_total", "counter", "Hardware-counter drains completed");
   for (int d : ids) w.line_u("kgs_pmc_samples_total", dev_labels_[d], nullptr, snaps[d].I.pmc_samples);
+  w.head("kgs_pmc_read_seconds_total", "counter", "Time spent draining hardware counters");
+  for (int d : ids) w.line("kgs_pmc_read_seconds_total", dev_labels_[d], nullptr, snaps[d].I.pmc_read_seconds);
   w.head("kgs_pmc_errors_total", "counter", "Hardware-counter drains that failed");
   for (int d : ids) w.line_u("kgs_pmc_errors_total", dev_labels_[d], nullptr, snaps[d].I.pmc_errors);
   w.head("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples");

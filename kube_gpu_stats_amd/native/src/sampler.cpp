@@ -208,7 +208,10 @@ void Sampler::run(int dev) {
     // ---- PMC tier ------------------------------------------------------
     if (cfg_.pmc && pmc_) {
       PmcSample ps;
-      if (pmc_->sample(dev, ps) == 0) {
+      const int64_t p0 = mono_ns();
+      const int prc = pmc_->sample(dev, ps);
+      I.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
+      if (prc == 0) {
         ps.seq = ++pmc_seq;
         st.pmc_ring.push(ps);
         st.pmc_latest.store(ps);

@@ -1,0 +1,45 @@
+"""Kubernetes manifests parse and wire the exporter the way the code expects."""
+import os
+
+import yaml
+
+from kube_gpu_stats_amd.exporter.main import build_parser
+
+DEPLOY = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "deploy")
+
+
+def load(name):
+    with open(os.path.join(DEPLOY, name)) as f:
+        return [d for d in yaml.safe_load_all(f) if d]
+
+
+def test_daemonset_args_are_valid_exporter_flags():
+    docs = load("daemonset.yaml")
+    ds = next(d for d in docs if d["kind"] == "DaemonSet")
+    spec = ds["spec"]["template"]["spec"]
+    assert spec["hostPID"] is True
+    c = spec["containers"][0]
+    a = build_parser().parse_args(c["args"])
+    assert a.pmc == "rocprofiler" and a.hz == 10.0 and a.listen == "0.0.0.0:9400"
+    env = {e["name"]: e for e in c["env"]}
+    assert env["NODE_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName"
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert "/var/lib/kubelet/pod-resources" in mounts and "/dev/kfd" in mounts
+    assert c["readinessProbe"]["httpGet"]["path"] == "/healthz"
+
+
+def test_monitoring_rules_reference_exported_families():
+    from kube_gpu_stats_amd.models.schema import BY_NAME
+
+    docs = load("monitoring.yaml")
+    rule = next(d for d in docs if d["kind"] == "PrometheusRule")
+    exprs = " ".join(r["expr"] for g in rule["spec"]["groups"] for r in g["rules"])
+    for fam in ("container_gpu_sm_util", "amdgpu_gfx_busy_seconds_total", "amdgpu_hbm_used_bytes", "kgs_up",
+                "amdgpu_xgmi_read_bytes_total"):
+        assert fam in exprs and fam in BY_NAME
+
+
+def test_report_cronjob_has_rbac():
+    docs = load("reports-cronjob.yaml")
+    kinds = {d["kind"] for d in docs}
+    assert {"ServiceAccount", "ClusterRole", "ClusterRoleBinding", "CronJob"} <= kinds

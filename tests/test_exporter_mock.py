@@ -51,7 +51,7 @@ def test_prometheus_exposition_is_valid(mock_exporter):
     fams = {f.name: f for f in text_string_to_metric_families(body)}
     for name in ["container_gpu_sm_util", "amdgpu_gfx_busy_percent", "amdgpu_hbm_used_bytes", "amdgpu_power_watts",
                  "amdgpu_temperature_celsius", "amdgpu_energy_joules", "amdgpu_xgmi_read_bytes",
-                 "amdgpu_mfma_util_percent", "amdgpu_hbm_read_bytes_per_second", "amdgpu_process_hbm_bytes",
+                 "amdgpu_mfma_util_percent", "amdgpu_vmem_busy_percent", "amdgpu_process_hbm_bytes",
                  "kgs_samples", "kgs_sample_read_seconds", "amdgpu_topology_link", "amdgpu_device_info"]:
         assert name in fams, name
     compat = fams["container_gpu_sm_util"].samples

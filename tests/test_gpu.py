@@ -193,11 +193,13 @@ def test_rocprofiler_counters_exporter_process(torch_dev):
             ls.run_stream()
             torch.cuda.synchronize()
         m2 = parse_text(sc.get())
-        rd = [v for lb, v in m2["amdgpu_hbm_read_bytes_per_second"]]
+        vmem = [v for lb, v in m2["amdgpu_vmem_busy_percent"]]
+        clk = [v for lb, v in m2["amdgpu_gpu_clock_effective_mhz"]]
         pmc_n = [v for lb, v in m2["kgs_pmc_samples_total"]]
-        print(json.dumps({"mfma_util": mfma, "hbm_read_Bps": rd, "pmc_samples": pmc_n}))
+        print(json.dumps({"mfma_util": mfma, "vmem_busy": vmem, "clock_mhz": clk, "pmc_samples": pmc_n}))
         assert mfma[0] > 50, mfma
-        assert rd[0] > 1e12, rd
+        assert vmem[0] > 30, vmem     # triad keeps the TA units busy
+        assert 1000 < clk[0] < 2600, clk
         assert pmc_n[0] > 200
     finally:
         try:

@@ -1,0 +1,93 @@
+"""Renderer ↔ metric catalogue consistency, and the ``kgs`` CLI subcommands."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+from prometheus_client.parser import text_string_to_metric_families
+
+from kube_gpu_stats_amd.models.schema import BY_NAME, CATALOG
+
+from fixtures import reference_podlist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rendered_families_match_catalog(mock_exporter):
+    ex = mock_exporter(n_gpus=3, pmc_source="mock", proc_every=1, link_every=1)
+    ex.set_device_owners(0, [{"pod": "p", "namespace": "n", "container": "c"}])
+    time.sleep(0.4)
+    fams = list(text_string_to_metric_families(ex.render()))
+    names = {f.name for f in fams}
+    # prometheus_client strips _total from counter family names
+    catalog = {f.name[:-6] if f.type == "counter" and f.name.endswith("_total") else f.name for f in CATALOG}
+    assert names == catalog, (names ^ catalog)
+    for fam in fams:
+        cat = BY_NAME.get(fam.name) or BY_NAME.get(fam.name + "_total")
+        assert cat.type == fam.type, fam.name
+        for s in fam.samples:
+            allowed = set(cat.labels) | set(cat.extra)
+            assert set(s.labels) <= allowed, (fam.name, set(s.labels) - allowed)
+
+
+def _kgs(*args, **kw):
+    return subprocess.run([sys.executable, "-m", "kube_gpu_stats_amd.cli", *args], cwd=REPO, capture_output=True,
+                          text=True, timeout=120, **kw)
+
+
+def test_cli_who_use_gpu_compat_from_file(tmp_path):
+    p = tmp_path / "pods.json"
+    p.write_text(json.dumps(reference_podlist()))
+    r = _kgs("who-use-gpu", "--compat", "--source", "file", "--pods-json", str(p))
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0] == "'nodeName'"
+    assert lines[-3:] == ["Total GPU: 7", "tesla-v100\t6", "<unspecified>\t1"]
+
+
+def test_cli_who_use_gpu_json_and_env_override(tmp_path):
+    p = tmp_path / "pods.json"
+    p.write_text(json.dumps(reference_podlist()))
+    env = dict(os.environ, KGS_RESOURCE="nvidia.com/gpu", KGS_FORMAT="json")
+    r = _kgs("who-use-gpu", "--source", "file", "--pods-json", str(p), env=env)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out["total"] == 8 and out["pods"][0]["pod"] == "new-style"
+
+
+def test_cli_topo_mock():
+    r = _kgs("topo", "--backend", "mock", "--mock-gpus", "4")
+    assert r.returncode == 0, r.stderr
+    topo = json.loads(r.stdout)
+    assert len(topo["devices"]) == 4 and len(topo["edges"]) == 12
+    assert all(len([x for x in topo["links"] if x["gpu"] == g]) == 3 for g in range(4))
+
+
+def test_topology_ring_order():
+    from kube_gpu_stats_amd.parallel.topology import discover, node_graph, prometheus_lines, ring_order
+
+    topo = discover("mock", 8)
+    g = node_graph(topo)
+    assert all(len(v) == 7 for v in g.values())  # MI355X: all-to-all xGMI
+    ring = ring_order(g)
+    assert len(ring) == 8 and all(ring[(i + 1) % 8] in g[ring[i]] for i in range(8))
+    assert len(prometheus_lines(topo, "n")) == 56
+
+
+def test_cli_exporter_mock_process():
+    p = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--backend", "mock",
+                          "--mock-gpus", "2", "--listen", "127.0.0.1:0", "--control-stdin", "--hz", "50"],
+                         cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        ready = json.loads(p.stdout.readline())
+        assert ready["event"] == "ready" and ready["backend"] == "mock" and len(ready["devices"]) == 2
+        time.sleep(0.3)
+        r = _kgs("scrape", f"http://127.0.0.1:{ready['port']}/metrics", "--match", "kgs_up{")
+        assert r.stdout.count("kgs_up{") == 2
+    finally:
+        p.stdin.write("quit\n")
+        p.stdin.flush()
+        out, _ = p.communicate(timeout=30)
+    stopped = json.loads(out.splitlines()[-1])
+    assert stopped["event"] == "stopped" and stopped["integrals"][0]["reads"] > 0

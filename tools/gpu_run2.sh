@@ -11,3 +11,4 @@ step() {  # name limit cmd...
 }
 step pmc_probe 300 python tools/pmc_probe_run.py
 step pmc_debug 240 python tools/pmc_debug.py
+step bench 300 python bench.py --steps 40 --warmup 3 --out gpurun_out/r2_bench.json

@@ -14,13 +14,19 @@ PROBE = os.path.join(REPO, "kube_gpu_stats_amd", "native", "build", "pmc_probe")
 LIB = os.path.join(REPO, "kube_gpu_stats_amd", "lib", "libkgs_pmc.so")
 
 SETS = {
-    "tcc": ["GRBM_COUNT:max", "GRBM_GUI_ACTIVE:max", "TCC_EA0_RDREQ", "TCC_EA0_WRREQ", "TCC_REQ", "TCC_HIT",
-            "TCC_MISS", "TCC_EA0_RDREQ_DRAM"],
-    "sq": ["GRBM_COUNT:max", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES",
-           "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_VALU_MFMA_BUSY_CYCLES"],
-    "grbm_ta": ["GRBM_COUNT:max", "GRBM_GUI_ACTIVE:max", "GRBM_TC_BUSY:max", "GRBM_EA_BUSY:max",
-                "TA_BUSY_cycles", "TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TA_FLAT_READ_WAVEFRONTS_sum"],
+    "base": ["GRBM_COUNT:max", "GRBM_GUI_ACTIVE:max", "SQ_VALU_MFMA_BUSY_CYCLES"],
+    "tcc_ea": ["GRBM_COUNT:max", "TCC_EA0_RDREQ", "TCC_EA0_WRREQ"],
+    "tcc_hm": ["GRBM_COUNT:max", "TCC_HIT", "TCC_MISS"],
+    "tcc_req": ["GRBM_COUNT:max", "TCC_REQ", "TCC_BUBBLE"],
+    "derived": ["GRBM_COUNT:max", "FETCH_SIZE", "WRITE_SIZE"],
+    "sq_waves": ["GRBM_COUNT:max", "SQ_WAVES", "SQ_BUSY_CYCLES"],
+    "sq_insts": ["GRBM_COUNT:max", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_MFMA"],
+    "sq_cycles": ["GRBM_COUNT:max", "SQ_WAVE_CYCLES", "SQ_BUSY_CU_CYCLES", "SQ_ACTIVE_INST_VALU"],
+    "grbm": ["GRBM_COUNT:max", "GRBM_TC_BUSY:max", "GRBM_EA_BUSY:max", "GRBM_SPI_BUSY:max", "GRBM_CP_BUSY:max"],
+    "tcp": ["GRBM_COUNT:max", "TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum"],
+    "ta": ["GRBM_COUNT:max", "TA_BUSY_avr", "TA_FLAT_READ_WAVEFRONTS_sum"],
 }
+
 
 
 def main():
@@ -41,7 +47,8 @@ def main():
     torch.cuda.synchronize()
     for name, counters in SETS.items():
         period = "50"
-        p = subprocess.Popen([PROBE, LIB, str(gpu_id), "9", period, *counters], stdout=subprocess.PIPE, text=True)
+        p = subprocess.Popen([PROBE, LIB, str(gpu_id), "4.8", period, *counters], stdout=subprocess.PIPE, text=True,
+                             env=dict(os.environ, KGS_PMC_MODE="cumulative"))
         first = p.stdout.readline()
         phases = []
 
@@ -53,10 +60,10 @@ def main():
             phases.append((ph, t0 + 0.2, time.time()))
 
         time.sleep(0.3)
-        run("idle", lambda: time.sleep(0.02))
-        run("mfma", ls.run_mfma)
-        run("triad", lambda: load.triad_f32(ls.a, ls.b, ls.c, 1.5, nt=False))
-        run("copy", lambda: load.copy_f32(ls.a, ls.c))
+        run("idle", lambda: time.sleep(0.02), 1.0)
+        run("mfma", ls.run_mfma, 1.0)
+        run("triad", lambda: load.triad_f32(ls.a, ls.b, ls.c, 1.5, nt=False), 1.0)
+        run("copy", lambda: load.copy_f32(ls.a, ls.c), 1.0)
         rest, _ = p.communicate(timeout=60)
         lines = [json.loads(x) for x in (first + rest).splitlines() if x.startswith("{")]
         res = {"info": lines[0], "summary": lines[-1], "phases": {}}
