@@ -48,7 +48,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--hz", type=float, default=100.0, help="sampler rate per GPU")
+    ap.add_argument("--hz", type=float, default=1000.0,
+                    help="sampler tick rate per GPU: one hardware-counter drain per tick (PMFW table ≤100 Hz)")
     ap.add_argument("--pmc", default="auto", choices=["auto", "rocprofiler", "none"])
     ap.add_argument("--scrape-hz", type=float, default=10.0)
     ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per step on MI355X")
@@ -119,16 +120,26 @@ class MockLoad:
         return f"0000:{0x11 + 0x10 * device:02x}:00.0"  # mock provider's BDF scheme
 
 
-def timed(ctx, load, k: int) -> float:
-    """Barrier + sync on both sides; returns the MAX over ranks of the wall time."""
+PHASES: dict[str, list[float]] = {}
+
+
+def timed(ctx, load, k: int, name: str = "") -> float:
+    """Barrier + sync on both sides; returns the MAX over ranks of the wall time.
+
+    The wall-clock (epoch) bounds of each phase are kept in PHASES so a
+    rocprofv3 kernel trace of the run can be split into exporter-off / -on
+    phases (tools/rocprof_overhead.py)."""
     D.barrier(ctx)
     load.sync()
+    w0 = time.time()
     t0 = time.perf_counter()
     for _ in range(k):
         load.step()
     load.sync()
     D.barrier(ctx)
     dt = time.perf_counter() - t0
+    if name:
+        PHASES[name] = [w0, time.time()]
     return D.all_reduce(ctx, [dt], "max")[0]
 
 
@@ -227,7 +238,7 @@ def main(argv=None) -> int:
     calib = load.calibrate()
 
     # phase A: no exporter
-    t_a = timed(ctx, load, a.steps)
+    t_a = timed(ctx, load, a.steps, "A_off")
 
     # start the node exporter over every local rank's GPU
     bdfs = D.all_gather_object(ctx, (ctx.local_rank, load.pci_bdf(ctx.local_rank)))
@@ -257,7 +268,7 @@ def main(argv=None) -> int:
         t_w0 = time.perf_counter()
         scraper.start(a.scrape_hz)
     # phase B: exporter on (timed)
-    t_b = timed(ctx, load, a.steps)
+    t_b = timed(ctx, load, a.steps, "B_on")
     if exp is not None:
         scraper.stop()
         after = parse_text(scraper.get())
@@ -265,7 +276,7 @@ def main(argv=None) -> int:
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
-    t_c = timed(ctx, load, a.steps)
+    t_c = timed(ctx, load, a.steps, "C_off")
 
     result = None
     if exp is not None:
@@ -313,6 +324,7 @@ def main(argv=None) -> int:
             "pmc_error": exp.ready.get("pmc_error"),
             "load": calib,
             "observed_during_load": observed(after),
+            "phases_wall": PHASES,
             "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in stopped.get("integrals") or [])
             / max(1, sum(i.get("pmc_samples", 0) for i in stopped.get("integrals") or [])),
             "pmfw_read_us_mean": 1e6 * sum(i.get("read_seconds", 0) for i in stopped.get("integrals") or [])

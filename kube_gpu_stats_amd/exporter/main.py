@@ -32,7 +32,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "backend", "amdsmi", "device provider: amdsmi (MI355X) or mock")
     add_flag(ap, "mock-gpus", 8, "mock provider: number of GPUs")
     add_flag(ap, "mock-fail-rate", 0.0, "mock provider: injected read-failure probability")
-    add_flag(ap, "hz", 10.0, "fast-tier sampling rate per GPU (1/10/100 Hz tiers)")
+    add_flag(ap, "hz", 10.0, "sampler tick rate per GPU (1/10/100 Hz tiers; hardware counters every tick)")
+    add_flag(ap, "pmfw-hz", 100.0, "cap on PMFW metrics-table reads/s (firmware refreshes it every ~20 ms)")
     add_flag(ap, "proc-every", 10, "per-process tier every N fast ticks (0 = off)")
     add_flag(ap, "link-every", 100, "xGMI link tier every N fast ticks (0 = off)")
     add_flag(ap, "pmc", "none", "hardware counters: none | rocprofiler | mock")
@@ -58,6 +59,7 @@ def config_from_args(a) -> dict:
         "backend": a.backend,
         "mock": {"n_gpus": a.mock_gpus, "fail_rate": a.mock_fail_rate},
         "hz": a.hz,
+        "pmfw_hz": a.pmfw_hz,
         "proc_every": a.proc_every,
         "link_every": a.link_every,
         "pin_numa": a.pin_numa,

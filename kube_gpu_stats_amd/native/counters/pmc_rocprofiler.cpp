@@ -51,6 +51,8 @@ struct Agent {
   std::string err;
   std::vector<int> instances;         // records seen per counter in the last read
   size_t last_records = 0;
+  std::vector<int> rec_map;           // record index -> counter index (-1 = not ours)
+  std::vector<rocprofiler_counter_instance_id_t> rec_ids;
 };
 
 std::mutex g_mu;
@@ -175,17 +177,30 @@ int read_raw(Agent* a, std::vector<double>& vals) {
   vals.assign(a->names.size(), 0.0);
   a->instances.assign(a->names.size(), 0);
   a->last_records = n;
-  for (size_t i = 0; i < n && i < a->recs.size(); ++i) {
-    rocprofiler_counter_id_t cid{};
-    if (rocprofiler_query_record_counter_id(a->recs[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
-    for (size_t k = 0; k < a->ids.size(); ++k) {
-      if (a->ids[k] != cid.handle) continue;
-      const double v = a->recs[i].counter_value;
-      if (a->is_max[k] == 1) vals[k] = std::max(vals[k], v);
-      else vals[k] += v;  // sum, or sum then mean below
-      a->instances[k]++;
-      break;
+  if (n > a->recs.size()) n = a->recs.size();
+  // The service returns the same instances in the same order every read, so
+  // the record → counter map is resolved once and then only validated by
+  // instance id (saves one SDK lookup per record: ≈600 per read with TA/TD).
+  bool cached = a->rec_map.size() == n;
+  for (size_t i = 0; cached && i < n; ++i) cached = a->rec_ids[i] == a->recs[i].id;
+  if (!cached) {
+    a->rec_map.assign(n, -1);
+    a->rec_ids.assign(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+      a->rec_ids[i] = a->recs[i].id;
+      rocprofiler_counter_id_t cid{};
+      if (rocprofiler_query_record_counter_id(a->recs[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
+      for (size_t k = 0; k < a->ids.size(); ++k)
+        if (a->ids[k] == cid.handle) a->rec_map[i] = static_cast<int>(k);
     }
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const int k = a->rec_map[i];
+    if (k < 0) continue;
+    const double v = a->recs[i].counter_value;
+    if (a->is_max[k] == 1) vals[k] = std::max(vals[k], v);
+    else vals[k] += v;  // sum, or sum then mean below
+    a->instances[k]++;
   }
   for (size_t k = 0; k < vals.size(); ++k)
     if (a->is_max[k] == 2 && a->instances[k] > 0) vals[k] /= a->instances[k];

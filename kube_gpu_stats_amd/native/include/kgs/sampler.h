@@ -27,7 +27,8 @@
 namespace kgs {
 
 struct SamplerConfig {
-  double hz = 10.0;            // fast tier rate
+  double hz = 10.0;            // tick rate: counter (PMC) tier runs every tick
+  double pmfw_hz = 100.0;      // PMFW-table tier rate cap (table refreshes every ≈20 ms; 0 = every tick)
   int proc_every = 10;         // mid tier every N ticks (0 disables)
   int link_every = 100;        // slow tier every N ticks (0 disables)
   bool pin_numa = true;

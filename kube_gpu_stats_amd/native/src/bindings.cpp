@@ -42,6 +42,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.vmem_frac = get<double>(m, "vmem_frac", c.mock_pmc.vmem_frac);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
+  c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
   c.sampler.proc_every = get<int>(d, "proc_every", c.sampler.proc_every);
   c.sampler.link_every = get<int>(d, "link_every", c.sampler.link_every);
   c.sampler.pin_numa = get<bool>(d, "pin_numa", c.sampler.pin_numa);

@@ -155,6 +155,9 @@ void Sampler::run(int dev) {
   pthread_setname_np(pthread_self(), tname);
 
   const int64_t period_ns = static_cast<int64_t>(1e9 / cfg_.hz);
+  const uint64_t pmfw_every = cfg_.pmfw_hz > 0 && cfg_.pmfw_hz < cfg_.hz
+                                  ? static_cast<uint64_t>(cfg_.hz / cfg_.pmfw_hz + 0.5)
+                                  : 1;
   Integrals I;
   GpuSample prev;
   bool have_prev = false;
@@ -164,45 +167,49 @@ void Sampler::run(int dev) {
   std::vector<LinkInfo> links;
 
   while (!stop_.load(std::memory_order_relaxed)) {
-    // ---- fast tier -----------------------------------------------------
-    GpuSample s;
-    const int64_t t0 = mono_ns();
-    const int rc = be_->read_metrics(dev, s);
-    const int64_t t1 = mono_ns();
-    const double us = (t1 - t0) * 1e-3;
-    int b = 0;
-    while (b < kReadHistBuckets && us > kReadHistBoundsUs[b]) ++b;
-    st.read_hist[b].fetch_add(1, std::memory_order_relaxed);
-    ++I.reads;
-    I.read_seconds += (t1 - t0) * 1e-9;
+    // ---- fast tier: the PMFW table (refreshed by firmware every ≈20 ms) is
+    // read every `pmfw_every` ticks, i.e. at ≤ pmfw_hz however fast the
+    // counter tier runs.  A failing device backs off on this tier. ----------
     int backoff_shift = 0;
-    if (rc == 0) {
-      s.read_ns = static_cast<uint32_t>(t1 - t0);
-      if (s.mono_ns == 0) s.mono_ns = t1;
-      st.up.store(1, std::memory_order_relaxed);
-      st.consecutive_errors.store(0, std::memory_order_relaxed);
-      st.last_ok_mono_ns.store(t1, std::memory_order_relaxed);
-      const bool distinct = !have_prev || !(s.valid & kFFwTs) || s.fw_ts != prev.fw_ts;
-      if (distinct) {
-        integrate(dev, have_prev ? &prev : nullptr, s, I);
-        s.seq = ++seq;
-        ++I.distinct_samples;
-        st.ring.push(s);
-        st.latest.store(s);
-        prev = s;
-        have_prev = true;
+    if (tick % pmfw_every == 0 || st.consecutive_errors.load(std::memory_order_relaxed) > 0) {
+      GpuSample s;
+      const int64_t t0 = mono_ns();
+      const int rc = be_->read_metrics(dev, s);
+      const int64_t t1 = mono_ns();
+      const double us = (t1 - t0) * 1e-3;
+      int b = 0;
+      while (b < kReadHistBuckets && us > kReadHistBoundsUs[b]) ++b;
+      st.read_hist[b].fetch_add(1, std::memory_order_relaxed);
+      ++I.reads;
+      I.read_seconds += (t1 - t0) * 1e-9;
+      if (rc == 0) {
+        s.read_ns = static_cast<uint32_t>(t1 - t0);
+        if (s.mono_ns == 0) s.mono_ns = t1;
+        st.up.store(1, std::memory_order_relaxed);
+        st.consecutive_errors.store(0, std::memory_order_relaxed);
+        st.last_ok_mono_ns.store(t1, std::memory_order_relaxed);
+        const bool distinct = !have_prev || !(s.valid & kFFwTs) || s.fw_ts != prev.fw_ts;
+        if (distinct) {
+          integrate(dev, have_prev ? &prev : nullptr, s, I);
+          s.seq = ++seq;
+          ++I.distinct_samples;
+          st.ring.push(s);
+          st.latest.store(s);
+          prev = s;
+          have_prev = true;
+        } else {
+          // Same PMFW table: refresh host-side fields only (HBM occupancy).
+          prev.vram_used_bytes = s.vram_used_bytes;
+          prev.mono_ns = s.mono_ns;
+          prev.wall_ns = s.wall_ns;
+          st.latest.store(prev);
+        }
       } else {
-        // Same PMFW table: refresh host-side fields only (HBM occupancy).
-        prev.vram_used_bytes = s.vram_used_bytes;
-        prev.mono_ns = s.mono_ns;
-        prev.wall_ns = s.wall_ns;
-        st.latest.store(prev);
+        ++I.read_errors;
+        const uint64_t ce = st.consecutive_errors.fetch_add(1, std::memory_order_relaxed) + 1;
+        if (ce >= 3) st.up.store(0, std::memory_order_relaxed);
+        backoff_shift = ce > 10 ? 10 : static_cast<int>(ce);
       }
-    } else {
-      ++I.read_errors;
-      const uint64_t ce = st.consecutive_errors.fetch_add(1, std::memory_order_relaxed) + 1;
-      if (ce >= 3) st.up.store(0, std::memory_order_relaxed);
-      backoff_shift = ce > 10 ? 10 : static_cast<int>(ce);
     }
 
     // ---- PMC tier ------------------------------------------------------

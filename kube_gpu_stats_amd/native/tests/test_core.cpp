@@ -104,6 +104,7 @@ static void test_sampler() {
   auto pmc = make_mock_counter_source(*be, mc, MockPmcConfig{});
   SamplerConfig sc;
   sc.hz = 1000;
+  sc.pmfw_hz = 0;  // read the (mock) table every tick
   sc.proc_every = 5;
   sc.link_every = 7;
   sc.pin_numa = false;

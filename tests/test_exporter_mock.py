@@ -17,7 +17,7 @@ def get(port, path):
 
 
 def test_distinct_samples_follow_firmware_cadence(mock_exporter):
-    ex = mock_exporter(hz=200, mock={"fw_period_s": 0.02})
+    ex = mock_exporter(hz=200, pmfw_hz=0, mock={"fw_period_s": 0.02})
     time.sleep(1.0)
     I = ex.integrals(0)
     # 200 reads/s but only ~50 distinct PMFW tables/s
