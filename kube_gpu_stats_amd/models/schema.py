@@ -62,6 +62,11 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link.", extra=("link",)),
     F("amdgpu_xgmi_link_up", "gauge", "xGMI link status per port.", extra=("link",)),
     F("amdgpu_pcie_bandwidth_bytes_total", "counter", "PCIe accumulated bandwidth (GB granularity)."),
+    # ---- RAS / link health -------------------------------------------------------------------
+    F("amdgpu_ecc_errors_total", "counter", "Accumulated ECC errors by type.", extra=("type",), source="amdsmi",
+      tier="slow"),
+    F("amdgpu_xgmi_error_status", "gauge", "xGMI error status (0 none, 1 error, 2 multiple).", source="amdsmi",
+      tier="slow"),
     # ---- hardware counters (rocprofiler-sdk device counting) -----------------------------------
     F("amdgpu_pmc_total", "counter", "Raw hardware counter since exporter start.", extra=("counter",),
       source="rocprofiler", tier="pmc"),

@@ -50,6 +50,13 @@ struct LinkInfo {
   uint64_t read_kb = 0, write_kb = 0;
 };
 
+// RAS / link health (slow tier).
+struct HealthInfo {
+  uint64_t ecc_correctable = 0, ecc_uncorrectable = 0, ecc_deferred = 0;
+  int xgmi_error_status = -1;   // amdsmi_xgmi_status_t: 0 ok, 1 error, 2 multiple; -1 unknown
+  bool ecc_valid = false;
+};
+
 struct TopoEdge {
   int src = 0, dst = 0;
   int link_type = 0;            // 2 = xGMI, 1 = PCIe
@@ -72,6 +79,8 @@ class Backend {
   virtual int read_links(int dev, std::vector<LinkInfo>& out) = 0;
   // Pairwise topology among the visible devices.
   virtual int topology(std::vector<TopoEdge>& out) = 0;
+  // Slow tier: ECC totals and xGMI error status.
+  virtual int read_health(int dev, HealthInfo& out) { return -1; }
 };
 
 // Mock provider configuration (tests, plumbing benchmark).
@@ -85,6 +94,7 @@ struct MockConfig {
   int vanish_dev = -1;          // device that starts failing after vanish_after_s
   double vanish_after_s = 0;
   uint64_t energy_wrap_at = 0;  // if >0 the energy accumulator wraps at this value
+  uint64_t ecc_correctable_per_s = 0;  // injected correctable ECC error rate
   uint64_t seed = 1;
   std::string hostname_seed;    // reserved
 };

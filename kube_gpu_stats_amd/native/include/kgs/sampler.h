@@ -51,6 +51,7 @@ struct DeviceState {
   mutable std::mutex slow_mu;  // guards the two shared_ptrs below
   std::shared_ptr<const std::vector<ProcInfo>> procs;
   std::shared_ptr<const std::vector<LinkInfo>> links;
+  std::shared_ptr<const HealthInfo> health;
   int64_t procs_mono_ns = 0;
 
   std::atomic<int> up{0};
@@ -66,6 +67,10 @@ struct DeviceState {
   std::shared_ptr<const std::vector<LinkInfo>> get_links() const {
     std::lock_guard<std::mutex> g(slow_mu);
     return links;
+  }
+  std::shared_ptr<const HealthInfo> get_health() const {
+    std::lock_guard<std::mutex> g(slow_mu);
+    return health;
   }
 };
 

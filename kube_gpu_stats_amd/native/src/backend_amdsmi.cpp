@@ -168,6 +168,22 @@ class AmdSmiBackend final : public Backend {
     return 0;
   }
 
+  int read_health(int d, HealthInfo& out) override {
+    std::lock_guard<std::mutex> g(smi_mu_);
+    amdsmi_error_count_t ec;
+    std::memset(&ec, 0, sizeof ec);
+    out.ecc_valid = amdsmi_get_gpu_total_ecc_count(devs_[d]->h, &ec) == AMDSMI_STATUS_SUCCESS;
+    if (out.ecc_valid) {
+      out.ecc_correctable = ec.correctable_count;
+      out.ecc_uncorrectable = ec.uncorrectable_count;
+      out.ecc_deferred = ec.deferred_count;
+    }
+    amdsmi_xgmi_status_t xs;
+    out.xgmi_error_status =
+        amdsmi_gpu_xgmi_error_status(devs_[d]->h, &xs) == AMDSMI_STATUS_SUCCESS ? static_cast<int>(xs) : -1;
+    return out.ecc_valid || out.xgmi_error_status >= 0 ? 0 : -1;
+  }
+
   int topology(std::vector<TopoEdge>& out) override {
     std::lock_guard<std::mutex> g(smi_mu_);
     out.clear();

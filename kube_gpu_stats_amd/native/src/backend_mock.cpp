@@ -164,6 +164,16 @@ class MockBackend final : public Backend {
     return 0;
   }
 
+  int read_health(int d, HealthInfo& out) override {
+    const double t = (mono_ns() - t0_) * 1e-9;
+    out.ecc_valid = true;
+    out.ecc_correctable = static_cast<uint64_t>(t * static_cast<double>(cfg_.ecc_correctable_per_s));
+    out.ecc_uncorrectable = 0;
+    out.ecc_deferred = 0;
+    out.xgmi_error_status = 0;
+    return 0;
+  }
+
   int topology(std::vector<TopoEdge>& out) override {
     out.clear();
     for (int a = 0; a < cfg_.n_gpus; ++a)

@@ -34,6 +34,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.vanish_after_s = get<double>(m, "vanish_after_s", c.mock.vanish_after_s);
     c.mock.energy_wrap_at = get<uint64_t>(m, "energy_wrap_at", c.mock.energy_wrap_at);
     c.mock.seed = get<uint64_t>(m, "seed", c.mock.seed);
+    c.mock.ecc_correctable_per_s = get<uint64_t>(m, "ecc_correctable_per_s", c.mock.ecc_correctable_per_s);
   }
   if (d.contains("mock_pmc")) {
     py::dict m = d["mock_pmc"].cast<py::dict>();

@@ -280,6 +280,19 @@ void Exporter::render(std::string& out) {
       w.line("amdgpu_xgmi_link_info", lb, nullptr, 1);
     }
   }
+  w.head("amdgpu_ecc_errors_total", "counter", "Accumulated ECC errors by type (slow tier)");
+  for (int d : ids) {
+    auto h = S.state(d).get_health();
+    if (!h || !h->ecc_valid) continue;
+    w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"correctable\"", h->ecc_correctable);
+    w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"uncorrectable\"", h->ecc_uncorrectable);
+    w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"deferred\"", h->ecc_deferred);
+  }
+  w.head("amdgpu_xgmi_error_status", "gauge", "xGMI error status: 0 none, 1 error, 2 multiple errors");
+  for (int d : ids) {
+    auto h = S.state(d).get_health();
+    if (h && h->xgmi_error_status >= 0) w.line("amdgpu_xgmi_error_status", dev_labels_[d], nullptr, h->xgmi_error_status);
+  }
   w.head("amdgpu_pcie_bandwidth_bytes_total", "counter", "PCIe accumulated bandwidth from the PMFW table (GB granularity)");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPcie)) w.line_u("amdgpu_pcie_bandwidth_bytes_total", dev_labels_[d], nullptr, snaps[d].s.pcie_bw_acc_gb * 1000000000ull);
 

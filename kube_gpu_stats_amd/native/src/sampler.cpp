@@ -243,6 +243,12 @@ void Sampler::run(int dev) {
         std::lock_guard<std::mutex> g(st.slow_mu);
         st.links = std::move(l);
       }
+      HealthInfo h;
+      if (be_->read_health(dev, h) == 0) {
+        auto hp = std::make_shared<const HealthInfo>(h);
+        std::lock_guard<std::mutex> g(st.slow_mu);
+        st.health = std::move(hp);
+      }
     }
     ++tick;
 
