@@ -122,14 +122,16 @@ def build_load(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
-def build_tsan_test(verbose: bool = False) -> str:
-    """Host-only concurrency test of the seqlock / ring / sampler under TSAN."""
-    out = os.path.join(HERE, "build", "test_core_tsan")
+def build_tsan_test(verbose: bool = False, sanitizer: str = "thread") -> str:
+    """Host-only test of the seqlock / ring / sampler under a sanitizer
+    (``thread``, or ``address,undefined``)."""
+    tag = "tsan" if sanitizer == "thread" else "asan"
+    out = os.path.join(HERE, "build", f"test_core_{tag}")
     srcs = [os.path.join(HERE, "tests", "test_core.cpp")] + [
         os.path.join(HERE, "src", f) for f in ("sampler.cpp", "backend_mock.cpp", "pmc.cpp", "gpu_metrics.cpp", "util.cpp")]
     os.makedirs(os.path.dirname(out), exist_ok=True)
     if _stale(out, srcs + _headers() + [__file__]):
-        _run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+        _run(["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-pthread",
               "-I" + os.path.join(HERE, "include"), *srcs, "-o", out, "-ldl"], verbose)
     return out
 

@@ -73,8 +73,29 @@ class PromClient:
             p["time"] = to_unix(at)
         return self._get("/query", p)
 
-    def query_range(self, q: str, start, end, step_s: int) -> dict:
-        return self._get("/query_range", {"query": q, "start": to_unix(start), "end": to_unix(end), "step": step_s})
+    MAX_POINTS = 11000  # Prometheus rejects range queries above 11 000 points per series
+
+    def query_range(self, q: str, start, end, step_s: int, max_points: int | None = None) -> dict:
+        """``/query_range``; windows longer than ``max_points`` steps are split into
+        chunks and the per-series values concatenated."""
+        s, e = to_unix(start), to_unix(end)
+        cap = max_points or self.MAX_POINTS
+        if (e - s) // step_s + 1 <= cap:
+            return self._get("/query_range", {"query": q, "start": s, "end": e, "step": step_s})
+        merged: dict[tuple, dict] = {}
+        body = None
+        t = s
+        while t <= e:
+            t_end = min(e, t + (cap - 1) * step_s)
+            body = self._get("/query_range", {"query": q, "start": t, "end": t_end, "step": step_s})
+            for r in body["data"]["result"]:
+                key = tuple(sorted(r["metric"].items()))
+                slot = merged.setdefault(key, {"metric": r["metric"], "values": []})
+                slot["values"].extend(r.get("values", []))
+            t = t_end + step_s
+        body = dict(body)
+        body["data"] = {"resultType": "matrix", "result": list(merged.values())}
+        return body
 
 
 def result(body: dict) -> list[dict]:

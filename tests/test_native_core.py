@@ -47,12 +47,15 @@ def test_gpu_type_label(N):
 
 
 @pytest.mark.slow
-def test_tsan_seqlock_ring_sampler():
+@pytest.mark.parametrize("sanitizer,marker", [("thread", "ThreadSanitizer"),
+                                              ("address,undefined", "runtime error")])
+def test_sanitized_seqlock_ring_sampler(sanitizer, marker):
     from kube_gpu_stats_amd.native import build
 
-    exe = build.build_tsan_test()
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    exe = build.build_tsan_test(sanitizer=sanitizer)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, UBSAN_OPTIONS="print_stacktrace=1", ASAN_OPTIONS="detect_leaks=1"))
     out = r.stdout + r.stderr
     assert r.returncode == 0, out
-    assert "ThreadSanitizer" not in out, out
+    assert marker not in out and "AddressSanitizer" not in out, out
     assert "ALL OK" in out
