@@ -156,6 +156,13 @@ class ExporterProc:
             cmd += ["--pmc", "rocprofiler" if a.pmc in ("auto", "rocprofiler") else "none"]
         env = dict(os.environ)
         env.setdefault("KGS_NO_BUILD", "1")
+        if not a.mock and env.get("ROCP_TOOL_LIBRARIES"):
+            # Running under rocprofv3: rocprofiler configuration closes before the
+            # exporter could force-register, so join as a listed tool library.
+            from kube_gpu_stats_amd.native import pmc_lib_path
+
+            env["ROCP_TOOL_LIBRARIES"] = env["ROCP_TOOL_LIBRARIES"] + ":" + pmc_lib_path()
+            env["KGS_PMC_AS_TOOL"] = "1"
         self.log = open(log_path, "w")
         self.p = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.log,
                                   text=True, env=env)

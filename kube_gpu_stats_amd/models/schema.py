@@ -75,8 +75,6 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active % of clocks (window).", source="rocprofiler", tier="pmc"),
     F("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy % of active cycles (window).",
       source="rocprofiler", tier="pmc"),
-    F("amdgpu_vmem_data_busy_percent", "gauge", "Vector-memory data unit (TD) busy % of active cycles (window).",
-      source="rocprofiler", tier="pmc"),
     F("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT (window).",
       source="rocprofiler", tier="pmc"),
     # ---- per process -------------------------------------------------------------------------

@@ -211,11 +211,25 @@ int read_raw(Agent* a, std::vector<double>& vals) {
 
 extern "C" {
 
+// Tool-library entry point.  Normally the exporter registers itself with
+// rocprofiler_force_configure() before HSA starts; when the exporter process
+// runs under another rocprofiler tool (e.g. rocprofv3 tracing a benchmark),
+// configuration is closed by the time we are dlopen'd, so the parent lists this
+// library in ROCP_TOOL_LIBRARIES and sets KGS_PMC_AS_TOOL=1 instead.
+rocprofiler_tool_configure_result_t* rocprofiler_configure(uint32_t version, const char* runtime_version,
+                                                           uint32_t priority, rocprofiler_client_id_t* id) {
+  const char* as_tool = std::getenv("KGS_PMC_AS_TOOL");
+  if (!as_tool || std::strcmp(as_tool, "1") != 0) return nullptr;
+  return configure(version, runtime_version, priority, id);
+}
+
 int kgs_pmc_init(char* err, int errlen) {
   static std::once_flag once;
   static int rc = 0;
   std::call_once(once, [&] {
-    rocprofiler_status_t s = rocprofiler_force_configure(&configure);
+    const char* as_tool = std::getenv("KGS_PMC_AS_TOOL");
+    const bool tool_mode = as_tool && std::strcmp(as_tool, "1") == 0;
+    rocprofiler_status_t s = tool_mode ? ROCPROFILER_STATUS_SUCCESS : rocprofiler_force_configure(&configure);
     if (s != ROCPROFILER_STATUS_SUCCESS) {
       g_init_err = std::string("rocprofiler_force_configure: ") + st_str(s) +
                    " (HSA already initialised in this process? run the exporter in its own process)";

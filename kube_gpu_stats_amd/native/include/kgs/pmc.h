@@ -30,8 +30,9 @@ enum PmcIndex : int {
   kPmcGrbmGuiActive = 1,  // GRBM_GUI_ACTIVE (max over XCC): clocks the GPU had work
   kPmcMfmaBusy = 2,       // SQ_VALU_MFMA_BUSY_CYCLES (sum over SIMDs)
   kPmcTaBusy = 3,         // TA_TA_BUSY (mean over TA instances): vector-memory address unit busy cycles
-  kPmcTdBusy = 4,         // TD_TD_BUSY (mean over TD instances): vector-memory data return busy cycles
-  kPmcCount = 5,
+  kPmcCount = 4,
+  // TD_TD_BUSY tracks TA_TA_BUSY on every load tried and doubles the drain cost
+  // (288 more instances, ≈+110 µs per read), so it is not in the default set.
 };
 static_assert(kPmcCount <= kMaxPmc, "PmcSample too small");
 
@@ -46,7 +47,6 @@ struct PmcRates {
   double gpu_active_pct = 0;     // 100 * ΔGUI_ACTIVE / ΔGRBM_COUNT
   double mfma_util_pct = 0;      // 100 * ΔMFMA_BUSY / (ΔGUI_ACTIVE * SIMD_NUM)  (rocprofv3 MfmaUtil)
   double vmem_busy_pct = 0;      // 100 * ΔTA_BUSY(avg) / ΔGUI_ACTIVE
-  double vmem_data_busy_pct = 0; // 100 * ΔTD_BUSY(avg) / ΔGUI_ACTIVE
   double gpu_clock_mhz = 0;      // ΔGRBM_COUNT / Δt
   double dt_s = 0;
 };

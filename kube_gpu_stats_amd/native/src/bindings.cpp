@@ -220,7 +220,6 @@ class PyExporter {
       o["gpu_active_pct"] = r.gpu_active_pct;
       o["mfma_util_pct"] = r.mfma_util_pct;
       o["vmem_busy_pct"] = r.vmem_busy_pct;
-      o["vmem_data_busy_pct"] = r.vmem_data_busy_pct;
       o["gpu_clock_mhz"] = r.gpu_clock_mhz;
       o["pmc_dt_s"] = r.dt_s;
     }

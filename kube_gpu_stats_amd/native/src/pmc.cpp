@@ -12,9 +12,9 @@ namespace kgs {
 
 namespace {
 const char* const kNames[kPmcCount] = {
-    "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY", "TD_TD_BUSY",
+    "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY",
 };
-const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg, kReduceAvg};
+const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg};
 
 int64_t mono_ns() {
   timespec ts;
@@ -40,7 +40,6 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
   if (act > 0) {
     r.mfma_util_pct = 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0);
     r.vmem_busy_pct = 100.0 * d(kPmcTaBusy) / act;
-    r.vmem_data_busy_pct = 100.0 * d(kPmcTdBusy) / act;
   }
   r.gpu_clock_mhz = cnt / dt * 1e-6;
   return r;
@@ -64,7 +63,6 @@ class MockCounterSource final : public CounterSource {
     s.value[kPmcGrbmGuiActive] = static_cast<uint64_t>(clk * busy_s);
     s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
     s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac);
-    s.value[kPmcTdBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac * 0.8);
     s.mono_ns = now;
     s.read_ns = 1000;
     return 0;

@@ -317,8 +317,6 @@ void Exporter::render(std::string& out) {
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
     w.head("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
-    w.head("amdgpu_vmem_data_busy_percent", "gauge", "Vector-memory data unit (TD) busy percent of active cycles over the window");
-    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_vmem_data_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_data_busy_pct);
     w.head("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_clock_effective_mhz", dev_labels_[d], nullptr, snaps[d].r.gpu_clock_mhz);
   }

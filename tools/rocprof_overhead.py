@@ -45,7 +45,7 @@ def main():
     res = {"trace": os.path.relpath(path), "kernels_total": len(rows)}
     for kind, per_step in (("mfma", 1), ("triad", a.triads)):
         xs = by[kind]
-        skip = (a.warmup + 1) * per_step
+        skip = a.warmup * per_step + 1  # the calibration step launches one of each
         n = a.steps * per_step
         ph = {"A_off": xs[skip:skip + n], "B_on": xs[skip + n:skip + 2 * n], "C_off": xs[skip + 2 * n:skip + 3 * n]}
         if any(len(v) != n for v in ph.values()):
