@@ -56,16 +56,19 @@ def parse_args(argv=None):
     ap.add_argument("--mfma-blocks", type=int, default=2048)
     ap.add_argument("--stream-gib", type=float, default=6.0)
     ap.add_argument("--triads", type=int, default=2)
+    ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per step when N > 1 (0 = off)")
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
     ap.add_argument("--mock-step-ms", type=float, default=20.0)
     ap.add_argument("--out", default="", help="also write the result JSON here")
+    ap.add_argument("--attach", default="", help="host:port of an exporter started with --control-http; it is "
+                    "paused for phases A/C instead of being spawned (lets rocprofv3 trace the bench alone)")
     return ap.parse_args(argv)
 
 
 # ----------------------------------------------------------------------------- load
 class GpuLoad:
-    def __init__(self, a, device: int):
+    def __init__(self, a, device: int, ctx=None):
         import torch
 
         from kube_gpu_stats_amd.ops.load import LoadStep
@@ -74,11 +77,21 @@ class GpuLoad:
         self.ls = LoadStep(device=device, mfma_blocks=a.mfma_blocks, mfma_iters=a.mfma_iters,
                            stream_bytes=int(a.stream_gib * (1 << 30)))
         self.triads = a.triads
+        # xGMI traffic for N > 1: one RCCL all-reduce per step over the
+        # point-to-point xGMI mesh, so the exporter's per-link counters move.
+        self.ar = None
+        if ctx is not None and ctx.is_dist and a.xgmi_mib > 0:
+            self.ar = torch.ones(int(a.xgmi_mib) << 18, dtype=torch.float32, device=torch.device("cuda", device))
 
     def step(self):
         self.ls.run_mfma()
         for _ in range(self.triads):
             self.ls.run_stream()
+        if self.ar is not None:
+            import torch.distributed as dist
+
+            dist.all_reduce(self.ar)
+            self.ar.mul_(0.5)  # keep values bounded across steps
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -144,6 +157,36 @@ def timed(ctx, load, k: int, name: str = "") -> float:
 
 
 # ----------------------------------------------------------------------------- exporter
+class AttachedExporter:
+    """An already-running exporter (``--control-http``) driven over HTTP."""
+
+    def __init__(self, hostport: str):
+        host, _, port = hostport.rpartition(":")
+        self.port = int(port)
+        self.sc = Scraper(host or "127.0.0.1", self.port)
+        m = parse_text(self.sc.get())
+        info = m.get("kgs_build_info", [({}, 0)])[0][0]
+        self.ready = {"pmc": info.get("pmc_source", "none"), "pmc_error": "",
+                      "hz": float(info.get("sample_hz", "0") or 0)}
+
+    def pause(self):
+        self.sc.get("/control/pause")
+
+    def resume(self):
+        self.sc.get("/control/resume")
+
+    def stop(self) -> dict:
+        self.pause()
+        m = parse_text(self.sc.get())
+        fam = lambda n: {lb["gpu"]: v for lb, v in m.get(n, [])}  # noqa: E731
+        reads, rs, pmc, prs = (fam("kgs_reads_total"), fam("kgs_read_seconds_total"),
+                               fam("kgs_pmc_samples_total"), fam("kgs_pmc_read_seconds_total"))
+        hist = fam("kgs_sample_read_seconds_sum")
+        return {"integrals": [{"gpu": g, "reads": reads[g], "read_seconds": hist.get(g, rs.get(g, 0.0)),
+                               "pmc_samples": pmc.get(g, 0), "pmc_read_seconds": prs.get(g, 0.0),
+                               "overruns": fam("kgs_sampler_overruns_total").get(g, 0)} for g in sorted(reads)]}
+
+
 class ExporterProc:
     def __init__(self, a, bdfs: list[str], log_path: str):
         cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
@@ -217,6 +260,19 @@ def sample_counts(m: dict) -> tuple[dict, dict]:
     return pmfw, pmc
 
 
+def xgmi_rates(before: dict, after: dict, win: float) -> dict:
+    """xGMI bytes/s per GPU (all links, read + write) over the timed window, from the
+    exporter's PMFW per-link accumulators."""
+    def tot(m):
+        out: dict = {}
+        for fam in ("amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total"):
+            for lb, v in m.get(fam, []):
+                out[lb["gpu"]] = out.get(lb["gpu"], 0.0) + v
+        return out
+    b, a_ = tot(before), tot(after)
+    return {g: round((a_[g] - b.get(g, 0.0)) / win / 1e9, 3) for g in a_} if win > 0 else {}
+
+
 def observed(m: dict) -> dict:
     """What the exporter saw of the load (window gauges of the last scrape), per GPU."""
     out: dict = {}
@@ -237,14 +293,18 @@ def main(argv=None) -> int:
         if ctx.rank == 0:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
     n = ctx.world
-    load = (MockLoad if a.mock else GpuLoad)(a, ctx.local_rank)
+    load = MockLoad(a, ctx.local_rank) if a.mock else GpuLoad(a, ctx.local_rank, ctx)
 
     for _ in range(a.warmup):
         load.step()
     load.sync()
     calib = load.calibrate()
 
-    # phase A: no exporter
+    # phase A: no exporter (an attached exporter is paused: process up, no reads)
+    attached = None
+    if a.attach and ctx.local_rank == 0:
+        attached = AttachedExporter(a.attach)
+        attached.pause()
     t_a = timed(ctx, load, a.steps, "A_off")
 
     # start the node exporter over every local rank's GPU
@@ -255,7 +315,11 @@ def main(argv=None) -> int:
     if ctx.local_rank == 0:
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
         try:
-            exp = ExporterProc(a, bdfs, os.path.join(REPO, "gpurun_out", f"bench_exporter_r{ctx.rank}.log"))
+            if attached is not None:
+                attached.resume()
+                exp = attached
+            else:
+                exp = ExporterProc(a, bdfs, os.path.join(REPO, "gpurun_out", f"bench_exporter_r{ctx.rank}.log"))
         except Exception as e:  # noqa: BLE001
             err = str(e)
     err = D.broadcast_object(ctx, err)
@@ -314,7 +378,8 @@ def main(argv=None) -> int:
             "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + rocprofiler PMC, "
                                 f"{a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",
                        "global_batch": n, "seq_len": a.steps, "parallelism": f"dp{n}",
-                       "hz": a.hz, "sample_source": "pmc" if pmc_on else "pmfw"},
+                       "hz": exp.ready.get("hz") or a.hz, "sample_source": "pmc" if pmc_on else "pmfw",
+                       "exporter": "attached" if a.attach else "spawned"},
             "samples_per_sec_per_gpu": total / max(1, len(per_gpu)),
             "pmc_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmc_rate.items()},
             "pmfw_distinct_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmfw_rate.items()},
@@ -331,6 +396,7 @@ def main(argv=None) -> int:
             "pmc_error": exp.ready.get("pmc_error"),
             "load": calib,
             "observed_during_load": observed(after),
+            "xgmi_GBps_per_gpu": xgmi_rates(before, after, win),
             "phases_wall": PHASES,
             "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in stopped.get("integrals") or [])
             / max(1, sum(i.get("pmc_samples", 0) for i in stopped.get("integrals") or [])),

@@ -50,6 +50,7 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "static-owners", "", "JSON file mapping device id -> {pod,namespace,container}")
     add_flag(ap, "attribution-interval", 1.0, "attribution refresh period (s)")
     add_flag(ap, "control-stdin", False, "accept 'quit' on stdin")
+    add_flag(ap, "control-http", False, "serve /control/pause and /control/resume (benchmarks only)")
     return ap
 
 
@@ -72,6 +73,7 @@ def config_from_args(a) -> dict:
         "window_s": a.window,
         "per_process": a.per_process,
         "compat_unallocated": a.compat_unallocated,
+        "control_http": a.control_http,
         "bdfs": [b for b in (a.bdfs.split(",") if isinstance(a.bdfs, str) else a.bdfs) if b],
     }
     return cfg

@@ -46,6 +46,7 @@ struct ExporterConfig {
   bool per_process = true;
   bool compat_series = true;        // container_gpu_sm_util (reference contract)
   bool compat_unallocated = false;  // also emit it for GPUs with no pod (pod_name="")
+  bool control_http = false;        // serve /control/pause|resume (benchmarks only)
 };
 
 class HttpServer;
@@ -78,6 +79,10 @@ class Exporter {
   std::string devices_json();
   std::string samples_json(int dev, int n);
   bool healthy() const;
+  // Stop / restart the sampler threads (HTTP and state stay up; integrals continue).
+  void pause_sampling();
+  void resume_sampling();
+  bool sampling() const;
 
   // self metrics
   std::atomic<uint64_t> scrapes{0};

@@ -60,6 +60,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.per_process = get<bool>(d, "per_process", c.per_process);
   c.compat_series = get<bool>(d, "compat_series", c.compat_series);
   c.compat_unallocated = get<bool>(d, "compat_unallocated", c.compat_unallocated);
+  c.control_http = get<bool>(d, "control_http", c.control_http);
   return c;
 }
 
@@ -296,6 +297,15 @@ class PyExporter {
     return o;
   }
   bool healthy() const { return ex_.healthy(); }
+  void pause() {
+    py::gil_scoped_release r;
+    ex_.pause_sampling();
+  }
+  void resume() {
+    py::gil_scoped_release r;
+    ex_.resume_sampling();
+  }
+  bool sampling() const { return ex_.sampling(); }
 
  private:
   void check(int d) const {
@@ -341,7 +351,10 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("set_pid_owners", &PyExporter::set_pid_owners)
       .def("set_node_name", &PyExporter::set_node_name)
       .def("stats", &PyExporter::stats)
-      .def("healthy", &PyExporter::healthy);
+      .def("healthy", &PyExporter::healthy)
+      .def("pause", &PyExporter::pause)
+      .def("resume", &PyExporter::resume)
+      .def_property_readonly("sampling", &PyExporter::sampling);
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
   m.def("pmc_counter_names", [] {

@@ -122,6 +122,14 @@ void Exporter::stop() {
 
 int Exporter::port() const { return http_ ? http_->port() : -1; }
 
+void Exporter::pause_sampling() {
+  if (sampler_) sampler_->stop();
+}
+void Exporter::resume_sampling() {
+  if (sampler_) sampler_->start();
+}
+bool Exporter::sampling() const { return sampler_ && sampler_->running(); }
+
 void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
   std::lock_guard<std::mutex> g(mu_);
   auto m = owners_ ? std::make_shared<std::map<int, std::vector<Owner>>>(*owners_)

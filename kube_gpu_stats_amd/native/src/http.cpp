@@ -199,6 +199,10 @@ void HttpServer::loop() {
         } else if (target == "/metrics") {
           ex_->render(body);
           respond(c, 200, "OK", "text/plain; version=0.0.4; charset=utf-8", body);
+        } else if (ex_->config().control_http && (target == "/control/pause" || target == "/control/resume")) {
+          if (target == "/control/pause") ex_->pause_sampling();
+          else ex_->resume_sampling();
+          respond(c, 200, "OK", "application/json", ex_->sampling() ? "{\"sampling\":true}" : "{\"sampling\":false}");
         } else if (target == "/healthz") {
           const bool ok = ex_->healthy();
           respond(c, ok ? 200 : 503, ok ? "OK" : "Service Unavailable", "text/plain", ok ? "ok\n" : "no device sampled\n");

@@ -162,6 +162,13 @@ void Sampler::run(int dev) {
   GpuSample prev;
   bool have_prev = false;
   uint64_t seq = 0, pmc_seq = 0, tick = 0;
+  {  // resume after a pause: counters and sequence numbers continue
+    st.integ.load(I);
+    GpuSample last;
+    if (st.latest.load(last)) seq = last.seq;
+    PmcSample lp;
+    if (st.pmc_latest.load(lp)) pmc_seq = lp.seq;
+  }
   int64_t next = mono_ns();
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;
