@@ -107,7 +107,13 @@ class AmdSmiBackend final : public Backend {
     Dev& dv = *devs_[d];
     int rc = -1;
     if (dv.fd_metrics >= 0) {
-      const ssize_t n = pread(dv.fd_metrics, dv.buf, sizeof dv.buf, 0);
+      ssize_t n = pread(dv.fd_metrics, dv.buf, sizeof dv.buf, 0);
+      if (n <= 0) {
+        // The driver can invalidate an open sysfs file (GPU reset / hot unplug): reopen once.
+        close(dv.fd_metrics);
+        dv.fd_metrics = open((dv.info.sysfs_dir + "/gpu_metrics").c_str(), O_RDONLY | O_CLOEXEC);
+        n = dv.fd_metrics >= 0 ? pread(dv.fd_metrics, dv.buf, sizeof dv.buf, 0) : -1;
+      }
       if (n > 0 && gpu_metrics_revision(dv.buf, static_cast<size_t>(n)) == 0x0108)
         rc = parse_gpu_metrics_v1_8(dv.buf, static_cast<size_t>(n), s);
     }
