@@ -91,13 +91,11 @@ void Exporter::build_static_labels() {
   for (int d = 0; d < be_->device_count(); ++d) {
     const DeviceInfo& in = be_->info(d);
     std::string lb;
+    // Per-series identity is (gpu, uuid); bdf, type, serial, ... live once in
+    // amdgpu_device_info (join on gpu/uuid) — keeps an 8-GPU scrape ≈30 % smaller.
     lb += "gpu=\"" + std::to_string(d) + "\"";
     lb += ",uuid=\"";
     append_label_value(lb, in.uuid);
-    lb += "\",bdf=\"";
-    append_label_value(lb, in.bdf);
-    lb += "\",gpu_type=\"";
-    append_label_value(lb, cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override);
     lb += '"';
     dev_labels_.push_back(std::move(lb));
   }

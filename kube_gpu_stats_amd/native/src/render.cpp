@@ -150,6 +150,9 @@ void Exporter::render(std::string& out) {
   for (int d : ids) {
     const DeviceInfo& in = be_->info(d);
     std::string lb = dev_labels_[static_cast<size_t>(d)];
+    kv(lb, "bdf", in.bdf);
+    kv(lb, "gpu_type", cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override);
+    kv(lb, "kubernetes_io_hostname", node);
     kv(lb, "serial", in.serial);
     kv(lb, "market_name", in.market_name);
     kv(lb, "gfx_target", in.gfx_target);
