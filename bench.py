@@ -293,6 +293,14 @@ def main(argv=None) -> int:
         if ctx.rank == 0:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
     n = ctx.world
+    if ctx.local_rank == 0 and not a.attach:
+        # The exporter child runs with KGS_NO_BUILD=1: make sure its artefacts exist
+        # (incremental no-op when the in-tree .so files are current).
+        from kube_gpu_stats_amd.native import build as B
+
+        B.build_native()
+        if not a.mock:
+            B.build_pmc()
     load = MockLoad(a, ctx.local_rank) if a.mock else GpuLoad(a, ctx.local_rank, ctx)
 
     for _ in range(a.warmup):

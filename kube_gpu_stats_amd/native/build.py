@@ -88,7 +88,7 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
 
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = out + ".tmp"
+    tmp = f"{out}.{os.getpid()}.tmp"  # concurrent builders (one per rank) never share a temp file
     _run(["g++", "-shared", "-pthread", "-o", tmp, *objs, "-L" + os.path.join(ROCM, "lib"), "-lamd_smi",
           "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl"], verbose)
     os.replace(tmp, out)
@@ -101,7 +101,7 @@ def build_pmc(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale(out, [src, __file__]):
         return out
     os.makedirs(LIB, exist_ok=True)
-    tmp = out + ".tmp"
+    tmp = f"{out}.{os.getpid()}.tmp"  # concurrent builders (one per rank) never share a temp file
     _run(["g++", *CXXFLAGS, "-fvisibility=default", "-D__HIP_PLATFORM_AMD__=1", "-I" + os.path.join(ROCM, "include"), "-shared", src, "-o", tmp,
           "-L" + os.path.join(ROCM, "lib"), "-lrocprofiler-sdk", "-lhsa-runtime64",
           "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
@@ -115,7 +115,7 @@ def build_load(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale(out, [src, __file__]):
         return out
     os.makedirs(LIB, exist_ok=True)
-    tmp = out + ".tmp"
+    tmp = f"{out}.{os.getpid()}.tmp"  # concurrent builders (one per rank) never share a temp file
     _run([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC",
           "-shared", src, "-o", tmp], verbose)
     os.replace(tmp, out)
