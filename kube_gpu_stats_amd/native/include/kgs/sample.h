@@ -39,6 +39,7 @@ enum SampleField : uint64_t {
   kFAcc = 1ull << 14,        // gfx/mem activity accumulators present
   kFThrottle = 1ull << 15,
   kFFwTs = 1ull << 16,
+  kFXccAcc = 1ull << 17,     // per-XCC busy accumulators present
 };
 
 // One hardware reading of one GPU (the PMFW metrics table + HBM occupancy).
@@ -54,6 +55,8 @@ struct GpuSample {
   float gfx_busy_pct = 0;      // instantaneous, average over XCCs
   float umc_busy_pct = 0;      // memory-controller (HBM) activity
   float gfx_busy_xcc[kMaxXcc] = {};
+  float gfx_busy_xcc_window[kMaxXcc] = {};  // per-XCC exact mean since the previous distinct sample
+  uint64_t gfx_busy_acc_xcc[kMaxXcc] = {};  // PMFW per-XCC busy accumulators
   // Exact means over the interval since the previous distinct sample, derived
   // from the PMFW activity accumulators (no aliasing: every PMFW tick counts).
   float gfx_busy_window_pct = -1;

@@ -95,6 +95,8 @@ class MockBackend final : public Backend {
     s.accumulation_counter = static_cast<uint64_t>(std::llround(ms));
     s.gfx_activity_acc = static_cast<uint64_t>(std::llround(util_integral(d, tf) * 1000.0));
     s.mem_activity_acc = static_cast<uint64_t>(std::llround(util_integral(d, tf) * 500.0));
+    for (int x = 0; x < kMaxXcc; ++x) s.gfx_busy_acc_xcc[x] = s.gfx_activity_acc;
+    s.valid |= kFXccAcc;
     s.temp_hotspot_c = static_cast<float>(40 + 0.4 * u);
     s.temp_mem_c = static_cast<float>(35 + 0.2 * u);
     s.temp_vrsoc_c = static_cast<float>(38 + 0.1 * u);

@@ -77,6 +77,8 @@ py::dict sample_dict(const GpuSample& s) {
   o["umc_busy_pct"] = s.umc_busy_pct;
   o["gfx_busy_xcc"] = std::vector<float>(s.gfx_busy_xcc, s.gfx_busy_xcc + s.num_xcc);
   o["gfx_busy_window_pct"] = s.gfx_busy_window_pct;
+  o["gfx_busy_xcc_window"] = std::vector<float>(s.gfx_busy_xcc_window, s.gfx_busy_xcc_window + s.num_xcc);
+  o["gfx_busy_acc_xcc"] = std::vector<uint64_t>(s.gfx_busy_acc_xcc, s.gfx_busy_acc_xcc + s.num_xcc);
   o["umc_busy_window_pct"] = s.umc_busy_window_pct;
   o["dt_s"] = s.dt_s;
   o["temp_hotspot_c"] = s.temp_hotspot_c;

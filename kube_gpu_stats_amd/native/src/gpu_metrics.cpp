@@ -59,6 +59,7 @@ enum : size_t {
   kXcpBase = 344,        // struct amdgpu_xcp_metrics_v1_2[8], 440 B each
   kXcpStride = 440,
   kXcpGfxBusyInst = 0,   // u32[8] %
+  kXcpGfxBusyAcc = 120,  // u64[8] accumulated % (same units as gfx_activity_acc)
 };
 
 inline bool na16(uint16_t v) { return v == 0xFFFF; }
@@ -145,15 +146,20 @@ int parse_gpu_metrics_v1_8(const uint8_t* b, size_t len, GpuSample& s) {
   if (na16(nparts) || nparts == 0) nparts = 1;
   if (nparts > kV18NumXcp) nparts = kV18NumXcp;
   uint32_t nxcc = 0;
+  bool xcc_acc = true;
   for (int p = 0; p < nparts && nxcc < static_cast<uint32_t>(kMaxXcc); ++p) {
-    const size_t base = kXcpBase + static_cast<size_t>(p) * kXcpStride + kXcpGfxBusyInst;
+    const size_t base = kXcpBase + static_cast<size_t>(p) * kXcpStride;
     for (int x = 0; x < kMaxXcc && nxcc < static_cast<uint32_t>(kMaxXcc); ++x) {
-      const uint32_t v = rd<uint32_t>(b, base + 4 * x);
+      const uint32_t v = rd<uint32_t>(b, base + kXcpGfxBusyInst + 4 * x);
       if (na32(v)) continue;
+      const uint64_t acc = rd<uint64_t>(b, base + kXcpGfxBusyAcc + 8 * x);
+      xcc_acc &= !na64(acc);
+      s.gfx_busy_acc_xcc[nxcc] = na64(acc) ? 0 : acc;
       s.gfx_busy_xcc[nxcc++] = static_cast<float>(v);
     }
   }
   if (nxcc) { s.num_xcc = nxcc; valid |= kFGfxBusyXcc; }
+  if (nxcc && xcc_acc) valid |= kFXccAcc;
 
   s.valid |= valid;
   return 0;

@@ -182,14 +182,16 @@ void Exporter::render(std::string& out) {
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_gfx_busy_percent", dev_labels_[d], nullptr, snaps[d].g);
   w.head("amdgpu_gfx_busy_instant_percent", "gauge", "GFX-engine busy percent in the latest PMFW table");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFGfxBusy)) w.line("amdgpu_gfx_busy_instant_percent", dev_labels_[d], nullptr, snaps[d].s.gfx_busy_pct);
-  w.head("amdgpu_gfx_busy_xcc_percent", "gauge", "Instantaneous busy percent per XCC (accelerator complex die)");
+  w.head("amdgpu_gfx_busy_xcc_percent", "gauge",
+         "Busy percent per XCC (accelerator complex die) over the last PMFW interval (per-XCC accumulators)");
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFGfxBusyXcc)) continue;
     for (uint32_t c = 0; c < x.s.num_xcc && c < static_cast<uint32_t>(kMaxXcc); ++c) {
       char e[24];
       std::snprintf(e, sizeof e, "xcc=\"%u\"", c);
-      w.line("amdgpu_gfx_busy_xcc_percent", dev_labels_[d], e, x.s.gfx_busy_xcc[c]);
+      w.line("amdgpu_gfx_busy_xcc_percent", dev_labels_[d], e,
+             x.s.dt_s > 0 ? x.s.gfx_busy_xcc_window[c] : x.s.gfx_busy_xcc[c]);
     }
   }
   w.head("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller (UMC) activity percent, mean over the exporter window");

@@ -129,6 +129,19 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
   }
   g = g < 0 ? 0 : (g > 100 ? 100 : g);
   u = u < 0 ? 0 : (u > 100 ? 100 : u);
+  // Per-XCC (XCD) window means from the per-partition accumulators: shows load
+  // imbalance across the 8 dies that the device-wide number averages away.
+  for (uint32_t x = 0; x < cur.num_xcc && x < static_cast<uint32_t>(kMaxXcc); ++x) {
+    double v = cur.gfx_busy_xcc[x];
+    uint64_t dx;
+    if ((cur.valid & kFXccAcc) && (prev->valid & kFXccAcc) && (cur.valid & kFAcc) && (prev->valid & kFAcc) &&
+        acc_delta(prev->accumulation_counter, cur.accumulation_counter, dc) && dc > 0 &&
+        cur.gfx_busy_acc_xcc[x] >= prev->gfx_busy_acc_xcc[x]) {
+      dx = cur.gfx_busy_acc_xcc[x] - prev->gfx_busy_acc_xcc[x];
+      v = static_cast<double>(dx) / static_cast<double>(dc);
+    }
+    cur.gfx_busy_xcc_window[x] = static_cast<float>(v < 0 ? 0 : (v > 100 ? 100 : v));
+  }
   cur.gfx_busy_window_pct = static_cast<float>(g);
   cur.umc_busy_window_pct = static_cast<float>(u);
   I.gfx_busy_seconds += g * 0.01 * dt;

@@ -153,8 +153,11 @@ def test_load_throughput_and_util_accumulators(N, torch_dev):
         torch.cuda.synchronize()  # keep the queue short: the window below must see *this* load
     w = ex.window(0, 1.0)
     integ = ex.integrals(0)
+    snap = ex.snapshot(0)
     wall = time.time() - t0
     ex.stop()
+    # per-XCC accumulators: every one of the 8 dies is busy under a full-grid MFMA load
+    assert len(snap["gfx_busy_xcc_window"]) == 8 and min(snap["gfx_busy_xcc_window"]) > 90, snap
     print(json.dumps({"window": w, "integrals": integ, "wall_s": wall}))
     assert w["gfx_busy_pct"] > 90, w
     # PMFW cadence ≈ 50 Hz of distinct tables

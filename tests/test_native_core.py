@@ -28,6 +28,8 @@ def test_parse_captured_mi355x_table(N):
     assert s["gfxclk_mhz"] == [157] * 7 + [158]
     assert s["uclk_mhz"] == 2000 and s["socclk_mhz"] == 38
     assert s["num_xcc"] == 8 and s["gfx_busy_xcc"] == [0.0] * 8
+    assert s["gfx_busy_acc_xcc"][:2] == [1144238836, 1143176127]  # xcp_stats[0].gfx_busy_acc
+    assert s["valid"] & (1 << 17)
 
 
 def test_parser_rejects_other_revisions(N):
