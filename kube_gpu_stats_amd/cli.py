@@ -26,10 +26,19 @@ def main(argv=None) -> int:
     tp = sub.add_parser("topo", help="print device inventory + xGMI topology as JSON")
     tp.add_argument("--backend", default="amdsmi")
     tp.add_argument("--mock-gpus", type=int, default=8)
+    sub.add_parser("bench", help="run the headline benchmark (bench.py; flags pass through)", add_help=False)
     sp = sub.add_parser("scrape", help="scrape an exporter once and print selected families")
     sp.add_argument("url", nargs="?", default="http://127.0.0.1:9400/metrics")
     sp.add_argument("--match", default="")
 
+    if argv and argv[0] == "bench":
+        import os
+        import runpy
+
+        bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+        sys.argv = [bench] + argv[1:]
+        runpy.run_path(bench, run_name="__main__")
+        return 0
     a = ap.parse_args(argv)
     if a.cmd == "exporter":
         return exporter_main.run(a)

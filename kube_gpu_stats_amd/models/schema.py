@@ -86,6 +86,8 @@ CATALOG: tuple[Family, ...] = (
       extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
     F("amdgpu_process_gfx_seconds_total", "counter", "GFX engine time of the process (driver-reported).",
       extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
+    F("amdgpu_process_cu_seconds_total", "counter", "∫ occupied-CU share dt; rate() = the process' compute share.",
+      extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
     # ---- exporter self-metrics ---------------------------------------------------------------
     F("kgs_up", "gauge", "1 if the device's last read succeeded.", source="self"),
     F("kgs_last_sample_age_seconds", "gauge", "Seconds since the last successful read.", source="self"),

@@ -39,6 +39,10 @@ struct ProcInfo {
   uint64_t gfx_ns = 0;         // cumulative engine time (if the driver reports it)
   uint32_t cu_occupancy = 0;   // CUs in use by the process' waves
   uint32_t evicted_ms = 0;
+  // ∫ cu_occupancy / num_cu dt, integrated by the sampler across reads: ROCm compute
+  // runs on user-mode queues the driver does not time (gfx_ns reads 0 on MI355X), so
+  // CU-occupancy-seconds is the per-process compute-share counter.
+  double cu_seconds = 0;
 };
 
 struct LinkInfo {

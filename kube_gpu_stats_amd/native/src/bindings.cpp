@@ -242,6 +242,7 @@ class PyExporter {
       o["cpu_bytes"] = x.cpu_bytes;
       o["gfx_ns"] = x.gfx_ns;
       o["cu_occupancy"] = x.cu_occupancy;
+      o["cu_seconds"] = x.cu_seconds;
       o["evicted_ms"] = x.evicted_ms;
       l.append(o);
     }

@@ -358,6 +358,10 @@ void Exporter::render(std::string& out) {
     w.head("amdgpu_process_gfx_seconds_total", "counter", "GFX engine time consumed by the process (driver-reported; 0 where unsupported)");
     for (int d : ids)
       if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line("amdgpu_process_gfx_seconds_total", proc_labels(d, p), nullptr, p.gfx_ns * 1e-9);
+    w.head("amdgpu_process_cu_seconds_total", "counter",
+           "Integral of the process' CU-occupancy share (occupied CUs / all CUs) over time; rate() = compute share");
+    for (int d : ids)
+      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line("amdgpu_process_cu_seconds_total", proc_labels(d, p), nullptr, p.cu_seconds);
   }
 
   // ---- self metrics ------------------------------------------------------

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <unordered_map>
 
 namespace kgs {
 
@@ -185,6 +186,8 @@ void Sampler::run(int dev) {
   int64_t next = mono_ns();
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;
+  std::unordered_map<uint32_t, double> cu_seconds;  // pid -> ∫ occupancy share dt
+  int64_t last_proc_ns = 0;
 
   while (!stop_.load(std::memory_order_relaxed)) {
     // ---- fast tier: the PMFW table (refreshed by firmware every ≈20 ms) is
@@ -251,10 +254,22 @@ void Sampler::run(int dev) {
     // ---- mid / slow tiers -----------------------------------------------
     if (cfg_.proc_every > 0 && tick % static_cast<uint64_t>(cfg_.proc_every) == 0) {
       if (be_->read_procs(dev, procs) == 0) {
+        const int64_t now_p = mono_ns();
+        const double dt = last_proc_ns ? (now_p - last_proc_ns) * 1e-9 : 0.0;
+        const double ncu = info.num_cu > 0 ? info.num_cu : 256.0;
+        std::unordered_map<uint32_t, double> next_cu;
+        for (ProcInfo& p : procs) {
+          auto it = cu_seconds.find(p.pid);
+          const double prev_cu = it == cu_seconds.end() ? 0.0 : it->second;
+          p.cu_seconds = prev_cu + (it == cu_seconds.end() ? 0.0 : p.cu_occupancy / ncu * dt);
+          next_cu[p.pid] = p.cu_seconds;
+        }
+        cu_seconds.swap(next_cu);  // processes that exited drop out
+        last_proc_ns = now_p;
         auto p = std::make_shared<const std::vector<ProcInfo>>(procs);
         std::lock_guard<std::mutex> g(st.slow_mu);
         st.procs = std::move(p);
-        st.procs_mono_ns = mono_ns();
+        st.procs_mono_ns = now_p;
       }
     }
     if (cfg_.link_every > 0 && tick % static_cast<uint64_t>(cfg_.link_every) == 0) {

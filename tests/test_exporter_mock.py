@@ -123,6 +123,17 @@ def test_fault_isolation_vanishing_device(mock_exporter):
     assert age["1"] > 0.3 and age["0"] < 0.1
 
 
+def test_process_cu_seconds_integral(mock_exporter):
+    ex = mock_exporter(n_gpus=2, hz=100, proc_every=2)
+    time.sleep(0.2)
+    a = {p["pid"]: p["cu_seconds"] for p in ex.procs(1)}
+    time.sleep(1.0)
+    b = {p["pid"]: p["cu_seconds"] for p in ex.procs(1)}
+    # mock processes occupy 128 of 256 CUs → half a CU-share-second per second
+    for pid in b:
+        assert (b[pid] - a[pid]) == pytest.approx(0.5, abs=0.06)
+
+
 def test_energy_counter_survives_accumulator_wrap(mock_exporter):
     # accumulator wraps every ~0.4 J·2^16 units → many wraps per second
     ex = mock_exporter(n_gpus=1, hz=100, mock={"energy_wrap_at": 1 << 26, "fw_period_s": 0.01})

@@ -154,8 +154,12 @@ def test_load_throughput_and_util_accumulators(N, torch_dev):
     w = ex.window(0, 1.0)
     integ = ex.integrals(0)
     snap = ex.snapshot(0)
+    procs = ex.procs(0)
     wall = time.time() - t0
     ex.stop()
+    print(json.dumps({"procs": procs}))
+    # this process' waves occupy CUs; the occupancy integral grows (PIDs are host-namespace)
+    assert any(p["cu_occupancy"] > 0 and p["cu_seconds"] > 0 for p in procs), procs
     # per-XCC accumulators: every one of the 8 dies is busy under a full-grid MFMA load
     assert len(snap["gfx_busy_xcc_window"]) == 8 and min(snap["gfx_busy_xcc_window"]) > 90, snap
     print(json.dumps({"window": w, "integrals": integ, "wall_s": wall}))
