@@ -125,7 +125,8 @@ def get_pod_by_servers(c: PromClient, q: Queries, start, end, step_s: int, compa
 
 
 # --------------------------------------------------------------------------- aggregation (L3)
-def stats_pod_results(util_body: dict, servers: dict, server_pods: dict, compat: bool) -> list[list]:
+def stats_pod_results(util_body: dict, servers: dict, server_pods: dict, compat: bool,
+                      show_finished: bool = False) -> list[list]:
     """Reference stats_pod_results :62-94 (F3)."""
     vals: dict[str, dict[str, float]] = {}
     for res in result(util_body):
@@ -141,6 +142,8 @@ def stats_pod_results(util_body: dict, servers: dict, server_pods: dict, compat:
         for pod in sorted(pods):  # the reference iterates a set (unspecified order); sorted is stable
             cards = server_pods.get(server, {}).get(pod)
             if cards is None:  # finished pod with util but no allocation (:87-90, Q7)
+                if show_finished and not compat:
+                    lines.append([server, pod + " (finished)", 0, vals.get(server, {}).get(pod, 0.0)])
                 continue
             lines.append([server, pod, cards, vals.get(server, {}).get(pod, 0.0)])
     return lines
@@ -185,7 +188,7 @@ def stats_server_results(util_body: dict, servers: dict, time_range_s: float, st
 
 # --------------------------------------------------------------------------- report (L4)
 def run_report(c: PromClient, q: Queries, end: datetime | float, window_s: float, step_s: int, compat: bool,
-               mode: str = "pod", missing: str = "skip", out=sys.stdout) -> list[list]:
+               mode: str = "pod", missing: str = "skip", out=sys.stdout, show_finished: bool = False) -> list[list]:
     if isinstance(end, (int, float)):
         end = datetime.fromtimestamp(end)
     start = end - timedelta(seconds=window_s)
@@ -195,7 +198,7 @@ def run_report(c: PromClient, q: Queries, end: datetime | float, window_s: float
         pods = None if compat else get_pod_by_servers(c, q, start, end, step_s, compat, out)
         return stats_server_results(util, servers, window_s, step_s, compat, missing, pods)
     pods = get_pod_by_servers(c, q, start, end, step_s, compat, out)     # M4, M5
-    return stats_pod_results(util, servers, pods, compat)
+    return stats_pod_results(util, servers, pods, compat, show_finished)
 
 
 def format_rows(rows: list[list], mode: str, fmt: str, compat: bool) -> str:
@@ -227,6 +230,7 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "type-label", "label_amd_com_gpu_product_name", "kube_node_labels label holding the GPU type")
     add_flag(ap, "util-metric", "container_gpu_sm_util", "utilisation series")
     add_flag(ap, "format", "table", "table | json | csv")
+    add_flag(ap, "show-finished", False, "also list pods with utilisation but no live allocation (reference drops them)")
     return ap
 
 
@@ -235,7 +239,7 @@ def run(a) -> int:
     q = (Queries.compat(a.namespace) if a.compat else
          Queries.amd(a.namespace, a.step, a.resource, a.type_label, a.util_metric))
     end = a.end if a.end else (datetime.now() if a.compat else time.time())
-    rows = run_report(c, q, end, a.window, a.step, a.compat, a.mode, a.missing)
+    rows = run_report(c, q, end, a.window, a.step, a.compat, a.mode, a.missing, show_finished=a.show_finished)
     print(format_rows(rows, a.mode, a.format, a.compat))
     return 0
 

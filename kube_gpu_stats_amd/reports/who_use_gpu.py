@@ -181,15 +181,18 @@ def census(pods: dict, compat: bool, resources: tuple[str, ...] = (AMD_GPU_RESOU
     return rows, total, per_type
 
 
-HEADER = ["Namespace", "Node", "Pod", "GPU Type", "GPU Cores"]
+HEADER = ["Namespace", "Node", "Pod", "GPU Type", "GPU Cores"]  # reference header (who:11); counts devices (Q16)
+HEADER_FIXED = ["Namespace", "Node", "Pod", "GPU Type", "GPUs"]
 
 
-def format_report(rows: list[Row], total: int, per_type: dict[str, int], fmt: str = "table") -> str:
+def format_report(rows: list[Row], total: int, per_type: dict[str, int], fmt: str = "table",
+                  compat: bool = True) -> str:
+    header = HEADER if compat else HEADER_FIXED
     if fmt == "json":
         return json.dumps({"pods": [r.__dict__ for r in rows], "total": total, "per_type": per_type}, indent=2)
     if fmt == "csv":
-        return render_csv(HEADER, [r.as_list() for r in rows])
-    lines = [render(HEADER, [r.as_list() for r in rows]), "Total GPU: %d" % total]
+        return render_csv(header, [r.as_list() for r in rows])
+    lines = [render(header, [r.as_list() for r in rows]), "Total GPU: %d" % total]
     lines += ["%s\t%d" % (t, n) for t, n in per_type.items()]
     return "\n".join(lines)
 
@@ -220,7 +223,7 @@ def run(a) -> int:
         with open(a.nodes_json) as f:
             nodes = {n["metadata"]["name"]: n for n in json.load(f).get("items", [])}
     rows, total, per_type = census(pods, a.compat, resources, nodes, a.include_finished)
-    print(format_report(rows, total, per_type, "table" if a.compat else a.format))
+    print(format_report(rows, total, per_type, "table" if a.compat else a.format, compat=a.compat))
     return 0
 
 

@@ -109,6 +109,9 @@ def test_who_use_gpu_compat_golden():
     text = W.format_report(rows, total, per_type)
     assert text.splitlines()[-3:] == ["Total GPU: 7", "tesla-v100\t6", "<unspecified>\t1"]
     assert "| Namespace |  Node  |   Pod   |    GPU Type   | GPU Cores |" in text
+    # Q16: the column counts devices, so fixed mode names it "GPUs"
+    fixed = W.format_report(rows, total, per_type, compat=False)
+    assert "GPU Cores" not in fixed and "GPUs |" in fixed
 
 
 def test_who_use_gpu_fixed_mode():

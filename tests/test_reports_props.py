@@ -39,6 +39,21 @@ def test_pod_report_properties(series, alloc, inventory):
     assert {(r[0], r[1]) for r in rows} == expected
 
 
+def test_show_finished_lists_unallocated_pods():
+    """Q7: the reference silently drops pods that have utilisation but no live
+    allocation; ``show_finished`` lists them as finished with 0 cards."""
+    util = {"data": {"result": [
+        {"metric": {"kubernetes_io_hostname": "n1", "pod_name": "live"}, "values": [[0, "40"], [1, "60"]]},
+        {"metric": {"kubernetes_io_hostname": "n1", "pod_name": "gone"}, "values": [[0, "10"]]}]}}
+    servers = {"n1": (8, 1, "MI355X")}
+    alloc = {"n1": {"live": 2}}
+    assert [r[1] for r in G.stats_pod_results(util, servers, alloc, compat=False)] == ["live"]
+    rows = G.stats_pod_results(util, servers, alloc, compat=False, show_finished=True)
+    assert sorted((r[1], r[2], round(r[3])) for r in rows) == [("gone (finished)", 0, 10), ("live", 2, 50)]
+    # compat keeps the reference behaviour regardless
+    assert [r[1] for r in G.stats_pod_results(util, servers, alloc, compat=True, show_finished=True)] == ["live"]
+
+
 @settings(max_examples=60, deadline=None)
 @given(series=st.lists(st.tuples(pods, st.lists(st.floats(0, 100, allow_nan=False), min_size=1, max_size=10)),
                        min_size=1, max_size=5))
