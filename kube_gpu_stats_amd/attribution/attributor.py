@@ -8,6 +8,13 @@
   held by exactly one container; its pod UID always comes from its cgroup.
 * Optional static mapping file (JSON ``{"<device id>": {"pod":..,"namespace":..,
   "container":..}}``) for nodes without a kubelet socket (and the 1-GPU box).
+
+Failure handling: the kubelet socket may not exist yet when the
+DaemonSet pod starts and disappears while kubelet restarts.  The client is
+created lazily once the socket shows up and re-created after a failed call; the
+last good GPU→pod table is kept for ``stale_after_s`` so a kubelet restart does
+not strip the pod labels from every series, then dropped.  The loop's own health
+is exported as ``kgs_attribution_*`` on /metrics.
 """
 from __future__ import annotations
 
@@ -25,19 +32,66 @@ L = log.get("attribution")
 
 class Attributor:
     def __init__(self, exporter, socket_path: str | None = None, static_map: str | None = None,
-                 resources=GPU_RESOURCES, interval_s: float = 1.0, proc_root: str = "/proc"):
+                 resources=GPU_RESOURCES, interval_s: float = 1.0, proc_root: str = "/proc",
+                 stale_after_s: float = 30.0):
         self.ex = exporter
         self.interval_s = interval_s
         self.proc_root = proc_root
         self.resources = tuple(resources)
         self.index = DeviceIndex(exporter.devices())
-        self.client = PodResourcesClient(socket_path) if socket_path and os.path.exists(socket_path) else None
+        self.socket_path = socket_path
+        self.client: PodResourcesClient | None = None
         self.static_map = static_map
+        self.stale_after_s = stale_after_s
         self.owners: dict[int, list[dict]] = {}
+        self.kubelet_owners: dict[int, list[dict]] = {}
+        self.last_kubelet_ok = 0.0
         self.errors = 0
+        self.reconnects = 0
         self.updates = 0
         self._stop = threading.Event()
         self._th: threading.Thread | None = None
+        self._connect()
+
+    # ------------------------------------------------------------------ kubelet
+    def _connect(self) -> bool:
+        if self.client is None and self.socket_path and os.path.exists(self.socket_path):
+            self.client = PodResourcesClient(self.socket_path)
+            return True
+        return self.client is not None
+
+    def _drop_client(self) -> None:
+        if self.client is not None:
+            try:
+                self.client.close()
+            except Exception:  # noqa: BLE001
+                pass
+            self.client = None
+            self.reconnects += 1
+
+    def _kubelet_owners(self) -> dict[int, list[dict]]:
+        """Allocations from kubelet, or the last good table while it is briefly away."""
+        if self.socket_path and self._connect():
+            try:
+                owners: dict[int, list[dict]] = {}
+                for a in self.client.gpu_allocations(self.resources):
+                    i = self.index.resolve(a.device_id)
+                    if i is None:
+                        continue
+                    o = {"pod": a.pod, "namespace": a.namespace, "container": a.container}
+                    if o not in owners.setdefault(i, []):
+                        owners[i].append(o)
+                self.kubelet_owners = owners
+                self.last_kubelet_ok = time.monotonic()
+                return owners
+            except Exception as e:  # noqa: BLE001 - grpc.RpcError and decode errors alike
+                self.errors += 1
+                L.warning("kubelet pod-resources List failed: %s", e)
+                self._drop_client()
+        if self.kubelet_owners and time.monotonic() - self.last_kubelet_ok > self.stale_after_s:
+            L.warning("kubelet unreachable for %.0fs: dropping pod attribution", self.stale_after_s)
+            self.kubelet_owners = {}
+        return self.kubelet_owners
 
     # ------------------------------------------------------------------ one pass
     def device_owners(self) -> dict[int, list[dict]]:
@@ -50,12 +104,8 @@ class Attributor:
                         owners.setdefault(i, []).append(
                             {"pod": o.get("pod", ""), "namespace": o.get("namespace", ""),
                              "container": o.get("container", "")})
-        if self.client is not None:
-            for a in self.client.gpu_allocations(self.resources):
-                i = self.index.resolve(a.device_id)
-                if i is None:
-                    continue
-                o = {"pod": a.pod, "namespace": a.namespace, "container": a.container}
+        for i, lst in self._kubelet_owners().items():
+            for o in lst:
                 if o not in owners.setdefault(i, []):
                     owners[i].append(o)
         return owners
@@ -81,6 +131,36 @@ class Attributor:
         self.owners = owners
         self.ex.set_pid_owners(self.pid_owners(owners))
         self.updates += 1
+        self.publish()
+
+    def self_metrics(self) -> str:
+        age = time.monotonic() - self.last_kubelet_ok if self.last_kubelet_ok else -1.0
+        connected = 1 if self.client is not None else 0
+        return "\n".join([
+            "# HELP kgs_attribution_updates_total Attribution passes completed",
+            "# TYPE kgs_attribution_updates_total counter",
+            f"kgs_attribution_updates_total {self.updates}",
+            "# HELP kgs_attribution_errors_total Failed attribution passes / kubelet calls",
+            "# TYPE kgs_attribution_errors_total counter",
+            f"kgs_attribution_errors_total {self.errors}",
+            "# HELP kgs_attribution_kubelet_reconnects_total Pod-resources client re-creations",
+            "# TYPE kgs_attribution_kubelet_reconnects_total counter",
+            f"kgs_attribution_kubelet_reconnects_total {self.reconnects}",
+            "# HELP kgs_attribution_kubelet_connected 1 if a pod-resources client is open",
+            "# TYPE kgs_attribution_kubelet_connected gauge",
+            f"kgs_attribution_kubelet_connected {connected}",
+            "# HELP kgs_attribution_kubelet_age_seconds Seconds since the last good kubelet List (-1: never)",
+            "# TYPE kgs_attribution_kubelet_age_seconds gauge",
+            f"kgs_attribution_kubelet_age_seconds {age:.3f}",
+            "# HELP kgs_attribution_allocated_gpus GPUs with at least one owning container",
+            "# TYPE kgs_attribution_allocated_gpus gauge",
+            f"kgs_attribution_allocated_gpus {sum(1 for v in self.owners.values() if v)}",
+        ]) + "\n"
+
+    def publish(self) -> None:
+        setter = getattr(self.ex, "set_extra_metrics", None)
+        if setter is not None:
+            setter(self.self_metrics())
 
     # ------------------------------------------------------------------ thread
     def _run(self) -> None:
@@ -90,6 +170,7 @@ class Attributor:
             except Exception as e:  # noqa: BLE001 - keep attributing; kubelet restarts are normal
                 self.errors += 1
                 L.warning("attribution pass failed: %s", e)
+                self.publish()
             self._stop.wait(self.interval_s)
 
     def start(self) -> "Attributor":
@@ -101,5 +182,4 @@ class Attributor:
         self._stop.set()
         if self._th:
             self._th.join(timeout=5)
-        if self.client:
-            self.client.close()
+        self._drop_client()

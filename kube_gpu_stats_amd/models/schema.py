@@ -95,6 +95,8 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_reads_total", "counter", "Sampler reads attempted.", source="self"),
     F("kgs_read_errors_total", "counter", "Sampler reads that failed.", source="self"),
     F("kgs_sampler_overruns_total", "counter", "Ticks that overran the period.", source="self"),
+    F("kgs_device_recoveries_total", "counter",
+      "Backend re-opens / AMD SMI re-inits that restored reads after a failure streak (GPU reset).", source="self"),
     F("kgs_pmc_samples_total", "counter", "Hardware-counter drains completed.", source="self"),
     F("kgs_pmc_errors_total", "counter", "Hardware-counter drains that failed.", source="self"),
     F("kgs_pmc_read_seconds_total", "counter", "Time spent draining hardware counters.", source="self"),
@@ -107,6 +109,18 @@ CATALOG: tuple[Family, ...] = (
       "self"),
     F("kgs_build_info", "gauge", "Build / configuration (1).",
       ("kubernetes_io_hostname", "version", "backend", "pmc_source", "sample_hz"), "self"),
+    # ---- attribution loop (Python control plane, pushed via set_extra_metrics) ---------------
+    F("kgs_attribution_updates_total", "counter", "Attribution passes completed.", (), "attribution", "attr"),
+    F("kgs_attribution_errors_total", "counter", "Failed attribution passes / kubelet calls.", (), "attribution",
+      "attr"),
+    F("kgs_attribution_kubelet_reconnects_total", "counter", "Pod-resources client re-creations.", (),
+      "attribution", "attr"),
+    F("kgs_attribution_kubelet_connected", "gauge", "1 if a pod-resources client is open.", (), "attribution",
+      "attr"),
+    F("kgs_attribution_kubelet_age_seconds", "gauge", "Seconds since the last good kubelet List (-1: never).", (),
+      "attribution", "attr"),
+    F("kgs_attribution_allocated_gpus", "gauge", "GPUs with at least one owning container.", (), "attribution",
+      "attr"),
 )
 
 BY_NAME = {f.name: f for f in CATALOG}

@@ -85,6 +85,11 @@ class Backend {
   virtual int topology(std::vector<TopoEdge>& out) = 0;
   // Slow tier: ECC totals and xGMI error status.
   virtual int read_health(int dev, HealthInfo& out) { return -1; }
+  // Called by the sampler after repeated read failures (GPU reset, driver
+  // reload): reopen file handles, re-resolve the device and, if needed,
+  // re-initialise the management library.  0 when the device reads again;
+  // the sampler then drops its accumulator baseline (counters restart).
+  virtual int recover(int dev) { return -1; }
 };
 
 // Mock provider configuration (tests, plumbing benchmark).
@@ -97,6 +102,8 @@ struct MockConfig {
   double stall_s = 0;           // extra latency injected into every read
   int vanish_dev = -1;          // device that starts failing after vanish_after_s
   double vanish_after_s = 0;
+  double vanish_for_s = -1;     // >=0: the device is back after this long, but only
+                                // once recover() ran (models a GPU reset that needs a reopen)
   uint64_t energy_wrap_at = 0;  // if >0 the energy accumulator wraps at this value
   uint64_t ecc_correctable_per_s = 0;  // injected correctable ECC error rate
   uint64_t seed = 1;

@@ -72,6 +72,9 @@ class Exporter {
   void set_device_owners(int dev, std::vector<Owner> owners);
   void set_pid_owners(std::unordered_map<uint32_t, PidOwner> m);
   void set_node_name(const std::string& n);
+  // Pre-rendered exposition text from the control plane (attribution
+  // self-metrics) appended to every /metrics body; swapped atomically.
+  void set_extra_metrics(std::string text);
 
   // Prometheus text exposition of everything (the /metrics body).
   void render(std::string& out);
@@ -107,6 +110,7 @@ class Exporter {
   std::shared_ptr<const std::map<int, std::vector<Owner>>> owners_;
   std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> pid_owners_;
   std::string node_name_;
+  std::shared_ptr<const std::string> extra_;
 };
 
 // Escape a Prometheus label value.

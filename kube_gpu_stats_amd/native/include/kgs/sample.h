@@ -112,6 +112,8 @@ struct Integrals {
   uint64_t pmc_errors = 0;
   double read_seconds = 0;       // total time spent in backend reads
   double pmc_read_seconds = 0;   // total time spent in counter drains
+  uint64_t recoveries = 0;       // successful Backend::recover() after a failure streak
+  uint64_t recover_attempts = 0;
 };
 static_assert(std::is_trivially_copyable<Integrals>::value, "seqlock payload");
 

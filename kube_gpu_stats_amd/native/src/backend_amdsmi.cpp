@@ -67,6 +67,7 @@ class AmdSmiBackend final : public Backend {
   }
 
   bool init(std::string& err, const std::string& sysfs_root) {
+    sysfs_root_ = sysfs_root;
     amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
     if (st != AMDSMI_STATUS_SUCCESS) {
       err = "amdsmi_init failed: status " + std::to_string(static_cast<int>(st));
@@ -117,7 +118,10 @@ class AmdSmiBackend final : public Backend {
       if (n > 0 && gpu_metrics_revision(dv.buf, static_cast<size_t>(n)) == 0x0108)
         rc = parse_gpu_metrics_v1_8(dv.buf, static_cast<size_t>(n), s);
     }
-    if (rc != 0) rc = read_metrics_amdsmi(dv, s);
+    if (rc != 0) {
+      std::lock_guard<std::mutex> g(smi_mu_);
+      rc = read_metrics_amdsmi_locked(dv, s);
+    }
     if (rc != 0) return rc;
     read_vram(dv, s);
     s.mono_ns = now_ns(CLOCK_MONOTONIC);
@@ -212,7 +216,63 @@ class AmdSmiBackend final : public Backend {
     return 0;
   }
 
+  // After a GPU reset or driver reload: (1) reopen the sysfs files, re-resolving
+  // the DRM card by PCI address (card numbers can change on reload); (2) if the
+  // table still does not read, re-initialise AMD SMI (stale handles) at most
+  // once per 10 s for all devices and remap every handle by BDF.
+  int recover(int d) override {
+    std::lock_guard<std::mutex> g(smi_mu_);
+    Dev& dv = *devs_[d];
+    const std::string dir = find_sysfs_dir(sysfs_root_, -1, dv.info.bdf);
+    if (!dir.empty() && dir != dv.info.sysfs_dir) dv.info.sysfs_dir = dir;
+    open_files(dv);
+    GpuSample s;
+    if (dv.fd_metrics >= 0) {
+      const ssize_t n = pread(dv.fd_metrics, dv.buf, sizeof dv.buf, 0);
+      if (n > 0 && parse_gpu_metrics_v1_8(dv.buf, static_cast<size_t>(n), s) == 0) return 0;
+    }
+    const int64_t now = now_ns(CLOCK_MONOTONIC);
+    if (now - last_reinit_ns_ < 10000000000LL) return -1;
+    last_reinit_ns_ = now;
+    ++reinits_;
+    if (!reinit_locked()) return -1;
+    return read_metrics_amdsmi_locked(dv, s);
+  }
+
  private:
+  bool reinit_locked() {
+    if (inited_) amdsmi_shut_down();
+    inited_ = amdsmi_init(AMDSMI_INIT_AMD_GPUS) == AMDSMI_STATUS_SUCCESS;
+    if (!inited_) return false;
+    uint32_t nsock = 0;
+    if (amdsmi_get_socket_handles(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS) return false;
+    std::vector<amdsmi_socket_handle> socks(nsock);
+    amdsmi_get_socket_handles(&nsock, socks.data());
+    for (auto s : socks) {
+      uint32_t np = 0;
+      if (amdsmi_get_processor_handles(s, &np, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+      std::vector<amdsmi_processor_handle> hs(np);
+      amdsmi_get_processor_handles(s, &np, hs.data());
+      for (auto h : hs) {
+        amdsmi_bdf_t bdf;
+        if (amdsmi_get_gpu_device_bdf(h, &bdf) != AMDSMI_STATUS_SUCCESS) continue;
+        const std::string b = fmt_bdf(bdf);
+        for (auto& dv : devs_)
+          if (dv->info.bdf == b) dv->h = h;
+      }
+    }
+    return true;
+  }
+
+  static void open_files(Dev& d) {
+    if (d.fd_metrics >= 0) close(d.fd_metrics);
+    if (d.fd_vram_used >= 0) close(d.fd_vram_used);
+    d.fd_metrics = d.fd_vram_used = -1;
+    if (d.info.sysfs_dir.empty()) return;
+    d.fd_metrics = open((d.info.sysfs_dir + "/gpu_metrics").c_str(), O_RDONLY | O_CLOEXEC);
+    d.fd_vram_used = open((d.info.sysfs_dir + "/mem_info_vram_used").c_str(), O_RDONLY | O_CLOEXEC);
+  }
+
   void add_device(amdsmi_processor_handle h, const std::string& sysfs_root) {
     auto d = std::make_unique<Dev>();
     d->h = h;
@@ -255,8 +315,7 @@ class AmdSmiBackend final : public Backend {
 
     in.sysfs_dir = find_sysfs_dir(sysfs_root, in.drm_card, in.bdf);
     if (!in.sysfs_dir.empty()) {
-      d->fd_metrics = open((in.sysfs_dir + "/gpu_metrics").c_str(), O_RDONLY | O_CLOEXEC);
-      d->fd_vram_used = open((in.sysfs_dir + "/mem_info_vram_used").c_str(), O_RDONLY | O_CLOEXEC);
+      open_files(*d);
       std::string tot;
       if (read_small_file(in.sysfs_dir + "/mem_info_vram_total", tot)) in.vram_total_bytes = std::strtoull(tot.c_str(), nullptr, 10);
     }
@@ -300,6 +359,7 @@ class AmdSmiBackend final : public Backend {
       }
     }
     amdsmi_vram_usage_t vu;
+    std::lock_guard<std::mutex> g(smi_mu_);
     if (amdsmi_get_gpu_vram_usage(dv.h, &vu) == AMDSMI_STATUS_SUCCESS) {
       s.vram_used_bytes = static_cast<uint64_t>(vu.vram_used) * 1048576ull;
       s.vram_total_bytes = static_cast<uint64_t>(vu.vram_total) * 1048576ull;
@@ -308,7 +368,7 @@ class AmdSmiBackend final : public Backend {
   }
 
   // Generic path for any other table revision (e.g. a future driver).
-  int read_metrics_amdsmi(Dev& dv, GpuSample& s) {
+  int read_metrics_amdsmi_locked(Dev& dv, GpuSample& s) {
     amdsmi_gpu_metrics_t m;
     std::memset(&m, 0, sizeof m);
     if (amdsmi_get_gpu_metrics_info(dv.h, &m) != AMDSMI_STATUS_SUCCESS) return -1;
@@ -342,6 +402,9 @@ class AmdSmiBackend final : public Backend {
   }
 
   bool inited_ = false;
+  std::string sysfs_root_;
+  int64_t last_reinit_ns_ = 0;
+  uint64_t reinits_ = 0;
   std::mutex smi_mu_;
   std::vector<std::unique_ptr<Dev>> devs_;
 };

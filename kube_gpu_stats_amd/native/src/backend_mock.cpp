@@ -5,6 +5,7 @@
 // check the exporter's integrals against analytic values.  Fault injection
 // covers the failure modes of SURVEY.md §5.3: read errors, stalls, a device
 // that disappears, accumulator wrap.
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <ctime>
@@ -74,12 +75,31 @@ class MockBackend final : public Backend {
     return cfg_.util_base * t + cfg_.util_amp / w * (std::cos(ph) - std::cos(w * t + ph));
   }
 
+  // A vanished device stays gone for vanish_for_s, then needs recover(): like a
+  // GPU reset, the firmware restarts with its accumulators at zero.
+  bool gone(int d, double t) const {
+    if (cfg_.vanish_dev != d || t < cfg_.vanish_after_s) return false;
+    if (cfg_.vanish_for_s < 0 || t < cfg_.vanish_after_s + cfg_.vanish_for_s) return true;
+    return reset_ns_.load(std::memory_order_acquire) == 0;
+  }
+
+  int recover(int d) override {
+    const int64_t now = mono_ns();
+    if (cfg_.vanish_dev != d || cfg_.vanish_for_s < 0) return gone(d, (now - t0_) * 1e-9) ? -1 : 0;
+    if ((now - t0_) * 1e-9 < cfg_.vanish_after_s + cfg_.vanish_for_s) return -1;
+    int64_t expect = 0;
+    reset_ns_.compare_exchange_strong(expect, now, std::memory_order_acq_rel);
+    return 0;
+  }
+
   int read_metrics(int d, GpuSample& s) override {
     const int64_t now = mono_ns();
-    const double t = (now - t0_) * 1e-9;
+    double t = (now - t0_) * 1e-9;
     if (cfg_.stall_s > 0) std::this_thread::sleep_for(std::chrono::duration<double>(cfg_.stall_s));
-    if (cfg_.vanish_dev == d && t >= cfg_.vanish_after_s) return -2;
+    if (gone(d, t)) return -2;
     if (cfg_.fail_rate > 0 && next_uniform(d) < cfg_.fail_rate) return -1;
+    const int64_t rs = reset_ns_.load(std::memory_order_acquire);
+    if (d == cfg_.vanish_dev && rs != 0) t = (now - rs) * 1e-9;  // firmware clock restarted
 
     // Firmware time: quantised to the PMFW cadence.
     const double tf = std::floor(t / cfg_.fw_period_s) * cfg_.fw_period_s;
@@ -133,8 +153,8 @@ class MockBackend final : public Backend {
 
   int read_procs(int d, std::vector<ProcInfo>& out) override {
     out.clear();
-    if (cfg_.vanish_dev == d && (mono_ns() - t0_) * 1e-9 >= cfg_.vanish_after_s) return -2;
     const double t = (mono_ns() - t0_) * 1e-9;
+    if (gone(d, t)) return -2;
     for (int k = 0; k < 1 + (d % 2); ++k) {
       ProcInfo p;
       p.pid = static_cast<uint32_t>(100000 + d * 10 + k);
@@ -196,6 +216,7 @@ class MockBackend final : public Backend {
 
   MockConfig cfg_;
   int64_t t0_;
+  std::atomic<int64_t> reset_ns_{0};
   std::vector<DeviceInfo> infos_;
   std::vector<uint64_t> rng_;
   std::vector<std::mutex> rng_mu_;

@@ -32,6 +32,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.stall_s = get<double>(m, "stall_s", c.mock.stall_s);
     c.mock.vanish_dev = get<int>(m, "vanish_dev", c.mock.vanish_dev);
     c.mock.vanish_after_s = get<double>(m, "vanish_after_s", c.mock.vanish_after_s);
+    c.mock.vanish_for_s = get<double>(m, "vanish_for_s", c.mock.vanish_for_s);
     c.mock.energy_wrap_at = get<uint64_t>(m, "energy_wrap_at", c.mock.energy_wrap_at);
     c.mock.seed = get<uint64_t>(m, "seed", c.mock.seed);
     c.mock.ecc_correctable_per_s = get<uint64_t>(m, "ecc_correctable_per_s", c.mock.ecc_correctable_per_s);
@@ -187,6 +188,8 @@ class PyExporter {
     o["reads"] = I.reads;
     o["read_errors"] = I.read_errors;
     o["overruns"] = I.overruns;
+    o["recoveries"] = I.recoveries;
+    o["recover_attempts"] = I.recover_attempts;
     o["pmc_samples"] = I.pmc_samples;
     o["pmc_errors"] = I.pmc_errors;
     o["read_seconds"] = I.read_seconds;
@@ -291,6 +294,7 @@ class PyExporter {
     ex_.set_pid_owners(std::move(mm));
   }
   void set_node_name(const std::string& n) { ex_.set_node_name(n); }
+  void set_extra_metrics(const std::string& t) { ex_.set_extra_metrics(t); }
   py::dict stats() const {
     py::dict o;
     o["scrapes"] = ex_.scrapes.load();
@@ -353,6 +357,7 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("set_device_owners", &PyExporter::set_device_owners)
       .def("set_pid_owners", &PyExporter::set_pid_owners)
       .def("set_node_name", &PyExporter::set_node_name)
+      .def("set_extra_metrics", &PyExporter::set_extra_metrics)
       .def("stats", &PyExporter::stats)
       .def("healthy", &PyExporter::healthy)
       .def("pause", &PyExporter::pause)

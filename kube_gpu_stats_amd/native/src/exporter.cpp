@@ -148,6 +148,13 @@ void Exporter::set_node_name(const std::string& n) {
   node_name_ = n;
 }
 
+void Exporter::set_extra_metrics(std::string text) {
+  if (!text.empty() && text.back() != '\n') text += '\n';
+  auto p = std::make_shared<const std::string>(std::move(text));
+  std::lock_guard<std::mutex> g(mu_);
+  extra_ = std::move(p);
+}
+
 std::shared_ptr<const std::map<int, std::vector<Owner>>> Exporter::owners() const {
   std::lock_guard<std::mutex> g(mu_);
   return owners_;

@@ -84,9 +84,11 @@ void Exporter::render(std::string& out) {
   std::vector<char> sampled(static_cast<size_t>(nd), 0);
   for (int d : ids) sampled[static_cast<size_t>(d)] = 1;
   std::string node;
+  std::shared_ptr<const std::string> extra;
   {
     std::lock_guard<std::mutex> g(mu_);
     node = node_name_;
+    extra = extra_;
   }
   const auto own = owners();
   const auto pown = pid_owners();
@@ -380,6 +382,9 @@ void Exporter::render(std::string& out) {
   for (int d : ids) w.line_u("kgs_read_errors_total", dev_labels_[d], nullptr, snaps[d].I.read_errors);
   w.head("kgs_sampler_overruns_total", "counter", "Ticks whose work overran the sampling period");
   for (int d : ids) w.line_u("kgs_sampler_overruns_total", dev_labels_[d], nullptr, snaps[d].I.overruns);
+  w.head("kgs_device_recoveries_total", "counter",
+         "Device re-opens / management-library re-inits that restored reads after a failure streak");
+  for (int d : ids) w.line_u("kgs_device_recoveries_total", dev_labels_[d], nullptr, snaps[d].I.recoveries);
   w.head("kgs_pmc_samples_total", "counter", "Hardware-counter drains completed");
   for (int d : ids) w.line_u("kgs_pmc_samples_total", dev_labels_[d], nullptr, snaps[d].I.pmc_samples);
   w.head("kgs_pmc_read_seconds_total", "counter", "Time spent draining hardware counters");
@@ -425,6 +430,7 @@ void Exporter::render(std::string& out) {
     kv(lb, "sample_hz", std::to_string(S.config().hz));
     w.line("kgs_build_info", lb, nullptr, 1);
   }
+  if (extra) out += *extra;
 
   const int64_t dt = mono_ns() - t0;
   scrapes.fetch_add(1);

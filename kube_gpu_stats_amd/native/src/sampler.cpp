@@ -212,8 +212,11 @@ void Sampler::run(int dev) {
         st.consecutive_errors.store(0, std::memory_order_relaxed);
         st.last_ok_mono_ns.store(t1, std::memory_order_relaxed);
         const bool distinct = !have_prev || !(s.valid & kFFwTs) || s.fw_ts != prev.fw_ts;
+        // Firmware clock went backwards: the SMU restarted (GPU reset), so every
+        // accumulator restarted too — re-baseline instead of reading a wrap.
+        const bool reset = have_prev && (s.valid & kFFwTs) && (prev.valid & kFFwTs) && s.fw_ts < prev.fw_ts;
         if (distinct) {
-          integrate(dev, have_prev ? &prev : nullptr, s, I);
+          integrate(dev, have_prev && !reset ? &prev : nullptr, s, I);
           s.seq = ++seq;
           ++I.distinct_samples;
           st.ring.push(s);
@@ -232,6 +235,15 @@ void Sampler::run(int dev) {
         const uint64_t ce = st.consecutive_errors.fetch_add(1, std::memory_order_relaxed) + 1;
         if (ce >= 3) st.up.store(0, std::memory_order_relaxed);
         backoff_shift = ce > 10 ? 10 : static_cast<int>(ce);
+        // Every 4th failure of a streak (≈ every 4·max_backoff once backed off):
+        // let the backend reopen / re-initialise the device.
+        if (ce % 4 == 0) {
+          ++I.recover_attempts;
+          if (be_->recover(dev) == 0) {
+            ++I.recoveries;
+            have_prev = false;
+          }
+        }
       }
     }
 

@@ -149,10 +149,53 @@ static void test_sampler() {
               static_cast<unsigned long long>(I0.read_errors));
 }
 
+// Reset + recover() on one device while readers hammer every device.
+static void test_recovery() {
+  MockConfig mc;
+  mc.n_gpus = 2;
+  mc.fw_period_s = 0.002;
+  mc.vanish_dev = 1;
+  mc.vanish_after_s = 0.1;
+  mc.vanish_for_s = 0.1;
+  auto be = make_mock_backend(mc);
+  SamplerConfig sc;
+  sc.hz = 500;
+  sc.pmfw_hz = 0;
+  sc.proc_every = 3;
+  sc.link_every = 5;
+  sc.pin_numa = false;
+  sc.pmc = false;
+  sc.max_backoff_ms = 10;
+  Sampler s(be.get(), nullptr, sc);
+  s.start();
+  std::atomic<bool> done{false};
+  std::thread rd([&] {
+    while (!done)
+      for (int d = 0; d < 2; ++d) {
+        double g, u;
+        int n;
+        s.window_busy(d, 0.05, g, u, n);
+        Integrals I;
+        s.state(d).integ.load(I);
+      }
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(500));
+  done = true;
+  rd.join();
+  s.stop();
+  Integrals I1;
+  s.state(1).integ.load(I1);
+  CHECK(I1.recoveries == 1);
+  CHECK(s.state(1).up.load() == 1);
+  CHECK(I1.energy_joules > 0);
+  std::printf("recovery ok (%llu attempts)\n", static_cast<unsigned long long>(I1.recover_attempts));
+}
+
 int main() {
   test_seqlock();
   test_ring();
   test_sampler();
+  test_recovery();
   std::printf("ALL OK\n");
   return 0;
 }

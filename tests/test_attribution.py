@@ -119,3 +119,32 @@ def test_attributor_survives_kubelet_outage(mock_exporter, tmp_path):
     time.sleep(0.3)  # kubelet gone: passes fail, thread keeps running
     a.stop()
     assert a.updates >= 1 and a.errors >= 1
+
+
+def test_attributor_late_kubelet_reconnect_and_stale_drop(mock_exporter, tmp_path):
+    """Socket absent at start → connects when it appears; a kubelet restart keeps
+    the last table for stale_after_s, reconnects, and drops it only past that."""
+    ex = mock_exporter(n_gpus=2)
+    sock = str(tmp_path / "kubelet.sock")
+    a = Attributor(ex, sock, stale_after_s=0.5)
+    a.update_once()
+    assert a.client is None and a.owners == {}
+    with FakeKubelet(sock, sample_response()):
+        a.update_once()
+        assert a.client is not None and sorted(a.owners) == [0, 1]
+    a.update_once()  # kubelet gone: the call fails, the last table is kept
+    assert a.errors == 1 and a.reconnects == 1 and sorted(a.owners) == [0, 1]
+    m = parse_text(ex.render())
+    assert {lb["pod_name"] for lb, _ in m["container_gpu_sm_util"]} == {"train-0"}
+    assert m["kgs_attribution_errors_total"][0][1] == 1
+    assert m["kgs_attribution_kubelet_connected"][0][1] == 0
+    with FakeKubelet(sock, sample_response()):  # kubelet back: new client
+        a.update_once()
+        assert a.client is not None and a.errors == 1
+    a.update_once()
+    assert sorted(a.owners) == [0, 1] and a.errors == 2  # gone again, table still fresh
+    time.sleep(0.6)
+    a.update_once()
+    assert a.owners == {}  # past stale_after_s: pod labels dropped
+    assert "container_gpu_sm_util" not in parse_text(ex.render())
+    a.stop()

@@ -123,6 +123,29 @@ def test_fault_isolation_vanishing_device(mock_exporter):
     assert age["1"] > 0.3 and age["0"] < 0.1
 
 
+def test_device_recovers_after_reset(mock_exporter):
+    """A GPU that drops out (reset) comes back once the backend re-opens it; its
+    firmware clock and accumulators restart at zero, and the sampler re-baselines
+    instead of reading a wrap: counters stay monotonic, the window stays sane."""
+    ex = mock_exporter(n_gpus=2, hz=200, max_backoff_ms=40,
+                       mock={"vanish_dev": 1, "vanish_after_s": 0.3, "vanish_for_s": 0.3, "util_amp": 0.0001,
+                             "util_base": 60, "fw_period_s": 0.01})
+    time.sleep(0.25)
+    e0 = ex.integrals(1)["energy_joules"]
+    busy0 = ex.integrals(1)["gfx_busy_seconds"]
+    time.sleep(0.2)
+    assert ex.integrals(1)["up"] == 0
+    time.sleep(0.8)
+    I = ex.integrals(1)
+    assert I["up"] == 1 and I["recoveries"] == 1 and I["recover_attempts"] >= 1, I
+    assert I["energy_joules"] > e0 and I["gfx_busy_seconds"] > busy0
+    w = ex.window(1, 0.2)
+    assert w["gfx_busy_pct"] == pytest.approx(60, abs=2), w
+    m = parse_text(ex.render())
+    rec = {lb["gpu"]: v for lb, v in m["kgs_device_recoveries_total"]}
+    assert rec == {"0": 0.0, "1": 1.0}
+
+
 def test_process_cu_seconds_integral(mock_exporter):
     ex = mock_exporter(n_gpus=2, hz=100, proc_every=2)
     time.sleep(0.2)

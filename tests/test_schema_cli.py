@@ -15,9 +15,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_rendered_families_match_catalog(mock_exporter):
+    from kube_gpu_stats_amd.attribution.attributor import Attributor
+
     ex = mock_exporter(n_gpus=3, pmc_source="mock", proc_every=1, link_every=1)
     ex.set_device_owners(0, [{"pod": "p", "namespace": "n", "container": "c"}])
     time.sleep(0.4)
+    Attributor(ex, socket_path=None).publish()
     fams = list(text_string_to_metric_families(ex.render()))
     names = {f.name for f in fams}
     # prometheus_client strips _total from counter family names
