@@ -254,6 +254,16 @@ class ExporterProc:
         return {}
 
 
+def proc_cpu_seconds(pid: int) -> float:
+    """utime + stime of a process (all threads), seconds; 0 if unreadable."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, IndexError, ValueError):
+        return 0.0
+
+
 def sample_counts(m: dict) -> tuple[dict, dict]:
     pmfw = {lb["gpu"]: v for lb, v in m.get("kgs_samples_total", [])}
     pmc = {lb["gpu"]: v for lb, v in m.get("kgs_pmc_samples_total", [])}
@@ -341,9 +351,12 @@ def main(argv=None) -> int:
     scraper = None
     before = after = {}
     t_w0 = t_w1 = 0.0
+    exp_pid = int(exp.ready.get("pid", 0) or 0) if exp is not None else 0
+    cpu0 = cpu1 = 0.0
     if exp is not None:
         scraper = Scraper("127.0.0.1", exp.port)
         before = parse_text(scraper.get())
+        cpu0 = proc_cpu_seconds(exp_pid)
         t_w0 = time.perf_counter()
         scraper.start(a.scrape_hz)
     # phase B: exporter on (timed)
@@ -352,6 +365,7 @@ def main(argv=None) -> int:
         scraper.stop()
         after = parse_text(scraper.get())
         t_w1 = time.perf_counter()
+        cpu1 = proc_cpu_seconds(exp_pid)
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
@@ -400,6 +414,7 @@ def main(argv=None) -> int:
             "t_off_a_s": t_a,
             "t_on_s": t_b,
             "t_off_c_s": t_c,
+            "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
             "pmc_source": exp.ready.get("pmc"),
             "pmc_error": exp.ready.get("pmc_error"),
             "load": calib,

@@ -1,0 +1,139 @@
+"""Grafana dashboard for the exporter, generated from code so its PromQL stays in
+step with the metric catalogue (``schema.CATALOG``; ``tests/test_deploy.py``
+checks every series name used here against it).
+
+    python -m kube_gpu_stats_amd.models.dashboard > deploy/grafana-dashboard.json
+
+Rows: fleet (allocation + the reference's per-pod utilisation), per-GPU
+utilisation (PMFW window + per-XCC + matrix-core counters), memory / power /
+thermals, xGMI, per-process, and exporter health.
+"""
+from __future__ import annotations
+
+import json
+
+_NODE = 'kubernetes_io_hostname=~"$node"'
+
+
+def _panel(pid: int, title: str, exprs: list[tuple[str, str]], x: int, y: int, w: int = 12, h: int = 8,
+           unit: str = "short", kind: str = "timeseries", maxv: float | None = None) -> dict:
+    p = {
+        "id": pid, "type": kind, "title": title, "datasource": {"type": "prometheus", "uid": "${datasource}"},
+        "gridPos": {"x": x, "y": y, "w": w, "h": h},
+        "targets": [{"refId": chr(ord("A") + i), "expr": e, "legendFormat": lg} for i, (e, lg) in enumerate(exprs)],
+        "fieldConfig": {"defaults": {"unit": unit}, "overrides": []},
+    }
+    if maxv is not None:
+        p["fieldConfig"]["defaults"]["max"] = maxv
+        p["fieldConfig"]["defaults"]["min"] = 0
+    return p
+
+
+def _row(pid: int, title: str, y: int) -> dict:
+    return {"id": pid, "type": "row", "title": title, "collapsed": False, "gridPos": {"x": 0, "y": y, "w": 24, "h": 1},
+            "panels": []}
+
+
+def _dev(metric: str) -> str:
+    """A per-device family joined to its node through amdgpu_device_info (series carry gpu/uuid only)."""
+    return (f"{metric} * on (instance, gpu) group_left (kubernetes_io_hostname) "
+            f"max by (instance, gpu, kubernetes_io_hostname) (amdgpu_device_info{{{_NODE}}})")
+
+
+def build() -> dict:
+    panels: list[dict] = []
+    pid = 0
+    y = 0
+
+    def add(p):
+        nonlocal pid
+        pid += 1
+        p["id"] = pid
+        panels.append(p)
+
+    add(_row(0, "Fleet", y)); y += 1
+    add(_panel(0, "Per-pod GPU utilisation (reference contract)",
+               [(f"avg(container_gpu_sm_util{{{_NODE}}}) by (kubernetes_io_hostname, pod_name)",
+                 "{{kubernetes_io_hostname}} / {{pod_name}}")], 0, y, unit="percent", maxv=100))
+    add(_panel(0, "Allocated GPUs per node",
+               [(f"count by (kubernetes_io_hostname) (container_gpu_sm_util{{{_NODE},pod_name!=\"\"}})",
+                 "{{kubernetes_io_hostname}}")], 12, y))
+    y += 8
+    add(_row(0, "Utilisation", y)); y += 1
+    add(_panel(0, "GFX busy (exact, from PMFW accumulators)",
+               [(_dev("100 * rate(amdgpu_gfx_busy_seconds_total[1m])"), "{{kubernetes_io_hostname}} gpu{{gpu}}")],
+               0, y, unit="percent", maxv=100))
+    add(_panel(0, "Matrix-core (MFMA) busy",
+               [(_dev("amdgpu_mfma_util_percent"), "{{kubernetes_io_hostname}} gpu{{gpu}}")], 12, y, unit="percent",
+               maxv=100))
+    y += 8
+    add(_panel(0, "Per-XCC busy (die imbalance)",
+               [(_dev("amdgpu_gfx_busy_xcc_percent"), "gpu{{gpu}} xcc{{xcc}}")], 0, y, unit="percent", maxv=100))
+    add(_panel(0, "HBM controller busy / vector-memory busy",
+               [(_dev("amdgpu_umc_busy_percent"), "umc gpu{{gpu}}"),
+                (_dev("amdgpu_vmem_busy_percent"), "vmem gpu{{gpu}}")], 12, y, unit="percent", maxv=100))
+    y += 8
+    add(_row(0, "Memory, power, thermals", y)); y += 1
+    add(_panel(0, "HBM3E used", [(_dev("amdgpu_hbm_used_bytes"), "gpu{{gpu}}")], 0, y, w=8, unit="bytes"))
+    add(_panel(0, "Power", [(_dev("amdgpu_power_watts"), "gpu{{gpu}}")], 8, y, w=8, unit="watt"))
+    add(_panel(0, "Hotspot / HBM temperature",
+               [(_dev('amdgpu_temperature_celsius{sensor=~"hotspot|hbm"}'), "gpu{{gpu}} {{sensor}}")], 16, y, w=8,
+               unit="celsius"))
+    y += 8
+    add(_panel(0, "Energy per hour", [(_dev("3600 * rate(amdgpu_energy_joules_total[5m])"), "gpu{{gpu}}")], 0, y,
+               w=12, unit="joule"))
+    add(_panel(0, "Effective shader clock", [(_dev("amdgpu_gpu_clock_effective_mhz"), "gpu{{gpu}}")], 12, y, w=12,
+               unit="MHz"))
+    y += 8
+    add(_row(0, "xGMI", y)); y += 1
+    add(_panel(0, "xGMI traffic per GPU (read + write, all links)",
+               [(_dev("sum by (instance, gpu) (rate(amdgpu_xgmi_read_bytes_total[1m]) + "
+                      "rate(amdgpu_xgmi_write_bytes_total[1m]))"), "gpu{{gpu}}")], 0, y, unit="Bps"))
+    add(_panel(0, "xGMI errors", [(_dev("amdgpu_xgmi_error_status"), "gpu{{gpu}}")], 12, y))
+    y += 8
+    add(_row(0, "Processes", y)); y += 1
+    add(_panel(0, "HBM per process", [("amdgpu_process_hbm_bytes", "{{pod}} pid {{pid}} gpu{{gpu}}")], 0, y,
+               unit="bytes"))
+    add(_panel(0, "Compute share per process (occupied-CU fraction)",
+               [("rate(amdgpu_process_cu_seconds_total[1m])", "{{pod}} pid {{pid}} gpu{{gpu}}")], 12, y,
+               unit="percentunit", maxv=1))
+    y += 8
+    add(_row(0, "Exporter health", y)); y += 1
+    add(_panel(0, "Samples / s per GPU (PMFW distinct, counters)",
+               [(_dev("rate(kgs_samples_total[1m])"), "pmfw gpu{{gpu}}"),
+                (_dev("rate(kgs_pmc_samples_total[1m])"), "pmc gpu{{gpu}}")], 0, y, w=8))
+    add(_panel(0, "Scrape render time", [("kgs_scrape_render_last_seconds", "{{instance}}")], 8, y, w=8, unit="s"))
+    add(_panel(0, "Sampler up / recoveries / attribution age",
+               [(_dev("kgs_up"), "up gpu{{gpu}}"), (_dev("increase(kgs_device_recoveries_total[1h])"),
+                                                   "recoveries gpu{{gpu}}"),
+                ("kgs_attribution_kubelet_age_seconds", "kubelet age {{instance}}")], 16, y, w=8))
+
+    return {
+        "title": "MI355X GPU stats (kube_gpu_stats_amd)",
+        "uid": "kgs-mi355x",
+        "schemaVersion": 39,
+        "version": 1,
+        "time": {"from": "now-6h", "to": "now"},
+        "refresh": "30s",
+        "tags": ["amd", "mi355x", "gpu"],
+        "templating": {"list": [
+            {"name": "datasource", "type": "datasource", "query": "prometheus"},
+            {"name": "node", "type": "query", "datasource": {"type": "prometheus", "uid": "${datasource}"},
+             "query": "label_values(amdgpu_device_info, kubernetes_io_hostname)", "includeAll": True,
+             "multi": True, "current": {"text": "All", "value": "$__all"}},
+        ]},
+        "panels": panels,
+    }
+
+
+def exprs(d: dict | None = None) -> list[str]:
+    d = d or build()
+    return [t["expr"] for p in d["panels"] for t in p.get("targets", [])]
+
+
+def render() -> str:
+    return json.dumps(build(), indent=1, sort_keys=True) + "\n"
+
+
+if __name__ == "__main__":
+    print(render(), end="")

@@ -28,6 +28,23 @@ def test_daemonset_args_are_valid_exporter_flags():
     assert c["readinessProbe"]["httpGet"]["path"] == "/healthz"
 
 
+PROMQL_WORDS = {"avg", "sum", "max", "min", "count", "rate", "increase", "avg_over_time", "label_values", "by", "or",
+                "and", "on", "without", "group_left", "group_right"}
+LABELS = {"kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "gpu", "instance", "sensor", "pod",
+          "pid", "xcc"}
+
+
+def unknown_series(exprs: str) -> set:
+    """Series names used in PromQL that the exporter does not emit (catalogue check)."""
+    import re
+
+    from kube_gpu_stats_amd.models.schema import BY_NAME
+
+    bare = re.sub(r"\{[^}]*\}|\[[^]]*\]|\"[^\"]*\"", "", exprs)
+    names = {n for n in re.findall(r"[a-zA-Z_:][a-zA-Z0-9_:]*", bare) if ":" not in n}
+    return {n for n in names - PROMQL_WORDS - LABELS if n not in BY_NAME}
+
+
 def test_monitoring_rules_reference_exported_families():
     from kube_gpu_stats_amd.models.schema import BY_NAME
 
@@ -37,9 +54,21 @@ def test_monitoring_rules_reference_exported_families():
     for fam in ("container_gpu_sm_util", "amdgpu_gfx_busy_seconds_total", "amdgpu_hbm_used_bytes", "kgs_up",
                 "amdgpu_xgmi_read_bytes_total"):
         assert fam in exprs and fam in BY_NAME
+    assert not unknown_series(exprs)
 
 
 def test_report_cronjob_has_rbac():
     docs = load("reports-cronjob.yaml")
     kinds = {d["kind"] for d in docs}
     assert {"ServiceAccount", "ClusterRole", "ClusterRoleBinding", "CronJob"} <= kinds
+
+
+def test_grafana_dashboard_is_current_and_uses_exported_families():
+    from kube_gpu_stats_amd.models import dashboard
+
+    with open(os.path.join(DEPLOY, "grafana-dashboard.json")) as f:
+        assert f.read() == dashboard.render(), "regenerate: python -m kube_gpu_stats_amd.models.dashboard"
+    ex = dashboard.exprs()
+    assert len(ex) >= 15
+    assert not unknown_series(" ".join(ex))
+    assert any("container_gpu_sm_util" in e for e in ex)
