@@ -264,6 +264,26 @@ def proc_cpu_seconds(pid: int) -> float:
         return 0.0
 
 
+def thread_cpu_seconds(pid: int) -> dict:
+    """Per-thread utime + stime, keyed ``<comm>/<tid>`` (finds spinning helper threads)."""
+    out = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                raw = f.read()
+            comm = raw[raw.index("(") + 1:raw.rindex(")")]
+            fields = raw.rsplit(")", 1)[1].split()
+            out[f"{comm}/{tid}"] = (int(fields[11]) + int(fields[12])) / tck
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
 def sample_counts(m: dict) -> tuple[dict, dict]:
     pmfw = {lb["gpu"]: v for lb, v in m.get("kgs_samples_total", [])}
     pmc = {lb["gpu"]: v for lb, v in m.get("kgs_pmc_samples_total", [])}
@@ -353,10 +373,13 @@ def main(argv=None) -> int:
     t_w0 = t_w1 = 0.0
     exp_pid = int(exp.ready.get("pid", 0) or 0) if exp is not None else 0
     cpu0 = cpu1 = 0.0
+    thr0: dict = {}
+    thr1: dict = {}
     if exp is not None:
         scraper = Scraper("127.0.0.1", exp.port)
         before = parse_text(scraper.get())
         cpu0 = proc_cpu_seconds(exp_pid)
+        thr0 = thread_cpu_seconds(exp_pid)
         t_w0 = time.perf_counter()
         scraper.start(a.scrape_hz)
     # phase B: exporter on (timed)
@@ -366,6 +389,7 @@ def main(argv=None) -> int:
         after = parse_text(scraper.get())
         t_w1 = time.perf_counter()
         cpu1 = proc_cpu_seconds(exp_pid)
+        thr1 = thread_cpu_seconds(exp_pid)
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
@@ -415,6 +439,8 @@ def main(argv=None) -> int:
             "t_on_s": t_b,
             "t_off_c_s": t_c,
             "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
+            "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / win, 4) for k, v in thr1.items()
+                                             if win > 0 and v - thr0.get(k, 0.0) > 0.005 * win},
             "pmc_source": exp.ready.get("pmc"),
             "pmc_error": exp.ready.get("pmc_error"),
             "load": calib,
