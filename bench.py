@@ -41,6 +41,7 @@ from kube_gpu_stats_amd.parallel import dist as D  # noqa: E402
 from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text  # noqa: E402
 
 METRIC = "counter samples/sec/GPU + p50 scrape latency at 8×MI355X; GPU-time overhead %"
+AUTO_PMC = "rocprofiler"
 
 
 def parse_args(argv=None):
@@ -50,7 +51,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--hz", type=float, default=1000.0,
                     help="sampler tick rate per GPU: one hardware-counter drain per tick (PMFW table ≤100 Hz)")
-    ap.add_argument("--pmc", default="auto", choices=["auto", "rocprofiler", "none"])
+    ap.add_argument("--pmc", default="auto", choices=["auto", "aqlprofile", "rocprofiler", "none"],
+                    help="counter reader (auto = %s)" % AUTO_PMC)
     ap.add_argument("--scrape-hz", type=float, default=10.0)
     ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per step on MI355X")
     ap.add_argument("--mfma-blocks", type=int, default=2048)
@@ -196,10 +198,12 @@ class ExporterProc:
         if a.mock:
             cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock"]
         else:
-            cmd += ["--pmc", "rocprofiler" if a.pmc in ("auto", "rocprofiler") else "none"]
+            pmc = AUTO_PMC if a.pmc == "auto" else a.pmc
+            cmd += ["--pmc", pmc]
         env = dict(os.environ)
         env.setdefault("KGS_NO_BUILD", "1")
-        if not a.mock and env.get("ROCP_TOOL_LIBRARIES"):
+        if not a.mock and "--pmc" in cmd and cmd[cmd.index("--pmc") + 1] == "rocprofiler" \
+                and env.get("ROCP_TOOL_LIBRARIES"):
             # Running under rocprofv3: rocprofiler configuration closes before the
             # exporter could force-register, so join as a listed tool library.
             from kube_gpu_stats_amd.native import pmc_lib_path
@@ -331,6 +335,7 @@ def main(argv=None) -> int:
         B.build_native()
         if not a.mock:
             B.build_pmc()
+            B.build_pmc_aql()
     load = MockLoad(a, ctx.local_rank) if a.mock else GpuLoad(a, ctx.local_rank, ctx)
 
     for _ in range(a.warmup):

@@ -36,8 +36,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pmfw-hz", 100.0, "cap on PMFW metrics-table reads/s (firmware refreshes it every ~20 ms)")
     add_flag(ap, "proc-every", 10, "per-process tier every N fast ticks (0 = off)")
     add_flag(ap, "link-every", 100, "xGMI link tier every N fast ticks (0 = off)")
-    add_flag(ap, "pmc", "none", "hardware counters: none | rocprofiler | mock")
-    add_flag(ap, "pmc-lib", "", "path of libkgs_pmc.so (default: in-tree build)")
+    add_flag(ap, "pmc", "none", "hardware counters: none | aqlprofile (direct CP reads) | rocprofiler "
+                                "(rocprofiler-sdk device counting) | mock")
+    add_flag(ap, "pmc-lib", "", "counter reader library (default: the in-tree one for --pmc)")
     add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
     add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
     add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
@@ -65,7 +66,7 @@ def config_from_args(a) -> dict:
         "link_every": a.link_every,
         "pin_numa": a.pin_numa,
         "pmc_source": a.pmc,
-        "pmc_lib": a.pmc_lib or pmc_lib_path(),
+        "pmc_lib": a.pmc_lib or pmc_lib_path(a.pmc),
         "listen_addr": host or "0.0.0.0",
         "port": int(port),
         "node_name": a.node_name,

@@ -29,7 +29,8 @@ def load(rebuild: bool = True):
     return _mod
 
 
-def pmc_lib_path() -> str:
+def pmc_lib_path(source: str = "rocprofiler") -> str:
+    """In-tree counter reader for a --pmc source: aqlprofile (direct) or rocprofiler."""
     from . import build
 
-    return build.pmc_lib_path()
+    return build.pmc_aql_lib_path() if source == "aqlprofile" else build.pmc_lib_path()

@@ -45,6 +45,10 @@ def pmc_lib_path() -> str:
     return os.path.join(LIB, "libkgs_pmc.so")
 
 
+def pmc_aql_lib_path() -> str:
+    return os.path.join(LIB, "libkgs_pmc_aql.so")
+
+
 def load_lib_path() -> str:
     return os.path.join(LIB, "libkgs_load.so")
 
@@ -109,6 +113,21 @@ def build_pmc(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_pmc_aql(force: bool = False, verbose: bool = False) -> str:
+    """Direct CP counter reader over aqlprofile (no profiler framework, no spinning helper thread)."""
+    out = pmc_aql_lib_path()
+    src = os.path.join(HERE, "counters", "pmc_aqlprofile.cpp")
+    if not force and not _stale(out, [src, __file__]):
+        return out
+    os.makedirs(LIB, exist_ok=True)
+    tmp = f"{out}.{os.getpid()}.tmp"
+    _run(["g++", *CXXFLAGS, "-fvisibility=default", "-D__HIP_PLATFORM_AMD__=1", "-I" + os.path.join(ROCM, "include"),
+          "-shared", src, "-o", tmp, "-L" + os.path.join(ROCM, "lib"), "-lhsa-runtime64", "-lhsa-amd-aqlprofile64",
+          "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
+    os.replace(tmp, out)
+    return out
+
+
 def build_load(force: bool = False, verbose: bool = False) -> str:
     out = load_lib_path()
     src = os.path.join(PKG, "ops", "hip", "load_kernels.hip")
@@ -140,7 +159,8 @@ def build_all(force: bool = False, verbose: bool = False, hip: bool = True) -> d
     res = {"native": build_native(force, verbose)}
     try:
         res["pmc"] = build_pmc(force, verbose)
-    except RuntimeError as e:  # rocprofiler-sdk headers missing on a host-only image
+        res["pmc_aql"] = build_pmc_aql(force, verbose)
+    except RuntimeError as e:  # ROCm profiling headers missing on a host-only image
         res["pmc_error"] = str(e)
     if hip:
         res["load"] = build_load(force, verbose)

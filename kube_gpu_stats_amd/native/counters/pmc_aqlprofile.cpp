@@ -1,0 +1,418 @@
+// libkgs_pmc_aql.so — device-wide hardware counters straight from the CP, with
+// no profiler framework in between.
+//
+// Same C ABI as pmc_rocprofiler.cpp (kgs_pmc_init/open/sample/info/mode/close),
+// so the exporter's dlopen bridge (src/pmc.cpp) loads either.  Why a second
+// reader: once rocprofiler-sdk's device-counting context is started, HSA's
+// async-events thread re-arms a KFD event wait in a tight loop and burns one
+// full CPU core per exporter, whatever the sample rate (measured: profiles/r1/
+// pmc_helper_thread.md).  This reader registers no async handler at all:
+//
+//   * one private AQL queue per GPU (HSA_QUEUE_TYPE_SINGLE, no error callback);
+//   * aqlprofile (hsa_ven_amd_aqlprofile.h, the v1 packet builder that ships
+//     with ROCm) fills vendor-specific PM4-IB AQL packets: START once (programs
+//     and enables the counters), then READ per sample (copies the running
+//     counters into a fine-grained host buffer);
+//   * each READ carries an interrupt-capable completion signal and the sampler
+//     thread waits on it in HSA_WAIT_STATE_BLOCKED, so the CPU sleeps while the
+//     CP works;
+//   * results are folded per counter over every block instance / XCC sample
+//     (max for GRBM clocks, sum for SQ busy cycles, mean for TA busy), the same
+//     reductions as the rocprofiler path, and reported cumulative since START.
+//
+// Counter selects for gfx950 (block, event) come from ROCm's own definitions
+// (/opt/rocm/share/rocprofiler-sdk/counter_defs.yaml); any other counter can be
+// asked for as "BLOCK:event" (e.g. "SQ:4" for SQ_WAVES).
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <hsa/hsa_ven_amd_aqlprofile.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int kMaxCounters = 16;
+
+struct Sel {
+  const char* name;
+  hsa_ven_amd_aqlprofile_block_name_t block;
+  const char* block_name;  // aqlprofile block-id query name
+  uint32_t event;
+};
+
+// gfx950 selects (counter_defs.yaml, architectures: gfx950).
+const Sel kGfx950[] = {
+    {"GRBM_COUNT", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, "GRBM", 0},
+    {"GRBM_GUI_ACTIVE", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, "GRBM", 2},
+    {"SQ_BUSY_CYCLES", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, "SQ", 3},
+    {"SQ_WAVES", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, "SQ", 4},
+    {"SQ_VALU_MFMA_BUSY_CYCLES", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, "SQ", 93},
+    {"TA_TA_BUSY", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TA, "TA", 13},
+    {"TCC_HIT", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, "TCC", 21},
+    {"TCC_EA0_RDREQ", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, "TCC", 42},
+};
+
+struct BlockNameId {
+  const char* name;
+  hsa_ven_amd_aqlprofile_block_name_t id;
+};
+const BlockNameId kBlocks[] = {
+    {"GRBM", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM}, {"SQ", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ},
+    {"TA", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TA},     {"TD", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TD},
+    {"TCC", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC},   {"TCP", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCP},
+    {"SPI", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI},   {"CPC", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPC},
+    {"CPF", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPF},   {"GRBMSE", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBMSE},
+};
+
+struct Agent {
+  hsa_agent_t agent{};
+  uint32_t gpu_id = 0;  // KFD gpu_id (== HSA_AMD_AGENT_INFO_DRIVER_UID)
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t sig{};
+  std::vector<std::string> names;
+  std::vector<int> reduce;                           // 0 sum, 1 max, 2 mean
+  std::vector<hsa_ven_amd_aqlprofile_event_t> events;
+  std::vector<int> ev_counter;                       // event index -> counter index
+  hsa_ven_amd_aqlprofile_profile_t prof{};
+  void* cmd = nullptr;
+  void* out = nullptr;
+  hsa_ext_amd_aql_pm4_packet_t start_pkt{}, read_pkt{}, stop_pkt{};
+  bool started = false;
+  std::string err;
+  uint64_t reads = 0, timeouts = 0;
+  uint32_t last_results = 0;
+  std::vector<uint32_t> instances;                   // results folded per counter (last read)
+  std::vector<double> vals;
+};
+
+std::mutex g_mu;
+std::vector<Agent*> g_agents;
+hsa_amd_memory_pool_t g_host_pool{};
+bool g_have_pool = false;
+std::string g_init_err;
+
+void set_err(char* err, int len, const std::string& s) {
+  if (err && len > 0) std::snprintf(err, static_cast<size_t>(len), "%s", s.c_str());
+}
+
+std::string aql_error() {
+  const char* s = nullptr;
+  if (hsa_ven_amd_aqlprofile_error_string(&s) == HSA_STATUS_SUCCESS && s) return s;
+  return "unknown";
+}
+
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+hsa_status_t find_host_pool(hsa_amd_memory_pool_t pool, void*) {
+  hsa_amd_segment_t seg;
+  if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT) || !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED))
+    return HSA_STATUS_SUCCESS;
+  g_host_pool = pool;
+  g_have_pool = true;
+  return HSA_STATUS_INFO_BREAK;
+}
+
+hsa_status_t on_agent(hsa_agent_t agent, void*) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(agent, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_CPU && !g_have_pool) {
+    hsa_amd_agent_iterate_memory_pools(agent, find_host_pool, nullptr);
+  } else if (t == HSA_DEVICE_TYPE_GPU) {
+    Agent* a = new Agent();
+    a->agent = agent;
+    hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DRIVER_UID), &a->gpu_id);
+    g_agents.push_back(a);
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+bool resolve(const std::string& name, hsa_ven_amd_aqlprofile_block_name_t& block, std::string& block_name,
+             uint32_t& event) {
+  for (const Sel& s : kGfx950)
+    if (name == s.name) {
+      block = s.block;
+      block_name = s.block_name;
+      event = s.event;
+      return true;
+    }
+  const size_t c = name.find(':');
+  if (c == std::string::npos) return false;
+  block_name = name.substr(0, c);
+  for (const BlockNameId& b : kBlocks)
+    if (block_name == b.name) {
+      block = b.id;
+      event = static_cast<uint32_t>(std::strtoul(name.c_str() + c + 1, nullptr, 10));
+      return true;
+    }
+  return false;
+}
+
+void* host_alloc(Agent* a, size_t bytes) {
+  void* p = nullptr;
+  if (hsa_amd_memory_pool_allocate(g_host_pool, bytes, 0, &p) != HSA_STATUS_SUCCESS) return nullptr;
+  if (hsa_amd_agents_allow_access(1, &a->agent, nullptr, p) != HSA_STATUS_SUCCESS) {
+    hsa_amd_memory_pool_free(p);
+    return nullptr;
+  }
+  std::memset(p, 0, bytes);
+  return p;
+}
+
+// Put one PM4-IB vendor packet on the agent's private queue and wait for it.
+int submit(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, uint64_t timeout_ns) {
+  hsa_queue_t* q = a->queue;
+  hsa_signal_store_relaxed(a->sig, 1);
+  const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
+  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+  }
+  auto* slot = reinterpret_cast<hsa_ext_amd_aql_pm4_packet_t*>(q->base_address) + (idx & (q->size - 1));
+  std::memcpy(slot->pm4_command, tmpl.pm4_command, sizeof slot->pm4_command);
+  slot->completion_signal = a->sig;
+  const uint16_t header = static_cast<uint16_t>(
+      (HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(q->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+  const int64_t end = mono_ns() + static_cast<int64_t>(timeout_ns);
+  // BLOCKED: ROCr spins briefly, then sleeps on the signal's KFD event.
+  while (hsa_signal_wait_scacquire(a->sig, HSA_SIGNAL_CONDITION_LT, 1, timeout_ns, HSA_WAIT_STATE_BLOCKED) != 0) {
+    if (mono_ns() > end) {
+      ++a->timeouts;
+      return -1;
+    }
+  }
+  return 0;
+}
+
+struct Fold {
+  Agent* a;
+  uint32_t n = 0;
+};
+
+hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlprofile_info_data_t* d, void* ud) {
+  if (type != HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA) return HSA_STATUS_SUCCESS;
+  Fold* f = static_cast<Fold*>(ud);
+  Agent* a = f->a;
+  ++f->n;
+  for (size_t e = 0; e < a->events.size(); ++e) {
+    const auto& ev = a->events[e];
+    if (ev.block_name != d->pmc_data.event.block_name || ev.block_index != d->pmc_data.event.block_index ||
+        ev.counter_id != d->pmc_data.event.counter_id)
+      continue;
+    const int k = a->ev_counter[e];
+    const double v = static_cast<double>(d->pmc_data.result);
+    if (a->reduce[static_cast<size_t>(k)] == 1) a->vals[static_cast<size_t>(k)] = std::max(a->vals[static_cast<size_t>(k)], v);
+    else a->vals[static_cast<size_t>(k)] += v;
+    a->instances[static_cast<size_t>(k)]++;
+    break;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+int read_values(Agent* a) {
+  std::memset(a->out, 0, a->prof.output_buffer.size);
+  if (submit(a, a->read_pkt, 1000000000ull) != 0) return -2;
+  ++a->reads;
+  a->vals.assign(a->names.size(), 0.0);
+  a->instances.assign(a->names.size(), 0);
+  Fold f{a};
+  if (hsa_ven_amd_aqlprofile_iterate_data(&a->prof, on_data, &f) != HSA_STATUS_SUCCESS) return -3;
+  a->last_results = f.n;
+  for (size_t k = 0; k < a->vals.size(); ++k)
+    if (a->reduce[k] == 2 && a->instances[k] > 0) a->vals[k] /= a->instances[k];
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kgs_pmc_init(char* err, int errlen) {
+  static std::once_flag once;
+  static int rc = 0;
+  std::call_once(once, [&] {
+    if (hsa_init() != HSA_STATUS_SUCCESS) {
+      g_init_err = "hsa_init failed";
+      rc = -2;
+      return;
+    }
+    hsa_iterate_agents(on_agent, nullptr);
+    if (!g_have_pool) {
+      g_init_err = "no fine-grained host memory pool";
+      rc = -3;
+      return;
+    }
+    if (g_agents.empty()) {
+      g_init_err = "no GPU agents";
+      rc = -4;
+    }
+  });
+  if (rc != 0) set_err(err, errlen, g_init_err);
+  return rc;
+}
+
+int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_max, int n, char* err, int errlen) {
+  if (n <= 0 || n > kMaxCounters) {
+    set_err(err, errlen, "bad counter count");
+    return -1;
+  }
+  std::lock_guard<std::mutex> g(g_mu);
+  for (size_t h = 0; h < g_agents.size(); ++h) {
+    Agent* a = g_agents[h];
+    if (a->gpu_id != kfd_gpu_id) continue;
+    if (a->started) {
+      set_err(err, errlen, "agent already open");
+      return -1;
+    }
+    a->names.assign(names, names + n);
+    a->reduce.assign(is_max, is_max + n);
+    a->events.clear();
+    a->ev_counter.clear();
+    std::string missing;
+    for (int k = 0; k < n; ++k) {
+      hsa_ven_amd_aqlprofile_block_name_t block;
+      std::string bname;
+      uint32_t event;
+      if (!resolve(a->names[static_cast<size_t>(k)], block, bname, event)) {
+        missing += (missing.empty() ? "" : ",") + a->names[static_cast<size_t>(k)];
+        continue;
+      }
+      // one event per block instance (TA per CU, SQ per SE, GRBM per XCC ...)
+      hsa_ven_amd_aqlprofile_profile_t q{};
+      q.agent = a->agent;
+      hsa_ven_amd_aqlprofile_id_query_t id{bname.c_str(), 0, 0};
+      uint32_t inst = 1;
+      if (hsa_ven_amd_aqlprofile_get_info(&q, HSA_VEN_AMD_AQLPROFILE_INFO_BLOCK_ID, &id) == HSA_STATUS_SUCCESS &&
+          id.instance_count > 0)
+        inst = id.instance_count;
+      for (uint32_t i = 0; i < inst; ++i) {
+        hsa_ven_amd_aqlprofile_event_t ev{block, i, event};
+        bool ok = false;
+        if (hsa_ven_amd_aqlprofile_validate_event(a->agent, &ev, &ok) != HSA_STATUS_SUCCESS || !ok) continue;
+        a->events.push_back(ev);
+        a->ev_counter.push_back(k);
+      }
+    }
+    if (a->events.empty()) {
+      set_err(err, errlen, "no valid counter events (unresolved: " + missing + ")");
+      return -1;
+    }
+    if (!a->queue) {
+      if (hsa_queue_create(a->agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX,
+                           &a->queue) != HSA_STATUS_SUCCESS) {
+        set_err(err, errlen, "hsa_queue_create failed");
+        return -1;
+      }
+      if (hsa_signal_create(1, 0, nullptr, &a->sig) != HSA_STATUS_SUCCESS) {
+        set_err(err, errlen, "hsa_signal_create failed");
+        return -1;
+      }
+    }
+    hsa_ven_amd_aqlprofile_profile_t& p = a->prof;
+    p = hsa_ven_amd_aqlprofile_profile_t{};
+    p.agent = a->agent;
+    p.type = HSA_VEN_AMD_AQLPROFILE_EVENT_TYPE_PMC;
+    p.events = a->events.data();
+    p.event_count = static_cast<uint32_t>(a->events.size());
+    uint32_t cmd_sz = 0, out_sz = 0;
+    if (hsa_ven_amd_aqlprofile_get_info(&p, HSA_VEN_AMD_AQLPROFILE_INFO_COMMAND_BUFFER_SIZE, &cmd_sz) !=
+            HSA_STATUS_SUCCESS ||
+        hsa_ven_amd_aqlprofile_get_info(&p, HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA_SIZE, &out_sz) != HSA_STATUS_SUCCESS) {
+      set_err(err, errlen, "aqlprofile get_info: " + aql_error());
+      return -1;
+    }
+    a->cmd = host_alloc(a, cmd_sz);
+    a->out = host_alloc(a, out_sz);
+    if (!a->cmd || !a->out) {
+      set_err(err, errlen, "host buffer allocation failed");
+      return -1;
+    }
+    p.command_buffer = {a->cmd, cmd_sz};
+    p.output_buffer = {a->out, out_sz};
+    if (hsa_ven_amd_aqlprofile_start(&p, &a->start_pkt) != HSA_STATUS_SUCCESS ||
+        hsa_ven_amd_aqlprofile_read(&p, &a->read_pkt) != HSA_STATUS_SUCCESS ||
+        hsa_ven_amd_aqlprofile_stop(&p, &a->stop_pkt) != HSA_STATUS_SUCCESS) {
+      set_err(err, errlen, "aqlprofile packet build: " + aql_error());
+      return -1;
+    }
+    if (std::getenv("KGS_AQL_DRY")) {  // packets built, nothing submitted (bring-up)
+      char b[160];
+      std::snprintf(b, sizeof b, "dry: events=%zu cmd=%u out=%u", a->events.size(), cmd_sz, out_sz);
+      set_err(err, errlen, b);
+      return -1;
+    }
+    if (submit(a, a->start_pkt, 1000000000ull) != 0) {
+      set_err(err, errlen, "START packet did not complete within 1 s");
+      return -1;
+    }
+    a->started = true;
+    if (read_values(a) != 0) {
+      set_err(err, errlen, "initial READ failed");
+      submit(a, a->stop_pkt, 1000000000ull);
+      a->started = false;
+      return -1;
+    }
+    if (!missing.empty()) a->err = "unresolved: " + missing;
+    return static_cast<int>(h);
+  }
+  set_err(err, errlen, "no HSA GPU agent with kfd gpu_id " + std::to_string(kfd_gpu_id));
+  return -1;
+}
+
+int kgs_pmc_sample(int handle, uint64_t* out, int n, uint32_t* read_ns) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  if (!a->started) return -1;
+  const int64_t t0 = mono_ns();
+  const int rc = read_values(a);
+  if (read_ns) *read_ns = static_cast<uint32_t>(mono_ns() - t0);
+  if (rc != 0) return rc;
+  for (int k = 0; k < n && static_cast<size_t>(k) < a->vals.size(); ++k) out[k] = static_cast<uint64_t>(a->vals[static_cast<size_t>(k)]);
+  return 0;
+}
+
+int kgs_pmc_info(int handle, char* buf, int len) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  std::string o = "impl=aqlprofile;mode=cumulative;events=" + std::to_string(a->events.size()) +
+                  ";results=" + std::to_string(a->last_results) + ";timeouts=" + std::to_string(a->timeouts);
+  for (size_t k = 0; k < a->names.size(); ++k)
+    o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
+  if (!a->err.empty()) o += ";" + a->err;
+  set_err(buf, len, o);
+  return 0;
+}
+
+int kgs_pmc_mode(int handle) { return handle >= 0 && static_cast<size_t>(handle) < g_agents.size() ? 1 : -1; }
+
+void kgs_pmc_close(int handle) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return;
+  std::lock_guard<std::mutex> g(g_mu);
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  if (a->started) {
+    submit(a, a->stop_pkt, 1000000000ull);
+    a->started = false;
+  }
+}
+
+}  // extern "C"

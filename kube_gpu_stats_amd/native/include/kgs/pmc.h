@@ -70,9 +70,12 @@ struct MockPmcConfig {
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,
                                                         const MockPmcConfig& cfg);
-// dlopen `lib_path` (libkgs_pmc.so) and open one device-counting context per
-// device.  nullptr + err on failure (no permission, no HSA, ...).
-std::unique_ptr<CounterSource> make_rocprofiler_counter_source(const std::string& lib_path, const Backend& be,
-                                                               const std::vector<int>& devices, std::string& err);
+// dlopen `lib_path` — libkgs_pmc_aql.so (direct aqlprofile reader, "aqlprofile")
+// or libkgs_pmc.so (rocprofiler-sdk device counting, "rocprofiler"); both export
+// the kgs_pmc_* C ABI — and open one counting session per device.  nullptr +
+// err on failure (no permission, no HSA, ...).
+std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
+                                                      const Backend& be, const std::vector<int>& devices,
+                                                      std::string& err);
 
 }  // namespace kgs

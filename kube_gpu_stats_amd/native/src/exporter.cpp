@@ -73,8 +73,8 @@ bool Exporter::init() {
     for (int d = 0; d < be_->device_count(); ++d) devs.push_back(d);
   if (cfg_.pmc_source == "mock") {
     pmc_ = make_mock_counter_source(*be_, cfg_.mock, cfg_.mock_pmc);
-  } else if (cfg_.pmc_source == "rocprofiler") {
-    pmc_ = make_rocprofiler_counter_source(cfg_.pmc_lib, *be_, devs, pmc_err_);
+  } else if (cfg_.pmc_source == "rocprofiler" || cfg_.pmc_source == "aqlprofile") {
+    pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, pmc_err_);
   } else if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
     err_ = "unknown pmc_source '" + cfg_.pmc_source + "'";
     return false;

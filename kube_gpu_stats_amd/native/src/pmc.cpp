@@ -83,6 +83,7 @@ using info_fn = int (*)(int, char*, int);
 
 class DlCounterSource final : public CounterSource {
  public:
+  explicit DlCounterSource(std::string name) : name_(std::move(name)) {}
   ~DlCounterSource() override {
     if (close_)
       for (int h : handles_)
@@ -102,7 +103,7 @@ class DlCounterSource final : public CounterSource {
     close_ = reinterpret_cast<close_fn>(dlsym(lib_, "kgs_pmc_close"));
     info_ = reinterpret_cast<info_fn>(dlsym(lib_, "kgs_pmc_info"));
     if (!init || !open_ || !sample_ || !close_) {
-      err = "libkgs_pmc.so: missing symbols";
+      err = path + ": missing kgs_pmc_* symbols";
       return false;
     }
     char ebuf[512] = {};
@@ -128,7 +129,7 @@ class DlCounterSource final : public CounterSource {
     return opened > 0;
   }
 
-  std::string name() const override { return "rocprofiler"; }
+  std::string name() const override { return name_; }
 
   std::string info(int dev) const override {
     if (!info_ || dev < 0 || dev >= static_cast<int>(handles_.size()) || handles_[dev] < 0) return "closed";
@@ -155,6 +156,7 @@ class DlCounterSource final : public CounterSource {
   close_fn close_ = nullptr;
   info_fn info_ = nullptr;
   std::vector<int> handles_;
+  std::string name_;
 };
 
 }  // namespace
@@ -164,9 +166,10 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend&, const Mo
   return std::make_unique<MockCounterSource>(bcfg, cfg);
 }
 
-std::unique_ptr<CounterSource> make_rocprofiler_counter_source(const std::string& lib_path, const Backend& be,
-                                                               const std::vector<int>& devices, std::string& err) {
-  auto s = std::make_unique<DlCounterSource>();
+std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
+                                                      const Backend& be, const std::vector<int>& devices,
+                                                      std::string& err) {
+  auto s = std::make_unique<DlCounterSource>(name);
   if (!s->load(lib_path, be, devices, err)) return nullptr;
   return s;
 }

@@ -61,3 +61,29 @@ def test_sanitized_seqlock_ring_sampler(sanitizer, marker):
     assert r.returncode == 0, out
     assert marker not in out and "AddressSanitizer" not in out, out
     assert "ALL OK" in out
+
+
+@pytest.mark.slow
+def test_cmake_build_matches_python_build(tmp_path):
+    """The CMake route (image builds) produces a working module from the same sources."""
+    import shutil
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = tmp_path / "kube_gpu_stats_amd"
+    shutil.copytree(os.path.join(repo, "kube_gpu_stats_amd"), pkg,
+                    ignore=shutil.ignore_patterns("*.so", "build", "__pycache__"))
+    bdir = tmp_path / "build"
+    subprocess.run(["cmake", "-S", str(pkg / "native"), "-B", str(bdir), "-G", "Ninja", "-DKGS_BUILD_LOAD=OFF"],
+                   check=True, capture_output=True, timeout=300)
+    subprocess.run(["cmake", "--build", str(bdir), "-j", "8"], check=True, capture_output=True, timeout=900)
+    assert (pkg / "lib" / "libkgs_pmc.so").exists()
+    code = ("import time, kube_gpu_stats_amd.native as n; N = n.load(rebuild=False); "
+            "e = N.Exporter({'backend': 'mock', 'mock': {'n_gpus': 2}, 'port': -1, 'hz': 100, 'pin_numa': False}); "
+            "e.start(); time.sleep(0.2); assert 'kgs_up' in e.render(); "
+            "print(N.__file__); e.stop()")
+    r = subprocess.run([sys.executable, "-c", code], cwd=tmp_path, capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "KGS_NO_BUILD": "1", "PYTHONPATH": str(tmp_path)})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().startswith(str(pkg))

@@ -7,8 +7,13 @@
 //   pmc_threads <libkgs_pmc.so> <kfd_gpu_id>
 #include <dirent.h>
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <sched.h>
+#include <signal.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -97,7 +102,32 @@ static void report(const char* phase, const std::map<int, T>& before, double sec
   std::fflush(stdout);
 }
 
+// SIGUSR2: dump the receiving thread's user-space stack (diagnostic only).
+static void on_usr2(int) {
+  void* fr[32];
+  const int n = backtrace(fr, 32);
+  const char hdr[] = "--- backtrace\n";
+  if (write(2, hdr, sizeof hdr - 1) < 0) {
+  }
+  backtrace_symbols_fd(fr, n, 2);
+}
+
+static int hottest(const std::map<int, T>& a, const std::map<int, T>& b) {
+  int best = -1;
+  double bu = 0.2;
+  for (auto& kv : b) {
+    auto it = a.find(kv.first);
+    const double u = kv.second.cpu - (it == a.end() ? 0.0 : it->second.cpu);
+    if (u > bu && kv.first != static_cast<int>(getpid())) {
+      bu = u;
+      best = kv.first;
+    }
+  }
+  return best;
+}
+
 int main(int argc, char** argv) {
+  signal(SIGUSR2, on_usr2);
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s libkgs_pmc.so kfd_gpu_id\n", argv[0]);
     return 2;
@@ -127,18 +157,50 @@ int main(int argc, char** argv) {
   }
   report("after_open_idle_1s", t1, 1.0, true);
   auto t2 = threads();
+  {  // locate the spinner, sample its stack, optionally demote it
+    auto a = threads();
+    std::this_thread::sleep_for(std::chrono::milliseconds(300));
+    const int spin = hottest(a, threads());
+    std::printf("{\"spinner_tid\":%d}\n", spin);
+    std::fflush(stdout);
+    if (spin > 0) {
+      for (int i = 0; i < 4; ++i) {
+        syscall(SYS_tgkill, getpid(), spin, SIGUSR2);
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      }
+      if (std::getenv("KGS_PROBE_SCHED_IDLE")) {
+        sched_param sp{};
+        const int rc = sched_setscheduler(spin, SCHED_IDLE, &sp);
+        std::printf("{\"sched_idle_rc\":%d}\n", rc);
+      }
+    }
+    t2 = threads();
+  }
+  std::vector<double> lat_us;
+  uint64_t first[3] = {}, last[3] = {};
+  int rc_bad = 0;
   std::thread s([&] {
     uint64_t v[3];
     uint32_t ns;
+    if (sample(h, first, 3, &ns) != 0) ++rc_bad;
     const auto end = std::chrono::steady_clock::now() + std::chrono::seconds(1);
     auto next = std::chrono::steady_clock::now();
     while (std::chrono::steady_clock::now() < end) {
-      sample(h, v, 3, &ns);
+      if (sample(h, v, 3, &ns) != 0) ++rc_bad;
+      else std::memcpy(last, v, sizeof v);
+      lat_us.push_back(ns * 1e-3);
       next += std::chrono::milliseconds(1);
       std::this_thread::sleep_until(next);
     }
   });
   report("sampling_1khz_1s", t2, 1.0, true);
   s.join();
+  std::sort(lat_us.begin(), lat_us.end());
+  if (!lat_us.empty())
+    std::printf("{\"samples\":%zu,\"errors\":%d,\"read_us_p50\":%.1f,\"read_us_p99\":%.1f,"
+                "\"delta\":{\"GRBM_COUNT\":%llu,\"GRBM_GUI_ACTIVE\":%llu,\"SQ_VALU_MFMA_BUSY_CYCLES\":%llu}}\n",
+                lat_us.size(), rc_bad, lat_us[lat_us.size() / 2], lat_us[lat_us.size() * 99 / 100],
+                static_cast<unsigned long long>(last[0] - first[0]), static_cast<unsigned long long>(last[1] - first[1]),
+                static_cast<unsigned long long>(last[2] - first[2]));
   return 0;
 }
