@@ -202,6 +202,7 @@ class ExporterProc:
             cmd += ["--pmc", pmc]
         env = dict(os.environ)
         env.setdefault("KGS_NO_BUILD", "1")
+        env.setdefault("PYTHONFAULTHANDLER", "1")  # a native fault leaves a trace in the exporter log
         if not a.mock and "--pmc" in cmd and cmd[cmd.index("--pmc") + 1] == "rocprofiler" \
                 and env.get("ROCP_TOOL_LIBRARIES"):
             # Running under rocprofv3: rocprofiler configuration closes before the

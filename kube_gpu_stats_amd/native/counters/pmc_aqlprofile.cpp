@@ -111,6 +111,18 @@ std::string aql_error() {
   return "unknown";
 }
 
+bool debug() {
+  static const bool on = std::getenv("KGS_AQL_DEBUG") != nullptr;
+  return on;
+}
+#define KGS_DBG(...)                      \
+  do {                                    \
+    if (debug()) {                        \
+      std::fprintf(stderr, "[aql] " __VA_ARGS__); \
+      std::fflush(stderr);                \
+    }                                     \
+  } while (0)
+
 int64_t mono_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -302,16 +314,20 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       q.agent = a->agent;
       hsa_ven_amd_aqlprofile_id_query_t id{bname.c_str(), 0, 0};
       uint32_t inst = 1;
-      if (hsa_ven_amd_aqlprofile_get_info(&q, HSA_VEN_AMD_AQLPROFILE_INFO_BLOCK_ID, &id) == HSA_STATUS_SUCCESS &&
-          id.instance_count > 0)
-        inst = id.instance_count;
+      const hsa_status_t qs = hsa_ven_amd_aqlprofile_get_info(&q, HSA_VEN_AMD_AQLPROFILE_INFO_BLOCK_ID, &id);
+      if (qs == HSA_STATUS_SUCCESS && id.instance_count > 0) inst = id.instance_count;
+      KGS_DBG("%s: block %s id=%u instances=%u (query status %d)\n", a->names[static_cast<size_t>(k)].c_str(),
+              bname.c_str(), id.id, id.instance_count, static_cast<int>(qs));
+      uint32_t valid = 0;
       for (uint32_t i = 0; i < inst; ++i) {
         hsa_ven_amd_aqlprofile_event_t ev{block, i, event};
         bool ok = false;
         if (hsa_ven_amd_aqlprofile_validate_event(a->agent, &ev, &ok) != HSA_STATUS_SUCCESS || !ok) continue;
         a->events.push_back(ev);
         a->ev_counter.push_back(k);
+        ++valid;
       }
+      KGS_DBG("%s: %u/%u instances valid\n", a->names[static_cast<size_t>(k)].c_str(), valid, inst);
     }
     if (a->events.empty()) {
       set_err(err, errlen, "no valid counter events (unresolved: " + missing + ")");
@@ -335,20 +351,28 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     p.events = a->events.data();
     p.event_count = static_cast<uint32_t>(a->events.size());
     uint32_t cmd_sz = 0, out_sz = 0;
+    KGS_DBG("get_info sizes for %zu events\n", a->events.size());
     if (hsa_ven_amd_aqlprofile_get_info(&p, HSA_VEN_AMD_AQLPROFILE_INFO_COMMAND_BUFFER_SIZE, &cmd_sz) !=
             HSA_STATUS_SUCCESS ||
         hsa_ven_amd_aqlprofile_get_info(&p, HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA_SIZE, &out_sz) != HSA_STATUS_SUCCESS) {
       set_err(err, errlen, "aqlprofile get_info: " + aql_error());
       return -1;
     }
+    // The v1 size query does not grow with the event count on gfx950 (8 KiB
+    // for 2 events and for 17: START then overruns it); both buffers are host
+    // memory, so size them generously.
+    cmd_sz = std::max<uint32_t>(cmd_sz, 256u << 10);
+    out_sz = std::max<uint32_t>(out_sz, 64u << 10);
     a->cmd = host_alloc(a, cmd_sz);
     a->out = host_alloc(a, out_sz);
     if (!a->cmd || !a->out) {
       set_err(err, errlen, "host buffer allocation failed");
       return -1;
     }
+    std::memset(a->cmd, 0xAB, cmd_sz);  // dry mode measures how much START/READ/STOP wrote
     p.command_buffer = {a->cmd, cmd_sz};
     p.output_buffer = {a->out, out_sz};
+    KGS_DBG("cmd=%u out=%u; building START/READ/STOP\n", cmd_sz, out_sz);
     if (hsa_ven_amd_aqlprofile_start(&p, &a->start_pkt) != HSA_STATUS_SUCCESS ||
         hsa_ven_amd_aqlprofile_read(&p, &a->read_pkt) != HSA_STATUS_SUCCESS ||
         hsa_ven_amd_aqlprofile_stop(&p, &a->stop_pkt) != HSA_STATUS_SUCCESS) {
@@ -356,8 +380,12 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       return -1;
     }
     if (std::getenv("KGS_AQL_DRY")) {  // packets built, nothing submitted (bring-up)
-      char b[160];
-      std::snprintf(b, sizeof b, "dry: events=%zu cmd=%u out=%u", a->events.size(), cmd_sz, out_sz);
+      const auto* c = static_cast<const uint8_t*>(a->cmd);
+      uint32_t used = cmd_sz;
+      while (used > 0 && c[used - 1] == 0xAB) --used;
+      char b[200];
+      std::snprintf(b, sizeof b, "dry: events=%zu cmd=%u cmd_used=%u out=%u", a->events.size(), cmd_sz, used,
+                    out_sz);
       set_err(err, errlen, b);
       return -1;
     }

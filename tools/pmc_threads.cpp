@@ -126,8 +126,20 @@ static int hottest(const std::map<int, T>& a, const std::map<int, T>& b) {
   return best;
 }
 
+static void on_segv(int sig) {
+  void* fr[48];
+  const int n = backtrace(fr, 48);
+  const char hdr[] = "--- SIGSEGV backtrace\n";
+  if (write(2, hdr, sizeof hdr - 1) < 0) {
+  }
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int main(int argc, char** argv) {
   signal(SIGUSR2, on_usr2);
+  signal(SIGSEGV, on_segv);
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s libkgs_pmc.so kfd_gpu_id\n", argv[0]);
     return 2;
@@ -148,9 +160,24 @@ int main(int argc, char** argv) {
   }
   report("after_init_idle_1s", t0, 1.0, true);
   auto t1 = threads();
-  const char* names[] = {"GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"};
-  const int is_max[] = {1, 1, 0};
-  const int h = open(std::strtoull(argv[2], nullptr, 10), names, is_max, 3, err, sizeof err);
+  // optional counter list after the gpu id: NAME[:max|:mean] ...  (default: the first three of the exporter's)
+  std::vector<std::string> nm = {"GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"};
+  std::vector<int> red = {1, 1, 0};
+  if (argc > 3) {
+    nm.clear();
+    red.clear();
+    for (int i = 3; i < argc; ++i) {
+      std::string a = argv[i];
+      const size_t c = a.find(':');
+      const std::string r = c == std::string::npos ? "" : a.substr(c + 1);
+      nm.push_back(c == std::string::npos ? a : a.substr(0, c));
+      red.push_back(r == "max" ? 1 : r == "mean" ? 2 : 0);
+    }
+  }
+  std::vector<const char*> names;
+  for (auto& x : nm) names.push_back(x.c_str());
+  const int nc = static_cast<int>(names.size());
+  const int h = open(std::strtoull(argv[2], nullptr, 10), names.data(), red.data(), nc, err, sizeof err);
   if (h < 0) {
     std::printf("{\"error\":\"open: %s\"}\n", err);
     return 1;
@@ -177,16 +204,16 @@ int main(int argc, char** argv) {
     t2 = threads();
   }
   std::vector<double> lat_us;
-  uint64_t first[3] = {}, last[3] = {};
+  uint64_t first[16] = {}, last[16] = {};
   int rc_bad = 0;
   std::thread s([&] {
-    uint64_t v[3];
+    uint64_t v[16];
     uint32_t ns;
-    if (sample(h, first, 3, &ns) != 0) ++rc_bad;
+    if (sample(h, first, nc, &ns) != 0) ++rc_bad;
     const auto end = std::chrono::steady_clock::now() + std::chrono::seconds(1);
     auto next = std::chrono::steady_clock::now();
     while (std::chrono::steady_clock::now() < end) {
-      if (sample(h, v, 3, &ns) != 0) ++rc_bad;
+      if (sample(h, v, nc, &ns) != 0) ++rc_bad;
       else std::memcpy(last, v, sizeof v);
       lat_us.push_back(ns * 1e-3);
       next += std::chrono::milliseconds(1);
@@ -197,10 +224,13 @@ int main(int argc, char** argv) {
   s.join();
   std::sort(lat_us.begin(), lat_us.end());
   if (!lat_us.empty())
-    std::printf("{\"samples\":%zu,\"errors\":%d,\"read_us_p50\":%.1f,\"read_us_p99\":%.1f,"
-                "\"delta\":{\"GRBM_COUNT\":%llu,\"GRBM_GUI_ACTIVE\":%llu,\"SQ_VALU_MFMA_BUSY_CYCLES\":%llu}}\n",
-                lat_us.size(), rc_bad, lat_us[lat_us.size() / 2], lat_us[lat_us.size() * 99 / 100],
-                static_cast<unsigned long long>(last[0] - first[0]), static_cast<unsigned long long>(last[1] - first[1]),
-                static_cast<unsigned long long>(last[2] - first[2]));
+  {
+    std::printf("{\"samples\":%zu,\"errors\":%d,\"read_us_p50\":%.1f,\"read_us_p99\":%.1f,\"delta\":{",
+                lat_us.size(), rc_bad, lat_us[lat_us.size() / 2], lat_us[lat_us.size() * 99 / 100]);
+    for (int k = 0; k < nc; ++k)
+      std::printf("%s\"%s\":%llu", k ? "," : "", nm[static_cast<size_t>(k)].c_str(),
+                  static_cast<unsigned long long>(last[k] - first[k]));
+    std::printf("}}\n");
+  }
   return 0;
 }
