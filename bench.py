@@ -41,7 +41,7 @@ from kube_gpu_stats_amd.parallel import dist as D  # noqa: E402
 from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text  # noqa: E402
 
 METRIC = "counter samples/sec/GPU + p50 scrape latency at 8×MI355X; GPU-time overhead %"
-AUTO_PMC = "rocprofiler"
+AUTO_PMC = "aqlprofile"  # direct CP reads: same counters, ≈10× less exporter CPU than rocprofiler-sdk
 
 
 def parse_args(argv=None):

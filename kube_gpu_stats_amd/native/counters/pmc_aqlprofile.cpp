@@ -77,10 +77,12 @@ const BlockNameId kBlocks[] = {
 struct Agent {
   hsa_agent_t agent{};
   uint32_t gpu_id = 0;  // KFD gpu_id (== HSA_AMD_AGENT_INFO_DRIVER_UID)
+  uint32_t cu_count = 0;  // enabled CUs (256 on MI355X)
   hsa_queue_t* queue = nullptr;
   hsa_signal_t sig{};
   std::vector<std::string> names;
   std::vector<int> reduce;                           // 0 sum, 1 max, 2 mean
+  std::vector<char> per_cu;                          // counter's block has one instance per CU
   std::vector<hsa_ven_amd_aqlprofile_event_t> events;
   std::vector<int> ev_counter;                       // event index -> counter index
   hsa_ven_amd_aqlprofile_profile_t prof{};
@@ -152,6 +154,7 @@ hsa_status_t on_agent(hsa_agent_t agent, void*) {
     Agent* a = new Agent();
     a->agent = agent;
     hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DRIVER_UID), &a->gpu_id);
+    hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &a->cu_count);
     g_agents.push_back(a);
   }
   return HSA_STATUS_SUCCESS;
@@ -250,8 +253,12 @@ int read_values(Agent* a) {
   Fold f{a};
   if (hsa_ven_amd_aqlprofile_iterate_data(&a->prof, on_data, &f) != HSA_STATUS_SUCCESS) return -3;
   a->last_results = f.n;
+  // Mean of a per-CU block (TA/TD/TCP): the packets read every instance slot of
+  // every SE (16 per SE on gfx950), but only cu_count of them exist (8 per SE
+  // on MI355X); the absent ones read 0.  Average over the CUs that exist.
   for (size_t k = 0; k < a->vals.size(); ++k)
-    if (a->reduce[k] == 2 && a->instances[k] > 0) a->vals[k] /= a->instances[k];
+    if (a->reduce[k] == 2 && a->instances[k] > 0)
+      a->vals[k] /= (a->per_cu[k] && a->cu_count > 0) ? a->cu_count : a->instances[k];
   return 0;
 }
 
@@ -300,6 +307,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     a->reduce.assign(is_max, is_max + n);
     a->events.clear();
     a->ev_counter.clear();
+    a->per_cu.assign(static_cast<size_t>(n), 0);
     std::string missing;
     for (int k = 0; k < n; ++k) {
       hsa_ven_amd_aqlprofile_block_name_t block;
@@ -309,6 +317,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
         missing += (missing.empty() ? "" : ",") + a->names[static_cast<size_t>(k)];
         continue;
       }
+      a->per_cu[static_cast<size_t>(k)] = bname == "TA" || bname == "TD" || bname == "TCP";
       // one event per block instance (TA per CU, SQ per SE, GRBM per XCC ...)
       hsa_ven_amd_aqlprofile_profile_t q{};
       q.agent = a->agent;
@@ -422,7 +431,8 @@ int kgs_pmc_sample(int handle, uint64_t* out, int n, uint32_t* read_ns) {
 int kgs_pmc_info(int handle, char* buf, int len) {
   if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
   Agent* a = g_agents[static_cast<size_t>(handle)];
-  std::string o = "impl=aqlprofile;mode=cumulative;events=" + std::to_string(a->events.size()) +
+  std::string o = "impl=aqlprofile;mode=cumulative;cu=" + std::to_string(a->cu_count) +
+                  ";events=" + std::to_string(a->events.size()) +
                   ";results=" + std::to_string(a->last_results) + ";timeouts=" + std::to_string(a->timeouts);
   for (size_t k = 0; k < a->names.size(); ++k)
     o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);

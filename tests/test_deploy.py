@@ -20,7 +20,7 @@ def test_daemonset_args_are_valid_exporter_flags():
     assert spec["hostPID"] is True
     c = spec["containers"][0]
     a = build_parser().parse_args(c["args"])
-    assert a.pmc == "rocprofiler" and a.hz == 10.0 and a.listen == "0.0.0.0:9400"
+    assert a.pmc == "aqlprofile" and a.hz == 10.0 and a.listen == "0.0.0.0:9400"
     env = {e["name"]: e for e in c["env"]}
     assert env["NODE_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName"
     mounts = {m["mountPath"] for m in c["volumeMounts"]}

@@ -168,8 +168,18 @@ def test_load_throughput_and_util_accumulators(N, torch_dev):
     assert 30 <= integ["distinct_samples"] / wall <= 120, integ
 
 
-def test_rocprofiler_counters_exporter_process(torch_dev):
-    """Exporter process with --pmc rocprofiler sees MFMA busy + HBM traffic of *this* process' kernels."""
+def _proc_cpu_seconds(pid: int) -> float:
+    with open(f"/proc/{pid}/stat") as f:
+        fields = f.read().rsplit(")", 1)[1].split()
+    return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+
+
+@pytest.mark.parametrize("reader", ["aqlprofile", "rocprofiler"])
+def test_counter_reader_exporter_process(torch_dev, reader):
+    """Exporter process with --pmc <reader> sees MFMA busy + HBM traffic of *this* process' kernels.
+
+    aqlprofile (direct CP reads, the default) must also stay cheap on the host:
+    the rocprofiler-sdk path keeps one HSA helper thread spinning (≈1 core)."""
     import torch
 
     from kube_gpu_stats_amd.ops.load import LoadStep
@@ -178,17 +188,18 @@ def test_rocprofiler_counters_exporter_process(torch_dev):
     p = torch.cuda.get_device_properties(0)
     bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
     cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz", "100",
-           "--pmc", "rocprofiler", "--control-stdin", "--bdfs", bdf]
+           "--pmc", reader, "--control-stdin", "--bdfs", bdf]
     proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                             text=True)
     try:
         ready = json.loads(proc.stdout.readline())
         print(json.dumps(ready)[:2000])
         assert ready["event"] == "ready", ready
-        if ready["pmc"] != "rocprofiler":
-            pytest.fail("rocprofiler counters unavailable: " + ready.get("pmc_error", ""))
+        if ready["pmc"] != reader:
+            pytest.fail(f"{reader} counters unavailable: " + ready.get("pmc_error", ""))
         sc = Scraper("127.0.0.1", ready["port"])
         ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=3 << 30)
+        cpu0, w0 = _proc_cpu_seconds(proc.pid), time.time()
         t0 = time.time()
         while time.time() - t0 < 2.0:
             ls.run_mfma()
@@ -203,11 +214,15 @@ def test_rocprofiler_counters_exporter_process(torch_dev):
         vmem = [v for lb, v in m2["amdgpu_vmem_busy_percent"]]
         clk = [v for lb, v in m2["amdgpu_gpu_clock_effective_mhz"]]
         pmc_n = [v for lb, v in m2["kgs_pmc_samples_total"]]
-        print(json.dumps({"mfma_util": mfma, "vmem_busy": vmem, "clock_mhz": clk, "pmc_samples": pmc_n}))
+        cores = (_proc_cpu_seconds(proc.pid) - cpu0) / (time.time() - w0)
+        print(json.dumps({"reader": reader, "mfma_util": mfma, "vmem_busy": vmem, "clock_mhz": clk,
+                          "pmc_samples": pmc_n, "exporter_cpu_cores": cores, "pmc_info": ready.get("pmc_info")}))
         assert mfma[0] > 50, mfma
         assert vmem[0] > 30, vmem     # triad keeps the TA units busy
         assert 1000 < clk[0] < 2600, clk
         assert pmc_n[0] > 200
+        if reader == "aqlprofile":
+            assert cores < 0.5, cores  # no spinning helper thread (rocprofiler path: ≈1.0)
     finally:
         try:
             proc.stdin.write("quit\n")
