@@ -44,7 +44,9 @@ CATALOG: tuple[Family, ...] = (
     # ---- utilisation ------------------------------------------------------------------------
     F("amdgpu_gfx_busy_percent", "gauge", "GFX busy %, time-weighted mean over the window from PMFW accumulators."),
     F("amdgpu_gfx_busy_instant_percent", "gauge", "GFX busy % in the latest PMFW table."),
-    F("amdgpu_gfx_busy_xcc_percent", "gauge", "Instantaneous busy % per XCC.", extra=("xcc",)),
+    F("amdgpu_gfx_busy_xcc_percent", "gauge",
+      "Busy % per XCC over the last firmware interval, from the per-partition accumulators "
+      "(instant value when those are absent); shows load imbalance across the 8 dies.", extra=("xcc",)),
     F("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller activity %, window mean."),
     F("amdgpu_gfx_busy_seconds_total", "counter", "∫ GFX busy fraction dt; rate() = exact mean utilisation."),
     F("amdgpu_umc_busy_seconds_total", "counter", "∫ UMC busy fraction dt."),

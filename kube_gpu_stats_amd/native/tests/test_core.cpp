@@ -7,13 +7,21 @@
 //     by more than the ring can explain, and never a torn slot.
 //  3. Sampler over the mock backend with fault injection, readers calling
 //     window_busy / window_pmc / integ concurrently, then stop().
+//  4. Recovery: a device that resets mid-run is re-opened and re-baselined.
+//  5. PMFW table parser fuzz (ASAN build): random, truncated and mutated
+//     v1.8-shaped buffers, each in an exactly-sized heap block so any read past
+//     `len` is caught; the parser must reject or parse, never overrun.
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
 #include <vector>
 
+#include <cstring>
+#include <random>
+
 #include "kgs/backend.h"
+#include "kgs/gpu_metrics.h"
 #include "kgs/pmc.h"
 #include "kgs/sampler.h"
 #include "kgs/seqlock.h"
@@ -191,7 +199,51 @@ static void test_recovery() {
   std::printf("recovery ok (%llu attempts)\n", static_cast<unsigned long long>(I1.recover_attempts));
 }
 
+static void test_parser_fuzz() {
+  std::mt19937_64 rng(12345);
+  // a syntactically valid v1.8 header: structure_size 3872, format 1, content 8
+  auto make = [&](size_t len) {
+    std::vector<uint8_t> b(len);
+    for (auto& x : b) x = static_cast<uint8_t>(rng());
+    if (len >= 4) {
+      b[0] = 3872 & 0xFF;
+      b[1] = 3872 >> 8;
+      b[2] = 1;
+      b[3] = 8;
+    }
+    return b;
+  };
+  int parsed = 0, rejected = 0;
+  for (int it = 0; it < 20000; ++it) {
+    size_t len;
+    switch (it % 4) {
+      case 0: len = rng() % 64; break;                  // tiny
+      case 1: len = 3872; break;                        // full size, random body
+      case 2: len = rng() % 3872; break;                // truncated
+      default: len = 3872 + rng() % 256; break;         // longer than the table
+    }
+    std::vector<uint8_t> b = make(len);
+    if (it % 8 == 5 && len > 400) b[338] = static_cast<uint8_t>(rng());  // num_partition field
+    // exact-size heap copy: ASAN flags any byte read past len
+    uint8_t* heap = len ? static_cast<uint8_t*>(std::malloc(len)) : nullptr;
+    if (len) std::memcpy(heap, b.data(), len);
+    GpuSample s;
+    const int rc = parse_gpu_metrics_v1_8(heap, len, s);
+    (void)gpu_metrics_revision(heap, len);
+    if (rc == 0) {
+      ++parsed;
+      CHECK(s.num_xcc <= static_cast<uint32_t>(kMaxXcc));
+    } else {
+      ++rejected;
+    }
+    std::free(heap);
+  }
+  CHECK(parsed > 0 && rejected > 0);
+  std::printf("parser fuzz ok (%d parsed, %d rejected)\n", parsed, rejected);
+}
+
 int main() {
+  test_parser_fuzz();
   test_seqlock();
   test_ring();
   test_sampler();
