@@ -49,10 +49,13 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--hz", type=float, default=1000.0,
-                    help="sampler tick rate per GPU: one hardware-counter drain per tick (PMFW table ≤100 Hz)")
+    ap.add_argument("--hz", type=float, default=8000.0,
+                    help="sampler tick rate per GPU: one hardware-counter drain per tick (PMFW table ≤100 Hz); "
+                    "8 kHz costs ≈0.08 exporter cores/GPU with pipelined reads (profiles/r1/pipelined)")
     ap.add_argument("--pmc", default="auto", choices=["auto", "aqlprofile", "rocprofiler", "none"],
                     help="counter reader (auto = %s)" % AUTO_PMC)
+    ap.add_argument("--pmc-pipeline", type=int, default=1, choices=[0, 1],
+                    help="aqlprofile reader: pipelined READs (1) or submit-and-wait per sample (0)")
     ap.add_argument("--scrape-hz", type=float, default=10.0)
     ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per step on MI355X")
     ap.add_argument("--mfma-blocks", type=int, default=2048)
@@ -199,7 +202,7 @@ class ExporterProc:
             cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock"]
         else:
             pmc = AUTO_PMC if a.pmc == "auto" else a.pmc
-            cmd += ["--pmc", pmc]
+            cmd += ["--pmc", pmc, "--pmc-pipeline" if a.pmc_pipeline else "--no-pmc-pipeline"]
         env = dict(os.environ)
         env.setdefault("KGS_NO_BUILD", "1")
         env.setdefault("PYTHONFAULTHANDLER", "1")  # a native fault leaves a trace in the exporter log

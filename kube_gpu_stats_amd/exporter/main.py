@@ -39,6 +39,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pmc", "none", "hardware counters: none | aqlprofile (direct CP reads) | rocprofiler "
                                 "(rocprofiler-sdk device counting) | mock")
     add_flag(ap, "pmc-lib", "", "counter reader library (default: the in-tree one for --pmc)")
+    add_flag(ap, "pmc-pipeline", True, "aqlprofile reader: overlap each counter READ's CP round trip with the "
+                                       "tick sleep (the sample is stamped with the CP read time)")
     add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
     add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
     add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
@@ -67,6 +69,7 @@ def config_from_args(a) -> dict:
         "pin_numa": a.pin_numa,
         "pmc_source": a.pmc,
         "pmc_lib": a.pmc_lib or pmc_lib_path(a.pmc),
+        "pmc_pipeline": a.pmc_pipeline,
         "listen_addr": host or "0.0.0.0",
         "port": int(port),
         "node_name": a.node_name,
@@ -122,8 +125,8 @@ def run(a) -> int:
         pass
     attr.stop()
     ex.stop()
-    print(json.dumps({"event": "stopped", "integrals": [ex.integrals(i) for i in range(ex.device_count)]}),
-          flush=True)
+    print(json.dumps({"event": "stopped", "integrals": [ex.integrals(i) for i in range(ex.device_count)],
+                      "pmc_info": [ex.pmc_info(i) for i in range(ex.device_count)]}), flush=True)
     return 0
 
 

@@ -79,7 +79,7 @@ struct Agent {
   uint32_t gpu_id = 0;  // KFD gpu_id (== HSA_AMD_AGENT_INFO_DRIVER_UID)
   uint32_t cu_count = 0;  // enabled CUs (256 on MI355X)
   hsa_queue_t* queue = nullptr;
-  hsa_signal_t sig{};
+  hsa_signal_t sig{};                                // START/STOP and synchronous READs
   std::vector<std::string> names;
   std::vector<int> reduce;                           // 0 sum, 1 max, 2 mean
   std::vector<char> per_cu;                          // counter's block has one instance per CU
@@ -90,6 +90,22 @@ struct Agent {
   void* out = nullptr;
   hsa_ext_amd_aql_pm4_packet_t start_pkt{}, read_pkt{}, stop_pkt{};
   bool started = false;
+  // Pipelined mode: two READ slots, each with its own command/output buffer and
+  // completion signal.  A sample() collects the READ submitted on the previous
+  // call (normally finished long ago) and submits the next one without waiting,
+  // so the sampler thread never blocks on the CP round trip.
+  bool pipelined = false;
+  hsa_ven_amd_aqlprofile_profile_t pprof[2]{};
+  void* pcmd[2] = {nullptr, nullptr};
+  void* pout[2] = {nullptr, nullptr};
+  hsa_ext_amd_aql_pm4_packet_t pread[2]{};
+  hsa_signal_t psig[2]{};
+  int64_t psubmit_ns[2] = {0, 0};
+  int inflight = -1;                                 // slot with a READ on the queue, -1 none
+  int64_t rtt_ns = 0;                                // CP round trip of a synchronous READ (EWMA)
+  uint64_t ready_on_poll = 0, waited_on_poll = 0;    // pipelined: READ already done / had to wait
+  int64_t host_ns = 0;                               // host time spent inside sample()
+  uint32_t cmd_sz = 0, out_sz = 0;
   std::string err;
   uint64_t reads = 0, timeouts = 0;
   uint32_t last_results = 0;
@@ -192,31 +208,41 @@ void* host_alloc(Agent* a, size_t bytes) {
   return p;
 }
 
-// Put one PM4-IB vendor packet on the agent's private queue and wait for it.
-int submit(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, uint64_t timeout_ns) {
+// Put one PM4-IB vendor packet on the agent's private queue (no wait).
+void enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig) {
   hsa_queue_t* q = a->queue;
-  hsa_signal_store_relaxed(a->sig, 1);
+  hsa_signal_store_relaxed(sig, 1);
   const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
   while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
   }
   auto* slot = reinterpret_cast<hsa_ext_amd_aql_pm4_packet_t*>(q->base_address) + (idx & (q->size - 1));
   std::memcpy(slot->pm4_command, tmpl.pm4_command, sizeof slot->pm4_command);
-  slot->completion_signal = a->sig;
+  slot->completion_signal = sig;
   const uint16_t header = static_cast<uint16_t>(
       (HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
       (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
       (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(q->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+}
+
+// Wait for a packet's completion signal.  BLOCKED: ROCr spins briefly, then
+// sleeps on the signal's KFD event.
+int wait_done(Agent* a, hsa_signal_t sig, uint64_t timeout_ns) {
   const int64_t end = mono_ns() + static_cast<int64_t>(timeout_ns);
-  // BLOCKED: ROCr spins briefly, then sleeps on the signal's KFD event.
-  while (hsa_signal_wait_scacquire(a->sig, HSA_SIGNAL_CONDITION_LT, 1, timeout_ns, HSA_WAIT_STATE_BLOCKED) != 0) {
+  while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, timeout_ns, HSA_WAIT_STATE_BLOCKED) != 0) {
     if (mono_ns() > end) {
       ++a->timeouts;
       return -1;
     }
   }
   return 0;
+}
+
+// Put one packet on the queue and wait for it.
+int submit(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, uint64_t timeout_ns) {
+  enqueue(a, tmpl, a->sig);
+  return wait_done(a, a->sig, timeout_ns);
 }
 
 struct Fold {
@@ -244,14 +270,13 @@ hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
   return HSA_STATUS_SUCCESS;
 }
 
-int read_values(Agent* a) {
-  std::memset(a->out, 0, a->prof.output_buffer.size);
-  if (submit(a, a->read_pkt, 1000000000ull) != 0) return -2;
+// Fold one completed READ's output buffer into a->vals.
+int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
   ++a->reads;
   a->vals.assign(a->names.size(), 0.0);
   a->instances.assign(a->names.size(), 0);
   Fold f{a};
-  if (hsa_ven_amd_aqlprofile_iterate_data(&a->prof, on_data, &f) != HSA_STATUS_SUCCESS) return -3;
+  if (hsa_ven_amd_aqlprofile_iterate_data(prof, on_data, &f) != HSA_STATUS_SUCCESS) return -3;
   a->last_results = f.n;
   // Mean of a per-CU block (TA/TD/TCP): the packets read every instance slot of
   // every SE (16 per SE on gfx950), but only cu_count of them exist (8 per SE
@@ -262,9 +287,79 @@ int read_values(Agent* a) {
   return 0;
 }
 
+int read_values(Agent* a) {
+  std::memset(a->out, 0, a->prof.output_buffer.size);
+  const int64_t t0 = mono_ns();
+  if (submit(a, a->read_pkt, 1000000000ull) != 0) return -2;
+  const int64_t rtt = mono_ns() - t0;
+  a->rtt_ns = a->rtt_ns ? (7 * a->rtt_ns + rtt) / 8 : rtt;
+  return fold(a, &a->prof);
+}
+
+// Pipelined sample: collect the READ in flight, submit the next one.  Returns the
+// collected values' estimated CP read time in *ts (submit + half a round trip).
+int read_pipelined(Agent* a, int64_t* ts) {
+  if (a->inflight < 0) {  // first call (or after an error): one synchronous read to prime
+    const int64_t t0 = mono_ns();
+    const int rc = read_values(a);
+    if (rc != 0) return rc;
+    if (ts) *ts = t0 + a->rtt_ns / 2;
+    std::memset(a->pout[0], 0, a->pprof[0].output_buffer.size);
+    a->psubmit_ns[0] = mono_ns();
+    enqueue(a, a->pread[0], a->psig[0]);
+    a->inflight = 0;
+    return 0;
+  }
+  const int k = a->inflight;
+  if (hsa_signal_load_scacquire(a->psig[k]) < 1) {
+    ++a->ready_on_poll;
+  } else {
+    ++a->waited_on_poll;
+    if (wait_done(a, a->psig[k], 1000000000ull) != 0) {
+      a->inflight = -1;  // the packet may still complete later; its slot is re-armed before reuse
+      return -2;
+    }
+  }
+  const int rc = fold(a, &a->pprof[k]);
+  if (ts) *ts = a->psubmit_ns[k] + a->rtt_ns / 2;
+  const int n = k ^ 1;
+  std::memset(a->pout[n], 0, a->pprof[n].output_buffer.size);
+  a->psubmit_ns[n] = mono_ns();
+  enqueue(a, a->pread[n], a->psig[n]);
+  a->inflight = n;
+  return rc;
+}
+
+// Second READ slot for pipelined mode: same events, own buffers and signal.
+// Only its READ packet is ever submitted (START/STOP come from the main profile).
+bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err) {
+  for (int k = 0; k < 2; ++k) {
+    hsa_ven_amd_aqlprofile_profile_t& p = a->pprof[k];
+    p = a->prof;
+    a->pcmd[k] = host_alloc(a, cmd_sz);
+    a->pout[k] = host_alloc(a, out_sz);
+    if (!a->pcmd[k] || !a->pout[k] || hsa_signal_create(1, 0, nullptr, &a->psig[k]) != HSA_STATUS_SUCCESS) {
+      err = "pipeline buffer allocation failed";
+      return false;
+    }
+    p.command_buffer = {a->pcmd[k], cmd_sz};
+    p.output_buffer = {a->pout[k], out_sz};
+    hsa_ext_amd_aql_pm4_packet_t s{}, t{};
+    if (hsa_ven_amd_aqlprofile_start(&p, &s) != HSA_STATUS_SUCCESS ||
+        hsa_ven_amd_aqlprofile_read(&p, &a->pread[k]) != HSA_STATUS_SUCCESS ||
+        hsa_ven_amd_aqlprofile_stop(&p, &t) != HSA_STATUS_SUCCESS) {
+      err = "aqlprofile pipeline packet build: " + aql_error();
+      return false;
+    }
+  }
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64_t* sample_ns);
 
 int kgs_pmc_init(char* err, int errlen) {
   static std::once_flag once;
@@ -381,6 +476,8 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     std::memset(a->cmd, 0xAB, cmd_sz);  // dry mode measures how much START/READ/STOP wrote
     p.command_buffer = {a->cmd, cmd_sz};
     p.output_buffer = {a->out, out_sz};
+    a->cmd_sz = cmd_sz;
+    a->out_sz = out_sz;
     KGS_DBG("cmd=%u out=%u; building START/READ/STOP\n", cmd_sz, out_sz);
     if (hsa_ven_amd_aqlprofile_start(&p, &a->start_pkt) != HSA_STATUS_SUCCESS ||
         hsa_ven_amd_aqlprofile_read(&p, &a->read_pkt) != HSA_STATUS_SUCCESS ||
@@ -417,14 +514,54 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
 }
 
 int kgs_pmc_sample(int handle, uint64_t* out, int n, uint32_t* read_ns) {
+  return kgs_pmc_sample_ts(handle, out, n, read_ns, nullptr);
+}
+
+// Like kgs_pmc_sample, plus the CLOCK_MONOTONIC time (ns) the values were read
+// by the CP.  In pipelined mode the values are those of the READ submitted on
+// the previous call, so this time precedes the call; read_ns is the host time
+// spent in the call (fold + submit), not the CP round trip.
+int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64_t* sample_ns) {
   if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
   Agent* a = g_agents[static_cast<size_t>(handle)];
   if (!a->started) return -1;
   const int64_t t0 = mono_ns();
-  const int rc = read_values(a);
-  if (read_ns) *read_ns = static_cast<uint32_t>(mono_ns() - t0);
+  int64_t ts = 0;
+  int rc;
+  if (a->pipelined) {
+    rc = read_pipelined(a, &ts);
+  } else {
+    rc = read_values(a);
+    ts = t0 + a->rtt_ns / 2;
+  }
+  const int64_t t1 = mono_ns();
+  a->host_ns += t1 - t0;
+  if (read_ns) *read_ns = static_cast<uint32_t>(t1 - t0);
+  if (sample_ns) *sample_ns = ts;
   if (rc != 0) return rc;
   for (int k = 0; k < n && static_cast<size_t>(k) < a->vals.size(); ++k) out[k] = static_cast<uint64_t>(a->vals[static_cast<size_t>(k)]);
+  return 0;
+}
+
+// Switch a handle between synchronous READs (submit + wait every sample) and
+// pipelined READs (collect the previous one, submit the next).  0 = ok.
+int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  std::lock_guard<std::mutex> g(g_mu);
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  if (!a->started) return -1;
+  if (a->inflight >= 0) {  // drain before changing mode
+    wait_done(a, a->psig[a->inflight], 1000000000ull);
+    a->inflight = -1;
+  }
+  if (on && !a->pcmd[0]) {
+    std::string e;
+    if (!setup_pipeline(a, a->cmd_sz, a->out_sz, e)) {
+      set_err(err, errlen, e);
+      return -1;
+    }
+  }
+  a->pipelined = on != 0;
   return 0;
 }
 
@@ -433,7 +570,11 @@ int kgs_pmc_info(int handle, char* buf, int len) {
   Agent* a = g_agents[static_cast<size_t>(handle)];
   std::string o = "impl=aqlprofile;mode=cumulative;cu=" + std::to_string(a->cu_count) +
                   ";events=" + std::to_string(a->events.size()) +
-                  ";results=" + std::to_string(a->last_results) + ";timeouts=" + std::to_string(a->timeouts);
+                  ";results=" + std::to_string(a->last_results) + ";timeouts=" + std::to_string(a->timeouts) +
+                  ";pipelined=" + std::to_string(a->pipelined ? 1 : 0) + ";rtt_us=" + std::to_string(a->rtt_ns / 1000) +
+                  ";reads=" + std::to_string(a->reads) + ";ready_on_poll=" + std::to_string(a->ready_on_poll) +
+                  ";waited_on_poll=" + std::to_string(a->waited_on_poll) +
+                  ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads : 0.0);
   for (size_t k = 0; k < a->names.size(); ++k)
     o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
   if (!a->err.empty()) o += ";" + a->err;
@@ -448,6 +589,10 @@ void kgs_pmc_close(int handle) {
   std::lock_guard<std::mutex> g(g_mu);
   Agent* a = g_agents[static_cast<size_t>(handle)];
   if (a->started) {
+    if (a->inflight >= 0) {
+      wait_done(a, a->psig[a->inflight], 1000000000ull);
+      a->inflight = -1;
+    }
     submit(a, a->stop_pkt, 1000000000ull);
     a->started = false;
   }

@@ -38,6 +38,7 @@ struct ExporterConfig {
   std::vector<std::string> bdfs;    // restrict sampling to these PCI addresses (empty = all)
   std::string pmc_source = "none";  // "none" | "rocprofiler" | "mock"
   std::string pmc_lib;              // path of libkgs_pmc.so
+  bool pmc_pipeline = true;         // overlap counter READs with the tick sleep (aqlprofile reader)
   std::string listen_addr = "0.0.0.0";
   int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
   std::string node_name;
@@ -81,6 +82,12 @@ class Exporter {
   std::string topology_json();
   std::string devices_json();
   std::string samples_json(int dev, int n);
+  // Full-rate hardware-counter stream of one GPU, oldest first: the last `n`
+  // drains, or (since > 0) every drain with seq > since still in the ring, so a
+  // client polling with the last seq it saw receives the stream without gaps.
+  // Each entry carries the cumulative counts and the rates over the interval
+  // since the previous drain.
+  std::string counters_json(int dev, int n, uint64_t since);
   bool healthy() const;
   // Stop / restart the sampler threads (HTTP and state stay up; integrals continue).
   void pause_sampling();

@@ -73,9 +73,12 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 // dlopen `lib_path` — libkgs_pmc_aql.so (direct aqlprofile reader, "aqlprofile")
 // or libkgs_pmc.so (rocprofiler-sdk device counting, "rocprofiler"); both export
 // the kgs_pmc_* C ABI — and open one counting session per device.  nullptr +
-// err on failure (no permission, no HSA, ...).
+// err on failure (no permission, no HSA, ...).  `pipelined` asks a reader that
+// exports kgs_pmc_set_pipelined (aqlprofile) to overlap each READ's CP round
+// trip with the sampler's sleep: a sample returns the READ submitted on the
+// previous tick, stamped with the time the CP executed it.
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
-                                                      std::string& err);
+                                                      bool pipelined, std::string& err);
 
 }  // namespace kgs

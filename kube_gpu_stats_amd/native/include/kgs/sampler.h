@@ -38,6 +38,11 @@ struct SamplerConfig {
 };
 
 constexpr size_t kRing = 1024;          // ≥10 s of history at 100 Hz
+// Counter samples decimated to one per kPmcSlowNs feed the window gauges, so a
+// 1 s window is covered at any tick rate (the full-rate ring holds 85 ms at 12 kHz).
+constexpr size_t kPmcSlowRing = 2048;
+constexpr size_t kPmcRing = 8192;       // raw counter stream: ≥1 s at 8 kHz (/counters)
+constexpr int64_t kPmcSlowNs = 5000000;  // 5 ms → ≥10 s of history
 constexpr int kReadHistBuckets = 12;    // backend read latency histogram
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 
@@ -46,7 +51,8 @@ struct DeviceState {
   SampleRing<GpuSample, kRing> ring;
   Seqlock<Integrals> integ;
   Seqlock<PmcSample> pmc_latest;
-  SampleRing<PmcSample, kRing> pmc_ring;
+  SampleRing<PmcSample, kPmcRing> pmc_ring;         // every counter drain
+  SampleRing<PmcSample, kPmcSlowRing> pmc_slow_ring;  // ≥ kPmcSlowNs apart (window gauges)
 
   mutable std::mutex slow_mu;  // guards the two shared_ptrs below
   std::shared_ptr<const std::vector<ProcInfo>> procs;

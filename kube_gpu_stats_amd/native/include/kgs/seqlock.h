@@ -84,6 +84,35 @@ class SampleRing {
   uint64_t head() const { return head_.load(std::memory_order_acquire); }
   static constexpr size_t capacity() { return N; }
 
+  // The i-th most recent entry (0 = newest); false if absent or torn.
+  bool at(uint64_t i, T& out) const {
+    const uint64_t h = head();
+    if (i >= h || i >= N - 1) return false;
+    return slots_[(h - 1 - i) & (N - 1)].load(out, 4);
+  }
+
+  // Number of entries a reader can walk back over (one slot of slack for the writer).
+  size_t available() const {
+    const uint64_t h = head();
+    return static_cast<size_t>(h < N - 1 ? h : N - 1);
+  }
+
+  // Visit the most recent entries newest-first, one seqlock load at a time,
+  // until `fn(entry)` returns false; returns the number visited.  A scrape that
+  // needs the last second of a ring reads only that second, not the whole ring.
+  template <class F>
+  size_t visit_recent(F&& fn) const {
+    const uint64_t h = head();
+    T v;
+    size_t n = 0;
+    for (uint64_t i = 0; i < h && i < N - 1; ++i) {
+      if (!slots_[(h - 1 - i) & (N - 1)].load(v, 4)) continue;
+      ++n;
+      if (!fn(static_cast<const T&>(v))) break;
+    }
+    return n;
+  }
+
   // Copy up to `max` most recent entries (newest first) into out[]; returns count.
   size_t recent(T* out, size_t max) const {
     const uint64_t h = head();

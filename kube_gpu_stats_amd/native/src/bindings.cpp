@@ -53,6 +53,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.bdfs = get<std::vector<std::string>>(d, "bdfs", c.bdfs);
   c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);
   c.pmc_lib = get<std::string>(d, "pmc_lib", c.pmc_lib);
+  c.pmc_pipeline = get<bool>(d, "pmc_pipeline", c.pmc_pipeline);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);
   c.node_name = get<std::string>(d, "node_name", c.node_name);

@@ -74,7 +74,7 @@ bool Exporter::init() {
   if (cfg_.pmc_source == "mock") {
     pmc_ = make_mock_counter_source(*be_, cfg_.mock, cfg_.mock_pmc);
   } else if (cfg_.pmc_source == "rocprofiler" || cfg_.pmc_source == "aqlprofile") {
-    pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, pmc_err_);
+    pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, cfg_.pmc_pipeline, pmc_err_);
   } else if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
     err_ = "unknown pmc_source '" + cfg_.pmc_source + "'";
     return false;
@@ -260,6 +260,58 @@ std::string Exporter::samples_json(int dev, int n) {
     o += ",\"vram_used_bytes\":" + std::to_string(s.vram_used_bytes) + ",\"read_ns\":" + std::to_string(s.read_ns) + '}';
   }
   o += ']';
+  return o;
+}
+
+std::string Exporter::counters_json(int dev, int n, uint64_t since) {
+  if (!sampler_ || dev < 0 || dev >= sampler_->device_count()) return "{\"samples\":[]}";
+  const int cap = static_cast<int>(kPmcRing) - 2;
+  if (n <= 0) n = 1;
+  if (since > 0 || n > cap) n = cap;
+  std::vector<PmcSample> buf;
+  buf.reserve(static_cast<size_t>(n) + 1);
+  // newest first; one extra (older) entry gives the first returned sample its rates
+  sampler_->state(dev).pmc_ring.visit_recent([&](const PmcSample& p) {
+    buf.push_back(p);
+    if (since > 0 && p.seq <= since) return false;
+    return buf.size() < static_cast<size_t>(n) + 1;
+  });
+  const int num_cu = be_->info(dev).num_cu;
+  std::string o = "{\"gpu\":" + std::to_string(dev) + ",\"counters\":[";
+  for (int i = 0; i < kPmcCount; ++i) {
+    if (i) o += ',';
+    jstr(o, pmc_counter_name(i));
+  }
+  o += "],\"samples\":[";
+  bool first = true;
+  for (size_t i = buf.size(); i-- > 0;) {  // oldest first
+    const PmcSample& p = buf[i];
+    if (since > 0 && p.seq <= since) continue;
+    if (since == 0 && i + 1 == buf.size() && buf.size() > static_cast<size_t>(n)) continue;  // rate base only
+    if (!first) o += ',';
+    first = false;
+    o += "{\"seq\":" + std::to_string(p.seq) + ",\"mono_ns\":" + std::to_string(p.mono_ns) + ",\"v\":[";
+    for (int k = 0; k < kPmcCount; ++k) {
+      if (k) o += ',';
+      o += std::to_string(p.value[k]);
+    }
+    o += ']';
+    if (i + 1 < buf.size()) {
+      const PmcRates r = pmc_rates(buf[i + 1], p, num_cu);
+      o += ",\"dt_us\":";
+      jnum(o, r.dt_s * 1e6);
+      o += ",\"gpu_active_pct\":";
+      jnum(o, r.gpu_active_pct);
+      o += ",\"mfma_util_pct\":";
+      jnum(o, r.mfma_util_pct);
+      o += ",\"vmem_busy_pct\":";
+      jnum(o, r.vmem_busy_pct);
+      o += ",\"gpu_clock_mhz\":";
+      jnum(o, r.gpu_clock_mhz);
+    }
+    o += '}';
+  }
+  o += "]}";
   return o;
 }
 

@@ -40,6 +40,16 @@ int query_int(const std::string& q, const char* key, int dflt) {
   return dflt;
 }
 
+uint64_t query_u64(const std::string& q, const char* key, uint64_t dflt) {
+  const std::string k = std::string(key) + "=";
+  size_t p = 0;
+  while ((p = q.find(k, p)) != std::string::npos) {
+    if (p == 0 || q[p - 1] == '&' || q[p - 1] == '?') return std::strtoull(q.c_str() + p + k.size(), nullptr, 10);
+    p += k.size();
+  }
+  return dflt;
+}
+
 void respond(Conn& c, int code, const char* reason, const char* ctype, const std::string& body) {
   c.out.clear();
   c.out_off = 0;
@@ -213,10 +223,15 @@ void HttpServer::loop() {
         } else if (target == "/samples") {
           respond(c, 200, "OK", "application/json",
                   ex_->samples_json(query_int(query, "gpu", 0), query_int(query, "n", 100)));
+        } else if (target == "/counters") {
+          respond(c, 200, "OK", "application/json",
+                  ex_->counters_json(query_int(query, "gpu", 0), query_int(query, "n", 100),
+                                     query_u64(query, "since", 0)));
         } else if (target == "/") {
           respond(c, 200, "OK", "text/html",
                   "<html><body><h1>kube_gpu_stats_amd exporter</h1><a href=\"/metrics\">/metrics</a> "
-                  "<a href=\"/topology\">/topology</a> <a href=\"/devices\">/devices</a></body></html>\n");
+                  "<a href=\"/topology\">/topology</a> <a href=\"/devices\">/devices</a> "
+                  "<a href=\"/samples\">/samples</a> <a href=\"/counters\">/counters</a></body></html>\n");
         } else {
           respond(c, 404, "Not Found", "text/plain", "not found\n");
         }

@@ -78,6 +78,8 @@ class MockCounterSource final : public CounterSource {
 using init_fn = int (*)(char*, int);
 using open_fn = int (*)(uint64_t, const char* const*, const int*, int, char*, int);
 using sample_fn = int (*)(int, uint64_t*, int, uint32_t*);
+using sample_ts_fn = int (*)(int, uint64_t*, int, uint32_t*, int64_t*);
+using pipelined_fn = int (*)(int, int, char*, int);
 using close_fn = void (*)(int);
 using info_fn = int (*)(int, char*, int);
 
@@ -91,7 +93,8 @@ class DlCounterSource final : public CounterSource {
     // The library stays loaded: HSA/rocprofiler must not be unloaded mid-process.
   }
 
-  bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, std::string& err) {
+  bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, bool pipelined,
+            std::string& err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!lib_) {
       err = std::string("dlopen failed: ") + dlerror();
@@ -102,6 +105,8 @@ class DlCounterSource final : public CounterSource {
     sample_ = reinterpret_cast<sample_fn>(dlsym(lib_, "kgs_pmc_sample"));
     close_ = reinterpret_cast<close_fn>(dlsym(lib_, "kgs_pmc_close"));
     info_ = reinterpret_cast<info_fn>(dlsym(lib_, "kgs_pmc_info"));
+    sample_ts_ = reinterpret_cast<sample_ts_fn>(dlsym(lib_, "kgs_pmc_sample_ts"));    // optional
+    auto set_pipe = reinterpret_cast<pipelined_fn>(dlsym(lib_, "kgs_pmc_set_pipelined"));  // optional
     if (!init || !open_ || !sample_ || !close_) {
       err = path + ": missing kgs_pmc_* symbols";
       return false;
@@ -125,6 +130,11 @@ class DlCounterSource final : public CounterSource {
       handles_[static_cast<size_t>(d)] = h;
       if (h >= 0) ++opened;
       else err += "dev" + std::to_string(d) + ": " + ebuf + "; ";
+      if (h >= 0 && pipelined && set_pipe) {
+        ebuf[0] = 0;
+        if (set_pipe(h, 1, ebuf, sizeof ebuf) != 0)  // stays synchronous, still usable
+          err += "dev" + std::to_string(d) + " pipelined reads unavailable: " + ebuf + "; ";
+      }
     }
     return opened > 0;
   }
@@ -141,11 +151,13 @@ class DlCounterSource final : public CounterSource {
   int sample(int dev, PmcSample& s) override {
     if (dev < 0 || dev >= static_cast<int>(handles_.size()) || handles_[dev] < 0) return -1;
     uint32_t rns = 0;
-    const int rc = sample_(handles_[dev], s.value, kPmcCount, &rns);
+    int64_t ts = 0;
+    const int rc = sample_ts_ ? sample_ts_(handles_[dev], s.value, kPmcCount, &rns, &ts)
+                              : sample_(handles_[dev], s.value, kPmcCount, &rns);
     if (rc != 0) return rc;
     s.n = kPmcCount;
     s.read_ns = rns;
-    s.mono_ns = mono_ns();
+    s.mono_ns = ts > 0 ? ts : mono_ns();  // when the CP read the counters (pipelined: previous call)
     return 0;
   }
 
@@ -153,6 +165,7 @@ class DlCounterSource final : public CounterSource {
   void* lib_ = nullptr;
   open_fn open_ = nullptr;
   sample_fn sample_ = nullptr;
+  sample_ts_fn sample_ts_ = nullptr;
   close_fn close_ = nullptr;
   info_fn info_ = nullptr;
   std::vector<int> handles_;
@@ -168,9 +181,9 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend&, const Mo
 
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
-                                                      std::string& err) {
+                                                      bool pipelined, std::string& err) {
   auto s = std::make_unique<DlCounterSource>(name);
-  if (!s->load(lib_path, be, devices, err)) return nullptr;
+  if (!s->load(lib_path, be, devices, pipelined, err)) return nullptr;
   return s;
 }
 

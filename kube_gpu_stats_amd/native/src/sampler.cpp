@@ -176,6 +176,7 @@ void Sampler::run(int dev) {
   GpuSample prev;
   bool have_prev = false;
   uint64_t seq = 0, pmc_seq = 0, tick = 0;
+  int64_t last_slow_ns = 0;
   {  // resume after a pause: counters and sequence numbers continue
     st.integ.load(I);
     GpuSample last;
@@ -256,6 +257,10 @@ void Sampler::run(int dev) {
       if (prc == 0) {
         ps.seq = ++pmc_seq;
         st.pmc_ring.push(ps);
+        if (ps.mono_ns - last_slow_ns >= kPmcSlowNs) {
+          st.pmc_slow_ring.push(ps);
+          last_slow_ns = ps.mono_ns;
+        }
         st.pmc_latest.store(ps);
         ++I.pmc_samples;
       } else {
@@ -324,20 +329,17 @@ void Sampler::run(int dev) {
 }
 
 bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, int& n) const {
-  static thread_local std::vector<GpuSample> buf(kRing);
   const DeviceState& st = *states_[dev];
-  const size_t got = st.ring.recent(buf.data(), kRing);
   double wsum = 0, g = 0, u = 0;
   n = 0;
-  for (size_t i = 0; i < got; ++i) {
-    const GpuSample& s = buf[i];
-    if (s.dt_s <= 0 || s.gfx_busy_window_pct < 0) continue;
+  st.ring.visit_recent([&](const GpuSample& s) {
+    if (s.dt_s <= 0 || s.gfx_busy_window_pct < 0) return true;
     g += s.gfx_busy_window_pct * s.dt_s;
     u += s.umc_busy_window_pct * s.dt_s;
     wsum += s.dt_s;
     ++n;
-    if (wsum >= window_s) break;
-  }
+    return wsum < window_s;
+  });
   if (wsum <= 0) {
     GpuSample s;
     if (!st.latest.load(s)) return false;
@@ -352,17 +354,36 @@ bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, in
 }
 
 bool Sampler::window_pmc(int dev, double window_s, PmcRates& out) const {
-  static thread_local std::vector<PmcSample> buf(kRing);
   const DeviceState& st = *states_[dev];
-  const size_t got = st.pmc_ring.recent(buf.data(), kRing);
-  if (got < 2) return false;
-  const PmcSample& b = buf[0];
-  size_t ai = 1;
-  for (size_t i = 1; i < got; ++i) {
-    ai = i;
-    if ((b.mono_ns - buf[i].mono_ns) * 1e-9 >= window_s) break;
+  PmcSample b;
+  if (!st.pmc_latest.load(b)) return false;
+  // Binary search the decimated ring (time-ordered, newest first) for the newest
+  // entry at least window_s older than `b`; fall back to the oldest one held.
+  const int64_t want = b.mono_ns - static_cast<int64_t>(window_s * 1e9);
+  size_t lo = 0, hi = st.pmc_slow_ring.available();
+  if (hi == 0) return false;
+  PmcSample a, e;
+  bool have_a = false;
+  while (lo < hi) {
+    const size_t mid = lo + (hi - lo) / 2;
+    if (!st.pmc_slow_ring.at(mid, e)) {  // torn / overwritten under us: treat as too new
+      lo = mid + 1;
+      continue;
+    }
+    if (e.mono_ns <= want) {
+      a = e;
+      have_a = true;
+      hi = mid;
+    } else {
+      lo = mid + 1;
+    }
   }
-  out = pmc_rates(buf[ai], b, be_->info(dev).num_cu);
+  if (!have_a) {  // window longer than the history: use the oldest entry
+    const size_t n = st.pmc_slow_ring.available();
+    if (n == 0 || !st.pmc_slow_ring.at(n - 1, a)) return false;
+  }
+  if (a.mono_ns >= b.mono_ns) return false;
+  out = pmc_rates(a, b, be_->info(dev).num_cu);
   return out.dt_s > 0;
 }
 

@@ -198,3 +198,45 @@ def test_render_latency_8_gpus(mock_exporter):
     mean_ms = st["render_ns_total"] / st["scrapes"] / 1e6
     assert mean_ms < 20, mean_ms  # generous for CI; bench reports the real p50
     assert not math.isnan(mean_ms)
+
+
+def test_counter_stream_endpoint_is_gapless(mock_exporter):
+    """/counters: full-rate counter drains, oldest first; polling with ``since``
+    returns every drain exactly once (no gaps, no repeats) while the ring holds it."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0,
+                       mock={"util_base": 50, "util_amp": 0.0001})
+    time.sleep(0.3)
+    body = json.load(get(ex.port, "/counters?gpu=0&n=50"))
+    assert body["counters"][:3] == ["GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"]
+    s = body["samples"]
+    assert len(s) == 50
+    seqs = [x["seq"] for x in s]
+    assert seqs == list(range(seqs[0], seqs[0] + 50))
+    assert all("mfma_util_pct" in x for x in s)  # the extra base sample gives the first one its rates
+    # mock: 50 % busy, MFMA busy 60 % of active time
+    assert abs(sum(x["gpu_active_pct"] for x in s) / len(s) - 50) < 5
+    assert abs(sum(x["mfma_util_pct"] for x in s) / len(s) - 60) < 6
+    assert all(200 < x["dt_us"] < 20000 for x in s)
+    last = seqs[-1]
+    got = []
+    for _ in range(5):
+        time.sleep(0.1)
+        b = json.load(get(ex.port, f"/counters?gpu=0&since={last}"))
+        new = [x["seq"] for x in b["samples"]]
+        if new:
+            assert new[0] == last + 1, (last, new[:3])
+            last = new[-1]
+        got += new
+    assert got == list(range(seqs[-1] + 1, last + 1)) and len(got) > 300
+    assert json.load(get(ex.port, "/counters?gpu=7"))["samples"] == []
+
+
+def test_counter_window_covers_full_window_at_high_rate(mock_exporter):
+    """At 8 kHz the 1024-deep full-rate ring spans 128 ms; the window gauges use the
+    decimated ring, so a 1 s window really covers ≈1 s."""
+    ex = mock_exporter(n_gpus=1, hz=8000, pmc_source="mock", proc_every=0, link_every=0, window_s=1.0)
+    time.sleep(1.5)
+    w = ex.window(0, 1.0)
+    assert 0.95 <= w["pmc_dt_s"] <= 1.05, w
+    w = ex.window(0, 0.2)
+    assert 0.19 <= w["pmc_dt_s"] <= 0.21, w

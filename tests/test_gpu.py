@@ -174,21 +174,26 @@ def _proc_cpu_seconds(pid: int) -> float:
     return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
 
 
-@pytest.mark.parametrize("reader", ["aqlprofile", "rocprofiler"])
-def test_counter_reader_exporter_process(torch_dev, reader):
+@pytest.mark.parametrize("mode", ["aqlprofile", "aqlprofile-sync", "rocprofiler"])
+def test_counter_reader_exporter_process(torch_dev, mode):
     """Exporter process with --pmc <reader> sees MFMA busy + HBM traffic of *this* process' kernels.
 
     aqlprofile (direct CP reads, the default) must also stay cheap on the host:
-    the rocprofiler-sdk path keeps one HSA helper thread spinning (≈1 core)."""
+    the rocprofiler-sdk path keeps one HSA helper thread spinning (≈1 core).
+    ``aqlprofile`` runs pipelined READs (the default), ``aqlprofile-sync``
+    submits and waits per sample."""
     import torch
 
     from kube_gpu_stats_amd.ops.load import LoadStep
     from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
 
+    reader = mode.split("-")[0]
     p = torch.cuda.get_device_properties(0)
     bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
     cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz", "100",
            "--pmc", reader, "--control-stdin", "--bdfs", bdf]
+    if mode == "aqlprofile-sync":
+        cmd.append("--no-pmc-pipeline")
     proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                             text=True)
     try:
@@ -215,7 +220,7 @@ def test_counter_reader_exporter_process(torch_dev, reader):
         clk = [v for lb, v in m2["amdgpu_gpu_clock_effective_mhz"]]
         pmc_n = [v for lb, v in m2["kgs_pmc_samples_total"]]
         cores = (_proc_cpu_seconds(proc.pid) - cpu0) / (time.time() - w0)
-        print(json.dumps({"reader": reader, "mfma_util": mfma, "vmem_busy": vmem, "clock_mhz": clk,
+        print(json.dumps({"mode": mode, "mfma_util": mfma, "vmem_busy": vmem, "clock_mhz": clk,
                           "pmc_samples": pmc_n, "exporter_cpu_cores": cores, "pmc_info": ready.get("pmc_info")}))
         assert mfma[0] > 50, mfma
         assert vmem[0] > 30, vmem     # triad keeps the TA units busy
@@ -223,13 +228,17 @@ def test_counter_reader_exporter_process(torch_dev, reader):
         assert pmc_n[0] > 200
         if reader == "aqlprofile":
             assert cores < 0.5, cores  # no spinning helper thread (rocprofiler path: ≈1.0)
+            want = "pipelined=0" if mode.endswith("-sync") else "pipelined=1"
+            assert want in ready["pmc_info"][0], ready["pmc_info"]
     finally:
+        out = err = ""
         try:
             proc.stdin.write("quit\n")
             proc.stdin.flush()
-            proc.wait(timeout=30)
+            out, err = proc.communicate(timeout=30)
         except Exception:  # noqa: BLE001
             proc.kill()
-        err = proc.stderr.read()
+            out, err = proc.communicate()
+        print(out[-3000:])  # "stopped" event: integrals + the reader's final pmc_info
         if err:
             print(err[-4000:])
