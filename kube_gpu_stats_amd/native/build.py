@@ -147,11 +147,14 @@ def build_tsan_test(verbose: bool = False, sanitizer: str = "thread") -> str:
     tag = "tsan" if sanitizer == "thread" else "asan"
     out = os.path.join(HERE, "build", f"test_core_{tag}")
     srcs = [os.path.join(HERE, "tests", "test_core.cpp")] + [
-        os.path.join(HERE, "src", f) for f in ("sampler.cpp", "backend_mock.cpp", "pmc.cpp", "gpu_metrics.cpp", "util.cpp")]
+        os.path.join(HERE, "src", f) for f in ("sampler.cpp", "backend_mock.cpp", "pmc.cpp", "gpu_metrics.cpp", "util.cpp",
+                                              "exporter.cpp", "render.cpp", "http.cpp", "backend_amdsmi.cpp")]
     os.makedirs(os.path.dirname(out), exist_ok=True)
     if _stale(out, srcs + _headers() + [__file__]):
         _run(["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-pthread",
-              "-I" + os.path.join(HERE, "include"), *srcs, "-o", out, "-ldl"], verbose)
+              "-I" + os.path.join(HERE, "include"), "-I" + os.path.join(ROCM, "include"), *srcs, "-o", out,
+              "-L" + os.path.join(ROCM, "lib"), "-lamd_smi", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl"],
+             verbose)
     return out
 
 

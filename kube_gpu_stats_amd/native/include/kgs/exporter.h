@@ -99,6 +99,7 @@ class Exporter {
   std::atomic<uint64_t> render_ns_total{0};
   std::atomic<uint64_t> render_ns_last{0};
   std::atomic<uint64_t> http_requests{0};
+  std::atomic<size_t> last_render_bytes_{64 * 1024};  // sizes the next render's buffer
 
  private:
   void build_static_labels();
@@ -118,6 +119,13 @@ class Exporter {
   std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> pid_owners_;
   std::string node_name_;
   std::shared_ptr<const std::string> extra_;
+  // Render caches (guarded by mu_): the device-info + topology block changes only
+  // with the node name; a device's xGMI link-info block only when the slow tier
+  // publishes a new link table (compared by pointer; the held shared_ptr keeps
+  // the address from being reused).
+  std::shared_ptr<const std::string> static_block_;
+  std::string static_block_node_;
+  std::vector<std::pair<std::shared_ptr<const std::vector<LinkInfo>>, std::shared_ptr<const std::string>>> link_blocks_;
 };
 
 // Escape a Prometheus label value.

@@ -62,6 +62,10 @@ struct GpuSample {
   float gfx_busy_window_pct = -1;
   float umc_busy_window_pct = -1;
   float dt_s = 0;              // firmware time since the previous distinct sample
+  // Running sums of the sampler's integrals at this sample (Integrals::
+  // gfx_busy_seconds / umc_busy_seconds / sampled_seconds): the mean over any
+  // window is a difference of two samples, found by binary search of the ring.
+  double cum_gfx_s = 0, cum_umc_s = 0, cum_dt_s = 0;
 
   float temp_hotspot_c = 0, temp_mem_c = 0, temp_vrsoc_c = 0;
   float power_w = 0;

@@ -6,6 +6,7 @@
 // exactly those label keys plus namespace/container/gpu/uuid, which the
 // reference's `avg ... by` averages away.  Everything else is
 // the amdgpu_* / kgs_* families documented in models/schema.py.
+#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstring>
@@ -16,13 +17,16 @@
 namespace kgs {
 
 void append_label_value(std::string& out, const std::string& v) {
-  for (char c : v) {
-    switch (c) {
-      case '\\': out += "\\\\"; break;
-      case '"': out += "\\\""; break;
-      case '\n': out += "\\n"; break;
-      default: out += c;
-    }
+  // Label values almost never need escaping: append unescaped spans in bulk.
+  const char* p = v.data();
+  const char* const end = p + v.size();
+  while (p < end) {
+    const char* q = p;
+    while (q < end && *q != '\\' && *q != '"' && *q != '\n') ++q;
+    out.append(p, q);
+    if (q == end) break;
+    out += *q == '\n' ? "\\n" : (*q == '"' ? "\\\"" : "\\\\");
+    p = q + 1;
   }
 }
 
@@ -34,35 +38,62 @@ int64_t mono_ns() {
   return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
 }
 
-// Small append-only writer; numbers go through std::to_chars (shortest
-// round-trip form) so the hot path never touches locale-dependent printf.
+// Append-only writer over a raw buffer: one capacity check and memcpy per
+// piece instead of std::string's per-append bookkeeping (the 8-GPU page is
+// ≈950 lines / 100 KB).  Numbers go through std::to_chars (shortest round-trip
+// form), so the hot path never touches locale-dependent printf.  finish()
+// trims the string to what was written.
 struct W {
   std::string& o;
+  char* p = nullptr;
+  char* end = nullptr;
+  explicit W(std::string& s, size_t cap) : o(s) {
+    o.resize(cap);
+    p = &o[0];
+    end = p + o.size();
+  }
+  void grow(size_t n) {
+    const size_t used = static_cast<size_t>(p - o.data());
+    o.resize(std::max(o.size() * 2, used + n + 4096));
+    p = &o[0] + used;
+    end = &o[0] + o.size();
+  }
+  void put(const char* s, size_t n) {
+    if (static_cast<size_t>(end - p) < n) grow(n);
+    std::memcpy(p, s, n);
+    p += n;
+  }
+  void put(const std::string& s) { put(s.data(), s.size()); }
+  void put(const char* s) { put(s, std::strlen(s)); }
+  void put(char c) {
+    if (p == end) grow(1);
+    *p++ = c;
+  }
+  void finish() { o.resize(static_cast<size_t>(p - o.data())); }
   void num(double v) {
-    if (std::isnan(v)) { o += "NaN"; return; }
-    if (std::isinf(v)) { o += v > 0 ? "+Inf" : "-Inf"; return; }
-    char b[40];
-    auto r = std::to_chars(b, b + sizeof b, v);
-    o.append(b, r.ptr);
+    if (std::isnan(v)) { put("NaN", 3); return; }
+    if (std::isinf(v)) { put(v > 0 ? "+Inf" : "-Inf", 4); return; }
+    if (end - p < 40) grow(40);
+    p = std::to_chars(p, end, v).ptr;
   }
   void u64(uint64_t v) {
-    char b[24];
-    auto r = std::to_chars(b, b + sizeof b, v);
-    o.append(b, r.ptr);
+    if (end - p < 24) grow(24);
+    p = std::to_chars(p, end, v).ptr;
   }
   void head(const char* name, const char* type, const char* help) {
-    o += "# HELP "; o += name; o += ' '; o += help; o += "\n# TYPE "; o += name; o += ' '; o += type; o += '\n';
+    put("# HELP ", 7); put(name); put(' '); put(help); put("\n# TYPE ", 8); put(name); put(' '); put(type); put('\n');
   }
   // name{base,extra} value
+  void labels(const char* name, const std::string& base, const char* extra) {
+    put(name); put('{'); put(base);
+    if (extra && *extra) { put(','); put(extra); }
+    put("} ", 2);
+  }
   void line(const char* name, const std::string& base, const char* extra, double v) {
-    o += name; o += '{'; o += base;
-    if (extra && *extra) { o += ','; o += extra; }
-    o += "} "; num(v); o += '\n';
+    labels(name, base, extra); num(v); put('\n');
   }
   void line_u(const char* name, const std::string& base, const char* extra, uint64_t v) {
-    o += name; o += '{'; o += base;
-    if (extra && *extra) { o += ','; o += extra; }
-    o += "} "; u64(v); o += '\n';
+    labels(name, base, extra); u64(v); put('\n');
   }
 };
 
@@ -70,14 +101,53 @@ void kv(std::string& o, const char* k, const std::string& v, bool comma = true) 
   if (comma) o += ',';
   o += k; o += "=\""; append_label_value(o, v); o += '"';
 }
+// Integer-valued label without a std::to_string temporary.
+void kvi(std::string& o, const char* k, int64_t v) {
+  char b[24];
+  auto r = std::to_chars(b, b + sizeof b, v);
+  o += ','; o += k; o += "=\""; o.append(b, r.ptr); o += '"';
+}
+
+// `le` labels of the read-latency histogram and `counter` labels of the PMC
+// family never change: format them once.
+const std::vector<std::string>& hist_le_labels() {
+  static const std::vector<std::string> v = [] {
+    std::vector<std::string> out;
+    for (int b = 0; b <= kReadHistBuckets; ++b) {
+      std::string e = "le=\"";
+      if (b < kReadHistBuckets) {
+        char nb[32];
+        auto r = std::to_chars(nb, nb + sizeof nb, kReadHistBoundsUs[b] * 1e-6);
+        e.append(nb, r.ptr);
+      } else {
+        e += "+Inf";
+      }
+      e += '"';
+      out.push_back(std::move(e));
+    }
+    return out;
+  }();
+  return v;
+}
+const std::vector<std::string>& pmc_counter_labels() {
+  static const std::vector<std::string> v = [] {
+    std::vector<std::string> out;
+    for (int i = 0; i < kPmcCount; ++i) out.push_back(std::string("counter=\"") + pmc_counter_name(i) + '"');
+    return out;
+  }();
+  return v;
+}
+const char* const kXccLabels[kMaxXcc] = {"xcc=\"0\"", "xcc=\"1\"", "xcc=\"2\"", "xcc=\"3\"",
+                                         "xcc=\"4\"", "xcc=\"5\"", "xcc=\"6\"", "xcc=\"7\""};
+const char* const kLinkLabels[kMaxXgmi] = {"link=\"0\"", "link=\"1\"", "link=\"2\"", "link=\"3\"",
+                                           "link=\"4\"", "link=\"5\"", "link=\"6\"", "link=\"7\""};
 
 }  // namespace
 
 void Exporter::render(std::string& out) {
   const int64_t t0 = mono_ns();
   out.clear();
-  out.reserve(64 * 1024);
-  W w{out};
+  W w(out, last_render_bytes_.load(std::memory_order_relaxed) + 8192);
   Sampler& S = *sampler_;
   const int nd = S.device_count();
   const std::vector<int>& ids = S.sampled_devices();
@@ -147,37 +217,54 @@ void Exporter::render(std::string& out) {
     }
   }
 
-  // ---- device info / topology -------------------------------------------
-  w.head("amdgpu_device_info", "gauge", "Static device information (value is always 1)");
-  for (int d : ids) {
-    const DeviceInfo& in = be_->info(d);
-    std::string lb = dev_labels_[static_cast<size_t>(d)];
-    kv(lb, "bdf", in.bdf);
-    kv(lb, "gpu_type", cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override);
-    kv(lb, "kubernetes_io_hostname", node);
-    kv(lb, "serial", in.serial);
-    kv(lb, "market_name", in.market_name);
-    kv(lb, "gfx_target", in.gfx_target);
-    kv(lb, "numa_node", std::to_string(in.numa_node));
-    kv(lb, "num_cu", std::to_string(in.num_cu));
-    kv(lb, "num_xcc", std::to_string(in.num_xcc));
-    kv(lb, "kfd_gpu_id", std::to_string(in.kfd_gpu_id));
-    kv(lb, "hip_id", std::to_string(in.hip_id));
-    w.line("amdgpu_device_info", lb, nullptr, 1);
+  // ---- device info / topology (static: cached per node name) -------------
+  std::string lb;  // scratch label buffer, reused (no per-line allocation)
+  lb.reserve(512);
+  std::shared_ptr<const std::string> sblock;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (static_block_ && static_block_node_ == node) sblock = static_block_;
   }
-  if (!topo_.empty()) {
-    w.head("amdgpu_topology_link", "gauge", "Pairwise link between visible GPUs (1); labels carry type/hops/weight");
-    for (const TopoEdge& e : topo_) {
-      if (!sampled[static_cast<size_t>(e.src)]) continue;
-      std::string lb = dev_labels_[static_cast<size_t>(e.src)];
-      kv(lb, "peer_gpu", std::to_string(e.dst));
-      kv(lb, "peer_bdf", be_->info(e.dst).bdf);
-      kv(lb, "link_type", e.link_type == 2 ? "xgmi" : (e.link_type == 1 ? "pcie" : "other"));
-      kv(lb, "hops", std::to_string(e.hops));
-      kv(lb, "weight", std::to_string(e.weight));
-      w.line("amdgpu_topology_link", lb, nullptr, 1);
+  if (!sblock) {
+    std::string blk;
+    W b(blk, 16384);
+    b.head("amdgpu_device_info", "gauge", "Static device information (value is always 1)");
+    for (int d : ids) {
+      const DeviceInfo& in = be_->info(d);
+      lb.assign(dev_labels_[static_cast<size_t>(d)]);
+      kv(lb, "bdf", in.bdf);
+      kv(lb, "gpu_type", cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override);
+      kv(lb, "kubernetes_io_hostname", node);
+      kv(lb, "serial", in.serial);
+      kv(lb, "market_name", in.market_name);
+      kv(lb, "gfx_target", in.gfx_target);
+      kvi(lb, "numa_node", in.numa_node);
+      kvi(lb, "num_cu", in.num_cu);
+      kvi(lb, "num_xcc", in.num_xcc);
+      kvi(lb, "kfd_gpu_id", in.kfd_gpu_id);
+      kvi(lb, "hip_id", in.hip_id);
+      b.line("amdgpu_device_info", lb, nullptr, 1);
     }
+    if (!topo_.empty()) {
+      b.head("amdgpu_topology_link", "gauge", "Pairwise link between visible GPUs (1); labels carry type/hops/weight");
+      for (const TopoEdge& e : topo_) {
+        if (!sampled[static_cast<size_t>(e.src)]) continue;
+        lb.assign(dev_labels_[static_cast<size_t>(e.src)]);
+        kvi(lb, "peer_gpu", e.dst);
+        kv(lb, "peer_bdf", be_->info(e.dst).bdf);
+        kv(lb, "link_type", e.link_type == 2 ? "xgmi" : (e.link_type == 1 ? "pcie" : "other"));
+        kvi(lb, "hops", e.hops);
+        kvi(lb, "weight", e.weight);
+        b.line("amdgpu_topology_link", lb, nullptr, 1);
+      }
+    }
+    b.finish();
+    sblock = std::make_shared<const std::string>(std::move(blk));
+    std::lock_guard<std::mutex> g(mu_);
+    static_block_ = sblock;
+    static_block_node_ = node;
   }
+  w.put(*sblock);
 
   // ---- utilisation -------------------------------------------------------
   w.head("amdgpu_gfx_busy_percent", "gauge", "GFX-engine busy percent, time-weighted mean over the exporter window (PMFW accumulators)");
@@ -190,9 +277,7 @@ void Exporter::render(std::string& out) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFGfxBusyXcc)) continue;
     for (uint32_t c = 0; c < x.s.num_xcc && c < static_cast<uint32_t>(kMaxXcc); ++c) {
-      char e[24];
-      std::snprintf(e, sizeof e, "xcc=\"%u\"", c);
-      w.line("amdgpu_gfx_busy_xcc_percent", dev_labels_[d], e,
+      w.line("amdgpu_gfx_busy_xcc_percent", dev_labels_[d], kXccLabels[c],
              x.s.dt_s > 0 ? x.s.gfx_busy_xcc_window[c] : x.s.gfx_busy_xcc[c]);
     }
   }
@@ -246,9 +331,7 @@ void Exporter::render(std::string& out) {
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
     for (int l = 0; l < kMaxXgmi; ++l) {
       if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
-      char e[24];
-      std::snprintf(e, sizeof e, "link=\"%d\"", l);
-      w.line_u("amdgpu_xgmi_read_bytes_total", dev_labels_[d], e, x.s.xgmi_read_kb[l] * 1024ull);
+      w.line_u("amdgpu_xgmi_read_bytes_total", dev_labels_[d], kLinkLabels[l], x.s.xgmi_read_kb[l] * 1024ull);
     }
   }
   w.head("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link (PMFW accumulator)");
@@ -257,9 +340,7 @@ void Exporter::render(std::string& out) {
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
     for (int l = 0; l < kMaxXgmi; ++l) {
       if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
-      char e[24];
-      std::snprintf(e, sizeof e, "link=\"%d\"", l);
-      w.line_u("amdgpu_xgmi_write_bytes_total", dev_labels_[d], e, x.s.xgmi_write_kb[l] * 1024ull);
+      w.line_u("amdgpu_xgmi_write_bytes_total", dev_labels_[d], kLinkLabels[l], x.s.xgmi_write_kb[l] * 1024ull);
     }
   }
   w.head("amdgpu_xgmi_link_up", "gauge", "xGMI link status per port (1 up, 0 down)");
@@ -268,24 +349,37 @@ void Exporter::render(std::string& out) {
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
     for (int l = 0; l < kMaxXgmi; ++l) {
       if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
-      char e[24];
-      std::snprintf(e, sizeof e, "link=\"%d\"", l);
-      w.line("amdgpu_xgmi_link_up", dev_labels_[d], e, x.s.xgmi_link_up[l] ? 1 : 0);
+      w.line("amdgpu_xgmi_link_up", dev_labels_[d], kLinkLabels[l], x.s.xgmi_link_up[l] ? 1 : 0);
     }
   }
   w.head("amdgpu_xgmi_link_info", "gauge", "Per-link peer and speed (slow tier, value 1)");
   for (int d : ids) {
     auto links = S.state(d).get_links();
     if (!links) continue;
-    for (const LinkInfo& li : *links) {
-      std::string lb = dev_labels_[d];
-      kv(lb, "link", std::to_string(li.link));
-      kv(lb, "peer_bdf", li.peer_bdf);
-      kv(lb, "link_type", li.link_type == 2 ? "xgmi" : (li.link_type == 1 ? "pcie" : "other"));
-      kv(lb, "bit_rate_gbps", std::to_string(li.bit_rate_gbps));
-      kv(lb, "max_bandwidth_gbps", std::to_string(li.max_bw_gbps));
-      w.line("amdgpu_xgmi_link_info", lb, nullptr, 1);
+    std::shared_ptr<const std::string> lblock;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (link_blocks_.size() < static_cast<size_t>(nd)) link_blocks_.resize(static_cast<size_t>(nd));
+      if (link_blocks_[d].first == links) lblock = link_blocks_[d].second;
     }
+    if (!lblock) {  // the slow tier published a new link table: re-render this device's lines
+      std::string blk;
+      W b(blk, 4096);
+      for (const LinkInfo& li : *links) {
+        lb.assign(dev_labels_[d]);
+        kvi(lb, "link", li.link);
+        kv(lb, "peer_bdf", li.peer_bdf);
+        kv(lb, "link_type", li.link_type == 2 ? "xgmi" : (li.link_type == 1 ? "pcie" : "other"));
+        kvi(lb, "bit_rate_gbps", li.bit_rate_gbps);
+        kvi(lb, "max_bandwidth_gbps", li.max_bw_gbps);
+        b.line("amdgpu_xgmi_link_info", lb, nullptr, 1);
+      }
+      b.finish();
+      lblock = std::make_shared<const std::string>(std::move(blk));
+      std::lock_guard<std::mutex> g(mu_);
+      link_blocks_[d] = {links, lblock};
+    }
+    w.put(*lblock);
   }
   w.head("amdgpu_ecc_errors_total", "counter", "Accumulated ECC errors by type (slow tier)");
   for (int d : ids) {
@@ -311,12 +405,8 @@ void Exporter::render(std::string& out) {
     for (int d : ids) {
       const Snap& x = snaps[d];
       if (!x.pmc_have) continue;
-      for (int i = 0; i < kPmcCount; ++i) {
-        std::string e = "counter=\"";
-        e += pmc_counter_name(i);
-        e += '"';
-        w.line_u("amdgpu_pmc_total", dev_labels_[d], e.c_str(), x.p.value[i]);
-      }
+      for (int i = 0; i < kPmcCount; ++i)
+        w.line_u("amdgpu_pmc_total", dev_labels_[d], pmc_counter_labels()[static_cast<size_t>(i)].c_str(), x.p.value[i]);
     }
     w.head("amdgpu_mfma_util_percent", "gauge", "Matrix-core (MFMA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
@@ -331,39 +421,45 @@ void Exporter::render(std::string& out) {
   // ---- per-process attribution ------------------------------------------
   if (cfg_.per_process) {
     w.head("amdgpu_process_hbm_bytes", "gauge", "HBM bytes held by a process, attributed to its pod when known");
-    std::string tmp;
-    auto proc_labels = [&](int d, const ProcInfo& p) {
-      std::string lb = dev_labels_[d];
-      kv(lb, "pid", std::to_string(p.pid));
-      kv(lb, "process", p.name);
+    // Labels of every process line, built once per render and shared by the
+    // five per-process families.
+    std::vector<std::shared_ptr<const std::vector<ProcInfo>>> procs(static_cast<size_t>(nd));
+    static thread_local std::vector<std::string> plabels;
+    static thread_local std::vector<std::pair<int, const ProcInfo*>> plist;
+    plist.clear();
+    for (int d : ids) {
+      procs[d] = S.state(d).get_procs();
+      if (procs[d]) for (const ProcInfo& p : *procs[d]) plist.emplace_back(d, &p);
+    }
+    if (plabels.size() < plist.size()) plabels.resize(plist.size());
+    const std::string none;
+    for (size_t i = 0; i < plist.size(); ++i) {
+      const int d = plist[i].first;
+      const ProcInfo& p = *plist[i].second;
+      std::string& l = plabels[i];
+      l.assign(dev_labels_[d]);
+      kvi(l, "pid", p.pid);
+      kv(l, "process", p.name);
       const PidOwner* po = nullptr;
       if (pown) {
         auto it = pown->find(p.pid);
         if (it != pown->end()) po = &it->second;
       }
-      kv(lb, "pod", po ? po->pod : std::string());
-      kv(lb, "namespace", po ? po->ns : std::string());
-      kv(lb, "container", po ? po->container : std::string());
-      kv(lb, "pod_uid", po ? po->pod_uid : std::string());
-      return lb;
-    };
-    std::vector<std::shared_ptr<const std::vector<ProcInfo>>> procs(static_cast<size_t>(nd));
-    for (int d : ids) procs[d] = S.state(d).get_procs();
-    for (int d : ids)
-      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line_u("amdgpu_process_hbm_bytes", proc_labels(d, p), nullptr, p.vram_bytes);
+      kv(l, "pod", po ? po->pod : none);
+      kv(l, "namespace", po ? po->ns : none);
+      kv(l, "container", po ? po->container : none);
+      kv(l, "pod_uid", po ? po->pod_uid : none);
+    }
+    for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_hbm_bytes", plabels[i], nullptr, plist[i].second->vram_bytes);
     w.head("amdgpu_process_gtt_bytes", "gauge", "GTT (host-mapped) bytes held by a process");
-    for (int d : ids)
-      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line_u("amdgpu_process_gtt_bytes", proc_labels(d, p), nullptr, p.gtt_bytes);
+    for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_gtt_bytes", plabels[i], nullptr, plist[i].second->gtt_bytes);
     w.head("amdgpu_process_cu_occupancy", "gauge", "Compute units occupied by the process' waves");
-    for (int d : ids)
-      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line_u("amdgpu_process_cu_occupancy", proc_labels(d, p), nullptr, p.cu_occupancy);
+    for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_cu_occupancy", plabels[i], nullptr, plist[i].second->cu_occupancy);
     w.head("amdgpu_process_gfx_seconds_total", "counter", "GFX engine time consumed by the process (driver-reported; 0 where unsupported)");
-    for (int d : ids)
-      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line("amdgpu_process_gfx_seconds_total", proc_labels(d, p), nullptr, p.gfx_ns * 1e-9);
+    for (size_t i = 0; i < plist.size(); ++i) w.line("amdgpu_process_gfx_seconds_total", plabels[i], nullptr, plist[i].second->gfx_ns * 1e-9);
     w.head("amdgpu_process_cu_seconds_total", "counter",
            "Integral of the process' CU-occupancy share (occupied CUs / all CUs) over time; rate() = compute share");
-    for (int d : ids)
-      if (procs[d]) for (const ProcInfo& p : *procs[d]) w.line("amdgpu_process_cu_seconds_total", proc_labels(d, p), nullptr, p.cu_seconds);
+    for (size_t i = 0; i < plist.size(); ++i) w.line("amdgpu_process_cu_seconds_total", plabels[i], nullptr, plist[i].second->cu_seconds);
   }
 
   // ---- self metrics ------------------------------------------------------
@@ -399,16 +495,7 @@ void Exporter::render(std::string& out) {
     uint64_t cum = 0;
     for (int b = 0; b <= kReadHistBuckets; ++b) {
       cum += st.read_hist[b].load(std::memory_order_relaxed);
-      std::string e = "le=\"";
-      if (b < kReadHistBuckets) {
-        char nb[32];
-        auto r = std::to_chars(nb, nb + sizeof nb, kReadHistBoundsUs[b] * 1e-6);
-        e.append(nb, r.ptr);
-      } else {
-        e += "+Inf";
-      }
-      e += '"';
-      w.line_u("kgs_sample_read_seconds_bucket", dev_labels_[d], e.c_str(), cum);
+      w.line_u("kgs_sample_read_seconds_bucket", dev_labels_[d], hist_le_labels()[static_cast<size_t>(b)].c_str(), cum);
     }
     w.line("kgs_sample_read_seconds_sum", dev_labels_[d], nullptr, snaps[d].I.read_seconds);
     w.line_u("kgs_sample_read_seconds_count", dev_labels_[d], nullptr, cum);
@@ -430,7 +517,9 @@ void Exporter::render(std::string& out) {
     kv(lb, "sample_hz", std::to_string(S.config().hz));
     w.line("kgs_build_info", lb, nullptr, 1);
   }
-  if (extra) out += *extra;
+  if (extra) w.put(*extra);
+  w.finish();
+  last_render_bytes_.store(out.size(), std::memory_order_relaxed);
 
   const int64_t dt = mono_ns() - t0;
   scrapes.fetch_add(1);

@@ -218,6 +218,9 @@ void Sampler::run(int dev) {
         const bool reset = have_prev && (s.valid & kFFwTs) && (prev.valid & kFFwTs) && s.fw_ts < prev.fw_ts;
         if (distinct) {
           integrate(dev, have_prev && !reset ? &prev : nullptr, s, I);
+          s.cum_gfx_s = I.gfx_busy_seconds;
+          s.cum_umc_s = I.umc_busy_seconds;
+          s.cum_dt_s = I.sampled_seconds;
           s.seq = ++seq;
           ++I.distinct_samples;
           st.ring.push(s);
@@ -330,26 +333,45 @@ void Sampler::run(int dev) {
 
 bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, int& n) const {
   const DeviceState& st = *states_[dev];
-  double wsum = 0, g = 0, u = 0;
   n = 0;
-  st.ring.visit_recent([&](const GpuSample& s) {
-    if (s.dt_s <= 0 || s.gfx_busy_window_pct < 0) return true;
-    g += s.gfx_busy_window_pct * s.dt_s;
-    u += s.umc_busy_window_pct * s.dt_s;
-    wsum += s.dt_s;
-    ++n;
-    return wsum < window_s;
-  });
-  if (wsum <= 0) {
-    GpuSample s;
-    if (!st.latest.load(s)) return false;
-    gfx = s.gfx_busy_pct;
-    umc = s.umc_busy_pct;
-    n = 1;
-    return true;
+  GpuSample b, a, e;
+  if (st.ring.at(0, b) && b.cum_dt_s > 0) {
+    // Newest ring entry with at least window_s of firmware time after it: the
+    // window mean is the difference of the two running sums (O(log ring) loads).
+    const double want = b.cum_dt_s - window_s;
+    size_t lo = 1, hi = st.ring.available();
+    bool have = false;
+    while (lo < hi) {
+      const size_t mid = lo + (hi - lo) / 2;
+      if (!st.ring.at(mid, e)) {  // torn / overwritten under us: treat as too new
+        lo = mid + 1;
+        continue;
+      }
+      if (e.cum_dt_s <= want) {
+        a = e;
+        have = true;
+        hi = mid;
+      } else {
+        lo = mid + 1;
+      }
+    }
+    if (!have) {  // window longer than the history held: use the oldest entry
+      const size_t m = st.ring.available();
+      have = m > 1 && st.ring.at(m - 1, a);
+    }
+    if (have && b.cum_dt_s > a.cum_dt_s) {
+      const double dt = b.cum_dt_s - a.cum_dt_s;
+      gfx = 100.0 * (b.cum_gfx_s - a.cum_gfx_s) / dt;
+      umc = 100.0 * (b.cum_umc_s - a.cum_umc_s) / dt;
+      n = static_cast<int>(b.seq - a.seq);
+      return true;
+    }
   }
-  gfx = g / wsum;
-  umc = u / wsum;
+  GpuSample s;
+  if (!st.latest.load(s)) return false;
+  gfx = s.gfx_busy_pct;
+  umc = s.umc_busy_pct;
+  n = 1;
   return true;
 }
 

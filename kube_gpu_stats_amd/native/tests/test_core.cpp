@@ -8,10 +8,15 @@
 //  3. Sampler over the mock backend with fault injection, readers calling
 //     window_busy / window_pmc / integ concurrently, then stop().
 //  4. Recovery: a device that resets mid-run is re-opened and re-baselined.
+//  6. Exporter: concurrent /metrics renders and /counters streams while the
+//     samplers run at 2 kHz, the slow tier republishes link tables and the node
+//     name changes (render caches under the exporter mutex).
 //  5. PMFW table parser fuzz (ASAN build): random, truncated and mutated
 //     v1.8-shaped buffers, each in an exactly-sized heap block so any read past
 //     `len` is caught; the parser must reject or parse, never overrun.
 #include <atomic>
+#include <chrono>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
@@ -21,6 +26,7 @@
 #include <random>
 
 #include "kgs/backend.h"
+#include "kgs/exporter.h"
 #include "kgs/gpu_metrics.h"
 #include "kgs/pmc.h"
 #include "kgs/sampler.h"
@@ -242,7 +248,58 @@ static void test_parser_fuzz() {
   std::printf("parser fuzz ok (%d parsed, %d rejected)\n", parsed, rejected);
 }
 
+static void test_exporter_concurrent() {
+  ExporterConfig c;
+  c.backend = "mock";
+  c.mock.n_gpus = 4;
+  c.sampler.hz = 2000;
+  c.sampler.pin_numa = false;
+  c.sampler.proc_every = 20;
+  c.sampler.link_every = 50;  // new link table every 25 ms: the link-block cache churns
+  c.pmc_source = "mock";
+  c.port = -1;
+  c.node_name = "node-a";
+  Exporter ex(c);
+  CHECK(ex.init());
+  ex.start();
+  std::atomic<bool> stop{false};
+  std::atomic<int> renders{0}, streams{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 3; ++t)
+    th.emplace_back([&] {
+      std::string out;
+      while (!stop.load()) {
+        ex.render(out);
+        CHECK(out.find("amdgpu_topology_link{") != std::string::npos);
+        CHECK(out.find("amdgpu_xgmi_link_info{") != std::string::npos || renders.load() < 50);
+        CHECK(out.back() == '\n');
+        ++renders;
+      }
+    });
+  th.emplace_back([&] {
+    uint64_t since = 0;
+    while (!stop.load()) {
+      const std::string j = ex.counters_json(streams.load() % 4, 64, since);
+      CHECK(j.find("\"samples\":[") != std::string::npos);
+      ++streams;
+    }
+  });
+  for (int i = 0; i < 40; ++i) {
+    ex.set_node_name(i % 2 ? "node-b" : "node-a");
+    std::this_thread::sleep_for(std::chrono::milliseconds(25));
+  }
+  stop = true;
+  for (auto& t : th) t.join();
+  ex.stop();
+  std::string out;
+  ex.render(out);
+  CHECK(out.find("kubernetes_io_hostname=\"node-a\"") == std::string::npos);  // last rename: node-b
+  CHECK(renders.load() > 10 && streams.load() > 10);
+  std::printf("exporter concurrent ok (%d renders, %d streams)\n", renders.load(), streams.load());
+}
+
 int main() {
+  test_exporter_concurrent();
   test_parser_fuzz();
   test_seqlock();
   test_ring();
