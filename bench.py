@@ -18,7 +18,9 @@ One rank per GPU.  A *step* is one fixed block of synthetic load on every GPU
 and sampling rate are fixed).  A counter sample is one hardware-counter drain
 (GRBM/SQ/TCC values advance on every drain) when rocprofiler-sdk counting is
 available, else one distinct PMFW table (new firmware timestamp).  Overhead % =
-100 · (t_B / mean(t_A, t_C) − 1), same device, same process.
+100 · (t_B / mean(t_A, t_C) − 1), same device, same process.  Scrape latency is
+request → last body byte on a keep-alive connection, as a Prometheus server sees
+it (utils/scrape.py; body decoding happens after the clock stops).
 
 The exporter runs as its own process (as in production: DaemonSet vs workload),
 launched by local rank 0 over the PCI addresses of every local rank's GPU.
