@@ -94,3 +94,32 @@ def test_cli_exporter_mock_process():
         out, _ = p.communicate(timeout=30)
     stopped = json.loads(out.splitlines()[-1])
     assert stopped["event"] == "stopped" and stopped["integrals"][0]["reads"] > 0
+
+
+def test_cli_dmon_rows_and_counter_bursts(mock_exporter):
+    """`kgs dmon` against a live (mock) exporter: one row per GPU per poll, rates
+    from counter deltas, and min/max MFMA from the full-rate /counters stream."""
+    import io
+
+    from kube_gpu_stats_amd.reports import dmon
+
+    ex = mock_exporter(n_gpus=2, hz=1000, pmc_source="mock", proc_every=100, link_every=1000,
+                       mock={"util_base": 50, "util_amp": 30, "util_period_s": 0.5})
+    time.sleep(0.3)
+    buf = io.StringIO()
+    a = dmon.build_parser().parse_args([f"127.0.0.1:{ex.port}", "--interval", "0.2", "--count", "3", "--counters",
+                                        "--json"])
+    assert dmon.run(a, out=buf) == 0
+    rows = [json.loads(x) for x in buf.getvalue().splitlines()]
+    assert [r["gpu"] for r in rows] == ["0", "1"] * 3
+    last = rows[-2:]
+    for r in last:
+        assert 0 <= r["gfx"] <= 100 and r["hbm_gb"] > 0 and r["power_w"] > 0
+        assert r["energy_w"] is not None and r["energy_w"] > 0      # rate from the energy counter
+        assert r["drains"] >= 100                                    # ≈200 drains per 0.2 s at 1 kHz
+        assert 55 <= r["mfma_min"] <= r["mfma_max"] <= 65             # mock: MFMA busy 60 % of active cycles
+    buf = io.StringIO()
+    a = dmon.build_parser().parse_args([f"http://127.0.0.1:{ex.port}", "--interval", "0.1", "--count", "2"])
+    dmon.run(a, out=buf)
+    lines = buf.getvalue().splitlines()
+    assert lines[0].split()[:4] == ["GPU", "POD", "GFX%", "MFMA%"] and len(lines) == 1 + 2 * 2
