@@ -45,6 +45,7 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
     add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
     add_flag(ap, "window", 1.0, "gauge averaging window in seconds")
+    add_flag(ap, "hbm-full-bw", 8.41e12, "HBM bytes/s at 100%% UMC activity (MI355X calibration, profiles/umc_calib.md)")
     add_flag(ap, "bdfs", "", "comma-separated PCI addresses to sample (default all)")
     add_flag(ap, "pin-numa", True, "pin each sampler thread to its GPU's NUMA node")
     add_flag(ap, "per-process", True, "export per-process HBM/CU metrics")
@@ -75,6 +76,7 @@ def config_from_args(a) -> dict:
         "node_name": a.node_name,
         "gpu_type_override": a.gpu_type,
         "window_s": a.window,
+        "hbm_bytes_per_s_at_full_umc": a.hbm_full_bw,
         "per_process": a.per_process,
         "compat_unallocated": a.compat_unallocated,
         "control_http": a.control_http,

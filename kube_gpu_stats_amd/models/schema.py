@@ -50,6 +50,11 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller activity %, window mean."),
     F("amdgpu_gfx_busy_seconds_total", "counter", "∫ GFX busy fraction dt; rate() = exact mean utilisation."),
     F("amdgpu_umc_busy_seconds_total", "counter", "∫ UMC busy fraction dt."),
+    F("amdgpu_hbm_bandwidth_bytes_per_second", "gauge",
+      "HBM read+write bandwidth, window mean, from UMC activity × the MI355X calibration (1 % = 84.1 GB/s, "
+      "±0.6 % over stream loads of 3.1–5.5 TB/s; profiles/umc_calib.md)."),
+    F("amdgpu_hbm_bytes_total", "counter",
+      "HBM bytes moved (read+write), ∫ bandwidth dt from the UMC accumulators; rate() = bandwidth."),
     # ---- memory ------------------------------------------------------------------------------
     F("amdgpu_hbm_used_bytes", "gauge", "HBM3E bytes in use.", source="sysfs"),
     F("amdgpu_hbm_total_bytes", "gauge", "HBM3E capacity (288 GB on MI355X).", source="sysfs", tier="init"),

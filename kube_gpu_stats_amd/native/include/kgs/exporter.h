@@ -44,6 +44,9 @@ struct ExporterConfig {
   std::string node_name;
   std::string gpu_type_override;
   double window_s = 1.0;            // gauge averaging window
+  // HBM bytes/s at 100 % UMC (memory-controller) activity: the PMFW activity is
+  // linear in bandwidth, 11.89 %/(TB/s) on MI355X (profiles/umc_calib.md).
+  double hbm_bytes_per_s_at_full_umc = 8.41e12;
   bool per_process = true;
   bool compat_series = true;        // container_gpu_sm_util (reference contract)
   bool compat_unallocated = false;  // also emit it for GPUs with no pod (pod_name="")

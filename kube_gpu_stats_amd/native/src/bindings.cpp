@@ -54,6 +54,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);
   c.pmc_lib = get<std::string>(d, "pmc_lib", c.pmc_lib);
   c.pmc_pipeline = get<bool>(d, "pmc_pipeline", c.pmc_pipeline);
+  c.hbm_bytes_per_s_at_full_umc = get<double>(d, "hbm_bytes_per_s_at_full_umc", c.hbm_bytes_per_s_at_full_umc);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);
   c.node_name = get<std::string>(d, "node_name", c.node_name);

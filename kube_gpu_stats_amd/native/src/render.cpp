@@ -287,6 +287,12 @@ void Exporter::render(std::string& out) {
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_gfx_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.gfx_busy_seconds);
   w.head("amdgpu_umc_busy_seconds_total", "counter", "Integral of UMC busy fraction over firmware time");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_umc_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds);
+  const double full_bw = cfg_.hbm_bytes_per_s_at_full_umc;
+  w.head("amdgpu_hbm_bandwidth_bytes_per_second", "gauge",
+         "HBM read+write bandwidth over the exporter window, from UMC activity (MI355X calibration: 1 % = 84.1 GB/s)");
+  for (int d : ids) if (snaps[d].busy) w.line("amdgpu_hbm_bandwidth_bytes_per_second", dev_labels_[d], nullptr, snaps[d].u * 0.01 * full_bw);
+  w.head("amdgpu_hbm_bytes_total", "counter", "HBM bytes moved (read+write), integral of the UMC-derived bandwidth");
+  for (int d : ids) if (snaps[d].have) w.line("amdgpu_hbm_bytes_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds * full_bw);
 
   // ---- memory ------------------------------------------------------------
   w.head("amdgpu_hbm_used_bytes", "gauge", "HBM3E bytes in use");
