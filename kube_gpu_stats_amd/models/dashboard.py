@@ -69,9 +69,12 @@ def build() -> dict:
     y += 8
     add(_panel(0, "Per-XCC busy (die imbalance)",
                [(_dev("amdgpu_gfx_busy_xcc_percent"), "gpu{{gpu}} xcc{{xcc}}")], 0, y, unit="percent", maxv=100))
+    add(_panel(0, "HBM bandwidth (UMC activity, MI355X calibration)",
+               [(_dev("rate(amdgpu_hbm_bytes_total[1m])"), "gpu{{gpu}}")], 12, y, unit="Bps"))
+    y += 8
     add(_panel(0, "HBM controller busy / vector-memory busy",
                [(_dev("amdgpu_umc_busy_percent"), "umc gpu{{gpu}}"),
-                (_dev("amdgpu_vmem_busy_percent"), "vmem gpu{{gpu}}")], 12, y, unit="percent", maxv=100))
+                (_dev("amdgpu_vmem_busy_percent"), "vmem gpu{{gpu}}")], 0, y, unit="percent", maxv=100))
     y += 8
     add(_row(0, "Memory, power, thermals", y)); y += 1
     add(_panel(0, "HBM3E used", [(_dev("amdgpu_hbm_used_bytes"), "gpu{{gpu}}")], 0, y, w=8, unit="bytes"))

@@ -242,3 +242,39 @@ def test_counter_reader_exporter_process(torch_dev, mode):
         print(out[-3000:])  # "stopped" event: integrals + the reader's final pmc_info
         if err:
             print(err[-4000:])
+
+
+def test_hbm_bandwidth_estimate_tracks_stream_kernels(N, torch_dev):
+    """amdgpu_hbm_bandwidth_bytes_per_second (UMC activity × MI355X calibration)
+    agrees with the bytes a triad loop moves, and reads ~0 under a pure MFMA load."""
+    import torch
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.utils.scrape import parse_text
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=6 << 30)
+    ls()
+    torch.cuda.synchronize()
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 100, "proc_every": 0, "link_every": 0,
+                     "window_s": 1.0})
+    ex.start()
+    try:
+        t0 = time.time()
+        k = 0
+        while time.time() - t0 < 1.6:
+            ls.run_stream()
+            torch.cuda.synchronize()
+            k += 1
+        measured = ls.bytes * k / (time.time() - t0)
+        est = parse_text(ex.render())["amdgpu_hbm_bandwidth_bytes_per_second"][0][1]
+        t0 = time.time()
+        while time.time() - t0 < 1.6:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+        idle_est = parse_text(ex.render())["amdgpu_hbm_bandwidth_bytes_per_second"][0][1]
+    finally:
+        ex.stop()
+    print(json.dumps({"measured_Bps": measured, "estimate_Bps": est, "mfma_estimate_Bps": idle_est}))
+    assert measured > 3e12, measured
+    assert abs(est / measured - 1) < 0.10, (est, measured)
+    assert idle_est < 0.05e12, idle_est
