@@ -35,7 +35,8 @@ CATALOG: tuple[Family, ...] = (
       "pmfw+kubelet", "fast"),
     # ---- inventory / topology -------------------------------------------------------------
     F("amdgpu_device_info", "gauge", "Static device information (1).", extra=(
-        "bdf", "gpu_type", "kubernetes_io_hostname", "serial", "market_name", "gfx_target", "numa_node", "num_cu", "num_xcc", "kfd_gpu_id", "hip_id"),
+        "bdf", "gpu_type", "kubernetes_io_hostname", "serial", "market_name", "gfx_target", "numa_node", "num_cu", "num_xcc", "kfd_gpu_id", "hip_id",
+        "compute_partition", "memory_partition", "partition_id"),
       source="amdsmi", tier="init"),
     F("amdgpu_topology_link", "gauge", "Pairwise link between visible GPUs (1).",
       extra=("peer_gpu", "peer_bdf", "link_type", "hops", "weight"), source="amdsmi", tier="init"),

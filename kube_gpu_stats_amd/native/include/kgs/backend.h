@@ -30,6 +30,12 @@ struct DeviceInfo {
   int drm_card = -1;
   int hip_id = -1;
   std::string sysfs_dir;       // /sys/class/drm/cardN/device
+  // MI355X partitioning: compute SPX (all 8 XCDs one device) … CPX (one XCD per
+  // device), memory NPS1 / NPS2; each compute partition is its own device with a
+  // partition id.  "" / -1 where the driver does not report it.
+  std::string compute_partition;
+  std::string memory_partition;
+  int partition_id = -1;
 };
 
 struct ProcInfo {

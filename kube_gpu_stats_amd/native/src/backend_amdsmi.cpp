@@ -300,7 +300,12 @@ class AmdSmiBackend final : public Backend {
     if (amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS) {
       in.kfd_gpu_id = kfd.kfd_id;
       in.kfd_node = kfd.node_id == 0xFFFFFFFFu ? -1 : static_cast<int>(kfd.node_id);
+      in.partition_id = kfd.current_partition_id == 0xFFFFFFFFu ? -1 : static_cast<int>(kfd.current_partition_id);
     }
+    char part[64] = {};
+    if (amdsmi_get_gpu_compute_partition(h, part, sizeof part - 1) == AMDSMI_STATUS_SUCCESS) in.compute_partition = part;
+    std::memset(part, 0, sizeof part);
+    if (amdsmi_get_gpu_memory_partition(h, part, sizeof part - 1) == AMDSMI_STATUS_SUCCESS) in.memory_partition = part;
     amdsmi_enumeration_info_t en;
     std::memset(&en, 0, sizeof en);
     if (amdsmi_get_gpu_enumeration_info(h, &en) == AMDSMI_STATUS_SUCCESS) {

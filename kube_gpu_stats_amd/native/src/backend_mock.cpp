@@ -54,6 +54,9 @@ class MockBackend final : public Backend {
       in.kfd_node = 2 + d;
       in.drm_card = 8 * d;
       in.hip_id = d;
+      in.compute_partition = "SPX";
+      in.memory_partition = "NPS1";
+      in.partition_id = 0;
       infos_.push_back(in);
       rng_.push_back(cfg_.seed * 0x9E3779B97F4A7C15ull + static_cast<uint64_t>(d) + 1);
     }

@@ -125,6 +125,9 @@ py::dict info_dict(const DeviceInfo& in) {
   o["kfd_node"] = in.kfd_node;
   o["drm_card"] = in.drm_card;
   o["hip_id"] = in.hip_id;
+  o["compute_partition"] = in.compute_partition;
+  o["memory_partition"] = in.memory_partition;
+  o["partition_id"] = in.partition_id;
   o["sysfs_dir"] = in.sysfs_dir;
   return o;
 }

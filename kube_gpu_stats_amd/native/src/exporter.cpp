@@ -194,6 +194,11 @@ std::string Exporter::devices_json() {
          ",\"drm_card\":" + std::to_string(in.drm_card) + ",\"hip_id\":" + std::to_string(in.hip_id) +
          ",\"sysfs_dir\":";
     jstr(o, in.sysfs_dir);
+    o += ",\"compute_partition\":";
+    jstr(o, in.compute_partition);
+    o += ",\"memory_partition\":";
+    jstr(o, in.memory_partition);
+    o += ",\"partition_id\":" + std::to_string(in.partition_id);
     o += ",\"cpu_pinned\":" + std::to_string(sampler_ ? sampler_->state(d).cpu_pinned.load() : -1);
     o += '}';
   }

@@ -243,6 +243,9 @@ void Exporter::render(std::string& out) {
       kvi(lb, "num_xcc", in.num_xcc);
       kvi(lb, "kfd_gpu_id", in.kfd_gpu_id);
       kvi(lb, "hip_id", in.hip_id);
+      kv(lb, "compute_partition", in.compute_partition);
+      kv(lb, "memory_partition", in.memory_partition);
+      kvi(lb, "partition_id", in.partition_id);
       b.line("amdgpu_device_info", lb, nullptr, 1);
     }
     if (!topo_.empty()) {

@@ -36,6 +36,8 @@ def test_amdsmi_backend_inventory(N):
     assert d["num_cu"] == 256 and d["num_xcc"] == 8, d
     assert d["vram_total_bytes"] > 250e9, d  # 288 GB HBM3E
     assert d["sysfs_dir"].endswith("/device"), d
+    assert d["compute_partition"] in ("SPX", "DPX", "QPX", "CPX"), d  # MI355X compute partition modes
+    assert d["memory_partition"].startswith("NPS"), d
     ex.start()
     time.sleep(0.5)
     s = ex.snapshot(0)
