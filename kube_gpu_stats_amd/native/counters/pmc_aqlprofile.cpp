@@ -270,6 +270,50 @@ hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
   return HSA_STATUS_SUCCESS;
 }
 
+// Bring-up aid (KGS_AQL_DUMP=1): decode the PM4 indirect buffer behind a vendor
+// packet — type-3 opcode histogram plus the first packets verbatim — so the cost
+// of START / READ on the command processor can be reasoned about.
+void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+  uint32_t dw[13];
+  std::memcpy(dw, pkt.pm4_command, sizeof dw);
+  std::fprintf(stderr, "[aql-dump] %s pm4_command:", name);
+  for (int i = 0; i < 13; ++i) std::fprintf(stderr, " %08x", dw[i]);
+  std::fprintf(stderr, "\n");
+  const uint32_t op = (dw[0] >> 8) & 0xFF;
+  if (op != 0x3F && op != 0x33) {  // INDIRECT_BUFFER (0x3f) / INDIRECT_BUFFER_CONST (0x33)
+    std::fprintf(stderr, "[aql-dump] %s: first packet opcode 0x%02x is not an IB\n", name, op);
+    return;
+  }
+  const uint64_t addr = (static_cast<uint64_t>(dw[1]) | (static_cast<uint64_t>(dw[2] & 0xFFFF) << 32)) & ~3ull;
+  const uint32_t ndw = dw[3] & 0xFFFFF;
+  const uint32_t* ib = reinterpret_cast<const uint32_t*>(addr);
+  std::fprintf(stderr, "[aql-dump] %s IB at %#llx, %u dwords\n", name, static_cast<unsigned long long>(addr), ndw);
+  uint32_t hist[256] = {};
+  uint32_t i = 0, shown = 0;
+  while (i < ndw) {
+    const uint32_t h = ib[i];
+    const uint32_t type = h >> 30;
+    if (type == 2) { ++i; continue; }  // type-2 filler
+    if (type != 3) {
+      std::fprintf(stderr, "[aql-dump] %s: non type-3 header %08x at dword %u\n", name, h, i);
+      break;
+    }
+    const uint32_t opc = (h >> 8) & 0xFF, cnt = ((h >> 16) & 0x3FFF) + 2;
+    ++hist[opc];
+    if (shown < 48) {
+      std::fprintf(stderr, "[aql-dump] %s +%u op=0x%02x len=%u:", name, i, opc, cnt);
+      for (uint32_t k = 1; k < cnt && k < 8; ++k) std::fprintf(stderr, " %08x", ib[i + k]);
+      std::fprintf(stderr, "\n");
+      ++shown;
+    }
+    i += cnt;
+  }
+  std::fprintf(stderr, "[aql-dump] %s opcode histogram:", name);
+  for (int k = 0; k < 256; ++k)
+    if (hist[k]) std::fprintf(stderr, " 0x%02x:%u", k, hist[k]);
+  std::fprintf(stderr, "\n");
+}
+
 // Fold one completed READ's output buffer into a->vals.
 int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
   ++a->reads;
@@ -484,6 +528,11 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
         hsa_ven_amd_aqlprofile_stop(&p, &a->stop_pkt) != HSA_STATUS_SUCCESS) {
       set_err(err, errlen, "aqlprofile packet build: " + aql_error());
       return -1;
+    }
+    if (std::getenv("KGS_AQL_DUMP")) {
+      dump_packet("START", a->start_pkt);
+      dump_packet("READ", a->read_pkt);
+      dump_packet("STOP", a->stop_pkt);
     }
     if (std::getenv("KGS_AQL_DRY")) {  // packets built, nothing submitted (bring-up)
       const auto* c = static_cast<const uint8_t*>(a->cmd);

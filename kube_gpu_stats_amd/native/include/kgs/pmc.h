@@ -42,8 +42,19 @@ enum PmcReduce : int { kReduceSum = 0, kReduceMax = 1, kReduceAvg = 2 };
 const char* pmc_counter_name(int idx);
 int pmc_counter_reduce(int idx);
 
+// Counter sets (bits of PmcSample::mask).  Every READ costs the command
+// processor time that a dispatch-bound workload on the same GPU feels
+// (profiles/launch_overhead.md): the TA block alone is 512 instance reads of
+// the 560 in `full`, so the default `base` set drops it and keeps the READ to
+// 48 register reads (GRBM × 8 XCC, MFMA busy × 32 SE).
+constexpr uint32_t kPmcSetBase = (1u << kPmcGrbmCount) | (1u << kPmcGrbmGuiActive) | (1u << kPmcMfmaBusy);
+constexpr uint32_t kPmcSetFull = kPmcSetBase | (1u << kPmcTaBusy);
+// "base" | "full" → mask; 0 for an unknown name.
+uint32_t pmc_set_mask(const std::string& name);
+
 // Derived quantities over an interval between two cumulative samples.
 struct PmcRates {
+  bool have_vmem = false;        // TA counter in the set
   double gpu_active_pct = 0;     // 100 * ΔGUI_ACTIVE / ΔGRBM_COUNT
   double mfma_util_pct = 0;      // 100 * ΔMFMA_BUSY / (ΔGUI_ACTIVE * SIMD_NUM)  (rocprofv3 MfmaUtil)
   double vmem_busy_pct = 0;      // 100 * ΔTA_BUSY(avg) / ΔGUI_ACTIVE
@@ -66,6 +77,7 @@ struct MockPmcConfig {
   double clock_mhz = 2100;
   double mfma_frac = 0.6;       // fraction of active time the MFMA pipes are busy
   double vmem_frac = 0.3;       // fraction of active time the TA units are busy
+  uint32_t mask = kPmcSetFull;  // counters the mock "reads"
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,
@@ -79,6 +91,6 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 // previous tick, stamped with the time the CP executed it.
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
-                                                      bool pipelined, std::string& err);
+                                                      bool pipelined, uint32_t mask, std::string& err);
 
 }  // namespace kgs

@@ -97,6 +97,7 @@ struct PmcSample {
   int64_t mono_ns = 0;
   uint32_t read_ns = 0;
   uint32_t n = 0;
+  uint32_t mask = 0;           // bit i set: value[i] was read (PmcIndex)
   uint64_t value[kMaxPmc] = {};
 };
 static_assert(std::is_trivially_copyable<PmcSample>::value, "seqlock payload");

@@ -54,6 +54,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);
   c.pmc_lib = get<std::string>(d, "pmc_lib", c.pmc_lib);
   c.pmc_pipeline = get<bool>(d, "pmc_pipeline", c.pmc_pipeline);
+  c.pmc_set = get<std::string>(d, "pmc_set", c.pmc_set);
   c.hbm_bytes_per_s_at_full_umc = get<double>(d, "hbm_bytes_per_s_at_full_umc", c.hbm_bytes_per_s_at_full_umc);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);
@@ -212,7 +213,8 @@ class PyExporter {
     o["mono_ns"] = p.mono_ns;
     o["read_ns"] = p.read_ns;
     py::dict v;
-    for (int i = 0; i < kPmcCount; ++i) v[pmc_counter_name(i)] = p.value[i];
+    for (int i = 0; i < kPmcCount; ++i)
+      if (p.mask & (1u << i)) v[pmc_counter_name(i)] = p.value[i];
     o["values"] = v;
     return o;
   }
@@ -230,7 +232,7 @@ class PyExporter {
     if (ex_.sampler()->window_pmc(d, window_s, r)) {
       o["gpu_active_pct"] = r.gpu_active_pct;
       o["mfma_util_pct"] = r.mfma_util_pct;
-      o["vmem_busy_pct"] = r.vmem_busy_pct;
+      if (r.have_vmem) o["vmem_busy_pct"] = r.vmem_busy_pct;
       o["gpu_clock_mhz"] = r.gpu_clock_mhz;
       o["pmc_dt_s"] = r.dt_s;
     }

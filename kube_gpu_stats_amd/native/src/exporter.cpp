@@ -71,10 +71,17 @@ bool Exporter::init() {
   std::vector<int> devs = sc.devices;
   if (devs.empty())
     for (int d = 0; d < be_->device_count(); ++d) devs.push_back(d);
+  const uint32_t pmc_mask = pmc_set_mask(cfg_.pmc_set);
+  if (pmc_mask == 0) {
+    err_ = "unknown pmc_set '" + cfg_.pmc_set + "' (base | full)";
+    return false;
+  }
   if (cfg_.pmc_source == "mock") {
-    pmc_ = make_mock_counter_source(*be_, cfg_.mock, cfg_.mock_pmc);
+    MockPmcConfig mp = cfg_.mock_pmc;
+    mp.mask = pmc_mask;
+    pmc_ = make_mock_counter_source(*be_, cfg_.mock, mp);
   } else if (cfg_.pmc_source == "rocprofiler" || cfg_.pmc_source == "aqlprofile") {
-    pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, cfg_.pmc_pipeline, pmc_err_);
+    pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, cfg_.pmc_pipeline, pmc_mask, pmc_err_);
   } else if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
     err_ = "unknown pmc_source '" + cfg_.pmc_source + "'";
     return false;
@@ -298,7 +305,8 @@ std::string Exporter::counters_json(int dev, int n, uint64_t since) {
     o += "{\"seq\":" + std::to_string(p.seq) + ",\"mono_ns\":" + std::to_string(p.mono_ns) + ",\"v\":[";
     for (int k = 0; k < kPmcCount; ++k) {
       if (k) o += ',';
-      o += std::to_string(p.value[k]);
+      if (p.mask & (1u << k)) o += std::to_string(p.value[k]);
+      else o += "null";
     }
     o += ']';
     if (i + 1 < buf.size()) {
@@ -309,8 +317,10 @@ std::string Exporter::counters_json(int dev, int n, uint64_t since) {
       jnum(o, r.gpu_active_pct);
       o += ",\"mfma_util_pct\":";
       jnum(o, r.mfma_util_pct);
-      o += ",\"vmem_busy_pct\":";
-      jnum(o, r.vmem_busy_pct);
+      if (r.have_vmem) {
+        o += ",\"vmem_busy_pct\":";
+        jnum(o, r.vmem_busy_pct);
+      }
       o += ",\"gpu_clock_mhz\":";
       jnum(o, r.gpu_clock_mhz);
     }

@@ -26,6 +26,12 @@ int64_t mono_ns() {
 const char* pmc_counter_name(int idx) { return (idx >= 0 && idx < kPmcCount) ? kNames[idx] : "?"; }
 int pmc_counter_reduce(int idx) { return (idx >= 0 && idx < kPmcCount) ? kReduce[idx] : kReduceSum; }
 
+uint32_t pmc_set_mask(const std::string& name) {
+  if (name == "base" || name.empty()) return kPmcSetBase;
+  if (name == "full") return kPmcSetFull;
+  return 0;
+}
+
 PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
   PmcRates r;
   const double dt = (b.mono_ns - a.mono_ns) * 1e-9;
@@ -37,9 +43,10 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
   const double cnt = d(kPmcGrbmCount), act = d(kPmcGrbmGuiActive);
   const double cu = num_cu > 0 ? num_cu : 256;
   if (cnt > 0) r.gpu_active_pct = 100.0 * act / cnt;
+  r.have_vmem = (a.mask & b.mask & (1u << kPmcTaBusy)) != 0;
   if (act > 0) {
     r.mfma_util_pct = 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0);
-    r.vmem_busy_pct = 100.0 * d(kPmcTaBusy) / act;
+    if (r.have_vmem) r.vmem_busy_pct = 100.0 * d(kPmcTaBusy) / act;
   }
   r.gpu_clock_mhz = cnt / dt * 1e-6;
   return r;
@@ -63,6 +70,9 @@ class MockCounterSource final : public CounterSource {
     s.value[kPmcGrbmGuiActive] = static_cast<uint64_t>(clk * busy_s);
     s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
     s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac);
+    s.mask = c_.mask;
+    for (int i = 0; i < kPmcCount; ++i)
+      if (!(s.mask & (1u << i))) s.value[i] = 0;
     s.mono_ns = now;
     s.read_ns = 1000;
     return 0;
@@ -94,7 +104,7 @@ class DlCounterSource final : public CounterSource {
   }
 
   bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, bool pipelined,
-            std::string& err) {
+            uint32_t mask, std::string& err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!lib_) {
       err = std::string("dlopen failed: ") + dlerror();
@@ -118,15 +128,19 @@ class DlCounterSource final : public CounterSource {
     }
     const char* names[kPmcCount];
     int is_max[kPmcCount];
+    nsel_ = 0;
     for (int i = 0; i < kPmcCount; ++i) {
-      names[i] = kNames[i];
-      is_max[i] = kReduce[i];
+      if (!(mask & (1u << i))) continue;
+      names[nsel_] = kNames[i];
+      is_max[nsel_] = kReduce[i];
+      sel_[nsel_++] = i;
     }
+    mask_ = mask;
     int opened = 0;
     handles_.assign(static_cast<size_t>(be.device_count()), -1);
     for (int d : devices) {
       ebuf[0] = 0;
-      const int h = open_(be.info(d).kfd_gpu_id, names, is_max, kPmcCount, ebuf, sizeof ebuf);
+      const int h = open_(be.info(d).kfd_gpu_id, names, is_max, nsel_, ebuf, sizeof ebuf);
       handles_[static_cast<size_t>(d)] = h;
       if (h >= 0) ++opened;
       else err += "dev" + std::to_string(d) + ": " + ebuf + "; ";
@@ -152,9 +166,12 @@ class DlCounterSource final : public CounterSource {
     if (dev < 0 || dev >= static_cast<int>(handles_.size()) || handles_[dev] < 0) return -1;
     uint32_t rns = 0;
     int64_t ts = 0;
-    const int rc = sample_ts_ ? sample_ts_(handles_[dev], s.value, kPmcCount, &rns, &ts)
-                              : sample_(handles_[dev], s.value, kPmcCount, &rns);
+    uint64_t v[kPmcCount] = {};
+    const int rc = sample_ts_ ? sample_ts_(handles_[dev], v, nsel_, &rns, &ts)
+                              : sample_(handles_[dev], v, nsel_, &rns);
     if (rc != 0) return rc;
+    for (int k = 0; k < nsel_; ++k) s.value[sel_[k]] = v[k];  // reader order → PmcIndex
+    s.mask = mask_;
     s.n = kPmcCount;
     s.read_ns = rns;
     s.mono_ns = ts > 0 ? ts : mono_ns();  // when the CP read the counters (pipelined: previous call)
@@ -166,6 +183,9 @@ class DlCounterSource final : public CounterSource {
   open_fn open_ = nullptr;
   sample_fn sample_ = nullptr;
   sample_ts_fn sample_ts_ = nullptr;
+  int sel_[kPmcCount] = {};  // reader's counter k is PmcIndex sel_[k]
+  int nsel_ = 0;
+  uint32_t mask_ = 0;
   close_fn close_ = nullptr;
   info_fn info_ = nullptr;
   std::vector<int> handles_;
@@ -181,9 +201,9 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend&, const Mo
 
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
-                                                      bool pipelined, std::string& err) {
+                                                      bool pipelined, uint32_t mask, std::string& err) {
   auto s = std::make_unique<DlCounterSource>(name);
-  if (!s->load(lib_path, be, devices, pipelined, err)) return nullptr;
+  if (!s->load(lib_path, be, devices, pipelined, mask, err)) return nullptr;
   return s;
 }
 

@@ -415,14 +415,14 @@ void Exporter::render(std::string& out) {
       const Snap& x = snaps[d];
       if (!x.pmc_have) continue;
       for (int i = 0; i < kPmcCount; ++i)
-        w.line_u("amdgpu_pmc_total", dev_labels_[d], pmc_counter_labels()[static_cast<size_t>(i)].c_str(), x.p.value[i]);
+        if (x.p.mask & (1u << i)) w.line_u("amdgpu_pmc_total", dev_labels_[d], pmc_counter_labels()[static_cast<size_t>(i)].c_str(), x.p.value[i]);
     }
     w.head("amdgpu_mfma_util_percent", "gauge", "Matrix-core (MFMA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
     w.head("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active percent of clocks over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
     w.head("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy percent of active cycles over the window");
-    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
+    for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_vmem) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
     w.head("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_clock_effective_mhz", dev_labels_[d], nullptr, snaps[d].r.gpu_clock_mhz);
   }

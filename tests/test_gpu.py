@@ -176,14 +176,15 @@ def _proc_cpu_seconds(pid: int) -> float:
     return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
 
 
-@pytest.mark.parametrize("mode", ["aqlprofile", "aqlprofile-sync", "rocprofiler"])
+@pytest.mark.parametrize("mode", ["aqlprofile", "aqlprofile-full", "aqlprofile-sync", "rocprofiler"])
 def test_counter_reader_exporter_process(torch_dev, mode):
     """Exporter process with --pmc <reader> sees MFMA busy + HBM traffic of *this* process' kernels.
 
     aqlprofile (direct CP reads, the default) must also stay cheap on the host:
     the rocprofiler-sdk path keeps one HSA helper thread spinning (≈1 core).
-    ``aqlprofile`` runs pipelined READs (the default), ``aqlprofile-sync``
-    submits and waits per sample."""
+    ``aqlprofile`` runs pipelined READs of the base set (the default),
+    ``aqlprofile-full`` adds the TA block (vector-memory busy), ``aqlprofile-sync``
+    submits and waits per sample; the rocprofiler-sdk reader runs the full set."""
     import torch
 
     from kube_gpu_stats_amd.ops.load import LoadStep
@@ -196,6 +197,8 @@ def test_counter_reader_exporter_process(torch_dev, mode):
            "--pmc", reader, "--control-stdin", "--bdfs", bdf]
     if mode == "aqlprofile-sync":
         cmd.append("--no-pmc-pipeline")
+    full = mode in ("aqlprofile-full", "rocprofiler")
+    cmd += ["--pmc-set", "full" if full else "base"]
     proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                             text=True)
     try:
@@ -218,14 +221,17 @@ def test_counter_reader_exporter_process(torch_dev, mode):
             ls.run_stream()
             torch.cuda.synchronize()
         m2 = parse_text(sc.get())
-        vmem = [v for lb, v in m2["amdgpu_vmem_busy_percent"]]
+        vmem = [v for lb, v in m2.get("amdgpu_vmem_busy_percent", [])]
         clk = [v for lb, v in m2["amdgpu_gpu_clock_effective_mhz"]]
         pmc_n = [v for lb, v in m2["kgs_pmc_samples_total"]]
         cores = (_proc_cpu_seconds(proc.pid) - cpu0) / (time.time() - w0)
         print(json.dumps({"mode": mode, "mfma_util": mfma, "vmem_busy": vmem, "clock_mhz": clk,
                           "pmc_samples": pmc_n, "exporter_cpu_cores": cores, "pmc_info": ready.get("pmc_info")}))
         assert mfma[0] > 50, mfma
-        assert vmem[0] > 30, vmem     # triad keeps the TA units busy
+        if full:
+            assert vmem[0] > 30, vmem     # triad keeps the TA units busy
+        else:
+            assert not vmem, vmem         # base set: no TA block read
         assert 1000 < clk[0] < 2600, clk
         assert pmc_n[0] > 200
         if reader == "aqlprofile":

@@ -1,0 +1,117 @@
+"""GPU probe: does the counter tier slow a *launch-bound* workload?
+
+bench.py's load is made of long kernels (40 ms MFMA, 1 ms triads), which would
+hide any contention for the command processor: the exporter's READ packets are
+processed by the same CP firmware that dispatches the workload's kernels.  This
+runs back-to-back tiny kernels (a 64 KiB float4 copy, ≈2–3 µs each) and
+measures kernels/s with the exporter off, then on at several tick rates, then
+off again.  Writes gpurun_out/launch_overhead.json.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main() -> int:
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+
+    dev = torch.device("cuda", 0)
+    src = torch.rand(16384, device=dev)
+    dst = torch.empty_like(src)
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+    def rate(secs: float = 2.0, batch: int = 2000) -> float:
+        load.copy_f32(src, dst, nblocks=64)
+        torch.cuda.synchronize()
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            for _ in range(batch):
+                load.copy_f32(src, dst, nblocks=64)
+            torch.cuda.synchronize()
+            n += batch
+        return n / (time.perf_counter() - t0)
+
+    def graph_rate(secs: float = 2.0) -> float:
+        """Same kernels from a captured HIP graph (launch overhead on the host removed)."""
+        s = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            load.copy_f32(src, dst, nblocks=64, stream=s)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(500):
+                    load.copy_f32(src, dst, nblocks=64, stream=s)
+        torch.cuda.synchronize()
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            g.replay()
+            torch.cuda.synchronize()
+            n += 500
+        return n / (time.perf_counter() - t0)
+
+    def exporter(hz: float, pmc_set: str = "base", pmc: str = "aqlprofile"):
+        cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz",
+               str(hz), "--pmc", pmc, "--pmc-set", pmc_set, "--control-stdin", "--bdfs", bdf, "--proc-every",
+               str(max(1, int(hz // 10))), "--link-every", str(max(1, int(hz)))]
+        pr = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                              env=dict(os.environ, KGS_NO_BUILD="1"))
+        ready = json.loads(pr.stdout.readline())
+        assert ready.get("event") == "ready", ready
+        time.sleep(1.0)
+        return pr
+
+    rows = []
+
+    def measure(name, hz=None, pmc_set="base", pmc="aqlprofile"):
+        pr = exporter(hz, pmc_set, pmc) if hz else None
+        try:
+            r = {"phase": name, "hz": hz or 0, "pmc": pmc if hz else "", "set": pmc_set if hz else "",
+                 "eager_kernels_per_s": rate(), "graph_kernels_per_s": graph_rate()}
+        finally:
+            if pr is not None:
+                pr.stdin.write("quit\n")
+                pr.stdin.flush()
+                pr.communicate(timeout=30)
+        print(json.dumps(r), flush=True)
+        rows.append(r)
+
+    plan = [(h, "base", "aqlprofile") for h in (100, 1000, 8000)]
+    plan += [(h, "full", "aqlprofile") for h in (100, 1000)]
+    plan += [(0, "pmfw", "none")]  # PMFW/procs tiers only (no counter READs) at 1 kHz ticks
+    if len(sys.argv) > 1:
+        plan = [(float(x.split(":")[0]), x.split(":")[1], x.split(":")[2]) for x in sys.argv[1:]]
+    measure("off_a")
+    for hz, st, pmc in plan:
+        if pmc == "none":
+            measure("pmfw_only_1000", 1000, "base", "none")
+        else:
+            measure(f"{pmc}_{st}_{hz:g}", hz, st, pmc)
+    measure("off_b")
+    base_e = 0.5 * (rows[0]["eager_kernels_per_s"] + rows[-1]["eager_kernels_per_s"])
+    base_g = 0.5 * (rows[0]["graph_kernels_per_s"] + rows[-1]["graph_kernels_per_s"])
+    for r in rows:
+        r["eager_slowdown_pct"] = 100 * (base_e / r["eager_kernels_per_s"] - 1)
+        r["graph_slowdown_pct"] = 100 * (base_g / r["graph_kernels_per_s"] - 1)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "launch_overhead.json"), "w") as f:
+        json.dump(rows, f, indent=1)
+    for r in rows:
+        print(f"{r['phase']:>10}  eager {r['eager_kernels_per_s']:10.0f}/s ({r['eager_slowdown_pct']:+.2f} %)  "
+              f"graph {r['graph_kernels_per_s']:10.0f}/s ({r['graph_slowdown_pct']:+.2f} %)")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
