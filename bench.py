@@ -6,7 +6,9 @@ GPU-time overhead %, under synthetic gfx950 load (BASELINE.json "metric").
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 One rank per GPU.  A *step* is one fixed block of synthetic load on every GPU
-(an MFMA-bound bf16 kernel + HBM triads, ops/hip/load_kernels.hip).  Phases:
+(an MFMA-bound bf16 kernel + HBM triads, ops/hip/load_kernels.hip, + a HIP
+graph of 2000 tiny copies: the dispatch-bound part, where the counter reader's
+command-processor packets would cost the workload time).  Phases:
 
   A  K steps, no exporter running                       (baseline, untimed for the result line)
   B  K steps with the node exporter sampling every used GPU at --hz (PMFW table,
@@ -65,6 +67,9 @@ def parse_args(argv=None):
     ap.add_argument("--mfma-blocks", type=int, default=2048)
     ap.add_argument("--stream-gib", type=float, default=6.0)
     ap.add_argument("--triads", type=int, default=2)
+    ap.add_argument("--tiny-kernels", type=int, default=2000,
+                    help="dispatch-bound part of each step: a HIP graph of this many 64 KiB copies (≈1.7 µs each); "
+                    "it is where counter READs on the command processor would show up (0 = off)")
     ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per step when N > 1 (0 = off)")
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
@@ -86,6 +91,25 @@ class GpuLoad:
         self.ls = LoadStep(device=device, mfma_blocks=a.mfma_blocks, mfma_iters=a.mfma_iters,
                            stream_bytes=int(a.stream_gib * (1 << 30)))
         self.triads = a.triads
+        # Dispatch-bound component: back-to-back tiny kernels replayed from a HIP
+        # graph.  Long kernels hide command-processor contention; these expose it.
+        self.graph = None
+        self.tiny = int(a.tiny_kernels)
+        if self.tiny > 0:
+            from kube_gpu_stats_amd.ops import load as L
+
+            self.tsrc = torch.rand(16384, device=torch.device("cuda", device))
+            self.tdst = torch.empty_like(self.tsrc)
+            s = torch.cuda.Stream(device=device)
+            s.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(s):
+                L.copy_f32(self.tsrc, self.tdst, nblocks=64, stream=s)
+                s.synchronize()
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph, stream=s):
+                    for _ in range(self.tiny):
+                        L.copy_f32(self.tsrc, self.tdst, nblocks=64, stream=s)
+            torch.cuda.current_stream(device).wait_stream(s)
         # xGMI traffic for N > 1: one RCCL all-reduce per step over the
         # point-to-point xGMI mesh, so the exporter's per-link counters move.
         self.ar = None
@@ -96,6 +120,8 @@ class GpuLoad:
         self.ls.run_mfma()
         for _ in range(self.triads):
             self.ls.run_stream()
+        if self.graph is not None:
+            self.graph.replay()
         if self.ar is not None:
             import torch.distributed as dist
 
@@ -114,11 +140,18 @@ class GpuLoad:
         e[1].record()
         self.ls.run_stream()
         e[2].record()
+        if self.graph is not None:
+            self.graph.replay()
+        e[3].record()
         torch.cuda.synchronize()
         mfma_s = e[0].elapsed_time(e[1]) * 1e-3
         tri_s = e[1].elapsed_time(e[2]) * 1e-3
-        return {"mfma_ms": mfma_s * 1e3, "mfma_tflops": self.ls.flops / mfma_s / 1e12,
-                "triad_ms": tri_s * 1e3, "triad_tbps": self.ls.bytes / tri_s / 1e12}
+        out = {"mfma_ms": mfma_s * 1e3, "mfma_tflops": self.ls.flops / mfma_s / 1e12,
+               "triad_ms": tri_s * 1e3, "triad_tbps": self.ls.bytes / tri_s / 1e12}
+        if self.graph is not None:
+            g_s = e[2].elapsed_time(e[3]) * 1e-3
+            out.update({"tiny_graph_ms": g_s * 1e3, "tiny_kernels_per_s": self.tiny / g_s})
+        return out
 
     def pci_bdf(self, device: int) -> str:
         p = self.torch.cuda.get_device_properties(device)
@@ -432,7 +465,7 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (gfx950 MFMA bf16 + HBM triad load; random-init operands)" if not a.mock
+            "data": "synthetic (gfx950 MFMA bf16 + HBM triad + HIP-graph tiny-kernel load; random-init operands)" if not a.mock
             else "synthetic mock provider (CPU plumbing)",
             "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + rocprofiler PMC, "
                                 f"{a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",

@@ -39,6 +39,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pmc", "none", "hardware counters: none | aqlprofile (direct CP reads) | rocprofiler "
                                 "(rocprofiler-sdk device counting) | mock")
     add_flag(ap, "pmc-lib", "", "counter reader library (default: the in-tree one for --pmc)")
+    add_flag(ap, "pmc-lean", 2, "aqlprofile READ packet: 0 as built (per-XCC CS_PARTIAL_FLUSH + full cache "
+                                "invalidate), 1 no flushes, 2 no flushes + L2 writeback only (default), 3 no cache op")
     add_flag(ap, "pmc-set", "base", "counter set: base (GRBM clocks/active + MFMA busy, 48 register reads) | "
                                     "full (+ TA vector-memory busy, 560 reads: costs dispatch-bound workloads more)")
     add_flag(ap, "pmc-pipeline", True, "aqlprofile reader: overlap each counter READ's CP round trip with the "
@@ -74,6 +76,7 @@ def config_from_args(a) -> dict:
         "pmc_lib": a.pmc_lib or pmc_lib_path(a.pmc),
         "pmc_pipeline": a.pmc_pipeline,
         "pmc_set": a.pmc_set,
+        "pmc_lean": a.pmc_lean,
         "listen_addr": host or "0.0.0.0",
         "port": int(port),
         "node_name": a.node_name,

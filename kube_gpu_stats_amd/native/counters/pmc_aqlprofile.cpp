@@ -106,6 +106,7 @@ struct Agent {
   uint64_t ready_on_poll = 0, waited_on_poll = 0;    // pipelined: READ already done / had to wait
   int64_t host_ns = 0;                               // host time spent inside sample()
   uint32_t cmd_sz = 0, out_sz = 0;
+  int lean_changed = 0;                              // packets rewritten by lean_read_ib
   std::string err;
   uint64_t reads = 0, timeouts = 0;
   uint32_t last_results = 0;
@@ -274,8 +275,10 @@ hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
 // packet — type-3 opcode histogram plus the first packets verbatim — so the cost
 // of START / READ on the command processor can be reasoned about.
 void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+  // pm4_command[0] is the vendor format (AMD_AQL_FORMAT_PM4_IB); the 4-dword
+  // INDIRECT_BUFFER jump command follows it.
   uint32_t dw[13];
-  std::memcpy(dw, pkt.pm4_command, sizeof dw);
+  std::memcpy(dw, pkt.pm4_command + 1, sizeof dw);
   std::fprintf(stderr, "[aql-dump] %s pm4_command:", name);
   for (int i = 0; i < 13; ++i) std::fprintf(stderr, " %08x", dw[i]);
   std::fprintf(stderr, "\n");
@@ -300,7 +303,7 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
     }
     const uint32_t opc = (h >> 8) & 0xFF, cnt = ((h >> 16) & 0x3FFF) + 2;
     ++hist[opc];
-    if (shown < 48) {
+    if (shown < 16 || (opc != 0x40 && opc != 0x79 && shown < 200)) {
       std::fprintf(stderr, "[aql-dump] %s +%u op=0x%02x len=%u:", name, i, opc, cnt);
       for (uint32_t k = 1; k < cnt && k < 8; ++k) std::fprintf(stderr, " %08x", ib[i + k]);
       std::fprintf(stderr, "\n");
@@ -312,6 +315,53 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
   for (int k = 0; k < 256; ++k)
     if (hist[k]) std::fprintf(stderr, " 0x%02x:%u", k, hist[k]);
   std::fprintf(stderr, "\n");
+}
+
+// Lean READ.  aqlprofile's READ IB (decoded with KGS_AQL_DUMP=1,
+// profiles/read_packet.md) brackets the per-XCC register copies with a
+// CS_PARTIAL_FLUSH on every XCC and ends with an ACQUIRE_MEM that invalidates
+// the shader I$/K$, the vector L1 and the L2 (with writeback).  That is what a
+// per-dispatch profiler needs; a device-wide sampler of free-running busy
+// counters needs neither the flushes nor the invalidations, and both cost a
+// dispatch-bound workload on the same GPU (profiles/launch_overhead.md).
+// Modes: 0 = aqlprofile's packets as built; 1 = CS_PARTIAL_FLUSH → NOP;
+// 2 (default) = 1 + ACQUIRE_MEM reduced to the L2 writeback that publishes the
+// CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Returns packets changed.
+int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
+  if (mode <= 0) return 0;
+  uint32_t dw[4];
+  std::memcpy(dw, pkt.pm4_command + 1, sizeof dw);
+  if (((dw[0] >> 8) & 0xFF) != 0x3F) return -1;
+  const uint64_t addr = (static_cast<uint64_t>(dw[1]) | (static_cast<uint64_t>(dw[2] & 0xFFFF) << 32)) & ~3ull;
+  const uint32_t ndw = dw[3] & 0xFFFFF;
+  uint32_t* ib = reinterpret_cast<uint32_t*>(addr);
+  auto nop = [&](uint32_t at, uint32_t len) { ib[at] = (3u << 30) | ((len - 2) << 16) | (0x10u << 8); };
+  int changed = 0;
+  for (uint32_t i = 0; i < ndw;) {
+    const uint32_t h = ib[i];
+    if ((h >> 30) == 2) { ++i; continue; }
+    if ((h >> 30) != 3) return -2;
+    const uint32_t opc = (h >> 8) & 0xFF, len = ((h >> 16) & 0x3FFF) + 2;
+    if (opc == 0x46 && (ib[i + 1] & 0x3F) == 7) {  // EVENT_WRITE CS_PARTIAL_FLUSH
+      nop(i, len);
+      ++changed;
+    } else if (opc == 0x58 && mode == 2) {         // ACQUIRE_MEM: keep TC_WB_ACTION_ENA only
+      ib[i + 1] &= (1u << 18);
+      ++changed;
+    } else if (opc == 0x58 && mode == 3) {
+      nop(i, len);
+      ++changed;
+    }
+    i += len;
+  }
+  return changed;
+}
+
+int g_lean = 2;  // kgs_pmc_configure("lean", m) before kgs_pmc_open; KGS_AQL_LEAN overrides
+
+int lean_mode() {
+  const char* e = std::getenv("KGS_AQL_LEAN");
+  return e ? std::atoi(e) : g_lean;
 }
 
 // Fold one completed READ's output buffer into a->vals.
@@ -395,6 +445,7 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
       err = "aqlprofile pipeline packet build: " + aql_error();
       return false;
     }
+    if (lean_mode() > 0) lean_read_ib(a->pread[k], lean_mode());
   }
   return true;
 }
@@ -404,6 +455,16 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
 extern "C" {
 
 int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64_t* sample_ns);
+
+// Reader options, applied to counter sessions opened afterwards.  Keys: "lean"
+// (READ packet mode 0-3, see lean_read_ib).  0 = ok, -1 = unknown key / value.
+int kgs_pmc_configure(const char* key, int value) {
+  if (key && std::strcmp(key, "lean") == 0 && value >= 0 && value <= 3) {
+    g_lean = value;
+    return 0;
+  }
+  return -1;
+}
 
 int kgs_pmc_init(char* err, int errlen) {
   static std::once_flag once;
@@ -529,6 +590,11 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       set_err(err, errlen, "aqlprofile packet build: " + aql_error());
       return -1;
     }
+    if (lean_mode() > 0) {
+      const int ch = lean_read_ib(a->read_pkt, lean_mode());
+      KGS_DBG("lean READ mode %d: %d packets changed\n", lean_mode(), ch);
+      a->lean_changed = ch;
+    }
     if (std::getenv("KGS_AQL_DUMP")) {
       dump_packet("START", a->start_pkt);
       dump_packet("READ", a->read_pkt);
@@ -623,7 +689,8 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";pipelined=" + std::to_string(a->pipelined ? 1 : 0) + ";rtt_us=" + std::to_string(a->rtt_ns / 1000) +
                   ";reads=" + std::to_string(a->reads) + ";ready_on_poll=" + std::to_string(a->ready_on_poll) +
                   ";waited_on_poll=" + std::to_string(a->waited_on_poll) +
-                  ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads : 0.0);
+                  ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads : 0.0) +
+                  ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed);
   for (size_t k = 0; k < a->names.size(); ++k)
     o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
   if (!a->err.empty()) o += ";" + a->err;

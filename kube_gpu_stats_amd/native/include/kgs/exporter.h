@@ -40,6 +40,7 @@ struct ExporterConfig {
   std::string pmc_lib;              // path of libkgs_pmc.so
   bool pmc_pipeline = true;         // overlap counter READs with the tick sleep (aqlprofile reader)
   std::string pmc_set = "base";     // "base" (GRBM + MFMA busy) | "full" (+ TA busy: 10x the register reads)
+  int pmc_lean = 2;                 // READ packet: 0 as aqlprofile builds it .. 2 no flushes/invalidations (default)
   std::string listen_addr = "0.0.0.0";
   int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
   std::string node_name;

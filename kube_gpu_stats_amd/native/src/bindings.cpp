@@ -55,6 +55,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.pmc_lib = get<std::string>(d, "pmc_lib", c.pmc_lib);
   c.pmc_pipeline = get<bool>(d, "pmc_pipeline", c.pmc_pipeline);
   c.pmc_set = get<std::string>(d, "pmc_set", c.pmc_set);
+  c.pmc_lean = get<int>(d, "pmc_lean", c.pmc_lean);
   c.hbm_bytes_per_s_at_full_umc = get<double>(d, "hbm_bytes_per_s_at_full_umc", c.hbm_bytes_per_s_at_full_umc);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);

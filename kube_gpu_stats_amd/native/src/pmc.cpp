@@ -90,6 +90,7 @@ using open_fn = int (*)(uint64_t, const char* const*, const int*, int, char*, in
 using sample_fn = int (*)(int, uint64_t*, int, uint32_t*);
 using sample_ts_fn = int (*)(int, uint64_t*, int, uint32_t*, int64_t*);
 using pipelined_fn = int (*)(int, int, char*, int);
+using configure_fn = int (*)(const char*, int);
 using close_fn = void (*)(int);
 using info_fn = int (*)(int, char*, int);
 
@@ -104,7 +105,7 @@ class DlCounterSource final : public CounterSource {
   }
 
   bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, bool pipelined,
-            uint32_t mask, std::string& err) {
+            uint32_t mask, int lean, std::string& err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!lib_) {
       err = std::string("dlopen failed: ") + dlerror();
@@ -121,6 +122,8 @@ class DlCounterSource final : public CounterSource {
       err = path + ": missing kgs_pmc_* symbols";
       return false;
     }
+    auto configure = reinterpret_cast<configure_fn>(dlsym(lib_, "kgs_pmc_configure"));  // optional
+    if (configure && lean >= 0) configure("lean", lean);
     char ebuf[512] = {};
     if (init(ebuf, sizeof ebuf) != 0) {
       err = std::string("kgs_pmc_init: ") + ebuf;
@@ -201,9 +204,9 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend&, const Mo
 
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
-                                                      bool pipelined, uint32_t mask, std::string& err) {
+                                                      bool pipelined, uint32_t mask, int lean, std::string& err) {
   auto s = std::make_unique<DlCounterSource>(name);
-  if (!s->load(lib_path, be, devices, pipelined, mask, err)) return nullptr;
+  if (!s->load(lib_path, be, devices, pipelined, mask, lean, err)) return nullptr;
   return s;
 }
 

@@ -61,24 +61,48 @@ def main() -> int:
             n += 500
         return n / (time.perf_counter() - t0)
 
-    def exporter(hz: float, pmc_set: str = "base", pmc: str = "aqlprofile"):
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
+
+    def observe(port: int) -> dict:
+        """Counter sanity under a known load: MFMA util / clock over a 1.2 s MFMA loop."""
+        sc = Scraper("127.0.0.1", port)
+        m0 = parse_text(sc.scrape_once())
+        t0 = time.time()
+        while time.time() - t0 < 1.2:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+        m = parse_text(sc.scrape_once())
+        g = lambda mm, f: (mm.get(f) or [({}, None)])[0][1]  # noqa: E731
+        dt = time.time() - t0
+        return {"mfma_util_pct": g(m, "amdgpu_mfma_util_percent"), "clock_mhz": g(m, "amdgpu_gpu_clock_effective_mhz"),
+                "pmc_samples_per_s": ((g(m, "kgs_pmc_samples_total") or 0) - (g(m0, "kgs_pmc_samples_total") or 0)) / dt}
+
+    def exporter(hz: float, pmc_set: str = "base", pmc: str = "aqlprofile", lean: int = 0):
         cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz",
                str(hz), "--pmc", pmc, "--pmc-set", pmc_set, "--control-stdin", "--bdfs", bdf, "--proc-every",
                str(max(1, int(hz // 10))), "--link-every", str(max(1, int(hz)))]
         pr = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
-                              env=dict(os.environ, KGS_NO_BUILD="1"))
+                              env=dict(os.environ, KGS_NO_BUILD="1", KGS_AQL_LEAN=str(lean)))
         ready = json.loads(pr.stdout.readline())
         assert ready.get("event") == "ready", ready
+        pr.port = ready["port"]
+        pr.info = (ready.get("pmc_info") or [""])[0]
         time.sleep(1.0)
         return pr
 
     rows = []
 
-    def measure(name, hz=None, pmc_set="base", pmc="aqlprofile"):
-        pr = exporter(hz, pmc_set, pmc) if hz else None
+    def measure(name, hz=None, pmc_set="base", pmc="aqlprofile", lean=0):
+        pr = exporter(hz, pmc_set, pmc, lean) if hz else None
         try:
-            r = {"phase": name, "hz": hz or 0, "pmc": pmc if hz else "", "set": pmc_set if hz else "",
+            r = {"phase": name, "hz": hz or 0, "pmc": pmc if hz else "", "set": pmc_set if hz else "", "lean": lean,
                  "eager_kernels_per_s": rate(), "graph_kernels_per_s": graph_rate()}
+            if pr is not None and pmc != "none":
+                r["observed"] = observe(pr.port)
+                r["pmc_info"] = pr.info[:400]
         finally:
             if pr is not None:
                 pr.stdin.write("quit\n")
@@ -87,17 +111,14 @@ def main() -> int:
         print(json.dumps(r), flush=True)
         rows.append(r)
 
-    plan = [(h, "base", "aqlprofile") for h in (100, 1000, 8000)]
-    plan += [(h, "full", "aqlprofile") for h in (100, 1000)]
-    plan += [(0, "pmfw", "none")]  # PMFW/procs tiers only (no counter READs) at 1 kHz ticks
-    if len(sys.argv) > 1:
-        plan = [(float(x.split(":")[0]), x.split(":")[1], x.split(":")[2]) for x in sys.argv[1:]]
+    # spec hz:set:reader[:lean]
+    specs = sys.argv[1:] or ["100:base:aqlprofile", "1000:base:aqlprofile", "8000:base:aqlprofile",
+                             "100:full:aqlprofile", "1000:full:aqlprofile", "1000:base:none"]
     measure("off_a")
-    for hz, st, pmc in plan:
-        if pmc == "none":
-            measure("pmfw_only_1000", 1000, "base", "none")
-        else:
-            measure(f"{pmc}_{st}_{hz:g}", hz, st, pmc)
+    for spec in specs:
+        f = spec.split(":")
+        hz, st, pmc, lean = float(f[0]), f[1], f[2], int(f[3]) if len(f) > 3 else 0
+        measure(f"{pmc}_{st}_{hz:g}_l{lean}", hz, st, pmc, lean)
     measure("off_b")
     base_e = 0.5 * (rows[0]["eager_kernels_per_s"] + rows[-1]["eager_kernels_per_s"])
     base_g = 0.5 * (rows[0]["graph_kernels_per_s"] + rows[-1]["graph_kernels_per_s"])
@@ -108,7 +129,7 @@ def main() -> int:
     with open(os.path.join(REPO, "gpurun_out", "launch_overhead.json"), "w") as f:
         json.dump(rows, f, indent=1)
     for r in rows:
-        print(f"{r['phase']:>10}  eager {r['eager_kernels_per_s']:10.0f}/s ({r['eager_slowdown_pct']:+.2f} %)  "
+        print(f"{r['phase']:>24}  {json.dumps(r.get('observed', {}))}  eager {r['eager_kernels_per_s']:10.0f}/s ({r['eager_slowdown_pct']:+.2f} %)  "
               f"graph {r['graph_kernels_per_s']:10.0f}/s ({r['graph_slowdown_pct']:+.2f} %)")
     return 0
 

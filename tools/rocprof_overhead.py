@@ -29,12 +29,13 @@ def main():
     ap.add_argument("--warmup", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--triads", type=int, default=2)
+    ap.add_argument("--tiny", type=int, default=2000, help="tiny copy kernels per step (bench --tiny-kernels)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     path = find_trace(a.dir)
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    by = {"mfma": [], "triad": []}
+    by = {"mfma": [], "triad": [], "copy": []}
     for r in rows:
         name = r["Kernel_Name"]
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3  # µs
@@ -42,10 +43,15 @@ def main():
             by["mfma"].append(dur)
         elif "triad_f32_kernel" in name:
             by["triad"].append(dur)
+        elif "copy_f32_kernel" in name:
+            by["copy"].append(dur)
     res = {"trace": os.path.relpath(path), "kernels_total": len(rows)}
-    for kind, per_step in (("mfma", 1), ("triad", a.triads)):
+    kinds = [("mfma", 1), ("triad", a.triads)] + ([("copy", a.tiny)] if a.tiny else [])
+    for kind, per_step in kinds:
         xs = by[kind]
-        skip = a.warmup * per_step + 1  # the calibration step launches one of each
+        # the calibration step launches one mfma + one triad (+ one graph replay);
+        # the tiny-kernel graph is preceded by one eager warm-up copy
+        skip = a.warmup * per_step + (1 if kind != "copy" else 1 + per_step)
         n = a.steps * per_step
         ph = {"A_off": xs[skip:skip + n], "B_on": xs[skip + n:skip + 2 * n], "C_off": xs[skip + 2 * n:skip + 3 * n]}
         if any(len(v) != n for v in ph.values()):
@@ -64,7 +70,7 @@ def main():
                  "B (exporter on), C (exporter off).", "",
                  "| kernel | launches/phase | A off mean µs | B on mean µs | C off mean µs | overhead % (B vs mean(A,C)) |",
                  "|---|---|---|---|---|---|"]
-        for kind in ("mfma", "triad"):
+        for kind, _ in kinds:
             r = res[kind]
             if "error" in r:
                 lines.append(f"| {kind} | {r['error']} | | | | |")
