@@ -62,6 +62,8 @@ def parse_args(argv=None):
                     help="aqlprofile reader: pipelined READs (1) or submit-and-wait per sample (0)")
     ap.add_argument("--pmc-set", default="base", choices=["base", "full"],
                     help="counter set: base (GRBM + MFMA busy) or full (+ TA busy, 10x the CP register reads)")
+    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
+                    help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=10.0)
     ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per step on MI355X")
     ap.add_argument("--mfma-blocks", type=int, default=2048)
@@ -239,7 +241,8 @@ class ExporterProc:
             cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock"]
         else:
             pmc = AUTO_PMC if a.pmc == "auto" else a.pmc
-            cmd += ["--pmc", pmc, "--pmc-pipeline" if a.pmc_pipeline else "--no-pmc-pipeline", "--pmc-set", a.pmc_set]
+            cmd += ["--pmc", pmc, "--pmc-pipeline" if a.pmc_pipeline else "--no-pmc-pipeline", "--pmc-set", a.pmc_set,
+                    "--pmc-lean", str(a.pmc_lean)]
         env = dict(os.environ)
         env.setdefault("KGS_NO_BUILD", "1")
         env.setdefault("PYTHONFAULTHANDLER", "1")  # a native fault leaves a trace in the exporter log
