@@ -85,6 +85,15 @@ CATALOG: tuple[Family, ...] = (
       source="rocprofiler", tier="pmc"),
     F("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT (window).",
       source="rocprofiler", tier="pmc"),
+    F("amdgpu_mfma_util_xcc_percent", "gauge",
+      "Matrix-core busy % of one XCD's active SIMD cycles (window; aqlprofile reader, results placed on XCDs in "
+      "the READ buffer's XCC-major order, verified against an XCC-gated load).  An XCD left idle while others "
+      "saturate is a workgroup→XCD mapping problem, invisible in the device-wide gauges.",
+      extra=("xcc",), source="rocprofiler", tier="pmc"),
+    F("amdgpu_gpu_active_xcc_percent", "gauge",
+      "GRBM GUI-active % of clocks of one XCD (window): a dispatch is in flight on it.  A chip-wide kernel keeps "
+      "every XCD active, even one with no waves; the MFMA split shows where waves run.",
+      extra=("xcc",), source="rocprofiler", tier="pmc"),
     # ---- per process -------------------------------------------------------------------------
     F("amdgpu_process_hbm_bytes", "gauge", "HBM bytes held by a process.",
       extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),

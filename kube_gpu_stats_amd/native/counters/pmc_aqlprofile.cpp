@@ -112,7 +112,46 @@ struct Agent {
   uint32_t last_results = 0;
   std::vector<uint32_t> instances;                   // results folded per counter (last read)
   std::vector<double> vals;
+  // Per-XCD fold.  Each result's XCD coordinate is resolved once, on the first
+  // READ, with hsa_ven_amd_aqlprofile_iterate_event_coord and cached by the
+  // result's position in the output buffer (fixed by the event list, the same in
+  // every READ slot).  -1 = no XCD coordinate.
+  std::vector<int> res_xcd;
+  std::vector<std::pair<int, uint32_t>> res_slot;     // result ordinal → (counter, index among its results)
+  bool res_xcd_done = false;
+  const char* xcd_from = "none";                     // "coord" | "order" | "none"
+  uint32_t num_xcc = 1;                              // HSA_AMD_AGENT_INFO_NUM_XCC
+  std::vector<double> vals_xcd;                      // [counter * kMaxXcd + xcd]
+  std::vector<uint32_t> xcd_seen;                    // per counter: bit x = XCD x contributed
 };
+
+constexpr int kMaxXcd = 8;
+int g_xcd_coord_id = -1;  // id of the "XCD" event coordinate (hsa_ven_amd_aqlprofile_iterate_event_ids)
+
+hsa_status_t on_coord_id(int id, const char* name) {
+  if (name && std::strcmp(name, "XCD") == 0) g_xcd_coord_id = id;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t on_coord(int, int id, int, int coordinate, const char*, void* ud) {
+  if (id == g_xcd_coord_id) *static_cast<int*>(ud) = coordinate;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t on_coord_print(int pos, int id, int extent, int coordinate, const char* name, void*) {
+  std::fprintf(stderr, " %s(%d)=%d/%d@%d", name ? name : "?", id, coordinate, extent, pos);
+  return HSA_STATUS_SUCCESS;
+}
+
+// Bring-up aid (KGS_AQL_DUMP_RESULTS=<n>): every result of the n-th READ with its
+// sample id and every event coordinate aqlprofile reports for it.
+int64_t dump_results_at() {
+  static const int64_t n = [] {
+    const char* e = std::getenv("KGS_AQL_DUMP_RESULTS");
+    return e ? std::atoll(e) : -1LL;
+  }();
+  return n;
+}
 
 std::mutex g_mu;
 std::vector<Agent*> g_agents;
@@ -172,6 +211,9 @@ hsa_status_t on_agent(hsa_agent_t agent, void*) {
     a->agent = agent;
     hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DRIVER_UID), &a->gpu_id);
     hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &a->cu_count);
+    if (hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_NUM_XCC), &a->num_xcc) !=
+            HSA_STATUS_SUCCESS || a->num_xcc == 0)
+      a->num_xcc = 1;
     g_agents.push_back(a);
   }
   return HSA_STATUS_SUCCESS;
@@ -255,17 +297,39 @@ hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
   if (type != HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA) return HSA_STATUS_SUCCESS;
   Fold* f = static_cast<Fold*>(ud);
   Agent* a = f->a;
-  ++f->n;
+  const uint32_t ord = f->n++;
+  if (!a->res_xcd_done) {
+    int x = -1;
+    if (g_xcd_coord_id >= 0)
+      hsa_ven_amd_aqlprofile_iterate_event_coord(a->agent, d->pmc_data.event, d->sample_id, on_coord, &x);
+    a->res_xcd.push_back(x);
+    a->res_slot.emplace_back(-1, 0);
+  }
+  if (static_cast<int64_t>(a->reads) == dump_results_at()) {
+    std::fprintf(stderr, "[aql-res] ord=%u sid=%u block=%d idx=%u ev=%u val=%llu coords:", ord, d->sample_id,
+                 static_cast<int>(d->pmc_data.event.block_name), d->pmc_data.event.block_index,
+                 d->pmc_data.event.counter_id, static_cast<unsigned long long>(d->pmc_data.result));
+    hsa_ven_amd_aqlprofile_iterate_event_coord(a->agent, d->pmc_data.event, d->sample_id, on_coord_print, nullptr);
+    std::fprintf(stderr, "\n");
+  }
   for (size_t e = 0; e < a->events.size(); ++e) {
     const auto& ev = a->events[e];
     if (ev.block_name != d->pmc_data.event.block_name || ev.block_index != d->pmc_data.event.block_index ||
         ev.counter_id != d->pmc_data.event.counter_id)
       continue;
-    const int k = a->ev_counter[e];
+    const size_t k = static_cast<size_t>(a->ev_counter[e]);
     const double v = static_cast<double>(d->pmc_data.result);
-    if (a->reduce[static_cast<size_t>(k)] == 1) a->vals[static_cast<size_t>(k)] = std::max(a->vals[static_cast<size_t>(k)], v);
-    else a->vals[static_cast<size_t>(k)] += v;
-    a->instances[static_cast<size_t>(k)]++;
+    const bool is_max = a->reduce[k] == 1;
+    if (is_max) a->vals[k] = std::max(a->vals[k], v);
+    else a->vals[k] += v;
+    if (!a->res_xcd_done) a->res_slot.back() = {static_cast<int>(k), a->instances[k]};
+    a->instances[k]++;
+    const int x = ord < a->res_xcd.size() ? a->res_xcd[ord] : -1;
+    if (x >= 0 && x < kMaxXcd) {  // within one XCD the same reduction, except mean → sum
+      double& vx = a->vals_xcd[k * kMaxXcd + static_cast<size_t>(x)];
+      vx = is_max ? std::max(vx, v) : vx + v;
+      a->xcd_seen[k] |= 1u << x;
+    }
     break;
   }
   return HSA_STATUS_SUCCESS;
@@ -364,13 +428,55 @@ int lean_mode() {
   return e ? std::atoi(e) : g_lean;
 }
 
+// Decide each result's XCD after the first fold.  Preferred: aqlprofile's XCD
+// event coordinate, when it spreads the results over every XCC.  Fallback: the
+// output order, XCC-major — a counter's i-th of m results sits on XCD
+// i·num_xcc/m.  On MI355X / ROCm 7.2 the coordinate reads XCD 0 for all 48
+// results, and the buffer holds 8 XCC-major groups of [GRBM_COUNT,
+// GRBM_GUI_ACTIVE, SQ MFMA busy × 4 SEs]; an MFMA load gated on HW_REG_XCC_ID
+// to XCDs {0, 2} shows up on exactly those two under the order placement
+// (profiles/r1/xcd/README.md, tests/test_gpu.py::test_per_xcd_counters_follow_xcc_gated_load).
+void place_xcds(Agent* a) {
+  uint32_t seen = 0;
+  for (int x : a->res_xcd)
+    if (x >= 0 && x < kMaxXcd) seen |= 1u << x;
+  const uint32_t nx = a->num_xcc;
+  if (nx > 1 && nx <= static_cast<uint32_t>(kMaxXcd) && static_cast<uint32_t>(__builtin_popcount(seen)) == nx) {
+    a->xcd_from = "coord";
+    return;
+  }
+  a->xcd_from = "none";
+  if (nx < 2 || nx > static_cast<uint32_t>(kMaxXcd)) {
+    a->res_xcd.assign(a->res_xcd.size(), -1);
+    return;
+  }
+  for (size_t k = 0; k < a->instances.size(); ++k)
+    if (a->instances[k] % nx != 0) {  // not a whole number of results per XCC: no guess
+      a->res_xcd.assign(a->res_xcd.size(), -1);
+      return;
+    }
+  for (size_t o = 0; o < a->res_slot.size() && o < a->res_xcd.size(); ++o) {
+    const auto [k, i] = a->res_slot[o];
+    a->res_xcd[o] = k < 0 ? -1 : static_cast<int>(i * nx / a->instances[static_cast<size_t>(k)]);
+  }
+  a->xcd_from = "order";
+}
+
 // Fold one completed READ's output buffer into a->vals.
 int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
   ++a->reads;
   a->vals.assign(a->names.size(), 0.0);
   a->instances.assign(a->names.size(), 0);
+  a->vals_xcd.assign(a->names.size() * kMaxXcd, 0.0);
+  a->xcd_seen.assign(a->names.size(), 0);
+  if (!a->res_xcd_done) {  // a failed first fold leaves no partial table
+    a->res_xcd.clear();
+    a->res_slot.clear();
+  }
   Fold f{a};
   if (hsa_ven_amd_aqlprofile_iterate_data(prof, on_data, &f) != HSA_STATUS_SUCCESS) return -3;
+  if (!a->res_xcd_done) place_xcds(a);  // the first fold's per-XCD values are never returned (open's READ)
+  a->res_xcd_done = true;
   a->last_results = f.n;
   // Mean of a per-CU block (TA/TD/TCP): the packets read every instance slot of
   // every SE (16 per SE on gfx950), but only cu_count of them exist (8 per SE
@@ -476,6 +582,7 @@ int kgs_pmc_init(char* err, int errlen) {
       return;
     }
     hsa_iterate_agents(on_agent, nullptr);
+    hsa_ven_amd_aqlprofile_iterate_event_ids(on_coord_id);  // finds the "XCD" coordinate for the per-XCD fold
     if (!g_have_pool) {
       g_init_err = "no fine-grained host memory pool";
       rc = -3;
@@ -658,6 +765,24 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
   return 0;
 }
 
+// Per-XCD values of reader counter `counter` from the last completed sample,
+// cumulative like kgs_pmc_sample (max over the XCD's instances for max-reduced
+// counters, sum otherwise).  Returns the number of XCDs written, 0..n-1 all
+// present, or 0 when the results carry no XCD coordinate.  Call from the thread
+// that samples the handle, after kgs_pmc_sample[_ts].
+int kgs_pmc_sample_xcd(int handle, int counter, uint64_t* out, int max_xcd) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size() || !out) return -1;
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  if (counter < 0 || static_cast<size_t>(counter) >= a->xcd_seen.size()) return -1;
+  const uint32_t seen = a->xcd_seen[static_cast<size_t>(counter)];
+  int n = 0;
+  while (n < max_xcd && n < kMaxXcd && ((seen >> n) & 1u)) {
+    out[n] = static_cast<uint64_t>(a->vals_xcd[static_cast<size_t>(counter) * kMaxXcd + static_cast<size_t>(n)]);
+    ++n;
+  }
+  return (seen >> n) ? 0 : n;  // a gap (or more XCDs than the caller holds): do not guess
+}
+
 // Switch a handle between synchronous READs (submit + wait every sample) and
 // pipelined READs (collect the previous one, submit the next).  0 = ok.
 int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
@@ -690,7 +815,9 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";reads=" + std::to_string(a->reads) + ";ready_on_poll=" + std::to_string(a->ready_on_poll) +
                   ";waited_on_poll=" + std::to_string(a->waited_on_poll) +
                   ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads : 0.0) +
-                  ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed);
+                  ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed) +
+                  ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
+                  a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc);
   for (size_t k = 0; k < a->names.size(); ++k)
     o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
   if (!a->err.empty()) o += ";" + a->err;

@@ -60,6 +60,13 @@ struct PmcRates {
   double vmem_busy_pct = 0;      // 100 * ΔTA_BUSY(avg) / ΔGUI_ACTIVE
   double gpu_clock_mhz = 0;      // ΔGRBM_COUNT / Δt
   double dt_s = 0;
+  // Per XCD (both samples carry the breakdown): active % of clocks, and MFMA
+  // busy % of that XCD's active SIMD cycles (num_cu / n_xcd CUs × 4 SIMDs).
+  // An imbalance here is a workgroup→XCD mapping problem, invisible in the
+  // device-wide numbers.
+  int n_xcd = 0;
+  double xcd_active_pct[kMaxXcc] = {};
+  double xcd_mfma_util_pct[kMaxXcc] = {};
 };
 PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu);
 
@@ -78,6 +85,8 @@ struct MockPmcConfig {
   double mfma_frac = 0.6;       // fraction of active time the MFMA pipes are busy
   double vmem_frac = 0.3;       // fraction of active time the TA units are busy
   uint32_t mask = kPmcSetFull;  // counters the mock "reads"
+  int n_xcd = 8;                // per-XCD breakdown (0 = none)
+  double xcd_skew = 0.0;        // XCD x is active (1 - skew·x) of XCD 0's cycles
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,

@@ -99,6 +99,12 @@ struct PmcSample {
   uint32_t n = 0;
   uint32_t mask = 0;           // bit i set: value[i] was read (PmcIndex)
   uint64_t value[kMaxPmc] = {};
+  // Per-XCD breakdown (MI355X: 8 XCDs, each with its own GRBM and 4 SEs of SQs;
+  // workgroups are dispatched round-robin over them).  n_xcd = 0 when the
+  // reader could not place its results on XCDs.  Cumulative like value[].
+  uint32_t n_xcd = 0;
+  uint64_t xcd_active[kMaxXcc] = {};  // GRBM_GUI_ACTIVE of each XCD
+  uint64_t xcd_mfma[kMaxXcc] = {};    // SQ_VALU_MFMA_BUSY_CYCLES summed over each XCD's SEs
 };
 static_assert(std::is_trivially_copyable<PmcSample>::value, "seqlock payload");
 

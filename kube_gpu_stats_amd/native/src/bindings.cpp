@@ -42,6 +42,8 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.clock_mhz = get<double>(m, "clock_mhz", c.mock_pmc.clock_mhz);
     c.mock_pmc.mfma_frac = get<double>(m, "mfma_frac", c.mock_pmc.mfma_frac);
     c.mock_pmc.vmem_frac = get<double>(m, "vmem_frac", c.mock_pmc.vmem_frac);
+    c.mock_pmc.n_xcd = get<int>(m, "n_xcd", c.mock_pmc.n_xcd);
+    c.mock_pmc.xcd_skew = get<double>(m, "xcd_skew", c.mock_pmc.xcd_skew);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -217,6 +219,10 @@ class PyExporter {
     for (int i = 0; i < kPmcCount; ++i)
       if (p.mask & (1u << i)) v[pmc_counter_name(i)] = p.value[i];
     o["values"] = v;
+    if (p.n_xcd > 0) {
+      o["xcd_active"] = std::vector<uint64_t>(p.xcd_active, p.xcd_active + p.n_xcd);
+      o["xcd_mfma"] = std::vector<uint64_t>(p.xcd_mfma, p.xcd_mfma + p.n_xcd);
+    }
     return o;
   }
   py::dict window(int d, double window_s) const {
@@ -236,6 +242,10 @@ class PyExporter {
       if (r.have_vmem) o["vmem_busy_pct"] = r.vmem_busy_pct;
       o["gpu_clock_mhz"] = r.gpu_clock_mhz;
       o["pmc_dt_s"] = r.dt_s;
+      if (r.n_xcd > 0) {
+        o["xcd_mfma_util_pct"] = std::vector<double>(r.xcd_mfma_util_pct, r.xcd_mfma_util_pct + r.n_xcd);
+        o["xcd_active_pct"] = std::vector<double>(r.xcd_active_pct, r.xcd_active_pct + r.n_xcd);
+      }
     }
     return o;
   }

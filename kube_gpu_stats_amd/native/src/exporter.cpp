@@ -323,6 +323,14 @@ std::string Exporter::counters_json(int dev, int n, uint64_t since) {
       }
       o += ",\"gpu_clock_mhz\":";
       jnum(o, r.gpu_clock_mhz);
+      if (r.n_xcd > 0) {
+        o += ",\"xcd_mfma_util_pct\":[";
+        for (int x = 0; x < r.n_xcd; ++x) {
+          if (x) o += ',';
+          jnum(o, r.xcd_mfma_util_pct[x]);
+        }
+        o += "]";
+      }
     }
     o += '}';
   }

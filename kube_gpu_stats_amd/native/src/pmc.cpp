@@ -4,6 +4,7 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cmath>
 #include <ctime>
 #include <mutex>
@@ -49,6 +50,17 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
     if (r.have_vmem) r.vmem_busy_pct = 100.0 * d(kPmcTaBusy) / act;
   }
   r.gpu_clock_mhz = cnt / dt * 1e-6;
+  const uint32_t nx = std::min(a.n_xcd, b.n_xcd);
+  if (nx > 0 && nx <= static_cast<uint32_t>(kMaxXcc) && a.n_xcd == b.n_xcd) {
+    r.n_xcd = static_cast<int>(nx);
+    const double simds = cu / nx * 4.0;
+    for (uint32_t x = 0; x < nx; ++x) {
+      const double ax = b.xcd_active[x] >= a.xcd_active[x] ? static_cast<double>(b.xcd_active[x] - a.xcd_active[x]) : 0.0;
+      const double mx = b.xcd_mfma[x] >= a.xcd_mfma[x] ? static_cast<double>(b.xcd_mfma[x] - a.xcd_mfma[x]) : 0.0;
+      if (cnt > 0) r.xcd_active_pct[x] = 100.0 * ax / cnt;
+      if (ax > 0) r.xcd_mfma_util_pct[x] = 100.0 * mx / (ax * simds);
+    }
+  }
   return r;
 }
 
@@ -73,6 +85,16 @@ class MockCounterSource final : public CounterSource {
     s.mask = c_.mask;
     for (int i = 0; i < kPmcCount; ++i)
       if (!(s.mask & (1u << i))) s.value[i] = 0;
+    // XCD x is busy (1 - skew·x) of the time XCD 0 is (GUI_ACTIVE reduces by max
+    // over XCDs, so XCD 0 carries the device value); MFMA cycles split likewise.
+    s.n_xcd = static_cast<uint32_t>(std::clamp(c_.n_xcd, 0, kMaxXcc));
+    double wsum = 0;
+    for (uint32_t x = 0; x < s.n_xcd; ++x) wsum += 1.0 - c_.xcd_skew * x;
+    for (uint32_t x = 0; x < s.n_xcd; ++x) {
+      const double w = 1.0 - c_.xcd_skew * x;
+      s.xcd_active[x] = static_cast<uint64_t>(clk * busy_s * w);
+      s.xcd_mfma[x] = wsum > 0 ? static_cast<uint64_t>(s.value[kPmcMfmaBusy] * (w / wsum)) : 0;
+    }
     s.mono_ns = now;
     s.read_ns = 1000;
     return 0;
@@ -89,6 +111,7 @@ using init_fn = int (*)(char*, int);
 using open_fn = int (*)(uint64_t, const char* const*, const int*, int, char*, int);
 using sample_fn = int (*)(int, uint64_t*, int, uint32_t*);
 using sample_ts_fn = int (*)(int, uint64_t*, int, uint32_t*, int64_t*);
+using sample_xcd_fn = int (*)(int, int, uint64_t*, int);
 using pipelined_fn = int (*)(int, int, char*, int);
 using configure_fn = int (*)(const char*, int);
 using close_fn = void (*)(int);
@@ -133,11 +156,14 @@ class DlCounterSource final : public CounterSource {
     int is_max[kPmcCount];
     nsel_ = 0;
     for (int i = 0; i < kPmcCount; ++i) {
+      reader_idx_[i] = -1;
       if (!(mask & (1u << i))) continue;
       names[nsel_] = kNames[i];
       is_max[nsel_] = kReduce[i];
+      reader_idx_[i] = nsel_;
       sel_[nsel_++] = i;
     }
+    sample_xcd_ = reinterpret_cast<sample_xcd_fn>(dlsym(lib_, "kgs_pmc_sample_xcd"));  // optional
     mask_ = mask;
     int opened = 0;
     handles_.assign(static_cast<size_t>(be.device_count()), -1);
@@ -177,6 +203,12 @@ class DlCounterSource final : public CounterSource {
     s.mask = mask_;
     s.n = kPmcCount;
     s.read_ns = rns;
+    s.n_xcd = 0;
+    if (sample_xcd_ && reader_idx_[kPmcGrbmGuiActive] >= 0 && reader_idx_[kPmcMfmaBusy] >= 0) {
+      const int na = sample_xcd_(handles_[dev], reader_idx_[kPmcGrbmGuiActive], s.xcd_active, kMaxXcc);
+      const int nm = sample_xcd_(handles_[dev], reader_idx_[kPmcMfmaBusy], s.xcd_mfma, kMaxXcc);
+      if (na > 0 && na == nm) s.n_xcd = static_cast<uint32_t>(na);
+    }
     s.mono_ns = ts > 0 ? ts : mono_ns();  // when the CP read the counters (pipelined: previous call)
     return 0;
   }
@@ -186,7 +218,9 @@ class DlCounterSource final : public CounterSource {
   open_fn open_ = nullptr;
   sample_fn sample_ = nullptr;
   sample_ts_fn sample_ts_ = nullptr;
+  sample_xcd_fn sample_xcd_ = nullptr;
   int sel_[kPmcCount] = {};  // reader's counter k is PmcIndex sel_[k]
+  int reader_idx_[kPmcCount] = {};  // inverse: PmcIndex → reader counter, -1 not read
   int nsel_ = 0;
   uint32_t mask_ = 0;
   close_fn close_ = nullptr;

@@ -425,6 +425,22 @@ void Exporter::render(std::string& out) {
     for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_vmem) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
     w.head("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_clock_effective_mhz", dev_labels_[d], nullptr, snaps[d].r.gpu_clock_mhz);
+    bool any_xcd = false;
+    for (int d : ids) any_xcd |= snaps[d].pmc_rates && snaps[d].r.n_xcd > 0;
+    if (any_xcd) {
+      w.head("amdgpu_mfma_util_xcc_percent", "gauge",
+             "Matrix-core (MFMA) busy percent of one XCD's active cycles over the window (hardware counters)");
+      for (int d : ids)
+        if (snaps[d].pmc_rates)
+          for (int x = 0; x < snaps[d].r.n_xcd; ++x)
+            w.line("amdgpu_mfma_util_xcc_percent", dev_labels_[d], kXccLabels[x], snaps[d].r.xcd_mfma_util_pct[x]);
+      w.head("amdgpu_gpu_active_xcc_percent", "gauge",
+             "GRBM GUI-active percent of clocks of one XCD over the window (a dispatch in flight, not waves resident)");
+      for (int d : ids)
+        if (snaps[d].pmc_rates)
+          for (int x = 0; x < snaps[d].r.n_xcd; ++x)
+            w.line("amdgpu_gpu_active_xcc_percent", dev_labels_[d], kXccLabels[x], snaps[d].r.xcd_active_pct[x]);
+    }
   }
 
   // ---- per-process attribution ------------------------------------------

@@ -38,13 +38,23 @@ thread_local char g_err[256];
 // SALU work that issues beside the matrix pipe, and the block ends with 20 wait
 // states before the compiler's first read of the accumulators
 // (cdna_hip_programming.md §5.7 item 2).
+//
+// xcc_mask: a workgroup runs the loop only if bit <its XCC> is set, read from the
+// hardware (HW_REG_XCC_ID) rather than assumed from blockIdx — this is how the
+// per-XCD counter tests load exactly the XCDs they name.  xcc_out (optional)
+// receives each workgroup's XCC id.
 __global__ __launch_bounds__(kBlock) void mfma_bf16_kernel(const unsigned short* __restrict__ A,
                                                            const unsigned short* __restrict__ B,
-                                                           float* __restrict__ C, int iters) {
+                                                           float* __restrict__ C, int iters, unsigned xcc_mask,
+                                                           int* __restrict__ xcc_out) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = (blockIdx.x * kBlock + threadIdx.x) / kWave;
   const int r = lane & 15;          // A row / B column within a 16-wide tile
   const int kb = (lane >> 4) * 8;   // k base of this lane's 8 elements
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 0xF;
+  if (xcc_out && threadIdx.x == 0) xcc_out[blockIdx.x] = static_cast<int>(xcc);
 
   bf16x8 a, b0, b1, b2, b3;
 #pragma unroll
@@ -56,7 +66,7 @@ __global__ __launch_bounds__(kBlock) void mfma_bf16_kernel(const unsigned short*
     b3[j] = static_cast<short>(B[(kb + j) * 64 + 48 + r]);
   }
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
-  int n = iters;
+  int n = ((xcc_mask >> xcc) & 1u) ? iters : 0;
   if (n > 0) {
     asm volatile(
         "s_nop 4\n"
@@ -157,11 +167,17 @@ const char* kgs_load_last_error() { return g_err; }
 int kgs_load_block_size() { return kBlock; }
 
 // C must hold nblocks * 4 waves * 16 * 64 floats.
-int kgs_load_mfma_bf16(const void* A, const void* B, float* C, int nblocks, int iters, void* stream) {
+int kgs_load_mfma_bf16_xcc(const void* A, const void* B, float* C, int nblocks, int iters, unsigned xcc_mask,
+                           int* xcc_out, void* stream) {
   if (nblocks <= 0 || iters < 0) return check(hipErrorInvalidValue, "mfma_bf16 args");
   hipLaunchKernelGGL(mfma_bf16_kernel, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), C, iters);
+                     static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), C, iters,
+                     xcc_mask, xcc_out);
   return check(hipGetLastError(), "mfma_bf16 launch");
+}
+
+int kgs_load_mfma_bf16(const void* A, const void* B, float* C, int nblocks, int iters, void* stream) {
+  return kgs_load_mfma_bf16_xcc(A, B, C, nblocks, iters, 0xFFFFu, nullptr, stream);
 }
 
 // n must be a multiple of 4 and pointers 16-byte aligned.

@@ -33,6 +33,8 @@ def lib() -> ctypes.CDLL:
         L.kgs_load_last_error.restype = ctypes.c_char_p
         L.kgs_load_mfma_bf16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_void_p]
+        L.kgs_load_mfma_bf16_xcc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
         L.kgs_load_triad_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
                                          ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.kgs_load_triad_f32_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
@@ -67,6 +69,25 @@ def mfma_bf16(A, B, C, nblocks: int, iters: int, stream=None) -> None:
     assert A.device == B.device == C.device and A.is_cuda
     _check(lib().kgs_load_mfma_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), int(nblocks), int(iters),
                                     _stream_ptr(stream)))
+
+
+def mfma_bf16_xcc(A, B, C, nblocks: int, iters: int, xcc_mask: int, xcc_out=None, stream=None) -> None:
+    """mfma_bf16 on the XCDs in ``xcc_mask`` only: a workgroup whose hardware XCC id
+    (HW_REG_XCC_ID) is not in the mask skips the loop and writes zeros.  ``xcc_out``
+    (int32 [nblocks], optional) receives every workgroup's XCC id."""
+    import torch
+
+    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and C.dtype == torch.float32
+    assert tuple(A.shape) == (16, 32) and tuple(B.shape) == (32, 64), (A.shape, B.shape)
+    assert A.is_contiguous() and B.is_contiguous() and C.is_contiguous()
+    assert C.numel() >= nblocks * WAVES_PER_BLOCK * 16 * 64, "C too small for the grid"
+    assert A.device == B.device == C.device and A.is_cuda
+    out_ptr = 0
+    if xcc_out is not None:
+        assert xcc_out.dtype == torch.int32 and xcc_out.numel() >= nblocks and xcc_out.device == A.device
+        out_ptr = xcc_out.data_ptr()
+    _check(lib().kgs_load_mfma_bf16_xcc(A.data_ptr(), B.data_ptr(), C.data_ptr(), int(nblocks), int(iters),
+                                        int(xcc_mask) & 0xFFFF, out_ptr, _stream_ptr(stream)))
 
 
 def triad_f32(a, b, c, s: float, nblocks: int = 0, stream=None, nt: bool = True) -> None:

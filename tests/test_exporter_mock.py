@@ -258,3 +258,32 @@ def test_pmc_counter_sets(N, mock_exporter):
     assert s["v"][3] is None and "vmem_busy_pct" not in s
     with pytest.raises(RuntimeError, match="unknown pmc_set"):
         N.Exporter({"backend": "mock", "pmc_source": "mock", "pmc_set": "everything"})
+
+
+def test_per_xcd_counter_breakdown(mock_exporter):
+    """Per-XCD GUI-active and MFMA busy: XCD x of the mock is active (1 - 0.05·x) of
+    XCD 0's cycles and holds that share of the MFMA cycles, so its MFMA busy per
+    active SIMD cycle is 0.6 · 8 / Σ(1 - 0.05·x) for every x."""
+    ex = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0,
+                       mock={"util_base": 50, "util_amp": 0.0001}, mock_pmc={"xcd_skew": 0.05})
+    time.sleep(0.5)
+    w = ex.window(0, 0.3)
+    wsum = sum(1 - 0.05 * x for x in range(8))
+    assert len(w["xcd_active_pct"]) == 8
+    for x in range(8):
+        assert w["xcd_active_pct"][x] == pytest.approx(50 * (1 - 0.05 * x), abs=2.5)
+        assert w["xcd_mfma_util_pct"][x] == pytest.approx(100 * 0.6 * 8 / wsum, abs=3)
+    m = parse_text(ex.render())
+    got = {lb["xcc"]: v for lb, v in m["amdgpu_mfma_util_xcc_percent"]}
+    assert sorted(got) == [str(x) for x in range(8)]
+    assert {lb["xcc"] for lb, _ in m["amdgpu_gpu_active_xcc_percent"]} == set(got)
+    p = ex.pmc(0)
+    assert len(p["xcd_mfma"]) == 8 and sum(p["xcd_mfma"]) <= p["values"]["SQ_VALU_MFMA_BUSY_CYCLES"]
+    s = json.load(get(ex.port, "/counters?gpu=0&n=2"))["samples"][-1]
+    assert len(s["xcd_mfma_util_pct"]) == 8
+    # a reader without the breakdown emits no per-XCD families
+    flat = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0, mock_pmc={"n_xcd": 0})
+    time.sleep(0.3)
+    mf = parse_text(flat.render())
+    assert "amdgpu_mfma_util_xcc_percent" not in mf and "amdgpu_mfma_util_percent" in mf
+    assert "xcd_mfma_util_pct" not in flat.window(0, 0.2)

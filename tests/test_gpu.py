@@ -252,6 +252,79 @@ def test_counter_reader_exporter_process(torch_dev, mode):
             print(err[-4000:])
 
 
+def test_per_xcd_counters_follow_xcc_gated_load(torch_dev):
+    """Per-XCD MFMA busy / GUI-active from the aqlprofile reader land on the XCDs the
+    load really ran on.  The gated MFMA kernel reads its XCC id from the hardware
+    (HW_REG_XCC_ID) and works only on XCDs 0 and 2, so the reader's XCD coordinate
+    must match the hardware id (an order swap would light up other XCDs)."""
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(16, 32, generator=g).to(torch.bfloat16).to(torch_dev)
+    B = torch.randn(32, 64, generator=g).to(torch.bfloat16).to(torch_dev)
+    blocks = 2048
+    C = torch.empty(blocks * 4 * 16 * 64, device=torch_dev)
+    ids = torch.full((blocks,), -1, dtype=torch.int32, device=torch_dev)
+    load.mfma_bf16_xcc(A, B, C, blocks, 2, 0xFF, ids)
+    torch.cuda.synchronize()
+    hist = torch.bincount(ids.cpu().long(), minlength=8).tolist()
+    first = ids[:16].cpu().tolist()
+    print(json.dumps({"xcc_histogram": hist, "first_16_workgroups": first}))
+    assert len(hist) == 8 and min(hist) > 0, hist  # SPX: all 8 XCDs take workgroups
+    # gated numerics: a workgroup on an XCD outside the mask writes zeros
+    load.mfma_bf16_xcc(A, B, C, blocks, 3, 0b101, ids)
+    torch.cuda.synchronize()
+    ref = (A.float() @ B.float()) * 3
+    got = C.view(blocks, 4, 16, 64)
+    on = (ids == 0) | (ids == 2)
+    torch.testing.assert_close(got[on][0, 0], ref, rtol=1e-5, atol=1e-4)
+    assert torch.count_nonzero(got[~on]).item() == 0
+
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz", "200",
+           "--pmc", "aqlprofile", "--control-stdin", "--bdfs", bdf, "--proc-every", "0", "--link-every", "0"]
+    # KGS_AQL_DUMP_RESULTS: the reader logs every result of its 250th READ (≈1.2 s
+    # into the load) with aqlprofile's event coordinates — the raw layout evidence
+    # (profiles/r1/xcd/).
+    proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True, env=dict(os.environ, KGS_AQL_DUMP_RESULTS="250"))
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
+        sc = Scraper("127.0.0.1", ready["port"])
+        t0 = time.time()
+        while time.time() - t0 < 1.6:
+            load.mfma_bf16_xcc(A, B, C, blocks, 20000, 0b101)
+            torch.cuda.synchronize()
+        m = parse_text(sc.get())
+        mfma = {int(lb["xcc"]): v for lb, v in m.get("amdgpu_mfma_util_xcc_percent", [])}
+        act = {int(lb["xcc"]): v for lb, v in m.get("amdgpu_gpu_active_xcc_percent", [])}
+        gfx = {int(lb["xcc"]): v for lb, v in m.get("amdgpu_gfx_busy_xcc_percent", [])}
+        print(json.dumps({"mfma_util_xcc": mfma, "gpu_active_xcc": act, "pmfw_gfx_busy_xcc": gfx,
+                          "pmc_info": ready.get("pmc_info")}))
+        assert sorted(mfma) == list(range(8)), mfma
+        assert mfma[0] > 50 and mfma[2] > 50, mfma
+        assert max(mfma[x] for x in (1, 3, 4, 5, 6, 7)) < 5, mfma
+        # GUI-active is "a dispatch in flight", not "waves resident": the idle XCDs
+        # read ~100 % too while the chip-wide kernel runs (profiles/r1/xcd/README.md).
+        assert act[0] > 80 and act[2] > 80, act
+        assert "xcd=8:" in ready["pmc_info"][0], ready["pmc_info"]  # all 8 XCDs placed
+    finally:
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            out, err = proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            out, err = proc.communicate()
+        print("\n".join(ln for ln in err.splitlines() if ln.startswith("[aql-res]")))
+        print(out[-1500:])
+
+
 def test_hbm_bandwidth_estimate_tracks_stream_kernels(N, torch_dev):
     """amdgpu_hbm_bandwidth_bytes_per_second (UMC activity × MI355X calibration)
     agrees with the bytes a triad loop moves, and reads ~0 under a pure MFMA load."""
