@@ -67,8 +67,8 @@ def build() -> dict:
                [(_dev("amdgpu_mfma_util_percent"), "{{kubernetes_io_hostname}} gpu{{gpu}}")], 12, y, unit="percent",
                maxv=100))
     y += 8
-    add(_panel(0, "Per-XCC busy (die imbalance)",
-               [(_dev("amdgpu_gfx_busy_xcc_percent"), "gpu{{gpu}} xcc{{xcc}}")], 0, y, unit="percent", maxv=100))
+    add(_panel(0, "Per-XCD MFMA busy (workgroup→XCD imbalance)",
+               [(_dev("amdgpu_mfma_util_xcc_percent"), "gpu{{gpu}} xcd{{xcc}}")], 0, y, unit="percent", maxv=100))
     add(_panel(0, "HBM bandwidth (UMC activity, MI355X calibration)",
                [(_dev("rate(amdgpu_hbm_bytes_total[1m])"), "gpu{{gpu}}")], 12, y, unit="Bps"))
     y += 8

@@ -47,7 +47,8 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_gfx_busy_instant_percent", "gauge", "GFX busy % in the latest PMFW table."),
     F("amdgpu_gfx_busy_xcc_percent", "gauge",
       "Busy % per XCC over the last firmware interval, from the per-partition accumulators "
-      "(instant value when those are absent); shows load imbalance across the 8 dies.", extra=("xcc",)),
+      "(instant value when those are absent).  Busy means a dispatch in flight on that XCC: a chip-wide kernel keeps "
+      "all 8 at ~100 % even when waves run on a few; amdgpu_mfma_util_xcc_percent shows where they run.", extra=("xcc",)),
     F("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller activity %, window mean."),
     F("amdgpu_gfx_busy_seconds_total", "counter", "∫ GFX busy fraction dt; rate() = exact mean utilisation."),
     F("amdgpu_umc_busy_seconds_total", "counter", "∫ UMC busy fraction dt."),

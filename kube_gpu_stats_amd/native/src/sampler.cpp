@@ -130,8 +130,10 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
   }
   g = g < 0 ? 0 : (g > 100 ? 100 : g);
   u = u < 0 ? 0 : (u > 100 ? 100 : u);
-  // Per-XCC (XCD) window means from the per-partition accumulators: shows load
-  // imbalance across the 8 dies that the device-wide number averages away.
+  // Per-XCC (XCD) window means from the per-partition accumulators.  PMFW counts
+  // an XCC busy while a dispatch is in flight on it, so a chip-wide kernel keeps
+  // all 8 near 100 % even when waves run on a few (profiles/r1/xcd/README.md);
+  // the counter tier's per-XCD MFMA split shows where they run.
   for (uint32_t x = 0; x < cur.num_xcc && x < static_cast<uint32_t>(kMaxXcc); ++x) {
     double v = cur.gfx_busy_xcc[x];
     uint64_t dx;

@@ -23,7 +23,8 @@ from ..utils.scrape import Scraper, parse_text
 
 COLS = [("gpu", "GPU", 3), ("pod", "POD", 18), ("gfx", "GFX%", 5), ("mfma", "MFMA%", 5), ("vmem", "VMEM%", 5),
         ("umc", "UMC%", 5), ("hbm_gb", "HBM_GB", 7), ("hbm_pct", "HBM%", 5), ("power_w", "PWR_W", 6),
-        ("energy_w", "AVG_W", 6), ("temp_c", "TEMP", 4), ("clk_mhz", "MHZ", 5), ("xgmi_gbps", "XGMI_GB/s", 9)]
+        ("energy_w", "AVG_W", 6), ("temp_c", "TEMP", 4), ("clk_mhz", "MHZ", 5), ("xgmi_gbps", "XGMI_GB/s", 9),
+        ("xcd_mfma", "MFMA%_PER_XCD", 31)]
 BURST_COLS = [("mfma_min", "MFMA_MIN", 8), ("mfma_max", "MFMA_MAX", 8), ("drains", "DRAINS", 6)]
 
 
@@ -56,6 +57,15 @@ def _pods(m: dict) -> dict[str, str]:
     return {g: ",".join(sorted(p)) for g, p in pods.items()}
 
 
+def _xcd_split(m: dict, fam: str) -> dict[str, str]:
+    """GPU → per-XCD values as "a/b/c/..." in XCD order (MI355X: 8)."""
+    per: dict[str, dict[int, float]] = {}
+    for lb, v in m.get(fam, []):
+        if "gpu" in lb and lb.get("xcc", "").isdigit():
+            per.setdefault(lb["gpu"], {})[int(lb["xcc"])] = v
+    return {g: "/".join(f"{x[k]:.0f}" for k in sorted(x)) for g, x in per.items()}
+
+
 def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
     """One row per GPU from a scrape (and the previous one, for rates)."""
     gfx = _by_gpu(cur, "amdgpu_gfx_busy_percent")
@@ -72,6 +82,7 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
     penergy = _by_gpu(prev, "amdgpu_energy_joules_total") if prev else {}
     pxgmi = _sum_by_gpu(prev, "amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total") if prev else {}
     pods = _pods(cur)
+    xcd = _xcd_split(cur, "amdgpu_mfma_util_xcc_percent")
     gpus = sorted(set(gfx) | set(used) | set(power), key=lambda g: int(g) if g.isdigit() else 0)
     rows = []
     for g in gpus:
@@ -79,7 +90,7 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
              "umc": umc.get(g), "hbm_gb": used[g] / 1e9 if g in used else None,
              "hbm_pct": 100.0 * used[g] / total[g] if total.get(g) and g in used else None,
              "power_w": power.get(g), "temp_c": temp.get(g), "clk_mhz": clk.get(g), "energy_w": None,
-             "xgmi_gbps": None}
+             "xgmi_gbps": None, "xcd_mfma": xcd.get(g)}
         if dt > 0 and g in penergy and g in energy and energy[g] >= penergy[g]:
             r["energy_w"] = (energy[g] - penergy[g]) / dt
         if dt > 0 and g in pxgmi and g in xgmi and xgmi[g] >= pxgmi[g]:

@@ -118,6 +118,7 @@ def test_cli_dmon_rows_and_counter_bursts(mock_exporter):
         assert r["energy_w"] is not None and r["energy_w"] > 0      # rate from the energy counter
         assert r["drains"] >= 100                                    # ≈200 drains per 0.2 s at 1 kHz
         assert 55 <= r["mfma_min"] <= r["mfma_max"] <= 65             # mock: MFMA busy 60 % of active cycles
+        assert [55 <= float(x) <= 65 for x in r["xcd_mfma"].split("/")] == [True] * 8  # per-XCD split
     buf = io.StringIO()
     a = dmon.build_parser().parse_args([f"http://127.0.0.1:{ex.port}", "--interval", "0.1", "--count", "2"])
     dmon.run(a, out=buf)
