@@ -33,6 +33,12 @@ CATALOG: tuple[Family, ...] = (
       "consumed by `avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)`.",
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
       "pmfw+kubelet", "fast"),
+    F("container_gpu_mfma_util", "gauge",
+      "Matrix-core (MFMA) busy % of active cycles of the GPU allocated to the pod (window), same labels as "
+      "container_gpu_sm_util.  GFX busy counts a GPU busy while any dispatch is in flight; this says how much of "
+      "that was matrix work.  `kgs gpu-util-stats --util-metric container_gpu_mfma_util` reports it per pod.",
+      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      "rocprofiler+kubelet", "pmc"),
     # ---- inventory / topology -------------------------------------------------------------
     F("amdgpu_device_info", "gauge", "Static device information (1).", extra=(
         "bdf", "gpu_type", "kubernetes_io_hostname", "serial", "market_name", "gfx_target", "numa_node", "num_cu", "num_xcc", "kfd_gpu_id", "hip_id",

@@ -188,12 +188,12 @@ void Exporter::render(std::string& out) {
 
   // ---- reference-compatible series (F5) ---------------------------------
   if (cfg_.compat_series) {
-    w.head("container_gpu_sm_util", "gauge",
-           "GFX-engine (compute) busy percent of the GPU allocated to the pod, averaged over the exporter window "
-           "(reference metric contract; label nvidia_gpu_type kept for compatibility)");
+    // Pod labels of every (GPU, owner) pair, built once for both per-pod families.
+    static thread_local std::vector<std::pair<int, std::string>> pod_lines;
+    pod_lines.clear();
     for (int d : ids) {
       const Snap& x = snaps[static_cast<size_t>(d)];
-      if (!x.busy) continue;
+      if (!x.busy && !x.pmc_rates) continue;
       const DeviceInfo& in = be_->info(d);
       const std::string type = cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override;
       auto emit = [&](const Owner* o) {
@@ -206,7 +206,7 @@ void Exporter::render(std::string& out) {
         kv(lb, "container_name", o ? o->container : std::string());
         kv(lb, "gpu", std::to_string(d));
         kv(lb, "uuid", in.uuid);
-        w.line("container_gpu_sm_util", lb, nullptr, x.g);
+        pod_lines.emplace_back(d, std::move(lb));
       };
       auto it = own ? own->find(d) : decltype(own->end()){};
       if (own && it != own->end() && !it->second.empty()) {
@@ -214,6 +214,23 @@ void Exporter::render(std::string& out) {
       } else if (cfg_.compat_unallocated) {
         emit(nullptr);
       }
+    }
+    w.head("container_gpu_sm_util", "gauge",
+           "GFX-engine (compute) busy percent of the GPU allocated to the pod, averaged over the exporter window "
+           "(reference metric contract; label nvidia_gpu_type kept for compatibility)");
+    for (const auto& [d, lb] : pod_lines)
+      if (snaps[static_cast<size_t>(d)].busy) w.line("container_gpu_sm_util", lb, nullptr, snaps[static_cast<size_t>(d)].g);
+    bool any_mfma = false;
+    for (const auto& pl : pod_lines) any_mfma |= snaps[static_cast<size_t>(pl.first)].pmc_rates;
+    if (any_mfma) {
+      // Same labels, hardware-counter matrix-core busy: GFX busy counts a GPU busy
+      // while any dispatch is in flight; this says how much of it was MFMA work.
+      w.head("container_gpu_mfma_util", "gauge",
+             "Matrix-core (MFMA) busy percent of active cycles of the GPU allocated to the pod, over the exporter "
+             "window (hardware counters; same labels as container_gpu_sm_util)");
+      for (const auto& [d, lb] : pod_lines)
+        if (snaps[static_cast<size_t>(d)].pmc_rates)
+          w.line("container_gpu_mfma_util", lb, nullptr, snaps[static_cast<size_t>(d)].r.mfma_util_pct);
     }
   }
 

@@ -287,3 +287,21 @@ def test_per_xcd_counter_breakdown(mock_exporter):
     mf = parse_text(flat.render())
     assert "amdgpu_mfma_util_xcc_percent" not in mf and "amdgpu_mfma_util_percent" in mf
     assert "xcd_mfma_util_pct" not in flat.window(0, 0.2)
+
+
+def test_per_pod_mfma_series_follows_compat_labels(mock_exporter):
+    """container_gpu_mfma_util: the counter tier's MFMA busy under the reference
+    series' labels, so the per-pod report can run on it unchanged."""
+    ex = mock_exporter(n_gpus=2, hz=500, pmc_source="mock", proc_every=0, link_every=0, compat_unallocated=True,
+                       mock={"util_base": 50, "util_amp": 0.0001})
+    ex.set_device_owners(0, [{"pod": "train-0", "namespace": "ml", "container": "main"}])
+    time.sleep(0.4)
+    m = parse_text(ex.render())
+    sm = {lb["gpu"]: lb for lb, _ in m["container_gpu_sm_util"]}
+    mf = {lb["gpu"]: (lb, v) for lb, v in m["container_gpu_mfma_util"]}
+    assert set(mf) == set(sm) == {"0", "1"}
+    assert mf["0"][0] == sm["0"] and mf["0"][0]["pod_name"] == "train-0"
+    assert mf["0"][1] == pytest.approx(60, abs=3)  # mock: MFMA busy 60 % of active cycles
+    plain = mock_exporter(n_gpus=1, hz=100, proc_every=0, link_every=0, compat_unallocated=True)
+    time.sleep(0.3)
+    assert "container_gpu_mfma_util" not in parse_text(plain.render())  # no counter tier, no series
