@@ -94,7 +94,7 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         objs = list(ex.map(compile_one, srcs))
     tmp = f"{out}.{os.getpid()}.tmp"  # concurrent builders (one per rank) never share a temp file
     _run(["g++", "-shared", "-pthread", "-o", tmp, *objs, "-L" + os.path.join(ROCM, "lib"), "-lamd_smi",
-          "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl"], verbose)
+          "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl", "-lz"], verbose)
     os.replace(tmp, out)
     return out
 
@@ -153,7 +153,7 @@ def build_tsan_test(verbose: bool = False, sanitizer: str = "thread") -> str:
     if _stale(out, srcs + _headers() + [__file__]):
         _run(["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-pthread",
               "-I" + os.path.join(HERE, "include"), "-I" + os.path.join(ROCM, "include"), *srcs, "-o", out,
-              "-L" + os.path.join(ROCM, "lib"), "-lamd_smi", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl"],
+              "-L" + os.path.join(ROCM, "lib"), "-lamd_smi", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl", "-lz"],
              verbose)
     return out
 

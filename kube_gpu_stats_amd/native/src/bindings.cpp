@@ -68,6 +68,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.compat_series = get<bool>(d, "compat_series", c.compat_series);
   c.compat_unallocated = get<bool>(d, "compat_unallocated", c.compat_unallocated);
   c.control_http = get<bool>(d, "control_http", c.control_http);
+  c.gzip_level = get<int>(d, "gzip_level", c.gzip_level);
   return c;
 }
 

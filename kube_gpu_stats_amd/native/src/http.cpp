@@ -9,6 +9,9 @@
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
+#include <zlib.h>
+
+#include <strings.h>
 
 #include <cerrno>
 #include <cstdlib>
@@ -50,7 +53,57 @@ uint64_t query_u64(const std::string& q, const char* key, uint64_t dflt) {
   return dflt;
 }
 
-void respond(Conn& c, int code, const char* reason, const char* ctype, const std::string& body) {
+// Case-insensitive search for a header line `name:` whose value contains `token`.
+bool header_has(const std::string& req, const char* name, const char* token) {
+  const size_t nl = std::strlen(name);
+  size_t p = req.find("\r\n");
+  while (p != std::string::npos) {
+    const size_t s = p + 2;
+    const size_t e = req.find("\r\n", s);
+    const size_t end = e == std::string::npos ? req.size() : e;
+    if (end - s > nl && req[s + nl] == ':' && strncasecmp(req.c_str() + s, name, nl) == 0) {
+      const std::string v = req.substr(s + nl + 1, end - s - nl - 1);
+      if (v.find(token) != std::string::npos) return true;
+    }
+    p = e;
+  }
+  return false;
+}
+
+// One-shot gzip (RFC 1952) of `in` into `out`; reuses the deflate state across calls.
+class Gzip {
+ public:
+  ~Gzip() {
+    if (init_) deflateEnd(&z_);
+  }
+  bool compress(const std::string& in, std::string& out, int level) {
+    if (!init_ || level != level_) {
+      if (init_) deflateEnd(&z_);
+      z_ = z_stream{};
+      init_ = deflateInit2(&z_, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) == Z_OK;
+      level_ = level;
+      if (!init_) return false;
+    } else if (deflateReset(&z_) != Z_OK) {
+      return false;
+    }
+    out.resize(deflateBound(&z_, in.size()) + 64);
+    z_.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(in.data()));
+    z_.avail_in = static_cast<uInt>(in.size());
+    z_.next_out = reinterpret_cast<Bytef*>(&out[0]);
+    z_.avail_out = static_cast<uInt>(out.size());
+    const int rc = deflate(&z_, Z_FINISH);
+    out.resize(z_.total_out);
+    return rc == Z_STREAM_END;
+  }
+
+ private:
+  z_stream z_{};
+  bool init_ = false;
+  int level_ = -1;
+};
+
+void respond(Conn& c, int code, const char* reason, const char* ctype, const std::string& body,
+             const char* encoding = nullptr) {
   c.out.clear();
   c.out_off = 0;
   c.out.reserve(body.size() + 256);
@@ -60,6 +113,11 @@ void respond(Conn& c, int code, const char* reason, const char* ctype, const std
   c.out += reason;
   c.out += "\r\nContent-Type: ";
   c.out += ctype;
+  if (encoding) {
+    c.out += "\r\nContent-Encoding: ";
+    c.out += encoding;
+    c.out += "\r\nVary: Accept-Encoding";
+  }
   c.out += "\r\nContent-Length: ";
   c.out += std::to_string(body.size());
   c.out += c.close_after ? "\r\nConnection: close\r\n\r\n" : "\r\nConnection: keep-alive\r\n\r\n";
@@ -119,7 +177,8 @@ void HttpServer::stop() {
 void HttpServer::loop() {
   pthread_setname_np(pthread_self(), "kgs-http");
   std::unordered_map<int, Conn> conns;
-  std::string body;
+  std::string body, zbody;
+  Gzip gz;
   epoll_event evs[64];
   auto drop = [&](int fd) {
     epoll_ctl(efd_, EPOLL_CTL_DEL, fd, nullptr);
@@ -208,7 +267,11 @@ void HttpServer::loop() {
           respond(c, 405, "Method Not Allowed", "text/plain", "only GET\n");
         } else if (target == "/metrics") {
           ex_->render(body);
-          respond(c, 200, "OK", "text/plain; version=0.0.4; charset=utf-8", body);
+          const int lvl = ex_->config().gzip_level;
+          if (lvl > 0 && header_has(req, "Accept-Encoding", "gzip") && gz.compress(body, zbody, lvl))
+            respond(c, 200, "OK", "text/plain; version=0.0.4; charset=utf-8", zbody, "gzip");
+          else
+            respond(c, 200, "OK", "text/plain; version=0.0.4; charset=utf-8", body);
         } else if (ex_->config().control_http && (target == "/control/pause" || target == "/control/resume")) {
           if (target == "/control/pause") ex_->pause_sampling();
           else ex_->resume_sampling();

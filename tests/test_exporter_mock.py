@@ -305,3 +305,31 @@ def test_per_pod_mfma_series_follows_compat_labels(mock_exporter):
     plain = mock_exporter(n_gpus=1, hz=100, proc_every=0, link_every=0, compat_unallocated=True)
     time.sleep(0.3)
     assert "container_gpu_mfma_util" not in parse_text(plain.render())  # no counter tier, no series
+
+
+def test_metrics_gzip_negotiation(mock_exporter):
+    """--gzip-level: gzip only for clients that send Accept-Encoding: gzip; the
+    decompressed page is a normal exposition.  Off by default."""
+    import gzip
+
+    ex = mock_exporter(n_gpus=2, hz=100, gzip_level=1)
+    off = mock_exporter(n_gpus=1, hz=100)
+    time.sleep(0.3)
+    c = http.client.HTTPConnection("127.0.0.1", ex.port, timeout=5)
+    for _ in range(2):  # keep-alive, deflate state reused
+        c.request("GET", "/metrics", headers={"Accept-Encoding": "gzip, deflate"})
+        r = c.getresponse()
+        raw = r.read()
+        assert r.getheader("Content-Encoding") == "gzip" and r.getheader("Vary") == "Accept-Encoding"
+        body = gzip.decompress(raw).decode()
+        assert "kgs_up" in body and len(raw) < len(body) / 3
+        assert len(list(text_string_to_metric_families(body))) > 10
+    c.request("GET", "/metrics")
+    r = c.getresponse()
+    assert r.getheader("Content-Encoding") is None and b"kgs_up" in r.read()
+    c.close()
+    c = http.client.HTTPConnection("127.0.0.1", off.port, timeout=5)
+    c.request("GET", "/metrics", headers={"accept-encoding": "gzip"})
+    r = c.getresponse()
+    assert r.getheader("Content-Encoding") is None and b"kgs_up" in r.read()
+    c.close()
