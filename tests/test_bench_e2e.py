@@ -91,3 +91,46 @@ def test_end_to_end_exporter_to_report(mock_exporter, tmp_path):
                                      "pod_name": "train-0"}
     finally:
         fp.stop()
+
+
+def test_multi_node_exporters_to_reports(mock_exporter):
+    """"Multi-node" without a cluster: two exporters with their own
+    --node-name feed one (fake) Prometheus; the per-pod report (F3), the per-node
+    report (F4) and the per-pod MFMA report all span both nodes."""
+    a = mock_exporter(n_gpus=2, hz=200, window_s=0.2, node_name="node-a", pmc_source="mock",
+                      mock={"util_base": 60, "util_amp": 0.0001, "fw_period_s": 0.01}, mock_pmc={"mfma_frac": 0.6})
+    b = mock_exporter(n_gpus=2, hz=200, window_s=0.2, node_name="node-b", pmc_source="mock",
+                      mock={"util_base": 30, "util_amp": 0.0001, "fw_period_s": 0.01}, mock_pmc={"mfma_frac": 0.3})
+    a.set_device_owners(0, [{"pod": "train-0", "namespace": "ml", "container": "main"}])
+    a.set_device_owners(1, [{"pod": "train-0", "namespace": "ml", "container": "main"}])
+    b.set_device_owners(1, [{"pod": "infer-1", "namespace": "ml", "container": "srv"}])
+    fp = FakeProm()
+    url = fp.start()
+    try:
+        time.sleep(0.4)
+        sa, sb = Scraper("127.0.0.1", a.port), Scraper("127.0.0.1", b.port)
+        t0 = 1_700_000_000.0
+        for i in range(6):
+            fp.ingest(parse_text(sa.scrape_once()), t0 + 10 * i, {"instance": "node-a:9400"})
+            fp.ingest(parse_text(sb.scrape_once()), t0 + 10 * i, {"instance": "node-b:9400"})
+            time.sleep(0.05)
+        for metric in ("container_gpu_sm_util", "container_gpu_mfma_util"):
+            q = G.Queries.amd("ml", 10, util_metric=metric)
+            fp.add_instant(q.total, [{"metric": {"node": n, q.type_label: "MI355X"}, "value": [t0, "8"]}
+                                     for n in ("node-a", "node-b")])
+            fp.add_instant(q.used, [{"metric": {"node": "node-a"}, "value": [t0, "2"]},
+                                    {"metric": {"node": "node-b"}, "value": [t0, "1"]}])
+            fp.add_instant(q.live, [{"metric": {"pod": p}, "value": [t0, "1"]} for p in ("train-0", "infer-1")])
+            fp.add_range(q.req, [{"metric": {"node": "node-a", "pod": "train-0"}, "values": [[t0, "2"]]},
+                                 {"metric": {"node": "node-b", "pod": "infer-1"}, "values": [[t0, "1"]]}])
+            rows = sorted(G.run_report(PromClient(url), q, t0 + 50, 50, 10, compat=False))
+            want = (60.0, 30.0)  # mock: GFX busy 60 / 30 %, MFMA busy 60 / 30 % of active cycles
+            assert [r[:3] for r in rows] == [["node-a", "train-0", 2], ["node-b", "infer-1", 1]], rows
+            assert rows[0][3] == pytest.approx(want[0], abs=2) and rows[1][3] == pytest.approx(want[1], abs=2), rows
+            if metric == "container_gpu_sm_util":
+                nodes = G.run_report(PromClient(url), q, t0 + 50, 50, 10, compat=False, mode="node")
+                assert [(r[0], r[1], r[3], r[4]) for r in nodes] == [("node-a", "MI355X", 2, 8),
+                                                                    ("node-b", "MI355X", 1, 8)], nodes
+                assert nodes[0][2] == pytest.approx(60, abs=2) and nodes[1][2] == pytest.approx(30, abs=2), nodes
+    finally:
+        fp.stop()
