@@ -3,6 +3,7 @@
 
 #include <poll.h>
 #include <pthread.h>
+#include <sys/prctl.h>
 #include <sched.h>
 #include <sys/eventfd.h>
 #include <unistd.h>
@@ -169,6 +170,10 @@ void Sampler::run(int dev) {
   char tname[16];
   std::snprintf(tname, sizeof tname, "kgs-gpu%d", dev);
   pthread_setname_np(pthread_self(), tname);
+  // The default 50 µs timer slack is 40 % of an 8 kHz period: wake on time.
+  // (KGS_TIMERSLACK_NS overrides, for interference experiments.)
+  const char* slack = std::getenv("KGS_TIMERSLACK_NS");
+  prctl(PR_SET_TIMERSLACK, slack ? std::strtoul(slack, nullptr, 10) : 1000UL, 0, 0, 0);
 
   const int64_t period_ns = static_cast<int64_t>(1e9 / cfg_.hz);
   const uint64_t pmfw_every = cfg_.pmfw_hz > 0 && cfg_.pmfw_hz < cfg_.hz
@@ -187,6 +192,7 @@ void Sampler::run(int dev) {
     if (st.pmc_latest.load(lp)) pmc_seq = lp.seq;
   }
   int64_t next = mono_ns();
+  int late_streak = 0;  // consecutive overrun ticks
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;
   std::unordered_map<uint32_t, double> cu_seconds;  // pid -> ∫ occupancy share dt
@@ -320,8 +326,14 @@ void Sampler::run(int dev) {
     const int64_t now = mono_ns();
     if (next <= now) {
       ++I.overruns;
+      // A tick that ran long (the PMFW table read is ≈50–130 µs, longer than a
+      // kHz period) is followed by one immediate tick, so the counter tier keeps
+      // its rate; a second overrun in a row means the rate is beyond the work,
+      // and then the thread sleeps a quarter period instead of spinning.
       next = now + (backoff_shift ? step : 0);
-      if (next <= now) next = now + period_ns / 4;  // never spin
+      if (next <= now && ++late_streak > 1) next = now + period_ns / 4;
+    } else {
+      late_streak = 0;
     }
     st.integ.store(I);
     // Sleep until the absolute deadline or until stop() signals the eventfd.
