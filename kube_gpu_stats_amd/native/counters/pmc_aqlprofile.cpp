@@ -13,9 +13,15 @@
 //     with ROCm) fills vendor-specific PM4-IB AQL packets: START once (programs
 //     and enables the counters), then READ per sample (copies the running
 //     counters into a fine-grained host buffer);
-//   * each READ carries an interrupt-capable completion signal and the sampler
-//     thread waits on it in HSA_WAIT_STATE_BLOCKED, so the CPU sleeps while the
-//     CP works;
+//   * READs are pipelined over two slots: each sample collects the READ
+//     submitted on the previous tick (its completion signal is normally set
+//     already) and submits the next, so the sampler never waits out the CP
+//     round trip; a READ that is not done yet is waited for in
+//     HSA_WAIT_STATE_BLOCKED;
+//   * the READ IB is made lean (no per-XCC CS_PARTIAL_FLUSH, an L2 writeback
+//     instead of the full cache invalidate) and its AQL header has no acquire
+//     fence, only the system-scope release that orders the completion signal
+//     after the results (profiles/launch_overhead.md);
 //   * results are folded per counter over every block instance / XCC sample
 //     (max for GRBM clocks, sum for SQ busy cycles, mean for TA busy), the same
 //     reductions as the rocprofiler path, and reported cumulative since START.
@@ -251,8 +257,47 @@ void* host_alloc(Agent* a, size_t bytes) {
   return p;
 }
 
+// AQL header fence scopes of the pipelined READ packets: KGS_AQL_FENCE =
+// <scope> or <acquire>,<release> with scopes sys | agent | none; default
+// none,sys.  A system-scope acquire makes every XCC's CP invalidate its caches
+// before the packet; a READ reads only registers, so it needs none.  The release
+// is what orders the completion signal after the COPY_DATA results: without it
+// the host reads stale values (run r40: MFMA util 57 % for 91 %).  Dropping the
+// acquire cuts the READ's cost to a dispatch-bound stream from ≈7 % to ≈5 % at
+// 8 kHz with identical counter values (runs r40/r41, profiles/launch_overhead.md).
+// START, STOP and synchronous READs keep system scope both ways.
+int parse_scope(const char* s, size_t n) {
+  if (n == 3 && std::strncmp(s, "sys", 3) == 0) return static_cast<int>(HSA_FENCE_SCOPE_SYSTEM);
+  if (n == 5 && std::strncmp(s, "agent", 5) == 0) return static_cast<int>(HSA_FENCE_SCOPE_AGENT);
+  return static_cast<int>(HSA_FENCE_SCOPE_NONE);
+}
+std::pair<int, int> read_fences() {
+  static const std::pair<int, int> v = [] {
+    const char* e = std::getenv("KGS_AQL_FENCE");
+    if (!e) return std::make_pair(static_cast<int>(HSA_FENCE_SCOPE_NONE), static_cast<int>(HSA_FENCE_SCOPE_SYSTEM));
+    const char* c = std::strchr(e, ',');
+    if (!c) return std::make_pair(parse_scope(e, std::strlen(e)), parse_scope(e, std::strlen(e)));
+    return std::make_pair(parse_scope(e, static_cast<size_t>(c - e)), parse_scope(c + 1, std::strlen(c + 1)));
+  }();
+  return v;
+}
+constexpr std::pair<int, int> kSystemFences{HSA_FENCE_SCOPE_SYSTEM, HSA_FENCE_SCOPE_SYSTEM};
+
+// Completion signals of the pipelined READ slots (KGS_AQL_SIGNAL = interrupt |
+// poll).  The pipelined reader polls the previous READ's signal, so it needs no
+// interrupt; a signal whose only consumer is the GPU agent is a plain memory
+// word (no KFD event, no interrupt per READ).
+bool poll_signals() {
+  static const bool on = [] {
+    const char* e = std::getenv("KGS_AQL_SIGNAL");
+    return e && std::strcmp(e, "poll") == 0;
+  }();
+  return on;
+}
+
 // Put one PM4-IB vendor packet on the agent's private queue (no wait).
-void enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig) {
+void enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig,
+             std::pair<int, int> fences = kSystemFences) {
   hsa_queue_t* q = a->queue;
   hsa_signal_store_relaxed(sig, 1);
   const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
@@ -263,8 +308,8 @@ void enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t si
   slot->completion_signal = sig;
   const uint16_t header = static_cast<uint16_t>(
       (HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
-      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+      (fences.first << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+      (fences.second << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(q->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
 }
@@ -506,7 +551,7 @@ int read_pipelined(Agent* a, int64_t* ts) {
     if (ts) *ts = t0 + a->rtt_ns / 2;
     std::memset(a->pout[0], 0, a->pprof[0].output_buffer.size);
     a->psubmit_ns[0] = mono_ns();
-    enqueue(a, a->pread[0], a->psig[0]);
+    enqueue(a, a->pread[0], a->psig[0], read_fences());
     a->inflight = 0;
     return 0;
   }
@@ -525,7 +570,7 @@ int read_pipelined(Agent* a, int64_t* ts) {
   const int n = k ^ 1;
   std::memset(a->pout[n], 0, a->pprof[n].output_buffer.size);
   a->psubmit_ns[n] = mono_ns();
-  enqueue(a, a->pread[n], a->psig[n]);
+  enqueue(a, a->pread[n], a->psig[n], read_fences());
   a->inflight = n;
   return rc;
 }
@@ -538,7 +583,9 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
     p = a->prof;
     a->pcmd[k] = host_alloc(a, cmd_sz);
     a->pout[k] = host_alloc(a, out_sz);
-    if (!a->pcmd[k] || !a->pout[k] || hsa_signal_create(1, 0, nullptr, &a->psig[k]) != HSA_STATUS_SUCCESS) {
+    const hsa_status_t sc = poll_signals() ? hsa_amd_signal_create(1, 1, &a->agent, 0, &a->psig[k])
+                                           : hsa_signal_create(1, 0, nullptr, &a->psig[k]);
+    if (!a->pcmd[k] || !a->pout[k] || sc != HSA_STATUS_SUCCESS) {
       err = "pipeline buffer allocation failed";
       return false;
     }
@@ -817,7 +864,8 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads : 0.0) +
                   ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed) +
                   ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
-                  a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc);
+                  a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc) + ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
+                  ";signal=" + (poll_signals() ? "poll" : "interrupt");
   for (size_t k = 0; k < a->names.size(); ++k)
     o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
   if (!a->err.empty()) o += ";" + a->err;

@@ -160,8 +160,10 @@ def test_load_throughput_and_util_accumulators(N, torch_dev):
     wall = time.time() - t0
     ex.stop()
     print(json.dumps({"procs": procs}))
-    # this process' waves occupy CUs; the occupancy integral grows (PIDs are host-namespace)
-    assert any(p["cu_occupancy"] > 0 and p["cu_seconds"] > 0 for p in procs), procs
+    # this process' waves occupy CUs; the occupancy integral grows (PIDs are host-namespace).
+    # The instantaneous cu_occupancy of the last list can already be 0 (the loop ended
+    # with a synchronize), so the integral is the check.
+    assert any(p["cu_seconds"] > 0.2 for p in procs), procs
     # per-XCC accumulators: every one of the 8 dies is busy under a full-grid MFMA load
     assert len(snap["gfx_busy_xcc_window"]) == 8 and min(snap["gfx_busy_xcc_window"]) > 90, snap
     print(json.dumps({"window": w, "integrals": integ, "wall_s": wall}))

@@ -89,6 +89,10 @@ def main() -> int:
         env = dict(os.environ, KGS_NO_BUILD="1", KGS_AQL_LEAN=str(lean))
         if "slack" in opts:
             env["KGS_TIMERSLACK_NS"] = str(opts["slack"])
+        if "fence" in opts:
+            env["KGS_AQL_FENCE"] = opts["fence"]
+        if "signal" in opts:
+            env["KGS_AQL_SIGNAL"] = opts["signal"]
         pr = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
         ready = json.loads(pr.stdout.readline())
         assert ready.get("event") == "ready", ready
@@ -116,7 +120,8 @@ def main() -> int:
         rows.append(r)
 
     # spec hz:set:reader[:lean[:key=value...]]   keys: proc=<proc-every> (0 = no per-process tier),
-    # slack=<ns> (sampler timer slack), "off" = a phase with no exporter
+    # slack=<ns> (sampler timer slack), fence=sys|agent|none (AQL header fences of the
+    # reader's packets), signal=interrupt|poll (READ completion signals); "off" = no exporter
     specs = sys.argv[1:] or ["100:base:aqlprofile", "1000:base:aqlprofile", "8000:base:aqlprofile",
                              "100:full:aqlprofile", "1000:full:aqlprofile", "1000:base:none"]
     # The first exporter started in a fresh box slowed the graph replay by ≈38 % in
