@@ -359,6 +359,8 @@ def observed(m: dict) -> dict:
                      ("amdgpu_power_watts", "power_w"), ("amdgpu_gpu_clock_effective_mhz", "clock_mhz")):
         for lb, v in m.get(fam, []):
             out.setdefault(lb["gpu"], {})[key] = round(v, 2)
+    for lb, v in m.get("amdgpu_mfma_util_xcc_percent", []):  # XCD order 0..7
+        out.setdefault(lb["gpu"], {}).setdefault("mfma_util_xcd_pct", []).append(round(v, 1))
     return out
 
 

@@ -125,6 +125,17 @@ def run(a) -> int:
 
     signal.signal(signal.SIGTERM, _sig)
     signal.signal(signal.SIGINT, _sig)
+
+    # Counter hand-over, like a profiling pause: SIGUSR1 gives the hardware counters
+    # to another profiler (`kubectl exec <pod> -- kill -USR1 1`, then rocprofv3 --pmc
+    # on that node), SIGUSR2 takes them back.  The PMFW / per-process tiers keep going.
+    def _pmc(signum, _frame):
+        on = signum == signal.SIGUSR2
+        ex.set_pmc_enabled(on)
+        L.warning("hardware counters %s", "re-acquired" if on else "released to other profilers")
+
+    signal.signal(signal.SIGUSR1, _pmc)
+    signal.signal(signal.SIGUSR2, _pmc)
     if a.control_stdin:
         def _stdin():
             for line in sys.stdin:

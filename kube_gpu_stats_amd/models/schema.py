@@ -124,6 +124,9 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_samples_total", "counter", "Hardware-counter drains completed.", source="self"),
     F("kgs_pmc_errors_total", "counter", "Hardware-counter drains that failed.", source="self"),
     F("kgs_pmc_read_seconds_total", "counter", "Time spent draining hardware counters.", source="self"),
+    F("kgs_pmc_enabled", "gauge", "1 while the exporter holds the counters, 0 after handing them to another profiler "
+      "(SIGUSR1; SIGUSR2 takes them back).", source="self"),
+    F("kgs_pmc_releases_total", "counter", "Counter hand-overs to another profiler.", source="self"),
     F("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples.", source="self"),
     F("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read.", extra=("le",), source="self"),
     F("kgs_scrapes_total", "counter", "Scrapes rendered.", ("kubernetes_io_hostname",), "self"),

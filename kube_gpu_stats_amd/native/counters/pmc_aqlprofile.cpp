@@ -707,6 +707,13 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
         return -1;
       }
     }
+    // A re-open rebuilt a->events: the pipelined READ slots of the previous session
+    // (reused, same event list) must point at the new array.
+    for (int k = 0; k < 2; ++k)
+      if (a->pcmd[k]) {
+        a->pprof[k].events = a->events.data();
+        a->pprof[k].event_count = static_cast<uint32_t>(a->events.size());
+      }
     hsa_ven_amd_aqlprofile_profile_t& p = a->prof;
     p = hsa_ven_amd_aqlprofile_profile_t{};
     p.agent = a->agent;
@@ -726,8 +733,12 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     // memory, so size them generously.
     cmd_sz = std::max<uint32_t>(cmd_sz, 256u << 10);
     out_sz = std::max<uint32_t>(out_sz, 64u << 10);
-    a->cmd = host_alloc(a, cmd_sz);
-    a->out = host_alloc(a, out_sz);
+    // Re-open after kgs_pmc_close (the exporter handed the counters to another
+    // profiler and takes them back): reuse the buffers when they are big enough.
+    if (a->cmd && a->cmd_sz < cmd_sz) { hsa_amd_memory_pool_free(a->cmd); a->cmd = nullptr; }
+    if (a->out && a->out_sz < out_sz) { hsa_amd_memory_pool_free(a->out); a->out = nullptr; }
+    if (!a->cmd) a->cmd = host_alloc(a, cmd_sz);
+    if (!a->out) a->out = host_alloc(a, out_sz);
     if (!a->cmd || !a->out) {
       set_err(err, errlen, "host buffer allocation failed");
       return -1;

@@ -102,6 +102,10 @@ class Exporter {
   void pause_sampling();
   void resume_sampling();
   bool sampling() const;
+  // Hand the hardware counters to another profiler (false: every sampler STOPs
+  // its counting session and skips the PMC tier) or take them back (true).
+  void set_pmc_enabled(bool on);
+  bool pmc_enabled() const;
 
   // self metrics
   std::atomic<uint64_t> scrapes{0};
@@ -109,6 +113,7 @@ class Exporter {
   std::atomic<uint64_t> render_ns_last{0};
   std::atomic<uint64_t> http_requests{0};
   std::atomic<size_t> last_render_bytes_{64 * 1024};  // sizes the next render's buffer
+  std::atomic<bool> pmc_wanted_{true};
 
  private:
   void build_static_labels();

@@ -78,6 +78,12 @@ class CounterSource {
   virtual int sample(int dev, PmcSample& out) = 0;
   // Human-readable diagnostics (mode, per-counter instance counts, missing counters).
   virtual std::string info(int dev) const { return name(); }
+  // Hand the device's counters back (STOP: another profiler wants the perfmon
+  // block, as with `rocprofv3 --pmc`) / program them again (START; counts restart
+  // at 0).  Called only from the device's sampler thread.  0 = ok, <0 = failed or
+  // unsupported.
+  virtual int release(int dev) { return -1; }
+  virtual int acquire(int dev) { return -1; }
 };
 
 struct MockPmcConfig {

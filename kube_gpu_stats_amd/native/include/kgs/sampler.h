@@ -65,6 +65,13 @@ struct DeviceState {
   std::atomic<uint64_t> consecutive_errors{0};
   std::atomic<uint64_t> read_hist[kReadHistBuckets + 1] = {};
   std::atomic<int> cpu_pinned{-1};
+  // Counter hand-over (`kgs exporter` SIGUSR1 / SIGUSR2, /control/pmc/*): the
+  // control plane sets pmc_want; the sampler thread releases / re-acquires the
+  // counters itself and reports the state in pmc_on.
+  std::atomic<int> pmc_want{1};
+  std::atomic<int> pmc_on{0};
+  std::atomic<uint64_t> pmc_releases{0};
+  PmcSample pmc_base;  // totals carried over hand-overs (sampler thread only; survives pause/resume)
 
   std::shared_ptr<const std::vector<ProcInfo>> get_procs() const {
     std::lock_guard<std::mutex> g(slow_mu);
@@ -99,6 +106,9 @@ class Sampler {
   bool window_busy(int dev, double window_s, double& gfx_pct, double& umc_pct, int& n) const;
   // Counter-derived rates over the trailing window.
   bool window_pmc(int dev, double window_s, PmcRates& out) const;
+  // Ask every sampled device's thread to hand its counters to another profiler
+  // (false) or to take them back (true).  Takes effect within one tick.
+  void set_pmc_wanted(bool on);
 
  private:
   void run(int dev);

@@ -331,6 +331,8 @@ class PyExporter {
     py::gil_scoped_release r;
     ex_.resume_sampling();
   }
+  void set_pmc_enabled(bool on) { ex_.set_pmc_enabled(on); }
+  bool pmc_enabled() const { return ex_.pmc_enabled(); }
   bool sampling() const { return ex_.sampling(); }
 
  private:
@@ -381,7 +383,10 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("healthy", &PyExporter::healthy)
       .def("pause", &PyExporter::pause)
       .def("resume", &PyExporter::resume)
-      .def_property_readonly("sampling", &PyExporter::sampling);
+      .def_property_readonly("sampling", &PyExporter::sampling)
+      .def("set_pmc_enabled", &PyExporter::set_pmc_enabled, py::arg("on"),
+           "Hand the hardware counters to another profiler (False) or take them back (True)")
+      .def_property_readonly("pmc_enabled", &PyExporter::pmc_enabled);
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
   m.def("pmc_counter_names", [] {

@@ -134,6 +134,11 @@ void Exporter::resume_sampling() {
   if (sampler_) sampler_->start();
 }
 bool Exporter::sampling() const { return sampler_ && sampler_->running(); }
+void Exporter::set_pmc_enabled(bool on) {
+  pmc_wanted_.store(on);
+  if (sampler_) sampler_->set_pmc_wanted(on);
+}
+bool Exporter::pmc_enabled() const { return pmc_wanted_.load(); }
 
 void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
   std::lock_guard<std::mutex> g(mu_);

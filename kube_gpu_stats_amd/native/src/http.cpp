@@ -276,6 +276,9 @@ void HttpServer::loop() {
           if (target == "/control/pause") ex_->pause_sampling();
           else ex_->resume_sampling();
           respond(c, 200, "OK", "application/json", ex_->sampling() ? "{\"sampling\":true}" : "{\"sampling\":false}");
+        } else if (ex_->config().control_http && (target == "/control/pmc/release" || target == "/control/pmc/acquire")) {
+          ex_->set_pmc_enabled(target == "/control/pmc/acquire");
+          respond(c, 200, "OK", "application/json", ex_->pmc_enabled() ? "{\"pmc\":true}" : "{\"pmc\":false}");
         } else if (target == "/healthz") {
           const bool ok = ex_->healthy();
           respond(c, ok ? 200 : 503, ok ? "OK" : "Service Unavailable", "text/plain", ok ? "ok\n" : "no device sampled\n");

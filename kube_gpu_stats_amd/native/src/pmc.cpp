@@ -5,6 +5,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <ctime>
 #include <mutex>
@@ -68,10 +69,36 @@ namespace {
 
 class MockCounterSource final : public CounterSource {
  public:
-  MockCounterSource(const MockConfig& b, const MockPmcConfig& c) : b_(b), c_(c), t0_(mono_ns()) {}
+  MockCounterSource(const MockConfig& b, const MockPmcConfig& c, int n_dev)
+      : b_(b), c_(c), t0_(mono_ns()), restart_(static_cast<size_t>(std::max(n_dev, 1)), 0) {}
   std::string name() const override { return "mock"; }
+  int release(int) override { return 0; }
+  int acquire(int dev) override {  // like a re-START: the counts restart at 0
+    if (dev < 0 || static_cast<size_t>(dev) >= restart_.size()) return -1;
+    restart_[static_cast<size_t>(dev)] = mono_ns();
+    return 0;
+  }
   int sample(int dev, PmcSample& s) override {
     const int64_t now = mono_ns();
+    fill(dev, now, s);
+    const int64_t r = dev >= 0 && static_cast<size_t>(dev) < restart_.size() ? restart_[static_cast<size_t>(dev)] : 0;
+    if (r > 0) {
+      PmcSample z;
+      fill(dev, r, z);
+      for (int i = 0; i < kPmcCount; ++i) s.value[i] -= std::min(s.value[i], z.value[i]);
+      for (uint32_t x = 0; x < s.n_xcd; ++x) {
+        s.xcd_active[x] -= std::min(s.xcd_active[x], z.xcd_active[x]);
+        s.xcd_mfma[x] -= std::min(s.xcd_mfma[x], z.xcd_mfma[x]);
+      }
+    }
+    s.mono_ns = now;
+    s.read_ns = 1000;
+    return 0;
+  }
+
+ private:
+  // Cumulative counts since the source opened, at time `now`.
+  void fill(int dev, int64_t now, PmcSample& s) const {
     const double t = (now - t0_) * 1e-9;
     const double w = 6.283185307179586 / b_.util_period_s, ph = 0.7 * dev;
     // ∫ util/100 dt  (fraction-seconds)
@@ -95,15 +122,12 @@ class MockCounterSource final : public CounterSource {
       s.xcd_active[x] = static_cast<uint64_t>(clk * busy_s * w);
       s.xcd_mfma[x] = wsum > 0 ? static_cast<uint64_t>(s.value[kPmcMfmaBusy] * (w / wsum)) : 0;
     }
-    s.mono_ns = now;
-    s.read_ns = 1000;
-    return 0;
   }
 
- private:
   MockConfig b_;
   MockPmcConfig c_;
   int64_t t0_;
+  std::vector<int64_t> restart_;  // per device: time of the last acquire (0 = never released)
 };
 
 // --- dlopen bridge -------------------------------------------------------
@@ -165,21 +189,54 @@ class DlCounterSource final : public CounterSource {
     }
     sample_xcd_ = reinterpret_cast<sample_xcd_fn>(dlsym(lib_, "kgs_pmc_sample_xcd"));  // optional
     mask_ = mask;
+    for (int k = 0; k < nsel_; ++k) {
+      names_[k] = names[k];
+      is_max_[k] = is_max[k];
+    }
+    set_pipe_ = set_pipe;
+    pipelined_ = pipelined;
     int opened = 0;
-    handles_.assign(static_cast<size_t>(be.device_count()), -1);
+    handles_ = std::vector<std::atomic<int>>(static_cast<size_t>(be.device_count()));
+    for (auto& h : handles_) h.store(-1);
+    kfd_ids_.assign(static_cast<size_t>(be.device_count()), 0);
     for (int d : devices) {
-      ebuf[0] = 0;
-      const int h = open_(be.info(d).kfd_gpu_id, names, is_max, nsel_, ebuf, sizeof ebuf);
-      handles_[static_cast<size_t>(d)] = h;
-      if (h >= 0) ++opened;
-      else err += "dev" + std::to_string(d) + ": " + ebuf + "; ";
-      if (h >= 0 && pipelined && set_pipe) {
-        ebuf[0] = 0;
-        if (set_pipe(h, 1, ebuf, sizeof ebuf) != 0)  // stays synchronous, still usable
-          err += "dev" + std::to_string(d) + " pipelined reads unavailable: " + ebuf + "; ";
-      }
+      kfd_ids_[static_cast<size_t>(d)] = be.info(d).kfd_gpu_id;
+      std::string e;
+      if (open_dev(d, e) == 0) ++opened;
+      else err += "dev" + std::to_string(d) + ": " + e + "; ";
+      if (!e.empty() && handles_[static_cast<size_t>(d)] >= 0) err += "dev" + std::to_string(d) + " " + e + "; ";
     }
     return opened > 0;
+  }
+
+  // Open the device's counting session (START), pipelined if asked.  A failed
+  // switch to pipelined reads leaves a usable synchronous session (note in err).
+  int open_dev(int d, std::string& err) {
+    char ebuf[512] = {};
+    const int h = open_(kfd_ids_[static_cast<size_t>(d)], names_, is_max_, nsel_, ebuf, sizeof ebuf);
+    handles_[static_cast<size_t>(d)] = h;
+    if (h < 0) {
+      err = ebuf;
+      return -1;
+    }
+    if (pipelined_ && set_pipe_) {
+      ebuf[0] = 0;
+      if (set_pipe_(h, 1, ebuf, sizeof ebuf) != 0) err = std::string("pipelined reads unavailable: ") + ebuf;
+    }
+    return 0;
+  }
+
+  int release(int dev) override {
+    if (dev < 0 || dev >= static_cast<int>(handles_.size()) || handles_[static_cast<size_t>(dev)] < 0) return -1;
+    close_(handles_[static_cast<size_t>(dev)]);
+    handles_[static_cast<size_t>(dev)] = -1;
+    return 0;
+  }
+  int acquire(int dev) override {
+    if (dev < 0 || dev >= static_cast<int>(handles_.size())) return -1;
+    if (handles_[static_cast<size_t>(dev)] >= 0) return 0;
+    std::string e;
+    return open_dev(dev, e);
   }
 
   std::string name() const override { return name_; }
@@ -219,21 +276,28 @@ class DlCounterSource final : public CounterSource {
   sample_fn sample_ = nullptr;
   sample_ts_fn sample_ts_ = nullptr;
   sample_xcd_fn sample_xcd_ = nullptr;
+  pipelined_fn set_pipe_ = nullptr;
+  bool pipelined_ = false;
+  const char* names_[kPmcCount] = {};
+  int is_max_[kPmcCount] = {};
+  std::vector<uint64_t> kfd_ids_;
   int sel_[kPmcCount] = {};  // reader's counter k is PmcIndex sel_[k]
   int reader_idx_[kPmcCount] = {};  // inverse: PmcIndex → reader counter, -1 not read
   int nsel_ = 0;
   uint32_t mask_ = 0;
   close_fn close_ = nullptr;
   info_fn info_ = nullptr;
-  std::vector<int> handles_;
+  // Written by the device's sampler thread (release / acquire), read by info()
+  // from the HTTP / control threads.
+  std::vector<std::atomic<int>> handles_;
   std::string name_;
 };
 
 }  // namespace
 
-std::unique_ptr<CounterSource> make_mock_counter_source(const Backend&, const MockConfig& bcfg,
+std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,
                                                         const MockPmcConfig& cfg) {
-  return std::make_unique<MockCounterSource>(bcfg, cfg);
+  return std::make_unique<MockCounterSource>(bcfg, cfg, be.device_count());
 }
 
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,

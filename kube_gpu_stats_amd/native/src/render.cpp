@@ -529,6 +529,13 @@ void Exporter::render(std::string& out) {
   for (int d : ids) w.line("kgs_pmc_read_seconds_total", dev_labels_[d], nullptr, snaps[d].I.pmc_read_seconds);
   w.head("kgs_pmc_errors_total", "counter", "Hardware-counter drains that failed");
   for (int d : ids) w.line_u("kgs_pmc_errors_total", dev_labels_[d], nullptr, snaps[d].I.pmc_errors);
+  if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
+    w.head("kgs_pmc_enabled", "gauge",
+           "1 while the exporter holds the GPU's hardware counters, 0 after it handed them to another profiler");
+    for (int d : ids) w.line_u("kgs_pmc_enabled", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_on.load()));
+    w.head("kgs_pmc_releases_total", "counter", "Times the counters were handed to another profiler (SIGUSR1, /control/pmc/release)");
+    for (int d : ids) w.line_u("kgs_pmc_releases_total", dev_labels_[d], nullptr, S.state(d).pmc_releases.load());
+  }
   w.head("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples");
   for (int d : ids) w.line("kgs_sampled_seconds_total", dev_labels_[d], nullptr, snaps[d].I.sampled_seconds);
   w.head("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read");

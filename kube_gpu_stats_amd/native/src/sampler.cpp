@@ -80,7 +80,12 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
       if (d >= 0 && d < n) dev_ids_.push_back(d);
   }
   if (cfg_.hz <= 0) cfg_.hz = 1;
+  for (int d : dev_ids_) states_[static_cast<size_t>(d)]->pmc_on.store(cfg_.pmc && pmc_ ? 1 : 0);
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+}
+
+void Sampler::set_pmc_wanted(bool on) {
+  for (int d : dev_ids_) states_[static_cast<size_t>(d)]->pmc_want.store(on ? 1 : 0);
 }
 
 Sampler::~Sampler() {
@@ -193,6 +198,8 @@ void Sampler::run(int dev) {
   }
   int64_t next = mono_ns();
   int late_streak = 0;  // consecutive overrun ticks
+  PmcSample& pmc_base = st.pmc_base;
+  int64_t last_acquire_fail_ns = 0;
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;
   std::unordered_map<uint32_t, double> cu_seconds;  // pid -> ∫ occupancy share dt
@@ -260,12 +267,42 @@ void Sampler::run(int dev) {
     }
 
     // ---- PMC tier ------------------------------------------------------
+    bool pmc_now = false;
     if (cfg_.pmc && pmc_) {
+      const int want = st.pmc_want.load(std::memory_order_relaxed);
+      if (want != st.pmc_on.load(std::memory_order_relaxed)) {
+        const int64_t now_c = mono_ns();
+        if (!want) {
+          pmc_->release(dev);  // a failed STOP still ends our READs
+          st.pmc_on.store(0);
+          st.pmc_releases.fetch_add(1, std::memory_order_relaxed);
+          // The next START restarts the counts at 0: carry the published totals
+          // as a base so the exported counters stay monotonic.
+          PmcSample last;
+          if (st.pmc_latest.load(last)) pmc_base = last;
+        } else if (now_c - last_acquire_fail_ns >= 1000000000LL) {  // after a failed START: ≤ 1 retry/s
+          if (pmc_->acquire(dev) == 0) {
+            st.pmc_on.store(1);
+          } else {
+            last_acquire_fail_ns = now_c;
+            ++I.pmc_errors;
+          }
+        }
+      }
+      pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
+    }
+    if (pmc_now) {
       PmcSample ps;
       const int64_t p0 = mono_ns();
       const int prc = pmc_->sample(dev, ps);
       I.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
       if (prc == 0) {
+        for (int i = 0; i < kPmcCount; ++i) ps.value[i] += pmc_base.value[i];
+        if (pmc_base.n_xcd == ps.n_xcd)
+          for (uint32_t x = 0; x < ps.n_xcd && x < static_cast<uint32_t>(kMaxXcc); ++x) {
+            ps.xcd_active[x] += pmc_base.xcd_active[x];
+            ps.xcd_mfma[x] += pmc_base.xcd_mfma[x];
+          }
         ps.seq = ++pmc_seq;
         st.pmc_ring.push(ps);
         if (ps.mono_ns - last_slow_ns >= kPmcSlowNs) {

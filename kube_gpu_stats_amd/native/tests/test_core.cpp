@@ -9,8 +9,9 @@
 //     window_busy / window_pmc / integ concurrently, then stop().
 //  4. Recovery: a device that resets mid-run is re-opened and re-baselined.
 //  6. Exporter: concurrent /metrics renders and /counters streams while the
-//     samplers run at 2 kHz, the slow tier republishes link tables and the node
-//     name changes (render caches under the exporter mutex).
+//     samplers run at 2 kHz, the slow tier republishes link tables, the node
+//     name changes (render caches under the exporter mutex) and the counters are
+//     handed over and taken back.
 //  5. PMFW table parser fuzz (ASAN build): random, truncated and mutated
 //     v1.8-shaped buffers, each in an exactly-sized heap block so any read past
 //     `len` is caught; the parser must reject or parse, never overrun.
@@ -286,6 +287,7 @@ static void test_exporter_concurrent() {
   });
   for (int i = 0; i < 40; ++i) {
     ex.set_node_name(i % 2 ? "node-b" : "node-a");
+    if (i % 4 == 0) ex.set_pmc_enabled(i % 8 != 0);  // counter hand-over while the samplers run
     std::this_thread::sleep_for(std::chrono::milliseconds(25));
   }
   stop = true;
@@ -295,6 +297,8 @@ static void test_exporter_concurrent() {
   ex.render(out);
   CHECK(out.find("kubernetes_io_hostname=\"node-a\"") == std::string::npos);  // last rename: node-b
   CHECK(renders.load() > 10 && streams.load() > 10);
+  CHECK(out.find("kgs_pmc_enabled{gpu=\"0\"") != std::string::npos);
+  CHECK(ex.sampler()->state(0).pmc_releases.load() == 5);  // released at i = 0, 8, 16, 24, 32
   std::printf("exporter concurrent ok (%d renders, %d streams)\n", renders.load(), streams.load());
 }
 

@@ -333,3 +333,64 @@ def test_metrics_gzip_negotiation(mock_exporter):
     r = c.getresponse()
     assert r.getheader("Content-Encoding") is None and b"kgs_up" in r.read()
     c.close()
+
+
+def test_counter_handover_keeps_totals_monotonic(mock_exporter):
+    """set_pmc_enabled(False): the sampler STOPs its counters (another profiler may
+    program them) and skips the PMC tier; True re-STARTs them.  Exported totals carry
+    over the restart, so counters stay monotonic."""
+    ex = mock_exporter(n_gpus=2, hz=500, pmc_source="mock", proc_every=0, link_every=0,
+                       mock={"util_base": 50, "util_amp": 0.0001})
+    time.sleep(0.3)
+    tot = lambda m: {lb["gpu"]: v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT"}  # noqa: E731
+    m0 = parse_text(ex.render())
+    assert {lb["gpu"]: v for lb, v in m0["kgs_pmc_enabled"]} == {"0": 1.0, "1": 1.0}
+    ex.set_pmc_enabled(False)
+    assert ex.pmc_enabled is False
+    time.sleep(0.1)
+    m1 = parse_text(ex.render())
+    n1 = ex.integrals(0)["pmc_samples"]
+    time.sleep(0.3)
+    m2 = parse_text(ex.render())
+    assert ex.integrals(0)["pmc_samples"] == n1                      # no READs while released
+    assert {lb["gpu"]: v for lb, v in m2["kgs_pmc_enabled"]} == {"0": 0.0, "1": 0.0}
+    assert {lb["gpu"]: v for lb, v in m2["kgs_pmc_releases_total"]} == {"0": 1.0, "1": 1.0}
+    assert ex.integrals(1)["reads"] > 0                              # PMFW tier keeps sampling
+    ex.set_pmc_enabled(True)
+    time.sleep(0.4)
+    m3 = parse_text(ex.render())
+    assert ex.integrals(0)["pmc_samples"] > n1 + 50
+    assert {lb["gpu"]: v for lb, v in m3["kgs_pmc_enabled"]} == {"0": 1.0, "1": 1.0}
+    for g in ("0", "1"):
+        assert tot(m0)[g] <= tot(m1)[g] <= tot(m2)[g] < tot(m3)[g]   # monotonic across the re-START
+    w = ex.window(0, 0.2)
+    assert w["gpu_active_pct"] == pytest.approx(50, abs=3) and w["mfma_util_pct"] == pytest.approx(60, abs=3)
+
+
+def test_exporter_process_counter_handover_signals(tmp_path):
+    """`kgs exporter`: SIGUSR1 releases the counters, SIGUSR2 takes them back."""
+    import os
+    import signal
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--backend", "mock",
+                          "--mock-gpus", "1", "--pmc", "mock", "--hz", "200", "--listen", "127.0.0.1:0",
+                          "--control-stdin", "--no-pin-numa"], cwd=repo, stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        ready = json.loads(p.stdout.readline())
+        port = ready["port"]
+        en = lambda: parse_text(get(port, "/metrics").read().decode())["kgs_pmc_enabled"][0][1]  # noqa: E731
+        assert en() == 1.0
+        p.send_signal(signal.SIGUSR1)
+        time.sleep(0.3)
+        assert en() == 0.0
+        p.send_signal(signal.SIGUSR2)
+        time.sleep(0.3)
+        assert en() == 1.0
+    finally:
+        p.stdin.write("quit\n")
+        p.stdin.flush()
+        p.communicate(timeout=30)

@@ -327,6 +327,68 @@ def test_per_xcd_counters_follow_xcc_gated_load(torch_dev):
         print(out[-1500:])
 
 
+def test_counter_handover_stop_and_restart(torch_dev):
+    """SIGUSR1 makes the aqlprofile reader STOP its counting session (another
+    profiler may program the counters); SIGUSR2 re-STARTs it.  Counters read right
+    after the re-START, and the exported totals stay monotonic."""
+    import signal
+
+    import torch
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
+                             "--hz", "1000", "--pmc", "aqlprofile", "--control-stdin", "--bdfs", bdf,
+                             "--proc-every", "0", "--link-every", "0"],
+                            cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
+
+    def load(secs):
+        t0 = time.time()
+        while time.time() - t0 < secs:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
+        sc = Scraper("127.0.0.1", ready["port"])
+        one = lambda m, f: m[f][0][1]  # noqa: E731
+        load(1.2)
+        m0 = parse_text(sc.get())
+        proc.send_signal(signal.SIGUSR1)
+        time.sleep(0.3)
+        m1 = parse_text(sc.get())
+        time.sleep(0.5)
+        m2 = parse_text(sc.get())
+        proc.send_signal(signal.SIGUSR2)
+        load(1.5)
+        m3 = parse_text(sc.get())
+        print(json.dumps({k: [one(m, "amdgpu_mfma_util_percent"), one(m, "kgs_pmc_enabled"),
+                              one(m, "kgs_pmc_samples_total")] for k, m in (("m0", m0), ("m1", m1), ("m2", m2),
+                                                                           ("m3", m3))}))
+        assert one(m0, "amdgpu_mfma_util_percent") > 50 and one(m0, "kgs_pmc_enabled") == 1
+        assert one(m2, "kgs_pmc_enabled") == 0 and one(m2, "kgs_pmc_samples_total") == one(m1, "kgs_pmc_samples_total")
+        assert one(m3, "kgs_pmc_enabled") == 1 and one(m3, "kgs_pmc_releases_total") == 1
+        assert one(m3, "amdgpu_mfma_util_percent") > 50                    # counters read right after re-START
+        grbm = lambda m: [v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT"][0]  # noqa: E731
+        assert grbm(m0) <= grbm(m2) < grbm(m3)
+    finally:
+        out = err = ""
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            out, err = proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            out, err = proc.communicate()
+        print(out[-1500:])
+        print(err[-1500:])
+
+
 def test_hbm_bandwidth_estimate_tracks_stream_kernels(N, torch_dev):
     """amdgpu_hbm_bandwidth_bytes_per_second (UMC activity × MI355X calibration)
     agrees with the bytes a triad loop moves, and reads ~0 under a pure MFMA load."""
