@@ -45,6 +45,10 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                     "full (+ TA vector-memory busy, 560 reads: costs dispatch-bound workloads more)")
     add_flag(ap, "pmc-pipeline", True, "aqlprofile reader: overlap each counter READ's CP round trip with the "
                                        "tick sleep (the sample is stamped with the CP read time)")
+    add_flag(ap, "pmc-reclaim-s", 10.0, "re-START the counters after they stalled this long (a foreign profiler "
+                                        "stopped or reprogrammed them; 0 = never, SIGUSR1 hand-over disables it)")
+    add_flag(ap, "pmc-refresh-s", 60.0, "re-START (reprogram) the counters this often, in case another profiler "
+                                        "changed their selects (0 = never; SIGUSR1 hand-over disables it)")
     add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
     add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
     add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
@@ -79,6 +83,8 @@ def config_from_args(a) -> dict:
         "pmc_pipeline": a.pmc_pipeline,
         "pmc_set": a.pmc_set,
         "pmc_lean": a.pmc_lean,
+        "pmc_reclaim_s": a.pmc_reclaim_s,
+        "pmc_refresh_s": a.pmc_refresh_s,
         "listen_addr": host or "0.0.0.0",
         "port": int(port),
         "node_name": a.node_name,

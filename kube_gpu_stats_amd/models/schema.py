@@ -127,6 +127,11 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_enabled", "gauge", "1 while the exporter holds the counters, 0 after handing them to another profiler "
       "(SIGUSR1; SIGUSR2 takes them back).", source="self"),
     F("kgs_pmc_releases_total", "counter", "Counter hand-overs to another profiler.", source="self"),
+    F("kgs_pmc_stalled", "gauge", "1 while GRBM_COUNT shows no plausible clock: another profiler stopped or "
+      "reprogrammed the counters (the counter-tier gauges are withheld meanwhile).", source="self"),
+    F("kgs_pmc_reclaims_total", "counter", "Automatic counter re-STARTs after a stall of --pmc-reclaim-s.", source="self"),
+    F("kgs_pmc_refreshes_total", "counter", "Periodic counter re-STARTs (--pmc-refresh-s): reprogram selects that "
+      "another profiler may have changed without stalling GRBM_COUNT.", source="self"),
     F("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples.", source="self"),
     F("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read.", extra=("le",), source="self"),
     F("kgs_scrapes_total", "counter", "Scrapes rendered.", ("kubernetes_io_hostname",), "self"),

@@ -93,6 +93,7 @@ struct MockPmcConfig {
   uint32_t mask = kPmcSetFull;  // counters the mock "reads"
   int n_xcd = 8;                // per-XCD breakdown (0 = none)
   double xcd_skew = 0.0;        // XCD x is active (1 - skew·x) of XCD 0's cycles
+  double freeze_after_s = 0.0;  // counts stop this long after each (re)START, as after a foreign STOP (0 = never)
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,

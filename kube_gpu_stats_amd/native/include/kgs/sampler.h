@@ -33,6 +33,17 @@ struct SamplerConfig {
   int link_every = 100;        // slow tier every N ticks (0 disables)
   bool pin_numa = true;
   bool pmc = false;            // drain hardware counters every tick
+  // A foreign profiler (rocprofv3 --pmc) that STOPs or reprograms the perfmon
+  // block leaves the exporter reading frozen or foreign counts (run r44).  The
+  // counters are "stalled" when GRBM_COUNT has not advanced at a plausible clock
+  // for kPmcStallNs; after pmc_reclaim_s of stall the sampler re-STARTs its
+  // session (0 = never).  While handed over (SIGUSR1) nothing is reclaimed.
+  double pmc_reclaim_s = 10.0;
+  // A profiler that reprograms the counter selects can leave GRBM_COUNT counting
+  // something clock-like (no stall) while our MFMA slot counts its event (run
+  // r45: MFMA util 0 under load).  Nothing in the READ shows that, so the session
+  // is also re-STARTed (selects reprogrammed) every pmc_refresh_s (0 = never).
+  double pmc_refresh_s = 60.0;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
 };
@@ -44,6 +55,8 @@ constexpr size_t kPmcSlowRing = 2048;
 constexpr size_t kPmcRing = 8192;       // raw counter stream: ≥1 s at 8 kHz (/counters)
 constexpr int64_t kPmcSlowNs = 5000000;  // 5 ms → ≥10 s of history
 constexpr int kReadHistBuckets = 12;    // backend read latency histogram
+constexpr int64_t kPmcStallNs = 500000000;  // GRBM_COUNT without a plausible clock this long = stalled
+constexpr double kPlausibleMhzLo = 100.0, kPlausibleMhzHi = 4000.0;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 
 struct DeviceState {
@@ -71,6 +84,9 @@ struct DeviceState {
   std::atomic<int> pmc_want{1};
   std::atomic<int> pmc_on{0};
   std::atomic<uint64_t> pmc_releases{0};
+  std::atomic<int> pmc_stalled{0};          // counters frozen / implausible for ≥ kPmcStallNs
+  std::atomic<uint64_t> pmc_reclaims{0};    // automatic re-STARTs after a stall
+  std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
   PmcSample pmc_base;  // totals carried over hand-overs (sampler thread only; survives pause/resume)
 
   std::shared_ptr<const std::vector<ProcInfo>> get_procs() const {

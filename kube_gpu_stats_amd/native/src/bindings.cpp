@@ -44,6 +44,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.vmem_frac = get<double>(m, "vmem_frac", c.mock_pmc.vmem_frac);
     c.mock_pmc.n_xcd = get<int>(m, "n_xcd", c.mock_pmc.n_xcd);
     c.mock_pmc.xcd_skew = get<double>(m, "xcd_skew", c.mock_pmc.xcd_skew);
+    c.mock_pmc.freeze_after_s = get<double>(m, "freeze_after_s", c.mock_pmc.freeze_after_s);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -51,6 +52,8 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.link_every = get<int>(d, "link_every", c.sampler.link_every);
   c.sampler.pin_numa = get<bool>(d, "pin_numa", c.sampler.pin_numa);
   c.sampler.max_backoff_ms = get<int>(d, "max_backoff_ms", c.sampler.max_backoff_ms);
+  c.sampler.pmc_reclaim_s = get<double>(d, "pmc_reclaim_s", c.sampler.pmc_reclaim_s);
+  c.sampler.pmc_refresh_s = get<double>(d, "pmc_refresh_s", c.sampler.pmc_refresh_s);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
   c.bdfs = get<std::vector<std::string>>(d, "bdfs", c.bdfs);
   c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);

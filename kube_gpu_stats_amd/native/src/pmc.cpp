@@ -80,8 +80,10 @@ class MockCounterSource final : public CounterSource {
   }
   int sample(int dev, PmcSample& s) override {
     const int64_t now = mono_ns();
-    fill(dev, now, s);
     const int64_t r = dev >= 0 && static_cast<size_t>(dev) < restart_.size() ? restart_[static_cast<size_t>(dev)] : 0;
+    int64_t t = now;
+    if (c_.freeze_after_s > 0) t = std::min(now, (r > 0 ? r : t0_) + static_cast<int64_t>(c_.freeze_after_s * 1e9));
+    fill(dev, t, s);
     if (r > 0) {
       PmcSample z;
       fill(dev, r, z);

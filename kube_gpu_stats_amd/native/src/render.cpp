@@ -183,7 +183,9 @@ void Exporter::render(std::string& out) {
     st.integ.load(x.I);
     x.busy = x.have && S.window_busy(d, cfg_.window_s, x.g, x.u, x.n);
     x.pmc_have = st.pmc_latest.load(x.p);
-    x.pmc_rates = x.pmc_have && S.window_pmc(d, cfg_.window_s, x.r);
+    // Stalled counters (a foreign profiler STOPped / reprogrammed them) give no
+    // rate gauges rather than wrong ones; the raw totals and kgs_pmc_stalled stay.
+    x.pmc_rates = x.pmc_have && !st.pmc_stalled.load(std::memory_order_relaxed) && S.window_pmc(d, cfg_.window_s, x.r);
   }
 
   // ---- reference-compatible series (F5) ---------------------------------
@@ -535,6 +537,13 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_enabled", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_on.load()));
     w.head("kgs_pmc_releases_total", "counter", "Times the counters were handed to another profiler (SIGUSR1, /control/pmc/release)");
     for (int d : ids) w.line_u("kgs_pmc_releases_total", dev_labels_[d], nullptr, S.state(d).pmc_releases.load());
+    w.head("kgs_pmc_stalled", "gauge",
+           "1 while GRBM_COUNT shows no plausible clock (another profiler stopped or reprogrammed the counters)");
+    for (int d : ids) w.line_u("kgs_pmc_stalled", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_stalled.load()));
+    w.head("kgs_pmc_reclaims_total", "counter", "Automatic counter re-STARTs after a stall (--pmc-reclaim-s)");
+    for (int d : ids) w.line_u("kgs_pmc_reclaims_total", dev_labels_[d], nullptr, S.state(d).pmc_reclaims.load());
+    w.head("kgs_pmc_refreshes_total", "counter", "Periodic counter re-STARTs that reprogram the selects (--pmc-refresh-s)");
+    for (int d : ids) w.line_u("kgs_pmc_refreshes_total", dev_labels_[d], nullptr, S.state(d).pmc_refreshes.load());
   }
   w.head("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples");
   for (int d : ids) w.line("kgs_sampled_seconds_total", dev_labels_[d], nullptr, snaps[d].I.sampled_seconds);

@@ -200,6 +200,11 @@ void Sampler::run(int dev) {
   int late_streak = 0;  // consecutive overrun ticks
   PmcSample& pmc_base = st.pmc_base;
   int64_t last_acquire_fail_ns = 0;
+  bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
+  uint64_t prev_ps_count = 0;
+  int64_t prev_ps_ns = 0;
+  int64_t last_plausible_ns = mono_ns();
+  int64_t last_start_ns = mono_ns();  // last (re)START of the counter session
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;
   std::unordered_map<uint32_t, double> cu_seconds;  // pid -> ∫ occupancy share dt
@@ -275,6 +280,7 @@ void Sampler::run(int dev) {
         if (!want) {
           pmc_->release(dev);  // a failed STOP still ends our READs
           st.pmc_on.store(0);
+          st.pmc_stalled.store(0);
           st.pmc_releases.fetch_add(1, std::memory_order_relaxed);
           // The next START restarts the counts at 0: carry the published totals
           // as a base so the exported counters stay monotonic.
@@ -283,6 +289,9 @@ void Sampler::run(int dev) {
         } else if (now_c - last_acquire_fail_ns >= 1000000000LL) {  // after a failed START: ≤ 1 retry/s
           if (pmc_->acquire(dev) == 0) {
             st.pmc_on.store(1);
+            have_prev_ps = false;
+            last_plausible_ns = now_c;
+            last_start_ns = now_c;
           } else {
             last_acquire_fail_ns = now_c;
             ++I.pmc_errors;
@@ -297,6 +306,18 @@ void Sampler::run(int dev) {
       const int prc = pmc_->sample(dev, ps);
       I.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
       if (prc == 0) {
+        // Stall detection: GRBM_COUNT free-runs at the shader clock while our
+        // session is programmed; frozen or foreign counts give no plausible clock.
+        if (have_prev_ps && ps.mono_ns > prev_ps_ns) {
+          const uint64_t raw = ps.value[kPmcGrbmCount];
+          const double mhz = raw >= prev_ps_count ? (raw - prev_ps_count) * 1e3 / (ps.mono_ns - prev_ps_ns) : 0.0;
+          if (mhz >= kPlausibleMhzLo && mhz <= kPlausibleMhzHi) last_plausible_ns = ps.mono_ns;
+        }
+        prev_ps_count = ps.value[kPmcGrbmCount];
+        prev_ps_ns = ps.mono_ns;
+        have_prev_ps = true;
+        const int64_t stall = ps.mono_ns - last_plausible_ns;
+        st.pmc_stalled.store(stall >= kPmcStallNs ? 1 : 0, std::memory_order_relaxed);
         for (int i = 0; i < kPmcCount; ++i) ps.value[i] += pmc_base.value[i];
         if (pmc_base.n_xcd == ps.n_xcd)
           for (uint32_t x = 0; x < ps.n_xcd && x < static_cast<uint32_t>(kMaxXcc); ++x) {
@@ -311,6 +332,25 @@ void Sampler::run(int dev) {
         }
         st.pmc_latest.store(ps);
         ++I.pmc_samples;
+        const bool reclaim = cfg_.pmc_reclaim_s > 0 && stall >= static_cast<int64_t>(cfg_.pmc_reclaim_s * 1e9);
+        const bool refresh = cfg_.pmc_refresh_s > 0 &&
+                             ps.mono_ns - last_start_ns >= static_cast<int64_t>(cfg_.pmc_refresh_s * 1e9);
+        if ((reclaim || refresh) && st.pmc_want.load(std::memory_order_relaxed)) {
+          // STOP + START our session (selects reprogrammed, counts from 0); totals
+          // carry over like a hand-over.
+          pmc_base = ps;
+          pmc_->release(dev);
+          last_start_ns = ps.mono_ns;
+          if (pmc_->acquire(dev) == 0) {
+            (reclaim ? st.pmc_reclaims : st.pmc_refreshes).fetch_add(1, std::memory_order_relaxed);
+          } else {
+            st.pmc_on.store(0);
+            last_acquire_fail_ns = ps.mono_ns;
+            ++I.pmc_errors;
+          }
+          have_prev_ps = false;
+          last_plausible_ns = mono_ns();  // a full reclaim period before the next one
+        }
       } else {
         ++I.pmc_errors;
       }

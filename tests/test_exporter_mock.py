@@ -394,3 +394,48 @@ def test_exporter_process_counter_handover_signals(tmp_path):
         p.stdin.write("quit\n")
         p.stdin.flush()
         p.communicate(timeout=30)
+
+
+def test_stalled_counters_are_withheld_then_reclaimed(mock_exporter):
+    """A foreign profiler that STOPs the counters leaves GRBM_COUNT frozen (run r44).
+    The exporter flags kgs_pmc_stalled, withholds the counter-tier gauges instead of
+    publishing zeros, and re-STARTs its session after --pmc-reclaim-s."""
+    ex = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0, window_s=0.2,
+                       pmc_reclaim_s=1.2, mock={"util_base": 50, "util_amp": 0.0001},
+                       mock_pmc={"freeze_after_s": 0.3})
+    time.sleep(0.25)
+    m = parse_text(ex.render())
+    assert m["kgs_pmc_stalled"][0][1] == 0 and "amdgpu_mfma_util_percent" in m
+    time.sleep(0.75)  # frozen since 0.3 s: stalled after another 0.5 s
+    m = parse_text(ex.render())
+    assert m["kgs_pmc_stalled"][0][1] == 1
+    assert "amdgpu_mfma_util_percent" not in m and "amdgpu_gpu_clock_effective_mhz" not in m
+    grbm = lambda mm: [v for lb, v in mm["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT"][0]  # noqa: E731
+    before = grbm(m)
+    t0 = time.time()
+    while time.time() - t0 < 3 and parse_text(ex.render())["kgs_pmc_reclaims_total"][0][1] < 1:
+        time.sleep(0.05)
+    time.sleep(0.15)  # counting again for 0.3 s after the re-START
+    m = parse_text(ex.render())
+    assert m["kgs_pmc_reclaims_total"][0][1] >= 1 and m["kgs_pmc_stalled"][0][1] == 0
+    assert grbm(m) > before                      # totals continue monotonically after the re-START
+    assert m["amdgpu_mfma_util_percent"][0][1] == pytest.approx(60, abs=5)
+    off = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0, pmc_reclaim_s=0,
+                        mock_pmc={"freeze_after_s": 0.2})
+    time.sleep(1.0)
+    m = parse_text(off.render())
+    assert m["kgs_pmc_stalled"][0][1] == 1 and m["kgs_pmc_reclaims_total"][0][1] == 0  # reclaim disabled
+
+
+def test_periodic_counter_refresh(mock_exporter):
+    """--pmc-refresh-s re-STARTs the session on a schedule (selects reprogrammed);
+    totals and rates are continuous across it."""
+    ex = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0, window_s=0.2,
+                       pmc_refresh_s=0.3, mock={"util_base": 50, "util_amp": 0.0001})
+    time.sleep(1.1)
+    m = parse_text(ex.render())
+    assert 2 <= m["kgs_pmc_refreshes_total"][0][1] <= 4 and m["kgs_pmc_reclaims_total"][0][1] == 0
+    assert m["kgs_pmc_stalled"][0][1] == 0
+    assert m["amdgpu_gpu_active_percent"][0][1] == pytest.approx(50, abs=5)
+    g = [v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT"][0]
+    assert g == pytest.approx(2100e6 * 1.1, rel=0.1)  # 2100 MHz mock clock × ≈1.1 s, refreshes included
