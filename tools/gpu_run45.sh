@@ -11,12 +11,12 @@ step() {
   echo "== $name rc=$rc"; tail -1 "gpurun_out/r45/${name}.log" | cut -c1-200
   if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step pytest_gpu 400 python -u -m pytest tests -m gpu -x -v -s --timeout 120 --timeout-method thread
-step bench_8k 200 python bench.py --out gpurun_out/r45/bench_8k.json
+
+
 USER_CMD='import torch; a=torch.randn(4096,4096,device="cuda"); [a@a for _ in range(20)]; torch.cuda.synchronize(); print("user profiler run ok")'
 metrics() { curl -s 127.0.0.1:19559/metrics | grep -E "^kgs_pmc_(enabled|stalled|reclaims_total|samples_total)|^amdgpu_gpu_clock_effective|^amdgpu_mfma_util_percent" > gpurun_out/r45/m_$1.txt; }
 timeout -k 10 300 python -m kube_gpu_stats_amd.cli exporter --listen 127.0.0.1:19559 --hz 8000 --pmc aqlprofile \
-   --pmc-reclaim-s 5 --proc-every 800 --link-every 8000 > gpurun_out/r45/exporter.log 2>&1 &
+   --pmc-reclaim-s 5 --pmc-refresh-s 0 --proc-every 800 --link-every 8000 > gpurun_out/r45/exporter.log 2>&1 &
 TP=$!
 sleep 8
 metrics start
@@ -32,8 +32,11 @@ ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 28
 t0 = time.time()
 while time.time() - t0 < 2.0:
     ls.run_mfma(); torch.cuda.synchronize()
+import urllib.request
+body = urllib.request.urlopen('http://127.0.0.1:19559/metrics', timeout=5).read().decode()
+print([l for l in body.splitlines() if l.startswith(('amdgpu_mfma_util_percent', 'amdgpu_gpu_active_percent'))])
 print('mfma load done')" > gpurun_out/r45/mfma_load.log 2>&1
 metrics after_load
 kill $(pgrep -P $TP); wait $TP
 for t in start after_user after_reclaim after_load; do echo "-- $t"; cat gpurun_out/r45/m_$t.txt | sed 's/{gpu="0",uuid="[^"]*"}//'; done
-rm -rf gpurun_out/r45/prof_user; du -sh gpurun_out
+cat gpurun_out/r45/mfma_load.log | cut -c1-300; rm -rf gpurun_out/r45/prof_user; du -sh gpurun_out
