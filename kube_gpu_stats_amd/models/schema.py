@@ -97,6 +97,9 @@ CATALOG: tuple[Family, ...] = (
       "the READ buffer's XCC-major order, verified against an XCC-gated load).  An XCD left idle while others "
       "saturate is a workgroup→XCD mapping problem, invisible in the device-wide gauges.",
       extra=("xcc",), source="rocprofiler", tier="pmc"),
+    F("amdgpu_vmem_busy_xcc_percent", "gauge",
+      "Vector-memory address unit (TA) busy % of one XCD's active cycles, mean over its CUs (window; --pmc-set full).",
+      extra=("xcc",), source="rocprofiler", tier="pmc"),
     F("amdgpu_gpu_active_xcc_percent", "gauge",
       "GRBM GUI-active % of clocks of one XCD (window): a dispatch is in flight on it.  A chip-wide kernel keeps "
       "every XCD active, even one with no waves; the MFMA split shows where waves run.",

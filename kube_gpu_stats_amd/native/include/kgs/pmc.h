@@ -67,6 +67,8 @@ struct PmcRates {
   int n_xcd = 0;
   double xcd_active_pct[kMaxXcc] = {};
   double xcd_mfma_util_pct[kMaxXcc] = {};
+  bool have_xcd_vmem = false;    // TA read per XCD (full set)
+  double xcd_vmem_busy_pct[kMaxXcc] = {};  // TA busy, mean over the XCD's CUs, % of its active cycles
 };
 PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu);
 

@@ -105,6 +105,7 @@ struct PmcSample {
   uint32_t n_xcd = 0;
   uint64_t xcd_active[kMaxXcc] = {};  // GRBM_GUI_ACTIVE of each XCD
   uint64_t xcd_mfma[kMaxXcc] = {};    // SQ_VALU_MFMA_BUSY_CYCLES summed over each XCD's SEs
+  uint64_t xcd_ta[kMaxXcc] = {};      // TA_TA_BUSY summed over each XCD's TA instances (full set; 0 otherwise)
 };
 static_assert(std::is_trivially_copyable<PmcSample>::value, "seqlock payload");
 

@@ -249,6 +249,8 @@ class PyExporter {
       if (r.n_xcd > 0) {
         o["xcd_mfma_util_pct"] = std::vector<double>(r.xcd_mfma_util_pct, r.xcd_mfma_util_pct + r.n_xcd);
         o["xcd_active_pct"] = std::vector<double>(r.xcd_active_pct, r.xcd_active_pct + r.n_xcd);
+        if (r.have_xcd_vmem)
+          o["xcd_vmem_busy_pct"] = std::vector<double>(r.xcd_vmem_busy_pct, r.xcd_vmem_busy_pct + r.n_xcd);
       }
     }
     return o;

@@ -61,6 +61,13 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
       if (cnt > 0) r.xcd_active_pct[x] = 100.0 * ax / cnt;
       if (ax > 0) r.xcd_mfma_util_pct[x] = 100.0 * mx / (ax * simds);
     }
+    r.have_xcd_vmem = r.have_vmem;
+    if (r.have_xcd_vmem)
+      for (uint32_t x = 0; x < nx; ++x) {
+        const double ax = b.xcd_active[x] >= a.xcd_active[x] ? static_cast<double>(b.xcd_active[x] - a.xcd_active[x]) : 0.0;
+        const double tx = b.xcd_ta[x] >= a.xcd_ta[x] ? static_cast<double>(b.xcd_ta[x] - a.xcd_ta[x]) : 0.0;
+        if (ax > 0) r.xcd_vmem_busy_pct[x] = 100.0 * tx / (cu / nx) / ax;
+      }
   }
   return r;
 }
@@ -91,6 +98,7 @@ class MockCounterSource final : public CounterSource {
       for (uint32_t x = 0; x < s.n_xcd; ++x) {
         s.xcd_active[x] -= std::min(s.xcd_active[x], z.xcd_active[x]);
         s.xcd_mfma[x] -= std::min(s.xcd_mfma[x], z.xcd_mfma[x]);
+        s.xcd_ta[x] -= std::min(s.xcd_ta[x], z.xcd_ta[x]);
       }
     }
     s.mono_ns = now;
@@ -123,6 +131,8 @@ class MockCounterSource final : public CounterSource {
       const double w = 1.0 - c_.xcd_skew * x;
       s.xcd_active[x] = static_cast<uint64_t>(clk * busy_s * w);
       s.xcd_mfma[x] = wsum > 0 ? static_cast<uint64_t>(s.value[kPmcMfmaBusy] * (w / wsum)) : 0;
+      // TA: vmem_frac of the XCD's active cycles on each of its 32 CUs (256-CU mock)
+      s.xcd_ta[x] = (s.mask & (1u << kPmcTaBusy)) ? static_cast<uint64_t>(clk * busy_s * w * c_.vmem_frac * 32.0) : 0;
     }
   }
 
@@ -267,6 +277,9 @@ class DlCounterSource final : public CounterSource {
       const int na = sample_xcd_(handles_[dev], reader_idx_[kPmcGrbmGuiActive], s.xcd_active, kMaxXcc);
       const int nm = sample_xcd_(handles_[dev], reader_idx_[kPmcMfmaBusy], s.xcd_mfma, kMaxXcc);
       if (na > 0 && na == nm) s.n_xcd = static_cast<uint32_t>(na);
+      if (s.n_xcd > 0 && reader_idx_[kPmcTaBusy] >= 0 &&
+          sample_xcd_(handles_[dev], reader_idx_[kPmcTaBusy], s.xcd_ta, kMaxXcc) != static_cast<int>(s.n_xcd))
+        std::fill(s.xcd_ta, s.xcd_ta + kMaxXcc, 0);
     }
     s.mono_ns = ts > 0 ? ts : mono_ns();  // when the CP read the counters (pipelined: previous call)
     return 0;

@@ -453,6 +453,16 @@ void Exporter::render(std::string& out) {
         if (snaps[d].pmc_rates)
           for (int x = 0; x < snaps[d].r.n_xcd; ++x)
             w.line("amdgpu_mfma_util_xcc_percent", dev_labels_[d], kXccLabels[x], snaps[d].r.xcd_mfma_util_pct[x]);
+      bool any_xcd_vmem = false;
+      for (int d : ids) any_xcd_vmem |= snaps[d].pmc_rates && snaps[d].r.n_xcd > 0 && snaps[d].r.have_xcd_vmem;
+      if (any_xcd_vmem) {
+        w.head("amdgpu_vmem_busy_xcc_percent", "gauge",
+               "Vector-memory address unit (TA) busy percent of one XCD's active cycles, mean over its CUs (full set)");
+        for (int d : ids)
+          if (snaps[d].pmc_rates && snaps[d].r.have_xcd_vmem)
+            for (int x = 0; x < snaps[d].r.n_xcd; ++x)
+              w.line("amdgpu_vmem_busy_xcc_percent", dev_labels_[d], kXccLabels[x], snaps[d].r.xcd_vmem_busy_pct[x]);
+      }
       w.head("amdgpu_gpu_active_xcc_percent", "gauge",
              "GRBM GUI-active percent of clocks of one XCD over the window (a dispatch in flight, not waves resident)");
       for (int d : ids)

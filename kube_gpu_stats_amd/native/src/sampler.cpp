@@ -323,6 +323,7 @@ void Sampler::run(int dev) {
           for (uint32_t x = 0; x < ps.n_xcd && x < static_cast<uint32_t>(kMaxXcc); ++x) {
             ps.xcd_active[x] += pmc_base.xcd_active[x];
             ps.xcd_mfma[x] += pmc_base.xcd_mfma[x];
+            ps.xcd_ta[x] += pmc_base.xcd_ta[x];
           }
         ps.seq = ++pmc_seq;
         st.pmc_ring.push(ps);

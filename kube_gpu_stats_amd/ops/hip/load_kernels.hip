@@ -136,6 +136,20 @@ __global__ __launch_bounds__(kBlock) void triad_f32_kernel(const f32x4* __restri
   for (; i < hi; i += kBlock) st<NT>(ld<NT>(a + i) + s * ld<NT>(b + i), c + i);
 }
 
+// Triad on the XCDs in xcc_mask only (HW_REG_XCC_ID), for the per-XCD
+// vector-memory counter test; workgroups elsewhere return at once.
+__global__ __launch_bounds__(kBlock) void triad_xcc_kernel(const f32x4* __restrict__ a, const f32x4* __restrict__ b,
+                                                           f32x4* __restrict__ c, float s, size_t n4,
+                                                           unsigned xcc_mask) {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  if (!((xcc_mask >> (xcc & 0xF)) & 1u)) return;
+  const size_t per = (n4 + gridDim.x - 1) / gridDim.x;
+  const size_t lo = static_cast<size_t>(blockIdx.x) * per;
+  const size_t hi = lo + per < n4 ? lo + per : n4;
+  for (size_t i = lo + threadIdx.x; i < hi; i += kBlock) st<true>(ld<true>(a + i) + s * ld<true>(b + i), c + i);
+}
+
 __global__ __launch_bounds__(kBlock) void copy_f32_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
                                                           size_t n4) {
   const size_t per = (n4 + gridDim.x - 1) / gridDim.x;
@@ -197,6 +211,15 @@ int kgs_load_triad_f32_ex(const float* a, const float* b, float* c, float s, siz
 
 int kgs_load_triad_f32(const float* a, const float* b, float* c, float s, size_t n, int nblocks, void* stream) {
   return kgs_load_triad_f32_ex(a, b, c, s, n, nblocks, 1, stream);
+}
+
+int kgs_load_triad_f32_xcc(const float* a, const float* b, float* c, float s, size_t n, int nblocks,
+                           unsigned xcc_mask, void* stream) {
+  if ((n & 3) || nblocks <= 0) return check(hipErrorInvalidValue, "triad_f32_xcc args");
+  hipLaunchKernelGGL(triad_xcc_kernel, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b), reinterpret_cast<f32x4*>(c),
+                     s, n / 4, xcc_mask);
+  return check(hipGetLastError(), "triad_f32_xcc launch");
 }
 
 int kgs_load_copy_f32(const float* src, float* dst, size_t n, int nblocks, void* stream) {

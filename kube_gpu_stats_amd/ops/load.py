@@ -37,6 +37,8 @@ def lib() -> ctypes.CDLL:
                                              ctypes.c_int, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
         L.kgs_load_triad_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
                                          ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.kgs_load_triad_f32_xcc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                             ctypes.c_size_t, ctypes.c_int, ctypes.c_uint, ctypes.c_void_p]
         L.kgs_load_triad_f32_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
                                             ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.kgs_load_copy_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
@@ -103,6 +105,18 @@ def triad_f32(a, b, c, s: float, nblocks: int = 0, stream=None, nt: bool = True)
         nblocks = default_stream_blocks(n)
     _check(lib().kgs_load_triad_f32_ex(a.data_ptr(), b.data_ptr(), c.data_ptr(), float(s), n, int(nblocks),
                                        int(bool(nt)), _stream_ptr(stream)))
+
+
+def triad_f32_xcc(a, b, c, s: float, xcc_mask: int, nblocks: int = 0, stream=None) -> None:
+    """triad_f32 on the XCDs in ``xcc_mask`` only (hardware XCC id); elements owned by
+    workgroups on other XCDs are left untouched."""
+    import torch
+
+    assert a.dtype == b.dtype == c.dtype == torch.float32 and a.numel() == b.numel() == c.numel()
+    assert a.numel() % 4 == 0 and a.is_cuda and a.is_contiguous() and b.is_contiguous() and c.is_contiguous()
+    nb = nblocks or default_stream_blocks(a.numel())
+    _check(lib().kgs_load_triad_f32_xcc(a.data_ptr(), b.data_ptr(), c.data_ptr(), float(s), a.numel(), nb,
+                                        int(xcc_mask) & 0xFFFF, _stream_ptr(stream)))
 
 
 def copy_f32(src, dst, nblocks: int = 0, stream=None) -> None:

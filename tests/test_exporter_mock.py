@@ -439,3 +439,17 @@ def test_periodic_counter_refresh(mock_exporter):
     assert m["amdgpu_gpu_active_percent"][0][1] == pytest.approx(50, abs=5)
     g = [v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT"][0]
     assert g == pytest.approx(2100e6 * 1.1, rel=0.1)  # 2100 MHz mock clock × ≈1.1 s, refreshes included
+
+
+def test_per_xcd_vmem_busy_full_set(mock_exporter):
+    """--pmc-set full adds TA busy per XCD (mean over the XCD's CUs): the mock keeps
+    the TA units busy 30 % of every XCD's active cycles."""
+    ex = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0, pmc_set="full",
+                       mock={"util_base": 50, "util_amp": 0.0001}, mock_pmc={"xcd_skew": 0.05})
+    base = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0)
+    time.sleep(0.5)
+    w = ex.window(0, 0.3)
+    assert w["xcd_vmem_busy_pct"] == pytest.approx([30.0] * 8, abs=1.5)
+    m = parse_text(ex.render())
+    assert len(m["amdgpu_vmem_busy_xcc_percent"]) == 8
+    assert "amdgpu_vmem_busy_xcc_percent" not in parse_text(base.render())  # base set: no TA block

@@ -327,6 +327,59 @@ def test_per_xcd_counters_follow_xcc_gated_load(torch_dev):
         print(out[-1500:])
 
 
+def test_per_xcd_vmem_follows_xcc_gated_stream(torch_dev):
+    """--pmc-set full: TA (vector-memory) busy per XCD lands on the XCDs a gated HBM
+    triad runs on ({1, 6}, chosen by HW_REG_XCC_ID), and the gated triad computes
+    exactly the elements of those XCDs' workgroups."""
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    n = 1 << 28  # 1 GiB per array
+    a = torch.rand(n, device=torch_dev)
+    b = torch.rand(n, device=torch_dev)
+    c = torch.zeros(n, device=torch_dev)
+    nb = load.default_stream_blocks(n)
+    load.triad_f32_xcc(a, b, c, 2.0, 0b01000010, nblocks=nb)
+    torch.cuda.synchronize()
+    per = (n // 4 + nb - 1) // nb * 4  # elements per workgroup
+    blk = torch.arange(n, device=torch_dev) // per
+    on = ((blk % 8) == 1) | ((blk % 8) == 6)  # round-robin XCD placement (profiles/r1/xcd)
+    torch.testing.assert_close(c[on], (a + 2.0 * b)[on])
+    assert torch.count_nonzero(c[~on]).item() == 0
+    del blk, on
+
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
+                             "--hz", "200", "--pmc", "aqlprofile", "--pmc-set", "full", "--control-stdin", "--bdfs", bdf,
+                             "--proc-every", "0", "--link-every", "0"],
+                            cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
+        sc = Scraper("127.0.0.1", ready["port"])
+        t0 = time.time()
+        while time.time() - t0 < 1.6:
+            load.triad_f32_xcc(a, b, c, 2.0, 0b01000010, nblocks=nb)
+            torch.cuda.synchronize()
+        m = parse_text(sc.get())
+        vm = {int(lb["xcc"]): v for lb, v in m.get("amdgpu_vmem_busy_xcc_percent", [])}
+        print(json.dumps({"vmem_busy_xcc": vm, "pmc_info": ready.get("pmc_info")}))
+        assert sorted(vm) == list(range(8)), vm
+        assert vm[1] > 20 and vm[6] > 20, vm
+        assert max(vm[x] for x in (0, 2, 3, 4, 5, 7)) < 0.25 * min(vm[1], vm[6]), vm
+    finally:
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            proc.communicate()
+
+
 def test_counter_handover_stop_and_restart(torch_dev):
     """SIGUSR1 makes the aqlprofile reader STOP its counting session (another
     profiler may program the counters); SIGUSR2 re-STARTs it.  Counters read right
