@@ -455,7 +455,11 @@ def main(argv=None) -> int:
         pmfw_rate = {g: (a_pmfw[g] - b_pmfw.get(g, 0)) / win for g in gpus}
         pmc_rate = {g: (a_pmc.get(g, 0) - b_pmc.get(g, 0)) / win for g in gpus}
         pmc_on = exp.ready.get("pmc", "none") != "none" and sum(pmc_rate.values()) > 0
-        per_gpu = pmc_rate if pmc_on else pmfw_rate
+        # Per GPU: its counter stream if it delivered one, else its PMFW table rate, so one
+        # device whose counter tier failed to open lowers the total by its own share only.
+        per_gpu = {g: (pmc_rate[g] if pmc_on and pmc_rate[g] > 0 else pmfw_rate[g]) for g in gpus}
+        n_pmc = sum(1 for g in gpus if pmc_on and pmc_rate[g] > 0)
+        source = "pmc" if n_pmc == len(gpus) else ("pmfw" if n_pmc == 0 else f"pmc on {n_pmc}/{len(gpus)} GPUs")
         total = sum(per_gpu.values())
         t_off = 0.5 * (t_a + t_c)
         result = {
@@ -475,7 +479,7 @@ def main(argv=None) -> int:
             "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + rocprofiler PMC, "
                                 f"{a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",
                        "global_batch": n, "seq_len": a.steps, "parallelism": f"dp{n}",
-                       "hz": exp.ready.get("hz") or a.hz, "sample_source": "pmc" if pmc_on else "pmfw",
+                       "hz": exp.ready.get("hz") or a.hz, "sample_source": source,
                        "exporter": "attached" if a.attach else "spawned"},
             "samples_per_sec_per_gpu": total / max(1, len(per_gpu)),
             "pmc_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmc_rate.items()},
