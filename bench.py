@@ -72,6 +72,14 @@ def parse_args(argv=None):
     ap.add_argument("--tiny-kernels", type=int, default=2000,
                     help="dispatch-bound part of each step: a HIP graph of this many 64 KiB copies (≈1.7 µs each); "
                     "it is where counter READs on the command processor would show up (0 = off)")
+    ap.add_argument("--load", default="synthetic", choices=["synthetic", "train"],
+                    help="GPU work per step: the synthetic gfx950 kernels (default) or a PyTorch bf16 "
+                    "decoder training step (forward + backward + AdamW, DDP when N > 1)")
+    ap.add_argument("--train-dim", type=int, default=4096)
+    ap.add_argument("--train-layers", type=int, default=4)
+    ap.add_argument("--train-batch", type=int, default=4)
+    ap.add_argument("--train-seq", type=int, default=2048)
+    ap.add_argument("--train-vocab", type=int, default=32768)
     ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per step when N > 1 (0 = off)")
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
@@ -158,6 +166,90 @@ class GpuLoad:
     def pci_bdf(self, device: int) -> str:
         p = self.torch.cuda.get_device_properties(device)
         return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+
+class TrainLoad(GpuLoad):
+    """``--load train``: one PyTorch bf16 training step per bench step instead of the
+    synthetic kernels: a decoder stack (RMSNorm, causal SDPA, SwiGLU MLP) forward +
+    backward + AdamW, DDP over RCCL when N > 1.  Hundreds of library kernels
+    (hipBLASLt GEMMs, flash attention, elementwise) per step, which is the kind of
+    workload a DaemonSet exporter shares the GPU with.  Random-init weights and
+    synthetic tokens; the exporter is measured exactly as with the synthetic load."""
+
+    def __init__(self, a, device: int, ctx=None):
+        import torch
+        import torch.nn as nn
+        import torch.nn.functional as F
+
+        self.torch = torch
+        dev = torch.device("cuda", device) if device >= 0 else torch.device("cpu")  # cpu: tests only
+        d, h, L, ff = a.train_dim, a.train_dim // 128, a.train_layers, int(a.train_dim * 8 / 3 / 256 + 0.5) * 256
+        self.batch, self.seq, self.vocab = a.train_batch, a.train_seq, a.train_vocab
+
+        class Block(nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.n1 = nn.RMSNorm(d)
+                self.qkv = nn.Linear(d, 3 * d, bias=False)
+                self.o = nn.Linear(d, d, bias=False)
+                self.n2 = nn.RMSNorm(d)
+                self.up = nn.Linear(d, 2 * ff, bias=False)
+                self.down = nn.Linear(ff, d, bias=False)
+
+            def forward(self, x):
+                B, S, _ = x.shape
+                q, k, v = self.qkv(self.n1(x)).view(B, S, 3, h, d // h).permute(2, 0, 3, 1, 4)
+                y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+                x = x + self.o(y.transpose(1, 2).reshape(B, S, d))
+                g, u = self.up(self.n2(x)).chunk(2, dim=-1)
+                return x + self.down(F.silu(g) * u)
+
+        class Model(nn.Module):
+            def __init__(self, vocab):
+                super().__init__()
+                self.emb = nn.Embedding(vocab, d)
+                self.blocks = nn.ModuleList(Block() for _ in range(L))
+                self.norm = nn.RMSNorm(d)
+                self.head = nn.Linear(d, vocab, bias=False)
+
+            def forward(self, t):
+                x = self.emb(t)
+                for b in self.blocks:
+                    x = b(x)
+                return self.head(self.norm(x))
+
+        torch.manual_seed(1234)
+        model = Model(self.vocab).to(device=dev, dtype=torch.bfloat16)
+        self.params = sum(p.numel() for p in model.parameters())
+        if ctx is not None and ctx.is_dist:
+            from torch.nn.parallel import DistributedDataParallel
+
+            model = DistributedDataParallel(model, device_ids=[device], bucket_cap_mb=256)
+        self.model = model
+        self.opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=dev.type == "cuda")
+        g = torch.Generator(device=dev).manual_seed(1234 + (ctx.rank if ctx is not None else 0))
+        self.tok = torch.randint(0, self.vocab, (self.batch, self.seq + 1), device=dev, generator=g)
+        self.F = F
+
+    def step(self):
+        logits = self.model(self.tok[:, :-1])
+        loss = self.F.cross_entropy(logits.float().view(-1, self.vocab), self.tok[:, 1:].reshape(-1))
+        loss.backward()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+
+    def calibrate(self) -> dict:
+        torch = self.torch
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.step()
+        e1.record()
+        torch.cuda.synchronize()
+        s = e0.elapsed_time(e1) * 1e-3
+        toks = self.batch * self.seq
+        # 6·N·T for the dense weights + causal attention (fwd 2·S·d per token per layer, x3 with bwd)
+        return {"train_step_ms": s * 1e3, "train_tokens_per_s": toks / s, "train_params": self.params,
+                "train_tflops": 6.0 * self.params * toks / s / 1e12}
 
 
 class MockLoad:
@@ -382,7 +474,12 @@ def main(argv=None) -> int:
         if not a.mock:
             B.build_pmc()
             B.build_pmc_aql()
-    load = MockLoad(a, ctx.local_rank) if a.mock else GpuLoad(a, ctx.local_rank, ctx)
+    if a.mock:
+        load = MockLoad(a, ctx.local_rank)
+    elif a.load == "train":
+        load = TrainLoad(a, ctx.local_rank, ctx)
+    else:
+        load = GpuLoad(a, ctx.local_rank, ctx)
 
     for _ in range(a.warmup):
         load.step()
@@ -474,13 +571,16 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (gfx950 MFMA bf16 + HBM triad + HIP-graph tiny-kernel load; random-init operands)" if not a.mock
-            else "synthetic mock provider (CPU plumbing)",
+            "data": ("synthetic mock provider (CPU plumbing)" if a.mock
+                     else f"synthetic tokens, random-init {a.train_layers}-layer d={a.train_dim} bf16 decoder "
+                     "training step (fwd + bwd + AdamW) as the GPU load" if a.load == "train"
+                     else "synthetic (gfx950 MFMA bf16 + HBM triad + HIP-graph tiny-kernel load; random-init operands)"),
             "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + rocprofiler PMC, "
                                 f"{a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",
                        "global_batch": n, "seq_len": a.steps, "parallelism": f"dp{n}",
                        "hz": exp.ready.get("hz") or a.hz, "sample_source": source,
-                       "exporter": "attached" if a.attach else "spawned"},
+                       "exporter": "attached" if a.attach else "spawned",
+                       "load": "mock" if a.mock else a.load},
             "samples_per_sec_per_gpu": total / max(1, len(per_gpu)),
             "pmc_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmc_rate.items()},
             "pmfw_distinct_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmfw_rate.items()},

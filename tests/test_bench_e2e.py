@@ -134,3 +134,28 @@ def test_multi_node_exporters_to_reports(mock_exporter):
                 assert nodes[0][2] == pytest.approx(60, abs=2) and nodes[1][2] == pytest.approx(30, abs=2), nodes
     finally:
         fp.stop()
+
+
+def test_train_load_steps_on_cpu():
+    """bench.py --load train: the decoder step runs, learns (loss falls on a fixed batch),
+    and calibrate() reports the step's rate.  Tiny dims; CPU stands in for cuda:0."""
+    import torch
+
+    import bench
+
+    a = bench.parse_args(["--load", "train", "--train-dim", "128", "--train-layers", "2",
+                          "--train-batch", "2", "--train-seq", "32", "--train-vocab", "512"])
+    ld = bench.TrainLoad(a, -1, None)
+    # loss on the fixed batch before / after a few steps
+    F = torch.nn.functional
+
+    def loss():
+        with torch.no_grad():
+            lg = ld.model(ld.tok[:, :-1])
+            return F.cross_entropy(lg.float().view(-1, lg.shape[-1]), ld.tok[:, 1:].reshape(-1)).item()
+
+    l0 = loss()
+    for _ in range(5):
+        ld.step()
+    assert loss() < l0
+    assert ld.params > 0
