@@ -81,6 +81,10 @@ def parse_args(argv=None):
     ap.add_argument("--train-seq", type=int, default=2048)
     ap.add_argument("--train-vocab", type=int, default=32768)
     ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per step when N > 1 (0 = off)")
+    ap.add_argument("--interleave", type=int, default=4,
+                    help="after phase B: this many off/on block pairs (ABBA order; exporter paused vs sampling "
+                    "and scraped, --steps/4 steps per block) -> overhead_interleaved_pct, which cancels the "
+                    "slow thermal/power drift that an A-B-C comparison sees (0 = off)")
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
     ap.add_argument("--mock-step-ms", type=float, default=20.0)
@@ -292,6 +296,40 @@ def timed(ctx, load, k: int, name: str = "") -> float:
     return D.all_reduce(ctx, [dt], "max")[0]
 
 
+def interleaved(ctx, load, exp, a) -> dict:
+    """Off/on blocks in ABBA order (off,on, on,off, ...) with the exporter process up:
+    *off* = sampling paused (no PMFW / counter reads, no scrapes), *on* = sampling at
+    --hz and scraped at --scrape-hz.  Pairs of adjacent blocks see the same thermal
+    and power state, so slow drift cancels; the A-B-C phases cannot do that."""
+    if a.interleave <= 0:
+        return {}
+    blk = max(3, a.steps // 4)
+    t_on = t_off = 0.0
+    blocks = []
+    for r in range(a.interleave):
+        for on in ((False, True) if r % 2 == 0 else (True, False)):
+            sc = None
+            if exp is not None:
+                if on:
+                    exp.resume()
+                    sc = Scraper("127.0.0.1", exp.port).start(a.scrape_hz)
+                else:
+                    exp.pause()
+            D.barrier(ctx)
+            dt = timed(ctx, load, blk)
+            if sc is not None:
+                sc.stop()
+            blocks.append([int(on), round(dt, 6)])
+            if on:
+                t_on += dt
+            else:
+                t_off += dt
+    if exp is not None:
+        exp.resume()
+    return {"overhead_interleaved_pct": 100.0 * (t_on / t_off - 1.0), "interleave_blocks": blocks,
+            "interleave_steps_per_block": blk}
+
+
 # ----------------------------------------------------------------------------- exporter
 class AttachedExporter:
     """An already-running exporter (``--control-http``) driven over HTTP."""
@@ -327,7 +365,7 @@ class ExporterProc:
     def __init__(self, a, bdfs: list[str], log_path: str):
         cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
                "--hz", str(a.hz), "--proc-every", str(max(1, int(a.hz // 10))),
-               "--link-every", str(max(1, int(a.hz))), "--control-stdin", "--node-name", "bench-node",
+               "--link-every", str(max(1, int(a.hz))), "--control-stdin", "--control-http", "--node-name", "bench-node",
                "--bdfs", ",".join(bdfs)]
         if a.mock:
             cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock"]
@@ -351,6 +389,13 @@ class ExporterProc:
                                   text=True, env=env)
         self.ready = self._wait_ready(120.0)
         self.port = int(self.ready["port"])
+        self.sc = Scraper("127.0.0.1", self.port)
+
+    def pause(self):
+        self.sc.get("/control/pause")
+
+    def resume(self):
+        self.sc.get("/control/resume")
 
     def _wait_ready(self, timeout: float) -> dict:
         end = time.time() + timeout
@@ -538,6 +583,7 @@ def main(argv=None) -> int:
         t_w1 = time.perf_counter()
         cpu1 = proc_cpu_seconds(exp_pid)
         thr1 = thread_cpu_seconds(exp_pid)
+    inter = interleaved(ctx, load, exp, a)
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
@@ -593,6 +639,7 @@ def main(argv=None) -> int:
             "t_off_a_s": t_a,
             "t_on_s": t_b,
             "t_off_c_s": t_c,
+            **inter,
             "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
             "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / win, 4) for k, v in thr1.items()
                                              if win > 0 and v - thr0.get(k, 0.0) > 0.005 * win},

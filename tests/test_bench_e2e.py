@@ -41,6 +41,10 @@ def test_bench_contract_single_process():
     assert res["value"] > 50  # mock PMC at 100 Hz
     assert res["p50_scrape_ms"] < 50
     assert abs(res["ms_per_step"] - 20.0) < 10
+    # interleaved ABBA off/on blocks: 4 pairs, alternating order, exporter paused / sampling
+    blocks = res["interleave_blocks"]
+    assert [b[0] for b in blocks] == [0, 1, 1, 0, 0, 1, 1, 0]
+    assert abs(res["overhead_interleaved_pct"]) < 50
 
 
 @pytest.mark.slow
