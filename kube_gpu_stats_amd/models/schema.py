@@ -39,6 +39,23 @@ CATALOG: tuple[Family, ...] = (
       "that was matrix work.  `kgs gpu-util-stats --util-metric container_gpu_mfma_util` reports it per pod.",
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
       "rocprofiler+kubelet", "pmc"),
+    F("container_gpu_busy_seconds_total", "counter",
+      "GFX-busy seconds of the GPU allocated to the pod, counted from the allocation (PMFW accumulators).  "
+      "`100 * avg(rate(container_gpu_busy_seconds_total[1h])) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)` "
+      "is the exact hourly per-pod utilisation whatever the scrape interval — the default source of "
+      "`kgs gpu-util-stats` (fixed mode).  Same labels as container_gpu_sm_util.",
+      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      "pmfw+kubelet", "fast"),
+    F("container_gpu_mfma_busy_seconds_total", "counter",
+      "MFMA-busy seconds (all SIMDs busy with matrix work for 1 s = 1) of the GPU allocated to the pod, counted from "
+      "the allocation (hardware counters).  Same labels as container_gpu_sm_util.",
+      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      "rocprofiler+kubelet", "pmc"),
+    F("kgs_gpu_owner", "gauge",
+      "1 per (GPU, pod, container) allocation reported by the kubelet: the join target that puts pod labels on any "
+      "amdgpu_* series (`... * on (gpu, uuid) group_left(pod_name, namespace) kgs_gpu_owner`).",
+      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      "kubelet", "attribution"),
     # ---- inventory / topology -------------------------------------------------------------
     F("amdgpu_device_info", "gauge", "Static device information (1).", extra=(
         "bdf", "gpu_type", "kubernetes_io_hostname", "serial", "market_name", "gfx_target", "numa_node", "num_cu", "num_xcc", "kfd_gpu_id", "hip_id",
@@ -87,6 +104,9 @@ CATALOG: tuple[Family, ...] = (
       source="rocprofiler", tier="pmc"),
     F("amdgpu_mfma_util_percent", "gauge", "Matrix-core busy % of active cycles (window).", source="rocprofiler",
       tier="pmc"),
+    F("amdgpu_mfma_busy_seconds_total", "counter",
+      "∫ MFMA-busy share of all SIMD cycles dt (per drain: ΔSQ_VALU_MFMA_BUSY_CYCLES / (SIMDs·ΔGRBM_COUNT) · Δt); "
+      "rate() = matrix-core utilisation of wall time.", source="rocprofiler", tier="pmc"),
     F("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active % of clocks (window).", source="rocprofiler", tier="pmc"),
     F("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy % of active cycles (window).",
       source="rocprofiler", tier="pmc"),
@@ -136,6 +156,11 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_refreshes_total", "counter", "Periodic counter re-STARTs (--pmc-refresh-s): reprogram selects that "
       "another profiler may have changed without stalling GRBM_COUNT.", source="self"),
     F("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples.", source="self"),
+    F("kgs_slow_reads_total", "counter",
+      "Management-library reads by the node-wide slow thread (tier=procs: process list; tier=links: xGMI link "
+      "table + RAS).  They never run on the per-GPU sampler threads.", extra=("tier",), source="self"),
+    F("kgs_slow_read_seconds_total", "counter", "Time the node-wide slow thread spent in management-library calls.",
+      source="self"),
     F("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read.", extra=("le",), source="self"),
     F("kgs_scrapes_total", "counter", "Scrapes rendered.", ("kubernetes_io_hostname",), "self"),
     F("kgs_scrape_render_seconds_total", "counter", "Time spent rendering /metrics.", ("kubernetes_io_hostname",),

@@ -36,6 +36,9 @@ struct DeviceInfo {
   std::string compute_partition;
   std::string memory_partition;
   int partition_id = -1;
+  // XCCs of the physical GPU's PMFW table this device owns: [xcc_first,
+  // xcc_first + num_xcc).  SPX: 0 and all of them (gpu_metrics.h restrict_to_xccs).
+  uint32_t xcc_first = 0;
 };
 
 struct ProcInfo {
@@ -100,9 +103,20 @@ class Backend {
 
 // Mock provider configuration (tests, plumbing benchmark).
 struct MockConfig {
-  int n_gpus = 8;
+  int n_gpus = 8;               // physical GPUs
   double fw_period_s = 0.020;   // PMFW cadence measured on MI355X (≈20 ms)
+  // Load curve per GPU (per XCC when partitioned): a sine base ± amp, or, with
+  // square_duty > 0, a square wave at base + amp for the first square_duty of
+  // every period and base − amp for the rest (bursty jobs between scrapes).
   double util_base = 50, util_amp = 40, util_period_s = 10;
+  double square_duty = 0;
+  // "SPX" | "DPX" | "QPX" | "CPX": each GPU shows up as this many devices, all
+  // with the GPU's BDF, one partition_id each, XCC curve g·8 + x per XCC.
+  std::string compute_partition = "SPX";
+  // AMD SMI latency model: the management-library calls take this long and hold
+  // one process-wide lock while they do (amdsmi serialises callers); the PMFW
+  // table read is a per-device sysfs pread (no lock).  0 = instantaneous.
+  double proc_latency_s = 0, link_latency_s = 0, health_latency_s = 0, metrics_latency_s = 0;
   uint64_t vram_total_bytes = 309220868096ull;  // 288 GiB HBM3E as reported by sysfs
   double fail_rate = 0;         // probability a read returns an error
   double stall_s = 0;           // extra latency injected into every read
@@ -117,6 +131,11 @@ struct MockConfig {
 };
 
 std::unique_ptr<Backend> make_mock_backend(const MockConfig& cfg);
+// The mock's closed-form load: busy percent of exporter device `dev` at mock time
+// t (s since the backend started), and ∫_0^t of it (percent·s).  Partition
+// devices average their XCCs' curves.  Shared with the mock counter source.
+double mock_device_util(const MockConfig& cfg, int dev, double t);
+double mock_device_util_integral(const MockConfig& cfg, int dev, double t);
 // Returns nullptr and fills `err` if AMD SMI cannot be initialised.
 std::unique_ptr<Backend> make_amdsmi_backend(std::string& err, const std::string& sysfs_root = "/sys");
 

@@ -24,6 +24,10 @@ namespace kgs {
 
 struct Owner {
   std::string pod, ns, container;
+  // The GPU's busy integrals when this owner was first seen on it: the per-pod
+  // counters (container_gpu_busy_seconds_total, ...) count from 0 at allocation.
+  double base_busy_s = 0, base_mfma_s = 0;
+  bool same(const Owner& o) const { return pod == o.pod && ns == o.ns && container == o.container; }
 };
 struct PidOwner {
   std::string pod, ns, container, pod_uid;
@@ -45,7 +49,13 @@ struct ExporterConfig {
   int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
   std::string node_name;
   std::string gpu_type_override;
-  double window_s = 1.0;            // gauge averaging window
+  // Gauge averaging window.  Default = a typical Prometheus scrape interval, so
+  // consecutive scrapes' gauges tile time instead of sampling 1 s of every 15;
+  // the exact per-pod accounting uses the *_seconds_total counters anyway.
+  double window_s = 15.0;
+  // A device whose last good read (PMFW) or counter drain (PMC) is older than
+  // this exports no window gauges: frozen values are worse than a gap.
+  double stale_s = 5.0;
   // HBM bytes/s at 100 % UMC (memory-controller) activity: the PMFW activity is
   // linear in bandwidth, 11.89 %/(TB/s) on MI355X (profiles/umc_calib.md).
   double hbm_bytes_per_s_at_full_umc = 8.41e12;
@@ -106,6 +116,9 @@ class Exporter {
   // its counting session and skips the PMC tier) or take them back (true).
   void set_pmc_enabled(bool on);
   bool pmc_enabled() const;
+  // Sampler tick rate (benchmarks switch tiers in place; integrals continue).
+  void set_sample_rate(double hz);
+  double sample_rate() const;
 
   // self metrics
   std::atomic<uint64_t> scrapes{0};

@@ -126,6 +126,9 @@ struct Integrals {
   double pmc_read_seconds = 0;   // total time spent in counter drains
   uint64_t recoveries = 0;       // successful Backend::recover() after a failure streak
   uint64_t recover_attempts = 0;
+  // ∫ MFMA-busy fraction of wall time dt from the counter stream: per drain,
+  // ΔMFMA_BUSY / (SIMDs · ΔGRBM_COUNT) · Δt (all SIMDs busy with MFMA for 1 s = 1).
+  double mfma_busy_seconds = 0;
 };
 static_assert(std::is_trivially_copyable<Integrals>::value, "seqlock payload");
 

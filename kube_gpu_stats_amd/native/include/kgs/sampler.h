@@ -1,11 +1,18 @@
 // Per-GPU sampler threads (SURVEY.md §3.4 "HOT LOOP", §2.3 device fan-out).
 //
 // One std::thread per device, pinned to the CPUs of the GPU's NUMA node, wakes
-// on an absolute CLOCK_MONOTONIC deadline and
-//   * every tick   : reads the PMFW table + HBM occupancy (fast tier) and, if
-//                    enabled, drains the hardware counters (PMC tier);
-//   * every Nth    : reads the per-process list (mid tier);
-//   * every Mth    : reads per-link xGMI metrics (slow tier).
+// on an absolute CLOCK_MONOTONIC deadline and every tick reads the PMFW table +
+// HBM occupancy (fast tier, capped at pmfw_hz) and, if enabled, drains the
+// hardware counters (PMC tier).  Those two are per-device files / queues: the
+// per-GPU thread never takes a node-wide lock.
+//
+// The management-library tiers — per-process list (mid tier, every proc_every
+// ticks' worth of time), xGMI link table + RAS health (slow tier, every
+// link_every ticks' worth) — go through AMD SMI, which serialises callers on one
+// process-wide mutex and takes milliseconds per call.  They run on ONE node-wide
+// "kgs-slow" thread that walks the devices in turn, so a slow
+// amdsmi_get_gpu_process_list on GPU 3 can never delay GPU 5's 8 kHz counter
+// drain (profiles/r2/mock_scaling.md).
 // A sample counts as *distinct* only when the firmware timestamp moved
 // (BASELINE.md measurement rule).  Results are published through seqlocks; the
 // scrape path never calls into the driver.
@@ -29,8 +36,8 @@ namespace kgs {
 struct SamplerConfig {
   double hz = 10.0;            // tick rate: counter (PMC) tier runs every tick
   double pmfw_hz = 100.0;      // PMFW-table tier rate cap (table refreshes every ≈20 ms; 0 = every tick)
-  int proc_every = 10;         // mid tier every N ticks (0 disables)
-  int link_every = 100;        // slow tier every N ticks (0 disables)
+  int proc_every = 10;         // mid tier period = proc_every / hz seconds (0 disables)
+  int link_every = 100;        // slow tier period = link_every / hz seconds (0 disables)
   bool pin_numa = true;
   bool pmc = false;            // drain hardware counters every tick
   // A foreign profiler (rocprofv3 --pmc) that STOPs or reprograms the perfmon
@@ -88,6 +95,9 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_reclaims{0};    // automatic re-STARTs after a stall
   std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
   PmcSample pmc_base;  // totals carried over hand-overs (sampler thread only; survives pause/resume)
+  // Slow-thread self metrics: completed passes and their latency per tier.
+  std::atomic<uint64_t> proc_reads{0}, proc_errors{0}, link_reads{0};
+  std::atomic<uint64_t> slow_ns_total{0};
 
   std::shared_ptr<const std::vector<ProcInfo>> get_procs() const {
     std::lock_guard<std::mutex> g(slow_mu);
@@ -125,9 +135,14 @@ class Sampler {
   // Ask every sampled device's thread to hand its counters to another profiler
   // (false) or to take them back (true).  Takes effect within one tick.
   void set_pmc_wanted(bool on);
+  // Change the tick rate (stops and restarts the threads; integrals continue).
+  void set_hz(double hz);
+  // Node-wide slow thread: passes completed and whether it is running.
+  uint64_t slow_passes() const { return slow_passes_.load(); }
 
  private:
   void run(int dev);
+  void run_slow();
   void integrate(int dev, const GpuSample* prev, GpuSample& cur, Integrals& I);
 
   Backend* be_;
@@ -136,6 +151,11 @@ class Sampler {
   std::vector<std::unique_ptr<DeviceState>> states_;
   std::vector<int> dev_ids_;
   std::vector<std::thread> threads_;
+  std::thread slow_thread_;
+  std::atomic<uint64_t> slow_passes_{0};
+  // Per-device process CU-occupancy integrals (slow thread only; survive pause/resume).
+  std::vector<std::vector<std::pair<uint32_t, double>>> cu_seconds_;
+  std::vector<int64_t> last_proc_ns_;
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
   int stop_fd_ = -1;  // eventfd: readable once stop() was called; sampler threads ppoll() on it

@@ -43,7 +43,9 @@ class Seqlock {
   }
 
   // Reader side: any number of threads.  Returns false if never written.
-  bool load(T& out, int max_spins = 1 << 20) const {
+  // `version`, if given, receives the number of completed stores the copy came
+  // from (SampleRing uses it to tell a slot's current lap from a newer one).
+  bool load(T& out, int max_spins = 1 << 20, uint64_t* version = nullptr) const {
     uint64_t buf[kWords];
     for (int spin = 0; spin < max_spins; ++spin) {
       const uint64_t s0 = seq_.load(std::memory_order_acquire);
@@ -54,6 +56,7 @@ class Seqlock {
       if (s0 == s1) {
         if (s0 == 0) return false;
         std::memcpy(&out, buf, sizeof(T));
+        if (version) *version = s0 >> 1;
         return true;
       }
     }
@@ -70,6 +73,13 @@ class Seqlock {
 // Fixed-capacity history ring of seqlocked slots.  The writer publishes slot
 // `head % N` and then advances `head`; a reader walking back from `head` gets
 // every slot that was not overwritten while it read (torn slots are skipped).
+//
+// Generation check: entry e (0-based push index) lives in slot e % N and is that
+// slot's (e / N + 1)-th store.  A reader that was descheduled long enough for
+// the writer to lap it finds a *newer* entry in the slot — untorn, but the wrong
+// one — and the slot's store count tells it so.  Binary searches over the ring
+// (Sampler::window_busy / window_pmc) rely on entries being time-ordered, so a
+// lapped slot reads as absent, never as a newer sample under an old index.
 template <class T, size_t N>
 class SampleRing {
   static_assert((N & (N - 1)) == 0, "capacity must be a power of two");
@@ -84,11 +94,15 @@ class SampleRing {
   uint64_t head() const { return head_.load(std::memory_order_acquire); }
   static constexpr size_t capacity() { return N; }
 
-  // The i-th most recent entry (0 = newest); false if absent or torn.
-  bool at(uint64_t i, T& out) const {
-    const uint64_t h = head();
+  // The i-th most recent entry (0 = newest) as of this call's `head`; false if
+  // absent, torn, or already overwritten by a later lap of the writer.
+  bool at(uint64_t i, T& out) const { return at_from(head(), i, out); }
+
+  // Same, relative to a head value the caller read once (a consistent view
+  // across several lookups of one search).
+  bool at_from(uint64_t h, uint64_t i, T& out) const {
     if (i >= h || i >= N - 1) return false;
-    return slots_[(h - 1 - i) & (N - 1)].load(out, 4);
+    return load_entry(h - 1 - i, out);
   }
 
   // Number of entries a reader can walk back over (one slot of slack for the writer).
@@ -106,7 +120,7 @@ class SampleRing {
     T v;
     size_t n = 0;
     for (uint64_t i = 0; i < h && i < N - 1; ++i) {
-      if (!slots_[(h - 1 - i) & (N - 1)].load(v, 4)) continue;
+      if (!load_entry(h - 1 - i, v)) continue;
       ++n;
       if (!fn(static_cast<const T&>(v))) break;
     }
@@ -118,12 +132,19 @@ class SampleRing {
     const uint64_t h = head();
     size_t n = 0;
     for (uint64_t i = 0; i < max && i < h && i < N - 1; ++i) {
-      if (slots_[(h - 1 - i) & (N - 1)].load(out[n], 4)) ++n;
+      if (load_entry(h - 1 - i, out[n])) ++n;
     }
     return n;
   }
 
  private:
+  // Entry `e` (push index), only if its slot still holds that lap.
+  bool load_entry(uint64_t e, T& out) const {
+    uint64_t ver = 0;
+    if (!slots_[e & (N - 1)].load(out, 4, &ver)) return false;
+    return ver == e / N + 1;
+  }
+
   alignas(64) std::atomic<uint64_t> head_{0};
   Seqlock<T> slots_[N];
 };

@@ -53,6 +53,7 @@ struct Dev {
   DeviceInfo info;
   int fd_metrics = -1;
   int fd_vram_used = -1;
+  bool partitioned = false;  // a DPX/QPX/CPX partition: restrict the table to its XCCs
   alignas(64) uint8_t buf[4096];
 };
 
@@ -123,6 +124,7 @@ class AmdSmiBackend final : public Backend {
       rc = read_metrics_amdsmi_locked(dv, s);
     }
     if (rc != 0) return rc;
+    if (dv.partitioned) restrict_to_xccs(s, dv.info.xcc_first, dv.info.num_xcc);
     read_vram(dv, s);
     s.mono_ns = now_ns(CLOCK_MONOTONIC);
     s.wall_ns = now_ns(CLOCK_REALTIME);
@@ -163,11 +165,22 @@ class AmdSmiBackend final : public Backend {
     std::memset(&lm, 0, sizeof lm);
     amdsmi_status_t st = amdsmi_get_link_metrics(devs_[d]->h, &lm);
     if (st != AMDSMI_STATUS_SUCCESS) return -static_cast<int>(st);
-    for (uint32_t i = 0; i < lm.num_links && i < AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK; ++i) {
+    // `num_links` counts the *connected* ports, but the array is indexed by
+    // physical port (the PMFW xgmi_*_data_acc index): on MI355X port 0 is the
+    // disabled self port (BDF all ones) and the 7 peers sit on ports 1..7, so
+    // num_links = 7 while the last peer is links[7] (measured,
+    // profiles/r2/xgmi/).  Walk every port slot the PMFW table has and keep the
+    // ones that name a peer.
+    uint32_t found = 0;
+    for (uint32_t i = 0; i < AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK && found < lm.num_links; ++i) {
+      const auto& e = lm.links[i];
+      const bool disabled = e.bdf.domain_number == 0xFFFFFFFFFFFFull || e.bdf.as_uint == ~0ull;
+      const bool empty = e.bdf.as_uint == 0 && e.link_type == 0 && e.bit_rate == 0;
+      if (disabled || empty) continue;
+      ++found;
       LinkInfo li;
       li.link = static_cast<int>(i);
-      li.peer_bdf = lm.links[i].bdf.as_uint == ~0ull ? std::string() : fmt_bdf(lm.links[i].bdf);
-      if (lm.links[i].bdf.domain_number == 0xFFFFFFFFFFFFull) li.peer_bdf.clear();
+      li.peer_bdf = fmt_bdf(e.bdf);
       li.link_type = static_cast<int>(lm.links[i].link_type);
       li.bit_rate_gbps = lm.links[i].bit_rate;
       li.max_bw_gbps = lm.links[i].max_bandwidth;
@@ -324,11 +337,20 @@ class AmdSmiBackend final : public Backend {
       std::string tot;
       if (read_small_file(in.sysfs_dir + "/mem_info_vram_total", tot)) in.vram_total_bytes = std::strtoull(tot.c_str(), nullptr, 10);
     }
-    // Probe the table once for the XCC count.
+    // Probe the table once for the XCC count.  A compute partition (DPX/QPX/CPX)
+    // is its own device over the physical GPU's table: it owns a contiguous
+    // share of the XCCs by partition id (gpu_metrics.h restrict_to_xccs).
     GpuSample s;
     if (d->fd_metrics >= 0) {
       const ssize_t n = pread(d->fd_metrics, d->buf, sizeof d->buf, 0);
       if (n > 0 && parse_gpu_metrics_v1_8(d->buf, static_cast<size_t>(n), s) == 0) in.num_xcc = s.num_xcc;
+    }
+    const uint32_t parts = partitions_of_mode(in.compute_partition.c_str());
+    if (parts > 1 && in.num_xcc >= parts && in.partition_id >= 0 && static_cast<uint32_t>(in.partition_id) < parts) {
+      const uint32_t per = in.num_xcc / parts;
+      in.xcc_first = per * static_cast<uint32_t>(in.partition_id);
+      in.num_xcc = per;
+      d->partitioned = true;
     }
     devs_.push_back(std::move(d));
   }

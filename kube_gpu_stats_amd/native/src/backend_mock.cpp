@@ -12,7 +12,10 @@
 #include <mutex>
 #include <thread>
 
+#include <algorithm>
+
 #include "kgs/backend.h"
+#include "kgs/gpu_metrics.h"
 
 namespace kgs {
 namespace {
@@ -30,53 +33,84 @@ int64_t wall_ns() {
 
 constexpr double kTwoPi = 6.283185307179586;
 
+double clamp100(double u) { return u < 0 ? 0 : (u > 100 ? 100 : u); }
+
+int parts_of(const MockConfig& c) {
+  const uint32_t n = partitions_of_mode(c.compute_partition.c_str());
+  return n == 0 ? 1 : static_cast<int>(n);
+}
+
+// Curve k: busy percent at t, and its integral from 0 (percent·s).
+double curve_util(const MockConfig& c, int k, double t) {
+  if (c.square_duty > 0) {
+    const double ph = t / c.util_period_s - std::floor(t / c.util_period_s);
+    return ph < c.square_duty ? clamp100(c.util_base + c.util_amp) : clamp100(c.util_base - c.util_amp);
+  }
+  return clamp100(c.util_base + c.util_amp * std::sin(kTwoPi * t / c.util_period_s + 0.7 * k));
+}
+double curve_integral(const MockConfig& c, int k, double t) {
+  if (c.square_duty > 0) {
+    const double T = c.util_period_s, on = c.square_duty * T;
+    const double hi = clamp100(c.util_base + c.util_amp), lo = clamp100(c.util_base - c.util_amp);
+    const double n = std::floor(t / T), r = t - n * T;
+    return n * (on * hi + (T - on) * lo) + std::min(r, on) * hi + std::max(0.0, r - on) * lo;
+  }
+  // closed form (clamping ignored when base ± amp stays inside [0, 100])
+  const double w = kTwoPi / c.util_period_s, ph = 0.7 * k;
+  return c.util_base * t + c.util_amp / w * (std::cos(ph) - std::cos(w * t + ph));
+}
+
+// XCC x of physical GPU g runs curve g·8 + x when partitioned; an SPX device d runs curve d.
+int xcc_curve(const MockConfig& c, int gpu, int x) { return gpu * kMaxXcc + x; }
+
+void sleep_s(double s) {
+  if (s > 0) std::this_thread::sleep_for(std::chrono::duration<double>(s));
+}
+
 class MockBackend final : public Backend {
  public:
-  explicit MockBackend(const MockConfig& c) : cfg_(c), t0_(mono_ns()) {
-    for (int d = 0; d < cfg_.n_gpus; ++d) {
-      DeviceInfo in;
-      in.index = d;
-      char bdf[32];
-      std::snprintf(bdf, sizeof bdf, "0000:%02x:00.0", 0x11 + 0x10 * d);
-      in.bdf = bdf;
-      char uuid[64];
-      std::snprintf(uuid, sizeof uuid, "mock-75a3-0000-1000-80b8-%012d", d);
-      in.uuid = uuid;
-      in.serial = "MOCK" + std::to_string(d);
-      in.market_name = "AMD Instinct MI355 OAM";
-      in.gpu_type = gpu_type_from_market_name(in.market_name);
-      in.gfx_target = "gfx950";
-      in.numa_node = d < cfg_.n_gpus / 2 ? 0 : 1;
-      in.num_cu = 256;
-      in.num_xcc = 8;
-      in.vram_total_bytes = cfg_.vram_total_bytes;
-      in.kfd_gpu_id = 40000 + d;
-      in.kfd_node = 2 + d;
-      in.drm_card = 8 * d;
-      in.hip_id = d;
-      in.compute_partition = "SPX";
-      in.memory_partition = "NPS1";
-      in.partition_id = 0;
-      infos_.push_back(in);
-      rng_.push_back(cfg_.seed * 0x9E3779B97F4A7C15ull + static_cast<uint64_t>(d) + 1);
+  explicit MockBackend(const MockConfig& c) : cfg_(c), t0_(mono_ns()), parts_(parts_of(c)) {
+    const int xcc_per = kMaxXcc / parts_;
+    for (int g = 0; g < cfg_.n_gpus; ++g) {
+      for (int p = 0; p < parts_; ++p) {
+        const int d = g * parts_ + p;
+        DeviceInfo in;
+        in.index = d;
+        char bdf[32];
+        std::snprintf(bdf, sizeof bdf, "0000:%02x:00.0", 0x11 + 0x10 * g);
+        in.bdf = bdf;  // every partition of a GPU shares its PCI function
+        char uuid[64];
+        std::snprintf(uuid, sizeof uuid, "mock-75a3-0000-1000-80b8-%012d", d);
+        in.uuid = uuid;
+        in.serial = "MOCK" + std::to_string(g);
+        in.market_name = "AMD Instinct MI355 OAM";
+        in.gpu_type = gpu_type_from_market_name(in.market_name);
+        in.gfx_target = "gfx950";
+        in.numa_node = g < cfg_.n_gpus / 2 ? 0 : 1;
+        in.num_cu = 256 / parts_;
+        in.num_xcc = static_cast<uint32_t>(xcc_per);
+        in.xcc_first = static_cast<uint32_t>(p * xcc_per);
+        in.vram_total_bytes = cfg_.vram_total_bytes;
+        in.kfd_gpu_id = 40000 + d;
+        in.kfd_node = 2 + d;
+        in.drm_card = 8 * g + p;
+        in.hip_id = d;
+        in.compute_partition = cfg_.compute_partition;
+        in.memory_partition = "NPS1";
+        in.partition_id = p;
+        infos_.push_back(in);
+        rng_.push_back(cfg_.seed * 0x9E3779B97F4A7C15ull + static_cast<uint64_t>(d) + 1);
+      }
     }
-    rng_mu_ = std::vector<std::mutex>(static_cast<size_t>(cfg_.n_gpus));
+    rng_mu_ = std::vector<std::mutex>(infos_.size());
   }
 
   std::string name() const override { return "mock"; }
-  int device_count() const override { return cfg_.n_gpus; }
+  int device_count() const override { return static_cast<int>(infos_.size()); }
   const DeviceInfo& info(int d) const override { return infos_[d]; }
 
-  // Utilisation in percent at firmware time t (seconds).
-  double util(int d, double t) const {
-    const double u = cfg_.util_base + cfg_.util_amp * std::sin(kTwoPi * t / cfg_.util_period_s + 0.7 * d);
-    return u < 0 ? 0 : (u > 100 ? 100 : u);
-  }
-  // ∫_0^t util dt (percent·seconds), closed form (clamping ignored when base±amp ∈ [0,100]).
-  double util_integral(int d, double t) const {
-    const double w = kTwoPi / cfg_.util_period_s, ph = 0.7 * d;
-    return cfg_.util_base * t + cfg_.util_amp / w * (std::cos(ph) - std::cos(w * t + ph));
-  }
+  double util(int d, double t) const { return mock_device_util(cfg_, d, t); }
+  double util_integral(int d, double t) const { return mock_device_util_integral(cfg_, d, t); }
 
   // A vanished device stays gone for vanish_for_s, then needs recover(): like a
   // GPU reset, the firmware restarts with its accumulators at zero.
@@ -98,6 +132,7 @@ class MockBackend final : public Backend {
   int read_metrics(int d, GpuSample& s) override {
     const int64_t now = mono_ns();
     double t = (now - t0_) * 1e-9;
+    sleep_s(cfg_.metrics_latency_s);
     if (cfg_.stall_s > 0) std::this_thread::sleep_for(std::chrono::duration<double>(cfg_.stall_s));
     if (gone(d, t)) return -2;
     if (cfg_.fail_rate > 0 && next_uniform(d) < cfg_.fail_rate) return -1;
@@ -106,19 +141,30 @@ class MockBackend final : public Backend {
 
     // Firmware time: quantised to the PMFW cadence.
     const double tf = std::floor(t / cfg_.fw_period_s) * cfg_.fw_period_s;
-    const double u = util(d, tf);
+    // The PMFW table is per physical GPU: every XCC's busy and accumulator, the
+    // chip-wide mean, then (partitions) the device's own XCCs.
+    const int g = d / parts_;
+    const double u = parts_ > 1 ? chip_util(g, tf) : util(d, tf);
+    const double ui = parts_ > 1 ? chip_util_integral(g, tf) : util_integral(d, tf);
     s.fw_ts = static_cast<uint64_t>(tf * 1e8) + 1000;  // 10 ns units, never 0
     s.gfx_busy_pct = static_cast<float>(u);
     s.umc_busy_pct = static_cast<float>(u * 0.5);
     s.num_xcc = 8;
-    for (int x = 0; x < kMaxXcc; ++x) s.gfx_busy_xcc[x] = static_cast<float>(u);
     // Accumulators in PMFW units: accumulation_counter ticks once per ms,
     // gfx_activity_acc adds the busy percent every tick.
     const double ms = tf * 1000.0;
     s.accumulation_counter = static_cast<uint64_t>(std::llround(ms));
-    s.gfx_activity_acc = static_cast<uint64_t>(std::llround(util_integral(d, tf) * 1000.0));
-    s.mem_activity_acc = static_cast<uint64_t>(std::llround(util_integral(d, tf) * 500.0));
-    for (int x = 0; x < kMaxXcc; ++x) s.gfx_busy_acc_xcc[x] = s.gfx_activity_acc;
+    s.gfx_activity_acc = static_cast<uint64_t>(std::llround(ui * 1000.0));
+    s.mem_activity_acc = static_cast<uint64_t>(std::llround(ui * 500.0));
+    for (int x = 0; x < kMaxXcc; ++x) {
+      if (parts_ > 1) {
+        s.gfx_busy_xcc[x] = static_cast<float>(curve_util(cfg_, xcc_curve(cfg_, g, x), tf));
+        s.gfx_busy_acc_xcc[x] = static_cast<uint64_t>(std::llround(curve_integral(cfg_, xcc_curve(cfg_, g, x), tf) * 1000.0));
+      } else {
+        s.gfx_busy_xcc[x] = static_cast<float>(u);
+        s.gfx_busy_acc_xcc[x] = s.gfx_activity_acc;
+      }
+    }
     s.valid |= kFXccAcc;
     s.temp_hotspot_c = static_cast<float>(40 + 0.4 * u);
     s.temp_mem_c = static_cast<float>(35 + 0.2 * u);
@@ -149,12 +195,27 @@ class MockBackend final : public Backend {
     s.vram_used_bytes = (1ull << 30) + static_cast<uint64_t>(u * 1e9);
     s.valid |= kFGfxBusy | kFUmcBusy | kFGfxBusyXcc | kFTempHotspot | kFTempMem | kFTempVrSoc | kFPower |
                kFEnergy | kFGfxClk | kFUclk | kFSocClk | kFXgmi | kFPcie | kFVram | kFAcc | kFFwTs;
+    if (parts_ > 1) restrict_to_xccs(s, infos_[d].xcc_first, infos_[d].num_xcc);
     s.mono_ns = mono_ns();
     s.wall_ns = wall_ns();
     return 0;
   }
 
+  // Chip-wide mean over the 8 XCC curves of physical GPU g (partitioned mock).
+  double chip_util(int g, double t) const {
+    double u = 0;
+    for (int x = 0; x < kMaxXcc; ++x) u += curve_util(cfg_, xcc_curve(cfg_, g, x), t);
+    return u / kMaxXcc;
+  }
+  double chip_util_integral(int g, double t) const {
+    double u = 0;
+    for (int x = 0; x < kMaxXcc; ++x) u += curve_integral(cfg_, xcc_curve(cfg_, g, x), t);
+    return u / kMaxXcc;
+  }
+
   int read_procs(int d, std::vector<ProcInfo>& out) override {
+    std::lock_guard<std::mutex> lk(smi_mu_);
+    sleep_s(cfg_.proc_latency_s);
     out.clear();
     const double t = (mono_ns() - t0_) * 1e-9;
     if (gone(d, t)) return -2;
@@ -171,14 +232,17 @@ class MockBackend final : public Backend {
   }
 
   int read_links(int d, std::vector<LinkInfo>& out) override {
+    std::lock_guard<std::mutex> lk(smi_mu_);
+    sleep_s(cfg_.link_latency_s);
     out.clear();
     const double t = (mono_ns() - t0_) * 1e-9;
     int l = 0;
+    const int g = d / parts_;
     for (int p = 0; p < cfg_.n_gpus; ++p) {
-      if (p == d) continue;
+      if (p == g) continue;
       LinkInfo li;
-      li.link = ++l;
-      li.peer_bdf = infos_[p].bdf;
+      li.link = ++l;  // port 0 is the disabled self port, as on MI355X
+      li.peer_bdf = infos_[static_cast<size_t>(p * parts_)].bdf;
       li.link_type = 2;
       li.bit_rate_gbps = 38;
       li.max_bw_gbps = 608;
@@ -190,6 +254,8 @@ class MockBackend final : public Backend {
   }
 
   int read_health(int d, HealthInfo& out) override {
+    std::lock_guard<std::mutex> lk(smi_mu_);
+    sleep_s(cfg_.health_latency_s);
     const double t = (mono_ns() - t0_) * 1e-9;
     out.ecc_valid = true;
     out.ecc_correctable = static_cast<uint64_t>(t * static_cast<double>(cfg_.ecc_correctable_per_s));
@@ -201,9 +267,14 @@ class MockBackend final : public Backend {
 
   int topology(std::vector<TopoEdge>& out) override {
     out.clear();
-    for (int a = 0; a < cfg_.n_gpus; ++a)
-      for (int b = 0; b < cfg_.n_gpus; ++b)
-        if (a != b) out.push_back(TopoEdge{a, b, 2, 1, 15});
+    const int n = device_count();
+    for (int a = 0; a < n; ++a)
+      for (int b = 0; b < n; ++b) {
+        if (a == b) continue;
+        // partitions of one GPU share the die fabric: 0 hops; other GPUs: one xGMI hop
+        if (a / parts_ == b / parts_) out.push_back(TopoEdge{a, b, 2, 0, 0});
+        else out.push_back(TopoEdge{a, b, 2, 1, 15});
+      }
     return 0;
   }
 
@@ -219,6 +290,8 @@ class MockBackend final : public Backend {
 
   MockConfig cfg_;
   int64_t t0_;
+  int parts_;              // devices per physical GPU (compute partitions)
+  std::mutex smi_mu_;      // the management library's process-wide lock (latency model)
   std::atomic<int64_t> reset_ns_{0};
   std::vector<DeviceInfo> infos_;
   std::vector<uint64_t> rng_;
@@ -228,5 +301,23 @@ class MockBackend final : public Backend {
 }  // namespace
 
 std::unique_ptr<Backend> make_mock_backend(const MockConfig& cfg) { return std::make_unique<MockBackend>(cfg); }
+
+double mock_device_util(const MockConfig& cfg, int dev, double t) {
+  const int parts = parts_of(cfg);
+  if (parts == 1) return curve_util(cfg, dev, t);
+  const int g = dev / parts, p = dev % parts, per = kMaxXcc / parts;
+  double u = 0;
+  for (int x = p * per; x < (p + 1) * per; ++x) u += curve_util(cfg, xcc_curve(cfg, g, x), t);
+  return u / per;
+}
+
+double mock_device_util_integral(const MockConfig& cfg, int dev, double t) {
+  const int parts = parts_of(cfg);
+  if (parts == 1) return curve_integral(cfg, dev, t);
+  const int g = dev / parts, p = dev % parts, per = kMaxXcc / parts;
+  double u = 0;
+  for (int x = p * per; x < (p + 1) * per; ++x) u += curve_integral(cfg, xcc_curve(cfg, g, x), t);
+  return u / per;
+}
 
 }  // namespace kgs

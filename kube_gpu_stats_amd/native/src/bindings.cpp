@@ -36,6 +36,12 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.energy_wrap_at = get<uint64_t>(m, "energy_wrap_at", c.mock.energy_wrap_at);
     c.mock.seed = get<uint64_t>(m, "seed", c.mock.seed);
     c.mock.ecc_correctable_per_s = get<uint64_t>(m, "ecc_correctable_per_s", c.mock.ecc_correctable_per_s);
+    c.mock.square_duty = get<double>(m, "square_duty", c.mock.square_duty);
+    c.mock.compute_partition = get<std::string>(m, "compute_partition", c.mock.compute_partition);
+    c.mock.proc_latency_s = get<double>(m, "proc_latency_s", c.mock.proc_latency_s);
+    c.mock.link_latency_s = get<double>(m, "link_latency_s", c.mock.link_latency_s);
+    c.mock.health_latency_s = get<double>(m, "health_latency_s", c.mock.health_latency_s);
+    c.mock.metrics_latency_s = get<double>(m, "metrics_latency_s", c.mock.metrics_latency_s);
   }
   if (d.contains("mock_pmc")) {
     py::dict m = d["mock_pmc"].cast<py::dict>();
@@ -67,6 +73,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.node_name = get<std::string>(d, "node_name", c.node_name);
   c.gpu_type_override = get<std::string>(d, "gpu_type_override", c.gpu_type_override);
   c.window_s = get<double>(d, "window_s", c.window_s);
+  c.stale_s = get<double>(d, "stale_s", c.stale_s);
   c.per_process = get<bool>(d, "per_process", c.per_process);
   c.compat_series = get<bool>(d, "compat_series", c.compat_series);
   c.compat_unallocated = get<bool>(d, "compat_unallocated", c.compat_unallocated);
@@ -136,6 +143,7 @@ py::dict info_dict(const DeviceInfo& in) {
   o["compute_partition"] = in.compute_partition;
   o["memory_partition"] = in.memory_partition;
   o["partition_id"] = in.partition_id;
+  o["xcc_first"] = in.xcc_first;
   o["sysfs_dir"] = in.sysfs_dir;
   return o;
 }
@@ -207,6 +215,11 @@ class PyExporter {
     o["pmc_errors"] = I.pmc_errors;
     o["read_seconds"] = I.read_seconds;
     o["pmc_read_seconds"] = I.pmc_read_seconds;
+    o["mfma_busy_seconds"] = I.mfma_busy_seconds;
+    const DeviceState& st = ex_.sampler()->state(d);
+    o["proc_reads"] = st.proc_reads.load();
+    o["link_reads"] = st.link_reads.load();
+    o["slow_read_seconds"] = st.slow_ns_total.load() * 1e-9;
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
     return o;
@@ -337,6 +350,12 @@ class PyExporter {
     ex_.resume_sampling();
   }
   void set_pmc_enabled(bool on) { ex_.set_pmc_enabled(on); }
+  void set_sample_rate(double hz) {
+    py::gil_scoped_release r;
+    ex_.set_sample_rate(hz);
+  }
+  double sample_rate() const { return ex_.sample_rate(); }
+  uint64_t slow_passes() const { return ex_.sampler()->slow_passes(); }
   bool pmc_enabled() const { return ex_.pmc_enabled(); }
   bool sampling() const { return ex_.sampling(); }
 
@@ -391,7 +410,11 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def_property_readonly("sampling", &PyExporter::sampling)
       .def("set_pmc_enabled", &PyExporter::set_pmc_enabled, py::arg("on"),
            "Hand the hardware counters to another profiler (False) or take them back (True)")
-      .def_property_readonly("pmc_enabled", &PyExporter::pmc_enabled);
+      .def_property_readonly("pmc_enabled", &PyExporter::pmc_enabled)
+      .def("set_sample_rate", &PyExporter::set_sample_rate, py::arg("hz"),
+           "Change the sampler tick rate in place (threads restart; integrals continue)")
+      .def_property_readonly("sample_rate", &PyExporter::sample_rate)
+      .def_property_readonly("slow_passes", &PyExporter::slow_passes);
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
   m.def("pmc_counter_names", [] {

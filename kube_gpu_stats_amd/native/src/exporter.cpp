@@ -140,10 +140,27 @@ void Exporter::set_pmc_enabled(bool on) {
 }
 bool Exporter::pmc_enabled() const { return pmc_wanted_.load(); }
 
+void Exporter::set_sample_rate(double hz) {
+  if (sampler_) sampler_->set_hz(hz);
+}
+double Exporter::sample_rate() const { return sampler_ ? sampler_->config().hz : 0.0; }
+
 void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
+  Integrals I;
+  if (sampler_ && dev >= 0 && dev < sampler_->device_count()) sampler_->state(dev).integ.load(I);
   std::lock_guard<std::mutex> g(mu_);
   auto m = owners_ ? std::make_shared<std::map<int, std::vector<Owner>>>(*owners_)
                    : std::make_shared<std::map<int, std::vector<Owner>>>();
+  const auto prev = m->find(dev);
+  for (Owner& x : o) {
+    // An owner already on this GPU keeps its base; a new one starts counting now.
+    const Owner* kept = nullptr;
+    if (prev != m->end())
+      for (const Owner& y : prev->second)
+        if (y.same(x)) kept = &y;
+    x.base_busy_s = kept ? kept->base_busy_s : I.gfx_busy_seconds;
+    x.base_mfma_s = kept ? kept->base_mfma_s : I.mfma_busy_seconds;
+  }
   if (o.empty()) m->erase(dev);
   else (*m)[dev] = std::move(o);
   owners_ = std::move(m);

@@ -2,6 +2,7 @@
 #include "kgs/gpu_metrics.h"
 
 #include <cstring>
+#include <string>
 
 namespace kgs {
 
@@ -163,6 +164,39 @@ int parse_gpu_metrics_v1_8(const uint8_t* b, size_t len, GpuSample& s) {
 
   s.valid |= valid;
   return 0;
+}
+
+void restrict_to_xccs(GpuSample& s, uint32_t first, uint32_t count) {
+  if (count == 0 || first + count > s.num_xcc || (first == 0 && count == s.num_xcc)) return;
+  double inst = 0, acc = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const uint32_t x = first + k;
+    s.gfx_busy_xcc[k] = s.gfx_busy_xcc[x];
+    s.gfx_busy_acc_xcc[k] = s.gfx_busy_acc_xcc[x];
+    s.gfxclk_mhz[k] = s.gfxclk_mhz[x];
+    inst += s.gfx_busy_xcc[x];
+    acc += static_cast<double>(s.gfx_busy_acc_xcc[k]);
+  }
+  for (uint32_t k = count; k < static_cast<uint32_t>(kMaxXcc); ++k) {
+    s.gfx_busy_xcc[k] = 0;
+    s.gfx_busy_acc_xcc[k] = 0;
+    s.gfxclk_mhz[k] = 0;
+  }
+  s.num_xcc = count;
+  s.gfx_busy_pct = static_cast<float>(inst / count);
+  // Per-XCC accumulators share gfx_activity_acc's units (accumulated percent per
+  // accumulation_counter tick), so their mean is the partition's activity
+  // accumulator and Sampler::integrate needs no partition logic.
+  if (s.valid & kFXccAcc) s.gfx_activity_acc = static_cast<uint64_t>(acc / count + 0.5);
+}
+
+uint32_t partitions_of_mode(const char* mode) {
+  if (!mode) return 1;
+  const std::string m(mode);
+  if (m == "DPX") return 2;
+  if (m == "QPX") return 4;
+  if (m == "CPX") return 8;
+  return 1;
 }
 
 }  // namespace kgs

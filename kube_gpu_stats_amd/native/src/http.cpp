@@ -29,7 +29,29 @@ struct Conn {
   std::string out;
   size_t out_off = 0;
   bool close_after = false;
+  bool loopback = false;  // peer is 127.0.0.0/8 or ::1: may use /control/*
 };
+
+bool peer_is_loopback(const sockaddr_storage& a) {
+  if (a.ss_family == AF_INET)
+    return (ntohl(reinterpret_cast<const sockaddr_in&>(a).sin_addr.s_addr) >> 24) == 127;
+  if (a.ss_family == AF_INET6) {
+    const in6_addr& x = reinterpret_cast<const sockaddr_in6&>(a).sin6_addr;
+    if (IN6_IS_ADDR_LOOPBACK(&x)) return true;
+    return IN6_IS_ADDR_V4MAPPED(&x) && x.s6_addr[12] == 127;
+  }
+  return false;
+}
+
+double query_double(const std::string& q, const char* key, double dflt) {
+  const std::string k = std::string(key) + "=";
+  size_t p = 0;
+  while ((p = q.find(k, p)) != std::string::npos) {
+    if (p == 0 || q[p - 1] == '&') return std::strtod(q.c_str() + p + k.size(), nullptr);
+    p += k.size();
+  }
+  return dflt;
+}
 
 void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
 
@@ -216,7 +238,9 @@ void HttpServer::loop() {
       if (fd == wake_fd_) continue;
       if (fd == lfd_) {
         for (;;) {
-          const int c = accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          sockaddr_storage peer{};
+          socklen_t plen = sizeof peer;
+          const int c = accept4(lfd_, reinterpret_cast<sockaddr*>(&peer), &plen, SOCK_NONBLOCK | SOCK_CLOEXEC);
           if (c < 0) break;
           int one = 1;
           setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
@@ -224,7 +248,7 @@ void HttpServer::loop() {
           ev.events = EPOLLIN;
           ev.data.fd = c;
           epoll_ctl(efd_, EPOLL_CTL_ADD, c, &ev);
-          conns[c];
+          conns[c].loopback = peer_is_loopback(peer);
         }
         continue;
       }
@@ -272,13 +296,22 @@ void HttpServer::loop() {
             respond(c, 200, "OK", "text/plain; version=0.0.4; charset=utf-8", zbody, "gzip");
           else
             respond(c, 200, "OK", "text/plain; version=0.0.4; charset=utf-8", body);
+        } else if (target.compare(0, 9, "/control/") == 0 && !c.loopback) {
+          // Control is for processes on the exporter's own host / pod network
+          // namespace (`kubectl exec <pod> -- kgs pmc release`), never for scrapers.
+          respond(c, 403, "Forbidden", "text/plain", "control endpoints are loopback-only\n");
+        } else if (target == "/control/pmc/release" || target == "/control/pmc/acquire") {
+          ex_->set_pmc_enabled(target == "/control/pmc/acquire");
+          respond(c, 200, "OK", "application/json", ex_->pmc_enabled() ? "{\"pmc\":true}" : "{\"pmc\":false}");
         } else if (ex_->config().control_http && (target == "/control/pause" || target == "/control/resume")) {
           if (target == "/control/pause") ex_->pause_sampling();
           else ex_->resume_sampling();
           respond(c, 200, "OK", "application/json", ex_->sampling() ? "{\"sampling\":true}" : "{\"sampling\":false}");
-        } else if (ex_->config().control_http && (target == "/control/pmc/release" || target == "/control/pmc/acquire")) {
-          ex_->set_pmc_enabled(target == "/control/pmc/acquire");
-          respond(c, 200, "OK", "application/json", ex_->pmc_enabled() ? "{\"pmc\":true}" : "{\"pmc\":false}");
+        } else if (ex_->config().control_http && target == "/control/rate") {
+          // Benchmarks: switch the tick rate in place (one exporter serves every tier).
+          const double hz = query_double(query, "hz", 0);
+          if (hz > 0) ex_->set_sample_rate(hz);
+          respond(c, 200, "OK", "application/json", "{\"hz\":" + std::to_string(ex_->sample_rate()) + "}");
         } else if (target == "/healthz") {
           const bool ok = ex_->healthy();
           respond(c, ok ? 200 : 503, ok ? "OK" : "Service Unavailable", "text/plain", ok ? "ok\n" : "no device sampled\n");

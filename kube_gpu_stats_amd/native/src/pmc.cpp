@@ -110,9 +110,8 @@ class MockCounterSource final : public CounterSource {
   // Cumulative counts since the source opened, at time `now`.
   void fill(int dev, int64_t now, PmcSample& s) const {
     const double t = (now - t0_) * 1e-9;
-    const double w = 6.283185307179586 / b_.util_period_s, ph = 0.7 * dev;
-    // ∫ util/100 dt  (fraction-seconds)
-    const double busy_s = (b_.util_base * t + b_.util_amp / w * (std::cos(ph) - std::cos(w * t + ph))) / 100.0;
+    // ∫ util/100 dt (fraction-seconds): the mock backend's load curve for this device
+    const double busy_s = mock_device_util_integral(b_, dev, t) / 100.0;
     const double clk = c_.clock_mhz * 1e6;
     s.n = kPmcCount;
     s.value[kPmcGrbmCount] = static_cast<uint64_t>(clk * t);

@@ -176,16 +176,26 @@ void Exporter::render(std::string& out) {
   };
   static thread_local std::vector<Snap> snaps;
   snaps.assign(static_cast<size_t>(nd), Snap{});
+  const int64_t stale_ns = static_cast<int64_t>(cfg_.stale_s * 1e9);
   for (int d : ids) {
     Snap& x = snaps[static_cast<size_t>(d)];
     const DeviceState& st = S.state(d);
     x.have = st.latest.load(x.s);
     st.integ.load(x.I);
-    x.busy = x.have && S.window_busy(d, cfg_.window_s, x.g, x.u, x.n);
+    // Window gauges only from live data: a device that is down, or whose last
+    // good read is older than stale_s (reads failing, sampling paused), exports
+    // no busy gauges rather than its last value frozen; the counters stay.
+    const int64_t ok_ns = st.last_ok_mono_ns.load(std::memory_order_relaxed);
+    const bool pmfw_fresh = st.up.load(std::memory_order_relaxed) && ok_ns > 0 && now - ok_ns <= stale_ns;
+    x.busy = x.have && pmfw_fresh && S.window_busy(d, cfg_.window_s, x.g, x.u, x.n);
     x.pmc_have = st.pmc_latest.load(x.p);
-    // Stalled counters (a foreign profiler STOPped / reprogrammed them) give no
-    // rate gauges rather than wrong ones; the raw totals and kgs_pmc_stalled stay.
-    x.pmc_rates = x.pmc_have && !st.pmc_stalled.load(std::memory_order_relaxed) && S.window_pmc(d, cfg_.window_s, x.r);
+    // Counter rates only while we hold the counters and drains keep arriving:
+    // handed over (pmc_on = 0), stalled (a foreign profiler STOPped /
+    // reprogrammed them) or stale → no rate gauges rather than wrong or frozen
+    // ones; the raw totals and kgs_pmc_enabled / kgs_pmc_stalled stay.
+    x.pmc_rates = x.pmc_have && st.pmc_on.load(std::memory_order_relaxed) &&
+                  !st.pmc_stalled.load(std::memory_order_relaxed) && now - x.p.mono_ns <= stale_ns &&
+                  S.window_pmc(d, cfg_.window_s, x.r);
   }
 
   // ---- reference-compatible series (F5) ---------------------------------
@@ -193,9 +203,11 @@ void Exporter::render(std::string& out) {
     // Pod labels of every (GPU, owner) pair, built once for both per-pod families.
     static thread_local std::vector<std::pair<int, std::string>> pod_lines;
     pod_lines.clear();
+    static thread_local std::vector<const Owner*> pod_owner;  // parallel to pod_lines (nullptr: unallocated)
+    pod_owner.clear();
     for (int d : ids) {
       const Snap& x = snaps[static_cast<size_t>(d)];
-      if (!x.busy && !x.pmc_rates) continue;
+      if (!x.have) continue;
       const DeviceInfo& in = be_->info(d);
       const std::string type = cfg_.gpu_type_override.empty() ? in.gpu_type : cfg_.gpu_type_override;
       auto emit = [&](const Owner* o) {
@@ -209,6 +221,7 @@ void Exporter::render(std::string& out) {
         kv(lb, "gpu", std::to_string(d));
         kv(lb, "uuid", in.uuid);
         pod_lines.emplace_back(d, std::move(lb));
+        pod_owner.push_back(o);
       };
       auto it = own ? own->find(d) : decltype(own->end()){};
       if (own && it != own->end() && !it->second.empty()) {
@@ -222,6 +235,39 @@ void Exporter::render(std::string& out) {
            "(reference metric contract; label nvidia_gpu_type kept for compatibility)");
     for (const auto& [d, lb] : pod_lines)
       if (snaps[static_cast<size_t>(d)].busy) w.line("container_gpu_sm_util", lb, nullptr, snaps[static_cast<size_t>(d)].g);
+    // Exact per-pod accounting: the GPU's busy integral since the pod was given
+    // it.  rate() / increase() over any range is the exact mean utilisation,
+    // whatever the scrape interval — the gauge above only sees its window.
+    w.head("container_gpu_busy_seconds_total", "counter",
+           "GFX-engine busy seconds of the GPU allocated to the pod, counted from allocation (PMFW accumulators; "
+           "100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)");
+    for (size_t i = 0; i < pod_lines.size(); ++i) {
+      const Owner* o = pod_owner[i];
+      const double v = snaps[static_cast<size_t>(pod_lines[i].first)].I.gfx_busy_seconds - (o ? o->base_busy_s : 0.0);
+      w.line("container_gpu_busy_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
+    }
+    bool any_pmc_int = false;
+    for (const auto& pl : pod_lines) any_pmc_int |= snaps[static_cast<size_t>(pl.first)].pmc_have;
+    if (any_pmc_int) {
+      w.head("container_gpu_mfma_busy_seconds_total", "counter",
+             "MFMA-busy seconds (all SIMDs busy with matrix work for 1 s = 1) of the GPU allocated to the pod, counted "
+             "from allocation (hardware counters)");
+      for (size_t i = 0; i < pod_lines.size(); ++i) {
+        const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
+        if (!x.pmc_have) continue;
+        const Owner* o = pod_owner[i];
+        const double v = x.I.mfma_busy_seconds - (o ? o->base_mfma_s : 0.0);
+        w.line("container_gpu_mfma_busy_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
+      }
+    }
+    bool any_owner = false;
+    for (const Owner* o : pod_owner) any_owner |= o != nullptr;
+    if (any_owner) {
+      w.head("kgs_gpu_owner", "gauge",
+             "1 for every (GPU, pod, container) allocation the kubelet reports: join target for any amdgpu_* series");
+      for (size_t i = 0; i < pod_lines.size(); ++i)
+        if (pod_owner[i]) w.line("kgs_gpu_owner", pod_lines[i].second, nullptr, 1);
+    }
     bool any_mfma = false;
     for (const auto& pl : pod_lines) any_mfma |= snaps[static_cast<size_t>(pl.first)].pmc_rates;
     if (any_mfma) {
@@ -436,6 +482,9 @@ void Exporter::render(std::string& out) {
       for (int i = 0; i < kPmcCount; ++i)
         if (x.p.mask & (1u << i)) w.line_u("amdgpu_pmc_total", dev_labels_[d], pmc_counter_labels()[static_cast<size_t>(i)].c_str(), x.p.value[i]);
     }
+    w.head("amdgpu_mfma_busy_seconds_total", "counter",
+           "Integral of the MFMA-busy share of all SIMD cycles over time (hardware counters); rate() = matrix-core utilisation");
+    for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);
     w.head("amdgpu_mfma_util_percent", "gauge", "Matrix-core (MFMA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
     w.head("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active percent of clocks over the window");
@@ -555,6 +604,15 @@ void Exporter::render(std::string& out) {
     w.head("kgs_pmc_refreshes_total", "counter", "Periodic counter re-STARTs that reprogram the selects (--pmc-refresh-s)");
     for (int d : ids) w.line_u("kgs_pmc_refreshes_total", dev_labels_[d], nullptr, S.state(d).pmc_refreshes.load());
   }
+  w.head("kgs_slow_reads_total", "counter",
+         "Management-library reads by the node-wide slow thread (per-process list / xGMI link table + RAS)");
+  for (int d : ids) {
+    const DeviceState& st = S.state(d);
+    w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"procs\"", st.proc_reads.load(std::memory_order_relaxed));
+    w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"links\"", st.link_reads.load(std::memory_order_relaxed));
+  }
+  w.head("kgs_slow_read_seconds_total", "counter", "Time the node-wide slow thread spent in management-library calls");
+  for (int d : ids) w.line("kgs_slow_read_seconds_total", dev_labels_[d], nullptr, S.state(d).slow_ns_total.load(std::memory_order_relaxed) * 1e-9);
   w.head("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples");
   for (int d : ids) w.line("kgs_sampled_seconds_total", dev_labels_[d], nullptr, snaps[d].I.sampled_seconds);
   w.head("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read");

@@ -13,7 +13,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
-#include <unordered_map>
+#include <algorithm>
+#include <climits>
 
 namespace kgs {
 
@@ -81,7 +82,17 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
   }
   if (cfg_.hz <= 0) cfg_.hz = 1;
   for (int d : dev_ids_) states_[static_cast<size_t>(d)]->pmc_on.store(cfg_.pmc && pmc_ ? 1 : 0);
+  cu_seconds_.resize(static_cast<size_t>(n));
+  last_proc_ns_.assign(static_cast<size_t>(n), 0);
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+}
+
+void Sampler::set_hz(double hz) {
+  if (hz <= 0) return;
+  const bool was = running_.load();
+  stop();
+  cfg_.hz = hz;
+  if (was) start();
 }
 
 void Sampler::set_pmc_wanted(bool on) {
@@ -100,6 +111,7 @@ void Sampler::start() {
   while (read(stop_fd_, &drain, sizeof drain) > 0) {
   }
   for (int d : dev_ids_) threads_.emplace_back([this, d] { run(d); });
+  if (cfg_.proc_every > 0 || cfg_.link_every > 0) slow_thread_ = std::thread([this] { run_slow(); });
 }
 
 void Sampler::stop() {
@@ -111,6 +123,7 @@ void Sampler::stop() {
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   threads_.clear();
+  if (slow_thread_.joinable()) slow_thread_.join();
   running_.store(false);
 }
 
@@ -201,14 +214,10 @@ void Sampler::run(int dev) {
   PmcSample& pmc_base = st.pmc_base;
   int64_t last_acquire_fail_ns = 0;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
-  uint64_t prev_ps_count = 0;
+  uint64_t prev_ps_count = 0, prev_ps_mfma = 0;
   int64_t prev_ps_ns = 0;
   int64_t last_plausible_ns = mono_ns();
   int64_t last_start_ns = mono_ns();  // last (re)START of the counter session
-  std::vector<ProcInfo> procs;
-  std::vector<LinkInfo> links;
-  std::unordered_map<uint32_t, double> cu_seconds;  // pid -> ∫ occupancy share dt
-  int64_t last_proc_ns = 0;
 
   while (!stop_.load(std::memory_order_relaxed)) {
     // ---- fast tier: the PMFW table (refreshed by firmware every ≈20 ms) is
@@ -313,7 +322,16 @@ void Sampler::run(int dev) {
           const double mhz = raw >= prev_ps_count ? (raw - prev_ps_count) * 1e3 / (ps.mono_ns - prev_ps_ns) : 0.0;
           if (mhz >= kPlausibleMhzLo && mhz <= kPlausibleMhzHi) last_plausible_ns = ps.mono_ns;
         }
+        if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcMfmaBusy)) &&
+            ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcMfmaBusy] >= prev_ps_mfma) {
+          // MFMA-busy share of all SIMD-cycles in the interval, times its length.
+          const double simds = (info.num_cu > 0 ? info.num_cu : 256) * 4.0;
+          const double frac = static_cast<double>(ps.value[kPmcMfmaBusy] - prev_ps_mfma) /
+                              (simds * static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count));
+          I.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
+        }
         prev_ps_count = ps.value[kPmcGrbmCount];
+        prev_ps_mfma = ps.value[kPmcMfmaBusy];
         prev_ps_ns = ps.mono_ns;
         have_prev_ps = true;
         const int64_t stall = ps.mono_ns - last_plausible_ns;
@@ -357,40 +375,6 @@ void Sampler::run(int dev) {
       }
     }
 
-    // ---- mid / slow tiers -----------------------------------------------
-    if (cfg_.proc_every > 0 && tick % static_cast<uint64_t>(cfg_.proc_every) == 0) {
-      if (be_->read_procs(dev, procs) == 0) {
-        const int64_t now_p = mono_ns();
-        const double dt = last_proc_ns ? (now_p - last_proc_ns) * 1e-9 : 0.0;
-        const double ncu = info.num_cu > 0 ? info.num_cu : 256.0;
-        std::unordered_map<uint32_t, double> next_cu;
-        for (ProcInfo& p : procs) {
-          auto it = cu_seconds.find(p.pid);
-          const double prev_cu = it == cu_seconds.end() ? 0.0 : it->second;
-          p.cu_seconds = prev_cu + (it == cu_seconds.end() ? 0.0 : p.cu_occupancy / ncu * dt);
-          next_cu[p.pid] = p.cu_seconds;
-        }
-        cu_seconds.swap(next_cu);  // processes that exited drop out
-        last_proc_ns = now_p;
-        auto p = std::make_shared<const std::vector<ProcInfo>>(procs);
-        std::lock_guard<std::mutex> g(st.slow_mu);
-        st.procs = std::move(p);
-        st.procs_mono_ns = now_p;
-      }
-    }
-    if (cfg_.link_every > 0 && tick % static_cast<uint64_t>(cfg_.link_every) == 0) {
-      if (be_->read_links(dev, links) == 0) {
-        auto l = std::make_shared<const std::vector<LinkInfo>>(links);
-        std::lock_guard<std::mutex> g(st.slow_mu);
-        st.links = std::move(l);
-      }
-      HealthInfo h;
-      if (be_->read_health(dev, h) == 0) {
-        auto hp = std::make_shared<const HealthInfo>(h);
-        std::lock_guard<std::mutex> g(st.slow_mu);
-        st.health = std::move(hp);
-      }
-    }
     ++tick;
 
     // ---- schedule --------------------------------------------------------
@@ -423,19 +407,105 @@ void Sampler::run(int dev) {
   st.integ.store(I);
 }
 
+// Node-wide management-library tiers (see sampler.h).  Each due device is read
+// in turn; the per-GPU threads never wait on these calls.
+void Sampler::run_slow() {
+  pthread_setname_np(pthread_self(), "kgs-slow");
+  const int64_t tick_ns = static_cast<int64_t>(1e9 / cfg_.hz);
+  const int64_t proc_ns = cfg_.proc_every > 0 ? tick_ns * cfg_.proc_every : 0;
+  const int64_t link_ns = cfg_.link_every > 0 ? tick_ns * cfg_.link_every : 0;
+  int64_t next_proc = mono_ns(), next_link = next_proc;
+  std::vector<ProcInfo> procs;
+  std::vector<LinkInfo> links;
+  while (!stop_.load(std::memory_order_relaxed)) {
+    const int64_t t0 = mono_ns();
+    if (proc_ns > 0 && t0 >= next_proc) {
+      for (int dev : dev_ids_) {
+        if (stop_.load(std::memory_order_relaxed)) break;
+        DeviceState& st = *states_[static_cast<size_t>(dev)];
+        const int64_t a = mono_ns();
+        if (be_->read_procs(dev, procs) == 0) {
+          const int64_t now_p = mono_ns();
+          int64_t& last = last_proc_ns_[static_cast<size_t>(dev)];
+          const double dt = last ? (now_p - last) * 1e-9 : 0.0;
+          const int cu = be_->info(dev).num_cu;
+          const double ncu = cu > 0 ? cu : 256.0;
+          auto& cs = cu_seconds_[static_cast<size_t>(dev)];  // (pid, ∫ occupancy share dt), sorted by pid
+          std::vector<std::pair<uint32_t, double>> next_cs;
+          next_cs.reserve(procs.size());
+          for (ProcInfo& p : procs) {
+            auto it = std::lower_bound(cs.begin(), cs.end(), std::make_pair(p.pid, -1.0));
+            const bool known = it != cs.end() && it->first == p.pid;
+            p.cu_seconds = known ? it->second + p.cu_occupancy / ncu * dt : 0.0;
+            next_cs.emplace_back(p.pid, p.cu_seconds);
+          }
+          std::sort(next_cs.begin(), next_cs.end());
+          cs.swap(next_cs);  // processes that exited drop out
+          last = now_p;
+          auto sp = std::make_shared<const std::vector<ProcInfo>>(procs);
+          {
+            std::lock_guard<std::mutex> g(st.slow_mu);
+            st.procs = std::move(sp);
+            st.procs_mono_ns = now_p;
+          }
+          st.proc_reads.fetch_add(1, std::memory_order_relaxed);
+        } else {
+          st.proc_errors.fetch_add(1, std::memory_order_relaxed);
+        }
+        st.slow_ns_total.fetch_add(static_cast<uint64_t>(mono_ns() - a), std::memory_order_relaxed);
+      }
+      next_proc += proc_ns;
+      if (next_proc <= mono_ns()) next_proc = mono_ns() + proc_ns;  // a pass overran: skip, do not burst
+    }
+    if (link_ns > 0 && mono_ns() >= next_link) {
+      for (int dev : dev_ids_) {
+        if (stop_.load(std::memory_order_relaxed)) break;
+        DeviceState& st = *states_[static_cast<size_t>(dev)];
+        const int64_t a = mono_ns();
+        if (be_->read_links(dev, links) == 0) {
+          auto l = std::make_shared<const std::vector<LinkInfo>>(links);
+          std::lock_guard<std::mutex> g(st.slow_mu);
+          st.links = std::move(l);
+        }
+        HealthInfo h;
+        if (be_->read_health(dev, h) == 0) {
+          auto hp = std::make_shared<const HealthInfo>(h);
+          std::lock_guard<std::mutex> g(st.slow_mu);
+          st.health = std::move(hp);
+        }
+        st.link_reads.fetch_add(1, std::memory_order_relaxed);
+        st.slow_ns_total.fetch_add(static_cast<uint64_t>(mono_ns() - a), std::memory_order_relaxed);
+      }
+      next_link += link_ns;
+      if (next_link <= mono_ns()) next_link = mono_ns() + link_ns;
+    }
+    slow_passes_.fetch_add(1, std::memory_order_relaxed);
+    int64_t next = INT64_MAX;
+    if (proc_ns > 0) next = next_proc;
+    if (link_ns > 0 && next_link < next) next = next_link;
+    const int64_t wait = next - mono_ns();
+    if (wait > 0) {
+      timespec ts{static_cast<time_t>(wait / 1000000000LL), static_cast<long>(wait % 1000000000LL)};
+      pollfd pfd{stop_fd_, POLLIN, 0};
+      ppoll(&pfd, 1, &ts, nullptr);
+    }
+  }
+}
+
 bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, int& n) const {
   const DeviceState& st = *states_[dev];
   n = 0;
   GpuSample b, a, e;
-  if (st.ring.at(0, b) && b.cum_dt_s > 0) {
+  const uint64_t h = st.ring.head();  // one view of the ring for the whole search
+  if (st.ring.at_from(h, 0, b) && b.cum_dt_s > 0) {
     // Newest ring entry with at least window_s of firmware time after it: the
     // window mean is the difference of the two running sums (O(log ring) loads).
     const double want = b.cum_dt_s - window_s;
-    size_t lo = 1, hi = st.ring.available();
+    size_t lo = 1, hi = std::min<uint64_t>(h, kRing - 1);
     bool have = false;
     while (lo < hi) {
       const size_t mid = lo + (hi - lo) / 2;
-      if (!st.ring.at(mid, e)) {  // torn / overwritten under us: treat as too new
+      if (!st.ring.at_from(h, mid, e)) {  // torn / lapped under us: treat as too new
         lo = mid + 1;
         continue;
       }
@@ -448,8 +518,8 @@ bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, in
       }
     }
     if (!have) {  // window longer than the history held: use the oldest entry
-      const size_t m = st.ring.available();
-      have = m > 1 && st.ring.at(m - 1, a);
+      const size_t m = std::min<uint64_t>(h, kRing - 1);
+      have = m > 1 && st.ring.at_from(h, m - 1, a);
     }
     if (have && b.cum_dt_s > a.cum_dt_s) {
       const double dt = b.cum_dt_s - a.cum_dt_s;
@@ -474,13 +544,14 @@ bool Sampler::window_pmc(int dev, double window_s, PmcRates& out) const {
   // Binary search the decimated ring (time-ordered, newest first) for the newest
   // entry at least window_s older than `b`; fall back to the oldest one held.
   const int64_t want = b.mono_ns - static_cast<int64_t>(window_s * 1e9);
-  size_t lo = 0, hi = st.pmc_slow_ring.available();
+  const uint64_t h = st.pmc_slow_ring.head();
+  size_t lo = 0, hi = std::min<uint64_t>(h, kPmcSlowRing - 1);
   if (hi == 0) return false;
   PmcSample a, e;
   bool have_a = false;
   while (lo < hi) {
     const size_t mid = lo + (hi - lo) / 2;
-    if (!st.pmc_slow_ring.at(mid, e)) {  // torn / overwritten under us: treat as too new
+    if (!st.pmc_slow_ring.at_from(h, mid, e)) {  // torn / lapped under us: treat as too new
       lo = mid + 1;
       continue;
     }
@@ -493,8 +564,8 @@ bool Sampler::window_pmc(int dev, double window_s, PmcRates& out) const {
     }
   }
   if (!have_a) {  // window longer than the history: use the oldest entry
-    const size_t n = st.pmc_slow_ring.available();
-    if (n == 0 || !st.pmc_slow_ring.at(n - 1, a)) return false;
+    const size_t n = std::min<uint64_t>(h, kPmcSlowRing - 1);
+    if (n == 0 || !st.pmc_slow_ring.at_from(h, n - 1, a)) return false;
   }
   if (a.mono_ns >= b.mono_ns) return false;
   out = pmc_rates(a, b, be_->info(dev).num_cu);
