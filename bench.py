@@ -3,26 +3,34 @@
 GPU-time overhead %, under synthetic gfx950 load (BASELINE.json "metric").
 
     python bench.py --gpus N --steps K --warmup W
-    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-One rank per GPU.  A *step* is one fixed block of synthetic load on every GPU
-(an MFMA-bound bf16 kernel + HBM triads, ops/hip/load_kernels.hip, + a HIP
-graph of 2000 tiny copies: the dispatch-bound part, where the counter reader's
-command-processor packets would cost the workload time).  Phases:
+With N > 1 and no torchrun environment, bench.py starts N rank processes itself
+(``torch.distributed.run``, 127.0.0.1) before anything touches a GPU, and exits
+with their status; under torchrun it is one of those ranks.  One rank per GPU;
+rank 0 prints the result line.
 
-  A  K steps, no exporter running                       (baseline, untimed for the result line)
-  B  K steps with the node exporter sampling every used GPU at --hz (PMFW table,
-     HBM, per-process list, xGMI, and hardware counters through rocprofiler-sdk)
-     while rank 0 scrapes /metrics at --scrape-hz      (THE timed region)
-  C  K steps, exporter stopped again                    (second baseline)
+A *step* is a fixed block of synthetic load on every GPU: a *unit* (an MFMA-bound
+bf16 kernel + HBM triads, ops/hip/load_kernels.hip, + a HIP graph of 2000 tiny
+copies — the dispatch-bound part, where the counter reader's command-processor
+packets would cost the workload time) repeated until the step lasts ≥ --step-ms
+(default 500 ms), so every timed region is long against timer and DVFS noise.
 
-``value`` = counter samples/s summed over the N GPUs (weak scaling: per-GPU work
-and sampling rate are fixed).  A counter sample is one hardware-counter drain
-(GRBM/SQ/TCC values advance on every drain) when rocprofiler-sdk counting is
-available, else one distinct PMFW table (new firmware timestamp).  Overhead % =
-100 · (t_B / mean(t_A, t_C) − 1), same device, same process.  Scrape latency is
-request → last body byte on a keep-alive connection, as a Prometheus server sees
-it (utils/scrape.py; body decoding happens after the clock stops).
+  A  K steps, no exporter process                       (baseline)
+  B  K steps, node exporter sampling every GPU at --hz (PMFW table, HBM, per-process
+     list, xGMI, hardware counters) and scraped at --scrape-hz      (THE timed region)
+  I  --rounds rounds of one block per condition — exporter paused, then each rate of
+     --hz-list — in alternating order (off,100,8k | 8k,100,off | ...), --block-steps
+     steps per block, scraped while sampling.  Per round, overhead = t_on/t_off − 1;
+     the result is the mean over rounds ± a 95 % t-interval.  Adjacent blocks share
+     thermal and power state, so slow drift cancels (A/B/C cannot do that).
+  C  K steps, exporter stopped                           (second baseline)
+
+``value`` = counter samples/s summed over the N GPUs (the driver's contract: the
+whole-job aggregate; weak scaling, per-GPU rate fixed).  ``samples_per_sec_per_gpu``
+is the per-GPU figure the metric name refers to.  A counter sample is one hardware-
+counter drain (values advance on every drain), or one distinct PMFW table where
+the counter tier is unavailable.  Scrape latency is request → last body byte on a
+keep-alive connection, as a Prometheus server sees it (utils/scrape.py).
 
 The exporter runs as its own process (as in production: DaemonSet vs workload),
 launched by local rank 0 over the PCI addresses of every local rank's GPU.
@@ -32,8 +40,10 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import select
+import socket
 import subprocess
 import sys
 import time
@@ -45,57 +55,126 @@ from kube_gpu_stats_amd.parallel import dist as D  # noqa: E402
 from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text  # noqa: E402
 
 METRIC = "counter samples/sec/GPU + p50 scrape latency at 8×MI355X; GPU-time overhead %"
-AUTO_PMC = "aqlprofile"  # direct CP reads: same counters, ≈10× less exporter CPU than rocprofiler-sdk
+PMC_READER = "aqlprofile"  # direct CP reads (native/counters/pmc_aqlprofile.cpp)
 
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--hz", type=float, default=8000.0,
-                    help="sampler tick rate per GPU: one hardware-counter drain per tick (PMFW table ≤100 Hz); "
-                    "8 kHz costs ≈0.08 exporter cores/GPU with pipelined reads (profiles/r1/pipelined)")
-    ap.add_argument("--pmc", default="auto", choices=["auto", "aqlprofile", "rocprofiler", "none"],
-                    help="counter reader (auto = %s)" % AUTO_PMC)
+                    help="primary sampler tick rate per GPU (phase B): one hardware-counter drain per tick "
+                    "(PMFW table ≤ 100 Hz); 8 kHz costs ≈0.05 exporter cores/GPU (profiles/r1/pipelined)")
+    ap.add_argument("--hz-list", default="100",
+                    help="further tick rates measured in the interleaved rounds (BASELINE config 4 = 100 Hz); "
+                    "'' = primary only")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "aqlprofile", "none"],
+                    help="counter reader (auto = %s)" % PMC_READER)
     ap.add_argument("--pmc-pipeline", type=int, default=1, choices=[0, 1],
                     help="aqlprofile reader: pipelined READs (1) or submit-and-wait per sample (0)")
     ap.add_argument("--pmc-set", default="base", choices=["base", "full"],
                     help="counter set: base (GRBM + MFMA busy) or full (+ TA busy, 10x the CP register reads)")
     ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
-    ap.add_argument("--scrape-hz", type=float, default=10.0)
-    ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per step on MI355X")
+    ap.add_argument("--scrape-hz", type=float, default=20.0)
+    ap.add_argument("--step-ms", type=float, default=500.0,
+                    help="each step repeats the load unit until it lasts at least this long")
+    ap.add_argument("--rounds", type=int, default=16, help="interleaved rounds (0 = off)")
+    ap.add_argument("--block-steps", type=int, default=2, help="steps per interleaved block")
+    ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per unit on MI355X")
     ap.add_argument("--mfma-blocks", type=int, default=2048)
     ap.add_argument("--stream-gib", type=float, default=6.0)
     ap.add_argument("--triads", type=int, default=2)
     ap.add_argument("--tiny-kernels", type=int, default=2000,
-                    help="dispatch-bound part of each step: a HIP graph of this many 64 KiB copies (≈1.7 µs each); "
+                    help="dispatch-bound part of each unit: a HIP graph of this many 64 KiB copies (≈1.7 µs each); "
                     "it is where counter READs on the command processor would show up (0 = off)")
     ap.add_argument("--load", default="synthetic", choices=["synthetic", "train"],
-                    help="GPU work per step: the synthetic gfx950 kernels (default) or a PyTorch bf16 "
+                    help="GPU work per unit: the synthetic gfx950 kernels (default) or a PyTorch bf16 "
                     "decoder training step (forward + backward + AdamW, DDP when N > 1)")
     ap.add_argument("--train-dim", type=int, default=4096)
     ap.add_argument("--train-layers", type=int, default=4)
     ap.add_argument("--train-batch", type=int, default=4)
     ap.add_argument("--train-seq", type=int, default=2048)
     ap.add_argument("--train-vocab", type=int, default=32768)
-    ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per step when N > 1 (0 = off)")
-    ap.add_argument("--interleave", type=int, default=4,
-                    help="after phase B: this many off/on block pairs (ABBA order; exporter paused vs sampling "
-                    "and scraped, --steps/4 steps per block) -> overhead_interleaved_pct, which cancels the "
-                    "slow thermal/power drift that an A-B-C comparison sees (0 = off)")
+    ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per unit when N > 1 (0 = off)")
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
-    ap.add_argument("--mock-step-ms", type=float, default=20.0)
+    ap.add_argument("--mock-step-ms", type=float, default=20.0, help="mock: duration of one load unit")
+    ap.add_argument("--mock-latency", type=int, default=1, choices=[0, 1],
+                    help="mock: model AMD SMI call latency under one global lock (profiles/r2/mock_scaling.md)")
     ap.add_argument("--out", default="", help="also write the result JSON here")
     ap.add_argument("--attach", default="", help="host:port of an exporter started with --control-http; it is "
                     "paused for phases A/C instead of being spawned (lets rocprofv3 trace the bench alone)")
     return ap.parse_args(argv)
 
 
+def tiers(a) -> list[float]:
+    """Every tick rate measured: the primary --hz plus --hz-list, ascending."""
+    extra = [float(x) for x in str(a.hz_list).split(",") if x.strip()]
+    return sorted({float(a.hz), *extra})
+
+
+# ----------------------------------------------------------------------------- rank launch
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(a, argv: list[str]) -> int:
+    """``--gpus N`` without a torchrun environment: start N ranks (one per GPU) with
+    torch.distributed.run as a child process and return its exit status.  This
+    process never initialises a GPU (no HIP call happens before the children run),
+    so nothing here is replaced by exec and no device is held twice."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, cwd=REPO, env=env)
+
+
+# ----------------------------------------------------------------------------- statistics
+T975 = {1: 12.706, 2: 4.303, 3: 3.182, 4: 2.776, 5: 2.571, 6: 2.447, 7: 2.365, 8: 2.306, 9: 2.262, 10: 2.228,
+        11: 2.201, 12: 2.179, 13: 2.160, 14: 2.145, 15: 2.131, 16: 2.120, 17: 2.110, 18: 2.101, 19: 2.093,
+        20: 2.086, 24: 2.064, 29: 2.045, 39: 2.023, 59: 2.001}
+
+
+def t975(df: int) -> float:
+    """Two-sided 95 % Student-t quantile (table; 1.96 beyond 60 degrees of freedom)."""
+    if df <= 0:
+        return float("nan")
+    for k in sorted(T975):
+        if df <= k:
+            return T975[k]
+    return 1.96
+
+
+def mean_ci95(xs: list[float]) -> tuple[float, float, float]:
+    """(mean, 95 % half-width, sample SD) of paired differences."""
+    n = len(xs)
+    if n == 0:
+        return float("nan"), float("nan"), float("nan")
+    m = sum(xs) / n
+    if n == 1:
+        return m, float("nan"), float("nan")
+    sd = math.sqrt(sum((x - m) ** 2 for x in xs) / (n - 1))
+    return m, t975(n - 1) * sd / math.sqrt(n), sd
+
+
 # ----------------------------------------------------------------------------- load
-class GpuLoad:
+class Load:
+    """A step = ``reps`` back-to-back units (set by calibrate_reps)."""
+
+    reps = 1
+
+    def step(self):
+        for _ in range(self.reps):
+            self.unit()
+
+
+class GpuLoad(Load):
     def __init__(self, a, device: int, ctx=None):
         import torch
 
@@ -130,7 +209,7 @@ class GpuLoad:
         if ctx is not None and ctx.is_dist and a.xgmi_mib > 0:
             self.ar = torch.ones(int(a.xgmi_mib) << 18, dtype=torch.float32, device=torch.device("cuda", device))
 
-    def step(self):
+    def unit(self):
         self.ls.run_mfma()
         for _ in range(self.triads):
             self.ls.run_stream()
@@ -235,7 +314,7 @@ class TrainLoad(GpuLoad):
         self.tok = torch.randint(0, self.vocab, (self.batch, self.seq + 1), device=dev, generator=g)
         self.F = F
 
-    def step(self):
+    def unit(self):
         logits = self.model(self.tok[:, :-1])
         loss = self.F.cross_entropy(logits.float().view(-1, self.vocab), self.tok[:, 1:].reshape(-1))
         loss.backward()
@@ -246,7 +325,7 @@ class TrainLoad(GpuLoad):
         torch = self.torch
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        self.step()
+        self.unit()
         e1.record()
         torch.cuda.synchronize()
         s = e0.elapsed_time(e1) * 1e-3
@@ -256,78 +335,21 @@ class TrainLoad(GpuLoad):
                 "train_tflops": 6.0 * self.params * toks / s / 1e12}
 
 
-class MockLoad:
+class MockLoad(Load):
     def __init__(self, a, device: int):
         self.dt = a.mock_step_ms * 1e-3
 
-    def step(self):
+    def unit(self):
         time.sleep(self.dt)  # releases the GIL like a GPU sync would
 
     def sync(self):
         pass
 
     def calibrate(self) -> dict:
-        return {"mock_step_ms": self.dt * 1e3}
+        return {"mock_unit_ms": self.dt * 1e3}
 
     def pci_bdf(self, device: int) -> str:
         return f"0000:{0x11 + 0x10 * device:02x}:00.0"  # mock provider's BDF scheme
-
-
-PHASES: dict[str, list[float]] = {}
-
-
-def timed(ctx, load, k: int, name: str = "") -> float:
-    """Barrier + sync on both sides; returns the MAX over ranks of the wall time.
-
-    The wall-clock (epoch) bounds of each phase are kept in PHASES so a
-    rocprofv3 kernel trace of the run can be split into exporter-off / -on
-    phases (tools/rocprof_overhead.py)."""
-    D.barrier(ctx)
-    load.sync()
-    w0 = time.time()
-    t0 = time.perf_counter()
-    for _ in range(k):
-        load.step()
-    load.sync()
-    D.barrier(ctx)
-    dt = time.perf_counter() - t0
-    if name:
-        PHASES[name] = [w0, time.time()]
-    return D.all_reduce(ctx, [dt], "max")[0]
-
-
-def interleaved(ctx, load, exp, a) -> dict:
-    """Off/on blocks in ABBA order (off,on, on,off, ...) with the exporter process up:
-    *off* = sampling paused (no PMFW / counter reads, no scrapes), *on* = sampling at
-    --hz and scraped at --scrape-hz.  Pairs of adjacent blocks see the same thermal
-    and power state, so slow drift cancels; the A-B-C phases cannot do that."""
-    if a.interleave <= 0:
-        return {}
-    blk = max(3, a.steps // 4)
-    t_on = t_off = 0.0
-    blocks = []
-    for r in range(a.interleave):
-        for on in ((False, True) if r % 2 == 0 else (True, False)):
-            sc = None
-            if exp is not None:
-                if on:
-                    exp.resume()
-                    sc = Scraper("127.0.0.1", exp.port).start(a.scrape_hz)
-                else:
-                    exp.pause()
-            D.barrier(ctx)
-            dt = timed(ctx, load, blk)
-            if sc is not None:
-                sc.stop()
-            blocks.append([int(on), round(dt, 6)])
-            if on:
-                t_on += dt
-            else:
-                t_off += dt
-    if exp is not None:
-        exp.resume()
-    return {"overhead_interleaved_pct": 100.0 * (t_on / t_off - 1.0), "interleave_blocks": blocks,
-            "interleave_steps_per_block": blk}
 
 
 # ----------------------------------------------------------------------------- exporter
@@ -349,6 +371,9 @@ class AttachedExporter:
     def resume(self):
         self.sc.get("/control/resume")
 
+    def set_rate(self, hz: float):
+        self.sc.get(f"/control/rate?hz={hz:g}")
+
     def stop(self) -> dict:
         self.pause()
         m = parse_text(self.sc.get())
@@ -363,27 +388,22 @@ class AttachedExporter:
 
 class ExporterProc:
     def __init__(self, a, bdfs: list[str], log_path: str):
+        # Production tiers: per-process list at 10 Hz, xGMI links + RAS at 1 Hz (node-wide
+        # slow thread), gauges over a 2 s window (phase B is ~10 s).
         cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
-               "--hz", str(a.hz), "--proc-every", str(max(1, int(a.hz // 10))),
-               "--link-every", str(max(1, int(a.hz))), "--control-stdin", "--control-http", "--node-name", "bench-node",
-               "--bdfs", ",".join(bdfs)]
+               "--hz", str(a.hz), "--proc-period", "0.1", "--link-period", "1.0", "--window", "2",
+               "--control-stdin", "--control-http", "--node-name", "bench-node", "--bdfs", ",".join(bdfs)]
         if a.mock:
             cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock"]
+            if a.mock_latency:
+                cmd += ["--mock-latency"]
         else:
-            pmc = AUTO_PMC if a.pmc == "auto" else a.pmc
+            pmc = PMC_READER if a.pmc == "auto" else a.pmc
             cmd += ["--pmc", pmc, "--pmc-pipeline" if a.pmc_pipeline else "--no-pmc-pipeline", "--pmc-set", a.pmc_set,
                     "--pmc-lean", str(a.pmc_lean)]
         env = dict(os.environ)
         env.setdefault("KGS_NO_BUILD", "1")
         env.setdefault("PYTHONFAULTHANDLER", "1")  # a native fault leaves a trace in the exporter log
-        if not a.mock and "--pmc" in cmd and cmd[cmd.index("--pmc") + 1] == "rocprofiler" \
-                and env.get("ROCP_TOOL_LIBRARIES"):
-            # Running under rocprofv3: rocprofiler configuration closes before the
-            # exporter could force-register, so join as a listed tool library.
-            from kube_gpu_stats_amd.native import pmc_lib_path
-
-            env["ROCP_TOOL_LIBRARIES"] = env["ROCP_TOOL_LIBRARIES"] + ":" + pmc_lib_path()
-            env["KGS_PMC_AS_TOOL"] = "1"
         self.log = open(log_path, "w")
         self.p = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.log,
                                   text=True, env=env)
@@ -396,6 +416,9 @@ class ExporterProc:
 
     def resume(self):
         self.sc.get("/control/resume")
+
+    def set_rate(self, hz: float):
+        self.sc.get(f"/control/rate?hz={hz:g}")
 
     def _wait_ready(self, timeout: float) -> dict:
         end = time.time() + timeout
@@ -501,15 +524,147 @@ def observed(m: dict) -> dict:
     return out
 
 
-# ----------------------------------------------------------------------------- main
-def main(argv=None) -> int:
-    a = parse_args(argv)
-    use_cuda = not a.mock
-    ctx = D.init_from_env(use_cuda)
-    if ctx.world != a.gpus:
-        if ctx.rank == 0:
-            print(f"warning: --gpus {a.gpus} but WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
+# ----------------------------------------------------------------------------- phases
+PHASES: dict[str, list[float]] = {}
+
+
+def timed(ctx, load, k: int, name: str = "") -> float:
+    """Barrier + sync on both sides; returns the MAX over ranks of the wall time.
+
+    The wall-clock (epoch) bounds of each named phase are kept in PHASES so a
+    rocprofv3 kernel trace of the run can be split into exporter-off / -on
+    phases (tools/rocprof_overhead.py)."""
+    D.barrier(ctx)
+    load.sync()
+    w0 = time.time()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        load.step()
+    load.sync()
+    D.barrier(ctx)
+    dt = time.perf_counter() - t0
+    if name:
+        PHASES[name] = [w0, time.time()]
+    return D.all_reduce(ctx, [dt], "max")[0]
+
+
+def calibrate_reps(ctx, load, step_ms: float) -> tuple[int, float]:
+    """Units per step so one step lasts ≥ step_ms on the slowest rank."""
+    load.unit()
+    load.sync()
+    D.barrier(ctx)
+    t0 = time.perf_counter()
+    load.unit()
+    load.sync()
+    unit_s = D.all_reduce(ctx, [time.perf_counter() - t0], "max")[0]
+    return max(1, math.ceil(step_ms * 1e-3 / max(unit_s, 1e-6))), unit_s
+
+
+class Rates:
+    """Per-GPU sample counts over a set of windows, from /metrics counter deltas."""
+
+    def __init__(self):
+        self.pmc: dict[str, float] = {}
+        self.pmfw: dict[str, float] = {}
+        self.secs = 0.0
+
+    def add(self, before: dict, after: dict, secs: float) -> None:
+        bp, bc = sample_counts(before)
+        ap_, ac = sample_counts(after)
+        for g in ap_:
+            self.pmfw[g] = self.pmfw.get(g, 0.0) + ap_[g] - bp.get(g, 0.0)
+            self.pmc[g] = self.pmc.get(g, 0.0) + ac.get(g, 0.0) - bc.get(g, 0.0)
+        self.secs += secs
+
+    def per_gpu(self, pmc_on: bool) -> tuple[dict, str]:
+        """Per GPU: its counter stream if it delivered one, else its PMFW table rate,
+        so one device whose counter tier failed lowers the total by its own share only."""
+        if self.secs <= 0:
+            return {}, "none"
+        gpus = sorted(self.pmfw, key=int)
+        out, n_pmc = {}, 0
+        for g in gpus:
+            if pmc_on and self.pmc.get(g, 0) > 0:
+                out[g] = self.pmc[g] / self.secs
+                n_pmc += 1
+            else:
+                out[g] = self.pmfw[g] / self.secs
+        src = "pmc" if n_pmc == len(gpus) else ("pmfw" if n_pmc == 0 else f"pmc on {n_pmc}/{len(gpus)} GPUs")
+        return out, src
+
+
+def pct(xs: list[float], q: float) -> float | None:
+    if not xs:
+        return None
+    s = sorted(xs)
+    return s[min(len(s) - 1, int(q * len(s)))]
+
+
+def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
+    """Rounds of blocks: exporter paused (0) and sampling at each rate in ``hzs``,
+    order reversed every other round (0,100,8k | 8k,100,0 | ...).  Paused means the
+    sampler threads are stopped — no PMFW read, no counter READ, no scrape — while
+    the process and its counter session stay up, so the paired difference is the
+    cost of sampling + scraping (phase A/C vs B adds the cost of the process and
+    of holding the counters, ≈0 on MI355X; see ``overhead_abc_pct``)."""
+    if a.rounds <= 0:
+        return {}
+    conds = [0.0] + list(hzs)
+    rows: list[dict] = []
+    rates = {h: Rates() for h in hzs}
+    lat: dict[float, list[float]] = {h: [] for h in hzs}
+    paused_reads = 0.0
+    for r in range(a.rounds):
+        order = conds if r % 2 == 0 else conds[::-1]
+        times = {}
+        for c in order:
+            sc = None
+            before: dict = {}
+            w0 = 0.0
+            if exp is not None:
+                if c == 0:
+                    exp.pause()
+                else:
+                    exp.set_rate(c)
+                    exp.resume()
+                before = parse_text(exp.sc.get())
+                if c > 0:
+                    sc = Scraper("127.0.0.1", exp.port).start(a.scrape_hz)
+                w0 = time.perf_counter()
+            dt = timed(ctx, load, a.block_steps)
+            if exp is not None:
+                if sc is not None:
+                    sc.stop()
+                after = parse_text(exp.sc.get())
+                win = time.perf_counter() - w0
+                if c > 0:
+                    rates[c].add(before, after, win)
+                    lat[c].extend(sc.latencies_s)
+                else:  # paused really means no reads
+                    rb = {lb["gpu"]: v for lb, v in before.get("kgs_reads_total", [])}
+                    paused_reads += sum(v - rb.get(g, 0.0) for g, v in
+                                        ((lb["gpu"], v) for lb, v in after.get("kgs_reads_total", [])))
+            times[c] = dt
+        rows.append(times)
+    if exp is not None:
+        exp.set_rate(a.hz)
+        exp.resume()
+    out: dict = {"rounds": a.rounds, "block_steps": a.block_steps, "block_order": "alternating",
+                 "paused_reads": paused_reads, "tiers": {}}
+    for h in hzs:
+        diffs = [100.0 * (row[h] / row[0.0] - 1.0) for row in rows]
+        m, ci, sd = mean_ci95(diffs)
+        out["tiers"][f"{h:g}"] = {"overhead_pct": m, "overhead_ci95_pct": ci, "overhead_sd_pct": sd,
+                                  "overhead_per_round_pct": [round(d, 4) for d in diffs],
+                                  "_rates": rates[h], "_lat": lat[h]}
+    out["block_seconds"] = [[f"{c:g}", round(row[c], 6)] for row in rows for c in row]
+    return out
+
+
+def run(a, ctx) -> dict | None:
     n = ctx.world
+    hzs = tiers(a)
+    a.hz = hzs[-1]  # the fastest tier is the primary (phase B)
     if ctx.local_rank == 0 and not a.attach:
         # The exporter child runs with KGS_NO_BUILD=1: make sure its artefacts exist
         # (incremental no-op when the in-tree .so files are current).
@@ -517,7 +672,6 @@ def main(argv=None) -> int:
 
         B.build_native()
         if not a.mock:
-            B.build_pmc()
             B.build_pmc_aql()
     if a.mock:
         load = MockLoad(a, ctx.local_rank)
@@ -526,10 +680,11 @@ def main(argv=None) -> int:
     else:
         load = GpuLoad(a, ctx.local_rank, ctx)
 
+    calib = load.calibrate()
+    load.reps, unit_s = calibrate_reps(ctx, load, a.step_ms)
     for _ in range(a.warmup):
         load.step()
     load.sync()
-    calib = load.calibrate()
 
     # phase A: no exporter (an attached exporter is paused: process up, no reads)
     attached = None
@@ -547,6 +702,7 @@ def main(argv=None) -> int:
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
         try:
             if attached is not None:
+                attached.set_rate(a.hz)
                 attached.resume()
                 exp = attached
             else:
@@ -555,116 +711,141 @@ def main(argv=None) -> int:
             err = str(e)
     err = D.broadcast_object(ctx, err)
     if err:
-        if ctx.rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "error": err}))
-        D.destroy(ctx)
-        return 1
+        return {"metric": METRIC, "value": None, "error": err}
     time.sleep(a.settle)
 
-    scraper = None
+    # phase B: exporter on at the primary rate, scraped (THE timed region)
+    sc_b = None
     before = after = {}
-    t_w0 = t_w1 = 0.0
+    win = 0.0
     exp_pid = int(exp.ready.get("pid", 0) or 0) if exp is not None else 0
     cpu0 = cpu1 = 0.0
     thr0: dict = {}
     thr1: dict = {}
     if exp is not None:
-        scraper = Scraper("127.0.0.1", exp.port)
-        before = parse_text(scraper.get())
-        cpu0 = proc_cpu_seconds(exp_pid)
-        thr0 = thread_cpu_seconds(exp_pid)
-        t_w0 = time.perf_counter()
-        scraper.start(a.scrape_hz)
-    # phase B: exporter on (timed)
+        sc_b = Scraper("127.0.0.1", exp.port)
+        before = parse_text(sc_b.get())
+        cpu0, thr0 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
+        w0 = time.perf_counter()
+        sc_b.start(a.scrape_hz)
     t_b = timed(ctx, load, a.steps, "B_on")
     if exp is not None:
-        scraper.stop()
-        after = parse_text(scraper.get())
-        t_w1 = time.perf_counter()
-        cpu1 = proc_cpu_seconds(exp_pid)
-        thr1 = thread_cpu_seconds(exp_pid)
-    inter = interleaved(ctx, load, exp, a)
+        sc_b.stop()
+        after = parse_text(sc_b.get())
+        win = time.perf_counter() - w0
+        cpu1, thr1 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
+
+    inter = interleaved(ctx, load, exp, a, hzs)
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
     t_c = timed(ctx, load, a.steps, "C_off")
+    if exp is None:
+        return None
 
-    result = None
-    if exp is not None:
-        b_pmfw, b_pmc = sample_counts(before)
-        a_pmfw, a_pmc = sample_counts(after)
-        win = t_w1 - t_w0
-        gpus = sorted(a_pmfw, key=int)
-        pmfw_rate = {g: (a_pmfw[g] - b_pmfw.get(g, 0)) / win for g in gpus}
-        pmc_rate = {g: (a_pmc.get(g, 0) - b_pmc.get(g, 0)) / win for g in gpus}
-        pmc_on = exp.ready.get("pmc", "none") != "none" and sum(pmc_rate.values()) > 0
-        # Per GPU: its counter stream if it delivered one, else its PMFW table rate, so one
-        # device whose counter tier failed to open lowers the total by its own share only.
-        per_gpu = {g: (pmc_rate[g] if pmc_on and pmc_rate[g] > 0 else pmfw_rate[g]) for g in gpus}
-        n_pmc = sum(1 for g in gpus if pmc_on and pmc_rate[g] > 0)
-        source = "pmc" if n_pmc == len(gpus) else ("pmfw" if n_pmc == 0 else f"pmc on {n_pmc}/{len(gpus)} GPUs")
-        total = sum(per_gpu.values())
-        t_off = 0.5 * (t_a + t_c)
-        result = {
-            "metric": METRIC,
-            "value": total,
-            "unit": "samples/s",
-            "n_gpus": n,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": t_b * 1e3 / a.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": ("synthetic mock provider (CPU plumbing)" if a.mock
-                     else f"synthetic tokens, random-init {a.train_layers}-layer d={a.train_dim} bf16 decoder "
-                     "training step (fwd + bwd + AdamW) as the GPU load" if a.load == "train"
-                     else "synthetic (gfx950 MFMA bf16 + HBM triad + HIP-graph tiny-kernel load; random-init operands)"),
-            "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + rocprofiler PMC, "
-                                f"{a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",
-                       "global_batch": n, "seq_len": a.steps, "parallelism": f"dp{n}",
-                       "hz": exp.ready.get("hz") or a.hz, "sample_source": source,
-                       "exporter": "attached" if a.attach else "spawned",
-                       "load": "mock" if a.mock else a.load},
-            "samples_per_sec_per_gpu": total / max(1, len(per_gpu)),
-            "pmc_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmc_rate.items()},
-            "pmfw_distinct_samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pmfw_rate.items()},
-            "p50_scrape_ms": scraper.percentile(0.5) * 1e3,
-            "p99_scrape_ms": scraper.percentile(0.99) * 1e3,
-            "scrapes": len(scraper.latencies_s),
-            "scrape_errors": scraper.errors,
-            "scrape_bytes_avg": scraper.bytes / max(1, len(scraper.latencies_s)),
-            "overhead_pct": 100.0 * (t_b / t_off - 1.0),
-            "t_off_a_s": t_a,
-            "t_on_s": t_b,
-            "t_off_c_s": t_c,
-            **inter,
-            "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
-            "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / win, 4) for k, v in thr1.items()
-                                             if win > 0 and v - thr0.get(k, 0.0) > 0.005 * win},
-            "pmc_source": exp.ready.get("pmc"),
-            "pmc_error": exp.ready.get("pmc_error"),
-            "load": calib,
-            "observed_during_load": observed(after),
-            "xgmi_GBps_per_gpu": xgmi_rates(before, after, win),
-            "phases_wall": PHASES,
-            "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in stopped.get("integrals") or [])
-            / max(1, sum(i.get("pmc_samples", 0) for i in stopped.get("integrals") or [])),
-            "pmfw_read_us_mean": 1e6 * sum(i.get("read_seconds", 0) for i in stopped.get("integrals") or [])
-            / max(1, sum(i.get("reads", 0) for i in stopped.get("integrals") or [])),
-            "exporter_integrals": stopped.get("integrals"),
-        }
+    pmc_on = exp.ready.get("pmc", "none") != "none"
+    rb = Rates()
+    rb.add(before, after, win)
+    per_gpu, source = rb.per_gpu(pmc_on)
+    total = sum(per_gpu.values())
+    lat_primary = list(sc_b.latencies_s)
+    tier_out = {}
+    for h, t in inter.get("tiers", {}).items():
+        r: Rates = t.pop("_rates")
+        lat: list = t.pop("_lat")
+        pg, src = r.per_gpu(pmc_on)
+        if float(h) == a.hz:
+            lat_primary += lat
+        tier_out[h] = {"samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pg.items()},
+                       "aggregate_samples_per_sec": round(sum(pg.values()), 2), "sample_source": src,
+                       "p50_scrape_ms": (pct(lat, 0.5) or 0) * 1e3, "p99_scrape_ms": (pct(lat, 0.99) or 0) * 1e3,
+                       "scrapes": len(lat), **{k: v for k, v in t.items()}}
+    inter["tiers"] = tier_out
+    prim = tier_out.get(f"{a.hz:g}", {})
+    step_s = t_b / a.steps
+    integrals = stopped.get("integrals") or []
+    return {
+        "metric": METRIC,
+        "value": total,
+        "unit": f"samples/s (sum over the {n} GPU{'s' if n > 1 else ''})",
+        "n_gpus": n,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": step_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": ("synthetic mock provider (CPU plumbing)" if a.mock
+                 else f"synthetic tokens, random-init {a.train_layers}-layer d={a.train_dim} bf16 decoder "
+                 "training step (fwd + bwd + AdamW) as the GPU load" if a.load == "train"
+                 else "synthetic (gfx950 MFMA bf16 + HBM triad + HIP-graph tiny-kernel load; random-init operands)"),
+        "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + hardware counters "
+                            f"({exp.ready.get('pmc')}), {a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",
+                   "global_batch": n, "seq_len": int(round(a.hz * step_s)), "parallelism": f"dp{n}",
+                   "batch_meaning": "GPUs sampled per tick (one counter drain each)",
+                   "seq_len_meaning": "sampler ticks per GPU per timed step",
+                   "hz": a.hz, "hz_tiers": hzs, "sample_source": source,
+                   "exporter": "attached" if a.attach else "spawned", "load": "mock" if a.mock else a.load,
+                   "units_per_step": load.reps, "unit_ms": unit_s * 1e3},
+        "value_semantics": "aggregate over all GPUs (driver contract); per-GPU in samples_per_sec_per_gpu",
+        "samples_per_sec_per_gpu": total / max(1, len(per_gpu)),
+        "aggregate_samples_per_sec": total,
+        "pmc_samples_per_sec_per_gpu": {g: round((rb.pmc.get(g, 0) / win) if win > 0 else 0, 2) for g in per_gpu},
+        "pmfw_distinct_samples_per_sec_per_gpu": {g: round((rb.pmfw.get(g, 0) / win) if win > 0 else 0, 2)
+                                                  for g in per_gpu},
+        "p50_scrape_ms": (pct(lat_primary, 0.5) or 0) * 1e3,
+        "p99_scrape_ms": (pct(lat_primary, 0.99) or 0) * 1e3,
+        "scrapes": len(lat_primary),
+        "scrape_errors": sc_b.errors,
+        "scrape_bytes_avg": sc_b.bytes / max(1, len(sc_b.latencies_s)),
+        # headline overhead: paired interleaved rounds at the primary rate (mean ± 95 % CI)
+        "overhead_pct": prim.get("overhead_pct"),
+        "overhead_ci95_pct": prim.get("overhead_ci95_pct"),
+        "overhead_abc_pct": 100.0 * (t_b / (0.5 * (t_a + t_c)) - 1.0),
+        "t_off_a_s": t_a,
+        "t_on_s": t_b,
+        "t_off_c_s": t_c,
+        "interleaved": inter,
+        "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
+        "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / win, 4) for k, v in thr1.items()
+                                         if win > 0 and v - thr0.get(k, 0.0) > 0.005 * win},
+        "pmc_source": exp.ready.get("pmc"),
+        "pmc_error": exp.ready.get("pmc_error"),
+        "load": calib,
+        "observed_during_load": observed(after),
+        "xgmi_GBps_per_gpu": xgmi_rates(before, after, win),
+        "phases_wall": PHASES,
+        "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in integrals)
+        / max(1, sum(i.get("pmc_samples", 0) for i in integrals)),
+        "pmfw_read_us_mean": 1e6 * sum(i.get("read_seconds", 0) for i in integrals)
+        / max(1, sum(i.get("reads", 0) for i in integrals)),
+        "exporter_integrals": integrals,
+    }
+
+
+# ----------------------------------------------------------------------------- main
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(a, argv)
+    ctx = D.init_from_env(not a.mock)
+    if ctx.world != a.gpus and ctx.rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {ctx.world}; measuring {ctx.world} rank(s)", file=sys.stderr)
+    result = run(a, ctx)
     # make the result visible to rank 0 if the exporter lived elsewhere (single node: it is rank 0)
     result = D.broadcast_object(ctx, result)
+    rc = 0
     if ctx.rank == 0 and result is not None:
         line = json.dumps(result)
         print(line, flush=True)
         if a.out:
             with open(a.out, "w") as f:
                 f.write(line + "\n")
+        rc = 1 if result.get("value") is None else 0
     D.destroy(ctx)
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

@@ -26,16 +26,26 @@ from ..utils.config import add_flag
 
 L = log.get("exporter")
 
+# AMD SMI call latencies of the mock's latency model: rounded up from the
+# per-call latencies measured on MI355X (profiles/r2/amdsmi_latency.md).
+MOCK_LATENCY = {"proc_latency_s": 2e-3, "link_latency_s": 5e-4, "health_latency_s": 5e-4, "metrics_latency_s": 1e-4}
+
 
 def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.ArgumentParser:
     ap = ap or argparse.ArgumentParser(prog="kgs exporter", description=__doc__.splitlines()[0])
     add_flag(ap, "backend", "amdsmi", "device provider: amdsmi (MI355X) or mock")
     add_flag(ap, "mock-gpus", 8, "mock provider: number of GPUs")
     add_flag(ap, "mock-fail-rate", 0.0, "mock provider: injected read-failure probability")
+    add_flag(ap, "mock-latency", False, "mock provider: model AMD SMI latency (process list 2 ms, link table and RAS "
+                                        "0.5 ms each, under one global lock; PMFW table read 0.1 ms, unlocked)")
+    add_flag(ap, "mock-partition", "SPX", "mock provider: compute partition mode (SPX | DPX | QPX | CPX)")
     add_flag(ap, "hz", 10.0, "sampler tick rate per GPU (1/10/100 Hz tiers; hardware counters every tick)")
     add_flag(ap, "pmfw-hz", 100.0, "cap on PMFW metrics-table reads/s (firmware refreshes it every ~20 ms)")
     add_flag(ap, "proc-every", 10, "per-process tier every N fast ticks (0 = off)")
     add_flag(ap, "link-every", 100, "xGMI link tier every N fast ticks (0 = off)")
+    add_flag(ap, "proc-period", 0.0, "per-process tier period in seconds (overrides --proc-every; survives rate "
+                                     "changes)")
+    add_flag(ap, "link-period", 0.0, "xGMI link + RAS tier period in seconds (overrides --link-every)")
     add_flag(ap, "pmc", "none", "hardware counters: none | aqlprofile (direct CP reads) | rocprofiler "
                                 "(rocprofiler-sdk device counting) | mock")
     add_flag(ap, "pmc-lib", "", "counter reader library (default: the in-tree one for --pmc)")
@@ -52,7 +62,11 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
     add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
     add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
-    add_flag(ap, "window", 1.0, "gauge averaging window in seconds")
+    add_flag(ap, "window", 15.0, "gauge averaging window in seconds (default: one typical scrape interval, so "
+                                 "successive scrapes' gauges tile time; exact per-pod accounting uses the "
+                                 "container_gpu_busy_seconds_total counter)")
+    add_flag(ap, "stale-after", 5.0, "drop a device's window gauges when its last good read / counter drain is "
+                                     "older than this (seconds)")
     add_flag(ap, "hbm-full-bw", 8.41e12, "HBM bytes/s at 100%% UMC activity (MI355X calibration, profiles/umc_calib.md)")
     add_flag(ap, "bdfs", "", "comma-separated PCI addresses to sample (default all)")
     add_flag(ap, "pin-numa", True, "pin each sampler thread to its GPU's NUMA node")
@@ -72,11 +86,14 @@ def config_from_args(a) -> dict:
     host, _, port = a.listen.rpartition(":")
     cfg = {
         "backend": a.backend,
-        "mock": {"n_gpus": a.mock_gpus, "fail_rate": a.mock_fail_rate},
+        "mock": {"n_gpus": a.mock_gpus, "fail_rate": a.mock_fail_rate, "compute_partition": a.mock_partition,
+                 **(MOCK_LATENCY if a.mock_latency else {})},
         "hz": a.hz,
         "pmfw_hz": a.pmfw_hz,
         "proc_every": a.proc_every,
         "link_every": a.link_every,
+        "proc_period_s": a.proc_period,
+        "link_period_s": a.link_period,
         "pin_numa": a.pin_numa,
         "pmc_source": a.pmc,
         "pmc_lib": a.pmc_lib or pmc_lib_path(a.pmc),
@@ -90,6 +107,7 @@ def config_from_args(a) -> dict:
         "node_name": a.node_name,
         "gpu_type_override": a.gpu_type,
         "window_s": a.window,
+        "stale_s": a.stale_after,
         "hbm_bytes_per_s_at_full_umc": a.hbm_full_bw,
         "per_process": a.per_process,
         "compat_unallocated": a.compat_unallocated,

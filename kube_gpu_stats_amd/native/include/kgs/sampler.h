@@ -38,6 +38,9 @@ struct SamplerConfig {
   double pmfw_hz = 100.0;      // PMFW-table tier rate cap (table refreshes every ≈20 ms; 0 = every tick)
   int proc_every = 10;         // mid tier period = proc_every / hz seconds (0 disables)
   int link_every = 100;        // slow tier period = link_every / hz seconds (0 disables)
+  // Absolute periods (seconds) for the two tiers; > 0 overrides the *_every
+  // ticks, so a tick-rate change (set_hz) leaves them alone.
+  double proc_period_s = 0, link_period_s = 0;
   bool pin_numa = true;
   bool pmc = false;            // drain hardware counters every tick
   // A foreign profiler (rocprofv3 --pmc) that STOPs or reprograms the perfmon

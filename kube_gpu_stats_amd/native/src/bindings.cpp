@@ -56,6 +56,8 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
   c.sampler.proc_every = get<int>(d, "proc_every", c.sampler.proc_every);
   c.sampler.link_every = get<int>(d, "link_every", c.sampler.link_every);
+  c.sampler.proc_period_s = get<double>(d, "proc_period_s", c.sampler.proc_period_s);
+  c.sampler.link_period_s = get<double>(d, "link_period_s", c.sampler.link_period_s);
   c.sampler.pin_numa = get<bool>(d, "pin_numa", c.sampler.pin_numa);
   c.sampler.max_backoff_ms = get<int>(d, "max_backoff_ms", c.sampler.max_backoff_ms);
   c.sampler.pmc_reclaim_s = get<double>(d, "pmc_reclaim_s", c.sampler.pmc_reclaim_s);

@@ -111,7 +111,8 @@ void Sampler::start() {
   while (read(stop_fd_, &drain, sizeof drain) > 0) {
   }
   for (int d : dev_ids_) threads_.emplace_back([this, d] { run(d); });
-  if (cfg_.proc_every > 0 || cfg_.link_every > 0) slow_thread_ = std::thread([this] { run_slow(); });
+  if (cfg_.proc_every > 0 || cfg_.link_every > 0 || cfg_.proc_period_s > 0 || cfg_.link_period_s > 0)
+    slow_thread_ = std::thread([this] { run_slow(); });
 }
 
 void Sampler::stop() {
@@ -412,8 +413,12 @@ void Sampler::run(int dev) {
 void Sampler::run_slow() {
   pthread_setname_np(pthread_self(), "kgs-slow");
   const int64_t tick_ns = static_cast<int64_t>(1e9 / cfg_.hz);
-  const int64_t proc_ns = cfg_.proc_every > 0 ? tick_ns * cfg_.proc_every : 0;
-  const int64_t link_ns = cfg_.link_every > 0 ? tick_ns * cfg_.link_every : 0;
+  const int64_t proc_ns = cfg_.proc_period_s > 0 ? static_cast<int64_t>(cfg_.proc_period_s * 1e9)
+                        : cfg_.proc_every > 0   ? tick_ns * cfg_.proc_every
+                                                : 0;
+  const int64_t link_ns = cfg_.link_period_s > 0 ? static_cast<int64_t>(cfg_.link_period_s * 1e9)
+                        : cfg_.link_every > 0   ? tick_ns * cfg_.link_every
+                                                : 0;
   int64_t next_proc = mono_ns(), next_link = next_proc;
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;

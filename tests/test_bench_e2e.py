@@ -28,30 +28,44 @@ def _last_json(out: str) -> dict:
     return json.loads(lines[-1])
 
 
+FAST = ["--step-ms", "60", "--rounds", "4", "--block-steps", "1", "--settle", "0.3"]
+
+
 @pytest.mark.slow
 def test_bench_contract_single_process():
-    r = subprocess.run([sys.executable, "bench.py", "--mock", "--steps", "20", "--warmup", "1", "--settle", "0.5"],
+    r = subprocess.run([sys.executable, "bench.py", "--mock", "--steps", "10", "--warmup", "1", *FAST],
                        cwd=REPO, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     res = _last_json(r.stdout)
     assert KEYS <= set(res)
-    assert res["n_gpus"] == 1 and res["steps"] == 20 and res["higher_is_better"] is True
+    assert res["n_gpus"] == 1 and res["steps"] == 10 and res["higher_is_better"] is True
     assert res["scaling"] == "weak" and res["dtype"] == "bf16"
-    assert res["config"]["parallelism"] == "dp1"
-    assert res["value"] > 50  # mock PMC at 100 Hz
-    assert res["p50_scrape_ms"] < 50
-    assert abs(res["ms_per_step"] - 20.0) < 10
-    # interleaved ABBA off/on blocks: 4 pairs, alternating order, exporter paused / sampling
-    blocks = res["interleave_blocks"]
-    assert [b[0] for b in blocks] == [0, 1, 1, 0, 0, 1, 1, 0]
-    assert abs(res["overhead_interleaved_pct"]) < 50
+    cfg = res["config"]
+    assert cfg["parallelism"] == "dp1" and cfg["global_batch"] == 1
+    # a step is ≥ --step-ms of load (whole 20 ms mock units), and seq_len = ticks per GPU per step
+    assert cfg["units_per_step"] == 3 and res["ms_per_step"] == pytest.approx(60, abs=15)
+    assert cfg["seq_len"] == pytest.approx(cfg["hz"] * res["ms_per_step"] / 1e3, rel=0.01)
+    assert cfg["hz_tiers"] == [100.0, 8000.0]
+    assert res["value"] > 0.95 * 8000  # mock counters at the 8 kHz primary tier
+    assert res["p50_scrape_ms"] < 50 and res["scrapes"] > 10
+    inter = res["interleaved"]
+    # alternating rounds over (paused, 100 Hz, 8 kHz); paused blocks really do not read
+    order = [c for c, _ in inter["block_seconds"]]
+    assert order[:6] == ["0", "100", "8000", "8000", "100", "0"]
+    assert inter["paused_reads"] == 0
+    for hz in ("100", "8000"):
+        t = inter["tiers"][hz]
+        assert len(t["overhead_per_round_pct"]) == 4
+        assert t["overhead_ci95_pct"] > 0 and abs(t["overhead_pct"]) < 50
+        assert t["samples_per_sec_per_gpu"]["0"] == pytest.approx(float(hz), rel=0.05)
+    assert res["overhead_pct"] == inter["tiers"]["8000"]["overhead_pct"]
 
 
 @pytest.mark.slow
 def test_bench_contract_torchrun_gloo_world2():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2", "--mock",
-                        "--steps", "15", "--warmup", "1", "--settle", "0.5"],
+                        "--steps", "6", "--warmup", "1", *FAST],
                        cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     res = _last_json(r.stdout)
@@ -59,6 +73,22 @@ def test_bench_contract_torchrun_gloo_world2():
     # both ranks' GPUs sampled by the one node exporter → aggregate ≈ 2 × per-GPU
     assert len(res["pmc_samples_per_sec_per_gpu"]) == 2
     assert res["value"] == pytest.approx(sum(res["pmc_samples_per_sec_per_gpu"].values()), rel=0.01)
+
+
+@pytest.mark.slow
+def test_bench_self_spawns_ranks_without_torchrun():
+    """`python bench.py --gpus 4` (no torchrun env) launches 4 ranks itself, so a plain
+    invocation — the driver's scaling runs included — measures N GPUs, not 1."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--mock", "--gpus", "4", "--steps", "6", "--warmup", "1", *FAST],
+                       cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    res = _last_json(r.stdout)
+    assert res["n_gpus"] == 4 and res["config"]["parallelism"] == "dp4" and res["config"]["global_batch"] == 4
+    assert sorted(res["pmc_samples_per_sec_per_gpu"]) == ["0", "1", "2", "3"]
+    # weak scaling: value is the node aggregate, the per-GPU rate stays at the tick rate
+    assert res["samples_per_sec_per_gpu"] == pytest.approx(8000, rel=0.05)
+    assert res["value"] == pytest.approx(4 * res["samples_per_sec_per_gpu"], rel=1e-6)
 
 
 def test_end_to_end_exporter_to_report(mock_exporter, tmp_path):
