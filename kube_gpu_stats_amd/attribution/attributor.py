@@ -4,8 +4,13 @@
   allocations), resolved to exporter GPU indices.  Fills the labels of the
   reference-contract series ``container_gpu_sm_util{pod_name,...}``
   (reference gpu_util_stats.py:159).
-* PID → pod: a process found on a GPU inherits that GPU's owner when the GPU is
-  held by exactly one container; its pod UID always comes from its cgroup.
+* PID → pod, per (GPU, PID): the process's own cgroup names its pod UID and
+  container ID; a pod directory (poddir.py: the node's PodList) turns those into
+  pod / namespace / container, so processes of different pods sharing one GPU are
+  told apart.  Without a directory entry, a process inherits its GPU's owner only
+  when the GPU has exactly one owner AND the process's cgroup names a pod that is
+  not the exporter's own (the exporter's counter queues make it show up in every
+  GPU's process list; host processes have no pod UID) — ADVICE r1.
 * Optional static mapping file (JSON ``{"<device id>": {"pod":..,"namespace":..,
   "container":..}}``) for nodes without a kubelet socket (and the 1-GPU box).
 
@@ -25,6 +30,7 @@ import time
 
 from ..utils import log
 from .cgroup import pid_cgroup
+from .poddir import PodDirectory
 from .podresources import GPU_RESOURCES, DeviceIndex, PodResourcesClient
 
 L = log.get("attribution")
@@ -33,12 +39,15 @@ L = log.get("attribution")
 class Attributor:
     def __init__(self, exporter, socket_path: str | None = None, static_map: str | None = None,
                  resources=GPU_RESOURCES, interval_s: float = 1.0, proc_root: str = "/proc",
-                 stale_after_s: float = 30.0):
+                 stale_after_s: float = 30.0, sysfs_root: str | None = "/sys",
+                 pod_directory: PodDirectory | None = None, self_pid: int | None = None):
         self.ex = exporter
         self.interval_s = interval_s
         self.proc_root = proc_root
         self.resources = tuple(resources)
-        self.index = DeviceIndex(exporter.devices())
+        self.index = DeviceIndex(exporter.devices(), sysfs_root)
+        self.poddir = pod_directory
+        self.own_pod_uid = pid_cgroup(self_pid if self_pid is not None else os.getpid(), proc_root).pod_uid
         self.socket_path = socket_path
         self.client: PodResourcesClient | None = None
         self.static_map = static_map
@@ -110,16 +119,28 @@ class Attributor:
                     owners[i].append(o)
         return owners
 
-    def pid_owners(self, owners: dict[int, list[dict]]) -> dict[int, dict]:
-        out: dict[int, dict] = {}
+    def pid_owners(self, owners: dict[int, list[dict]]) -> dict[tuple[int, int], dict]:
+        """{(gpu, pid): {pod, namespace, container, pod_uid}} for every process the
+        exporter's process tier sees on every GPU."""
+        out: dict[tuple[int, int], dict] = {}
+        if self.poddir is not None:
+            self.poddir.refresh()
+        cgroups: dict[int, object] = {}
         for gpu in range(self.ex.device_count):
-            single = owners.get(gpu, [])
+            gpu_owners = owners.get(gpu, [])
             for p in self.ex.procs(gpu):
                 pid = int(p["pid"])
-                cg = pid_cgroup(pid, self.proc_root)
-                o = dict(single[0]) if len(single) == 1 else {"pod": "", "namespace": "", "container": ""}
-                o["pod_uid"] = cg.pod_uid
-                out[pid] = o
+                cg = cgroups.get(pid)
+                if cg is None:
+                    cg = cgroups[pid] = pid_cgroup(pid, self.proc_root)
+                o = {"pod": "", "namespace": "", "container": "", "pod_uid": cg.pod_uid}
+                ref = self.poddir.lookup(cg.pod_uid, cg.container_id) if self.poddir is not None else None
+                if ref is not None:
+                    o.update(pod=ref.pod, namespace=ref.namespace, container=ref.container)
+                elif cg.pod_uid and cg.pod_uid != self.own_pod_uid and len(gpu_owners) == 1:
+                    o.update(pod=gpu_owners[0]["pod"], namespace=gpu_owners[0]["namespace"],
+                             container=gpu_owners[0]["container"])
+                out[(gpu, pid)] = o
         return out
 
     def update_once(self) -> None:

@@ -76,73 +76,97 @@ class PodResourcesClient:
 
 
 class DeviceIndex:
-    """Resolve a device-plugin device ID to the exporter's GPU index."""
+    """Resolve a device-plugin device ID to the exporter's device index.
 
-    def __init__(self, devices: list[dict]):
-        self._map: dict[str, int] = {}
+    Every key is exact (case-insensitive); an ID that matches nothing, or matches
+    more than one exporter device, resolves to ``None`` — a wrong pod label is
+    worse than none.  Accepted:
+
+    * PCI address (``0000:72:00.0`` / ``72:00.0``).  Under compute partitioning
+      (DPX/QPX/CPX) every partition of a GPU shares its PCI function; the address
+      then names the function's own partition, partition 0 (the other partitions
+      are ``amdgpu_xcp_*`` platform devices).
+    * UUID; serial when unique (partitions share their GPU's serial).
+    * DRM names ``card<N>`` / ``renderD<128+N>`` and KFD node ``kfd<N>``.
+    * ``amdgpu_xcp_<n>``: the partition platform device, resolved through sysfs
+      (``<sysfs>/devices/platform/amdgpu_xcp_<n>/drm/card<M>`` → the device whose
+      DRM card is M).  Never by the number alone: XCP numbers are node-global and
+      do not follow exporter indices.
+    * The exporter index itself, as the whole ID (``"3"``).
+    * Prefixed forms (``gpu-0000:72:00.0``): the tail after the last ``-``/``_``
+      only when that tail is a PCI address or UUID key, never a bare number.
+    """
+
+    def __init__(self, devices: list[dict], sysfs_root: str | None = "/sys"):
+        self._map: dict[str, set[int]] = {}
+        self._strong: set[str] = set()  # keys a prefixed ID may resolve through
+        by_bdf: dict[str, list[dict]] = {}
+        card_to_idx: dict[int, int] = {}
         for d in devices:
             i = int(d["index"])
-            for key in (d.get("bdf"), d.get("uuid"), d.get("serial"), str(i)):
-                if key:
-                    self._map[str(key).lower()] = i
-            bdf = (d.get("bdf") or "").lower()
-            if bdf.startswith("0000:"):
-                self._map[bdf[5:]] = i          # "72:00.0"
-            if d.get("drm_card", -1) is not None and int(d.get("drm_card", -1)) >= 0:
-                self._map[f"card{int(d['drm_card'])}"] = i
+            self._add(str(i), i)
+            if d.get("uuid"):
+                self._add(d["uuid"], i, strong=True)
+            if d.get("serial"):
+                self._add(d["serial"], i)
+            card = int(d.get("drm_card", -1) if d.get("drm_card") is not None else -1)
+            if card >= 0:
+                self._add(f"card{card}", i)
+                self._add(f"renderD{128 + card}", i)
+                card_to_idx[card] = i
+            if int(d.get("kfd_node", -1) if d.get("kfd_node") is not None else -1) >= 0:
+                self._add(f"kfd{int(d['kfd_node'])}", i)
+            if d.get("bdf"):
+                by_bdf.setdefault(d["bdf"].lower(), []).append(d)
+        for bdf, ds in by_bdf.items():
+            if len(ds) > 1:  # partitions: the PCI function is partition 0
+                ds = [d for d in ds if int(d.get("partition_id", -1)) == 0] or ds
+            for d in ds:
+                self._add(bdf, int(d["index"]), strong=True)
+                if bdf.startswith("0000:"):
+                    self._add(bdf[5:], int(d["index"]), strong=True)
+        for xcp, card in _xcp_cards(sysfs_root).items():
+            if card in card_to_idx:
+                self._add(xcp, card_to_idx[card], strong=True)
+
+    def _add(self, key: str, i: int, strong: bool = False) -> None:
+        k = str(key).lower()
+        self._map.setdefault(k, set()).add(i)
+        if strong:
+            self._strong.add(k)
+
+    def _one(self, k: str) -> int | None:
+        s = self._map.get(k)
+        return next(iter(s)) if s and len(s) == 1 else None
 
     def resolve(self, device_id: str) -> int | None:
         k = device_id.strip().lower()
         if k in self._map:
-            return self._map[k]
-        # "gpu-0000:72:00.0" / "amdgpu_xcp_3"-style prefixes
+            return self._one(k)
         for sep in ("-", "_"):
             tail = k.rsplit(sep, 1)[-1]
-            if tail in self._map:
-                return self._map[tail]
+            if tail != k and tail in self._strong:
+                return self._one(tail)
         return None
 
 
-# --------------------------------------------------------------------------- fake kubelet
-class FakeKubelet:
-    """In-process kubelet pod-resources server on a unix socket (tests, BASELINE config 5 rehearsal)."""
-
-    def __init__(self, socket_path: str, response: proto.ListPodResourcesResponse,
-                 allocatable: proto.AllocatableResourcesResponse | None = None):
-        import grpc
-        from concurrent import futures
-
-        self.socket_path = socket_path
-        self.response = response
-        self.allocatable = allocatable or proto.AllocatableResourcesResponse()
-        self.calls = 0
-        outer = self
-
-        class Handler(grpc.GenericRpcHandler):
-            def service(self, details):
-                if details.method == LIST_METHOD:
-                    def list_(req, ctx):
-                        outer.calls += 1
-                        return outer.response.encode()
-                    return grpc.unary_unary_rpc_method_handler(list_, request_deserializer=_identity,
-                                                               response_serializer=_identity)
-                if details.method == ALLOCATABLE_METHOD:
-                    return grpc.unary_unary_rpc_method_handler(lambda r, c: outer.allocatable.encode(),
-                                                               request_deserializer=_identity,
-                                                               response_serializer=_identity)
-                return None
-
-        self._server = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
-        self._server.add_generic_rpc_handlers((Handler(),))
-        if os.path.exists(socket_path):
-            os.unlink(socket_path)
-        self._server.add_insecure_port(f"unix://{socket_path}")
-
-    def __enter__(self):
-        self._server.start()
-        return self
-
-    def __exit__(self, *exc):
-        self._server.stop(0)
-        if os.path.exists(self.socket_path):
-            os.unlink(self.socket_path)
+def _xcp_cards(sysfs_root: str | None) -> dict[str, int]:
+    """``amdgpu_xcp_<n>`` platform devices → their DRM card number."""
+    out: dict[str, int] = {}
+    if not sysfs_root:
+        return out
+    base = os.path.join(sysfs_root, "devices", "platform")
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return out
+    for name in names:
+        if not name.startswith("amdgpu_xcp"):
+            continue
+        try:
+            for e in os.listdir(os.path.join(base, name, "drm")):
+                if e.startswith("card") and e[4:].isdigit():
+                    out[name.replace(".", "_").lower()] = int(e[4:])
+        except OSError:
+            continue
+    return out

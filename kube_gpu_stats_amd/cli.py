@@ -1,4 +1,4 @@
-"""``kgs`` command line: exporter | who-use-gpu | gpu-util-stats | dmon | topo | scrape | bench.
+"""``kgs`` command line: exporter | who-use-gpu | gpu-util-stats | dmon | topo | pmc | scrape | bench.
 
 The reference ships two scripts with no arguments (who_use_gpu.py:61-62,
 gpu_util_stats.py:165-166).  They become subcommands here, every hard-coded
@@ -27,6 +27,14 @@ def main(argv=None) -> int:
     tp = sub.add_parser("topo", help="print device inventory + xGMI topology as JSON")
     tp.add_argument("--backend", default="amdsmi")
     tp.add_argument("--mock-gpus", type=int, default=8)
+    tp.add_argument("--format", default="json", choices=["json", "prom"],
+                    help="json inventory, or amdgpu_xgmi_neighbor{bdf,peer_bdf} lines (node topology export)")
+    tp.add_argument("--node-name", default="")
+    pm = sub.add_parser("pmc", help="hand the hardware counters of a running exporter to another profiler (release) "
+                                    "or back (acquire); run inside the exporter pod: kubectl exec <pod> -- kgs pmc release")
+    pm.add_argument("action", choices=["release", "acquire", "status"])
+    pm.add_argument("--exporter", default="127.0.0.1:9400", help="host:port of the exporter (loopback only)")
+    pm.add_argument("--pid-file", default="", help="signal the PID in this file instead of using HTTP")
     sub.add_parser("bench", help="run the headline benchmark (bench.py; flags pass through)", add_help=False)
     sp = sub.add_parser("scrape", help="scrape an exporter once and print selected families")
     sp.add_argument("url", nargs="?", default="http://127.0.0.1:9400/metrics")
@@ -50,10 +58,18 @@ def main(argv=None) -> int:
     if a.cmd == "dmon":
         return dmon.run(a)
     if a.cmd == "topo":
-        from .parallel.topology import discover
+        from .parallel.topology import discover, prometheus_lines
 
-        print(json.dumps(discover(a.backend, a.mock_gpus), indent=2))
+        topo = discover(a.backend, a.mock_gpus)
+        if a.format == "prom":
+            print("# HELP amdgpu_xgmi_neighbor Direct xGMI link between two GPUs of this node (1)")
+            print("# TYPE amdgpu_xgmi_neighbor gauge")
+            print("\n".join(prometheus_lines(topo, a.node_name or topo.get("node", ""))))
+        else:
+            print(json.dumps(topo, indent=2))
         return 0
+    if a.cmd == "pmc":
+        return pmc_control(a)
     if a.cmd == "scrape":
         import urllib.request
 
@@ -63,6 +79,31 @@ def main(argv=None) -> int:
                 print(line)
         return 0
     return 1
+
+
+def pmc_control(a) -> int:
+    """Counter hand-over from inside the exporter's pod.  The DaemonSet runs with
+    hostPID, so PID 1 there is the host's init — never signal it; use the exporter's
+    loopback-only /control/pmc/* endpoints, or the PID it wrote to --pid-file."""
+    if a.pid_file:
+        import os
+        import signal
+
+        with open(a.pid_file) as f:
+            pid = int(f.read().strip())
+        if a.action != "status":
+            os.kill(pid, signal.SIGUSR1 if a.action == "release" else signal.SIGUSR2)
+        print(json.dumps({"pid": pid, "action": a.action}))
+        return 0
+    import urllib.request
+
+    path = {"release": "/control/pmc/release", "acquire": "/control/pmc/acquire"}.get(a.action)
+    if path:
+        print(urllib.request.urlopen(f"http://{a.exporter}{path}", timeout=10).read().decode())
+        return 0
+    body = urllib.request.urlopen(f"http://{a.exporter}/metrics", timeout=10).read().decode()
+    print("\n".join(ln for ln in body.splitlines() if ln.startswith(("kgs_pmc_enabled", "kgs_pmc_stalled"))))
+    return 0
 
 
 if __name__ == "__main__":

@@ -75,6 +75,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pod-resources-socket", "/var/lib/kubelet/pod-resources/kubelet.sock", "kubelet pod-resources socket")
     add_flag(ap, "static-owners", "", "JSON file mapping device id -> {pod,namespace,container}")
     add_flag(ap, "attribution-interval", 1.0, "attribution refresh period (s)")
+    add_flag(ap, "pod-directory", "", "pod UID / container ID → pod names for per-process attribution: 'api' "
+                                      "(in-cluster API server, this node's pods) or 'file:<PodList JSON>' ('' = off)")
+    add_flag(ap, "pid-file", "", "write the exporter's PID here (hand-over: `kgs pmc release` signals it)")
     add_flag(ap, "control-stdin", False, "accept 'quit' on stdin")
     add_flag(ap, "control-http", False, "serve /control/pause and /control/resume (benchmarks only)")
     add_flag(ap, "gzip-level", 0, "gzip /metrics at this zlib level for clients that accept it (0 = off; level 1 "
@@ -136,8 +139,14 @@ def run(a) -> int:
         return 2
     from ..attribution.attributor import Attributor
 
+    from ..attribution.poddir import PodDirectory
+
+    pdir = PodDirectory(a.pod_directory, node=a.node_name) if a.pod_directory else None
     attr = Attributor(ex, a.pod_resources_socket, a.static_owners or None,
-                      interval_s=a.attribution_interval).start()
+                      interval_s=a.attribution_interval, pod_directory=pdir).start()
+    if a.pid_file:
+        with open(a.pid_file, "w") as f:
+            f.write(f"{os.getpid()}\n")
     print(json.dumps({"event": "ready", "port": ex.port, "pid": os.getpid(), "backend": ex.backend_name,
                       "pmc": ex.pmc_name, "pmc_error": ex.pmc_error, "devices": ex.devices(),
                       "pmc_info": [ex.pmc_info(i) for i in range(ex.device_count)],
@@ -151,8 +160,10 @@ def run(a) -> int:
     signal.signal(signal.SIGINT, _sig)
 
     # Counter hand-over, like a profiling pause: SIGUSR1 gives the hardware counters
-    # to another profiler (`kubectl exec <pod> -- kill -USR1 1`, then rocprofv3 --pmc
-    # on that node), SIGUSR2 takes them back.  The PMFW / per-process tiers keep going.
+    # to another profiler, SIGUSR2 takes them back; the PMFW / per-process tiers keep
+    # going.  In the DaemonSet (hostPID) PID 1 is the host's init, so signal the
+    # exporter's own PID — `kubectl exec <pod> -- kgs pmc release` does that through
+    # the loopback-only /control/pmc/* endpoints (or the --pid-file).
     def _pmc(signum, _frame):
         on = signum == signal.SIGUSR2
         ex.set_pmc_enabled(on)

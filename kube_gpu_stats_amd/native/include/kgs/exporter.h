@@ -90,7 +90,10 @@ class Exporter {
   int port() const;
 
   void set_device_owners(int dev, std::vector<Owner> owners);
-  void set_pid_owners(std::unordered_map<uint32_t, PidOwner> m);
+  // Keyed by pid_key(gpu, pid): one process can hold several GPUs that belong
+  // to different pods (or to none), and each line carries its own GPU's answer.
+  void set_pid_owners(std::unordered_map<uint64_t, PidOwner> m);
+  static uint64_t pid_key(int gpu, uint32_t pid) { return (static_cast<uint64_t>(static_cast<uint32_t>(gpu)) << 32) | pid; }
   void set_node_name(const std::string& n);
   // Pre-rendered exposition text from the control plane (attribution
   // self-metrics) appended to every /metrics body; swapped atomically.
@@ -131,7 +134,7 @@ class Exporter {
  private:
   void build_static_labels();
   std::shared_ptr<const std::map<int, std::vector<Owner>>> owners() const;
-  std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> pid_owners() const;
+  std::shared_ptr<const std::unordered_map<uint64_t, PidOwner>> pid_owners() const;
 
   ExporterConfig cfg_;
   std::string err_, pmc_err_;
@@ -143,7 +146,7 @@ class Exporter {
   std::vector<TopoEdge> topo_;
   mutable std::mutex mu_;
   std::shared_ptr<const std::map<int, std::vector<Owner>>> owners_;
-  std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> pid_owners_;
+  std::shared_ptr<const std::unordered_map<uint64_t, PidOwner>> pid_owners_;
   std::string node_name_;
   std::shared_ptr<const std::string> extra_;
   // Render caches (guarded by mu_): the device-info + topology block changes only

@@ -98,6 +98,11 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_reclaims{0};    // automatic re-STARTs after a stall
   std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
   PmcSample pmc_base;  // totals carried over hand-overs (sampler thread only; survives pause/resume)
+  // Last distinct PMFW sample (sampler thread only).  Kept across pause/resume:
+  // the firmware accumulators keep counting while the thread is stopped, so the
+  // first sample after a resume integrates the paused interval exactly.
+  GpuSample pmfw_prev;
+  bool have_pmfw_prev = false;
   // Slow-thread self metrics: completed passes and their latency per tier.
   std::atomic<uint64_t> proc_reads{0}, proc_errors{0}, link_reads{0};
   std::atomic<uint64_t> slow_ns_total{0};

@@ -323,12 +323,15 @@ class PyExporter {
     }
     ex_.set_device_owners(d, std::move(v));
   }
+  // {(gpu, pid): {pod, namespace, container, pod_uid}}
   void set_pid_owners(const py::dict& m) {
-    std::unordered_map<uint32_t, PidOwner> mm;
+    std::unordered_map<uint64_t, PidOwner> mm;
     for (auto kvp : m) {
+      auto key = kvp.first.cast<std::pair<int, uint32_t>>();
       py::dict o = kvp.second.cast<py::dict>();
-      mm[kvp.first.cast<uint32_t>()] = PidOwner{get<std::string>(o, "pod", ""), get<std::string>(o, "namespace", ""),
-                                                get<std::string>(o, "container", ""), get<std::string>(o, "pod_uid", "")};
+      mm[Exporter::pid_key(key.first, key.second)] =
+          PidOwner{get<std::string>(o, "pod", ""), get<std::string>(o, "namespace", ""),
+                   get<std::string>(o, "container", ""), get<std::string>(o, "pod_uid", "")};
     }
     ex_.set_pid_owners(std::move(mm));
   }

@@ -166,8 +166,8 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
   owners_ = std::move(m);
 }
 
-void Exporter::set_pid_owners(std::unordered_map<uint32_t, PidOwner> m) {
-  auto p = std::make_shared<const std::unordered_map<uint32_t, PidOwner>>(std::move(m));
+void Exporter::set_pid_owners(std::unordered_map<uint64_t, PidOwner> m) {
+  auto p = std::make_shared<const std::unordered_map<uint64_t, PidOwner>>(std::move(m));
   std::lock_guard<std::mutex> g(mu_);
   pid_owners_ = std::move(p);
 }
@@ -188,7 +188,7 @@ std::shared_ptr<const std::map<int, std::vector<Owner>>> Exporter::owners() cons
   std::lock_guard<std::mutex> g(mu_);
   return owners_;
 }
-std::shared_ptr<const std::unordered_map<uint32_t, PidOwner>> Exporter::pid_owners() const {
+std::shared_ptr<const std::unordered_map<uint64_t, PidOwner>> Exporter::pid_owners() const {
   std::lock_guard<std::mutex> g(mu_);
   return pid_owners_;
 }

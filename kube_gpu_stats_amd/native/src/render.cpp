@@ -545,7 +545,7 @@ void Exporter::render(std::string& out) {
       kv(l, "process", p.name);
       const PidOwner* po = nullptr;
       if (pown) {
-        auto it = pown->find(p.pid);
+        auto it = pown->find(pid_key(d, p.pid));
         if (it != pown->end()) po = &it->second;
       }
       kv(l, "pod", po ? po->pod : none);

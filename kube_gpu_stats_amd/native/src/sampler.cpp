@@ -199,8 +199,8 @@ void Sampler::run(int dev) {
                                   ? static_cast<uint64_t>(cfg_.hz / cfg_.pmfw_hz + 0.5)
                                   : 1;
   Integrals I;
-  GpuSample prev;
-  bool have_prev = false;
+  GpuSample& prev = st.pmfw_prev;
+  bool& have_prev = st.have_pmfw_prev;
   uint64_t seq = 0, pmc_seq = 0, tick = 0;
   int64_t last_slow_ns = 0;
   {  // resume after a pause: counters and sequence numbers continue

@@ -11,7 +11,8 @@ import pytest
 from kube_gpu_stats_amd.attribution import proto
 from kube_gpu_stats_amd.attribution.attributor import Attributor
 from kube_gpu_stats_amd.attribution.cgroup import parse_cgroup_text
-from kube_gpu_stats_amd.attribution.podresources import DeviceIndex, FakeKubelet, PodResourcesClient
+from fakekubelet import FakeKubelet
+from kube_gpu_stats_amd.attribution.podresources import DeviceIndex, PodResourcesClient
 from kube_gpu_stats_amd.utils.scrape import parse_text
 
 
@@ -148,3 +149,128 @@ def test_attributor_late_kubelet_reconnect_and_stale_drop(mock_exporter, tmp_pat
     assert a.owners == {}  # past stale_after_s: pod labels dropped
     assert "container_gpu_sm_util" not in parse_text(ex.render())
     a.stop()
+
+
+def _cpx_devices(n_gpus=1):
+    return [{"index": g * 8 + p, "bdf": f"0000:{0x11 + 0x10 * g:02x}:00.0", "uuid": f"u-{g}-{p}",
+             "serial": f"MOCK{g}", "drm_card": 8 * g + p, "kfd_node": 2 + 8 * g + p, "partition_id": p}
+            for g in range(n_gpus) for p in range(8)]
+
+
+def _fake_xcp_sysfs(root, xcp_to_card: dict[int, int]):
+    for n, card in xcp_to_card.items():
+        d = root / "devices" / "platform" / f"amdgpu_xcp.{n}" / "drm" / f"card{card}"
+        d.mkdir(parents=True)
+
+
+def test_device_index_partitions_resolve_explicitly(tmp_path):
+    """CPX: 8 devices share one BDF.  XCP IDs resolve through sysfs to the device
+    owning that DRM card — never by their number (amdgpu_xcp_3 is not GPU 3)."""
+    devs = _cpx_devices(2)  # GPU 0 → devices 0..7 (cards 0..7), GPU 1 → 8..15 (cards 8..15)
+    # node-global XCP numbering: the secondary partitions of both GPUs, 7 each
+    xcp = {n: (n // 7) * 8 + 1 + n % 7 for n in range(14)}
+    _fake_xcp_sysfs(tmp_path, xcp)
+    idx = DeviceIndex(devs, str(tmp_path))
+    assert idx.resolve("amdgpu_xcp_3") == 4          # xcp 3 → card 4 → GPU 0 partition 4
+    assert idx.resolve("amdgpu_xcp_10") == 12        # xcp 10 → card 12 → GPU 1 partition 4
+    assert idx.resolve("amdgpu_xcp_99") is None      # unknown XCP: no guess
+    assert idx.resolve("0000:11:00.0") == 0          # the PCI function is partition 0
+    assert idx.resolve("0000:21:00.0") == 8
+    assert idx.resolve("MOCK0") is None              # serial shared by 8 partitions: ambiguous
+    assert idx.resolve("gpu-3") is None              # bare-number tails never resolve
+    assert idx.resolve("card13") == 13 and idx.resolve("renderD133") == 5
+    assert idx.resolve("3") == 3                     # the whole ID as an exporter index is exact
+    assert DeviceIndex(devs, None).resolve("amdgpu_xcp_3") is None  # no sysfs, no XCP map
+
+
+def test_cpx_partitions_each_carry_their_own_xcc(mock_exporter, tmp_path):
+    """1 MI355X in CPX mode = 8 devices; 8 pods each get their partition's XCC busy
+    (mock XCC x runs 50 + 40·sin(0.7·x) over a 1000 s period: ≈ constant here)."""
+    import math
+
+    ex = mock_exporter(n_gpus=1, hz=200, window_s=0.2,
+                       mock={"compute_partition": "CPX", "util_period_s": 1000.0, "fw_period_s": 0.005})
+    devs = ex.devices()
+    assert len(devs) == 8 and {d["bdf"] for d in devs} == {"0000:11:00.0"}
+    assert [d["partition_id"] for d in devs] == list(range(8)) and all(d["num_xcc"] == 1 for d in devs)
+    assert [d["xcc_first"] for d in devs] == list(range(8)) and devs[0]["compute_partition"] == "CPX"
+    _fake_xcp_sysfs(tmp_path / "sys", {n: n + 1 for n in range(7)})  # xcp n → card n+1 → partition n+1
+    sock = str(tmp_path / "kubelet.sock")
+    ids = ["0000:11:00.0"] + [f"amdgpu_xcp_{n}" for n in range(7)]
+    resp = proto.ListPodResourcesResponse([
+        proto.PodResources(f"job-{p}", "ml", [proto.ContainerResources("main", [
+            proto.ContainerDevices("amd.com/gpu", [ids[p]])])]) for p in range(8)])
+    with FakeKubelet(sock, resp):
+        time.sleep(0.3)
+        Attributor(ex, sock, sysfs_root=str(tmp_path / "sys")).update_once()
+        m = parse_text(ex.render())
+    got = {lb["pod_name"]: (int(lb["gpu"]), v) for lb, v in m["container_gpu_sm_util"]}
+    assert sorted(got) == [f"job-{p}" for p in range(8)]
+    for p in range(8):
+        gpu, v = got[f"job-{p}"]
+        assert gpu == p
+        assert v == pytest.approx(50 + 40 * math.sin(0.7 * p), abs=1.0), (p, v)
+    assert len({round(v) for _, v in got.values()}) == 8  # eight distinct series
+
+
+class _StubExporter:
+    """Duck-typed exporter for the PID→pod logic: fixed process lists per GPU."""
+
+    def __init__(self, procs: dict[int, list[int]]):
+        self._procs = procs
+        self.device_count = len(procs)
+
+    def devices(self):
+        return [{"index": g, "bdf": f"0000:{0x11 + 0x10 * g:02x}:00.0"} for g in self._procs]
+
+    def procs(self, gpu):
+        return [{"pid": p} for p in self._procs[gpu]]
+
+
+def test_pid_owners_keyed_by_gpu_and_pid(tmp_path):
+    """one PID on two GPUs of different pods gets each GPU's owner on that
+    GPU's line; a host process (no pod UID) and the exporter's own pod inherit nothing;
+    with a pod directory every process gets its own pod, shared GPU or not."""
+    from kube_gpu_stats_amd.attribution.poddir import PodDirectory
+
+    proc_root = tmp_path / "proc"
+    uid = {42: "0a1b2c3d-1111-2222-3333-444455550042", 99: "0a1b2c3d-1111-2222-3333-444455550099",
+           51: "0a1b2c3d-1111-2222-3333-444455550051"}
+    for pid in (42, 99, 51, 7, 1000):
+        (proc_root / str(pid)).mkdir(parents=True)
+        text = (f"0::/kubepods/pod{uid[pid]}/" + f"{pid:064x}\n") if pid in uid else "0::/user.slice/session-2.scope\n"
+        (proc_root / str(pid) / "cgroup").write_text(text)
+    (proc_root / "1000" / "cgroup").write_text(f"0::/kubepods/pod{uid[99]}/" + "e" * 64 + "\n")  # exporter = pod 99
+    ex = _StubExporter({0: [42, 7, 1000], 1: [42, 51, 1000]})
+    owners = {0: [{"pod": "a", "namespace": "ml", "container": "c"}],
+              1: [{"pod": "b", "namespace": "ml", "container": "c"}]}
+    a = Attributor(ex, None, proc_root=str(proc_root), self_pid=1000)
+    out = a.pid_owners(owners)
+    assert out[(0, 42)]["pod"] == "a" and out[(1, 42)]["pod"] == "b"   # each GPU's own owner
+    assert out[(0, 7)]["pod"] == "" and out[(0, 7)]["pod_uid"] == ""     # host process
+    assert out[(0, 1000)]["pod"] == "" and out[(1, 1000)]["pod"] == ""  # the exporter itself
+    # pod directory: UID / container ID → the process's real pod
+    pl = {"items": [
+        {"metadata": {"name": "real-42", "namespace": "team", "uid": uid[42]},
+         "status": {"containerStatuses": [{"name": "w", "containerID": "containerd://" + f"{42:064x}"}]}},
+        {"metadata": {"name": "real-51", "namespace": "team", "uid": uid[51]}}]}
+    f = tmp_path / "pods.json"
+    f.write_text(json.dumps(pl))
+    a2 = Attributor(ex, None, proc_root=str(proc_root), self_pid=1000, pod_directory=PodDirectory(f"file:{f}"))
+    out2 = a2.pid_owners(owners)
+    assert (out2[(0, 42)]["pod"], out2[(0, 42)]["container"]) == ("real-42", "w")
+    assert out2[(1, 42)]["pod"] == "real-42" and out2[(1, 51)]["pod"] == "real-51"
+    assert out2[(0, 7)]["pod"] == ""
+
+
+def test_pid_owner_labels_per_gpu_line(mock_exporter):
+    ex = mock_exporter(n_gpus=2, proc_every=1)
+    time.sleep(0.3)
+    pid0 = ex.procs(0)[0]["pid"]
+    pid1 = ex.procs(1)[0]["pid"]
+    ex.set_pid_owners({(0, pid0): {"pod": "p0", "namespace": "n", "container": "c", "pod_uid": "u0"},
+                       (1, pid0): {"pod": "WRONG", "namespace": "n", "container": "c", "pod_uid": "u0"},
+                       (1, pid1): {"pod": "p1", "namespace": "n", "container": "c", "pod_uid": "u1"}})
+    m = parse_text(ex.render())
+    lines = {(lb["gpu"], lb["pid"]): lb["pod"] for lb, _ in m["amdgpu_process_hbm_bytes"]}
+    assert lines[("0", str(pid0))] == "p0" and lines[("1", str(pid1))] == "p1"

@@ -11,9 +11,9 @@ import pytest
 
 from kube_gpu_stats_amd.attribution import proto
 from kube_gpu_stats_amd.attribution.attributor import Attributor
-from kube_gpu_stats_amd.attribution.podresources import FakeKubelet
+from fakekubelet import FakeKubelet
 from kube_gpu_stats_amd.reports import gpu_util_stats as G
-from kube_gpu_stats_amd.reports.fakeprom import FakeProm
+from fakeprom import FakeProm
 from kube_gpu_stats_amd.reports.promql import PromClient
 from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
 

@@ -26,6 +26,21 @@ def test_daemonset_args_are_valid_exporter_flags():
     mounts = {m["mountPath"] for m in c["volumeMounts"]}
     assert "/var/lib/kubelet/pod-resources" in mounts and "/dev/kfd" in mounts
     assert c["readinessProbe"]["httpGet"]["path"] == "/healthz"
+    assert a.pod_directory == "api" and a.window == 15.0
+    # the pod directory lists pods: the exporter's service account must be allowed to
+    sa = spec["serviceAccountName"]
+    role = next(d for d in docs if d["kind"] == "ClusterRole")
+    binding = next(d for d in docs if d["kind"] == "ClusterRoleBinding")
+    assert any("pods" in r["resources"] and "list" in r["verbs"] for r in role["rules"])
+    assert binding["subjects"][0]["name"] == sa and binding["roleRef"]["name"] == role["metadata"]["name"]
+
+
+def test_daemonset_handover_does_not_signal_pid1():
+    """hostPID: PID 1 in the pod is the host's init."""
+    with open(os.path.join(DEPLOY, "daemonset.yaml")) as f:
+        text = f.read()
+    assert "kill -USR1 1" not in text.replace("Never `kill -USR1 1`", "")
+    assert "kgs pmc release" in text
 
 
 PROMQL_WORDS = {"avg", "sum", "max", "min", "count", "rate", "increase", "avg_over_time", "label_values", "by", "or",

@@ -45,7 +45,7 @@ def test_integral_matches_analytic_mean(mock_exporter):
 def test_prometheus_exposition_is_valid(mock_exporter):
     ex = mock_exporter(n_gpus=2, pmc_source="mock", proc_every=1, link_every=1)
     ex.set_device_owners(0, [{"pod": "train-0", "namespace": "ml", "container": "main"}])
-    ex.set_pid_owners({100000: {"pod": "train-0", "namespace": "ml", "container": "main", "pod_uid": "u-1"}})
+    ex.set_pid_owners({(0, 100000): {"pod": "train-0", "namespace": "ml", "container": "main", "pod_uid": "u-1"}})
     time.sleep(0.5)
     body = ex.render()
     fams = {f.name: f for f in text_string_to_metric_families(body)}

@@ -9,7 +9,7 @@ import pytest
 
 from kube_gpu_stats_amd.reports import gpu_util_stats as G
 from kube_gpu_stats_amd.reports import who_use_gpu as W
-from kube_gpu_stats_amd.reports.fakeprom import FakeProm
+from fakeprom import FakeProm
 from kube_gpu_stats_amd.reports.promql import PromClient, PromError
 from kube_gpu_stats_amd.reports.table import render
 

@@ -8,7 +8,7 @@ from hypothesis import given, settings
 from hypothesis import strategies as st
 
 from kube_gpu_stats_amd.reports import gpu_util_stats as G
-from kube_gpu_stats_amd.reports.fakeprom import FakeProm
+from fakeprom import FakeProm
 from kube_gpu_stats_amd.reports.promql import PromClient
 from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
 

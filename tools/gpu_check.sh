@@ -1,0 +1,34 @@
+#!/bin/bash
+# One gpurun call: the round's hardware checkpoint.  Every GPU step has its own
+# time limit; a test failure (rc 1) does not stop the script, a timeout / signal /
+# abort (rc >= 124) does — nothing else touches the GPU after that.
+#   gpurun --timeout 1100 -- 'bash tools/gpu_check.sh <tag> [steps...]'
+# steps (default: probe tests smoke bench): probe tests smoke bench bench2 rocprof
+set -u
+TAG=${1:-r2}; shift || true
+STEPS=${*:-probe tests smoke bench}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name (limit ${lim}s) $(date +%T)"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
+           run probe_xgmi 90 python tools/probe_xgmi.py ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider ;;
+    smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
+    bench) run bench 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" ;;
+    bench2) run bench_b 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench_b.json" ;;
+    rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run -- python3 bench.py --steps 10 --warmup 2 --rounds 4 --out "$OUT/bench_rocprof.json" ;;
+  esac
+done
+echo "== done $(date +%T)"

@@ -18,7 +18,10 @@ def timeit(fn, n=200):
     xs = []
     for _ in range(n):
         t0 = time.perf_counter()
-        fn()
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 - e.g. AMDSMI_STATUS_INVAL: not supported on this part
+            return {"error": repr(e)[:200]}
         xs.append((time.perf_counter() - t0) * 1e6)
     xs.sort()
     return {"n": n, "p50_us": round(xs[n // 2], 1), "p99_us": round(xs[int(n * 0.99)], 1),
