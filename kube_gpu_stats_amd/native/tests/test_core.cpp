@@ -4,7 +4,8 @@
 //  1. Seqlock: one writer publishing self-consistent payloads (every word equal
 //     to the sequence), many readers; a torn read would show mixed words.
 //  2. SampleRing: readers walking back from head never see a slot out of order
-//     by more than the ring can explain, and never a torn slot.
+//     by more than the ring can explain, and never a torn slot; a reader lapped
+//     by the writer gets "absent", never a newer entry (generation check).
 //  3. Sampler over the mock backend with fault injection, readers calling
 //     window_busy / window_pmc / integ concurrently, then stop().
 //  4. Recovery: a device that resets mid-run is re-opened and re-baselined.
@@ -106,6 +107,59 @@ static void test_ring() {
   CHECK(n == 63);
   for (size_t i = 0; i < n; ++i) CHECK(buf[i].w[0] == 100000 - i);
   std::printf("ring ok\n");
+}
+
+// Generation check: a reader that holds an old head while
+// the writer laps the ring must get "absent", never a newer entry under the old
+// index — window searches rely on entries being time-ordered.
+static void test_ring_lap() {
+  SampleRing<Payload, 64> ring;
+  Payload p;
+  for (uint64_t s = 1; s <= 100; ++s) {
+    for (auto& x : p.w) x = s;
+    ring.push(p);
+  }
+  const uint64_t h = ring.head();  // entry e = h - 1 - i carries value e + 1
+  Payload out;
+  CHECK(ring.at_from(h, 5, out) && out.w[0] == h - 5);
+  for (uint64_t s = 101; s <= 100 + 64; ++s) {  // one full lap
+    for (auto& x : p.w) x = s;
+    ring.push(p);
+  }
+  for (uint64_t i = 0; i < 63; ++i) CHECK(!ring.at_from(h, i, out));  // every old slot now holds a newer lap
+  CHECK(ring.at(0, out) && out.w[0] == 164);
+  // Concurrent: a slow reader's lookups are either exact or absent.
+  std::atomic<bool> done{false};
+  std::atomic<uint64_t> exact{0}, lapped{0};
+  std::thread wr([&] {
+    Payload q;
+    for (uint64_t s = 165; s <= 200000; ++s) {
+      for (auto& x : q.w) x = s;
+      ring.push(q);
+    }
+    done = true;
+  });
+  std::thread rd([&] {
+    Payload o;
+    while (!done) {
+      const uint64_t hh = ring.head();
+      std::this_thread::yield();  // let the writer run ahead
+      for (uint64_t i = 0; i < 63; i += 7) {
+        if (ring.at_from(hh, i, o)) {
+          for (auto x : o.w) CHECK(x == o.w[0]);
+          CHECK(o.w[0] == hh - i);
+          ++exact;
+        } else {
+          ++lapped;
+        }
+      }
+    }
+  });
+  wr.join();
+  rd.join();
+  CHECK(exact > 0);
+  std::printf("ring lap ok (%llu exact, %llu lapped)\n", static_cast<unsigned long long>(exact.load()),
+              static_cast<unsigned long long>(lapped.load()));
 }
 
 static void test_sampler() {
@@ -307,6 +361,7 @@ int main() {
   test_parser_fuzz();
   test_seqlock();
   test_ring();
+  test_ring_lap();
   test_sampler();
   test_recovery();
   std::printf("ALL OK\n");

@@ -15,10 +15,15 @@ Reference: gpu_util_stats/gpu_util_stats.py.
 order M1 → M2 → M3 → M4 → M5) and reproduces its arithmetic and
 output exactly, quirks included (Q1 overwrite, Q2 divide-by-range, Q5 first
 sample, Q6 string counts, Q7 finished pods dropped, Q8 JSON dump on stdout).
-The default mode keeps the join semantics but fixes the quirks: server-side
-``avg_over_time`` per step (Q4), max card count (Q5), ints (Q6), series of one
-node combined card-weighted (Q1), time-weighted means with ``--missing`` (Q2/Q3),
-AMD resource/label names, debug output on stderr (Q8).
+The default mode keeps the join semantics but fixes the quirks: exact per-step
+means (Q4) from the exporter's per-pod counter
+``100 * avg(rate(container_gpu_busy_seconds_total[step])) by (...)`` — the
+integral of the PMFW busy accumulators since the pod got the GPU, so bursts
+between scrapes count; a gauge (``--util-metric container_gpu_sm_util``) gets
+``avg_over_time`` instead, which only sees what the exporter's window saw at each
+scrape — max card count (Q5), ints (Q6), series of one node combined
+card-weighted (Q1), time-weighted means with ``--missing`` (Q2/Q3), AMD
+resource/label names, debug output on stderr (Q8).
 """
 from __future__ import annotations
 
@@ -65,10 +70,11 @@ class Queries:
 
     @classmethod
     def amd(cls, namespace: str, step_s: int, resource: str = "amd_com_gpu",
-            type_label: str = "label_amd_com_gpu_product_name", util_metric: str = "container_gpu_sm_util") -> "Queries":
+            type_label: str = "label_amd_com_gpu_product_name",
+            util_metric: str = "container_gpu_busy_seconds_total") -> "Queries":
         ns = f'namespace="{namespace}",' if namespace else ""
         return cls(
-            util=(f"avg(avg_over_time({util_metric}[{step_s}s])) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)"),
+            util=util_query(util_metric, step_s),
             total=(f'max(kube_node_status_allocatable{{resource="{resource}"}} * on (node) '
                    f"group_left({type_label}) max(kube_node_labels) by (node, {type_label})) by (node, {type_label})"),
             used=(f'sum(max(kube_pod_container_resource_requests{{resource="{resource}",node!=""}} '
@@ -78,6 +84,16 @@ class Queries:
             req=f'max(kube_pod_container_resource_requests{{resource="{resource}"}}) by (node, pod)',
             type_label=type_label,
         )
+
+
+def util_query(metric: str, step_s: int) -> str:
+    """Per-(node, type, pod) utilisation percent per step.  A ``*_seconds_total``
+    counter (busy seconds since allocation) gives the exact mean over each step,
+    ``100 * rate``; a gauge can only be averaged at the scrapes."""
+    by = "by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)"
+    if metric.endswith("_seconds_total"):
+        return f"100 * avg(rate({metric}[{step_s}s])) {by}"
+    return f"avg(avg_over_time({metric}[{step_s}s])) {by}"
 
 
 # --------------------------------------------------------------------------- collectors (L2)
@@ -228,7 +244,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "missing", "skip", "node mode: treat missing samples as skip | zero")
     add_flag(ap, "resource", "amd_com_gpu", "KSM resource label value of the GPU resource")
     add_flag(ap, "type-label", "label_amd_com_gpu_product_name", "kube_node_labels label holding the GPU type")
-    add_flag(ap, "util-metric", "container_gpu_sm_util", "utilisation series")
+    add_flag(ap, "util-metric", "container_gpu_busy_seconds_total",
+             "utilisation series: a *_seconds_total busy counter (exact, rate() per step; default) or a percent "
+             "gauge such as container_gpu_sm_util / container_gpu_mfma_util (avg_over_time of the scrapes)")
     add_flag(ap, "format", "table", "table | json | csv")
     add_flag(ap, "show-finished", False, "also list pods with utilisation but no live allocation (reference drops them)")
     return ap

@@ -1,4 +1,4 @@
-"""In-process fake Prometheus HTTP API (tests, CPU plumbing config, demos).
+"""In-process fake Prometheus HTTP API (tests only).
 
 Two kinds of answers:
 
@@ -18,8 +18,32 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from urllib.parse import parse_qs, urlparse
 
 LOOKBACK_S = 300.0
-_AVG_BY = re.compile(r"^\s*avg\((.+)\)\s*by\s*\(([^)]*)\)\s*$")
+_AVG_BY = re.compile(r"^\s*(?:([0-9.]+)\s*\*\s*)?avg\((.+)\)\s*by\s*\(([^)]*)\)\s*$")
 _AOT = re.compile(r"^\s*avg_over_time\(\s*([a-zA-Z_:][a-zA-Z0-9_:]*)\s*\[(\d+)([smh])\]\s*\)\s*$")
+_RATE = re.compile(r"^\s*(rate|increase)\(\s*([a-zA-Z_:][a-zA-Z0-9_:]*)\s*\[(\d+)([smh])\]\s*\)\s*$")
+_UNIT = {"s": 1, "m": 60, "h": 3600}
+
+
+def extrapolated(pts: list[tuple[float, float]], start: float, end: float, is_rate: bool) -> float | None:
+    """Prometheus' extrapolatedRate (promql/functions.go) for a counter over (start, end]."""
+    if len(pts) < 2:
+        return None
+    result, prev = 0.0, pts[0][1]
+    for _, v in pts[1:]:
+        result += v - prev if v >= prev else v  # counter reset: count from 0
+        prev = v
+    t0, t1 = pts[0][0], pts[-1][0]
+    sampled = t1 - t0
+    if sampled <= 0:
+        return None
+    avg_gap = sampled / (len(pts) - 1)
+    to_start, to_end = t0 - start, end - t1
+    if result > 0 and pts[0][1] >= 0:  # a counter does not extrapolate below zero
+        to_start = min(to_start, sampled * (pts[0][1] / result))
+    thr = avg_gap * 1.1
+    interval = sampled + (to_start if to_start < thr else avg_gap / 2) + (to_end if to_end < thr else avg_gap / 2)
+    result *= interval / sampled
+    return result / (end - start) if is_rate else result
 _NAME = re.compile(r"^\s*([a-zA-Z_:][a-zA-Z0-9_:]*)\s*$")
 
 
@@ -53,6 +77,16 @@ class FakeProm:
 
     # ------------------------------------------------------------------ evaluation
     def _inner(self, expr: str, t: float) -> list[tuple[dict, float]]:
+        m = _RATE.match(expr)
+        if m:
+            fn, name, n, unit = m.group(1), m.group(2), int(m.group(3)), m.group(4)
+            rng = n * _UNIT[unit]
+            out = []
+            for key, pts in self.series.get(name, {}).items():
+                v = extrapolated([(ts, x) for ts, x in pts if t - rng < ts <= t], t - rng, t, fn == "rate")
+                if v is not None:
+                    out.append((dict(key), v))
+            return out
         m = _AOT.match(expr)
         if m:
             name, n, unit = m.group(1), int(m.group(2)), m.group(3)
@@ -80,12 +114,13 @@ class FakeProm:
         m = _AVG_BY.match(q)
         if not m:
             raise ValueError(f"unsupported query {q!r}")
-        by = [x.strip() for x in m.group(2).split(",") if x.strip()]
+        k = float(m.group(1)) if m.group(1) else 1.0
+        by = [x.strip() for x in m.group(3).split(",") if x.strip()]
         groups: dict[tuple, list[float]] = {}
-        for labels, v in self._inner(m.group(1), t):
-            groups.setdefault(tuple(labels.get(k, "") for k in by), []).append(v)
-        return [{"metric": {k: g[i] for i, k in enumerate(by) if g[i] != ""}, "value": [t, repr(sum(vs) / len(vs))]}
-                for g, vs in sorted(groups.items())]
+        for labels, v in self._inner(m.group(2), t):
+            groups.setdefault(tuple(labels.get(b, "") for b in by), []).append(v)
+        return [{"metric": {b: g[i] for i, b in enumerate(by) if g[i] != ""},
+                 "value": [t, repr(k * sum(vs) / len(vs))]} for g, vs in sorted(groups.items())]
 
     def eval_range(self, q: str, start: float, end: float, step: float) -> list[dict]:
         out: dict[tuple, dict] = {}

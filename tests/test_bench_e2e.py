@@ -109,7 +109,7 @@ def test_end_to_end_exporter_to_report(mock_exporter, tmp_path):
             for i in range(6):  # six "scrapes", 10 s apart in TSDB time
                 fp.ingest(parse_text(sc.scrape_once()), t0 + 10 * i)
                 time.sleep(0.05)
-        q = G.Queries.amd("ml", 10)
+        q = G.Queries.amd("ml", 10, util_metric="container_gpu_sm_util")  # gauge path; counters: test_accounting
         fp.add_instant(q.total, [{"metric": {"node": "node-a", q.type_label: "MI355X"}, "value": [t0, "8"]}])
         fp.add_instant(q.used, [{"metric": {"node": "node-a"}, "value": [t0, "2"]}])
         fp.add_instant(q.live, [{"metric": {"pod": "train-0"}, "value": [t0, "1"]}])

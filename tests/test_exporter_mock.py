@@ -356,6 +356,9 @@ def test_counter_handover_keeps_totals_monotonic(mock_exporter):
     assert {lb["gpu"]: v for lb, v in m2["kgs_pmc_enabled"]} == {"0": 0.0, "1": 0.0}
     assert {lb["gpu"]: v for lb, v in m2["kgs_pmc_releases_total"]} == {"0": 1.0, "1": 1.0}
     assert ex.integrals(1)["reads"] > 0                              # PMFW tier keeps sampling
+    # while released, no rate gauge may keep its last pre-hand-over value
+    assert not m2.get("amdgpu_mfma_util_percent") and not m2.get("container_gpu_mfma_util")
+    assert m2["amdgpu_gfx_busy_percent"]                              # the PMFW gauges stay
     ex.set_pmc_enabled(True)
     time.sleep(0.4)
     m3 = parse_text(ex.render())
@@ -453,3 +456,53 @@ def test_per_xcd_vmem_busy_full_set(mock_exporter):
     m = parse_text(ex.render())
     assert len(m["amdgpu_vmem_busy_xcc_percent"]) == 8
     assert "amdgpu_vmem_busy_xcc_percent" not in parse_text(base.render())  # base set: no TA block
+
+
+def test_stale_devices_export_no_window_gauges(mock_exporter):
+    """a device whose reads keep failing drops its busy gauges (and its
+    container_gpu_sm_util, which feeds the per-pod report) after stale_s instead of
+    repeating its last value; counters and kgs_up stay."""
+    ex = mock_exporter(n_gpus=2, hz=200, window_s=0.2, stale_s=0.3, max_backoff_ms=50,
+                       mock={"vanish_dev": 1, "vanish_after_s": 0.4})
+    for g in (0, 1):
+        ex.set_device_owners(g, [{"pod": f"p{g}", "namespace": "n", "container": "c"}])
+    time.sleep(0.3)
+    m = parse_text(ex.render())
+    assert sorted(lb["gpu"] for lb, _ in m["amdgpu_gfx_busy_percent"]) == ["0", "1"]
+    time.sleep(0.8)  # device 1 has failed for ≥ 0.4 s > stale_s
+    m = parse_text(ex.render())
+    assert sorted(lb["gpu"] for lb, _ in m["amdgpu_gfx_busy_percent"]) == ["0"]
+    assert sorted(lb["pod_name"] for lb, _ in m["container_gpu_sm_util"]) == ["p0"]
+    assert sorted(lb["gpu"] for lb, _ in m["amdgpu_gfx_busy_seconds_total"]) == ["0", "1"]
+    assert {lb["gpu"]: v for lb, v in m["kgs_up"]} == {"0": 1.0, "1": 0.0}
+    # paused sampling: everything goes stale, nothing frozen is exported
+    ex.pause()
+    time.sleep(0.5)
+    assert not parse_text(ex.render()).get("amdgpu_gfx_busy_percent")
+    ex.resume()
+
+
+def test_slow_tiers_never_stall_the_counter_threads(mock_exporter):
+    """the per-process / link / RAS reads go through one
+    process-wide AMD SMI lock and take milliseconds.  With the mock's latency
+    model (2 ms process list, 0.5 ms link table and RAS, all under one lock; 0.1 ms
+    table read) and those tiers at 50 / 20 Hz on 8 GPUs — the slow thread holds
+    the lock ~90 % of the time — every GPU's counter tier still delivers its rate."""
+    hz = 2000
+    ex = mock_exporter(n_gpus=8, hz=hz, pmc_source="mock", proc_period_s=0.02, link_period_s=0.05,
+                       mock={"proc_latency_s": 2e-3, "link_latency_s": 5e-4, "health_latency_s": 5e-4,
+                             "metrics_latency_s": 1e-4})
+    time.sleep(0.3)
+    n0 = [ex.integrals(g)["pmc_samples"] for g in range(8)]
+    t0 = time.time()
+    time.sleep(1.5)
+    n1 = [ex.integrals(g)["pmc_samples"] for g in range(8)]
+    dt = time.time() - t0
+    rates = [(b - a) / dt for a, b in zip(n0, n1)]
+    assert min(rates) > 0.95 * hz, rates
+    I = [ex.integrals(g) for g in range(8)]
+    assert all(i["proc_reads"] > 10 and i["link_reads"] > 5 for i in I), I
+    # the locked calls happened on the slow thread: its time per pass ≈ 8 × (2 + 0.5 + 0.5) ms
+    slow = sum(i["slow_read_seconds"] for i in I)
+    assert slow > 0.5, slow
+    assert ex.slow_passes > 10

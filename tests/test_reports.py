@@ -85,7 +85,9 @@ def test_pod_report_fixed_mode_ints_and_max_cards(prom):
 def test_amd_queries_mention_amd_resource():
     q = G.Queries.amd("ml", 3600)
     assert 'resource="amd_com_gpu"' in q.total and 'resource="amd_com_gpu"' in q.req
-    assert "avg_over_time(container_gpu_sm_util[3600s])" in q.util
+    assert q.util == ("100 * avg(rate(container_gpu_busy_seconds_total[3600s])) "
+                      "by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)")
+    assert "avg_over_time(container_gpu_sm_util[3600s])" in G.Queries.amd("ml", 3600, util_metric="container_gpu_sm_util").util
     assert 'namespace="ml"' in q.live
     assert 'namespace=' not in G.Queries.amd("", 60).live
 

@@ -98,7 +98,7 @@ def test_multi_node_rehearsal(N):
         for k in range(4):
             for ex in exs:
                 fp.ingest(parse_text(Scraper("127.0.0.1", ex.port).get()), t0 + 15 * k)
-        q = G.Queries.amd("ml", 15)
+        q = G.Queries.amd("ml", 15, util_metric="container_gpu_sm_util")
         fp.add_instant(q.total, [{"metric": {"node": f"node-{i}", q.type_label: "MI355X"}, "value": [t0, "2"]}
                                  for i in range(3)])
         fp.add_instant(q.used, [{"metric": {"node": f"node-{i}"}, "value": [t0, "1"]} for i in range(3)])
