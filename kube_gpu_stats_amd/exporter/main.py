@@ -6,9 +6,15 @@ one ``{"event": "ready", ...}`` JSON line on stdout once ``/metrics`` is being
 served, then runs until SIGTERM/SIGINT (or ``quit`` on stdin with
 ``--control-stdin``).
 
-Run it in its own process: with ``--pmc rocprofiler`` it registers a
-rocprofiler-sdk tool and initialises HSA itself, which must happen before any
-HIP runtime in the same process.
+Run it in its own process: with ``--pmc aqlprofile`` it initialises HSA and
+opens a private AQL queue per GPU for its counter READs, which must not share a
+process with a workload's HIP runtime.
+
+One counter reader ships: the direct aqlprofile CP reader.  The rocprofiler-sdk
+device-counting reader (``native/counters/pmc_rocprofiler.cpp``) is a test-only
+cross-check of its numbers: ``--pmc rocprofiler`` is refused unless
+``KGS_PMC_CROSSCHECK=1`` (tests/test_gpu.py sets it) — no runtime choice of
+backends in the product.
 """
 from __future__ import annotations
 
@@ -46,8 +52,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "proc-period", 0.0, "per-process tier period in seconds (overrides --proc-every; survives rate "
                                      "changes)")
     add_flag(ap, "link-period", 0.0, "xGMI link + RAS tier period in seconds (overrides --link-every)")
-    add_flag(ap, "pmc", "none", "hardware counters: none | aqlprofile (direct CP reads) | rocprofiler "
-                                "(rocprofiler-sdk device counting) | mock")
+    add_flag(ap, "pmc", "none", "hardware counters: none | aqlprofile (direct CP reads on a private AQL queue) "
+                                "| mock (tests)")
     add_flag(ap, "pmc-lib", "", "counter reader library (default: the in-tree one for --pmc)")
     add_flag(ap, "pmc-lean", 2, "aqlprofile READ packet: 0 as built (per-XCC CS_PARTIAL_FLUSH + full cache "
                                 "invalidate), 1 no flushes, 2 no flushes + L2 writeback only (default), 3 no cache op")
@@ -122,6 +128,13 @@ def config_from_args(a) -> dict:
 
 
 def run(a) -> int:
+    if a.pmc == "rocprofiler" and os.environ.get("KGS_PMC_CROSSCHECK") != "1":
+        L.error("--pmc rocprofiler is a test-only cross-check reader (set KGS_PMC_CROSSCHECK=1 in tests)")
+        print(json.dumps({"event": "error", "error": "--pmc rocprofiler is test-only"}), flush=True)
+        return 2
+    if a.pmc not in ("none", "aqlprofile", "mock", "rocprofiler"):
+        print(json.dumps({"event": "error", "error": f"unknown --pmc {a.pmc!r}"}), flush=True)
+        return 2
     N = load_native()
     cfg = config_from_args(a)
     try:

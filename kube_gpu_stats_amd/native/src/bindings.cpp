@@ -117,6 +117,7 @@ py::dict sample_dict(const GpuSample& s) {
   o["xgmi_write_kb"] = std::vector<uint64_t>(s.xgmi_write_kb, s.xgmi_write_kb + kMaxXgmi);
   o["xgmi_link_up"] = std::vector<uint16_t>(s.xgmi_link_up, s.xgmi_link_up + kMaxXgmi);
   o["xgmi_link_speed_gbps"] = s.xgmi_link_speed_gbps;
+  o["xgmi_link_width"] = s.xgmi_link_width;
   o["pcie_bw_acc_gb"] = s.pcie_bw_acc_gb;
   o["pcie_link_width"] = s.pcie_link_width;
   o["pcie_link_speed_01gts"] = s.pcie_link_speed_01gts;

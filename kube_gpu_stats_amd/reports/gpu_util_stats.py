@@ -119,7 +119,8 @@ def get_gpu_servers(c: PromClient, q: Queries, compat: bool) -> dict[str, tuple]
 def get_pod_by_servers(c: PromClient, q: Queries, start, end, step_s: int, compat: bool,
                        out=sys.stdout) -> dict[str, dict[str, object]]:
     """{node: {pod: cards}} for live pods — reference get_pod_by_servers :129-151 (M4, M5)."""
-    live = {m["metric"]["pod"] for m in result(c.query(q.live))}
+    # M4 is the reference's query_prom_instant, which sends no proxy (:32, Q9)
+    live = {m["metric"]["pod"] for m in result(c.query(q.live, proxied=not compat))}
     res = {}
     for m in result(c.query_range(q.req, start, end, step_s)):
         node = m["metric"].get("node", "<unknown>")

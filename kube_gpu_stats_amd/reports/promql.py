@@ -4,8 +4,10 @@ Reference: ``query_prom`` (gpu_util_stats.py:14-27, ``/query_range``) and
 ``query_prom_instant`` (:29-34, ``/query``), plus the two inline instant GETs of
 ``get_gpu_servers`` (:103-108, :115-120).  Differences, all deliberate:
 
-* one configured session — the proxy applies to every call (the reference skips
-  it for the instant client, :32 vs :24 — Q9);
+* the proxy applies to every call by default; ``--compat`` reproduces the
+  reference's inconsistency — its live-pod instant query (M4, ``query_prom_instant``
+  :29-34) goes out without the proxy, :32 vs :24 (Q9; call order/proxy pattern
+  T,T,T,F,T pinned by tests/test_reports.py);
 * HTTP and Prometheus-level errors raise ``PromError`` (the reference KeyErrors
   on ``['data']`` — Q10);
 * optional retries with backoff; the 5 s timeout stays the default (:24).
@@ -39,19 +41,33 @@ class PromClient:
         self.timeout_s = timeout_s
         self.retries = retries
         self.s = session or requests.Session()
+        self.proxy = proxy
         if proxy:
             self.s.proxies = {"http": proxy, "https": proxy}
+        self._direct = None  # lazily: a session without the configured proxy
         self.calls: list[tuple[str, dict]] = []
+        self.proxied: list[bool] = []  # per call, parallel to ``calls``
 
-    def _get(self, path: str, params: dict) -> dict:
+    def _session(self, proxied: bool):
+        if proxied or not self.proxy:
+            return self.s
+        if self._direct is None:
+            import requests
+
+            self._direct = requests.Session()
+        return self._direct
+
+    def _get(self, path: str, params: dict, proxied: bool = True) -> dict:
         import requests
 
         url = self.base_url + path
         last = None
+        sess = self._session(proxied)
         for attempt in range(self.retries + 1):
             try:
                 self.calls.append((path, dict(params)))
-                r = self.s.get(url, params=params, timeout=self.timeout_s)
+                self.proxied.append(bool(self.proxy) and proxied)
+                r = sess.get(url, params=params, timeout=self.timeout_s)
                 try:
                     body = r.json()
                 except ValueError as e:
@@ -67,11 +83,11 @@ class PromClient:
                     time.sleep(min(2.0, 0.2 * (2 ** attempt)))
         raise last if isinstance(last, PromError) else PromError(str(last))
 
-    def query(self, q: str, at=None) -> dict:
+    def query(self, q: str, at=None, proxied: bool = True) -> dict:
         p = {"query": q}
         if at is not None:
             p["time"] = to_unix(at)
-        return self._get("/query", p)
+        return self._get("/query", p, proxied)
 
     MAX_POINTS = 11000  # Prometheus rejects range queries above 11 000 points per series
 

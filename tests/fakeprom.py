@@ -53,6 +53,7 @@ class FakeProm:
         self.canned_range: dict[str, list] = {}
         self.series: dict[str, dict[tuple, list[tuple[float, float]]]] = {}
         self.calls: list[tuple[str, dict]] = []
+        self.via_proxy: list[bool] = []
         self._srv: ThreadingHTTPServer | None = None
         self._th: threading.Thread | None = None
         self.lock = threading.Lock()
@@ -160,6 +161,9 @@ class FakeProm:
         class H(BaseHTTPRequestHandler):
             def do_GET(self):  # noqa: N802
                 u = urlparse(self.path)
+                # a request sent through an HTTP proxy (this server doubling as one)
+                # carries the absolute URL in its request line
+                outer.via_proxy.append(self.path.startswith("http"))
                 params = {k: v[-1] for k, v in parse_qs(u.query).items()}
                 code, body = outer.handle(u.path, params)
                 data = json.dumps(body).encode()

@@ -3,6 +3,7 @@ exact integrals, Prometheus exposition, HTTP endpoints, fault isolation."""
 import http.client
 import json
 import math
+import os
 import time
 import urllib.request
 
@@ -10,6 +11,8 @@ import pytest
 from prometheus_client.parser import text_string_to_metric_families
 
 from kube_gpu_stats_amd.utils.scrape import parse_text
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def get(port, path):
@@ -506,3 +509,16 @@ def test_slow_tiers_never_stall_the_counter_threads(mock_exporter):
     slow = sum(i["slow_read_seconds"] for i in I)
     assert slow > 0.5, slow
     assert ex.slow_passes > 10
+
+
+def test_rocprofiler_reader_is_test_only():
+    """one counter reader in the product; the rocprofiler-sdk
+    reader is a cross-check that only tests can select."""
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k != "KGS_PMC_CROSSCHECK"}
+    r = subprocess.run([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--backend", "mock",
+                        "--listen", "127.0.0.1:0", "--pmc", "rocprofiler"],
+                       cwd=REPO, capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 2 and "test-only" in r.stdout

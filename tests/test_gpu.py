@@ -202,7 +202,7 @@ def test_counter_reader_exporter_process(torch_dev, mode):
     full = mode in ("aqlprofile-full", "rocprofiler")
     cmd += ["--pmc-set", "full" if full else "base"]
     proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                            text=True)
+                            text=True, env=dict(os.environ, KGS_PMC_CROSSCHECK="1"))
     try:
         ready = json.loads(proc.stdout.readline())
         print(json.dumps(ready)[:2000])
@@ -476,3 +476,155 @@ def test_hbm_bandwidth_estimate_tracks_stream_kernels(N, torch_dev):
     assert measured > 3e12, measured
     assert abs(est / measured - 1) < 0.10, (est, measured)
     assert idle_est < 0.05e12, idle_est
+
+
+def _bdf0():
+    import torch
+
+    p = torch.cuda.get_device_properties(0)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+
+def _keep(name: str, text: str) -> None:
+    """Raw evidence for profiles/ (merged back from the GPU box)."""
+    d = os.path.join(REPO, "gpurun_out", "gpu_tests")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, name), "w") as f:
+        f.write(text)
+
+
+def test_xgmi_links_topology_and_neighbor_export(N):
+    """N3 on hardware.  A 1-GPU lease of an 8-GPU MI355X node still sees the node's
+    xGMI fabric: the link table lists every peer by PCI address on its physical port
+    (port 0 is the disabled self port, peers on 1..7 — the table's num_links counts
+    peers only, round 1 dropped the last one), the PMFW table reports those ports up
+    with a link width and speed, and `kgs topo --format prom` exports one
+    amdgpu_xgmi_neighbor line per peer."""
+    from kube_gpu_stats_amd.utils.scrape import parse_text
+
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 50, "link_period_s": 0.05, "proc_period_s": 0})
+    ex.start()
+    t0 = time.time()
+    while time.time() - t0 < 3 and not ex.links(0):
+        time.sleep(0.05)
+    time.sleep(0.3)
+    links, snap, topo = ex.links(0), ex.snapshot(0), json.loads(ex.topology_json())
+    body = ex.render()
+    ex.stop()
+    _keep("xgmi_topology.json", json.dumps({"links": links, "topology": topo,
+                                            "pmfw": {k: snap[k] for k in ("xgmi_link_up", "xgmi_link_width",
+                                                                          "xgmi_link_speed_gbps", "xgmi_read_kb",
+                                                                          "xgmi_write_kb")}}, indent=1))
+    own = ex.devices()[0]["bdf"]
+    assert topo["devices"][0]["bdf"] == own
+    assert len(links) >= 1, "no xGMI links reported"
+    assert all(li["link_type"] == 2 for li in links), links          # AMDSMI_LINK_TYPE_XGMI
+    peers = [li["peer_bdf"] for li in links]
+    assert all(peers) and len(set(peers)) == len(peers) and own not in peers, peers
+    assert all(li["bit_rate_gbps"] > 0 and li["max_bw_gbps"] > 0 for li in links), links
+    ports = sorted(li["link"] for li in links)
+    assert 0 not in ports                                              # the self port is not a link
+    if os.environ.get("KGS_EXPECT_XGMI_PEERS"):
+        assert len(links) == int(os.environ["KGS_EXPECT_XGMI_PEERS"]), links
+    # PMFW agrees port by port: up exactly on the link table's ports
+    assert snap["xgmi_link_width"] > 0 and snap["xgmi_link_speed_gbps"] > 0, snap
+    up = snap["xgmi_link_up"]
+    assert [p for p in range(8) if up[p] == 1] == ports, (up, ports)
+    m = parse_text(body)
+    info = {lb["peer_bdf"] for lb, _ in m["amdgpu_xgmi_link_info"]}
+    assert info == set(peers)
+    assert sorted(int(lb["link"]) for lb, _ in m["amdgpu_xgmi_read_bytes_total"]) == ports
+    r = subprocess.run([sys.executable, "-m", "kube_gpu_stats_amd.cli", "topo", "--format", "prom",
+                        "--node-name", "n1"], cwd=REPO, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    _keep("kgs_topo_prom.txt", r.stdout)
+    nb = [ln for ln in r.stdout.splitlines() if ln.startswith("amdgpu_xgmi_neighbor{")]
+    assert len(nb) == 2 * len(peers)  # undirected: own→peer and peer→own
+    assert all(f'bdf="{own}"' in ln or f'peer_bdf="{own}"' in ln for ln in nb)
+
+
+def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
+    """The reference's contract end to end on MI355X: the exporter
+    process (amdsmi backend) with a static GPU→pod map emits
+    container_gpu_sm_util{kubernetes_io_hostname, nvidia_gpu_type="MI355X",
+    pod_name="train-0"} > 90 under the MFMA load; scrapes feed a (fake)
+    Prometheus; `gpu-util-stats` in fixed mode (exact busy-seconds counter) and in
+    --compat (the reference's own five queries) both report train-0 busy."""
+    import torch
+
+    from fakeprom import FakeProm
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.reports import gpu_util_stats as G
+    from kube_gpu_stats_amd.reports.promql import PromClient
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    bdf = _bdf0()
+    owners = tmp_path / "owners.json"
+    owners.write_text(json.dumps({bdf: {"pod": "train-0", "namespace": "ml", "container": "main"}}))
+    proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
+                             "--hz", "100", "--window", "1", "--node-name", "gpu-node-1", "--bdfs", bdf,
+                             "--static-owners", str(owners), "--control-stdin", "--pod-resources-socket", ""],
+                            cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    fp = FakeProm()
+    url = fp.start()
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready", ready
+        sc = Scraper("127.0.0.1", ready["port"])
+        ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
+        ls.run_mfma()
+        torch.cuda.synchronize()
+        t0 = time.time()
+        stamps, bodies = [], []
+        next_scrape = t0 + 1.5
+        while time.time() - t0 < 4.6:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+            if time.time() >= next_scrape:
+                body = sc.get()
+                ts = time.time()
+                fp.ingest(parse_text(body), ts)
+                stamps.append(ts)
+                bodies.append(body)
+                next_scrape += 0.25
+        _keep("f5_scrape.txt", bodies[-1])
+        m = parse_text(bodies[-1])
+        sm = [(lb, v) for lb, v in m["container_gpu_sm_util"]]
+        assert len(sm) == 1, sm
+        lb, v = sm[0]
+        assert (lb["kubernetes_io_hostname"], lb["nvidia_gpu_type"], lb["pod_name"]) == ("gpu-node-1", "MI355X",
+                                                                                        "train-0"), lb
+        assert v > 90, v
+        busy = m["container_gpu_busy_seconds_total"][0][1]
+        assert busy > 2.0, busy  # ≥ 3 s of MFMA load since the owner appeared
+        assert [x[0]["pod_name"] for x in m["kgs_gpu_owner"]] == ["train-0"]
+        assert len(stamps) >= 5
+        end = stamps[-1]
+        # fixed mode: 100 * avg(rate(container_gpu_busy_seconds_total[1s])) per pod
+        q = G.Queries.amd("ml", 1)
+        qc = G.Queries.compat("ml")
+        for qq in (q, qc):
+            fp.add_instant(qq.total, [{"metric": {"node": "gpu-node-1", qq.type_label: "MI355X"},
+                                       "value": [end, "8"]}])
+            fp.add_instant(qq.used, [{"metric": {"node": "gpu-node-1"}, "value": [end, "1"]}])
+            fp.add_instant(qq.live, [{"metric": {"pod": "train-0"}, "value": [end, "1"]}])
+            fp.add_range(qq.req, [{"metric": {"node": "gpu-node-1", "pod": "train-0"}, "values": [[end, "1"]]}])
+        rows = G.run_report(PromClient(url), q, end, 2, 1, compat=False)
+        assert [r[:3] for r in rows] == [["gpu-node-1", "train-0", 1]], rows
+        assert rows[0][3] > 90, rows
+        import io
+
+        out = io.StringIO()
+        crow = G.run_report(PromClient(url), qc, end, 2, 1, compat=True, out=out)
+        assert [r[:3] for r in crow] == [["gpu-node-1", "train-0", "1"]], crow  # reference's string cards
+        assert crow[0][3] > 90, crow
+        print(json.dumps({"gauge": v, "busy_seconds": busy, "fixed": rows, "compat": crow}))
+    finally:
+        fp.stop()
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            proc.communicate()

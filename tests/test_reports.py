@@ -42,6 +42,25 @@ def test_gpu_util_stats_compat_golden(prom):
         assert prm["step"] == 3600 and prm["end"] - prm["start"] == 86400
 
 
+def test_compat_reproduces_reference_proxy_pattern(prom, monkeypatch):
+    """the reference proxies M1-M3 and M5 but not the instant
+    query M4 (gpu_util_stats.py:32 vs :24,107,119): pattern T,T,T,F,T.  --compat keeps
+    it; the fixed mode proxies every call.  The fake Prometheus doubles as the proxy
+    and sees absolute-URL request lines for proxied calls."""
+    for k in ("NO_PROXY", "no_proxy", "HTTP_PROXY", "http_proxy"):
+        monkeypatch.delenv(k, raising=False)
+    fp, url = prom
+    q = install_reference_scenario(fp)
+    proxy = url.rsplit("/api/v1", 1)[0]
+    c = PromClient(url, proxy=proxy)
+    G.run_report(c, q, datetime.fromtimestamp(T_END), WINDOW, STEP, compat=True, out=io.StringIO())
+    assert c.proxied == [True, True, True, False, True]
+    assert fp.via_proxy[-5:] == [True, True, True, False, True]
+    c2 = PromClient(url, proxy=proxy)
+    G.run_report(c2, q, datetime.fromtimestamp(T_END), WINDOW, STEP, compat=False, out=io.StringIO())
+    assert all(c2.proxied) and all(fp.via_proxy[-5:])
+
+
 def test_node_report_compat_golden(prom):
     fp, url = prom
     q = install_reference_scenario(fp)
