@@ -32,9 +32,12 @@ from ..utils.config import add_flag
 
 L = log.get("exporter")
 
-# AMD SMI call latencies of the mock's latency model: rounded up from the
-# per-call latencies measured on MI355X (profiles/r2/amdsmi_latency.md).
-MOCK_LATENCY = {"proc_latency_s": 2e-3, "link_latency_s": 5e-4, "health_latency_s": 5e-4, "metrics_latency_s": 1e-4}
+# AMD SMI call latencies of the mock's latency model, from the per-call latencies
+# measured on MI355X (profiles/r2/amdsmi_latency.md): link metrics p99 0.99 ms, ECC
+# count p99 0.75 ms, PMFW table pread mean 0.125 ms; the process list (p50 74 µs with
+# one process) is modelled at 0.5 ms for a node with many GPU processes.
+MOCK_LATENCY = {"proc_latency_s": 5e-4, "link_latency_s": 1e-3, "health_latency_s": 7.5e-4,
+                "metrics_latency_s": 1.25e-4}
 
 
 def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.ArgumentParser:
@@ -42,8 +45,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "backend", "amdsmi", "device provider: amdsmi (MI355X) or mock")
     add_flag(ap, "mock-gpus", 8, "mock provider: number of GPUs")
     add_flag(ap, "mock-fail-rate", 0.0, "mock provider: injected read-failure probability")
-    add_flag(ap, "mock-latency", False, "mock provider: model AMD SMI latency (process list 2 ms, link table and RAS "
-                                        "0.5 ms each, under one global lock; PMFW table read 0.1 ms, unlocked)")
+    add_flag(ap, "mock-latency", False, "mock provider: model AMD SMI latency as measured on MI355X (process list "
+                                        "0.5 ms, link table 1 ms, RAS 0.75 ms, under one global lock; PMFW table "
+                                        "read 0.125 ms, unlocked)")
     add_flag(ap, "mock-partition", "SPX", "mock provider: compute partition mode (SPX | DPX | QPX | CPX)")
     add_flag(ap, "hz", 10.0, "sampler tick rate per GPU (1/10/100 Hz tiers; hardware counters every tick)")
     add_flag(ap, "pmfw-hz", 100.0, "cap on PMFW metrics-table reads/s (firmware refreshes it every ~20 ms)")

@@ -409,7 +409,7 @@ def test_counter_handover_stop_and_restart(torch_dev):
         ready = json.loads(proc.stdout.readline())
         assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
         sc = Scraper("127.0.0.1", ready["port"])
-        one = lambda m, f: m[f][0][1]  # noqa: E731
+        one = lambda m, f: m[f][0][1] if m.get(f) else None  # noqa: E731
         load(1.2)
         m0 = parse_text(sc.get())
         proc.send_signal(signal.SIGUSR1)
@@ -425,6 +425,7 @@ def test_counter_handover_stop_and_restart(torch_dev):
                                                                            ("m3", m3))}))
         assert one(m0, "amdgpu_mfma_util_percent") > 50 and one(m0, "kgs_pmc_enabled") == 1
         assert one(m2, "kgs_pmc_enabled") == 0 and one(m2, "kgs_pmc_samples_total") == one(m1, "kgs_pmc_samples_total")
+        assert one(m2, "amdgpu_mfma_util_percent") is None  # no frozen gauge while released
         assert one(m3, "kgs_pmc_enabled") == 1 and one(m3, "kgs_pmc_releases_total") == 1
         assert one(m3, "amdgpu_mfma_util_percent") > 50                    # counters read right after re-START
         grbm = lambda m: [v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT"][0]  # noqa: E731

@@ -4,8 +4,9 @@ the 2/4/8-GPU fan-out rehearsal of SURVEY.md §4.3).  NOT hardware numbers.
 For N mock GPUs × tick rate: achieved samples/s/GPU (counter tier, worst GPU),
 sampler overruns per GPU per second, p50/p99 /metrics latency over keep-alive
 HTTP, body size, and exporter CPU cost (process CPU seconds per wall second).
-With ``--latency`` the mock models AMD SMI: process list 2 ms, link table and RAS
-0.5 ms each, all under one process-wide lock, PMFW table read 0.1 ms — the
+Rows with the latency model use AMD SMI call latencies measured on MI355X
+(exporter/main.py MOCK_LATENCY, profiles/r2/amdsmi_latency.md) under one
+process-wide lock — the
 per-process tier at 10 Hz and the link tier at 1 Hz run on the node-wide slow
 thread, never on the per-GPU threads (profiles/r2/mock_scaling.md).
     python tools/mock_scaling.py [--latency] [--out profiles/r2/mock_scaling.md]
@@ -27,7 +28,7 @@ def cpu_s() -> float:
     return r.ru_utime + r.ru_stime
 
 
-LATENCY = {"proc_latency_s": 2e-3, "link_latency_s": 5e-4, "health_latency_s": 5e-4, "metrics_latency_s": 1e-4}
+from kube_gpu_stats_amd.exporter.main import MOCK_LATENCY as LATENCY  # noqa: E402  (MI355X-measured)
 
 
 def one(N, n_gpus: int, hz: float, latency: bool, secs: float = 2.0, scrapes: int = 200) -> dict:
@@ -72,8 +73,9 @@ def main():
                  f"`tools/mock_scaling.py` in the build container ({os.cpu_count()} CPUs): native exporter, mock "
                  "N-GPU provider + mock counter source, one sampler thread per GPU plus the node-wide slow thread "
                  "(per-process tier 10 Hz, link + RAS tier 1 Hz), 200 keep-alive scrapes of /metrics per row.  "
-                 "`latency` rows model AMD SMI: process list 2 ms, link table and RAS 0.5 ms each under ONE "
-                 "process-wide lock, PMFW table read 0.1 ms unlocked.", "",
+                 "`latency` rows model AMD SMI with the call latencies measured on MI355X "
+                 "(`profiles/r2/amdsmi_latency.md`: process list 0.5 ms, link table 1 ms, RAS 0.75 ms under ONE "
+                 "process-wide lock, PMFW table read 0.125 ms unlocked).", "",
                  "| GPUs | tick Hz | AMD SMI latency model | samples/s/GPU | worst GPU % of nominal | overruns/s/GPU | "
                  "proc-list reads/s/GPU | p50 scrape ms | p99 scrape ms | /metrics KiB | exporter CPU cores |",
                  "|---|---|---|---|---|---|---|---|---|---|---|"]
