@@ -1,0 +1,61 @@
+"""Offline checks of the evidence tools (no GPU): the rocprofv3 trace splitter
+assigns kernels to bench segments by launch order."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rocprof_overhead_splits_by_condition(tmp_path):
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import rocprof_overhead as R
+
+    res = {"steps": 3, "warmup": 1, "config": {"units_per_step": 2},
+           "interleaved": {"block_steps": 1, "block_seconds": [["0", 1], ["100", 1], ["8000", 1],
+                                                               ["8000", 1], ["100", 1], ["0", 1]]}}
+    tiny, triads = 3, 2
+    dur = {"A_off": 100, "B_on_8k": 102, "C_off": 100, "I_paused": 100, "I_100Hz": 100, "I_8000Hz": 101,
+           "calib": 50, "calib_reps": 50, "warmup": 50}
+    rows, t = [], 0
+
+    def launch(name, d):
+        nonlocal t
+        rows.append({"Kernel_Name": name, "Start_Timestamp": t, "End_Timestamp": t + d})
+        t += d + 10
+
+    def unit(d):
+        launch("mfma_bf16_kernel(...)", d * 1000)
+        for _ in range(triads):
+            launch("triad_f32_kernel(...)", d * 10)
+        for _ in range(tiny):
+            launch("copy_f32_kernel(...)", d)
+
+    launch("copy_f32_kernel(...)", 50)          # eager warm-up copy before graph capture
+    launch("mfma_bf16_kernel(...)", 50 * 1000)  # calibrate(): 1 mfma, 1 triad, 1 graph replay
+    launch("triad_f32_kernel(...)", 500)
+    for _ in range(tiny):
+        launch("copy_f32_kernel(...)", 50)
+    launch("elementwise_kernel<torch>", 7)      # foreign kernels are ignored
+    for label, units in R.segments(res, triads, tiny):
+        for _ in range(units):
+            unit(dur[label])
+    d = tmp_path / "trace" / "host" / "123"
+    d.mkdir(parents=True)
+    with open(d / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        w.writerows(rows)
+    bj = tmp_path / "bench.json"
+    bj.write_text(json.dumps(res) + "\n")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "rocprof_overhead.py"), str(tmp_path / "trace"),
+                          str(bj), "--triads", str(triads), "--tiny", str(tiny), "--out", str(tmp_path / "o.md")],
+                         capture_output=True, text=True, check=True).stdout
+    r = json.loads(out)["kernels"]
+    for kind in ("mfma", "triad", "copy"):
+        k = r[kind]
+        assert abs(k["B_vs_AC_pct"] - 2.0) < 1e-9, k
+        assert abs(k["I_8000Hz_vs_paused_pct"] - 1.0) < 1e-9 and abs(k["I_100Hz_vs_paused_pct"]) < 1e-9, k
+    assert "| mfma |" in (tmp_path / "o.md").read_text()

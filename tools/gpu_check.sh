@@ -28,7 +28,7 @@ for s in $STEPS; do
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" ;;
     bench2) run bench_b 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench_b.json" ;;
-    rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run -- python3 bench.py --steps 10 --warmup 2 --rounds 4 --out "$OUT/bench_rocprof.json" ;;
+    rocprof) run rocprof 1000 bash tools/gpu_rocprof.sh "$OUT/rocprof" ;;
   esac
 done
 echo "== done $(date +%T)"

@@ -1,12 +1,21 @@
-"""Split a rocprofv3 kernel trace of ``bench.py`` into its phases and compare
-per-kernel GPU time with the exporter off (A, C) and on (B).
+"""Split a rocprofv3 kernel trace of ``bench.py`` by exporter condition and compare
+per-kernel GPU time: no exporter process (phases A, C), sampling at 8 kHz (B), and
+the interleaved blocks (paused / 100 Hz / 8 kHz).
 
-bench.py launches, per rank: W warm-up steps, one calibration step, then K steps
-in each of phases A, B, C; a step is one ``mfma_bf16_kernel`` followed by
-``--triads`` ``triad_f32_kernel`` launches.  Kernels are assigned to phases by
-launch order, so no clock translation between rocprofv3 and Python is needed.
+bench.py launches, per rank, in this order (``load`` units: one
+``mfma_bf16_kernel``, ``--triads`` ``triad_f32_kernel``, one replay of the
+``--tiny-kernels`` copy graph):
 
-    python tools/rocprof_overhead.py <trace dir> --warmup W --steps K [--triads 2] [--out md]
+* ``calibrate()``: 1 mfma, 1 triad, 1 graph replay (after 1 eager warm-up copy);
+* ``calibrate_reps()``: 2 units;
+* warm-up W steps, A K steps, B K steps, the interleaved blocks in
+  ``interleaved.block_seconds`` order (``block_steps`` steps each), C K steps —
+  every step ``config.units_per_step`` units.
+
+Kernels are assigned to segments by launch order, so no clock translation between
+rocprofv3 and Python is needed.
+
+    python tools/rocprof_overhead.py <trace dir> <bench.json> [--out md]
 """
 import argparse
 import csv
@@ -23,61 +32,85 @@ def find_trace(d: str) -> str:
     return c[-1]
 
 
+def segments(res: dict, triads: int, tiny: int) -> list[tuple[str, int]]:
+    """(label, units) in launch order after the calibration launches."""
+    reps = res["config"]["units_per_step"]
+    k, w = res["steps"], res["warmup"]
+    inter = res.get("interleaved") or {}
+    bs = inter.get("block_steps", 0)
+    seg = [("calib_reps", 2), ("warmup", w * reps), ("A_off", k * reps), ("B_on_8k", k * reps)]
+    seg += [(f"I_{'paused' if c == '0' else c + 'Hz'}", bs * reps) for c, _ in inter.get("block_seconds", [])]
+    seg += [("C_off", k * reps)]
+    return seg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--warmup", type=int, required=True)
-    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("bench_json")
     ap.add_argument("--triads", type=int, default=2)
-    ap.add_argument("--tiny", type=int, default=2000, help="tiny copy kernels per step (bench --tiny-kernels)")
+    ap.add_argument("--tiny", type=int, default=2000)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
+    with open(a.bench_json) as f:
+        res = json.loads(f.read().strip().splitlines()[-1])
     path = find_trace(a.dir)
-    rows = list(csv.DictReader(open(path)))
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     by = {"mfma": [], "triad": [], "copy": []}
-    for r in rows:
-        name = r["Kernel_Name"]
-        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3  # µs
+    with open(path) as f:
+        rows = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                       for r in csv.DictReader(f)), key=lambda x: x[0])
+    for t0, t1, name in rows:
+        dur = (t1 - t0) * 1e-3  # µs
         if "mfma_bf16_kernel" in name:
             by["mfma"].append(dur)
         elif "triad_f32_kernel" in name:
             by["triad"].append(dur)
         elif "copy_f32_kernel" in name:
             by["copy"].append(dur)
-    res = {"trace": os.path.relpath(path), "kernels_total": len(rows)}
-    kinds = [("mfma", 1), ("triad", a.triads)] + ([("copy", a.tiny)] if a.tiny else [])
-    for kind, per_step in kinds:
-        xs = by[kind]
-        # the calibration step launches one mfma + one triad (+ one graph replay);
-        # the tiny-kernel graph is preceded by one eager warm-up copy
-        skip = a.warmup * per_step + (1 if kind != "copy" else 1 + per_step)
-        n = a.steps * per_step
-        ph = {"A_off": xs[skip:skip + n], "B_on": xs[skip + n:skip + 2 * n], "C_off": xs[skip + 2 * n:skip + 3 * n]}
-        if any(len(v) != n for v in ph.values()):
-            res[kind] = {"error": f"expected {3 * n + skip} launches, found {len(xs)}"}
+    per_unit = {"mfma": 1, "triad": a.triads, "copy": a.tiny}
+    calib = {"mfma": 1, "triad": 1, "copy": 1 + a.tiny}
+    seg = segments(res, a.triads, a.tiny)
+    out = {"trace": os.path.relpath(path), "kernels_total": len(rows), "kernels": {}}
+    for kind, xs in by.items():
+        if per_unit[kind] == 0:
             continue
-        med = {k: statistics.median(v) for k, v in ph.items()}
-        mean = {k: statistics.fmean(v) for k, v in ph.items()}
-        off = 0.5 * (mean["A_off"] + mean["C_off"])
-        res[kind] = {"median_us": med, "mean_us": mean, "launches_per_phase": n,
-                     "gpu_time_overhead_pct": 100.0 * (mean["B_on"] / off - 1.0)}
-    print(json.dumps(res, indent=1))
+        i = calib[kind]
+        groups: dict[str, list[float]] = {}
+        for label, units in seg:
+            n = units * per_unit[kind]
+            key = label if not label.startswith("I_") else label
+            groups.setdefault(key, []).extend(xs[i:i + n])
+            i += n
+        if i != len(xs):
+            out["kernels"][kind] = {"error": f"expected {i} launches, found {len(xs)}"}
+            continue
+        mean = {g: statistics.fmean(v) for g, v in groups.items() if v}
+        base_abc = 0.5 * (mean["A_off"] + mean["C_off"])
+        r = {"mean_us": {g: round(m, 3) for g, m in mean.items()},
+             "launches": {g: len(v) for g, v in groups.items()},
+             "B_vs_AC_pct": 100.0 * (mean["B_on_8k"] / base_abc - 1.0)}
+        if "I_paused" in mean:
+            for g in mean:
+                if g.startswith("I_") and g != "I_paused":
+                    r[f"{g}_vs_paused_pct"] = 100.0 * (mean[g] / mean["I_paused"] - 1.0)
+        out["kernels"][kind] = r
+    print(json.dumps(out, indent=1))
     if a.out:
-        lines = ["# GPU-time overhead from a rocprofv3 kernel trace of bench.py", "",
-                 f"Trace: `{res['trace']}` ({res['kernels_total']} kernels). Phases by launch order: "
-                 f"warm-up {a.warmup} + 1 calibration step, then {a.steps} steps each of A (exporter off), "
-                 "B (exporter on), C (exporter off).", "",
-                 "| kernel | launches/phase | A off mean µs | B on mean µs | C off mean µs | overhead % (B vs mean(A,C)) |",
-                 "|---|---|---|---|---|---|"]
-        for kind, _ in kinds:
-            r = res[kind]
+        conds = ["A_off", "B_on_8k", "C_off", "I_paused", "I_100Hz", "I_8000Hz"]
+        lines = ["# Per-kernel GPU time by exporter condition (rocprofv3 kernel trace of bench.py)", "",
+                 f"Trace: `{out['trace']}` ({out['kernels_total']} kernels), assigned to bench segments by "
+                 "launch order (`tools/rocprof_overhead.py`).  A / C: no exporter process; B: sampling at 8 kHz; "
+                 "I_*: interleaved blocks, exporter paused or sampling at 100 Hz / 8 kHz.", "",
+                 "| kernel | " + " | ".join(f"{c} mean µs" for c in conds) + " | B vs A/C % | 100 Hz vs paused % | "
+                 "8 kHz vs paused % |", "|---" * (len(conds) + 4) + "|"]
+        for kind, r in out["kernels"].items():
             if "error" in r:
-                lines.append(f"| {kind} | {r['error']} | | | | |")
+                lines.append(f"| {kind} | {r['error']} |")
                 continue
             m = r["mean_us"]
-            lines.append(f"| {kind} | {r['launches_per_phase']} | {m['A_off']:.1f} | {m['B_on']:.1f} | "
-                         f"{m['C_off']:.1f} | {r['gpu_time_overhead_pct']:+.3f} |")
+            cells = " | ".join(f"{m[c]:.3f}" if c in m else "" for c in conds)
+            lines.append(f"| {kind} | {cells} | {r['B_vs_AC_pct']:+.3f} | {r.get('I_100Hz_vs_paused_pct', 0):+.3f} | "
+                         f"{r.get('I_8000Hz_vs_paused_pct', 0):+.3f} |")
         with open(a.out, "w") as f:
             f.write("\n".join(lines) + "\n")
 
