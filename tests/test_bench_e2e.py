@@ -57,7 +57,10 @@ def test_bench_contract_single_process():
         t = inter["tiers"][hz]
         assert len(t["overhead_per_round_pct"]) == 4
         assert t["overhead_ci95_pct"] > 0 and abs(t["overhead_pct"]) < 50
-        assert t["samples_per_sec_per_gpu"]["0"] == pytest.approx(float(hz), rel=0.05)
+        # 4 blocks of ~60 ms: at 100 Hz that is ~25 ticks, so whole-tick quantisation at
+        # each block edge alone is ±4 per cent; 8 kHz has ~2000 ticks and is held tighter
+        tol = 0.15 if hz == "100" else 0.05
+        assert t["samples_per_sec_per_gpu"]["0"] == pytest.approx(float(hz), rel=tol)
     assert res["overhead_pct"] == inter["tiers"]["8000"]["overhead_pct"]
 
 
