@@ -7,8 +7,9 @@ reads one exporter directly: every ``--interval`` it scrapes ``/metrics`` and
 prints one row per GPU.  Rates (xGMI bytes/s, average power from the energy
 counter) come from counter deltas between two polls.  With ``--counters`` it
 also drains the full-rate counter stream (``/counters?since=``) and reports
-the min / max of per-drain MFMA utilisation inside each interval.  At an 8 kHz
-tick that exposes bursts the 1 s window gauges average away.
+the min / max of per-drain MFMA utilisation, the number of busy bursts and the
+exact busy duty cycle inside each interval (``segments``).  At an 8 kHz tick
+that exposes bursts the 1 s window gauges average away.
 """
 from __future__ import annotations
 
@@ -25,7 +26,40 @@ COLS = [("gpu", "GPU", 3), ("pod", "POD", 18), ("gfx", "GFX%", 5), ("mfma", "MFM
         ("umc", "UMC%", 5), ("hbm_gb", "HBM_GB", 7), ("hbm_pct", "HBM%", 5), ("power_w", "PWR_W", 6),
         ("energy_w", "AVG_W", 6), ("temp_c", "TEMP", 4), ("clk_mhz", "MHZ", 5), ("xgmi_gbps", "XGMI_GB/s", 9),
         ("xcd_mfma", "MFMA%_PER_XCD", 31)]
-BURST_COLS = [("mfma_min", "MFMA_MIN", 8), ("mfma_max", "MFMA_MAX", 8), ("drains", "DRAINS", 6)]
+BURST_COLS = [("mfma_min", "MFMA_MIN", 8), ("mfma_max", "MFMA_MAX", 8), ("bursts", "BURSTS", 6),
+              ("duty", "DUTY%", 5), ("drains", "DRAINS", 6)]
+
+
+def segments(samples: list[dict], key: str = "gpu_active_pct", hi: float = 60.0,
+             lo: float = 20.0) -> tuple[list[tuple[int, int]], float, float]:
+    """Busy segments of a full-rate counter stream (``/counters`` samples, oldest
+    first, each covering ``dt_us`` up to its ``mono_ns``).
+
+    Returns ``(segments, busy_s, span_s)``: the ``[start_ns, end_ns)`` runs where
+    ``key`` rose to ≥ ``hi`` and had not yet fallen to ≤ ``lo`` (hysteresis, so a
+    burst that straddles a drain boundary is one segment), the exact busy integral
+    Σ key/100 · dt over the samples, and the time they span.  At an 8 kHz drain
+    rate a 1 ms kernel is ~8 drains: the stream resolves each burst, where the
+    ≈50 Hz PMFW table only sees their average."""
+    segs: list[tuple[int, int]] = []
+    busy = span = 0.0
+    start = None
+    for x in samples:
+        if key not in x or "dt_us" not in x:
+            continue
+        v, dt_ns = float(x[key]), float(x["dt_us"]) * 1e3
+        t1 = int(x["mono_ns"])
+        t0 = int(t1 - dt_ns)
+        busy += v * 0.01 * dt_ns * 1e-9
+        span += dt_ns * 1e-9
+        if start is None and v >= hi:
+            start = t0
+        elif start is not None and v <= lo:
+            segs.append((start, t0))
+            start = None
+    if start is not None and samples:
+        segs.append((start, int(samples[-1]["mono_ns"])))
+    return segs, busy, span
 
 
 def _by_gpu(m: dict, fam: str, **match) -> dict[str, float]:
@@ -136,7 +170,10 @@ class CounterStream:
             if s:
                 self.since[g] = s[-1]["seq"]
             vals = [x["mfma_util_pct"] for x in s if "mfma_util_pct" in x]
+            segs, busy, span = segments(s) if since else ([], 0.0, 0.0)
             out[g] = {"mfma_min": min(vals) if vals else None, "mfma_max": max(vals) if vals else None,
+                      "bursts": len(segs) if since else None,
+                      "duty": 100.0 * busy / span if span > 0 else None,
                       "drains": len(s) if since else None}
         return out
 

@@ -41,7 +41,10 @@ def test_bursty_pod_counter_report_is_exact_gauge_misses(mock_exporter):
     url = fp.start()
     stamps = []
     try:
-        for k in range(k0, k0 + 13):
+        # 17 scrapes = 12 s of data for a 6 s report window at a 3 s step: the first step's
+        # range (end-9, end-6] lies inside the data (the client sends whole seconds), so
+        # rate() never extrapolates from the series start (a true Prometheus artefact)
+        for k in range(k0, k0 + 17):
             at = offset + k * PERIOD + phase
             time.sleep(max(0.0, at - time.time()))
             ts = time.time()

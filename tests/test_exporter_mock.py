@@ -492,17 +492,28 @@ def test_slow_tiers_never_stall_the_counter_threads(mock_exporter):
     table read) and those tiers at 50 / 20 Hz on 8 GPUs — the slow thread holds
     the lock ~90 % of the time — every GPU's counter tier still delivers its rate."""
     hz = 2000
-    ex = mock_exporter(n_gpus=8, hz=hz, pmc_source="mock", proc_period_s=0.02, link_period_s=0.05,
-                       mock={"proc_latency_s": 2e-3, "link_latency_s": 5e-4, "health_latency_s": 5e-4,
-                             "metrics_latency_s": 1e-4})
-    time.sleep(0.3)
-    n0 = [ex.integrals(g)["pmc_samples"] for g in range(8)]
-    t0 = time.time()
-    time.sleep(1.5)
-    n1 = [ex.integrals(g)["pmc_samples"] for g in range(8)]
-    dt = time.time() - t0
-    rates = [(b - a) / dt for a, b in zip(n0, n1)]
-    assert min(rates) > 0.95 * hz, rates
+    lat = {"proc_latency_s": 2e-3, "link_latency_s": 5e-4, "health_latency_s": 5e-4, "metrics_latency_s": 1e-4}
+
+    def rates(ex):
+        time.sleep(0.3)
+        n0 = [ex.integrals(g)["pmc_samples"] for g in range(8)]
+        t0 = time.time()
+        time.sleep(1.5)
+        n1 = [ex.integrals(g)["pmc_samples"] for g in range(8)]
+        dt = time.time() - t0
+        return [(b - a) / dt for a, b in zip(n0, n1)]
+
+    ex = mock_exporter(n_gpus=8, hz=hz, pmc_source="mock", proc_period_s=0.02, link_period_s=0.05, mock=lat)
+    on = rates(ex)
+    ex.stop()
+    # control: the same 8 counter threads with no slow tier at all, on the same (shared,
+    # possibly busy) CPUs — the slow tiers may cost nothing beyond what the host costs both
+    ctl = mock_exporter(n_gpus=8, hz=hz, pmc_source="mock", proc_period_s=0, link_period_s=0, proc_every=0,
+                        link_every=0, mock=lat)
+    off = rates(ctl)
+    ctl.stop()
+    assert min(on) > 0.95 * min(hz, sum(off) / len(off)), (on, off)
+    assert min(on) > 0.85 * hz, (on, off)
     I = [ex.integrals(g) for g in range(8)]
     assert all(i["proc_reads"] > 10 and i["link_reads"] > 5 for i in I), I
     # the locked calls happened on the slow thread: its time per pass ≈ 8 × (2 + 0.5 + 0.5) ms

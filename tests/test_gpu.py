@@ -629,3 +629,91 @@ def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
         except Exception:  # noqa: BLE001
             proc.kill()
             proc.communicate()
+
+
+def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
+    """What the 8 kHz counter tier buys ("the headline value is a
+    dial"): a 200 Hz train of ~1 ms MFMA bursts — far inside one ≈20 ms PMFW table
+    period — is resolved burst by burst by the exporter's full-rate /counters stream
+    (one segment per launched burst, burst length and duty cycle as the host timed
+    them), while every PMFW table of the same interval only sees their average."""
+    import urllib.request
+
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+    from kube_gpu_stats_amd.reports.dmon import segments
+
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(16, 32, generator=g).to(torch.bfloat16).to(torch_dev)
+    B = torch.randn(32, 64, generator=g).to(torch.bfloat16).to(torch_dev)
+    blocks = 2048
+    C = torch.empty(blocks * 4 * 16 * 64, device=torch_dev)
+    load.mfma_bf16(A, B, C, blocks, 1000)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    load.mfma_bf16(A, B, C, blocks, 4000)
+    e1.record()
+    torch.cuda.synchronize()
+    iters = max(200, int(4000 * 1.0 / e0.elapsed_time(e1)))  # ≈1 ms per burst
+    cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz", "8000",
+           "--pmc", "aqlprofile", "--control-stdin", "--bdfs", _bdf0(), "--proc-every", "0", "--link-every", "0"]
+    proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True)
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
+        base = f"http://127.0.0.1:{ready['port']}"
+        time.sleep(0.3)
+        period, bursts = 0.005, []
+        w0 = time.time_ns()
+        nxt = time.monotonic()
+        t_end = nxt + 0.7  # the 8192-deep full-rate ring holds ≈1 s at 8 kHz
+        while time.monotonic() < t_end:
+            t0 = time.monotonic_ns()
+            load.mfma_bf16(A, B, C, blocks, iters)
+            torch.cuda.synchronize()
+            bursts.append((t0, time.monotonic_ns()))
+            nxt += period
+            d = nxt - time.monotonic()
+            if d > 0:
+                time.sleep(d)
+        w1 = time.time_ns()
+        time.sleep(0.05)
+        cnt = json.load(urllib.request.urlopen(base + "/counters?gpu=0&n=8190", timeout=10))["samples"]
+        pm = json.load(urllib.request.urlopen(base + "/samples?gpu=0&n=200", timeout=10))
+    finally:
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            proc.communicate()
+    lo, hi = bursts[0][0] - 2_000_000, bursts[-1][1] + 2_000_000
+    win = [x for x in cnt if lo <= x["mono_ns"] <= hi]
+    segs, busy, span = segments(win)
+    host_len = sorted(b - a for a, b in bursts)[len(bursts) // 2] * 1e-6
+    seg_len = sorted(e - s for s, e in segs)[len(segs) // 2] * 1e-6 if segs else 0.0
+    host_duty = sum(b - a for a, b in bursts) * 1e-9 / span if span else 0.0
+    act = [x["gpu_active_pct"] for x in win if "gpu_active_pct" in x]
+    # PMFW tables published while the burst train ran (host wall clock)
+    pm_in = [s["gfx_busy_window_pct"] for s in pm if w0 + 25_000_000 <= s["wall_ns"] <= w1]
+    summary = {"bursts_launched": len(bursts), "iters": iters, "drains_in_window": len(win),
+               "drain_rate_hz": len(win) / span if span else 0, "segments": len(segs),
+               "median_burst_ms_host": host_len, "median_segment_ms_counters": seg_len,
+               "duty_counters": busy / span if span else 0, "duty_host": host_duty,
+               "active_pct_min": min(act), "active_pct_max": max(act),
+               "pmfw_tables_in_window": len(pm_in), "pmfw_gfx_busy_pct": pm_in,
+               "first_50ms_active_pct": [[round((x["mono_ns"] - lo) * 1e-6, 3), round(x["gpu_active_pct"], 1)]
+                                         for x in win if x["mono_ns"] - lo <= 52_000_000 and "gpu_active_pct" in x]}
+    _keep("burst_resolution.json", json.dumps(summary, indent=1))
+    print(json.dumps({k: v for k, v in summary.items() if k != "first_50ms_active_pct"}))
+    assert summary["drain_rate_hz"] > 7000, summary
+    assert abs(len(segs) - len(bursts)) <= max(3, 0.05 * len(bursts)), summary
+    assert abs(seg_len - host_len) < 0.35 * host_len + 0.25, summary  # ±2 drains of 125 µs + launch/sync jitter
+    assert min(act) < 5 and max(act) > 90, summary
+    assert abs(summary["duty_counters"] - host_duty) < 0.08, summary
+    assert len(pm_in) >= 10, summary                  # ≈50 tables/s
+    assert max(pm_in) < 70, summary                   # every table averages bursts with gaps

@@ -5,6 +5,8 @@ import subprocess
 import sys
 import time
 
+import pytest
+
 from prometheus_client.parser import text_string_to_metric_families
 
 from kube_gpu_stats_amd.models.schema import BY_NAME, CATALOG
@@ -96,6 +98,31 @@ def test_cli_exporter_mock_process():
     assert stopped["event"] == "stopped" and stopped["integrals"][0]["reads"] > 0
 
 
+def test_dmon_segments_resolve_bursts_with_hysteresis():
+    """segments(): a 200 Hz train of 1 ms bursts sampled every 125 µs (8 kHz) gives
+    one segment per burst — a burst split across drain boundaries, or dipping to
+    50 % inside, stays one — and the exact busy integral / duty of 20 %."""
+    from kube_gpu_stats_amd.reports.dmon import segments
+
+    dt_ns = 125_000
+    samples, t = [], 10_000_000
+    for k in range(1600):  # 0.2 s
+        t += dt_ns
+        phase = (t - dt_ns - 10_000_000) % 5_000_000  # interval start within the 5 ms period
+        v = 100.0 if phase < 1_000_000 else 0.0
+        if phase == 500_000:
+            v = 50.0  # a dip inside a burst: above the low threshold, no new segment
+        samples.append({"seq": k, "mono_ns": t, "dt_us": dt_ns / 1e3, "gpu_active_pct": v})
+    segs, busy, span = segments(samples)
+    assert len(segs) == 40
+    assert all(e - s == 1_000_000 for s, e in segs)
+    assert all(b[0] - a[0] == 5_000_000 for a, b in zip(segs, segs[1:]))
+    assert span == pytest.approx(0.2) and busy / span == pytest.approx(0.2 - 0.5 * 40 * 125e-6 / 0.2, rel=1e-6)
+    # an open burst at the end closes at the last sample; entries without rates are skipped
+    segs2, _, _ = segments([{"seq": 0, "mono_ns": 5}] + samples[:4])
+    assert segs2 == [(samples[0]["mono_ns"] - dt_ns, samples[3]["mono_ns"])]
+
+
 def test_cli_dmon_rows_and_counter_bursts(mock_exporter):
     """`kgs dmon` against a live (mock) exporter: one row per GPU per poll, rates
     from counter deltas, and min/max MFMA from the full-rate /counters stream."""
@@ -119,6 +146,7 @@ def test_cli_dmon_rows_and_counter_bursts(mock_exporter):
         assert r["drains"] >= 100                                    # ≈200 drains per 0.2 s at 1 kHz
         assert 55 <= r["mfma_min"] <= r["mfma_max"] <= 65             # mock: MFMA busy 60 % of active cycles
         assert [55 <= float(x) <= 65 for x in r["xcd_mfma"].split("/")] == [True] * 8  # per-XCD split
+        assert 15 <= r["duty"] <= 85 and r["bursts"] is not None     # mock GPU active 50 ± 30 %
     buf = io.StringIO()
     a = dmon.build_parser().parse_args([f"http://127.0.0.1:{ex.port}", "--interval", "0.1", "--count", "2"])
     dmon.run(a, out=buf)

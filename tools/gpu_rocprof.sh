@@ -14,7 +14,7 @@ python3 -m kube_gpu_stats_amd.cli exporter --listen 127.0.0.1:19400 --hz 8000 --
 EXP=$!
 for i in $(seq 60); do grep -q '"event": "ready"' "$OUT/exporter.out" 2>/dev/null && break; sleep 1; done
 if ! grep -q '"event": "ready"' "$OUT/exporter.out"; then echo "exporter not ready"; kill $EXP; exit 1; fi
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 bench.py --steps 6 --warmup 2 \
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 bench.py --steps 6 --warmup 2 \
   --step-ms 150 --rounds 8 --attach 127.0.0.1:19400 --out "$OUT/bench_rocprof.json" > "$OUT/bench.log" 2>&1
 RC=$?
 kill $EXP; wait $EXP 2>/dev/null
@@ -22,6 +22,8 @@ echo "rocprof rc=$RC"
 if [ $RC -ne 0 ]; then tail -20 "$OUT/bench.log"; exit $RC; fi
 python3 tools/rocprof_overhead.py "$OUT/trace" "$OUT/bench_rocprof.json" --out "$OUT/rocprof_overhead.md" > "$OUT/split.json"
 RC=$?
-find "$OUT/trace" -name '*kernel_trace.csv' -delete
+# keep only the per-kernel statistics: the trace itself is hundreds of MB, and
+# gpurun copies nothing back once gpurun_out/ passes 64 MiB
+find "$OUT/trace" -type f ! -name '*stats.csv' -delete
 cat "$OUT/rocprof_overhead.md"
 exit $RC
