@@ -18,6 +18,12 @@ packets would cost the workload time) repeated until the step lasts ≥ --step-m
   A  K steps, no exporter process                       (baseline)
   B  K steps, node exporter sampling every GPU at --hz (PMFW table, HBM, per-process
      list, xGMI, hardware counters) and scraped at --scrape-hz      (THE timed region)
+  R  untimed: a train of ~1 ms MFMA bursts every 5 ms on every GPU, read back from the
+     exporter's full-rate /counters stream — how many bursts the primary rate resolves
+     (``burst_resolution``)
+  Q  untimed: every GPU idle; the exporter's READ rate, the PMFW GFX busy and the
+     SPI-busy share it reports, in the default adaptive mode and in profiling mode
+     (``quiet_gpu``) — the cost of sampling that GPU-time overhead cannot show
   I  --rounds rounds of one block per condition — exporter paused, then each rate of
      --hz-list — in alternating order (off,100,8k | 8k,100,off | ...), --block-steps
      steps per block, scraped while sampling.  Per round, overhead = t_on/t_off − 1;
@@ -74,7 +80,7 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-pipeline", type=int, default=1, choices=[0, 1],
                     help="aqlprofile reader: pipelined READs (1) or submit-and-wait per sample (0)")
     ap.add_argument("--pmc-set", default="base", choices=["base", "full"],
-                    help="counter set: base (GRBM + MFMA busy) or full (+ TA busy, 10x the CP register reads)")
+                    help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register reads)")
     ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=20.0)
@@ -99,6 +105,13 @@ def parse_args(argv=None):
     ap.add_argument("--train-vocab", type=int, default=32768)
     ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per unit when N > 1 (0 = off)")
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
+    ap.add_argument("--burst-s", type=float, default=0.6,
+                    help="phase R: length of the MFMA burst train read back from /counters (0 = off; the "
+                    "full-rate ring holds ≈1 s at 8 kHz)")
+    ap.add_argument("--burst-ms", type=float, default=1.0, help="phase R: length of one burst")
+    ap.add_argument("--burst-period-ms", type=float, default=5.0, help="phase R: burst period")
+    ap.add_argument("--quiet-s", type=float, default=1.5,
+                    help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
     ap.add_argument("--mock-step-ms", type=float, default=20.0, help="mock: duration of one load unit")
     ap.add_argument("--mock-latency", type=int, default=1, choices=[0, 1],
@@ -224,6 +237,14 @@ class GpuLoad(Load):
     def sync(self):
         self.torch.cuda.synchronize()
 
+    def burst(self, ms: float) -> None:
+        """One MFMA kernel of ≈``ms`` milliseconds, waited for (phase R)."""
+        from kube_gpu_stats_amd.ops import load as L
+
+        iters = max(50, int(self.ls.mfma_iters * ms / max(self.mfma_ms, 1e-3)))
+        L.mfma_bf16(self.ls.A, self.ls.B, self.ls.C, self.ls.mfma_blocks, iters)
+        self.torch.cuda.synchronize()
+
     def calibrate(self) -> dict:
         """Per-kernel throughput (events), outside every timed region."""
         torch = self.torch
@@ -238,6 +259,7 @@ class GpuLoad(Load):
         e[3].record()
         torch.cuda.synchronize()
         mfma_s = e[0].elapsed_time(e[1]) * 1e-3
+        self.mfma_ms = mfma_s * 1e3
         tri_s = e[1].elapsed_time(e[2]) * 1e-3
         out = {"mfma_ms": mfma_s * 1e3, "mfma_tflops": self.ls.flops / mfma_s / 1e12,
                "triad_ms": tri_s * 1e3, "triad_tbps": self.ls.bytes / tri_s / 1e12}
@@ -314,6 +336,8 @@ class TrainLoad(GpuLoad):
         self.tok = torch.randint(0, self.vocab, (self.batch, self.seq + 1), device=dev, generator=g)
         self.F = F
 
+    burst = None  # phase R runs on the synthetic load only
+
     def unit(self):
         logits = self.model(self.tok[:, :-1])
         loss = self.F.cross_entropy(logits.float().view(-1, self.vocab), self.tok[:, 1:].reshape(-1))
@@ -341,6 +365,9 @@ class MockLoad(Load):
 
     def unit(self):
         time.sleep(self.dt)  # releases the GIL like a GPU sync would
+
+    def burst(self, ms: float) -> None:
+        time.sleep(ms * 1e-3)  # plumbing only: the mock counters do not follow the host
 
     def sync(self):
         pass
@@ -373,6 +400,9 @@ class AttachedExporter:
 
     def set_rate(self, hz: float):
         self.sc.get(f"/control/rate?hz={hz:g}")
+
+    def set_idle_hz(self, hz: float) -> float:
+        return json.loads(self.sc.get(f"/control/pmc/idle?hz={hz:g}")).get("pmc_idle_hz", 0.0)
 
     def stop(self) -> dict:
         self.pause()
@@ -419,6 +449,9 @@ class ExporterProc:
 
     def set_rate(self, hz: float):
         self.sc.get(f"/control/rate?hz={hz:g}")
+
+    def set_idle_hz(self, hz: float) -> float:
+        return json.loads(self.sc.get(f"/control/pmc/idle?hz={hz:g}")).get("pmc_idle_hz", 0.0)
 
     def _wait_ready(self, timeout: float) -> dict:
         end = time.time() + timeout
@@ -661,6 +694,102 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
     return out
 
 
+def burst_train(ctx, load, exp, a) -> dict:
+    """Phase R — what the primary rate resolves ("the headline value is a
+    dial").  Every rank fires a train of ≈``--burst-ms`` MFMA kernels, one every
+    ``--burst-period-ms``, for ``--burst-s``; the node exporter keeps sampling at the
+    primary rate.  Rank 0 then reads each GPU's full-rate ``/counters`` stream and
+    counts busy segments (reports/dmon.py ``segments``): at 8 kHz every launched
+    burst is its own segment and the busy integral matches the host's duty cycle,
+    where the ≈50 Hz PMFW table only sees the average.  Untimed; not in any overhead."""
+    if a.burst_s <= 0 or getattr(load, "burst", None) is None:
+        return {}
+    idle_hz = exp.set_idle_hz(-1) if exp is not None else 0.0  # hz < 0 only reads the setting
+    if exp is not None:
+        exp.set_idle_hz(0)  # profiling mode: READ every tick
+    D.barrier(ctx)
+    period = a.burst_period_ms * 1e-3
+    bursts: list[tuple[int, int]] = []
+    nxt = time.monotonic()
+    t_end = nxt + a.burst_s
+    while time.monotonic() < t_end:
+        t0 = time.monotonic_ns()
+        load.burst(a.burst_ms)
+        bursts.append((t0, time.monotonic_ns()))
+        nxt += period
+        d = nxt - time.monotonic()
+        if d > 0:
+            time.sleep(d)
+    everyone = D.all_gather_object(ctx, (load.pci_bdf(ctx.local_rank), bursts))
+    if exp is None:
+        return {}
+    exp.set_idle_hz(idle_hz)
+    import urllib.request
+
+    from kube_gpu_stats_amd.reports.dmon import segments
+
+    base = f"http://127.0.0.1:{exp.port}"
+    gpu_of = {d["bdf"]: str(d["gpu"]) for d in json.load(urllib.request.urlopen(base + "/devices", timeout=10))}
+    per: dict[str, dict] = {}
+    for bdf, bs in everyone:
+        g = gpu_of.get(bdf)
+        if g is None or not bs:
+            continue
+        body = json.load(urllib.request.urlopen(f"{base}/counters?gpu={g}&n=8190", timeout=10))
+        lo, hi = bs[0][0] - 2_000_000, bs[-1][1] + 2_000_000
+        win = [x for x in body.get("samples", []) if lo <= x["mono_ns"] <= hi]
+        segs, busy, span = segments(win)
+        med = lambda xs: sorted(xs)[len(xs) // 2] * 1e-6 if xs else None  # noqa: E731
+        per[g] = {"launched": len(bs), "segments": len(segs), "drains": len(win),
+                  "drains_per_s": round(len(win) / span, 1) if span else None,
+                  "covered_s": round(span, 4),
+                  "median_burst_ms_host": med([e - s for s, e in bs]),
+                  "median_segment_ms": med([e - s for s, e in segs]),
+                  "duty_host": round(sum(e - s for s, e in bs) * 1e-9 / span, 4) if span else None,
+                  "duty_counters": round(busy / span, 4) if span else None}
+    return {"burst_ms": a.burst_ms, "period_ms": a.burst_period_ms, "train_s": a.burst_s,
+            "mode": "profiling (--pmc-idle-hz 0: every tick READs)", "mock": bool(a.mock), "per_gpu": per}
+
+
+def quiet_gpu(ctx, exp, a) -> dict:
+    """Phase Q — what the exporter does to an idle GPU (untimed).  Every counter READ
+    is a command-processor packet that the PMFW GFX busy — the source of
+    container_gpu_sm_util — counts as ≈80 µs of work, so a GPU READ every tick at
+    8 kHz reads ~99 % busy while idle.  With the GPU idle on every rank, rank 0
+    reads from the exporter's own counters, per GPU: the READ rate, the PMFW GFX
+    busy (exact, from amdgpu_gfx_busy_seconds_total) and the SPI-busy share of
+    clocks, first in the default adaptive mode (a quiet GPU is READ at
+    --pmc-idle-hz) and then in profiling mode (every tick) for contrast."""
+    if a.quiet_s <= 0:
+        return {}
+    D.barrier(ctx)
+    out: dict = {}
+    if exp is not None:
+        default_idle = exp.set_idle_hz(-1)  # hz < 0 only reads the setting
+        for mode, hz in (("adaptive", default_idle), ("profiling", 0.0)):
+            exp.set_idle_hz(hz)
+            time.sleep(0.2)
+            m0, t0 = parse_text(exp.sc.get()), time.perf_counter()
+            time.sleep(a.quiet_s)
+            m1, dt = parse_text(exp.sc.get()), time.perf_counter() - t0
+            fam = lambda m, n, **kw: {lb["gpu"]: v for lb, v in m.get(n, [])  # noqa: E731
+                                      if all(lb.get(k) == w for k, w in kw.items())}
+            r0, r1 = fam(m0, "kgs_pmc_samples_total"), fam(m1, "kgs_pmc_samples_total")
+            g0, g1 = fam(m0, "amdgpu_gfx_busy_seconds_total"), fam(m1, "amdgpu_gfx_busy_seconds_total")
+            c0, c1 = fam(m0, "amdgpu_pmc_total", counter="GRBM_COUNT"), fam(m1, "amdgpu_pmc_total", counter="GRBM_COUNT")
+            s0, s1 = (fam(m0, "amdgpu_pmc_total", counter="GRBM_SPI_BUSY"),
+                      fam(m1, "amdgpu_pmc_total", counter="GRBM_SPI_BUSY"))
+            out[mode] = {"pmc_idle_hz": hz, "per_gpu": {
+                g: {"reads_per_s": round((r1[g] - r0.get(g, 0)) / dt, 1),
+                    "pmfw_gfx_busy_pct": round(100 * (g1.get(g, 0) - g0.get(g, 0)) / dt, 3),
+                    "gpu_active_pct": (round(100 * (s1[g] - s0.get(g, 0)) / (c1[g] - c0.get(g, 0)), 3)
+                                       if g in s1 and g in c1 and c1[g] > c0.get(g, 0) else None)}
+                for g in sorted(r1, key=int)}}
+        exp.set_idle_hz(default_idle)
+    D.barrier(ctx)
+    return out
+
+
 def run(a, ctx) -> dict | None:
     n = ctx.world
     hzs = tiers(a)
@@ -735,6 +864,8 @@ def run(a, ctx) -> dict | None:
         win = time.perf_counter() - w0
         cpu1, thr1 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
 
+    resolution = burst_train(ctx, load, exp, a)
+    quiet = quiet_gpu(ctx, exp, a)
     inter = interleaved(ctx, load, exp, a, hzs)
     stopped = exp.stop() if exp is not None else {}
 
@@ -807,6 +938,8 @@ def run(a, ctx) -> dict | None:
         "t_on_s": t_b,
         "t_off_c_s": t_c,
         "interleaved": inter,
+        "burst_resolution": resolution,
+        "quiet_gpu": quiet,
         "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
         "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / win, 4) for k, v in thr1.items()
                                          if win > 0 and v - thr0.get(k, 0.0) > 0.005 * win},

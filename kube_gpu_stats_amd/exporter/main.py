@@ -69,6 +69,10 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                         "stopped or reprogrammed them; 0 = never, SIGUSR1 hand-over disables it)")
     add_flag(ap, "pmc-refresh-s", 60.0, "re-START (reprogram) the counters this often, in case another profiler "
                                         "changed their selects (0 = never; SIGUSR1 hand-over disables it)")
+    add_flag(ap, "pmc-idle-hz", 100.0, "counter READ rate while the GPU has no wave in flight: every READ is a "
+                                       "command-processor packet that GFX busy / GUI-active count as work (≈80 / "
+                                       "190 µs each), so a quiet GPU is read at this rate and a busy one every tick "
+                                       "(0 = every tick: profiling mode)")
     add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
     add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
     add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
@@ -115,6 +119,7 @@ def config_from_args(a) -> dict:
         "pmc_lean": a.pmc_lean,
         "pmc_reclaim_s": a.pmc_reclaim_s,
         "pmc_refresh_s": a.pmc_refresh_s,
+        "pmc_idle_hz": a.pmc_idle_hz,
         "listen_addr": host or "0.0.0.0",
         "port": int(port),
         "node_name": a.node_name,

@@ -107,7 +107,8 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_mfma_busy_seconds_total", "counter",
       "∫ MFMA-busy share of all SIMD cycles dt (per drain: ΔSQ_VALU_MFMA_BUSY_CYCLES / (SIMDs·ΔGRBM_COUNT) · Δt); "
       "rate() = matrix-core utilisation of wall time.", source="rocprofiler", tier="pmc"),
-    F("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active % of clocks (window).", source="rocprofiler", tier="pmc"),
+    F("amdgpu_gpu_active_percent", "gauge", "% of clocks a shader engine had waves to run (GRBM_SPI_BUSY, window); "
+      "unlike the PMFW GFX busy it does not count the exporter's own counter READs.", source="rocprofiler", tier="pmc"),
     F("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy % of active cycles (window).",
       source="rocprofiler", tier="pmc"),
     F("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT (window).",
@@ -121,8 +122,8 @@ CATALOG: tuple[Family, ...] = (
       "Vector-memory address unit (TA) busy % of one XCD's active cycles, mean over its CUs (window; --pmc-set full).",
       extra=("xcc",), source="rocprofiler", tier="pmc"),
     F("amdgpu_gpu_active_xcc_percent", "gauge",
-      "GRBM GUI-active % of clocks of one XCD (window): a dispatch is in flight on it.  A chip-wide kernel keeps "
-      "every XCD active, even one with no waves; the MFMA split shows where waves run.",
+      "GRBM SPI-busy % of clocks of one XCD (window): one of its shader engines has waves to run.  Unlike GUI-active "
+      "(which reads ~100 % on every XCD while any chip-wide dispatch is in flight) it shows where waves run.",
       extra=("xcc",), source="rocprofiler", tier="pmc"),
     # ---- per process -------------------------------------------------------------------------
     F("amdgpu_process_hbm_bytes", "gauge", "HBM bytes held by a process.",
@@ -155,6 +156,10 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_reclaims_total", "counter", "Automatic counter re-STARTs after a stall of --pmc-reclaim-s.", source="self"),
     F("kgs_pmc_refreshes_total", "counter", "Periodic counter re-STARTs (--pmc-refresh-s): reprogram selects that "
       "another profiler may have changed without stalling GRBM_COUNT.", source="self"),
+    F("kgs_pmc_quiet", "gauge", "1 while the last counter READ interval saw no wave and no MFMA cycle: READs drop to "
+      "--pmc-idle-hz so the exporter's own packets do not read as GPU activity.", source="self"),
+    F("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU.",
+      source="self"),
     F("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples.", source="self"),
     F("kgs_slow_reads_total", "counter",
       "Management-library reads by the node-wide slow thread (tier=procs: process list; tier=links: xGMI link "

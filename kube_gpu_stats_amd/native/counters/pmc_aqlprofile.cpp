@@ -60,6 +60,7 @@ struct Sel {
 const Sel kGfx950[] = {
     {"GRBM_COUNT", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, "GRBM", 0},
     {"GRBM_GUI_ACTIVE", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, "GRBM", 2},
+    {"GRBM_SPI_BUSY", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, "GRBM", 11},
     {"SQ_BUSY_CYCLES", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, "SQ", 3},
     {"SQ_WAVES", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, "SQ", 4},
     {"SQ_VALU_MFMA_BUSY_CYCLES", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, "SQ", 93},
@@ -106,6 +107,8 @@ struct Agent {
   void* pout[2] = {nullptr, nullptr};
   hsa_ext_amd_aql_pm4_packet_t pread[2]{};
   hsa_signal_t psig[2]{};
+  uint32_t pcmd_sz = 0, pout_sz = 0;                 // allocated sizes of the slot buffers
+  std::vector<hsa_ven_amd_aqlprofile_event_t> pipe_events;  // event list the slot packets were built for
   int64_t psubmit_ns[2] = {0, 0};
   int inflight = -1;                                 // slot with a READ on the queue, -1 none
   int64_t rtt_ns = 0;                                // CP round trip of a synchronous READ (EWMA)
@@ -435,7 +438,9 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
 // dispatch-bound workload on the same GPU (profiles/launch_overhead.md).
 // Modes: 0 = aqlprofile's packets as built; 1 = CS_PARTIAL_FLUSH → NOP;
 // 2 (default) = 1 + ACQUIRE_MEM reduced to the L2 writeback that publishes the
-// CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Returns packets changed.
+// CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Cost-attribution modes
+// (KGS_AQL_LEAN only; the counter values they return are stale): 4 = 3 + no
+// COPY_DATA, 5 = every packet of the IB a NOP.  Returns packets changed.
 int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
   if (mode <= 0) return 0;
   uint32_t dw[4];
@@ -451,13 +456,18 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
     if ((h >> 30) == 2) { ++i; continue; }
     if ((h >> 30) != 3) return -2;
     const uint32_t opc = (h >> 8) & 0xFF, len = ((h >> 16) & 0x3FFF) + 2;
-    if (opc == 0x46 && (ib[i + 1] & 0x3F) == 7) {  // EVENT_WRITE CS_PARTIAL_FLUSH
+    if (mode >= 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
+      if (opc != 0x10) {
+        nop(i, len);
+        ++changed;
+      }
+    } else if (opc == 0x46 && (ib[i + 1] & 0x3F) == 7) {  // EVENT_WRITE CS_PARTIAL_FLUSH
       nop(i, len);
       ++changed;
     } else if (opc == 0x58 && mode == 2) {         // ACQUIRE_MEM: keep TC_WB_ACTION_ENA only
       ib[i + 1] &= (1u << 18);
       ++changed;
-    } else if (opc == 0x58 && mode == 3) {
+    } else if (opc == 0x58 && mode >= 3) {
       nop(i, len);
       ++changed;
     }
@@ -478,7 +488,7 @@ int lean_mode() {
 // output order, XCC-major — a counter's i-th of m results sits on XCD
 // i·num_xcc/m.  On MI355X / ROCm 7.2 the coordinate reads XCD 0 for all 48
 // results, and the buffer holds 8 XCC-major groups of [GRBM_COUNT,
-// GRBM_GUI_ACTIVE, SQ MFMA busy × 4 SEs]; an MFMA load gated on HW_REG_XCC_ID
+// GRBM_GUI_ACTIVE (now GRBM_SPI_BUSY), SQ MFMA busy × 4 SEs]; an MFMA load gated on HW_REG_XCC_ID
 // to XCDs {0, 2} shows up on exactly those two under the order placement
 // (profiles/r1/xcd/README.md, tests/test_gpu.py::test_per_xcd_counters_follow_xcc_gated_load).
 void place_xcds(Agent* a) {
@@ -575,16 +585,31 @@ int read_pipelined(Agent* a, int64_t* ts) {
   return rc;
 }
 
-// Second READ slot for pipelined mode: same events, own buffers and signal.
-// Only its READ packet is ever submitted (START/STOP come from the main profile).
+bool same_events(const std::vector<hsa_ven_amd_aqlprofile_event_t>& x,
+                 const std::vector<hsa_ven_amd_aqlprofile_event_t>& y) {
+  if (x.size() != y.size()) return false;
+  for (size_t i = 0; i < x.size(); ++i)
+    if (x[i].block_name != y[i].block_name || x[i].block_index != y[i].block_index || x[i].counter_id != y[i].counter_id)
+      return false;
+  return true;
+}
+
+// Two READ slots for pipelined mode: the session's events, own buffers and
+// signals.  Only their READ packets are ever submitted (START/STOP come from the
+// main profile).  Called again when a re-open changed the event list: the slot
+// packets of the previous list would otherwise be folded against the new one.
 bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err) {
   for (int k = 0; k < 2; ++k) {
     hsa_ven_amd_aqlprofile_profile_t& p = a->pprof[k];
     p = a->prof;
-    a->pcmd[k] = host_alloc(a, cmd_sz);
-    a->pout[k] = host_alloc(a, out_sz);
-    const hsa_status_t sc = poll_signals() ? hsa_amd_signal_create(1, 1, &a->agent, 0, &a->psig[k])
-                                           : hsa_signal_create(1, 0, nullptr, &a->psig[k]);
+    if (a->pcmd[k] && a->pcmd_sz < cmd_sz) { hsa_amd_memory_pool_free(a->pcmd[k]); a->pcmd[k] = nullptr; }
+    if (a->pout[k] && a->pout_sz < out_sz) { hsa_amd_memory_pool_free(a->pout[k]); a->pout[k] = nullptr; }
+    if (!a->pcmd[k]) a->pcmd[k] = host_alloc(a, cmd_sz);
+    if (!a->pout[k]) a->pout[k] = host_alloc(a, out_sz);
+    hsa_status_t sc = HSA_STATUS_SUCCESS;
+    if (!a->psig[k].handle)
+      sc = poll_signals() ? hsa_amd_signal_create(1, 1, &a->agent, 0, &a->psig[k])
+                          : hsa_signal_create(1, 0, nullptr, &a->psig[k]);
     if (!a->pcmd[k] || !a->pout[k] || sc != HSA_STATUS_SUCCESS) {
       err = "pipeline buffer allocation failed";
       return false;
@@ -600,6 +625,9 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
     }
     if (lean_mode() > 0) lean_read_ib(a->pread[k], lean_mode());
   }
+  a->pcmd_sz = std::max(a->pcmd_sz, cmd_sz);
+  a->pout_sz = std::max(a->pout_sz, out_sz);
+  a->pipe_events = a->events;
   return true;
 }
 
@@ -659,6 +687,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     }
     a->names.assign(names, names + n);
     a->reduce.assign(is_max, is_max + n);
+    const std::vector<hsa_ven_amd_aqlprofile_event_t> prev_events = a->events;
     a->events.clear();
     a->ev_counter.clear();
     a->per_cu.assign(static_cast<size_t>(n), 0);
@@ -708,12 +737,15 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       }
     }
     // A re-open rebuilt a->events: the pipelined READ slots of the previous session
-    // (reused, same event list) must point at the new array.
+    // must point at the new array (same list: a hand-over / refresh re-START), or
+    // be rebuilt by the next kgs_pmc_set_pipelined (another list).
     for (int k = 0; k < 2; ++k)
       if (a->pcmd[k]) {
         a->pprof[k].events = a->events.data();
         a->pprof[k].event_count = static_cast<uint32_t>(a->events.size());
       }
+    if (a->pcmd[0] && !same_events(a->pipe_events, a->events)) a->pipelined = false;
+    if (!same_events(prev_events, a->events)) a->res_xcd_done = false;  // result layout changed: place XCDs again
     hsa_ven_amd_aqlprofile_profile_t& p = a->prof;
     p = hsa_ven_amd_aqlprofile_profile_t{};
     p.agent = a->agent;
@@ -852,7 +884,7 @@ int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
     wait_done(a, a->psig[a->inflight], 1000000000ull);
     a->inflight = -1;
   }
-  if (on && !a->pcmd[0]) {
+  if (on && (!a->pcmd[0] || !same_events(a->pipe_events, a->events))) {
     std::string e;
     if (!setup_pipeline(a, a->cmd_sz, a->out_sz, e)) {
       set_err(err, errlen, e);

@@ -27,7 +27,7 @@ namespace kgs {
 // Index of each base counter inside PmcSample::value.
 enum PmcIndex : int {
   kPmcGrbmCount = 0,      // GRBM_COUNT (max over XCC): free-running GPU clocks
-  kPmcGrbmGuiActive = 1,  // GRBM_GUI_ACTIVE (max over XCC): clocks the GPU had work
+  kPmcGrbmActive = 1,     // GRBM_SPI_BUSY (max over XCC): clocks a shader engine had waves to run
   kPmcMfmaBusy = 2,       // SQ_VALU_MFMA_BUSY_CYCLES (sum over SIMDs)
   kPmcTaBusy = 3,         // TA_TA_BUSY (mean over TA instances): vector-memory address unit busy cycles
   kPmcCount = 4,
@@ -47,7 +47,21 @@ int pmc_counter_reduce(int idx);
 // (profiles/launch_overhead.md): the TA block alone is 512 instance reads of
 // the 560 in `full`, so the default `base` set drops it and keeps the READ to
 // 48 register reads (GRBM × 8 XCC, MFMA busy × 32 SE).
-constexpr uint32_t kPmcSetBase = (1u << kPmcGrbmCount) | (1u << kPmcGrbmGuiActive) | (1u << kPmcMfmaBusy);
+//
+// Activity is GRBM_SPI_BUSY, not GRBM_GUI_ACTIVE.  GUI-active — like the PMFW
+// GFX-activity accumulator behind amdgpu_gfx_busy_percent — counts the graphics
+// pipe busy while ANY packet is in flight, our own READs included: on an idle
+// MI355X every READ reads as ≈190 µs of GUI-active and ≈80 µs of PMFW GFX busy,
+// whatever the packet holds (even an IB of NOPs), so an idle GPU sampled at
+// 8 kHz reads ~99 % active (profiles/r2/idle_busy/).  SPI busy needs waves: it
+// reads 0.65 % under 8 kHz of READs alone and 95 % under an MFMA load, for
+// queues created before or after the counters started.  (SQ_BUSY_CYCLES /
+// SQ_WAVES read 0 for other processes' kernels in device mode, and the SPI
+// block's own wave counter misses queues that predate the session;
+// profiles/r2/immunity/.)  GRBM has two counter slots per XCC, so SPI busy
+// takes GUI-active's.  It is also the sampler's READ-immune activity test for
+// the adaptive READ rate (SamplerConfig::pmc_idle_hz).
+constexpr uint32_t kPmcSetBase = (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcMfmaBusy);
 constexpr uint32_t kPmcSetFull = kPmcSetBase | (1u << kPmcTaBusy);
 // "base" | "full" → mask; 0 for an unknown name.
 uint32_t pmc_set_mask(const std::string& name);
@@ -55,9 +69,9 @@ uint32_t pmc_set_mask(const std::string& name);
 // Derived quantities over an interval between two cumulative samples.
 struct PmcRates {
   bool have_vmem = false;        // TA counter in the set
-  double gpu_active_pct = 0;     // 100 * ΔGUI_ACTIVE / ΔGRBM_COUNT
-  double mfma_util_pct = 0;      // 100 * ΔMFMA_BUSY / (ΔGUI_ACTIVE * SIMD_NUM)  (rocprofv3 MfmaUtil)
-  double vmem_busy_pct = 0;      // 100 * ΔTA_BUSY(avg) / ΔGUI_ACTIVE
+  double gpu_active_pct = 0;     // 100 * ΔSPI_BUSY / ΔGRBM_COUNT (READ-immune)
+  double mfma_util_pct = 0;      // 100 * ΔMFMA_BUSY / (ΔSPI_BUSY * SIMD_NUM)  (rocprofv3 MfmaUtil, per active cycle)
+  double vmem_busy_pct = 0;      // 100 * ΔTA_BUSY(avg) / ΔSPI_BUSY
   double gpu_clock_mhz = 0;      // ΔGRBM_COUNT / Δt
   double dt_s = 0;
   // Per XCD (both samples carry the breakdown): active % of clocks, and MFMA

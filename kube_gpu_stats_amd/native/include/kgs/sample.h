@@ -103,7 +103,7 @@ struct PmcSample {
   // workgroups are dispatched round-robin over them).  n_xcd = 0 when the
   // reader could not place its results on XCDs.  Cumulative like value[].
   uint32_t n_xcd = 0;
-  uint64_t xcd_active[kMaxXcc] = {};  // GRBM_GUI_ACTIVE of each XCD
+  uint64_t xcd_active[kMaxXcc] = {};  // GRBM_SPI_BUSY of each XCD
   uint64_t xcd_mfma[kMaxXcc] = {};    // SQ_VALU_MFMA_BUSY_CYCLES summed over each XCD's SEs
   uint64_t xcd_ta[kMaxXcc] = {};      // TA_TA_BUSY summed over each XCD's TA instances (full set; 0 otherwise)
 };

@@ -54,6 +54,17 @@ struct SamplerConfig {
   // r45: MFMA util 0 under load).  Nothing in the READ shows that, so the session
   // is also re-STARTed (selects reprogrammed) every pmc_refresh_s (0 = never).
   double pmc_refresh_s = 60.0;
+  // Adaptive READ rate.  Every counter READ is a packet on the command processor
+  // that GUI-active and the PMFW GFX busy (container_gpu_sm_util's source) count
+  // as ≈190 / ≈80 µs of work: at 8 kHz an idle GPU reads ~99 % busy
+  // (profiles/r2/idle_busy/).  While the last READ interval had waves for less
+  // than kQuietActiveFrac of its clocks and no MFMA cycle (GRBM_SPI_BUSY and
+  // MFMA busy, both blind to READs), the device is "quiet" and READs drop to
+  // pmc_idle_hz; the first READ that sees work puts it back on every tick.
+  // Cumulative counters keep every integral exact; only the time resolution of
+  // idle stretches drops.  0 = READ every tick (profiling mode: full resolution,
+  // and the PMFW GFX busy reads the READs as work).
+  double pmc_idle_hz = 100.0;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
 };
@@ -67,6 +78,8 @@ constexpr int64_t kPmcSlowNs = 5000000;  // 5 ms → ≥10 s of history
 constexpr int kReadHistBuckets = 12;    // backend read latency histogram
 constexpr int64_t kPmcStallNs = 500000000;  // GRBM_COUNT without a plausible clock this long = stalled
 constexpr double kPlausibleMhzLo = 100.0, kPlausibleMhzHi = 4000.0;
+// Adaptive READ rate: an interval whose SPI-busy share is below this is quiet.
+constexpr double kQuietActiveFrac = 0.02;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 
 struct DeviceState {
@@ -97,6 +110,8 @@ struct DeviceState {
   std::atomic<int> pmc_stalled{0};          // counters frozen / implausible for ≥ kPmcStallNs
   std::atomic<uint64_t> pmc_reclaims{0};    // automatic re-STARTs after a stall
   std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
+  std::atomic<int> pmc_quiet{0};            // last READ interval had no wave: READs at pmc_idle_hz
+  std::atomic<uint64_t> pmc_quiet_skips{0};  // ticks that skipped their READ while quiet
   PmcSample pmc_base;  // totals carried over hand-overs (sampler thread only; survives pause/resume)
   // Last distinct PMFW sample (sampler thread only).  Kept across pause/resume:
   // the firmware accumulators keep counting while the thread is stopped, so the
@@ -145,6 +160,9 @@ class Sampler {
   void set_pmc_wanted(bool on);
   // Change the tick rate (stops and restarts the threads; integrals continue).
   void set_hz(double hz);
+  // Quiet-GPU counter READ rate (SamplerConfig::pmc_idle_hz), in place.
+  void set_pmc_idle_hz(double hz) { pmc_idle_hz_.store(hz < 0 ? 0 : hz, std::memory_order_relaxed); }
+  double pmc_idle_hz() const { return pmc_idle_hz_.load(std::memory_order_relaxed); }
   // Node-wide slow thread: passes completed and whether it is running.
   uint64_t slow_passes() const { return slow_passes_.load(); }
 
@@ -161,6 +179,7 @@ class Sampler {
   std::vector<std::thread> threads_;
   std::thread slow_thread_;
   std::atomic<uint64_t> slow_passes_{0};
+  std::atomic<double> pmc_idle_hz_{0.0};
   // Per-device process CU-occupancy integrals (slow thread only; survive pause/resume).
   std::vector<std::vector<std::pair<uint32_t, double>>> cu_seconds_;
   std::vector<int64_t> last_proc_ns_;

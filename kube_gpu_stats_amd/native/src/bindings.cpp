@@ -62,6 +62,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.max_backoff_ms = get<int>(d, "max_backoff_ms", c.sampler.max_backoff_ms);
   c.sampler.pmc_reclaim_s = get<double>(d, "pmc_reclaim_s", c.sampler.pmc_reclaim_s);
   c.sampler.pmc_refresh_s = get<double>(d, "pmc_refresh_s", c.sampler.pmc_refresh_s);
+  c.sampler.pmc_idle_hz = get<double>(d, "pmc_idle_hz", c.sampler.pmc_idle_hz);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
   c.bdfs = get<std::vector<std::string>>(d, "bdfs", c.bdfs);
   c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);
@@ -160,6 +161,7 @@ class PyExporter {
     py::gil_scoped_release r;
     ex_.start();
   }
+  Sampler* sampler() const { return ex_.sampler(); }
   void stop() {
     py::gil_scoped_release r;
     ex_.stop();
@@ -223,6 +225,8 @@ class PyExporter {
     o["proc_reads"] = st.proc_reads.load();
     o["link_reads"] = st.link_reads.load();
     o["slow_read_seconds"] = st.slow_ns_total.load() * 1e-9;
+    o["pmc_quiet"] = st.pmc_quiet.load();
+    o["pmc_quiet_skips"] = st.pmc_quiet_skips.load();
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
     return o;
@@ -420,6 +424,12 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("set_sample_rate", &PyExporter::set_sample_rate, py::arg("hz"),
            "Change the sampler tick rate in place (threads restart; integrals continue)")
       .def_property_readonly("sample_rate", &PyExporter::sample_rate)
+      .def_property(
+          "pmc_idle_hz", [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_idle_hz() : 0.0; },
+          [](PyExporter& e, double hz) {
+            if (e.sampler()) e.sampler()->set_pmc_idle_hz(hz);
+          },
+          "Counter READ rate while the GPU has no wave (adaptive; 0 = every tick)")
       .def_property_readonly("slow_passes", &PyExporter::slow_passes);
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);

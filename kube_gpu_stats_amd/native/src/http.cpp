@@ -303,6 +303,13 @@ void HttpServer::loop() {
         } else if (target == "/control/pmc/release" || target == "/control/pmc/acquire") {
           ex_->set_pmc_enabled(target == "/control/pmc/acquire");
           respond(c, 200, "OK", "application/json", ex_->pmc_enabled() ? "{\"pmc\":true}" : "{\"pmc\":false}");
+        } else if (target == "/control/pmc/idle") {
+          // Quiet-GPU counter READ rate (--pmc-idle-hz); hz=0 = READ every tick (profiling mode).
+          Sampler* s = ex_->sampler();
+          const double hz = query_double(query, "hz", -1.0);
+          if (s && hz >= 0) s->set_pmc_idle_hz(hz);
+          respond(c, 200, "OK", "application/json",
+                  "{\"pmc_idle_hz\":" + std::to_string(s ? s->pmc_idle_hz() : 0.0) + "}");
         } else if (ex_->config().control_http && (target == "/control/pause" || target == "/control/resume")) {
           if (target == "/control/pause") ex_->pause_sampling();
           else ex_->resume_sampling();

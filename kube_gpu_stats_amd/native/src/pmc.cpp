@@ -14,7 +14,7 @@ namespace kgs {
 
 namespace {
 const char* const kNames[kPmcCount] = {
-    "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY",
+    "GRBM_COUNT", "GRBM_SPI_BUSY", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY",
 };
 const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg};
 
@@ -42,13 +42,16 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
   auto d = [&](int i) {
     return b.value[i] >= a.value[i] ? static_cast<double>(b.value[i] - a.value[i]) : 0.0;
   };
-  const double cnt = d(kPmcGrbmCount), act = d(kPmcGrbmGuiActive);
+  const double cnt = d(kPmcGrbmCount), act = d(kPmcGrbmActive);
   const double cu = num_cu > 0 ? num_cu : 256;
   if (cnt > 0) r.gpu_active_pct = 100.0 * act / cnt;
   r.have_vmem = (a.mask & b.mask & (1u << kPmcTaBusy)) != 0;
   if (act > 0) {
-    r.mfma_util_pct = 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0);
-    if (r.have_vmem) r.vmem_busy_pct = 100.0 * d(kPmcTaBusy) / act;
+    // Shares of the active (SPI-busy) cycles, capped: over a single ~125 µs drain a
+    // kernel's tail can leave MFMA / TA cycles in an interval whose SPI-busy count
+    // is a few hundred clocks.
+    r.mfma_util_pct = std::min(100.0, 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0));
+    if (r.have_vmem) r.vmem_busy_pct = std::min(100.0, 100.0 * d(kPmcTaBusy) / act);
   }
   r.gpu_clock_mhz = cnt / dt * 1e-6;
   const uint32_t nx = std::min(a.n_xcd, b.n_xcd);
@@ -59,14 +62,14 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
       const double ax = b.xcd_active[x] >= a.xcd_active[x] ? static_cast<double>(b.xcd_active[x] - a.xcd_active[x]) : 0.0;
       const double mx = b.xcd_mfma[x] >= a.xcd_mfma[x] ? static_cast<double>(b.xcd_mfma[x] - a.xcd_mfma[x]) : 0.0;
       if (cnt > 0) r.xcd_active_pct[x] = 100.0 * ax / cnt;
-      if (ax > 0) r.xcd_mfma_util_pct[x] = 100.0 * mx / (ax * simds);
+      if (ax > 0) r.xcd_mfma_util_pct[x] = std::min(100.0, 100.0 * mx / (ax * simds));
     }
     r.have_xcd_vmem = r.have_vmem;
     if (r.have_xcd_vmem)
       for (uint32_t x = 0; x < nx; ++x) {
         const double ax = b.xcd_active[x] >= a.xcd_active[x] ? static_cast<double>(b.xcd_active[x] - a.xcd_active[x]) : 0.0;
         const double tx = b.xcd_ta[x] >= a.xcd_ta[x] ? static_cast<double>(b.xcd_ta[x] - a.xcd_ta[x]) : 0.0;
-        if (ax > 0) r.xcd_vmem_busy_pct[x] = 100.0 * tx / (cu / nx) / ax;
+        if (ax > 0) r.xcd_vmem_busy_pct[x] = std::min(100.0, 100.0 * tx / (cu / nx) / ax);
       }
   }
   return r;
@@ -115,7 +118,7 @@ class MockCounterSource final : public CounterSource {
     const double clk = c_.clock_mhz * 1e6;
     s.n = kPmcCount;
     s.value[kPmcGrbmCount] = static_cast<uint64_t>(clk * t);
-    s.value[kPmcGrbmGuiActive] = static_cast<uint64_t>(clk * busy_s);
+    s.value[kPmcGrbmActive] = static_cast<uint64_t>(clk * busy_s);
     s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
     s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac);
     s.mask = c_.mask;
@@ -272,8 +275,8 @@ class DlCounterSource final : public CounterSource {
     s.n = kPmcCount;
     s.read_ns = rns;
     s.n_xcd = 0;
-    if (sample_xcd_ && reader_idx_[kPmcGrbmGuiActive] >= 0 && reader_idx_[kPmcMfmaBusy] >= 0) {
-      const int na = sample_xcd_(handles_[dev], reader_idx_[kPmcGrbmGuiActive], s.xcd_active, kMaxXcc);
+    if (sample_xcd_ && reader_idx_[kPmcGrbmActive] >= 0 && reader_idx_[kPmcMfmaBusy] >= 0) {
+      const int na = sample_xcd_(handles_[dev], reader_idx_[kPmcGrbmActive], s.xcd_active, kMaxXcc);
       const int nm = sample_xcd_(handles_[dev], reader_idx_[kPmcMfmaBusy], s.xcd_mfma, kMaxXcc);
       if (na > 0 && na == nm) s.n_xcd = static_cast<uint32_t>(na);
       if (s.n_xcd > 0 && reader_idx_[kPmcTaBusy] >= 0 &&

@@ -487,7 +487,9 @@ void Exporter::render(std::string& out) {
     for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);
     w.head("amdgpu_mfma_util_percent", "gauge", "Matrix-core (MFMA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
-    w.head("amdgpu_gpu_active_percent", "gauge", "GRBM GUI-active percent of clocks over the window");
+    w.head("amdgpu_gpu_active_percent", "gauge",
+           "Percent of clocks a shader engine had waves to run (GRBM_SPI_BUSY) over the window; unlike the PMFW GFX busy "
+           "it does not count the exporter's own counter READs");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
     w.head("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_vmem) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
@@ -603,6 +605,12 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_reclaims_total", dev_labels_[d], nullptr, S.state(d).pmc_reclaims.load());
     w.head("kgs_pmc_refreshes_total", "counter", "Periodic counter re-STARTs that reprogram the selects (--pmc-refresh-s)");
     for (int d : ids) w.line_u("kgs_pmc_refreshes_total", dev_labels_[d], nullptr, S.state(d).pmc_refreshes.load());
+    w.head("kgs_pmc_quiet", "gauge",
+           "1 while the last counter READ interval saw no wave and no MFMA cycle: READs run at --pmc-idle-hz, so the "
+           "exporter's own command-processor packets do not read as GPU activity");
+    for (int d : ids) w.line_u("kgs_pmc_quiet", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_quiet.load()));
+    w.head("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU");
+    for (int d : ids) w.line_u("kgs_pmc_quiet_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_quiet_skips.load());
   }
   w.head("kgs_slow_reads_total", "counter",
          "Management-library reads by the node-wide slow thread (per-process list / xGMI link table + RAS)");

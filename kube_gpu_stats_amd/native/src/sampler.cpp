@@ -81,6 +81,7 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
       if (d >= 0 && d < n) dev_ids_.push_back(d);
   }
   if (cfg_.hz <= 0) cfg_.hz = 1;
+  pmc_idle_hz_.store(cfg_.pmc_idle_hz < 0 ? 0 : cfg_.pmc_idle_hz);
   for (int d : dev_ids_) states_[static_cast<size_t>(d)]->pmc_on.store(cfg_.pmc && pmc_ ? 1 : 0);
   cu_seconds_.resize(static_cast<size_t>(n));
   last_proc_ns_.assign(static_cast<size_t>(n), 0);
@@ -215,7 +216,9 @@ void Sampler::run(int dev) {
   PmcSample& pmc_base = st.pmc_base;
   int64_t last_acquire_fail_ns = 0;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
-  uint64_t prev_ps_count = 0, prev_ps_mfma = 0;
+  uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0;
+  bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
+  int64_t last_pmc_ns = 0;
   int64_t prev_ps_ns = 0;
   int64_t last_plausible_ns = mono_ns();
   int64_t last_start_ns = mono_ns();  // last (re)START of the counter session
@@ -300,6 +303,7 @@ void Sampler::run(int dev) {
           if (pmc_->acquire(dev) == 0) {
             st.pmc_on.store(1);
             have_prev_ps = false;
+            quiet = false;
             last_plausible_ns = now_c;
             last_start_ns = now_c;
           } else {
@@ -310,9 +314,17 @@ void Sampler::run(int dev) {
       }
       pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
     }
+    if (pmc_now && quiet) {
+      const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
+      if (idle_hz > 0 && idle_hz < cfg_.hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / idle_hz)) {
+        pmc_now = false;
+        st.pmc_quiet_skips.fetch_add(1, std::memory_order_relaxed);
+      }
+    }
     if (pmc_now) {
       PmcSample ps;
       const int64_t p0 = mono_ns();
+      last_pmc_ns = p0;
       const int prc = pmc_->sample(dev, ps);
       I.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
       if (prc == 0) {
@@ -331,8 +343,21 @@ void Sampler::run(int dev) {
                               (simds * static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count));
           I.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
         }
+        // Quiet = a shader engine had waves for < kQuietActiveFrac of the clocks
+        // since the previous READ, and no MFMA cycle ran.  Both counters are
+        // (nearly) blind to our own READs: SPI busy reads 0.65 % with nothing but
+        // 8 kHz of READs on the GPU (profiles/r2/immunity/).
+        if (have_prev_ps && ps.value[kPmcGrbmCount] > prev_ps_count) {
+          const double act = static_cast<double>(ps.value[kPmcGrbmActive] - std::min(ps.value[kPmcGrbmActive], prev_ps_active));
+          const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
+          quiet = act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma;
+        } else {
+          quiet = false;
+        }
+        st.pmc_quiet.store(quiet ? 1 : 0, std::memory_order_relaxed);
         prev_ps_count = ps.value[kPmcGrbmCount];
         prev_ps_mfma = ps.value[kPmcMfmaBusy];
+        prev_ps_active = ps.value[kPmcGrbmActive];
         prev_ps_ns = ps.mono_ns;
         have_prev_ps = true;
         const int64_t stall = ps.mono_ns - last_plausible_ns;
@@ -369,6 +394,7 @@ void Sampler::run(int dev) {
             ++I.pmc_errors;
           }
           have_prev_ps = false;
+          quiet = false;
           last_plausible_ns = mono_ns();  // a full reclaim period before the next one
         }
       } else {

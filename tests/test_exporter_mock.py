@@ -210,7 +210,7 @@ def test_counter_stream_endpoint_is_gapless(mock_exporter):
                        mock={"util_base": 50, "util_amp": 0.0001})
     time.sleep(0.3)
     body = json.load(get(ex.port, "/counters?gpu=0&n=50"))
-    assert body["counters"][:3] == ["GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"]
+    assert body["counters"][:3] == ["GRBM_COUNT", "GRBM_SPI_BUSY", "SQ_VALU_MFMA_BUSY_CYCLES"]
     s = body["samples"]
     assert len(s) == 50
     seqs = [x["seq"] for x in s]
@@ -246,12 +246,12 @@ def test_counter_window_covers_full_window_at_high_rate(mock_exporter):
 
 
 def test_pmc_counter_sets(N, mock_exporter):
-    """base set (default): GRBM + MFMA busy only — no TA, so no vmem gauge; full adds TA."""
+    """base set (default): GRBM clocks + SPI busy + MFMA busy — no TA, so no vmem gauge; full adds TA."""
     base = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0)
     full = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0, pmc_set="full")
     time.sleep(0.4)
     mb, mf = parse_text(base.render()), parse_text(full.render())
-    assert {lb["counter"] for lb, _ in mb["amdgpu_pmc_total"]} == {"GRBM_COUNT", "GRBM_GUI_ACTIVE",
+    assert {lb["counter"] for lb, _ in mb["amdgpu_pmc_total"]} == {"GRBM_COUNT", "GRBM_SPI_BUSY",
                                                                    "SQ_VALU_MFMA_BUSY_CYCLES"}
     assert "TA_TA_BUSY" in {lb["counter"] for lb, _ in mf["amdgpu_pmc_total"]}
     assert "amdgpu_vmem_busy_percent" not in mb and abs(mf["amdgpu_vmem_busy_percent"][0][1] - 30) < 3
@@ -533,3 +533,39 @@ def test_rocprofiler_reader_is_test_only():
                         "--listen", "127.0.0.1:0", "--pmc", "rocprofiler"],
                        cwd=REPO, capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 2 and "test-only" in r.stdout
+
+
+def test_quiet_gpu_counter_reads_drop_to_idle_rate(mock_exporter):
+    """Adaptive READ rate (profiles/r2/idle_busy/): every counter READ is a packet the
+    GPU's busy gauges count as work, so while the READ-immune SPI-busy / MFMA counters
+    show nothing the sampler READs at pmc_idle_hz, and on every tick again as soon
+    as work shows up.  Integrals stay exact: the duty cycle of a square load is
+    read the same with or without the idle rate."""
+    def rate(ex, secs=1.0):
+        n0 = ex.integrals(0)["pmc_samples"]
+        time.sleep(secs)
+        return (ex.integrals(0)["pmc_samples"] - n0) / secs
+
+    idle = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=50,
+                         mock={"util_base": 0, "util_amp": 0})
+    time.sleep(0.2)
+    r_idle = rate(idle)
+    m = parse_text(idle.render())
+    assert 30 <= r_idle <= 80, r_idle                       # ≈ pmc_idle_hz, not 2000
+    assert m["kgs_pmc_quiet"][0][1] == 1 and m["kgs_pmc_quiet_skips_total"][0][1] > 1000
+    idle.pmc_idle_hz = 0                                   # profiling mode: every tick
+    time.sleep(0.05)
+    assert rate(idle, 0.5) > 1400                          # (2000 less timer slack on a shared CPU)
+    assert json.load(get(idle.port, "/control/pmc/idle?hz=25"))["pmc_idle_hz"] == 25
+    time.sleep(0.05)
+    assert 10 <= rate(idle, 1.0) <= 45
+    idle.stop()
+
+    # square load: 100 % for 0.1 s of every 0.4 s → every tick while busy, idle rate otherwise
+    sq = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=50,
+                       window_s=1.2, mock={"square_duty": 0.25, "util_period_s": 0.4, "util_base": 50, "util_amp": 50})
+    time.sleep(0.3)
+    r_sq = rate(sq, 1.2)
+    assert 0.25 * 2000 * 0.6 <= r_sq <= 0.25 * 2000 + 0.75 * 50 + 150, r_sq
+    w = sq.window(0, 1.2)
+    assert w["gpu_active_pct"] == pytest.approx(25, abs=4), w      # the integral is exact at any READ rate

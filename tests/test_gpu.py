@@ -479,6 +479,11 @@ def test_hbm_bandwidth_estimate_tracks_stream_kernels(N, torch_dev):
     assert idle_est < 0.05e12, idle_est
 
 
+# Exporter flags for a profiling session: every tick READs the counters, idle or not
+# (the default READs a quiet GPU at --pmc-idle-hz only).
+PROFILING_MODE = ["--pmc-idle-hz", "0"]
+
+
 def _bdf0():
     import torch
 
@@ -634,9 +639,12 @@ def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
 def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
     """What the 8 kHz counter tier buys ("the headline value is a
     dial"): a 200 Hz train of ~1 ms MFMA bursts — far inside one ≈20 ms PMFW table
-    period — is resolved burst by burst by the exporter's full-rate /counters stream
-    (one segment per launched burst, burst length and duty cycle as the host timed
-    them), while every PMFW table of the same interval only sees their average."""
+    period — is resolved burst by burst by the exporter's full-rate /counters stream:
+    one GPU-active segment per launched burst, burst length and duty cycle as the
+    host timed them.  GPU-active (GRBM_SPI_BUSY: a shader engine has waves) is
+    READ-immune; the PMFW GFX busy counts every counter READ on the command
+    processor as ≈80 µs of work, so at 8 kHz in profiling mode it reads the gaps
+    between bursts as busy (profiles/r2/idle_busy/)."""
     import urllib.request
 
     import torch
@@ -658,7 +666,8 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
     torch.cuda.synchronize()
     iters = max(200, int(4000 * 1.0 / e0.elapsed_time(e1)))  # ≈1 ms per burst
     cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz", "8000",
-           "--pmc", "aqlprofile", "--control-stdin", "--bdfs", _bdf0(), "--proc-every", "0", "--link-every", "0"]
+           "--pmc", "aqlprofile", "--control-stdin", "--bdfs", _bdf0(), "--proc-every", "0", "--link-every", "0",
+           *PROFILING_MODE]
     proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                             text=True)
     try:
@@ -693,27 +702,96 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
             proc.communicate()
     lo, hi = bursts[0][0] - 2_000_000, bursts[-1][1] + 2_000_000
     win = [x for x in cnt if lo <= x["mono_ns"] <= hi]
-    segs, busy, span = segments(win)
-    host_len = sorted(b - a for a, b in bursts)[len(bursts) // 2] * 1e-6
-    seg_len = sorted(e - s for s, e in segs)[len(segs) // 2] * 1e-6 if segs else 0.0
+    segs, busy, span = segments(win, key="gpu_active_pct")
+    med = lambda xs: sorted(xs)[len(xs) // 2] * 1e-6 if xs else 0.0  # noqa: E731
+    host_len, seg_len = med([b - a for a, b in bursts]), med([e - s for s, e in segs])
     host_duty = sum(b - a for a, b in bursts) * 1e-9 / span if span else 0.0
-    act = [x["gpu_active_pct"] for x in win if "gpu_active_pct" in x]
-    # PMFW tables published while the burst train ran (host wall clock)
+    sh = [x["gpu_active_pct"] for x in win if "gpu_active_pct" in x]
     pm_in = [s["gfx_busy_window_pct"] for s in pm if w0 + 25_000_000 <= s["wall_ns"] <= w1]
     summary = {"bursts_launched": len(bursts), "iters": iters, "drains_in_window": len(win),
                "drain_rate_hz": len(win) / span if span else 0, "segments": len(segs),
                "median_burst_ms_host": host_len, "median_segment_ms_counters": seg_len,
-               "duty_counters": busy / span if span else 0, "duty_host": host_duty,
-               "active_pct_min": min(act), "active_pct_max": max(act),
+               "duty_host": host_duty, "duty_counters": busy / span if span else 0,
+               "gpu_active_pct_min_max": [min(sh), max(sh)] if sh else None,
+               "mfma_pct_max": max((x.get("mfma_util_pct", 0) for x in win), default=None),
                "pmfw_tables_in_window": len(pm_in), "pmfw_gfx_busy_pct": pm_in,
-               "first_50ms_active_pct": [[round((x["mono_ns"] - lo) * 1e-6, 3), round(x["gpu_active_pct"], 1)]
-                                         for x in win if x["mono_ns"] - lo <= 52_000_000 and "gpu_active_pct" in x]}
+               "first_50ms": [[round((x["mono_ns"] - lo) * 1e-6, 3), round(x["gpu_active_pct"], 1),
+                               round(x.get("mfma_util_pct", 0), 1)]
+                              for x in win if x["mono_ns"] - lo <= 52_000_000 and "gpu_active_pct" in x]}
     _keep("burst_resolution.json", json.dumps(summary, indent=1))
-    print(json.dumps({k: v for k, v in summary.items() if k != "first_50ms_active_pct"}))
+    print(json.dumps({k: v for k, v in summary.items() if k != "first_50ms"}))
     assert summary["drain_rate_hz"] > 7000, summary
     assert abs(len(segs) - len(bursts)) <= max(3, 0.05 * len(bursts)), summary
     assert abs(seg_len - host_len) < 0.35 * host_len + 0.25, summary  # ±2 drains of 125 µs + launch/sync jitter
-    assert min(act) < 5 and max(act) > 90, summary
+    assert min(sh) < 5 and max(sh) > 90, summary
     assert abs(summary["duty_counters"] - host_duty) < 0.08, summary
     assert len(pm_in) >= 10, summary                  # ≈50 tables/s
-    assert max(pm_in) < 70, summary                   # every table averages bursts with gaps
+    assert min(pm_in) > 70, summary                   # profiling mode: PMFW reads the READs as work
+
+
+def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
+    """Every counter READ is a command-processor packet that the PMFW GFX busy (the
+    source of container_gpu_sm_util) counts as ≈80 µs of work: READ every tick at
+    8 kHz and an idle MI355X reads ~99 % busy.  By default the sampler READs a quiet
+    GPU — SPI busy < 2 % and no MFMA cycle in the last interval, both READ-immune —
+    at --pmc-idle-hz (100 Hz), so the idle GPU reads <1 % busy, and a load still
+    gets every tick."""
+    import urllib.request
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    import torch
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
+    ls.run_mfma()
+    torch.cuda.synchronize()
+    proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
+                             "--hz", "8000", "--pmc", "aqlprofile", "--control-stdin", "--bdfs", _bdf0(),
+                             "--proc-every", "0", "--link-every", "0", "--window", "1.5"],
+                            cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
+        sc = Scraper("127.0.0.1", ready["port"])
+        ctl = f"http://127.0.0.1:{ready['port']}/control/pmc/idle"
+        one = lambda m, f: m[f][0][1] if m.get(f) else None  # noqa: E731
+        rows = {}
+        for mode, hz in (("adaptive", 100), ("profiling", 0)):
+            urllib.request.urlopen(f"{ctl}?hz={hz}", timeout=5).read()
+            time.sleep(0.3)
+            n0 = one(parse_text(sc.get()), "kgs_pmc_samples_total")
+            time.sleep(1.8)  # idle: this process launches nothing
+            m = parse_text(sc.get())
+            rows[mode] = {"reads_per_s": (one(m, "kgs_pmc_samples_total") - n0) / 1.8,
+                          "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent"),
+                          "gpu_active_pct": one(m, "amdgpu_gpu_active_percent"),
+                          "quiet": one(m, "kgs_pmc_quiet")}
+        urllib.request.urlopen(f"{ctl}?hz=100", timeout=5).read()
+        n0 = one(parse_text(sc.get()), "kgs_pmc_samples_total")
+        t0 = time.time()
+        while time.time() - t0 < 1.6:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+        m = parse_text(sc.get())
+        rows["mfma_load"] = {"reads_per_s": (one(m, "kgs_pmc_samples_total") - n0) / (time.time() - t0),
+                             "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent"),
+                             "gpu_active_pct": one(m, "amdgpu_gpu_active_percent"),
+                             "mfma_util_pct": one(m, "amdgpu_mfma_util_percent"), "quiet": one(m, "kgs_pmc_quiet")}
+    finally:
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            proc.communicate()
+    _keep("idle_gpu_not_busy.json", json.dumps(rows, indent=1))
+    print(json.dumps(rows))
+    a, p, ld = rows["adaptive"], rows["profiling"], rows["mfma_load"]
+    assert a["quiet"] == 1 and 60 <= a["reads_per_s"] <= 140, a
+    assert a["pmfw_gfx_busy_pct"] < 2 and a["gpu_active_pct"] < 1, a
+    assert p["reads_per_s"] > 7000 and p["pmfw_gfx_busy_pct"] > 80, p   # the effect the idle rate removes
+    assert p["gpu_active_pct"] < 2, p                                    # ... which SPI busy does not see
+    assert ld["reads_per_s"] > 7000 and ld["quiet"] == 0, ld              # a loaded GPU gets every tick
+    assert ld["gpu_active_pct"] > 80 and ld["mfma_util_pct"] > 50, ld

@@ -14,11 +14,12 @@ def test_rocprof_overhead_splits_by_condition(tmp_path):
     import rocprof_overhead as R
 
     res = {"steps": 3, "warmup": 1, "config": {"units_per_step": 2},
+           "burst_resolution": {"per_gpu": {"0": {"launched": 4}}},
            "interleaved": {"block_steps": 1, "block_seconds": [["0", 1], ["100", 1], ["8000", 1],
                                                                ["8000", 1], ["100", 1], ["0", 1]]}}
     tiny, triads = 3, 2
     dur = {"A_off": 100, "B_on_8k": 102, "C_off": 100, "I_paused": 100, "I_100Hz": 100, "I_8000Hz": 101,
-           "calib": 50, "calib_reps": 50, "warmup": 50}
+           "calib": 50, "calib_reps": 50, "warmup": 50, "R_bursts": 1}
     rows, t = [], 0
 
     def launch(name, d):
@@ -39,9 +40,11 @@ def test_rocprof_overhead_splits_by_condition(tmp_path):
     for _ in range(tiny):
         launch("copy_f32_kernel(...)", 50)
     launch("elementwise_kernel<torch>", 7)      # foreign kernels are ignored
-    for label, units in R.segments(res, triads, tiny):
+    for label, units, extra in R.segments(res, triads, tiny):
         for _ in range(units):
             unit(dur[label])
+        for _ in range(extra.get("mfma", 0)):      # phase R: bare MFMA bursts
+            launch("mfma_bf16_kernel(...)", dur[label] * 1000)
     d = tmp_path / "trace" / "host" / "123"
     d.mkdir(parents=True)
     with open(d / "run_kernel_trace.csv", "w", newline="") as f:

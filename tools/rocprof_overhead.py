@@ -8,7 +8,8 @@ bench.py launches, per rank, in this order (``load`` units: one
 
 * ``calibrate()``: 1 mfma, 1 triad, 1 graph replay (after 1 eager warm-up copy);
 * ``calibrate_reps()``: 2 units;
-* warm-up W steps, A K steps, B K steps, the interleaved blocks in
+* warm-up W steps, A K steps, B K steps, the phase-R burst train (MFMA kernels
+  only, ``burst_resolution.per_gpu.*.launched``), the interleaved blocks in
   ``interleaved.block_seconds`` order (``block_steps`` steps each), C K steps —
   every step ``config.units_per_step`` units.
 
@@ -32,15 +33,19 @@ def find_trace(d: str) -> str:
     return c[-1]
 
 
-def segments(res: dict, triads: int, tiny: int) -> list[tuple[str, int]]:
-    """(label, units) in launch order after the calibration launches."""
+def segments(res: dict, triads: int, tiny: int) -> list[tuple[str, int, dict]]:
+    """(label, units, extra launches per kernel kind) in launch order after the
+    calibration launches."""
     reps = res["config"]["units_per_step"]
     k, w = res["steps"], res["warmup"]
     inter = res.get("interleaved") or {}
     bs = inter.get("block_steps", 0)
-    seg = [("calib_reps", 2), ("warmup", w * reps), ("A_off", k * reps), ("B_on_8k", k * reps)]
-    seg += [(f"I_{'paused' if c == '0' else c + 'Hz'}", bs * reps) for c, _ in inter.get("block_seconds", [])]
-    seg += [("C_off", k * reps)]
+    bursts = max((g.get("launched", 0) for g in ((res.get("burst_resolution") or {}).get("per_gpu") or {}).values()),
+                 default=0)
+    seg = [("calib_reps", 2, {}), ("warmup", w * reps, {}), ("A_off", k * reps, {}), ("B_on_8k", k * reps, {}),
+           ("R_bursts", 0, {"mfma": bursts})]
+    seg += [(f"I_{'paused' if c == '0' else c + 'Hz'}", bs * reps, {}) for c, _ in inter.get("block_seconds", [])]
+    seg += [("C_off", k * reps, {})]
     return seg
 
 
@@ -76,8 +81,8 @@ def main():
             continue
         i = calib[kind]
         groups: dict[str, list[float]] = {}
-        for label, units in seg:
-            n = units * per_unit[kind]
+        for label, units, extra in seg:
+            n = units * per_unit[kind] + extra.get(kind, 0)
             key = label if not label.startswith("I_") else label
             groups.setdefault(key, []).extend(xs[i:i + n])
             i += n
