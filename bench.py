@@ -751,7 +751,7 @@ def burst_train(ctx, load, exp, a) -> dict:
             "mode": "profiling (--pmc-idle-hz 0: every tick READs)", "mock": bool(a.mock), "per_gpu": per}
 
 
-def quiet_gpu(ctx, exp, a) -> dict:
+def quiet_gpu(ctx, load, exp, a) -> dict:
     """Phase Q — what the exporter does to an idle GPU (untimed).  Every counter READ
     is a command-processor packet that the PMFW GFX busy — the source of
     container_gpu_sm_util — counts as ≈80 µs of work, so a GPU READ every tick at
@@ -763,6 +763,7 @@ def quiet_gpu(ctx, exp, a) -> dict:
     if a.quiet_s <= 0:
         return {}
     D.barrier(ctx)
+    load.sync()  # the barrier's own kernel is done: every GPU is idle from here
     out: dict = {}
     if exp is not None:
         default_idle = exp.set_idle_hz(-1)  # hz < 0 only reads the setting
@@ -786,7 +787,7 @@ def quiet_gpu(ctx, exp, a) -> dict:
                                        if g in s1 and g in c1 and c1[g] > c0.get(g, 0) else None)}
                 for g in sorted(r1, key=int)}}
         exp.set_idle_hz(default_idle)
-    D.barrier(ctx)
+    D.cpu_barrier(ctx)  # the other ranks wait here without a spinning RCCL kernel on their GPUs
     return out
 
 
@@ -865,7 +866,7 @@ def run(a, ctx) -> dict | None:
         cpu1, thr1 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
 
     resolution = burst_train(ctx, load, exp, a)
-    quiet = quiet_gpu(ctx, exp, a)
+    quiet = quiet_gpu(ctx, load, exp, a)
     inter = interleaved(ctx, load, exp, a, hzs)
     stopped = exp.stop() if exp is not None else {}
 

@@ -19,6 +19,7 @@ class Ctx:
     local_world: int = 1
     backend: str = ""
     cuda: bool = False
+    cpu_group: object = None  # gloo group: waits that must not put a kernel on the GPU
 
     @property
     def is_dist(self) -> bool:
@@ -40,6 +41,10 @@ def init_from_env(use_cuda: bool) -> Ctx:
             torch.cuda.set_device(local_rank)
             ctx.backend = "nccl"  # RCCL over xGMI on ROCm
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            # An RCCL barrier is a kernel that spins on every GPU until the last rank
+            # arrives: a rank waiting on it is not idle.  Waits that must leave the
+            # GPUs idle (bench phase Q) go through a CPU-only gloo group.
+            ctx.cpu_group = dist.new_group(backend="gloo")
         else:
             ctx.backend = "gloo"
             dist.init_process_group("gloo")
@@ -60,6 +65,14 @@ def barrier(ctx: Ctx) -> None:
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier()
+
+
+def cpu_barrier(ctx: Ctx) -> None:
+    """Barrier that launches nothing on the GPU (gloo over TCP)."""
+    if ctx.is_dist:
+        import torch.distributed as dist
+
+        dist.barrier(group=ctx.cpu_group) if ctx.cpu_group is not None else dist.barrier()
 
 
 def all_reduce(ctx: Ctx, values: list[float], op: str = "max") -> list[float]:
