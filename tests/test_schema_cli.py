@@ -152,3 +152,35 @@ def test_cli_dmon_rows_and_counter_bursts(mock_exporter):
     dmon.run(a, out=buf)
     lines = buf.getvalue().splitlines()
     assert lines[0].split()[:4] == ["GPU", "POD", "GFX%", "MFMA%"] and len(lines) == 1 + 2 * 2
+
+
+def test_cli_record_chrome_trace(mock_exporter, tmp_path):
+    """`kgs record`: drain the full-rate /counters stream of every GPU into a Chrome
+    trace (counter tracks + busy segments); no drain is lost at 1 kHz with 100 ms polls,
+    and --profiling switches the exporter to READ every tick only for the capture."""
+    from kube_gpu_stats_amd.reports import record
+
+    ex = mock_exporter(n_gpus=2, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=50,
+                       mock={"square_duty": 0.5, "util_period_s": 0.2, "util_base": 50, "util_amp": 50})
+    time.sleep(0.3)
+    out = tmp_path / "t.json"
+    a = record.build_parser().parse_args([f"127.0.0.1:{ex.port}", "--seconds", "1.0", "--poll-ms", "100",
+                                          "--profiling", "--out", str(out)])
+    import io
+
+    buf = io.StringIO()
+    assert record.run(a, out=buf) == 0
+    res = json.loads(buf.getvalue())
+    assert ex.pmc_idle_hz == 50                                    # restored after the capture
+    for g in ("0", "1"):
+        s = res["gpus"][g]
+        assert s["lost"] == 0 and s["drains"] >= 700, s            # every tick, square load or not
+        assert 35 <= s["duty_pct"] <= 65 and 3 <= s["busy_segments"] <= 7, s  # 0.1 s on / 0.1 s off
+    tr = json.loads(out.read_text())
+    ev = tr["traceEvents"]
+    names = {e["args"]["name"] for e in ev if e["ph"] == "M" and e["name"] == "process_name"}
+    assert names == {"GPU 0 (0000:11:00.0)", "GPU 1 (0000:21:00.0)"}
+    assert sum(1 for e in ev if e["ph"] == "C" and e["name"] == "GPU active %" and e["pid"] == 0) == \
+        res["gpus"]["0"]["drains"]
+    busy = [e for e in ev if e["ph"] == "X" and e["pid"] == 0]
+    assert busy and all(80_000 <= e["dur"] <= 120_000 for e in busy[1:-1])   # µs: 0.1 s blocks
