@@ -347,7 +347,8 @@ void Sampler::run(int dev) {
         // since the previous READ, and no MFMA cycle ran.  Both counters are
         // (nearly) blind to our own READs: SPI busy reads 0.65 % with nothing but
         // 8 kHz of READs on the GPU (profiles/r2/immunity/).
-        if (have_prev_ps && ps.value[kPmcGrbmCount] > prev_ps_count) {
+        // Without the activity counter in the set a device is never quiet.
+        if (have_prev_ps && (ps.mask & (1u << kPmcGrbmActive)) && ps.value[kPmcGrbmCount] > prev_ps_count) {
           const double act = static_cast<double>(ps.value[kPmcGrbmActive] - std::min(ps.value[kPmcGrbmActive], prev_ps_active));
           const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
           quiet = act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma;
