@@ -86,6 +86,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pin-numa", True, "pin each sampler thread to its GPU's NUMA node")
     add_flag(ap, "per-process", True, "export per-process HBM/CU metrics")
     add_flag(ap, "compat-unallocated", False, "emit container_gpu_sm_util for GPUs no pod holds")
+    add_flag(ap, "sm-util-source", "pmfw", "what container_gpu_sm_util / container_gpu_busy_seconds_total measure: pmfw "
+                                           "(firmware GFX busy: a dispatch in flight; counts counter READs as work) | "
+                                           "counters (GRBM_SPI_BUSY: waves in a shader engine; READ-immune; needs --pmc)")
     add_flag(ap, "pod-resources-socket", "/var/lib/kubelet/pod-resources/kubelet.sock", "kubelet pod-resources socket")
     add_flag(ap, "static-owners", "", "JSON file mapping device id -> {pod,namespace,container}")
     add_flag(ap, "attribution-interval", 1.0, "attribution refresh period (s)")
@@ -129,6 +132,7 @@ def config_from_args(a) -> dict:
         "hbm_bytes_per_s_at_full_umc": a.hbm_full_bw,
         "per_process": a.per_process,
         "compat_unallocated": a.compat_unallocated,
+        "sm_util_source": a.sm_util_source,
         "control_http": a.control_http,
         "gzip_level": a.gzip_level,
         "bdfs": [b for b in (a.bdfs.split(",") if isinstance(a.bdfs, str) else a.bdfs) if b],
@@ -140,6 +144,11 @@ def run(a) -> int:
     if a.pmc == "rocprofiler" and os.environ.get("KGS_PMC_CROSSCHECK") != "1":
         L.error("--pmc rocprofiler is a test-only cross-check reader (set KGS_PMC_CROSSCHECK=1 in tests)")
         print(json.dumps({"event": "error", "error": "--pmc rocprofiler is test-only"}), flush=True)
+        return 2
+    if a.sm_util_source == "counters" and a.pmc == "none":
+        ap_err = "--sm-util-source counters needs the counter tier (--pmc aqlprofile)"
+        print(json.dumps({"event": "error", "error": ap_err}), flush=True)
+        L.error(ap_err)
         return 2
     if a.pmc not in ("none", "aqlprofile", "mock", "rocprofiler"):
         print(json.dumps({"event": "error", "error": f"unknown --pmc {a.pmc!r}"}), flush=True)

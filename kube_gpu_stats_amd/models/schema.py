@@ -104,6 +104,10 @@ CATALOG: tuple[Family, ...] = (
       source="rocprofiler", tier="pmc"),
     F("amdgpu_mfma_util_percent", "gauge", "Matrix-core busy % of active cycles (window).", source="rocprofiler",
       tier="pmc"),
+    F("amdgpu_gpu_active_seconds_total", "counter",
+      "∫ GPU-active share of clocks dt (per drain: ΔGRBM_SPI_BUSY / ΔGRBM_COUNT · Δt); rate() = GPU-active fraction, "
+      "blind to the exporter's own counter READs (the --sm-util-source counters integral).", source="rocprofiler",
+      tier="pmc"),
     F("amdgpu_mfma_busy_seconds_total", "counter",
       "∫ MFMA-busy share of all SIMD cycles dt (per drain: ΔSQ_VALU_MFMA_BUSY_CYCLES / (SIMDs·ΔGRBM_COUNT) · Δt); "
       "rate() = matrix-core utilisation of wall time.", source="rocprofiler", tier="pmc"),

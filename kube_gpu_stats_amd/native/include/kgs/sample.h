@@ -129,6 +129,9 @@ struct Integrals {
   // ∫ MFMA-busy fraction of wall time dt from the counter stream: per drain,
   // ΔMFMA_BUSY / (SIMDs · ΔGRBM_COUNT) · Δt (all SIMDs busy with MFMA for 1 s = 1).
   double mfma_busy_seconds = 0;
+  // ∫ GPU-active (GRBM_SPI_BUSY share of clocks) dt from the counter stream: the
+  // READ-immune busy integral (--sm-util-source counters).
+  double active_seconds = 0;
 };
 static_assert(std::is_trivially_copyable<Integrals>::value, "seqlock payload");
 

@@ -80,6 +80,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.per_process = get<bool>(d, "per_process", c.per_process);
   c.compat_series = get<bool>(d, "compat_series", c.compat_series);
   c.compat_unallocated = get<bool>(d, "compat_unallocated", c.compat_unallocated);
+  c.sm_util_source = get<std::string>(d, "sm_util_source", c.sm_util_source);
   c.control_http = get<bool>(d, "control_http", c.control_http);
   c.gzip_level = get<int>(d, "gzip_level", c.gzip_level);
   return c;
@@ -221,6 +222,7 @@ class PyExporter {
     o["read_seconds"] = I.read_seconds;
     o["pmc_read_seconds"] = I.pmc_read_seconds;
     o["mfma_busy_seconds"] = I.mfma_busy_seconds;
+    o["active_seconds"] = I.active_seconds;
     const DeviceState& st = ex_.sampler()->state(d);
     o["proc_reads"] = st.proc_reads.load();
     o["link_reads"] = st.link_reads.load();

@@ -48,6 +48,10 @@ Exporter::Exporter(ExporterConfig cfg) : cfg_(std::move(cfg)) {
 Exporter::~Exporter() { stop(); }
 
 bool Exporter::init() {
+  if (cfg_.sm_util_source != "pmfw" && cfg_.sm_util_source != "counters") {
+    err_ = "unknown sm_util_source '" + cfg_.sm_util_source + "' (pmfw | counters)";
+    return false;
+  }
   if (cfg_.backend == "mock") {
     be_ = make_mock_backend(cfg_.mock);
   } else if (cfg_.backend == "amdsmi") {
@@ -160,6 +164,7 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
         if (y.same(x)) kept = &y;
     x.base_busy_s = kept ? kept->base_busy_s : I.gfx_busy_seconds;
     x.base_mfma_s = kept ? kept->base_mfma_s : I.mfma_busy_seconds;
+    x.base_active_s = kept ? kept->base_active_s : I.active_seconds;
   }
   if (o.empty()) m->erase(dev);
   else (*m)[dev] = std::move(o);

@@ -230,20 +230,36 @@ void Exporter::render(std::string& out) {
         emit(nullptr);
       }
     }
-    w.head("container_gpu_sm_util", "gauge",
-           "GFX-engine (compute) busy percent of the GPU allocated to the pod, averaged over the exporter window "
-           "(reference metric contract; label nvidia_gpu_type kept for compatibility)");
-    for (const auto& [d, lb] : pod_lines)
-      if (snaps[static_cast<size_t>(d)].busy) w.line("container_gpu_sm_util", lb, nullptr, snaps[static_cast<size_t>(d)].g);
+    const bool from_counters = cfg_.sm_util_source == "counters";
+    if (from_counters) {
+      w.head("container_gpu_sm_util", "gauge",
+             "GPU-active percent (GRBM_SPI_BUSY: a shader engine has waves) of the GPU allocated to the pod, averaged "
+             "over the exporter window (reference metric contract; --sm-util-source counters)");
+      for (const auto& [d, lb] : pod_lines) {
+        const Snap& x = snaps[static_cast<size_t>(d)];
+        if (x.pmc_rates) w.line("container_gpu_sm_util", lb, nullptr, x.r.gpu_active_pct);
+      }
+    } else {
+      w.head("container_gpu_sm_util", "gauge",
+             "GFX-engine (compute) busy percent of the GPU allocated to the pod, averaged over the exporter window "
+             "(reference metric contract; label nvidia_gpu_type kept for compatibility)");
+      for (const auto& [d, lb] : pod_lines)
+        if (snaps[static_cast<size_t>(d)].busy) w.line("container_gpu_sm_util", lb, nullptr, snaps[static_cast<size_t>(d)].g);
+    }
     // Exact per-pod accounting: the GPU's busy integral since the pod was given
     // it.  rate() / increase() over any range is the exact mean utilisation,
     // whatever the scrape interval — the gauge above only sees its window.
     w.head("container_gpu_busy_seconds_total", "counter",
-           "GFX-engine busy seconds of the GPU allocated to the pod, counted from allocation (PMFW accumulators; "
-           "100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)");
+           from_counters ? "GPU-active seconds (GRBM_SPI_BUSY) of the GPU allocated to the pod, counted from allocation "
+                           "(hardware counters; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)"
+                         : "GFX-engine busy seconds of the GPU allocated to the pod, counted from allocation (PMFW "
+                           "accumulators; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)");
     for (size_t i = 0; i < pod_lines.size(); ++i) {
       const Owner* o = pod_owner[i];
-      const double v = snaps[static_cast<size_t>(pod_lines[i].first)].I.gfx_busy_seconds - (o ? o->base_busy_s : 0.0);
+      const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
+      if (from_counters && !x.pmc_have) continue;
+      const double v = from_counters ? x.I.active_seconds - (o ? o->base_active_s : 0.0)
+                                     : x.I.gfx_busy_seconds - (o ? o->base_busy_s : 0.0);
       w.line("container_gpu_busy_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
     }
     bool any_pmc_int = false;
@@ -482,6 +498,10 @@ void Exporter::render(std::string& out) {
       for (int i = 0; i < kPmcCount; ++i)
         if (x.p.mask & (1u << i)) w.line_u("amdgpu_pmc_total", dev_labels_[d], pmc_counter_labels()[static_cast<size_t>(i)].c_str(), x.p.value[i]);
     }
+    w.head("amdgpu_gpu_active_seconds_total", "counter",
+           "Integral of the GPU-active share of clocks (GRBM_SPI_BUSY, hardware counters) over time; rate() = GPU-active "
+           "fraction, blind to the exporter's own counter READs");
+    for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_gpu_active_seconds_total", dev_labels_[d], nullptr, snaps[d].I.active_seconds);
     w.head("amdgpu_mfma_busy_seconds_total", "counter",
            "Integral of the MFMA-busy share of all SIMD cycles over time (hardware counters); rate() = matrix-core utilisation");
     for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);

@@ -343,6 +343,12 @@ void Sampler::run(int dev) {
                               (simds * static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count));
           I.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
         }
+        if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcGrbmActive)) &&
+            ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcGrbmActive] >= prev_ps_active) {
+          const double frac = static_cast<double>(ps.value[kPmcGrbmActive] - prev_ps_active) /
+                              static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
+          I.active_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
+        }
         // Quiet = a shader engine had waves for < kQuietActiveFrac of the clocks
         // since the previous READ, and no MFMA cycle ran.  Both counters are
         // (nearly) blind to our own READs: SPI busy reads 0.65 % with nothing but

@@ -93,3 +93,23 @@ def test_busy_counter_starts_at_allocation_and_survives_owner_refresh(mock_expor
     ex.set_device_owners(0, [])
     assert "container_gpu_busy_seconds_total" not in parse_text(ex.render()) or \
         not parse_text(ex.render())["container_gpu_busy_seconds_total"]
+
+
+def test_sm_util_from_counters(N, mock_exporter):
+    """--sm-util-source counters: the reference-contract gauge and the per-pod busy
+    counter come from the counter tier's GPU-active (GRBM_SPI_BUSY, blind to the
+    exporter's own READs) instead of the PMFW GFX busy."""
+    ex = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", window_s=0.5, sm_util_source="counters",
+                       mock={"util_base": 60, "util_amp": 0.0001, "fw_period_s": 0.005})
+    time.sleep(0.3)
+    ex.set_device_owners(0, [{"pod": "p", "namespace": "ml", "container": "c"}])
+    time.sleep(0.6)
+    m = parse_text(ex.render())
+    (lb, sm), = m["container_gpu_sm_util"]
+    assert lb["pod_name"] == "p" and sm == pytest.approx(60, abs=3)
+    busy = m["container_gpu_busy_seconds_total"][0][1]
+    assert busy == pytest.approx(0.6 * 0.6, abs=0.08)              # from the allocation, counter integral
+    act = m["amdgpu_gpu_active_seconds_total"][0][1]
+    assert act > busy and act == pytest.approx(ex.integrals(0)["active_seconds"], rel=0.05)
+    with pytest.raises(RuntimeError, match="sm_util_source"):
+        N.Exporter({"backend": "mock", "sm_util_source": "bogus"})
