@@ -797,3 +797,51 @@ def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
     assert p["gpu_active_pct"] < 2, p                                    # ... which SPI busy does not see
     assert ld["reads_per_s"] > 7000 and ld["quiet"] == 0, ld              # a loaded GPU gets every tick
     assert ld["gpu_active_pct"] > 80 and ld["mfma_util_pct"] > 50, ld
+
+
+def test_sm_util_from_counters_follows_load_and_idle(torch_dev, tmp_path):
+    """--sm-util-source counters on MI355X: the reference-contract gauge reads the
+    counter tier's GPU-active (GRBM_SPI_BUSY) — >80 under the MFMA load, ~0 once idle
+    even with counters READ every tick at 8 kHz (where the PMFW GFX busy reads ~99 %)."""
+    import torch
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    bdf = _bdf0()
+    owners = tmp_path / "owners.json"
+    owners.write_text(json.dumps({bdf: {"pod": "train-0", "namespace": "ml", "container": "main"}}))
+    proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
+                             "--hz", "8000", "--pmc", "aqlprofile", *PROFILING_MODE, "--window", "1",
+                             "--sm-util-source", "counters", "--node-name", "gpu-node-1", "--bdfs", bdf,
+                             "--static-owners", str(owners), "--control-stdin", "--pod-resources-socket", "",
+                             "--proc-every", "0", "--link-every", "0"],
+                            cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
+        sc = Scraper("127.0.0.1", ready["port"])
+        ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
+        t0 = time.time()
+        while time.time() - t0 < 1.5:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+        busy = parse_text(sc.get())
+        time.sleep(1.5)
+        idle = parse_text(sc.get())
+    finally:
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            proc.communicate()
+    one = lambda m, f: m[f][0][1] if m.get(f) else None  # noqa: E731
+    row = {k: {"sm_util": one(m, "container_gpu_sm_util"), "busy_s": one(m, "container_gpu_busy_seconds_total"),
+               "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent")} for k, m in (("load", busy), ("idle", idle))}
+    print(json.dumps(row))
+    assert busy["container_gpu_sm_util"][0][0]["pod_name"] == "train-0"
+    assert row["load"]["sm_util"] > 80 and row["load"]["busy_s"] > 1.0, row
+    assert row["idle"]["sm_util"] < 2 and row["idle"]["pmfw_gfx_busy_pct"] > 80, row   # READs fill PMFW, not SPI
+    assert row["idle"]["busy_s"] - row["load"]["busy_s"] < 0.1, row
