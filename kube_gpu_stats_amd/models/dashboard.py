@@ -60,8 +60,10 @@ def build() -> dict:
                  "{{kubernetes_io_hostname}}")], 12, y))
     y += 8
     add(_row(0, "Utilisation", y)); y += 1
-    add(_panel(0, "GFX busy (exact, from PMFW accumulators)",
-               [(_dev("100 * rate(amdgpu_gfx_busy_seconds_total[1m])"), "{{kubernetes_io_hostname}} gpu{{gpu}}")],
+    add(_panel(0, "GFX busy (PMFW) vs GPU-active (waves, READ-immune)",
+               [(_dev("100 * rate(amdgpu_gfx_busy_seconds_total[1m])"), "gfx busy {{kubernetes_io_hostname}} gpu{{gpu}}"),
+                (_dev("100 * rate(amdgpu_gpu_active_seconds_total[1m])"),
+                 "active {{kubernetes_io_hostname}} gpu{{gpu}}")],
                0, y, unit="percent", maxv=100))
     add(_panel(0, "Matrix-core (MFMA) busy",
                [(_dev("amdgpu_mfma_util_percent"), "{{kubernetes_io_hostname}} gpu{{gpu}}")], 12, y, unit="percent",
@@ -104,7 +106,8 @@ def build() -> dict:
     add(_row(0, "Exporter health", y)); y += 1
     add(_panel(0, "Samples / s per GPU (PMFW distinct, counters)",
                [(_dev("rate(kgs_samples_total[1m])"), "pmfw gpu{{gpu}}"),
-                (_dev("rate(kgs_pmc_samples_total[1m])"), "pmc gpu{{gpu}}")], 0, y, w=8))
+                (_dev("rate(kgs_pmc_samples_total[1m])"), "pmc gpu{{gpu}}"),
+                (_dev("kgs_pmc_quiet"), "quiet (idle READ rate) gpu{{gpu}}")], 0, y, w=8))
     add(_panel(0, "Scrape render time", [("kgs_scrape_render_last_seconds", "{{instance}}")], 8, y, w=8, unit="s"))
     add(_panel(0, "Sampler up / recoveries / attribution age",
                [(_dev("kgs_up"), "up gpu{{gpu}}"), (_dev("increase(kgs_device_recoveries_total[1h])"),
