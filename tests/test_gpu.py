@@ -845,3 +845,23 @@ def test_sm_util_from_counters_follows_load_and_idle(torch_dev, tmp_path):
     assert row["load"]["sm_util"] > 80 and row["load"]["busy_s"] > 1.0, row
     assert row["idle"]["sm_util"] < 2 and row["idle"]["pmfw_gfx_busy_pct"] > 80, row   # READs fill PMFW, not SPI
     assert row["idle"]["busy_s"] - row["load"]["busy_s"] < 0.1, row
+
+
+def test_counter_reader_reopen_with_another_event_list(tmp_path):
+    """libkgs_pmc_aql.so built its two pipelined READ slots once per GPU; a second
+    session with a different counter list folded the old packets' output against
+    the new list (GUI-active 0, SPI counters ~1e8; r2k/r2p).  The slots are now
+    rebuilt when the list changes: every session of one process reads sane values."""
+    out = tmp_path / "reopen.json"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "counter_immunity_probe.py"), "--pre-queue",
+                        "--sets", "grbm_spi,spi_first,no_sq", "--out", str(out)],
+                       cwd=REPO, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    sets = json.loads(out.read_text())["sets"]
+    print(json.dumps({k: v.get("phases") for k, v in sets.items()}))
+    for name in ("spi_first", "no_sq"):  # 2nd and 3rd session: other event lists than the first
+        idle = sets[name]["phases"]["idle_after"]
+        assert idle and 0.5 < idle["GRBM_GUI_ACTIVE"] <= 1.01, (name, idle)   # READs keep GUI-active up
+        assert all(0 <= v <= 1.01 for k, v in idle.items() if k not in ("drains", "secs")), (name, idle)
+    load = sets["grbm_spi"]["phases"]["mfma_load"]
+    assert load["GRBM:11"] > 0.8, load                                     # SPI busy sees the pre-existing queue
