@@ -146,9 +146,9 @@ def run(a) -> int:
         print(json.dumps({"event": "error", "error": "--pmc rocprofiler is test-only"}), flush=True)
         return 2
     if a.sm_util_source == "counters" and a.pmc == "none":
-        ap_err = "--sm-util-source counters needs the counter tier (--pmc aqlprofile)"
-        print(json.dumps({"event": "error", "error": ap_err}), flush=True)
-        L.error(ap_err)
+        msg = "--sm-util-source counters needs the counter tier (--pmc aqlprofile)"
+        print(json.dumps({"event": "error", "error": msg}), flush=True)
+        L.error(msg)
         return 2
     if a.pmc not in ("none", "aqlprofile", "mock", "rocprofiler"):
         print(json.dumps({"event": "error", "error": f"unknown --pmc {a.pmc!r}"}), flush=True)

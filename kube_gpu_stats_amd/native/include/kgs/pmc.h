@@ -100,6 +100,11 @@ class CounterSource {
   // unsupported.
   virtual int release(int dev) { return -1; }
   virtual int acquire(int dev) { return -1; }
+  // Quiet device (adaptive READ rate): return values read by this very call
+  // (synchronous READ) instead of those of the READ submitted on the previous
+  // one — at an idle rate of 100 Hz a pipelined sample would be 10 ms old, which
+  // doubles the time to notice that work started.  Sampler thread only.
+  virtual void set_fresh(int dev, bool fresh) {}
 };
 
 struct MockPmcConfig {

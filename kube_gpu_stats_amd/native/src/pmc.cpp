@@ -252,6 +252,12 @@ class DlCounterSource final : public CounterSource {
     std::string e;
     return open_dev(dev, e);
   }
+  void set_fresh(int dev, bool fresh) override {
+    if (!pipelined_ || !set_pipe_ || dev < 0 || dev >= static_cast<int>(handles_.size())) return;
+    const int h = handles_[static_cast<size_t>(dev)];
+    char ebuf[256] = {};
+    if (h >= 0) set_pipe_(h, fresh ? 0 : 1, ebuf, sizeof ebuf);  // a failed switch keeps the current mode
+  }
 
   std::string name() const override { return name_; }
 

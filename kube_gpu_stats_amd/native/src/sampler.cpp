@@ -218,6 +218,7 @@ void Sampler::run(int dev) {
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
   uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0;
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
+  bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
   int64_t last_pmc_ns = 0;
   int64_t prev_ps_ns = 0;
   int64_t last_plausible_ns = mono_ns();
@@ -304,6 +305,7 @@ void Sampler::run(int dev) {
             st.pmc_on.store(1);
             have_prev_ps = false;
             quiet = false;
+            fresh_mode = false;  // a (re)opened session reads pipelined
             last_plausible_ns = now_c;
             last_start_ns = now_c;
           } else {
@@ -362,6 +364,14 @@ void Sampler::run(int dev) {
           quiet = false;
         }
         st.pmc_quiet.store(quiet ? 1 : 0, std::memory_order_relaxed);
+        {
+          const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
+          const bool slow = quiet && idle_hz > 0 && idle_hz < cfg_.hz;
+          if (slow != fresh_mode) {
+            pmc_->set_fresh(dev, slow);
+            fresh_mode = slow;
+          }
+        }
         prev_ps_count = ps.value[kPmcGrbmCount];
         prev_ps_mfma = ps.value[kPmcMfmaBusy];
         prev_ps_active = ps.value[kPmcGrbmActive];
@@ -402,6 +412,7 @@ void Sampler::run(int dev) {
           }
           have_prev_ps = false;
           quiet = false;
+          fresh_mode = false;
           last_plausible_ns = mono_ns();  // a full reclaim period before the next one
         }
       } else {
