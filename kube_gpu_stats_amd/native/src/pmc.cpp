@@ -124,7 +124,7 @@ class MockCounterSource final : public CounterSource {
     s.mask = c_.mask;
     for (int i = 0; i < kPmcCount; ++i)
       if (!(s.mask & (1u << i))) s.value[i] = 0;
-    // XCD x is busy (1 - skew·x) of the time XCD 0 is (GUI_ACTIVE reduces by max
+    // XCD x is busy (1 - skew·x) of the time XCD 0 is (the active counter reduces by max
     // over XCDs, so XCD 0 carries the device value); MFMA cycles split likewise.
     s.n_xcd = static_cast<uint32_t>(std::clamp(c_.n_xcd, 0, kMaxXcc));
     double wsum = 0;

@@ -535,7 +535,7 @@ void Exporter::render(std::string& out) {
               w.line("amdgpu_vmem_busy_xcc_percent", dev_labels_[d], kXccLabels[x], snaps[d].r.xcd_vmem_busy_pct[x]);
       }
       w.head("amdgpu_gpu_active_xcc_percent", "gauge",
-             "GRBM GUI-active percent of clocks of one XCD over the window (a dispatch in flight, not waves resident)");
+             "GRBM SPI-busy percent of clocks of one XCD over the window (one of its shader engines has waves to run)");
       for (int d : ids)
         if (snaps[d].pmc_rates)
           for (int x = 0; x < snaps[d].r.n_xcd; ++x)
