@@ -11,8 +11,9 @@
 //  4. Recovery: a device that resets mid-run is re-opened and re-baselined.
 //  6. Exporter: concurrent /metrics renders and /counters streams while the
 //     samplers run at 2 kHz, the slow tier republishes link tables, the node
-//     name changes (render caches under the exporter mutex) and the counters are
-//     handed over and taken back.
+//     name changes (render caches under the exporter mutex), the counters are
+//     handed over and taken back, and a square load flips the devices between
+//     quiet (idle READ rate, changed at run time) and busy.
 //  5. PMFW table parser fuzz (ASAN build): random, truncated and mutated
 //     v1.8-shaped buffers, each in an exactly-sized heap block so any read past
 //     `len` is caught; the parser must reject or parse, never overrun.
@@ -314,6 +315,11 @@ static void test_exporter_concurrent() {
   c.pmc_source = "mock";
   c.port = -1;
   c.node_name = "node-a";
+  c.mock.square_duty = 0.5;  // 25 ms busy / 25 ms idle: quiet ↔ busy transitions
+  c.mock.util_period_s = 0.05;
+  c.mock.util_base = 50;
+  c.mock.util_amp = 50;
+  c.sampler.pmc_idle_hz = 200;
   Exporter ex(c);
   CHECK(ex.init());
   ex.start();
@@ -342,6 +348,7 @@ static void test_exporter_concurrent() {
   for (int i = 0; i < 40; ++i) {
     ex.set_node_name(i % 2 ? "node-b" : "node-a");
     if (i % 4 == 0) ex.set_pmc_enabled(i % 8 != 0);  // counter hand-over while the samplers run
+    ex.sampler()->set_pmc_idle_hz(i % 3 == 0 ? 0 : 200);  // profiling mode on / off at run time
     std::this_thread::sleep_for(std::chrono::milliseconds(25));
   }
   stop = true;
@@ -353,6 +360,7 @@ static void test_exporter_concurrent() {
   CHECK(renders.load() > 10 && streams.load() > 10);
   CHECK(out.find("kgs_pmc_enabled{gpu=\"0\"") != std::string::npos);
   CHECK(ex.sampler()->state(0).pmc_releases.load() == 5);  // released at i = 0, 8, 16, 24, 32
+  CHECK(ex.sampler()->state(0).pmc_quiet_skips.load() > 0);  // the idle halves were READ at the idle rate
   std::printf("exporter concurrent ok (%d renders, %d streams)\n", renders.load(), streams.load());
 }
 
