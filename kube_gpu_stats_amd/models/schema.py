@@ -93,7 +93,9 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_xgmi_read_bytes_total", "counter", "Bytes received per xGMI link.", extra=("link",)),
     F("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link.", extra=("link",)),
     F("amdgpu_xgmi_link_up", "gauge", "xGMI link status per port.", extra=("link",)),
-    F("amdgpu_pcie_bandwidth_bytes_total", "counter", "PCIe accumulated bandwidth (GB granularity)."),
+    F("amdgpu_pcie_bytes_total", "counter", "Bytes over the PCIe link, both directions: PMFW PCIe bandwidth "
+      "accumulator × MI355X calibration (105.7 B/unit; H2D 102.65, D2H 108.74 measured, ±3 %; profiles/r2/pcie/)."),
+    F("amdgpu_pcie_bandwidth_acc_total", "counter", "Raw PMFW PCIe bandwidth accumulator (amdsmi pcie_bandwidth_acc)."),
     # ---- RAS / link health -------------------------------------------------------------------
     F("amdgpu_ecc_errors_total", "counter", "Accumulated ECC errors by type.", extra=("type",), source="amdsmi",
       tier="slow"),

@@ -59,6 +59,12 @@ struct ExporterConfig {
   // HBM bytes/s at 100 % UMC (memory-controller) activity: the PMFW activity is
   // linear in bandwidth, 11.89 %/(TB/s) on MI355X (profiles/umc_calib.md).
   double hbm_bytes_per_s_at_full_umc = 8.41e12;
+  // Bytes per unit of the PMFW PCIe bandwidth accumulator.  amdsmi.h calls it
+  // "accumulated bandwidth (GB/sec)"; measured on MI355X (Gen5 x16) it advances
+  // by one unit per 102.65 B host→device and 108.74 B device→host, for 256 MiB
+  // and 2 GiB copies alike, 108.3 B full-duplex (profiles/r2/pcie/): one factor is
+  // good to ±3 %.
+  double pcie_bytes_per_acc_unit = 105.7;
   bool per_process = true;
   bool compat_series = true;        // container_gpu_sm_util (reference contract)
   bool compat_unallocated = false;  // also emit it for GPUs with no pod (pod_name="")

@@ -484,8 +484,16 @@ void Exporter::render(std::string& out) {
     auto h = S.state(d).get_health();
     if (h && h->xgmi_error_status >= 0) w.line("amdgpu_xgmi_error_status", dev_labels_[d], nullptr, h->xgmi_error_status);
   }
-  w.head("amdgpu_pcie_bandwidth_bytes_total", "counter", "PCIe accumulated bandwidth from the PMFW table (GB granularity)");
-  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPcie)) w.line_u("amdgpu_pcie_bandwidth_bytes_total", dev_labels_[d], nullptr, snaps[d].s.pcie_bw_acc_gb * 1000000000ull);
+  w.head("amdgpu_pcie_bytes_total", "counter",
+         "Bytes over the PCIe link (both directions), from the PMFW PCIe bandwidth accumulator times a MI355X "
+         "calibration (--pcie-bytes-per-unit; +-3 %); rate() = PCIe bandwidth");
+  for (int d : ids)
+    if (snaps[d].have && (snaps[d].s.valid & kFPcie))
+      w.line("amdgpu_pcie_bytes_total", dev_labels_[d], nullptr,
+             static_cast<double>(snaps[d].s.pcie_bw_acc_gb) * cfg_.pcie_bytes_per_acc_unit);
+  w.head("amdgpu_pcie_bandwidth_acc_total", "counter",
+         "Raw PMFW PCIe bandwidth accumulator (amdsmi pcie_bandwidth_acc; advances once per ~100 bytes moved)");
+  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPcie)) w.line_u("amdgpu_pcie_bandwidth_acc_total", dev_labels_[d], nullptr, snaps[d].s.pcie_bw_acc_gb);
 
   // ---- hardware counters (PMC tier) ----------------------------------------
   bool any_pmc = false;

@@ -4,8 +4,8 @@
 The reference only looks at GPUs through Prometheus, after the fact
 (gpu_util_stats.py:159) or as an allocation census (who_use_gpu.py:7-25).  This
 reads one exporter directly: every ``--interval`` it scrapes ``/metrics`` and
-prints one row per GPU.  Rates (xGMI bytes/s, average power from the energy
-counter) come from counter deltas between two polls.  With ``--counters`` it
+prints one row per GPU.  Rates (xGMI and PCIe bytes/s, average power from the
+energy counter) come from counter deltas between two polls.  With ``--counters`` it
 also drains the full-rate counter stream (``/counters?since=``) and reports
 the min / max of per-drain MFMA utilisation, the number of busy bursts and the
 exact busy duty cycle inside each interval (``segments``).  At an 8 kHz tick
@@ -25,7 +25,7 @@ from ..utils.scrape import Scraper, parse_text
 COLS = [("gpu", "GPU", 3), ("pod", "POD", 18), ("gfx", "GFX%", 5), ("mfma", "MFMA%", 5), ("vmem", "VMEM%", 5),
         ("umc", "UMC%", 5), ("hbm_gb", "HBM_GB", 7), ("hbm_pct", "HBM%", 5), ("power_w", "PWR_W", 6),
         ("energy_w", "AVG_W", 6), ("temp_c", "TEMP", 4), ("clk_mhz", "MHZ", 5), ("xgmi_gbps", "XGMI_GB/s", 9),
-        ("xcd_mfma", "MFMA%_PER_XCD", 31)]
+        ("pcie_gbps", "PCIE_GB/s", 9), ("xcd_mfma", "MFMA%_PER_XCD", 31)]
 BURST_COLS = [("mfma_min", "MFMA_MIN", 8), ("mfma_max", "MFMA_MAX", 8), ("bursts", "BURSTS", 6),
               ("duty", "DUTY%", 5), ("drains", "DRAINS", 6)]
 
@@ -113,6 +113,8 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
     clk = _by_gpu(cur, "amdgpu_gpu_clock_effective_mhz") or _by_gpu(cur, "amdgpu_clock_mhz", clock="gfx")
     energy = _by_gpu(cur, "amdgpu_energy_joules_total")
     xgmi = _sum_by_gpu(cur, "amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total")
+    pcie = _by_gpu(cur, "amdgpu_pcie_bytes_total")
+    ppcie = _by_gpu(prev, "amdgpu_pcie_bytes_total") if prev else {}
     penergy = _by_gpu(prev, "amdgpu_energy_joules_total") if prev else {}
     pxgmi = _sum_by_gpu(prev, "amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total") if prev else {}
     pods = _pods(cur)
@@ -124,11 +126,13 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
              "umc": umc.get(g), "hbm_gb": used[g] / 1e9 if g in used else None,
              "hbm_pct": 100.0 * used[g] / total[g] if total.get(g) and g in used else None,
              "power_w": power.get(g), "temp_c": temp.get(g), "clk_mhz": clk.get(g), "energy_w": None,
-             "xgmi_gbps": None, "xcd_mfma": xcd.get(g)}
+             "xgmi_gbps": None, "pcie_gbps": None, "xcd_mfma": xcd.get(g)}
         if dt > 0 and g in penergy and g in energy and energy[g] >= penergy[g]:
             r["energy_w"] = (energy[g] - penergy[g]) / dt
         if dt > 0 and g in pxgmi and g in xgmi and xgmi[g] >= pxgmi[g]:
             r["xgmi_gbps"] = (xgmi[g] - pxgmi[g]) / dt / 1e9
+        if dt > 0 and g in ppcie and g in pcie and pcie[g] >= ppcie[g]:
+            r["pcie_gbps"] = (pcie[g] - ppcie[g]) / dt / 1e9
         rows.append(r)
     return rows
 

@@ -867,3 +867,39 @@ def test_counter_reader_reopen_with_another_event_list(tmp_path):
         assert all(0 <= v <= 1.01 for k, v in idle.items() if k not in ("drains", "secs")), (name, idle)
     load = sets["grbm_spi"]["phases"]["mfma_load"]
     assert load["GRBM:11"] > 0.8, load                                     # SPI busy sees the pre-existing queue
+
+
+def test_pcie_bytes_counter_tracks_host_copies(N, torch_dev):
+    """amdgpu_pcie_bytes_total (PMFW PCIe bandwidth accumulator × the MI355X
+    calibration) follows the bytes pinned host↔device copies move, within the ±3 %
+    spread of the calibration (+ PMFW-table granularity).  Round 1 exported the raw
+    accumulator × 1e9 as bytes — 10⁷ too high (profiles/r2/pcie/)."""
+    import torch
+
+    from kube_gpu_stats_amd.utils.scrape import parse_text
+
+    n = (1 << 30) // 4
+    host = torch.empty(n, dtype=torch.float32).pin_memory()
+    dev = torch.empty(n, dtype=torch.float32, device=torch_dev)
+    dev.copy_(host)
+    torch.cuda.synchronize()
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 100, "proc_every": 0, "link_every": 0})
+    ex.start()
+    try:
+        time.sleep(0.3)
+        val = lambda: parse_text(ex.render())["amdgpu_pcie_bytes_total"][0][1]  # noqa: E731
+        out = {}
+        for name, fn in (("h2d", lambda: dev.copy_(host, non_blocking=True)),
+                         ("d2h", lambda: host.copy_(dev, non_blocking=True))):
+            b0, t0, moved = val(), time.time(), 0
+            while time.time() - t0 < 1.5:
+                fn()
+                torch.cuda.synchronize()
+                moved += n * 4
+            time.sleep(0.1)  # the PMFW table of the last copy
+            out[name] = {"moved": moved, "counted": val() - b0}
+    finally:
+        ex.stop()
+    print(json.dumps(out))
+    for name, r in out.items():
+        assert 0.93 < r["counted"] / r["moved"] < 1.07, (name, r)

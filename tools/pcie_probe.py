@@ -35,31 +35,42 @@ def main() -> int:
     dev = torch.empty(n, dtype=torch.float32, device="cuda")
     dev.copy_(host)
     torch.cuda.synchronize()
+    small_n = n // 8
+    s_h2d, s_d2h = torch.cuda.Stream(), torch.cuda.Stream()
+    host2 = torch.empty(n, dtype=torch.float32).pin_memory()
+    dev2 = torch.empty(n, dtype=torch.float32, device="cuda")
+    cases = [("idle", 0), ("h2d", n), ("d2h", n), ("h2d", small_n), ("d2h", small_n), ("both", n)]
     rows = []
-    for direction in ("idle", "h2d", "d2h"):
+    for direction, m in cases:
         time.sleep(0.3)
         s0, t0 = ex.snapshot(0), time.time()
         moved = 0
         while time.time() - t0 < a.secs:
             if direction == "h2d":
-                dev.copy_(host, non_blocking=True)
+                dev[:m].copy_(host[:m], non_blocking=True)
             elif direction == "d2h":
-                host.copy_(dev, non_blocking=True)
+                host[:m].copy_(dev[:m], non_blocking=True)
+            elif direction == "both":  # full duplex: one copy each way on its own stream
+                with torch.cuda.stream(s_h2d):
+                    dev.copy_(host, non_blocking=True)
+                with torch.cuda.stream(s_d2h):
+                    host2.copy_(dev2, non_blocking=True)
+                m = 2 * n
             else:
                 time.sleep(0.05)
                 continue
             torch.cuda.synchronize()
-            moved += n * 4
+            moved += m * 4
         wall = time.time() - t0
         time.sleep(0.1)
         s1 = ex.snapshot(0)
         dacc = s1["pcie_bw_acc_gb"] - s0["pcie_bw_acc_gb"]
         dcnt = s1["accumulation_counter"] - s0["accumulation_counter"]
         dfw = (s1["fw_ts"] - s0["fw_ts"]) * 1e-8
-        r = {"direction": direction, "bytes_moved": moved, "wall_s": round(wall, 3), "true_GBps": moved / wall / 1e9,
-             "d_pcie_bw_acc": dacc, "d_accumulation_counter": dcnt, "d_fw_s": round(dfw, 3),
-             "acc_as_GB": dacc, "acc_mean_GBps": dacc / dcnt if dcnt else None,
-             "acc_GB_if_mean_times_dt": (dacc / dcnt * dfw) if dcnt else None,
+        r = {"direction": direction, "copy_bytes": m * 4, "bytes_moved": moved, "wall_s": round(wall, 3),
+             "true_GBps": moved / wall / 1e9, "d_pcie_bw_acc": dacc, "d_accumulation_counter": dcnt,
+             "d_fw_s": round(dfw, 3), "acc_per_cycle": dacc / dcnt if dcnt else None,
+             "bytes_per_acc_unit": moved / dacc if dacc and moved else None,
              "link": [s1["pcie_link_width"], s1["pcie_link_speed_01gts"]]}
         print(json.dumps(r), flush=True)
         rows.append(r)
