@@ -903,3 +903,37 @@ def test_pcie_bytes_counter_tracks_host_copies(N, torch_dev):
     print(json.dumps(out))
     for name, r in out.items():
         assert 0.93 < r["counted"] / r["moved"] < 1.07, (name, r)
+
+
+def test_energy_counter_matches_socket_power(N, torch_dev):
+    """amdgpu_energy_joules_total (PMFW energy accumulator × 15.259 µJ) rises at the
+    socket power the same table reports: under the MFMA load their ratio is ~1."""
+    import torch
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 28)
+    ls.run_mfma()
+    torch.cuda.synchronize()
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 100, "proc_every": 0, "link_every": 0})
+    ex.start()
+    try:
+        time.sleep(0.3)
+        powers = []
+        i0 = ex.integrals(0)
+        s0 = ex.snapshot(0)
+        t0 = time.time()
+        while time.time() - t0 < 2.0:
+            ls.run_mfma()
+            torch.cuda.synchronize()
+            powers.append(ex.snapshot(0)["power_w"])
+        i1 = ex.integrals(0)
+        s1 = ex.snapshot(0)
+    finally:
+        ex.stop()
+    dt = (s1["fw_ts"] - s0["fw_ts"]) * 1e-8
+    watts = (i1["energy_joules"] - i0["energy_joules"]) / dt
+    mean_p = sum(powers) / len(powers)
+    print(json.dumps({"energy_rate_w": watts, "mean_socket_power_w": mean_p, "fw_dt_s": dt}))
+    assert mean_p > 500, mean_p                       # the MFMA load draws ~1.2 kW
+    assert 0.9 < watts / mean_p < 1.1, (watts, mean_p)
