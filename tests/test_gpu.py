@@ -937,3 +937,38 @@ def test_energy_counter_matches_socket_power(N, torch_dev):
     print(json.dumps({"energy_rate_w": watts, "mean_socket_power_w": mean_p, "fw_dt_s": dt}))
     assert mean_p > 500, mean_p                       # the MFMA load draws ~1.2 kW
     assert 0.9 < watts / mean_p < 1.1, (watts, mean_p)
+
+
+def test_hbm_used_and_process_hbm_track_an_allocation(N, torch_dev):
+    """A 16 GiB allocation shows up in amdgpu_hbm_used_bytes (sysfs VRAM used) and in
+    one process' amdgpu_process_hbm_bytes (AMD SMI process list; PIDs there are the
+    host's, so the process is the one whose VRAM grew), and goes away again."""
+    import torch
+
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 50, "proc_period_s": 0.1, "link_every": 0})
+    ex.start()
+
+    def state():
+        time.sleep(0.6)  # a few PMFW / process-list periods
+        return ex.snapshot(0)["vram_used_bytes"], {p["pid"]: p["vram_bytes"] for p in ex.procs(0)}
+
+    try:
+        torch.cuda.synchronize()
+        used0, p0 = state()
+        x = torch.empty(16 << 30, dtype=torch.uint8, device=torch_dev)
+        x.fill_(1)
+        torch.cuda.synchronize()
+        used1, p1 = state()
+        del x
+        torch.cuda.empty_cache()
+        used2, p2 = state()
+    finally:
+        ex.stop()
+    gib = float(1 << 30)
+    grew = max(p1, key=lambda pid: p1[pid] - p0.get(pid, 0)) if p1 else None
+    row = {"used_gib": [used0 / gib, used1 / gib, used2 / gib],
+           "proc_gib": [p0.get(grew, 0) / gib, p1.get(grew, 0) / gib, p2.get(grew, 0) / gib], "pid": grew}
+    print(json.dumps(row))
+    assert 15.5 < (used1 - used0) / gib < 16.8, row
+    assert 15.5 < (p1[grew] - p0.get(grew, 0)) / gib < 16.8, row
+    assert (used1 - used2) / gib > 15.5 and (p1[grew] - p2.get(grew, 0)) / gib > 15.5, row
