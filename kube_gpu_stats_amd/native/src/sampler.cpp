@@ -211,6 +211,10 @@ void Sampler::run(int dev) {
     PmcSample lp;
     if (st.pmc_latest.load(lp)) pmc_seq = lp.seq;
   }
+  // A thread that stopped (pause, rate change) while its device was quiet left
+  // the reader in synchronous mode: start pipelined, not quiet.
+  if (cfg_.pmc && pmc_ && st.pmc_on.load()) pmc_->set_fresh(dev, false);
+  st.pmc_quiet.store(0, std::memory_order_relaxed);
   int64_t next = mono_ns();
   int late_streak = 0;  // consecutive overrun ticks
   PmcSample& pmc_base = st.pmc_base;
