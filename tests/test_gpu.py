@@ -954,6 +954,7 @@ def test_hbm_used_and_process_hbm_track_an_allocation(N, torch_dev):
 
     try:
         torch.cuda.synchronize()
+        torch.cuda.empty_cache()  # blocks cached by earlier tests would be released below too
         used0, p0 = state()
         x = torch.empty(16 << 30, dtype=torch.uint8, device=torch_dev)
         x.fill_(1)
@@ -961,7 +962,10 @@ def test_hbm_used_and_process_hbm_track_an_allocation(N, torch_dev):
         used1, p1 = state()
         del x
         torch.cuda.empty_cache()
-        used2, p2 = state()
+        for _ in range(6):  # the driver's VRAM-used figure can lag the free
+            used2, p2 = state()
+            if used1 - used2 > 15.5 * (1 << 30):
+                break
     finally:
         ex.stop()
     gib = float(1 << 30)
