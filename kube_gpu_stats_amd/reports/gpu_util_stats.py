@@ -218,11 +218,24 @@ def run_report(c: PromClient, q: Queries, end: datetime | float, window_s: float
     return stats_pod_results(util, servers, pods, compat, show_finished)
 
 
-def format_rows(rows: list[list], mode: str, fmt: str, compat: bool) -> str:
+def idle_gpu_hours(rows: list[list], window_s: float) -> list[list]:
+    """Pod rows + the GPU-hours each pod held but left idle over the window:
+    cards × hours × (1 − util/100) — the waste figure an accounting report is for."""
+    h = window_s / 3600.0
+    return [[*r, float(r[2]) * h * (1.0 - min(100.0, max(0.0, r[3])) / 100.0)] for r in rows]
+
+
+def format_rows(rows: list[list], mode: str, fmt: str, compat: bool, idle_hours: bool = False) -> str:
     if compat:
         return "\n".join(str(r) for r in rows)  # :162-163 prints each row's repr
     header = ["Node", "Pod", "GPUs", "Util %"] if mode == "pod" else ["Node", "GPU Type", "Util %", "Used", "Total"]
-    disp = [[*r[:-1], f"{r[-1]:.2f}"] if mode == "pod" else [r[0], r[1], f"{r[2]:.2f}", r[3], r[4]] for r in rows]
+    if mode == "pod" and idle_hours:
+        header = header + ["Idle GPU-h"]
+        disp = [[r[0], r[1], r[2], f"{r[3]:.2f}", f"{r[4]:.2f}"] for r in rows]
+        if rows:
+            disp.append(["TOTAL", "", sum(int(r[2]) for r in rows), "", f"{sum(r[4] for r in rows):.2f}"])
+    else:
+        disp = [[*r[:-1], f"{r[-1]:.2f}"] if mode == "pod" else [r[0], r[1], f"{r[2]:.2f}", r[3], r[4]] for r in rows]
     if fmt == "json":
         return json.dumps([dict(zip(header, r)) for r in rows], indent=2)
     if fmt == "csv":
@@ -250,6 +263,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
              "gauge such as container_gpu_sm_util / container_gpu_mfma_util (avg_over_time of the scrapes)")
     add_flag(ap, "format", "table", "table | json | csv")
     add_flag(ap, "show-finished", False, "also list pods with utilisation but no live allocation (reference drops them)")
+    add_flag(ap, "idle-hours", False, "pod mode: add the GPU-hours each pod held but left idle (cards × window × "
+                                      "(1 − util)), and a total")
     return ap
 
 
@@ -259,7 +274,10 @@ def run(a) -> int:
          Queries.amd(a.namespace, a.step, a.resource, a.type_label, a.util_metric))
     end = a.end if a.end else (datetime.now() if a.compat else time.time())
     rows = run_report(c, q, end, a.window, a.step, a.compat, a.mode, a.missing, show_finished=a.show_finished)
-    print(format_rows(rows, a.mode, a.format, a.compat))
+    idle = bool(a.idle_hours) and a.mode == "pod" and not a.compat
+    if idle:
+        rows = idle_gpu_hours(rows, a.window)
+    print(format_rows(rows, a.mode, a.format, a.compat, idle_hours=idle))
     return 0
 
 

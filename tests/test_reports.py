@@ -165,3 +165,13 @@ def test_table_matches_prettytable_centering():
         "| odd |      22     |",
         "+-----+-------------+",
     ]
+
+
+def test_idle_gpu_hours_column_and_total():
+    """--idle-hours: cards × window hours × (1 − util) per pod, plus a total row."""
+    rows = G.idle_gpu_hours([["n1", "a", 4, 25.0], ["n1", "b", 2, 100.0], ["n2", "c", 1, 0.0]], 86400)
+    assert [r[4] for r in rows] == [72.0, 0.0, 24.0]
+    table = G.format_rows(rows, "pod", "table", compat=False, idle_hours=True)
+    assert "Idle GPU-h" in table and "TOTAL" in table and "96.00" in table
+    js = json.loads(G.format_rows(rows, "pod", "json", False, idle_hours=True))
+    assert js[0]["Idle GPU-h"] == 72.0 and len(js) == 3
