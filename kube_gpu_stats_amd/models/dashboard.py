@@ -90,6 +90,12 @@ def build() -> dict:
     add(_panel(0, "Effective shader clock", [(_dev("amdgpu_gpu_clock_effective_mhz"), "gpu{{gpu}}")], 12, y, w=12,
                unit="MHz"))
     y += 8
+    add(_panel(0, "Throttling by reason (PVIOL = ppt, TVIOL = socket_thermal)",
+               [(_dev("100 * rate(amdgpu_throttle_seconds_total[1m])"), "gpu{{gpu}} {{reason}}")], 0, y, w=12,
+               unit="percent", maxv=100))
+    add(_panel(0, "PCIe traffic (host link)", [(_dev("rate(amdgpu_pcie_bytes_total[1m])"), "gpu{{gpu}}")], 12, y,
+               w=12, unit="Bps"))
+    y += 8
     add(_row(0, "xGMI", y)); y += 1
     add(_panel(0, "xGMI traffic per GPU (read + write, all links)",
                [(_dev("sum by (instance, gpu) (rate(amdgpu_xgmi_read_bytes_total[1m]) + "

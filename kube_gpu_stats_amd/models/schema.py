@@ -88,6 +88,9 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_power_watts", "gauge", "Socket power."),
     F("amdgpu_energy_joules_total", "counter", "Energy since exporter start (wrap-safe)."),
     F("amdgpu_clock_mhz", "gauge", "Current clock (gfx = mean over XCCs, mem, soc).", extra=("clock",)),
+    F("amdgpu_throttle_seconds_total", "counter", "Seconds the GPU ran held back, per throttler (PMFW residency "
+      "accumulators ÷ accumulation cycles × time); 100 * rate() = violation % (amdsmi PVIOL for reason=\"ppt\", TVIOL "
+      "for reason=\"socket_thermal\").", extra=("reason",)),
     F("amdgpu_power_throttle_residency_total", "counter", "PMFW PPT throttle residency accumulator (raw)."),
     # ---- interconnect ------------------------------------------------------------------------
     F("amdgpu_xgmi_read_bytes_total", "counter", "Bytes received per xGMI link.", extra=("link",)),

@@ -110,6 +110,7 @@ struct MockConfig {
   // every period and base − amp for the rest (bursty jobs between scrapes).
   double util_base = 50, util_amp = 40, util_period_s = 10;
   double square_duty = 0;
+  double ppt_frac = 0;          // share of accumulation cycles the package-power throttler is active
   // "SPX" | "DPX" | "QPX" | "CPX": each GPU shows up as this many devices, all
   // with the GPU's BDF, one partition_id each, XCC curve g·8 + x per XCC.
   std::string compute_partition = "SPX";

@@ -77,6 +77,9 @@ struct GpuSample {
   uint64_t mem_activity_acc = 0;
   uint64_t accumulation_counter = 0;
   uint64_t ppt_residency_acc = 0, thm_residency_acc = 0;
+  // Throttler residency accumulators, kThrottleReasons order (each incremented
+  // every accumulation cycle its controller is active; amdsmi.h PVIOL/TVIOL).
+  uint64_t throttle_res_acc[5] = {};
   uint64_t xgmi_read_kb[kMaxXgmi] = {};
   uint64_t xgmi_write_kb[kMaxXgmi] = {};
   uint16_t xgmi_link_up[kMaxXgmi] = {};
@@ -111,6 +114,13 @@ static_assert(std::is_trivially_copyable<PmcSample>::value, "seqlock payload");
 
 // Running integrals maintained by the sampler so that Prometheus `rate()` over
 // any window gives exact averages regardless of scrape interval.
+// Throttlers the PMFW table accounts residency for (gpu_metrics v1.8).
+constexpr int kThrottleReasons = 5;
+inline const char* throttle_reason_name(int i) {
+  static const char* const n[kThrottleReasons] = {"prochot", "ppt", "socket_thermal", "vr_thermal", "hbm_thermal"};
+  return i >= 0 && i < kThrottleReasons ? n[i] : "?";
+}
+
 struct Integrals {
   double gfx_busy_seconds = 0;   // ∫ gfx busy fraction dt
   double umc_busy_seconds = 0;
@@ -132,6 +142,9 @@ struct Integrals {
   // ∫ GPU-active (GRBM_SPI_BUSY share of clocks) dt from the counter stream: the
   // READ-immune busy integral (--sm-util-source counters).
   double active_seconds = 0;
+  // ∫ throttled fraction dt per reason (Δresidency / Δaccumulation_counter per
+  // distinct PMFW table): seconds the GPU ran held back by each controller.
+  double throttle_seconds[kThrottleReasons] = {};
 };
 static_assert(std::is_trivially_copyable<Integrals>::value, "seqlock payload");
 

@@ -156,6 +156,9 @@ class MockBackend final : public Backend {
     s.accumulation_counter = static_cast<uint64_t>(std::llround(ms));
     s.gfx_activity_acc = static_cast<uint64_t>(std::llround(ui * 1000.0));
     s.mem_activity_acc = static_cast<uint64_t>(std::llround(ui * 500.0));
+    s.throttle_res_acc[1] = static_cast<uint64_t>(std::llround(ms * cfg_.ppt_frac));  // ppt
+    s.ppt_residency_acc = s.throttle_res_acc[1];
+    s.valid |= kFThrottle;
     for (int x = 0; x < kMaxXcc; ++x) {
       if (parts_ > 1) {
         s.gfx_busy_xcc[x] = static_cast<float>(curve_util(cfg_, xcc_curve(cfg_, g, x), tf));

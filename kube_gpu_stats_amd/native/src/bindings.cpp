@@ -37,6 +37,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.seed = get<uint64_t>(m, "seed", c.mock.seed);
     c.mock.ecc_correctable_per_s = get<uint64_t>(m, "ecc_correctable_per_s", c.mock.ecc_correctable_per_s);
     c.mock.square_duty = get<double>(m, "square_duty", c.mock.square_duty);
+    c.mock.ppt_frac = get<double>(m, "ppt_frac", c.mock.ppt_frac);
     c.mock.compute_partition = get<std::string>(m, "compute_partition", c.mock.compute_partition);
     c.mock.proc_latency_s = get<double>(m, "proc_latency_s", c.mock.proc_latency_s);
     c.mock.link_latency_s = get<double>(m, "link_latency_s", c.mock.link_latency_s);
@@ -224,6 +225,11 @@ class PyExporter {
     o["pmc_read_seconds"] = I.pmc_read_seconds;
     o["mfma_busy_seconds"] = I.mfma_busy_seconds;
     o["active_seconds"] = I.active_seconds;
+    {
+      py::dict t;
+      for (int r = 0; r < kThrottleReasons; ++r) t[throttle_reason_name(r)] = I.throttle_seconds[r];
+      o["throttle_seconds"] = t;
+    }
     const DeviceState& st = ex_.sampler()->state(d);
     o["proc_reads"] = st.proc_reads.load();
     o["link_reads"] = st.link_reads.load();

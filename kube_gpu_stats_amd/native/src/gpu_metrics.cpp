@@ -103,6 +103,11 @@ int parse_gpu_metrics_v1_8(const uint8_t* b, size_t len, GpuSample& s) {
   const uint32_t ppt = rd<uint32_t>(b, kPptRes), thm = rd<uint32_t>(b, kSocketThmRes);
   if (!na32(ppt)) { s.ppt_residency_acc = ppt; valid |= kFThrottle; }
   if (!na32(thm)) s.thm_residency_acc = thm;
+  const size_t res_off[kThrottleReasons] = {kProchotRes, kPptRes, kSocketThmRes, kVrThmRes, kHbmThmRes};
+  for (int r = 0; r < kThrottleReasons; ++r) {
+    const uint32_t v = rd<uint32_t>(b, res_off[r]);
+    s.throttle_res_acc[r] = na32(v) ? 0 : v;
+  }
 
   const uint16_t pwid = rd<uint16_t>(b, kPcieWidth), psp = rd<uint16_t>(b, kPcieSpeed);
   const uint64_t pbw = rd<uint64_t>(b, kPcieBwAcc), pbi = rd<uint64_t>(b, kPcieBwInst),

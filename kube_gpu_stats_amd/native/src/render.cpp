@@ -141,6 +141,10 @@ const char* const kXccLabels[kMaxXcc] = {"xcc=\"0\"", "xcc=\"1\"", "xcc=\"2\"", 
                                          "xcc=\"4\"", "xcc=\"5\"", "xcc=\"6\"", "xcc=\"7\""};
 const char* const kLinkLabels[kMaxXgmi] = {"link=\"0\"", "link=\"1\"", "link=\"2\"", "link=\"3\"",
                                            "link=\"4\"", "link=\"5\"", "link=\"6\"", "link=\"7\""};
+const char* const kThrottleLabels[kThrottleReasons] = {"reason=\"prochot\"", "reason=\"ppt\"",
+                                                       "reason=\"socket_thermal\"", "reason=\"vr_thermal\"",
+                                                       "reason=\"hbm_thermal\""};
+const char* throttle_label(int r) { return kThrottleLabels[r]; }
 
 }  // namespace
 
@@ -411,6 +415,13 @@ void Exporter::render(std::string& out) {
     if (x.s.valid & kFUclk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"mem\"", x.s.uclk_mhz);
     if (x.s.valid & kFSocClk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"soc\"", x.s.socclk_mhz);
   }
+  w.head("amdgpu_throttle_seconds_total", "counter",
+         "Seconds the GPU ran held back by each throttler (PMFW residency accumulators: prochot, ppt = package power, "
+         "socket / vr / hbm thermal); 100 * rate() = violation percent (amdsmi PVIOL / TVIOL)");
+  for (int d : ids)
+    if (snaps[d].have && (snaps[d].s.valid & kFThrottle))
+      for (int r = 0; r < kThrottleReasons; ++r)
+        w.line("amdgpu_throttle_seconds_total", dev_labels_[d], throttle_label(r), snaps[d].I.throttle_seconds[r]);
   w.head("amdgpu_power_throttle_residency_total", "counter", "PMFW package-power-tracking throttle residency accumulator (raw)");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFThrottle)) w.line_u("amdgpu_power_throttle_residency_total", dev_labels_[d], nullptr, snaps[d].s.ppt_residency_acc);
 

@@ -173,6 +173,16 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
   I.sampled_seconds += dt;
   if ((cur.valid & kFEnergy) && (prev->valid & kFEnergy) && cur.energy_acc >= prev->energy_acc)
     I.energy_joules += energy_units_to_joules(cur.energy_acc - prev->energy_acc);
+  // Throttler residencies: the fraction of accumulation cycles each controller was
+  // active (amdsmi.h PVIOL / TVIOL), times the interval.
+  if ((cur.valid & kFThrottle) && (prev->valid & kFThrottle) && (cur.valid & kFAcc) && (prev->valid & kFAcc) &&
+      acc_delta(prev->accumulation_counter, cur.accumulation_counter, dc) && dc > 0)
+    for (int r = 0; r < kThrottleReasons; ++r) {
+      uint64_t dr;
+      if (!acc_delta(prev->throttle_res_acc[r], cur.throttle_res_acc[r], dr)) continue;
+      const double f = static_cast<double>(dr) / static_cast<double>(dc);
+      I.throttle_seconds[r] += (f > 1.0 ? 1.0 : f) * dt;
+    }
 }
 
 void Sampler::run(int dev) {

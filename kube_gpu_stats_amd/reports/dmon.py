@@ -25,7 +25,7 @@ from ..utils.scrape import Scraper, parse_text
 COLS = [("gpu", "GPU", 3), ("pod", "POD", 18), ("gfx", "GFX%", 5), ("mfma", "MFMA%", 5), ("vmem", "VMEM%", 5),
         ("umc", "UMC%", 5), ("hbm_gb", "HBM_GB", 7), ("hbm_pct", "HBM%", 5), ("power_w", "PWR_W", 6),
         ("energy_w", "AVG_W", 6), ("temp_c", "TEMP", 4), ("clk_mhz", "MHZ", 5), ("xgmi_gbps", "XGMI_GB/s", 9),
-        ("pcie_gbps", "PCIE_GB/s", 9), ("xcd_mfma", "MFMA%_PER_XCD", 31)]
+        ("pcie_gbps", "PCIE_GB/s", 9), ("ppt_pct", "PVIOL%", 6), ("xcd_mfma", "MFMA%_PER_XCD", 31)]
 BURST_COLS = [("mfma_min", "MFMA_MIN", 8), ("mfma_max", "MFMA_MAX", 8), ("bursts", "BURSTS", 6),
               ("duty", "DUTY%", 5), ("drains", "DRAINS", 6)]
 
@@ -114,6 +114,8 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
     energy = _by_gpu(cur, "amdgpu_energy_joules_total")
     xgmi = _sum_by_gpu(cur, "amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total")
     pcie = _by_gpu(cur, "amdgpu_pcie_bytes_total")
+    ppt = _by_gpu(cur, "amdgpu_throttle_seconds_total", reason="ppt")
+    pppt = _by_gpu(prev, "amdgpu_throttle_seconds_total", reason="ppt") if prev else {}
     ppcie = _by_gpu(prev, "amdgpu_pcie_bytes_total") if prev else {}
     penergy = _by_gpu(prev, "amdgpu_energy_joules_total") if prev else {}
     pxgmi = _sum_by_gpu(prev, "amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total") if prev else {}
@@ -126,13 +128,15 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
              "umc": umc.get(g), "hbm_gb": used[g] / 1e9 if g in used else None,
              "hbm_pct": 100.0 * used[g] / total[g] if total.get(g) and g in used else None,
              "power_w": power.get(g), "temp_c": temp.get(g), "clk_mhz": clk.get(g), "energy_w": None,
-             "xgmi_gbps": None, "pcie_gbps": None, "xcd_mfma": xcd.get(g)}
+             "xgmi_gbps": None, "pcie_gbps": None, "ppt_pct": None, "xcd_mfma": xcd.get(g)}
         if dt > 0 and g in penergy and g in energy and energy[g] >= penergy[g]:
             r["energy_w"] = (energy[g] - penergy[g]) / dt
         if dt > 0 and g in pxgmi and g in xgmi and xgmi[g] >= pxgmi[g]:
             r["xgmi_gbps"] = (xgmi[g] - pxgmi[g]) / dt / 1e9
         if dt > 0 and g in ppcie and g in pcie and pcie[g] >= ppcie[g]:
             r["pcie_gbps"] = (pcie[g] - ppcie[g]) / dt / 1e9
+        if dt > 0 and g in pppt and g in ppt and ppt[g] >= pppt[g]:
+            r["ppt_pct"] = 100.0 * (ppt[g] - pppt[g]) / dt  # package-power throttling (amdsmi PVIOL)
         rows.append(r)
     return rows
 

@@ -569,3 +569,20 @@ def test_quiet_gpu_counter_reads_drop_to_idle_rate(mock_exporter):
     assert 0.25 * 2000 * 0.6 <= r_sq <= 0.25 * 2000 + 0.75 * 50 + 150, r_sq
     w = sq.window(0, 1.2)
     assert w["gpu_active_pct"] == pytest.approx(25, abs=4), w      # the integral is exact at any READ rate
+
+
+def test_throttle_seconds_by_reason(mock_exporter):
+    """amdgpu_throttle_seconds_total{reason}: per distinct PMFW table, Δresidency /
+    Δaccumulation_counter of each throttler times the interval (amdsmi PVIOL/TVIOL),
+    so 100 * rate() is the violation percent."""
+    ex = mock_exporter(n_gpus=1, hz=200, mock={"ppt_frac": 0.25, "fw_period_s": 0.005})
+    time.sleep(0.3)
+    i0, t0 = ex.integrals(0), time.time()
+    time.sleep(1.0)
+    i1, dt = ex.integrals(0), time.time() - t0
+    ppt = (i1["throttle_seconds"]["ppt"] - i0["throttle_seconds"]["ppt"]) / dt
+    assert ppt == pytest.approx(0.25, abs=0.03)
+    assert i1["throttle_seconds"]["socket_thermal"] == 0
+    m = parse_text(ex.render())
+    rs = {lb["reason"]: v for lb, v in m["amdgpu_throttle_seconds_total"]}
+    assert set(rs) == {"prochot", "ppt", "socket_thermal", "vr_thermal", "hbm_thermal"} and rs["ppt"] > 0.2

@@ -976,3 +976,38 @@ def test_hbm_used_and_process_hbm_track_an_allocation(N, torch_dev):
     assert 15.5 < (used1 - used0) / gib < 16.8, row
     assert 15.5 < (p1[grew] - p0.get(grew, 0)) / gib < 16.8, row
     assert (used1 - used2) / gib > 15.5 and (p1[grew] - p2.get(grew, 0)) / gib > 15.5, row
+
+
+def test_throttle_residency_under_load_and_idle(N, torch_dev):
+    """amdgpu_throttle_seconds_total{reason}: an idle MI355X is not held back; under
+    the MFMA load (≈1.2 kW, clocks below peak) the package-power throttler (ppt,
+    amdsmi PVIOL) is active for much of the time."""
+    import torch
+
+    from kube_gpu_stats_amd.ops.load import LoadStep
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 28)
+    ls.run_mfma()
+    torch.cuda.synchronize()
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 100, "proc_every": 0, "link_every": 0})
+    ex.start()
+    out = {}
+    try:
+        time.sleep(1.0)
+        for phase in ("idle", "load"):
+            i0, t0 = ex.integrals(0), time.time()
+            while time.time() - t0 < 2.0:
+                if phase == "load":
+                    ls.run_mfma()
+                    torch.cuda.synchronize()
+                else:
+                    time.sleep(0.05)
+            i1, dt = ex.integrals(0), time.time() - t0
+            out[phase] = {r: (i1["throttle_seconds"][r] - i0["throttle_seconds"][r]) / dt for r in i1["throttle_seconds"]}
+            out[phase]["power_w"] = ex.snapshot(0)["power_w"]
+    finally:
+        ex.stop()
+    _keep("throttle_residency.json", json.dumps(out, indent=1))
+    print(json.dumps(out))
+    assert all(v < 0.05 for k, v in out["idle"].items() if k != "power_w"), out
+    assert out["load"]["ppt"] > 0.3, out
