@@ -557,6 +557,20 @@ def observed(m: dict) -> dict:
     return out
 
 
+def throttled(before: dict, after: dict, win: float) -> dict:
+    """Per GPU and throttler, % of the timed window the GPU ran held back
+    (amdgpu_throttle_seconds_total deltas; reason="ppt" is the package-power cap)."""
+    out: dict = {}
+    if win <= 0:
+        return out
+    b = {(lb["gpu"], lb["reason"]): v for lb, v in before.get("amdgpu_throttle_seconds_total", [])}
+    for lb, v in after.get("amdgpu_throttle_seconds_total", []):
+        d = v - b.get((lb["gpu"], lb["reason"]), v)
+        if d > 0:
+            out.setdefault(lb["gpu"], {})[lb["reason"]] = round(100.0 * d / win, 2)
+    return out
+
+
 # ----------------------------------------------------------------------------- phases
 PHASES: dict[str, list[float]] = {}
 
@@ -948,6 +962,7 @@ def run(a, ctx) -> dict | None:
         "pmc_error": exp.ready.get("pmc_error"),
         "load": calib,
         "observed_during_load": observed(after),
+        "throttled_pct_during_load": throttled(before, after, win),
         "xgmi_GBps_per_gpu": xgmi_rates(before, after, win),
         "phases_wall": PHASES,
         "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in integrals)
