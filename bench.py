@@ -544,6 +544,14 @@ def xgmi_rates(before: dict, after: dict, win: float) -> dict:
     return {g: round((a_[g] - b.get(g, 0.0)) / win / 1e9, 3) for g in a_} if win > 0 else {}
 
 
+def allreduce_GBps(load, a, n: int, win: float):
+    """xGMI bytes/s per GPU that phase B's all-reduces imply (None without them)."""
+    if getattr(load, "ar", None) is None or n < 2 or win <= 0:
+        return None
+    size = load.ar.numel() * load.ar.element_size()
+    return round(2 * 2 * (n - 1) / n * size * a.steps * load.reps / win / 1e9, 3)
+
+
 def observed(m: dict) -> dict:
     """What the exporter saw of the load (window gauges of the last scrape), per GPU."""
     out: dict = {}
@@ -964,6 +972,9 @@ def run(a, ctx) -> dict | None:
         "observed_during_load": observed(after),
         "throttled_pct_during_load": throttled(before, after, win),
         "xgmi_GBps_per_gpu": xgmi_rates(before, after, win),
+        # what the phase-B all-reduces must have moved per GPU (read + write, bandwidth-optimal
+        # 2(N-1)/N each way): the measured / expected ratio pins the PMFW xGMI accumulator unit
+        "xgmi_allreduce_GBps_per_gpu_expected": allreduce_GBps(load, a, n, win),
         "phases_wall": PHASES,
         "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in integrals)
         / max(1, sum(i.get("pmc_samples", 0) for i in integrals)),

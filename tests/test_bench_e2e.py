@@ -221,3 +221,20 @@ def test_train_load_steps_on_cpu():
         ld.step()
     assert loss() < l0
     assert ld.params > 0
+
+
+def test_allreduce_expected_xgmi_rate():
+    """Phase B's all-reduces imply 2·2(N-1)/N·size bytes per GPU per call (read + write):
+    the figure the 8-GPU run's measured xgmi_GBps_per_gpu is checked against."""
+    import types
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    ar = types.SimpleNamespace(numel=lambda: 64 << 20, element_size=lambda: 4)  # 256 MiB
+    load = types.SimpleNamespace(ar=ar, reps=11)
+    a = types.SimpleNamespace(steps=20)
+    want = 2 * 2 * 7 / 8 * (256 << 20) * 20 * 11 / 10.0 / 1e9
+    assert bench.allreduce_GBps(load, a, 8, 10.0) == pytest.approx(want, abs=1e-3)
+    assert bench.allreduce_GBps(load, a, 1, 10.0) is None
+    assert bench.allreduce_GBps(types.SimpleNamespace(reps=1), a, 8, 10.0) is None
