@@ -298,6 +298,21 @@ bool poll_signals() {
   return on;
 }
 
+// Scheduling priority of the private READ queue (KGS_AQL_PRIORITY = low | normal |
+// high; unset = ROCr's default, normal).  The CP firmware arbitrates between the
+// compute queues mapped on a pipe; a low-priority READ queue should yield to a
+// dispatch-bound workload queue (profiles/launch_overhead.md).
+int queue_priority() {
+  static const int v = [] {
+    const char* e = std::getenv("KGS_AQL_PRIORITY");
+    if (!e) return -1;
+    if (std::strcmp(e, "low") == 0) return static_cast<int>(HSA_AMD_QUEUE_PRIORITY_LOW);
+    if (std::strcmp(e, "high") == 0) return static_cast<int>(HSA_AMD_QUEUE_PRIORITY_HIGH);
+    return static_cast<int>(HSA_AMD_QUEUE_PRIORITY_NORMAL);
+  }();
+  return v;
+}
+
 // Put one PM4-IB vendor packet on the agent's private queue (no wait).
 void enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig,
              std::pair<int, int> fences = kSystemFences) {
@@ -731,6 +746,10 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
         set_err(err, errlen, "hsa_queue_create failed");
         return -1;
       }
+      if (queue_priority() >= 0 &&
+          hsa_amd_queue_set_priority(a->queue, static_cast<hsa_amd_queue_priority_t>(queue_priority())) !=
+              HSA_STATUS_SUCCESS)
+        KGS_DBG("hsa_amd_queue_set_priority(%d) failed\n", queue_priority());
       if (hsa_signal_create(1, 0, nullptr, &a->sig) != HSA_STATUS_SUCCESS) {
         set_err(err, errlen, "hsa_signal_create failed");
         return -1;

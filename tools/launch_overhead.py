@@ -93,6 +93,8 @@ def main() -> int:
             env["KGS_AQL_FENCE"] = opts["fence"]
         if "signal" in opts:
             env["KGS_AQL_SIGNAL"] = opts["signal"]
+        if "prio" in opts:
+            env["KGS_AQL_PRIORITY"] = opts["prio"]
         pr = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
         ready = json.loads(pr.stdout.readline())
         assert ready.get("event") == "ready", ready
@@ -121,7 +123,8 @@ def main() -> int:
 
     # spec hz:set:reader[:lean[:key=value...]]   keys: proc=<proc-every> (0 = no per-process tier),
     # slack=<ns> (sampler timer slack), fence=sys|agent|none (AQL header fences of the
-    # reader's packets), signal=interrupt|poll (READ completion signals); "off" = no exporter
+    # reader's packets), signal=interrupt|poll (READ completion signals), prio=low|normal|high
+    # (READ queue priority); "off" = no exporter
     specs = sys.argv[1:] or ["100:base:aqlprofile", "1000:base:aqlprofile", "8000:base:aqlprofile",
                              "100:full:aqlprofile", "1000:full:aqlprofile", "1000:base:none"]
     # The first exporter started in a fresh box slowed the graph replay by ≈38 % in
