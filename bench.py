@@ -112,6 +112,8 @@ def parse_args(argv=None):
                     "full-rate ring holds ≈1 s at 8 kHz)")
     ap.add_argument("--burst-ms", type=float, default=1.0, help="phase R: length of one burst")
     ap.add_argument("--burst-period-ms", type=float, default=5.0, help="phase R: burst period")
+    ap.add_argument("--capacity-hz", default="16000,24000",
+                    help="phase S: tick rates above --hz to try under the load, one block each ('' = off)")
     ap.add_argument("--quiet-s", type=float, default=1.5,
                     help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
@@ -815,6 +817,53 @@ def quiet_gpu(ctx, load, exp, a) -> dict:
     return out
 
 
+def capacity(ctx, load, exp, a) -> dict:
+    """Phase S — how far the counter tier goes past the primary rate (untimed).  Under the
+    same load, one ``--block-steps`` block at each ``--capacity-hz`` rate: delivered
+    counter drains per GPU, the worst GPU's share of nominal, overruns per second and
+    host µs per drain.  ``max_rate_hz_98pct`` is the highest rate tried (the primary one
+    included) at which every GPU delivered ≥ 98 %: the headroom behind the headline
+    number, which is the configured tick rate delivered."""
+    rates = [float(x) for x in str(a.capacity_hz).split(",") if x.strip()]
+    if not rates:
+        return {}
+    out: dict = {"block_steps": a.block_steps, "rates": {}}
+    best = None
+    for hz in [a.hz] + rates:
+        w0 = 0.0
+        before: dict = {}
+        if exp is not None:
+            exp.set_rate(hz)
+            time.sleep(0.05)
+            before, w0 = parse_text(exp.sc.get()), time.perf_counter()
+        dt = timed(ctx, load, a.block_steps)
+        if exp is None:
+            continue
+        after, win = parse_text(exp.sc.get()), time.perf_counter() - w0
+        r = Rates()
+        r.add(before, after, win)
+        pg, src = r.per_gpu(exp.ready.get("pmc", "none") != "none")
+
+        def delta(fam):
+            b = {lb["gpu"]: v for lb, v in before.get(fam, [])}
+            return {lb["gpu"]: v - b.get(lb["gpu"], 0.0) for lb, v in after.get(fam, [])}
+
+        ov, rs = delta("kgs_sampler_overruns_total"), delta("kgs_pmc_read_seconds_total")
+        worst = min(pg.values()) / hz if pg else 0.0
+        out["rates"][f"{hz:g}"] = {
+            "samples_per_sec_per_gpu": {g: round(v, 1) for g, v in pg.items()}, "sample_source": src,
+            "worst_gpu_pct_of_nominal": round(100 * worst, 2),
+            "overruns_per_s_per_gpu": round(sum(ov.values()) / max(1, len(ov)) / win, 1) if win > 0 else None,
+            "host_us_per_drain": round(1e6 * sum(rs.values()) / max(1.0, sum(r.pmc.values())), 2),
+            "block_s": round(dt, 4)}
+        if worst >= 0.98:
+            best = hz if best is None else max(best, hz)
+    if exp is not None:
+        exp.set_rate(a.hz)
+    out["max_rate_hz_98pct"] = best
+    return out
+
+
 def run(a, ctx) -> dict | None:
     n = ctx.world
     hzs = tiers(a)
@@ -892,6 +941,7 @@ def run(a, ctx) -> dict | None:
     resolution = burst_train(ctx, load, exp, a)
     quiet = quiet_gpu(ctx, load, exp, a)
     inter = interleaved(ctx, load, exp, a, hzs)
+    cap = capacity(ctx, load, exp, a)
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
@@ -965,6 +1015,7 @@ def run(a, ctx) -> dict | None:
         "interleaved": inter,
         "burst_resolution": resolution,
         "quiet_gpu": quiet,
+        "capacity": cap,
         "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
         "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / win, 4) for k, v in thr1.items()
                                          if win > 0 and v - thr0.get(k, 0.0) > 0.005 * win},

@@ -87,6 +87,13 @@ def test_bench_contract_single_process():
     q = res["quiet_gpu"]
     assert q["adaptive"]["pmc_idle_hz"] == 100 and q["profiling"]["pmc_idle_hz"] == 0
     assert set(q["adaptive"]["per_gpu"]["0"]) == {"reads_per_s", "pmfw_gfx_busy_pct", "gpu_active_pct"}
+    # phase S plumbing: the primary rate and each capacity rate got a block, rate restored after
+    cap = res["capacity"]
+    assert list(cap["rates"]) == ["8000", "16000", "24000"]
+    for row in cap["rates"].values():
+        assert row["sample_source"] == "pmc" and row["samples_per_sec_per_gpu"]["0"] > 0
+        assert row["host_us_per_drain"] > 0
+    assert cap["rates"]["16000"]["samples_per_sec_per_gpu"]["0"] > cap["rates"]["8000"]["samples_per_sec_per_gpu"]["0"]
 
 
 @pytest.mark.slow

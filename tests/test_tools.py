@@ -16,10 +16,12 @@ def test_rocprof_overhead_splits_by_condition(tmp_path):
     res = {"steps": 3, "warmup": 1, "config": {"units_per_step": 2},
            "burst_resolution": {"per_gpu": {"0": {"launched": 4}}},
            "interleaved": {"block_steps": 1, "block_seconds": [["0", 1], ["100", 1], ["8000", 1],
-                                                               ["8000", 1], ["100", 1], ["0", 1]]}}
+                                                               ["8000", 1], ["100", 1], ["0", 1]]},
+           "capacity": {"block_steps": 1, "rates": {"8000": {}, "16000": {}}}}
     tiny, triads = 3, 2
     dur = {"A_off": 100, "B_on_8k": 102, "C_off": 100, "I_paused": 100, "I_100Hz": 100, "I_8000Hz": 101,
-           "calib": 50, "calib_reps": 50, "warmup": 50, "R_bursts": 1}
+           "calib": 50, "calib_reps": 50, "warmup": 50, "R_bursts": 1,
+           "S_8000Hz": 300, "S_16000Hz": 300}  # phase S sits between I and C: off by one would skew C
     rows, t = [], 0
 
     def launch(name, d):

@@ -45,6 +45,8 @@ def segments(res: dict, triads: int, tiny: int) -> list[tuple[str, int, dict]]:
     seg = [("calib_reps", 2, {}), ("warmup", w * reps, {}), ("A_off", k * reps, {}), ("B_on_8k", k * reps, {}),
            ("R_bursts", 0, {"mfma": bursts})]
     seg += [(f"I_{'paused' if c == '0' else c + 'Hz'}", bs * reps, {}) for c, _ in inter.get("block_seconds", [])]
+    cap = res.get("capacity") or {}
+    seg += [(f"S_{hz}Hz", cap.get("block_steps", 0) * reps, {}) for hz in cap.get("rates", {})]
     seg += [("C_off", k * reps, {})]
     return seg
 
