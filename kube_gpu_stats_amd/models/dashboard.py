@@ -59,6 +59,13 @@ def build() -> dict:
                [(f"count by (kubernetes_io_hostname) (container_gpu_sm_util{{{_NODE},pod_name!=\"\"}})",
                  "{{kubernetes_io_hostname}}")], 12, y))
     y += 8
+    add(_panel(0, "Power drawn by each pod's GPUs",
+               [(f"sum(rate(container_gpu_energy_joules_total{{{_NODE}}}[5m])) by (kubernetes_io_hostname, pod_name)",
+                 "{{kubernetes_io_hostname}} / {{pod_name}}")], 0, y, unit="watt"))
+    add(_panel(0, "Per-pod exact utilisation (busy-seconds counter)",
+               [(f"100 * avg(rate(container_gpu_busy_seconds_total{{{_NODE}}}[5m])) by (kubernetes_io_hostname, pod_name)",
+                 "{{kubernetes_io_hostname}} / {{pod_name}}")], 12, y, unit="percent", maxv=100))
+    y += 8
     add(_row(0, "Utilisation", y)); y += 1
     add(_panel(0, "GFX busy (PMFW) vs GPU-active (waves, READ-immune)",
                [(_dev("100 * rate(amdgpu_gfx_busy_seconds_total[1m])"), "gfx busy {{kubernetes_io_hostname}} gpu{{gpu}}"),

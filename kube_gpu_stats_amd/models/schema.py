@@ -51,6 +51,13 @@ CATALOG: tuple[Family, ...] = (
       "the allocation (hardware counters).  Same labels as container_gpu_sm_util.",
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
       "rocprofiler+kubelet", "pmc"),
+    F("container_gpu_energy_joules_total", "counter",
+      "Socket energy of the GPU allocated to the pod, counted from the allocation (PMFW energy accumulator).  "
+      "`sum(increase(container_gpu_energy_joules_total[1h])) by (kubernetes_io_hostname, pod_name)` is the pod's "
+      "hourly energy; `kgs gpu-util-stats --energy` reports it in kWh.  A GPU shared by several pods counts in full "
+      "for each.  Same labels as container_gpu_sm_util.",
+      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      "pmfw+kubelet", "fast"),
     F("kgs_gpu_owner", "gauge",
       "1 per (GPU, pod, container) allocation reported by the kubelet: the join target that puts pod labels on any "
       "amdgpu_* series (`... * on (gpu, uuid) group_left(pod_name, namespace) kgs_gpu_owner`).",
@@ -208,5 +215,11 @@ def markdown() -> str:
     return "\n".join(rows)
 
 
+PREAMBLE = ("# Metric catalogue\n\nGenerated by `python -m kube_gpu_stats_amd.models.schema` from "
+            "`kube_gpu_stats_amd/models/schema.py`; `tests/test_schema_cli.py` checks the renderer against it. Every "
+            "series also carries `gpu` and `uuid`; device attributes (bdf, type, serial, NUMA node, …) are in "
+            "`amdgpu_device_info`.\n\n")
+
+
 if __name__ == "__main__":
-    print(markdown())
+    print(PREAMBLE + markdown())

@@ -26,7 +26,7 @@ struct Owner {
   std::string pod, ns, container;
   // The GPU's busy integrals when this owner was first seen on it: the per-pod
   // counters (container_gpu_busy_seconds_total, ...) count from 0 at allocation.
-  double base_busy_s = 0, base_mfma_s = 0, base_active_s = 0;
+  double base_busy_s = 0, base_mfma_s = 0, base_active_s = 0, base_energy_j = 0;
   bool same(const Owner& o) const { return pod == o.pod && ns == o.ns && container == o.container; }
 };
 struct PidOwner {

@@ -165,6 +165,7 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
     x.base_busy_s = kept ? kept->base_busy_s : I.gfx_busy_seconds;
     x.base_mfma_s = kept ? kept->base_mfma_s : I.mfma_busy_seconds;
     x.base_active_s = kept ? kept->base_active_s : I.active_seconds;
+    x.base_energy_j = kept ? kept->base_energy_j : I.energy_joules;
   }
   if (o.empty()) m->erase(dev);
   else (*m)[dev] = std::move(o);

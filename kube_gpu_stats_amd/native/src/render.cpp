@@ -266,6 +266,17 @@ void Exporter::render(std::string& out) {
                                      : x.I.gfx_busy_seconds - (o ? o->base_busy_s : 0.0);
       w.line("container_gpu_busy_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
     }
+    // Per-pod energy: the GPU's socket energy since the pod was given it (a GPU
+    // shared by several pods counts in full for each: the pods hold it together).
+    w.head("container_gpu_energy_joules_total", "counter",
+           "Socket energy of the GPU allocated to the pod, counted from allocation (PMFW energy accumulator; "
+           "increase() over a window = joules the pod's GPU drew; same labels as container_gpu_sm_util)");
+    for (size_t i = 0; i < pod_lines.size(); ++i) {
+      const Owner* o = pod_owner[i];
+      const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
+      const double v = x.I.energy_joules - (o ? o->base_energy_j : 0.0);
+      w.line("container_gpu_energy_joules_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
+    }
     bool any_pmc_int = false;
     for (const auto& pl : pod_lines) any_pmc_int |= snaps[static_cast<size_t>(pl.first)].pmc_have;
     if (any_pmc_int) {

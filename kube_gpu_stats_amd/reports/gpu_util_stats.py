@@ -37,7 +37,7 @@ from datetime import datetime, timedelta
 from ..utils import log
 from ..utils.config import (REF_NAMESPACE, REF_PROM_URL, REF_PROXY, REF_STEP_S, REF_TIMEOUT_S, REF_WINDOW_S,
                             add_flag)
-from .promql import PromClient, result
+from .promql import PromClient, result, to_unix
 from .table import render, render_csv
 
 L = log.get("gpu_util_stats")
@@ -225,15 +225,49 @@ def idle_gpu_hours(rows: list[list], window_s: float) -> list[list]:
     return [[*r, float(r[2]) * h * (1.0 - min(100.0, max(0.0, r[3])) / 100.0)] for r in rows]
 
 
-def format_rows(rows: list[list], mode: str, fmt: str, compat: bool, idle_hours: bool = False) -> str:
+ENERGY_METRIC = "container_gpu_energy_joules_total"
+
+
+def energy_query(step_s: int, metric: str = ENERGY_METRIC) -> str:
+    """Joules per (node, pod) per step: the exporter's per-pod energy counter (socket
+    energy of the pod's GPUs since allocation), summed over the pod's GPUs."""
+    return f"sum(increase({metric}[{step_s}s])) by (kubernetes_io_hostname, pod_name)"
+
+
+def pod_energy_kwh(c: PromClient, start, end, step_s: int) -> dict[tuple[str, str], float]:
+    """{(node, pod): kWh} over (start, end].  The range query's first point covers the
+    step *before* ``start``, so it is left out: the kept points tile the window."""
+    t0 = to_unix(start)  # the start the range query is evaluated from (whole seconds)
+    out: dict[tuple[str, str], float] = {}
+    for r in result(c.query_range(energy_query(step_s), start, end, step_s)):
+        key = (r["metric"].get("kubernetes_io_hostname", ""), r["metric"].get("pod_name", ""))
+        j = sum(float(v) for ts, v in r.get("values", []) if float(ts) > t0 + 0.5)
+        out[key] = out.get(key, 0.0) + j / 3.6e6
+    return out
+
+
+def add_energy(rows: list[list], kwh: dict[tuple[str, str], float]) -> list[list]:
+    """Pod rows + the kWh their GPUs drew over the window (0 for a pod with no series)."""
+    return [[*r, kwh.get((r[0], str(r[1]).removesuffix(" (finished)")), 0.0)] for r in rows]
+
+
+def format_rows(rows: list[list], mode: str, fmt: str, compat: bool, idle_hours: bool = False,
+                extras: list[str] | None = None) -> str:
+    """Table / JSON / CSV.  Pod mode may carry extra numeric columns after Util %
+    (``extras`` headers; ``idle_hours`` is the "Idle GPU-h" one), totalled in a last row."""
     if compat:
         return "\n".join(str(r) for r in rows)  # :162-163 prints each row's repr
+    extras = list(extras or [])
+    if idle_hours and "Idle GPU-h" not in extras:
+        extras.insert(0, "Idle GPU-h")
     header = ["Node", "Pod", "GPUs", "Util %"] if mode == "pod" else ["Node", "GPU Type", "Util %", "Used", "Total"]
-    if mode == "pod" and idle_hours:
-        header = header + ["Idle GPU-h"]
-        disp = [[r[0], r[1], r[2], f"{r[3]:.2f}", f"{r[4]:.2f}"] for r in rows]
+    if mode == "pod" and extras:
+        header = header + extras
+        n = len(extras)
+        disp = [[r[0], r[1], r[2], f"{r[3]:.2f}", *(f"{x:.2f}" for x in r[4:4 + n])] for r in rows]
         if rows:
-            disp.append(["TOTAL", "", sum(int(r[2]) for r in rows), "", f"{sum(r[4] for r in rows):.2f}"])
+            disp.append(["TOTAL", "", sum(int(r[2]) for r in rows), "",
+                         *(f"{sum(r[4 + k] for r in rows):.2f}" for k in range(n))])
     else:
         disp = [[*r[:-1], f"{r[-1]:.2f}"] if mode == "pod" else [r[0], r[1], f"{r[2]:.2f}", r[3], r[4]] for r in rows]
     if fmt == "json":
@@ -265,6 +299,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "show-finished", False, "also list pods with utilisation but no live allocation (reference drops them)")
     add_flag(ap, "idle-hours", False, "pod mode: add the GPU-hours each pod held but left idle (cards × window × "
                                       "(1 − util)), and a total")
+    add_flag(ap, "energy", False, "pod mode: add the kWh each pod's GPUs drew over the window "
+                                  f"({ENERGY_METRIC}), and a total")
     return ap
 
 
@@ -274,10 +310,16 @@ def run(a) -> int:
          Queries.amd(a.namespace, a.step, a.resource, a.type_label, a.util_metric))
     end = a.end if a.end else (datetime.now() if a.compat else time.time())
     rows = run_report(c, q, end, a.window, a.step, a.compat, a.mode, a.missing, show_finished=a.show_finished)
-    idle = bool(a.idle_hours) and a.mode == "pod" and not a.compat
-    if idle:
-        rows = idle_gpu_hours(rows, a.window)
-    print(format_rows(rows, a.mode, a.format, a.compat, idle_hours=idle))
+    extras: list[str] = []
+    if a.mode == "pod" and not a.compat:
+        if a.idle_hours:
+            rows = idle_gpu_hours(rows, a.window)
+            extras.append("Idle GPU-h")
+        if a.energy:
+            e = end if isinstance(end, (int, float)) else end.timestamp()
+            rows = add_energy(rows, pod_energy_kwh(c, e - a.window, e, a.step))
+            extras.append("Energy kWh")
+    print(format_rows(rows, a.mode, a.format, a.compat, extras=extras))
     return 0
 
 

@@ -6,7 +6,8 @@ Two kinds of answers:
   golden harness drove the reference's five queries);
 * evaluated — a tiny TSDB fed from exporter scrapes (``ingest``) that evaluates
   the query shapes the report layer issues for the utilisation series:
-  ``avg(<metric>) by (l1, l2, ...)`` and ``avg(avg_over_time(<metric>[Ns])) by (...)``,
+  ``avg|sum|max(<metric>) by (l1, l2, ...)``, over a bare metric, ``avg_over_time``,
+  ``rate`` or ``increase`` of it,
   instant or ranged, with Prometheus' 5-minute staleness lookback.
 """
 from __future__ import annotations
@@ -18,7 +19,8 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from urllib.parse import parse_qs, urlparse
 
 LOOKBACK_S = 300.0
-_AVG_BY = re.compile(r"^\s*(?:([0-9.]+)\s*\*\s*)?avg\((.+)\)\s*by\s*\(([^)]*)\)\s*$")
+_AVG_BY = re.compile(r"^\s*(?:([0-9.]+)\s*\*\s*)?(avg|sum|max)\((.+)\)\s*by\s*\(([^)]*)\)\s*$")
+_AGG = {"avg": lambda vs: sum(vs) / len(vs), "sum": sum, "max": max}
 _AOT = re.compile(r"^\s*avg_over_time\(\s*([a-zA-Z_:][a-zA-Z0-9_:]*)\s*\[(\d+)([smh])\]\s*\)\s*$")
 _RATE = re.compile(r"^\s*(rate|increase)\(\s*([a-zA-Z_:][a-zA-Z0-9_:]*)\s*\[(\d+)([smh])\]\s*\)\s*$")
 _UNIT = {"s": 1, "m": 60, "h": 3600}
@@ -116,12 +118,13 @@ class FakeProm:
         if not m:
             raise ValueError(f"unsupported query {q!r}")
         k = float(m.group(1)) if m.group(1) else 1.0
-        by = [x.strip() for x in m.group(3).split(",") if x.strip()]
+        agg = _AGG[m.group(2)]
+        by = [x.strip() for x in m.group(4).split(",") if x.strip()]
         groups: dict[tuple, list[float]] = {}
-        for labels, v in self._inner(m.group(2), t):
+        for labels, v in self._inner(m.group(3), t):
             groups.setdefault(tuple(labels.get(b, "") for b in by), []).append(v)
         return [{"metric": {b: g[i] for i, b in enumerate(by) if g[i] != ""},
-                 "value": [t, repr(k * sum(vs) / len(vs))]} for g, vs in sorted(groups.items())]
+                 "value": [t, repr(k * agg(vs))]} for g, vs in sorted(groups.items())]
 
     def eval_range(self, q: str, start: float, end: float, step: float) -> list[dict]:
         out: dict[tuple, dict] = {}

@@ -113,3 +113,58 @@ def test_sm_util_from_counters(N, mock_exporter):
     assert act > busy and act == pytest.approx(ex.integrals(0)["active_seconds"], rel=0.05)
     with pytest.raises(RuntimeError, match="sm_util_source"):
         N.Exporter({"backend": "mock", "sm_util_source": "bogus"})
+
+
+def test_pod_energy_counter_starts_at_allocation(mock_exporter):
+    """container_gpu_energy_joules_total: the GPU's socket energy since the pod got it."""
+    ex = mock_exporter(n_gpus=1, hz=200, mock={"util_base": 60, "util_amp": 0.0001, "fw_period_s": 0.005})
+    time.sleep(0.3)
+    e0 = parse_text(ex.render())["amdgpu_energy_joules_total"][0][1]
+    ex.set_device_owners(0, [{"pod": "p", "namespace": "ml", "container": "c"}])
+    time.sleep(0.5)
+    m = parse_text(ex.render())
+    (lb, e_pod), = m["container_gpu_energy_joules_total"]
+    e1 = m["amdgpu_energy_joules_total"][0][1]
+    assert lb["pod_name"] == "p" and e_pod > 0
+    assert e_pod == pytest.approx(e1 - e0, rel=0.05, abs=1.0)  # counted from the allocation, not exporter start
+    assert e_pod < e1
+
+
+def test_report_energy_column_tiles_the_window(mock_exporter):
+    """gpu-util-stats --energy: the per-step increase() of the per-pod energy counter,
+    first range point (the step before the window) left out, adds up to the energy the
+    pod's GPU drew over the window."""
+    ex = mock_exporter(n_gpus=2, hz=200, node_name="node-a",
+                       mock={"util_base": 60, "util_amp": 0.0001, "fw_period_s": 0.005})
+    ex.set_device_owners(0, [{"pod": "two", "namespace": "ml", "container": "c"}])
+    ex.set_device_owners(1, [{"pod": "two", "namespace": "ml", "container": "c"}])
+    sc = Scraper("127.0.0.1", ex.port)
+    fp = FakeProm()
+    url = fp.start()
+    try:
+        stamps = []
+        t0 = time.time()
+        for k in range(18):  # every 0.25 s for 4.25 s
+            time.sleep(max(0.0, t0 + 0.25 * k - time.time()))
+            ts = time.time()
+            fp.ingest(parse_text(sc.get()), ts)
+            stamps.append(ts)
+        end, window, step = stamps[-1], 3, 1
+        kwh = G.pod_energy_kwh(PromClient(url), end - window, end, step)
+        assert list(kwh) == [("node-a", "two")]
+
+        def joules_at(t):  # both GPUs' counters, linear between scrapes
+            tot = 0.0
+            for key, pts in fp.series[G.ENERGY_METRIC].items():
+                for (ta, va), (tb, vb) in zip(pts, pts[1:]):
+                    if ta <= t <= tb:
+                        tot += va + (vb - va) * (t - ta) / (tb - ta)
+            return tot
+        want = joules_at(end) - joules_at(end - window)
+        assert want > 0 and kwh[("node-a", "two")] * 3.6e6 == pytest.approx(want, rel=0.05)
+        rows = G.add_energy([["node-a", "two", 2, 60.0], ["node-a", "gone (finished)", 0, 0.0]], kwh)
+        assert rows[0][4] == kwh[("node-a", "two")] and rows[1][4] == 0.0
+        table = G.format_rows(rows, "pod", "table", compat=False, extras=["Energy kWh"])
+        assert "Energy kWh" in table and "TOTAL" in table
+    finally:
+        fp.stop()
