@@ -622,13 +622,19 @@ def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
         # the load loop pauses for every scrape + ingest (≈ms each, 4 per second), and a 1 s
         # rate() range of a counter that moves in ≈20 ms PMFW steps is good to a few per cent
         assert rows[0][3] > 80, rows
+        # --energy: the pod's GPU energy over the 2 s window, as mean watts ≈ the socket power
+        kwh = G.pod_energy_kwh(PromClient(url), end - 2, end, 1)
+        watts = kwh[("gpu-node-1", "train-0")] * 3.6e6 / 2
+        pw = m["amdgpu_power_watts"][0][1]
+        assert 300 < watts < 1600 and watts == pytest.approx(pw, rel=0.25), (watts, pw)
         import io
 
         out = io.StringIO()
         crow = G.run_report(PromClient(url), qc, end, 2, 1, compat=True, out=out)
         assert [r[:3] for r in crow] == [["gpu-node-1", "train-0", "1"]], crow  # reference's string cards
         assert crow[0][3] > 80, crow
-        print(json.dumps({"gauge": v, "busy_seconds": busy, "fixed": rows, "compat": crow}))
+        print(json.dumps({"gauge": v, "busy_seconds": busy, "fixed": rows, "compat": crow, "pod_watts": watts,
+                          "power_w": pw}))
     finally:
         fp.stop()
         try:
