@@ -112,7 +112,7 @@ def parse_args(argv=None):
                     "full-rate ring holds ≈1 s at 8 kHz)")
     ap.add_argument("--burst-ms", type=float, default=1.0, help="phase R: length of one burst")
     ap.add_argument("--burst-period-ms", type=float, default=5.0, help="phase R: burst period")
-    ap.add_argument("--capacity-hz", default="16000,24000",
+    ap.add_argument("--capacity-hz", default="16000,24000,32000",
                     help="phase S: tick rates above --hz to try under the load, one block each ('' = off)")
     ap.add_argument("--quiet-s", type=float, default=1.5,
                     help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
@@ -827,8 +827,14 @@ def capacity(ctx, load, exp, a) -> dict:
     rates = [float(x) for x in str(a.capacity_hz).split(",") if x.strip()]
     if not rates:
         return {}
-    out: dict = {"block_steps": a.block_steps, "rates": {}}
+    out: dict = {"block_steps": a.block_steps, "mode": "profiling (--pmc-idle-hz 0: every tick READs)",
+                 "rates": {}}
     best = None
+    # Profiling mode: a GPU idle at a block edge would otherwise be READ at the idle
+    # rate until its first busy READ, which is the adaptive rate at work, not capacity.
+    idle_hz = exp.set_idle_hz(-1) if exp is not None else 0.0
+    if exp is not None:
+        exp.set_idle_hz(0)
     for hz in [a.hz] + rates:
         w0 = 0.0
         before: dict = {}
@@ -860,6 +866,7 @@ def capacity(ctx, load, exp, a) -> dict:
             best = hz if best is None else max(best, hz)
     if exp is not None:
         exp.set_rate(a.hz)
+        exp.set_idle_hz(idle_hz)
     out["max_rate_hz_98pct"] = best
     return out
 

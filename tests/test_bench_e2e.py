@@ -89,7 +89,7 @@ def test_bench_contract_single_process():
     assert set(q["adaptive"]["per_gpu"]["0"]) == {"reads_per_s", "pmfw_gfx_busy_pct", "gpu_active_pct"}
     # phase S plumbing: the primary rate and each capacity rate got a block, rate restored after
     cap = res["capacity"]
-    assert list(cap["rates"]) == ["8000", "16000", "24000"]
+    assert list(cap["rates"]) == ["8000", "16000", "24000", "32000"]
     for row in cap["rates"].values():
         assert row["sample_source"] == "pmc" and row["samples_per_sec_per_gpu"]["0"] > 0
         assert row["host_us_per_drain"] > 0
