@@ -110,6 +110,12 @@ struct Agent {
   uint32_t pcmd_sz = 0, pout_sz = 0;                 // allocated sizes of the slot buffers
   std::vector<hsa_ven_amd_aqlprofile_event_t> pipe_events;  // event list the slot packets were built for
   int64_t psubmit_ns[2] = {0, 0};
+  // KGS_AQL_PROFILE=<n>: CP timestamps of every pipelined READ (queue profiling on):
+  // queueing delay (submit → CP start) and execution (start → end), reported on
+  // stderr every n READs.  How long the CP makes a READ wait says how busy it
+  // is dispatching other queues' work (profiles/launch_overhead.md).
+  uint64_t prof_n = 0, prof_bad = 0;
+  int64_t prof_q_sum = 0, prof_q_max = 0, prof_x_sum = 0, prof_x_max = 0;
   int inflight = -1;                                 // slot with a READ on the queue, -1 none
   int64_t rtt_ns = 0;                                // CP round trip of a synchronous READ (EWMA)
   uint64_t ready_on_poll = 0, waited_on_poll = 0;    // pipelined: READ already done / had to wait
@@ -311,6 +317,38 @@ int queue_priority() {
     return static_cast<int>(HSA_AMD_QUEUE_PRIORITY_NORMAL);
   }();
   return v;
+}
+
+// KGS_AQL_PROFILE=<n>: report READ timestamps every n pipelined READs (0/unset = off).
+uint64_t profile_every() {
+  static const uint64_t n = [] {
+    const char* e = std::getenv("KGS_AQL_PROFILE");
+    return e ? std::strtoull(e, nullptr, 10) : 0ull;
+  }();
+  return n;
+}
+bool profile_ts() { return profile_every() > 0; }
+// HSA system clock → CLOCK_MONOTONIC ns, calibrated once (HSA timestamps are
+// ticks at HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY).
+struct ClockMap {
+  double ns_per_tick = 1.0;
+  int64_t off = 0;
+  bool ok = false;
+};
+const ClockMap& hsa_clock() {
+  static const ClockMap m = [] {
+    ClockMap c;
+    uint64_t f = 0, t = 0;
+    if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) != HSA_STATUS_SUCCESS || f == 0) return c;
+    const int64_t m0 = mono_ns();
+    hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t);
+    const int64_t m1 = mono_ns();
+    c.ns_per_tick = 1e9 / static_cast<double>(f);
+    c.off = (m0 + m1) / 2 - static_cast<int64_t>(static_cast<double>(t) * c.ns_per_tick);
+    c.ok = true;
+    return c;
+  }();
+  return m;
 }
 
 // Put one PM4-IB vendor packet on the agent's private queue (no wait).
@@ -590,6 +628,32 @@ int read_pipelined(Agent* a, int64_t* ts) {
       return -2;
     }
   }
+  if (profile_ts()) {
+    hsa_amd_profiling_dispatch_time_t t{};
+    const ClockMap& c = hsa_clock();
+    if (c.ok && hsa_amd_profiling_get_dispatch_time(a->agent, a->psig[k], &t) == HSA_STATUS_SUCCESS && t.start &&
+        t.end >= t.start) {
+      const int64_t st = static_cast<int64_t>(static_cast<double>(t.start) * c.ns_per_tick) + c.off;
+      const int64_t q = st - a->psubmit_ns[k], x = static_cast<int64_t>(static_cast<double>(t.end - t.start) * c.ns_per_tick);
+      ++a->prof_n;
+      a->prof_q_sum += q;
+      a->prof_x_sum += x;
+      a->prof_q_max = std::max(a->prof_q_max, q);
+      a->prof_x_max = std::max(a->prof_x_max, x);
+    } else {
+      ++a->prof_bad;
+    }
+    if (a->prof_n + a->prof_bad >= profile_every()) {
+      const double n = a->prof_n ? static_cast<double>(a->prof_n) : 1.0;
+      std::fprintf(stderr,
+                   "kgs-aql-prof t=%.3f reads=%llu no_ts=%llu qdelay_us mean=%.2f max=%.1f exec_us mean=%.2f "
+                   "max=%.1f\n",
+                   mono_ns() * 1e-9, static_cast<unsigned long long>(a->prof_n), static_cast<unsigned long long>(a->prof_bad),
+                   a->prof_q_sum / n / 1e3, a->prof_q_max / 1e3, a->prof_x_sum / n / 1e3, a->prof_x_max / 1e3);
+      a->prof_n = a->prof_bad = 0;
+      a->prof_q_sum = a->prof_q_max = a->prof_x_sum = a->prof_x_max = 0;
+    }
+  }
   const int rc = fold(a, &a->pprof[k]);
   if (ts) *ts = a->psubmit_ns[k] + a->rtt_ns / 2;
   const int n = k ^ 1;
@@ -746,6 +810,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
         set_err(err, errlen, "hsa_queue_create failed");
         return -1;
       }
+      if (profile_ts()) hsa_amd_profiling_set_profiler_enabled(a->queue, 1);
       if (queue_priority() >= 0 &&
           hsa_amd_queue_set_priority(a->queue, static_cast<hsa_amd_queue_priority_t>(queue_priority())) !=
               HSA_STATUS_SUCCESS)

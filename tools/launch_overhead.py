@@ -95,6 +95,10 @@ def main() -> int:
             env["KGS_AQL_SIGNAL"] = opts["signal"]
         if "prio" in opts:
             env["KGS_AQL_PRIORITY"] = opts["prio"]
+        if "prof" in opts:
+            env["KGS_AQL_PROFILE"] = opts["prof"]
+        if "idle" in opts:
+            cmd += ["--pmc-idle-hz", opts["idle"]]
         pr = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
         ready = json.loads(pr.stdout.readline())
         assert ready.get("event") == "ready", ready
@@ -107,12 +111,22 @@ def main() -> int:
 
     def measure(name, hz=None, pmc_set="base", pmc="aqlprofile", lean=0, opts=None):
         pr = exporter(hz, pmc_set, pmc, lean, opts) if hz else None
+
+        def mark(what):  # CLOCK_MONOTONIC marks to line up the reader's KGS_AQL_PROFILE lines
+            print(f"phase-mark {name}/{what} t={time.monotonic():.3f}", file=sys.stderr, flush=True)
+
         try:
+            mark("eager")
+            e = rate()
+            mark("graph")
+            g = graph_rate()
             r = {"phase": name, "hz": hz or 0, "pmc": pmc if hz else "", "set": pmc_set if hz else "", "lean": lean,
-                 "eager_kernels_per_s": rate(), "graph_kernels_per_s": graph_rate()}
+                 "eager_kernels_per_s": e, "graph_kernels_per_s": g}
             if pr is not None and pmc != "none":
+                mark("mfma")
                 r["observed"] = observe(pr.port)
                 r["pmc_info"] = pr.info[:400]
+            mark("end")
         finally:
             if pr is not None:
                 pr.stdin.write("quit\n")
@@ -124,7 +138,8 @@ def main() -> int:
     # spec hz:set:reader[:lean[:key=value...]]   keys: proc=<proc-every> (0 = no per-process tier),
     # slack=<ns> (sampler timer slack), fence=sys|agent|none (AQL header fences of the
     # reader's packets), signal=interrupt|poll (READ completion signals), prio=low|normal|high
-    # (READ queue priority); "off" = no exporter
+    # (READ queue priority), prof=<n> (CP timestamps of every READ: queueing delay and execution
+    # time on stderr every n READs), idle=<hz> (--pmc-idle-hz; 0 = READ every tick); "off" = no exporter
     specs = sys.argv[1:] or ["100:base:aqlprofile", "1000:base:aqlprofile", "8000:base:aqlprofile",
                              "100:full:aqlprofile", "1000:full:aqlprofile", "1000:base:none"]
     # The first exporter started in a fresh box slowed the graph replay by ≈38 % in
