@@ -188,6 +188,12 @@ CATALOG: tuple[Family, ...] = (
       "self"),
     F("kgs_scrape_render_last_seconds", "gauge", "Render time of the previous scrape.", ("kubernetes_io_hostname",),
       "self"),
+    F("kgs_http_connections", "gauge", "HTTP connections held open by the exporter.", ("kubernetes_io_hostname",),
+      "self"),
+    F("kgs_http_connections_closed_total", "counter",
+      "HTTP connections the exporter closed itself: idle past --http-idle-s (reason=idle) or evicted, least "
+      "recently active first, to admit one past --http-max-conns (reason=limit).",
+      ("kubernetes_io_hostname", "reason"), "self"),
     F("kgs_build_info", "gauge", "Build / configuration (1).",
       ("kubernetes_io_hostname", "version", "backend", "pmc_source", "sample_hz"), "self"),
     # ---- attribution loop (Python control plane, pushed via set_extra_metrics) ---------------

@@ -79,6 +79,12 @@ struct ExporterConfig {
   // Off by default: level 1 costs ≈0.6 ms per 8-GPU page (≈117 KB → 11 KB), about
   // eight times the render; worth it only where scrape bandwidth is scarce.
   int gzip_level = 0;
+  // HTTP connection hygiene: a keep-alive connection idle this long is closed (a
+  // scraper reconnects on its next scrape; 0 = never), and at most this many are
+  // held at once — past it the least recently active one is closed, so a client
+  // that opens connections and never reads cannot exhaust the exporter's fds.
+  double http_idle_s = 300.0;
+  int http_max_conns = 256;
 };
 
 class HttpServer;
@@ -140,6 +146,9 @@ class Exporter {
   std::atomic<uint64_t> render_ns_total{0};
   std::atomic<uint64_t> render_ns_last{0};
   std::atomic<uint64_t> http_requests{0};
+  std::atomic<uint64_t> http_conns_open{0};
+  std::atomic<uint64_t> http_closed_idle{0};   // closed after http_idle_s without traffic
+  std::atomic<uint64_t> http_closed_limit{0};  // evicted to admit a connection past http_max_conns
   std::atomic<size_t> last_render_bytes_{64 * 1024};  // sizes the next render's buffer
   std::atomic<bool> pmc_wanted_{true};
 

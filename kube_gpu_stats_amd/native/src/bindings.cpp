@@ -85,6 +85,8 @@ ExporterConfig parse_config(const py::dict& d) {
   c.pcie_bytes_per_acc_unit = get<double>(d, "pcie_bytes_per_acc_unit", c.pcie_bytes_per_acc_unit);
   c.control_http = get<bool>(d, "control_http", c.control_http);
   c.gzip_level = get<int>(d, "gzip_level", c.gzip_level);
+  c.http_idle_s = get<double>(d, "http_idle_s", c.http_idle_s);
+  c.http_max_conns = get<int>(d, "http_max_conns", c.http_max_conns);
   return c;
 }
 
@@ -357,6 +359,9 @@ class PyExporter {
     o["render_ns_total"] = ex_.render_ns_total.load();
     o["render_ns_last"] = ex_.render_ns_last.load();
     o["http_requests"] = ex_.http_requests.load();
+    o["http_conns_open"] = ex_.http_conns_open.load();
+    o["http_closed_idle"] = ex_.http_closed_idle.load();
+    o["http_closed_limit"] = ex_.http_closed_limit.load();
     return o;
   }
   bool healthy() const { return ex_.healthy(); }

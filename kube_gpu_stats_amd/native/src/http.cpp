@@ -16,6 +16,7 @@
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <unordered_map>
 
 #include "kgs/exporter.h"
@@ -30,7 +31,14 @@ struct Conn {
   size_t out_off = 0;
   bool close_after = false;
   bool loopback = false;  // peer is 127.0.0.0/8 or ::1: may use /control/*
+  int64_t active_ns = 0;  // last byte received or sent (idle timeout, eviction order)
 };
+
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
 
 bool peer_is_loopback(const sockaddr_storage& a) {
   if (a.ss_family == AF_INET)
@@ -206,11 +214,16 @@ void HttpServer::loop() {
     epoll_ctl(efd_, EPOLL_CTL_DEL, fd, nullptr);
     close(fd);
     conns.erase(fd);
+    ex_->http_conns_open.store(conns.size(), std::memory_order_relaxed);
   };
+  const ExporterConfig& cfg = ex_->config();
+  const int64_t idle_ns = cfg.http_idle_s > 0 ? static_cast<int64_t>(cfg.http_idle_s * 1e9) : 0;
+  const size_t max_conns = cfg.http_max_conns > 0 ? static_cast<size_t>(cfg.http_max_conns) : 0;
+  int64_t next_sweep = mono_ns();
   auto flush = [&](int fd, Conn& c) -> bool {  // false = connection gone
     while (c.out_off < c.out.size()) {
       const ssize_t n = send(fd, c.out.data() + c.out_off, c.out.size() - c.out_off, MSG_NOSIGNAL);
-      if (n > 0) { c.out_off += static_cast<size_t>(n); continue; }
+      if (n > 0) { c.out_off += static_cast<size_t>(n); c.active_ns = mono_ns(); continue; }
       if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
         epoll_event ev{};
         ev.events = EPOLLIN | EPOLLOUT;
@@ -242,18 +255,30 @@ void HttpServer::loop() {
           socklen_t plen = sizeof peer;
           const int c = accept4(lfd_, reinterpret_cast<sockaddr*>(&peer), &plen, SOCK_NONBLOCK | SOCK_CLOEXEC);
           if (c < 0) break;
+          if (max_conns > 0 && conns.size() >= max_conns) {  // evict the least recently active
+            auto lru = conns.begin();
+            for (auto jt = conns.begin(); jt != conns.end(); ++jt)
+              if (jt->second.active_ns < lru->second.active_ns) lru = jt;
+            drop(lru->first);
+            ex_->http_closed_limit.fetch_add(1, std::memory_order_relaxed);
+          }
           int one = 1;
           setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
           epoll_event ev{};
           ev.events = EPOLLIN;
           ev.data.fd = c;
           epoll_ctl(efd_, EPOLL_CTL_ADD, c, &ev);
-          conns[c].loopback = peer_is_loopback(peer);
+          Conn& nc = conns[c];
+          nc.loopback = peer_is_loopback(peer);
+          nc.active_ns = mono_ns();
+          ex_->http_conns_open.store(conns.size(), std::memory_order_relaxed);
         }
         continue;
       }
       auto it = conns.find(fd);
-      if (it == conns.end()) { close(fd); continue; }
+      // Dropped earlier in this batch (evicted): its fd is closed and off the epoll
+      // set already, and the number may belong to a newer connection or file.
+      if (it == conns.end()) continue;
       Conn& c = it->second;
       if (evs[i].events & EPOLLOUT) {
         if (!flush(fd, c)) continue;
@@ -264,7 +289,7 @@ void HttpServer::loop() {
       bool gone = false;
       for (;;) {
         const ssize_t r = recv(fd, buf, sizeof buf, 0);
-        if (r > 0) { c.in.append(buf, static_cast<size_t>(r)); if (c.in.size() > (1u << 16)) { gone = true; break; } continue; }
+        if (r > 0) { c.active_ns = mono_ns(); c.in.append(buf, static_cast<size_t>(r)); if (c.in.size() > (1u << 16)) { gone = true; break; } continue; }
         if (r == 0) { gone = true; break; }
         if (errno == EAGAIN || errno == EWOULDBLOCK) break;
         gone = true;
@@ -284,8 +309,7 @@ void HttpServer::loop() {
         const size_t q = target.find('?');
         if (q != std::string::npos) { query = target.substr(q + 1); target.resize(q); }
         const bool http10 = req.find("HTTP/1.0") != std::string::npos;
-        const bool conn_close = req.find("Connection: close") != std::string::npos ||
-                                req.find("connection: close") != std::string::npos;
+        const bool conn_close = header_has(req, "Connection", "close");
         c.close_after = conn_close || (http10 && req.find("eep-Alive") == std::string::npos);
         if (method != "GET" && method != "HEAD") {
           respond(c, 405, "Method Not Allowed", "text/plain", "only GET\n");
@@ -349,8 +373,22 @@ void HttpServer::loop() {
       }
       if (gone && conns.count(fd)) drop(fd);
     }
+    // Idle sweep after the batch (at most twice a second, O(connections)), so no
+    // event of this batch refers to a connection closed under it.
+    const int64_t now = mono_ns();
+    if (idle_ns > 0 && now >= next_sweep) {
+      next_sweep = now + 500000000LL;
+      std::vector<int> idle;
+      for (const auto& kvp : conns)
+        if (now - kvp.second.active_ns >= idle_ns) idle.push_back(kvp.first);
+      for (int fd : idle) {
+        drop(fd);
+        ex_->http_closed_idle.fetch_add(1, std::memory_order_relaxed);
+      }
+    }
   }
   for (auto& kvp : conns) close(kvp.first);
+  ex_->http_conns_open.store(0, std::memory_order_relaxed);
 }
 
 }  // namespace kgs

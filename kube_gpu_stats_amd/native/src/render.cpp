@@ -692,6 +692,12 @@ void Exporter::render(std::string& out) {
   w.line("kgs_scrape_render_seconds_total", nl, nullptr, render_ns_total.load() * 1e-9);
   w.head("kgs_scrape_render_last_seconds", "gauge", "Render time of the previous scrape");
   w.line("kgs_scrape_render_last_seconds", nl, nullptr, render_ns_last.load() * 1e-9);
+  w.head("kgs_http_connections", "gauge", "HTTP connections held open by the exporter");
+  w.line_u("kgs_http_connections", nl, nullptr, http_conns_open.load());
+  w.head("kgs_http_connections_closed_total", "counter",
+         "HTTP connections the exporter closed itself: idle past --http-idle-s, or evicted past --http-max-conns");
+  w.line_u("kgs_http_connections_closed_total", nl, "reason=\"idle\"", http_closed_idle.load());
+  w.line_u("kgs_http_connections_closed_total", nl, "reason=\"limit\"", http_closed_limit.load());
   w.head("kgs_build_info", "gauge", "Exporter build / configuration (value 1)");
   {
     std::string lb = nl;

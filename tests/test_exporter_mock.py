@@ -586,3 +586,37 @@ def test_throttle_seconds_by_reason(mock_exporter):
     m = parse_text(ex.render())
     rs = {lb["reason"]: v for lb, v in m["amdgpu_throttle_seconds_total"]}
     assert set(rs) == {"prochot", "ppt", "socket_thermal", "vr_thermal", "hbm_thermal"} and rs["ppt"] > 0.2
+
+
+def test_http_connection_cap_and_idle_timeout(mock_exporter):
+    """Clients that connect and never send cannot hold the exporter's fds: past
+    http_max_conns the least recently active connection is closed, and an idle
+    keep-alive connection is closed after http_idle_s; scrapes keep working."""
+    import socket
+
+    ex = mock_exporter(n_gpus=1, http_max_conns=4, http_idle_s=1.0)
+    port = ex.port
+    socks = []
+    for _ in range(6):
+        s = socket.create_connection(("127.0.0.1", port), timeout=5)
+        socks.append(s)
+        time.sleep(0.05)  # distinct activity times: eviction order is defined
+    # the two oldest were evicted to admit the 5th and 6th: they read EOF
+    for s in socks[:2]:
+        assert s.recv(1) == b""
+    socks[-1].sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
+    head = socks[-1].recv(65536)
+    assert head.startswith(b"HTTP/1.1 200"), head[:64]
+    m = parse_text(get(port, "/metrics").read().decode())  # a 7th connection: evicts one more
+    closed = {lb["reason"]: v for lb, v in m["kgs_http_connections_closed_total"]}
+    assert closed["limit"] == 3 and closed["idle"] == 0
+    assert m["kgs_http_connections"][0][1] == 4
+    time.sleep(2.2)  # idle timeout 1 s, sweep every 0.5 s
+    for s in socks[2:]:
+        assert s.recv(1) == b""  # every silent connection was closed
+        s.close()
+    m = parse_text(get(port, "/metrics").read().decode())
+    closed = {lb["reason"]: v for lb, v in m["kgs_http_connections_closed_total"]}
+    assert closed["idle"] >= 3 and closed["limit"] == 3
+    st = ex.stats()
+    assert st["http_closed_idle"] >= 3 and st["http_closed_limit"] == 3
