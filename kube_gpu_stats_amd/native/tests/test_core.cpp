@@ -14,10 +14,19 @@
 //     name changes (render caches under the exporter mutex), the counters are
 //     handed over and taken back, and a square load flips the devices between
 //     quiet (idle READ rate, changed at run time) and busy.
+//  7. HTTP server: keep-alive, pipelined requests split at random bytes, HEAD,
+//     gzip, bad methods / targets, oversized requests, and silent clients
+//     (evicted past the connection cap, closed when idle).
 //  5. PMFW table parser fuzz (ASAN build): random, truncated and mutated
 //     v1.8-shaped buffers, each in an exactly-sized heap block so any read past
 //     `len` is caught; the parser must reject or parse, never overrun.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <string>
 #include <cstdio>
@@ -364,7 +373,155 @@ static void test_exporter_concurrent() {
   std::printf("exporter concurrent ok (%d renders, %d streams)\n", renders.load(), streams.load());
 }
 
+// ---- 7. HTTP server ---------------------------------------------------------
+static int http_connect(int port) {
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  CHECK(fd >= 0);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons(static_cast<uint16_t>(port));
+  sa.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  CHECK(connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0);
+  timeval tv{5, 0};
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  return fd;
+}
+
+static void http_send(int fd, const std::string& s) {
+  size_t off = 0;
+  while (off < s.size()) {
+    const ssize_t n = send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+    if (n <= 0) return;  // the server may close first (oversized request)
+    off += static_cast<size_t>(n);
+  }
+}
+
+// Read `n` complete responses (status line + headers + Content-Length body; HEAD
+// responses carry no body).  Returns the status codes; fewer on EOF / timeout.
+static std::vector<int> http_read(int fd, int n, bool head, std::string* last_headers = nullptr) {
+  std::vector<int> codes;
+  std::string buf;
+  char tmp[8192];
+  while (static_cast<int>(codes.size()) < n) {
+    const size_t he = buf.find("\r\n\r\n");
+    if (he != std::string::npos) {
+      const std::string hdr = buf.substr(0, he);
+      size_t len = 0;
+      const size_t cl = hdr.find("Content-Length: ");
+      if (cl != std::string::npos) len = std::strtoul(hdr.c_str() + cl + 16, nullptr, 10);
+      if (head) len = 0;
+      if (buf.size() >= he + 4 + len) {
+        codes.push_back(std::atoi(hdr.c_str() + 9));
+        if (last_headers) *last_headers = hdr;
+        buf.erase(0, he + 4 + len);
+        continue;
+      }
+    }
+    const ssize_t r = recv(fd, tmp, sizeof tmp, 0);
+    if (r <= 0) break;
+    buf.append(tmp, static_cast<size_t>(r));
+  }
+  return codes;
+}
+
+// The server closed the connection (an oversized request may end in a reset:
+// the client's unread bytes are still in flight when the server closes).
+static bool http_eof(int fd) {
+  char c;
+  const ssize_t r = recv(fd, &c, 1, 0);
+  return r == 0 || (r < 0 && errno == ECONNRESET);
+}
+
+// The epoll server under the sanitizer: keep-alive, pipelined requests split at
+// arbitrary byte boundaries, HEAD, gzip, unknown methods and targets, oversized
+// requests, and clients that connect and never send (evicted past
+// http_max_conns, closed after http_idle_s) — while the samplers publish and the
+// renders run on the server thread.
+static void test_http_server() {
+  ExporterConfig c;
+  c.backend = "mock";
+  c.mock.n_gpus = 2;
+  c.sampler.hz = 1000;
+  c.sampler.pin_numa = false;
+  c.pmc_source = "mock";
+  c.listen_addr = "127.0.0.1";
+  c.port = 0;
+  c.node_name = "node-h";
+  c.gzip_level = 1;
+  c.http_max_conns = 8;
+  c.http_idle_s = 0.3;
+  Exporter ex(c);
+  CHECK(ex.init());
+  ex.start();
+  const int port = ex.port();
+  CHECK(port > 0);
+  {  // silent clients first (alone, so no active client is the least recently used):
+     // past the cap the least recently active go, the rest once idle for 0.3 s
+    std::vector<int> fds;
+    for (int i = 0; i < 12; ++i) {
+      fds.push_back(http_connect(port));
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+    for (int fd : fds) {
+      CHECK(http_eof(fd));
+      close(fd);
+    }
+    CHECK(ex.http_closed_limit.load() == 4 && ex.http_closed_idle.load() == 8);
+  }
+  std::atomic<int> ok{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 3; ++t)
+    th.emplace_back([&, t] {
+      std::mt19937 rng(1234 + t);
+      for (int i = 0; i < 25; ++i) {
+        const int fd = http_connect(port);
+        // two pipelined requests, split at a random byte
+        const std::string two =
+            "GET /metrics HTTP/1.1\r\nHost: x\r\n\r\nGET /healthz?x=1 HTTP/1.1\r\nHost: x\r\n\r\n";
+        const size_t cut = rng() % two.size();
+        http_send(fd, two.substr(0, cut));
+        std::this_thread::sleep_for(std::chrono::microseconds(rng() % 500));
+        http_send(fd, two.substr(cut));
+        std::vector<int> codes = http_read(fd, 2, false);
+        CHECK(codes.size() == 2 && codes[0] == 200 && codes[1] == 200);
+        http_send(fd, "HEAD /metrics HTTP/1.1\r\n\r\n");
+        codes = http_read(fd, 1, true);
+        CHECK(codes.size() == 1 && codes[0] == 200);
+        std::string hdr;
+        http_send(fd, "GET /metrics HTTP/1.1\r\naccept-encoding: gzip, deflate\r\n\r\n");
+        codes = http_read(fd, 1, false, &hdr);
+        CHECK(codes.size() == 1 && codes[0] == 200 && hdr.find("Content-Encoding: gzip") != std::string::npos);
+        http_send(fd, "POST /metrics HTTP/1.1\r\n\r\nGET /nope HTTP/1.1\r\n\r\nGET /counters?gpu=7&n=99999 HTTP/1.1\r\n\r\n");
+        codes = http_read(fd, 3, false);
+        CHECK(codes.size() == 3 && codes[0] == 405 && codes[1] == 404 && codes[2] == 200);
+        http_send(fd, "GET /devices HTTP/1.1\r\nConnection: close\r\n\r\n");
+        codes = http_read(fd, 1, false);
+        CHECK(codes.size() == 1 && codes[0] == 200 && http_eof(fd));
+        close(fd);
+        ++ok;
+      }
+    });
+  th.emplace_back([&] {  // oversized request without an end of headers: dropped
+    for (int i = 0; i < 5; ++i) {
+      const int fd = http_connect(port);
+      http_send(fd, "GET /metrics HTTP/1.1\r\nX: " + std::string(70000, 'a'));
+      CHECK(http_eof(fd));
+      close(fd);
+    }
+  });
+  for (auto& t : th) t.join();
+  CHECK(ok.load() == 75);
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  CHECK(ex.http_conns_open.load() == 0);
+  ex.stop();
+  std::printf("http server ok (%llu requests, %llu evicted, %llu idle-closed)\n",
+              static_cast<unsigned long long>(ex.http_requests.load()),
+              static_cast<unsigned long long>(ex.http_closed_limit.load()),
+              static_cast<unsigned long long>(ex.http_closed_idle.load()));
+}
+
 int main() {
+  test_http_server();
   test_exporter_concurrent();
   test_parser_fuzz();
   test_seqlock();
