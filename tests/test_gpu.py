@@ -1017,3 +1017,87 @@ def test_throttle_residency_under_load_and_idle(N, torch_dev):
     print(json.dumps(out))
     assert all(v < 0.05 for k, v in out["idle"].items() if k != "power_w"), out
     assert out["load"]["ppt"] > 0.3, out
+
+
+_TENANT = r"""
+import sys, time
+sys.path.insert(0, sys.argv[4])
+import torch
+from kube_gpu_stats_amd.ops.load import LoadStep
+gib, busy, secs = int(sys.argv[1]), sys.argv[2] == "1", float(sys.argv[3])
+x = torch.empty(gib << 30, dtype=torch.uint8, device="cuda")
+x.fill_(1)
+ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 26) if busy else None
+if ls is not None:
+    ls.run_mfma()
+torch.cuda.synchronize()
+print("ready", flush=True)
+t0 = time.time()
+while time.time() - t0 < secs:
+    if ls is not None:
+        ls.run_mfma()
+        torch.cuda.synchronize()
+    else:
+        time.sleep(0.05)
+print("done", flush=True)
+"""
+
+
+def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
+    """BASELINE config 3 on hardware: two processes share the GPU — tenant A runs a
+    full-grid MFMA loop holding 8 GiB, tenant B sits idle holding 3 GiB.  The
+    node-wide slow tier's process list attributes HBM to each (to ±0.75 GiB) and
+    the CU-occupancy integral gives A the compute share and B none; each process
+    line carries its own pod once the PID→pod table names them.  AMD SMI reports
+    host PIDs, so the tenants are found by their HBM."""
+    import select
+
+    import torch
+
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    env = dict(os.environ, KGS_NO_BUILD="1")
+    kids = [subprocess.Popen([sys.executable, "-c", _TENANT, gib, busy, "12", REPO], stdout=subprocess.PIPE,
+                             text=True, env=env) for gib, busy in (("8", "1"), ("3", "0"))]
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 50, "proc_period_s": 0.1, "link_every": 0})
+    ex.start()
+    try:
+        for k in kids:  # both tenants hold their memory (and A runs) before the window opens
+            end = time.time() + 120
+            line = ""
+            while time.time() < end and "ready" not in line:
+                r, _, _ = select.select([k.stdout], [], [], 1.0)
+                if r:
+                    line = k.stdout.readline()
+                assert k.poll() is None, "tenant exited early"
+            assert "ready" in line
+        time.sleep(0.6)
+        p0, t0 = {p["pid"]: p for p in ex.procs(0)}, time.time()
+        time.sleep(3.0)
+        p1, t1 = {p["pid"]: p for p in ex.procs(0)}, time.time()
+        gib = float(1 << 30)
+        a = [pid for pid, p in p1.items() if 8.0 <= p["vram_bytes"] / gib < 8.75]
+        b = [pid for pid, p in p1.items() if 3.0 <= p["vram_bytes"] / gib < 3.75]
+        row = {"procs": {pid: {"vram_gib": round(p["vram_bytes"] / gib, 3), "cu_occupancy": p["cu_occupancy"],
+                               "cu_share": round((p["cu_seconds"] - p0.get(pid, {}).get("cu_seconds", 0.0)) / (t1 - t0), 4)}
+                         for pid, p in p1.items()}}
+        print(json.dumps(row))
+        assert len(a) == 1 and len(b) == 1, row
+        share = {t: row["procs"][pid]["cu_share"] for t, pid in (("a", a[0]), ("b", b[0]))}
+        # KFD's cu_occupancy is an instantaneous wave count in CU units (r1: 0..256 under
+        # the MFMA loop, mean share ≈ 0.5 with the per-call syncs): A well above B.
+        assert share["a"] > 0.25 and share["b"] < 0.02, row
+        ex.set_pid_owners({(0, a[0]): {"pod": "tenant-a", "namespace": "ml", "container": "main", "pod_uid": "ua"},
+                           (0, b[0]): {"pod": "tenant-b", "namespace": "ml", "container": "main", "pod_uid": "ub"}})
+        body = ex.render()
+    finally:
+        ex.stop()
+        for k in kids:
+            k.kill()
+            k.wait()
+    lines = [ln for ln in body.splitlines() if ln.startswith("amdgpu_process_hbm_bytes{")]
+    la = [ln for ln in lines if f'pid="{a[0]}"' in ln]
+    lb = [ln for ln in lines if f'pid="{b[0]}"' in ln]
+    assert len(la) == 1 and 'pod="tenant-a"' in la[0], lines
+    assert len(lb) == 1 and 'pod="tenant-b"' in lb[0], lines
+    _keep("two_tenants.json", json.dumps(row, indent=1))
