@@ -107,6 +107,9 @@ CATALOG: tuple[Family, ...] = (
       "accumulator × MI355X calibration (105.7 B/unit; H2D 102.65, D2H 108.74 measured, ±3 %; profiles/r2/pcie/)."),
     F("amdgpu_pcie_bandwidth_acc_total", "counter", "Raw PMFW PCIe bandwidth accumulator (amdsmi pcie_bandwidth_acc)."),
     # ---- RAS / link health -------------------------------------------------------------------
+    F("amdgpu_ecc_block_errors_total", "counter",
+      "Accumulated ECC errors per RAS block (umc = HBM, gfx, xgmi_wafl, ...) and type, for the blocks with ECC enabled.",
+      extra=("block", "type"), source="amdsmi", tier="slow"),
     F("amdgpu_ecc_errors_total", "counter", "Accumulated ECC errors by type.", extra=("type",), source="amdsmi",
       tier="slow"),
     F("amdgpu_xgmi_error_status", "gauge", "xGMI error status (0 none, 1 error, 2 multiple).", source="amdsmi",

@@ -64,10 +64,18 @@ struct LinkInfo {
 };
 
 // RAS / link health (slow tier).
+// RAS blocks in amdsmi_gpu_block_t bit order (bit i = 1 << i): UMC (HBM), SDMA, GFX, ...
+constexpr int kEccBlocks = 19;
+extern const char* const kEccBlockNames[kEccBlocks];
+
 struct HealthInfo {
   uint64_t ecc_correctable = 0, ecc_uncorrectable = 0, ecc_deferred = 0;
   int xgmi_error_status = -1;   // amdsmi_xgmi_status_t: 0 ok, 1 error, 2 multiple; -1 unknown
   bool ecc_valid = false;
+  // Per-block counts for the blocks with ECC enabled whose counts could be read
+  // (bit i of ecc_block_mask = block i valid).
+  uint32_t ecc_block_mask = 0;
+  uint64_t ecc_block_ce[kEccBlocks] = {}, ecc_block_ue[kEccBlocks] = {}, ecc_block_de[kEccBlocks] = {};
 };
 
 struct TopoEdge {

@@ -54,6 +54,8 @@ struct Dev {
   int fd_metrics = -1;
   int fd_vram_used = -1;
   bool partitioned = false;  // a DPX/QPX/CPX partition: restrict the table to its XCCs
+  uint64_t ecc_mask = 0;     // blocks with ECC enabled (read once, slow thread only)
+  bool ecc_mask_read = false;
   alignas(64) uint8_t buf[4096];
 };
 
@@ -200,6 +202,25 @@ class AmdSmiBackend final : public Backend {
       out.ecc_correctable = ec.correctable_count;
       out.ecc_uncorrectable = ec.uncorrectable_count;
       out.ecc_deferred = ec.deferred_count;
+    }
+    // Per-block counts: the enabled mask is read once per device (it is fixed by
+    // the VBIOS / driver), then one sysfs-backed count per enabled block.
+    if (!devs_[d]->ecc_mask_read) {
+      uint64_t en = 0;
+      devs_[d]->ecc_mask = amdsmi_get_gpu_ecc_enabled(devs_[d]->h, &en) == AMDSMI_STATUS_SUCCESS ? en : 0;
+      devs_[d]->ecc_mask_read = true;
+    }
+    out.ecc_block_mask = 0;
+    for (int b = 0; b < kEccBlocks; ++b) {
+      if (!(devs_[d]->ecc_mask & (1ULL << b))) continue;
+      amdsmi_error_count_t bc;
+      std::memset(&bc, 0, sizeof bc);
+      if (amdsmi_get_gpu_ecc_count(devs_[d]->h, static_cast<amdsmi_gpu_block_t>(1ULL << b), &bc) != AMDSMI_STATUS_SUCCESS)
+        continue;
+      out.ecc_block_mask |= 1u << b;
+      out.ecc_block_ce[b] = bc.correctable_count;
+      out.ecc_block_ue[b] = bc.uncorrectable_count;
+      out.ecc_block_de[b] = bc.deferred_count;
     }
     amdsmi_xgmi_status_t xs;
     out.xgmi_error_status =

@@ -264,6 +264,9 @@ class MockBackend final : public Backend {
     out.ecc_correctable = static_cast<uint64_t>(t * static_cast<double>(cfg_.ecc_correctable_per_s));
     out.ecc_uncorrectable = 0;
     out.ecc_deferred = 0;
+    // UMC (HBM) carries the correctable errors; GFX and xGMI are enabled and clean.
+    out.ecc_block_mask = (1u << 0) | (1u << 2) | (1u << 7);
+    out.ecc_block_ce[0] = out.ecc_correctable;
     out.xgmi_error_status = 0;
     return 0;
   }

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <charconv>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <ctime>
 
@@ -500,6 +501,22 @@ void Exporter::render(std::string& out) {
     w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"correctable\"", h->ecc_correctable);
     w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"uncorrectable\"", h->ecc_uncorrectable);
     w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"deferred\"", h->ecc_deferred);
+  }
+  w.head("amdgpu_ecc_block_errors_total", "counter",
+         "Accumulated ECC errors per RAS block (umc = HBM, gfx, xgmi_wafl, ...) and type, for the blocks with ECC enabled");
+  for (int d : ids) {
+    auto h = S.state(d).get_health();
+    if (!h || !h->ecc_block_mask) continue;
+    char lb[96];
+    for (int b = 0; b < kEccBlocks; ++b) {
+      if (!(h->ecc_block_mask & (1u << b))) continue;
+      const uint64_t v[3] = {h->ecc_block_ce[b], h->ecc_block_ue[b], h->ecc_block_de[b]};
+      const char* ty[3] = {"correctable", "uncorrectable", "deferred"};
+      for (int k = 0; k < 3; ++k) {
+        std::snprintf(lb, sizeof lb, "block=\"%s\",type=\"%s\"", kEccBlockNames[b], ty[k]);
+        w.line_u("amdgpu_ecc_block_errors_total", dev_labels_[d], lb, v[k]);
+      }
+    }
   }
   w.head("amdgpu_xgmi_error_status", "gauge", "xGMI error status: 0 none, 1 error, 2 multiple errors");
   for (int d : ids) {

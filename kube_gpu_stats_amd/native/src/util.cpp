@@ -6,6 +6,10 @@
 
 namespace kgs {
 
+const char* const kEccBlockNames[kEccBlocks] = {"umc", "sdma", "gfx", "mmhub", "athub", "pcie_bif", "hdp",
+                                                "xgmi_wafl", "df", "smn", "sem", "mp0", "mp1", "fuse",
+                                                "mca", "vcn", "jpeg", "ih", "mpio"};
+
 std::string gpu_type_from_market_name(const std::string& m) {
   // "AMD Instinct MI355 OAM" -> "MI355X"; "AMD Instinct MI300X" -> "MI300X".
   for (size_t i = 0; i + 2 < m.size(); ++i) {

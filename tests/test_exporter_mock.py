@@ -620,3 +620,19 @@ def test_http_connection_cap_and_idle_timeout(mock_exporter):
     assert closed["idle"] >= 3 and closed["limit"] == 3
     st = ex.stats()
     assert st["http_closed_idle"] >= 3 and st["http_closed_limit"] == 3
+
+
+def test_ecc_totals_and_per_block_counts(mock_exporter):
+    """RAS tier (node-wide slow thread): device totals by type and per-block counts for
+    the blocks with ECC enabled; on the mock the HBM controller (umc) carries the
+    correctable errors and gfx / xgmi_wafl are enabled and clean."""
+    ex = mock_exporter(n_gpus=2, link_period_s=0.05, mock={"ecc_correctable_per_s": 1000})
+    time.sleep(0.4)
+    m = parse_text(ex.render())
+    tot = {(lb["gpu"], lb["type"]): v for lb, v in m["amdgpu_ecc_errors_total"]}
+    blk = {(lb["gpu"], lb["block"], lb["type"]): v for lb, v in m["amdgpu_ecc_block_errors_total"]}
+    for g in ("0", "1"):
+        assert {b for (gg, b, _) in blk if gg == g} == {"umc", "gfx", "xgmi_wafl"}
+        assert tot[(g, "correctable")] > 0
+        assert blk[(g, "umc", "correctable")] == tot[(g, "correctable")]
+        assert blk[(g, "gfx", "uncorrectable")] == 0 and blk[(g, "xgmi_wafl", "deferred")] == 0

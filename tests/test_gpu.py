@@ -1101,3 +1101,28 @@ def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
     assert len(la) == 1 and 'pod="tenant-a"' in la[0], lines
     assert len(lb) == 1 and 'pod="tenant-b"' in lb[0], lines
     _keep("two_tenants.json", json.dumps(row, indent=1))
+
+
+def test_ecc_per_block_counts_on_mi355x(N):
+    """The RAS tier reads the ECC-enabled block mask once and a count per enabled block:
+    on MI355X the HBM controllers (umc) have ECC, and every block's counts are
+    exported next to the device totals (all 0 on a healthy card)."""
+    ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 20, "link_period_s": 0.1, "proc_period_s": 0})
+    ex.start()
+    try:
+        time.sleep(0.8)
+        body = ex.render()
+    finally:
+        ex.stop()
+    from kube_gpu_stats_amd.utils.scrape import parse_text
+
+    m = parse_text(body)
+    tot = {lb["type"]: v for lb, v in m.get("amdgpu_ecc_errors_total", []) if lb["gpu"] == "0"}
+    blk = {(lb["block"], lb["type"]): v for lb, v in m.get("amdgpu_ecc_block_errors_total", []) if lb["gpu"] == "0"}
+    _keep("ecc_blocks.json", json.dumps({"totals": tot, "blocks": {f"{b}/{t}": v for (b, t), v in blk.items()}},
+                                        indent=1))
+    print(json.dumps({"totals": tot, "blocks": sorted({b for b, _ in blk})}))
+    assert tot, "device ECC totals missing"
+    assert ("umc", "correctable") in blk, sorted(blk)
+    for ty in ("correctable", "uncorrectable", "deferred"):
+        assert sum(v for (b, t), v in blk.items() if t == ty) >= 0
