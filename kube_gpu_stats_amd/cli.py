@@ -1,4 +1,4 @@
-"""``kgs`` command line: exporter | who-use-gpu | gpu-util-stats | dmon | record | topo | pmc | scrape | bench.
+"""``kgs`` command line: exporter | who-use-gpu | gpu-util-stats | ps | dmon | record | topo | pmc | scrape | bench.
 
 The reference ships two scripts with no arguments (who_use_gpu.py:61-62,
 gpu_util_stats.py:165-166).  They become subcommands here, every hard-coded
@@ -18,11 +18,13 @@ def main(argv=None) -> int:
     sub = ap.add_subparsers(dest="cmd", required=True)
 
     from .exporter import main as exporter_main
-    from .reports import dmon, gpu_util_stats, record, who_use_gpu
+    from .reports import dmon, gpu_util_stats, ps, record, who_use_gpu
 
     exporter_main.build_parser(sub.add_parser("exporter", help="run the node exporter"))
     who_use_gpu.build_parser(sub.add_parser("who-use-gpu", help="per-pod GPU allocation census (F1)"))
     gpu_util_stats.build_parser(sub.add_parser("gpu-util-stats", help="per-pod / per-node utilisation report (F2-F4)"))
+    ps.build_parser(sub.add_parser("ps", help="processes using a node's GPUs now: pod, HBM, compute share (from one "
+                                              "exporter)"))
     dmon.build_parser(sub.add_parser("dmon", help="live per-GPU rows from one exporter (util, MFMA, HBM, power, xGMI)"))
     record.build_parser(sub.add_parser("record", help="capture an exporter's full-rate counter stream as a Chrome / "
                                                       "Perfetto trace (GPU-active, MFMA, clock, busy segments)"))
@@ -57,6 +59,8 @@ def main(argv=None) -> int:
         return who_use_gpu.run(a)
     if a.cmd == "gpu-util-stats":
         return gpu_util_stats.run(a)
+    if a.cmd == "ps":
+        return ps.run(a)
     if a.cmd == "dmon":
         return dmon.run(a)
     if a.cmd == "record":

@@ -636,3 +636,35 @@ def test_ecc_totals_and_per_block_counts(mock_exporter):
         assert tot[(g, "correctable")] > 0
         assert blk[(g, "umc", "correctable")] == tot[(g, "correctable")]
         assert blk[(g, "gfx", "uncorrectable")] == 0 and blk[(g, "xgmi_wafl", "deferred")] == 0
+
+
+def test_kgs_ps_lists_processes_with_pods_and_compute_share(mock_exporter):
+    """`kgs ps`: one row per (GPU, process) from the exporter's per-process families,
+    with its pod and its compute share over the interval (rate of the CU-seconds
+    counter; the mock's processes occupy 128 of 256 CUs = 50 %)."""
+    import argparse
+    import io
+
+    from kube_gpu_stats_amd.reports import ps
+
+    ex = mock_exporter(n_gpus=2, proc_period_s=0.05)
+    ex.set_pid_owners({(0, 100000): {"pod": "train-0", "namespace": "ml", "container": "main", "pod_uid": "u0"},
+                       (1, 100010): {"pod": "a", "namespace": "ml", "container": "c", "pod_uid": "ua"},
+                       (1, 100011): {"pod": "b", "namespace": "dev", "container": "c", "pod_uid": "ub"}})
+    time.sleep(0.3)
+    args = lambda **kw: argparse.Namespace(**{"url": f"127.0.0.1:{ex.port}", "interval": 0.6, "gpu": "",  # noqa: E731
+                                              "pod": "", "format": "json", **kw})
+    buf = io.StringIO()
+    assert ps.run(args(), out=buf) == 0
+    rows = json.loads(buf.getvalue())
+    by = {(r["gpu"], r["pid"]): r for r in rows}
+    assert set(by) == {("0", 100000), ("1", 100010), ("1", 100011)}
+    assert by[("0", 100000)]["pod"] == "train-0" and by[("1", 100011)]["namespace"] == "dev"
+    assert abs(by[("1", 100011)]["hbm_gib"] - 2.0) < 1e-6
+    for r in rows:
+        assert abs(r["cu_share_pct"] - 50.0) < 8, r
+    buf = io.StringIO()
+    ps.run(args(format="table", pod="b", interval=0), out=buf)
+    table = buf.getvalue()
+    assert "| GPU |" in table.replace("  ", " ") or "GPU" in table.splitlines()[1]
+    assert " b " in table and "train-0" not in table and table.count("\n") == 5  # rule, header, rule, 1 row, rule
