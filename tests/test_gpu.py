@@ -1126,3 +1126,37 @@ def test_ecc_per_block_counts_on_mi355x(N):
     assert ("umc", "correctable") in blk, sorted(blk)
     for ty in ("correctable", "uncorrectable", "deferred"):
         assert sum(v for (b, t), v in blk.items() if t == ty) >= 0
+
+
+def test_counter_reader_in_process_next_to_hip(N, torch_dev):
+    """The aqlprofile reader (libkgs_pmc_aql.so) also runs inside a process whose HIP
+    runtime is already up: its own HSA client, private AQL queue and START/READ
+    packets coexist with torch's queues, and it sees this process's MFMA loop on
+    every XCD (r2an probe: 95 % MFMA util)."""
+    import torch
+
+    from kube_gpu_stats_amd.native import pmc_lib_path
+    from kube_gpu_stats_amd.ops import load
+
+    A = torch.randn(16, 32).to(torch.bfloat16).to(torch_dev)
+    B = torch.randn(32, 64).to(torch.bfloat16).to(torch_dev)
+    C = torch.empty(2048 * 4 * 16 * 64, device=torch_dev)
+    load.mfma_bf16(A, B, C, 2048, 2000)
+    torch.cuda.synchronize()
+    ex = N.Exporter({"backend": "amdsmi", "hz": 1000, "port": -1, "pmc_source": "aqlprofile",
+                     "pmc_lib": pmc_lib_path("aqlprofile"), "proc_period_s": 0, "link_period_s": 0})
+    assert not ex.pmc_error, ex.pmc_error
+    ex.start()
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 1.5:
+            load.mfma_bf16(A, B, C, 2048, 20000)
+            torch.cuda.synchronize()
+        w = ex.window(0, 1.0)
+        i = ex.integrals(0)
+    finally:
+        ex.stop()
+    print(json.dumps({"window": w, "pmc_samples": i["pmc_samples"]}))
+    assert i["pmc_samples"] >= 1000 and i["pmc_errors"] == 0, i
+    assert w["mfma_util_pct"] > 80, w
+    assert len(w["xcd_mfma_util_pct"]) == 8 and min(w["xcd_mfma_util_pct"]) > 70, w
