@@ -86,9 +86,9 @@ def parse_args(argv=None):
     ap.add_argument("--scrape-hz", type=float, default=20.0)
     ap.add_argument("--step-ms", type=float, default=500.0,
                     help="each step repeats the load unit until it lasts at least this long")
-    ap.add_argument("--rounds", type=int, default=32,
-                    help="interleaved rounds (0 = off); 32 x 3 blocks of ~1 s put the 95 %% CI of the "
-                         "overhead under 0.1 %% on a power-capped MI355X (per-round sd ~0.25 %%)")
+    ap.add_argument("--rounds", type=int, default=48,
+                    help="interleaved rounds (0 = off); 48 x 3 blocks of ~1 s put the 95 %% CI of the "
+                         "overhead under 0.1 %% on a power-capped MI355X (per-round sd 0.18-0.28 %%: r2ag, r2aj)")
     ap.add_argument("--block-steps", type=int, default=2, help="steps per interleaved block")
     ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per unit on MI355X")
     ap.add_argument("--mfma-blocks", type=int, default=2048)
