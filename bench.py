@@ -652,6 +652,41 @@ class Rates:
         return out, src
 
 
+class PmfwProbe:
+    """Rank-local PMFW table reads at interleaved-block edges (one ≈46 µs sysfs pread
+    each), independent of the exporter — which is paused in the "off" blocks: the
+    block's average socket power and package-power throttle residency, from the
+    table's own energy / PPT-residency accumulators and firmware clock.  Shows
+    whether a sampling rate changes the GPU's power state (profiles/r2/r2aq)."""
+
+    def __init__(self, bdf: str):
+        self.path = f"/sys/bus/pci/devices/{bdf}/gpu_metrics"
+        try:
+            from kube_gpu_stats_amd.native import load
+
+            self.N = load(rebuild=False)  # built by local rank 0 long before the rounds
+            self.read()
+        except Exception:  # noqa: BLE001 - mock runs, other table revisions: no probe
+            self.N = None
+
+    def read(self) -> dict | None:
+        if self.N is None:
+            return None
+        with open(self.path, "rb") as f:
+            return self.N.parse_gpu_metrics_v1_8(f.read())
+
+    @staticmethod
+    def delta(a: dict | None, b: dict | None) -> dict | None:
+        if not a or not b or b["fw_ts"] <= a["fw_ts"]:
+            return None
+        dt = (b["fw_ts"] - a["fw_ts"]) * 1e-8  # firmware clock: 10 ns
+        out = {"power_w": (b["energy_acc"] - a["energy_acc"]) / 65536.0 / dt}  # 2^-16 J units
+        dc = b["accumulation_counter"] - a["accumulation_counter"]
+        if dc > 0 and b["ppt_residency_acc"] >= a["ppt_residency_acc"]:
+            out["ppt_pct"] = 100.0 * (b["ppt_residency_acc"] - a["ppt_residency_acc"]) / dc
+        return out
+
+
 def pct(xs: list[float], q: float) -> float | None:
     if not xs:
         return None
@@ -670,6 +705,8 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
         return {}
     conds = [0.0] + list(hzs)
     rows: list[dict] = []
+    probe = None if a.mock else PmfwProbe(load.pci_bdf(ctx.local_rank))
+    pw: dict[float, list[dict]] = {c: [] for c in conds}  # per block: power / ppt of this rank's GPU
     rates = {h: Rates() for h in hzs}
     lat: dict[float, list[float]] = {h: [] for h in hzs}
     paused_reads = 0.0
@@ -690,7 +727,11 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
                 if c > 0:
                     sc = Scraper("127.0.0.1", exp.port).start(a.scrape_hz)
                 w0 = time.perf_counter()
+            p0 = probe.read() if probe is not None else None
             dt = timed(ctx, load, a.block_steps)
+            d = PmfwProbe.delta(p0, probe.read() if probe is not None else None)
+            if d:
+                pw[c].append(d)
             if exp is not None:
                 if sc is not None:
                     sc.stop()
@@ -717,6 +758,22 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
                                   "overhead_per_round_pct": [round(d, 4) for d in diffs],
                                   "_rates": rates[h], "_lat": lat[h]}
     out["block_seconds"] = [[f"{c:g}", round(row[c], 6)] for row in rows for c in row]
+    # Power state per condition of this rank's GPU (the result carries rank 0's).
+    power: dict = {}
+    for c in conds:
+        ws = [d["power_w"] for d in pw[c]]
+        ps = [d["ppt_pct"] for d in pw[c] if "ppt_pct" in d]
+        if ws:
+            power[f"{c:g}"] = {"blocks": len(ws), "power_w_mean": round(sum(ws) / len(ws), 2),
+                               "ppt_pct_mean": round(sum(ps) / len(ps), 3) if ps else None}
+            if c > 0 and len(pw[c]) == len(pw[0.0]):  # paired by round, like the timings
+                m, ci, _ = mean_ci95([x["power_w"] - y["power_w"] for x, y in zip(pw[c], pw[0.0])])
+                power[f"{c:g}"]["power_w_vs_paused"] = round(m, 2)
+                power[f"{c:g}"]["power_w_vs_paused_ci95"] = round(ci, 2)
+    if power:
+        out["power"] = {"by_condition": power,
+                        "note": "PMFW energy / PPT-residency accumulators read by the bench itself at every "
+                                "block edge ('0' = exporter paused)"}
     return out
 
 
