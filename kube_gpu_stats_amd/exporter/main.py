@@ -101,6 +101,10 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "control-http", False, "serve /control/pause and /control/resume (benchmarks only)")
     add_flag(ap, "gzip-level", 0, "gzip /metrics at this zlib level for clients that accept it (0 = off; level 1 "
                                   "costs ≈0.6 ms per 8-GPU page and shrinks it ≈10×)")
+    add_flag(ap, "metric-allow", "", "only these /metrics families: comma-separated globs, e.g. "
+                                     "'container_gpu_*,amdgpu_gfx_*,kgs_up' ('' = all)")
+    add_flag(ap, "metric-deny", "", "drop these /metrics families (globs; wins over --metric-allow), e.g. "
+                                    "'amdgpu_*_xcc_percent,kgs_sample_read_seconds'")
     add_flag(ap, "http-idle-s", 300.0, "close a keep-alive HTTP connection idle this long (0 = never)")
     add_flag(ap, "http-max-conns", 256, "HTTP connections held at once; past it the least recently active one is "
                                         "closed (0 = unlimited)")
@@ -143,6 +147,8 @@ def config_from_args(a) -> dict:
         "gzip_level": a.gzip_level,
         "http_idle_s": a.http_idle_s,
         "http_max_conns": a.http_max_conns,
+        "metric_allow": a.metric_allow,
+        "metric_deny": a.metric_deny,
         "bdfs": [b for b in (a.bdfs.split(",") if isinstance(a.bdfs, str) else a.bdfs) if b],
     }
     return cfg

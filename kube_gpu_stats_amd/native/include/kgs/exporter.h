@@ -85,6 +85,24 @@ struct ExporterConfig {
   // that opens connections and never reads cannot exhaust the exporter's fds.
   double http_idle_s = 300.0;
   int http_max_conns = 256;
+  // Families on /metrics: comma-separated globs ('*', '?') over family names.  Empty
+  // allow = every family; deny wins.  A histogram's _bucket/_sum/_count lines follow
+  // their family.  Trims the per-node series count (≈150 per GPU with every tier on).
+  std::string metric_allow;
+  std::string metric_deny;
+};
+
+// The --metric-allow / --metric-deny decision for one family name.
+class FamilyFilter {
+ public:
+  FamilyFilter() = default;
+  FamilyFilter(const std::string& allow, const std::string& deny);
+  bool active() const { return !allow_.empty() || !deny_.empty(); }
+  bool allowed(const char* name) const;
+  bool allowed(const std::string& name) const { return allowed(name.c_str()); }
+
+ private:
+  std::vector<std::string> allow_, deny_;
 };
 
 class HttpServer;
@@ -163,6 +181,7 @@ class Exporter {
   std::unique_ptr<CounterSource> pmc_;
   std::unique_ptr<Sampler> sampler_;
   std::unique_ptr<HttpServer> http_;
+  FamilyFilter filter_;                   // --metric-allow / --metric-deny
   std::vector<std::string> dev_labels_;   // pre-rendered `gpu="0",uuid=...,...`
   std::vector<TopoEdge> topo_;
   mutable std::mutex mu_;

@@ -87,6 +87,8 @@ ExporterConfig parse_config(const py::dict& d) {
   c.gzip_level = get<int>(d, "gzip_level", c.gzip_level);
   c.http_idle_s = get<double>(d, "http_idle_s", c.http_idle_s);
   c.http_max_conns = get<int>(d, "http_max_conns", c.http_max_conns);
+  c.metric_allow = get<std::string>(d, "metric_allow", c.metric_allow);
+  c.metric_deny = get<std::string>(d, "metric_deny", c.metric_deny);
   return c;
 }
 

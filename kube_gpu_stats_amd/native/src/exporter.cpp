@@ -1,6 +1,8 @@
 // Exporter lifecycle, attribution tables and JSON endpoints.  See exporter.h.
 #include "kgs/exporter.h"
 
+#include <cstring>
+
 #include <unistd.h>
 
 #include <cstdio>
@@ -37,7 +39,71 @@ void jnum(std::string& o, double v) {
 }
 }  // namespace
 
-Exporter::Exporter(ExporterConfig cfg) : cfg_(std::move(cfg)) {
+namespace {
+
+// fnmatch-style: '*' any run, '?' one character.
+bool glob_match(const char* p, const char* s) {
+  const char* star = nullptr;
+  const char* resume = nullptr;
+  while (*s) {
+    if (*p == '?' || *p == *s) {
+      ++p;
+      ++s;
+    } else if (*p == '*') {
+      star = p++;
+      resume = s;
+    } else if (star) {
+      p = star + 1;
+      s = ++resume;
+    } else {
+      return false;
+    }
+  }
+  while (*p == '*') ++p;
+  return *p == 0;
+}
+
+std::vector<std::string> split_globs(const std::string& csv) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i <= csv.size()) {
+    size_t j = csv.find(',', i);
+    if (j == std::string::npos) j = csv.size();
+    std::string t = csv.substr(i, j - i);
+    while (!t.empty() && t.front() == ' ') t.erase(t.begin());
+    while (!t.empty() && t.back() == ' ') t.pop_back();
+    if (!t.empty()) out.push_back(t);
+    i = j + 1;
+  }
+  return out;
+}
+
+}  // namespace
+
+FamilyFilter::FamilyFilter(const std::string& allow, const std::string& deny)
+    : allow_(split_globs(allow)), deny_(split_globs(deny)) {}
+
+bool FamilyFilter::allowed(const char* name) const {
+  if (!active()) return true;
+  // A histogram's series follow their family: kgs_x_bucket / _sum / _count → kgs_x.
+  std::string base(name);
+  for (const char* suf : {"_bucket", "_sum", "_count"}) {
+    const size_t n = std::strlen(suf);
+    if (base.size() > n && base.compare(base.size() - n, n, suf) == 0) {
+      base.resize(base.size() - n);
+      break;
+    }
+  }
+  bool ok = allow_.empty();
+  for (const std::string& g : allow_)
+    if (glob_match(g.c_str(), base.c_str())) { ok = true; break; }
+  if (!ok) return false;
+  for (const std::string& g : deny_)
+    if (glob_match(g.c_str(), base.c_str())) return false;
+  return true;
+}
+
+Exporter::Exporter(ExporterConfig cfg) : cfg_(std::move(cfg)), filter_(cfg_.metric_allow, cfg_.metric_deny) {
   node_name_ = cfg_.node_name;
   if (node_name_.empty()) {
     char h[256] = {};

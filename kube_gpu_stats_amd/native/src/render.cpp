@@ -48,7 +48,20 @@ struct W {
   std::string& o;
   char* p = nullptr;
   char* end = nullptr;
-  explicit W(std::string& s, size_t cap) : o(s) {
+  // --metric-allow / --metric-deny: one decision per run of lines of one family
+  // (names are string literals, so consecutive lines share the pointer).
+  const FamilyFilter* ff = nullptr;
+  const char* last_name = nullptr;
+  bool last_ok = true;
+  bool ok(const char* name) {
+    if (!ff) return true;
+    if (name != last_name) {
+      last_name = name;
+      last_ok = ff->allowed(name);
+    }
+    return last_ok;
+  }
+  explicit W(std::string& s, size_t cap, const FamilyFilter* f = nullptr) : o(s), ff(f && f->active() ? f : nullptr) {
     o.resize(cap);
     p = &o[0];
     end = p + o.size();
@@ -82,6 +95,7 @@ struct W {
     p = std::to_chars(p, end, v).ptr;
   }
   void head(const char* name, const char* type, const char* help) {
+    if (!ok(name)) return;
     put("# HELP ", 7); put(name); put(' '); put(help); put("\n# TYPE ", 8); put(name); put(' '); put(type); put('\n');
   }
   // name{base,extra} value
@@ -91,9 +105,11 @@ struct W {
     put("} ", 2);
   }
   void line(const char* name, const std::string& base, const char* extra, double v) {
+    if (!ok(name)) return;
     labels(name, base, extra); num(v); put('\n');
   }
   void line_u(const char* name, const std::string& base, const char* extra, uint64_t v) {
+    if (!ok(name)) return;
     labels(name, base, extra); u64(v); put('\n');
   }
 };
@@ -152,7 +168,7 @@ const char* throttle_label(int r) { return kThrottleLabels[r]; }
 void Exporter::render(std::string& out) {
   const int64_t t0 = mono_ns();
   out.clear();
-  W w(out, last_render_bytes_.load(std::memory_order_relaxed) + 8192);
+  W w(out, last_render_bytes_.load(std::memory_order_relaxed) + 8192, &filter_);
   Sampler& S = *sampler_;
   const int nd = S.device_count();
   const std::vector<int>& ids = S.sampled_devices();
@@ -324,7 +340,7 @@ void Exporter::render(std::string& out) {
   }
   if (!sblock) {
     std::string blk;
-    W b(blk, 16384);
+    W b(blk, 16384, &filter_);
     b.head("amdgpu_device_info", "gauge", "Static device information (value is always 1)");
     for (int d : ids) {
       const DeviceInfo& in = be_->info(d);
@@ -477,7 +493,7 @@ void Exporter::render(std::string& out) {
     }
     if (!lblock) {  // the slow tier published a new link table: re-render this device's lines
       std::string blk;
-      W b(blk, 4096);
+      W b(blk, 4096, &filter_);
       for (const LinkInfo& li : *links) {
         lb.assign(dev_labels_[d]);
         kvi(lb, "link", li.link);
@@ -724,7 +740,25 @@ void Exporter::render(std::string& out) {
     kv(lb, "sample_hz", std::to_string(S.config().hz));
     w.line("kgs_build_info", lb, nullptr, 1);
   }
-  if (extra) w.put(*extra);
+  if (extra && !filter_.active()) {
+    w.put(*extra);
+  } else if (extra) {  // the control plane's text block: filter it line by line
+    const std::string& x = *extra;
+    size_t i = 0;
+    while (i < x.size()) {
+      size_t e = x.find('\n', i);
+      if (e == std::string::npos) e = x.size();
+      size_t s = i;
+      if (x.compare(i, 7, "# HELP ") == 0 || x.compare(i, 7, "# TYPE ") == 0) s = i + 7;
+      size_t n = s;
+      while (n < e && x[n] != '{' && x[n] != ' ') ++n;
+      if (filter_.allowed(x.substr(s, n - s))) {
+        w.put(x.data() + i, e - i);
+        w.put('\n');
+      }
+      i = e + 1;
+    }
+  }
   w.finish();
   last_render_bytes_.store(out.size(), std::memory_order_relaxed);
 

@@ -668,3 +668,33 @@ def test_kgs_ps_lists_processes_with_pods_and_compute_share(mock_exporter):
     table = buf.getvalue()
     assert "| GPU |" in table.replace("  ", " ") or "GPU" in table.splitlines()[1]
     assert " b " in table and "train-0" not in table and table.count("\n") == 5  # rule, header, rule, 1 row, rule
+
+
+def test_metric_allow_deny_filters_families(mock_exporter):
+    """--metric-allow / --metric-deny trim /metrics by family (globs; deny wins; a
+    histogram's _bucket/_sum/_count follow it; the control plane's text block too)."""
+    full = mock_exporter(n_gpus=2, pmc_source="mock", proc_every=1, link_every=1)
+    deny = mock_exporter(n_gpus=2, pmc_source="mock", proc_every=1, link_every=1,
+                         metric_deny="amdgpu_*_xcc_percent, kgs_sample_read_seconds,amdgpu_xgmi_link_info,"
+                                     "amdgpu_device_info,kgs_attribution_*")
+    allow = mock_exporter(n_gpus=2, pmc_source="mock", proc_every=1, link_every=1,
+                          metric_allow="container_gpu_*,amdgpu_gfx_busy_percent,kgs_up,kgs_attribution_updates_total",
+                          metric_deny="container_gpu_mfma_*")
+    for ex in (full, deny, allow):
+        ex.set_device_owners(0, [{"pod": "train-0", "namespace": "ml", "container": "main"}])
+        ex.set_extra_metrics("# HELP kgs_attribution_updates_total x\n# TYPE kgs_attribution_updates_total counter\n"
+                             "kgs_attribution_updates_total 3\n# HELP kgs_attribution_errors_total y\n"
+                             "# TYPE kgs_attribution_errors_total counter\nkgs_attribution_errors_total 0\n")
+    time.sleep(0.5)
+    fams = {}
+    for name, ex in (("full", full), ("deny", deny), ("allow", allow)):
+        body = ex.render()
+        fams[name] = {f.name for f in text_string_to_metric_families(body)}  # still valid exposition
+    dropped = fams["full"] - fams["deny"]
+    assert {"amdgpu_gfx_busy_xcc_percent", "amdgpu_mfma_util_xcc_percent", "kgs_sample_read_seconds",
+            "amdgpu_xgmi_link_info", "amdgpu_device_info", "kgs_attribution_updates", "kgs_attribution_errors"} <= dropped
+    assert all(f.startswith(("amdgpu_", "kgs_sample_read", "kgs_attribution")) for f in dropped), dropped
+    assert "container_gpu_sm_util" in fams["deny"] and "amdgpu_topology_link" in fams["deny"]
+    assert fams["allow"] == {"container_gpu_sm_util", "container_gpu_busy_seconds", "container_gpu_energy_joules",
+                             "amdgpu_gfx_busy_percent", "kgs_up", "kgs_attribution_updates"}, fams["allow"]
+    assert len(fams["deny"]) < len(fams["full"])
