@@ -736,7 +736,9 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
     assert min(sh) < 5 and max(sh) > 90, summary
     assert abs(summary["duty_counters"] - host_duty) < 0.08, summary
     assert len(pm_in) >= 10, summary                  # ≈50 tables/s
-    assert min(pm_in) > 70, summary                   # profiling mode: PMFW reads the READs as work
+    # profiling mode: PMFW reads the READs as work — far above the ≈20 % true duty
+    # (r2q: 99.6-100; r2at: min 69.5 on a box draining at 7.65 kHz)
+    assert min(pm_in) > 50, summary
 
 
 def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
