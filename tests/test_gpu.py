@@ -910,7 +910,9 @@ def test_pcie_bytes_counter_tracks_host_copies(N, torch_dev):
         ex.stop()
     print(json.dumps(out))
     for name, r in out.items():
-        assert 0.93 < r["counted"] / r["moved"] < 1.07, (name, r)
+        # one factor for both directions (±3 %, profiles/r2/pcie/) + table granularity; the
+        # check is the unit (round 1 exported the accumulator ×10⁹), not the last percent
+        assert 0.90 < r["counted"] / r["moved"] < 1.10, (name, r)
 
 
 def test_energy_counter_matches_socket_power(N, torch_dev):
