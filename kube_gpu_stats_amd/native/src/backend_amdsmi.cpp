@@ -203,12 +203,15 @@ class AmdSmiBackend final : public Backend {
       out.ecc_uncorrectable = ec.uncorrectable_count;
       out.ecc_deferred = ec.deferred_count;
     }
-    // Per-block counts: the enabled mask is read once per device (it is fixed by
-    // the VBIOS / driver), then one sysfs-backed count per enabled block.
+    // Per-block counts: the enabled mask is fixed by the VBIOS / driver, so it is kept
+    // once read (a failed read is retried on the next RAS pass), then one sysfs-backed
+    // count per enabled block.
     if (!devs_[d]->ecc_mask_read) {
       uint64_t en = 0;
-      devs_[d]->ecc_mask = amdsmi_get_gpu_ecc_enabled(devs_[d]->h, &en) == AMDSMI_STATUS_SUCCESS ? en : 0;
-      devs_[d]->ecc_mask_read = true;
+      if (amdsmi_get_gpu_ecc_enabled(devs_[d]->h, &en) == AMDSMI_STATUS_SUCCESS) {
+        devs_[d]->ecc_mask = en;
+        devs_[d]->ecc_mask_read = true;
+      }
     }
     out.ecc_block_mask = 0;
     for (int b = 0; b < kEccBlocks; ++b) {

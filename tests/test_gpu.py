@@ -1186,3 +1186,52 @@ def test_counter_reader_in_process_next_to_hip(N, torch_dev):
     assert i["pmc_samples"] >= 1000 and i["pmc_errors"] == 0, i
     assert w["mfma_util_pct"] > 80, w
     assert len(w["xcd_mfma_util_pct"]) == 8 and min(w["xcd_mfma_util_pct"]) > 70, w
+
+
+def test_mfma_busy_counter_reproduces_kernel_flops(N, torch_dev):
+    """Accuracy, not just direction: the counter tier's MFMA busy (share of SPI-busy
+    cycles) × GPU-active × the counted clock × 1024 SIMDs × the dense bf16 MFMA rate
+    (1024 FLOP per busy SIMD-cycle: 2.5 PFLOP/s at 2.4 GHz) reproduces the TFLOP/s the
+    bf16 MFMA kernel achieves by its own event timing, within 10 %."""
+    import math
+
+    import torch
+
+    from kube_gpu_stats_amd.native import pmc_lib_path
+    from kube_gpu_stats_amd.ops.load import LoadStep
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 26)
+    ls.run_mfma()
+    torch.cuda.synchronize()
+    ex = N.Exporter({"backend": "amdsmi", "hz": 1000, "port": -1, "pmc_source": "aqlprofile",
+                     "pmc_lib": pmc_lib_path("aqlprofile"), "proc_period_s": 0, "link_period_s": 0})
+    assert not ex.pmc_error, ex.pmc_error
+    ex.start()
+    try:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ls.run_mfma()
+        e1.record()
+        torch.cuda.synchronize()
+        k = max(50, math.ceil(1.6 / (e0.elapsed_time(e1) * 1e-3)))  # ≈1.6 s of back-to-back kernels
+        time.sleep(0.2)
+        e0.record()
+        for _ in range(k):
+            ls.run_mfma()
+        e1.record()
+        torch.cuda.synchronize()
+        w = ex.window(0, 1.0)  # the last second of the loop (≤ 1 tick of idle after it)
+    finally:
+        ex.stop()
+    measured = k * ls.flops / (e0.elapsed_time(e1) * 1e-3)
+    simds = 256 * 4
+    busy_simd_cycles_per_s = (w["mfma_util_pct"] / 100) * (w["gpu_active_pct"] / 100) * simds * w["gpu_clock_mhz"] * 1e6
+    predicted = busy_simd_cycles_per_s * 1024
+    row = {"kernels": k, "measured_tflops": measured / 1e12, "predicted_tflops": predicted / 1e12,
+           "ratio": predicted / measured, "flop_per_busy_simd_cycle": measured / busy_simd_cycles_per_s,
+           "mfma_util_pct": w["mfma_util_pct"], "gpu_active_pct": w["gpu_active_pct"],
+           "clock_mhz": w["gpu_clock_mhz"]}
+    _keep("mfma_flops_crosscheck.json", json.dumps(row, indent=1))
+    print(json.dumps(row))
+    assert measured > 1e15, row  # the kernel runs near the dense peak (bench: 1.9 PFLOP/s)
+    assert 0.9 < row["ratio"] < 1.1, row
