@@ -88,6 +88,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "compat-unallocated", False, "emit container_gpu_sm_util for GPUs no pod holds")
     add_flag(ap, "pcie-bytes-per-unit", 105.7, "bytes per unit of the PMFW PCIe bandwidth accumulator "
                                               "(MI355X calibration, profiles/r2/pcie/)")
+    add_flag(ap, "xgmi-bytes-per-unit", 1024.0, "bytes per unit of the PMFW xGMI link accumulators (amdsmi.h: KB; "
+                                               "correct with bench.py's N > 1 expected / measured ratio)")
     add_flag(ap, "sm-util-source", "pmfw", "what container_gpu_sm_util / container_gpu_busy_seconds_total measure: pmfw "
                                            "(firmware GFX busy: a dispatch in flight; counts counter READs as work) | "
                                            "counters (GRBM_SPI_BUSY: waves in a shader engine; READ-immune; needs --pmc)")
@@ -143,6 +145,7 @@ def config_from_args(a) -> dict:
         "compat_unallocated": a.compat_unallocated,
         "sm_util_source": a.sm_util_source,
         "pcie_bytes_per_acc_unit": a.pcie_bytes_per_unit,
+        "xgmi_bytes_per_acc_unit": a.xgmi_bytes_per_unit,
         "control_http": a.control_http,
         "gzip_level": a.gzip_level,
         "http_idle_s": a.http_idle_s,

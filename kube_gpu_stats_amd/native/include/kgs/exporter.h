@@ -65,6 +65,11 @@ struct ExporterConfig {
   // and 2 GiB copies alike, 108.3 B full-duplex (profiles/r2/pcie/): one factor is
   // good to ±3 %.
   double pcie_bytes_per_acc_unit = 105.7;
+  // Bytes per unit of the PMFW per-link xGMI accumulators (xgmi_read/write_data_acc):
+  // amdsmi.h documents KB.  Not yet pinned against traffic on hardware (a 1-GPU lease
+  // has no peer); bench.py's N > 1 result carries the bytes its all-reduces imply
+  // next to the measured rate, and their ratio is the correction.
+  double xgmi_bytes_per_acc_unit = 1024.0;
   bool per_process = true;
   bool compat_series = true;        // container_gpu_sm_util (reference contract)
   bool compat_unallocated = false;  // also emit it for GPUs with no pod (pod_name="")

@@ -83,6 +83,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.compat_unallocated = get<bool>(d, "compat_unallocated", c.compat_unallocated);
   c.sm_util_source = get<std::string>(d, "sm_util_source", c.sm_util_source);
   c.pcie_bytes_per_acc_unit = get<double>(d, "pcie_bytes_per_acc_unit", c.pcie_bytes_per_acc_unit);
+  c.xgmi_bytes_per_acc_unit = get<double>(d, "xgmi_bytes_per_acc_unit", c.xgmi_bytes_per_acc_unit);
   c.control_http = get<bool>(d, "control_http", c.control_http);
   c.gzip_level = get<int>(d, "gzip_level", c.gzip_level);
   c.http_idle_s = get<double>(d, "http_idle_s", c.http_idle_s);

@@ -460,7 +460,8 @@ void Exporter::render(std::string& out) {
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
     for (int l = 0; l < kMaxXgmi; ++l) {
       if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
-      w.line_u("amdgpu_xgmi_read_bytes_total", dev_labels_[d], kLinkLabels[l], x.s.xgmi_read_kb[l] * 1024ull);
+      w.line("amdgpu_xgmi_read_bytes_total", dev_labels_[d], kLinkLabels[l],
+             static_cast<double>(x.s.xgmi_read_kb[l]) * cfg_.xgmi_bytes_per_acc_unit);
     }
   }
   w.head("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link (PMFW accumulator)");
@@ -469,7 +470,8 @@ void Exporter::render(std::string& out) {
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
     for (int l = 0; l < kMaxXgmi; ++l) {
       if (x.s.xgmi_link_up[l] == 0xFFFF) continue;
-      w.line_u("amdgpu_xgmi_write_bytes_total", dev_labels_[d], kLinkLabels[l], x.s.xgmi_write_kb[l] * 1024ull);
+      w.line("amdgpu_xgmi_write_bytes_total", dev_labels_[d], kLinkLabels[l],
+             static_cast<double>(x.s.xgmi_write_kb[l]) * cfg_.xgmi_bytes_per_acc_unit);
     }
   }
   w.head("amdgpu_xgmi_link_up", "gauge", "xGMI link status per port (1 up, 0 down)");

@@ -698,3 +698,22 @@ def test_metric_allow_deny_filters_families(mock_exporter):
     assert fams["allow"] == {"container_gpu_sm_util", "container_gpu_busy_seconds", "container_gpu_energy_joules",
                              "amdgpu_gfx_busy_percent", "kgs_up", "kgs_attribution_updates"}, fams["allow"]
     assert len(fams["deny"]) < len(fams["full"])
+
+
+def test_xgmi_bytes_unit_is_configurable(mock_exporter):
+    """amdgpu_xgmi_*_bytes_total = PMFW accumulator units × --xgmi-bytes-per-unit
+    (amdsmi.h: KB; a multi-GPU bench run's expected / measured ratio corrects it)."""
+    ex = mock_exporter(n_gpus=2, hz=200)
+    time.sleep(0.4)
+    ex.pause()
+    m = parse_text(ex.render())
+    kb = ex.samples(0, 1)[-1]["xgmi_read_kb"]
+    got = {lb["link"]: v for lb, v in m["amdgpu_xgmi_read_bytes_total"] if lb["gpu"] == "0"}
+    assert got and all(got[k] == kb[int(k)] * 1024 for k in got), (got, kb)
+    ex2 = mock_exporter(n_gpus=2, hz=200, xgmi_bytes_per_acc_unit=1000.0)
+    time.sleep(0.4)
+    ex2.pause()
+    kb2 = ex2.samples(0, 1)[-1]["xgmi_read_kb"]
+    m2 = parse_text(ex2.render())
+    got2 = {lb["link"]: v for lb, v in m2["amdgpu_xgmi_read_bytes_total"] if lb["gpu"] == "0"}
+    assert got2 and all(got2[k] == kb2[int(k)] * 1000 for k in got2), (got2, kb2)
