@@ -687,6 +687,16 @@ class PmfwProbe:
         return out
 
 
+def scrape_at(sc) -> tuple[dict, float]:
+    """One /metrics scrape and the time it was rendered (the request is sent at ``t``;
+    the exporter renders within ~0.1 ms).  Count deltas between two scrapes cover
+    exactly the interval between their ``t``s — timing after the parse instead would
+    move the window by the parse time of the page (≈10 ms per GPU's worth of series)."""
+    t = time.perf_counter()
+    body = sc.get()
+    return parse_text(body), t
+
+
 def pct(xs: list[float], q: float) -> float | None:
     if not xs:
         return None
@@ -723,10 +733,9 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
                 else:
                     exp.set_rate(c)
                     exp.resume()
-                before = parse_text(exp.sc.get())
                 if c > 0:
                     sc = Scraper("127.0.0.1", exp.port).start(a.scrape_hz)
-                w0 = time.perf_counter()
+                before, w0 = scrape_at(exp.sc)
             p0 = probe.read() if probe is not None else None
             dt = timed(ctx, load, a.block_steps)
             d = PmfwProbe.delta(p0, probe.read() if probe is not None else None)
@@ -735,8 +744,8 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
             if exp is not None:
                 if sc is not None:
                     sc.stop()
-                after = parse_text(exp.sc.get())
-                win = time.perf_counter() - w0
+                after, w1 = scrape_at(exp.sc)
+                win = w1 - w0
                 if c > 0:
                     rates[c].add(before, after, win)
                     lat[c].extend(sc.latencies_s)
@@ -853,9 +862,10 @@ def quiet_gpu(ctx, load, exp, a) -> dict:
         for mode, hz in (("adaptive", default_idle), ("profiling", 0.0)):
             exp.set_idle_hz(hz)
             time.sleep(0.2)
-            m0, t0 = parse_text(exp.sc.get()), time.perf_counter()
+            m0, t0 = scrape_at(exp.sc)
             time.sleep(a.quiet_s)
-            m1, dt = parse_text(exp.sc.get()), time.perf_counter() - t0
+            m1, t1 = scrape_at(exp.sc)
+            dt = t1 - t0
             fam = lambda m, n, **kw: {lb["gpu"]: v for lb, v in m.get(n, [])  # noqa: E731
                                       if all(lb.get(k) == w for k, w in kw.items())}
             r0, r1 = fam(m0, "kgs_pmc_samples_total"), fam(m1, "kgs_pmc_samples_total")
@@ -898,11 +908,12 @@ def capacity(ctx, load, exp, a) -> dict:
         if exp is not None:
             exp.set_rate(hz)
             time.sleep(0.05)
-            before, w0 = parse_text(exp.sc.get()), time.perf_counter()
+            before, w0 = scrape_at(exp.sc)
         dt = timed(ctx, load, a.block_steps)
         if exp is None:
             continue
-        after, win = parse_text(exp.sc.get()), time.perf_counter() - w0
+        after, w1 = scrape_at(exp.sc)
+        win = w1 - w0
         r = Rates()
         r.add(before, after, win)
         pg, src = r.per_gpu(exp.ready.get("pmc", "none") != "none")
@@ -987,20 +998,21 @@ def run(a, ctx) -> dict | None:
     win = 0.0
     exp_pid = int(exp.ready.get("pid", 0) or 0) if exp is not None else 0
     cpu0 = cpu1 = 0.0
+    cpu_win = 0.0
     thr0: dict = {}
     thr1: dict = {}
     if exp is not None:
         sc_b = Scraper("127.0.0.1", exp.port)
-        before = parse_text(sc_b.get())
-        cpu0, thr0 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
-        w0 = time.perf_counter()
+        cpu0, thr0, c_t0 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid), time.perf_counter()
+        before, w0 = scrape_at(sc_b)  # counts as of the render, timed at the request
         sc_b.start(a.scrape_hz)
     t_b = timed(ctx, load, a.steps, "B_on")
     if exp is not None:
         sc_b.stop()
-        after = parse_text(sc_b.get())
-        win = time.perf_counter() - w0
+        after, w1 = scrape_at(sc_b)
+        win = w1 - w0
         cpu1, thr1 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
+        cpu_win = time.perf_counter() - c_t0
 
     resolution = burst_train(ctx, load, exp, a)
     quiet = quiet_gpu(ctx, load, exp, a)
@@ -1080,9 +1092,9 @@ def run(a, ctx) -> dict | None:
         "burst_resolution": resolution,
         "quiet_gpu": quiet,
         "capacity": cap,
-        "exporter_cpu_cores": round((cpu1 - cpu0) / win, 4) if win > 0 and exp_pid else None,
-        "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / win, 4) for k, v in thr1.items()
-                                         if win > 0 and v - thr0.get(k, 0.0) > 0.005 * win},
+        "exporter_cpu_cores": round((cpu1 - cpu0) / cpu_win, 4) if cpu_win > 0 and exp_pid else None,
+        "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / cpu_win, 4) for k, v in thr1.items()
+                                         if cpu_win > 0 and v - thr0.get(k, 0.0) > 0.005 * cpu_win},
         "pmc_source": exp.ready.get("pmc"),
         "pmc_error": exp.ready.get("pmc_error"),
         "load": calib,
