@@ -71,10 +71,14 @@ def run(a, out=sys.stdout) -> int:
     sc = Scraper(u.hostname or "127.0.0.1", u.port or 80)
     prev, dt = None, 0.0
     if a.interval > 0:
-        prev, t0 = parse_text(sc.scrape_once()), time.monotonic()
-        time.sleep(a.interval)
-        dt = time.monotonic() - t0
-    rows = rows_from(prev, parse_text(sc.scrape_once()), dt)
+        t0 = time.monotonic()  # the exporter renders right after the request
+        prev = parse_text(sc.scrape_once())
+        time.sleep(max(0.0, a.interval - (time.monotonic() - t0)))
+    t1 = time.monotonic()
+    cur = parse_text(sc.scrape_once())
+    if prev is not None:
+        dt = t1 - t0
+    rows = rows_from(prev, cur, dt)
     rows = [r for r in rows if (not a.gpu or r["gpu"] == a.gpu) and (not a.pod or r["pod"] == a.pod)]
     if a.format == "json":
         out.write(json.dumps(rows) + "\n")
