@@ -65,10 +65,10 @@ class PodDirectory:
             with open(self.source[5:]) as f:
                 return json.load(f)
         if self.source == "api":
-            from ..reports.who_use_gpu import _api_get
+            from ..reports.who_use_gpu import api_list
 
             sel = f"?fieldSelector=spec.nodeName%3D{self.node}" if self.node else ""
-            return _api_get("/api/v1/pods" + sel, self.timeout_s)
+            return api_list("/api/v1/pods" + sel, self.timeout_s)
         raise ValueError(f"unknown pod directory source {self.source!r}")
 
     def refresh(self, force: bool = False) -> None:

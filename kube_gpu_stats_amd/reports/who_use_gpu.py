@@ -136,8 +136,28 @@ def load_pods(source: str, kubectl: str, path: str, timeout: float) -> dict:
             raise RuntimeError(f"kubectl failed ({r.returncode}): {r.stderr.strip()}")
         return json.loads(r.stdout)
     if source == "api":
-        return _api_get("/api/v1/pods", timeout)
+        return api_list("/api/v1/pods", timeout)
     raise ValueError(source)
+
+
+def api_list(path: str, timeout: float, limit: int = 500, get=None) -> dict:
+    """A LIST over the API server in pages of ``limit`` (``metadata.continue``), as
+    kubectl does: a cluster of tens of thousands of pods is never one response."""
+    import urllib.parse
+
+    get = get or _api_get
+    sep = "&" if "?" in path else "?"
+    items: list = []
+    token = ""
+    while True:
+        q = f"{path}{sep}limit={limit}" + (f"&continue={urllib.parse.quote(token, safe='')}" if token else "")
+        page = get(q, timeout)
+        items.extend(page.get("items") or [])
+        token = (page.get("metadata") or {}).get("continue") or ""
+        if not token:
+            page["items"] = items
+            page.setdefault("metadata", {}).pop("continue", None)
+            return page
 
 
 def _api_get(path: str, timeout: float) -> dict:

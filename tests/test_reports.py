@@ -175,3 +175,28 @@ def test_idle_gpu_hours_column_and_total():
     assert "Idle GPU-h" in table and "TOTAL" in table and "96.00" in table
     js = json.loads(G.format_rows(rows, "pod", "json", False, idle_hours=True))
     assert js[0]["Idle GPU-h"] == 72.0 and len(js) == 3
+
+
+def test_api_pod_list_follows_continue_tokens():
+    """`--source api` lists pods in pages (limit + metadata.continue) like kubectl."""
+    from kube_gpu_stats_amd.reports.who_use_gpu import api_list
+
+    pages = {"": (["a", "b"], "t1"), "t1": (["c", "d"], "t/2=="), "t/2==": (["e"], "")}
+    seen = []
+
+    def get(path, timeout):
+        seen.append(path)
+        tok = ""
+        if "continue=" in path:
+            import urllib.parse
+
+            tok = urllib.parse.unquote(path.split("continue=")[1])
+        names, nxt = pages[tok]
+        return {"kind": "PodList", "metadata": {"continue": nxt} if nxt else {},
+                "items": [{"metadata": {"name": n}} for n in names]}
+
+    out = api_list("/api/v1/pods?fieldSelector=spec.nodeName%3Dn1", 5.0, limit=2, get=get)
+    assert [p["metadata"]["name"] for p in out["items"]] == ["a", "b", "c", "d", "e"]
+    assert "continue" not in out["metadata"] and out["kind"] == "PodList"
+    assert seen[0] == "/api/v1/pods?fieldSelector=spec.nodeName%3Dn1&limit=2"
+    assert seen[2].endswith("&limit=2&continue=t%2F2%3D%3D")
