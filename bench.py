@@ -28,7 +28,11 @@ packets would cost the workload time) repeated until the step lasts ≥ --step-m
      --hz-list — in alternating order (off,100,8k | 8k,100,off | ...), --block-steps
      steps per block, scraped while sampling.  Per round, overhead = t_on/t_off − 1;
      the result is the mean over rounds ± a 95 % t-interval.  Adjacent blocks share
-     thermal and power state, so slow drift cancels (A/B/C cannot do that).
+     thermal and power state, so slow drift cancels (A/B/C cannot do that).  The bench
+     reads the PMFW table itself at every block edge: power and package-power throttle
+     residency per condition (``interleaved.power``; profiles/r2/r2aq).
+  S  untimed: one block at each --capacity-hz rate in profiling mode — delivered drains,
+     overruns, host µs per drain (``capacity``)
   C  K steps, exporter stopped                           (second baseline)
 
 ``value`` = counter samples/s summed over the N GPUs (the driver's contract: the
