@@ -251,6 +251,62 @@ def add_energy(rows: list[list], kwh: dict[tuple[str, str], float]) -> list[list
     return [[*r, kwh.get((r[0], str(r[1]).removesuffix(" (finished)")), 0.0)] for r in rows]
 
 
+POD_NS_QUERY = "max(kube_pod_status_phase) by (namespace, pod)"  # kube-state-metrics, any phase
+
+
+def pod_namespaces(c: PromClient, start, end, step_s: int) -> dict[str, str]:
+    """pod → namespace over the window (kube-state-metrics; pods that finished in it too)."""
+    out: dict[str, str] = {}
+    for r in result(c.query_range(POD_NS_QUERY, start, end, step_s)):
+        m = r["metric"]
+        if m.get("pod"):
+            out.setdefault(m["pod"], m.get("namespace", ""))
+    return out
+
+
+NS_HEADER = ["Namespace", "Pods", "GPUs", "GPU-h", "Busy GPU-h", "Util %", "Idle GPU-h"]
+
+
+def by_namespace(rows: list[list], pod_ns: dict[str, str], window_s: float,
+                 extras: list[str] | None = None) -> tuple[list[str], list[list]]:
+    """Roll pod rows ([node, pod, cards, util %, *extras]) up per namespace — the
+    team-level view of the same accounting: GPU-hours held (cards × window, as the
+    pod report assumes), busy GPU-hours (× util), their ratio, the idle rest, and
+    the extras' totals (e.g. Energy kWh; "Idle GPU-h" is a column already).  Sorted
+    by GPU-hours held, with a total."""
+    extras = list(extras or [])
+    keep = [k for k, e in enumerate(extras) if e != "Idle GPU-h"]
+    h = window_s / 3600.0
+    agg: dict[str, dict] = {}
+    for r in rows:
+        node, pod, cards, util = r[0], str(r[1]).removesuffix(" (finished)"), float(r[2]), float(r[3])
+        a = agg.setdefault(pod_ns.get(pod, "<unknown>"),
+                           {"pods": set(), "gpus": 0.0, "gpu_h": 0.0, "busy_h": 0.0, "extra": [0.0] * len(keep)})
+        a["pods"].add((node, pod))
+        a["gpus"] += cards
+        a["gpu_h"] += cards * h
+        a["busy_h"] += cards * h * min(100.0, max(0.0, util)) / 100.0
+        for j, k in enumerate(keep):
+            a["extra"][j] += float(r[4 + k])
+    header = NS_HEADER + [extras[k] for k in keep]
+    out = []
+    for ns, a in sorted(agg.items(), key=lambda kv: (-kv[1]["gpu_h"], kv[0])):
+        util = 100.0 * a["busy_h"] / a["gpu_h"] if a["gpu_h"] > 0 else 0.0
+        out.append([ns, len(a["pods"]), a["gpus"], a["gpu_h"], a["busy_h"], util, a["gpu_h"] - a["busy_h"], *a["extra"]])
+    if out:
+        tot = [sum(r[i] for r in out) for i in range(1, len(header))]
+        tot[4] = 100.0 * tot[3] / tot[2] if tot[2] > 0 else 0.0  # util of the totals, not a sum of percents
+        out.append(["TOTAL", *tot])
+    return header, out
+
+
+def format_namespace_rows(header: list[str], rows: list[list], fmt: str) -> str:
+    if fmt == "json":
+        return json.dumps([dict(zip(header, r)) for r in rows], indent=2)
+    disp = [[r[0], r[1], f"{r[2]:g}", *(f"{x:.2f}" for x in r[3:])] for r in rows]
+    return render_csv(header, disp) if fmt == "csv" else render(header, disp)
+
+
 def format_rows(rows: list[list], mode: str, fmt: str, compat: bool, idle_hours: bool = False,
                 extras: list[str] | None = None) -> str:
     """Table / JSON / CSV.  Pod mode may carry extra numeric columns after Util %
@@ -301,6 +357,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                       "(1 − util)), and a total")
     add_flag(ap, "energy", False, "pod mode: add the kWh each pod's GPUs drew over the window "
                                   f"({ENERGY_METRIC}), and a total")
+    add_flag(ap, "group-by", "pod", "pod mode: pod (one row per pod) | namespace (per-namespace GPU-hours held, "
+                                    "busy and idle, util, + the extras' totals)")
     return ap
 
 
@@ -319,6 +377,13 @@ def run(a) -> int:
             e = end if isinstance(end, (int, float)) else end.timestamp()
             rows = add_energy(rows, pod_energy_kwh(c, e - a.window, e, a.step))
             extras.append("Energy kWh")
+        if a.group_by == "namespace":
+            e = end if isinstance(end, (int, float)) else end.timestamp()
+            header, ns_rows = by_namespace(rows, pod_namespaces(c, e - a.window, e, a.step), a.window, extras)
+            print(format_namespace_rows(header, ns_rows, a.format))
+            return 0
+    elif a.group_by != "pod":
+        raise SystemExit("--group-by namespace needs pod mode without --compat")
     print(format_rows(rows, a.mode, a.format, a.compat, extras=extras))
     return 0
 

@@ -200,3 +200,71 @@ def test_api_pod_list_follows_continue_tokens():
     assert "continue" not in out["metadata"] and out["kind"] == "PodList"
     assert seen[0] == "/api/v1/pods?fieldSelector=spec.nodeName%3Dn1&limit=2"
     assert seen[2].endswith("&limit=2&continue=t%2F2%3D%3D")
+
+
+def test_util_report_rolls_up_per_namespace():
+    """gpu-util-stats --group-by namespace: GPU-hours held / busy / idle and util per
+    namespace from the pod rows (+ extras' totals), namespaces from kube-state-metrics."""
+    from kube_gpu_stats_amd.reports import gpu_util_stats as G
+
+    rows = [["n1", "a", 4, 50.0, 1.5], ["n1", "b", 2, 100.0, 0.5], ["n2", "c", 8, 25.0, 2.0],
+            ["n2", "d (finished)", 1, 10.0, 0.1]]
+    pod_ns = {"a": "ml", "b": "ml", "c": "vision", "d": "vision"}
+    header, out = G.by_namespace(rows, pod_ns, 86400, ["Energy kWh"])
+    assert header == G.NS_HEADER + ["Energy kWh"]
+    by = {r[0]: r for r in out}
+    # vision: 9 cards × 24 h = 216 GPU-h; busy 8·24·0.25 + 1·24·0.10 = 50.4
+    assert by["vision"][1:3] == [2, 9.0] and by["vision"][3] == 216.0
+    assert abs(by["vision"][4] - 50.4) < 1e-9 and abs(by["vision"][6] - 165.6) < 1e-9
+    assert abs(by["vision"][7] - 2.1) < 1e-9
+    # ml: 6 cards = 144 GPU-h, busy 4·24·0.5 + 2·24 = 96 → 66.7 %
+    assert abs(by["ml"][5] - 100 * 96 / 144) < 1e-9
+    assert [r[0] for r in out] == ["vision", "ml", "TOTAL"]  # most GPU-hours first
+    tot = by["TOTAL"]
+    assert tot[1] == 4 and tot[3] == 360.0 and abs(tot[5] - 100 * (96 + 50.4) / 360) < 1e-9
+    text = G.format_namespace_rows(header, out, "table")
+    assert "vision" in text and "TOTAL" in text
+    # idle-hours as an extra is not double counted (it is a column already)
+    h2, _ = G.by_namespace([r[:4] + [0.0, r[4]] for r in rows], pod_ns, 86400, ["Idle GPU-h", "Energy kWh"])
+    assert h2 == G.NS_HEADER + ["Energy kWh"]
+
+
+def test_pod_namespaces_from_ksm_range_query():
+    from fakeprom import FakeProm
+
+    from kube_gpu_stats_amd.reports import gpu_util_stats as G
+    from kube_gpu_stats_amd.reports.promql import PromClient
+
+    fp = FakeProm()
+    fp.canned_range[G.POD_NS_QUERY] = [
+        {"metric": {"namespace": "ml", "pod": "a"}, "values": [[1, "1"]]},
+        {"metric": {"namespace": "vision", "pod": "c"}, "values": [[1, "1"]]}]
+    url = fp.start()
+    try:
+        assert G.pod_namespaces(PromClient(url), 0, 3600, 600) == {"a": "ml", "c": "vision"}
+    finally:
+        fp.stop()
+
+
+def test_cli_group_by_namespace_end_to_end(prom, capsys):
+    """`kgs gpu-util-stats --group-by namespace --format json` over the fake Prometheus."""
+    fp, url = prom
+    q = G.Queries.amd("", STEP)
+    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "pod_name": "p"},
+                           "values": [[T_END - 3600, "40"], [T_END, "60"]]},
+                          {"metric": {"kubernetes_io_hostname": "n1", "pod_name": "r"},
+                           "values": [[T_END - 3600, "100"], [T_END, "100"]]}])
+    fp.add_instant(q.total, [{"metric": {"node": "n1", q.type_label: "MI355X"}, "value": [T_END, "8"]}])
+    fp.add_instant(q.used, [{"metric": {"node": "n1"}, "value": [T_END, "6"]}])
+    fp.add_instant(q.live, [{"metric": {"pod": "p"}, "value": [T_END, "1"]},
+                            {"metric": {"pod": "r"}, "value": [T_END, "1"]}])
+    fp.add_range(q.req, [{"metric": {"node": "n1", "pod": "p"}, "values": [[T_END, "4"]]},
+                         {"metric": {"node": "n1", "pod": "r"}, "values": [[T_END, "2"]]}])
+    fp.add_range(G.POD_NS_QUERY, [{"metric": {"namespace": "ml", "pod": "p"}, "values": [[T_END, "1"]]},
+                                  {"metric": {"namespace": "infer", "pod": "r"}, "values": [[T_END, "1"]]}])
+    G.main(["--prom-url", url, "--namespace", "", "--window", "7200", "--step", str(STEP), "--end", str(T_END),
+            "--group-by", "namespace", "--format", "json"])
+    got = {r["Namespace"]: r for r in json.loads(capsys.readouterr().out)}
+    assert got["ml"]["GPU-h"] == 8.0 and got["ml"]["Util %"] == 50.0 and got["ml"]["Idle GPU-h"] == 4.0
+    assert got["infer"]["GPU-h"] == 4.0 and got["infer"]["Busy GPU-h"] == 4.0
+    assert got["TOTAL"]["Pods"] == 2 and abs(got["TOTAL"]["Util %"] - 100 * 8 / 12) < 1e-9
