@@ -103,11 +103,14 @@ def build() -> dict:
     add(_panel(0, "PCIe traffic (host link)", [(_dev("rate(amdgpu_pcie_bytes_total[1m])"), "gpu{{gpu}}")], 12, y,
                w=12, unit="Bps"))
     y += 8
-    add(_row(0, "xGMI", y)); y += 1
+    add(_row(0, "xGMI and RAS", y)); y += 1
     add(_panel(0, "xGMI traffic per GPU (read + write, all links)",
                [(_dev("sum by (instance, gpu) (rate(amdgpu_xgmi_read_bytes_total[1m]) + "
                       "rate(amdgpu_xgmi_write_bytes_total[1m]))"), "gpu{{gpu}}")], 0, y, unit="Bps"))
-    add(_panel(0, "xGMI errors", [(_dev("amdgpu_xgmi_error_status"), "gpu{{gpu}}")], 12, y))
+    add(_panel(0, "xGMI errors", [(_dev("amdgpu_xgmi_error_status"), "gpu{{gpu}}")], 12, y, w=6))
+    add(_panel(0, "ECC errors per RAS block (1 h)",
+               [(_dev("sum by (instance, gpu, block, type) (increase(amdgpu_ecc_block_errors_total[1h]))"),
+                 "gpu{{gpu}} {{block}} {{type}}")], 18, y, w=6))
     y += 8
     add(_row(0, "Processes", y)); y += 1
     add(_panel(0, "HBM per process", [("amdgpu_process_hbm_bytes", "{{pod}} pid {{pid}} gpu{{gpu}}")], 0, y,
@@ -116,12 +119,24 @@ def build() -> dict:
                [("rate(amdgpu_process_cu_seconds_total[1m])", "{{pod}} pid {{pid}} gpu{{gpu}}")], 12, y,
                unit="percentunit", maxv=1))
     y += 8
+    add(_panel(0, "Shared GPUs: compute share per pod",
+               [("sum by (kubernetes_io_hostname, gpu, namespace, pod) "
+                 "(rate(amdgpu_process_cu_seconds_total{pod!=\"\"}[5m]))", "{{namespace}}/{{pod}} gpu{{gpu}}")],
+               0, y, unit="percentunit", maxv=1))
+    add(_panel(0, "Shared GPUs: HBM per pod",
+               [("sum by (kubernetes_io_hostname, gpu, namespace, pod) (amdgpu_process_hbm_bytes{pod!=\"\"})",
+                 "{{namespace}}/{{pod}} gpu{{gpu}}")], 12, y, unit="bytes"))
+    y += 8
     add(_row(0, "Exporter health", y)); y += 1
     add(_panel(0, "Samples / s per GPU (PMFW distinct, counters)",
                [(_dev("rate(kgs_samples_total[1m])"), "pmfw gpu{{gpu}}"),
                 (_dev("rate(kgs_pmc_samples_total[1m])"), "pmc gpu{{gpu}}"),
                 (_dev("kgs_pmc_quiet"), "quiet (idle READ rate) gpu{{gpu}}")], 0, y, w=8))
-    add(_panel(0, "Scrape render time", [("kgs_scrape_render_last_seconds", "{{instance}}")], 8, y, w=8, unit="s"))
+    add(_panel(0, "Scrape render time / HTTP connections",
+               [("kgs_scrape_render_last_seconds", "render s {{instance}}"),
+                ("kgs_http_connections", "connections {{instance}}"),
+                ("increase(kgs_http_connections_closed_total[1h])", "closed/h {{reason}} {{instance}}")],
+               8, y, w=8))
     add(_panel(0, "Sampler up / recoveries / attribution age",
                [(_dev("kgs_up"), "up gpu{{gpu}}"), (_dev("increase(kgs_device_recoveries_total[1h])"),
                                                    "recoveries gpu{{gpu}}"),

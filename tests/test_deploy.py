@@ -46,7 +46,7 @@ def test_daemonset_handover_does_not_signal_pid1():
 PROMQL_WORDS = {"avg", "sum", "max", "min", "count", "rate", "increase", "avg_over_time", "label_values", "by", "or",
                 "and", "on", "without", "group_left", "group_right"}
 LABELS = {"kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "gpu", "instance", "sensor", "pod",
-          "pid", "xcc", "block"}
+          "pid", "xcc", "block", "type", "reason"}
 
 
 def unknown_series(exprs: str) -> set:
