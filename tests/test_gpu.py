@@ -1083,7 +1083,7 @@ def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     env = dict(os.environ, KGS_NO_BUILD="1")
-    kids = [subprocess.Popen([sys.executable, "-c", _TENANT, gib, busy, "12", REPO], stdout=subprocess.PIPE,
+    kids = [subprocess.Popen([sys.executable, "-c", _TENANT, gib, busy, "15", REPO], stdout=subprocess.PIPE,
                              text=True, env=env) for gib, busy in (("8", "1"), ("3", "0"))]
     ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 50, "proc_period_s": 0.1, "link_every": 0})
     ex.start()
@@ -1115,7 +1115,14 @@ def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
         assert share["a"] > 0.25 and share["b"] < 0.02, row
         ex.set_pid_owners({(0, a[0]): {"pod": "tenant-a", "namespace": "ml", "container": "main", "pod_uid": "ua"},
                            (0, b[0]): {"pod": "tenant-b", "namespace": "ml", "container": "main", "pod_uid": "ub"}})
-        body = ex.render()
+        # `kgs ps` view of the same node: two renders 1 s apart (the CLI scrapes /metrics)
+        from kube_gpu_stats_amd.reports import ps
+        from kube_gpu_stats_amd.utils.scrape import parse_text
+
+        t_a, body0 = time.time(), ex.render()
+        time.sleep(1.0)
+        t_b, body = time.time(), ex.render()
+        ps_rows = {r["pod"]: r for r in ps.rows_from(parse_text(body0), parse_text(body), t_b - t_a) if r["pod"]}
     finally:
         ex.stop()
         for k in kids:
@@ -1126,7 +1133,11 @@ def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
     lb = [ln for ln in lines if f'pid="{b[0]}"' in ln]
     assert len(la) == 1 and 'pod="tenant-a"' in la[0], lines
     assert len(lb) == 1 and 'pod="tenant-b"' in lb[0], lines
+    row["kgs_ps"] = ps_rows
     _keep("two_tenants.json", json.dumps(row, indent=1))
+    assert set(ps_rows) == {"tenant-a", "tenant-b"}, ps_rows
+    assert 8.0 <= ps_rows["tenant-a"]["hbm_gib"] < 8.75 and ps_rows["tenant-a"]["cu_share_pct"] > 25, ps_rows
+    assert 3.0 <= ps_rows["tenant-b"]["hbm_gib"] < 3.75 and ps_rows["tenant-b"]["cu_share_pct"] < 2, ps_rows
 
 
 def test_ecc_per_block_counts_on_mi355x(N):
