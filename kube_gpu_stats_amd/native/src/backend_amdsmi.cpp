@@ -59,6 +59,21 @@ struct Dev {
   alignas(64) uint8_t buf[4096];
 };
 
+// /proc/<pid>/comm without the trailing newline ("" if unreadable).
+std::string proc_comm(uint32_t pid) {
+  char path[64];
+  std::snprintf(path, sizeof path, "/proc/%u/comm", pid);
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return {};
+  char buf[64];
+  const ssize_t n = read(fd, buf, sizeof buf);
+  close(fd);
+  if (n <= 0) return {};
+  size_t len = static_cast<size_t>(n);
+  while (len > 0 && (buf[len - 1] == '\n' || buf[len - 1] == 0)) --len;
+  return std::string(buf, len);
+}
+
 class AmdSmiBackend final : public Backend {
  public:
   ~AmdSmiBackend() override {
@@ -134,21 +149,28 @@ class AmdSmiBackend final : public Backend {
   }
 
   int read_procs(int d, std::vector<ProcInfo>& out) override {
-    std::lock_guard<std::mutex> g(smi_mu_);
     out.clear();
-    uint32_t n = 0;
-    amdsmi_status_t st = amdsmi_get_gpu_process_list(devs_[d]->h, &n, nullptr);
-    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return -static_cast<int>(st);
-    if (n == 0) return 0;
-    std::vector<amdsmi_proc_info_t> list(n + 8);
-    uint32_t cap = static_cast<uint32_t>(list.size());
-    st = amdsmi_get_gpu_process_list(devs_[d]->h, &cap, list.data());
-    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return -static_cast<int>(st);
+    std::vector<amdsmi_proc_info_t> list;
+    uint32_t cap = 0;
+    {
+      std::lock_guard<std::mutex> g(smi_mu_);
+      uint32_t n = 0;
+      amdsmi_status_t st = amdsmi_get_gpu_process_list(devs_[d]->h, &n, nullptr);
+      if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return -static_cast<int>(st);
+      if (n == 0) return 0;
+      list.resize(n + 8);
+      cap = static_cast<uint32_t>(list.size());
+      st = amdsmi_get_gpu_process_list(devs_[d]->h, &cap, list.data());
+      if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return -static_cast<int>(st);
+    }
     for (uint32_t i = 0; i < cap && i < list.size(); ++i) {
       const auto& p = list[i];
       ProcInfo pi;
       pi.pid = p.pid;
-      pi.name = p.name;
+      pi.name.assign(p.name, strnlen(p.name, sizeof p.name));
+      // AMD SMI leaves the name empty where it cannot read it (seen on the gpurun box);
+      // with hostPID (the DaemonSet) the host's /proc has it.
+      if (pi.name.empty()) pi.name = proc_comm(p.pid);
       pi.vram_bytes = p.memory_usage.vram_mem;
       pi.gtt_bytes = p.memory_usage.gtt_mem;
       pi.cpu_bytes = p.memory_usage.cpu_mem;
