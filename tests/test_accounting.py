@@ -160,8 +160,14 @@ def test_report_energy_column_tiles_the_window(mock_exporter):
                     if ta <= t <= tb:
                         tot += va + (vb - va) * (t - ta) / (tb - ta)
             return tot
-        want = joules_at(end) - joules_at(end - window)
-        assert want > 0 and kwh[("node-a", "two")] * 3.6e6 == pytest.approx(want, rel=0.05)
+        # the range query runs on whole seconds (to_unix, like the reference): compare over
+        # the same window, so an energy transient near the first scrapes cannot sit in one
+        # window and not the other
+        e_int = float(int(end))
+        want = joules_at(e_int) - joules_at(e_int - window)
+        gaps = [round(b - a, 3) for a, b in zip(stamps, stamps[1:])]
+        assert want > 0 and kwh[("node-a", "two")] * 3.6e6 == pytest.approx(want, rel=0.05), \
+            {"got_j": kwh[("node-a", "two")] * 3.6e6, "want_j": want, "end": end, "scrape_gaps_s": gaps}
         rows = G.add_energy([["node-a", "two", 2, 60.0], ["node-a", "gone (finished)", 0, 0.0]], kwh)
         assert rows[0][4] == kwh[("node-a", "two")] and rows[1][4] == 0.0
         table = G.format_rows(rows, "pod", "table", compat=False, extras=["Energy kWh"])
