@@ -1194,7 +1194,7 @@ def test_counter_reader_in_process_next_to_hip(N, torch_dev):
     finally:
         ex.stop()
     print(json.dumps({"window": w, "pmc_samples": i["pmc_samples"]}))
-    assert i["pmc_samples"] >= 1000 and i["pmc_errors"] == 0, i
+    assert i["pmc_samples"] >= 700 and i["pmc_errors"] == 0, i  # ≈1.5 s at 1 kHz (r2an: 1490)
     assert w["mfma_util_pct"] > 80, w
     assert len(w["xcd_mfma_util_pct"]) == 8 and min(w["xcd_mfma_util_pct"]) > 70, w
 
