@@ -80,6 +80,11 @@ constexpr int64_t kPmcStallNs = 500000000;  // GRBM_COUNT without a plausible cl
 constexpr double kPlausibleMhzLo = 100.0, kPlausibleMhzHi = 4000.0;
 // Adaptive READ rate: an interval whose SPI-busy share is below this is quiet.
 constexpr double kQuietActiveFrac = 0.02;
+// ... and the device counts as quiet only after this long of quiet intervals in a
+// row: a host sync between kernels leaves the GPU idle for tens of µs, which is not
+// worth a drop to the idle READ rate (the first READ after it would come up to one
+// idle period late, and every tick in between is a lost sample).
+constexpr int64_t kQuietHoldNs = 5000000;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 
 struct DeviceState {

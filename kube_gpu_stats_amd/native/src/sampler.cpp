@@ -232,6 +232,7 @@ void Sampler::run(int dev) {
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
   uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0;
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
+  int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
   int64_t last_pmc_ns = 0;
   int64_t prev_ps_ns = 0;
@@ -319,6 +320,7 @@ void Sampler::run(int dev) {
             st.pmc_on.store(1);
             have_prev_ps = false;
             quiet = false;
+            quiet_since_ns = 0;
             fresh_mode = false;  // a (re)opened session reads pipelined
             last_plausible_ns = now_c;
             last_start_ns = now_c;
@@ -370,13 +372,18 @@ void Sampler::run(int dev) {
         // (nearly) blind to our own READs: SPI busy reads 0.65 % with nothing but
         // 8 kHz of READs on the GPU (profiles/r2/immunity/).
         // Without the activity counter in the set a device is never quiet.
+        bool quiet_interval = false;
         if (have_prev_ps && (ps.mask & (1u << kPmcGrbmActive)) && ps.value[kPmcGrbmCount] > prev_ps_count) {
           const double act = static_cast<double>(ps.value[kPmcGrbmActive] - std::min(ps.value[kPmcGrbmActive], prev_ps_active));
           const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
-          quiet = act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma;
-        } else {
-          quiet = false;
+          quiet_interval = act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma;
         }
+        if (!quiet_interval) {
+          quiet_since_ns = 0;
+        } else if (quiet_since_ns == 0) {
+          quiet_since_ns = prev_ps_ns;  // the interval began at the previous READ
+        }
+        quiet = quiet_interval && ps.mono_ns - quiet_since_ns >= kQuietHoldNs;
         st.pmc_quiet.store(quiet ? 1 : 0, std::memory_order_relaxed);
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
@@ -426,6 +433,7 @@ void Sampler::run(int dev) {
           }
           have_prev_ps = false;
           quiet = false;
+          quiet_since_ns = 0;
           fresh_mode = false;
           last_plausible_ns = mono_ns();  // a full reclaim period before the next one
         }
