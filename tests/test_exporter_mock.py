@@ -717,3 +717,23 @@ def test_xgmi_bytes_unit_is_configurable(mock_exporter):
     m2 = parse_text(ex2.render())
     got2 = {lb["link"]: v for lb, v in m2["amdgpu_xgmi_read_bytes_total"] if lb["gpu"] == "0"}
     assert got2 and all(got2[k] == kb2[int(k)] * 1000 for k in got2), (got2, kb2)
+
+
+def test_short_idle_gaps_do_not_drop_to_the_idle_rate(mock_exporter):
+    """Quiet hysteresis (r2be): a busy GPU whose kernels are separated by short gaps
+    (here 2 ms idle in every 20 ms) stays on every tick — a device counts as quiet
+    only after 5 ms of quiet READ intervals; a 25 ms gap still drops to the idle rate."""
+    def skips_per_s(ex, secs=1.0):
+        k0 = ex.integrals(0)["pmc_quiet_skips"]
+        time.sleep(secs)
+        return (ex.integrals(0)["pmc_quiet_skips"] - k0) / secs
+
+    short = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=50,
+                          mock={"square_duty": 0.9, "util_period_s": 0.02, "util_base": 50, "util_amp": 50})
+    time.sleep(0.3)
+    assert skips_per_s(short) == 0                       # 2 ms gaps: never quiet
+    short.stop()
+    long_gap = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=50,
+                             mock={"square_duty": 0.5, "util_period_s": 0.05, "util_base": 50, "util_amp": 50})
+    time.sleep(0.3)
+    assert skips_per_s(long_gap) > 200                   # 25 ms gaps: ≈20 ms of each at the idle rate
