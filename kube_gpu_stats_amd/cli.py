@@ -39,6 +39,8 @@ def main(argv=None) -> int:
     pm.add_argument("action", choices=["release", "acquire", "status"])
     pm.add_argument("--exporter", default="127.0.0.1:9400", help="host:port of the exporter (loopback only)")
     pm.add_argument("--pid-file", default="", help="signal the PID in this file instead of using HTTP")
+    pm.add_argument("--gpu", type=int, default=-1, help="this GPU only (exporter index; default every GPU). Each "
+                    "GPU's own sampler thread acts, so a hung GPU never delays the others")
     sub.add_parser("bench", help="run the headline benchmark (bench.py; flags pass through)", add_help=False)
     sp = sub.add_parser("scrape", help="scrape an exporter once and print selected families")
     sp.add_argument("url", nargs="?", default="http://127.0.0.1:9400/metrics")
@@ -97,6 +99,8 @@ def pmc_control(a) -> int:
         import os
         import signal
 
+        if a.gpu >= 0:
+            raise SystemExit("--gpu needs the HTTP control endpoint (drop --pid-file)")
         with open(a.pid_file) as f:
             pid = int(f.read().strip())
         if a.action != "status":
@@ -107,10 +111,13 @@ def pmc_control(a) -> int:
 
     path = {"release": "/control/pmc/release", "acquire": "/control/pmc/acquire"}.get(a.action)
     if path:
-        print(urllib.request.urlopen(f"http://{a.exporter}{path}", timeout=10).read().decode())
+        q = f"?gpu={a.gpu}" if a.gpu >= 0 else ""
+        print(urllib.request.urlopen(f"http://{a.exporter}{path}{q}", timeout=10).read().decode())
         return 0
     body = urllib.request.urlopen(f"http://{a.exporter}/metrics", timeout=10).read().decode()
-    print("\n".join(ln for ln in body.splitlines() if ln.startswith(("kgs_pmc_enabled", "kgs_pmc_stalled"))))
+    print("\n".join(ln for ln in body.splitlines()
+                    if ln.startswith(("kgs_pmc_enabled", "kgs_pmc_stalled", "kgs_pmc_failed", "kgs_sampler_thread_hung"))
+                    and (a.gpu < 0 or f'gpu="{a.gpu}"' in ln)))
     return 0
 
 

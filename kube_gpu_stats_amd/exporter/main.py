@@ -73,6 +73,14 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                        "command-processor packet that GFX busy / GUI-active count as work (≈80 / "
                                        "190 µs each), so a quiet GPU is read at this rate and a busy one every tick "
                                        "(0 = every tick: profiling mode)")
+    add_flag(ap, "pmc-timeout-ms", 250, "bound of every wait on the command processor (counter READ, START, STOP, "
+                                        "queue slot): a wedged CP costs one timeout, never a hang")
+    add_flag(ap, "pmc-breaker-k", 3, "consecutive failed counter drains that open the counter tier's circuit breaker "
+                                     "(kgs_pmc_failed = 1: READs stop, the reader's queue is recreated)")
+    add_flag(ap, "pmc-retry-s", 1.0, "first retry (reset + re-START) after the breaker opened; doubles per failed retry")
+    add_flag(ap, "pmc-retry-max-s", 60.0, "longest retry interval of the counter tier's breaker")
+    add_flag(ap, "stop-timeout", 1.0, "shutdown waits this long for the sampler threads, then abandons any stuck in a "
+                                      "device call (the exporter still exits on SIGTERM during a GPU hang)")
     add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
     add_flag(ap, "node-name", os.environ.get("NODE_NAME", ""), "kubernetes_io_hostname label (downward API NODE_NAME)")
     add_flag(ap, "gpu-type", "", "override the nvidia_gpu_type / gpu_type label value")
@@ -134,6 +142,11 @@ def config_from_args(a) -> dict:
         "pmc_reclaim_s": a.pmc_reclaim_s,
         "pmc_refresh_s": a.pmc_refresh_s,
         "pmc_idle_hz": a.pmc_idle_hz,
+        "pmc_timeout_ms": a.pmc_timeout_ms,
+        "pmc_breaker_k": a.pmc_breaker_k,
+        "pmc_retry_s": a.pmc_retry_s,
+        "pmc_retry_max_s": a.pmc_retry_max_s,
+        "stop_timeout_s": a.stop_timeout,
         "listen_addr": host or "0.0.0.0",
         "port": int(port),
         "node_name": a.node_name,
@@ -231,7 +244,14 @@ def run(a) -> int:
     attr.stop()
     ex.stop()
     print(json.dumps({"event": "stopped", "integrals": [ex.integrals(i) for i in range(ex.device_count)],
-                      "pmc_info": [ex.pmc_info(i) for i in range(ex.device_count)]}), flush=True)
+                      "pmc_info": [ex.pmc_info(i) for i in range(ex.device_count)],
+                      "abandoned_threads": ex.abandoned_threads}), flush=True)
+    if ex.abandoned_threads:
+        # A sampler thread is stuck in a device call (a hung GPU): leave without
+        # running the runtime's static destructors under it.
+        L.warning("%d sampler thread(s) stuck in a device call; exiting without teardown", ex.abandoned_threads)
+        sys.stderr.flush()
+        os._exit(0)
     return 0
 
 

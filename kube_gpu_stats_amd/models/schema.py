@@ -38,7 +38,7 @@ CATALOG: tuple[Family, ...] = (
       "container_gpu_sm_util.  GFX busy counts a GPU busy while any dispatch is in flight; this says how much of "
       "that was matrix work.  `kgs gpu-util-stats --util-metric container_gpu_mfma_util` reports it per pod.",
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
-      "rocprofiler+kubelet", "pmc"),
+      "counters+kubelet", "pmc"),
     F("container_gpu_busy_seconds_total", "counter",
       "GFX-busy seconds of the GPU allocated to the pod, counted from the allocation (PMFW accumulators).  "
       "`100 * avg(rate(container_gpu_busy_seconds_total[1h])) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)` "
@@ -50,12 +50,21 @@ CATALOG: tuple[Family, ...] = (
       "MFMA-busy seconds (all SIMDs busy with matrix work for 1 s = 1) of the GPU allocated to the pod, counted from "
       "the allocation (hardware counters).  Same labels as container_gpu_sm_util.",
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
-      "rocprofiler+kubelet", "pmc"),
+      "counters+kubelet", "pmc"),
+    F("container_gpu_cu_seconds_total", "counter",
+      "CU-occupancy seconds of the pod's own processes on the GPU (occupied CUs / all CUs, integrated by the "
+      "per-process tier; processes that exited included), counted from the allocation.  100 * rate() is the pod's "
+      "compute share: on a GPU shared by several pods each is billed its own share "
+      "(`kgs gpu-util-stats --util-metric container_gpu_cu_seconds_total`), where container_gpu_busy_seconds_total "
+      "bills each the whole GPU.  Same labels as container_gpu_sm_util.",
+      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      "amdsmi-procs+cgroups+kubelet", "procs"),
     F("container_gpu_energy_joules_total", "counter",
       "Socket energy of the GPU allocated to the pod, counted from the allocation (PMFW energy accumulator).  "
-      "`sum(increase(container_gpu_energy_joules_total[1h])) by (kubernetes_io_hostname, pod_name)` is the pod's "
-      "hourly energy; `kgs gpu-util-stats --energy` reports it in kWh.  A GPU shared by several pods counts in full "
-      "for each.  Same labels as container_gpu_sm_util.",
+      "`sum(increase(container_gpu_energy_joules_total[1h])) by (kubernetes_io_hostname, namespace, pod_name)` is "
+      "the pod's hourly energy; `kgs gpu-util-stats --energy` reports it in kWh.  A GPU shared by several pods "
+      "counts in full for each; a compute partition (DPX/QPX/CPX) counts its XCCs' GFX-busy share of the socket's "
+      "energy, so partitions add up to the socket.  Same labels as container_gpu_sm_util.",
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
       "pmfw+kubelet", "fast"),
     F("kgs_gpu_owner", "gauge",
@@ -93,12 +102,12 @@ CATALOG: tuple[Family, ...] = (
     # ---- thermals / power / clocks -----------------------------------------------------------
     F("amdgpu_temperature_celsius", "gauge", "Temperature by sensor (hotspot, hbm, vrsoc).", extra=("sensor",)),
     F("amdgpu_power_watts", "gauge", "Socket power."),
-    F("amdgpu_energy_joules_total", "counter", "Energy since exporter start (wrap-safe)."),
+    F("amdgpu_energy_joules_total", "counter", "Energy since exporter start (wrap-safe); a compute partition counts "
+      "its XCCs' GFX-busy share of the socket's energy."),
     F("amdgpu_clock_mhz", "gauge", "Current clock (gfx = mean over XCCs, mem, soc).", extra=("clock",)),
     F("amdgpu_throttle_seconds_total", "counter", "Seconds the GPU ran held back, per throttler (PMFW residency "
       "accumulators ÷ accumulation cycles × time); 100 * rate() = violation % (amdsmi PVIOL for reason=\"ppt\", TVIOL "
       "for reason=\"socket_thermal\").", extra=("reason",)),
-    F("amdgpu_power_throttle_residency_total", "counter", "PMFW PPT throttle residency accumulator (raw)."),
     # ---- interconnect ------------------------------------------------------------------------
     F("amdgpu_xgmi_read_bytes_total", "counter", "Bytes received per xGMI link.", extra=("link",)),
     F("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link.", extra=("link",)),
@@ -114,36 +123,36 @@ CATALOG: tuple[Family, ...] = (
       tier="slow"),
     F("amdgpu_xgmi_error_status", "gauge", "xGMI error status (0 none, 1 error, 2 multiple).", source="amdsmi",
       tier="slow"),
-    # ---- hardware counters (rocprofiler-sdk device counting) -----------------------------------
+    # ---- hardware counters (direct command-processor reader, native/counters/pmc_aqlprofile.cpp) --
     F("amdgpu_pmc_total", "counter", "Raw hardware counter since exporter start.", extra=("counter",),
-      source="rocprofiler", tier="pmc"),
-    F("amdgpu_mfma_util_percent", "gauge", "Matrix-core busy % of active cycles (window).", source="rocprofiler",
+      source="counters", tier="pmc"),
+    F("amdgpu_mfma_util_percent", "gauge", "Matrix-core busy % of active cycles (window).", source="counters",
       tier="pmc"),
     F("amdgpu_gpu_active_seconds_total", "counter",
       "∫ GPU-active share of clocks dt (per drain: ΔGRBM_SPI_BUSY / ΔGRBM_COUNT · Δt); rate() = GPU-active fraction, "
-      "blind to the exporter's own counter READs (the --sm-util-source counters integral).", source="rocprofiler",
+      "blind to the exporter's own counter READs (the --sm-util-source counters integral).", source="counters",
       tier="pmc"),
     F("amdgpu_mfma_busy_seconds_total", "counter",
       "∫ MFMA-busy share of all SIMD cycles dt (per drain: ΔSQ_VALU_MFMA_BUSY_CYCLES / (SIMDs·ΔGRBM_COUNT) · Δt); "
-      "rate() = matrix-core utilisation of wall time.", source="rocprofiler", tier="pmc"),
+      "rate() = matrix-core utilisation of wall time.", source="counters", tier="pmc"),
     F("amdgpu_gpu_active_percent", "gauge", "% of clocks a shader engine had waves to run (GRBM_SPI_BUSY, window); "
-      "unlike the PMFW GFX busy it does not count the exporter's own counter READs.", source="rocprofiler", tier="pmc"),
+      "unlike the PMFW GFX busy it does not count the exporter's own counter READs.", source="counters", tier="pmc"),
     F("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy % of active cycles (window).",
-      source="rocprofiler", tier="pmc"),
+      source="counters", tier="pmc"),
     F("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT (window).",
-      source="rocprofiler", tier="pmc"),
+      source="counters", tier="pmc"),
     F("amdgpu_mfma_util_xcc_percent", "gauge",
       "Matrix-core busy % of one XCD's active SIMD cycles (window; aqlprofile reader, results placed on XCDs in "
       "the READ buffer's XCC-major order, verified against an XCC-gated load).  An XCD left idle while others "
       "saturate is a workgroup→XCD mapping problem, invisible in the device-wide gauges.",
-      extra=("xcc",), source="rocprofiler", tier="pmc"),
+      extra=("xcc",), source="counters", tier="pmc"),
     F("amdgpu_vmem_busy_xcc_percent", "gauge",
       "Vector-memory address unit (TA) busy % of one XCD's active cycles, mean over its CUs (window; --pmc-set full).",
-      extra=("xcc",), source="rocprofiler", tier="pmc"),
+      extra=("xcc",), source="counters", tier="pmc"),
     F("amdgpu_gpu_active_xcc_percent", "gauge",
       "GRBM SPI-busy % of clocks of one XCD (window): one of its shader engines has waves to run.  Unlike GUI-active "
       "(which reads ~100 % on every XCD while any chip-wide dispatch is in flight) it shows where waves run.",
-      extra=("xcc",), source="rocprofiler", tier="pmc"),
+      extra=("xcc",), source="counters", tier="pmc"),
     # ---- per process -------------------------------------------------------------------------
     F("amdgpu_process_hbm_bytes", "gauge", "HBM bytes held by a process.",
       extra=("pid", "process", "pod", "namespace", "container", "pod_uid"), source="amdsmi", tier="mid"),
@@ -178,6 +187,16 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_quiet", "gauge", "1 while the last counter READ interval saw no wave and no MFMA cycle: READs drop to "
       "--pmc-idle-hz so the exporter's own packets do not read as GPU activity.", source="self"),
     F("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU.",
+      source="self"),
+    F("kgs_pmc_failed", "gauge", "1 while the counter tier's circuit breaker is open: --pmc-breaker-k consecutive "
+      "counter drains failed (a wedged command processor).  READs stop; after --pmc-retry-s (doubling to "
+      "--pmc-retry-max-s) the reader's AQL queue is recreated and the counters re-STARTed.  The PMFW tier of the "
+      "same GPU runs on its own thread and keeps reporting.", source="self"),
+    F("kgs_pmc_breaker_trips_total", "counter", "Times the counter tier's circuit breaker opened.", source="self"),
+    F("kgs_pmc_retries_total", "counter", "Reader resets + re-STARTs attempted while the breaker was open.",
+      source="self"),
+    F("kgs_sampler_thread_hung", "gauge", "1 if a sampler thread of the device was stuck in a device call when "
+      "sampling last stopped: it was abandoned (--stop-timeout) and that tier restarts once the call returns.",
       source="self"),
     F("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples.", source="self"),
     F("kgs_slow_reads_total", "counter",

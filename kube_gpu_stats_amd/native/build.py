@@ -117,11 +117,12 @@ def build_pmc_aql(force: bool = False, verbose: bool = False) -> str:
     """Direct CP counter reader over aqlprofile (no profiler framework, no spinning helper thread)."""
     out = pmc_aql_lib_path()
     src = os.path.join(HERE, "counters", "pmc_aqlprofile.cpp")
-    if not force and not _stale(out, [src, __file__]):
+    if not force and not _stale(out, [src, os.path.join(HERE, "include", "kgs", "aql_ring.h"), __file__]):
         return out
     os.makedirs(LIB, exist_ok=True)
     tmp = f"{out}.{os.getpid()}.tmp"
     _run(["g++", *CXXFLAGS, "-fvisibility=default", "-D__HIP_PLATFORM_AMD__=1", "-I" + os.path.join(ROCM, "include"),
+          "-I" + os.path.join(HERE, "include"),
           "-shared", src, "-o", tmp, "-L" + os.path.join(ROCM, "lib"), "-lhsa-runtime64", "-lhsa-amd-aqlprofile64",
           "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose)
     os.replace(tmp, out)

@@ -24,7 +24,19 @@
 //     after the results (profiles/launch_overhead.md);
 //   * results are folded per counter over every block instance / XCC sample
 //     (max for GRBM clocks, sum for SQ busy cycles, mean for TA busy), the same
-//     reductions as the rocprofiler path, and reported cumulative since START.
+//     reductions as the rocprofiler path, and reported cumulative since START;
+//   * every wait is bounded (fault boundary): a queue slot is
+//     reserved only when there is room (include/kgs/aql_ring.h), a completion is
+//     waited for at most --pmc-timeout-ms, and kgs_pmc_abort() makes a blocked
+//     call return at once (Sampler::stop()).  A wedged command processor costs the
+//     caller one timeout per call, never a spin; kgs_pmc_reset() destroys the
+//     agent's queue so the next open starts on a fresh one.
+//
+// Threading: every call on one handle comes from one thread (the device's
+// sampler thread); handles of different GPUs share no lock, so a slow or hung
+// GPU never delays another's READs.  kgs_pmc_info() may be called from any
+// thread: it reads atomics and the error string under a lock that is never held
+// across a wait.
 //
 // Counter selects for gfx950 (block, event) come from ROCm's own definitions
 // (/opt/rocm/share/rocprofiler-sdk/counter_defs.yaml); any other counter can be
@@ -32,6 +44,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <hsa/hsa_ven_amd_aqlprofile.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -44,6 +57,8 @@
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include "kgs/aql_ring.h"
 
 namespace {
 
@@ -122,8 +137,13 @@ struct Agent {
   int64_t host_ns = 0;                               // host time spent inside sample()
   uint32_t cmd_sz = 0, out_sz = 0;
   int lean_changed = 0;                              // packets rewritten by lean_read_ib
-  std::string err;
-  uint64_t reads = 0, timeouts = 0;
+  std::string err;                                   // guarded by info_mu (read by kgs_pmc_info from any thread)
+  std::mutex info_mu;                                // never held across a wait
+  std::atomic<uint64_t> reads{0}, timeouts{0};
+  std::atomic<uint64_t> enqueue_timeouts{0};         // no queue slot within the deadline (CP not consuming)
+  std::atomic<uint64_t> aborted{0};                  // waits cut short by kgs_pmc_abort
+  std::atomic<uint64_t> resets{0};                   // queues destroyed by kgs_pmc_reset
+  std::atomic<int> abort{0};                         // kgs_pmc_abort: blocked / new waits return at once
   uint32_t last_results = 0;
   std::vector<uint32_t> instances;                   // results folded per counter (last read)
   std::vector<double> vals;
@@ -168,8 +188,11 @@ int64_t dump_results_at() {
   return n;
 }
 
-std::mutex g_mu;
-std::vector<Agent*> g_agents;
+std::vector<Agent*> g_agents;  // built once by kgs_pmc_init, never resized afterwards
+// Upper bound of every wait on the command processor: a queue slot, a READ, a
+// START / STOP.  A READ takes ≈10-200 µs; 250 ms is three orders of magnitude of
+// slack and still lets a sampler notice a wedged CP within a second.
+std::atomic<int64_t> g_timeout_ns{250000000};
 hsa_amd_memory_pool_t g_host_pool{};
 bool g_have_pool = false;
 std::string g_init_err;
@@ -351,14 +374,24 @@ const ClockMap& hsa_clock() {
   return m;
 }
 
-// Put one PM4-IB vendor packet on the agent's private queue (no wait).
-void enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig,
-             std::pair<int, int> fences = kSystemFences) {
+// Put one PM4-IB vendor packet on the agent's private queue.  Waits for a free
+// slot at most g_timeout_ns (a full queue means the CP stopped consuming it);
+// 0 = queued, -1 = no slot (timeout or abort; nothing was reserved).
+int enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig,
+            std::pair<int, int> fences = kSystemFences) {
   hsa_queue_t* q = a->queue;
-  hsa_signal_store_relaxed(sig, 1);
-  const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
-  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+  if (!q) return -1;
+  uint64_t idx = 0;
+  const kgs::SlotResult r = kgs::reserve_slot(
+      q->size, mono_ns() + g_timeout_ns.load(std::memory_order_relaxed), &a->abort,
+      [q] { return hsa_queue_load_read_index_scacquire(q); }, [q] { return hsa_queue_load_write_index_relaxed(q); },
+      [q](uint64_t i) { hsa_queue_store_write_index_relaxed(q, i + 1); }, [] { return mono_ns(); },
+      [] { sched_yield(); }, idx);
+  if (r != kgs::SlotResult::kOk) {
+    (r == kgs::SlotResult::kAborted ? a->aborted : a->enqueue_timeouts).fetch_add(1, std::memory_order_relaxed);
+    return -1;
   }
+  hsa_signal_store_relaxed(sig, 1);
   auto* slot = reinterpret_cast<hsa_ext_amd_aql_pm4_packet_t*>(q->base_address) + (idx & (q->size - 1));
   std::memcpy(slot->pm4_command, tmpl.pm4_command, sizeof slot->pm4_command);
   slot->completion_signal = sig;
@@ -368,25 +401,32 @@ void enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t si
       (fences.second << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(q->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+  return 0;
 }
 
-// Wait for a packet's completion signal.  BLOCKED: ROCr spins briefly, then
-// sleeps on the signal's KFD event.
-int wait_done(Agent* a, hsa_signal_t sig, uint64_t timeout_ns) {
-  const int64_t end = mono_ns() + static_cast<int64_t>(timeout_ns);
-  while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, timeout_ns, HSA_WAIT_STATE_BLOCKED) != 0) {
+// Wait for a packet's completion signal, at most g_timeout_ns, in 10 ms slices so
+// that kgs_pmc_abort() ends the wait promptly.  BLOCKED: ROCr spins briefly, then
+// sleeps on the signal's KFD event.  0 = done, -1 = timeout, -3 = aborted.
+int wait_done(Agent* a, hsa_signal_t sig) {
+  const int64_t end = mono_ns() + g_timeout_ns.load(std::memory_order_relaxed);
+  constexpr uint64_t kSliceNs = 10000000;
+  while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, kSliceNs, HSA_WAIT_STATE_BLOCKED) != 0) {
+    if (a->abort.load(std::memory_order_relaxed)) {
+      a->aborted.fetch_add(1, std::memory_order_relaxed);
+      return -3;
+    }
     if (mono_ns() > end) {
-      ++a->timeouts;
+      a->timeouts.fetch_add(1, std::memory_order_relaxed);
       return -1;
     }
   }
   return 0;
 }
 
-// Put one packet on the queue and wait for it.
-int submit(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, uint64_t timeout_ns) {
-  enqueue(a, tmpl, a->sig);
-  return wait_done(a, a->sig, timeout_ns);
+// Put one packet on the queue and wait for it (both bounded).
+int submit(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl) {
+  if (enqueue(a, tmpl, a->sig) != 0) return -1;
+  return wait_done(a, a->sig);
 }
 
 struct Fold {
@@ -406,7 +446,7 @@ hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
     a->res_xcd.push_back(x);
     a->res_slot.emplace_back(-1, 0);
   }
-  if (static_cast<int64_t>(a->reads) == dump_results_at()) {
+  if (static_cast<int64_t>(a->reads.load(std::memory_order_relaxed)) == dump_results_at()) {
     std::fprintf(stderr, "[aql-res] ord=%u sid=%u block=%d idx=%u ev=%u val=%llu coords:", ord, d->sample_id,
                  static_cast<int>(d->pmc_data.event.block_name), d->pmc_data.event.block_index,
                  d->pmc_data.event.counter_id, static_cast<unsigned long long>(d->pmc_data.result));
@@ -572,7 +612,7 @@ void place_xcds(Agent* a) {
 
 // Fold one completed READ's output buffer into a->vals.
 int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
-  ++a->reads;
+  a->reads.fetch_add(1, std::memory_order_relaxed);
   a->vals.assign(a->names.size(), 0.0);
   a->instances.assign(a->names.size(), 0);
   a->vals_xcd.assign(a->names.size() * kMaxXcd, 0.0);
@@ -598,7 +638,7 @@ int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
 int read_values(Agent* a) {
   std::memset(a->out, 0, a->prof.output_buffer.size);
   const int64_t t0 = mono_ns();
-  if (submit(a, a->read_pkt, 1000000000ull) != 0) return -2;
+  if (submit(a, a->read_pkt) != 0) return -2;
   const int64_t rtt = mono_ns() - t0;
   a->rtt_ns = a->rtt_ns ? (7 * a->rtt_ns + rtt) / 8 : rtt;
   return fold(a, &a->prof);
@@ -614,8 +654,7 @@ int read_pipelined(Agent* a, int64_t* ts) {
     if (ts) *ts = t0 + a->rtt_ns / 2;
     std::memset(a->pout[0], 0, a->pprof[0].output_buffer.size);
     a->psubmit_ns[0] = mono_ns();
-    enqueue(a, a->pread[0], a->psig[0], read_fences());
-    a->inflight = 0;
+    a->inflight = enqueue(a, a->pread[0], a->psig[0], read_fences()) == 0 ? 0 : -1;
     return 0;
   }
   const int k = a->inflight;
@@ -623,7 +662,7 @@ int read_pipelined(Agent* a, int64_t* ts) {
     ++a->ready_on_poll;
   } else {
     ++a->waited_on_poll;
-    if (wait_done(a, a->psig[k], 1000000000ull) != 0) {
+    if (wait_done(a, a->psig[k]) != 0) {
       a->inflight = -1;  // the packet may still complete later; its slot is re-armed before reuse
       return -2;
     }
@@ -659,8 +698,9 @@ int read_pipelined(Agent* a, int64_t* ts) {
   const int n = k ^ 1;
   std::memset(a->pout[n], 0, a->pprof[n].output_buffer.size);
   a->psubmit_ns[n] = mono_ns();
-  enqueue(a, a->pread[n], a->psig[n], read_fences());
-  a->inflight = n;
+  // No slot for the next READ: these values stand, the next call primes again
+  // (and fails there if the CP is still not consuming).
+  a->inflight = enqueue(a, a->pread[n], a->psig[n], read_fences()) == 0 ? n : -1;
   return rc;
 }
 
@@ -718,9 +758,14 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
 
 // Reader options, applied to counter sessions opened afterwards.  Keys: "lean"
 // (READ packet mode 0-3, see lean_read_ib).  0 = ok, -1 = unknown key / value.
+// "timeout_ms" (1..60000): bound of every wait on the CP (default 250).
 int kgs_pmc_configure(const char* key, int value) {
   if (key && std::strcmp(key, "lean") == 0 && value >= 0 && value <= 3) {
     g_lean = value;
+    return 0;
+  }
+  if (key && std::strcmp(key, "timeout_ms") == 0 && value >= 1 && value <= 60000) {
+    g_timeout_ns.store(static_cast<int64_t>(value) * 1000000LL);
     return 0;
   }
   return -1;
@@ -756,7 +801,6 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     set_err(err, errlen, "bad counter count");
     return -1;
   }
-  std::lock_guard<std::mutex> g(g_mu);
   for (size_t h = 0; h < g_agents.size(); ++h) {
     Agent* a = g_agents[h];
     if (a->gpu_id != kfd_gpu_id) continue;
@@ -815,10 +859,10 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
           hsa_amd_queue_set_priority(a->queue, static_cast<hsa_amd_queue_priority_t>(queue_priority())) !=
               HSA_STATUS_SUCCESS)
         KGS_DBG("hsa_amd_queue_set_priority(%d) failed\n", queue_priority());
-      if (hsa_signal_create(1, 0, nullptr, &a->sig) != HSA_STATUS_SUCCESS) {
-        set_err(err, errlen, "hsa_signal_create failed");
-        return -1;
-      }
+    }
+    if (!a->sig.handle && hsa_signal_create(1, 0, nullptr, &a->sig) != HSA_STATUS_SUCCESS) {  // kept across resets
+      set_err(err, errlen, "hsa_signal_create failed");
+      return -1;
     }
     // A re-open rebuilt a->events: the pipelined READ slots of the previous session
     // must point at the new array (same list: a hand-over / refresh re-START), or
@@ -891,18 +935,23 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       set_err(err, errlen, b);
       return -1;
     }
-    if (submit(a, a->start_pkt, 1000000000ull) != 0) {
-      set_err(err, errlen, "START packet did not complete within 1 s");
+    a->inflight = -1;
+    if (submit(a, a->start_pkt) != 0) {
+      set_err(err, errlen, "START packet did not complete within " +
+                               std::to_string(g_timeout_ns.load() / 1000000) + " ms");
       return -1;
     }
     a->started = true;
     if (read_values(a) != 0) {
       set_err(err, errlen, "initial READ failed");
-      submit(a, a->stop_pkt, 1000000000ull);
+      submit(a, a->stop_pkt);
       a->started = false;
       return -1;
     }
-    if (!missing.empty()) a->err = "unresolved: " + missing;
+    if (!missing.empty()) {
+      std::lock_guard<std::mutex> g(a->info_mu);
+      a->err = "unresolved: " + missing;
+    }
     return static_cast<int>(h);
   }
   set_err(err, errlen, "no HSA GPU agent with kfd gpu_id " + std::to_string(kfd_gpu_id));
@@ -961,11 +1010,10 @@ int kgs_pmc_sample_xcd(int handle, int counter, uint64_t* out, int max_xcd) {
 // pipelined READs (collect the previous one, submit the next).  0 = ok.
 int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
   if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
-  std::lock_guard<std::mutex> g(g_mu);
   Agent* a = g_agents[static_cast<size_t>(handle)];
   if (!a->started) return -1;
-  if (a->inflight >= 0) {  // drain before changing mode
-    wait_done(a, a->psig[a->inflight], 1000000000ull);
+  if (a->inflight >= 0) {  // drain before changing mode (bounded; a READ still queued is re-armed before reuse)
+    wait_done(a, a->psig[a->inflight]);
     a->inflight = -1;
   }
   if (on && (!a->pcmd[0] || !same_events(a->pipe_events, a->events))) {
@@ -984,36 +1032,69 @@ int kgs_pmc_info(int handle, char* buf, int len) {
   Agent* a = g_agents[static_cast<size_t>(handle)];
   std::string o = "impl=aqlprofile;mode=cumulative;cu=" + std::to_string(a->cu_count) +
                   ";events=" + std::to_string(a->events.size()) +
-                  ";results=" + std::to_string(a->last_results) + ";timeouts=" + std::to_string(a->timeouts) +
+                  ";results=" + std::to_string(a->last_results) + ";timeouts=" + std::to_string(a->timeouts.load()) +
+                  ";enqueue_timeouts=" + std::to_string(a->enqueue_timeouts.load()) +
+                  ";aborted=" + std::to_string(a->aborted.load()) + ";resets=" + std::to_string(a->resets.load()) +
+                  ";timeout_ms=" + std::to_string(g_timeout_ns.load() / 1000000) +
                   ";pipelined=" + std::to_string(a->pipelined ? 1 : 0) + ";rtt_us=" + std::to_string(a->rtt_ns / 1000) +
-                  ";reads=" + std::to_string(a->reads) + ";ready_on_poll=" + std::to_string(a->ready_on_poll) +
+                  ";reads=" + std::to_string(a->reads.load()) + ";ready_on_poll=" + std::to_string(a->ready_on_poll) +
                   ";waited_on_poll=" + std::to_string(a->waited_on_poll) +
-                  ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads : 0.0) +
+                  ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads.load() : 0.0) +
                   ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed) +
                   ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
                   a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc) + ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
                   ";signal=" + (poll_signals() ? "poll" : "interrupt");
   for (size_t k = 0; k < a->names.size(); ++k)
     o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
-  if (!a->err.empty()) o += ";" + a->err;
+  {
+    std::lock_guard<std::mutex> g(a->info_mu);
+    if (!a->err.empty()) o += ";" + a->err;
+  }
   set_err(buf, len, o);
   return 0;
 }
 
 int kgs_pmc_mode(int handle) { return handle >= 0 && static_cast<size_t>(handle) < g_agents.size() ? 1 : -1; }
 
+// STOP the session (bounded: a wedged CP costs at most two timeouts).
 void kgs_pmc_close(int handle) {
   if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return;
-  std::lock_guard<std::mutex> g(g_mu);
   Agent* a = g_agents[static_cast<size_t>(handle)];
   if (a->started) {
     if (a->inflight >= 0) {
-      wait_done(a, a->psig[a->inflight], 1000000000ull);
+      wait_done(a, a->psig[a->inflight]);
       a->inflight = -1;
     }
-    submit(a, a->stop_pkt, 1000000000ull);
+    submit(a, a->stop_pkt);
     a->started = false;
   }
+}
+
+// Abort flag of one agent: while set, every wait and queue-slot reservation on it
+// returns at once with an error (Sampler::stop() sets it so a sampler thread
+// blocked on a wedged CP exits; start() clears it).  Any thread.
+int kgs_pmc_abort(int handle, int on) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  g_agents[static_cast<size_t>(handle)]->abort.store(on ? 1 : 0);
+  return 0;
+}
+
+// Circuit-breaker reset for a wedged command processor: forget the session and
+// destroy the agent's READ queue (packets still on it never complete); the next
+// kgs_pmc_open creates a fresh queue and re-STARTs.  The buffers, signals and
+// pipelined READ slots are kept (signals are re-armed before every use).  Call
+// only from the handle's thread, after kgs_pmc_close.
+int kgs_pmc_reset(int handle) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  a->started = false;
+  a->inflight = -1;
+  if (a->queue) {
+    hsa_queue_destroy(a->queue);
+    a->queue = nullptr;
+  }
+  a->resets.fetch_add(1, std::memory_order_relaxed);
+  return 0;
 }
 
 }  // extern "C"

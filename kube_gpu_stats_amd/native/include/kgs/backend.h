@@ -107,6 +107,10 @@ class Backend {
   // re-initialise the management library.  0 when the device reads again;
   // the sampler then drops its accumulator baseline (counters restart).
   virtual int recover(int dev) { return -1; }
+  // Mock provider only (bench.py --mock phase X, tests): account a peer copy of
+  // `bytes` from device src to device dst on the xGMI link between them, as the
+  // PMFW per-link accumulators would.  -1 where unsupported.
+  virtual int inject_xgmi(int src, int dst, uint64_t bytes) { return -1; }
 };
 
 // Mock provider configuration (tests, plumbing benchmark).
@@ -135,6 +139,13 @@ struct MockConfig {
                                 // once recover() ran (models a GPU reset that needs a reopen)
   uint64_t energy_wrap_at = 0;  // if >0 the energy accumulator wraps at this value
   uint64_t ecc_correctable_per_s = 0;  // injected correctable ECC error rate
+  // Per-process load: process k of every device holds proc_cu_share[k] of its CUs
+  // (empty: 1 + dev % 2 processes at half the CUs each).  Two tenants sharing one
+  // GPU with shares {0.6, 0.0} is the shared-GPU billing test.
+  std::vector<double> proc_cu_share;
+  // Background xGMI traffic on every link, following the util curve (1 GB/s per
+  // link at 100 %); off, only inject_xgmi() moves the link accumulators.
+  bool xgmi_bg = true;
   uint64_t seed = 1;
   std::string hostname_seed;    // reserved
 };

@@ -26,7 +26,7 @@ struct Owner {
   std::string pod, ns, container;
   // The GPU's busy integrals when this owner was first seen on it: the per-pod
   // counters (container_gpu_busy_seconds_total, ...) count from 0 at allocation.
-  double base_busy_s = 0, base_mfma_s = 0, base_active_s = 0, base_energy_j = 0;
+  double base_busy_s = 0, base_mfma_s = 0, base_active_s = 0, base_energy_j = 0, base_cu_s = 0;
   bool same(const Owner& o) const { return pod == o.pod && ns == o.ns && container == o.container; }
 };
 struct PidOwner {
@@ -45,6 +45,7 @@ struct ExporterConfig {
   bool pmc_pipeline = true;         // overlap counter READs with the tick sleep (aqlprofile reader)
   std::string pmc_set = "base";     // "base" (GRBM + MFMA busy) | "full" (+ TA busy: 10x the register reads)
   int pmc_lean = 2;                 // READ packet: 0 as aqlprofile builds it .. 2 no flushes/invalidations (default)
+  int pmc_timeout_ms = 250;         // bound of every wait on the command processor (fault boundary)
   std::string listen_addr = "0.0.0.0";
   int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
   std::string node_name;
@@ -156,12 +157,15 @@ class Exporter {
   void pause_sampling();
   void resume_sampling();
   bool sampling() const;
-  // Hand the hardware counters to another profiler (false: every sampler STOPs
-  // its counting session and skips the PMC tier) or take them back (true).
-  void set_pmc_enabled(bool on);
+  // Hand the hardware counters to another profiler (false: the device's sampler
+  // STOPs its counting session and skips the PMC tier) or take them back (true);
+  // dev < 0 = every device.  Each device's own thread acts, so a hung GPU does
+  // not delay the others.
+  void set_pmc_enabled(bool on, int dev = -1);
   bool pmc_enabled() const;
   // Sampler tick rate (benchmarks switch tiers in place; integrals continue).
-  void set_sample_rate(double hz);
+  // false if hz is outside (0, kMaxHz].
+  bool set_sample_rate(double hz);
   double sample_rate() const;
 
   // self metrics

@@ -1,17 +1,22 @@
 // Hardware performance-counter sources for the high-rate tier (BASELINE.json
 // config 4: MFMA-busy + memory-pipe busy at 100 Hz and beyond).
 //
-// The real source is the rocprofiler-sdk *device counting service* driven from
-// our own HSA client (native/counters/pmc_rocprofiler.cpp, built as a separate
-// shared object `libkgs_pmc.so` and dlopen'd only when counters are enabled, so
-// the exporter never pulls HSA into a process that does not want it).  Reads
-// are agent-wide: every wave on the GPU is counted regardless of which process
-// launched it, and no kernel is dispatched by the reader.
+// The product source is the direct command-processor reader
+// (native/counters/pmc_aqlprofile.cpp → libkgs_pmc_aql.so): one private AQL queue
+// per GPU carrying aqlprofile-built PM4 START / READ packets, no profiler
+// framework in between.  It is a separate shared object, dlopen'd only when
+// counters are enabled, so the exporter never pulls HSA into a process that does
+// not want it.  Reads are agent-wide: every wave on the GPU is counted whichever
+// process launched it, and the reader dispatches no kernel.
+// (native/counters/pmc_rocprofiler.cpp, the rocprofiler-sdk device-counting
+// reader with the same C ABI, is kept for tests and cross-checks only: its HSA
+// event thread burns a core, profiles/r1/pmc_helper_thread.md.)
 //
-// Counter set — chosen by measurement on MI355X / ROCm 7.2 (profiles/pmc_probe.md):
-// under device counting GRBM, SQ_VALU_MFMA_BUSY_CYCLES, TA and TD count; the
-// other SQ counters and every TCC counter read (near) zero, so HBM bandwidth
-// comes from the PMFW UMC-activity accumulators instead.  GRBM has 2 slots.
+// Counter set — chosen by measurement on MI355X / ROCm 7.2 (profiles/aql_probe.md,
+// profiles/pmc_probe.md): device-wide, GRBM, SQ_VALU_MFMA_BUSY_CYCLES, TA and TD
+// count; the other SQ counters and every TCC counter read (near) zero, so HBM
+// bandwidth comes from the PMFW UMC-activity accumulators instead.  GRBM has 2
+// slots.
 #pragma once
 
 #include <cstdint>
@@ -70,7 +75,11 @@ uint32_t pmc_set_mask(const std::string& name);
 struct PmcRates {
   bool have_vmem = false;        // TA counter in the set
   double gpu_active_pct = 0;     // 100 * ΔSPI_BUSY / ΔGRBM_COUNT (READ-immune)
-  double mfma_util_pct = 0;      // 100 * ΔMFMA_BUSY / (ΔSPI_BUSY * SIMD_NUM)  (rocprofv3 MfmaUtil, per active cycle)
+  // 100 * ΔMFMA_BUSY / (ΔSPI_BUSY * SIMD_NUM): MFMA share of the SIMD cycles while a
+  // shader engine had waves.  Not rocprofv3's MfmaUtil (that divides by
+  // GRBM_GUI_ACTIVE, which counts our own READ packets as busy); the wall-clock
+  // figure is amdgpu_mfma_busy_seconds_total (Integrals::mfma_busy_seconds).
+  double mfma_util_pct = 0;
   double vmem_busy_pct = 0;      // 100 * ΔTA_BUSY(avg) / ΔSPI_BUSY
   double gpu_clock_mhz = 0;      // ΔGRBM_COUNT / Δt
   double dt_s = 0;
@@ -105,6 +114,17 @@ class CounterSource {
   // one — at an idle rate of 100 Hz a pipelined sample would be 10 ms old, which
   // doubles the time to notice that work started.  Sampler thread only.
   virtual void set_fresh(int dev, bool fresh) {}
+  // Fault boundary.  Every call above is bounded by the source's
+  // own deadline (a wedged command processor costs one timeout, never a hang).
+  // reset(): after release(), drop whatever the device's session ran on (the
+  // reader's AQL queue) so the next acquire() starts from scratch — the circuit
+  // breaker's recovery step.  Sampler thread only.  0 = ok.
+  virtual int reset(int dev) { return -1; }
+  // cancel(dev, true): calls blocked on the device (and new ones) return an error
+  // at once, until cancel(dev, false).  Any thread (Sampler::stop()).
+  virtual void cancel(int dev, bool on) {}
+  // Counters of the fault boundary (for kgs_pmc_* self-metrics): resets done.
+  virtual uint64_t resets(int dev) const { return 0; }
 };
 
 struct MockPmcConfig {
@@ -115,6 +135,16 @@ struct MockPmcConfig {
   int n_xcd = 8;                // per-XCD breakdown (0 = none)
   double xcd_skew = 0.0;        // XCD x is active (1 - skew·x) of XCD 0's cycles
   double freeze_after_s = 0.0;  // counts stop this long after each (re)START, as after a foreign STOP (0 = never)
+  // Fault injection for the counter tier's fault boundary (tests):
+  int slow_dev = -1;            // every sample on this device takes slow_s, then succeeds
+  double slow_s = 0.0;
+  int hang_dev = -1;            // after hang_after samples, samples on this device stop completing:
+  uint64_t hang_after = 0;
+  // ... each blocks hang_timeout_s and fails (a reader's deadline; cancel() ends it
+  // early); < 0: never returns at all, cancel() or not (a call stuck in the driver).
+  double hang_timeout_s = 0.25;
+  bool hang_heals_on_reset = false;  // reset() clears the hang (the recreated queue works)
+  int acquire_fail_dev = -1;    // acquire() fails on this device while its hang is active
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,
@@ -130,6 +160,7 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 // cache invalidations from the READ packet (native/counters/pmc_aqlprofile.cpp).
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
-                                                      bool pipelined, uint32_t mask, int lean, std::string& err);
+                                                      bool pipelined, uint32_t mask, int lean, std::string& err,
+                                                      int timeout_ms = 250);
 
 }  // namespace kgs

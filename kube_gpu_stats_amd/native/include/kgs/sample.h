@@ -90,11 +90,17 @@ struct GpuSample {
 
   uint64_t vram_used_bytes = 0;
   uint64_t vram_total_bytes = 0;
+
+  // Compute partitions (gpu_metrics.h restrict_to_xccs): the socket's energy
+  // accumulator is shared by energy_parts devices; each is billed its XCCs' share
+  // of the chip's GFX busy (Σ own / Σ all per-XCC busy accumulators).
+  uint32_t energy_parts = 1;
+  uint64_t xcc_acc_own = 0, xcc_acc_chip = 0;
 };
 static_assert(std::is_trivially_copyable<GpuSample>::value, "seqlock payload");
 
-// One drain of the hardware performance counters (rocprofiler-sdk device
-// counting service).  Values are cumulative since the counter source opened.
+// One drain of the hardware performance counters (the counter tier's reader,
+// pmc.h).  Values are cumulative since the counter source opened.
 struct PmcSample {
   uint64_t seq = 0;
   int64_t mono_ns = 0;

@@ -1,10 +1,22 @@
 // Per-GPU sampler threads (SURVEY.md §3.4 "HOT LOOP", §2.3 device fan-out).
 //
-// One std::thread per device, pinned to the CPUs of the GPU's NUMA node, wakes
-// on an absolute CLOCK_MONOTONIC deadline and every tick reads the PMFW table +
-// HBM occupancy (fast tier, capped at pmfw_hz) and, if enabled, drains the
-// hardware counters (PMC tier).  Those two are per-device files / queues: the
-// per-GPU thread never takes a node-wide lock.
+// Two std::threads per device, both pinned to the CPUs of the GPU's NUMA node and
+// woken on absolute CLOCK_MONOTONIC deadlines:
+//   * "kgs-pmfw<N>" reads the PMFW table + HBM occupancy (fast tier, at
+//     min(hz, pmfw_hz)) — power, temperature, clocks, GFX/UMC busy;
+//   * "kgs-gpu<N>" drains the hardware counters every tick (PMC tier, at hz).
+// They share nothing but the device's publication slots, so a counter READ that
+// blocks on a wedged command processor never silences the same GPU's power /
+// temperature / utilisation, and the ≈110 µs PMFW pread never makes an 8 kHz
+// counter tick overrun.  Neither takes a node-wide lock.
+//
+// Fault boundary of the counter tier: every CounterSource call is bounded by the
+// source's deadline; after pmc_breaker_k consecutive failures the breaker opens
+// (kgs_pmc_failed = 1): the session is released, and after pmc_retry_s (doubling
+// to pmc_retry_max_s) the source is reset (fresh AQL queue) and re-acquired.
+// stop() raises the source's cancel flag, waits at most stop_timeout_s for every
+// thread, and abandons (detaches) any thread still stuck in a call — a DaemonSet
+// pod then still exits on SIGTERM during the GPU hang it is reporting.
 //
 // The management-library tiers — per-process list (mid tier, every proc_every
 // ticks' worth of time), xGMI link table + RAS health (slow tier, every
@@ -20,10 +32,12 @@
 
 #include <atomic>
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "kgs/backend.h"
@@ -67,7 +81,16 @@ struct SamplerConfig {
   double pmc_idle_hz = 100.0;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
+  // Counter-tier circuit breaker: consecutive failed drains that open it, and the
+  // retry backoff (seconds, doubling per failed retry up to the max).
+  int pmc_breaker_k = 3;
+  double pmc_retry_s = 1.0, pmc_retry_max_s = 60.0;
+  // stop() waits this long for the sampler threads, then abandons the stuck ones.
+  double stop_timeout_s = 1.0;
 };
+
+constexpr double kMaxHz = 100000.0;     // tick-rate ceiling accepted at run time (set_hz)
+constexpr double kMinIdleHz = 0.01;     // pmc_idle_hz: 0 (off) or at least this
 
 constexpr size_t kRing = 1024;          // ≥10 s of history at 100 Hz
 // Counter samples decimated to one per kPmcSlowNs feed the window gauges, so a
@@ -76,6 +99,9 @@ constexpr size_t kPmcSlowRing = 2048;
 constexpr size_t kPmcRing = 8192;       // raw counter stream: ≥1 s at 8 kHz (/counters)
 constexpr int64_t kPmcSlowNs = 5000000;  // 5 ms → ≥10 s of history
 constexpr int kReadHistBuckets = 12;    // backend read latency histogram
+// A tick late by at most this many periods keeps the absolute schedule (the missed
+// ticks run back to back); later than that the schedule re-anchors.
+constexpr int64_t kCatchUpPeriods = 4;
 constexpr int64_t kPmcStallNs = 500000000;  // GRBM_COUNT without a plausible clock this long = stalled
 constexpr double kPlausibleMhzLo = 100.0, kPlausibleMhzHi = 4000.0;
 // Adaptive READ rate: an interval whose SPI-busy share is below this is quiet.
@@ -90,7 +116,8 @@ extern const double kReadHistBoundsUs[kReadHistBuckets];
 struct DeviceState {
   Seqlock<GpuSample> latest;
   SampleRing<GpuSample, kRing> ring;
-  Seqlock<Integrals> integ;
+  Seqlock<Integrals> integ;      // PMFW-tier fields (writer: kgs-pmfw<N>)
+  Seqlock<Integrals> pmc_integ;  // counter-tier fields (writer: kgs-gpu<N>)
   Seqlock<PmcSample> pmc_latest;
   SampleRing<PmcSample, kPmcRing> pmc_ring;         // every counter drain
   SampleRing<PmcSample, kPmcSlowRing> pmc_slow_ring;  // ≥ kPmcSlowNs apart (window gauges)
@@ -99,6 +126,9 @@ struct DeviceState {
   std::shared_ptr<const std::vector<ProcInfo>> procs;
   std::shared_ptr<const std::vector<LinkInfo>> links;
   std::shared_ptr<const HealthInfo> health;
+  // Per-pod CU-occupancy seconds on this GPU ("namespace/pod" → ∫ Σ share dt of the
+  // pod's processes), processes that exited included (slow tier).
+  std::shared_ptr<const std::map<std::string, double>> pod_cu;
   int64_t procs_mono_ns = 0;
 
   std::atomic<int> up{0};
@@ -117,7 +147,15 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
   std::atomic<int> pmc_quiet{0};            // last READ interval had no wave: READs at pmc_idle_hz
   std::atomic<uint64_t> pmc_quiet_skips{0};  // ticks that skipped their READ while quiet
+  // Counter-tier fault boundary (sampler.h header comment).
+  std::atomic<int> pmc_failed{0};            // breaker open: no READs until a retry succeeds
+  std::atomic<uint64_t> pmc_breaker_trips{0};
+  std::atomic<uint64_t> pmc_retries{0};      // reset + acquire attempts while the breaker is open
+  std::atomic<int> thread_hung{0};           // a sampler thread of this device was abandoned by stop()
   PmcSample pmc_base;  // totals carried over hand-overs (sampler thread only; survives pause/resume)
+  int pmc_fail_streak = 0;                   // counter thread only (survive pause/resume)
+  int64_t pmc_retry_at_ns = 0;
+  double pmc_backoff_s = 0;
   // Last distinct PMFW sample (sampler thread only).  Kept across pause/resume:
   // the firmware accumulators keep counting while the thread is stopped, so the
   // first sample after a resume integrates the paused interval exactly.
@@ -138,6 +176,23 @@ struct DeviceState {
   std::shared_ptr<const HealthInfo> get_health() const {
     std::lock_guard<std::mutex> g(slow_mu);
     return health;
+  }
+  std::shared_ptr<const std::map<std::string, double>> get_pod_cu() const {
+    std::lock_guard<std::mutex> g(slow_mu);
+    return pod_cu;
+  }
+  // Both tiers' integrals in one view (overruns: both threads').
+  Integrals integrals() const {
+    Integrals a, b;
+    integ.load(a);
+    pmc_integ.load(b);
+    a.overruns += b.overruns;
+    a.pmc_samples = b.pmc_samples;
+    a.pmc_errors = b.pmc_errors;
+    a.pmc_read_seconds = b.pmc_read_seconds;
+    a.mfma_busy_seconds = b.mfma_busy_seconds;
+    a.active_seconds = b.active_seconds;
+    return a;
   }
 };
 
@@ -160,20 +215,40 @@ class Sampler {
   bool window_busy(int dev, double window_s, double& gfx_pct, double& umc_pct, int& n) const;
   // Counter-derived rates over the trailing window.
   bool window_pmc(int dev, double window_s, PmcRates& out) const;
-  // Ask every sampled device's thread to hand its counters to another profiler
-  // (false) or to take them back (true).  Takes effect within one tick.
-  void set_pmc_wanted(bool on);
+  // Ask a device's counter thread (dev < 0: every sampled device's) to hand its
+  // counters to another profiler (false) or to take them back (true).  Takes
+  // effect within one tick of that device's own thread: a hung device never
+  // delays the others.
+  void set_pmc_wanted(bool on, int dev = -1);
   // Change the tick rate (stops and restarts the threads; integrals continue).
-  void set_hz(double hz);
-  // Quiet-GPU counter READ rate (SamplerConfig::pmc_idle_hz), in place.
-  void set_pmc_idle_hz(double hz) { pmc_idle_hz_.store(hz < 0 ? 0 : hz, std::memory_order_relaxed); }
+  // false (nothing changed) unless 0 < hz <= kMaxHz.
+  bool set_hz(double hz);
+  double hz() const { return hz_.load(std::memory_order_relaxed); }
+  // Quiet-GPU counter READ rate (SamplerConfig::pmc_idle_hz), in place; false
+  // (unchanged) unless hz == 0 or kMinIdleHz <= hz <= kMaxHz.
+  bool set_pmc_idle_hz(double hz);
   double pmc_idle_hz() const { return pmc_idle_hz_.load(std::memory_order_relaxed); }
   // Node-wide slow thread: passes completed and whether it is running.
   uint64_t slow_passes() const { return slow_passes_.load(); }
+  // Threads stop() gave up on (stuck in a device call); they are detached and
+  // exit on their own if the call ever returns.  The owner must then keep the
+  // backend, counter source and this sampler alive (Exporter leaks them).
+  uint64_t abandoned_threads() const { return abandoned_total_.load(); }
+  // (GPU, PID) → "namespace/pod" of the processes' pods, for the per-pod CU
+  // integrals (slow tier; the exporter pushes it with its PID → pod table).
+  void set_pid_pods(std::shared_ptr<const std::unordered_map<uint64_t, std::string>> m);
+  // ∫ CU-occupancy share dt of the pod `ns_pod` ("namespace/pod") on `dev`, 0 if none.
+  double pod_cu_seconds(int dev, const std::string& ns_pod) const;
 
  private:
-  void run(int dev);
-  void run_slow();
+  struct Worker;
+  void start_locked();
+  void stop_locked();
+  void spawn(int dev, int kind);
+  void run_pmfw(Worker& w);
+  void run_pmc(Worker& w);
+  void run_slow(Worker& w);
+  void pin(int dev, const char* fmt);
   void integrate(int dev, const GpuSample* prev, GpuSample& cur, Integrals& I);
 
   Backend* be_;
@@ -181,10 +256,16 @@ class Sampler {
   SamplerConfig cfg_;
   std::vector<std::unique_ptr<DeviceState>> states_;
   std::vector<int> dev_ids_;
-  std::vector<std::thread> threads_;
-  std::thread slow_thread_;
+  std::mutex life_mu_;  // start / stop / set_hz (HTTP control thread vs Python pause / resume)
+  std::vector<std::shared_ptr<Worker>> workers_;    // running threads (guarded by life_mu_)
+  std::vector<std::shared_ptr<Worker>> abandoned_;  // detached, maybe still stuck (guarded by life_mu_)
+  std::atomic<uint64_t> abandoned_total_{0};
+  std::atomic<double> hz_{10.0};
   std::atomic<uint64_t> slow_passes_{0};
   std::atomic<double> pmc_idle_hz_{0.0};
+  mutable std::mutex pid_pods_mu_;
+  std::shared_ptr<const std::unordered_map<uint64_t, std::string>> pid_pods_;
+  std::vector<std::map<std::string, double>> pod_cu_;  // slow thread only
   // Per-device process CU-occupancy integrals (slow thread only; survive pause/resume).
   std::vector<std::vector<std::pair<uint32_t, double>>> cu_seconds_;
   std::vector<int64_t> last_proc_ns_;

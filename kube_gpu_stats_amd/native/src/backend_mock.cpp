@@ -13,6 +13,8 @@
 #include <thread>
 
 #include <algorithm>
+#include <array>
+#include <memory>
 
 #include "kgs/backend.h"
 #include "kgs/gpu_metrics.h"
@@ -103,6 +105,20 @@ class MockBackend final : public Backend {
       }
     }
     rng_mu_ = std::vector<std::mutex>(infos_.size());
+    for (int g = 0; g < cfg_.n_gpus; ++g) inj_.push_back(std::make_unique<LinkInj>());
+  }
+
+  // Port l (1 .. n_gpus-1) of GPU g faces the l-th other GPU in index order
+  // (port 0 is the disabled self port, as on MI355X); read_links reports the same.
+  int link_of(int g, int peer) const { return peer < g ? peer + 1 : peer; }
+
+  int inject_xgmi(int src, int dst, uint64_t bytes) override {
+    const int gs = src / parts_, gd = dst / parts_;
+    if (src < 0 || dst < 0 || src >= device_count() || dst >= device_count() || gs == gd) return -1;
+    const uint64_t kb = bytes / 1024;
+    inj_[static_cast<size_t>(gs)]->wr[static_cast<size_t>(link_of(gs, gd))].fetch_add(kb);
+    inj_[static_cast<size_t>(gd)]->rd[static_cast<size_t>(link_of(gd, gs))].fetch_add(kb);
+    return 0;
   }
 
   std::string name() const override { return "mock"; }
@@ -173,8 +189,9 @@ class MockBackend final : public Backend {
     s.temp_mem_c = static_cast<float>(35 + 0.2 * u);
     s.temp_vrsoc_c = static_cast<float>(38 + 0.1 * u);
     s.power_w = static_cast<float>(200 + 8 * u);
-    // energy: ∫ (200 + 8u) dt in 2^-16 J units
-    double ej = 200 * tf + 8 * util_integral(d, tf);
+    // energy: ∫ (200 + 8u) dt in 2^-16 J units — of the socket: partitions of one
+    // GPU read the same accumulator, as on hardware
+    double ej = 200 * tf + 8 * ui;
     uint64_t e = static_cast<uint64_t>(ej * 65536.0);
     if (cfg_.energy_wrap_at) e %= cfg_.energy_wrap_at;
     s.energy_acc = e;
@@ -184,9 +201,10 @@ class MockBackend final : public Backend {
     for (int l = 0; l < kMaxXgmi; ++l) {
       const bool up = l >= 1 && l < cfg_.n_gpus;
       // 1 GB/s per link at 100 % utilisation, link 0 is the unused self-port.
-      const uint64_t kb = up ? static_cast<uint64_t>(util_integral(d, tf) * 1e4) : 0;
-      s.xgmi_read_kb[l] = kb;
-      s.xgmi_write_kb[l] = kb / 2;
+      const uint64_t kb = up && cfg_.xgmi_bg ? static_cast<uint64_t>(util_integral(d, tf) * 1e4) : 0;
+      const LinkInj& in = *inj_[static_cast<size_t>(g)];
+      s.xgmi_read_kb[l] = kb + in.rd[static_cast<size_t>(l)].load();
+      s.xgmi_write_kb[l] = kb / 2 + in.wr[static_cast<size_t>(l)].load();
       s.xgmi_link_up[l] = up ? 1 : 0xFFFF;
     }
     s.xgmi_link_speed_gbps = 38;
@@ -222,13 +240,17 @@ class MockBackend final : public Backend {
     out.clear();
     const double t = (mono_ns() - t0_) * 1e-9;
     if (gone(d, t)) return -2;
-    for (int k = 0; k < 1 + (d % 2); ++k) {
+    const bool shares = !cfg_.proc_cu_share.empty();
+    const int n = shares ? static_cast<int>(cfg_.proc_cu_share.size()) : 1 + (d % 2);
+    for (int k = 0; k < n; ++k) {
       ProcInfo p;
       p.pid = static_cast<uint32_t>(100000 + d * 10 + k);
       p.name = "python3";
       p.vram_bytes = (1ull << 30) * static_cast<uint64_t>(k + 1);
-      p.gfx_ns = static_cast<uint64_t>(util_integral(d, t) * 1e7 / (1 + (d % 2)));
-      p.cu_occupancy = 128;
+      p.gfx_ns = static_cast<uint64_t>(util_integral(d, t) * 1e7 / n);
+      p.cu_occupancy = shares ? static_cast<uint32_t>(std::lround(cfg_.proc_cu_share[static_cast<size_t>(k)] *
+                                                                  infos_[static_cast<size_t>(d)].num_cu))
+                              : 128;
       out.push_back(p);
     }
     return 0;
@@ -249,8 +271,9 @@ class MockBackend final : public Backend {
       li.link_type = 2;
       li.bit_rate_gbps = 38;
       li.max_bw_gbps = 608;
-      li.read_kb = static_cast<uint64_t>(util_integral(d, t) * 1e4);
-      li.write_kb = li.read_kb / 2;
+      const uint64_t bg = cfg_.xgmi_bg ? static_cast<uint64_t>(util_integral(d, t) * 1e4) : 0;
+      li.read_kb = bg + inj_[static_cast<size_t>(g)]->rd[static_cast<size_t>(li.link)].load();
+      li.write_kb = bg / 2 + inj_[static_cast<size_t>(g)]->wr[static_cast<size_t>(li.link)].load();
       out.push_back(li);
     }
     return 0;
@@ -294,9 +317,14 @@ class MockBackend final : public Backend {
     return (x >> 11) * (1.0 / 9007199254740992.0);
   }
 
+  struct LinkInj {  // injected peer-copy KB per port of one physical GPU
+    std::array<std::atomic<uint64_t>, kMaxXgmi> rd{}, wr{};
+  };
+
   MockConfig cfg_;
   int64_t t0_;
   int parts_;              // devices per physical GPU (compute partitions)
+  std::vector<std::unique_ptr<LinkInj>> inj_;
   std::mutex smi_mu_;      // the management library's process-wide lock (latency model)
   std::atomic<int64_t> reset_ns_{0};
   std::vector<DeviceInfo> infos_;

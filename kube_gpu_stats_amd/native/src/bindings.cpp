@@ -43,6 +43,8 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.link_latency_s = get<double>(m, "link_latency_s", c.mock.link_latency_s);
     c.mock.health_latency_s = get<double>(m, "health_latency_s", c.mock.health_latency_s);
     c.mock.metrics_latency_s = get<double>(m, "metrics_latency_s", c.mock.metrics_latency_s);
+    c.mock.proc_cu_share = get<std::vector<double>>(m, "proc_cu_share", c.mock.proc_cu_share);
+    c.mock.xgmi_bg = get<bool>(m, "xgmi_bg", c.mock.xgmi_bg);
   }
   if (d.contains("mock_pmc")) {
     py::dict m = d["mock_pmc"].cast<py::dict>();
@@ -52,6 +54,13 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.n_xcd = get<int>(m, "n_xcd", c.mock_pmc.n_xcd);
     c.mock_pmc.xcd_skew = get<double>(m, "xcd_skew", c.mock_pmc.xcd_skew);
     c.mock_pmc.freeze_after_s = get<double>(m, "freeze_after_s", c.mock_pmc.freeze_after_s);
+    c.mock_pmc.slow_dev = get<int>(m, "slow_dev", c.mock_pmc.slow_dev);
+    c.mock_pmc.slow_s = get<double>(m, "slow_s", c.mock_pmc.slow_s);
+    c.mock_pmc.hang_dev = get<int>(m, "hang_dev", c.mock_pmc.hang_dev);
+    c.mock_pmc.hang_after = get<uint64_t>(m, "hang_after", c.mock_pmc.hang_after);
+    c.mock_pmc.hang_timeout_s = get<double>(m, "hang_timeout_s", c.mock_pmc.hang_timeout_s);
+    c.mock_pmc.hang_heals_on_reset = get<bool>(m, "hang_heals_on_reset", c.mock_pmc.hang_heals_on_reset);
+    c.mock_pmc.acquire_fail_dev = get<int>(m, "acquire_fail_dev", c.mock_pmc.acquire_fail_dev);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -65,12 +74,17 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmc_refresh_s = get<double>(d, "pmc_refresh_s", c.sampler.pmc_refresh_s);
   c.sampler.pmc_idle_hz = get<double>(d, "pmc_idle_hz", c.sampler.pmc_idle_hz);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
+  c.sampler.pmc_breaker_k = get<int>(d, "pmc_breaker_k", c.sampler.pmc_breaker_k);
+  c.sampler.pmc_retry_s = get<double>(d, "pmc_retry_s", c.sampler.pmc_retry_s);
+  c.sampler.pmc_retry_max_s = get<double>(d, "pmc_retry_max_s", c.sampler.pmc_retry_max_s);
+  c.sampler.stop_timeout_s = get<double>(d, "stop_timeout_s", c.sampler.stop_timeout_s);
   c.bdfs = get<std::vector<std::string>>(d, "bdfs", c.bdfs);
   c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);
   c.pmc_lib = get<std::string>(d, "pmc_lib", c.pmc_lib);
   c.pmc_pipeline = get<bool>(d, "pmc_pipeline", c.pmc_pipeline);
   c.pmc_set = get<std::string>(d, "pmc_set", c.pmc_set);
   c.pmc_lean = get<int>(d, "pmc_lean", c.pmc_lean);
+  c.pmc_timeout_ms = get<int>(d, "pmc_timeout_ms", c.pmc_timeout_ms);
   c.hbm_bytes_per_s_at_full_umc = get<double>(d, "hbm_bytes_per_s_at_full_umc", c.hbm_bytes_per_s_at_full_umc);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);
@@ -211,8 +225,7 @@ class PyExporter {
   }
   py::dict integrals(int d) const {
     check(d);
-    Integrals I;
-    ex_.sampler()->state(d).integ.load(I);
+    const Integrals I = ex_.sampler()->state(d).integrals();
     py::dict o;
     o["gfx_busy_seconds"] = I.gfx_busy_seconds;
     o["umc_busy_seconds"] = I.umc_busy_seconds;
@@ -243,6 +256,13 @@ class PyExporter {
     o["pmc_quiet_skips"] = st.pmc_quiet_skips.load();
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
+    o["pmc_on"] = st.pmc_on.load();
+    o["pmc_failed"] = st.pmc_failed.load();
+    o["pmc_breaker_trips"] = st.pmc_breaker_trips.load();
+    o["pmc_retries"] = st.pmc_retries.load();
+    o["pmc_releases"] = st.pmc_releases.load();
+    o["thread_hung"] = st.thread_hung.load();
+    o["pmc_resets"] = ex_.counters() ? ex_.counters()->resets(d) : 0;
     return o;
   }
   py::object pmc(int d) const {
@@ -376,11 +396,20 @@ class PyExporter {
     py::gil_scoped_release r;
     ex_.resume_sampling();
   }
-  void set_pmc_enabled(bool on) { ex_.set_pmc_enabled(on); }
-  void set_sample_rate(double hz) {
-    py::gil_scoped_release r;
-    ex_.set_sample_rate(hz);
+  void set_pmc_enabled(bool on, int gpu) {
+    if (gpu >= 0) check(gpu);
+    ex_.set_pmc_enabled(on, gpu);
   }
+  void set_sample_rate(double hz) {
+    bool ok;
+    {
+      py::gil_scoped_release r;
+      ok = ex_.set_sample_rate(hz);
+    }
+    if (!ok) throw py::value_error("hz must be within (0, 100000]");
+  }
+  uint64_t abandoned_threads() const { return ex_.sampler()->abandoned_threads(); }
+  int inject_xgmi(int src, int dst, uint64_t bytes) { return ex_.backend()->inject_xgmi(src, dst, bytes); }
   double sample_rate() const { return ex_.sample_rate(); }
   uint64_t slow_passes() const { return ex_.sampler()->slow_passes(); }
   bool pmc_enabled() const { return ex_.pmc_enabled(); }
@@ -435,8 +464,12 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("pause", &PyExporter::pause)
       .def("resume", &PyExporter::resume)
       .def_property_readonly("sampling", &PyExporter::sampling)
-      .def("set_pmc_enabled", &PyExporter::set_pmc_enabled, py::arg("on"),
-           "Hand the hardware counters to another profiler (False) or take them back (True)")
+      .def("set_pmc_enabled", &PyExporter::set_pmc_enabled, py::arg("on"), py::arg("gpu") = -1,
+           "Hand the hardware counters to another profiler (False) or take them back (True); gpu=-1: every GPU")
+      .def_property_readonly("abandoned_threads", &PyExporter::abandoned_threads,
+                             "sampler threads stop() gave up on (stuck in a device call)")
+      .def("inject_xgmi", &PyExporter::inject_xgmi, py::arg("src"), py::arg("dst"), py::arg("bytes"),
+           "mock backend only: account a peer copy of `bytes` from GPU src to GPU dst on the link between them")
       .def_property_readonly("pmc_enabled", &PyExporter::pmc_enabled)
       .def("set_sample_rate", &PyExporter::set_sample_rate, py::arg("hz"),
            "Change the sampler tick rate in place (threads restart; integrals continue)")
@@ -444,7 +477,8 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def_property(
           "pmc_idle_hz", [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_idle_hz() : 0.0; },
           [](PyExporter& e, double hz) {
-            if (e.sampler()) e.sampler()->set_pmc_idle_hz(hz);
+            if (e.sampler() && !e.sampler()->set_pmc_idle_hz(hz))
+              throw py::value_error("pmc_idle_hz must be 0 or within [0.01, 100000]");
           },
           "Counter READ rate while the GPU has no wave (adaptive; 0 = every tick)")
       .def_property_readonly("slow_passes", &PyExporter::slow_passes);

@@ -111,7 +111,16 @@ Exporter::Exporter(ExporterConfig cfg) : cfg_(std::move(cfg)), filter_(cfg_.metr
   }
 }
 
-Exporter::~Exporter() { stop(); }
+Exporter::~Exporter() {
+  stop();
+  // A sampler thread stuck in a device call (abandoned by stop()) still points
+  // into the sampler, the backend and the counter source: keep them alive.
+  if (sampler_ && sampler_->abandoned_threads() > 0) {
+    (void)sampler_.release();
+    (void)pmc_.release();
+    (void)be_.release();
+  }
+}
 
 bool Exporter::init() {
   if (cfg_.sm_util_source != "pmfw" && cfg_.sm_util_source != "counters") {
@@ -151,7 +160,8 @@ bool Exporter::init() {
     mp.mask = pmc_mask;
     pmc_ = make_mock_counter_source(*be_, cfg_.mock, mp);
   } else if (cfg_.pmc_source == "rocprofiler" || cfg_.pmc_source == "aqlprofile") {
-    pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, cfg_.pmc_pipeline, pmc_mask, cfg_.pmc_lean, pmc_err_);
+    pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, cfg_.pmc_pipeline, pmc_mask, cfg_.pmc_lean,
+                                  pmc_err_, cfg_.pmc_timeout_ms);
   } else if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
     err_ = "unknown pmc_source '" + cfg_.pmc_source + "'";
     return false;
@@ -204,20 +214,18 @@ void Exporter::resume_sampling() {
   if (sampler_) sampler_->start();
 }
 bool Exporter::sampling() const { return sampler_ && sampler_->running(); }
-void Exporter::set_pmc_enabled(bool on) {
-  pmc_wanted_.store(on);
-  if (sampler_) sampler_->set_pmc_wanted(on);
+void Exporter::set_pmc_enabled(bool on, int dev) {
+  if (dev < 0) pmc_wanted_.store(on);
+  if (sampler_) sampler_->set_pmc_wanted(on, dev);
 }
 bool Exporter::pmc_enabled() const { return pmc_wanted_.load(); }
 
-void Exporter::set_sample_rate(double hz) {
-  if (sampler_) sampler_->set_hz(hz);
-}
-double Exporter::sample_rate() const { return sampler_ ? sampler_->config().hz : 0.0; }
+bool Exporter::set_sample_rate(double hz) { return sampler_ && sampler_->set_hz(hz); }
+double Exporter::sample_rate() const { return sampler_ ? sampler_->hz() : 0.0; }
 
 void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
   Integrals I;
-  if (sampler_ && dev >= 0 && dev < sampler_->device_count()) sampler_->state(dev).integ.load(I);
+  if (sampler_ && dev >= 0 && dev < sampler_->device_count()) I = sampler_->state(dev).integrals();
   std::lock_guard<std::mutex> g(mu_);
   auto m = owners_ ? std::make_shared<std::map<int, std::vector<Owner>>>(*owners_)
                    : std::make_shared<std::map<int, std::vector<Owner>>>();
@@ -232,6 +240,7 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
     x.base_mfma_s = kept ? kept->base_mfma_s : I.mfma_busy_seconds;
     x.base_active_s = kept ? kept->base_active_s : I.active_seconds;
     x.base_energy_j = kept ? kept->base_energy_j : I.energy_joules;
+    x.base_cu_s = kept ? kept->base_cu_s : (sampler_ ? sampler_->pod_cu_seconds(dev, x.ns + "/" + x.pod) : 0.0);
   }
   if (o.empty()) m->erase(dev);
   else (*m)[dev] = std::move(o);
@@ -239,6 +248,12 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
 }
 
 void Exporter::set_pid_owners(std::unordered_map<uint64_t, PidOwner> m) {
+  if (sampler_) {  // (GPU, PID) → "namespace/pod": the slow tier's per-pod CU integrals
+    auto pods = std::make_shared<std::unordered_map<uint64_t, std::string>>();
+    for (const auto& [k, po] : m)
+      if (!po.pod.empty()) (*pods)[k] = po.ns + "/" + po.pod;
+    sampler_->set_pid_pods(std::move(pods));
+  }
   auto p = std::make_shared<const std::unordered_map<uint64_t, PidOwner>>(std::move(m));
   std::lock_guard<std::mutex> g(mu_);
   pid_owners_ = std::move(p);

@@ -173,6 +173,12 @@ int parse_gpu_metrics_v1_8(const uint8_t* b, size_t len, GpuSample& s) {
 
 void restrict_to_xccs(GpuSample& s, uint32_t first, uint32_t count) {
   if (count == 0 || first + count > s.num_xcc || (first == 0 && count == s.num_xcc)) return;
+  s.energy_parts = s.num_xcc / count;
+  s.xcc_acc_own = s.xcc_acc_chip = 0;
+  for (uint32_t x = 0; x < s.num_xcc && x < static_cast<uint32_t>(kMaxXcc); ++x) {
+    s.xcc_acc_chip += s.gfx_busy_acc_xcc[x];
+    if (x >= first && x < first + count) s.xcc_acc_own += s.gfx_busy_acc_xcc[x];
+  }
   double inst = 0, acc = 0;
   for (uint32_t k = 0; k < count; ++k) {
     const uint32_t x = first + k;

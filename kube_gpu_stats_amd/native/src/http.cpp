@@ -325,24 +325,40 @@ void HttpServer::loop() {
           // namespace (`kubectl exec <pod> -- kgs pmc release`), never for scrapers.
           respond(c, 403, "Forbidden", "text/plain", "control endpoints are loopback-only\n");
         } else if (target == "/control/pmc/release" || target == "/control/pmc/acquire") {
-          ex_->set_pmc_enabled(target == "/control/pmc/acquire");
-          respond(c, 200, "OK", "application/json", ex_->pmc_enabled() ? "{\"pmc\":true}" : "{\"pmc\":false}");
+          // ?gpu=N: that device only (its own sampler thread acts; a hung GPU delays nobody).
+          const int gpu = query_int(query, "gpu", -1);
+          Sampler* s = ex_->sampler();
+          if (gpu >= 0 && (!s || gpu >= s->device_count())) {
+            respond(c, 400, "Bad Request", "text/plain", "gpu out of range\n");
+          } else {
+            const bool on = target == "/control/pmc/acquire";
+            ex_->set_pmc_enabled(on, gpu);
+            std::string j = gpu >= 0 ? "{\"gpu\":" + std::to_string(gpu) + ",\"pmc\":" + (on ? "true" : "false") + "}"
+                                     : std::string(ex_->pmc_enabled() ? "{\"pmc\":true}" : "{\"pmc\":false}");
+            respond(c, 200, "OK", "application/json", j);
+          }
         } else if (target == "/control/pmc/idle") {
-          // Quiet-GPU counter READ rate (--pmc-idle-hz); hz=0 = READ every tick (profiling mode).
+          // Quiet-GPU counter READ rate (--pmc-idle-hz); hz=0 = READ every tick (profiling
+          // mode); hz < 0 (or none) only reads the setting.  Out of range → 400.
           Sampler* s = ex_->sampler();
           const double hz = query_double(query, "hz", -1.0);
-          if (s && hz >= 0) s->set_pmc_idle_hz(hz);
-          respond(c, 200, "OK", "application/json",
-                  "{\"pmc_idle_hz\":" + std::to_string(s ? s->pmc_idle_hz() : 0.0) + "}");
+          if (s && hz >= 0 && !s->set_pmc_idle_hz(hz)) {
+            respond(c, 400, "Bad Request", "text/plain", "hz must be 0 or within [0.01, 100000]\n");
+          } else {
+            respond(c, 200, "OK", "application/json",
+                    "{\"pmc_idle_hz\":" + std::to_string(s ? s->pmc_idle_hz() : 0.0) + "}");
+          }
         } else if (ex_->config().control_http && (target == "/control/pause" || target == "/control/resume")) {
           if (target == "/control/pause") ex_->pause_sampling();
           else ex_->resume_sampling();
           respond(c, 200, "OK", "application/json", ex_->sampling() ? "{\"sampling\":true}" : "{\"sampling\":false}");
         } else if (ex_->config().control_http && target == "/control/rate") {
           // Benchmarks: switch the tick rate in place (one exporter serves every tier).
-          const double hz = query_double(query, "hz", 0);
-          if (hz > 0) ex_->set_sample_rate(hz);
-          respond(c, 200, "OK", "application/json", "{\"hz\":" + std::to_string(ex_->sample_rate()) + "}");
+          const double hz = query_double(query, "hz", -1.0);
+          if (hz != -1.0 && !ex_->set_sample_rate(hz))
+            respond(c, 400, "Bad Request", "text/plain", "hz must be within (0, 100000]\n");
+          else
+            respond(c, 200, "OK", "application/json", "{\"hz\":" + std::to_string(ex_->sample_rate()) + "}");
         } else if (target == "/healthz") {
           const bool ok = ex_->healthy();
           respond(c, ok ? 200 : 503, ok ? "OK" : "Service Unavailable", "text/plain", ok ? "ok\n" : "no device sampled\n");

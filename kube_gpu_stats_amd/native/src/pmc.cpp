@@ -1,12 +1,16 @@
 // Counter-source plumbing: counter catalogue, derived rates, the mock source and
-// the dlopen bridge to libkgs_pmc.so (rocprofiler-sdk device counting).
+// the dlopen bridge to the counter readers (libkgs_pmc_aql.so, the direct CP
+// reader; libkgs_pmc.so, rocprofiler-sdk device counting, tests only).
 #include "kgs/pmc.h"
 
 #include <dlfcn.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
+#include <thread>
 #include <ctime>
 #include <mutex>
 
@@ -80,15 +84,42 @@ namespace {
 class MockCounterSource final : public CounterSource {
  public:
   MockCounterSource(const MockConfig& b, const MockPmcConfig& c, int n_dev)
-      : b_(b), c_(c), t0_(mono_ns()), restart_(static_cast<size_t>(std::max(n_dev, 1)), 0) {}
+      : b_(b), c_(c), t0_(mono_ns()), restart_(static_cast<size_t>(std::max(n_dev, 1)), 0) {
+    for (int d = 0; d < std::max(n_dev, 1); ++d) fault_.push_back(std::make_unique<Fault>());
+  }
   std::string name() const override { return "mock"; }
   int release(int) override { return 0; }
   int acquire(int dev) override {  // like a re-START: the counts restart at 0
     if (dev < 0 || static_cast<size_t>(dev) >= restart_.size()) return -1;
+    if (dev == c_.acquire_fail_dev && hung(dev)) return -1;
     restart_[static_cast<size_t>(dev)] = mono_ns();
     return 0;
   }
+  int reset(int dev) override {
+    if (dev < 0 || static_cast<size_t>(dev) >= fault_.size()) return -1;
+    Fault& f = *fault_[static_cast<size_t>(dev)];
+    f.resets.fetch_add(1);
+    if (c_.hang_heals_on_reset && dev == c_.hang_dev) f.healed.store(1);
+    return 0;
+  }
+  void cancel(int dev, bool on) override {
+    if (dev < 0 || static_cast<size_t>(dev) >= fault_.size()) return;
+    fault_[static_cast<size_t>(dev)]->cancelled.store(on ? 1 : 0);
+  }
+  uint64_t resets(int dev) const override {
+    return dev >= 0 && static_cast<size_t>(dev) < fault_.size() ? fault_[static_cast<size_t>(dev)]->resets.load() : 0;
+  }
   int sample(int dev, PmcSample& s) override {
+    if (dev >= 0 && static_cast<size_t>(dev) < fault_.size()) {
+      Fault& f = *fault_[static_cast<size_t>(dev)];
+      if (dev == c_.slow_dev && c_.slow_s > 0 && wait_cancel(f, c_.slow_s)) return -3;
+      const uint64_t n = f.samples.fetch_add(1) + 1;
+      if (dev == c_.hang_dev && !f.healed.load() && n > c_.hang_after) {
+        if (c_.hang_timeout_s < 0)
+          for (;;) pause();  // stuck for good, cancel or not: only abandoning the thread helps
+        return wait_cancel(f, c_.hang_timeout_s) ? -3 : -2;  // aborted / deadline passed
+      }
+    }
     const int64_t now = mono_ns();
     const int64_t r = dev >= 0 && static_cast<size_t>(dev) < restart_.size() ? restart_[static_cast<size_t>(dev)] : 0;
     int64_t t = now;
@@ -138,10 +169,31 @@ class MockCounterSource final : public CounterSource {
     }
   }
 
+  struct Fault {
+    std::atomic<uint64_t> samples{0}, resets{0};
+    std::atomic<int> healed{0};
+    std::atomic<int> cancelled{0};
+  };
+  bool hung(int dev) const {
+    const Fault& f = *fault_[static_cast<size_t>(dev)];
+    return dev == c_.hang_dev && !f.healed.load() && f.samples.load() > c_.hang_after;
+  }
+  // Sleep up to `s` seconds in 1 ms steps (a condition variable's timed wait is
+  // not intercepted by GCC 11's TSAN); true if cancel() cut it short.
+  static bool wait_cancel(Fault& f, double s) {
+    const int64_t end = mono_ns() + static_cast<int64_t>(s * 1e9);
+    while (mono_ns() < end) {
+      if (f.cancelled.load()) return true;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    return f.cancelled.load() != 0;
+  }
+
   MockConfig b_;
   MockPmcConfig c_;
   int64_t t0_;
   std::vector<int64_t> restart_;  // per device: time of the last acquire (0 = never released)
+  std::vector<std::unique_ptr<Fault>> fault_;
 };
 
 // --- dlopen bridge -------------------------------------------------------
@@ -154,6 +206,8 @@ using pipelined_fn = int (*)(int, int, char*, int);
 using configure_fn = int (*)(const char*, int);
 using close_fn = void (*)(int);
 using info_fn = int (*)(int, char*, int);
+using abort_fn = int (*)(int, int);
+using reset_fn = int (*)(int);
 
 class DlCounterSource final : public CounterSource {
  public:
@@ -166,7 +220,7 @@ class DlCounterSource final : public CounterSource {
   }
 
   bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, bool pipelined,
-            uint32_t mask, int lean, std::string& err) {
+            uint32_t mask, int lean, int timeout_ms, std::string& err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!lib_) {
       err = std::string("dlopen failed: ") + dlerror();
@@ -185,6 +239,9 @@ class DlCounterSource final : public CounterSource {
     }
     auto configure = reinterpret_cast<configure_fn>(dlsym(lib_, "kgs_pmc_configure"));  // optional
     if (configure && lean >= 0) configure("lean", lean);
+    if (configure && timeout_ms > 0) configure("timeout_ms", timeout_ms);
+    abort_ = reinterpret_cast<abort_fn>(dlsym(lib_, "kgs_pmc_abort"));  // optional (aqlprofile reader)
+    reset_ = reinterpret_cast<reset_fn>(dlsym(lib_, "kgs_pmc_reset"));  // optional
     char ebuf[512] = {};
     if (init(ebuf, sizeof ebuf) != 0) {
       err = std::string("kgs_pmc_init: ") + ebuf;
@@ -212,6 +269,9 @@ class DlCounterSource final : public CounterSource {
     int opened = 0;
     handles_ = std::vector<std::atomic<int>>(static_cast<size_t>(be.device_count()));
     for (auto& h : handles_) h.store(-1);
+    agent_ = std::vector<std::atomic<int>>(static_cast<size_t>(be.device_count()));
+    for (auto& h : agent_) h.store(-1);
+    resets_ = std::vector<std::atomic<uint64_t>>(static_cast<size_t>(be.device_count()));
     kfd_ids_.assign(static_cast<size_t>(be.device_count()), 0);
     for (int d : devices) {
       kfd_ids_[static_cast<size_t>(d)] = be.info(d).kfd_gpu_id;
@@ -229,6 +289,7 @@ class DlCounterSource final : public CounterSource {
     char ebuf[512] = {};
     const int h = open_(kfd_ids_[static_cast<size_t>(d)], names_, is_max_, nsel_, ebuf, sizeof ebuf);
     handles_[static_cast<size_t>(d)] = h;
+    if (h >= 0) agent_[static_cast<size_t>(d)] = h;  // the reader's handle is its agent index: stable
     if (h < 0) {
       err = ebuf;
       return -1;
@@ -251,6 +312,22 @@ class DlCounterSource final : public CounterSource {
     if (handles_[static_cast<size_t>(dev)] >= 0) return 0;
     std::string e;
     return open_dev(dev, e);
+  }
+  int reset(int dev) override {
+    if (dev < 0 || dev >= static_cast<int>(handles_.size())) return -1;
+    if (handles_[static_cast<size_t>(dev)] >= 0) release(dev);
+    const int a = agent_[static_cast<size_t>(dev)];
+    if (!reset_ || a < 0) return -1;
+    resets_[static_cast<size_t>(dev)].fetch_add(1);
+    return reset_(a);
+  }
+  void cancel(int dev, bool on) override {
+    if (!abort_ || dev < 0 || dev >= static_cast<int>(agent_.size())) return;
+    const int a = agent_[static_cast<size_t>(dev)];
+    if (a >= 0) abort_(a, on ? 1 : 0);
+  }
+  uint64_t resets(int dev) const override {
+    return dev >= 0 && dev < static_cast<int>(resets_.size()) ? resets_[static_cast<size_t>(dev)].load() : 0;
   }
   void set_fresh(int dev, bool fresh) override {
     if (!pipelined_ || !set_pipe_ || dev < 0 || dev >= static_cast<int>(handles_.size())) return;
@@ -310,6 +387,10 @@ class DlCounterSource final : public CounterSource {
   uint32_t mask_ = 0;
   close_fn close_ = nullptr;
   info_fn info_ = nullptr;
+  abort_fn abort_ = nullptr;
+  reset_fn reset_ = nullptr;
+  std::vector<std::atomic<int>> agent_;  // per device: reader agent index once opened (-1 never)
+  std::vector<std::atomic<uint64_t>> resets_;
   // Written by the device's sampler thread (release / acquire), read by info()
   // from the HTTP / control threads.
   std::vector<std::atomic<int>> handles_;
@@ -325,9 +406,10 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
-                                                      bool pipelined, uint32_t mask, int lean, std::string& err) {
+                                                      bool pipelined, uint32_t mask, int lean, std::string& err,
+                                                      int timeout_ms) {
   auto s = std::make_unique<DlCounterSource>(name);
-  if (!s->load(lib_path, be, devices, pipelined, mask, lean, err)) return nullptr;
+  if (!s->load(lib_path, be, devices, pipelined, mask, lean, timeout_ms, err)) return nullptr;
   return s;
 }
 

@@ -202,7 +202,7 @@ void Exporter::render(std::string& out) {
     Snap& x = snaps[static_cast<size_t>(d)];
     const DeviceState& st = S.state(d);
     x.have = st.latest.load(x.s);
-    st.integ.load(x.I);
+    x.I = st.integrals();
     // Window gauges only from live data: a device that is down, or whose last
     // good read is older than stale_s (reads failing, sampling paused), exports
     // no busy gauges rather than its last value frozen; the counters stay.
@@ -283,11 +283,38 @@ void Exporter::render(std::string& out) {
                                      : x.I.gfx_busy_seconds - (o ? o->base_busy_s : 0.0);
       w.line("container_gpu_busy_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
     }
+    // Per-pod compute share: the CU-occupancy seconds of the pod's
+    // own processes on this GPU (per-process tier, PID → pod from cgroups), kept
+    // after they exit.  On a GPU shared by several pods each is billed its own
+    // share, where container_gpu_busy_seconds_total bills each the whole GPU.
+    bool any_cu = false;
+    for (size_t i = 0; i < pod_lines.size() && !any_cu; ++i) any_cu = pod_owner[i] != nullptr && cfg_.per_process;
+    if (any_cu) {
+      w.head("container_gpu_cu_seconds_total", "counter",
+             "CU-occupancy seconds of the pod's own processes on the GPU (occupied CUs / all CUs, integrated; "
+             "processes that exited included), counted from allocation; 100 * rate() = the pod's compute share of "
+             "the GPU, exact on GPUs shared by several pods (same labels as container_gpu_sm_util)");
+      for (size_t i = 0; i < pod_lines.size(); ++i) {
+        const Owner* o = pod_owner[i];
+        if (!o) continue;
+        const int d = pod_lines[i].first;
+        auto pc = S.state(d).get_pod_cu();
+        double v = 0;
+        if (pc) {
+          auto it = pc->find(o->ns + "/" + o->pod);
+          if (it != pc->end()) v = it->second;
+        }
+        v -= o->base_cu_s;
+        w.line("container_gpu_cu_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
+      }
+    }
     // Per-pod energy: the GPU's socket energy since the pod was given it (a GPU
-    // shared by several pods counts in full for each: the pods hold it together).
+    // shared by several pods counts in full for each: the pods hold it together;
+    // a compute partition's energy is its share of the socket's, sampler.cpp).
     w.head("container_gpu_energy_joules_total", "counter",
-           "Socket energy of the GPU allocated to the pod, counted from allocation (PMFW energy accumulator; "
-           "increase() over a window = joules the pod's GPU drew; same labels as container_gpu_sm_util)");
+           "Socket energy of the GPU allocated to the pod, counted from allocation (PMFW energy accumulator; a "
+           "compute partition gets its XCCs' busy share of the socket's; increase() over a window = joules the "
+           "pod's GPU drew; same labels as container_gpu_sm_util)");
     for (size_t i = 0; i < pod_lines.size(); ++i) {
       const Owner* o = pod_owner[i];
       const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
@@ -427,7 +454,9 @@ void Exporter::render(std::string& out) {
   }
   w.head("amdgpu_power_watts", "gauge", "Socket power in watts");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPower)) w.line("amdgpu_power_watts", dev_labels_[d], nullptr, snaps[d].s.power_w);
-  w.head("amdgpu_energy_joules_total", "counter", "Energy consumed since the exporter started (wrap-safe integration of the PMFW accumulator)");
+  w.head("amdgpu_energy_joules_total", "counter",
+         "Energy consumed since the exporter started (wrap-safe integration of the PMFW accumulator; a compute "
+         "partition counts its XCCs' GFX-busy share of the socket's energy, so partitions add up to the socket)");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_energy_joules_total", dev_labels_[d], nullptr, snaps[d].I.energy_joules);
   w.head("amdgpu_clock_mhz", "gauge", "Current clock frequency (gfx = mean over XCCs)");
   for (int d : ids) {
@@ -450,8 +479,6 @@ void Exporter::render(std::string& out) {
     if (snaps[d].have && (snaps[d].s.valid & kFThrottle))
       for (int r = 0; r < kThrottleReasons; ++r)
         w.line("amdgpu_throttle_seconds_total", dev_labels_[d], throttle_label(r), snaps[d].I.throttle_seconds[r]);
-  w.head("amdgpu_power_throttle_residency_total", "counter", "PMFW package-power-tracking throttle residency accumulator (raw)");
-  for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFThrottle)) w.line_u("amdgpu_power_throttle_residency_total", dev_labels_[d], nullptr, snaps[d].s.ppt_residency_acc);
 
   // ---- interconnect ------------------------------------------------------
   w.head("amdgpu_xgmi_read_bytes_total", "counter", "Bytes received per xGMI link (PMFW accumulator)");
@@ -556,7 +583,8 @@ void Exporter::render(std::string& out) {
   bool any_pmc = false;
   for (int d : ids) any_pmc |= snaps[d].pmc_have;
   if (any_pmc) {
-    w.head("amdgpu_pmc_total", "counter", "Raw hardware counter (rocprofiler-sdk device counting), cumulative since exporter start");
+    w.head("amdgpu_pmc_total", "counter",
+           "Raw hardware counter (direct command-processor reader), cumulative since exporter start");
     for (int d : ids) {
       const Snap& x = snaps[d];
       if (!x.pmc_have) continue;
@@ -570,7 +598,10 @@ void Exporter::render(std::string& out) {
     w.head("amdgpu_mfma_busy_seconds_total", "counter",
            "Integral of the MFMA-busy share of all SIMD cycles over time (hardware counters); rate() = matrix-core utilisation");
     for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);
-    w.head("amdgpu_mfma_util_percent", "gauge", "Matrix-core (MFMA) busy percent of active cycles over the window");
+    w.head("amdgpu_mfma_util_percent", "gauge",
+           "Matrix-core (MFMA) busy percent of the SIMD cycles while a shader engine had waves (GRBM_SPI_BUSY), over "
+           "the window; not rocprofv3 MfmaUtil (GUI-active based): the wall-clock share is "
+           "rate(amdgpu_mfma_busy_seconds_total)");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
     w.head("amdgpu_gpu_active_percent", "gauge",
            "Percent of clocks a shader engine had waves to run (GRBM_SPI_BUSY) over the window; unlike the PMFW GFX busy "
@@ -696,7 +727,19 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_quiet", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_quiet.load()));
     w.head("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU");
     for (int d : ids) w.line_u("kgs_pmc_quiet_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_quiet_skips.load());
+    w.head("kgs_pmc_failed", "gauge",
+           "1 while the counter tier's circuit breaker is open: consecutive counter drains failed (a wedged command "
+           "processor); READs stop, the reader's queue is recreated and re-STARTed with exponential backoff");
+    for (int d : ids) w.line_u("kgs_pmc_failed", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_failed.load()));
+    w.head("kgs_pmc_breaker_trips_total", "counter", "Times the counter tier's circuit breaker opened");
+    for (int d : ids) w.line_u("kgs_pmc_breaker_trips_total", dev_labels_[d], nullptr, S.state(d).pmc_breaker_trips.load());
+    w.head("kgs_pmc_retries_total", "counter", "Reader resets + re-STARTs attempted while the breaker was open");
+    for (int d : ids) w.line_u("kgs_pmc_retries_total", dev_labels_[d], nullptr, S.state(d).pmc_retries.load());
   }
+  w.head("kgs_sampler_thread_hung", "gauge",
+         "1 if a sampler thread of the device was stuck in a device call when sampling last stopped (it was "
+         "abandoned; that tier restarts once the call returns)");
+  for (int d : ids) w.line_u("kgs_sampler_thread_hung", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).thread_hung.load()));
   w.head("kgs_slow_reads_total", "counter",
          "Management-library reads by the node-wide slow thread (per-process list / xGMI link table + RAS)");
   for (int d : ids) {
@@ -739,7 +782,7 @@ void Exporter::render(std::string& out) {
     kv(lb, "version", "0.1.0");
     kv(lb, "backend", be_->name());
     kv(lb, "pmc_source", pmc_ ? pmc_->name() : std::string("none"));
-    kv(lb, "sample_hz", std::to_string(S.config().hz));
+    kv(lb, "sample_hz", std::to_string(S.hz()));
     w.line("kgs_build_info", lb, nullptr, 1);
   }
   if (extra && !filter_.active()) {

@@ -41,7 +41,20 @@ bool acc_delta(uint64_t prev, uint64_t cur, uint64_t& d) {
   return false;  // counter reset
 }
 
+enum WorkerKind : int { kPmfw = 0, kPmc = 1, kSlow = 2 };
+
 }  // namespace
+
+// One sampler thread.  Shared with the thread itself, so a thread that stop()
+// abandons still has a live `done` / `abandoned` pair to look at when (if) its
+// stuck call returns — and then exits without touching the sampler.
+struct Sampler::Worker {
+  int dev = -1;
+  int kind = kPmfw;
+  std::thread t;
+  std::atomic<bool> done{false};
+  std::atomic<bool> abandoned{false};
+};
 
 std::vector<int> numa_cpus(int node) {
   std::vector<int> cpus;
@@ -80,53 +93,177 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
     for (int d : cfg_.devices)
       if (d >= 0 && d < n) dev_ids_.push_back(d);
   }
-  if (cfg_.hz <= 0) cfg_.hz = 1;
-  pmc_idle_hz_.store(cfg_.pmc_idle_hz < 0 ? 0 : cfg_.pmc_idle_hz);
-  for (int d : dev_ids_) states_[static_cast<size_t>(d)]->pmc_on.store(cfg_.pmc && pmc_ ? 1 : 0);
+  if (!(cfg_.hz > 0)) cfg_.hz = 1;
+  if (cfg_.hz > kMaxHz) cfg_.hz = kMaxHz;
+  hz_.store(cfg_.hz);
+  if (cfg_.pmc_breaker_k < 1) cfg_.pmc_breaker_k = 1;
+  if (!(cfg_.pmc_retry_s > 0)) cfg_.pmc_retry_s = 1.0;
+  if (cfg_.pmc_retry_max_s < cfg_.pmc_retry_s) cfg_.pmc_retry_max_s = cfg_.pmc_retry_s;
+  const double ih = cfg_.pmc_idle_hz;
+  pmc_idle_hz_.store(!(ih > 0) ? 0.0 : std::clamp(ih, kMinIdleHz, kMaxHz));
+  for (int d : dev_ids_) {
+    DeviceState& st = *states_[static_cast<size_t>(d)];
+    st.pmc_on.store(cfg_.pmc && pmc_ ? 1 : 0);
+    st.pmc_backoff_s = cfg_.pmc_retry_s;
+  }
   cu_seconds_.resize(static_cast<size_t>(n));
+  pod_cu_.resize(static_cast<size_t>(n));
   last_proc_ns_.assign(static_cast<size_t>(n), 0);
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
 }
 
-void Sampler::set_hz(double hz) {
-  if (hz <= 0) return;
+bool Sampler::set_hz(double hz) {
+  if (!(hz > 0 && hz <= kMaxHz)) return false;
+  std::lock_guard<std::mutex> lk(life_mu_);
   const bool was = running_.load();
-  stop();
-  cfg_.hz = hz;
-  if (was) start();
+  stop_locked();
+  hz_.store(hz);
+  if (was) start_locked();
+  return true;
 }
 
-void Sampler::set_pmc_wanted(bool on) {
-  for (int d : dev_ids_) states_[static_cast<size_t>(d)]->pmc_want.store(on ? 1 : 0);
+bool Sampler::set_pmc_idle_hz(double hz) {
+  if (!(hz == 0 || (hz >= kMinIdleHz && hz <= kMaxHz))) return false;
+  pmc_idle_hz_.store(hz, std::memory_order_relaxed);
+  return true;
+}
+
+void Sampler::set_pmc_wanted(bool on, int dev) {
+  for (int d : dev_ids_)
+    if (dev < 0 || d == dev) states_[static_cast<size_t>(d)]->pmc_want.store(on ? 1 : 0);
+}
+
+void Sampler::set_pid_pods(std::shared_ptr<const std::unordered_map<uint64_t, std::string>> m) {
+  std::lock_guard<std::mutex> g(pid_pods_mu_);
+  pid_pods_ = std::move(m);
+}
+
+double Sampler::pod_cu_seconds(int dev, const std::string& ns_pod) const {
+  if (dev < 0 || dev >= device_count()) return 0.0;
+  auto m = states_[static_cast<size_t>(dev)]->get_pod_cu();
+  if (!m) return 0.0;
+  auto it = m->find(ns_pod);
+  return it == m->end() ? 0.0 : it->second;
 }
 
 Sampler::~Sampler() {
   stop();
-  if (stop_fd_ >= 0) close(stop_fd_);
+  // An abandoned thread may still be inside a backend / counter-source call; it
+  // exits without touching `this`, but its stop flag lives here: leave the fd.
+  if (stop_fd_ >= 0 && abandoned_total_.load() == 0) close(stop_fd_);
 }
 
 void Sampler::start() {
+  std::lock_guard<std::mutex> lk(life_mu_);
+  start_locked();
+}
+
+void Sampler::stop() {
+  std::lock_guard<std::mutex> lk(life_mu_);
+  stop_locked();
+}
+
+void Sampler::spawn(int dev, int kind) {
+  auto w = std::make_shared<Worker>();
+  w->dev = dev;
+  w->kind = kind;
+  w->t = std::thread([this, w] {
+    if (w->kind == kPmfw) run_pmfw(*w);
+    else if (w->kind == kPmc) run_pmc(*w);
+    else run_slow(*w);
+    w->done.store(true, std::memory_order_release);
+  });
+  workers_.push_back(std::move(w));
+}
+
+void Sampler::start_locked() {
   if (running_.exchange(true)) return;
   stop_.store(false);
   uint64_t drain;
   while (read(stop_fd_, &drain, sizeof drain) > 0) {
   }
-  for (int d : dev_ids_) threads_.emplace_back([this, d] { run(d); });
-  if (cfg_.proc_every > 0 || cfg_.link_every > 0 || cfg_.proc_period_s > 0 || cfg_.link_period_s > 0)
-    slow_thread_ = std::thread([this] { run_slow(); });
+  // A (device, tier) whose abandoned thread is still stuck gets no second thread:
+  // two threads on one device's reader would break its one-thread-per-handle rule.
+  auto stuck = [&](int dev, int kind) {
+    for (const auto& w : abandoned_)
+      if (w->dev == dev && w->kind == kind && !w->done.load(std::memory_order_acquire)) return true;
+    return false;
+  };
+  abandoned_.erase(std::remove_if(abandoned_.begin(), abandoned_.end(),
+                                  [](const std::shared_ptr<Worker>& w) { return w->done.load(); }),
+                   abandoned_.end());
+  const bool pmc = cfg_.pmc && pmc_;
+  for (int d : dev_ids_) {
+    DeviceState& st = *states_[static_cast<size_t>(d)];
+    bool hung = false;
+    if (!stuck(d, kPmfw)) spawn(d, kPmfw);
+    else hung = true;
+    if (pmc) {
+      if (!stuck(d, kPmc)) {
+        pmc_->cancel(d, false);
+        spawn(d, kPmc);
+      } else {
+        hung = true;
+      }
+    }
+    st.thread_hung.store(hung ? 1 : 0);
+  }
+  if ((cfg_.proc_every > 0 || cfg_.link_every > 0 || cfg_.proc_period_s > 0 || cfg_.link_period_s > 0) &&
+      !stuck(-1, kSlow))
+    spawn(-1, kSlow);
 }
 
-void Sampler::stop() {
+void Sampler::stop_locked() {
   if (!running_.load()) return;
   stop_.store(true);
   const uint64_t one = 1;
   if (write(stop_fd_, &one, sizeof one) < 0) {
   }
-  for (auto& t : threads_)
-    if (t.joinable()) t.join();
-  threads_.clear();
-  if (slow_thread_.joinable()) slow_thread_.join();
+  // Calls blocked on a device's counters (a wedged CP) return at once.
+  if (cfg_.pmc && pmc_)
+    for (int d : dev_ids_) pmc_->cancel(d, true);
+  const int64_t deadline = mono_ns() + static_cast<int64_t>(cfg_.stop_timeout_s * 1e9);
+  for (;;) {
+    bool all = true;
+    for (const auto& w : workers_) all = all && w->done.load(std::memory_order_acquire);
+    if (all || mono_ns() >= deadline) break;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  for (auto& w : workers_) {
+    if (w->done.load(std::memory_order_acquire)) {
+      w->t.join();
+      continue;
+    }
+    // Stuck inside a device call: detach.  The thread checks `abandoned` after
+    // every such call and exits without touching this sampler.
+    w->abandoned.store(true, std::memory_order_release);
+    w->t.detach();
+    if (w->dev >= 0) states_[static_cast<size_t>(w->dev)]->thread_hung.store(1);
+    abandoned_total_.fetch_add(1);
+    abandoned_.push_back(w);
+  }
+  workers_.clear();
   running_.store(false);
+}
+
+void Sampler::pin(int dev, const char* fmt) {
+  DeviceState& st = *states_[static_cast<size_t>(dev)];
+  if (cfg_.pin_numa) {
+    const std::vector<int> cpus = numa_cpus(be_->info(dev).numa_node);
+    if (!cpus.empty()) {
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      for (int c : cpus) CPU_SET(c, &set);
+      if (pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0) st.cpu_pinned.store(static_cast<int>(cpus.size()));
+    }
+  }
+  char tname[16];
+  std::snprintf(tname, sizeof tname, fmt, dev);
+  pthread_setname_np(pthread_self(), tname);
+  // The default 50 µs timer slack is 40 % of an 8 kHz period: wake on time.
+  // (KGS_TIMERSLACK_NS overrides, for interference experiments.)
+  const char* slack = std::getenv("KGS_TIMERSLACK_NS");
+  prctl(PR_SET_TIMERSLACK, slack ? std::strtoul(slack, nullptr, 10) : 1000UL, 0, 0, 0);
 }
 
 void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integrals& I) {
@@ -171,8 +308,22 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
   I.gfx_busy_seconds += g * 0.01 * dt;
   I.umc_busy_seconds += u * 0.01 * dt;
   I.sampled_seconds += dt;
-  if ((cur.valid & kFEnergy) && (prev->valid & kFEnergy) && cur.energy_acc >= prev->energy_acc)
-    I.energy_joules += energy_units_to_joules(cur.energy_acc - prev->energy_acc);
+  if ((cur.valid & kFEnergy) && (prev->valid & kFEnergy) && cur.energy_acc >= prev->energy_acc) {
+    double e = energy_units_to_joules(cur.energy_acc - prev->energy_acc);
+    // Compute partitions (DPX/QPX/CPX) read one socket's energy accumulator: each
+    // takes its XCCs' share of the chip's GFX busy over the interval (an equal
+    // share while the chip is idle), so the partitions' counters add up to the
+    // socket's energy instead of counting it once per partition.
+    if (cur.energy_parts > 1) {
+      double share = 1.0 / cur.energy_parts;
+      if ((cur.valid & kFXccAcc) && (prev->valid & kFXccAcc) && cur.xcc_acc_chip > prev->xcc_acc_chip &&
+          cur.xcc_acc_own >= prev->xcc_acc_own)
+        share = static_cast<double>(cur.xcc_acc_own - prev->xcc_acc_own) /
+                static_cast<double>(cur.xcc_acc_chip - prev->xcc_acc_chip);
+      e *= std::clamp(share, 0.0, 1.0);
+    }
+    I.energy_joules += e;
+  }
   // Throttler residencies: the fraction of accumulation cycles each controller was
   // active (amdsmi.h PVIOL / TVIOL), times the interval.
   if ((cur.valid & kFThrottle) && (prev->valid & kFThrottle) && (cur.valid & kFAcc) && (prev->valid & kFAcc) &&
@@ -185,50 +336,139 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
     }
 }
 
-void Sampler::run(int dev) {
-  DeviceState& st = *states_[dev];
-  const DeviceInfo& info = be_->info(dev);
-  if (cfg_.pin_numa) {
-    const std::vector<int> cpus = numa_cpus(info.numa_node);
-    if (!cpus.empty()) {
-      cpu_set_t set;
-      CPU_ZERO(&set);
-      for (int c : cpus) CPU_SET(c, &set);
-      if (pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0) st.cpu_pinned.store(static_cast<int>(cpus.size()));
-    }
-  }
-  char tname[16];
-  std::snprintf(tname, sizeof tname, "kgs-gpu%d", dev);
-  pthread_setname_np(pthread_self(), tname);
-  // The default 50 µs timer slack is 40 % of an 8 kHz period: wake on time.
-  // (KGS_TIMERSLACK_NS overrides, for interference experiments.)
-  const char* slack = std::getenv("KGS_TIMERSLACK_NS");
-  prctl(PR_SET_TIMERSLACK, slack ? std::strtoul(slack, nullptr, 10) : 1000UL, 0, 0, 0);
-
-  const int64_t period_ns = static_cast<int64_t>(1e9 / cfg_.hz);
-  const uint64_t pmfw_every = cfg_.pmfw_hz > 0 && cfg_.pmfw_hz < cfg_.hz
-                                  ? static_cast<uint64_t>(cfg_.hz / cfg_.pmfw_hz + 0.5)
-                                  : 1;
+// ---- PMFW tier: the firmware metrics table + HBM occupancy --------------------
+// At min(hz, pmfw_hz): the table refreshes every ≈20 ms, so reading it faster
+// only re-reads the same table.  A failing device backs off; every 4th failure
+// of a streak asks the backend to re-open / re-initialise it.
+void Sampler::run_pmfw(Worker& w) {
+  const int dev = w.dev;
+  DeviceState& st = *states_[static_cast<size_t>(dev)];
+  Backend* const be = be_;
+  pin(dev, "kgs-pmfw%d");
+  const double hz = hz_.load();
+  const double rate = cfg_.pmfw_hz > 0 && cfg_.pmfw_hz < hz ? cfg_.pmfw_hz : hz;
+  const int64_t period_ns = static_cast<int64_t>(1e9 / rate);
   Integrals I;
   GpuSample& prev = st.pmfw_prev;
   bool& have_prev = st.have_pmfw_prev;
-  uint64_t seq = 0, pmc_seq = 0, tick = 0;
-  int64_t last_slow_ns = 0;
-  {  // resume after a pause: counters and sequence numbers continue
+  uint64_t seq = 0;
+  {  // resume after a pause: integrals and sequence numbers continue
     st.integ.load(I);
     GpuSample last;
     if (st.latest.load(last)) seq = last.seq;
+  }
+  int64_t next = mono_ns();
+  while (!stop_.load(std::memory_order_relaxed)) {
+    int backoff_shift = 0;
+    GpuSample s;
+    const int64_t t0 = mono_ns();
+    const int rc = be->read_metrics(dev, s);
+    const int64_t t1 = mono_ns();
+    if (w.abandoned.load(std::memory_order_acquire)) return;  // stop() gave up on us while we were in the call
+    const double us = (t1 - t0) * 1e-3;
+    int b = 0;
+    while (b < kReadHistBuckets && us > kReadHistBoundsUs[b]) ++b;
+    st.read_hist[b].fetch_add(1, std::memory_order_relaxed);
+    ++I.reads;
+    I.read_seconds += (t1 - t0) * 1e-9;
+    if (rc == 0) {
+      s.read_ns = static_cast<uint32_t>(t1 - t0);
+      if (s.mono_ns == 0) s.mono_ns = t1;
+      st.up.store(1, std::memory_order_relaxed);
+      st.consecutive_errors.store(0, std::memory_order_relaxed);
+      st.last_ok_mono_ns.store(t1, std::memory_order_relaxed);
+      const bool distinct = !have_prev || !(s.valid & kFFwTs) || s.fw_ts != prev.fw_ts;
+      // Firmware clock went backwards: the SMU restarted (GPU reset), so every
+      // accumulator restarted too — re-baseline instead of reading a wrap.
+      const bool reset = have_prev && (s.valid & kFFwTs) && (prev.valid & kFFwTs) && s.fw_ts < prev.fw_ts;
+      if (distinct) {
+        integrate(dev, have_prev && !reset ? &prev : nullptr, s, I);
+        s.cum_gfx_s = I.gfx_busy_seconds;
+        s.cum_umc_s = I.umc_busy_seconds;
+        s.cum_dt_s = I.sampled_seconds;
+        s.seq = ++seq;
+        ++I.distinct_samples;
+        st.ring.push(s);
+        st.latest.store(s);
+        prev = s;
+        have_prev = true;
+      } else {
+        // Same PMFW table: refresh host-side fields only (HBM occupancy).
+        prev.vram_used_bytes = s.vram_used_bytes;
+        prev.mono_ns = s.mono_ns;
+        prev.wall_ns = s.wall_ns;
+        st.latest.store(prev);
+      }
+    } else {
+      ++I.read_errors;
+      const uint64_t ce = st.consecutive_errors.fetch_add(1, std::memory_order_relaxed) + 1;
+      if (ce >= 3) st.up.store(0, std::memory_order_relaxed);
+      backoff_shift = ce > 10 ? 10 : static_cast<int>(ce);
+      // Every 4th failure of a streak (≈ every 4·max_backoff once backed off):
+      // let the backend reopen / re-initialise the device.
+      if (ce % 4 == 0) {
+        ++I.recover_attempts;
+        const int rr = be->recover(dev);
+        if (w.abandoned.load(std::memory_order_acquire)) return;
+        if (rr == 0) {
+          ++I.recoveries;
+          have_prev = false;
+        }
+      }
+    }
+
+    int64_t step = period_ns;
+    if (backoff_shift > 0) {
+      step = period_ns << backoff_shift;
+      const int64_t cap = static_cast<int64_t>(cfg_.max_backoff_ms) * 1000000LL;
+      if (step > cap) step = cap > period_ns ? cap : period_ns;
+    }
+    next += step;
+    const int64_t now = mono_ns();
+    if (next <= now) {
+      ++I.overruns;
+      // Late by a few periods (a long read, a descheduled thread): keep the
+      // absolute schedule, the missed ticks run at once and the rate holds.
+      // Further behind: re-anchor and sleep a quarter period instead of bursting.
+      if (backoff_shift) next = now + step;
+      else if (now - next > kCatchUpPeriods * step) next = now + period_ns / 4;
+    }
+    st.integ.store(I);
+    const int64_t wait = next - now;
+    timespec ts{static_cast<time_t>(wait / 1000000000LL), static_cast<long>(wait % 1000000000LL)};
+    pollfd pfd{stop_fd_, POLLIN, 0};
+    ppoll(&pfd, 1, &ts, nullptr);
+  }
+  st.integ.store(I);
+}
+
+// ---- counter tier: one hardware-counter drain per tick ------------------------
+void Sampler::run_pmc(Worker& w) {
+  const int dev = w.dev;
+  DeviceState& st = *states_[static_cast<size_t>(dev)];
+  CounterSource* const src = pmc_;
+  const DeviceInfo& info = be_->info(dev);
+  pin(dev, "kgs-gpu%d");
+  const double hz = hz_.load();
+  const int64_t period_ns = static_cast<int64_t>(1e9 / hz);
+  auto gone = [&w] { return w.abandoned.load(std::memory_order_acquire); };
+  Integrals P;
+  uint64_t pmc_seq = 0;
+  int64_t last_slow_ns = 0;
+  {  // resume after a pause: counters and sequence numbers continue
+    st.pmc_integ.load(P);
     PmcSample lp;
     if (st.pmc_latest.load(lp)) pmc_seq = lp.seq;
   }
   // A thread that stopped (pause, rate change) while its device was quiet left
   // the reader in synchronous mode: start pipelined, not quiet.
-  if (cfg_.pmc && pmc_ && st.pmc_on.load()) pmc_->set_fresh(dev, false);
+  if (st.pmc_on.load()) {
+    src->set_fresh(dev, false);
+    if (gone()) return;
+  }
   st.pmc_quiet.store(0, std::memory_order_relaxed);
   int64_t next = mono_ns();
-  int late_streak = 0;  // consecutive overrun ticks
   PmcSample& pmc_base = st.pmc_base;
-  int64_t last_acquire_fail_ns = 0;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
   uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0;
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
@@ -238,103 +478,79 @@ void Sampler::run(int dev) {
   int64_t prev_ps_ns = 0;
   int64_t last_plausible_ns = mono_ns();
   int64_t last_start_ns = mono_ns();  // last (re)START of the counter session
+  // A fresh START restarts every count at 0: the interval from START to the first
+  // READ is then counted exactly (acquire → first READ was dropped).
+  auto started_at = [&](int64_t t) {
+    have_prev_ps = true;
+    prev_ps_count = prev_ps_mfma = prev_ps_active = 0;
+    prev_ps_ns = t;
+    quiet = false;
+    quiet_since_ns = 0;
+    fresh_mode = false;  // a (re)opened session reads pipelined
+    last_plausible_ns = t;
+    last_start_ns = t;
+  };
+  // Totals of the published stream become the base of the next session's counts.
+  auto carry_base = [&] {
+    PmcSample last;
+    if (st.pmc_latest.load(last)) pmc_base = last;
+  };
+  // Open the breaker: stop READing this device, retry after the backoff.
+  auto trip = [&](int64_t now) {
+    st.pmc_failed.store(1);
+    st.pmc_breaker_trips.fetch_add(1, std::memory_order_relaxed);
+    carry_base();
+    src->release(dev);  // bounded by the source's deadline
+    st.pmc_on.store(0);
+    st.pmc_stalled.store(0);
+    st.pmc_quiet.store(0, std::memory_order_relaxed);
+    st.pmc_fail_streak = 0;
+    st.pmc_retry_at_ns = now + static_cast<int64_t>(st.pmc_backoff_s * 1e9);
+    st.pmc_backoff_s = std::min(st.pmc_backoff_s * 2, cfg_.pmc_retry_max_s);
+    have_prev_ps = false;
+  };
 
   while (!stop_.load(std::memory_order_relaxed)) {
-    // ---- fast tier: the PMFW table (refreshed by firmware every ≈20 ms) is
-    // read every `pmfw_every` ticks, i.e. at ≤ pmfw_hz however fast the
-    // counter tier runs.  A failing device backs off on this tier. ----------
-    int backoff_shift = 0;
-    if (tick % pmfw_every == 0 || st.consecutive_errors.load(std::memory_order_relaxed) > 0) {
-      GpuSample s;
-      const int64_t t0 = mono_ns();
-      const int rc = be_->read_metrics(dev, s);
-      const int64_t t1 = mono_ns();
-      const double us = (t1 - t0) * 1e-3;
-      int b = 0;
-      while (b < kReadHistBuckets && us > kReadHistBoundsUs[b]) ++b;
-      st.read_hist[b].fetch_add(1, std::memory_order_relaxed);
-      ++I.reads;
-      I.read_seconds += (t1 - t0) * 1e-9;
+    const int want = st.pmc_want.load(std::memory_order_relaxed);
+    // ---- hand-over: release on request ----------------------------------------
+    if (!want && st.pmc_on.load(std::memory_order_relaxed)) {
+      src->release(dev);  // a failed STOP still ends our READs
+      if (gone()) return;
+      st.pmc_on.store(0);
+      st.pmc_stalled.store(0);
+      st.pmc_releases.fetch_add(1, std::memory_order_relaxed);
+      // The next START restarts the counts at 0: carry the published totals
+      // as a base so the exported counters stay monotonic.
+      carry_base();
+    }
+    // ---- (re)acquire: after a hand-over, or a retry of an open breaker --------
+    if (want && !st.pmc_on.load(std::memory_order_relaxed) && mono_ns() >= st.pmc_retry_at_ns) {
+      const bool failed = st.pmc_failed.load() != 0;
+      if (failed) {  // wedged before: drop the old queue, then START on a fresh one
+        st.pmc_retries.fetch_add(1, std::memory_order_relaxed);
+        src->reset(dev);
+        if (gone()) return;
+      }
+      const int rc = src->acquire(dev);
+      if (gone()) return;
+      const int64_t now_c = mono_ns();
       if (rc == 0) {
-        s.read_ns = static_cast<uint32_t>(t1 - t0);
-        if (s.mono_ns == 0) s.mono_ns = t1;
-        st.up.store(1, std::memory_order_relaxed);
-        st.consecutive_errors.store(0, std::memory_order_relaxed);
-        st.last_ok_mono_ns.store(t1, std::memory_order_relaxed);
-        const bool distinct = !have_prev || !(s.valid & kFFwTs) || s.fw_ts != prev.fw_ts;
-        // Firmware clock went backwards: the SMU restarted (GPU reset), so every
-        // accumulator restarted too — re-baseline instead of reading a wrap.
-        const bool reset = have_prev && (s.valid & kFFwTs) && (prev.valid & kFFwTs) && s.fw_ts < prev.fw_ts;
-        if (distinct) {
-          integrate(dev, have_prev && !reset ? &prev : nullptr, s, I);
-          s.cum_gfx_s = I.gfx_busy_seconds;
-          s.cum_umc_s = I.umc_busy_seconds;
-          s.cum_dt_s = I.sampled_seconds;
-          s.seq = ++seq;
-          ++I.distinct_samples;
-          st.ring.push(s);
-          st.latest.store(s);
-          prev = s;
-          have_prev = true;
-        } else {
-          // Same PMFW table: refresh host-side fields only (HBM occupancy).
-          prev.vram_used_bytes = s.vram_used_bytes;
-          prev.mono_ns = s.mono_ns;
-          prev.wall_ns = s.wall_ns;
-          st.latest.store(prev);
-        }
+        st.pmc_on.store(1);
+        started_at(now_c);  // the breaker closes on the first good drain
       } else {
-        ++I.read_errors;
-        const uint64_t ce = st.consecutive_errors.fetch_add(1, std::memory_order_relaxed) + 1;
-        if (ce >= 3) st.up.store(0, std::memory_order_relaxed);
-        backoff_shift = ce > 10 ? 10 : static_cast<int>(ce);
-        // Every 4th failure of a streak (≈ every 4·max_backoff once backed off):
-        // let the backend reopen / re-initialise the device.
-        if (ce % 4 == 0) {
-          ++I.recover_attempts;
-          if (be_->recover(dev) == 0) {
-            ++I.recoveries;
-            have_prev = false;
-          }
+        ++P.pmc_errors;
+        if (failed) {
+          st.pmc_retry_at_ns = now_c + static_cast<int64_t>(st.pmc_backoff_s * 1e9);
+          st.pmc_backoff_s = std::min(st.pmc_backoff_s * 2, cfg_.pmc_retry_max_s);
+        } else {
+          st.pmc_retry_at_ns = now_c + 1000000000LL;  // after a failed START: ≤ 1 retry/s
         }
       }
     }
-
-    // ---- PMC tier ------------------------------------------------------
-    bool pmc_now = false;
-    if (cfg_.pmc && pmc_) {
-      const int want = st.pmc_want.load(std::memory_order_relaxed);
-      if (want != st.pmc_on.load(std::memory_order_relaxed)) {
-        const int64_t now_c = mono_ns();
-        if (!want) {
-          pmc_->release(dev);  // a failed STOP still ends our READs
-          st.pmc_on.store(0);
-          st.pmc_stalled.store(0);
-          st.pmc_releases.fetch_add(1, std::memory_order_relaxed);
-          // The next START restarts the counts at 0: carry the published totals
-          // as a base so the exported counters stay monotonic.
-          PmcSample last;
-          if (st.pmc_latest.load(last)) pmc_base = last;
-        } else if (now_c - last_acquire_fail_ns >= 1000000000LL) {  // after a failed START: ≤ 1 retry/s
-          if (pmc_->acquire(dev) == 0) {
-            st.pmc_on.store(1);
-            have_prev_ps = false;
-            quiet = false;
-            quiet_since_ns = 0;
-            fresh_mode = false;  // a (re)opened session reads pipelined
-            last_plausible_ns = now_c;
-            last_start_ns = now_c;
-          } else {
-            last_acquire_fail_ns = now_c;
-            ++I.pmc_errors;
-          }
-        }
-      }
-      pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
-    }
+    bool pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
     if (pmc_now && quiet) {
       const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
-      if (idle_hz > 0 && idle_hz < cfg_.hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / idle_hz)) {
+      if (idle_hz > 0 && idle_hz < hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / idle_hz)) {
         pmc_now = false;
         st.pmc_quiet_skips.fetch_add(1, std::memory_order_relaxed);
       }
@@ -343,9 +559,15 @@ void Sampler::run(int dev) {
       PmcSample ps;
       const int64_t p0 = mono_ns();
       last_pmc_ns = p0;
-      const int prc = pmc_->sample(dev, ps);
-      I.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
+      const int prc = src->sample(dev, ps);
+      if (gone()) return;
+      P.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
       if (prc == 0) {
+        st.pmc_fail_streak = 0;
+        if (st.pmc_failed.load(std::memory_order_relaxed)) {  // a retry worked: close the breaker
+          st.pmc_failed.store(0);
+          st.pmc_backoff_s = cfg_.pmc_retry_s;
+        }
         // Stall detection: GRBM_COUNT free-runs at the shader clock while our
         // session is programmed; frozen or foreign counts give no plausible clock.
         if (have_prev_ps && ps.mono_ns > prev_ps_ns) {
@@ -359,13 +581,13 @@ void Sampler::run(int dev) {
           const double simds = (info.num_cu > 0 ? info.num_cu : 256) * 4.0;
           const double frac = static_cast<double>(ps.value[kPmcMfmaBusy] - prev_ps_mfma) /
                               (simds * static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count));
-          I.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
+          P.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
         }
         if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcGrbmActive)) &&
             ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcGrbmActive] >= prev_ps_active) {
           const double frac = static_cast<double>(ps.value[kPmcGrbmActive] - prev_ps_active) /
                               static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
-          I.active_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
+          P.active_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
         }
         // Quiet = a shader engine had waves for < kQuietActiveFrac of the clocks
         // since the previous READ, and no MFMA cycle ran.  Both counters are
@@ -387,9 +609,10 @@ void Sampler::run(int dev) {
         st.pmc_quiet.store(quiet ? 1 : 0, std::memory_order_relaxed);
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
-          const bool slow = quiet && idle_hz > 0 && idle_hz < cfg_.hz;
+          const bool slow = quiet && idle_hz > 0 && idle_hz < hz;
           if (slow != fresh_mode) {
-            pmc_->set_fresh(dev, slow);
+            src->set_fresh(dev, slow);
+            if (gone()) return;
             fresh_mode = slow;
           }
         }
@@ -414,7 +637,7 @@ void Sampler::run(int dev) {
           last_slow_ns = ps.mono_ns;
         }
         st.pmc_latest.store(ps);
-        ++I.pmc_samples;
+        ++P.pmc_samples;
         const bool reclaim = cfg_.pmc_reclaim_s > 0 && stall >= static_cast<int64_t>(cfg_.pmc_reclaim_s * 1e9);
         const bool refresh = cfg_.pmc_refresh_s > 0 &&
                              ps.mono_ns - last_start_ns >= static_cast<int64_t>(cfg_.pmc_refresh_s * 1e9);
@@ -422,102 +645,128 @@ void Sampler::run(int dev) {
           // STOP + START our session (selects reprogrammed, counts from 0); totals
           // carry over like a hand-over.
           pmc_base = ps;
-          pmc_->release(dev);
-          last_start_ns = ps.mono_ns;
-          if (pmc_->acquire(dev) == 0) {
+          src->release(dev);
+          if (gone()) return;
+          const int arc = src->acquire(dev);
+          if (gone()) return;
+          const int64_t t = mono_ns();
+          if (arc == 0) {
             (reclaim ? st.pmc_reclaims : st.pmc_refreshes).fetch_add(1, std::memory_order_relaxed);
+            started_at(t);
           } else {
             st.pmc_on.store(0);
-            last_acquire_fail_ns = ps.mono_ns;
-            ++I.pmc_errors;
+            st.pmc_retry_at_ns = t + 1000000000LL;
+            ++P.pmc_errors;
+            have_prev_ps = false;
+            last_plausible_ns = t;
+            last_start_ns = t;
           }
-          have_prev_ps = false;
-          quiet = false;
-          quiet_since_ns = 0;
-          fresh_mode = false;
-          last_plausible_ns = mono_ns();  // a full reclaim period before the next one
         }
       } else {
-        ++I.pmc_errors;
+        ++P.pmc_errors;
+        if (++st.pmc_fail_streak >= cfg_.pmc_breaker_k) {
+          trip(mono_ns());
+          if (gone()) return;
+        }
       }
     }
 
-    ++tick;
-
     // ---- schedule --------------------------------------------------------
     int64_t step = period_ns;
-    if (backoff_shift > 0) {
-      step = period_ns << backoff_shift;
-      const int64_t cap = static_cast<int64_t>(cfg_.max_backoff_ms) * 1000000LL;
-      if (step > cap) step = cap > period_ns ? cap : period_ns;
-    }
+    // Nothing to READ (handed over / breaker open): poll the hand-over flag and the
+    // retry deadline at ≤ 100 Hz instead of every tick.
+    if (!st.pmc_on.load(std::memory_order_relaxed)) step = std::max<int64_t>(period_ns, 10000000LL);
     next += step;
     const int64_t now = mono_ns();
     if (next <= now) {
-      ++I.overruns;
-      // A tick that ran long (the PMFW table read is ≈50–130 µs, longer than a
-      // kHz period) is followed by one immediate tick, so the counter tier keeps
-      // its rate; a second overrun in a row means the rate is beyond the work,
-      // and then the thread sleeps a quarter period instead of spinning.
-      next = now + (backoff_shift ? step : 0);
-      if (next <= now && ++late_streak > 1) next = now + period_ns / 4;
-    } else {
-      late_streak = 0;
+      ++P.overruns;
+      // Late by a few periods (a slow drain, a descheduled thread): keep the
+      // absolute schedule, so the missed ticks run at once and the delivered rate
+      // stays the configured one.  Further behind, the rate is beyond the work (or
+      // the host stalled): re-anchor and sleep a quarter period instead of bursting.
+      if (now - next > kCatchUpPeriods * step) next = now + period_ns / 4;
     }
-    st.integ.store(I);
+    st.pmc_integ.store(P);
     // Sleep until the absolute deadline or until stop() signals the eventfd.
     const int64_t wait = next - now;
-    timespec ts{static_cast<time_t>(wait / 1000000000LL), static_cast<long>(wait % 1000000000LL)};
-    pollfd pfd{stop_fd_, POLLIN, 0};
-    ppoll(&pfd, 1, &ts, nullptr);
+    if (wait > 0) {
+      timespec ts{static_cast<time_t>(wait / 1000000000LL), static_cast<long>(wait % 1000000000LL)};
+      pollfd pfd{stop_fd_, POLLIN, 0};
+      ppoll(&pfd, 1, &ts, nullptr);
+    }
   }
-  st.integ.store(I);
+  st.pmc_integ.store(P);
 }
 
 // Node-wide management-library tiers (see sampler.h).  Each due device is read
 // in turn; the per-GPU threads never wait on these calls.
-void Sampler::run_slow() {
+void Sampler::run_slow(Worker& w) {
   pthread_setname_np(pthread_self(), "kgs-slow");
-  const int64_t tick_ns = static_cast<int64_t>(1e9 / cfg_.hz);
+  const int64_t tick_ns = static_cast<int64_t>(1e9 / hz_.load());
   const int64_t proc_ns = cfg_.proc_period_s > 0 ? static_cast<int64_t>(cfg_.proc_period_s * 1e9)
                         : cfg_.proc_every > 0   ? tick_ns * cfg_.proc_every
                                                 : 0;
   const int64_t link_ns = cfg_.link_period_s > 0 ? static_cast<int64_t>(cfg_.link_period_s * 1e9)
                         : cfg_.link_every > 0   ? tick_ns * cfg_.link_every
                                                 : 0;
+  Backend* const be = be_;
+  auto gone = [&w] { return w.abandoned.load(std::memory_order_acquire); };
   int64_t next_proc = mono_ns(), next_link = next_proc;
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;
   while (!stop_.load(std::memory_order_relaxed)) {
     const int64_t t0 = mono_ns();
     if (proc_ns > 0 && t0 >= next_proc) {
+      std::shared_ptr<const std::unordered_map<uint64_t, std::string>> pid_pods;
+      {
+        std::lock_guard<std::mutex> g(pid_pods_mu_);
+        pid_pods = pid_pods_;
+      }
       for (int dev : dev_ids_) {
         if (stop_.load(std::memory_order_relaxed)) break;
         DeviceState& st = *states_[static_cast<size_t>(dev)];
         const int64_t a = mono_ns();
-        if (be_->read_procs(dev, procs) == 0) {
+        const int rc = be->read_procs(dev, procs);
+        if (gone()) return;
+        if (rc == 0) {
           const int64_t now_p = mono_ns();
           int64_t& last = last_proc_ns_[static_cast<size_t>(dev)];
           const double dt = last ? (now_p - last) * 1e-9 : 0.0;
-          const int cu = be_->info(dev).num_cu;
+          const int cu = be->info(dev).num_cu;
           const double ncu = cu > 0 ? cu : 256.0;
           auto& cs = cu_seconds_[static_cast<size_t>(dev)];  // (pid, ∫ occupancy share dt), sorted by pid
+          auto& pods = pod_cu_[static_cast<size_t>(dev)];
+          bool pods_changed = false;
           std::vector<std::pair<uint32_t, double>> next_cs;
           next_cs.reserve(procs.size());
           for (ProcInfo& p : procs) {
             auto it = std::lower_bound(cs.begin(), cs.end(), std::make_pair(p.pid, -1.0));
             const bool known = it != cs.end() && it->first == p.pid;
-            p.cu_seconds = known ? it->second + p.cu_occupancy / ncu * dt : 0.0;
+            const double inc = known ? p.cu_occupancy / ncu * dt : 0.0;
+            p.cu_seconds = known ? it->second + inc : 0.0;
             next_cs.emplace_back(p.pid, p.cu_seconds);
+            // The pod's integral keeps what its processes ran after they exit: the
+            // per-pod compute share a shared GPU is billed by.
+            if (pid_pods) {
+              auto po = pid_pods->find((static_cast<uint64_t>(static_cast<uint32_t>(dev)) << 32) | p.pid);
+              if (po != pid_pods->end()) {
+                double& v = pods[po->second];
+                if (inc > 0 || v == 0) pods_changed = true;
+                v += inc;
+              }
+            }
           }
           std::sort(next_cs.begin(), next_cs.end());
           cs.swap(next_cs);  // processes that exited drop out
           last = now_p;
           auto sp = std::make_shared<const std::vector<ProcInfo>>(procs);
+          std::shared_ptr<const std::map<std::string, double>> pc;
+          if (pods_changed) pc = std::make_shared<const std::map<std::string, double>>(pods);
           {
             std::lock_guard<std::mutex> g(st.slow_mu);
             st.procs = std::move(sp);
             st.procs_mono_ns = now_p;
+            if (pc) st.pod_cu = std::move(pc);
           }
           st.proc_reads.fetch_add(1, std::memory_order_relaxed);
         } else {
@@ -533,13 +782,17 @@ void Sampler::run_slow() {
         if (stop_.load(std::memory_order_relaxed)) break;
         DeviceState& st = *states_[static_cast<size_t>(dev)];
         const int64_t a = mono_ns();
-        if (be_->read_links(dev, links) == 0) {
+        const int lrc = be->read_links(dev, links);
+        if (gone()) return;
+        if (lrc == 0) {
           auto l = std::make_shared<const std::vector<LinkInfo>>(links);
           std::lock_guard<std::mutex> g(st.slow_mu);
           st.links = std::move(l);
         }
         HealthInfo h;
-        if (be_->read_health(dev, h) == 0) {
+        const int hrc = be->read_health(dev, h);
+        if (gone()) return;
+        if (hrc == 0) {
           auto hp = std::make_shared<const HealthInfo>(h);
           std::lock_guard<std::mutex> g(st.slow_mu);
           st.health = std::move(hp);

@@ -20,6 +20,14 @@
 //  5. PMFW table parser fuzz (ASAN build): random, truncated and mutated
 //     v1.8-shaped buffers, each in an exactly-sized heap block so any read past
 //     `len` is caught; the parser must reject or parse, never overrun.
+//  8. AQL queue-slot reservation (aql_ring.h) against a fake queue whose read
+//     index never advances: a bounded error, never a spin; abort cuts it short.
+//  9. Counter-tier fault boundary: one GPU whose counter reads take 1 s, one whose
+//     reads stop returning at all; the same GPUs keep their PMFW tier, the others
+//     their counter rate, a per-GPU release does not wait for the hung one, and
+//     stop() abandons the stuck thread within its deadline.
+// 10. Circuit breaker: reads that time out open it (kgs_pmc_failed), a reset +
+//     re-acquire after the backoff closes it, and the totals stay monotonic.
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
@@ -37,6 +45,7 @@
 #include <cstring>
 #include <random>
 
+#include "kgs/aql_ring.h"
 #include "kgs/backend.h"
 #include "kgs/exporter.h"
 #include "kgs/gpu_metrics.h"
@@ -203,7 +212,7 @@ static void test_sampler() {
           s.window_busy(d, 0.05, g, u, n);
           s.window_pmc(d, 0.05, r);
           Integrals I;
-          s.state(d).integ.load(I);
+          I = s.state(d).integrals();
           auto p = s.state(d).get_procs();
           auto l = s.state(d).get_links();
           (void)p;
@@ -216,8 +225,8 @@ static void test_sampler() {
   for (auto& t : rd) t.join();
   s.stop();
   Integrals I0, I3;
-  s.state(0).integ.load(I0);
-  s.state(3).integ.load(I3);
+  I0 = s.state(0).integrals();
+  I3 = s.state(3).integrals();
   CHECK(I0.distinct_samples > 50);
   CHECK(I0.read_errors > 0);             // 10 % injected failures
   CHECK(s.state(0).up.load() == 1);
@@ -255,7 +264,7 @@ static void test_recovery() {
         int n;
         s.window_busy(d, 0.05, g, u, n);
         Integrals I;
-        s.state(d).integ.load(I);
+        I = s.state(d).integrals();
       }
   });
   std::this_thread::sleep_for(std::chrono::milliseconds(500));
@@ -263,7 +272,7 @@ static void test_recovery() {
   rd.join();
   s.stop();
   Integrals I1;
-  s.state(1).integ.load(I1);
+  I1 = s.state(1).integrals();
   CHECK(I1.recoveries == 1);
   CHECK(s.state(1).up.load() == 1);
   CHECK(I1.energy_joules > 0);
@@ -520,7 +529,164 @@ static void test_http_server() {
               static_cast<unsigned long long>(ex.http_closed_idle.load()));
 }
 
+static int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+static void test_reserve_slot() {
+  // A 64-slot queue the CP stopped consuming: read index stuck at 10, 64 packets in flight.
+  std::atomic<uint64_t> rd{10}, wr{74};
+  auto read_idx = [&] { return rd.load(); };
+  auto write_idx = [&] { return wr.load(); };
+  auto commit = [&](uint64_t i) { wr.store(i + 1); };
+  auto pause = [] { std::this_thread::yield(); };
+  uint64_t idx = 0;
+  int64_t t0 = now_ns();
+  SlotResult r = reserve_slot(64, t0 + 50000000, nullptr, read_idx, write_idx, commit, now_ns, pause, idx);
+  int64_t el = now_ns() - t0;
+  CHECK(r == SlotResult::kTimeout);
+  CHECK(el >= 50000000 && el < 500000000);  // at the deadline, not forever
+  CHECK(wr.load() == 74);                   // nothing reserved: no hole for the CP to stall on
+  std::atomic<int> abort{0};
+  std::thread aborter([&] {
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    abort.store(1);
+  });
+  t0 = now_ns();
+  r = reserve_slot(64, t0 + 5000000000LL, &abort, read_idx, write_idx, commit, now_ns, pause, idx);
+  el = now_ns() - t0;
+  aborter.join();
+  CHECK(r == SlotResult::kAborted && el < 1000000000);
+  CHECK(wr.load() == 74);
+  // The CP drains one packet: the next reservation gets slot 74 at once.
+  rd.store(11);
+  r = reserve_slot(64, now_ns() + 1000000, nullptr, read_idx, write_idx, commit, now_ns, pause, idx);
+  CHECK(r == SlotResult::kOk && idx == 74 && wr.load() == 75);
+  std::printf("reserve_slot ok (timeout %.1f ms)\n", 50.0);
+}
+
+static void test_pmc_fault_boundary() {
+  ExporterConfig c;
+  c.backend = "mock";
+  c.mock.n_gpus = 8;
+  c.mock.fw_period_s = 0.020;  // PMFW table cadence (≈50 distinct tables/s)
+  c.sampler.hz = 1000;
+  c.sampler.pmfw_hz = 100;
+  c.sampler.pin_numa = false;
+  c.sampler.proc_every = 0;
+  c.sampler.link_every = 0;
+  c.sampler.pmc_idle_hz = 0;
+  c.sampler.stop_timeout_s = 1.0;
+  c.pmc_source = "mock";
+  c.mock_pmc.slow_dev = 2;  // every counter read on GPU 2 takes 1 s
+  c.mock_pmc.slow_s = 1.0;
+  c.mock_pmc.hang_dev = 5;  // GPU 5's reads stop returning after 200
+  c.mock_pmc.hang_after = 200;
+  c.mock_pmc.hang_timeout_s = -1;
+  c.port = -1;
+  // Never deleted: the abandoned thread may outlive the test.  A global keeps it
+  // reachable, so the ASAN build's leak checker does not count it.
+  static Exporter* ex = nullptr;
+  ex = new Exporter(c);
+  CHECK(ex->init());
+  ex->start();
+  std::this_thread::sleep_for(std::chrono::milliseconds(500));
+  std::vector<Integrals> a(8), b(8);
+  for (int d = 0; d < 8; ++d) a[d] = ex->sampler()->state(d).integrals();
+  const int64_t t0 = now_ns();
+  std::this_thread::sleep_for(std::chrono::milliseconds(1500));
+  for (int d = 0; d < 8; ++d) b[d] = ex->sampler()->state(d).integrals();
+  const double secs = (now_ns() - t0) * 1e-9;
+  for (int d = 0; d < 8; ++d) {
+    const double pmfw = (b[d].distinct_samples - a[d].distinct_samples) / secs;
+    const double pmc = (b[d].pmc_samples - a[d].pmc_samples) / secs;
+    CHECK(pmfw >= 45);  // PMFW tier untouched on every GPU, the slow and the hung one included
+    if (d != 2 && d != 5) CHECK(pmc >= 0.98 * 1000 * (1 - 0.05));  // 5 % slack for TSAN scheduling
+  }
+  // Per-GPU hand-over: releasing the hung GPU returns at once, and every other GPU
+  // releases within a few of its own ticks.
+  int64_t r0 = now_ns();
+  ex->set_pmc_enabled(false, 5);
+  ex->set_pmc_enabled(false, 3);
+  CHECK(now_ns() - r0 < 10000000);
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  CHECK(ex->sampler()->state(3).pmc_on.load() == 0);
+  CHECK(ex->sampler()->state(5).pmc_on.load() == 1);  // its thread is stuck: nothing happened, nobody waited
+  ex->set_pmc_enabled(true, 3);
+  r0 = now_ns();
+  ex->stop();
+  const double stop_s = (now_ns() - r0) * 1e-9;
+  CHECK(stop_s < 2.0);
+  CHECK(ex->sampler()->abandoned_threads() == 1);
+  CHECK(ex->sampler()->state(5).thread_hung.load() == 1);
+  std::string out;
+  ex->render(out);
+  CHECK(out.find("kgs_sampler_thread_hung{gpu=\"5\"") != std::string::npos);
+  // Restart: every tier comes back except the stuck (GPU 5, counter) one.
+  ex->start();
+  std::this_thread::sleep_for(std::chrono::milliseconds(300));
+  const Integrals c5 = ex->sampler()->state(5).integrals();
+  std::this_thread::sleep_for(std::chrono::milliseconds(300));
+  CHECK(ex->sampler()->state(5).integrals().distinct_samples > c5.distinct_samples);
+  ex->stop();
+  std::printf("pmc fault boundary ok (stop %.3f s)\n", stop_s);
+}
+
+static void test_pmc_breaker() {
+  ExporterConfig c;
+  c.backend = "mock";
+  c.mock.n_gpus = 2;
+  c.mock.fw_period_s = 0.005;
+  c.sampler.hz = 1000;
+  c.sampler.pin_numa = false;
+  c.sampler.proc_every = 0;
+  c.sampler.link_every = 0;
+  c.sampler.pmc_idle_hz = 0;
+  c.sampler.pmc_breaker_k = 3;
+  c.sampler.pmc_retry_s = 0.1;
+  c.pmc_source = "mock";
+  c.mock_pmc.hang_dev = 1;      // after 100 reads, GPU 1's reads time out (50 ms each) ...
+  c.mock_pmc.hang_after = 100;
+  c.mock_pmc.hang_timeout_s = 0.05;
+  c.mock_pmc.hang_heals_on_reset = true;  // ... until the breaker resets its queue
+  c.port = -1;
+  Exporter ex(c);
+  CHECK(ex.init());
+  ex.start();
+  bool saw_failed = false;
+  std::string out;
+  for (int i = 0; i < 60 && !saw_failed; ++i) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    if (ex.sampler()->state(1).pmc_failed.load()) {
+      saw_failed = true;
+      ex.render(out);
+      CHECK(out.find("kgs_pmc_failed{gpu=\"1\",uuid=") != std::string::npos);
+    }
+  }
+  CHECK(saw_failed);
+  const Integrals f = ex.sampler()->state(1).integrals();
+  std::this_thread::sleep_for(std::chrono::milliseconds(600));  // retry after 0.1 s: reset heals, READs resume
+  const Integrals g = ex.sampler()->state(1).integrals();
+  ex.stop();
+  const DeviceState& st = ex.sampler()->state(1);
+  CHECK(st.pmc_failed.load() == 0);
+  CHECK(st.pmc_breaker_trips.load() == 1);
+  CHECK(st.pmc_retries.load() >= 1);
+  CHECK(ex.counters()->resets(1) >= 1);
+  CHECK(g.pmc_samples > f.pmc_samples + 200);
+  CHECK(f.pmc_errors >= 3);
+  CHECK(ex.sampler()->state(0).pmc_breaker_trips.load() == 0);
+  PmcSample p;
+  CHECK(st.pmc_latest.load(p) && p.value[kPmcGrbmCount] > 0);
+  std::printf("pmc breaker ok (%llu errors, %llu retries)\n", static_cast<unsigned long long>(g.pmc_errors),
+              static_cast<unsigned long long>(st.pmc_retries.load()));
+}
+
 int main() {
+  test_reserve_slot();
+  test_pmc_breaker();
+  test_pmc_fault_boundary();
   test_http_server();
   test_exporter_concurrent();
   test_parser_fuzz();

@@ -14,7 +14,15 @@ Reference: gpu_util_stats/gpu_util_stats.py.
 ``--compat`` issues the reference's five PromQL queries verbatim (M1-M5, in the
 order M1 → M2 → M3 → M4 → M5) and reproduces its arithmetic and
 output exactly, quirks included (Q1 overwrite, Q2 divide-by-range, Q5 first
-sample, Q6 string counts, Q7 finished pods dropped, Q8 JSON dump on stdout).
+sample, Q6 string counts, Q7 finished pods dropped, Q8 JSON dump on stdout), and
+the reference's cross-namespace join: only the live-pod filter is namespaced
+(:133), the request and util series are not (:137, :159), so two pods of one name
+in two namespaces merge.
+
+The default mode joins on (namespace, pod) throughout — the util series grouped
+``by (kubernetes_io_hostname, nvidia_gpu_type, namespace, pod_name)``, requests
+``by (node, namespace, pod)``, live pods ``by (namespace, pod)`` — and reports a
+Namespace column; its ``--namespace`` defaults to every namespace.
 The default mode keeps the join semantics but fixes the quirks: exact per-step
 means (Q4) from the exporter's per-pod counter
 ``100 * avg(rate(container_gpu_busy_seconds_total[step])) by (...)`` — the
@@ -80,17 +88,17 @@ class Queries:
             used=(f'sum(max(kube_pod_container_resource_requests{{resource="{resource}",node!=""}} '
                   f'* on (namespace, pod) group_left() max(kube_pod_status_phase{{phase="Running"}}) '
                   f"by (namespace, pod)) by (node, namespace, pod)) by (node) > 0"),
-            live=f'max(kube_pod_status_phase{{{ns}phase=~"Running|Pending"}}) by (pod) > 0',
-            req=f'max(kube_pod_container_resource_requests{{resource="{resource}"}}) by (node, pod)',
+            live=f'max(kube_pod_status_phase{{{ns}phase=~"Running|Pending"}}) by (namespace, pod) > 0',
+            req=f'max(kube_pod_container_resource_requests{{resource="{resource}"}}) by (node, namespace, pod)',
             type_label=type_label,
         )
 
 
 def util_query(metric: str, step_s: int) -> str:
-    """Per-(node, type, pod) utilisation percent per step.  A ``*_seconds_total``
-    counter (busy seconds since allocation) gives the exact mean over each step,
-    ``100 * rate``; a gauge can only be averaged at the scrapes."""
-    by = "by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)"
+    """Per-(node, type, namespace, pod) utilisation percent per step.  A
+    ``*_seconds_total`` counter (busy seconds since allocation) gives the exact mean
+    over each step, ``100 * rate``; a gauge can only be averaged at the scrapes."""
+    by = "by (kubernetes_io_hostname, nvidia_gpu_type, namespace, pod_name)"
     if metric.endswith("_seconds_total"):
         return f"100 * avg(rate({metric}[{step_s}s])) {by}"
     return f"avg(avg_over_time({metric}[{step_s}s])) {by}"
@@ -117,10 +125,14 @@ def get_gpu_servers(c: PromClient, q: Queries, compat: bool) -> dict[str, tuple]
 
 
 def get_pod_by_servers(c: PromClient, q: Queries, start, end, step_s: int, compat: bool,
-                       out=sys.stdout) -> dict[str, dict[str, object]]:
-    """{node: {pod: cards}} for live pods — reference get_pod_by_servers :129-151 (M4, M5)."""
+                       out=sys.stdout) -> dict[str, dict]:
+    """Live pods' cards per node — reference get_pod_by_servers :129-151 (M4, M5).
+    compat: {node: {pod: cards}}, joined on pod name only (:143-145); fixed:
+    {node: {(namespace, pod): cards}}."""
     # M4 is the reference's query_prom_instant, which sends no proxy (:32, Q9)
-    live = {m["metric"]["pod"] for m in result(c.query(q.live, proxied=not compat))}
+    live_rows = result(c.query(q.live, proxied=not compat))
+    live = ({m["metric"]["pod"] for m in live_rows} if compat
+            else {(m["metric"].get("namespace", ""), m["metric"]["pod"]) for m in live_rows})
     res = {}
     for m in result(c.query_range(q.req, start, end, step_s)):
         node = m["metric"].get("node", "<unknown>")
@@ -129,40 +141,67 @@ def get_pod_by_servers(c: PromClient, q: Queries, start, end, step_s: int, compa
             continue
         if compat:
             val = m["values"][0][1]  # first sample, string (Q5, Q6)
+            key = pod
         else:
             val = int(max(float(v[1]) for v in m["values"]))
-        if pod not in live:
+            key = (m["metric"].get("namespace", ""), pod)
+        if key not in live:
             continue
-        res.setdefault(node, {})[pod] = val
+        res.setdefault(node, {})[key] = val
     if compat:
         print(json.dumps(res, indent=2), file=out)  # :150 (Q8)
     else:
-        L.debug("live GPU pods: %s", json.dumps(res))
+        L.debug("live GPU pods: %s", {n: {"/".join(k): v for k, v in p.items()} for n, p in res.items()})
     return res
 
 
 # --------------------------------------------------------------------------- aggregation (L3)
+# Pod rows: compat [node, pod, cards, util] (the reference's, :92); fixed
+# [node, namespace, pod, cards, util, *extras].
+F_NODE, F_NS, F_POD, F_CARDS, F_UTIL, F_EXTRA = range(6)
+
+
+def _series_key(metric: dict, allocated: dict) -> tuple[str, str]:
+    """(namespace, pod) of a util series.  A series without a namespace label (an
+    exporter that predates it) joins the node's one allocation of that pod name,
+    when there is exactly one."""
+    pod = metric.get("pod_name", "")
+    ns = metric.get("namespace")
+    if ns is not None and ns != "":
+        return ns, pod
+    same = [k for k in allocated if k[1] == pod]
+    return same[0] if len(same) == 1 else ("", pod)
+
+
 def stats_pod_results(util_body: dict, servers: dict, server_pods: dict, compat: bool,
                       show_finished: bool = False) -> list[list]:
-    """Reference stats_pod_results :62-94 (F3)."""
-    vals: dict[str, dict[str, float]] = {}
+    """Reference stats_pod_results :62-94 (F3).  compat joins util and allocations on
+    the pod name (the reference's cross-namespace merge); fixed on (namespace, pod)."""
+    vals: dict[str, dict] = {}
     for res in result(util_body):
         server = res["metric"].get("kubernetes_io_hostname", "")
-        pod = res["metric"].get("pod_name", "")
+        key = (res["metric"].get("pod_name", "") if compat
+               else _series_key(res["metric"], server_pods.get(server, {})))
         v = [float(x[1]) for x in res.get("values", [])]
-        vals.setdefault(server, {})[pod] = sum(v) / len(v) if v else 0.0
+        vals.setdefault(server, {})[key] = sum(v) / len(v) if v else 0.0
     lines = []
     for server in sorted(servers):
         if server not in server_pods and server not in vals:
             continue
         pods = set(server_pods.get(server, {})) | set(vals.get(server, {}))
-        for pod in sorted(pods):  # the reference iterates a set (unspecified order); sorted is stable
-            cards = server_pods.get(server, {}).get(pod)
-            if cards is None:  # finished pod with util but no allocation (:87-90, Q7)
-                if show_finished and not compat:
-                    lines.append([server, pod + " (finished)", 0, vals.get(server, {}).get(pod, 0.0)])
+        for key in sorted(pods):  # the reference iterates a set (unspecified order); sorted is stable
+            cards = server_pods.get(server, {}).get(key)
+            u = vals.get(server, {}).get(key, 0.0)
+            if compat:
+                if cards is not None:  # finished pod with util but no allocation dropped (:87-90, Q7)
+                    lines.append([server, key, cards, u])
                 continue
-            lines.append([server, pod, cards, vals.get(server, {}).get(pod, 0.0)])
+            ns, pod = key
+            if cards is None:
+                if show_finished:
+                    lines.append([server, ns, pod + " (finished)", 0, u])
+                continue
+            lines.append([server, ns, pod, cards, u])
     return lines
 
 
@@ -183,8 +222,8 @@ def stats_server_results(util_body: dict, servers: dict, time_range_s: float, st
     per_node: dict[str, dict[float, list[tuple[float, float]]]] = {}
     for res in result(util_body):
         node = res["metric"].get("kubernetes_io_hostname", "")
-        pod = res["metric"].get("pod_name", "")
-        w = float((weights or {}).get(node, {}).get(pod, 1) or 1)
+        alloc = (weights or {}).get(node, {})
+        w = float(alloc.get(_series_key(res["metric"], alloc), 1) or 1)
         for ts, v in res.get("values", []):
             per_node.setdefault(node, {}).setdefault(float(ts), []).append((float(v), w))
     n_steps = max(1, int(round(time_range_s / step_s)))
@@ -219,75 +258,64 @@ def run_report(c: PromClient, q: Queries, end: datetime | float, window_s: float
 
 
 def idle_gpu_hours(rows: list[list], window_s: float) -> list[list]:
-    """Pod rows + the GPU-hours each pod held but left idle over the window:
-    cards × hours × (1 − util/100) — the waste figure an accounting report is for."""
+    """Pod rows (fixed layout) + the GPU-hours each pod held but left idle over the
+    window: cards × hours × (1 − util/100) — the waste figure an accounting report is for."""
     h = window_s / 3600.0
-    return [[*r, float(r[2]) * h * (1.0 - min(100.0, max(0.0, r[3])) / 100.0)] for r in rows]
+    return [[*r, float(r[F_CARDS]) * h * (1.0 - min(100.0, max(0.0, r[F_UTIL])) / 100.0)] for r in rows]
 
 
 ENERGY_METRIC = "container_gpu_energy_joules_total"
 
 
 def energy_query(step_s: int, metric: str = ENERGY_METRIC) -> str:
-    """Joules per (node, pod) per step: the exporter's per-pod energy counter (socket
-    energy of the pod's GPUs since allocation), summed over the pod's GPUs."""
-    return f"sum(increase({metric}[{step_s}s])) by (kubernetes_io_hostname, pod_name)"
+    """Joules per (node, namespace, pod) per step: the exporter's per-pod energy
+    counter (socket energy of the pod's GPUs since allocation), summed over its GPUs."""
+    return f"sum(increase({metric}[{step_s}s])) by (kubernetes_io_hostname, namespace, pod_name)"
 
 
-def pod_energy_kwh(c: PromClient, start, end, step_s: int) -> dict[tuple[str, str], float]:
-    """{(node, pod): kWh} over (start, end].  The range query's first point covers the
-    step *before* ``start``, so it is left out: the kept points tile the window."""
+def pod_energy_kwh(c: PromClient, start, end, step_s: int) -> dict[tuple[str, str, str], float]:
+    """{(node, namespace, pod): kWh} over (start, end].  The range query's first point
+    covers the step *before* ``start``, so it is left out: the kept points tile the window."""
     t0 = to_unix(start)  # the start the range query is evaluated from (whole seconds)
-    out: dict[tuple[str, str], float] = {}
+    out: dict[tuple[str, str, str], float] = {}
     for r in result(c.query_range(energy_query(step_s), start, end, step_s)):
-        key = (r["metric"].get("kubernetes_io_hostname", ""), r["metric"].get("pod_name", ""))
+        m = r["metric"]
+        key = (m.get("kubernetes_io_hostname", ""), m.get("namespace", ""), m.get("pod_name", ""))
         j = sum(float(v) for ts, v in r.get("values", []) if float(ts) > t0 + 0.5)
         out[key] = out.get(key, 0.0) + j / 3.6e6
     return out
 
 
-def add_energy(rows: list[list], kwh: dict[tuple[str, str], float]) -> list[list]:
-    """Pod rows + the kWh their GPUs drew over the window (0 for a pod with no series)."""
-    return [[*r, kwh.get((r[0], str(r[1]).removesuffix(" (finished)")), 0.0)] for r in rows]
-
-
-POD_NS_QUERY = "max(kube_pod_status_phase) by (namespace, pod)"  # kube-state-metrics, any phase
-
-
-def pod_namespaces(c: PromClient, start, end, step_s: int) -> dict[str, str]:
-    """pod → namespace over the window (kube-state-metrics; pods that finished in it too)."""
-    out: dict[str, str] = {}
-    for r in result(c.query_range(POD_NS_QUERY, start, end, step_s)):
-        m = r["metric"]
-        if m.get("pod"):
-            out.setdefault(m["pod"], m.get("namespace", ""))
-    return out
+def add_energy(rows: list[list], kwh: dict[tuple[str, str, str], float]) -> list[list]:
+    """Pod rows (fixed layout) + the kWh their GPUs drew over the window (0 for a pod with no series)."""
+    return [[*r, kwh.get((r[F_NODE], r[F_NS], str(r[F_POD]).removesuffix(" (finished)")), 0.0)] for r in rows]
 
 
 NS_HEADER = ["Namespace", "Pods", "GPUs", "GPU-h", "Busy GPU-h", "Util %", "Idle GPU-h"]
 
 
-def by_namespace(rows: list[list], pod_ns: dict[str, str], window_s: float,
+def by_namespace(rows: list[list], window_s: float,
                  extras: list[str] | None = None) -> tuple[list[str], list[list]]:
-    """Roll pod rows ([node, pod, cards, util %, *extras]) up per namespace — the
-    team-level view of the same accounting: GPU-hours held (cards × window, as the
-    pod report assumes), busy GPU-hours (× util), their ratio, the idle rest, and
-    the extras' totals (e.g. Energy kWh; "Idle GPU-h" is a column already).  Sorted
-    by GPU-hours held, with a total."""
+    """Roll pod rows ([node, namespace, pod, cards, util %, *extras]) up per
+    namespace — the team-level view of the same accounting: GPU-hours held (cards ×
+    window, as the pod report assumes), busy GPU-hours (× util), their ratio, the
+    idle rest, and the extras' totals (e.g. Energy kWh; "Idle GPU-h" is a column
+    already).  Sorted by GPU-hours held, with a total."""
     extras = list(extras or [])
     keep = [k for k, e in enumerate(extras) if e != "Idle GPU-h"]
     h = window_s / 3600.0
     agg: dict[str, dict] = {}
     for r in rows:
-        node, pod, cards, util = r[0], str(r[1]).removesuffix(" (finished)"), float(r[2]), float(r[3])
-        a = agg.setdefault(pod_ns.get(pod, "<unknown>"),
+        node, ns, pod = r[F_NODE], r[F_NS], str(r[F_POD]).removesuffix(" (finished)")
+        cards, util = float(r[F_CARDS]), float(r[F_UTIL])
+        a = agg.setdefault(ns or "<unknown>",
                            {"pods": set(), "gpus": 0.0, "gpu_h": 0.0, "busy_h": 0.0, "extra": [0.0] * len(keep)})
-        a["pods"].add((node, pod))
+        a["pods"].add((node, ns, pod))
         a["gpus"] += cards
         a["gpu_h"] += cards * h
         a["busy_h"] += cards * h * min(100.0, max(0.0, util)) / 100.0
         for j, k in enumerate(keep):
-            a["extra"][j] += float(r[4 + k])
+            a["extra"][j] += float(r[F_EXTRA + k])
     header = NS_HEADER + [extras[k] for k in keep]
     out = []
     for ns, a in sorted(agg.items(), key=lambda kv: (-kv[1]["gpu_h"], kv[0])):
@@ -316,16 +344,18 @@ def format_rows(rows: list[list], mode: str, fmt: str, compat: bool, idle_hours:
     extras = list(extras or [])
     if idle_hours and "Idle GPU-h" not in extras:
         extras.insert(0, "Idle GPU-h")
-    header = ["Node", "Pod", "GPUs", "Util %"] if mode == "pod" else ["Node", "GPU Type", "Util %", "Used", "Total"]
-    if mode == "pod" and extras:
+    header = (["Node", "Namespace", "Pod", "GPUs", "Util %"] if mode == "pod"
+              else ["Node", "GPU Type", "Util %", "Used", "Total"])
+    if mode == "pod":
         header = header + extras
         n = len(extras)
-        disp = [[r[0], r[1], r[2], f"{r[3]:.2f}", *(f"{x:.2f}" for x in r[4:4 + n])] for r in rows]
-        if rows:
-            disp.append(["TOTAL", "", sum(int(r[2]) for r in rows), "",
-                         *(f"{sum(r[4 + k] for r in rows):.2f}" for k in range(n))])
+        disp = [[r[F_NODE], r[F_NS], r[F_POD], r[F_CARDS], f"{r[F_UTIL]:.2f}",
+                 *(f"{x:.2f}" for x in r[F_EXTRA:F_EXTRA + n])] for r in rows]
+        if rows and extras:
+            disp.append(["TOTAL", "", "", sum(int(r[F_CARDS]) for r in rows), "",
+                         *(f"{sum(r[F_EXTRA + k] for r in rows):.2f}" for k in range(n))])
     else:
-        disp = [[*r[:-1], f"{r[-1]:.2f}"] if mode == "pod" else [r[0], r[1], f"{r[2]:.2f}", r[3], r[4]] for r in rows]
+        disp = [[r[0], r[1], f"{r[2]:.2f}", r[3], r[4]] for r in rows]
     if fmt == "json":
         return json.dumps([dict(zip(header, r)) for r in rows], indent=2)
     if fmt == "csv":
@@ -340,7 +370,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "proxy", "", f"HTTP proxy for every call (reference used {REF_PROXY})")
     add_flag(ap, "timeout", REF_TIMEOUT_S, "per-request timeout seconds")
     add_flag(ap, "retries", 0, "retries per request")
-    add_flag(ap, "namespace", REF_NAMESPACE, "namespace of the live-pod filter ('' = all)")
+    add_flag(ap, "namespace", "", f"namespace of the live-pod filter ('' = all; --compat: {REF_NAMESPACE!r}, the "
+                                  "reference's)")
     add_flag(ap, "window", float(REF_WINDOW_S), "report window seconds (reference: 1 day)")
     add_flag(ap, "step", REF_STEP_S, "query_range step seconds (reference: 3600)")
     add_flag(ap, "end", 0.0, "window end as unix seconds (default now)")
@@ -364,6 +395,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
 
 def run(a) -> int:
     c = PromClient(a.prom_url, a.proxy, a.timeout, a.retries)
+    if a.compat and not a.namespace:
+        a.namespace = REF_NAMESPACE  # gpu_util_stats.py:133
     q = (Queries.compat(a.namespace) if a.compat else
          Queries.amd(a.namespace, a.step, a.resource, a.type_label, a.util_metric))
     end = a.end if a.end else (datetime.now() if a.compat else time.time())
@@ -378,8 +411,7 @@ def run(a) -> int:
             rows = add_energy(rows, pod_energy_kwh(c, e - a.window, e, a.step))
             extras.append("Energy kWh")
         if a.group_by == "namespace":
-            e = end if isinstance(end, (int, float)) else end.timestamp()
-            header, ns_rows = by_namespace(rows, pod_namespaces(c, e - a.window, e, a.step), a.window, extras)
+            header, ns_rows = by_namespace(rows, a.window, extras)
             print(format_namespace_rows(header, ns_rows, a.format))
             return 0
     elif a.group_by != "pod":

@@ -64,14 +64,15 @@ def test_bursty_pod_counter_report_is_exact_gauge_misses(mock_exporter):
         for q in (q_cnt, q_gauge):
             fp.add_instant(q.total, [{"metric": {"node": "node-a", q.type_label: "MI355X"}, "value": [end, "8"]}])
             fp.add_instant(q.used, [{"metric": {"node": "node-a"}, "value": [end, "1"]}])
-            fp.add_instant(q.live, [{"metric": {"pod": "bursty"}, "value": [end, "1"]}])
-            fp.add_range(q.req, [{"metric": {"node": "node-a", "pod": "bursty"}, "values": [[end, "1"]]}])
+            fp.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": "bursty"}, "value": [end, "1"]}])
+            fp.add_range(q.req, [{"metric": {"node": "node-a", "namespace": "ml", "pod": "bursty"},
+                                  "values": [[end, "1"]]}])
         exact = 100.0 * DUTY
         rows = G.run_report(PromClient(url), q_cnt, end_f, window, step, compat=False)
-        assert [r[:3] for r in rows] == [["node-a", "bursty", 1]]
-        assert rows[0][3] == pytest.approx(exact, rel=0.01), rows
+        assert [r[:4] for r in rows] == [["node-a", "ml", "bursty", 1]]
+        assert rows[0][4] == pytest.approx(exact, rel=0.01), rows
         gauge = G.run_report(PromClient(url), q_gauge, end_f, window, step, compat=False)
-        assert abs(gauge[0][3] - exact) > 10, gauge  # the gauge only saw idle windows
+        assert abs(gauge[0][4] - exact) > 10, gauge  # the gauge only saw idle windows
     finally:
         fp.stop()
 
@@ -151,7 +152,7 @@ def test_report_energy_column_tiles_the_window(mock_exporter):
             stamps.append(ts)
         end, window, step = stamps[-1], 3, 1
         kwh = G.pod_energy_kwh(PromClient(url), end - window, end, step)
-        assert list(kwh) == [("node-a", "two")]
+        assert list(kwh) == [("node-a", "ml", "two")]
 
         def joules_at(t):  # both GPUs' counters, linear between scrapes
             tot = 0.0
@@ -166,11 +167,117 @@ def test_report_energy_column_tiles_the_window(mock_exporter):
         e_int = float(int(end))
         want = joules_at(e_int) - joules_at(e_int - window)
         gaps = [round(b - a, 3) for a, b in zip(stamps, stamps[1:])]
-        assert want > 0 and kwh[("node-a", "two")] * 3.6e6 == pytest.approx(want, rel=0.05), \
-            {"got_j": kwh[("node-a", "two")] * 3.6e6, "want_j": want, "end": end, "scrape_gaps_s": gaps}
-        rows = G.add_energy([["node-a", "two", 2, 60.0], ["node-a", "gone (finished)", 0, 0.0]], kwh)
-        assert rows[0][4] == kwh[("node-a", "two")] and rows[1][4] == 0.0
+        assert want > 0 and kwh[("node-a", "ml", "two")] * 3.6e6 == pytest.approx(want, rel=0.05), \
+            {"got_j": kwh[("node-a", "ml", "two")] * 3.6e6, "want_j": want, "end": end, "scrape_gaps_s": gaps}
+        rows = G.add_energy([["node-a", "ml", "two", 2, 60.0], ["node-a", "ml", "gone (finished)", 0, 0.0]], kwh)
+        assert rows[0][5] == kwh[("node-a", "ml", "two")] and rows[1][5] == 0.0
         table = G.format_rows(rows, "pod", "table", compat=False, extras=["Energy kWh"])
         assert "Energy kWh" in table and "TOTAL" in table
     finally:
         fp.stop()
+
+
+def test_shared_gpu_pods_billed_by_own_compute_share(mock_exporter):
+    """two pods share GPU 0; their processes hold 60 % and 0 % of its CUs.
+    container_gpu_busy_seconds_total bills each the whole GPU's busy time;
+    container_gpu_cu_seconds_total bills each its own processes' CU-occupancy share
+    (reference per-pod accounting: gpu_util_stats.py:62-94)."""
+    ex = mock_exporter(n_gpus=1, hz=100, proc_period_s=0.05, link_every=0,
+                       mock={"util_base": 70, "util_amp": 1e-4, "fw_period_s": 0.005, "proc_cu_share": [0.6, 0.0]})
+    ex.set_device_owners(0, [{"pod": "big", "namespace": "ml", "container": "c"},
+                             {"pod": "idle", "namespace": "dev", "container": "c"}])
+    # mock PIDs 100000 + 10·gpu + k: process 0 → big, process 1 → idle
+    ex.set_pid_owners({(0, 100000): {"pod": "big", "namespace": "ml", "container": "c"},
+                       (0, 100001): {"pod": "idle", "namespace": "dev", "container": "c"}})
+    time.sleep(0.3)
+
+    def per_pod(m, fam):
+        return {lb["pod_name"]: v for lb, v in m[fam]}
+
+    m0, t0 = parse_text(ex.render()), time.time()
+    time.sleep(1.5)
+    m1, dt = parse_text(ex.render()), time.time() - t0
+    cu = {p: 100 * (per_pod(m1, "container_gpu_cu_seconds_total")[p] - per_pod(m0, "container_gpu_cu_seconds_total")[p]) / dt
+          for p in ("big", "idle")}
+    busy = {p: 100 * (per_pod(m1, "container_gpu_busy_seconds_total")[p] -
+                      per_pod(m0, "container_gpu_busy_seconds_total")[p]) / dt for p in ("big", "idle")}
+    assert cu["big"] == pytest.approx(60, abs=4) and cu["idle"] == pytest.approx(0, abs=0.5), cu
+    assert busy["big"] == pytest.approx(70, abs=4) and busy["idle"] == pytest.approx(70, abs=4), busy  # whole GPU each
+    # The pod's integral keeps its exited processes' share: drop the PID table entry
+    # (process gone) and the counter holds its value.
+    before = per_pod(parse_text(ex.render()), "container_gpu_cu_seconds_total")["big"]
+    ex.set_pid_owners({})
+    time.sleep(0.3)
+    after = per_pod(parse_text(ex.render()), "container_gpu_cu_seconds_total")["big"]
+    assert after >= before > 0.5
+
+
+def test_report_util_metric_cu_seconds_splits_a_shared_gpu(mock_exporter):
+    """`gpu-util-stats --util-metric container_gpu_cu_seconds_total`: per-pod util from
+    the pods' own compute share on a shared GPU (60 / 0) instead of 70 / 70."""
+    ex = mock_exporter(n_gpus=1, hz=100, proc_period_s=0.05, link_every=0, node_name="node-a",
+                       mock={"util_base": 70, "util_amp": 1e-4, "fw_period_s": 0.005, "proc_cu_share": [0.6, 0.0]})
+    owners = [{"pod": "big", "namespace": "ml", "container": "c"}, {"pod": "idle", "namespace": "dev", "container": "c"}]
+    ex.set_device_owners(0, owners)
+    ex.set_pid_owners({(0, 100000): owners[0], (0, 100001): owners[1]})
+    sc = Scraper("127.0.0.1", ex.port)
+    fp = FakeProm()
+    url = fp.start()
+    try:
+        time.sleep(0.2)
+        stamps = []
+        t0 = time.time()
+        for k in range(14):
+            time.sleep(max(0.0, t0 + 0.25 * k - time.time()))
+            ts = time.time()
+            fp.ingest(parse_text(sc.get()), ts)
+            stamps.append(ts)
+        end = stamps[-1]
+        for metric, want in (("container_gpu_cu_seconds_total", {"big": 60, "idle": 0}),
+                             ("container_gpu_busy_seconds_total", {"big": 70, "idle": 70})):
+            q = G.Queries.amd("", 1, util_metric=metric)
+            fp.add_instant(q.total, [{"metric": {"node": "node-a", q.type_label: "MI355X"}, "value": [end, "1"]}])
+            fp.add_instant(q.used, [{"metric": {"node": "node-a"}, "value": [end, "1"]}])
+            fp.add_instant(q.live, [{"metric": {"namespace": o["namespace"], "pod": o["pod"]}, "value": [end, "1"]}
+                                    for o in owners])
+            fp.add_range(q.req, [{"metric": {"node": "node-a", "namespace": o["namespace"], "pod": o["pod"]},
+                                  "values": [[end, "1"]]} for o in owners])
+            rows = G.run_report(PromClient(url), q, end, 2, 1, compat=False)
+            got = {r[2]: r[4] for r in rows}
+            assert got["big"] == pytest.approx(want["big"], abs=5) and got["idle"] == pytest.approx(want["idle"], abs=5), \
+                (metric, rows)
+    finally:
+        fp.stop()
+
+
+def test_partitions_split_socket_energy(N):
+    """compute partitions read one socket energy accumulator.  Each partition
+    is billed its XCCs' share of the chip's GFX busy, so the partitions' energy adds up
+    to the socket's instead of counting it once per partition."""
+    cfg = {"backend": "mock", "hz": 200, "port": -1, "pin_numa": False, "proc_every": 0, "link_every": 0,
+           "mock": {"n_gpus": 1, "compute_partition": "CPX", "fw_period_s": 0.005, "util_base": 50, "util_amp": 40,
+                    "util_period_s": 0.5}}
+    cpx = N.Exporter(cfg)
+    cpx.start()
+    try:
+        time.sleep(0.3)
+        e0 = [cpx.integrals(d)["energy_joules"] for d in range(8)]
+        b0 = [cpx.integrals(d)["gfx_busy_seconds"] for d in range(8)]
+        time.sleep(1.2)
+        e1 = [cpx.integrals(d)["energy_joules"] for d in range(8)]
+        b1 = [cpx.integrals(d)["gfx_busy_seconds"] for d in range(8)]
+        parts = [b - a for a, b in zip(e0, e1)]
+        # the socket draws 200 W + 8 W per % of chip busy ≈ 600 W here: 1.2 s ≈ 720 J in total
+        assert 500 < sum(parts) < 950, parts
+        socket_w = sum(parts) / 1.2
+        chip = cpx.snapshot(0)
+        assert socket_w == pytest.approx(chip["power_w"], rel=0.35)
+        # each partition's share follows its XCC's busy share (the mock's XCC curves differ in phase)
+        busy = [b - a for a, b in zip(b0, b1)]
+        share_e = [p / sum(parts) for p in parts]
+        share_b = [x / sum(busy) for x in busy]
+        for se, sb in zip(share_e, share_b):
+            assert se == pytest.approx(sb, abs=0.03)
+        assert max(parts) < 0.5 * sum(parts)  # no partition is billed the whole socket
+    finally:
+        cpx.stop()

@@ -147,12 +147,13 @@ def test_end_to_end_exporter_to_report(mock_exporter, tmp_path):
         q = G.Queries.amd("ml", 10, util_metric="container_gpu_sm_util")  # gauge path; counters: test_accounting
         fp.add_instant(q.total, [{"metric": {"node": "node-a", q.type_label: "MI355X"}, "value": [t0, "8"]}])
         fp.add_instant(q.used, [{"metric": {"node": "node-a"}, "value": [t0, "2"]}])
-        fp.add_instant(q.live, [{"metric": {"pod": "train-0"}, "value": [t0, "1"]}])
-        fp.add_range(q.req, [{"metric": {"node": "node-a", "pod": "train-0"}, "values": [[t0, "2"]]}])
+        fp.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": "train-0"}, "value": [t0, "1"]}])
+        fp.add_range(q.req, [{"metric": {"node": "node-a", "namespace": "ml", "pod": "train-0"},
+                              "values": [[t0, "2"]]}])
         rows = G.run_report(PromClient(url), q, t0 + 50, 50, 10, compat=False)
         assert len(rows) == 1
-        node, pod, cards, util = rows[0]
-        assert (node, pod, cards) == ("node-a", "train-0", 2)
+        node, ns, pod, cards, util = rows[0]
+        assert (node, ns, pod, cards) == ("node-a", "ml", "train-0", 2)
         assert util == pytest.approx(60.0, abs=1.0)
         # the reference's own M1 query shape works unchanged against the exporter's series
         body = fp.eval_instant(G.REF_Q_UTIL, t0 + 50)
@@ -189,13 +190,16 @@ def test_multi_node_exporters_to_reports(mock_exporter):
                                      for n in ("node-a", "node-b")])
             fp.add_instant(q.used, [{"metric": {"node": "node-a"}, "value": [t0, "2"]},
                                     {"metric": {"node": "node-b"}, "value": [t0, "1"]}])
-            fp.add_instant(q.live, [{"metric": {"pod": p}, "value": [t0, "1"]} for p in ("train-0", "infer-1")])
-            fp.add_range(q.req, [{"metric": {"node": "node-a", "pod": "train-0"}, "values": [[t0, "2"]]},
-                                 {"metric": {"node": "node-b", "pod": "infer-1"}, "values": [[t0, "1"]]}])
+            fp.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": p}, "value": [t0, "1"]}
+                                    for p in ("train-0", "infer-1")])
+            fp.add_range(q.req, [{"metric": {"node": "node-a", "namespace": "ml", "pod": "train-0"},
+                                  "values": [[t0, "2"]]},
+                                 {"metric": {"node": "node-b", "namespace": "ml", "pod": "infer-1"},
+                                  "values": [[t0, "1"]]}])
             rows = sorted(G.run_report(PromClient(url), q, t0 + 50, 50, 10, compat=False))
             want = (60.0, 30.0)  # mock: GFX busy 60 / 30 %, MFMA busy 60 / 30 % of active cycles
-            assert [r[:3] for r in rows] == [["node-a", "train-0", 2], ["node-b", "infer-1", 1]], rows
-            assert rows[0][3] == pytest.approx(want[0], abs=2) and rows[1][3] == pytest.approx(want[1], abs=2), rows
+            assert [r[:4] for r in rows] == [["node-a", "ml", "train-0", 2], ["node-b", "ml", "infer-1", 1]], rows
+            assert rows[0][4] == pytest.approx(want[0], abs=2) and rows[1][4] == pytest.approx(want[1], abs=2), rows
             if metric == "container_gpu_sm_util":
                 nodes = G.run_report(PromClient(url), q, t0 + 50, 50, 10, compat=False, mode="node")
                 assert [(r[0], r[1], r[3], r[4]) for r in nodes] == [("node-a", "MI355X", 2, 8),

@@ -696,7 +696,8 @@ def test_metric_allow_deny_filters_families(mock_exporter):
     assert all(f.startswith(("amdgpu_", "kgs_sample_read", "kgs_attribution")) for f in dropped), dropped
     assert "container_gpu_sm_util" in fams["deny"] and "amdgpu_topology_link" in fams["deny"]
     assert fams["allow"] == {"container_gpu_sm_util", "container_gpu_busy_seconds", "container_gpu_energy_joules",
-                             "amdgpu_gfx_busy_percent", "kgs_up", "kgs_attribution_updates"}, fams["allow"]
+                             "container_gpu_cu_seconds", "amdgpu_gfx_busy_percent", "kgs_up",
+                             "kgs_attribution_updates"}, fams["allow"]
     assert len(fams["deny"]) < len(fams["full"])
 
 

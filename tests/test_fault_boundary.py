@@ -1,0 +1,230 @@
+"""Fault boundary of the counter tier on the mock provider.
+
+The reference bounds every external call with ``timeout=5``
+(/root/reference/gpu_util_stats/gpu_util_stats.py:24,32,107,119).  The exporter's
+hot path talks to the GPU's command processor; these tests drive a mock
+CounterSource that (i) takes 1 s per sample or (ii) stops returning at all, and
+check that the same GPU keeps its PMFW tier, the other GPUs keep their counter
+rate, a per-GPU hand-over never waits for the hung GPU, and stop() returns in
+bounded time.  The circuit breaker (kgs_pmc_failed) opens on consecutive failures
+and closes after a reset + re-acquire.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+
+import pytest
+
+from kube_gpu_stats_amd.utils.scrape import parse_text
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HZ = 1000
+
+
+def rates(ex, gpus, secs):
+    a = [ex.integrals(g) for g in gpus]
+    t0 = time.time()
+    time.sleep(secs)
+    b = [ex.integrals(g) for g in gpus]
+    dt = time.time() - t0
+    return ({g: (y["distinct_samples"] - x["distinct_samples"]) / dt for g, x, y in zip(gpus, a, b)},
+            {g: (y["pmc_samples"] - x["pmc_samples"]) / dt for g, x, y in zip(gpus, a, b)})
+
+
+def fault_exporter(mock_exporter, **mock_pmc):
+    # 20 ms PMFW cadence = 50 distinct tables/s at most; counters at 1 kHz.
+    return mock_exporter(n_gpus=8, hz=HZ, pmfw_hz=100, pmc_source="mock", proc_every=0, link_every=0,
+                         pmc_idle_hz=0, mock={"fw_period_s": 0.02}, mock_pmc=mock_pmc)
+
+
+def test_slow_counter_reads_do_not_silence_the_gpu_or_its_neighbours(mock_exporter):
+    ex = fault_exporter(mock_exporter, slow_dev=2, slow_s=1.0)
+    time.sleep(0.4)
+    pmfw, pmc = rates(ex, list(range(8)), 1.5)
+    assert pmfw[2] >= 45, pmfw                      # the slow GPU keeps power / temp / util
+    assert 0 < pmc[2] <= 2, pmc                     # ... while its counter reads crawl
+    for g in range(8):
+        assert pmfw[g] >= 45, pmfw
+        if g != 2:
+            assert pmc[g] >= 0.98 * HZ, pmc
+    m = parse_text(ex.render())
+    busy = {lb["gpu"]: v for lb, v in m["amdgpu_gfx_busy_percent"]}
+    assert "2" in busy                              # window gauges still fresh on the slow GPU
+    t0 = time.time()
+    ex.stop()                                       # cancel() ends the 1 s read at once
+    assert time.time() - t0 < 2.0
+    assert ex.abandoned_threads == 0
+
+
+def test_hung_counter_reads_are_isolated_and_stop_is_bounded(mock_exporter):
+    # After 100 reads GPU 5's counter reads never return, cancel or not (a call
+    # stuck in the driver): only abandoning its thread helps.
+    ex = fault_exporter(mock_exporter, hang_dev=5, hang_after=100, hang_timeout_s=-1)
+    time.sleep(0.5)
+    pmfw, pmc = rates(ex, list(range(8)), 1.5)
+    assert pmfw[5] >= 45, pmfw
+    assert pmc[5] == 0, pmc
+    for g in range(8):
+        if g != 5:
+            assert pmc[g] >= 0.98 * HZ, pmc
+    # Per-GPU hand-over: releasing the hung GPU returns at once; another GPU's
+    # release takes effect on that GPU's own next tick.
+    t0 = time.time()
+    ex.set_pmc_enabled(False, gpu=5)
+    ex.set_pmc_enabled(False, gpu=3)
+    assert time.time() - t0 < 0.05
+    time.sleep(0.1)
+    assert ex.integrals(3)["pmc_on"] == 0 and ex.integrals(3)["pmc_releases"] == 1
+    assert ex.integrals(5)["pmc_on"] == 1                    # its thread is stuck; nobody waited on it
+    assert all(ex.integrals(g)["pmc_on"] == 1 for g in (0, 1, 2, 4, 6, 7))
+    ex.set_pmc_enabled(True, gpu=3)
+    t0 = time.time()
+    ex.stop()
+    assert time.time() - t0 < 2.0
+    assert ex.abandoned_threads == 1
+    m = parse_text(ex.render())
+    hung = {lb["gpu"]: v for lb, v in m["kgs_sampler_thread_hung"]}
+    assert hung["5"] == 1 and sum(hung.values()) == 1
+    # Restart: every tier returns but the stuck one.
+    ex.start()
+    time.sleep(0.4)
+    pmfw, pmc = rates(ex, [3, 5], 0.5)
+    assert pmfw[5] >= 40 and pmc[5] == 0 and pmc[3] >= 0.9 * HZ
+
+
+def test_breaker_opens_on_timeouts_and_closes_after_reset(mock_exporter):
+    ex = mock_exporter(n_gpus=2, hz=HZ, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0,
+                       pmc_breaker_k=3, pmc_retry_s=0.2, mock={"fw_period_s": 0.005, "util_base": 50, "util_amp": 1e-4},
+                       mock_pmc={"hang_dev": 1, "hang_after": 200, "hang_timeout_s": 0.05, "hang_heals_on_reset": True})
+    failed_seen = False
+    t0 = time.time()
+    while time.time() - t0 < 2 and not failed_seen:
+        m = parse_text(ex.render())
+        failed = {lb["gpu"]: v for lb, v in m["kgs_pmc_failed"]}
+        failed_seen = failed["1"] == 1
+        time.sleep(0.01)
+    assert failed_seen and failed["0"] == 0
+    assert "1" not in {lb["gpu"] for lb, _ in m.get("amdgpu_mfma_util_percent", [])}  # no rate gauge while open
+    grbm0 = [v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT" and lb["gpu"] == "1"][0]
+    time.sleep(0.8)
+    m = parse_text(ex.render())
+    assert {lb["gpu"]: v for lb, v in m["kgs_pmc_failed"]} == {"0": 0, "1": 0}
+    assert {lb["gpu"]: v for lb, v in m["kgs_pmc_breaker_trips_total"]}["1"] == 1
+    assert {lb["gpu"]: v for lb, v in m["kgs_pmc_retries_total"]}["1"] >= 1
+    grbm1 = [v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT" and lb["gpu"] == "1"][0]
+    assert grbm1 > grbm0                                     # totals continue across the reset
+    i = ex.integrals(1)
+    assert i["pmc_failed"] == 0 and i["pmc_resets"] >= 1 and i["pmc_errors"] >= 3
+    assert ex.window(1, 0.2)["mfma_util_pct"] == pytest.approx(60, abs=5)
+
+
+def test_breaker_retries_back_off_exponentially(mock_exporter):
+    # Reads time out and re-acquire keeps failing: retries at 0.1, 0.2, 0.4, 0.8 s ...
+    ex = mock_exporter(n_gpus=1, hz=HZ, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0,
+                       pmc_breaker_k=2, pmc_retry_s=0.1, pmc_retry_max_s=0.4,
+                       mock_pmc={"hang_dev": 0, "hang_after": 50, "hang_timeout_s": 0.02, "acquire_fail_dev": 0})
+    time.sleep(2.0)
+    i = ex.integrals(0)
+    assert i["pmc_failed"] == 1 and i["pmc_breaker_trips"] == 1
+    # first trip ≈0.1 s in; retries at +0.1, +0.3, +0.7, +1.1, +1.5 (capped at 0.4 s)
+    assert 4 <= i["pmc_retries"] <= 6, i
+    assert i["reads"] > 0 and i["distinct_samples"] > 20      # PMFW tier unaffected throughout
+
+
+def test_control_endpoints_reject_out_of_range_rates(mock_exporter):
+    ex = mock_exporter(n_gpus=2, hz=200, pmc_source="mock", control_http=True)
+    base = f"http://127.0.0.1:{ex.port}"
+
+    def code(path):
+        try:
+            return urllib.request.urlopen(base + path, timeout=5).status
+        except urllib.error.HTTPError as e:
+            return e.code
+
+    assert code("/control/rate?hz=0") == 400
+    assert code("/control/rate?hz=1e9") == 400
+    assert code("/control/rate?hz=-5") == 400
+    assert code("/control/pmc/idle?hz=1e-12") == 400
+    assert code("/control/pmc/idle?hz=1e9") == 400
+    assert code("/control/pmc/release?gpu=99") == 400
+    assert ex.sample_rate == 200 and ex.pmc_idle_hz == 100
+    assert code("/control/rate?hz=400") == 200 and ex.sample_rate == 400
+    assert code("/control/pmc/idle?hz=0") == 200 and ex.pmc_idle_hz == 0
+    assert code("/control/pmc/idle?hz=0.5") == 200 and ex.pmc_idle_hz == 0.5
+    assert code("/control/rate") == 200                         # no hz: read only
+    body = json.loads(urllib.request.urlopen(base + "/control/pmc/release?gpu=1", timeout=5).read())
+    assert body == {"gpu": 1, "pmc": False}
+    time.sleep(0.1)
+    assert ex.integrals(1)["pmc_on"] == 0 and ex.integrals(0)["pmc_on"] == 1
+    with pytest.raises(ValueError):
+        ex.set_sample_rate(0)
+    with pytest.raises(ValueError):
+        ex.pmc_idle_hz = 1e-9
+
+
+def test_set_hz_concurrent_with_pause_resume(mock_exporter):
+    """set_hz, pause and resume from different threads are serialised."""
+    import threading
+
+    ex = mock_exporter(n_gpus=2, hz=500, pmc_source="mock", proc_every=3, link_every=5)
+    stop = threading.Event()
+
+    def flip():
+        while not stop.is_set():
+            ex.pause()
+            ex.resume()
+
+    th = threading.Thread(target=flip)
+    th.start()
+    for k in range(30):
+        ex.set_sample_rate(300 + 10 * k)
+        parse_text(ex.render())
+    stop.set()
+    th.join()
+    ex.resume()
+    time.sleep(0.2)
+    assert ex.sampling and ex.sample_rate == 590
+    n = ex.integrals(0)["pmc_samples"]
+    time.sleep(0.2)
+    assert ex.integrals(0)["pmc_samples"] > n
+
+
+def test_counter_integrals_count_start_to_first_read(mock_exporter):
+    """after every re-START the interval from START to the first READ is
+    counted (the counts restart at 0 at START), so periodic refreshes lose no time."""
+    ex = mock_exporter(n_gpus=1, hz=50, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0,
+                       pmc_refresh_s=0.1, mock={"util_base": 50, "util_amp": 1e-4})
+    time.sleep(0.3)
+    a, t0 = ex.integrals(0), time.time()
+    time.sleep(1.5)
+    b, dt = ex.integrals(0), time.time() - t0
+    # ≈15 refreshes at 50 Hz: dropping START → first READ (20 ms each) would lose ≈20 %
+    assert (b["active_seconds"] - a["active_seconds"]) / dt == pytest.approx(0.5, rel=0.04)
+    assert (b["mfma_busy_seconds"] - a["mfma_busy_seconds"]) / dt == pytest.approx(0.5 * 0.6, rel=0.05)
+
+
+def test_kgs_pmc_release_one_gpu_via_cli():
+    p = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--backend", "mock",
+                          "--mock-gpus", "4", "--pmc", "mock", "--hz", "200", "--listen", "127.0.0.1:0",
+                          "--control-stdin", "--no-pin-numa"], cwd=REPO, stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        port = json.loads(p.stdout.readline())["port"]
+        out = subprocess.run([sys.executable, "-m", "kube_gpu_stats_amd.cli", "pmc", "release", "--gpu", "2",
+                              "--exporter", f"127.0.0.1:{port}"], cwd=REPO, capture_output=True, text=True, timeout=60)
+        assert json.loads(out.stdout) == {"gpu": 2, "pmc": False}
+        time.sleep(0.2)
+        st = subprocess.run([sys.executable, "-m", "kube_gpu_stats_amd.cli", "pmc", "status",
+                             "--exporter", f"127.0.0.1:{port}"], cwd=REPO, capture_output=True, text=True, timeout=60)
+        en = {ln.split('gpu="')[1].split('"')[0]: float(ln.rsplit(" ", 1)[1])
+              for ln in st.stdout.splitlines() if ln.startswith("kgs_pmc_enabled")}
+        assert en == {"0": 1.0, "1": 1.0, "2": 0.0, "3": 1.0}
+    finally:
+        p.stdin.write("quit\n")
+        p.stdin.flush()
+        out, _ = p.communicate(timeout=30)
+    assert json.loads(out.strip().splitlines()[-1])["abandoned_threads"] == 0

@@ -71,30 +71,32 @@ def test_node_report_compat_golden(prom):
 
 def test_node_report_fixed_mode_fixes_q1_q2():
     util = {"data": {"result": [
-        {"metric": {"kubernetes_io_hostname": "n", "pod_name": "a"}, "values": [[0, "50"], [3600, "50"]]},
-        {"metric": {"kubernetes_io_hostname": "n", "pod_name": "b"}, "values": [[0, "90"], [3600, "90"]]},
+        {"metric": {"kubernetes_io_hostname": "n", "namespace": "ml", "pod_name": "a"}, "values": [[0, "50"], [3600, "50"]]},
+        {"metric": {"kubernetes_io_hostname": "n", "namespace": "ml", "pod_name": "b"}, "values": [[0, "90"], [3600, "90"]]},
     ]}}
     servers = {"n": (8, 6, "MI355X")}
     # card-weighted: a holds 6 cards, b holds 2 → (6*50 + 2*90)/8 = 60
-    rows = G.stats_server_results(util, servers, 7200, 3600, compat=False, weights={"n": {"a": 6, "b": 2}})
+    rows = G.stats_server_results(util, servers, 7200, 3600, compat=False,
+                                  weights={"n": {("ml", "a"): 6, ("ml", "b"): 2}})
     assert rows == [["n", "MI355X", 60.0, 6, 8]]
     rows = G.stats_server_results(util, servers, 4 * 3600, 3600, compat=False, missing="zero",
-                                  weights={"n": {"a": 1, "b": 1}})
+                                  weights={"n": {("ml", "a"): 1, ("ml", "b"): 1}})
     assert rows[0][2] == pytest.approx(70.0 * 2 / 4)
 
 
 def test_pod_report_fixed_mode_ints_and_max_cards(prom):
     fp, url = prom
     q = G.Queries.amd("ml", STEP)
-    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "pod_name": "p"},
+    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "namespace": "ml", "pod_name": "p"},
                            "values": [[T_END - 3600, "40"], [T_END, "60"]]}])
     fp.add_instant(q.total, [{"metric": {"node": "n1", q.type_label: "MI355X"}, "value": [T_END, "8"]}])
     fp.add_instant(q.used, [{"metric": {"node": "n1"}, "value": [T_END, "4"]}])
-    fp.add_instant(q.live, [{"metric": {"pod": "p"}, "value": [T_END, "1"]}])
-    fp.add_range(q.req, [{"metric": {"node": "n1", "pod": "p"}, "values": [[T_END - 3600, "2"], [T_END, "4"]]}])
+    fp.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": "p"}, "value": [T_END, "1"]}])
+    fp.add_range(q.req, [{"metric": {"node": "n1", "namespace": "ml", "pod": "p"},
+                          "values": [[T_END - 3600, "2"], [T_END, "4"]]}])
     out = io.StringIO()
     rows = G.run_report(PromClient(url), q, T_END, 7200, STEP, compat=False, out=out)
-    assert rows == [["n1", "p", 4, 50.0]]
+    assert rows == [["n1", "ml", "p", 4, 50.0]]
     assert out.getvalue() == ""  # no debug dump on stdout (Q8)
     table = G.format_rows(rows, "pod", "table", compat=False)
     assert "| n1   | p   |  4   | 50.00  |" in table or "50.00" in table
@@ -105,7 +107,8 @@ def test_amd_queries_mention_amd_resource():
     q = G.Queries.amd("ml", 3600)
     assert 'resource="amd_com_gpu"' in q.total and 'resource="amd_com_gpu"' in q.req
     assert q.util == ("100 * avg(rate(container_gpu_busy_seconds_total[3600s])) "
-                      "by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)")
+                      "by (kubernetes_io_hostname, nvidia_gpu_type, namespace, pod_name)")
+    assert q.live.endswith("by (namespace, pod) > 0") and q.req.endswith("by (node, namespace, pod)")
     assert "avg_over_time(container_gpu_sm_util[3600s])" in G.Queries.amd("ml", 3600, util_metric="container_gpu_sm_util").util
     assert 'namespace="ml"' in q.live
     assert 'namespace=' not in G.Queries.amd("", 60).live
@@ -169,8 +172,9 @@ def test_table_matches_prettytable_centering():
 
 def test_idle_gpu_hours_column_and_total():
     """--idle-hours: cards × window hours × (1 − util) per pod, plus a total row."""
-    rows = G.idle_gpu_hours([["n1", "a", 4, 25.0], ["n1", "b", 2, 100.0], ["n2", "c", 1, 0.0]], 86400)
-    assert [r[4] for r in rows] == [72.0, 0.0, 24.0]
+    rows = G.idle_gpu_hours([["n1", "ml", "a", 4, 25.0], ["n1", "ml", "b", 2, 100.0], ["n2", "dev", "c", 1, 0.0]],
+                            86400)
+    assert [r[5] for r in rows] == [72.0, 0.0, 24.0]
     table = G.format_rows(rows, "pod", "table", compat=False, idle_hours=True)
     assert "Idle GPU-h" in table and "TOTAL" in table and "96.00" in table
     js = json.loads(G.format_rows(rows, "pod", "json", False, idle_hours=True))
@@ -204,13 +208,12 @@ def test_api_pod_list_follows_continue_tokens():
 
 def test_util_report_rolls_up_per_namespace():
     """gpu-util-stats --group-by namespace: GPU-hours held / busy / idle and util per
-    namespace from the pod rows (+ extras' totals), namespaces from kube-state-metrics."""
+    namespace from the pod rows' own Namespace column (+ extras' totals)."""
     from kube_gpu_stats_amd.reports import gpu_util_stats as G
 
-    rows = [["n1", "a", 4, 50.0, 1.5], ["n1", "b", 2, 100.0, 0.5], ["n2", "c", 8, 25.0, 2.0],
-            ["n2", "d (finished)", 1, 10.0, 0.1]]
-    pod_ns = {"a": "ml", "b": "ml", "c": "vision", "d": "vision"}
-    header, out = G.by_namespace(rows, pod_ns, 86400, ["Energy kWh"])
+    rows = [["n1", "ml", "a", 4, 50.0, 1.5], ["n1", "ml", "b", 2, 100.0, 0.5], ["n2", "vision", "c", 8, 25.0, 2.0],
+            ["n2", "vision", "d (finished)", 1, 10.0, 0.1]]
+    header, out = G.by_namespace(rows, 86400, ["Energy kWh"])
     assert header == G.NS_HEADER + ["Energy kWh"]
     by = {r[0]: r for r in out}
     # vision: 9 cards × 24 h = 216 GPU-h; busy 8·24·0.25 + 1·24·0.10 = 50.4
@@ -225,44 +228,82 @@ def test_util_report_rolls_up_per_namespace():
     text = G.format_namespace_rows(header, out, "table")
     assert "vision" in text and "TOTAL" in text
     # idle-hours as an extra is not double counted (it is a column already)
-    h2, _ = G.by_namespace([r[:4] + [0.0, r[4]] for r in rows], pod_ns, 86400, ["Idle GPU-h", "Energy kWh"])
+    h2, _ = G.by_namespace([r[:5] + [0.0, r[5]] for r in rows], 86400, ["Idle GPU-h", "Energy kWh"])
     assert h2 == G.NS_HEADER + ["Energy kWh"]
 
 
-def test_pod_namespaces_from_ksm_range_query():
-    from fakeprom import FakeProm
+def install_two_namespaces(fp, q):
+    """train-0 in namespaces a and b on one node: 2 and 4 cards, 30 % and 80 % util."""
+    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "nvidia_gpu_type": "MI355X", "namespace": ns,
+                                      "pod_name": "train-0"}, "values": [[T_END - 3600, u], [T_END, u]]}
+                          for ns, u in (("a", "30"), ("b", "80"))])
+    fp.add_instant(q.total, [{"metric": {"node": "n1", q.type_label: "MI355X"}, "value": [T_END, "8"]}])
+    fp.add_instant(q.used, [{"metric": {"node": "n1"}, "value": [T_END, "6"]}])
+    fp.add_instant(q.live, [{"metric": {"namespace": ns, "pod": "train-0"}, "value": [T_END, "1"]} for ns in "ab"])
+    fp.add_range(q.req, [{"metric": {"node": "n1", "namespace": ns, "pod": "train-0"}, "values": [[T_END, c]]}
+                         for ns, c in (("a", "2"), ("b", "4"))])
 
-    from kube_gpu_stats_amd.reports import gpu_util_stats as G
-    from kube_gpu_stats_amd.reports.promql import PromClient
 
-    fp = FakeProm()
-    fp.canned_range[G.POD_NS_QUERY] = [
-        {"metric": {"namespace": "ml", "pod": "a"}, "values": [[1, "1"]]},
-        {"metric": {"namespace": "vision", "pod": "c"}, "values": [[1, "1"]]}]
-    url = fp.start()
-    try:
-        assert G.pod_namespaces(PromClient(url), 0, 3600, 600) == {"a": "ml", "c": "vision"}
-    finally:
-        fp.stop()
+def test_fixed_mode_keeps_equal_pod_names_in_two_namespaces_apart(prom):
+    """VERDICT r2 #5 / SURVEY §2.6: the reference's live filter is namespaced but its
+    request and util series are not (gpu_util_stats.py:133 vs :137, :159), so two
+    train-0 pods merge.  The fixed mode joins on (namespace, pod)."""
+    fp, url = prom
+    q = G.Queries.amd("", STEP)
+    install_two_namespaces(fp, q)
+    rows = G.run_report(PromClient(url), q, T_END, 7200, STEP, compat=False)
+    assert rows == [["n1", "a", "train-0", 2, 30.0], ["n1", "b", "train-0", 4, 80.0]]
+    table = G.format_rows(rows, "pod", "table", compat=False)
+    assert "Namespace" in table.splitlines()[1] or "Namespace" in table
+    idle = G.idle_gpu_hours(rows, 7200)
+    assert [round(r[5], 6) for r in idle] == [2 * 2 * 0.7, 4 * 2 * 0.2]
+    header, ns_rows = G.by_namespace(idle, 7200, ["Idle GPU-h"])
+    assert {r[0]: r[2] for r in ns_rows} == {"a": 2.0, "b": 4.0, "TOTAL": 6.0}
+    # only namespace b
+    qb = G.Queries.amd("b", STEP)
+    assert 'namespace="b"' in qb.live
+
+
+def test_compat_mode_still_merges_across_namespaces(prom):
+    """--compat reproduces the reference's join on pod name: the two train-0 series
+    and requests collapse into one row (the collision SURVEY §2.6 names)."""
+    fp, url = prom
+    q = G.Queries.compat("a")
+    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "nvidia_gpu_type": "MI355X",
+                                      "pod_name": "train-0"}, "values": [[T_END - 3600, "55"], [T_END, "55"]]}])
+    fp.add_instant(q.total, [{"metric": {"node": "n1", "label_nvidia_gpu_type": "MI355X"}, "value": [T_END, "8"]}])
+    fp.add_instant(q.used, [{"metric": {"node": "n1"}, "value": [T_END, "6"]}])
+    fp.add_instant(q.live, [{"metric": {"pod": "train-0"}, "value": [T_END, "1"]}])
+    fp.add_range(q.req, [{"metric": {"node": "n1", "pod": "train-0"}, "values": [[T_END, "2"]]}])
+    rows = G.run_report(PromClient(url), q, datetime.fromtimestamp(T_END), 7200, STEP, compat=True,
+                        out=io.StringIO())
+    assert rows == [["n1", "train-0", "2", 55.0]]
+
+
+def test_cli_namespace_default_all_in_fixed_mode_ava_in_compat():
+    a = G.build_parser().parse_args([])
+    assert a.namespace == ""
+    ap = G.build_parser().parse_args(["--compat"])
+    assert ap.compat and ap.namespace == ""  # resolved to the reference's 'ava' in run()
 
 
 def test_cli_group_by_namespace_end_to_end(prom, capsys):
-    """`kgs gpu-util-stats --group-by namespace --format json` over the fake Prometheus."""
+    """`kgs gpu-util-stats --group-by namespace --format json` over the fake Prometheus.
+    The r series carries no namespace label (an older exporter): it joins the node's
+    only allocation named r."""
     fp, url = prom
     q = G.Queries.amd("", STEP)
-    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "pod_name": "p"},
+    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "namespace": "ml", "pod_name": "p"},
                            "values": [[T_END - 3600, "40"], [T_END, "60"]]},
                           {"metric": {"kubernetes_io_hostname": "n1", "pod_name": "r"},
                            "values": [[T_END - 3600, "100"], [T_END, "100"]]}])
     fp.add_instant(q.total, [{"metric": {"node": "n1", q.type_label: "MI355X"}, "value": [T_END, "8"]}])
     fp.add_instant(q.used, [{"metric": {"node": "n1"}, "value": [T_END, "6"]}])
-    fp.add_instant(q.live, [{"metric": {"pod": "p"}, "value": [T_END, "1"]},
-                            {"metric": {"pod": "r"}, "value": [T_END, "1"]}])
-    fp.add_range(q.req, [{"metric": {"node": "n1", "pod": "p"}, "values": [[T_END, "4"]]},
-                         {"metric": {"node": "n1", "pod": "r"}, "values": [[T_END, "2"]]}])
-    fp.add_range(G.POD_NS_QUERY, [{"metric": {"namespace": "ml", "pod": "p"}, "values": [[T_END, "1"]]},
-                                  {"metric": {"namespace": "infer", "pod": "r"}, "values": [[T_END, "1"]]}])
-    G.main(["--prom-url", url, "--namespace", "", "--window", "7200", "--step", str(STEP), "--end", str(T_END),
+    fp.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": "p"}, "value": [T_END, "1"]},
+                            {"metric": {"namespace": "infer", "pod": "r"}, "value": [T_END, "1"]}])
+    fp.add_range(q.req, [{"metric": {"node": "n1", "namespace": "ml", "pod": "p"}, "values": [[T_END, "4"]]},
+                         {"metric": {"node": "n1", "namespace": "infer", "pod": "r"}, "values": [[T_END, "2"]]}])
+    G.main(["--prom-url", url, "--window", "7200", "--step", str(STEP), "--end", str(T_END),
             "--group-by", "namespace", "--format", "json"])
     got = {r["Namespace"]: r for r in json.loads(capsys.readouterr().out)}
     assert got["ml"]["GPU-h"] == 8.0 and got["ml"]["Util %"] == 50.0 and got["ml"]["Idle GPU-h"] == 4.0

@@ -28,6 +28,16 @@ SETS = {
     "tcc_req": ["GRBM_COUNT", "GRBM_GUI_ACTIVE", "TCC:6", "TCC:21", "TCC:23", "TCC:45"],
     "sq": ["GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ:4", "SQ:26", "SQ:3", "SQ_VALU_MFMA_BUSY_CYCLES"],
     "tcp": ["GRBM_COUNT", "GRBM_GUI_ACTIVE", "TCP:68", "TCP:69", "TA_TA_BUSY"],
+    # Round 3: is there a device-wide "command processor is the bottleneck" signal?
+    # CPC_ADC_DISPATCH_ALLOC_DONE (4) / CPC_TG_SEND (62) count dispatches and
+    # workgroups, which the exporter's own PM4 READs are not; the busy counters
+    # (CPC_CPC_STAT_BUSY 25, ME1 packet decode 13, CPF_CPF_STAT_BUSY 23, GRBM_CP*_BUSY)
+    # would also count the READs.  counter_defs.yaml, architectures: gfx950.
+    "cpc_dispatch": ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:4", "CPC:62"],
+    "cpc_busy": ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:25", "CPC:13", "CPF:23", "CPF:25"],
+    "cpc_gd": ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:61", "CPC:33"],
+    "grbm_cp": ["GRBM:3", "GRBM:30"],
+    "spi_csn": ["GRBM_COUNT", "GRBM_SPI_BUSY", "SPI:49", "SPI:52"],
 }
 
 
@@ -54,7 +64,7 @@ def child(names: list[str], secs: float) -> int:
     n = len(names)
     arr = (ctypes.c_char_p * n)(*[s.encode() for s in names])
     # GRBM is max-reduced, everything else summed (TA busy is a mean over CUs).
-    red = (ctypes.c_int * n)(*[1 if s.startswith("GRBM") else (2 if s == "TA_TA_BUSY" else 0) for s in names])
+    red = (ctypes.c_int * n)(*[1 if s.startswith("GRBM_") else (2 if s == "TA_TA_BUSY" else 0) for s in names])
     gid = kfd_gpu_ids()[0]
     L.kgs_pmc_open.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p,
                                ctypes.c_int]
@@ -76,7 +86,7 @@ def child(names: list[str], secs: float) -> int:
     return 0
 
 
-def parent() -> int:
+def parent(sets: list[str]) -> int:
     import torch
 
     from kube_gpu_stats_amd.ops import load
@@ -87,15 +97,38 @@ def parent() -> int:
     ls()
     torch.cuda.synchronize()
     nflt = ls.a.numel()
+    # Dispatch-bound phases: a HIP graph of 500 tiny copies (≈575 k kernels/s, the
+    # bench's worst case) and the same copies launched eagerly (host-bound).
+    tsrc = torch.rand(16384, device="cuda")
+    tdst = torch.empty_like(tsrc)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        load.copy_f32(tsrc, tdst, nblocks=64, stream=s)
+        s.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(500):
+                load.copy_f32(tsrc, tdst, nblocks=64, stream=s)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+
+    def eager():
+        for _ in range(200):
+            load.copy_f32(tsrc, tdst, nblocks=64)
+
     phases_def = {
-        "idle": (lambda: time.sleep(0.05), 0.0, 0.0),
-        "mfma": (ls.run_mfma, 0.0, 0.0),
-        "triad": (lambda: load.triad_f32(ls.a, ls.b, ls.c, 1.5), 8.0 * nflt, 4.0 * nflt),
-        "copy": (lambda: load.copy_f32(ls.b, ls.a), 4.0 * nflt, 4.0 * nflt),
+        "idle": (lambda: time.sleep(0.05), 0.0, 0.0, 0),
+        "mfma": (ls.run_mfma, 0.0, 0.0, 1),
+        "triad": (lambda: load.triad_f32(ls.a, ls.b, ls.c, 1.5), 8.0 * nflt, 4.0 * nflt, 1),
+        "copy": (lambda: load.copy_f32(ls.b, ls.a), 4.0 * nflt, 4.0 * nflt, 1),
+        "tiny_graph": (g.replay, 0.0, 0.0, 500),
+        "tiny_eager": (eager, 0.0, 0.0, 200),
     }
     result = {}
-    for sname, names in SETS.items():
-        p = subprocess.Popen([sys.executable, __file__, "--child", json.dumps(names), "14"], stdout=subprocess.PIPE,
+    for sname in sets:
+        names = SETS[sname]
+        p = subprocess.Popen([sys.executable, __file__, "--child", json.dumps(names), "18"], stdout=subprocess.PIPE,
                              text=True, cwd=REPO)
         first = json.loads(p.stdout.readline())
         if "error" in first:
@@ -105,19 +138,20 @@ def parent() -> int:
             continue
         time.sleep(0.5)
         marks = {}
-        for ph, (fn, rd, wr) in phases_def.items():
+        for ph, (fn, rd, wr, kern) in phases_def.items():
             t0 = time.time()
             k = 0
             while time.time() - t0 < 2.0:
                 fn()
                 torch.cuda.synchronize()
                 k += 1
-            marks[ph] = (t0 + 0.2, time.time() - 0.2, k, rd * k / (time.time() - t0), wr * k / (time.time() - t0))
+            el = time.time() - t0
+            marks[ph] = (t0 + 0.2, time.time() - 0.2, k, rd * k / el, wr * k / el, kern * k / el)
         rows = [json.loads(line) for line in p.stdout]
         p.wait()
         rows = [r for r in rows if r.get("rc") == 0]
         res = {"info": first["info"], "read_us_mean": sum(r["read_us"] for r in rows) / max(1, len(rows))}
-        for ph, (a, b, k, rd_bps, wr_bps) in marks.items():
+        for ph, (a, b, k, rd_bps, wr_bps, kps) in marks.items():
             win = [r for r in rows if a <= r["t"] <= b]
             if len(win) < 2:
                 continue
@@ -125,14 +159,17 @@ def parent() -> int:
             rates = {names[i]: (win[-1]["v"][i] - win[0]["v"][i]) / dt for i in range(len(names))}
             rates["expected_read_Bps"] = rd_bps
             rates["expected_write_Bps"] = wr_bps
+            rates["kernels_per_s"] = kps
             res[ph] = rates
         result[sname] = res
         print(sname, json.dumps(res), flush=True)
-    json.dump(result, open(os.path.join(REPO, "gpurun_out", "aql_probe.json"), "w"), indent=1)
+    out = os.environ.get("KGS_AQL_PROBE_OUT", os.path.join(REPO, "gpurun_out", "aql_probe.json"))
+    json.dump(result, open(out, "w"), indent=1)
     return 0
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         sys.exit(child(json.loads(sys.argv[2]), float(sys.argv[3])))
-    sys.exit(parent())
+    # optional: comma-separated set names (default: every set)
+    sys.exit(parent(sys.argv[1].split(",") if len(sys.argv) > 1 else list(SETS)))
