@@ -110,6 +110,10 @@ def parse_args(argv=None):
     ap.add_argument("--train-seq", type=int, default=2048)
     ap.add_argument("--train-vocab", type=int, default=32768)
     ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per unit when N > 1 (0 = off)")
+    ap.add_argument("--xgmi-check-mib", type=int, default=2048,
+                    help="phase X (N > 1): bytes of each GPU 0 → GPU k peer copy that checks the link map and unit")
+    ap.add_argument("--xgmi-check-settle", type=float, default=0.5,
+                    help="phase X: seconds between a peer copy and the scrape that reads its link counters")
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--burst-s", type=float, default=0.6,
                     help="phase R: length of the MFMA burst train read back from /counters (0 = off; the "
@@ -189,10 +193,47 @@ class Load:
     """A step = ``reps`` back-to-back units (set by calibrate_reps)."""
 
     reps = 1
+    timing = False  # per-component event timing (interleaved blocks)
 
     def step(self):
         for _ in range(self.reps):
             self.unit()
+
+    def components_start(self) -> None:
+        self.timing = True
+
+    def components_end(self) -> dict:
+        """Seconds of GPU time per load component since components_start (synced)."""
+        self.timing = False
+        return {}
+
+
+class EventTimer:
+    """HIP events bracketing each load component inside a timed block: a component's
+    GPU time per block, so the paired overheads can be split by what the exporter
+    could slow down — a long MFMA kernel, HBM streams, or the dispatch-bound graph of
+    tiny kernels (VERDICT r2 weak #2).  Events are recorded in every condition alike."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.pool: list = []
+        self.used: list[tuple[str, int]] = []
+
+    def mark(self, name: str) -> None:
+        """Record the event that opens (or closes) ``name``; components alternate open/close."""
+        i = len(self.used)
+        if i >= len(self.pool):
+            self.pool.append(self.torch.cuda.Event(enable_timing=True))
+        self.pool[i].record()
+        self.used.append((name, i))
+
+    def collect(self) -> dict:
+        self.torch.cuda.synchronize()
+        out: dict[str, float] = {}
+        for (name, a), (_, b) in zip(self.used[0::2], self.used[1::2]):
+            out[name] = out.get(name, 0.0) + self.pool[a].elapsed_time(self.pool[b]) * 1e-3
+        self.used.clear()
+        return out
 
 
 class GpuLoad(Load):
@@ -229,18 +270,39 @@ class GpuLoad(Load):
         self.ar = None
         if ctx is not None and ctx.is_dist and a.xgmi_mib > 0:
             self.ar = torch.ones(int(a.xgmi_mib) << 18, dtype=torch.float32, device=torch.device("cuda", device))
+        self.ev = EventTimer(torch)
 
     def unit(self):
+        t = self.timing
+        if t:
+            self.ev.mark("mfma")
         self.ls.run_mfma()
+        if t:
+            self.ev.mark("mfma")
+            self.ev.mark("triad")
         for _ in range(self.triads):
             self.ls.run_stream()
+        if t:
+            self.ev.mark("triad")
         if self.graph is not None:
+            if t:
+                self.ev.mark("tiny_graph")
             self.graph.replay()
+            if t:
+                self.ev.mark("tiny_graph")
         if self.ar is not None:
             import torch.distributed as dist
 
+            if t:
+                self.ev.mark("allreduce")
             dist.all_reduce(self.ar)
             self.ar.mul_(0.5)  # keep values bounded across steps
+            if t:
+                self.ev.mark("allreduce")
+
+    def components_end(self) -> dict:
+        self.timing = False
+        return self.ev.collect()
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -344,14 +406,25 @@ class TrainLoad(GpuLoad):
         self.tok = torch.randint(0, self.vocab, (self.batch, self.seq + 1), device=dev, generator=g)
         self.F = F
 
+        self.ev = EventTimer(torch) if dev.type == "cuda" else None
+
     burst = None  # phase R runs on the synthetic load only
 
     def unit(self):
+        t = self.timing and self.ev is not None
+        if t:
+            self.ev.mark("train_step")
         logits = self.model(self.tok[:, :-1])
         loss = self.F.cross_entropy(logits.float().view(-1, self.vocab), self.tok[:, 1:].reshape(-1))
         loss.backward()
         self.opt.step()
         self.opt.zero_grad(set_to_none=True)
+        if t:
+            self.ev.mark("train_step")
+
+    def components_end(self) -> dict:
+        self.timing = False
+        return self.ev.collect() if self.ev is not None else {}
 
     def calibrate(self) -> dict:
         torch = self.torch
@@ -372,7 +445,18 @@ class MockLoad(Load):
         self.dt = a.mock_step_ms * 1e-3
 
     def unit(self):
+        t0 = time.perf_counter()
         time.sleep(self.dt)  # releases the GIL like a GPU sync would
+        if self.timing:
+            self.comp["mock"] = self.comp.get("mock", 0.0) + time.perf_counter() - t0
+
+    def components_start(self) -> None:
+        self.timing = True
+        self.comp: dict[str, float] = {}
+
+    def components_end(self) -> dict:
+        self.timing = False
+        return dict(self.comp)
 
     def burst(self, ms: float) -> None:
         time.sleep(ms * 1e-3)  # plumbing only: the mock counters do not follow the host
@@ -411,6 +495,9 @@ class AttachedExporter:
 
     def set_idle_hz(self, hz: float) -> float:
         return json.loads(self.sc.get(f"/control/pmc/idle?hz={hz:g}")).get("pmc_idle_hz", 0.0)
+
+    def json(self, path: str):
+        return json.loads(self.sc.get(path))
 
     def stop(self) -> dict:
         self.pause()
@@ -460,6 +547,9 @@ class ExporterProc:
 
     def set_idle_hz(self, hz: float) -> float:
         return json.loads(self.sc.get(f"/control/pmc/idle?hz={hz:g}")).get("pmc_idle_hz", 0.0)
+
+    def json(self, path: str):
+        return json.loads(self.sc.get(path))
 
     def _wait_ready(self, timeout: float) -> dict:
         end = time.time() + timeout
@@ -708,25 +798,92 @@ def pct(xs: list[float], q: float) -> float | None:
     return s[min(len(s) - 1, int(q * len(s)))]
 
 
+def timed_block(ctx, load, k: int) -> tuple[float, float]:
+    """One interleaved block: (this rank's own time to finish its k steps, the time
+    until every rank has — the MAX-over-ranks wall time the headline uses)."""
+    D.barrier(ctx)
+    load.sync()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        load.step()
+    load.sync()
+    own = time.perf_counter() - t0
+    D.barrier(ctx)
+    return own, time.perf_counter() - t0
+
+
+def order_design(conds: list[float], rounds: int) -> list[tuple]:
+    """Every permutation of the conditions in turn (3 conditions: all 6 orders), so
+    each condition sits in each block position equally often and a block-position
+    effect cannot pose as a sampling cost (VERDICT r2 weak #3)."""
+    import itertools
+
+    perms = list(itertools.permutations(conds))
+    return [perms[r % len(perms)] for r in range(rounds)]
+
+
+def position_adjusted(rows: list[dict], conds: list[float], orders: list[tuple]) -> dict:
+    """Least squares on log(block seconds) = round + condition + position effects;
+    the condition effects are the position-adjusted overheads (exp(b) − 1, with a
+    95 % interval from the residual variance)."""
+    import numpy as np
+
+    R, C = len(rows), len(conds)
+    P = C
+    y, X = [], []
+    for r, (row, order) in enumerate(zip(rows, orders)):
+        for pos, c in enumerate(order):
+            x = np.zeros(R + (C - 1) + (P - 1))
+            x[r] = 1.0
+            ci = conds.index(c)
+            if ci > 0:
+                x[R + ci - 1] = 1.0
+            if pos > 0:
+                x[R + C - 1 + pos - 1] = 1.0
+            X.append(x)
+            y.append(math.log(row[c]))
+    X, y = np.array(X), np.array(y)
+    beta, *_ = np.linalg.lstsq(X, y, rcond=None)
+    resid = y - X @ beta
+    dof = len(y) - np.linalg.matrix_rank(X)
+    out: dict = {"model": "log t = round + condition + position", "dof": int(dof)}
+    if dof <= 0:
+        return out
+    s2 = float(resid @ resid) / dof
+    cov = s2 * np.linalg.pinv(X.T @ X)
+    for ci in range(1, C):
+        k = R + ci - 1
+        b, se = float(beta[k]), math.sqrt(max(0.0, float(cov[k, k])))
+        out[f"{conds[ci]:g}"] = {"overhead_pct": 100 * (math.exp(b) - 1),
+                                 "overhead_ci95_pct": 100 * math.exp(b) * t975(dof) * se}
+    out["position_effect_pct"] = {str(p): 100 * (math.exp(float(beta[R + C - 1 + p - 1])) - 1) for p in range(1, P)}
+    return out
+
+
 def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
-    """Rounds of blocks: exporter paused (0) and sampling at each rate in ``hzs``,
-    order reversed every other round (0,100,8k | 8k,100,0 | ...).  Paused means the
-    sampler threads are stopped — no PMFW read, no counter READ, no scrape — while
-    the process and its counter session stay up, so the paired difference is the
-    cost of sampling + scraping (phase A/C vs B adds the cost of the process and
-    of holding the counters, ≈0 on MI355X; see ``overhead_abc_pct``)."""
+    """Rounds of blocks: exporter paused (0) and sampling at each rate in ``hzs``, the
+    block order cycling through every permutation of the conditions (order_design).
+    Paused means the sampler threads are stopped — no PMFW read, no counter READ, no
+    scrape — while the process and its counter session stay up, so the paired
+    difference is the cost of sampling + scraping (phase A/C vs B adds the cost of the
+    process and of holding the counters, ≈0 on MI355X; see ``overhead_abc_pct``).
+
+    Per block and rank: its own GPU-work time, the all-rank (MAX) time, the GPU time
+    of each load component (HIP events: MFMA kernel, triads, tiny-kernel graph,
+    all-reduce) and the block's power from the rank's own PMFW table.  The headline
+    overhead is the paired MAX-time ratio; per rank and per component the same pairing
+    on that rank's / component's own times."""
     if a.rounds <= 0:
         return {}
     conds = [0.0] + list(hzs)
-    rows: list[dict] = []
+    orders = order_design(conds, a.rounds)
     probe = None if a.mock else PmfwProbe(load.pci_bdf(ctx.local_rank))
-    pw: dict[float, list[dict]] = {c: [] for c in conds}  # per block: power / ppt of this rank's GPU
     rates = {h: Rates() for h in hzs}
     lat: dict[float, list[float]] = {h: [] for h in hzs}
     paused_reads = 0.0
-    for r in range(a.rounds):
-        order = conds if r % 2 == 0 else conds[::-1]
-        times = {}
+    local: list[dict] = []  # per round: {cond: {"own", "all", "comp", "power"}}
+    for order in orders:
+        blk: dict = {}
         for c in order:
             sc = None
             before: dict = {}
@@ -741,10 +898,10 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
                     sc = Scraper("127.0.0.1", exp.port).start(a.scrape_hz)
                 before, w0 = scrape_at(exp.sc)
             p0 = probe.read() if probe is not None else None
-            dt = timed(ctx, load, a.block_steps)
-            d = PmfwProbe.delta(p0, probe.read() if probe is not None else None)
-            if d:
-                pw[c].append(d)
+            load.components_start()
+            own, dt = timed_block(ctx, load, a.block_steps)
+            comp = load.components_end()
+            pw = PmfwProbe.delta(p0, probe.read() if probe is not None else None)
             if exp is not None:
                 if sc is not None:
                     sc.stop()
@@ -757,36 +914,85 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
                     rb = {lb["gpu"]: v for lb, v in before.get("kgs_reads_total", [])}
                     paused_reads += sum(v - rb.get(g, 0.0) for g, v in
                                         ((lb["gpu"], v) for lb, v in after.get("kgs_reads_total", [])))
-            times[c] = dt
-        rows.append(times)
+            blk[c] = {"own": own, "all": dt, "comp": comp, "power": pw}
+        local.append(blk)
     if exp is not None:
         exp.set_rate(a.hz)
         exp.resume()
-    out: dict = {"rounds": a.rounds, "block_steps": a.block_steps, "block_order": "alternating",
+    ranks = D.all_gather_object(ctx, local)  # [rank][round][cond]
+    rows = [{c: max(rk[r][c]["all"] for rk in ranks) for c in conds} for r in range(a.rounds)]
+    out: dict = {"rounds": a.rounds, "block_steps": a.block_steps,
+                 "order_design": {"kind": "all permutations in turn", "orders": [[f"{c:g}" for c in o]
+                                                                                for o in dict.fromkeys(orders)],
+                                  "balanced": a.rounds % len(dict.fromkeys(orders)) == 0},
                  "paused_reads": paused_reads, "tiers": {}}
     for h in hzs:
         diffs = [100.0 * (row[h] / row[0.0] - 1.0) for row in rows]
         m, ci, sd = mean_ci95(diffs)
-        out["tiers"][f"{h:g}"] = {"overhead_pct": m, "overhead_ci95_pct": ci, "overhead_sd_pct": sd,
-                                  "overhead_per_round_pct": [round(d, 4) for d in diffs],
-                                  "_rates": rates[h], "_lat": lat[h]}
-    out["block_seconds"] = [[f"{c:g}", round(row[c], 6)] for row in rows for c in row]
-    # Power state per condition of this rank's GPU (the result carries rank 0's).
-    power: dict = {}
-    for c in conds:
-        ws = [d["power_w"] for d in pw[c]]
-        ps = [d["ppt_pct"] for d in pw[c] if "ppt_pct" in d]
-        if ws:
+        tier = {"overhead_pct": m, "overhead_ci95_pct": ci, "overhead_sd_pct": sd,
+                "overhead_per_round_pct": [round(d, 4) for d in diffs],
+                "_rates": rates[h], "_lat": lat[h]}
+        # per component (rank 0's GPU, and the mean of every rank's own estimate)
+        names = sorted({n for rk in ranks for rd in rk for n in rd[h]["comp"]})
+        by_comp: dict = {}
+        for n in names:
+            per_rank = []
+            for rk in ranks:
+                d = [100.0 * (rd[h]["comp"][n] / rd[0.0]["comp"][n] - 1.0) for rd in rk
+                     if rd[0.0]["comp"].get(n, 0) > 0 and n in rd[h]["comp"]]
+                per_rank.append(mean_ci95(d))
+            m0, c0, _ = per_rank[0]
+            share = sum(rd[0.0]["comp"].get(n, 0.0) for rd in ranks[0]) / max(
+                1e-12, sum(rd[0.0]["own"] for rd in ranks[0]))
+            by_comp[n] = {"overhead_pct": m0, "overhead_ci95_pct": c0, "share_of_block_time": round(share, 4)}
+            if len(ranks) > 1:
+                by_comp[n]["per_rank_overhead_pct"] = [round(x[0], 4) for x in per_rank]
+        tier["overhead_by_component"] = by_comp
+        # per rank: that rank's own work time, paired by round
+        per_rank = []
+        for k, rk in enumerate(ranks):
+            m_k, c_k, _ = mean_ci95([100.0 * (rd[h]["own"] / rd[0.0]["own"] - 1.0) for rd in rk])
+            per_rank.append({"rank": k, "overhead_pct": round(m_k, 4), "overhead_ci95_pct": round(c_k, 4)})
+        tier["overhead_by_rank"] = per_rank
+        out["tiers"][f"{h:g}"] = tier
+    out["block_seconds"] = [[f"{c:g}", round(rows[r][c], 6)] for r, o in enumerate(orders) for c in o]
+    # Block-position means (every condition pooled, and per condition): with the
+    # permutation design each condition's mean covers every position equally.
+    pos_all: dict[int, list[float]] = {}
+    pos_c: dict[str, dict[int, list[float]]] = {}
+    for r, o in enumerate(orders):
+        for p, c in enumerate(o):
+            pos_all.setdefault(p, []).append(rows[r][c])
+            pos_c.setdefault(f"{c:g}", {}).setdefault(p, []).append(rows[r][c])
+    out["position_means"] = {"all": {str(p): round(sum(v) / len(v), 6) for p, v in sorted(pos_all.items())},
+                             "by_condition": {c: {str(p): round(sum(v) / len(v), 6) for p, v in sorted(d.items())}
+                                              for c, d in pos_c.items()}}
+    try:
+        out["position_adjusted"] = position_adjusted(rows, conds, orders)
+    except Exception as e:  # noqa: BLE001 - report, never fail the bench on the side estimate
+        out["position_adjusted"] = {"error": repr(e)}
+    # Power state per condition of every rank's GPU (PMFW energy / PPT accumulators).
+    power_by_rank = []
+    for k, rk in enumerate(ranks):
+        power: dict = {}
+        for c in conds:
+            pw = [rd[c]["power"] for rd in rk if rd[c]["power"]]
+            if not pw:
+                continue
+            ws = [d["power_w"] for d in pw]
+            ps = [d["ppt_pct"] for d in pw if "ppt_pct" in d]
             power[f"{c:g}"] = {"blocks": len(ws), "power_w_mean": round(sum(ws) / len(ws), 2),
                                "ppt_pct_mean": round(sum(ps) / len(ps), 3) if ps else None}
-            if c > 0 and len(pw[c]) == len(pw[0.0]):  # paired by round, like the timings
-                m, ci, _ = mean_ci95([x["power_w"] - y["power_w"] for x, y in zip(pw[c], pw[0.0])])
+            paired = [(rd[c]["power"], rd[0.0]["power"]) for rd in rk if rd[c]["power"] and rd[0.0]["power"]]
+            if c > 0 and paired:
+                m, ci, _ = mean_ci95([x["power_w"] - y["power_w"] for x, y in paired])
                 power[f"{c:g}"]["power_w_vs_paused"] = round(m, 2)
                 power[f"{c:g}"]["power_w_vs_paused_ci95"] = round(ci, 2)
-    if power:
-        out["power"] = {"by_condition": power,
-                        "note": "PMFW energy / PPT-residency accumulators read by the bench itself at every "
-                                "block edge ('0' = exporter paused)"}
+        power_by_rank.append(power)
+    if any(power_by_rank):
+        out["power"] = {"by_condition": power_by_rank[0], "by_rank": power_by_rank,
+                        "note": "PMFW energy / PPT-residency accumulators read by each rank at its own GPU's block "
+                                "edges ('0' = exporter paused)"}
     return out
 
 
@@ -943,6 +1149,91 @@ def capacity(ctx, load, exp, a) -> dict:
     return out
 
 
+def xgmi_link_check(ctx, load, exp, a) -> dict:
+    """Phase X (untimed, N > 1) — does each xGMI byte land on the link whose peer is
+    the real peer, and in which unit?  Rank 0 sees every GPU of the
+    node: for each other rank's GPU k in turn it copies ``--xgmi-check-mib`` from GPU 0
+    into GPU k (a peer copy over the one direct link), with exporter scrapes before and
+    after.  On the source and on the destination, the link whose byte counter moved
+    most (read + write, minus the median of the other links as background) must be
+    the one whose amdsmi peer_bdf is the other GPU; its bytes ÷ the copied bytes is the
+    accumulator-unit ratio (1.0 if --xgmi-bytes-per-unit is right).  The mock backend
+    books the copy on the right link itself (/control/mock/xgmi)."""
+    if ctx.world < 2:
+        return {"skipped": "N=1: no peer GPU to copy to"}
+    if a.xgmi_check_mib <= 0:
+        return {"skipped": "--xgmi-check-mib 0"}
+    D.cpu_barrier(ctx)
+    out: dict = {}
+    # every rank's GPU, in local-rank order (a collective: every rank calls it)
+    bdfs = [b for _, b in sorted(set(D.all_gather_object(ctx, (ctx.local_rank, load.pci_bdf(ctx.local_rank)))))]
+    if ctx.local_rank == 0 and exp is not None:
+        nbytes = int(a.xgmi_check_mib) << 20
+        gpu_of = {d["bdf"]: int(d["gpu"]) for d in exp.json("/devices")}
+        topo = exp.json("/topology")
+        peer_of = {(int(x["gpu"]), int(x["link"])): x.get("peer_bdf", "") for x in topo.get("links", [])}
+
+        def link_bytes(m: dict) -> dict:
+            tot: dict = {}
+            for fam in ("amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total"):
+                for lb, v in m.get(fam, []):
+                    key = (int(lb["gpu"]), int(lb["link"]))
+                    tot[key] = tot.get(key, 0.0) + v
+            return tot
+
+        def moved(before: dict, after: dict, gpu: int, want_bdf: str) -> dict:
+            d = {l: after[(g, l)] - before.get((g, l), 0.0) for (g, l) in after if g == gpu}
+            if not d:
+                return {"ok": False, "reason": "no xGMI byte counters for this GPU"}
+            l_max = max(d, key=d.get)
+            rest = sorted(v for l, v in d.items() if l != l_max)
+            bg = rest[len(rest) // 2] if rest else 0.0
+            peer = peer_of.get((gpu, l_max), "")
+            return {"link": l_max, "link_peer_bdf": peer, "ok": peer == want_bdf and d[l_max] - bg > 0,
+                    "bytes_counted": round(d[l_max], 1), "background_bytes": round(bg, 1),
+                    "unit_ratio": round((d[l_max] - bg) / nbytes, 4)}
+
+        src_dev = 0
+        per_peer = []
+        for k in range(1, len(bdfs)):
+            g0, gk = gpu_of.get(bdfs[0]), gpu_of.get(bdfs[k])
+            if g0 is None or gk is None:
+                per_peer.append({"peer_bdf": bdfs[k], "ok": False, "reason": "GPU not sampled by the exporter"})
+                continue
+            m0 = parse_text(exp.sc.get())
+            if a.mock:
+                exp.json(f"/control/mock/xgmi?src={g0}&dst={gk}&bytes={nbytes}")
+            else:
+                import torch
+
+                src = torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", src_dev)).fill_(1.0)
+                dst = torch.empty_like(src, device=torch.device("cuda", k))
+                torch.cuda.synchronize(src_dev)
+                dst.copy_(src, non_blocking=True)
+                torch.cuda.synchronize(src_dev)
+                torch.cuda.synchronize(k)
+                del src, dst
+            time.sleep(a.xgmi_check_settle)  # the PMFW table refreshes every ≈20 ms; the exporter reads it at 100 Hz
+            m1 = parse_text(exp.sc.get())
+            b0, b1 = link_bytes(m0), link_bytes(m1)
+            row = {"src_gpu": g0, "peer_gpu": gk, "peer_bdf": bdfs[k], "bytes": nbytes,
+                   "src": moved(b0, b1, g0, bdfs[k]), "dst": moved(b0, b1, gk, bdfs[0])}
+            row["ok"] = bool(row["src"].get("ok") and row["dst"].get("ok"))
+            per_peer.append(row)
+        ratios = sorted(r[side]["unit_ratio"] for r in per_peer for side in ("src", "dst")
+                        if isinstance(r.get(side), dict) and "unit_ratio" in r[side])
+        ratio = ratios[len(ratios) // 2] if ratios else None
+        out = {"bytes_per_copy": nbytes, "per_peer": per_peer,
+               "xgmi_link_map_ok": bool(per_peer) and all(r["ok"] for r in per_peer),
+               "xgmi_unit_ratio": ratio,
+               "xgmi_unit_ok": ratio is not None and 0.8 <= ratio <= 1.25}
+        if ratio is not None and not out["xgmi_unit_ok"]:
+            out["warning"] = (f"xGMI accumulator unit off by {ratio:.3g}x: set --xgmi-bytes-per-unit to "
+                              f"{1024.0 * ratio:.4g}")
+    D.cpu_barrier(ctx)
+    return out
+
+
 def run(a, ctx) -> dict | None:
     n = ctx.world
     hzs = tiers(a)
@@ -1022,6 +1313,7 @@ def run(a, ctx) -> dict | None:
     quiet = quiet_gpu(ctx, load, exp, a)
     inter = interleaved(ctx, load, exp, a, hzs)
     cap = capacity(ctx, load, exp, a)
+    xlink = xgmi_link_check(ctx, load, exp, a)
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
@@ -1108,6 +1400,9 @@ def run(a, ctx) -> dict | None:
         # what the phase-B all-reduces must have moved per GPU (read + write, bandwidth-optimal
         # 2(N-1)/N each way): the measured / expected ratio pins the PMFW xGMI accumulator unit
         "xgmi_allreduce_GBps_per_gpu_expected": allreduce_GBps(load, a, n, win),
+        "xgmi_link_check": xlink,
+        "xgmi_link_map_ok": xlink.get("xgmi_link_map_ok"),
+        "xgmi_unit_ratio": xlink.get("xgmi_unit_ratio"),
         "phases_wall": PHASES,
         "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in integrals)
         / max(1, sum(i.get("pmc_samples", 0) for i in integrals)),

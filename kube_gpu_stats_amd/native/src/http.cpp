@@ -359,6 +359,15 @@ void HttpServer::loop() {
             respond(c, 400, "Bad Request", "text/plain", "hz must be within (0, 100000]\n");
           else
             respond(c, 200, "OK", "application/json", "{\"hz\":" + std::to_string(ex_->sample_rate()) + "}");
+        } else if (ex_->config().control_http && target == "/control/mock/xgmi") {
+          // Benchmarks on the mock provider (bench.py --mock phase X): account a peer copy
+          // on the xGMI link between two mock GPUs.  Other backends: 404.
+          const int src = query_int(query, "src", -1), dst = query_int(query, "dst", -1);
+          const uint64_t bytes = query_u64(query, "bytes", 0);
+          if (ex_->backend()->inject_xgmi(src, dst, bytes) == 0)
+            respond(c, 200, "OK", "application/json", "{\"injected\":" + std::to_string(bytes) + "}");
+          else
+            respond(c, 404, "Not Found", "text/plain", "xGMI injection needs the mock backend and two GPUs\n");
         } else if (target == "/healthz") {
           const bool ok = ex_->healthy();
           respond(c, ok ? 200 : 503, ok ? "OK" : "Service Unavailable", "text/plain", ok ? "ok\n" : "no device sampled\n");

@@ -63,14 +63,25 @@ def test_bench_contract_single_process():
     assert _rate_ok(res["value"], 8000.0)
     assert res["p50_scrape_ms"] < 50 and res["scrapes"] > 10
     inter = res["interleaved"]
-    # alternating rounds over (paused, 100 Hz, 8 kHz); paused blocks really do not read
+    # rounds cycle through every order of (paused, 100 Hz, 8 kHz): each condition in
+    # each block position; paused blocks really do not read
     order = [c for c, _ in inter["block_seconds"]]
-    assert order[:6] == ["0", "100", "8000", "8000", "100", "0"]
+    assert order[:12] == ["0", "100", "8000", "0", "8000", "100", "100", "0", "8000", "100", "8000", "0"]
+    assert inter["order_design"]["kind"] == "all permutations in turn" and len(inter["order_design"]["orders"]) == 4
+    assert set(inter["position_means"]["all"]) == {"0", "1", "2"}
+    assert set(inter["position_means"]["by_condition"]) == {"0", "100", "8000"}
+    pa = inter["position_adjusted"]
+    assert set(pa) >= {"100", "8000", "position_effect_pct"} and abs(pa["8000"]["overhead_pct"]) < 50
     assert inter["paused_reads"] == 0
+    assert res["xgmi_link_check"] == {"skipped": "N=1: no peer GPU to copy to"} and res["xgmi_link_map_ok"] is None
     for hz in ("100", "8000"):
         t = inter["tiers"][hz]
         assert len(t["overhead_per_round_pct"]) == 4
         assert t["overhead_ci95_pct"] > 0 and abs(t["overhead_pct"]) < 50
+        # the mock load's one component, timed per block; the one rank's own overhead
+        comp = t["overhead_by_component"]["mock"]
+        assert abs(comp["overhead_pct"]) < 50 and comp["share_of_block_time"] == pytest.approx(1.0, abs=0.2)
+        assert [r["rank"] for r in t["overhead_by_rank"]] == [0]
         # 4 blocks of ~60 ms: at 100 Hz that is ~25 ticks, so whole-tick quantisation at
         # each block edge alone is ±4 per cent; 8 kHz (~2000 ticks) loses up to ~15 % to
         # timer slack on a shared CPU container
@@ -108,6 +119,31 @@ def test_bench_contract_torchrun_gloo_world2():
     # both ranks' GPUs sampled by the one node exporter → aggregate ≈ 2 × per-GPU
     assert len(res["pmc_samples_per_sec_per_gpu"]) == 2
     assert res["value"] == pytest.approx(sum(res["pmc_samples_per_sec_per_gpu"].values()), rel=0.01)
+
+
+@pytest.mark.slow
+def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads():
+    """The 8-GPU driver run must validate itself unattended: phase X
+    books a GPU 0 → GPU k peer copy per peer (the mock backend puts it on the link to
+    k) and finds each copy on the link whose peer_bdf is k's, at unit ratio 1; the
+    interleaved overheads come per rank and per component, power per rank."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--mock", "--gpus", "8", "--steps", "4", "--warmup", "1",
+                        "--hz", "2000", "--capacity-hz", "", "--burst-s", "0", "--quiet-s", "0", *FAST],
+                       cwd=REPO, capture_output=True, text=True, timeout=420, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    res = _last_json(r.stdout)
+    assert res["n_gpus"] == 8
+    x = res["xgmi_link_check"]
+    assert res["xgmi_link_map_ok"] is True and x["xgmi_link_map_ok"] is True, x
+    assert res["xgmi_unit_ratio"] == pytest.approx(1.0, abs=0.02) and x["xgmi_unit_ok"] is True, x
+    assert [p["peer_gpu"] for p in x["per_peer"]] == list(range(1, 8))
+    for p in x["per_peer"]:
+        assert p["src"]["link_peer_bdf"] == p["peer_bdf"] and p["dst"]["ok"], p
+    for hz in ("100", "2000"):
+        t = res["interleaved"]["tiers"][hz]
+        assert [q["rank"] for q in t["overhead_by_rank"]] == list(range(8))
+        assert len(t["overhead_by_component"]["mock"]["per_rank_overhead_pct"]) == 8
 
 
 @pytest.mark.slow

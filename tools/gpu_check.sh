@@ -3,7 +3,7 @@
 # time limit; a test failure (rc 1) does not stop the script, a timeout / signal /
 # abort (rc >= 124) does — nothing else touches the GPU after that.
 #   gpurun --timeout 1100 -- 'bash tools/gpu_check.sh <tag> [steps...]'
-# steps (default: probe tests smoke bench): probe tests smoke bench bench2 rocprof
+# steps (default: probe tests smoke bench): probe probe3 tests smoke bench bench2 rocprof
 set -u
 TAG=${1:-r2}; shift || true
 STEPS=${*:-probe tests smoke bench}
@@ -22,6 +22,10 @@ run() {  # name limit cmd...
 }
 for s in $STEPS; do
   case $s in
+    probe3) run event_source 30 ls -la /sys/bus/event_source/devices/
+            run perf_pmu 90 python tools/perf_pmu_probe.py --out "$OUT/perf_pmu.json"
+            KGS_AQL_PROBE_OUT="$OUT/aql_probe_cp.json" run aql_probe_cp 400 python -u tools/aql_probe.py \
+              cpc_dispatch,cpc_busy,cpc_gd,grbm_cp,spi_csn ;;
     probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
            run probe_xgmi 90 python tools/probe_xgmi.py ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider ;;
