@@ -650,6 +650,14 @@ def allreduce_GBps(load, a, n: int, win: float):
     return round(2 * 2 * (n - 1) / n * size * a.steps * load.reps / win / 1e9, 3)
 
 
+def allreduce_ratio(measured: dict, expected) -> dict | None:
+    """Per GPU, the xGMI bytes its link counters saw during phase B ÷ the bytes its
+    all-reduces must have moved (None without all-reduces)."""
+    if not expected:
+        return None
+    return {g: round(v / expected, 4) for g, v in measured.items()}
+
+
 def observed(m: dict) -> dict:
     """What the exporter saw of the load (window gauges of the last scrape), per GPU."""
     out: dict = {}
@@ -1400,6 +1408,9 @@ def run(a, ctx) -> dict | None:
         # what the phase-B all-reduces must have moved per GPU (read + write, bandwidth-optimal
         # 2(N-1)/N each way): the measured / expected ratio pins the PMFW xGMI accumulator unit
         "xgmi_allreduce_GBps_per_gpu_expected": allreduce_GBps(load, a, n, win),
+        # measured ÷ expected per GPU: 1.0 if the link counters' unit is right and the
+        # all-reduces ran on xGMI (phase X pins the unit link by link)
+        "xgmi_allreduce_ratio_per_gpu": allreduce_ratio(xgmi_rates(before, after, win), allreduce_GBps(load, a, n, win)),
         "xgmi_link_check": xlink,
         "xgmi_link_map_ok": xlink.get("xgmi_link_map_ok"),
         "xgmi_unit_ratio": xlink.get("xgmi_unit_ratio"),

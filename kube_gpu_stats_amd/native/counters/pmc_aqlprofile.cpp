@@ -81,6 +81,10 @@ const Sel kGfx950[] = {
     {"SQ_VALU_MFMA_BUSY_CYCLES", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, "SQ", 93},
     {"TA_TA_BUSY", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TA, "TA", 13},
     {"TCC_HIT", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, "TCC", 21},
+    {"CPC_ADC_DISPATCH_ALLOC_DONE", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPC, "CPC", 4},
+    {"CPC_TG_SEND", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPC, "CPC", 62},
+    {"CPC_CPC_STAT_BUSY", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPC, "CPC", 25},
+    {"CPF_CPF_STAT_BUSY", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPF, "CPF", 23},
     {"TCC_EA0_RDREQ", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, "TCC", 42},
 };
 
