@@ -83,8 +83,9 @@ def parse_args(argv=None):
                     help="counter reader (auto = %s)" % PMC_READER)
     ap.add_argument("--pmc-pipeline", type=int, default=1, choices=[0, 1],
                     help="aqlprofile reader: pipelined READs (1) or submit-and-wait per sample (0)")
-    ap.add_argument("--pmc-set", default="base", choices=["base", "full"],
-                    help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register reads)")
+    ap.add_argument("--pmc-set", default="base", choices=["base", "full", "base+dispatch", "full+dispatch"],
+                    help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register "
+                    "reads); +dispatch adds the CP dispatch counter that drives the CP-bound READ rate")
     ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=20.0)
@@ -124,6 +125,8 @@ def parse_args(argv=None):
                     help="phase S: tick rates above --hz to try under the load, one block each ('' = off)")
     ap.add_argument("--quiet-s", type=float, default=1.5,
                     help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
+    ap.add_argument("--component-s", type=float, default=1.0,
+                    help="phase K: seconds each load component runs alone while the exporter samples (0 = off)")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
     ap.add_argument("--mock-step-ms", type=float, default=20.0, help="mock: duration of one load unit")
     ap.add_argument("--mock-latency", type=int, default=1, choices=[0, 1],
@@ -303,6 +306,18 @@ class GpuLoad(Load):
     def components_end(self) -> dict:
         self.timing = False
         return self.ev.collect()
+
+    def component_names(self) -> list[str]:
+        return ["mfma", "triad"] + (["tiny_graph"] if self.graph is not None else [])
+
+    def run_component(self, name: str) -> None:
+        """One launch of a single load component (phase K)."""
+        if name == "mfma":
+            self.ls.run_mfma()
+        elif name == "triad":
+            self.ls.run_stream()
+        elif name == "tiny_graph":
+            self.graph.replay()
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -1102,6 +1117,48 @@ def quiet_gpu(ctx, load, exp, a) -> dict:
     return out
 
 
+def component_rates(ctx, load, exp, a) -> dict:
+    """Phase K (untimed) — samples/s the exporter delivers at the primary rate while
+    each load component runs alone for --component-s: the long MFMA kernel, the HBM
+    triads, the dispatch-bound tiny-kernel graph.  With the CP-bound READ rate the
+    graph is read at --pmc-cpbound-hz and the MFMA / HBM work at every tick, so the
+    headline's blend is split into what each kind of work gets."""
+    names = getattr(load, "component_names", lambda: [])()
+    if a.component_s <= 0 or not names:
+        return {}
+    out: dict = {}
+    for name in names:
+        D.barrier(ctx)
+        load.sync()
+        before, w0 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < a.component_s:
+            load.run_component(name)
+            k += 1
+            if k % 4 == 0:
+                load.sync()
+        load.sync()
+        D.barrier(ctx)
+        if exp is None:
+            continue
+        after, w1 = scrape_at(exp.sc)
+        r = Rates()
+        r.add(before, after, w1 - w0)
+        pg, src = r.per_gpu(exp.ready.get("pmc", "none") != "none")
+        fam = lambda m, n: {lb["gpu"]: v for lb, v in m.get(n, [])}  # noqa: E731
+        cb0, cb1 = fam(before, "kgs_pmc_cpbound_skips_total"), fam(after, "kgs_pmc_cpbound_skips_total")
+        d0, d1 = fam(before, "amdgpu_kernel_dispatches_total"), fam(after, "amdgpu_kernel_dispatches_total")
+        win = w1 - w0
+        out[name] = {"samples_per_sec_per_gpu": {g: round(v, 1) for g, v in pg.items()}, "sample_source": src,
+                     "launches": k, "seconds": round(win, 3)}
+        if cb1:
+            out[name]["cpbound_skips_per_s"] = {g: round((v - cb0.get(g, 0)) / win, 1) for g, v in cb1.items()}
+        if d1:
+            out[name]["kernel_dispatches_per_s"] = {g: round((v - d0.get(g, 0)) / win, 1) for g, v in d1.items()}
+    return out
+
+
 def capacity(ctx, load, exp, a) -> dict:
     """Phase S — how far the counter tier goes past the primary rate (untimed).  Under the
     same load, one ``--block-steps`` block at each ``--capacity-hz`` rate: delivered
@@ -1321,6 +1378,7 @@ def run(a, ctx) -> dict | None:
     quiet = quiet_gpu(ctx, load, exp, a)
     inter = interleaved(ctx, load, exp, a, hzs)
     cap = capacity(ctx, load, exp, a)
+    comp_rates = component_rates(ctx, load, exp, a)
     xlink = xgmi_link_check(ctx, load, exp, a)
     stopped = exp.stop() if exp is not None else {}
 
@@ -1396,6 +1454,7 @@ def run(a, ctx) -> dict | None:
         "burst_resolution": resolution,
         "quiet_gpu": quiet,
         "capacity": cap,
+        "delivered_by_component": comp_rates,
         "exporter_cpu_cores": round((cpu1 - cpu0) / cpu_win, 4) if cpu_win > 0 and exp_pid else None,
         "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / cpu_win, 4) for k, v in thr1.items()
                                          if cpu_win > 0 and v - thr0.get(k, 0.0) > 0.005 * cpu_win},

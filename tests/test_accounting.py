@@ -227,7 +227,7 @@ def test_report_util_metric_cu_seconds_splits_a_shared_gpu(mock_exporter):
         time.sleep(0.2)
         stamps = []
         t0 = time.time()
-        for k in range(14):
+        for k in range(22):
             time.sleep(max(0.0, t0 + 0.25 * k - time.time()))
             ts = time.time()
             fp.ingest(parse_text(sc.get()), ts)
@@ -235,14 +235,16 @@ def test_report_util_metric_cu_seconds_splits_a_shared_gpu(mock_exporter):
         end = stamps[-1]
         for metric, want in (("container_gpu_cu_seconds_total", {"big": 60, "idle": 0}),
                              ("container_gpu_busy_seconds_total", {"big": 70, "idle": 70})):
-            q = G.Queries.amd("", 1, util_metric=metric)
+            q = G.Queries.amd("", 2, util_metric=metric)
             fp.add_instant(q.total, [{"metric": {"node": "node-a", q.type_label: "MI355X"}, "value": [end, "1"]}])
             fp.add_instant(q.used, [{"metric": {"node": "node-a"}, "value": [end, "1"]}])
             fp.add_instant(q.live, [{"metric": {"namespace": o["namespace"], "pod": o["pod"]}, "value": [end, "1"]}
                                     for o in owners])
             fp.add_range(q.req, [{"metric": {"node": "node-a", "namespace": o["namespace"], "pod": o["pod"]},
                                   "values": [[end, "1"]]} for o in owners])
-            rows = G.run_report(PromClient(url), q, end, 2, 1, compat=False)
+            # 2 s rate() steps: the per-process tier books CU-seconds at each 50 ms read,
+            # so a 1 s step on a loaded test host is off by the read jitter
+            rows = G.run_report(PromClient(url), q, end, 2, 2, compat=False)
             got = {r[2]: r[4] for r in rows}
             assert got["big"] == pytest.approx(want["big"], abs=5) and got["idle"] == pytest.approx(want["idle"], abs=5), \
                 (metric, rows)
