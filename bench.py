@@ -86,7 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-set", default="base", choices=["base", "full", "base+dispatch", "full+dispatch"],
                     help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register "
                     "reads); +dispatch adds the CP dispatch counter that drives the CP-bound READ rate")
-    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
+    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3, 6],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=20.0)
     ap.add_argument("--step-ms", type=float, default=500.0,
