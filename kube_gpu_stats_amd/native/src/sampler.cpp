@@ -685,6 +685,8 @@ void Sampler::run_pmc(Worker& w) {
             last_start_ns = t;
           }
         }
+      } else if (stop_.load(std::memory_order_relaxed)) {
+        break;  // stop() aborted the wait: not a device failure
       } else {
         ++P.pmc_errors;
         if (++st.pmc_fail_streak >= cfg_.pmc_breaker_k) {
