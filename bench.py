@@ -86,7 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-set", default="base", choices=["base", "full", "base+dispatch", "full+dispatch"],
                     help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register "
                     "reads); +dispatch adds the CP dispatch counter that drives the CP-bound READ rate")
-    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3, 6],
+    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=20.0)
     ap.add_argument("--step-ms", type=float, default=500.0,
@@ -424,6 +424,9 @@ class TrainLoad(GpuLoad):
         self.ev = EventTimer(torch) if dev.type == "cuda" else None
 
     burst = None  # phase R runs on the synthetic load only
+
+    def component_names(self) -> list[str]:
+        return []  # one component (the whole step): phase K has nothing to split
 
     def unit(self):
         t = self.timing and self.ev is not None
@@ -1123,8 +1126,10 @@ def component_rates(ctx, load, exp, a) -> dict:
     triads, the dispatch-bound tiny-kernel graph.  With the CP-bound READ rate the
     graph is read at --pmc-cpbound-hz and the MFMA / HBM work at every tick, so the
     headline's blend is split into what each kind of work gets."""
+    if a.component_s <= 0:
+        return {}
     names = getattr(load, "component_names", lambda: [])()
-    if a.component_s <= 0 or not names:
+    if not names:
         return {}
     out: dict = {}
     for name in names:

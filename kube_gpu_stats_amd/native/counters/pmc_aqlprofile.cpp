@@ -307,12 +307,9 @@ int parse_scope(const char* s, size_t n) {
   if (n == 5 && std::strncmp(s, "agent", 5) == 0) return static_cast<int>(HSA_FENCE_SCOPE_AGENT);
   return static_cast<int>(HSA_FENCE_SCOPE_NONE);
 }
-int lean_mode();
 std::pair<int, int> read_fences() {
   static const std::pair<int, int> v = [] {
     const char* e = std::getenv("KGS_AQL_FENCE");
-    if (!e && lean_mode() == 6)  // write-confirmed copies: no release needed (lean_read_ib)
-      return std::make_pair(static_cast<int>(HSA_FENCE_SCOPE_NONE), static_cast<int>(HSA_FENCE_SCOPE_NONE));
     if (!e) return std::make_pair(static_cast<int>(HSA_FENCE_SCOPE_NONE), static_cast<int>(HSA_FENCE_SCOPE_SYSTEM));
     const char* c = std::strchr(e, ',');
     if (!c) return std::make_pair(parse_scope(e, std::strlen(e)), parse_scope(e, std::strlen(e)));
@@ -540,12 +537,7 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
 // 2 (default) = 1 + ACQUIRE_MEM reduced to the L2 writeback that publishes the
 // CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Cost-attribution modes
 // (KGS_AQL_LEAN only; the counter values they return are stale): 4 = 3 + no
-// COPY_DATA, 5 = every packet of the IB a NOP.  6 ("confirm") = 3 + WR_CONFIRM on
-// every COPY_DATA: aqlprofile's copies already go to memory (DST_SEL 5, stream
-// policy), so once the CP waits for each write's confirmation the results are in
-// memory before the packet completes, and the READ needs neither an in-IB cache
-// writeback nor a system-scope release fence (read_fences() then defaults to
-// none,none: no L2 writeback per READ at all).  Returns packets changed.
+// COPY_DATA, 5 = every packet of the IB a NOP.  Returns packets changed.
 int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
   if (mode <= 0) return 0;
   uint32_t dw[4];
@@ -561,7 +553,7 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
     if ((h >> 30) == 2) { ++i; continue; }
     if ((h >> 30) != 3) return -2;
     const uint32_t opc = (h >> 8) & 0xFF, len = ((h >> 16) & 0x3FFF) + 2;
-    if (mode == 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
+    if (mode >= 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
       if (opc != 0x10) {
         nop(i, len);
         ++changed;
@@ -574,9 +566,6 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
       ++changed;
     } else if (opc == 0x58 && mode >= 3) {
       nop(i, len);
-      ++changed;
-    } else if (opc == 0x40 && mode == 6) {         // COPY_DATA: WR_CONFIRM (bit 20)
-      ib[i + 1] |= (1u << 20);
       ++changed;
     }
     i += len;
@@ -775,7 +764,7 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
 // (READ packet mode 0-3, see lean_read_ib).  0 = ok, -1 = unknown key / value.
 // "timeout_ms" (1..60000): bound of every wait on the CP (default 250).
 int kgs_pmc_configure(const char* key, int value) {
-  if (key && std::strcmp(key, "lean") == 0 && ((value >= 0 && value <= 3) || value == 6)) {
+  if (key && std::strcmp(key, "lean") == 0 && value >= 0 && value <= 3) {
     g_lean = value;
     return 0;
   }

@@ -26,13 +26,10 @@ for s in $STEPS; do
             run perf_pmu 90 python tools/perf_pmu_probe.py --out "$OUT/perf_pmu.json"
             KGS_AQL_PROBE_OUT="$OUT/aql_probe_cp.json" run aql_probe_cp 400 python -u tools/aql_probe.py \
               cpc_dispatch,cpc_busy,cpc_gd,grbm_cp,spi_csn ;;
-    launch6) run launch6 300 python -u tools/launch_overhead.py 8000:base:aqlprofile:2 8000:base:aqlprofile:6 \
-              1000:base:aqlprofile:6 off ;;
-    bench6) run bench6 600 python -u bench.py --steps 20 --warmup 5 --pmc-lean 6 --out "$OUT/bench6.json" ;;
+    trainpmfw) run trainpmfw 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
+              --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc none --out "$OUT/trainpmfw.json" ;;
     train2) run train2 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 2 --out "$OUT/train2.json" ;;
-    train6) run train6 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
-              --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 6 --out "$OUT/train6.json" ;;
     probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
            run probe_xgmi 90 python tools/probe_xgmi.py ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider ;;
