@@ -83,9 +83,9 @@ def parse_args(argv=None):
                     help="counter reader (auto = %s)" % PMC_READER)
     ap.add_argument("--pmc-pipeline", type=int, default=1, choices=[0, 1],
                     help="aqlprofile reader: pipelined READs (1) or submit-and-wait per sample (0)")
-    ap.add_argument("--pmc-set", default="base", choices=["base", "full", "base+dispatch", "full+dispatch"],
+    ap.add_argument("--pmc-set", default="base", choices=["base", "full"],
                     help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register "
-                    "reads); +dispatch adds the CP dispatch counter that drives the CP-bound READ rate")
+                    "reads)")
     ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=20.0)
@@ -1123,9 +1123,7 @@ def quiet_gpu(ctx, load, exp, a) -> dict:
 def component_rates(ctx, load, exp, a) -> dict:
     """Phase K (untimed) — samples/s the exporter delivers at the primary rate while
     each load component runs alone for --component-s: the long MFMA kernel, the HBM
-    triads, the dispatch-bound tiny-kernel graph.  With the CP-bound READ rate the
-    graph is read at --pmc-cpbound-hz and the MFMA / HBM work at every tick, so the
-    headline's blend is split into what each kind of work gets."""
+    triads, the dispatch-bound tiny-kernel graph (the headline's blend, split)."""
     if a.component_s <= 0:
         return {}
     names = getattr(load, "component_names", lambda: [])()
@@ -1151,16 +1149,8 @@ def component_rates(ctx, load, exp, a) -> dict:
         r = Rates()
         r.add(before, after, w1 - w0)
         pg, src = r.per_gpu(exp.ready.get("pmc", "none") != "none")
-        fam = lambda m, n: {lb["gpu"]: v for lb, v in m.get(n, [])}  # noqa: E731
-        cb0, cb1 = fam(before, "kgs_pmc_cpbound_skips_total"), fam(after, "kgs_pmc_cpbound_skips_total")
-        d0, d1 = fam(before, "amdgpu_kernel_dispatches_total"), fam(after, "amdgpu_kernel_dispatches_total")
-        win = w1 - w0
         out[name] = {"samples_per_sec_per_gpu": {g: round(v, 1) for g, v in pg.items()}, "sample_source": src,
-                     "launches": k, "seconds": round(win, 3)}
-        if cb1:
-            out[name]["cpbound_skips_per_s"] = {g: round((v - cb0.get(g, 0)) / win, 1) for g, v in cb1.items()}
-        if d1:
-            out[name]["kernel_dispatches_per_s"] = {g: round((v - d0.get(g, 0)) / win, 1) for g, v in d1.items()}
+                     "launches": k, "seconds": round(w1 - w0, 3)}
     return out
 
 

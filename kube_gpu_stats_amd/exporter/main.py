@@ -73,11 +73,6 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                        "command-processor packet that GFX busy / GUI-active count as work (≈80 / "
                                        "190 µs each), so a quiet GPU is read at this rate and a busy one every tick "
                                        "(0 = every tick: profiling mode)")
-    add_flag(ap, "pmc-cpbound-dispatch-hz", 100000.0, "with the dispatch counter (--pmc-set base+dispatch): a READ "
-                                                     "interval with at least this many kernel dispatches/s makes the "
-                                                     "GPU CP-bound, and its READs drop to --pmc-cpbound-hz (0 = off)")
-    add_flag(ap, "pmc-cpbound-hz", 1000.0, "counter READ rate while the GPU is dispatch-bound: each READ costs the "
-                                           "command processor ≈2 µs a µs-kernel stream would otherwise use")
     add_flag(ap, "pmc-timeout-ms", 250, "bound of every wait on the command processor (counter READ, START, STOP, "
                                         "queue slot): a wedged CP costs one timeout, never a hang")
     add_flag(ap, "pmc-breaker-k", 3, "consecutive failed counter drains that open the counter tier's circuit breaker "
@@ -148,8 +143,6 @@ def config_from_args(a) -> dict:
         "pmc_refresh_s": a.pmc_refresh_s,
         "pmc_idle_hz": a.pmc_idle_hz,
         "pmc_timeout_ms": a.pmc_timeout_ms,
-        "pmc_cpbound_dispatch_hz": a.pmc_cpbound_dispatch_hz,
-        "pmc_cpbound_hz": a.pmc_cpbound_hz,
         "pmc_breaker_k": a.pmc_breaker_k,
         "pmc_retry_s": a.pmc_retry_s,
         "pmc_retry_max_s": a.pmc_retry_max_s,

@@ -126,9 +126,6 @@ CATALOG: tuple[Family, ...] = (
     # ---- hardware counters (direct command-processor reader, native/counters/pmc_aqlprofile.cpp) --
     F("amdgpu_pmc_total", "counter", "Raw hardware counter since exporter start.", extra=("counter",),
       source="counters", tier="pmc"),
-    F("amdgpu_kernel_dispatches_total", "counter", "Kernel dispatches completed by the command processor "
-      "(CPC_ADC_DISPATCH_ALLOC_DONE, max over XCCs; --pmc-set …+dispatch); rate() = kernels/s, every process.",
-      source="counters", tier="pmc"),
     F("amdgpu_mfma_util_percent", "gauge", "Matrix-core busy % of active cycles (window).", source="counters",
       tier="pmc"),
     F("amdgpu_gpu_active_seconds_total", "counter",
@@ -190,12 +187,6 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_quiet", "gauge", "1 while the last counter READ interval saw no wave and no MFMA cycle: READs drop to "
       "--pmc-idle-hz so the exporter's own packets do not read as GPU activity.", source="self"),
     F("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU.",
-      source="self"),
-    F("kgs_pmc_cpbound", "gauge", "1 while the GPU is dispatch-bound (≥ --pmc-cpbound-dispatch-hz kernel "
-      "dispatches/s in the last READ interval; needs --pmc-set …+dispatch): counter READs drop to --pmc-cpbound-hz, "
-      "since each READ packet costs the command processor time a µs-kernel stream would otherwise use.",
-      source="self"),
-    F("kgs_pmc_cpbound_skips_total", "counter", "Sampler ticks that skipped their counter READ on a dispatch-bound GPU.",
       source="self"),
     F("kgs_pmc_failed", "gauge", "1 while the counter tier's circuit breaker is open: --pmc-breaker-k consecutive "
       "counter drains failed (a wedged command processor).  READs stop; after --pmc-retry-s (doubling to "

@@ -35,12 +35,7 @@ enum PmcIndex : int {
   kPmcGrbmActive = 1,     // GRBM_SPI_BUSY (max over XCC): clocks a shader engine had waves to run
   kPmcMfmaBusy = 2,       // SQ_VALU_MFMA_BUSY_CYCLES (sum over SIMDs)
   kPmcTaBusy = 3,         // TA_TA_BUSY (mean over TA instances): vector-memory address unit busy cycles
-  // CPC_ADC_DISPATCH_ALLOC_DONE (max over XCC): kernel dispatches the command
-  // processor's dispatch controller completed.  Counts the workload's dispatches,
-  // not our PM4 READ packets: the dispatch-bound ("CP-bound") signal of the
-  // adaptive READ rate (SamplerConfig::pmc_cpbound_dispatch_hz).
-  kPmcCpDispatch = 4,
-  kPmcCount = 5,
+  kPmcCount = 4,
   // TD_TD_BUSY tracks TA_TA_BUSY on every load tried and doubles the drain cost
   // (288 more instances, ≈+110 µs per read), so it is not in the default set.
 };
@@ -73,16 +68,12 @@ int pmc_counter_reduce(int idx);
 // the adaptive READ rate (SamplerConfig::pmc_idle_hz).
 constexpr uint32_t kPmcSetBase = (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcMfmaBusy);
 constexpr uint32_t kPmcSetFull = kPmcSetBase | (1u << kPmcTaBusy);
-constexpr uint32_t kPmcDispatchBit = 1u << kPmcCpDispatch;
-// "base" | "full", optionally "+dispatch" (the CP dispatch counter) → mask; 0 for
-// an unknown name.
+// "base" | "full" → mask; 0 for an unknown name.
 uint32_t pmc_set_mask(const std::string& name);
 
 // Derived quantities over an interval between two cumulative samples.
 struct PmcRates {
   bool have_vmem = false;        // TA counter in the set
-  bool have_dispatch = false;    // CP dispatch counter in the set
-  double dispatch_per_s = 0;     // kernel dispatches per second (CPC_ADC_DISPATCH_ALLOC_DONE)
   double gpu_active_pct = 0;     // 100 * ΔSPI_BUSY / ΔGRBM_COUNT (READ-immune)
   // 100 * ΔMFMA_BUSY / (ΔSPI_BUSY * SIMD_NUM): MFMA share of the SIMD cycles while a
   // shader engine had waves.  Not rocprofv3's MfmaUtil (that divides by
@@ -154,9 +145,6 @@ struct MockPmcConfig {
   double hang_timeout_s = 0.25;
   bool hang_heals_on_reset = false;  // reset() clears the hang (the recreated queue works)
   int acquire_fail_dev = -1;    // acquire() fails on this device while its hang is active
-  // Kernel dispatches per second of busy time (CPC dispatch counter): a square-wave
-  // load with a high value is a dispatch-bound workload (tests of the CP-bound rate).
-  double dispatch_per_busy_s = 0;
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,

@@ -79,15 +79,6 @@ struct SamplerConfig {
   // idle stretches drops.  0 = READ every tick (profiling mode: full resolution,
   // and the PMFW GFX busy reads the READs as work).
   double pmc_idle_hz = 100.0;
-  // CP-bound READ rate.  A READ is a packet the command processor handles between
-  // the workload's dispatches: on a dispatch-bound stream (µs kernels back to back)
-  // each READ costs that stream ≈2 µs at 8 kHz (profiles/launch_overhead.md).  With
-  // the CP dispatch counter in the set (--pmc-set base+dispatch), an interval that
-  // dispatched ≥ pmc_cpbound_dispatch_hz kernels/s puts the device in "CP-bound"
-  // mode: READs drop to pmc_cpbound_hz until the rate falls under half the
-  // threshold.  Long kernels (MFMA / HBM-bound work) keep every tick.  0 = off.
-  double pmc_cpbound_dispatch_hz = 100000.0;
-  double pmc_cpbound_hz = 1000.0;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
   // Counter-tier circuit breaker: consecutive failed drains that open it, and the
@@ -156,9 +147,6 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
   std::atomic<int> pmc_quiet{0};            // last READ interval had no wave: READs at pmc_idle_hz
   std::atomic<uint64_t> pmc_quiet_skips{0};  // ticks that skipped their READ while quiet
-  std::atomic<int> pmc_cpbound{0};          // dispatch-bound: READs at pmc_cpbound_hz
-  std::atomic<uint64_t> pmc_cpbound_skips{0};  // ticks that skipped their READ while CP-bound
-  std::atomic<double> dispatch_per_s{0.0};  // last READ interval's kernel dispatch rate (dispatch counter)
   // Counter-tier fault boundary (sampler.h header comment).
   std::atomic<int> pmc_failed{0};            // breaker open: no READs until a retry succeeds
   std::atomic<uint64_t> pmc_breaker_trips{0};

@@ -61,7 +61,6 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.hang_timeout_s = get<double>(m, "hang_timeout_s", c.mock_pmc.hang_timeout_s);
     c.mock_pmc.hang_heals_on_reset = get<bool>(m, "hang_heals_on_reset", c.mock_pmc.hang_heals_on_reset);
     c.mock_pmc.acquire_fail_dev = get<int>(m, "acquire_fail_dev", c.mock_pmc.acquire_fail_dev);
-    c.mock_pmc.dispatch_per_busy_s = get<double>(m, "dispatch_per_busy_s", c.mock_pmc.dispatch_per_busy_s);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -74,8 +73,6 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmc_reclaim_s = get<double>(d, "pmc_reclaim_s", c.sampler.pmc_reclaim_s);
   c.sampler.pmc_refresh_s = get<double>(d, "pmc_refresh_s", c.sampler.pmc_refresh_s);
   c.sampler.pmc_idle_hz = get<double>(d, "pmc_idle_hz", c.sampler.pmc_idle_hz);
-  c.sampler.pmc_cpbound_dispatch_hz = get<double>(d, "pmc_cpbound_dispatch_hz", c.sampler.pmc_cpbound_dispatch_hz);
-  c.sampler.pmc_cpbound_hz = get<double>(d, "pmc_cpbound_hz", c.sampler.pmc_cpbound_hz);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
   c.sampler.pmc_breaker_k = get<int>(d, "pmc_breaker_k", c.sampler.pmc_breaker_k);
   c.sampler.pmc_retry_s = get<double>(d, "pmc_retry_s", c.sampler.pmc_retry_s);
@@ -257,9 +254,6 @@ class PyExporter {
     o["slow_read_seconds"] = st.slow_ns_total.load() * 1e-9;
     o["pmc_quiet"] = st.pmc_quiet.load();
     o["pmc_quiet_skips"] = st.pmc_quiet_skips.load();
-    o["pmc_cpbound"] = st.pmc_cpbound.load();
-    o["pmc_cpbound_skips"] = st.pmc_cpbound_skips.load();
-    o["dispatch_per_s"] = st.dispatch_per_s.load();
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
     o["pmc_on"] = st.pmc_on.load();
@@ -306,7 +300,6 @@ class PyExporter {
       if (r.have_vmem) o["vmem_busy_pct"] = r.vmem_busy_pct;
       o["gpu_clock_mhz"] = r.gpu_clock_mhz;
       o["pmc_dt_s"] = r.dt_s;
-      if (r.have_dispatch) o["dispatch_per_s"] = r.dispatch_per_s;
       if (r.n_xcd > 0) {
         o["xcd_mfma_util_pct"] = std::vector<double>(r.xcd_mfma_util_pct, r.xcd_mfma_util_pct + r.n_xcd);
         o["xcd_active_pct"] = std::vector<double>(r.xcd_active_pct, r.xcd_active_pct + r.n_xcd);

@@ -18,9 +18,9 @@ namespace kgs {
 
 namespace {
 const char* const kNames[kPmcCount] = {
-    "GRBM_COUNT", "GRBM_SPI_BUSY", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY", "CPC_ADC_DISPATCH_ALLOC_DONE",
+    "GRBM_COUNT", "GRBM_SPI_BUSY", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY",
 };
-const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg, kReduceMax};
+const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg};
 
 int64_t mono_ns() {
   timespec ts;
@@ -33,15 +33,8 @@ const char* pmc_counter_name(int idx) { return (idx >= 0 && idx < kPmcCount) ? k
 int pmc_counter_reduce(int idx) { return (idx >= 0 && idx < kPmcCount) ? kReduce[idx] : kReduceSum; }
 
 uint32_t pmc_set_mask(const std::string& name) {
-  std::string n = name;
-  uint32_t extra = 0;
-  const size_t plus = n.find("+dispatch");
-  if (plus != std::string::npos && plus + 9 == n.size()) {
-    extra = kPmcDispatchBit;
-    n.resize(plus);
-  }
-  if (n == "base" || n.empty()) return kPmcSetBase | extra;
-  if (n == "full") return kPmcSetFull | extra;
+  if (name == "base" || name.empty()) return kPmcSetBase;
+  if (name == "full") return kPmcSetFull;
   return 0;
 }
 
@@ -65,8 +58,6 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
     if (r.have_vmem) r.vmem_busy_pct = std::min(100.0, 100.0 * d(kPmcTaBusy) / act);
   }
   r.gpu_clock_mhz = cnt / dt * 1e-6;
-  r.have_dispatch = (a.mask & b.mask & kPmcDispatchBit) != 0;
-  if (r.have_dispatch) r.dispatch_per_s = d(kPmcCpDispatch) / dt;
   const uint32_t nx = std::min(a.n_xcd, b.n_xcd);
   if (nx > 0 && nx <= static_cast<uint32_t>(kMaxXcc) && a.n_xcd == b.n_xcd) {
     r.n_xcd = static_cast<int>(nx);
@@ -161,7 +152,6 @@ class MockCounterSource final : public CounterSource {
     s.value[kPmcGrbmActive] = static_cast<uint64_t>(clk * busy_s);
     s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
     s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac);
-    s.value[kPmcCpDispatch] = static_cast<uint64_t>(busy_s * c_.dispatch_per_busy_s);
     s.mask = c_.mask;
     for (int i = 0; i < kPmcCount; ++i)
       if (!(s.mask & (1u << i))) s.value[i] = 0;

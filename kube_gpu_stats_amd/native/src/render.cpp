@@ -609,16 +609,6 @@ void Exporter::render(std::string& out) {
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
     w.head("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy percent of active cycles over the window");
     for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_vmem) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
-    bool any_dc = false;
-    for (int d : ids) any_dc |= snaps[d].pmc_have && (snaps[d].p.mask & kPmcDispatchBit);
-    if (any_dc) {
-      w.head("amdgpu_kernel_dispatches_total", "counter",
-             "Kernel dispatches the command processor completed (CPC_ADC_DISPATCH_ALLOC_DONE, max over XCCs), "
-             "cumulative; rate() = kernels launched per second on the GPU, every process");
-      for (int d : ids)
-        if (snaps[d].pmc_have && (snaps[d].p.mask & kPmcDispatchBit))
-          w.line_u("amdgpu_kernel_dispatches_total", dev_labels_[d], nullptr, snaps[d].p.value[kPmcCpDispatch]);
-    }
     w.head("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT over the window");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_clock_effective_mhz", dev_labels_[d], nullptr, snaps[d].r.gpu_clock_mhz);
     bool any_xcd = false;
@@ -737,17 +727,6 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_quiet", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_quiet.load()));
     w.head("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU");
     for (int d : ids) w.line_u("kgs_pmc_quiet_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_quiet_skips.load());
-    bool any_disp = false;
-    for (int d : ids) any_disp |= snaps[d].pmc_have && (snaps[d].p.mask & kPmcDispatchBit);
-    if (any_disp) {
-      w.head("kgs_pmc_cpbound", "gauge",
-             "1 while the GPU is dispatch-bound (>= --pmc-cpbound-dispatch-hz kernel dispatches/s in the last READ "
-             "interval): counter READs drop to --pmc-cpbound-hz, because each READ costs the command processor time "
-             "a dispatch-bound stream would otherwise use");
-      for (int d : ids) w.line_u("kgs_pmc_cpbound", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_cpbound.load()));
-      w.head("kgs_pmc_cpbound_skips_total", "counter", "Sampler ticks that skipped their counter READ on a dispatch-bound GPU");
-      for (int d : ids) w.line_u("kgs_pmc_cpbound_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_cpbound_skips.load());
-    }
     w.head("kgs_pmc_failed", "gauge",
            "1 while the counter tier's circuit breaker is open: consecutive counter drains failed (a wedged command "
            "processor); READs stop, the reader's queue is recreated and re-STARTed with exponential backoff");

@@ -470,9 +470,8 @@ void Sampler::run_pmc(Worker& w) {
   int64_t next = mono_ns();
   PmcSample& pmc_base = st.pmc_base;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
-  uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0, prev_ps_disp = 0;
+  uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0;
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
-  bool cpbound = false;              // dispatch-bound READ rate (SamplerConfig::pmc_cpbound_*)
   int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
   int64_t last_pmc_ns = 0;
@@ -483,10 +482,9 @@ void Sampler::run_pmc(Worker& w) {
   // READ is then counted exactly (acquire → first READ was dropped).
   auto started_at = [&](int64_t t) {
     have_prev_ps = true;
-    prev_ps_count = prev_ps_mfma = prev_ps_active = prev_ps_disp = 0;
+    prev_ps_count = prev_ps_mfma = prev_ps_active = 0;
     prev_ps_ns = t;
     quiet = false;
-    cpbound = false;
     quiet_since_ns = 0;
     fresh_mode = false;  // a (re)opened session reads pipelined
     last_plausible_ns = t;
@@ -556,12 +554,6 @@ void Sampler::run_pmc(Worker& w) {
         pmc_now = false;
         st.pmc_quiet_skips.fetch_add(1, std::memory_order_relaxed);
       }
-    } else if (pmc_now && cpbound) {
-      const double cb_hz = cfg_.pmc_cpbound_hz;
-      if (cb_hz > 0 && cb_hz < hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / cb_hz)) {
-        pmc_now = false;
-        st.pmc_cpbound_skips.fetch_add(1, std::memory_order_relaxed);
-      }
     }
     if (pmc_now) {
       PmcSample ps;
@@ -615,23 +607,9 @@ void Sampler::run_pmc(Worker& w) {
         }
         quiet = quiet_interval && ps.mono_ns - quiet_since_ns >= kQuietHoldNs;
         st.pmc_quiet.store(quiet ? 1 : 0, std::memory_order_relaxed);
-        // CP-bound: the interval dispatched kernels at ≥ the threshold rate (with
-        // hysteresis: it ends below half of it).  Only with the dispatch counter.
-        if (have_prev_ps && (ps.mask & kPmcDispatchBit) && ps.mono_ns > prev_ps_ns) {
-          const double disp = static_cast<double>(ps.value[kPmcCpDispatch] -
-                                                  std::min(ps.value[kPmcCpDispatch], prev_ps_disp));
-          const double dps = disp * 1e9 / static_cast<double>(ps.mono_ns - prev_ps_ns);
-          st.dispatch_per_s.store(dps, std::memory_order_relaxed);
-          const double thr = cfg_.pmc_cpbound_dispatch_hz;
-          cpbound = thr > 0 && !quiet && dps >= (cpbound ? 0.5 * thr : thr);
-        } else {
-          cpbound = false;
-        }
-        st.pmc_cpbound.store(cpbound ? 1 : 0, std::memory_order_relaxed);
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
-          const bool slow = (quiet && idle_hz > 0 && idle_hz < hz) ||
-                            (cpbound && cfg_.pmc_cpbound_hz > 0 && cfg_.pmc_cpbound_hz < hz);
+          const bool slow = quiet && idle_hz > 0 && idle_hz < hz;
           if (slow != fresh_mode) {
             src->set_fresh(dev, slow);
             if (gone()) return;
@@ -641,7 +619,6 @@ void Sampler::run_pmc(Worker& w) {
         prev_ps_count = ps.value[kPmcGrbmCount];
         prev_ps_mfma = ps.value[kPmcMfmaBusy];
         prev_ps_active = ps.value[kPmcGrbmActive];
-        prev_ps_disp = ps.value[kPmcCpDispatch];
         prev_ps_ns = ps.mono_ns;
         have_prev_ps = true;
         const int64_t stall = ps.mono_ns - last_plausible_ns;

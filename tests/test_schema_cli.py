@@ -19,7 +19,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_rendered_families_match_catalog(mock_exporter):
     from kube_gpu_stats_amd.attribution.attributor import Attributor
 
-    ex = mock_exporter(n_gpus=3, pmc_source="mock", pmc_set="full+dispatch", proc_every=1, link_every=1)
+    ex = mock_exporter(n_gpus=3, pmc_source="mock", pmc_set="full", proc_every=1, link_every=1)
     ex.set_device_owners(0, [{"pod": "p", "namespace": "n", "container": "c"}])
     time.sleep(0.4)
     Attributor(ex, socket_path=None).publish()

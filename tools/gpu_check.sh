@@ -26,6 +26,9 @@ for s in $STEPS; do
             run perf_pmu 90 python tools/perf_pmu_probe.py --out "$OUT/perf_pmu.json"
             KGS_AQL_PROBE_OUT="$OUT/aql_probe_cp.json" run aql_probe_cp 400 python -u tools/aql_probe.py \
               cpc_dispatch,cpc_busy,cpc_gd,grbm_cp,spi_csn ;;
+    bench3) run bench3 600 python -u bench.py --steps 20 --warmup 5 --pmc-lean 3 --out "$OUT/bench3.json" ;;
+    train3) run train3 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
+              --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 3 --out "$OUT/train3.json" ;;
     trainpmfw) run trainpmfw 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc none --out "$OUT/trainpmfw.json" ;;
     train2) run train2 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
