@@ -738,3 +738,31 @@ def test_short_idle_gaps_do_not_drop_to_the_idle_rate(mock_exporter):
                              mock={"square_duty": 0.5, "util_period_s": 0.05, "util_base": 50, "util_amp": 50})
     time.sleep(0.3)
     assert skips_per_s(long_gap) > 200                   # 25 ms gaps: ≈20 ms of each at the idle rate
+
+
+def test_mock_peer_copy_lands_on_the_link_to_that_peer(mock_exporter):
+    """a simulated GPU 0 → GPU 3 copy must move exactly the link whose
+    /topology peer_bdf is GPU 3 on the source (write) and the link back to GPU 0 on
+    the destination (read), by the copied bytes (default unit: KB accumulators)."""
+    ex = mock_exporter(n_gpus=8, pmfw_hz=200, link_every=1, mock={"xgmi_bg": False, "fw_period_s": 0.005})
+    time.sleep(0.2)
+    bdf = {int(d["gpu"]): d["bdf"] for d in json.load(get(ex.port, "/devices"))}
+    peer = {(int(x["gpu"]), int(x["link"])): x.get("peer_bdf", "") for x in json.load(get(ex.port, "/topology"))["links"]}
+
+    def links(fam):
+        return {(int(lb["gpu"]), int(lb["link"])): v for lb, v in parse_text(ex.render()).get(fam, [])}
+
+    w0, r0 = links("amdgpu_xgmi_write_bytes_total"), links("amdgpu_xgmi_read_bytes_total")
+    nbytes = 256 << 20
+    assert ex.inject_xgmi(0, 3, nbytes) == 0
+    assert ex.inject_xgmi(0, 0, nbytes) != 0  # no link to itself
+    time.sleep(0.2)
+    w1, r1 = links("amdgpu_xgmi_write_bytes_total"), links("amdgpu_xgmi_read_bytes_total")
+    dw = {k: w1[k] - w0.get(k, 0.0) for k in w1 if w1[k] != w0.get(k, 0.0)}
+    dr = {k: r1[k] - r0.get(k, 0.0) for k in r1 if r1[k] != r0.get(k, 0.0)}
+    assert len(dw) == 1 and len(dr) == 1, (dw, dr)
+    (src_key, src_b), = dw.items()
+    (dst_key, dst_b), = dr.items()
+    assert src_key[0] == 0 and peer[src_key] == bdf[3]
+    assert dst_key[0] == 3 and peer[dst_key] == bdf[0]
+    assert src_b == pytest.approx(nbytes, rel=1e-3) and dst_b == pytest.approx(nbytes, rel=1e-3)
