@@ -73,6 +73,12 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                        "command-processor packet that GFX busy / GUI-active count as work (≈80 / "
                                        "190 µs each), so a quiet GPU is read at this rate and a busy one every tick "
                                        "(0 = every tick: profiling mode)")
+    add_flag(ap, "pmc-busy-min", 0.0, "dispatch-gap READ rate: while the counter READ intervals have waves for less "
+                                      "than this share of their clocks (short kernels with dispatch gaps), READ at "
+                                      "--pmc-gap-hz, since every READ packet delays the workload's dispatches "
+                                      "(0 = off; ignored in profiling mode)")
+    add_flag(ap, "pmc-gap-hz", 1000.0, "counter READ rate in a dispatch gap (--pmc-busy-min)")
+    add_flag(ap, "pmc-gap-hold-ms", 1.0, "low-occupancy READ intervals in a row, in ms, before the gap rate applies")
     add_flag(ap, "pmc-timeout-ms", 250, "bound of every wait on the command processor (counter READ, START, STOP, "
                                         "queue slot): a wedged CP costs one timeout, never a hang")
     add_flag(ap, "pmc-breaker-k", 3, "consecutive failed counter drains that open the counter tier's circuit breaker "
@@ -142,6 +148,9 @@ def config_from_args(a) -> dict:
         "pmc_reclaim_s": a.pmc_reclaim_s,
         "pmc_refresh_s": a.pmc_refresh_s,
         "pmc_idle_hz": a.pmc_idle_hz,
+        "pmc_busy_min": a.pmc_busy_min,
+        "pmc_gap_hz": a.pmc_gap_hz,
+        "pmc_gap_hold_s": a.pmc_gap_hold_ms * 1e-3,
         "pmc_timeout_ms": a.pmc_timeout_ms,
         "pmc_breaker_k": a.pmc_breaker_k,
         "pmc_retry_s": a.pmc_retry_s,

@@ -79,6 +79,20 @@ struct SamplerConfig {
   // idle stretches drops.  0 = READ every tick (profiling mode: full resolution,
   // and the PMFW GFX busy reads the READs as work).
   double pmc_idle_hz = 100.0;
+  // Dispatch-gap READ rate.  Every READ is one more AQL packet for the command
+  // processor that also dispatches the workload's kernels, and a READ whose
+  // indirect buffer is all NOPs costs a bf16 training step as much as a real one
+  // (profiles/r3/README.md, r3e): the cost is per packet.  Long kernels hide it
+  // (SPI busy ≈97 % of the clocks, nothing to dispatch); a stream of short
+  // kernels with dispatch gaps between them does not.  While the READ intervals
+  // of the last pmc_gap_hold_s had waves for less than pmc_busy_min of their
+  // clocks, READs drop to pmc_gap_hz; the first interval at or above
+  // pmc_busy_min restores every tick.  Integrals stay exact (cumulative
+  // counters); only the time resolution of those stretches drops.  Off in
+  // profiling mode (pmc_idle_hz 0) and with pmc_busy_min 0.
+  double pmc_busy_min = 0.0;
+  double pmc_gap_hz = 1000.0;
+  double pmc_gap_hold_s = 0.001;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
   // Counter-tier circuit breaker: consecutive failed drains that open it, and the
@@ -147,6 +161,8 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
   std::atomic<int> pmc_quiet{0};            // last READ interval had no wave: READs at pmc_idle_hz
   std::atomic<uint64_t> pmc_quiet_skips{0};  // ticks that skipped their READ while quiet
+  std::atomic<int> pmc_gap{0};               // READ intervals below pmc_busy_min: READs at pmc_gap_hz
+  std::atomic<uint64_t> pmc_gap_skips{0};    // ticks that skipped their READ in a dispatch gap
   // Counter-tier fault boundary (sampler.h header comment).
   std::atomic<int> pmc_failed{0};            // breaker open: no READs until a retry succeeds
   std::atomic<uint64_t> pmc_breaker_trips{0};
@@ -228,6 +244,11 @@ class Sampler {
   // (unchanged) unless hz == 0 or kMinIdleHz <= hz <= kMaxHz.
   bool set_pmc_idle_hz(double hz);
   double pmc_idle_hz() const { return pmc_idle_hz_.load(std::memory_order_relaxed); }
+  // Dispatch-gap rate (SamplerConfig::pmc_busy_min): false (unchanged) unless
+  // 0 <= busy_min <= 1 and 0 < hz <= kMaxHz.
+  bool set_pmc_gap(double busy_min, double hz);
+  double pmc_busy_min() const { return pmc_busy_min_.load(std::memory_order_relaxed); }
+  double pmc_gap_hz() const { return pmc_gap_hz_.load(std::memory_order_relaxed); }
   // Node-wide slow thread: passes completed and whether it is running.
   uint64_t slow_passes() const { return slow_passes_.load(); }
   // Threads stop() gave up on (stuck in a device call); they are detached and
@@ -263,6 +284,8 @@ class Sampler {
   std::atomic<double> hz_{10.0};
   std::atomic<uint64_t> slow_passes_{0};
   std::atomic<double> pmc_idle_hz_{0.0};
+  std::atomic<double> pmc_busy_min_{0.0};
+  std::atomic<double> pmc_gap_hz_{1000.0};
   mutable std::mutex pid_pods_mu_;
   std::shared_ptr<const std::unordered_map<uint64_t, std::string>> pid_pods_;
   std::vector<std::map<std::string, double>> pod_cu_;  // slow thread only

@@ -73,6 +73,9 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmc_reclaim_s = get<double>(d, "pmc_reclaim_s", c.sampler.pmc_reclaim_s);
   c.sampler.pmc_refresh_s = get<double>(d, "pmc_refresh_s", c.sampler.pmc_refresh_s);
   c.sampler.pmc_idle_hz = get<double>(d, "pmc_idle_hz", c.sampler.pmc_idle_hz);
+  c.sampler.pmc_busy_min = get<double>(d, "pmc_busy_min", c.sampler.pmc_busy_min);
+  c.sampler.pmc_gap_hz = get<double>(d, "pmc_gap_hz", c.sampler.pmc_gap_hz);
+  c.sampler.pmc_gap_hold_s = get<double>(d, "pmc_gap_hold_s", c.sampler.pmc_gap_hold_s);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
   c.sampler.pmc_breaker_k = get<int>(d, "pmc_breaker_k", c.sampler.pmc_breaker_k);
   c.sampler.pmc_retry_s = get<double>(d, "pmc_retry_s", c.sampler.pmc_retry_s);
@@ -254,6 +257,8 @@ class PyExporter {
     o["slow_read_seconds"] = st.slow_ns_total.load() * 1e-9;
     o["pmc_quiet"] = st.pmc_quiet.load();
     o["pmc_quiet_skips"] = st.pmc_quiet_skips.load();
+    o["pmc_gap"] = st.pmc_gap.load();
+    o["pmc_gap_skips"] = st.pmc_gap_skips.load();
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
     o["pmc_on"] = st.pmc_on.load();
@@ -481,6 +486,18 @@ PYBIND11_MODULE(_kgs_native, m) {
               throw py::value_error("pmc_idle_hz must be 0 or within [0.01, 100000]");
           },
           "Counter READ rate while the GPU has no wave (adaptive; 0 = every tick)")
+      .def(
+          "set_pmc_gap",
+          [](PyExporter& e, double busy_min, double hz) {
+            if (e.sampler() && !e.sampler()->set_pmc_gap(busy_min, hz))
+              throw py::value_error("busy_min must be within [0, 1] and hz within (0, 100000]");
+          },
+          py::arg("busy_min"), py::arg("hz") = 1000.0,
+          "Dispatch-gap READ rate: READs at hz while the SPI-busy share stays below busy_min (0 = off)")
+      .def_property_readonly("pmc_busy_min",
+                             [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_busy_min() : 0.0; })
+      .def_property_readonly("pmc_gap_hz",
+                             [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_gap_hz() : 0.0; })
       .def_property_readonly("slow_passes", &PyExporter::slow_passes);
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);

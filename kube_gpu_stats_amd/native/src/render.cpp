@@ -727,6 +727,12 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_quiet", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_quiet.load()));
     w.head("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU");
     for (int d : ids) w.line_u("kgs_pmc_quiet_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_quiet_skips.load());
+    w.head("kgs_pmc_gap", "gauge",
+           "1 while the counter READ intervals had waves for less than --pmc-busy-min of their clocks (a dispatch-bound "
+           "or gappy kernel stream): READs run at --pmc-gap-hz, since each READ packet delays the workload's dispatches");
+    for (int d : ids) w.line_u("kgs_pmc_gap", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_gap.load()));
+    w.head("kgs_pmc_gap_skips_total", "counter", "Sampler ticks that skipped their counter READ in a dispatch gap");
+    for (int d : ids) w.line_u("kgs_pmc_gap_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_gap_skips.load());
     w.head("kgs_pmc_failed", "gauge",
            "1 while the counter tier's circuit breaker is open: consecutive counter drains failed (a wedged command "
            "processor); READs stop, the reader's queue is recreated and re-STARTed with exponential backoff");

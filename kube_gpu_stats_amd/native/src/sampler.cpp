@@ -101,6 +101,8 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
   if (cfg_.pmc_retry_max_s < cfg_.pmc_retry_s) cfg_.pmc_retry_max_s = cfg_.pmc_retry_s;
   const double ih = cfg_.pmc_idle_hz;
   pmc_idle_hz_.store(!(ih > 0) ? 0.0 : std::clamp(ih, kMinIdleHz, kMaxHz));
+  if (!set_pmc_gap(cfg_.pmc_busy_min, cfg_.pmc_gap_hz)) set_pmc_gap(0.0, 1000.0);
+  if (!(cfg_.pmc_gap_hold_s >= 0)) cfg_.pmc_gap_hold_s = 0.0;
   for (int d : dev_ids_) {
     DeviceState& st = *states_[static_cast<size_t>(d)];
     st.pmc_on.store(cfg_.pmc && pmc_ ? 1 : 0);
@@ -125,6 +127,13 @@ bool Sampler::set_hz(double hz) {
 bool Sampler::set_pmc_idle_hz(double hz) {
   if (!(hz == 0 || (hz >= kMinIdleHz && hz <= kMaxHz))) return false;
   pmc_idle_hz_.store(hz, std::memory_order_relaxed);
+  return true;
+}
+
+bool Sampler::set_pmc_gap(double busy_min, double hz) {
+  if (!(busy_min >= 0 && busy_min <= 1 && hz > 0 && hz <= kMaxHz)) return false;
+  pmc_busy_min_.store(busy_min, std::memory_order_relaxed);
+  pmc_gap_hz_.store(hz, std::memory_order_relaxed);
   return true;
 }
 
@@ -467,6 +476,8 @@ void Sampler::run_pmc(Worker& w) {
     if (gone()) return;
   }
   st.pmc_quiet.store(0, std::memory_order_relaxed);
+  st.pmc_gap.store(0, std::memory_order_relaxed);
+  const int64_t gap_hold_ns = static_cast<int64_t>(cfg_.pmc_gap_hold_s * 1e9);
   int64_t next = mono_ns();
   PmcSample& pmc_base = st.pmc_base;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
@@ -474,6 +485,8 @@ void Sampler::run_pmc(Worker& w) {
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
   int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
+  bool gap = false;                  // dispatch-gap READ rate (SamplerConfig::pmc_busy_min)
+  int64_t gap_since_ns = 0;          // start of the current run of low-occupancy intervals (0 = none)
   int64_t last_pmc_ns = 0;
   int64_t prev_ps_ns = 0;
   int64_t last_plausible_ns = mono_ns();
@@ -486,6 +499,8 @@ void Sampler::run_pmc(Worker& w) {
     prev_ps_ns = t;
     quiet = false;
     quiet_since_ns = 0;
+    gap = false;
+    gap_since_ns = 0;
     fresh_mode = false;  // a (re)opened session reads pipelined
     last_plausible_ns = t;
     last_start_ns = t;
@@ -504,6 +519,7 @@ void Sampler::run_pmc(Worker& w) {
     st.pmc_on.store(0);
     st.pmc_stalled.store(0);
     st.pmc_quiet.store(0, std::memory_order_relaxed);
+    st.pmc_gap.store(0, std::memory_order_relaxed);
     st.pmc_fail_streak = 0;
     st.pmc_retry_at_ns = now + static_cast<int64_t>(st.pmc_backoff_s * 1e9);
     st.pmc_backoff_s = std::min(st.pmc_backoff_s * 2, cfg_.pmc_retry_max_s);
@@ -548,11 +564,14 @@ void Sampler::run_pmc(Worker& w) {
       }
     }
     bool pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
-    if (pmc_now && quiet) {
+    if (pmc_now && (quiet || gap)) {
+      // Quiet (no waves) READs at the idle rate, a dispatch gap at the gap rate;
+      // profiling mode (idle rate 0) READs every tick.
       const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
-      if (idle_hz > 0 && idle_hz < hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / idle_hz)) {
+      const double slow_hz = quiet ? idle_hz : pmc_gap_hz_.load(std::memory_order_relaxed);
+      if (idle_hz > 0 && slow_hz < hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / slow_hz)) {
         pmc_now = false;
-        st.pmc_quiet_skips.fetch_add(1, std::memory_order_relaxed);
+        (quiet ? st.pmc_quiet_skips : st.pmc_gap_skips).fetch_add(1, std::memory_order_relaxed);
       }
     }
     if (pmc_now) {
@@ -594,11 +613,16 @@ void Sampler::run_pmc(Worker& w) {
         // (nearly) blind to our own READs: SPI busy reads 0.65 % with nothing but
         // 8 kHz of READs on the GPU (profiles/r2/immunity/).
         // Without the activity counter in the set a device is never quiet.
-        bool quiet_interval = false;
+        // A dispatch gap: the same share below pmc_busy_min (quiet intervals
+        // included, so an idle stretch between short kernels does not restart
+        // the hold).
+        bool quiet_interval = false, gap_interval = false;
         if (have_prev_ps && (ps.mask & (1u << kPmcGrbmActive)) && ps.value[kPmcGrbmCount] > prev_ps_count) {
           const double act = static_cast<double>(ps.value[kPmcGrbmActive] - std::min(ps.value[kPmcGrbmActive], prev_ps_active));
           const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
           quiet_interval = act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma;
+          const double busy_min = pmc_busy_min_.load(std::memory_order_relaxed);
+          gap_interval = busy_min > 0 && act < busy_min * clk;
         }
         if (!quiet_interval) {
           quiet_since_ns = 0;
@@ -607,6 +631,13 @@ void Sampler::run_pmc(Worker& w) {
         }
         quiet = quiet_interval && ps.mono_ns - quiet_since_ns >= kQuietHoldNs;
         st.pmc_quiet.store(quiet ? 1 : 0, std::memory_order_relaxed);
+        if (!gap_interval) {
+          gap_since_ns = 0;
+        } else if (gap_since_ns == 0) {
+          gap_since_ns = prev_ps_ns;
+        }
+        gap = gap_interval && !quiet && ps.mono_ns - gap_since_ns >= gap_hold_ns;
+        st.pmc_gap.store(gap ? 1 : 0, std::memory_order_relaxed);
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
           const bool slow = quiet && idle_hz > 0 && idle_hz < hz;

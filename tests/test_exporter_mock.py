@@ -5,6 +5,7 @@ import json
 import math
 import os
 import time
+import urllib.error
 import urllib.request
 
 import pytest
@@ -569,6 +570,48 @@ def test_quiet_gpu_counter_reads_drop_to_idle_rate(mock_exporter):
     assert 0.25 * 2000 * 0.6 <= r_sq <= 0.25 * 2000 + 0.75 * 50 + 150, r_sq
     w = sq.window(0, 1.2)
     assert w["gpu_active_pct"] == pytest.approx(25, abs=4), w      # the integral is exact at any READ rate
+
+
+def test_dispatch_gap_reads_drop_to_gap_rate(mock_exporter):
+    """Dispatch-gap READ rate (--pmc-busy-min): each READ packet delays the workload's
+    dispatches, and a READ whose IB is all NOPs costs a training step as much as a
+    real one (profiles/r3/README.md, r3e).  While the READ intervals show waves for
+    less than busy_min of the clocks, READs drop to the gap rate; a share at or
+    above busy_min, or profiling mode, READs every tick.  Integrals stay exact."""
+    def rate(ex, secs=1.0):
+        n0 = ex.integrals(0)["pmc_samples"]
+        time.sleep(secs)
+        return (ex.integrals(0)["pmc_samples"] - n0) / secs
+
+    ex = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=50,
+                       window_s=1.0, mock={"util_base": 50, "util_amp": 0})   # 50 % SPI-busy share
+    time.sleep(0.2)
+    assert ex.pmc_busy_min == 0 and rate(ex, 0.5) > 1400                  # off by default: every tick
+    ex.set_pmc_gap(0.9, 200)
+    time.sleep(0.05)
+    r_gap = rate(ex)
+    assert 150 <= r_gap <= 260, r_gap                                   # ≈ the gap rate, not 2000
+    m = parse_text(ex.render())
+    assert m["kgs_pmc_gap"][0][1] == 1 and m["kgs_pmc_gap_skips_total"][0][1] > 1000
+    assert m["kgs_pmc_quiet"][0][1] == 0
+    w = ex.window(0, 1.0)
+    assert w["gpu_active_pct"] == pytest.approx(50, abs=4), w             # exact at any READ rate
+    ex.set_pmc_gap(0.3, 200)                                            # 50 % ≥ 30 %: every tick again
+    time.sleep(0.05)
+    assert rate(ex, 0.5) > 1400
+    assert ex.integrals(0)["pmc_gap"] == 0
+    with urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/gap?min=0.9&hz=200", timeout=5) as r:
+        assert json.load(r) == {"pmc_busy_min": 0.9, "pmc_gap_hz": 200.0}
+    ex.pmc_idle_hz = 0                                                  # profiling mode overrides it
+    time.sleep(0.05)
+    assert rate(ex, 0.5) > 1400
+    for bad in ("min=1.5", "min=-0.5", "min=0.5&hz=0"):
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/gap?{bad}", timeout=5)
+        assert e.value.code == 400, bad
+    with pytest.raises(ValueError):
+        ex.set_pmc_gap(2.0)
+    assert ex.pmc_busy_min == 0.9 and ex.pmc_gap_hz == 200
 
 
 def test_throttle_seconds_by_reason(mock_exporter):

@@ -33,6 +33,23 @@ for s in $STEPS; do
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc none --out "$OUT/trainpmfw.json" ;;
     train2) run train2 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 2 --out "$OUT/train2.json" ;;
+    tdef|tpmfw|tagent|tl3agent|tnop|t1k|tgap*)
+        # training-step side runs, 36 rounds = every block order 6 times:
+        #   tdef (defaults) tpmfw (no READs) tagent (release fence at agent scope)
+        #   tl3agent (lean 3 + agent release) tnop (every READ packet a NOP: the bare
+        #   packet's cost; values stale) t1k (1 kHz tier) tgapNN (--pmc-busy-min 0.NN)
+        T=(python -u bench.py --load train --steps 10 --warmup 2 --rounds 36 --hz-list 100 --capacity-hz ""
+           --burst-s 0 --quiet-s 0 --component-s 0 --out "$OUT/$s.json")
+        case $s in
+          tdef) run $s 600 "${T[@]}" ;;
+          tpmfw) run $s 600 "${T[@]}" --pmc none ;;
+          tagent) KGS_AQL_FENCE=none,agent run $s 600 "${T[@]}" ;;
+          tl3agent) KGS_AQL_FENCE=none,agent KGS_AQL_LEAN=3 run $s 600 "${T[@]}" ;;
+          tnop) KGS_AQL_LEAN=5 run $s 600 "${T[@]}" ;;
+          t1k) run $s 600 "${T[@]}" --hz 1000 ;;
+          tgap*) run $s 600 "${T[@]}" --pmc-busy-min "0.${s#tgap}" ;;  # tgap90: --pmc-busy-min 0.90
+        esac ;;
+    bgap*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-busy-min "0.${s#bgap}" --out "$OUT/$s.json" ;;
     probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
            run probe_xgmi 90 python tools/probe_xgmi.py ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider ;;
