@@ -116,7 +116,8 @@ def pmc_control(a) -> int:
         return 0
     body = urllib.request.urlopen(f"http://{a.exporter}/metrics", timeout=10).read().decode()
     print("\n".join(ln for ln in body.splitlines()
-                    if ln.startswith(("kgs_pmc_enabled", "kgs_pmc_stalled", "kgs_pmc_failed", "kgs_sampler_thread_hung"))
+                    if ln.startswith(("kgs_pmc_enabled", "kgs_pmc_stalled", "kgs_pmc_failed", "kgs_pmc_quiet ",
+                                       "kgs_pmc_quiet{", "kgs_pmc_gap ", "kgs_pmc_gap{", "kgs_sampler_thread_hung"))
                     and (a.gpu < 0 or f'gpu="{a.gpu}"' in ln)))
     return 0
 
