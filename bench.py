@@ -89,9 +89,8 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-busy-min", type=float, default=0.0,
                     help="exporter --pmc-busy-min: READ at --pmc-gap-hz while the SPI-busy share is below this")
     ap.add_argument("--pmc-gap-hz", type=float, default=1000.0, help="exporter --pmc-gap-hz")
-    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3, 7, 8],
-                    help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it; "
-                         "7/8 = results written around the L2, no release fence)")
+    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
+                    help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=20.0)
     ap.add_argument("--step-ms", type=float, default=500.0,
                     help="each step repeats the load unit until it lasts at least this long")

@@ -127,11 +127,6 @@ struct Agent {
   hsa_ext_amd_aql_pm4_packet_t pread[2]{};
   hsa_signal_t psig[2]{};
   uint32_t pcmd_sz = 0, pout_sz = 0;                 // allocated sizes of the slot buffers
-  // Bypass READs (lean 7/8): the COPY_DATA destinations of each slot's READ, inside
-  // pout[k].  The slot is pre-filled with kUnlanded; a READ's values are folded
-  // once none of these dwords holds it any more.
-  std::vector<volatile uint32_t*> pdst[2];
-  std::atomic<uint64_t> land_waits{0}, land_timeouts{0};  // collections that had to wait / gave up waiting
   std::vector<hsa_ven_amd_aqlprofile_event_t> pipe_events;  // event list the slot packets were built for
   int64_t psubmit_ns[2] = {0, 0};
   // KGS_AQL_PROFILE=<n>: CP timestamps of every pipelined READ (queue profiling on):
@@ -312,20 +307,16 @@ int parse_scope(const char* s, size_t n) {
   if (n == 5 && std::strncmp(s, "agent", 5) == 0) return static_cast<int>(HSA_FENCE_SCOPE_AGENT);
   return static_cast<int>(HSA_FENCE_SCOPE_NONE);
 }
-int lean_mode();
-// Bypass READs (lean 7/8) write their results around the L2 and are checked for
-// arrival on the host, so they need no release fence either (see lean_read_ib).
 std::pair<int, int> read_fences() {
-  static const char* e = std::getenv("KGS_AQL_FENCE");
-  if (!e) {
-    const int rel = lean_mode() >= 7 ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_SYSTEM;
-    return std::make_pair(static_cast<int>(HSA_FENCE_SCOPE_NONE), rel);
-  }
-  const char* c = std::strchr(e, ',');
-  if (!c) return std::make_pair(parse_scope(e, std::strlen(e)), parse_scope(e, std::strlen(e)));
-  return std::make_pair(parse_scope(e, static_cast<size_t>(c - e)), parse_scope(c + 1, std::strlen(c + 1)));
+  static const std::pair<int, int> v = [] {
+    const char* e = std::getenv("KGS_AQL_FENCE");
+    if (!e) return std::make_pair(static_cast<int>(HSA_FENCE_SCOPE_NONE), static_cast<int>(HSA_FENCE_SCOPE_SYSTEM));
+    const char* c = std::strchr(e, ',');
+    if (!c) return std::make_pair(parse_scope(e, std::strlen(e)), parse_scope(e, std::strlen(e)));
+    return std::make_pair(parse_scope(e, static_cast<size_t>(c - e)), parse_scope(c + 1, std::strlen(c + 1)));
+  }();
+  return v;
 }
-constexpr uint32_t kUnlanded = 0xFFFFFFFFu;  // pre-fill of a bypass READ's output slot
 constexpr std::pair<int, int> kSystemFences{HSA_FENCE_SCOPE_SYSTEM, HSA_FENCE_SCOPE_SYSTEM};
 
 // Completion signals of the pipelined READ slots (KGS_AQL_SIGNAL = interrupt |
@@ -546,19 +537,8 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
 // 2 (default) = 1 + ACQUIRE_MEM reduced to the L2 writeback that publishes the
 // CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Cost-attribution modes
 // (KGS_AQL_LEAN only; the counter values they return are stale): 4 = 3 + no
-// COPY_DATA, 5 = every packet of the IB a NOP.
-// Bypass modes 7 / 8 = 3 + every COPY_DATA to memory with its destination cache
-// policy set to 2 / 3 (bits 26:25; aqlprofile builds 1, "stream").  Why: the
-// results land in fine-grained host memory that the GPU's L2 caches, so a READ
-// must end with an L2 writeback (the in-IB ACQUIRE_MEM or a release fence) before
-// the host can see them, and that writeback cleans every dirty line of every XCD's
-// L2 at 8 kHz — a cost to whatever work shares the GPU, even with an all-NOP IB
-// (profiles/r3/README.md, r3e).  Written around the L2 the results need neither;
-// the host checks that every destination dword has changed from kUnlanded before
-// it folds them.  `dsts` (modes 7/8) receives the destination dwords that lie in
-// [out, out + out_sz).  Returns packets changed.
-int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<volatile uint32_t*>* dsts = nullptr,
-                 const void* out = nullptr, size_t out_sz = 0) {
+// COPY_DATA, 5 = every packet of the IB a NOP.  Returns packets changed.
+int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
   if (mode <= 0) return 0;
   uint32_t dw[4];
   std::memcpy(dw, pkt.pm4_command + 1, sizeof dw);
@@ -573,18 +553,11 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<
     if ((h >> 30) == 2) { ++i; continue; }
     if ((h >> 30) != 3) return -2;
     const uint32_t opc = (h >> 8) & 0xFF, len = ((h >> 16) & 0x3FFF) + 2;
-    if (mode == 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
+    if (mode >= 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
       if (opc != 0x10) {
         nop(i, len);
         ++changed;
       }
-    } else if (mode >= 7 && opc == 0x40 && len == 6 && ((ib[i + 1] >> 8) & 0xF) == 5) {  // COPY_DATA → memory
-      const uint32_t policy = mode == 7 ? 2u : 3u;
-      ib[i + 1] = (ib[i + 1] & ~(3u << 25)) | (policy << 25);
-      ++changed;
-      const uint64_t dst = (static_cast<uint64_t>(ib[i + 4]) | (static_cast<uint64_t>(ib[i + 5]) << 32)) & ~3ull;
-      const uint64_t lo = reinterpret_cast<uint64_t>(out);
-      if (dsts && out && dst >= lo && dst + 4 <= lo + out_sz) dsts->push_back(reinterpret_cast<volatile uint32_t*>(dst));
     } else if (opc == 0x46 && (ib[i + 1] & 0x3F) == 7) {  // EVENT_WRITE CS_PARTIAL_FLUSH
       nop(i, len);
       ++changed;
@@ -675,34 +648,6 @@ int read_values(Agent* a) {
   return fold(a, &a->prof);
 }
 
-// Bypass READ (lean 7/8) of slot k completed: wait, briefly, until every result
-// dword has arrived in host memory.  Normally they have (the READ was submitted a
-// tick ago).  A dword still at kUnlanded after 200 µs is taken as it is: a
-// counter half that really reads 0xFFFFFFFF (once in 2^32) must not stall us.
-void wait_landed(Agent* a, int k) {
-  const int64_t t0 = mono_ns();
-  bool waited = false;
-  for (;;) {
-    bool all = true;
-    for (volatile uint32_t* p : a->pdst[k])
-      if (*p == kUnlanded) {
-        all = false;
-        break;
-      }
-    if (all) break;
-    if (!waited) {
-      waited = true;
-      ++a->land_waits;
-    }
-    if (mono_ns() - t0 > 200000) {
-      ++a->land_timeouts;
-      break;
-    }
-    __builtin_ia32_pause();
-  }
-  std::atomic_thread_fence(std::memory_order_acquire);
-}
-
 // Pipelined sample: collect the READ in flight, submit the next one.  Returns the
 // collected values' estimated CP read time in *ts (submit + half a round trip).
 int read_pipelined(Agent* a, int64_t* ts) {
@@ -711,7 +656,7 @@ int read_pipelined(Agent* a, int64_t* ts) {
     const int rc = read_values(a);
     if (rc != 0) return rc;
     if (ts) *ts = t0 + a->rtt_ns / 2;
-    std::memset(a->pout[0], a->pdst[0].empty() ? 0 : 0xFF, a->pprof[0].output_buffer.size);
+    std::memset(a->pout[0], 0, a->pprof[0].output_buffer.size);
     a->psubmit_ns[0] = mono_ns();
     a->inflight = enqueue(a, a->pread[0], a->psig[0], read_fences()) == 0 ? 0 : -1;
     return 0;
@@ -752,11 +697,10 @@ int read_pipelined(Agent* a, int64_t* ts) {
       a->prof_q_sum = a->prof_q_max = a->prof_x_sum = a->prof_x_max = 0;
     }
   }
-  if (!a->pdst[k].empty()) wait_landed(a, k);
   const int rc = fold(a, &a->pprof[k]);
   if (ts) *ts = a->psubmit_ns[k] + a->rtt_ns / 2;
   const int n = k ^ 1;
-  std::memset(a->pout[n], a->pdst[n].empty() ? 0 : 0xFF, a->pprof[n].output_buffer.size);
+  std::memset(a->pout[n], 0, a->pprof[n].output_buffer.size);
   a->psubmit_ns[n] = mono_ns();
   // No slot for the next READ: these values stand, the next call primes again
   // (and fails there if the CP is still not consuming).
@@ -802,8 +746,7 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
       err = "aqlprofile pipeline packet build: " + aql_error();
       return false;
     }
-    a->pdst[k].clear();
-    if (lean_mode() > 0) lean_read_ib(a->pread[k], lean_mode(), &a->pdst[k], a->pout[k], out_sz);
+    if (lean_mode() > 0) lean_read_ib(a->pread[k], lean_mode());
   }
   a->pcmd_sz = std::max(a->pcmd_sz, cmd_sz);
   a->pout_sz = std::max(a->pout_sz, out_sz);
@@ -818,10 +761,10 @@ extern "C" {
 int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64_t* sample_ns);
 
 // Reader options, applied to counter sessions opened afterwards.  Keys: "lean"
-// (READ packet mode 0-3, 7, 8, see lean_read_ib).  0 = ok, -1 = unknown key / value.
+// (READ packet mode 0-3, see lean_read_ib).  0 = ok, -1 = unknown key / value.
 // "timeout_ms" (1..60000): bound of every wait on the CP (default 250).
 int kgs_pmc_configure(const char* key, int value) {
-  if (key && std::strcmp(key, "lean") == 0 && ((value >= 0 && value <= 3) || value == 7 || value == 8)) {
+  if (key && std::strcmp(key, "lean") == 0 && value >= 0 && value <= 3) {
     g_lean = value;
     return 0;
   }
@@ -1102,7 +1045,6 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";waited_on_poll=" + std::to_string(a->waited_on_poll) +
                   ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads.load() : 0.0) +
                   ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed) +
-                  ";land_waits=" + std::to_string(a->land_waits.load()) + ";land_timeouts=" + std::to_string(a->land_timeouts.load()) +
                   ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
                   a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc) + ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
                   ";signal=" + (poll_signals() ? "poll" : "interrupt");

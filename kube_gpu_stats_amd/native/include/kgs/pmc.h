@@ -156,7 +156,7 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 // exports kgs_pmc_set_pipelined (aqlprofile) to overlap each READ's CP round
 // trip with the sampler's sleep: a sample returns the READ submitted on the
 // previous tick, stamped with the time the CP executed it.  `lean` (aqlprofile
-// reader: 0-3 / 7-8, -1 = reader default) strips the per-dispatch-profiling flushes and
+// reader: 0-3, -1 = reader default) strips the per-dispatch-profiling flushes and
 // cache invalidations from the READ packet (native/counters/pmc_aqlprofile.cpp).
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
