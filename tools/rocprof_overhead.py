@@ -10,8 +10,10 @@ bench.py launches, per rank, in this order (``load`` units: one
 * ``calibrate_reps()``: 2 units;
 * warm-up W steps, A K steps, B K steps, the phase-R burst train (MFMA kernels
   only, ``burst_resolution.per_gpu.*.launched``), the interleaved blocks in
-  ``interleaved.block_seconds`` order (``block_steps`` steps each), C K steps —
-  every step ``config.units_per_step`` units.
+  ``interleaved.block_seconds`` order (``block_steps`` steps each), the phase-S
+  capacity blocks, phase K (each component alone,
+  ``delivered_by_component.*.launches``), C K steps — every step
+  ``config.units_per_step`` units.
 
 Kernels are assigned to segments by launch order, so no clock translation between
 rocprofv3 and Python is needed.
@@ -47,6 +49,11 @@ def segments(res: dict, triads: int, tiny: int) -> list[tuple[str, int, dict]]:
     seg += [(f"I_{'paused' if c == '0' else c + 'Hz'}", bs * reps, {}) for c, _ in inter.get("block_seconds", [])]
     cap = res.get("capacity") or {}
     seg += [(f"S_{hz}Hz", cap.get("block_steps", 0) * reps, {}) for hz in cap.get("rates", {})]
+    # phase K: each component alone (``delivered_by_component.<name>.launches``)
+    kk = res.get("delivered_by_component") or {}
+    launches = lambda n: int((kk.get(n) or {}).get("launches", 0))  # noqa: E731
+    seg += [("K_mfma", 0, {"mfma": launches("mfma")}), ("K_triad", 0, {"triad": launches("triad")}),
+            ("K_tiny_graph", 0, {"copy": launches("tiny_graph") * tiny})]
     seg += [("C_off", k * reps, {})]
     return seg
 
