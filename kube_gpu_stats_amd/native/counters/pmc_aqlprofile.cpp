@@ -54,6 +54,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -100,6 +101,9 @@ const BlockNameId kBlocks[] = {
     {"CPF", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPF},   {"GRBMSE", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBMSE},
 };
 
+constexpr int kMaxSlots = 32;   // pipelined READ slots (2 × the largest batch)
+constexpr int kMaxBatch = kMaxSlots / 2;
+
 struct Agent {
   hsa_agent_t agent{};
   uint32_t gpu_id = 0;  // KFD gpu_id (== HSA_AMD_AGENT_INFO_DRIVER_UID)
@@ -121,14 +125,30 @@ struct Agent {
   // call (normally finished long ago) and submits the next one without waiting,
   // so the sampler thread never blocks on the CP round trip.
   bool pipelined = false;
-  hsa_ven_amd_aqlprofile_profile_t pprof[2]{};
-  void* pcmd[2] = {nullptr, nullptr};
-  void* pout[2] = {nullptr, nullptr};
-  hsa_ext_amd_aql_pm4_packet_t pread[2]{};
-  hsa_signal_t psig[2]{};
+  hsa_ven_amd_aqlprofile_profile_t pprof[kMaxSlots]{};
+  void* pcmd[kMaxSlots] = {};
+  void* pout[kMaxSlots] = {};
+  hsa_ext_amd_aql_pm4_packet_t pread[kMaxSlots]{};
+  hsa_signal_t psig[kMaxSlots]{};
   uint32_t pcmd_sz = 0, pout_sz = 0;                 // allocated sizes of the slot buffers
   std::vector<hsa_ven_amd_aqlprofile_event_t> pipe_events;  // event list the slot packets were built for
-  int64_t psubmit_ns[2] = {0, 0};
+  int64_t psubmit_ns[kMaxSlots] = {};
+  // Batched publication (kgs_pmc_configure("batch", B), B >= 2; see read_batched):
+  // 2B slots in two halves of B; only the last READ of a half writes the L2 back.
+  int batch = 1;                                     // B of the current slot set (1 = every READ publishes)
+  int nslots = 2;
+  std::vector<volatile uint32_t*> pdst[kMaxSlots];   // each slot's COPY_DATA destination dwords
+  int bfilled[2] = {0, 0};                           // READs submitted into each half since it was collected
+  int bnext = 0;                                     // next slot to submit
+  int blast = -1;                                    // last slot submitted (drain target), -1 none
+  bool bprimed = false;
+  struct Ready {
+    std::vector<double> vals, vals_xcd;
+    std::vector<uint32_t> xcd_seen;
+    int64_t ts = 0;
+  };
+  std::deque<Ready> bready;                          // folded samples not yet returned
+  std::atomic<uint64_t> land_waits{0}, land_timeouts{0};  // collections that had to wait / gave up waiting
   // KGS_AQL_PROFILE=<n>: CP timestamps of every pipelined READ (queue profiling on):
   // queueing delay (submit → CP start) and execution (start → end), reported on
   // stderr every n READs.  How long the CP makes a READ wait says how busy it
@@ -538,7 +558,8 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
 // CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Cost-attribution modes
 // (KGS_AQL_LEAN only; the counter values they return are stale): 4 = 3 + no
 // COPY_DATA, 5 = every packet of the IB a NOP.  Returns packets changed.
-int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
+int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<volatile uint32_t*>* dsts = nullptr,
+                 const void* out = nullptr, size_t out_sz = 0) {
   if (mode <= 0) return 0;
   uint32_t dw[4];
   std::memcpy(dw, pkt.pm4_command + 1, sizeof dw);
@@ -558,6 +579,10 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
         nop(i, len);
         ++changed;
       }
+    } else if (opc == 0x40 && len == 6 && ((ib[i + 1] >> 8) & 0xF) == 5) {  // COPY_DATA → memory: note where
+      const uint64_t dst = (static_cast<uint64_t>(ib[i + 4]) | (static_cast<uint64_t>(ib[i + 5]) << 32)) & ~3ull;
+      const uint64_t lo = reinterpret_cast<uint64_t>(out);
+      if (dsts && out && dst >= lo && dst + 4 <= lo + out_sz) dsts->push_back(reinterpret_cast<volatile uint32_t*>(dst));
     } else if (opc == 0x46 && (ib[i + 1] & 0x3F) == 7) {  // EVENT_WRITE CS_PARTIAL_FLUSH
       nop(i, len);
       ++changed;
@@ -574,10 +599,19 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode) {
 }
 
 int g_lean = 2;  // kgs_pmc_configure("lean", m) before kgs_pmc_open; KGS_AQL_LEAN overrides
+int g_batch = 1;  // kgs_pmc_configure("batch", B) before kgs_pmc_set_pipelined; KGS_AQL_BATCH overrides
 
 int lean_mode() {
   const char* e = std::getenv("KGS_AQL_LEAN");
   return e ? std::atoi(e) : g_lean;
+}
+
+// Batched publication needs READs whose IB does no cache operation (lean ≥ 2 with
+// the ACQUIRE_MEM dropped) next to the publishing one; below lean 2 it is off.
+int batch_size() {
+  const char* e = std::getenv("KGS_AQL_BATCH");
+  const int b = e ? std::atoi(e) : g_batch;
+  return lean_mode() >= 2 && lean_mode() <= 3 ? std::clamp(b, 1, kMaxBatch) : 1;
 }
 
 // Decide each result's XCD after the first fold.  Preferred: aqlprofile's XCD
@@ -708,6 +742,132 @@ int read_pipelined(Agent* a, int64_t* ts) {
   return rc;
 }
 
+// ---- batched publication ----------------------------------------------------
+// Every READ writes its results into fine-grained host memory that the GPU's L2
+// caches, so a READ must end with an L2 writeback before the host can see them,
+// and at 8 kHz that writeback is most of what a READ costs memory-bound work
+// (profiles/r3/README.md, r3e / r3g: the HBM triad pays +0.17 % with it and
+// +0.02 % without).  With a batch of B, the READs go round 2B slots in two
+// halves; within a half only the last READ (the publisher) keeps the writeback
+// and the system-scope release fence, the others have neither.  Packets on the
+// queue run in order (barrier bit), so when the publisher completes, its
+// writeback has pushed every earlier READ of the half out of the L2 as well; the
+// host then folds the half's B READs in order, each with its own CP time.
+// Samples come out one per call, B to 2B ticks late, and the L2 is written back
+// once per B samples instead of once per sample.  Every result dword is pre-set
+// to kUnlanded and checked before the fold (wait_landed): a dword the writeback
+// missed is waited for, briefly, and counted.
+constexpr uint32_t kUnlanded = 0xFFFFFFFFu;
+
+bool is_publisher(const Agent* a, int k) { return a->batch < 2 || k % a->batch == a->batch - 1; }
+
+void wait_landed(Agent* a, int k) {
+  const int64_t t0 = mono_ns();
+  bool waited = false;
+  for (;;) {
+    bool all = true;
+    for (volatile uint32_t* p : a->pdst[k])
+      if (*p == kUnlanded) {
+        all = false;
+        break;
+      }
+    if (all) break;
+    if (!waited) {
+      waited = true;
+      a->land_waits.fetch_add(1, std::memory_order_relaxed);
+    }
+    if (mono_ns() - t0 > 200000) {  // a counter half may really read 0xFFFFFFFF: take it
+      a->land_timeouts.fetch_add(1, std::memory_order_relaxed);
+      break;
+    }
+    sched_yield();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+}
+
+void batch_reset(Agent* a) {
+  a->bfilled[0] = a->bfilled[1] = 0;
+  a->bnext = 0;
+  a->blast = -1;
+  a->bprimed = false;
+  a->bready.clear();
+}
+
+// Wait (bounded) for the last READ submitted, then forget the batch state.
+void batch_drain(Agent* a) {
+  if (a->blast >= 0) wait_done(a, a->psig[a->blast]);
+  batch_reset(a);
+}
+
+// Fold half h (its publisher has completed) into the ready queue.
+void batch_collect(Agent* a, int h) {
+  for (int j = 0; j < a->batch; ++j) {
+    const int k = h * a->batch + j;
+    wait_landed(a, k);
+    if (fold(a, &a->pprof[k]) != 0) continue;
+    Agent::Ready r;
+    r.vals = a->vals;
+    r.vals_xcd = a->vals_xcd;
+    r.xcd_seen = a->xcd_seen;
+    r.ts = a->psubmit_ns[k] + a->rtt_ns / 2;
+    a->bready.push_back(std::move(r));
+  }
+  a->bfilled[h] = 0;
+}
+
+// One batched sample: collect a published half, submit the next READ, return the
+// oldest folded sample.  0 = values in a->vals / *ts, 1 = none yet (the first
+// half is still in flight), < 0 = error (the batch state is dropped).
+int read_batched(Agent* a, int64_t* ts) {
+  const int B = a->batch;
+  if (!a->bprimed) {  // first call (or after an error / mode switch): one synchronous READ
+    batch_reset(a);
+    const int64_t t0 = mono_ns();
+    const int rc = read_values(a);
+    if (rc != 0) return rc;
+    if (ts) *ts = t0 + a->rtt_ns / 2;
+    a->bprimed = true;
+    return 0;  // the next call starts the slot rotation
+  }
+  const int cur = a->bnext / B, old = cur ^ 1;
+  // The other half's publisher went out a tick or more ago: usually done.
+  if (a->bfilled[old] == B) {
+    if (hsa_signal_load_scacquire(a->psig[old * B + B - 1]) < 1) {
+      ++a->ready_on_poll;
+      batch_collect(a, old);
+    }
+  }
+  const int k = a->bnext, h = k / B;
+  if (a->bfilled[h] == B) {  // reusing a half not yet collected: wait for its publisher
+    ++a->waited_on_poll;
+    if (wait_done(a, a->psig[h * B + B - 1]) != 0) {
+      batch_reset(a);  // the packets may still complete later; their slots are re-armed before reuse
+      return -2;
+    }
+    batch_collect(a, h);
+  }
+  for (volatile uint32_t* p : a->pdst[k]) *p = kUnlanded;
+  std::atomic_thread_fence(std::memory_order_release);
+  a->psubmit_ns[k] = mono_ns();
+  const std::pair<int, int> none{HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_NONE};
+  if (enqueue(a, a->pread[k], a->psig[k], is_publisher(a, k) ? read_fences() : none) != 0) {
+    if (a->blast >= 0) wait_done(a, a->psig[a->blast]);
+    batch_reset(a);
+    return -2;
+  }
+  a->blast = k;
+  ++a->bfilled[h];
+  a->bnext = (k + 1) % a->nslots;
+  if (a->bready.empty()) return 1;
+  Agent::Ready& r = a->bready.front();
+  a->vals.swap(r.vals);
+  a->vals_xcd.swap(r.vals_xcd);
+  a->xcd_seen.swap(r.xcd_seen);
+  if (ts) *ts = r.ts;
+  a->bready.pop_front();
+  return 0;
+}
+
 bool same_events(const std::vector<hsa_ven_amd_aqlprofile_event_t>& x,
                  const std::vector<hsa_ven_amd_aqlprofile_event_t>& y) {
   if (x.size() != y.size()) return false;
@@ -722,7 +882,10 @@ bool same_events(const std::vector<hsa_ven_amd_aqlprofile_event_t>& x,
 // main profile).  Called again when a re-open changed the event list: the slot
 // packets of the previous list would otherwise be folded against the new one.
 bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err) {
-  for (int k = 0; k < 2; ++k) {
+  a->batch = batch_size();
+  a->nslots = a->batch >= 2 ? 2 * a->batch : 2;
+  batch_reset(a);
+  for (int k = 0; k < a->nslots; ++k) {
     hsa_ven_amd_aqlprofile_profile_t& p = a->pprof[k];
     p = a->prof;
     if (a->pcmd[k] && a->pcmd_sz < cmd_sz) { hsa_amd_memory_pool_free(a->pcmd[k]); a->pcmd[k] = nullptr; }
@@ -746,7 +909,11 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
       err = "aqlprofile pipeline packet build: " + aql_error();
       return false;
     }
-    if (lean_mode() > 0) lean_read_ib(a->pread[k], lean_mode());
+    // Batched: only the half's last READ writes the L2 back (lean 2); the others
+    // drop the ACQUIRE_MEM (lean 3).  Every slot notes its result dwords.
+    a->pdst[k].clear();
+    const int mode = a->batch >= 2 && !is_publisher(a, k) ? 3 : lean_mode();
+    if (mode > 0) lean_read_ib(a->pread[k], mode, &a->pdst[k], a->pout[k], out_sz);
   }
   a->pcmd_sz = std::max(a->pcmd_sz, cmd_sz);
   a->pout_sz = std::max(a->pout_sz, out_sz);
@@ -761,11 +928,16 @@ extern "C" {
 int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64_t* sample_ns);
 
 // Reader options, applied to counter sessions opened afterwards.  Keys: "lean"
-// (READ packet mode 0-3, see lean_read_ib).  0 = ok, -1 = unknown key / value.
+// (READ packet mode 0-3, see lean_read_ib), "batch" (1..16: READs per L2
+// writeback, see read_batched).  0 = ok, -1 = unknown key / value.
 // "timeout_ms" (1..60000): bound of every wait on the CP (default 250).
 int kgs_pmc_configure(const char* key, int value) {
   if (key && std::strcmp(key, "lean") == 0 && value >= 0 && value <= 3) {
     g_lean = value;
+    return 0;
+  }
+  if (key && std::strcmp(key, "batch") == 0 && value >= 1 && value <= kMaxBatch) {
+    g_batch = value;
     return 0;
   }
   if (key && std::strcmp(key, "timeout_ms") == 0 && value >= 1 && value <= 60000) {
@@ -871,7 +1043,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     // A re-open rebuilt a->events: the pipelined READ slots of the previous session
     // must point at the new array (same list: a hand-over / refresh re-START), or
     // be rebuilt by the next kgs_pmc_set_pipelined (another list).
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < kMaxSlots; ++k)
       if (a->pcmd[k]) {
         a->pprof[k].events = a->events.data();
         a->pprof[k].event_count = static_cast<uint32_t>(a->events.size());
@@ -940,6 +1112,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       return -1;
     }
     a->inflight = -1;
+    batch_reset(a);
     if (submit(a, a->start_pkt) != 0) {
       set_err(err, errlen, "START packet did not complete within " +
                                std::to_string(g_timeout_ns.load() / 1000000) + " ms");
@@ -977,7 +1150,9 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
   const int64_t t0 = mono_ns();
   int64_t ts = 0;
   int rc;
-  if (a->pipelined) {
+  if (a->pipelined && a->batch >= 2) {
+    rc = read_batched(a, &ts);
+  } else if (a->pipelined) {
     rc = read_pipelined(a, &ts);
   } else {
     rc = read_values(a);
@@ -1020,7 +1195,8 @@ int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
     wait_done(a, a->psig[a->inflight]);
     a->inflight = -1;
   }
-  if (on && (!a->pcmd[0] || !same_events(a->pipe_events, a->events))) {
+  batch_drain(a);
+  if (on && (!a->pcmd[0] || !same_events(a->pipe_events, a->events) || a->batch != batch_size())) {
     std::string e;
     if (!setup_pipeline(a, a->cmd_sz, a->out_sz, e)) {
       set_err(err, errlen, e);
@@ -1045,6 +1221,8 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";waited_on_poll=" + std::to_string(a->waited_on_poll) +
                   ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads.load() : 0.0) +
                   ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed) +
+                  ";batch=" + std::to_string(a->batch) + ";land_waits=" + std::to_string(a->land_waits.load()) +
+                  ";land_timeouts=" + std::to_string(a->land_timeouts.load()) +
                   ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
                   a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc) + ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
                   ";signal=" + (poll_signals() ? "poll" : "interrupt");
@@ -1069,6 +1247,7 @@ void kgs_pmc_close(int handle) {
       wait_done(a, a->psig[a->inflight]);
       a->inflight = -1;
     }
+    batch_drain(a);
     submit(a, a->stop_pkt);
     a->started = false;
   }
@@ -1093,6 +1272,7 @@ int kgs_pmc_reset(int handle) {
   Agent* a = g_agents[static_cast<size_t>(handle)];
   a->started = false;
   a->inflight = -1;
+  batch_reset(a);
   if (a->queue) {
     hsa_queue_destroy(a->queue);
     a->queue = nullptr;

@@ -46,6 +46,7 @@ struct ExporterConfig {
   std::string pmc_set = "base";     // "base" (GRBM + MFMA busy) | "full" (+ TA busy: 10x the register reads)
   int pmc_lean = 2;                 // READ packet: 0 as aqlprofile builds it .. 2 no flushes/invalidations (default)
   int pmc_timeout_ms = 250;         // bound of every wait on the command processor (fault boundary)
+  int pmc_batch = 1;                // counter READs per L2 writeback (aqlprofile reader; 1 = every READ)
   std::string listen_addr = "0.0.0.0";
   int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
   std::string node_name;

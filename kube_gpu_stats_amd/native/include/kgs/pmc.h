@@ -95,11 +95,15 @@ struct PmcRates {
 };
 PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu);
 
+constexpr int kPmcPending = 1;
+
 class CounterSource {
  public:
   virtual ~CounterSource() = default;
   virtual std::string name() const = 0;
-  // Fill `out.value[0..kPmcCount)` with cumulative counts for device `dev`.
+  // Fill `out.value[0..kPmcCount)` with cumulative counts for device `dev`.  0 =
+  // a sample, kPmcPending = no new sample yet (a batched reader's first READs are
+  // still unpublished; not a failure), < 0 = failed.
   virtual int sample(int dev, PmcSample& out) = 0;
   // Human-readable diagnostics (mode, per-counter instance counts, missing counters).
   virtual std::string info(int dev) const { return name(); }
@@ -145,6 +149,10 @@ struct MockPmcConfig {
   double hang_timeout_s = 0.25;
   bool hang_heals_on_reset = false;  // reset() clears the hang (the recreated queue works)
   int acquire_fail_dev = -1;    // acquire() fails on this device while its hang is active
+  // Batched publication like the aqlprofile reader's (kgs_pmc_configure("batch")):
+  // after each acquire the first `batch` samples return kPmcPending, then every
+  // sample is the one taken `batch` calls earlier (1 = off).
+  int batch = 1;
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,
@@ -161,6 +169,6 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
                                                       bool pipelined, uint32_t mask, int lean, std::string& err,
-                                                      int timeout_ms = 250);
+                                                      int timeout_ms = 250, int batch = 1);
 
 }  // namespace kgs

@@ -61,6 +61,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.hang_timeout_s = get<double>(m, "hang_timeout_s", c.mock_pmc.hang_timeout_s);
     c.mock_pmc.hang_heals_on_reset = get<bool>(m, "hang_heals_on_reset", c.mock_pmc.hang_heals_on_reset);
     c.mock_pmc.acquire_fail_dev = get<int>(m, "acquire_fail_dev", c.mock_pmc.acquire_fail_dev);
+    c.mock_pmc.batch = get<int>(m, "batch", c.mock_pmc.batch);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -88,6 +89,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.pmc_set = get<std::string>(d, "pmc_set", c.pmc_set);
   c.pmc_lean = get<int>(d, "pmc_lean", c.pmc_lean);
   c.pmc_timeout_ms = get<int>(d, "pmc_timeout_ms", c.pmc_timeout_ms);
+  c.pmc_batch = get<int>(d, "pmc_batch", c.pmc_batch);
   c.hbm_bytes_per_s_at_full_umc = get<double>(d, "hbm_bytes_per_s_at_full_umc", c.hbm_bytes_per_s_at_full_umc);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);

@@ -3,6 +3,7 @@
 // reader; libkgs_pmc.so, rocprofiler-sdk device counting, tests only).
 #include "kgs/pmc.h"
 
+#include <deque>
 #include <dlfcn.h>
 #include <unistd.h>
 
@@ -84,7 +85,8 @@ namespace {
 class MockCounterSource final : public CounterSource {
  public:
   MockCounterSource(const MockConfig& b, const MockPmcConfig& c, int n_dev)
-      : b_(b), c_(c), t0_(mono_ns()), restart_(static_cast<size_t>(std::max(n_dev, 1)), 0) {
+      : b_(b), c_(c), t0_(mono_ns()), restart_(static_cast<size_t>(std::max(n_dev, 1)), 0),
+        delayed_(static_cast<size_t>(std::max(n_dev, 1))) {
     for (int d = 0; d < std::max(n_dev, 1); ++d) fault_.push_back(std::make_unique<Fault>());
   }
   std::string name() const override { return "mock"; }
@@ -93,6 +95,7 @@ class MockCounterSource final : public CounterSource {
     if (dev < 0 || static_cast<size_t>(dev) >= restart_.size()) return -1;
     if (dev == c_.acquire_fail_dev && hung(dev)) return -1;
     restart_[static_cast<size_t>(dev)] = mono_ns();
+    delayed_[static_cast<size_t>(dev)].clear();
     return 0;
   }
   int reset(int dev) override {
@@ -137,6 +140,13 @@ class MockCounterSource final : public CounterSource {
     }
     s.mono_ns = now;
     s.read_ns = 1000;
+    if (c_.batch > 1 && dev >= 0 && static_cast<size_t>(dev) < delayed_.size()) {
+      std::deque<PmcSample>& q = delayed_[static_cast<size_t>(dev)];  // this device's sampler thread only
+      q.push_back(s);
+      if (q.size() <= static_cast<size_t>(c_.batch)) return kPmcPending;
+      s = q.front();
+      q.pop_front();
+    }
     return 0;
   }
 
@@ -193,6 +203,7 @@ class MockCounterSource final : public CounterSource {
   MockPmcConfig c_;
   int64_t t0_;
   std::vector<int64_t> restart_;  // per device: time of the last acquire (0 = never released)
+  std::vector<std::deque<PmcSample>> delayed_;  // per device: samples held back (MockPmcConfig::batch)
   std::vector<std::unique_ptr<Fault>> fault_;
 };
 
@@ -220,7 +231,7 @@ class DlCounterSource final : public CounterSource {
   }
 
   bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, bool pipelined,
-            uint32_t mask, int lean, int timeout_ms, std::string& err) {
+            uint32_t mask, int lean, int timeout_ms, int batch, std::string& err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!lib_) {
       err = std::string("dlopen failed: ") + dlerror();
@@ -240,6 +251,7 @@ class DlCounterSource final : public CounterSource {
     auto configure = reinterpret_cast<configure_fn>(dlsym(lib_, "kgs_pmc_configure"));  // optional
     if (configure && lean >= 0) configure("lean", lean);
     if (configure && timeout_ms > 0) configure("timeout_ms", timeout_ms);
+    if (configure && batch > 1 && configure("batch", batch) != 0) err += "reader ignores batch=" + std::to_string(batch) + "; ";
     abort_ = reinterpret_cast<abort_fn>(dlsym(lib_, "kgs_pmc_abort"));  // optional (aqlprofile reader)
     reset_ = reinterpret_cast<reset_fn>(dlsym(lib_, "kgs_pmc_reset"));  // optional
     char ebuf[512] = {};
@@ -407,9 +419,9 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
                                                       bool pipelined, uint32_t mask, int lean, std::string& err,
-                                                      int timeout_ms) {
+                                                      int timeout_ms, int batch) {
   auto s = std::make_unique<DlCounterSource>(name);
-  if (!s->load(lib_path, be, devices, pipelined, mask, lean, timeout_ms, err)) return nullptr;
+  if (!s->load(lib_path, be, devices, pipelined, mask, lean, timeout_ms, batch, err)) return nullptr;
   return s;
 }
 

@@ -693,6 +693,8 @@ void Sampler::run_pmc(Worker& w) {
             last_start_ns = t;
           }
         }
+      } else if (prc == kPmcPending) {
+        // A batched reader's first READs are not published yet: nothing to fold.
       } else if (stop_.load(std::memory_order_relaxed)) {
         break;  // stop() aborted the wait: not a device failure
       } else {

@@ -614,6 +614,25 @@ def test_dispatch_gap_reads_drop_to_gap_rate(mock_exporter):
     assert ex.pmc_busy_min == 0.9 and ex.pmc_gap_hz == 200
 
 
+def test_batched_counter_source_is_not_a_failure(mock_exporter):
+    """--pmc-batch: a reader that publishes every B-th READ returns kPmcPending for its
+    first B samples after each (re)START and then every sample B calls late.  The
+    sampler must neither count that as an error nor trip the breaker, and the
+    integrals stay exact (each sample carries its own CP time)."""
+    ex = mock_exporter(n_gpus=2, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0,
+                       window_s=1.0, mock={"util_base": 40, "util_amp": 0}, mock_pmc={"batch": 8},
+                       pmc_refresh_s=0.3)                       # a re-START every 0.3 s: pending again each time
+    time.sleep(1.3)
+    for g in (0, 1):
+        i = ex.integrals(g)
+        assert i["pmc_errors"] == 0 and i["pmc_breaker_trips"] == 0 and i["pmc_failed"] == 0, i
+        assert i["pmc_samples"] > 900, i
+    w = ex.window(0, 1.0)
+    assert w["gpu_active_pct"] == pytest.approx(40, abs=3), w
+    m = parse_text(ex.render())
+    assert m["kgs_pmc_refreshes_total"][0][1] >= 3
+
+
 def test_throttle_seconds_by_reason(mock_exporter):
     """amdgpu_throttle_seconds_total{reason}: per distinct PMFW table, Δresidency /
     Δaccumulation_counter of each throttler times the interval (amdsmi PVIOL/TVIOL),

@@ -33,7 +33,7 @@ for s in $STEPS; do
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc none --out "$OUT/trainpmfw.json" ;;
     train2) run train2 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 2 --out "$OUT/train2.json" ;;
-    tdef|tpmfw|tagent|tl3agent|tnop|t1k|tgap*)
+    tdef|tpmfw|tagent|tl3agent|tnop|t1k|tgap*|tbatch*)
         # training-step side runs, 36 rounds = every block order 6 times:
         #   tdef (defaults) tpmfw (no READs) tagent (release fence at agent scope)
         #   tl3agent (lean 3 + agent release) tnop (every READ packet a NOP: the bare
@@ -48,7 +48,9 @@ for s in $STEPS; do
           tnop) KGS_AQL_LEAN=5 run $s 600 "${T[@]}" ;;
           t1k) run $s 600 "${T[@]}" --hz 1000 ;;
           tgap*) run $s 600 "${T[@]}" --pmc-busy-min "0.${s#tgap}" ;;  # tgap90: --pmc-busy-min 0.90
+          tbatch*) run $s 600 "${T[@]}" --pmc-batch "${s#tbatch}" ;;      # tbatch8: --pmc-batch 8
         esac ;;
+    bbatch*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch "${s#bbatch}" --out "$OUT/$s.json" ;;
     bgap*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-busy-min "0.${s#bgap}" --out "$OUT/$s.json" ;;
     probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
            run probe_xgmi 90 python tools/probe_xgmi.py ;;
