@@ -89,7 +89,8 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-busy-min", type=float, default=0.0,
                     help="exporter --pmc-busy-min: READ at --pmc-gap-hz while the SPI-busy share is below this")
     ap.add_argument("--pmc-gap-hz", type=float, default=1000.0, help="exporter --pmc-gap-hz")
-    ap.add_argument("--pmc-batch", type=int, default=1, help="exporter --pmc-batch: counter READs per L2 writeback")
+    ap.add_argument("--pmc-batch", type=int, default=8, help="exporter --pmc-batch: counter READs per L2 writeback")
+    ap.add_argument("--pmc-publish-us", type=int, default=1000, help="exporter --pmc-publish-us")
     ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
     ap.add_argument("--scrape-hz", type=float, default=20.0)
@@ -555,7 +556,7 @@ class ExporterProc:
                     "--pmc-lean", str(a.pmc_lean)]
         cmd += ["--pmc-busy-min", f"{a.pmc_busy_min:g}", "--pmc-gap-hz", f"{a.pmc_gap_hz:g}"]
         if not a.mock:
-            cmd += ["--pmc-batch", str(a.pmc_batch)]
+            cmd += ["--pmc-batch", str(a.pmc_batch), "--pmc-publish-us", str(a.pmc_publish_us)]
         env = dict(os.environ)
         env.setdefault("KGS_NO_BUILD", "1")
         env.setdefault("PYTHONFAULTHANDLER", "1")  # a native fault leaves a trace in the exporter log
@@ -1438,7 +1439,7 @@ def run(a, ctx) -> dict | None:
                    "seq_len_meaning": "sampler ticks per GPU per timed step",
                    "hz": a.hz, "hz_tiers": hzs, "sample_source": source,
                    "pmc_gap": {"busy_min": a.pmc_busy_min, "hz": a.pmc_gap_hz} if a.pmc_busy_min > 0 else None,
-                   "pmc_batch": a.pmc_batch,
+                   "pmc_batch": a.pmc_batch, "pmc_publish_us": a.pmc_publish_us,
                    "exporter": "attached" if a.attach else "spawned", "load": "mock" if a.mock else a.load,
                    "units_per_step": load.reps, "unit_ms": unit_s * 1e3},
         "value_semantics": "aggregate over all GPUs (driver contract); per-GPU in samples_per_sec_per_gpu",

@@ -79,9 +79,12 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                       "(0 = off; ignored in profiling mode)")
     add_flag(ap, "pmc-gap-hz", 1000.0, "counter READ rate in a dispatch gap (--pmc-busy-min)")
     add_flag(ap, "pmc-gap-hold-ms", 1.0, "low-occupancy READ intervals in a row, in ms, before the gap rate applies")
-    add_flag(ap, "pmc-batch", 1, "counter READs per L2 writeback: a READ's results sit in the GPU's L2 until "
-                                 "written back, and that writeback is what READs cost memory-bound work; with B > 1 "
-                                 "only every B-th READ writes back (samples arrive B-2B ticks late; 1 = every READ)")
+    add_flag(ap, "pmc-batch", 8, "counter READs per L2 writeback: a READ's results sit in the GPU's L2 until "
+                                 "written back, and that writeback is half of what a READ costs a training step; "
+                                 "with B > 1 at most every B-th READ writes back (at 8 kHz samples arrive B-2B ticks "
+                                 "late; 1 = every READ)")
+    add_flag(ap, "pmc-publish-us", 1000, "longest a batched counter READ waits for its L2 writeback: a READ writes "
+                                         "back early when the next tick would be later (at <= 1 kHz every READ does)")
     add_flag(ap, "pmc-timeout-ms", 250, "bound of every wait on the command processor (counter READ, START, STOP, "
                                         "queue slot): a wedged CP costs one timeout, never a hang")
     add_flag(ap, "pmc-breaker-k", 3, "consecutive failed counter drains that open the counter tier's circuit breaker "
@@ -156,6 +159,7 @@ def config_from_args(a) -> dict:
         "pmc_gap_hold_s": a.pmc_gap_hold_ms * 1e-3,
         "pmc_timeout_ms": a.pmc_timeout_ms,
         "pmc_batch": a.pmc_batch,
+        "pmc_publish_us": a.pmc_publish_us,
         "pmc_breaker_k": a.pmc_breaker_k,
         "pmc_retry_s": a.pmc_retry_s,
         "pmc_retry_max_s": a.pmc_retry_max_s,

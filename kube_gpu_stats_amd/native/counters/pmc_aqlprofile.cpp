@@ -59,6 +59,7 @@
 #include <string>
 #include <vector>
 
+#include "kgs/aql_batch.h"
 #include "kgs/aql_ring.h"
 
 namespace {
@@ -101,8 +102,8 @@ const BlockNameId kBlocks[] = {
     {"CPF", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPF},   {"GRBMSE", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBMSE},
 };
 
-constexpr int kMaxSlots = 32;   // pipelined READ slots (2 × the largest batch)
-constexpr int kMaxBatch = kMaxSlots / 2;
+constexpr int kMaxBatch = kgs::BatchPlan::kMaxBatch;
+constexpr int kMaxSlots = 2 * kMaxBatch;  // pipelined READ slots (2 × the largest batch)
 
 struct Agent {
   hsa_agent_t agent{};
@@ -133,14 +134,13 @@ struct Agent {
   uint32_t pcmd_sz = 0, pout_sz = 0;                 // allocated sizes of the slot buffers
   std::vector<hsa_ven_amd_aqlprofile_event_t> pipe_events;  // event list the slot packets were built for
   int64_t psubmit_ns[kMaxSlots] = {};
-  // Batched publication (kgs_pmc_configure("batch", B), B >= 2; see read_batched):
-  // 2B slots in two halves of B; only the last READ of a half writes the L2 back.
+  // Batched publication (kgs_pmc_configure("batch", B), B >= 2; see read_batched
+  // and include/kgs/aql_batch.h): 2B slots in two halves of B; only a half's
+  // publisher writes the L2 back.
   int batch = 1;                                     // B of the current slot set (1 = every READ publishes)
   int nslots = 2;
+  kgs::BatchPlan plan;
   std::vector<volatile uint32_t*> pdst[kMaxSlots];   // each slot's COPY_DATA destination dwords
-  int bfilled[2] = {0, 0};                           // READs submitted into each half since it was collected
-  int bnext = 0;                                     // next slot to submit
-  int blast = -1;                                    // last slot submitted (drain target), -1 none
   bool bprimed = false;
   struct Ready {
     std::vector<double> vals, vals_xcd;
@@ -149,6 +149,7 @@ struct Agent {
   };
   std::deque<Ready> bready;                          // folded samples not yet returned
   std::atomic<uint64_t> land_waits{0}, land_timeouts{0};  // collections that had to wait / gave up waiting
+  std::atomic<uint64_t> publishes{0};                // batched READs that wrote the L2 back
   // KGS_AQL_PROFILE=<n>: CP timestamps of every pipelined READ (queue profiling on):
   // queueing delay (submit → CP start) and execution (start → end), reported on
   // stderr every n READs.  How long the CP makes a READ wait says how busy it
@@ -600,6 +601,9 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<
 
 int g_lean = 2;  // kgs_pmc_configure("lean", m) before kgs_pmc_open; KGS_AQL_LEAN overrides
 int g_batch = 1;  // kgs_pmc_configure("batch", B) before kgs_pmc_set_pipelined; KGS_AQL_BATCH overrides
+// kgs_pmc_configure("publish_us", t): the longest a batched READ waits for its
+// publisher (aql_batch.h); 0 = only a half's B-th READ publishes.
+int64_t g_publish_ns = 1000000;
 
 int lean_mode() {
   const char* e = std::getenv("KGS_AQL_LEAN");
@@ -745,21 +749,21 @@ int read_pipelined(Agent* a, int64_t* ts) {
 // ---- batched publication ----------------------------------------------------
 // Every READ writes its results into fine-grained host memory that the GPU's L2
 // caches, so a READ must end with an L2 writeback before the host can see them,
-// and at 8 kHz that writeback is most of what a READ costs memory-bound work
-// (profiles/r3/README.md, r3e / r3g: the HBM triad pays +0.17 % with it and
-// +0.02 % without).  With a batch of B, the READs go round 2B slots in two
-// halves; within a half only the last READ (the publisher) keeps the writeback
-// and the system-scope release fence, the others have neither.  Packets on the
-// queue run in order (barrier bit), so when the publisher completes, its
-// writeback has pushed every earlier READ of the half out of the L2 as well; the
-// host then folds the half's B READs in order, each with its own CP time.
-// Samples come out one per call, B to 2B ticks late, and the L2 is written back
-// once per B samples instead of once per sample.  Every result dword is pre-set
-// to kUnlanded and checked before the fold (wait_landed): a dword the writeback
-// missed is waited for, briefly, and counted.
+// and that writeback is about half of what a READ costs a training step
+// (profiles/r3/README.md, r3e / r3g).  With a batch of B the READs go round 2B
+// slots in two halves (include/kgs/aql_batch.h); only a half's publisher keeps
+// the writeback and the system-scope release fence.  Packets on the queue run in
+// order (barrier bit), so when the publisher completes, its writeback has pushed
+// every earlier READ of the half out of the L2 as well; the host then folds the
+// half's READs in order, each with its own CP time.  At 8 kHz a sample comes out
+// B to 2B ticks late and the L2 is written back once per B samples; a READ never
+// waits more than the publish interval (1 ms) for its publisher, so at low rates
+// every READ publishes.  Every result dword is pre-set to kUnlanded and checked
+// before the fold (wait_landed): a dword the writeback missed is waited for,
+// briefly, and counted.
 constexpr uint32_t kUnlanded = 0xFFFFFFFFu;
 
-bool is_publisher(const Agent* a, int k) { return a->batch < 2 || k % a->batch == a->batch - 1; }
+bool is_publisher(const Agent* a, int k) { return a->batch < 2 || a->plan.is_publisher(k); }
 
 void wait_landed(Agent* a, int k) {
   const int64_t t0 = mono_ns();
@@ -786,23 +790,23 @@ void wait_landed(Agent* a, int k) {
 }
 
 void batch_reset(Agent* a) {
-  a->bfilled[0] = a->bfilled[1] = 0;
-  a->bnext = 0;
-  a->blast = -1;
+  a->plan.reset();
   a->bprimed = false;
   a->bready.clear();
 }
 
 // Wait (bounded) for the last READ submitted, then forget the batch state.
 void batch_drain(Agent* a) {
-  if (a->blast >= 0) wait_done(a, a->psig[a->blast]);
+  if (a->batch >= 2 && a->plan.last() >= 0) wait_done(a, a->psig[a->plan.last()]);
   batch_reset(a);
 }
 
 // Fold half h (its publisher has completed) into the ready queue.
 void batch_collect(Agent* a, int h) {
-  for (int j = 0; j < a->batch; ++j) {
-    const int k = h * a->batch + j;
+  int ks[kMaxSlots];
+  const int n = a->plan.slots(h, ks);
+  for (int j = 0; j < n; ++j) {
+    const int k = ks[j];
     wait_landed(a, k);
     if (fold(a, &a->pprof[k]) != 0) continue;
     Agent::Ready r;
@@ -812,14 +816,14 @@ void batch_collect(Agent* a, int h) {
     r.ts = a->psubmit_ns[k] + a->rtt_ns / 2;
     a->bready.push_back(std::move(r));
   }
-  a->bfilled[h] = 0;
+  a->plan.collected(h);
 }
 
 // One batched sample: collect a published half, submit the next READ, return the
 // oldest folded sample.  0 = values in a->vals / *ts, 1 = none yet (the first
 // half is still in flight), < 0 = error (the batch state is dropped).
 int read_batched(Agent* a, int64_t* ts) {
-  const int B = a->batch;
+  kgs::BatchPlan& p = a->plan;
   if (!a->bprimed) {  // first call (or after an error / mode switch): one synchronous READ
     batch_reset(a);
     const int64_t t0 = mono_ns();
@@ -829,35 +833,33 @@ int read_batched(Agent* a, int64_t* ts) {
     a->bprimed = true;
     return 0;  // the next call starts the slot rotation
   }
-  const int cur = a->bnext / B, old = cur ^ 1;
+  const int cur = p.current_half(), old = cur ^ 1;
   // The other half's publisher went out a tick or more ago: usually done.
-  if (a->bfilled[old] == B) {
-    if (hsa_signal_load_scacquire(a->psig[old * B + B - 1]) < 1) {
-      ++a->ready_on_poll;
-      batch_collect(a, old);
-    }
+  if (p.closed(old) && hsa_signal_load_scacquire(a->psig[p.publisher(old)]) < 1) {
+    ++a->ready_on_poll;
+    batch_collect(a, old);
   }
-  const int k = a->bnext, h = k / B;
-  if (a->bfilled[h] == B) {  // reusing a half not yet collected: wait for its publisher
+  if (p.closed(cur)) {  // reusing a half not yet collected: wait for its publisher
     ++a->waited_on_poll;
-    if (wait_done(a, a->psig[h * B + B - 1]) != 0) {
+    if (wait_done(a, a->psig[p.publisher(cur)]) != 0) {
       batch_reset(a);  // the packets may still complete later; their slots are re-armed before reuse
       return -2;
     }
-    batch_collect(a, h);
+    batch_collect(a, cur);
   }
-  for (volatile uint32_t* p : a->pdst[k]) *p = kUnlanded;
+  const int k = p.next_slot(mono_ns());
+  for (volatile uint32_t* d : a->pdst[k]) *d = kUnlanded;
   std::atomic_thread_fence(std::memory_order_release);
   a->psubmit_ns[k] = mono_ns();
   const std::pair<int, int> none{HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_NONE};
-  if (enqueue(a, a->pread[k], a->psig[k], is_publisher(a, k) ? read_fences() : none) != 0) {
-    if (a->blast >= 0) wait_done(a, a->psig[a->blast]);
+  const bool pub = p.is_publisher(k);
+  if (enqueue(a, a->pread[k], a->psig[k], pub ? read_fences() : none) != 0) {
+    if (p.last() >= 0) wait_done(a, a->psig[p.last()]);
     batch_reset(a);
     return -2;
   }
-  a->blast = k;
-  ++a->bfilled[h];
-  a->bnext = (k + 1) % a->nslots;
+  p.submitted(k, a->psubmit_ns[k]);
+  if (pub) ++a->publishes;
   if (a->bready.empty()) return 1;
   Agent::Ready& r = a->bready.front();
   a->vals.swap(r.vals);
@@ -884,6 +886,7 @@ bool same_events(const std::vector<hsa_ven_amd_aqlprofile_event_t>& x,
 bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err) {
   a->batch = batch_size();
   a->nslots = a->batch >= 2 ? 2 * a->batch : 2;
+  if (a->batch >= 2) a->plan.configure(a->batch, g_publish_ns);
   batch_reset(a);
   for (int k = 0; k < a->nslots; ++k) {
     hsa_ven_amd_aqlprofile_profile_t& p = a->pprof[k];
@@ -929,8 +932,10 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
 
 // Reader options, applied to counter sessions opened afterwards.  Keys: "lean"
 // (READ packet mode 0-3, see lean_read_ib), "batch" (1..16: READs per L2
-// writeback, see read_batched).  0 = ok, -1 = unknown key / value.
+// writeback, see read_batched), "publish_us" (0..10^6: the longest a batched READ
+// waits for its publisher, default 1000; 0 = only the B-th READ publishes).
 // "timeout_ms" (1..60000): bound of every wait on the CP (default 250).
+// 0 = ok, -1 = unknown key / value.
 int kgs_pmc_configure(const char* key, int value) {
   if (key && std::strcmp(key, "lean") == 0 && value >= 0 && value <= 3) {
     g_lean = value;
@@ -938,6 +943,10 @@ int kgs_pmc_configure(const char* key, int value) {
   }
   if (key && std::strcmp(key, "batch") == 0 && value >= 1 && value <= kMaxBatch) {
     g_batch = value;
+    return 0;
+  }
+  if (key && std::strcmp(key, "publish_us") == 0 && value >= 0 && value <= 1000000) {
+    g_publish_ns = static_cast<int64_t>(value) * 1000;
     return 0;
   }
   if (key && std::strcmp(key, "timeout_ms") == 0 && value >= 1 && value <= 60000) {
@@ -1223,6 +1232,8 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed) +
                   ";batch=" + std::to_string(a->batch) + ";land_waits=" + std::to_string(a->land_waits.load()) +
                   ";land_timeouts=" + std::to_string(a->land_timeouts.load()) +
+                  ";publishes=" + std::to_string(a->publishes.load()) +
+                  ";publish_us=" + std::to_string(g_publish_ns / 1000) +
                   ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
                   a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc) + ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
                   ";signal=" + (poll_signals() ? "poll" : "interrupt");

@@ -46,7 +46,8 @@ struct ExporterConfig {
   std::string pmc_set = "base";     // "base" (GRBM + MFMA busy) | "full" (+ TA busy: 10x the register reads)
   int pmc_lean = 2;                 // READ packet: 0 as aqlprofile builds it .. 2 no flushes/invalidations (default)
   int pmc_timeout_ms = 250;         // bound of every wait on the command processor (fault boundary)
-  int pmc_batch = 1;                // counter READs per L2 writeback (aqlprofile reader; 1 = every READ)
+  int pmc_batch = 8;                // counter READs per L2 writeback (aqlprofile reader; 1 = every READ)
+  int pmc_publish_us = 1000;        // longest a batched READ waits for its L2 writeback (kgs/aql_batch.h)
   std::string listen_addr = "0.0.0.0";
   int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
   std::string node_name;

@@ -169,6 +169,6 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
                                                       bool pipelined, uint32_t mask, int lean, std::string& err,
-                                                      int timeout_ms = 250, int batch = 1);
+                                                      int timeout_ms = 250, int batch = 1, int publish_us = 1000);
 
 }  // namespace kgs

@@ -90,6 +90,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.pmc_lean = get<int>(d, "pmc_lean", c.pmc_lean);
   c.pmc_timeout_ms = get<int>(d, "pmc_timeout_ms", c.pmc_timeout_ms);
   c.pmc_batch = get<int>(d, "pmc_batch", c.pmc_batch);
+  c.pmc_publish_us = get<int>(d, "pmc_publish_us", c.pmc_publish_us);
   c.hbm_bytes_per_s_at_full_umc = get<double>(d, "hbm_bytes_per_s_at_full_umc", c.hbm_bytes_per_s_at_full_umc);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);

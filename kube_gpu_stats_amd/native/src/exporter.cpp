@@ -161,7 +161,8 @@ bool Exporter::init() {
     pmc_ = make_mock_counter_source(*be_, cfg_.mock, mp);
   } else if (cfg_.pmc_source == "rocprofiler" || cfg_.pmc_source == "aqlprofile") {
     pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, cfg_.pmc_pipeline, pmc_mask, cfg_.pmc_lean,
-                                  pmc_err_, cfg_.pmc_timeout_ms, cfg_.pmc_batch);
+                                  pmc_err_, cfg_.pmc_timeout_ms, cfg_.pmc_batch,
+                                  cfg_.pmc_publish_us);
   } else if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
     err_ = "unknown pmc_source '" + cfg_.pmc_source + "'";
     return false;

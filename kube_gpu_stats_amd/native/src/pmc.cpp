@@ -231,7 +231,7 @@ class DlCounterSource final : public CounterSource {
   }
 
   bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, bool pipelined,
-            uint32_t mask, int lean, int timeout_ms, int batch, std::string& err) {
+            uint32_t mask, int lean, int timeout_ms, int batch, int publish_us, std::string& err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!lib_) {
       err = std::string("dlopen failed: ") + dlerror();
@@ -252,6 +252,7 @@ class DlCounterSource final : public CounterSource {
     if (configure && lean >= 0) configure("lean", lean);
     if (configure && timeout_ms > 0) configure("timeout_ms", timeout_ms);
     if (configure && batch > 1 && configure("batch", batch) != 0) err += "reader ignores batch=" + std::to_string(batch) + "; ";
+    if (configure && batch > 1 && publish_us >= 0) configure("publish_us", publish_us);
     abort_ = reinterpret_cast<abort_fn>(dlsym(lib_, "kgs_pmc_abort"));  // optional (aqlprofile reader)
     reset_ = reinterpret_cast<reset_fn>(dlsym(lib_, "kgs_pmc_reset"));  // optional
     char ebuf[512] = {};
@@ -419,9 +420,9 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
                                                       bool pipelined, uint32_t mask, int lean, std::string& err,
-                                                      int timeout_ms, int batch) {
+                                                      int timeout_ms, int batch, int publish_us) {
   auto s = std::make_unique<DlCounterSource>(name);
-  if (!s->load(lib_path, be, devices, pipelined, mask, lean, timeout_ms, batch, err)) return nullptr;
+  if (!s->load(lib_path, be, devices, pipelined, mask, lean, timeout_ms, batch, publish_us, err)) return nullptr;
   return s;
 }
 

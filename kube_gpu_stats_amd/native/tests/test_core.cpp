@@ -45,6 +45,7 @@
 #include <cstring>
 #include <random>
 
+#include "kgs/aql_batch.h"
 #include "kgs/aql_ring.h"
 #include "kgs/backend.h"
 #include "kgs/exporter.h"
@@ -683,7 +684,62 @@ static void test_pmc_breaker() {
               static_cast<unsigned long long>(st.pmc_retries.load()));
 }
 
+static void test_batch_plan() {
+  // --pmc-batch 8, publish interval 1 ms (kgs/aql_batch.h).
+  BatchPlan p;
+  p.configure(8, 1000000);
+  CHECK(p.nslots() == 16 && p.publisher(0) == 7 && p.publisher(1) == 15);
+  int64_t t = 1000000000;
+  auto submit = [&](int64_t dt) {
+    t += dt;
+    const int k = p.next_slot(t);
+    p.submitted(k, t);
+    return k;
+  };
+  int ks[32];
+  // After a reset the tick interval is unknown: the first READ publishes at once.
+  CHECK(submit(0) == 7 && p.closed(0) && p.current_half() == 1);
+  CHECK(p.slots(0, ks) == 1 && ks[0] == 7);
+  p.collected(0);
+  // 8 kHz: half 1 fills in order and only its 8th READ (slot 15) publishes.
+  for (int j = 0; j < 8; ++j) CHECK(submit(125000) == 8 + j);
+  CHECK(p.closed(1) && !p.closed(0) && p.current_half() == 0 && p.last() == 15);
+  CHECK(p.slots(1, ks) == 8 && ks[0] == 8 && ks[6] == 14 && ks[7] == 15);
+  p.collected(1);
+  // Three 8 kHz READs, then the GPU goes quiet (100 Hz): the next READ would wait
+  // past 1 ms for a publisher, so it takes slot 7 and closes the half early.
+  CHECK(submit(125000) == 0 && submit(125000) == 1 && submit(125000) == 2);
+  CHECK(!p.closed(0));
+  CHECK(submit(10000000) == 7 && p.closed(0));
+  CHECK(p.slots(0, ks) == 4 && ks[0] == 0 && ks[1] == 1 && ks[2] == 2 && ks[3] == 7);
+  p.collected(0);
+  // At 100 Hz every READ publishes: halves of one READ, alternating.
+  for (int i = 0; i < 4; ++i) {
+    const int k = submit(10000000);
+    CHECK(k == (i % 2 == 0 ? 15 : 7));
+    CHECK(p.slots(k / 8, ks) == 1 && ks[0] == k);
+    p.collected(k / 8);
+  }
+  // 4 kHz: a READ publishes once the next would be due more than 1 ms after the
+  // half's first — 4 READs per writeback (the 1 kHz publication rate).
+  CHECK(submit(250000) == 8 && submit(250000) == 9 && submit(250000) == 10 && submit(250000) == 15);
+  p.collected(1);
+  // 1 kHz: every READ publishes.
+  CHECK(submit(1000000) == 7 && submit(1000000) == 15);
+  p.collected(0);
+  p.collected(1);
+  // A late tick (a sampler overrun) only shortens a half.
+  CHECK(submit(125000) == 0 && submit(900000) == 7);
+  p.collected(0);
+  // publish interval 0: only the B-th READ publishes, whatever the rate.
+  p.configure(4, 0);
+  for (int j = 0; j < 4; ++j) CHECK(submit(50000000) == j);
+  CHECK(p.closed(0) && p.slots(0, ks) == 4);
+  std::printf("batch plan ok\n");
+}
+
 int main() {
+  test_batch_plan();
   test_reserve_slot();
   test_pmc_breaker();
   test_pmc_fault_boundary();

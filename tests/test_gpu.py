@@ -648,7 +648,8 @@ def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
             proc.communicate()
 
 
-def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
+@pytest.mark.parametrize("batch", [1, 8])
+def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev, batch):
     """What the 8 kHz counter tier buys ("the headline value is a
     dial"): a 200 Hz train of ~1 ms MFMA bursts — far inside one ≈20 ms PMFW table
     period — is resolved burst by burst by the exporter's full-rate /counters stream:
@@ -656,7 +657,12 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
     host timed them.  GPU-active (GRBM_SPI_BUSY: a shader engine has waves) is
     READ-immune; the PMFW GFX busy counts every counter READ on the command
     processor as ≈80 µs of work, so at 8 kHz in profiling mode it reads the gaps
-    between bursts as busy (profiles/r2/idle_busy/)."""
+    between bursts as busy (profiles/r2/idle_busy/).
+
+    batch=8 (--pmc-batch 8): only every 8th READ writes the L2 back; the other
+    seven's results reach host memory with the publisher's writeback, 1-2 ms late,
+    and are folded in order with their own CP times — so the same bursts must come
+    out, at the same lengths, from samples that were published in batches."""
     import urllib.request
 
     import torch
@@ -679,7 +685,7 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
     iters = max(200, int(4000 * 1.0 / e0.elapsed_time(e1)))  # ≈1 ms per burst
     cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0", "--hz", "8000",
            "--pmc", "aqlprofile", "--control-stdin", "--bdfs", _bdf0(), "--proc-every", "0", "--link-every", "0",
-           *PROFILING_MODE]
+           *PROFILING_MODE, "--pmc-batch", str(batch)]
     proc = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                             text=True)
     try:
@@ -730,7 +736,8 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev):
                "first_50ms": [[round((x["mono_ns"] - lo) * 1e-6, 3), round(x["gpu_active_pct"], 1),
                                round(x.get("mfma_util_pct", 0), 1)]
                               for x in win if x["mono_ns"] - lo <= 52_000_000 and "gpu_active_pct" in x]}
-    _keep("burst_resolution.json", json.dumps(summary, indent=1))
+    summary["pmc_batch"] = batch
+    _keep("burst_resolution.json" if batch == 1 else f"burst_resolution_batch{batch}.json", json.dumps(summary, indent=1))
     print(json.dumps({k: v for k, v in summary.items() if k != "first_50ms"}))
     assert summary["drain_rate_hz"] > 7000, summary
     assert abs(len(segs) - len(bursts)) <= max(3, 0.05 * len(bursts)), summary
