@@ -33,7 +33,7 @@ for s in $STEPS; do
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc none --out "$OUT/trainpmfw.json" ;;
     train2) run train2 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 2 --out "$OUT/train2.json" ;;
-    tdef|tpmfw|tagent|tl3agent|tnop|t1k|tgap*|tbatch*)
+    tdef|tdef2|tpmfw|tagent|tl3agent|tnop|t1k|tgap*|tbatch*|tpub*|tnobatch)
         # training-step side runs, 36 rounds = every block order 6 times:
         #   tdef (defaults) tpmfw (no READs) tagent (release fence at agent scope)
         #   tl3agent (lean 3 + agent release) tnop (every READ packet a NOP: the bare
@@ -41,7 +41,7 @@ for s in $STEPS; do
         T=(python -u bench.py --load train --steps 10 --warmup 2 --rounds 36 --hz-list 100 --capacity-hz ""
            --burst-s 0 --quiet-s 0 --component-s 0 --out "$OUT/$s.json")
         case $s in
-          tdef) run $s 600 "${T[@]}" ;;
+          tdef|tdef2) run $s 600 "${T[@]}" ;;
           tpmfw) run $s 600 "${T[@]}" --pmc none ;;
           tagent) KGS_AQL_FENCE=none,agent run $s 600 "${T[@]}" ;;
           tl3agent) KGS_AQL_FENCE=none,agent KGS_AQL_LEAN=3 run $s 600 "${T[@]}" ;;
@@ -49,7 +49,11 @@ for s in $STEPS; do
           t1k) run $s 600 "${T[@]}" --hz 1000 ;;
           tgap*) run $s 600 "${T[@]}" --pmc-busy-min "0.${s#tgap}" ;;  # tgap90: --pmc-busy-min 0.90
           tbatch*) run $s 600 "${T[@]}" --pmc-batch "${s#tbatch}" ;;      # tbatch8: --pmc-batch 8
+          tpub*) run $s 600 "${T[@]}" --pmc-publish-us "${s#tpub}" ;;     # tpub0: count-only batches
+          tnobatch) run $s 600 "${T[@]}" --pmc-batch 1 ;;
         esac ;;
+    bpub*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-publish-us "${s#bpub}" --out "$OUT/$s.json" ;;
+    bnobatch) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch 1 --out "$OUT/$s.json" ;;
     bbatch*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch "${s#bbatch}" --out "$OUT/$s.json" ;;
     bgap*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-busy-min "0.${s#bgap}" --out "$OUT/$s.json" ;;
     probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
