@@ -200,6 +200,13 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_breaker_trips_total", "counter", "Times the counter tier's circuit breaker opened.", source="self"),
     F("kgs_pmc_retries_total", "counter", "Reader resets + re-STARTs attempted while the breaker was open.",
       source="self"),
+    F("kgs_pmc_publishes_total", "counter", "Counter READs that wrote the GPU's L2 back to publish their results "
+      "to the host.  With --pmc-batch B at most one READ in B does (the writeback is about half of what a READ "
+      "costs a training step); a READ never waits more than --pmc-publish-us for it, so at <= 1 kHz every READ "
+      "publishes.", source="self"),
+    F("kgs_pmc_unlanded_total", "counter", "Batched counter READ results still unwritten in host memory when their "
+      "batch was folded (taken after a 200 us wait).  Should stay 0; a rising count means --pmc-batch 1.",
+      source="self"),
     F("kgs_sampler_thread_hung", "gauge", "1 if a sampler thread of the device was stuck in a device call when "
       "sampling last stopped: it was abandoned (--stop-timeout) and that tier restarts once the call returns.",
       source="self"),

@@ -1163,9 +1163,11 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
     rc = read_batched(a, &ts);
   } else if (a->pipelined) {
     rc = read_pipelined(a, &ts);
+    if (rc == 0) ++a->publishes;  // every unbatched READ writes the L2 back
   } else {
     rc = read_values(a);
     ts = t0 + a->rtt_ns / 2;
+    if (rc == 0) ++a->publishes;
   }
   const int64_t t1 = mono_ns();
   a->host_ns += t1 - t0;
@@ -1214,6 +1216,19 @@ int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
   }
   a->pipelined = on != 0;
   return 0;
+}
+
+// Publication counters for the exporter's self-metrics (any thread: atomics only):
+// out[0] READs folded, out[1] READs that wrote the L2 back (every READ unless
+// batched), out[2] batched READ results still unwritten when their half was
+// folded (land timeouts: should stay 0).  Returns the number of values written.
+int kgs_pmc_stats(int handle, uint64_t* out, int n) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size() || !out) return -1;
+  const Agent* a = g_agents[static_cast<size_t>(handle)];
+  const uint64_t v[3] = {a->reads.load(), a->publishes.load(), a->land_timeouts.load()};
+  const int m = std::min(n, 3);
+  for (int i = 0; i < m; ++i) out[i] = v[i];
+  return m;
 }
 
 int kgs_pmc_info(int handle, char* buf, int len) {

@@ -129,6 +129,13 @@ class CounterSource {
   virtual void cancel(int dev, bool on) {}
   // Counters of the fault boundary (for kgs_pmc_* self-metrics): resets done.
   virtual uint64_t resets(int dev) const { return 0; }
+  // Publication of READ results (batched reader, include/kgs/aql_batch.h): READs
+  // folded, READs that wrote the GPU's L2 back, and results that had not reached
+  // host memory when folded.  Any thread.  false = the source does not say.
+  struct PublishStats {
+    uint64_t reads = 0, publishes = 0, unlanded = 0;
+  };
+  virtual bool publish_stats(int dev, PublishStats& out) const { return false; }
 };
 
 struct MockPmcConfig {

@@ -112,6 +112,13 @@ class MockCounterSource final : public CounterSource {
   uint64_t resets(int dev) const override {
     return dev >= 0 && static_cast<size_t>(dev) < fault_.size() ? fault_[static_cast<size_t>(dev)]->resets.load() : 0;
   }
+  bool publish_stats(int dev, PublishStats& out) const override {  // one writeback per `batch` READs
+    if (dev < 0 || static_cast<size_t>(dev) >= fault_.size()) return false;
+    out.reads = fault_[static_cast<size_t>(dev)]->samples.load();
+    out.publishes = out.reads / static_cast<uint64_t>(std::max(c_.batch, 1));
+    out.unlanded = 0;
+    return true;
+  }
   int sample(int dev, PmcSample& s) override {
     if (dev >= 0 && static_cast<size_t>(dev) < fault_.size()) {
       Fault& f = *fault_[static_cast<size_t>(dev)];
@@ -219,6 +226,7 @@ using close_fn = void (*)(int);
 using info_fn = int (*)(int, char*, int);
 using abort_fn = int (*)(int, int);
 using reset_fn = int (*)(int);
+using stats_fn = int (*)(int, uint64_t*, int);
 
 class DlCounterSource final : public CounterSource {
  public:
@@ -255,6 +263,7 @@ class DlCounterSource final : public CounterSource {
     if (configure && batch > 1 && publish_us >= 0) configure("publish_us", publish_us);
     abort_ = reinterpret_cast<abort_fn>(dlsym(lib_, "kgs_pmc_abort"));  // optional (aqlprofile reader)
     reset_ = reinterpret_cast<reset_fn>(dlsym(lib_, "kgs_pmc_reset"));  // optional
+    stats_ = reinterpret_cast<stats_fn>(dlsym(lib_, "kgs_pmc_stats"));  // optional
     char ebuf[512] = {};
     if (init(ebuf, sizeof ebuf) != 0) {
       err = std::string("kgs_pmc_init: ") + ebuf;
@@ -342,6 +351,17 @@ class DlCounterSource final : public CounterSource {
   uint64_t resets(int dev) const override {
     return dev >= 0 && dev < static_cast<int>(resets_.size()) ? resets_[static_cast<size_t>(dev)].load() : 0;
   }
+  // By agent, not by session handle: the totals survive hand-overs and resets.
+  bool publish_stats(int dev, PublishStats& out) const override {
+    if (!stats_ || dev < 0 || dev >= static_cast<int>(agent_.size())) return false;
+    const int a = agent_[static_cast<size_t>(dev)];
+    uint64_t v[3] = {};
+    if (a < 0 || stats_(a, v, 3) != 3) return false;
+    out.reads = v[0];
+    out.publishes = v[1];
+    out.unlanded = v[2];
+    return true;
+  }
   void set_fresh(int dev, bool fresh) override {
     if (!pipelined_ || !set_pipe_ || dev < 0 || dev >= static_cast<int>(handles_.size())) return;
     const int h = handles_[static_cast<size_t>(dev)];
@@ -402,6 +422,7 @@ class DlCounterSource final : public CounterSource {
   info_fn info_ = nullptr;
   abort_fn abort_ = nullptr;
   reset_fn reset_ = nullptr;
+  stats_fn stats_ = nullptr;
   std::vector<std::atomic<int>> agent_;  // per device: reader agent index once opened (-1 never)
   std::vector<std::atomic<uint64_t>> resets_;
   // Written by the device's sampler thread (release / acquire), read by info()

@@ -741,6 +741,23 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_breaker_trips_total", dev_labels_[d], nullptr, S.state(d).pmc_breaker_trips.load());
     w.head("kgs_pmc_retries_total", "counter", "Reader resets + re-STARTs attempted while the breaker was open");
     for (int d : ids) w.line_u("kgs_pmc_retries_total", dev_labels_[d], nullptr, S.state(d).pmc_retries.load());
+    if (pmc_) {
+      std::vector<std::pair<int, CounterSource::PublishStats>> ps;
+      for (int d : ids) {
+        CounterSource::PublishStats p;
+        if (pmc_->publish_stats(d, p)) ps.emplace_back(d, p);
+      }
+      if (!ps.empty()) {
+        w.head("kgs_pmc_publishes_total", "counter",
+               "Counter READs that wrote the GPU's L2 back to publish their results to the host (--pmc-batch: one per "
+               "batch of READs at high rates; every READ when unbatched)");
+        for (const auto& [d, p] : ps) w.line_u("kgs_pmc_publishes_total", dev_labels_[d], nullptr, p.publishes);
+        w.head("kgs_pmc_unlanded_total", "counter",
+               "Batched counter READ results not yet in host memory when their batch was folded (taken after a "
+               "200 us wait; should stay 0)");
+        for (const auto& [d, p] : ps) w.line_u("kgs_pmc_unlanded_total", dev_labels_[d], nullptr, p.unlanded);
+      }
+    }
   }
   w.head("kgs_sampler_thread_hung", "gauge",
          "1 if a sampler thread of the device was stuck in a device call when sampling last stopped (it was "

@@ -631,6 +631,11 @@ def test_batched_counter_source_is_not_a_failure(mock_exporter):
     assert w["gpu_active_pct"] == pytest.approx(40, abs=3), w
     m = parse_text(ex.render())
     assert m["kgs_pmc_refreshes_total"][0][1] >= 3
+    # one L2 writeback per 8 READs, every result landed
+    reads = ex.integrals(0)["pmc_samples"]
+    pub = m["kgs_pmc_publishes_total"][0][1]
+    assert 0.9 * reads / 8 <= pub <= 1.3 * reads / 8 + 10, (pub, reads)
+    assert [v for _, v in m["kgs_pmc_unlanded_total"]] == [0, 0]
 
 
 def test_throttle_seconds_by_reason(mock_exporter):
