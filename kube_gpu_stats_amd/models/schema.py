@@ -204,8 +204,10 @@ CATALOG: tuple[Family, ...] = (
       "to the host.  With --pmc-batch B at most one READ in B does (the writeback is about half of what a READ "
       "costs a training step); a READ never waits more than --pmc-publish-us for it, so at <= 1 kHz every READ "
       "publishes.", source="self"),
-    F("kgs_pmc_unlanded_total", "counter", "Batched counter READ results still unwritten in host memory when their "
-      "batch was folded (taken after a 200 us wait).  Should stay 0; a rising count means --pmc-batch 1.",
+    F("kgs_pmc_unlanded_total", "counter", "Batched counter READs dropped because a result was still unwritten in "
+      "host memory when their batch was folded (after a 200 us wait; the counters are cumulative, so the next sample "
+      "covers the interval).  Should stay near 0 (a result dword that really reads 0xFFFFFFFF is dropped too, about "
+      "one READ in 5e7); a steady rate means --pmc-batch 1.",
       source="self"),
     F("kgs_sampler_thread_hung", "gauge", "1 if a sampler thread of the device was stuck in a device call when "
       "sampling last stopped: it was abandoned (--stop-timeout) and that tier restarts once the call returns.",

@@ -760,12 +760,16 @@ int read_pipelined(Agent* a, int64_t* ts) {
 // waits more than the publish interval (1 ms) for its publisher, so at low rates
 // every READ publishes.  Every result dword is pre-set to kUnlanded and checked
 // before the fold (wait_landed): a dword the writeback missed is waited for,
-// briefly, and counted.
+// briefly; if it still reads kUnlanded the READ is dropped and counted.  The
+// counters are cumulative, so the next sample's interval covers a dropped one and
+// nothing is lost but resolution (a dword that really holds 0xFFFFFFFF, about one
+// READ in 5·10^7, is dropped the same way).
 constexpr uint32_t kUnlanded = 0xFFFFFFFFu;
 
 bool is_publisher(const Agent* a, int k) { return a->batch < 2 || a->plan.is_publisher(k); }
 
-void wait_landed(Agent* a, int k) {
+// true = every result dword of slot k was written (fold it), false = drop the READ.
+bool wait_landed(Agent* a, int k) {
   const int64_t t0 = mono_ns();
   bool waited = false;
   for (;;) {
@@ -780,13 +784,14 @@ void wait_landed(Agent* a, int k) {
       waited = true;
       a->land_waits.fetch_add(1, std::memory_order_relaxed);
     }
-    if (mono_ns() - t0 > 200000) {  // a counter half may really read 0xFFFFFFFF: take it
+    if (mono_ns() - t0 > 200000) {
       a->land_timeouts.fetch_add(1, std::memory_order_relaxed);
-      break;
+      return false;
     }
     sched_yield();
   }
   std::atomic_thread_fence(std::memory_order_acquire);
+  return true;
 }
 
 void batch_reset(Agent* a) {
@@ -807,8 +812,7 @@ void batch_collect(Agent* a, int h) {
   const int n = a->plan.slots(h, ks);
   for (int j = 0; j < n; ++j) {
     const int k = ks[j];
-    wait_landed(a, k);
-    if (fold(a, &a->pprof[k]) != 0) continue;
+    if (!wait_landed(a, k) || fold(a, &a->pprof[k]) != 0) continue;
     Agent::Ready r;
     r.vals = a->vals;
     r.vals_xcd = a->vals_xcd;

@@ -753,8 +753,8 @@ void Exporter::render(std::string& out) {
                "batch of READs at high rates; every READ when unbatched)");
         for (const auto& [d, p] : ps) w.line_u("kgs_pmc_publishes_total", dev_labels_[d], nullptr, p.publishes);
         w.head("kgs_pmc_unlanded_total", "counter",
-               "Batched counter READ results not yet in host memory when their batch was folded (taken after a "
-               "200 us wait; should stay 0)");
+               "Batched counter READs dropped because a result was not in host memory when their batch was folded "
+               "(after a 200 us wait; the next sample covers the interval; should stay near 0)");
         for (const auto& [d, p] : ps) w.line_u("kgs_pmc_unlanded_total", dev_labels_[d], nullptr, p.unlanded);
       }
     }
