@@ -63,4 +63,8 @@ def test_rocprof_overhead_splits_by_condition(tmp_path):
         k = r[kind]
         assert abs(k["B_vs_AC_pct"] - 2.0) < 1e-9, k
         assert abs(k["I_8000Hz_vs_paused_pct"] - 1.0) < 1e-9 and abs(k["I_100Hz_vs_paused_pct"]) < 1e-9, k
-    assert "| mfma |" in (tmp_path / "o.md").read_text()
+        # paired per round (two rounds of three blocks): every round says +1 % / 0 %
+        assert k["rounds"] == 2 and abs(k["I_8000Hz_vs_paused_paired_pct"] - 1.0) < 1e-9, k
+        assert abs(k["I_8000Hz_vs_paused_ci95_pct"]) < 1e-9 and abs(k["I_100Hz_vs_paused_paired_pct"]) < 1e-9, k
+    md = (tmp_path / "o.md").read_text()
+    assert "| mfma |" in md and "+1.000 ± 0.000" in md

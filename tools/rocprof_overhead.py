@@ -16,7 +16,10 @@ bench.py launches, per rank, in this order (``load`` units: one
   ``config.units_per_step`` units.
 
 Kernels are assigned to segments by launch order, so no clock translation between
-rocprofv3 and Python is needed.
+rocprofv3 and Python is needed.  The interleaved blocks come in rounds of one block
+per condition (bench.py's order design), so each tier's per-kernel difference to the
+paused block of the same round gives one paired value per round; the tables report
+their mean with a 95 % CI (t-quantile 1.96 · sd / sqrt(rounds)).
 
     python tools/rocprof_overhead.py <trace dir> <bench.json> [--out md]
 """
@@ -90,10 +93,12 @@ def main():
             continue
         i = calib[kind]
         groups: dict[str, list[float]] = {}
+        blocks: list[tuple[str, float]] = []  # interleaved blocks in order: (label, mean µs)
         for label, units, extra in seg:
             n = units * per_unit[kind] + extra.get(kind, 0)
-            key = label if not label.startswith("I_") else label
-            groups.setdefault(key, []).extend(xs[i:i + n])
+            groups.setdefault(label, []).extend(xs[i:i + n])
+            if label.startswith("I_") and n:
+                blocks.append((label, statistics.fmean(xs[i:i + n])))
             i += n
         if i != len(xs):
             out["kernels"][kind] = {"error": f"expected {i} launches, found {len(xs)}"}
@@ -107,6 +112,16 @@ def main():
             for g in mean:
                 if g.startswith("I_") and g != "I_paused":
                     r[f"{g}_vs_paused_pct"] = 100.0 * (mean[g] / mean["I_paused"] - 1.0)
+            ncond = len({lb for lb, _ in blocks})
+            rounds = [dict(blocks[j:j + ncond]) for j in range(0, len(blocks) - ncond + 1, ncond)]
+            for g in mean:
+                if not g.startswith("I_") or g == "I_paused":
+                    continue
+                d = [100.0 * (rd[g] / rd["I_paused"] - 1.0) for rd in rounds if g in rd and "I_paused" in rd]
+                if len(d) >= 2:
+                    r[f"{g}_vs_paused_paired_pct"] = statistics.fmean(d)
+                    r[f"{g}_vs_paused_ci95_pct"] = 1.96 * statistics.stdev(d) / len(d) ** 0.5
+                    r["rounds"] = len(d)
         out["kernels"][kind] = r
     print(json.dumps(out, indent=1))
     if a.out:
@@ -116,15 +131,20 @@ def main():
                  "launch order (`tools/rocprof_overhead.py`).  A / C: no exporter process; B: sampling at 8 kHz; "
                  "I_*: interleaved blocks, exporter paused or sampling at 100 Hz / 8 kHz.", "",
                  "| kernel | " + " | ".join(f"{c} mean µs" for c in conds) + " | B vs A/C % | 100 Hz vs paused % | "
-                 "8 kHz vs paused % |", "|---" * (len(conds) + 4) + "|"]
+                 "8 kHz vs paused % | 100 Hz paired (95 % CI) | 8 kHz paired (95 % CI) |", "|---" * (len(conds) + 6) + "|"]
         for kind, r in out["kernels"].items():
             if "error" in r:
                 lines.append(f"| {kind} | {r['error']} |")
                 continue
             m = r["mean_us"]
             cells = " | ".join(f"{m[c]:.3f}" if c in m else "" for c in conds)
+            pair = lambda g: (f"{r[g + '_vs_paused_paired_pct']:+.3f} ± {r[g + '_vs_paused_ci95_pct']:.3f}"  # noqa: E731
+                              if g + "_vs_paused_ci95_pct" in r else "")
             lines.append(f"| {kind} | {cells} | {r['B_vs_AC_pct']:+.3f} | {r.get('I_100Hz_vs_paused_pct', 0):+.3f} | "
-                         f"{r.get('I_8000Hz_vs_paused_pct', 0):+.3f} |")
+                         f"{r.get('I_8000Hz_vs_paused_pct', 0):+.3f} | {pair('I_100Hz')} | {pair('I_8000Hz')} |")
+        if any("rounds" in r for r in out["kernels"].values()):
+            lines += ["", f"Paired: {max(r.get('rounds', 0) for r in out['kernels'].values())} rounds, each tier's "
+                      "block against the paused block of the same round."]
         with open(a.out, "w") as f:
             f.write("\n".join(lines) + "\n")
 
