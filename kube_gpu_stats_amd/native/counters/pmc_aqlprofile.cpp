@@ -22,6 +22,12 @@
 //     instead of the full cache invalidate) and its AQL header has no acquire
 //     fence, only the system-scope release that orders the completion signal
 //     after the results (profiles/launch_overhead.md);
+//   * batched publication (--pmc-batch, default 8; read_batched and
+//     include/kgs/aql_batch.h): the READs rotate over 2B slots and only the last
+//     READ of each half keeps the L2 writeback and the release fence, at most
+//     1 ms after the half's first READ; its completion publishes the whole half
+//     (packets run in order), so at 8 kHz the L2 is written back 1000 times a
+//     second instead of 8000 (profiles/r3/README.md r3i-r3k);
 //   * results are folded per counter over every block instance / XCC sample
 //     (max for GRBM clocks, sum for SQ busy cycles, mean for TA busy), the same
 //     reductions as the rocprofiler path, and reported cumulative since START;
