@@ -142,6 +142,12 @@ def build() -> dict:
                [(_dev("kgs_up"), "up gpu{{gpu}}"), (_dev("increase(kgs_device_recoveries_total[1h])"),
                                                    "recoveries gpu{{gpu}}"),
                 ("kgs_attribution_kubelet_age_seconds", "kubelet age {{instance}}")], 16, y, w=8))
+    y += 8
+    # batched READ publication: ~1000 writebacks/s per GPU at 8 kHz (--pmc-batch 8), every
+    # READ at <= 1 kHz; dropped READs (results not in host memory) should stay at 0
+    add(_panel(0, "Counter READ publication (L2 writebacks / s, dropped READs / s)",
+               [(_dev("rate(kgs_pmc_publishes_total[1m])"), "writebacks gpu{{gpu}}"),
+                (_dev("rate(kgs_pmc_unlanded_total[5m])"), "dropped gpu{{gpu}}")], 0, y, w=8))
 
     return {
         "title": "MI355X GPU stats (kube_gpu_stats_amd)",
