@@ -223,6 +223,8 @@ def test_kgs_pmc_release_one_gpu_via_cli():
         en = {ln.split('gpu="')[1].split('"')[0]: float(ln.rsplit(" ", 1)[1])
               for ln in st.stdout.splitlines() if ln.startswith("kgs_pmc_enabled")}
         assert en == {"0": 1.0, "1": 1.0, "2": 0.0, "3": 1.0}
+        pub = [ln for ln in st.stdout.splitlines() if ln.startswith(("kgs_pmc_publishes_total", "kgs_pmc_unlanded_total"))]
+        assert len(pub) == 8, st.stdout  # READ publication counters of every GPU
     finally:
         p.stdin.write("quit\n")
         p.stdin.flush()
