@@ -781,21 +781,27 @@ def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
         for mode, hz in (("adaptive", 100), ("profiling", 0)):
             urllib.request.urlopen(f"{ctl}?hz={hz}", timeout=5).read()
             time.sleep(0.3)
-            n0 = one(parse_text(sc.get()), "kgs_pmc_samples_total")
+            m0 = parse_text(sc.get())
+            n0 = one(m0, "kgs_pmc_samples_total")
             time.sleep(1.8)  # idle: this process launches nothing
             m = parse_text(sc.get())
             rows[mode] = {"reads_per_s": (one(m, "kgs_pmc_samples_total") - n0) / 1.8,
+                          "publishes_per_s": (one(m, "kgs_pmc_publishes_total") - one(m0, "kgs_pmc_publishes_total")) / 1.8,
                           "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent"),
                           "gpu_active_pct": one(m, "amdgpu_gpu_active_percent"),
                           "quiet": one(m, "kgs_pmc_quiet")}
         urllib.request.urlopen(f"{ctl}?hz=100", timeout=5).read()
-        n0 = one(parse_text(sc.get()), "kgs_pmc_samples_total")
+        m0 = parse_text(sc.get())
+        n0 = one(m0, "kgs_pmc_samples_total")
         t0 = time.time()
         while time.time() - t0 < 1.6:
             ls.run_mfma()
             torch.cuda.synchronize()
         m = parse_text(sc.get())
-        rows["mfma_load"] = {"reads_per_s": (one(m, "kgs_pmc_samples_total") - n0) / (time.time() - t0),
+        dt = time.time() - t0
+        rows["mfma_load"] = {"reads_per_s": (one(m, "kgs_pmc_samples_total") - n0) / dt,
+                             "publishes_per_s": (one(m, "kgs_pmc_publishes_total") - one(m0, "kgs_pmc_publishes_total")) / dt,
+                             "unlanded": one(m, "kgs_pmc_unlanded_total"),
                              "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent"),
                              "gpu_active_pct": one(m, "amdgpu_gpu_active_percent"),
                              "mfma_util_pct": one(m, "amdgpu_mfma_util_percent"), "quiet": one(m, "kgs_pmc_quiet")}
@@ -816,6 +822,11 @@ def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
     assert p["gpu_active_pct"] < 2, p                                    # ... which SPI busy does not see
     assert ld["reads_per_s"] > 7000, ld  # a loaded GPU gets every tick (quiet again by the scrape after it)
     assert ld["gpu_active_pct"] > 80 and ld["mfma_util_pct"] > 50, ld
+    # batched publication (--pmc-batch 8, ≤ 1 ms): at 8 kHz about one READ in 8 writes the
+    # L2 back; the quiet GPU's synchronous 100 Hz READs each do
+    assert 0.08 * ld["reads_per_s"] <= ld["publishes_per_s"] <= 0.25 * ld["reads_per_s"], ld
+    assert ld["unlanded"] == 0, ld
+    assert a["publishes_per_s"] >= 0.9 * a["reads_per_s"], a
 
 
 def test_dispatch_gap_rate_follows_the_kernel_stream(torch_dev):
