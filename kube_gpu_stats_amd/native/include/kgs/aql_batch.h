@@ -17,6 +17,11 @@
 // second instead of 8000; at a quiet GPU's 100 Hz, or any --hz <= 1 kHz, every
 // READ publishes and a sample is one tick late, as without batching.
 //
+// The price is the delay line: after each (re)start of the rotation (a START, a
+// quiet GPU turning busy) about B calls return no sample (kPmcPending) while the
+// first half fills.  Nothing is lost but resolution — the counters are
+// cumulative, so the next sample's interval covers those ticks.
+//
 // Pure bookkeeping, single-threaded (one sampler thread per device), header-only
 // so the policy is unit-tested without a GPU (native/tests/test_core.cpp).
 #pragma once
