@@ -735,6 +735,33 @@ static void test_batch_plan() {
   p.configure(4, 0);
   for (int j = 0; j < 4; ++j) CHECK(submit(50000000) == j);
   CHECK(p.closed(0) && p.slots(0, ks) == 4);
+  // Random tick intervals (10 µs .. 3 ms): every half holds its first slots in order
+  // plus the publisher, never more than B READs, and no READ waits 1 ms or more for
+  // the submission of its publisher unless it is the half's only READ.
+  std::mt19937_64 rng(7);
+  std::uniform_int_distribution<int64_t> dt(10000, 3000000);
+  p.configure(8, 1000000);
+  int64_t first = 0;
+  int n_in_half = 0;
+  for (int i = 0; i < 20000; ++i) {
+    const int h = p.current_half();
+    if (p.closed(h)) p.collected(h);
+    const int64_t step = dt(rng);
+    t += step;
+    const int k = p.next_slot(t);
+    CHECK(k / 8 == h);
+    if (n_in_half == 0) first = t;
+    p.submitted(k, t);
+    ++n_in_half;
+    if (p.is_publisher(k)) {
+      CHECK(p.slots(h, ks) == n_in_half && n_in_half <= 8 && ks[n_in_half - 1] == k);
+      for (int j = 0; j + 1 < n_in_half; ++j) CHECK(ks[j] == h * 8 + j);
+      CHECK(n_in_half == 1 || t - first < 1000000 + 3000000);
+      n_in_half = 0;
+    } else {
+      CHECK(t - first < 1000000);  // a non-publisher is only submitted while the half is young
+    }
+  }
   std::printf("batch plan ok\n");
 }
 
