@@ -146,7 +146,6 @@ struct Agent {
   int batch = 1;                                     // B of the current slot set (1 = every READ publishes)
   int nslots = 2;
   kgs::BatchPlan plan;
-  hsa_signal_t shared_sig{};                         // KGS_AQL_BATCH_SIG=shared: every non-publisher's signal
   std::vector<volatile uint32_t*> pdst[kMaxSlots];   // each slot's COPY_DATA destination dwords
   bool bprimed = false;
   struct Ready {
@@ -458,36 +457,6 @@ int wait_done(Agent* a, hsa_signal_t sig) {
 // Put one packet on the queue and wait for it (both bounded).
 int submit(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl) {
   if (enqueue(a, tmpl, a->sig) != 0) return -1;
-  return wait_done(a, a->sig);
-}
-
-// Wait (bounded) until every packet queued so far has completed: a BARRIER_AND
-// packet (no dependencies, barrier bit) completes only after all packets before
-// it, and its completion signal is a->sig.  For READs whose own signal is not
-// waitable (shared non-publisher signal).  0 = done.
-int drain_queue(Agent* a) {
-  hsa_queue_t* q = a->queue;
-  if (!q) return -1;
-  uint64_t idx = 0;
-  const kgs::SlotResult r = kgs::reserve_slot(
-      q->size, mono_ns() + g_timeout_ns.load(std::memory_order_relaxed), &a->abort,
-      [q] { return hsa_queue_load_read_index_scacquire(q); }, [q] { return hsa_queue_load_write_index_relaxed(q); },
-      [q](uint64_t i) { hsa_queue_store_write_index_relaxed(q, i + 1); }, [] { return mono_ns(); },
-      [] { sched_yield(); }, idx);
-  if (r != kgs::SlotResult::kOk) {
-    (r == kgs::SlotResult::kAborted ? a->aborted : a->enqueue_timeouts).fetch_add(1, std::memory_order_relaxed);
-    return -1;
-  }
-  hsa_signal_store_relaxed(a->sig, 1);
-  auto* slot = reinterpret_cast<hsa_barrier_and_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  std::memset(reinterpret_cast<char*>(slot) + sizeof(uint16_t), 0, sizeof(*slot) - sizeof(uint16_t));
-  slot->completion_signal = a->sig;
-  const uint16_t header = static_cast<uint16_t>((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                                                (1 << HSA_PACKET_HEADER_BARRIER) |
-                                                (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                                (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-  __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
-  hsa_signal_store_screlease(q->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
   return wait_done(a, a->sig);
 }
 
@@ -805,23 +774,6 @@ constexpr uint32_t kUnlanded = 0xFFFFFFFFu;
 
 bool is_publisher(const Agent* a, int k) { return a->batch < 2 || a->plan.is_publisher(k); }
 
-// KGS_AQL_BATCH_SIG=shared (experiment): the non-publishers of a batch complete on
-// one shared signal whose only consumer is the GPU agent — a plain memory word, no
-// KFD event and no interrupt per READ — since nobody waits for them; only the
-// publisher keeps its own waitable signal.  Default "own": every slot its own.
-bool shared_batch_sig() {
-  static const bool on = [] {
-    const char* e = std::getenv("KGS_AQL_BATCH_SIG");
-    return e && std::strcmp(e, "shared") == 0;
-  }();
-  return on;
-}
-
-// The completion signal READ k is submitted with.
-hsa_signal_t read_signal(const Agent* a, int k) {
-  return a->batch >= 2 && a->shared_sig.handle && !a->plan.is_publisher(k) ? a->shared_sig : a->psig[k];
-}
-
 // true = every result dword of slot k was written (fold it), false = drop the READ.
 bool wait_landed(Agent* a, int k) {
   const int64_t t0 = mono_ns();
@@ -854,17 +806,9 @@ void batch_reset(Agent* a) {
   a->bready.clear();
 }
 
-// Wait (bounded) until the last READ submitted has completed.
-void batch_wait_last(Agent* a) {
-  const int k = a->plan.last();
-  if (a->batch < 2 || k < 0) return;
-  if (read_signal(a, k).handle == a->psig[k].handle) wait_done(a, a->psig[k]);
-  else drain_queue(a);
-}
-
 // Wait (bounded) for the last READ submitted, then forget the batch state.
 void batch_drain(Agent* a) {
-  batch_wait_last(a);
+  if (a->batch >= 2 && a->plan.last() >= 0) wait_done(a, a->psig[a->plan.last()]);
   batch_reset(a);
 }
 
@@ -919,8 +863,8 @@ int read_batched(Agent* a, int64_t* ts) {
   a->psubmit_ns[k] = mono_ns();
   const std::pair<int, int> none{HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_NONE};
   const bool pub = p.is_publisher(k);
-  if (enqueue(a, a->pread[k], read_signal(a, k), pub ? read_fences() : none) != 0) {
-    batch_wait_last(a);
+  if (enqueue(a, a->pread[k], a->psig[k], pub ? read_fences() : none) != 0) {
+    if (p.last() >= 0) wait_done(a, a->psig[p.last()]);
     batch_reset(a);
     return -2;
   }
@@ -953,9 +897,6 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
   a->batch = batch_size();
   a->nslots = a->batch >= 2 ? 2 * a->batch : 2;
   if (a->batch >= 2) a->plan.configure(a->batch, g_publish_ns);
-  if (a->batch >= 2 && shared_batch_sig() && !a->shared_sig.handle &&
-      hsa_amd_signal_create(1, 1, &a->agent, 0, &a->shared_sig) != HSA_STATUS_SUCCESS)
-    a->shared_sig.handle = 0;  // keep per-slot signals
   batch_reset(a);
   for (int k = 0; k < a->nslots; ++k) {
     hsa_ven_amd_aqlprofile_profile_t& p = a->pprof[k];
@@ -1318,7 +1259,6 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";land_timeouts=" + std::to_string(a->land_timeouts.load()) +
                   ";publishes=" + std::to_string(a->publishes.load()) +
                   ";publish_us=" + std::to_string(g_publish_ns / 1000) +
-                  ";batch_sig=" + (a->shared_sig.handle ? "shared" : "own") +
                   ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
                   a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc) + ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
                   ";signal=" + (poll_signals() ? "poll" : "interrupt");
