@@ -79,7 +79,7 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                       "(0 = off; ignored in profiling mode)")
     add_flag(ap, "pmc-gap-hz", 1000.0, "counter READ rate in a dispatch gap (--pmc-busy-min)")
     add_flag(ap, "pmc-gap-hold-ms", 1.0, "low-occupancy READ intervals in a row, in ms, before the gap rate applies")
-    add_flag(ap, "pmc-batch", 8, "counter READs per L2 writeback: a READ's results sit in the GPU's L2 until "
+    add_flag(ap, "pmc-batch", 8, choices=range(1, 17), help="counter READs per L2 writeback: a READ's results sit in the GPU's L2 until "
                                  "written back, and that writeback is half of what a READ costs a training step; "
                                  "with B > 1 at most every B-th READ writes back (at 8 kHz samples arrive B-2B ticks "
                                  "late; 1 = every READ)")
