@@ -68,3 +68,14 @@ def test_rocprof_overhead_splits_by_condition(tmp_path):
         assert abs(k["I_8000Hz_vs_paused_ci95_pct"]) < 1e-9 and abs(k["I_100Hz_vs_paused_paired_pct"]) < 1e-9, k
     md = (tmp_path / "o.md").read_text()
     assert "| mfma |" in md and "+1.000 ± 0.000" in md
+
+
+def test_soak_tool_on_the_mock(tmp_path):
+    """tools/soak.py rehearsed on the mock GPU: windows come out, nothing fails."""
+    out = tmp_path / "soak.json"
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "soak.py"), "--mock", "--seconds", "11",
+                    "--window", "5", "--hz", "500", "--out", str(out)], cwd=REPO, capture_output=True, text=True,
+                   check=True, timeout=120)
+    r = json.loads(out.read_text())
+    assert r["fail"] == [] and len(r["windows"]) >= 2, r
+    assert all(w["pmc_samples_per_s"] > 400 and w["pmfw_tables_per_s"] > 40 for w in r["windows"]), r
