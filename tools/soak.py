@@ -42,6 +42,25 @@ def cpu_s(pid: int) -> float:
     return (int(parts[11]) + int(parts[12])) / os.sysconf("SC_CLK_TCK")
 
 
+def thread_cpu(pid: int) -> dict:
+    """Per-thread utime + stime in seconds, keyed ``<comm>/<tid>``."""
+    out = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                raw = f.read()
+            fields = raw.rsplit(")", 1)[1].split()
+            out[f"{raw[raw.index('(') + 1:raw.rindex(')')]}/{tid}"] = (int(fields[11]) + int(fields[12])) / tck
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=240)
@@ -91,7 +110,7 @@ def main() -> int:
                 "kgs_scrapes_total", "kgs_sampler_thread_hung", "amdgpu_gpu_active_seconds_total")
         snap = lambda: {f: one(parse_text(sc.get()), f) for f in fams}  # noqa: E731
         t_start = time.time()
-        w_t0, w_m0, w_cpu0 = t_start, snap(), cpu_s(proc.pid)
+        w_t0, w_m0, w_cpu0, w_thr0 = t_start, snap(), cpu_s(proc.pid), thread_cpu(proc.pid)
         w_loaded = 0.0
         last_handover = t_start
         next_scrape = t_start
@@ -124,7 +143,7 @@ def main() -> int:
                 urllib.request.urlopen(base + "/control/pmc/acquire", timeout=10).read()
                 last_handover = time.time()
             if now - w_t0 >= a.window:
-                m1, t1, c1 = snap(), time.time(), cpu_s(proc.pid)
+                m1, t1, c1, thr1 = snap(), time.time(), cpu_s(proc.pid), thread_cpu(proc.pid)
                 dt = t1 - w_t0
                 d = {f: m1[f] - w_m0[f] for f in fams}
                 w = {"t": round(t1 - t_start, 1), "pmc_samples_per_s": round(d["kgs_pmc_samples_total"] / dt, 1),
@@ -137,10 +156,13 @@ def main() -> int:
                      "refreshes": d["kgs_pmc_refreshes_total"], "handovers": d["kgs_pmc_releases_total"],
                      "render_ms": round(1e3 * d["kgs_scrape_render_seconds_total"] / max(d["kgs_scrapes_total"], 1), 3),
                      "rss_mib": round(rss_mib(proc.pid), 1), "cpu_cores": round((c1 - w_cpu0) / dt, 4),
-                     "thread_hung": m1["kgs_sampler_thread_hung"]}
+                     "thread_hung": m1["kgs_sampler_thread_hung"],
+                     # the threads that used ≥ 1 % of a core in the window
+                     "cpu_by_thread": {k: round((v - w_thr0.get(k, 0.0)) / dt, 4) for k, v in thr1.items()
+                                       if v - w_thr0.get(k, 0.0) >= 0.01 * dt}}
                 windows.append(w)
                 print(json.dumps(w), flush=True)
-                w_t0, w_m0, w_cpu0, w_loaded = t1, m1, c1, 0.0
+                w_t0, w_m0, w_cpu0, w_thr0, w_loaded = t1, m1, c1, thr1, 0.0
     finally:
         try:
             proc.stdin.write("quit\n")
