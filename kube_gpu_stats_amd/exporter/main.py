@@ -51,8 +51,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "mock-partition", "SPX", "mock provider: compute partition mode (SPX | DPX | QPX | CPX)")
     add_flag(ap, "hz", 10.0, "sampler tick rate per GPU (1/10/100 Hz tiers; hardware counters every tick)")
     add_flag(ap, "pmfw-hz", 100.0, "cap on PMFW metrics-table reads/s (firmware refreshes it every ~20 ms)")
-    add_flag(ap, "proc-every", 10, "per-process tier every N fast ticks (0 = off)")
-    add_flag(ap, "link-every", 100, "xGMI link tier every N fast ticks (0 = off)")
+    add_flag(ap, "proc-every", 10, "per-process tier every N fast ticks, at most 10 Hz (0 = off)")
+    add_flag(ap, "link-every", 100, "xGMI link tier every N fast ticks, at most 1 Hz (0 = off)")
     add_flag(ap, "proc-period", 0.0, "per-process tier period in seconds (overrides --proc-every; survives rate "
                                      "changes)")
     add_flag(ap, "link-period", 0.0, "xGMI link + RAS tier period in seconds (overrides --link-every)")
@@ -133,8 +133,26 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     return ap
 
 
+# Floors of the tick-counted AMD SMI tiers.  --proc-every / --link-every count fast
+# ticks, which suits the 10 Hz DaemonSet rate; at the counter tier's kHz rates the
+# defaults (10 / 100 ticks) would poll AMD SMI's process list 800 times a second and
+# keep the node-wide slow thread on a core (r3q soak: 0.33-0.43 cores at 8 kHz).
+# Unless --proc-period / --link-period say otherwise, the tiers run no faster than
+# 10 Hz / 1 Hz.
+MIN_PROC_PERIOD_S = 0.1
+MIN_LINK_PERIOD_S = 1.0
+
+
+def tier_periods(a) -> tuple[float, float]:
+    """(per-process, link) tier periods in seconds; 0 = off."""
+    proc = a.proc_period or (max(a.proc_every / a.hz, MIN_PROC_PERIOD_S) if a.proc_every > 0 and a.hz > 0 else 0.0)
+    link = a.link_period or (max(a.link_every / a.hz, MIN_LINK_PERIOD_S) if a.link_every > 0 and a.hz > 0 else 0.0)
+    return proc, link
+
+
 def config_from_args(a) -> dict:
     host, _, port = a.listen.rpartition(":")
+    proc_period, link_period = tier_periods(a)
     cfg = {
         "backend": a.backend,
         "mock": {"n_gpus": a.mock_gpus, "fail_rate": a.mock_fail_rate, "compute_partition": a.mock_partition,
@@ -143,8 +161,8 @@ def config_from_args(a) -> dict:
         "pmfw_hz": a.pmfw_hz,
         "proc_every": a.proc_every,
         "link_every": a.link_every,
-        "proc_period_s": a.proc_period,
-        "link_period_s": a.link_period,
+        "proc_period_s": proc_period,
+        "link_period_s": link_period,
         "pin_numa": a.pin_numa,
         "pmc_source": a.pmc,
         "pmc_lib": a.pmc_lib or pmc_lib_path(a.pmc),

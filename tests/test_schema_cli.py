@@ -184,3 +184,19 @@ def test_cli_record_chrome_trace(mock_exporter, tmp_path):
         res["gpus"]["0"]["drains"]
     busy = [e for e in ev if e["ph"] == "X" and e["pid"] == 0]
     assert busy and all(80_000 <= e["dur"] <= 120_000 for e in busy[1:-1])   # µs: 0.1 s blocks
+
+
+def test_amd_smi_tiers_are_floored_at_khz_tick_rates():
+    """--proc-every / --link-every count fast ticks; at the counter tier's 8 kHz the
+    defaults would poll AMD SMI's process list 800×/s (r3q soak: the slow thread on
+    0.33-0.43 cores).  Unless a period is given, the tiers run at ≤ 10 Hz / ≤ 1 Hz."""
+    from kube_gpu_stats_amd.exporter.main import build_parser, config_from_args
+
+    def periods(*argv):
+        c = config_from_args(build_parser().parse_args(list(argv)))
+        return c["proc_period_s"], c["link_period_s"]
+
+    assert periods("--hz", "8000") == (0.1, 1.0)
+    assert periods("--hz", "10") == (1.0, 10.0)                     # the DaemonSet rate: as before
+    assert periods("--hz", "8000", "--proc-every", "0", "--link-every", "0") == (0.0, 0.0)
+    assert periods("--hz", "8000", "--proc-period", "0.02", "--link-period", "0.5") == (0.02, 0.5)  # explicit wins
