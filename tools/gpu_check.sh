@@ -60,6 +60,7 @@ for s in $STEPS; do
     bgap*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-busy-min "0.${s#bgap}" --out "$OUT/$s.json" ;;
     soak) run soak 420 python -u tools/soak.py --seconds 240 --out "$OUT/soak.json" ;;
     rss) run rss 180 python -u tools/rss_probe.py --out "$OUT/rss_probe.json" ;;
+    hsarss) run hsarss 300 python -u tools/hsa_rss_probe.py --out "$OUT/hsa_rss.json" ;;
     soak90) run soak90 240 python -u tools/soak.py --seconds 90 --out "$OUT/soak90.json" ;;
     probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
            run probe_xgmi 90 python tools/probe_xgmi.py ;;
