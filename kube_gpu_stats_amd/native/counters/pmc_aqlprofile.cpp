@@ -1044,8 +1044,12 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       return -1;
     }
     if (!a->queue) {
-      if (hsa_queue_create(a->agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX,
-                           &a->queue) != HSA_STATUS_SUCCESS) {
+      // The READ queue carries PM4 packets only: no kernel ever needs scratch or LDS
+      // on it.  KGS_AQL_QUEUE_SEGMENTS=max restores ROCr's defaults (measurement).
+      const bool max_seg = std::getenv("KGS_AQL_QUEUE_SEGMENTS") && std::strcmp(std::getenv("KGS_AQL_QUEUE_SEGMENTS"), "max") == 0;
+      const uint32_t seg = max_seg ? UINT32_MAX : 0;
+      if (hsa_queue_create(a->agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, seg, seg, &a->queue) !=
+          HSA_STATUS_SUCCESS) {
         set_err(err, errlen, "hsa_queue_create failed");
         return -1;
       }

@@ -3,7 +3,9 @@ which runtime switch changes it (the exporter's counter reader initialises HSA; 
 it the exporter's RSS goes from 36 to 391 MiB, 360 MiB of it anonymous — r3s).
 
 Each variant runs in a fresh child: load libhsa-runtime64, hsa_init(), then read
-VmRSS / RssAnon.
+VmRSS / RssAnon; the reader variants step through the exporter's counter reader
+(init, open + START on GPU 0, 400 pipelined samples) with the READ queue created
+without / with ROCr's default scratch and LDS segment sizes.
 
     python tools/hsa_rss_probe.py --out gpurun_out/hsa_rss.json
 """
@@ -44,18 +46,62 @@ def child() -> None:
     print(json.dumps(r))
 
 
+def reader_child() -> None:
+    """The exporter's counter reader step by step (libkgs_pmc_aql.so, in-tree)."""
+    import glob
+    import time
+
+    r = {"before": status()}
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kube_gpu_stats_amd",
+                                   "lib", "libkgs_pmc_aql.so"))
+    err = ctypes.create_string_buffer(512)
+    r["init_rc"] = lib.kgs_pmc_init(err, 512)
+    r["after_init"] = status()
+    gpu_id = 0
+    for f in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id")):
+        v = int(open(f).read().strip() or 0)
+        if v:
+            gpu_id = v
+            break
+    names = (ctypes.c_char_p * 3)(b"GRBM_COUNT", b"GRBM_SPI_BUSY", b"SQ_VALU_MFMA_BUSY_CYCLES")
+    is_max = (ctypes.c_int * 3)(1, 1, 0)
+    h = lib.kgs_pmc_open(ctypes.c_uint64(gpu_id), names, is_max, 3, err, 512)
+    r["open_handle"], r["open_err"] = h, err.value.decode(errors="replace")
+    r["after_open"] = status()
+    if h >= 0:
+        lib.kgs_pmc_set_pipelined(h, 1, err, 512)
+        out = (ctypes.c_uint64 * 3)()
+        rns = ctypes.c_uint32()
+        for _ in range(400):
+            lib.kgs_pmc_sample(h, out, 3, ctypes.byref(rns))
+            time.sleep(0.000125)
+        r["after_400_samples"] = status()
+        lib.kgs_pmc_close(h)
+    print(json.dumps(r))
+
+
+READER_VARIANTS = {
+    "reader_queue_segments_0": {},
+    "reader_queue_segments_max": {"KGS_AQL_QUEUE_SEGMENTS": "max"},
+}
+
+
 def main() -> int:
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         child()
+        return 0
+    if len(sys.argv) > 1 and sys.argv[1] == "--reader-child":
+        reader_child()
         return 0
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/hsa_rss.json")
     a = ap.parse_args()
     res = {}
-    for name, env in VARIANTS.items():
+    runs = [(n, v, "--child") for n, v in VARIANTS.items()] + [(n, v, "--reader-child") for n, v in READER_VARIANTS.items()]
+    for name, env, mode in runs:
         e = dict(os.environ)
         e.update(env)
-        p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=e, capture_output=True, text=True,
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), mode], env=e, capture_output=True, text=True,
                            timeout=120)
         try:
             res[name] = {"env": env, **json.loads(p.stdout.strip().splitlines()[-1])}
