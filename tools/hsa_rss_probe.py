@@ -80,6 +80,41 @@ def reader_child() -> None:
     print(json.dumps(r))
 
 
+def queue_child() -> None:
+    """RSS after creating one, then a second, AQL queue on the GPU agent (is the
+    per-queue context save/restore area the reader's cost, and per queue?)."""
+    r = {"before": status()}
+    hsa = ctypes.CDLL("/opt/rocm/lib/libhsa-runtime64.so.1", mode=ctypes.RTLD_GLOBAL)
+    r["hsa_init_rc"] = hsa.hsa_init()
+    r["after_init"] = status()
+    agents = []
+    CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p)
+
+    def on_agent(handle, _data):
+        dev = ctypes.c_uint32()
+        hsa.hsa_agent_get_info(ctypes.c_uint64(handle), 17, ctypes.byref(dev))  # HSA_AGENT_INFO_DEVICE
+        if dev.value == 1:  # HSA_DEVICE_TYPE_GPU
+            agents.append(handle)
+        return 0
+
+    cb = CB(on_agent)
+    hsa.hsa_iterate_agents(cb, None)
+    r["gpu_agents"] = len(agents)
+    qs = []
+    for i in range(2):
+        q = ctypes.c_void_p()
+        rc = hsa.hsa_queue_create(ctypes.c_uint64(agents[0]), ctypes.c_uint32(64), ctypes.c_uint32(1), None, None,
+                                  ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.byref(q))
+        r[f"queue{i + 1}_rc"] = rc
+        r[f"after_queue{i + 1}"] = status()
+        qs.append(q)
+    for q in qs:
+        if q.value:
+            hsa.hsa_queue_destroy(q)
+    r["after_destroy"] = status()
+    print(json.dumps(r))
+
+
 READER_VARIANTS = {
     "reader_queue_segments_0": {},
     "reader_queue_segments_max": {"KGS_AQL_QUEUE_SEGMENTS": "max"},
@@ -90,6 +125,9 @@ def main() -> int:
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         child()
         return 0
+    if len(sys.argv) > 1 and sys.argv[1] == "--queue-child":
+        queue_child()
+        return 0
     if len(sys.argv) > 1 and sys.argv[1] == "--reader-child":
         reader_child()
         return 0
@@ -98,6 +136,7 @@ def main() -> int:
     a = ap.parse_args()
     res = {}
     runs = [(n, v, "--child") for n, v in VARIANTS.items()] + [(n, v, "--reader-child") for n, v in READER_VARIANTS.items()]
+    runs += [("two_queues", {}, "--queue-child")]
     for name, env, mode in runs:
         e = dict(os.environ)
         e.update(env)
