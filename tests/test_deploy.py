@@ -87,3 +87,24 @@ def test_grafana_dashboard_is_current_and_uses_exported_families():
     assert len(ex) >= 15
     assert not unknown_series(" ".join(ex))
     assert any("container_gpu_sm_util" in e for e in ex)
+
+
+def _mib(q: str) -> float:
+    units = {"Ki": 1 / 1024, "Mi": 1, "Gi": 1024}
+    for u, f in units.items():
+        if q.endswith(u):
+            return float(q[:-2]) * f
+    return float(q) / 2**20
+
+
+def test_daemonset_memory_fits_the_counter_tier_on_8_gpus():
+    """Each GPU's private AQL READ queue pins ≈350 MiB of host memory on MI355X (the
+    KFD context save/restore area of a compute queue for 256 CUs + per-agent runtime
+    state; profiles/r3/README.md r3s-r3v): with --pmc=aqlprofile an 8-GPU node needs
+    ≈2.9 GiB, so a 512Mi limit (rounds 1-2) would OOM-kill the exporter."""
+    ds = next(d for d in load("daemonset.yaml") if d["kind"] == "DaemonSet")
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+    a = build_parser().parse_args(c["args"])
+    need = 40 + (8 * 350 if a.pmc == "aqlprofile" else 0)
+    res = c["resources"]
+    assert _mib(res["requests"]["memory"]) >= need and _mib(res["limits"]["memory"]) >= need, res
