@@ -59,7 +59,10 @@ def reader_child() -> None:
     r["after_init"] = status()
     gpu_id = 0
     for f in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id")):
-        v = int(open(f).read().strip() or 0)
+        try:
+            v = int(open(f).read().strip() or 0)
+        except OSError:
+            continue
         if v:
             gpu_id = v
             break
@@ -115,6 +118,13 @@ def queue_child() -> None:
     print(json.dumps(r))
 
 
+QUEUE_VARIANTS = {
+    "default": {},
+    "queue_dev_mem": {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1"},
+    "no_pc_sampling": {"HSA_DISABLE_PC_SAMPLING": "1"},
+    "no_coredump": {"HSA_DISABLE_COREDUMP_ON_EXCEPTION": "1"},
+}
+
 READER_VARIANTS = {
     "reader_queue_segments_0": {},
     "reader_queue_segments_max": {"KGS_AQL_QUEUE_SEGMENTS": "max"},
@@ -136,7 +146,7 @@ def main() -> int:
     a = ap.parse_args()
     res = {}
     runs = [(n, v, "--child") for n, v in VARIANTS.items()] + [(n, v, "--reader-child") for n, v in READER_VARIANTS.items()]
-    runs += [("two_queues", {}, "--queue-child")]
+    runs += [(f"two_queues_{n}", v, "--queue-child") for n, v in QUEUE_VARIANTS.items()]
     for name, env, mode in runs:
         e = dict(os.environ)
         e.update(env)
