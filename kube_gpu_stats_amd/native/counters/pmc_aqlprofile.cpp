@@ -155,7 +155,7 @@ struct Agent {
   };
   std::deque<Ready> bready;                          // folded samples not yet returned
   std::atomic<uint64_t> land_waits{0}, land_timeouts{0};  // collections that had to wait / gave up waiting
-  std::atomic<uint64_t> publishes{0};                // batched READs that wrote the L2 back
+  std::atomic<uint64_t> publishes{0};                // READs that wrote the L2 back (all, unless batched)
   // KGS_AQL_PROFILE=<n>: CP timestamps of every pipelined READ (queue profiling on):
   // queueing delay (submit → CP start) and execution (start → end), reported on
   // stderr every n READs.  How long the CP makes a READ wait says how busy it
@@ -839,6 +839,7 @@ int read_batched(Agent* a, int64_t* ts) {
     const int64_t t0 = mono_ns();
     const int rc = read_values(a);
     if (rc != 0) return rc;
+    ++a->publishes;  // a synchronous READ writes the L2 back
     if (ts) *ts = t0 + a->rtt_ns / 2;
     a->bprimed = true;
     return 0;  // the next call starts the slot rotation
@@ -1234,8 +1235,9 @@ int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
 
 // Publication counters for the exporter's self-metrics (any thread: atomics only):
 // out[0] READs folded, out[1] READs that wrote the L2 back (every READ unless
-// batched), out[2] batched READ results still unwritten when their half was
-// folded (land timeouts: should stay 0).  Returns the number of values written.
+// batched), out[2] batched READs dropped because a result was still unwritten
+// when their half was folded (should stay near 0).  Returns the number of values
+// written.
 int kgs_pmc_stats(int handle, uint64_t* out, int n) {
   if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size() || !out) return -1;
   const Agent* a = g_agents[static_cast<size_t>(handle)];
