@@ -33,7 +33,7 @@ for s in $STEPS; do
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc none --out "$OUT/trainpmfw.json" ;;
     train2) run train2 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 2 --out "$OUT/train2.json" ;;
-    tdef|tdef2|tpmfw|tagent|tl3agent|tnop|t1k|tgap*|tbatch*|tpub*|tnobatch|t16k)
+    tdef|tdef2|tpmfw|tagent|tl3agent|tnop|t1k|tgap*|tbatch*|tpub*|tnobatch|tnobatch2|t16k)
         # training-step side runs, 36 rounds = every block order 6 times:
         #   tdef (defaults) tpmfw (no READs) tagent (release fence at agent scope)
         #   tl3agent (lean 3 + agent release) tnop (every READ packet a NOP: the bare
@@ -50,7 +50,7 @@ for s in $STEPS; do
           tgap*) run $s 600 "${T[@]}" --pmc-busy-min "0.${s#tgap}" ;;  # tgap90: --pmc-busy-min 0.90
           tbatch*) run $s 600 "${T[@]}" --pmc-batch "${s#tbatch}" ;;      # tbatch8: --pmc-batch 8
           tpub*) run $s 600 "${T[@]}" --pmc-publish-us "${s#tpub}" ;;     # tpub0: count-only batches
-          tnobatch) run $s 600 "${T[@]}" --pmc-batch 1 ;;
+          tnobatch|tnobatch2) run $s 600 "${T[@]}" --pmc-batch 1 ;;
           t16k) run $s 600 "${T[@]}" --hz 16000 --pmc-batch 16 ;;
         esac ;;
     bpub*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-publish-us "${s#bpub}" --out "$OUT/$s.json" ;;
