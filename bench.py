@@ -716,6 +716,32 @@ def throttled(before: dict, after: dict, win: float) -> dict:
     return out
 
 
+def wake_lateness(before: dict, after: dict) -> dict:
+    """Per GPU, how late the counter thread woke against its tick deadlines during
+    phase B (kgs_sampler_wake_lateness_seconds deltas): the box's CPU contention,
+    which is what makes phase B fall short of the nominal rate on some boxes."""
+    out: dict = {}
+    fam = "kgs_sampler_wake_lateness_seconds"
+    b = {(lb["gpu"], lb["le"]): v for lb, v in before.get(fam + "_bucket", [])}
+    buckets: dict = {}
+    for lb, v in after.get(fam + "_bucket", []):
+        le = float("inf") if lb["le"] == "+Inf" else float(lb["le"])
+        buckets.setdefault(lb["gpu"], []).append((le, v - b.get((lb["gpu"], lb["le"]), 0.0)))
+    sums = {lb["gpu"]: v for lb, v in after.get(fam + "_sum", [])}
+    sums0 = {lb["gpu"]: v for lb, v in before.get(fam + "_sum", [])}
+    for g, bl in buckets.items():
+        bl.sort()
+        n = bl[-1][1] if bl else 0
+        if n <= 0:
+            continue
+        le = lambda t: max((c for x, c in bl if x <= t + 1e-12), default=0.0)  # noqa: E731  cumulative ≤ t
+        out[g] = {"ticks": int(n), "share_within_10us": round(le(10e-6) / n, 4),
+                  "share_within_100us": round(le(100e-6) / n, 4), "share_over_500us": round(1 - le(500e-6) / n, 5),
+                  "share_over_2500us": round(1 - le(2500e-6) / n, 5),
+                  "mean_us": round(1e6 * (sums.get(g, 0.0) - sums0.get(g, 0.0)) / n, 2)}
+    return out
+
+
 # ----------------------------------------------------------------------------- phases
 PHASES: dict[str, list[float]] = {}
 
@@ -1472,6 +1498,7 @@ def run(a, ctx) -> dict | None:
         "pmc_error": exp.ready.get("pmc_error"),
         "load": calib,
         "observed_during_load": observed(after),
+        "sampler_wake_lateness": wake_lateness(before, after),
         "throttled_pct_during_load": throttled(before, after, win),
         "xgmi_GBps_per_gpu": xgmi_rates(before, after, win),
         # what the phase-B all-reduces must have moved per GPU (read + write, bandwidth-optimal

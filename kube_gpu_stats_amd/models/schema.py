@@ -219,6 +219,9 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_slow_read_seconds_total", "counter", "Time the node-wide slow thread spent in management-library calls.",
       source="self"),
     F("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read.", extra=("le",), source="self"),
+    F("kgs_sampler_wake_lateness_seconds", "histogram", "How late the counter thread woke against each tick's "
+      "absolute deadline (CPU contention, idle-state exit); a tick more than 4 periods late is skipped and counted "
+      "in kgs_sampler_overruns_total.", extra=("le",), source="self"),
     F("kgs_scrapes_total", "counter", "Scrapes rendered.", ("kubernetes_io_hostname",), "self"),
     F("kgs_scrape_render_seconds_total", "counter", "Time spent rendering /metrics.", ("kubernetes_io_hostname",),
       "self"),

@@ -149,6 +149,10 @@ struct DeviceState {
   std::atomic<int64_t> last_ok_mono_ns{0};
   std::atomic<uint64_t> consecutive_errors{0};
   std::atomic<uint64_t> read_hist[kReadHistBuckets + 1] = {};
+  // Counter thread: how late each wake-up was against its absolute deadline (same
+  // buckets as read_hist) — the CPU contention / idle-state cost behind overruns.
+  std::atomic<uint64_t> wake_hist[kReadHistBuckets + 1] = {};
+  std::atomic<uint64_t> wake_late_ns{0};              // sum of the positive lateness
   std::atomic<int> cpu_pinned{-1};
   // Counter hand-over (`kgs exporter` SIGUSR1 / SIGUSR2, /control/pmc/*): the
   // control plane sets pmc_want; the sampler thread releases / re-acquires the

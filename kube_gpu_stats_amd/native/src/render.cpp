@@ -741,6 +741,19 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_breaker_trips_total", dev_labels_[d], nullptr, S.state(d).pmc_breaker_trips.load());
     w.head("kgs_pmc_retries_total", "counter", "Reader resets + re-STARTs attempted while the breaker was open");
     for (int d : ids) w.line_u("kgs_pmc_retries_total", dev_labels_[d], nullptr, S.state(d).pmc_retries.load());
+    w.head("kgs_sampler_wake_lateness_seconds", "histogram",
+           "How late the counter thread woke against each tick's absolute deadline (CPU contention, idle-state exit); "
+           "a tick later than 4 periods is skipped (kgs_sampler_overruns_total)");
+    for (int d : ids) {
+      const DeviceState& st = S.state(d);
+      uint64_t cum = 0;
+      for (int b = 0; b <= kReadHistBuckets; ++b) {
+        cum += st.wake_hist[b].load(std::memory_order_relaxed);
+        w.line_u("kgs_sampler_wake_lateness_seconds_bucket", dev_labels_[d], hist_le_labels()[static_cast<size_t>(b)].c_str(), cum);
+      }
+      w.line("kgs_sampler_wake_lateness_seconds_sum", dev_labels_[d], nullptr, st.wake_late_ns.load(std::memory_order_relaxed) * 1e-9);
+      w.line_u("kgs_sampler_wake_lateness_seconds_count", dev_labels_[d], nullptr, cum);
+    }
     if (pmc_) {
       std::vector<std::pair<int, CounterSource::PublishStats>> ps;
       for (int d : ids) {

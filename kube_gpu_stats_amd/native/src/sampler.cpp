@@ -729,6 +729,14 @@ void Sampler::run_pmc(Worker& w) {
       pollfd pfd{stop_fd_, POLLIN, 0};
       ppoll(&pfd, 1, &ts, nullptr);
     }
+    {  // wake-up lateness (kgs_sampler_wake_lateness_seconds)
+      const int64_t late = mono_ns() - next;
+      if (late > 0) st.wake_late_ns.fetch_add(static_cast<uint64_t>(late), std::memory_order_relaxed);
+      const double us = late * 1e-3;
+      int b = 0;
+      while (b < kReadHistBuckets && us > kReadHistBoundsUs[b]) ++b;
+      st.wake_hist[b].fetch_add(1, std::memory_order_relaxed);
+    }
   }
   st.pmc_integ.store(P);
 }
