@@ -833,3 +833,18 @@ def test_mock_peer_copy_lands_on_the_link_to_that_peer(mock_exporter):
     assert src_key[0] == 0 and peer[src_key] == bdf[3]
     assert dst_key[0] == 3 and peer[dst_key] == bdf[0]
     assert src_b == pytest.approx(nbytes, rel=1e-3) and dst_b == pytest.approx(nbytes, rel=1e-3)
+
+
+def test_wake_lateness_histogram(mock_exporter):
+    """kgs_sampler_wake_lateness_seconds: one observation per counter-thread tick,
+    cumulative buckets, a sum of the positive lateness."""
+    ex = mock_exporter(n_gpus=2, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0)
+    time.sleep(0.6)
+    m = parse_text(ex.render())
+    for g in ("0", "1"):
+        b = [(float("inf") if lb["le"] == "+Inf" else float(lb["le"]), v)
+             for lb, v in m["kgs_sampler_wake_lateness_seconds_bucket"] if lb["gpu"] == g]
+        counts = [v for _, v in sorted(b)]
+        n = [v for lb, v in m["kgs_sampler_wake_lateness_seconds_count"] if lb["gpu"] == g][0]
+        assert counts == sorted(counts) and counts[-1] == n and n > 300, (g, b, n)
+        assert [v for lb, v in m["kgs_sampler_wake_lateness_seconds_sum"] if lb["gpu"] == g][0] >= 0
