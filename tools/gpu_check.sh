@@ -55,7 +55,7 @@ for s in $STEPS; do
         esac ;;
     bpub*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-publish-us "${s#bpub}" --out "$OUT/$s.json" ;;
     b16k) run $s 600 python -u bench.py --steps 20 --warmup 5 --hz 16000 --pmc-batch 16 --out "$OUT/$s.json" ;;
-    bnobatch) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch 1 --out "$OUT/$s.json" ;;
+    bnobatch|bnobatch2) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch 1 --out "$OUT/$s.json" ;;
     bbatch*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch "${s#bbatch}" --out "$OUT/$s.json" ;;
     bgap*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-busy-min "0.${s#bgap}" --out "$OUT/$s.json" ;;
     soak) run soak 420 python -u tools/soak.py --seconds 240 --out "$OUT/soak.json" ;;
