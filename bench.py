@@ -1248,6 +1248,73 @@ def capacity(ctx, load, exp, a) -> dict:
     return out
 
 
+def _xgmi_rank0(a, exp, bdfs: list) -> dict:
+    """Phase X on local rank 0 (see xgmi_link_check)."""
+    nbytes = int(a.xgmi_check_mib) << 20
+    gpu_of = {d["bdf"]: int(d["gpu"]) for d in exp.json("/devices")}
+    topo = exp.json("/topology")
+    peer_of = {(int(x["gpu"]), int(x["link"])): x.get("peer_bdf", "") for x in topo.get("links", [])}
+
+    def link_bytes(m: dict) -> dict:
+        tot: dict = {}
+        for fam in ("amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total"):
+            for lb, v in m.get(fam, []):
+                key = (int(lb["gpu"]), int(lb["link"]))
+                tot[key] = tot.get(key, 0.0) + v
+        return tot
+
+    def moved(before: dict, after: dict, gpu: int, want_bdf: str) -> dict:
+        d = {l: after[(g, l)] - before.get((g, l), 0.0) for (g, l) in after if g == gpu}
+        if not d:
+            return {"ok": False, "reason": "no xGMI byte counters for this GPU"}
+        l_max = max(d, key=d.get)
+        rest = sorted(v for l, v in d.items() if l != l_max)
+        bg = rest[len(rest) // 2] if rest else 0.0
+        peer = peer_of.get((gpu, l_max), "")
+        return {"link": l_max, "link_peer_bdf": peer, "ok": peer == want_bdf and d[l_max] - bg > 0,
+                "bytes_counted": round(d[l_max], 1), "background_bytes": round(bg, 1),
+                "unit_ratio": round((d[l_max] - bg) / nbytes, 4)}
+
+    src_dev = 0
+    per_peer = []
+    for k in range(1, len(bdfs)):
+        g0, gk = gpu_of.get(bdfs[0]), gpu_of.get(bdfs[k])
+        if g0 is None or gk is None:
+            per_peer.append({"peer_bdf": bdfs[k], "ok": False, "reason": "GPU not sampled by the exporter"})
+            continue
+        m0 = parse_text(exp.sc.get())
+        if a.mock:
+            exp.json(f"/control/mock/xgmi?src={g0}&dst={gk}&bytes={nbytes}")
+        else:
+            import torch
+
+            src = torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", src_dev)).fill_(1.0)
+            dst = torch.empty_like(src, device=torch.device("cuda", k))
+            torch.cuda.synchronize(src_dev)
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize(src_dev)
+            torch.cuda.synchronize(k)
+            del src, dst
+        time.sleep(a.xgmi_check_settle)  # the PMFW table refreshes every ≈20 ms; the exporter reads it at 100 Hz
+        m1 = parse_text(exp.sc.get())
+        b0, b1 = link_bytes(m0), link_bytes(m1)
+        row = {"src_gpu": g0, "peer_gpu": gk, "peer_bdf": bdfs[k], "bytes": nbytes,
+               "src": moved(b0, b1, g0, bdfs[k]), "dst": moved(b0, b1, gk, bdfs[0])}
+        row["ok"] = bool(row["src"].get("ok") and row["dst"].get("ok"))
+        per_peer.append(row)
+    ratios = sorted(r[side]["unit_ratio"] for r in per_peer for side in ("src", "dst")
+                    if isinstance(r.get(side), dict) and "unit_ratio" in r[side])
+    ratio = ratios[len(ratios) // 2] if ratios else None
+    out = {"bytes_per_copy": nbytes, "per_peer": per_peer,
+           "xgmi_link_map_ok": bool(per_peer) and all(r["ok"] for r in per_peer),
+           "xgmi_unit_ratio": ratio,
+           "xgmi_unit_ok": ratio is not None and 0.8 <= ratio <= 1.25}
+    if ratio is not None and not out["xgmi_unit_ok"]:
+        out["warning"] = (f"xGMI accumulator unit off by {ratio:.3g}x: set --xgmi-bytes-per-unit to "
+                          f"{1024.0 * ratio:.4g}")
+    return out
+
+
 def xgmi_link_check(ctx, load, exp, a) -> dict:
     """Phase X (untimed, N > 1) — does each xGMI byte land on the link whose peer is
     the real peer, and in which unit?  Rank 0 sees every GPU of the
@@ -1267,68 +1334,10 @@ def xgmi_link_check(ctx, load, exp, a) -> dict:
     # every rank's GPU, in local-rank order (a collective: every rank calls it)
     bdfs = [b for _, b in sorted(set(D.all_gather_object(ctx, (ctx.local_rank, load.pci_bdf(ctx.local_rank)))))]
     if ctx.local_rank == 0 and exp is not None:
-        nbytes = int(a.xgmi_check_mib) << 20
-        gpu_of = {d["bdf"]: int(d["gpu"]) for d in exp.json("/devices")}
-        topo = exp.json("/topology")
-        peer_of = {(int(x["gpu"]), int(x["link"])): x.get("peer_bdf", "") for x in topo.get("links", [])}
-
-        def link_bytes(m: dict) -> dict:
-            tot: dict = {}
-            for fam in ("amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total"):
-                for lb, v in m.get(fam, []):
-                    key = (int(lb["gpu"]), int(lb["link"]))
-                    tot[key] = tot.get(key, 0.0) + v
-            return tot
-
-        def moved(before: dict, after: dict, gpu: int, want_bdf: str) -> dict:
-            d = {l: after[(g, l)] - before.get((g, l), 0.0) for (g, l) in after if g == gpu}
-            if not d:
-                return {"ok": False, "reason": "no xGMI byte counters for this GPU"}
-            l_max = max(d, key=d.get)
-            rest = sorted(v for l, v in d.items() if l != l_max)
-            bg = rest[len(rest) // 2] if rest else 0.0
-            peer = peer_of.get((gpu, l_max), "")
-            return {"link": l_max, "link_peer_bdf": peer, "ok": peer == want_bdf and d[l_max] - bg > 0,
-                    "bytes_counted": round(d[l_max], 1), "background_bytes": round(bg, 1),
-                    "unit_ratio": round((d[l_max] - bg) / nbytes, 4)}
-
-        src_dev = 0
-        per_peer = []
-        for k in range(1, len(bdfs)):
-            g0, gk = gpu_of.get(bdfs[0]), gpu_of.get(bdfs[k])
-            if g0 is None or gk is None:
-                per_peer.append({"peer_bdf": bdfs[k], "ok": False, "reason": "GPU not sampled by the exporter"})
-                continue
-            m0 = parse_text(exp.sc.get())
-            if a.mock:
-                exp.json(f"/control/mock/xgmi?src={g0}&dst={gk}&bytes={nbytes}")
-            else:
-                import torch
-
-                src = torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", src_dev)).fill_(1.0)
-                dst = torch.empty_like(src, device=torch.device("cuda", k))
-                torch.cuda.synchronize(src_dev)
-                dst.copy_(src, non_blocking=True)
-                torch.cuda.synchronize(src_dev)
-                torch.cuda.synchronize(k)
-                del src, dst
-            time.sleep(a.xgmi_check_settle)  # the PMFW table refreshes every ≈20 ms; the exporter reads it at 100 Hz
-            m1 = parse_text(exp.sc.get())
-            b0, b1 = link_bytes(m0), link_bytes(m1)
-            row = {"src_gpu": g0, "peer_gpu": gk, "peer_bdf": bdfs[k], "bytes": nbytes,
-                   "src": moved(b0, b1, g0, bdfs[k]), "dst": moved(b0, b1, gk, bdfs[0])}
-            row["ok"] = bool(row["src"].get("ok") and row["dst"].get("ok"))
-            per_peer.append(row)
-        ratios = sorted(r[side]["unit_ratio"] for r in per_peer for side in ("src", "dst")
-                        if isinstance(r.get(side), dict) and "unit_ratio" in r[side])
-        ratio = ratios[len(ratios) // 2] if ratios else None
-        out = {"bytes_per_copy": nbytes, "per_peer": per_peer,
-               "xgmi_link_map_ok": bool(per_peer) and all(r["ok"] for r in per_peer),
-               "xgmi_unit_ratio": ratio,
-               "xgmi_unit_ok": ratio is not None and 0.8 <= ratio <= 1.25}
-        if ratio is not None and not out["xgmi_unit_ok"]:
-            out["warning"] = (f"xGMI accumulator unit off by {ratio:.3g}x: set --xgmi-bytes-per-unit to "
-                              f"{1024.0 * ratio:.4g}")
+        try:
+            out = _xgmi_rank0(a, exp, bdfs)
+        except Exception as e:  # noqa: BLE001  a failed self-check must not take the run (and the other ranks) down
+            out = {"error": f"{type(e).__name__}: {e}", "xgmi_link_map_ok": False, "xgmi_unit_ratio": None}
     D.cpu_barrier(ctx)
     return out
 

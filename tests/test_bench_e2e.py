@@ -285,3 +285,29 @@ def test_allreduce_expected_xgmi_rate():
     assert bench.allreduce_GBps(load, a, 8, 10.0) == pytest.approx(want, abs=1e-3)
     assert bench.allreduce_GBps(load, a, 1, 10.0) is None
     assert bench.allreduce_GBps(types.SimpleNamespace(reps=1), a, 8, 10.0) is None
+
+
+def test_phase_x_failure_does_not_take_the_run_down(monkeypatch):
+    """Phase X runs on local rank 0 between two collectives: an exception there (a
+    failed peer copy, an exporter endpoint error) must end in the result, not in a
+    crashed rank 0 that leaves the other ranks waiting at the barrier."""
+    import importlib.util
+    import types
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    calls = []
+    monkeypatch.setattr(b.D, "cpu_barrier", lambda ctx: calls.append("barrier"))
+    monkeypatch.setattr(b.D, "all_gather_object", lambda ctx, obj: [(0, "0000:01:00.0"), (1, "0000:02:00.0")])
+
+    class Exp:
+        def json(self, path):
+            raise ConnectionError("exporter gone")
+
+    ctx = types.SimpleNamespace(world=2, rank=0, local_rank=0)
+    a = types.SimpleNamespace(xgmi_check_mib=64, mock=True, xgmi_check_settle=0.0)
+    load = types.SimpleNamespace(pci_bdf=lambda r: f"0000:0{r + 1}:00.0")
+    out = b.xgmi_link_check(ctx, load, Exp(), a)
+    assert out["xgmi_link_map_ok"] is False and "ConnectionError" in out["error"], out
+    assert calls == ["barrier", "barrier"]  # both collectives still reached
