@@ -148,6 +148,11 @@ def build() -> dict:
     add(_panel(0, "Counter READ publication (L2 writebacks / s, dropped READs / s)",
                [(_dev("rate(kgs_pmc_publishes_total[1m])"), "writebacks gpu{{gpu}}"),
                 (_dev("rate(kgs_pmc_unlanded_total[5m])"), "dropped gpu{{gpu}}")], 0, y, w=8))
+    # host CPU contention: how late the counter threads wake (overruns skip ticks past 4 periods)
+    add(_panel(0, "Sampler wake-up lateness p99 / overruns per s",
+               [(_dev("histogram_quantile(0.99, rate(kgs_sampler_wake_lateness_seconds_bucket[5m]))"),
+                 "p99 late s gpu{{gpu}}"),
+                (_dev("rate(kgs_sampler_overruns_total[5m])"), "overruns/s gpu{{gpu}}")], 8, y, w=8))
 
     return {
         "title": "MI355X GPU stats (kube_gpu_stats_amd)",

@@ -44,7 +44,7 @@ def test_daemonset_handover_does_not_signal_pid1():
 
 
 PROMQL_WORDS = {"avg", "sum", "max", "min", "count", "rate", "increase", "avg_over_time", "label_values", "by", "or",
-                "and", "on", "without", "group_left", "group_right"}
+                "and", "on", "without", "group_left", "group_right", "histogram_quantile"}
 LABELS = {"kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "gpu", "instance", "sensor", "pod",
           "pid", "xcc", "block", "type", "reason"}
 
@@ -57,7 +57,11 @@ def unknown_series(exprs: str) -> set:
 
     bare = re.sub(r"\{[^}]*\}|\[[^]]*\]|\"[^\"]*\"", "", exprs)
     names = {n for n in re.findall(r"[a-zA-Z_:][a-zA-Z0-9_:]*", bare) if ":" not in n}
-    return {n for n in names - PROMQL_WORDS - LABELS if n not in BY_NAME}
+    def known(n: str) -> bool:  # a histogram's series carry _bucket / _sum / _count
+        base = re.sub(r"_(bucket|sum|count)$", "", n)
+        return n in BY_NAME or (base in BY_NAME and BY_NAME[base].type == "histogram")
+
+    return {n for n in names - PROMQL_WORDS - LABELS if not known(n)}
 
 
 def test_monitoring_rules_reference_exported_families():
