@@ -409,7 +409,7 @@ const ClockMap& hsa_clock() {
 // slot at most g_timeout_ns (a full queue means the CP stopped consuming it);
 // 0 = queued, -1 = no slot (timeout or abort; nothing was reserved).
 int enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig,
-            std::pair<int, int> fences = kSystemFences) {
+            std::pair<int, int> fences = kSystemFences, bool barrier = true) {
   hsa_queue_t* q = a->queue;
   if (!q) return -1;
   uint64_t idx = 0;
@@ -427,7 +427,7 @@ int enqueue(Agent* a, const hsa_ext_amd_aql_pm4_packet_t& tmpl, hsa_signal_t sig
   std::memcpy(slot->pm4_command, tmpl.pm4_command, sizeof slot->pm4_command);
   slot->completion_signal = sig;
   const uint16_t header = static_cast<uint16_t>(
-      (HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+      (HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) | ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
       (fences.first << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
       (fences.second << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
@@ -774,6 +774,15 @@ constexpr uint32_t kUnlanded = 0xFFFFFFFFu;
 
 bool is_publisher(const Agent* a, int k) { return a->batch < 2 || a->plan.is_publisher(k); }
 
+// KGS_AQL_NOBARRIER=1 (experiment): non-publisher READs without the AQL barrier
+// bit, so the packet processor need not wait for the previous READ's completion
+// before taking the next; the publisher keeps it (it must follow every READ of
+// its half for its writeback to cover them).
+bool nonpub_barrier() {
+  static const bool on = std::getenv("KGS_AQL_NOBARRIER") == nullptr;
+  return on;
+}
+
 // true = every result dword of slot k was written (fold it), false = drop the READ.
 bool wait_landed(Agent* a, int k) {
   const int64_t t0 = mono_ns();
@@ -864,7 +873,7 @@ int read_batched(Agent* a, int64_t* ts) {
   a->psubmit_ns[k] = mono_ns();
   const std::pair<int, int> none{HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_NONE};
   const bool pub = p.is_publisher(k);
-  if (enqueue(a, a->pread[k], a->psig[k], pub ? read_fences() : none) != 0) {
+  if (enqueue(a, a->pread[k], a->psig[k], pub ? read_fences() : none, pub || nonpub_barrier()) != 0) {
     if (p.last() >= 0) wait_done(a, a->psig[p.last()]);
     batch_reset(a);
     return -2;
