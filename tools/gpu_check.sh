@@ -54,7 +54,7 @@ for s in $STEPS; do
           t16k) run $s 600 "${T[@]}" --hz 16000 --pmc-batch 16 ;;
         esac ;;
     bpub*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-publish-us "${s#bpub}" --out "$OUT/$s.json" ;;
-    bnobar) KGS_AQL_NOBARRIER=1 run $s 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/$s.json" ;;
+    bnobar|bnobar2) KGS_AQL_NOBARRIER=1 run $s 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/$s.json" ;;
     b16k) run $s 600 python -u bench.py --steps 20 --warmup 5 --hz 16000 --pmc-batch 16 --out "$OUT/$s.json" ;;
     bnobatch|bnobatch2) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch 1 --out "$OUT/$s.json" ;;
     bbatch*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch "${s#bbatch}" --out "$OUT/$s.json" ;;
