@@ -82,7 +82,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pmc-batch", 8, choices=range(1, 17), help="counter READs per L2 writeback: a READ's results sit in the GPU's L2 until "
                                  "written back, and that writeback is half of what a READ costs a training step; "
                                  "with B > 1 at most every B-th READ writes back (at 8 kHz samples arrive B-2B ticks "
-                                 "late; 1 = every READ)")
+                                 "late; 1 = every READ).  Trade-off: batching cuts the cost to long kernels and "
+                                 "training steps, but a stream of µs kernels pays +0.2-0.3 points more at 8 kHz "
+                                 "than unbatched (profiles/r3/README.md r3ab)")
     add_flag(ap, "pmc-publish-us", 1000, "longest a batched counter READ waits for its L2 writeback: a READ writes "
                                          "back early when the next tick would be later (at <= 1 kHz every READ does)")
     add_flag(ap, "pmc-timeout-ms", 250, "bound of every wait on the command processor (counter READ, START, STOP, "
@@ -110,9 +112,11 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                               "(MI355X calibration, profiles/r2/pcie/)")
     add_flag(ap, "xgmi-bytes-per-unit", 1024.0, "bytes per unit of the PMFW xGMI link accumulators (amdsmi.h: KB; "
                                                "correct with bench.py's N > 1 expected / measured ratio)")
-    add_flag(ap, "sm-util-source", "pmfw", "what container_gpu_sm_util / container_gpu_busy_seconds_total measure: pmfw "
-                                           "(firmware GFX busy: a dispatch in flight; counts counter READs as work) | "
-                                           "counters (GRBM_SPI_BUSY: waves in a shader engine; READ-immune; needs --pmc)")
+    add_flag(ap, "sm-util-source", "auto", "what container_gpu_sm_util / container_gpu_busy_seconds_total / "
+                                           "amdgpu_gfx_busy_* measure: auto (READ-immune: the counter tier's "
+                                           "GRBM_SPI_BUSY while it runs, the firmware GFX busy otherwise) | pmfw "
+                                           "(firmware GFX busy alone: a dispatch in flight, and every counter READ "
+                                           "packet as ~80 us of work) | counters (GRBM_SPI_BUSY alone; needs --pmc)")
     add_flag(ap, "pod-resources-socket", "/var/lib/kubelet/pod-resources/kubelet.sock", "kubelet pod-resources socket")
     add_flag(ap, "static-owners", "", "JSON file mapping device id -> {pod,namespace,container}")
     add_flag(ap, "attribution-interval", 1.0, "attribution refresh period (s)")

@@ -29,8 +29,11 @@ F = Family
 CATALOG: tuple[Family, ...] = (
     # ---- reference contract ------------------------------------------------------------
     F("container_gpu_sm_util", "gauge",
-      "GFX-engine busy % of the GPU allocated to the pod (mean over the exporter window). Reference contract: "
-      "consumed by `avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)`.",
+      "Busy % of the GPU allocated to the pod (mean over the exporter window), not counting the exporter's own "
+      "counter READs: with the default --sm-util-source auto, hardware-counter GPU-active (GRBM_SPI_BUSY: waves in a "
+      "shader engine) while the counter tier runs, the PMFW GFX busy otherwise (kgs_util_source_seconds_total says "
+      "which).  Reference contract: consumed by "
+      "`avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)`.",
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
       "pmfw+kubelet", "fast"),
     F("container_gpu_mfma_util", "gauge",
@@ -40,7 +43,8 @@ CATALOG: tuple[Family, ...] = (
       ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
       "counters+kubelet", "pmc"),
     F("container_gpu_busy_seconds_total", "counter",
-      "GFX-busy seconds of the GPU allocated to the pod, counted from the allocation (PMFW accumulators).  "
+      "Busy seconds of the GPU allocated to the pod, counted from the allocation (the integral behind "
+      "container_gpu_sm_util: READ-immune under --sm-util-source auto).  "
       "`100 * avg(rate(container_gpu_busy_seconds_total[1h])) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)` "
       "is the exact hourly per-pod utilisation whatever the scrape interval — the default source of "
       "`kgs gpu-util-stats` (fixed mode).  Same labels as container_gpu_sm_util.",
@@ -82,14 +86,26 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_xgmi_link_info", "gauge", "Per-link peer PCI address and speed (1).",
       extra=("link", "peer_bdf", "link_type", "bit_rate_gbps", "max_bandwidth_gbps"), source="amdsmi", tier="slow"),
     # ---- utilisation ------------------------------------------------------------------------
-    F("amdgpu_gfx_busy_percent", "gauge", "GFX busy %, time-weighted mean over the window from PMFW accumulators."),
+    F("amdgpu_gfx_busy_percent", "gauge",
+      "GPU busy %, time-weighted mean over the window — the same source as container_gpu_sm_util (default auto: "
+      "hardware-counter GPU-active while the counter tier runs, PMFW GFX busy otherwise; never the exporter's own "
+      "counter READs)."),
+    F("amdgpu_pmfw_gfx_busy_percent", "gauge",
+      "Firmware (PMFW) GFX busy %, window mean from the PMFW accumulators: a dispatch in flight — and each counter "
+      "READ packet of the exporter as ~80 us of work (99.7 % on an idle GPU READ at 8 kHz, profiles/r2/idle_busy/)."),
     F("amdgpu_gfx_busy_instant_percent", "gauge", "GFX busy % in the latest PMFW table."),
     F("amdgpu_gfx_busy_xcc_percent", "gauge",
       "Busy % per XCC over the last firmware interval, from the per-partition accumulators "
       "(instant value when those are absent).  Busy means a dispatch in flight on that XCC: a chip-wide kernel keeps "
       "all 8 at ~100 % even when waves run on a few; amdgpu_mfma_util_xcc_percent shows where they run.", extra=("xcc",)),
     F("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller activity %, window mean."),
-    F("amdgpu_gfx_busy_seconds_total", "counter", "∫ GFX busy fraction dt; rate() = exact mean utilisation."),
+    F("amdgpu_gfx_busy_seconds_total", "counter",
+      "∫ busy fraction dt of amdgpu_gfx_busy_percent's source; rate() = exact mean utilisation."),
+    F("amdgpu_pmfw_gfx_busy_seconds_total", "counter", "∫ PMFW GFX busy fraction dt (counts counter READs as work)."),
+    F("kgs_util_source_seconds_total", "counter",
+      "Firmware time the READ-immune busy integral took from each source: counters (GRBM_SPI_BUSY, while the "
+      "counter tier ran through the whole PMFW interval) or pmfw (counter tier off, handed over, failed or stale).",
+      extra=("source",), source="self"),
     F("amdgpu_umc_busy_seconds_total", "counter", "∫ UMC busy fraction dt."),
     F("amdgpu_hbm_bandwidth_bytes_per_second", "gauge",
       "HBM read+write bandwidth, window mean, from UMC activity × the MI355X calibration (1 % = 84.1 GB/s, "
@@ -214,9 +230,24 @@ CATALOG: tuple[Family, ...] = (
       source="self"),
     F("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples.", source="self"),
     F("kgs_slow_reads_total", "counter",
-      "Management-library reads by the node-wide slow thread (tier=procs: process list; tier=links: xGMI link "
-      "table + RAS).  They never run on the per-GPU sampler threads.", extra=("tier",), source="self"),
-    F("kgs_slow_read_seconds_total", "counter", "Time the node-wide slow thread spent in management-library calls.",
+      "Management-library reads by the device's slow thread kgs-slow<N> (tier=procs: process list; tier=links: xGMI "
+      "link table + RAS).  They never run on the PMFW or counter threads.", extra=("tier",), source="self"),
+    F("kgs_slow_read_seconds_total", "counter", "Time the device's slow thread spent in management-library calls.",
+      source="self"),
+    F("kgs_slow_errors_total", "counter", "Failed management-library reads of the device's slow thread, by tier "
+      "(procs, links, health).", extra=("tier",), source="self"),
+    F("kgs_slow_last_ok_age_seconds", "gauge",
+      "Seconds since the tier's last good read on the device (-1 = never).  Past --stale-after (or three tier "
+      "periods) its lines are dropped: per-process series (procs), amdgpu_xgmi_link_info (links), "
+      "amdgpu_xgmi_error_status (health).  Other devices' tiers run on their own threads.",
+      extra=("tier",), source="self"),
+    F("kgs_slow_call_seconds", "gauge", "How long the device's slow thread has been inside its current "
+      "management-library call (0 = none in flight): a call that never returns keeps growing here.", source="self"),
+    F("kgs_slow_thread_hung", "gauge", "1 if the device's slow thread was stuck in a management-library call when "
+      "sampling last stopped (abandoned after --stop-timeout; the slow tiers restart once the call returns).",
+      source="self"),
+    F("kgs_pmc_reordered_total", "counter", "Counter drains dropped because their command-processor time preceded "
+      "the previous drain's (the cumulative counts of the next drain cover the interval).  Should stay 0.",
       source="self"),
     F("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read.", extra=("le",), source="self"),
     F("kgs_sampler_wake_lateness_seconds", "histogram", "How late the counter thread woke against each tick's "

@@ -5,8 +5,13 @@ Artefacts (all land inside the package so gpurun snapshots carry them):
 * ``kube_gpu_stats_amd/_kgs_native*.so`` – C++17 data plane (sampler threads,
   seqlocks, PMFW table reader, renderer, epoll HTTP) + pybind11 bindings; links
   ``libamd_smi``.
+* ``kube_gpu_stats_amd/lib/libkgs_pmc_aql.so`` – the counter reader the exporter
+  dlopens for ``--pmc aqlprofile`` (the default counter tier): aqlprofile PM4
+  packets on a private AQL queue, pipelined and batched READs
+  (``counters/pmc_aqlprofile.cpp``, ``include/kgs/aql_batch.h``, ``aql_ring.h``).
 * ``kube_gpu_stats_amd/lib/libkgs_pmc.so`` – rocprofiler-sdk device-counting
-  reader (HSA client), dlopen'd by the exporter only when counters are on.
+  reader, a test-only cross-check (``--pmc rocprofiler`` needs
+  ``KGS_PMC_CROSSCHECK=1``; it keeps one HSA helper thread spinning).
 * ``kube_gpu_stats_amd/lib/libkgs_load.so`` – hand-written gfx950 HIP kernels
   (MFMA-bound, HBM-stream, xGMI peer copy) used as the synthetic load.
 
@@ -117,7 +122,9 @@ def build_pmc_aql(force: bool = False, verbose: bool = False) -> str:
     """Direct CP counter reader over aqlprofile (no profiler framework, no spinning helper thread)."""
     out = pmc_aql_lib_path()
     src = os.path.join(HERE, "counters", "pmc_aqlprofile.cpp")
-    if not force and not _stale(out, [src, os.path.join(HERE, "include", "kgs", "aql_ring.h"), __file__]):
+    deps = [src, os.path.join(HERE, "include", "kgs", "aql_ring.h"), os.path.join(HERE, "include", "kgs", "aql_batch.h"),
+            __file__]
+    if not force and not _stale(out, deps):
         return out
     os.makedirs(LIB, exist_ok=True)
     tmp = f"{out}.{os.getpid()}.tmp"

@@ -41,8 +41,8 @@
 // Threading: every call on one handle comes from one thread (the device's
 // sampler thread); handles of different GPUs share no lock, so a slow or hung
 // GPU never delays another's READs.  kgs_pmc_info() may be called from any
-// thread: it reads atomics and the error string under a lock that is never held
-// across a wait.
+// thread: it reads atomics, plus the error string and a snapshot of the session
+// layout under a lock that is never held across a wait.
 //
 // Counter selects for gfx950 (block, event) come from ROCm's own definitions
 // (/opt/rocm/share/rocprofiler-sdk/counter_defs.yaml); any other counter can be
@@ -117,6 +117,7 @@ struct Agent {
   uint32_t cu_count = 0;  // enabled CUs (256 on MI355X)
   hsa_queue_t* queue = nullptr;
   hsa_signal_t sig{};                                // START/STOP and synchronous READs
+  hsa_signal_t stall_sig{};                          // kgs_pmc_inject_stall: never signalled (test hook)
   std::vector<std::string> names;
   std::vector<int> reduce;                           // 0 sum, 1 max, 2 mean
   std::vector<char> per_cu;                          // counter's block has one instance per CU
@@ -163,18 +164,26 @@ struct Agent {
   uint64_t prof_n = 0, prof_bad = 0;
   int64_t prof_q_sum = 0, prof_q_max = 0, prof_x_sum = 0, prof_x_max = 0;
   int inflight = -1;                                 // slot with a READ on the queue, -1 none
-  int64_t rtt_ns = 0;                                // CP round trip of a synchronous READ (EWMA)
-  uint64_t ready_on_poll = 0, waited_on_poll = 0;    // pipelined: READ already done / had to wait
-  int64_t host_ns = 0;                               // host time spent inside sample()
+  // Written by the handle's thread only, read by kgs_pmc_info from any thread:
+  // relaxed atomics (single writer, load + store, no locked RMW on the hot path).
+  std::atomic<int64_t> rtt_ns{0};                    // CP round trip of a synchronous READ (EWMA)
+  std::atomic<uint64_t> ready_on_poll{0}, waited_on_poll{0};  // pipelined: READ already done / had to wait
+  std::atomic<int64_t> host_ns{0};                   // host time spent inside sample()
   uint32_t cmd_sz = 0, out_sz = 0;
   int lean_changed = 0;                              // packets rewritten by lean_read_ib
   std::string err;                                   // guarded by info_mu (read by kgs_pmc_info from any thread)
+  // Session layout for kgs_pmc_info (events, results per counter, XCD placement,
+  // batch, lean, pipelined), rebuilt by the handle's thread (snap_info) whenever it
+  // changes, guarded by info_mu: info never touches the vectors the hot path swaps
+  // and refolds.
+  std::string info_layout;
   std::mutex info_mu;                                // never held across a wait
   std::atomic<uint64_t> reads{0}, timeouts{0};
   std::atomic<uint64_t> enqueue_timeouts{0};         // no queue slot within the deadline (CP not consuming)
   std::atomic<uint64_t> aborted{0};                  // waits cut short by kgs_pmc_abort
   std::atomic<uint64_t> resets{0};                   // queues destroyed by kgs_pmc_reset
   std::atomic<int> abort{0};                         // kgs_pmc_abort: blocked / new waits return at once
+  std::atomic<int> stall_injected{0};                // kgs_pmc_inject_stall: a never-signalled barrier is on the queue
   uint32_t last_results = 0;
   std::vector<uint32_t> instances;                   // results folded per counter (last read)
   std::vector<double> vals;
@@ -255,6 +264,10 @@ int64_t mono_ns() {
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
 }
+
+// Single-writer counters of an Agent (the handle's thread), read by kgs_pmc_info.
+inline void bump(std::atomic<uint64_t>& c) { c.store(c.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed); }
+inline int64_t half_rtt(const Agent* a) { return a->rtt_ns.load(std::memory_order_relaxed) / 2; }
 
 hsa_status_t find_host_pool(hsa_amd_memory_pool_t pool, void*) {
   hsa_amd_segment_t seg;
@@ -658,6 +671,8 @@ void place_xcds(Agent* a) {
   a->xcd_from = "order";
 }
 
+void snap_info(Agent* a);
+
 // Fold one completed READ's output buffer into a->vals.
 int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
   a->reads.fetch_add(1, std::memory_order_relaxed);
@@ -671,9 +686,11 @@ int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
   }
   Fold f{a};
   if (hsa_ven_amd_aqlprofile_iterate_data(prof, on_data, &f) != HSA_STATUS_SUCCESS) return -3;
-  if (!a->res_xcd_done) place_xcds(a);  // the first fold's per-XCD values are never returned (open's READ)
+  const bool first = !a->res_xcd_done;
+  if (first) place_xcds(a);  // the first fold's per-XCD values are never returned (open's READ)
   a->res_xcd_done = true;
   a->last_results = f.n;
+  if (first) snap_info(a);
   // Mean of a per-CU block (TA/TD/TCP): the packets read every instance slot of
   // every SE (16 per SE on gfx950), but only cu_count of them exist (8 per SE
   // on MI355X); the absent ones read 0.  Average over the CUs that exist.
@@ -688,7 +705,8 @@ int read_values(Agent* a) {
   const int64_t t0 = mono_ns();
   if (submit(a, a->read_pkt) != 0) return -2;
   const int64_t rtt = mono_ns() - t0;
-  a->rtt_ns = a->rtt_ns ? (7 * a->rtt_ns + rtt) / 8 : rtt;
+  const int64_t prev = a->rtt_ns.load(std::memory_order_relaxed);
+  a->rtt_ns.store(prev ? (7 * prev + rtt) / 8 : rtt, std::memory_order_relaxed);
   return fold(a, &a->prof);
 }
 
@@ -699,7 +717,7 @@ int read_pipelined(Agent* a, int64_t* ts) {
     const int64_t t0 = mono_ns();
     const int rc = read_values(a);
     if (rc != 0) return rc;
-    if (ts) *ts = t0 + a->rtt_ns / 2;
+    if (ts) *ts = t0 + half_rtt(a);
     std::memset(a->pout[0], 0, a->pprof[0].output_buffer.size);
     a->psubmit_ns[0] = mono_ns();
     a->inflight = enqueue(a, a->pread[0], a->psig[0], read_fences()) == 0 ? 0 : -1;
@@ -707,9 +725,9 @@ int read_pipelined(Agent* a, int64_t* ts) {
   }
   const int k = a->inflight;
   if (hsa_signal_load_scacquire(a->psig[k]) < 1) {
-    ++a->ready_on_poll;
+    bump(a->ready_on_poll);
   } else {
-    ++a->waited_on_poll;
+    bump(a->waited_on_poll);
     if (wait_done(a, a->psig[k]) != 0) {
       a->inflight = -1;  // the packet may still complete later; its slot is re-armed before reuse
       return -2;
@@ -742,7 +760,7 @@ int read_pipelined(Agent* a, int64_t* ts) {
     }
   }
   const int rc = fold(a, &a->pprof[k]);
-  if (ts) *ts = a->psubmit_ns[k] + a->rtt_ns / 2;
+  if (ts) *ts = a->psubmit_ns[k] + half_rtt(a);
   const int n = k ^ 1;
   std::memset(a->pout[n], 0, a->pprof[n].output_buffer.size);
   a->psubmit_ns[n] = mono_ns();
@@ -781,6 +799,22 @@ bool is_publisher(const Agent* a, int k) { return a->batch < 2 || a->plan.is_pub
 bool nonpub_barrier() {
   static const bool on = std::getenv("KGS_AQL_NOBARRIER") == nullptr;
   return on;
+}
+
+// Rebuild the session-layout part of kgs_pmc_info (handle's thread only; called
+// when the layout changes: open, mode switch, the first fold of an event list).
+void snap_info(Agent* a) {
+  std::string o = ";events=" + std::to_string(a->events.size()) + ";results=" + std::to_string(a->last_results) +
+                  ";pipelined=" + std::to_string(a->pipelined ? 1 : 0) + ";lean=" + std::to_string(lean_mode()) + ":" +
+                  std::to_string(a->lean_changed) + ";batch=" + std::to_string(a->batch) +
+                  ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
+                  a->xcd_from;
+  if (!nonpub_barrier()) o += a->batch >= 2 ? ";nobarrier=1" : ";nobarrier=ignored(batch<2)";
+  if (queue_priority() >= 0) o += ";priority=" + std::to_string(queue_priority());
+  for (size_t k = 0; k < a->names.size(); ++k)
+    o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
+  std::lock_guard<std::mutex> g(a->info_mu);
+  a->info_layout.swap(o);
 }
 
 // true = every result dword of slot k was written (fold it), false = drop the READ.
@@ -832,7 +866,7 @@ void batch_collect(Agent* a, int h) {
     r.vals = a->vals;
     r.vals_xcd = a->vals_xcd;
     r.xcd_seen = a->xcd_seen;
-    r.ts = a->psubmit_ns[k] + a->rtt_ns / 2;
+    r.ts = a->psubmit_ns[k] + half_rtt(a);
     a->bready.push_back(std::move(r));
   }
   a->plan.collected(h);
@@ -849,23 +883,29 @@ int read_batched(Agent* a, int64_t* ts) {
     const int rc = read_values(a);
     if (rc != 0) return rc;
     ++a->publishes;  // a synchronous READ writes the L2 back
-    if (ts) *ts = t0 + a->rtt_ns / 2;
+    if (ts) *ts = t0 + half_rtt(a);
     a->bprimed = true;
     return 0;  // the next call starts the slot rotation
   }
-  const int cur = p.current_half(), old = cur ^ 1;
-  // The other half's publisher went out a tick or more ago: usually done.
-  if (p.closed(old) && hsa_signal_load_scacquire(a->psig[p.publisher(old)]) < 1) {
-    ++a->ready_on_poll;
-    batch_collect(a, old);
-  }
-  if (p.closed(cur)) {  // reusing a half not yet collected: wait for its publisher
-    ++a->waited_on_poll;
-    if (wait_done(a, a->psig[p.publisher(cur)]) != 0) {
-      batch_reset(a);  // the packets may still complete later; their slots are re-armed before reuse
-      return -2;
+  // Fold closed halves oldest first (BatchPlan::collect_order): the half the next
+  // READ reuses, if still closed, is older than the other one and is waited for;
+  // the other half's publisher went out a tick or more ago and is usually done.
+  const int other = p.current_half() ^ 1;
+  const bool other_done = p.closed(other) && hsa_signal_load_scacquire(a->psig[p.publisher(other)]) < 1;
+  int halves[2];
+  bool waits[2];
+  const int nh = p.collect_order(other_done, halves, waits);
+  for (int i = 0; i < nh; ++i) {
+    if (waits[i]) {  // reusing a half not yet collected: wait for its publisher
+      bump(a->waited_on_poll);
+      if (wait_done(a, a->psig[p.publisher(halves[i])]) != 0) {
+        batch_reset(a);  // the packets may still complete later; their slots are re-armed before reuse
+        return -2;
+      }
+    } else {
+      bump(a->ready_on_poll);
     }
-    batch_collect(a, cur);
+    batch_collect(a, halves[i]);
   }
   const int k = p.next_slot(mono_ns());
   for (volatile uint32_t* d : a->pdst[k]) *d = kUnlanded;
@@ -1162,6 +1202,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
       std::lock_guard<std::mutex> g(a->info_mu);
       a->err = "unresolved: " + missing;
     }
+    snap_info(a);
     return static_cast<int>(h);
   }
   set_err(err, errlen, "no HSA GPU agent with kfd gpu_id " + std::to_string(kfd_gpu_id));
@@ -1190,11 +1231,11 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
     if (rc == 0) ++a->publishes;  // every unbatched READ writes the L2 back
   } else {
     rc = read_values(a);
-    ts = t0 + a->rtt_ns / 2;
+    ts = t0 + half_rtt(a);
     if (rc == 0) ++a->publishes;
   }
   const int64_t t1 = mono_ns();
-  a->host_ns += t1 - t0;
+  a->host_ns.store(a->host_ns.load(std::memory_order_relaxed) + (t1 - t0), std::memory_order_relaxed);
   if (read_ns) *read_ns = static_cast<uint32_t>(t1 - t0);
   if (sample_ns) *sample_ns = ts;
   if (rc != 0) return rc;
@@ -1239,6 +1280,7 @@ int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
     }
   }
   a->pipelined = on != 0;
+  snap_info(a);
   return 0;
 }
 
@@ -1259,28 +1301,28 @@ int kgs_pmc_stats(int handle, uint64_t* out, int n) {
 int kgs_pmc_info(int handle, char* buf, int len) {
   if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
   Agent* a = g_agents[static_cast<size_t>(handle)];
+  const uint64_t reads = a->reads.load();
   std::string o = "impl=aqlprofile;mode=cumulative;cu=" + std::to_string(a->cu_count) +
-                  ";events=" + std::to_string(a->events.size()) +
-                  ";results=" + std::to_string(a->last_results) + ";timeouts=" + std::to_string(a->timeouts.load()) +
+                  ";timeouts=" + std::to_string(a->timeouts.load()) +
                   ";enqueue_timeouts=" + std::to_string(a->enqueue_timeouts.load()) +
                   ";aborted=" + std::to_string(a->aborted.load()) + ";resets=" + std::to_string(a->resets.load()) +
+                  ";stall_injected=" + std::to_string(a->stall_injected.load()) +
                   ";timeout_ms=" + std::to_string(g_timeout_ns.load() / 1000000) +
-                  ";pipelined=" + std::to_string(a->pipelined ? 1 : 0) + ";rtt_us=" + std::to_string(a->rtt_ns / 1000) +
-                  ";reads=" + std::to_string(a->reads.load()) + ";ready_on_poll=" + std::to_string(a->ready_on_poll) +
-                  ";waited_on_poll=" + std::to_string(a->waited_on_poll) +
-                  ";host_us_per_read=" + std::to_string(a->reads ? a->host_ns / 1000.0 / a->reads.load() : 0.0) +
-                  ";lean=" + std::to_string(lean_mode()) + ":" + std::to_string(a->lean_changed) +
-                  ";batch=" + std::to_string(a->batch) + ";land_waits=" + std::to_string(a->land_waits.load()) +
+                  ";rtt_us=" + std::to_string(a->rtt_ns.load(std::memory_order_relaxed) / 1000) +
+                  ";reads=" + std::to_string(reads) +
+                  ";ready_on_poll=" + std::to_string(a->ready_on_poll.load(std::memory_order_relaxed)) +
+                  ";waited_on_poll=" + std::to_string(a->waited_on_poll.load(std::memory_order_relaxed)) +
+                  ";host_us_per_read=" +
+                  std::to_string(reads ? a->host_ns.load(std::memory_order_relaxed) / 1000.0 / reads : 0.0) +
+                  ";land_waits=" + std::to_string(a->land_waits.load()) +
                   ";land_timeouts=" + std::to_string(a->land_timeouts.load()) +
                   ";publishes=" + std::to_string(a->publishes.load()) +
-                  ";publish_us=" + std::to_string(g_publish_ns / 1000) +
-                  ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
-                  a->xcd_from + ";num_xcc=" + std::to_string(a->num_xcc) + ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
+                  ";publish_us=" + std::to_string(g_publish_ns / 1000) + ";num_xcc=" + std::to_string(a->num_xcc) +
+                  ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
                   ";signal=" + (poll_signals() ? "poll" : "interrupt");
-  for (size_t k = 0; k < a->names.size(); ++k)
-    o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
   {
     std::lock_guard<std::mutex> g(a->info_mu);
+    o += a->info_layout;
     if (!a->err.empty()) o += ";" + a->err;
   }
   set_err(buf, len, o);
@@ -1328,7 +1370,48 @@ int kgs_pmc_reset(int handle) {
     hsa_queue_destroy(a->queue);
     a->queue = nullptr;
   }
+  if (a->stall_sig.handle) {  // its barrier packet went with the queue
+    hsa_signal_destroy(a->stall_sig);
+    a->stall_sig = hsa_signal_t{};
+  }
+  a->stall_injected.store(0);
   a->resets.fetch_add(1, std::memory_order_relaxed);
+  return 0;
+}
+
+// Test hook for the counter tier's fault boundary on hardware:
+// wedge the agent's READ queue the way a stuck command processor would.  An AQL
+// BARRIER_AND packet whose dependency signal is never signalled goes on the queue;
+// the packet processor stops there, so every later READ, STOP or START on this
+// queue never completes (the workload's own queues are untouched).  Only
+// kgs_pmc_reset — hsa_queue_destroy — clears it.  Call from the handle's thread.
+// 0 = injected, -1 = no queue / no slot / no signal.
+int kgs_pmc_inject_stall(int handle) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  Agent* a = g_agents[static_cast<size_t>(handle)];
+  hsa_queue_t* q = a->queue;
+  if (!q) return -1;
+  if (!a->stall_sig.handle && hsa_signal_create(1, 0, nullptr, &a->stall_sig) != HSA_STATUS_SUCCESS) return -1;
+  hsa_signal_store_relaxed(a->stall_sig, 1);
+  uint64_t idx = 0;
+  const kgs::SlotResult r = kgs::reserve_slot(
+      q->size, mono_ns() + g_timeout_ns.load(std::memory_order_relaxed), &a->abort,
+      [q] { return hsa_queue_load_read_index_scacquire(q); }, [q] { return hsa_queue_load_write_index_relaxed(q); },
+      [q](uint64_t i) { hsa_queue_store_write_index_relaxed(q, i + 1); }, [] { return mono_ns(); },
+      [] { sched_yield(); }, idx);
+  if (r != kgs::SlotResult::kOk) return -1;
+  auto* slot = reinterpret_cast<hsa_barrier_and_packet_t*>(q->base_address) + (idx & (q->size - 1));
+  slot->reserved0 = 0;
+  slot->reserved1 = 0;
+  for (hsa_signal_t& d : slot->dep_signal) d = hsa_signal_t{};
+  slot->dep_signal[0] = a->stall_sig;
+  slot->reserved2 = 0;
+  slot->completion_signal = hsa_signal_t{};
+  const uint16_t header = static_cast<uint16_t>((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                                                (1 << HSA_PACKET_HEADER_BARRIER));
+  __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(q->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+  a->stall_injected.store(1);
   return 0;
 }
 

@@ -98,6 +98,28 @@ class BatchPlan {
     closed_[half] = false;
   }
 
+  // Which closed halves to fold before the next READ, oldest first (ADVICE r3:
+  // folding them out of order hands the caller samples whose time and cumulative
+  // counts go backwards).  When both halves are closed, the current half — the one
+  // the next READ goes into — closed first: the other closed after it and is the
+  // newer.  A current half that is closed must be folded (wait[i] = true: block on
+  // its publisher) before its slots are reused; the other is folded only if its
+  // publisher is already done (`other_done`).  Returns how many entries of
+  // half/wait were written (0..2).
+  int collect_order(bool other_done, int* half, bool* wait) const {
+    const int cur = current_half(), other = cur ^ 1;
+    int n = 0;
+    if (closed_[cur]) {
+      half[n] = cur;
+      wait[n++] = true;
+    }
+    if (closed_[other] && other_done) {
+      half[n] = other;
+      wait[n++] = false;
+    }
+    return n;
+  }
+
  private:
   int b_ = 2;
   int64_t publish_ns_ = 0;

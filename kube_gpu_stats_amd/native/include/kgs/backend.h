@@ -122,6 +122,12 @@ struct MockConfig {
   // every period and base − amp for the rest (bursty jobs between scrapes).
   double util_base = 50, util_amp = 40, util_period_s = 10;
   double square_duty = 0;
+  // The PMFW GFX busy (gfx_busy, its accumulator, per-XCC) never reads below this
+  // percent, as on MI355X when the counter tier READs every tick (≈80 µs of PMFW
+  // busy per READ: 99.7 % on an idle GPU at 8 kHz, profiles/r2/idle_busy/).  The mock
+  // counter source still sees the true load.  Exact for square-wave loads (the
+  // floor lifts the low level); a sine load only has its instantaneous value floored.
+  double pmfw_busy_floor = 0;
   double ppt_frac = 0;          // share of accumulation cycles the package-power throttler is active
   // "SPX" | "DPX" | "QPX" | "CPX": each GPU shows up as this many devices, all
   // with the GPU's BDF, one partition_id each, XCC curve g·8 + x per XCC.
@@ -146,6 +152,16 @@ struct MockConfig {
   // Background xGMI traffic on every link, following the util curve (1 GB/s per
   // link at 100 %); off, only inject_xgmi() moves the link accumulators.
   bool xgmi_bg = true;
+  // Slow-tier fault injection (per-device isolation test): after
+  // slow_fault_after_s, calls of tier slow_fault_tier ("procs" | "links" |
+  // "health") on device slow_fault_dev either hang (kind "hang": block for
+  // slow_hang_s, < 0 = until the process exits, outside the management-library
+  // lock — a call stuck in one device's driver path) or fail (kind "error").
+  int slow_fault_dev = -1;
+  std::string slow_fault_tier = "procs";
+  std::string slow_fault_kind = "hang";
+  double slow_fault_after_s = 0;
+  double slow_hang_s = -1;
   uint64_t seed = 1;
   std::string hostname_seed;    // reserved
 };

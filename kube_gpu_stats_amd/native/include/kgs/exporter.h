@@ -26,7 +26,7 @@ struct Owner {
   std::string pod, ns, container;
   // The GPU's busy integrals when this owner was first seen on it: the per-pod
   // counters (container_gpu_busy_seconds_total, ...) count from 0 at allocation.
-  double base_busy_s = 0, base_mfma_s = 0, base_active_s = 0, base_energy_j = 0, base_cu_s = 0;
+  double base_busy_s = 0, base_mfma_s = 0, base_active_s = 0, base_energy_j = 0, base_cu_s = 0, base_util_s = 0;
   bool same(const Owner& o) const { return pod == o.pod && ns == o.ns && container == o.container; }
 };
 struct PidOwner {
@@ -76,12 +76,13 @@ struct ExporterConfig {
   bool per_process = true;
   bool compat_series = true;        // container_gpu_sm_util (reference contract)
   bool compat_unallocated = false;  // also emit it for GPUs with no pod (pod_name="")
-  // What container_gpu_sm_util / container_gpu_busy_seconds_total measure:
-  // "pmfw" = the firmware's GFX busy (a dispatch in flight; counts the counter
-  // tier's own READ packets as work, profiles/r2/idle_busy/), "counters" =
-  // GRBM_SPI_BUSY from the counter tier (a shader engine has waves; READ-immune at
-  // any tick rate, needs --pmc).
-  std::string sm_util_source = "pmfw";
+  // What container_gpu_sm_util / container_gpu_busy_seconds_total (and
+  // amdgpu_gfx_busy_*) measure: "auto" (default) = the READ-immune integral
+  // (Integrals::util_seconds: the counter tier's GRBM_SPI_BUSY while it runs, the
+  // PMFW GFX busy otherwise); "pmfw" = the firmware's GFX busy alone (a dispatch in
+  // flight; counts the counter tier's own READ packets as work,
+  // profiles/r2/idle_busy/); "counters" = GRBM_SPI_BUSY alone (needs --pmc).
+  std::string sm_util_source = "auto";
   bool control_http = false;        // serve /control/pause|resume (benchmarks only)
   // gzip level for /metrics when the client sends Accept-Encoding: gzip (0 = never).
   // Off by default: level 1 costs ≈0.6 ms per 8-GPU page (≈117 KB → 11 KB), about

@@ -129,6 +129,12 @@ class CounterSource {
   virtual void cancel(int dev, bool on) {}
   // Counters of the fault boundary (for kgs_pmc_* self-metrics): resets done.
   virtual uint64_t resets(int dev) const { return 0; }
+  // Test hook (the fault-boundary test on hardware): wedge the
+  // device's counter path the way a stuck command processor would — the aqlprofile
+  // reader puts a barrier packet that waits on a never-signalled signal at the head
+  // of its READ queue, so every later READ, STOP and START on that queue stalls —
+  // until reset() drops the queue.  Sampler thread only.  0 = ok.
+  virtual int inject_stall(int dev) { return -1; }
   // Publication of READ results (batched reader, include/kgs/aql_batch.h): READs
   // folded, READs that wrote the GPU's L2 back, and results that had not reached
   // host memory when folded.  Any thread.  false = the source does not say.

@@ -66,6 +66,9 @@ struct GpuSample {
   // gfx_busy_seconds / umc_busy_seconds / sampled_seconds): the mean over any
   // window is a difference of two samples, found by binary search of the ring.
   double cum_gfx_s = 0, cum_umc_s = 0, cum_dt_s = 0;
+  // Running READ-immune busy integral (Integrals::util_seconds) at this sample.
+  double cum_util_s = 0;
+  float util_window_pct = -1;  // its mean since the previous distinct sample
 
   float temp_hotspot_c = 0, temp_mem_c = 0, temp_vrsoc_c = 0;
   float power_w = 0;
@@ -148,6 +151,19 @@ struct Integrals {
   // ∫ GPU-active (GRBM_SPI_BUSY share of clocks) dt from the counter stream: the
   // READ-immune busy integral (--sm-util-source counters).
   double active_seconds = 0;
+  // Counter-tier continuity, published with the counter integrals: bumped on every
+  // break (release, breaker trip, failed re-START), and the CLOCK_MONOTONIC time of
+  // the last folded drain.  The PMFW thread uses a Δactive_seconds only across an
+  // interval with one epoch and a fresh drain (Sampler::run_pmfw).
+  uint64_t pmc_epoch = 0;
+  int64_t pmc_last_ns = 0;
+  // ∫ busy dt that does not count the exporter's own counter READs (the default
+  // --sm-util-source auto behind container_gpu_sm_util / container_gpu_busy_seconds_total):
+  // per PMFW interval, the counter tier's Δactive_seconds (GRBM_SPI_BUSY) while it
+  // covered the whole interval, else the PMFW GFX busy.  util_counter_seconds is the
+  // time the counter source covered.
+  double util_seconds = 0;
+  double util_counter_seconds = 0;
   // ∫ throttled fraction dt per reason (Δresidency / Δaccumulation_counter per
   // distinct PMFW table): seconds the GPU ran held back by each controller.
   double throttle_seconds[kThrottleReasons] = {};

@@ -21,10 +21,17 @@
 // The management-library tiers — per-process list (mid tier, every proc_every
 // ticks' worth of time), xGMI link table + RAS health (slow tier, every
 // link_every ticks' worth) — go through AMD SMI, which serialises callers on one
-// process-wide mutex and takes milliseconds per call.  They run on ONE node-wide
-// "kgs-slow" thread that walks the devices in turn, so a slow
-// amdsmi_get_gpu_process_list on GPU 3 can never delay GPU 5's 8 kHz counter
-// drain (profiles/r2/mock_scaling.md).
+// process-wide mutex and takes milliseconds per call.  They run on a third thread
+// per device, "kgs-slow<N>", so an amdsmi_get_gpu_process_list on GPU 3 can never
+// delay GPU 5's 8 kHz counter drain, and a call that hangs
+// on GPU 3 leaves GPU 5's per-process list, link table and per-pod CU-seconds
+// fresh.  Every slow-tier result carries the time of its last
+// good read; the renderer drops a device's per-process, link and RAS-status
+// lines once they are older than the exporter's stale_after, and exports each
+// tier's age (kgs_slow_last_ok_age_seconds) and any call in flight for longer
+// (kgs_slow_call_seconds).  A hang inside AMD SMI's own process-wide lock stalls
+// every device's slow thread alike — those tiers then all go stale, while the
+// PMFW and counter tiers (no AMD SMI call) keep sampling.
 // A sample counts as *distinct* only when the firmware timestamp moved
 // (BASELINE.md measurement rule).  Results are published through seqlocks; the
 // scrape path never calls into the driver.
@@ -126,6 +133,9 @@ constexpr double kQuietActiveFrac = 0.02;
 // idle period late, and every tick in between is a lost sample).
 constexpr int64_t kQuietHoldNs = 5000000;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
+// Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
+enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };
+inline const char* slow_tier_name(int t) { return t == kSlowProcs ? "procs" : t == kSlowLinks ? "links" : "health"; }
 
 struct DeviceState {
   Seqlock<GpuSample> latest;
@@ -172,6 +182,18 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_breaker_trips{0};
   std::atomic<uint64_t> pmc_retries{0};      // reset + acquire attempts while the breaker is open
   std::atomic<int> thread_hung{0};           // a sampler thread of this device was abandoned by stop()
+  std::atomic<uint64_t> pmc_reordered{0};    // drains dropped: CP time earlier than the previous drain's
+  // Test hook (Sampler::inject_pmc_stall, /control/pmc/stall with --control-http):
+  // the device's own counter thread asks the source to wedge its READ queue.
+  std::atomic<int> pmc_stall_req{0};
+  std::atomic<uint64_t> pmc_stalls_injected{0};
+  // Slow tiers (kgs-slow<N>): CLOCK_MONOTONIC of each tier's last good read (0 =
+  // never), and the start of the management-library call in flight (0 = none).
+  std::atomic<int64_t> procs_ok_ns{0}, links_ok_ns{0}, health_ok_ns{0};
+  std::atomic<int64_t> slow_call_ns{0};
+  std::atomic<int> slow_call_tier{-1};       // kSlowProcs | kSlowLinks | kSlowHealth while in a call
+  std::atomic<int> slow_hung{0};             // the slow thread was abandoned by stop() (stuck in a call)
+  std::atomic<uint64_t> link_errors{0}, health_errors{0};
   PmcSample pmc_base;  // totals carried over hand-overs (sampler thread only; survives pause/resume)
   int pmc_fail_streak = 0;                   // counter thread only (survive pause/resume)
   int64_t pmc_retry_at_ns = 0;
@@ -212,6 +234,8 @@ struct DeviceState {
     a.pmc_read_seconds = b.pmc_read_seconds;
     a.mfma_busy_seconds = b.mfma_busy_seconds;
     a.active_seconds = b.active_seconds;
+    a.pmc_epoch = b.pmc_epoch;
+    a.pmc_last_ns = b.pmc_last_ns;
     return a;
   }
 };
@@ -232,7 +256,8 @@ class Sampler {
 
   // Mean of gfx/umc busy over the trailing `window_s` of firmware time
   // (time-weighted by each sample's dt).  Returns false if no data.
-  bool window_busy(int dev, double window_s, double& gfx_pct, double& umc_pct, int& n) const;
+  // util_pct (optional): the READ-immune busy mean (GpuSample::cum_util_s) over the same window.
+  bool window_busy(int dev, double window_s, double& gfx_pct, double& umc_pct, int& n, double* util_pct = nullptr) const;
   // Counter-derived rates over the trailing window.
   bool window_pmc(int dev, double window_s, PmcRates& out) const;
   // Ask a device's counter thread (dev < 0: every sampled device's) to hand its
@@ -253,8 +278,15 @@ class Sampler {
   bool set_pmc_gap(double busy_min, double hz);
   double pmc_busy_min() const { return pmc_busy_min_.load(std::memory_order_relaxed); }
   double pmc_gap_hz() const { return pmc_gap_hz_.load(std::memory_order_relaxed); }
-  // Node-wide slow thread: passes completed and whether it is running.
+  // Slow-tier passes completed (all devices).
   uint64_t slow_passes() const { return slow_passes_.load(); }
+  // Test hook: the device's counter thread wedges its reader's queue
+  // (CounterSource::inject_stall) on its next tick.  false if dev is not sampled.
+  bool inject_pmc_stall(int dev);
+  // Slow-tier periods in force (ns; 0 = tier off): freshness checks size their
+  // deadline on these.
+  int64_t proc_period_ns() const;
+  int64_t link_period_ns() const;
   // Threads stop() gave up on (stuck in a device call); they are detached and
   // exit on their own if the call ever returns.  The owner must then keep the
   // backend, counter source and this sampler alive (Exporter leaks them).
@@ -273,6 +305,7 @@ class Sampler {
   void run_pmfw(Worker& w);
   void run_pmc(Worker& w);
   void run_slow(Worker& w);
+  void run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, Integrals& I, GpuSample& s);
   void pin(int dev, const char* fmt);
   void integrate(int dev, const GpuSample* prev, GpuSample& cur, Integrals& I);
 
@@ -292,10 +325,18 @@ class Sampler {
   std::atomic<double> pmc_gap_hz_{1000.0};
   mutable std::mutex pid_pods_mu_;
   std::shared_ptr<const std::unordered_map<uint64_t, std::string>> pid_pods_;
-  std::vector<std::map<std::string, double>> pod_cu_;  // slow thread only
-  // Per-device process CU-occupancy integrals (slow thread only; survive pause/resume).
+  std::vector<std::map<std::string, double>> pod_cu_;  // device's slow thread only
+  // Per-device process CU-occupancy integrals (device's slow thread only; survive pause/resume).
   std::vector<std::vector<std::pair<uint32_t, double>>> cu_seconds_;
   std::vector<int64_t> last_proc_ns_;
+  // READ-immune util integral: the counter-tier state seen at the previous distinct
+  // PMFW sample (each device's PMFW thread only; survive pause/resume).
+  struct UtilPrev {
+    bool have = false;
+    uint64_t epoch = 0;
+    double active_s = 0;
+  };
+  std::vector<UtilPrev> util_prev_;
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
   int stop_fd_ = -1;  // eventfd: readable once stop() was called; sampler threads ppoll() on it

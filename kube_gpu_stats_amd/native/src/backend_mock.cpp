@@ -6,6 +6,8 @@
 // covers the failure modes of SURVEY.md §5.3: read errors, stalls, a device
 // that disappears, accumulator wrap.
 #include <atomic>
+#include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <ctime>
@@ -69,9 +71,22 @@ void sleep_s(double s) {
   if (s > 0) std::this_thread::sleep_for(std::chrono::duration<double>(s));
 }
 
+// The load as the PMFW GFX busy sees it (MockConfig::pmfw_busy_floor): a square
+// wave's low level lifted to the floor.
+MockConfig pmfw_view(const MockConfig& c) {
+  MockConfig f = c;
+  if (c.pmfw_busy_floor > 0 && c.square_duty > 0) {
+    const double hi = std::max(clamp100(c.util_base + c.util_amp), c.pmfw_busy_floor);
+    const double lo = std::max(clamp100(c.util_base - c.util_amp), c.pmfw_busy_floor);
+    f.util_base = 0.5 * (hi + lo);
+    f.util_amp = 0.5 * (hi - lo);
+  }
+  return f;
+}
+
 class MockBackend final : public Backend {
  public:
-  explicit MockBackend(const MockConfig& c) : cfg_(c), t0_(mono_ns()), parts_(parts_of(c)) {
+  explicit MockBackend(const MockConfig& c) : cfg_(c), pmfw_(pmfw_view(c)), t0_(mono_ns()), parts_(parts_of(c)) {
     const int xcc_per = kMaxXcc / parts_;
     for (int g = 0; g < cfg_.n_gpus; ++g) {
       for (int p = 0; p < parts_; ++p) {
@@ -127,6 +142,11 @@ class MockBackend final : public Backend {
 
   double util(int d, double t) const { return mock_device_util(cfg_, d, t); }
   double util_integral(int d, double t) const { return mock_device_util_integral(cfg_, d, t); }
+  // What the PMFW GFX busy reads (the floor of MockConfig::pmfw_busy_floor applied).
+  double pmfw_util(int d, double t) const {
+    return std::max(mock_device_util(pmfw_, d, t), cfg_.pmfw_busy_floor);
+  }
+  double pmfw_util_integral(int d, double t) const { return mock_device_util_integral(pmfw_, d, t); }
 
   // A vanished device stays gone for vanish_for_s, then needs recover(): like a
   // GPU reset, the firmware restarts with its accumulators at zero.
@@ -160,8 +180,8 @@ class MockBackend final : public Backend {
     // The PMFW table is per physical GPU: every XCC's busy and accumulator, the
     // chip-wide mean, then (partitions) the device's own XCCs.
     const int g = d / parts_;
-    const double u = parts_ > 1 ? chip_util(g, tf) : util(d, tf);
-    const double ui = parts_ > 1 ? chip_util_integral(g, tf) : util_integral(d, tf);
+    const double u = parts_ > 1 ? chip_util(g, tf) : pmfw_util(d, tf);
+    const double ui = parts_ > 1 ? chip_util_integral(g, tf) : pmfw_util_integral(d, tf);
     s.fw_ts = static_cast<uint64_t>(tf * 1e8) + 1000;  // 10 ns units, never 0
     s.gfx_busy_pct = static_cast<float>(u);
     s.umc_busy_pct = static_cast<float>(u * 0.5);
@@ -234,7 +254,19 @@ class MockBackend final : public Backend {
     return u / kMaxXcc;
   }
 
+  // Slow-tier fault injection (MockConfig::slow_fault_*): 0 = no fault, -1 = the
+  // call fails.  A hang blocks here, before the management-library lock.
+  int slow_fault(int d, const char* tier) {
+    if (d != cfg_.slow_fault_dev || cfg_.slow_fault_tier != tier) return 0;
+    if ((mono_ns() - t0_) * 1e-9 < cfg_.slow_fault_after_s) return 0;
+    if (cfg_.slow_fault_kind == "error") return -1;
+    const int64_t end = cfg_.slow_hang_s < 0 ? INT64_MAX : mono_ns() + static_cast<int64_t>(cfg_.slow_hang_s * 1e9);
+    while (mono_ns() < end) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    return 0;
+  }
+
   int read_procs(int d, std::vector<ProcInfo>& out) override {
+    if (slow_fault(d, "procs") != 0) return -1;
     std::lock_guard<std::mutex> lk(smi_mu_);
     sleep_s(cfg_.proc_latency_s);
     out.clear();
@@ -257,6 +289,7 @@ class MockBackend final : public Backend {
   }
 
   int read_links(int d, std::vector<LinkInfo>& out) override {
+    if (slow_fault(d, "links") != 0) return -1;
     std::lock_guard<std::mutex> lk(smi_mu_);
     sleep_s(cfg_.link_latency_s);
     out.clear();
@@ -280,6 +313,7 @@ class MockBackend final : public Backend {
   }
 
   int read_health(int d, HealthInfo& out) override {
+    if (slow_fault(d, "health") != 0) return -1;
     std::lock_guard<std::mutex> lk(smi_mu_);
     sleep_s(cfg_.health_latency_s);
     const double t = (mono_ns() - t0_) * 1e-9;
@@ -322,6 +356,7 @@ class MockBackend final : public Backend {
   };
 
   MockConfig cfg_;
+  MockConfig pmfw_;        // cfg_ as the PMFW busy sees it (pmfw_busy_floor)
   int64_t t0_;
   int parts_;              // devices per physical GPU (compute partitions)
   std::vector<std::unique_ptr<LinkInj>> inj_;

@@ -37,6 +37,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.seed = get<uint64_t>(m, "seed", c.mock.seed);
     c.mock.ecc_correctable_per_s = get<uint64_t>(m, "ecc_correctable_per_s", c.mock.ecc_correctable_per_s);
     c.mock.square_duty = get<double>(m, "square_duty", c.mock.square_duty);
+    c.mock.pmfw_busy_floor = get<double>(m, "pmfw_busy_floor", c.mock.pmfw_busy_floor);
     c.mock.ppt_frac = get<double>(m, "ppt_frac", c.mock.ppt_frac);
     c.mock.compute_partition = get<std::string>(m, "compute_partition", c.mock.compute_partition);
     c.mock.proc_latency_s = get<double>(m, "proc_latency_s", c.mock.proc_latency_s);
@@ -45,6 +46,11 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.metrics_latency_s = get<double>(m, "metrics_latency_s", c.mock.metrics_latency_s);
     c.mock.proc_cu_share = get<std::vector<double>>(m, "proc_cu_share", c.mock.proc_cu_share);
     c.mock.xgmi_bg = get<bool>(m, "xgmi_bg", c.mock.xgmi_bg);
+    c.mock.slow_fault_dev = get<int>(m, "slow_fault_dev", c.mock.slow_fault_dev);
+    c.mock.slow_fault_tier = get<std::string>(m, "slow_fault_tier", c.mock.slow_fault_tier);
+    c.mock.slow_fault_kind = get<std::string>(m, "slow_fault_kind", c.mock.slow_fault_kind);
+    c.mock.slow_fault_after_s = get<double>(m, "slow_fault_after_s", c.mock.slow_fault_after_s);
+    c.mock.slow_hang_s = get<double>(m, "slow_hang_s", c.mock.slow_hang_s);
   }
   if (d.contains("mock_pmc")) {
     py::dict m = d["mock_pmc"].cast<py::dict>();
@@ -249,6 +255,9 @@ class PyExporter {
     o["pmc_read_seconds"] = I.pmc_read_seconds;
     o["mfma_busy_seconds"] = I.mfma_busy_seconds;
     o["active_seconds"] = I.active_seconds;
+    o["util_seconds"] = I.util_seconds;
+    o["util_counter_seconds"] = I.util_counter_seconds;
+    o["pmc_epoch"] = I.pmc_epoch;
     {
       py::dict t;
       for (int r = 0; r < kThrottleReasons; ++r) t[throttle_reason_name(r)] = I.throttle_seconds[r];
@@ -270,6 +279,10 @@ class PyExporter {
     o["pmc_retries"] = st.pmc_retries.load();
     o["pmc_releases"] = st.pmc_releases.load();
     o["thread_hung"] = st.thread_hung.load();
+    o["slow_hung"] = st.slow_hung.load();
+    o["proc_errors"] = st.proc_errors.load();
+    o["pmc_reordered"] = st.pmc_reordered.load();
+    o["pmc_stalls_injected"] = st.pmc_stalls_injected.load();
     o["pmc_resets"] = ex_.counters() ? ex_.counters()->resets(d) : 0;
     return o;
   }
@@ -294,11 +307,12 @@ class PyExporter {
   py::dict window(int d, double window_s) const {
     check(d);
     py::dict o;
-    double g = 0, u = 0;
+    double g = 0, u = 0, util = 0;
     int n = 0;
-    if (ex_.sampler()->window_busy(d, window_s, g, u, n)) {
+    if (ex_.sampler()->window_busy(d, window_s, g, u, n, &util)) {
       o["gfx_busy_pct"] = g;
       o["umc_busy_pct"] = u;
+      o["util_pct"] = util;
       o["n"] = n;
     }
     PmcRates r;
@@ -418,6 +432,10 @@ class PyExporter {
   }
   uint64_t abandoned_threads() const { return ex_.sampler()->abandoned_threads(); }
   int inject_xgmi(int src, int dst, uint64_t bytes) { return ex_.backend()->inject_xgmi(src, dst, bytes); }
+  bool inject_pmc_stall(int d) {
+    check(d);
+    return ex_.sampler()->inject_pmc_stall(d);
+  }
   double sample_rate() const { return ex_.sample_rate(); }
   uint64_t slow_passes() const { return ex_.sampler()->slow_passes(); }
   bool pmc_enabled() const { return ex_.pmc_enabled(); }
@@ -478,6 +496,9 @@ PYBIND11_MODULE(_kgs_native, m) {
                              "sampler threads stop() gave up on (stuck in a device call)")
       .def("inject_xgmi", &PyExporter::inject_xgmi, py::arg("src"), py::arg("dst"), py::arg("bytes"),
            "mock backend only: account a peer copy of `bytes` from GPU src to GPU dst on the link between them")
+      .def("inject_pmc_stall", &PyExporter::inject_pmc_stall, py::arg("gpu"),
+           "test hook: the GPU's counter thread wedges its reader's READ queue (a never-completing packet at its "
+           "head) on its next tick; the circuit breaker must recover by recreating the queue")
       .def_property_readonly("pmc_enabled", &PyExporter::pmc_enabled)
       .def("set_sample_rate", &PyExporter::set_sample_rate, py::arg("hz"),
            "Change the sampler tick rate in place (threads restart; integrals continue)")

@@ -123,8 +123,8 @@ Exporter::~Exporter() {
 }
 
 bool Exporter::init() {
-  if (cfg_.sm_util_source != "pmfw" && cfg_.sm_util_source != "counters") {
-    err_ = "unknown sm_util_source '" + cfg_.sm_util_source + "' (pmfw | counters)";
+  if (cfg_.sm_util_source != "auto" && cfg_.sm_util_source != "pmfw" && cfg_.sm_util_source != "counters") {
+    err_ = "unknown sm_util_source '" + cfg_.sm_util_source + "' (auto | pmfw | counters)";
     return false;
   }
   if (cfg_.backend == "mock") {
@@ -240,6 +240,7 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
     x.base_busy_s = kept ? kept->base_busy_s : I.gfx_busy_seconds;
     x.base_mfma_s = kept ? kept->base_mfma_s : I.mfma_busy_seconds;
     x.base_active_s = kept ? kept->base_active_s : I.active_seconds;
+    x.base_util_s = kept ? kept->base_util_s : I.util_seconds;
     x.base_energy_j = kept ? kept->base_energy_j : I.energy_joules;
     x.base_cu_s = kept ? kept->base_cu_s : (sampler_ ? sampler_->pod_cu_seconds(dev, x.ns + "/" + x.pod) : 0.0);
   }

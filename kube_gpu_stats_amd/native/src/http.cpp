@@ -372,6 +372,16 @@ void HttpServer::loop() {
             respond(c, 400, "Bad Request", "text/plain", "hz must be within (0, 100000]\n");
           else
             respond(c, 200, "OK", "application/json", "{\"hz\":" + std::to_string(ex_->sample_rate()) + "}");
+        } else if (ex_->config().control_http && target == "/control/pmc/stall") {
+          // Benchmarks / hardware tests only: wedge one GPU's counter READ queue (a
+          // never-completing packet at its head) so the circuit breaker must trip and
+          // recreate the queue (Sampler::inject_pmc_stall).
+          const int gpu = query_int(query, "gpu", -1);
+          Sampler* s = ex_->sampler();
+          if (!s || gpu < 0 || gpu >= s->device_count() || !s->inject_pmc_stall(gpu))
+            respond(c, 400, "Bad Request", "text/plain", "gpu out of range or no counter tier\n");
+          else
+            respond(c, 200, "OK", "application/json", "{\"gpu\":" + std::to_string(gpu) + ",\"stall\":true}");
         } else if (ex_->config().control_http && target == "/control/mock/xgmi") {
           // Benchmarks on the mock provider (bench.py --mock phase X): account a peer copy
           // on the xGMI link between two mock GPUs.  Other backends: 404.

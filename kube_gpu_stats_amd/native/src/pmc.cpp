@@ -94,6 +94,7 @@ class MockCounterSource final : public CounterSource {
   int acquire(int dev) override {  // like a re-START: the counts restart at 0
     if (dev < 0 || static_cast<size_t>(dev) >= restart_.size()) return -1;
     if (dev == c_.acquire_fail_dev && hung(dev)) return -1;
+    if (fault_[static_cast<size_t>(dev)]->stalled.load()) return -1;  // START waits behind the stall too
     restart_[static_cast<size_t>(dev)] = mono_ns();
     delayed_[static_cast<size_t>(dev)].clear();
     return 0;
@@ -103,6 +104,12 @@ class MockCounterSource final : public CounterSource {
     Fault& f = *fault_[static_cast<size_t>(dev)];
     f.resets.fetch_add(1);
     if (c_.hang_heals_on_reset && dev == c_.hang_dev) f.healed.store(1);
+    f.stalled.store(0);  // a fresh queue: the injected stall is gone with the old one
+    return 0;
+  }
+  int inject_stall(int dev) override {
+    if (dev < 0 || static_cast<size_t>(dev) >= fault_.size()) return -1;
+    fault_[static_cast<size_t>(dev)]->stalled.store(1);
     return 0;
   }
   void cancel(int dev, bool on) override {
@@ -123,6 +130,7 @@ class MockCounterSource final : public CounterSource {
     if (dev >= 0 && static_cast<size_t>(dev) < fault_.size()) {
       Fault& f = *fault_[static_cast<size_t>(dev)];
       if (dev == c_.slow_dev && c_.slow_s > 0 && wait_cancel(f, c_.slow_s)) return -3;
+      if (f.stalled.load()) return wait_cancel(f, c_.hang_timeout_s) ? -3 : -2;  // the reader's deadline
       const uint64_t n = f.samples.fetch_add(1) + 1;
       if (dev == c_.hang_dev && !f.healed.load() && n > c_.hang_after) {
         if (c_.hang_timeout_s < 0)
@@ -190,6 +198,7 @@ class MockCounterSource final : public CounterSource {
     std::atomic<uint64_t> samples{0}, resets{0};
     std::atomic<int> healed{0};
     std::atomic<int> cancelled{0};
+    std::atomic<int> stalled{0};  // inject_stall: every sample times out until reset()
   };
   bool hung(int dev) const {
     const Fault& f = *fault_[static_cast<size_t>(dev)];
@@ -227,6 +236,7 @@ using info_fn = int (*)(int, char*, int);
 using abort_fn = int (*)(int, int);
 using reset_fn = int (*)(int);
 using stats_fn = int (*)(int, uint64_t*, int);
+using stall_fn = int (*)(int);
 
 class DlCounterSource final : public CounterSource {
  public:
@@ -264,6 +274,7 @@ class DlCounterSource final : public CounterSource {
     abort_ = reinterpret_cast<abort_fn>(dlsym(lib_, "kgs_pmc_abort"));  // optional (aqlprofile reader)
     reset_ = reinterpret_cast<reset_fn>(dlsym(lib_, "kgs_pmc_reset"));  // optional
     stats_ = reinterpret_cast<stats_fn>(dlsym(lib_, "kgs_pmc_stats"));  // optional
+    stall_ = reinterpret_cast<stall_fn>(dlsym(lib_, "kgs_pmc_inject_stall"));  // optional (test hook)
     char ebuf[512] = {};
     if (init(ebuf, sizeof ebuf) != 0) {
       err = std::string("kgs_pmc_init: ") + ebuf;
@@ -351,6 +362,11 @@ class DlCounterSource final : public CounterSource {
   uint64_t resets(int dev) const override {
     return dev >= 0 && dev < static_cast<int>(resets_.size()) ? resets_[static_cast<size_t>(dev)].load() : 0;
   }
+  int inject_stall(int dev) override {
+    if (!stall_ || dev < 0 || dev >= static_cast<int>(handles_.size())) return -1;
+    const int h = handles_[static_cast<size_t>(dev)];
+    return h >= 0 ? stall_(h) : -1;
+  }
   // By agent, not by session handle: the totals survive hand-overs and resets.
   bool publish_stats(int dev, PublishStats& out) const override {
     if (!stats_ || dev < 0 || dev >= static_cast<int>(agent_.size())) return false;
@@ -423,6 +439,7 @@ class DlCounterSource final : public CounterSource {
   abort_fn abort_ = nullptr;
   reset_fn reset_ = nullptr;
   stats_fn stats_ = nullptr;
+  stall_fn stall_ = nullptr;
   std::vector<std::atomic<int>> agent_;  // per device: reader agent index once opened (-1 never)
   std::vector<std::atomic<uint64_t>> resets_;
   // Written by the device's sampler thread (release / acquire), read by info()

@@ -192,8 +192,9 @@ void Exporter::render(std::string& out) {
     Integrals I;
     PmcSample p;
     PmcRates r;
-    double g = 0, u = 0;
+    double g = 0, u = 0, util = 0;
     int n = 0;
+    bool procs_fresh = false, links_fresh = false, health_fresh = false;
   };
   static thread_local std::vector<Snap> snaps;
   snaps.assign(static_cast<size_t>(nd), Snap{});
@@ -208,7 +209,16 @@ void Exporter::render(std::string& out) {
     // no busy gauges rather than its last value frozen; the counters stay.
     const int64_t ok_ns = st.last_ok_mono_ns.load(std::memory_order_relaxed);
     const bool pmfw_fresh = st.up.load(std::memory_order_relaxed) && ok_ns > 0 && now - ok_ns <= stale_ns;
-    x.busy = x.have && pmfw_fresh && S.window_busy(d, cfg_.window_s, x.g, x.u, x.n);
+    x.busy = x.have && pmfw_fresh && S.window_busy(d, cfg_.window_s, x.g, x.u, x.n, &x.util);
+    // Slow tiers (per-device kgs-slow threads): a result older than stale_s — or
+    // than three of its tier's periods, if longer — is not exported as current.
+    auto fresh = [&](const std::atomic<int64_t>& ok, int64_t period) {
+      const int64_t t = ok.load(std::memory_order_acquire);
+      return t > 0 && now - t <= std::max(stale_ns, 3 * period);
+    };
+    x.procs_fresh = fresh(st.procs_ok_ns, S.proc_period_ns());
+    x.links_fresh = fresh(st.links_ok_ns, S.link_period_ns());
+    x.health_fresh = fresh(st.health_ok_ns, S.link_period_ns());
     x.pmc_have = st.pmc_latest.load(x.p);
     // Counter rates only while we hold the counters and drains keep arriving:
     // handed over (pmc_on = 0), stalled (a foreign profiler STOPped /
@@ -252,7 +262,16 @@ void Exporter::render(std::string& out) {
       }
     }
     const bool from_counters = cfg_.sm_util_source == "counters";
-    if (from_counters) {
+    const bool from_auto = cfg_.sm_util_source == "auto";
+    if (from_auto) {
+      w.head("container_gpu_sm_util", "gauge",
+             "Busy percent of the GPU allocated to the pod over the exporter window, not counting the exporter's own "
+             "counter READs: hardware-counter GPU-active (GRBM_SPI_BUSY) while the counter tier runs, PMFW GFX busy "
+             "otherwise (reference metric contract; label nvidia_gpu_type kept for compatibility)");
+      for (const auto& [d, lb] : pod_lines)
+        if (snaps[static_cast<size_t>(d)].busy)
+          w.line("container_gpu_sm_util", lb, nullptr, std::clamp(snaps[static_cast<size_t>(d)].util, 0.0, 100.0));
+    } else if (from_counters) {
       w.head("container_gpu_sm_util", "gauge",
              "GPU-active percent (GRBM_SPI_BUSY: a shader engine has waves) of the GPU allocated to the pod, averaged "
              "over the exporter window (reference metric contract; --sm-util-source counters)");
@@ -271,7 +290,10 @@ void Exporter::render(std::string& out) {
     // it.  rate() / increase() over any range is the exact mean utilisation,
     // whatever the scrape interval — the gauge above only sees its window.
     w.head("container_gpu_busy_seconds_total", "counter",
-           from_counters ? "GPU-active seconds (GRBM_SPI_BUSY) of the GPU allocated to the pod, counted from allocation "
+           from_auto ? "Busy seconds of the GPU allocated to the pod, counted from allocation, not counting the exporter's "
+                       "own counter READs (hardware-counter GPU-active while the counter tier runs, PMFW GFX busy "
+                       "otherwise; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)"
+           : from_counters ? "GPU-active seconds (GRBM_SPI_BUSY) of the GPU allocated to the pod, counted from allocation "
                            "(hardware counters; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)"
                          : "GFX-engine busy seconds of the GPU allocated to the pod, counted from allocation (PMFW "
                            "accumulators; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)");
@@ -279,8 +301,9 @@ void Exporter::render(std::string& out) {
       const Owner* o = pod_owner[i];
       const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
       if (from_counters && !x.pmc_have) continue;
-      const double v = from_counters ? x.I.active_seconds - (o ? o->base_active_s : 0.0)
-                                     : x.I.gfx_busy_seconds - (o ? o->base_busy_s : 0.0);
+      const double v = from_auto       ? x.I.util_seconds - (o ? o->base_util_s : 0.0)
+                       : from_counters ? x.I.active_seconds - (o ? o->base_active_s : 0.0)
+                                       : x.I.gfx_busy_seconds - (o ? o->base_busy_s : 0.0);
       w.line("container_gpu_busy_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
     }
     // Per-pod compute share: the CU-occupancy seconds of the pod's
@@ -410,8 +433,20 @@ void Exporter::render(std::string& out) {
   w.put(*sblock);
 
   // ---- utilisation -------------------------------------------------------
-  w.head("amdgpu_gfx_busy_percent", "gauge", "GFX-engine busy percent, time-weighted mean over the exporter window (PMFW accumulators)");
-  for (int d : ids) if (snaps[d].busy) w.line("amdgpu_gfx_busy_percent", dev_labels_[d], nullptr, snaps[d].g);
+  // amdgpu_gfx_busy_*: the same busy signal as container_gpu_sm_util (--sm-util-source;
+  // default auto: READ-immune); amdgpu_pmfw_gfx_busy_* is always the firmware's own.
+  const bool util_auto = cfg_.sm_util_source == "auto";
+  w.head("amdgpu_gfx_busy_percent", "gauge",
+         util_auto ? "GPU busy percent over the exporter window, not counting the exporter's own counter READs "
+                     "(hardware-counter GPU-active while the counter tier runs, PMFW GFX busy otherwise)"
+                   : "GFX-engine busy percent, time-weighted mean over the exporter window (PMFW accumulators)");
+  for (int d : ids)
+    if (snaps[d].busy)
+      w.line("amdgpu_gfx_busy_percent", dev_labels_[d], nullptr, util_auto ? std::clamp(snaps[d].util, 0.0, 100.0) : snaps[d].g);
+  w.head("amdgpu_pmfw_gfx_busy_percent", "gauge",
+         "Firmware (PMFW) GFX busy percent over the exporter window: a dispatch in flight, and each counter READ "
+         "packet of the exporter as ~80 us of work");
+  for (int d : ids) if (snaps[d].busy) w.line("amdgpu_pmfw_gfx_busy_percent", dev_labels_[d], nullptr, snaps[d].g);
   w.head("amdgpu_gfx_busy_instant_percent", "gauge", "GFX-engine busy percent in the latest PMFW table");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFGfxBusy)) w.line("amdgpu_gfx_busy_instant_percent", dev_labels_[d], nullptr, snaps[d].s.gfx_busy_pct);
   w.head("amdgpu_gfx_busy_xcc_percent", "gauge",
@@ -426,8 +461,25 @@ void Exporter::render(std::string& out) {
   }
   w.head("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller (UMC) activity percent, mean over the exporter window");
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_umc_busy_percent", dev_labels_[d], nullptr, snaps[d].u);
-  w.head("amdgpu_gfx_busy_seconds_total", "counter", "Integral of GFX busy fraction over firmware time; rate() gives exact mean utilisation");
-  for (int d : ids) if (snaps[d].have) w.line("amdgpu_gfx_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.gfx_busy_seconds);
+  w.head("amdgpu_gfx_busy_seconds_total", "counter",
+         util_auto ? "Integral of the GPU busy fraction (amdgpu_gfx_busy_percent's source) over firmware time; rate() "
+                     "gives exact mean utilisation"
+                   : "Integral of GFX busy fraction over firmware time; rate() gives exact mean utilisation");
+  for (int d : ids)
+    if (snaps[d].have)
+      w.line("amdgpu_gfx_busy_seconds_total", dev_labels_[d], nullptr, util_auto ? snaps[d].I.util_seconds : snaps[d].I.gfx_busy_seconds);
+  w.head("amdgpu_pmfw_gfx_busy_seconds_total", "counter",
+         "Integral of the firmware (PMFW) GFX busy fraction over firmware time (counts counter READs as work)");
+  for (int d : ids) if (snaps[d].have) w.line("amdgpu_pmfw_gfx_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.gfx_busy_seconds);
+  w.head("kgs_util_source_seconds_total", "counter",
+         "Firmware time the READ-immune busy integral (amdgpu_gfx_busy_seconds_total under --sm-util-source auto) "
+         "took from each source: counters (GRBM_SPI_BUSY) or pmfw (counter tier off, handed over, failed or stale)");
+  for (int d : ids) {
+    if (!snaps[d].have) continue;
+    w.line("kgs_util_source_seconds_total", dev_labels_[d], "source=\"counters\"", snaps[d].I.util_counter_seconds);
+    w.line("kgs_util_source_seconds_total", dev_labels_[d], "source=\"pmfw\"",
+           std::max(0.0, snaps[d].I.sampled_seconds - snaps[d].I.util_counter_seconds));
+  }
   w.head("amdgpu_umc_busy_seconds_total", "counter", "Integral of UMC busy fraction over firmware time");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_umc_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds);
   const double full_bw = cfg_.hbm_bytes_per_s_at_full_umc;
@@ -513,7 +565,7 @@ void Exporter::render(std::string& out) {
   w.head("amdgpu_xgmi_link_info", "gauge", "Per-link peer and speed (slow tier, value 1)");
   for (int d : ids) {
     auto links = S.state(d).get_links();
-    if (!links) continue;
+    if (!links || !snaps[d].links_fresh) continue;
     std::shared_ptr<const std::string> lblock;
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -566,7 +618,8 @@ void Exporter::render(std::string& out) {
   w.head("amdgpu_xgmi_error_status", "gauge", "xGMI error status: 0 none, 1 error, 2 multiple errors");
   for (int d : ids) {
     auto h = S.state(d).get_health();
-    if (h && h->xgmi_error_status >= 0) w.line("amdgpu_xgmi_error_status", dev_labels_[d], nullptr, h->xgmi_error_status);
+    if (h && h->xgmi_error_status >= 0 && snaps[d].health_fresh)
+      w.line("amdgpu_xgmi_error_status", dev_labels_[d], nullptr, h->xgmi_error_status);
   }
   w.head("amdgpu_pcie_bytes_total", "counter",
          "Bytes over the PCIe link (both directions), from the PMFW PCIe bandwidth accumulator times a MI355X "
@@ -649,6 +702,7 @@ void Exporter::render(std::string& out) {
     static thread_local std::vector<std::pair<int, const ProcInfo*>> plist;
     plist.clear();
     for (int d : ids) {
+      if (!snaps[d].procs_fresh) continue;  // a stuck / failing process list: no lines, not old ones
       procs[d] = S.state(d).get_procs();
       if (procs[d]) for (const ProcInfo& p : *procs[d]) plist.emplace_back(d, &p);
     }
@@ -741,6 +795,10 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_breaker_trips_total", dev_labels_[d], nullptr, S.state(d).pmc_breaker_trips.load());
     w.head("kgs_pmc_retries_total", "counter", "Reader resets + re-STARTs attempted while the breaker was open");
     for (int d : ids) w.line_u("kgs_pmc_retries_total", dev_labels_[d], nullptr, S.state(d).pmc_retries.load());
+    w.head("kgs_pmc_reordered_total", "counter",
+           "Counter drains dropped because their command-processor time preceded the previous drain's (the next "
+           "drain covers the interval; should stay 0)");
+    for (int d : ids) w.line_u("kgs_pmc_reordered_total", dev_labels_[d], nullptr, S.state(d).pmc_reordered.load());
     w.head("kgs_sampler_wake_lateness_seconds", "histogram",
            "How late the counter thread woke against each tick's absolute deadline (CPU contention, idle-state exit); "
            "a tick later than 4 periods is skipped (kgs_sampler_overruns_total)");
@@ -783,8 +841,41 @@ void Exporter::render(std::string& out) {
     w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"procs\"", st.proc_reads.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"links\"", st.link_reads.load(std::memory_order_relaxed));
   }
-  w.head("kgs_slow_read_seconds_total", "counter", "Time the node-wide slow thread spent in management-library calls");
+  w.head("kgs_slow_read_seconds_total", "counter", "Time the device's slow thread spent in management-library calls");
   for (int d : ids) w.line("kgs_slow_read_seconds_total", dev_labels_[d], nullptr, S.state(d).slow_ns_total.load(std::memory_order_relaxed) * 1e-9);
+  w.head("kgs_slow_errors_total", "counter", "Management-library reads of the device's slow thread that failed, by tier");
+  for (int d : ids) {
+    const DeviceState& st = S.state(d);
+    w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"procs\"", st.proc_errors.load(std::memory_order_relaxed));
+    w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"links\"", st.link_errors.load(std::memory_order_relaxed));
+    w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"health\"", st.health_errors.load(std::memory_order_relaxed));
+  }
+  w.head("kgs_slow_last_ok_age_seconds", "gauge",
+         "Seconds since the tier's last good management-library read on the device (-1 = never): per-process "
+         "lines, the link table and the RAS status are dropped once this passes --stale-after");
+  for (int d : ids) {
+    const DeviceState& st = S.state(d);
+    const std::atomic<int64_t>* oks[3] = {&st.procs_ok_ns, &st.links_ok_ns, &st.health_ok_ns};
+    const int64_t per[3] = {S.proc_period_ns(), S.link_period_ns(), S.link_period_ns()};
+    for (int t = 0; t < 3; ++t) {
+      if (per[t] <= 0) continue;
+      const int64_t ok = oks[t]->load(std::memory_order_acquire);
+      char tl[24];
+      std::snprintf(tl, sizeof tl, "tier=\"%s\"", slow_tier_name(t));
+      w.line("kgs_slow_last_ok_age_seconds", dev_labels_[d], tl, ok > 0 ? (now - ok) * 1e-9 : -1.0);
+    }
+  }
+  w.head("kgs_slow_call_seconds", "gauge",
+         "How long the device's slow thread has been inside its current management-library call (0 = none in "
+         "flight); a call that never returns keeps growing here");
+  for (int d : ids) {
+    const int64_t t = S.state(d).slow_call_ns.load(std::memory_order_acquire);
+    w.line("kgs_slow_call_seconds", dev_labels_[d], nullptr, t > 0 && now > t ? (now - t) * 1e-9 : 0.0);
+  }
+  w.head("kgs_slow_thread_hung", "gauge",
+         "1 if the device's slow thread was stuck in a management-library call when sampling last stopped (it was "
+         "abandoned; the slow tiers restart once the call returns)");
+  for (int d : ids) w.line_u("kgs_slow_thread_hung", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).slow_hung.load()));
   w.head("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples");
   for (int d : ids) w.line("kgs_sampled_seconds_total", dev_labels_[d], nullptr, snaps[d].I.sampled_seconds);
   w.head("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read");

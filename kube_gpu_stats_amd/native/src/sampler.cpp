@@ -111,7 +111,28 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
   cu_seconds_.resize(static_cast<size_t>(n));
   pod_cu_.resize(static_cast<size_t>(n));
   last_proc_ns_.assign(static_cast<size_t>(n), 0);
+  util_prev_.resize(static_cast<size_t>(n));
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+}
+
+bool Sampler::inject_pmc_stall(int dev) {
+  if (std::find(dev_ids_.begin(), dev_ids_.end(), dev) == dev_ids_.end() || !pmc_) return false;
+  states_[static_cast<size_t>(dev)]->pmc_stall_req.store(1);
+  return true;
+}
+
+int64_t Sampler::proc_period_ns() const {
+  const int64_t tick_ns = static_cast<int64_t>(1e9 / hz_.load());
+  return cfg_.proc_period_s > 0 ? static_cast<int64_t>(cfg_.proc_period_s * 1e9)
+         : cfg_.proc_every > 0  ? tick_ns * cfg_.proc_every
+                                : 0;
+}
+
+int64_t Sampler::link_period_ns() const {
+  const int64_t tick_ns = static_cast<int64_t>(1e9 / hz_.load());
+  return cfg_.link_period_s > 0 ? static_cast<int64_t>(cfg_.link_period_s * 1e9)
+         : cfg_.link_every > 0  ? tick_ns * cfg_.link_every
+                                : 0;
 }
 
 bool Sampler::set_hz(double hz) {
@@ -216,10 +237,14 @@ void Sampler::start_locked() {
       }
     }
     st.thread_hung.store(hung ? 1 : 0);
+    // One slow thread per device (sampler.h): a management-library call stuck on
+    // one GPU leaves the others' per-process / link / RAS tiers running.
+    if (proc_period_ns() > 0 || link_period_ns() > 0) {
+      const bool slow_stuck = stuck(d, kSlow);
+      if (!slow_stuck) spawn(d, kSlow);
+      st.slow_hung.store(slow_stuck ? 1 : 0);
+    }
   }
-  if ((cfg_.proc_every > 0 || cfg_.link_every > 0 || cfg_.proc_period_s > 0 || cfg_.link_period_s > 0) &&
-      !stuck(-1, kSlow))
-    spawn(-1, kSlow);
 }
 
 void Sampler::stop_locked() {
@@ -247,7 +272,8 @@ void Sampler::stop_locked() {
     // every such call and exits without touching this sampler.
     w->abandoned.store(true, std::memory_order_release);
     w->t.detach();
-    if (w->dev >= 0) states_[static_cast<size_t>(w->dev)]->thread_hung.store(1);
+    if (w->dev >= 0) (w->kind == kSlow ? states_[static_cast<size_t>(w->dev)]->slow_hung
+                                       : states_[static_cast<size_t>(w->dev)]->thread_hung).store(1);
     abandoned_total_.fetch_add(1);
     abandoned_.push_back(w);
   }
@@ -345,6 +371,46 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
     }
 }
 
+// ---- READ-immune busy integral (--sm-util-source auto) ------------------------
+// Per distinct PMFW interval (dt of firmware time, dgfx_s of PMFW GFX busy in it):
+// while the device's counter tier ran through the whole interval — same epoch as at
+// the previous PMFW sample, counters held and not stalled, a drain no older than
+// three of its slowest READ periods — the interval is billed the counter tier's
+// Δactive_seconds (GRBM_SPI_BUSY: waves in a shader engine, blind to the exporter's
+// own READ packets), else the PMFW GFX busy (a dispatch in flight; counts each READ
+// as ≈80 µs of work, profiles/r2/idle_busy/).  Either way the integral is exact
+// over any range covered by one source, and monotonic.
+void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, Integrals& I, GpuSample& s) {
+  DeviceState& st = *states_[static_cast<size_t>(dev)];
+  UtilPrev& up = util_prev_[static_cast<size_t>(dev)];
+  Integrals pc;
+  st.pmc_integ.load(pc);
+  double slow_hz = hz_.load(std::memory_order_relaxed);
+  const double idle = pmc_idle_hz_.load(std::memory_order_relaxed);
+  if (idle > 0) slow_hz = std::min(slow_hz, idle);
+  if (pmc_busy_min_.load(std::memory_order_relaxed) > 0 && idle > 0)
+    slow_hz = std::min(slow_hz, pmc_gap_hz_.load(std::memory_order_relaxed));
+  const int64_t fresh_ns = static_cast<int64_t>(3e9 / slow_hz) + 50000000LL;
+  const bool ok = st.pmc_on.load(std::memory_order_relaxed) && !st.pmc_stalled.load(std::memory_order_relaxed) &&
+                  !st.pmc_failed.load(std::memory_order_relaxed) && pc.pmc_last_ns > 0 &&
+                  now - pc.pmc_last_ns <= fresh_ns;
+  double du = 0;
+  if (dt_s > 0) {
+    if (ok && up.have && up.epoch == pc.pmc_epoch && pc.active_seconds >= up.active_s) {
+      du = std::min(pc.active_seconds - up.active_s, dt_s);
+      I.util_counter_seconds += dt_s;
+    } else {
+      du = std::clamp(dgfx_s, 0.0, dt_s);
+    }
+  }
+  I.util_seconds += du;
+  up.have = ok;
+  up.epoch = pc.pmc_epoch;
+  up.active_s = pc.active_seconds;
+  s.cum_util_s = I.util_seconds;
+  s.util_window_pct = dt_s > 0 ? static_cast<float>(100.0 * du / dt_s) : -1.0f;
+}
+
 // ---- PMFW tier: the firmware metrics table + HBM occupancy --------------------
 // At min(hz, pmfw_hz): the table refreshes every ≈20 ms, so reading it faster
 // only re-reads the same table.  A failing device backs off; every 4th failure
@@ -391,7 +457,9 @@ void Sampler::run_pmfw(Worker& w) {
       // accumulator restarted too — re-baseline instead of reading a wrap.
       const bool reset = have_prev && (s.valid & kFFwTs) && (prev.valid & kFFwTs) && s.fw_ts < prev.fw_ts;
       if (distinct) {
+        const double g0 = I.gfx_busy_seconds, d0 = I.sampled_seconds;
         integrate(dev, have_prev && !reset ? &prev : nullptr, s, I);
+        run_pmfw_util(dev, t1, I.gfx_busy_seconds - g0, I.sampled_seconds - d0, I, s);
         s.cum_gfx_s = I.gfx_busy_seconds;
         s.cum_umc_s = I.umc_busy_seconds;
         s.cum_dt_s = I.sampled_seconds;
@@ -512,6 +580,7 @@ void Sampler::run_pmc(Worker& w) {
   };
   // Open the breaker: stop READing this device, retry after the backoff.
   auto trip = [&](int64_t now) {
+    ++P.pmc_epoch;  // the counter integral stops here: the READ-immune util falls back to PMFW
     st.pmc_failed.store(1);
     st.pmc_breaker_trips.fetch_add(1, std::memory_order_relaxed);
     carry_base();
@@ -529,7 +598,12 @@ void Sampler::run_pmc(Worker& w) {
   while (!stop_.load(std::memory_order_relaxed)) {
     const int want = st.pmc_want.load(std::memory_order_relaxed);
     // ---- hand-over: release on request ----------------------------------------
+    if (st.pmc_stall_req.exchange(0, std::memory_order_relaxed) && st.pmc_on.load(std::memory_order_relaxed)) {
+      if (src->inject_stall(dev) == 0) st.pmc_stalls_injected.fetch_add(1, std::memory_order_relaxed);
+      if (gone()) return;
+    }
     if (!want && st.pmc_on.load(std::memory_order_relaxed)) {
+      ++P.pmc_epoch;
       src->release(dev);  // a failed STOP still ends our READs
       if (gone()) return;
       st.pmc_on.store(0);
@@ -551,6 +625,7 @@ void Sampler::run_pmc(Worker& w) {
       if (gone()) return;
       const int64_t now_c = mono_ns();
       if (rc == 0) {
+        ++P.pmc_epoch;
         st.pmc_on.store(1);
         started_at(now_c);  // the breaker closes on the first good drain
       } else {
@@ -581,7 +656,12 @@ void Sampler::run_pmc(Worker& w) {
       const int prc = src->sample(dev, ps);
       if (gone()) return;
       P.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
-      if (prc == 0) {
+      if (prc == 0 && have_prev_ps && ps.mono_ns < prev_ps_ns) {
+        // A drain stamped before the previous one: folding it would
+        // run the published totals and integrals backwards.  The counts are
+        // cumulative, so the next drain covers the interval; drop this one.
+        st.pmc_reordered.fetch_add(1, std::memory_order_relaxed);
+      } else if (prc == 0) {
         st.pmc_fail_streak = 0;
         if (st.pmc_failed.load(std::memory_order_relaxed)) {  // a retry worked: close the breaker
           st.pmc_failed.store(0);
@@ -669,6 +749,7 @@ void Sampler::run_pmc(Worker& w) {
         }
         st.pmc_latest.store(ps);
         ++P.pmc_samples;
+        P.pmc_last_ns = ps.mono_ns;
         const bool reclaim = cfg_.pmc_reclaim_s > 0 && stall >= static_cast<int64_t>(cfg_.pmc_reclaim_s * 1e9);
         const bool refresh = cfg_.pmc_refresh_s > 0 &&
                              ps.mono_ns - last_start_ns >= static_cast<int64_t>(cfg_.pmc_refresh_s * 1e9);
@@ -685,6 +766,7 @@ void Sampler::run_pmc(Worker& w) {
             (reclaim ? st.pmc_reclaims : st.pmc_refreshes).fetch_add(1, std::memory_order_relaxed);
             started_at(t);
           } else {
+            ++P.pmc_epoch;
             st.pmc_on.store(0);
             st.pmc_retry_at_ns = t + 1000000000LL;
             ++P.pmc_errors;
@@ -741,20 +823,31 @@ void Sampler::run_pmc(Worker& w) {
   st.pmc_integ.store(P);
 }
 
-// Node-wide management-library tiers (see sampler.h).  Each due device is read
-// in turn; the per-GPU threads never wait on these calls.
+// Management-library tiers of one device (see sampler.h): its per-process list
+// and its link table + RAS health, on its own "kgs-slow<N>" thread.  A call that
+// never returns stalls this device's slow tiers only; their results go stale
+// (the renderer drops them after stale_after) and stop() abandons the thread.
 void Sampler::run_slow(Worker& w) {
-  pthread_setname_np(pthread_self(), "kgs-slow");
-  const int64_t tick_ns = static_cast<int64_t>(1e9 / hz_.load());
-  const int64_t proc_ns = cfg_.proc_period_s > 0 ? static_cast<int64_t>(cfg_.proc_period_s * 1e9)
-                        : cfg_.proc_every > 0   ? tick_ns * cfg_.proc_every
-                                                : 0;
-  const int64_t link_ns = cfg_.link_period_s > 0 ? static_cast<int64_t>(cfg_.link_period_s * 1e9)
-                        : cfg_.link_every > 0   ? tick_ns * cfg_.link_every
-                                                : 0;
+  const int dev = w.dev;
+  DeviceState& st = *states_[static_cast<size_t>(dev)];
+  char tname[16];
+  std::snprintf(tname, sizeof tname, "kgs-slow%d", dev);
+  pthread_setname_np(pthread_self(), tname);
+  const int64_t proc_ns = proc_period_ns(), link_ns = link_period_ns();
   Backend* const be = be_;
   auto gone = [&w] { return w.abandoned.load(std::memory_order_acquire); };
-  int64_t next_proc = mono_ns(), next_link = next_proc;
+  // Bracket one management-library call: kgs_slow_call_seconds shows it while in flight.
+  auto begin = [&](int tier) {
+    st.slow_call_tier.store(tier, std::memory_order_relaxed);
+    st.slow_call_ns.store(mono_ns(), std::memory_order_release);
+  };
+  auto end = [&] { st.slow_call_ns.store(0, std::memory_order_release); };
+  // Stagger the devices' first passes over one period: with AMD SMI serialising
+  // callers, N threads waking together would queue behind each other every pass.
+  const int n_dev = std::max<int>(1, static_cast<int>(dev_ids_.size()));
+  const int pos = static_cast<int>(std::find(dev_ids_.begin(), dev_ids_.end(), dev) - dev_ids_.begin());
+  int64_t next_proc = mono_ns() + (proc_ns > 0 ? proc_ns / n_dev * pos : 0);
+  int64_t next_link = mono_ns() + (link_ns > 0 ? link_ns / n_dev * pos : 0);
   std::vector<ProcInfo> procs;
   std::vector<LinkInfo> links;
   while (!stop_.load(std::memory_order_relaxed)) {
@@ -765,84 +858,93 @@ void Sampler::run_slow(Worker& w) {
         std::lock_guard<std::mutex> g(pid_pods_mu_);
         pid_pods = pid_pods_;
       }
-      for (int dev : dev_ids_) {
-        if (stop_.load(std::memory_order_relaxed)) break;
-        DeviceState& st = *states_[static_cast<size_t>(dev)];
-        const int64_t a = mono_ns();
-        const int rc = be->read_procs(dev, procs);
-        if (gone()) return;
-        if (rc == 0) {
-          const int64_t now_p = mono_ns();
-          int64_t& last = last_proc_ns_[static_cast<size_t>(dev)];
-          const double dt = last ? (now_p - last) * 1e-9 : 0.0;
-          const int cu = be->info(dev).num_cu;
-          const double ncu = cu > 0 ? cu : 256.0;
-          auto& cs = cu_seconds_[static_cast<size_t>(dev)];  // (pid, ∫ occupancy share dt), sorted by pid
-          auto& pods = pod_cu_[static_cast<size_t>(dev)];
-          bool pods_changed = false;
-          std::vector<std::pair<uint32_t, double>> next_cs;
-          next_cs.reserve(procs.size());
-          for (ProcInfo& p : procs) {
-            auto it = std::lower_bound(cs.begin(), cs.end(), std::make_pair(p.pid, -1.0));
-            const bool known = it != cs.end() && it->first == p.pid;
-            const double inc = known ? p.cu_occupancy / ncu * dt : 0.0;
-            p.cu_seconds = known ? it->second + inc : 0.0;
-            next_cs.emplace_back(p.pid, p.cu_seconds);
-            // The pod's integral keeps what its processes ran after they exit: the
-            // per-pod compute share a shared GPU is billed by.
-            if (pid_pods) {
-              auto po = pid_pods->find((static_cast<uint64_t>(static_cast<uint32_t>(dev)) << 32) | p.pid);
-              if (po != pid_pods->end()) {
-                double& v = pods[po->second];
-                if (inc > 0 || v == 0) pods_changed = true;
-                v += inc;
-              }
+      const int64_t a = mono_ns();
+      begin(kSlowProcs);
+      const int rc = be->read_procs(dev, procs);
+      end();
+      if (gone()) return;
+      if (rc == 0) {
+        const int64_t now_p = mono_ns();
+        int64_t& last = last_proc_ns_[static_cast<size_t>(dev)];
+        const double dt = last ? (now_p - last) * 1e-9 : 0.0;
+        const int cu = be->info(dev).num_cu;
+        const double ncu = cu > 0 ? cu : 256.0;
+        auto& cs = cu_seconds_[static_cast<size_t>(dev)];  // (pid, ∫ occupancy share dt), sorted by pid
+        auto& pods = pod_cu_[static_cast<size_t>(dev)];
+        bool pods_changed = false;
+        std::vector<std::pair<uint32_t, double>> next_cs;
+        next_cs.reserve(procs.size());
+        for (ProcInfo& p : procs) {
+          auto it = std::lower_bound(cs.begin(), cs.end(), std::make_pair(p.pid, -1.0));
+          const bool known = it != cs.end() && it->first == p.pid;
+          const double inc = known ? p.cu_occupancy / ncu * dt : 0.0;
+          p.cu_seconds = known ? it->second + inc : 0.0;
+          next_cs.emplace_back(p.pid, p.cu_seconds);
+          // The pod's integral keeps what its processes ran after they exit: the
+          // per-pod compute share a shared GPU is billed by.
+          if (pid_pods) {
+            auto po = pid_pods->find((static_cast<uint64_t>(static_cast<uint32_t>(dev)) << 32) | p.pid);
+            if (po != pid_pods->end()) {
+              double& v = pods[po->second];
+              if (inc > 0 || v == 0) pods_changed = true;
+              v += inc;
             }
           }
-          std::sort(next_cs.begin(), next_cs.end());
-          cs.swap(next_cs);  // processes that exited drop out
-          last = now_p;
-          auto sp = std::make_shared<const std::vector<ProcInfo>>(procs);
-          std::shared_ptr<const std::map<std::string, double>> pc;
-          if (pods_changed) pc = std::make_shared<const std::map<std::string, double>>(pods);
-          {
-            std::lock_guard<std::mutex> g(st.slow_mu);
-            st.procs = std::move(sp);
-            st.procs_mono_ns = now_p;
-            if (pc) st.pod_cu = std::move(pc);
-          }
-          st.proc_reads.fetch_add(1, std::memory_order_relaxed);
-        } else {
-          st.proc_errors.fetch_add(1, std::memory_order_relaxed);
         }
-        st.slow_ns_total.fetch_add(static_cast<uint64_t>(mono_ns() - a), std::memory_order_relaxed);
+        std::sort(next_cs.begin(), next_cs.end());
+        cs.swap(next_cs);  // processes that exited drop out
+        last = now_p;
+        auto sp = std::make_shared<const std::vector<ProcInfo>>(procs);
+        std::shared_ptr<const std::map<std::string, double>> pc;
+        if (pods_changed) pc = std::make_shared<const std::map<std::string, double>>(pods);
+        {
+          std::lock_guard<std::mutex> g(st.slow_mu);
+          st.procs = std::move(sp);
+          st.procs_mono_ns = now_p;
+          if (pc) st.pod_cu = std::move(pc);
+        }
+        st.procs_ok_ns.store(now_p, std::memory_order_release);
+        st.proc_reads.fetch_add(1, std::memory_order_relaxed);
+      } else {
+        st.proc_errors.fetch_add(1, std::memory_order_relaxed);
       }
+      st.slow_ns_total.fetch_add(static_cast<uint64_t>(mono_ns() - a), std::memory_order_relaxed);
       next_proc += proc_ns;
       if (next_proc <= mono_ns()) next_proc = mono_ns() + proc_ns;  // a pass overran: skip, do not burst
     }
-    if (link_ns > 0 && mono_ns() >= next_link) {
-      for (int dev : dev_ids_) {
-        if (stop_.load(std::memory_order_relaxed)) break;
-        DeviceState& st = *states_[static_cast<size_t>(dev)];
-        const int64_t a = mono_ns();
-        const int lrc = be->read_links(dev, links);
-        if (gone()) return;
-        if (lrc == 0) {
-          auto l = std::make_shared<const std::vector<LinkInfo>>(links);
+    if (link_ns > 0 && mono_ns() >= next_link && !stop_.load(std::memory_order_relaxed)) {
+      const int64_t a = mono_ns();
+      begin(kSlowLinks);
+      const int lrc = be->read_links(dev, links);
+      end();
+      if (gone()) return;
+      if (lrc == 0) {
+        auto l = std::make_shared<const std::vector<LinkInfo>>(links);
+        {
           std::lock_guard<std::mutex> g(st.slow_mu);
           st.links = std::move(l);
         }
-        HealthInfo h;
-        const int hrc = be->read_health(dev, h);
-        if (gone()) return;
-        if (hrc == 0) {
-          auto hp = std::make_shared<const HealthInfo>(h);
+        st.links_ok_ns.store(mono_ns(), std::memory_order_release);
+      } else {
+        st.link_errors.fetch_add(1, std::memory_order_relaxed);
+      }
+      HealthInfo h;
+      begin(kSlowHealth);
+      const int hrc = be->read_health(dev, h);
+      end();
+      if (gone()) return;
+      if (hrc == 0) {
+        auto hp = std::make_shared<const HealthInfo>(h);
+        {
           std::lock_guard<std::mutex> g(st.slow_mu);
           st.health = std::move(hp);
         }
-        st.link_reads.fetch_add(1, std::memory_order_relaxed);
-        st.slow_ns_total.fetch_add(static_cast<uint64_t>(mono_ns() - a), std::memory_order_relaxed);
+        st.health_ok_ns.store(mono_ns(), std::memory_order_release);
+      } else {
+        st.health_errors.fetch_add(1, std::memory_order_relaxed);
       }
+      st.link_reads.fetch_add(1, std::memory_order_relaxed);
+      st.slow_ns_total.fetch_add(static_cast<uint64_t>(mono_ns() - a), std::memory_order_relaxed);
       next_link += link_ns;
       if (next_link <= mono_ns()) next_link = mono_ns() + link_ns;
     }
@@ -859,7 +961,7 @@ void Sampler::run_slow(Worker& w) {
   }
 }
 
-bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, int& n) const {
+bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, int& n, double* util) const {
   const DeviceState& st = *states_[dev];
   n = 0;
   GpuSample b, a, e;
@@ -892,6 +994,7 @@ bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, in
       const double dt = b.cum_dt_s - a.cum_dt_s;
       gfx = 100.0 * (b.cum_gfx_s - a.cum_gfx_s) / dt;
       umc = 100.0 * (b.cum_umc_s - a.cum_umc_s) / dt;
+      if (util) *util = 100.0 * (b.cum_util_s - a.cum_util_s) / dt;
       n = static_cast<int>(b.seq - a.seq);
       return true;
     }
@@ -900,6 +1003,7 @@ bool Sampler::window_busy(int dev, double window_s, double& gfx, double& umc, in
   if (!st.latest.load(s)) return false;
   gfx = s.gfx_busy_pct;
   umc = s.umc_busy_pct;
+  if (util) *util = s.util_window_pct >= 0 ? s.util_window_pct : s.gfx_busy_pct;
   n = 1;
   return true;
 }

@@ -762,6 +762,43 @@ static void test_batch_plan() {
       CHECK(t - first < 1000000);  // a non-publisher is only submitted while the half is young
     }
   }
+  // Collection order: the CP delays half A's publisher past the time
+  // half B closes, so both halves are closed when the sampler comes back.  The
+  // half the next READ reuses (A) is the older one and must be folded first, even
+  // when B's publisher is already done; folding B first would hand out samples
+  // whose time and cumulative counts go backwards.
+  p.configure(2, 0);
+  int hv[2];
+  bool wv[2];
+  CHECK(p.collect_order(true, hv, wv) == 0);  // nothing closed: nothing to fold
+  CHECK(submit(125000) == 0 && submit(125000) == 1 && p.closed(0) && p.current_half() == 1);
+  CHECK(p.collect_order(false, hv, wv) == 0);  // A closed, its publisher not done: keep filling B
+  CHECK(p.collect_order(true, hv, wv) == 1 && hv[0] == 0 && !wv[0]);  // the usual case: fold A, no wait
+  CHECK(submit(125000) == 2 && submit(125000) == 3 && p.closed(1) && p.current_half() == 0);
+  CHECK(p.collect_order(true, hv, wv) == 2 && hv[0] == 0 && wv[0] && hv[1] == 1 && !wv[1]);
+  CHECK(p.collect_order(false, hv, wv) == 1 && hv[0] == 0 && wv[0]);  // B still running: A only
+  p.collected(0);
+  CHECK(p.collect_order(true, hv, wv) == 1 && hv[0] == 1 && !wv[0]);
+  // A whole rotation driven through collect_order never folds a newer half first.
+  p.configure(3, 0);
+  int last_half_folded = -1, closes = 0;
+  std::vector<int> close_order, fold_order;
+  for (int i = 0; i < 600; ++i) {
+    const int n = p.collect_order((i % 7) != 0, hv, wv);
+    for (int j = 0; j < n; ++j) {
+      fold_order.push_back(hv[j]);
+      p.collected(hv[j]);
+      last_half_folded = hv[j];
+    }
+    const int k = p.next_slot(t += 125000);
+    p.submitted(k, t);
+    if (p.is_publisher(k)) {
+      close_order.push_back(k / 3);
+      ++closes;
+    }
+  }
+  CHECK(last_half_folded >= 0 && closes > 100);
+  for (size_t j = 0; j < fold_order.size(); ++j) CHECK(fold_order[j] == close_order[j]);  // FIFO
   std::printf("batch plan ok\n");
 }
 

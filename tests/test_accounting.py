@@ -283,3 +283,57 @@ def test_partitions_split_socket_energy(N):
         assert max(parts) < 0.5 * sum(parts)  # no partition is billed the whole socket
     finally:
         cpx.stop()
+
+
+def test_sm_util_auto_does_not_count_the_exporters_reads(mock_exporter):
+    """at kHz counter rates the PMFW GFX busy counts every counter READ
+    as ≈80 µs of work, so a bursty GPU read ≈100 % (modelled here by the mock's
+    pmfw_busy_floor 99).  The default --sm-util-source auto bills the pod the counter
+    tier's GPU-active while that tier runs — the true 25 % duty of a square load — and
+    falls back to the PMFW busy when the counters are handed over, without the
+    per-pod counter ever running backwards."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", window_s=0.8, pmc_idle_hz=0,
+                       mock={"square_duty": 0.25, "util_base": 50, "util_amp": 50, "util_period_s": 0.2,
+                             "pmfw_busy_floor": 99})
+    ex.set_device_owners(0, [{"pod": "p", "namespace": "n", "container": "c"}])
+    one = lambda m, f, **kw: [v for lb, v in m[f] if all(lb.get(k) == w for k, w in kw.items())][0]  # noqa: E731
+
+    def window(secs):
+        m0 = parse_text(ex.render())
+        time.sleep(secs)
+        m1 = parse_text(ex.render())
+        d = lambda f, **kw: one(m1, f, **kw) - one(m0, f, **kw)  # noqa: E731
+        dt = d("kgs_sampled_seconds_total")
+        return m1, {"busy": 100 * d("container_gpu_busy_seconds_total") / dt,
+                    "gfx": 100 * d("amdgpu_gfx_busy_seconds_total") / dt,
+                    "pmfw": 100 * d("amdgpu_pmfw_gfx_busy_seconds_total") / dt,
+                    "from_counters": d("kgs_util_source_seconds_total", source="counters") / dt,
+                    "pod_busy": one(m1, "container_gpu_busy_seconds_total")}
+
+    time.sleep(0.3)
+    m, on = window(1.6)
+    assert on["busy"] == pytest.approx(25, abs=3) and on["gfx"] == pytest.approx(25, abs=3), on
+    assert on["pmfw"] > 98 and on["from_counters"] > 0.95, on
+    assert one(m, "container_gpu_sm_util") == pytest.approx(25, abs=6)
+    ex.set_pmc_enabled(False)                     # counters handed over: PMFW is all there is
+    time.sleep(0.3)
+    _, off = window(1.0)
+    assert off["busy"] > 98 and off["from_counters"] < 0.05, off
+    ex.set_pmc_enabled(True)
+    time.sleep(0.3)
+    _, back = window(1.6)
+    assert back["busy"] == pytest.approx(25, abs=3) and back["from_counters"] > 0.95, back
+    assert on["pod_busy"] <= off["pod_busy"] <= back["pod_busy"]
+
+
+def test_sm_util_pmfw_source_keeps_the_firmware_busy(mock_exporter):
+    """--sm-util-source pmfw: the reference-contract series is the PMFW GFX busy,
+    READs included (the mock's floor), exactly as before round 4."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", window_s=0.8, pmc_idle_hz=0, sm_util_source="pmfw",
+                       mock={"square_duty": 0.25, "util_base": 50, "util_amp": 50, "util_period_s": 0.2,
+                             "pmfw_busy_floor": 99})
+    ex.set_device_owners(0, [{"pod": "p", "namespace": "n", "container": "c"}])
+    time.sleep(1.2)
+    m = parse_text(ex.render())
+    (_, sm), = m["container_gpu_sm_util"]
+    assert sm > 98

@@ -243,3 +243,112 @@ def test_kgs_pmc_release_one_gpu_via_cli():
         p.stdin.flush()
         out, _ = p.communicate(timeout=30)
     assert json.loads(out.strip().splitlines()[-1])["abandoned_threads"] == 0
+
+
+def test_injected_queue_stall_trips_the_breaker_and_a_fresh_queue_recovers(mock_exporter):
+    """VERDICT r3 #3, mock half (test_gpu.py runs the same on MI355X's real AQL
+    queue): inject_pmc_stall wedges GPU 1's READ path as a never-completing packet
+    at the head of its queue would.  The READs time out, the breaker opens within
+    K x timeout, the retry resets (recreates) the queue and re-STARTs, the totals
+    stay monotonic, and GPU 0 and both PMFW tiers never notice."""
+    ex = mock_exporter(n_gpus=2, hz=HZ, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0,
+                       pmc_breaker_k=3, pmc_retry_s=0.3, control_http=True,
+                       mock={"fw_period_s": 0.02}, mock_pmc={"hang_timeout_s": 0.1})
+    time.sleep(0.3)
+    g0 = lambda m: [v for lb, v in m["amdgpu_pmc_total"] if lb["counter"] == "GRBM_COUNT" and lb["gpu"] == "1"][0]  # noqa: E731
+    before = parse_text(ex.render())
+    body = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/stall?gpu=1", timeout=5).read())
+    assert body == {"gpu": 1, "stall": True}
+    t0 = time.time()
+    seen_failed, totals = None, [g0(before)]
+    pmfw, pmc = rates_once(ex, [0, 1], 0.6)                # while wedged / tripping
+    while time.time() - t0 < 3.0:
+        m = parse_text(ex.render())
+        totals.append(g0(m))
+        if seen_failed is None and {lb["gpu"]: v for lb, v in m["kgs_pmc_failed"]}["1"] == 1:
+            seen_failed = time.time() - t0
+        if seen_failed is not None and ex.integrals(1)["pmc_failed"] == 0:
+            break
+        time.sleep(0.02)
+    i = ex.integrals(1)
+    assert i["pmc_stalls_injected"] == 1 and i["pmc_breaker_trips"] == 1 and i["pmc_resets"] >= 1, i
+    assert seen_failed is not None and seen_failed < 3 * 0.1 + 0.5, seen_failed  # K x timeout + slack
+    assert i["pmc_failed"] == 0 and i["pmc_on"] == 1, i                          # re-STARTed on a fresh queue
+    assert all(b >= a for a, b in zip(totals, totals[1:])), totals               # monotonic throughout
+    time.sleep(0.2)
+    assert g0(parse_text(ex.render())) > totals[-1]                              # and counting again
+    assert pmc[0] >= 0.95 * HZ and pmfw[0] >= 40 and pmfw[1] >= 40, (pmc, pmfw)
+    assert ex.integrals(0)["pmc_breaker_trips"] == 0
+
+
+def _slow_fault_exporter(mock_exporter, **fault):
+    ex = mock_exporter(n_gpus=8, hz=100, proc_period_s=0.05, link_period_s=0.1, stale_s=0.5, stop_timeout_s=0.5,
+                       mock={"slow_fault_after_s": 0.4, **fault})
+    pids = {}
+    for g in range(8):
+        ex.set_device_owners(g, [{"pod": f"p{g}", "namespace": "n", "container": "c"}])
+        for k in range(1 + g % 2):  # the mock's processes on GPU g: PIDs 100000 + 10 g + k
+            pids[(g, 100000 + 10 * g + k)] = {"pod": f"p{g}", "namespace": "n", "container": "c", "pod_uid": f"u{g}"}
+    ex.set_pid_owners(pids)
+    return ex
+
+
+def _by_gpu(m, fam, **kw):
+    out: dict = {}
+    for lb, v in m.get(fam, []):
+        if all(lb.get(k) == w for k, w in kw.items()):
+            out.setdefault(lb["gpu"], []).append(v)
+    return out
+
+
+def test_slow_tier_hang_on_one_gpu_leaves_the_others_fresh(mock_exporter):
+    """GPU 3's process-list call hangs (outside the management-library
+    lock: a stuck driver path of that device).  Each GPU has its own slow thread, so
+    GPUs 0-2 and 4-7 keep fresh per-process lines and rising per-pod CU-seconds;
+    GPU 3's per-process lines disappear after --stale-after, its age gauge and
+    in-flight call gauge grow, and stop() is bounded (the stuck thread is abandoned)."""
+    ex = _slow_fault_exporter(mock_exporter, slow_fault_dev=3, slow_fault_tier="procs", slow_fault_kind="hang",
+                              slow_hang_s=4.0)
+    time.sleep(0.35)
+    m = parse_text(ex.render())
+    assert sorted(_by_gpu(m, "amdgpu_process_hbm_bytes")) == [str(g) for g in range(8)]
+    time.sleep(1.2)  # GPU 3 has been stuck for ≥ 0.8 s > stale_after
+    m1 = parse_text(ex.render())
+    time.sleep(0.4)
+    m2 = parse_text(ex.render())
+    assert sorted(_by_gpu(m2, "amdgpu_process_hbm_bytes")) == [str(g) for g in range(8) if g != 3]
+    age = {lb["gpu"]: v for lb, v in m2["kgs_slow_last_ok_age_seconds"] if lb["tier"] == "procs"}
+    assert age["3"] > 1.0 and max(v for g, v in age.items() if g != "3") < 0.3, age
+    call = {lb["gpu"]: v for lb, v in m2["kgs_slow_call_seconds"]}
+    assert call["3"] > 1.0 and max(v for g, v in call.items() if g != "3") < 0.1, call
+    cu1 = {lb["gpu"]: v for lb, v in m1["container_gpu_cu_seconds_total"]}
+    cu2 = {lb["gpu"]: v for lb, v in m2["container_gpu_cu_seconds_total"]}
+    assert all(cu2[str(g)] > cu1[str(g)] for g in range(8) if g != 3), (cu1, cu2)
+    assert cu2["3"] == cu1["3"]                     # no process list, no CU-seconds: not invented
+    # the other tiers of GPU 3 (links / RAS run after the process list on its thread) go stale
+    # with it; its PMFW tier keeps going
+    assert "3" in {lb["gpu"] for lb, _ in m2["amdgpu_gfx_busy_percent"]}
+    t0 = time.time()
+    ex.stop()
+    assert time.time() - t0 < 2.0
+    assert ex.abandoned_threads == 1 and ex.integrals(3)["slow_hung"] == 1
+    hung = {lb["gpu"]: v for lb, v in parse_text(ex.render())["kgs_slow_thread_hung"]}
+    assert hung["3"] == 1 and sum(hung.values()) == 1
+
+
+def test_slow_tier_errors_on_one_gpu_drop_only_its_link_table(mock_exporter):
+    """A failing link-table read on GPU 2 (error, not hang): its amdgpu_xgmi_link_info
+    lines go once stale, kgs_slow_errors_total{tier="links"} counts, and every other
+    GPU — and GPU 2's own process list and RAS — stay fresh."""
+    ex = _slow_fault_exporter(mock_exporter, slow_fault_dev=2, slow_fault_tier="links", slow_fault_kind="error")
+    time.sleep(0.35)
+    assert "2" in _by_gpu(parse_text(ex.render()), "amdgpu_xgmi_link_info")
+    time.sleep(1.2)
+    m = parse_text(ex.render())
+    links = _by_gpu(m, "amdgpu_xgmi_link_info")
+    assert sorted(links) == [str(g) for g in range(8) if g != 2]
+    err = {lb["gpu"]: v for lb, v in m["kgs_slow_errors_total"] if lb["tier"] == "links"}
+    assert err["2"] >= 5 and sum(v for g, v in err.items() if g != "2") == 0, err
+    assert "2" in _by_gpu(m, "amdgpu_process_hbm_bytes") and "2" in _by_gpu(m, "amdgpu_xgmi_error_status")
+    age = {(lb["gpu"], lb["tier"]): v for lb, v in m["kgs_slow_last_ok_age_seconds"]}
+    assert age[("2", "links")] > 0.7 and age[("2", "health")] < 0.4 and age[("2", "procs")] < 0.3, age

@@ -787,7 +787,7 @@ def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
             m = parse_text(sc.get())
             rows[mode] = {"reads_per_s": (one(m, "kgs_pmc_samples_total") - n0) / 1.8,
                           "publishes_per_s": (one(m, "kgs_pmc_publishes_total") - one(m0, "kgs_pmc_publishes_total")) / 1.8,
-                          "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent"),
+                          "pmfw_gfx_busy_pct": one(m, "amdgpu_pmfw_gfx_busy_percent"),
                           "gpu_active_pct": one(m, "amdgpu_gpu_active_percent"),
                           "quiet": one(m, "kgs_pmc_quiet")}
         urllib.request.urlopen(f"{ctl}?hz=100", timeout=5).read()
@@ -802,7 +802,7 @@ def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
         rows["mfma_load"] = {"reads_per_s": (one(m, "kgs_pmc_samples_total") - n0) / dt,
                              "publishes_per_s": (one(m, "kgs_pmc_publishes_total") - one(m0, "kgs_pmc_publishes_total")) / dt,
                              "unlanded": one(m, "kgs_pmc_unlanded_total"),
-                             "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent"),
+                             "pmfw_gfx_busy_pct": one(m, "amdgpu_pmfw_gfx_busy_percent"),
                              "gpu_active_pct": one(m, "amdgpu_gpu_active_percent"),
                              "mfma_util_pct": one(m, "amdgpu_mfma_util_percent"), "quiet": one(m, "kgs_pmc_quiet")}
     finally:
@@ -939,7 +939,7 @@ def test_sm_util_from_counters_follows_load_and_idle(torch_dev, tmp_path):
             proc.communicate()
     one = lambda m, f: m[f][0][1] if m.get(f) else None  # noqa: E731
     row = {k: {"sm_util": one(m, "container_gpu_sm_util"), "busy_s": one(m, "container_gpu_busy_seconds_total"),
-               "pmfw_gfx_busy_pct": one(m, "amdgpu_gfx_busy_percent")} for k, m in (("load", busy), ("idle", idle))}
+               "pmfw_gfx_busy_pct": one(m, "amdgpu_pmfw_gfx_busy_percent")} for k, m in (("load", busy), ("idle", idle))}
     print(json.dumps(row))
     assert busy["container_gpu_sm_util"][0][0]["pod_name"] == "train-0"
     assert row["load"]["sm_util"] > 80 and row["load"]["busy_s"] > 1.0, row

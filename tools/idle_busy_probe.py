@@ -81,7 +81,7 @@ def one(label: str, hz: float, pmc: str, extra: list[str], bdf: str, secs: float
         m = parse_text(Scraper("127.0.0.1", ready["port"]).get())
         g = lambda f: m[f][0][1] if m.get(f) else None  # noqa: E731
         out = {"config": label, "hz": hz, "pmc": ready.get("pmc"), "extra": extra, "env": env or {},
-               "pmfw_gfx_busy_pct": g("amdgpu_gfx_busy_percent"), "gpu_active_pct": g("amdgpu_gpu_active_percent"),
+               "pmfw_gfx_busy_pct": g("amdgpu_pmfw_gfx_busy_percent"), "gpu_active_pct": g("amdgpu_gpu_active_percent"),
                "mfma_util_pct": g("amdgpu_mfma_util_percent"), "power_w": g("amdgpu_power_watts"),
                "clock_mhz": g("amdgpu_gpu_clock_effective_mhz"), "quiet": g("kgs_pmc_quiet"),
                "reads_total": g("kgs_pmc_samples_total")}
