@@ -164,7 +164,7 @@ class Exporter {
   // STOPs its counting session and skips the PMC tier) or take them back (true);
   // dev < 0 = every device.  Each device's own thread acts, so a hung GPU does
   // not delay the others.
-  void set_pmc_enabled(bool on, int dev = -1);
+  void set_pmc_enabled(bool on, int dev = -1, bool drop_queue = false);
   bool pmc_enabled() const;
   // Sampler tick rate (benchmarks switch tiers in place; integrals continue).
   // false if hz is outside (0, kMaxHz].

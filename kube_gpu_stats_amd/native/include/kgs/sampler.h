@@ -168,6 +168,7 @@ struct DeviceState {
   // control plane sets pmc_want; the sampler thread releases / re-acquires the
   // counters itself and reports the state in pmc_on.
   std::atomic<int> pmc_want{1};
+  std::atomic<int> pmc_drop_queue{0};       // with a release: destroy the READ queue too
   std::atomic<int> pmc_on{0};
   std::atomic<uint64_t> pmc_releases{0};
   std::atomic<int> pmc_stalled{0};          // counters frozen / implausible for ≥ kPmcStallNs
@@ -264,7 +265,10 @@ class Sampler {
   // counters to another profiler (false) or to take them back (true).  Takes
   // effect within one tick of that device's own thread: a hung device never
   // delays the others.
-  void set_pmc_wanted(bool on, int dev = -1);
+  // drop_queue (release only): also destroy the reader's READ queue
+  // (CounterSource::reset), so nothing of the counter tier stays mapped on the GPU
+  // until the next acquire — the benchmark's "released" condition.
+  void set_pmc_wanted(bool on, int dev = -1, bool drop_queue = false);
   // Change the tick rate (stops and restarts the threads; integrals continue).
   // false (nothing changed) unless 0 < hz <= kMaxHz.
   bool set_hz(double hz);

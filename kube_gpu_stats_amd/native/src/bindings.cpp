@@ -418,9 +418,9 @@ class PyExporter {
     py::gil_scoped_release r;
     ex_.resume_sampling();
   }
-  void set_pmc_enabled(bool on, int gpu) {
+  void set_pmc_enabled(bool on, int gpu, bool drop_queue) {
     if (gpu >= 0) check(gpu);
-    ex_.set_pmc_enabled(on, gpu);
+    ex_.set_pmc_enabled(on, gpu, drop_queue);
   }
   void set_sample_rate(double hz) {
     bool ok;
@@ -491,7 +491,9 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("resume", &PyExporter::resume)
       .def_property_readonly("sampling", &PyExporter::sampling)
       .def("set_pmc_enabled", &PyExporter::set_pmc_enabled, py::arg("on"), py::arg("gpu") = -1,
-           "Hand the hardware counters to another profiler (False) or take them back (True); gpu=-1: every GPU")
+           py::arg("drop_queue") = false,
+           "Hand the hardware counters to another profiler (False) or take them back (True); gpu=-1: every GPU; "
+           "drop_queue (with False): also destroy the counter reader's READ queue")
       .def_property_readonly("abandoned_threads", &PyExporter::abandoned_threads,
                              "sampler threads stop() gave up on (stuck in a device call)")
       .def("inject_xgmi", &PyExporter::inject_xgmi, py::arg("src"), py::arg("dst"), py::arg("bytes"),

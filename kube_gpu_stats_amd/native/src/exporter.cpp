@@ -215,9 +215,9 @@ void Exporter::resume_sampling() {
   if (sampler_) sampler_->start();
 }
 bool Exporter::sampling() const { return sampler_ && sampler_->running(); }
-void Exporter::set_pmc_enabled(bool on, int dev) {
+void Exporter::set_pmc_enabled(bool on, int dev, bool drop_queue) {
   if (dev < 0) pmc_wanted_.store(on);
-  if (sampler_) sampler_->set_pmc_wanted(on, dev);
+  if (sampler_) sampler_->set_pmc_wanted(on, dev, drop_queue);
 }
 bool Exporter::pmc_enabled() const { return pmc_wanted_.load(); }
 

@@ -332,7 +332,9 @@ void HttpServer::loop() {
             respond(c, 400, "Bad Request", "text/plain", "gpu out of range\n");
           } else {
             const bool on = target == "/control/pmc/acquire";
-            ex_->set_pmc_enabled(on, gpu);
+            // drop_queue=1 (release): destroy the READ queue as well (benchmarks'
+            // "released" condition: nothing of the counter tier left on the GPU).
+            ex_->set_pmc_enabled(on, gpu, query_int(query, "drop_queue", 0) != 0);
             std::string j = gpu >= 0 ? "{\"gpu\":" + std::to_string(gpu) + ",\"pmc\":" + (on ? "true" : "false") + "}"
                                      : std::string(ex_->pmc_enabled() ? "{\"pmc\":true}" : "{\"pmc\":false}");
             respond(c, 200, "OK", "application/json", j);

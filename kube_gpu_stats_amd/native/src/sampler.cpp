@@ -158,9 +158,13 @@ bool Sampler::set_pmc_gap(double busy_min, double hz) {
   return true;
 }
 
-void Sampler::set_pmc_wanted(bool on, int dev) {
+void Sampler::set_pmc_wanted(bool on, int dev, bool drop_queue) {
   for (int d : dev_ids_)
-    if (dev < 0 || d == dev) states_[static_cast<size_t>(d)]->pmc_want.store(on ? 1 : 0);
+    if (dev < 0 || d == dev) {
+      DeviceState& st = *states_[static_cast<size_t>(d)];
+      if (!on && drop_queue) st.pmc_drop_queue.store(1);
+      st.pmc_want.store(on ? 1 : 0);
+    }
 }
 
 void Sampler::set_pid_pods(std::shared_ptr<const std::unordered_map<uint64_t, std::string>> m) {
@@ -612,6 +616,10 @@ void Sampler::run_pmc(Worker& w) {
       // The next START restarts the counts at 0: carry the published totals
       // as a base so the exported counters stay monotonic.
       carry_base();
+    }
+    if (!want && st.pmc_drop_queue.exchange(0)) {  // "released": no queue left mapped either
+      src->reset(dev);
+      if (gone()) return;
     }
     // ---- (re)acquire: after a hand-over, or a retry of an open breaker --------
     if (want && !st.pmc_on.load(std::memory_order_relaxed) && mono_ns() >= st.pmc_retry_at_ns) {
