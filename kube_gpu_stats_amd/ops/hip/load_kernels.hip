@@ -10,8 +10,10 @@
 //                 result is checkable against torch.
 //  * triad_f32  — HBM bound: c = a + s·b with 16-byte (float4) accesses,
 //                 grid sized to ≫256 CUs, nontemporal loads (once-read stream).
-//  * copy_f32   — float4 copy; with a peer-device source pointer this is the
-//                 xGMI peer-read load (hipDeviceEnablePeerAccess first).
+//  * copy_f32   — float4 copy; with a peer-device source or destination pointer
+//                 this is the xGMI peer load (hipDeviceEnablePeerAccess first).
+//  * gather64 / reread — HBM-model validation patterns: random 64 B lines over
+//                 a large buffer, and repeated sweeps of a cache-resident one.
 //
 // C ABI only (loaded with ctypes by kube_gpu_stats_amd/ops/load.py).
 #include <hip/hip_runtime.h>
@@ -166,6 +168,49 @@ __global__ __launch_bounds__(kBlock) void copy_f32_kernel(const f32x4* __restric
   for (; i < hi; i += kBlock) st<true>(ld<true>(src + i), dst + i);
 }
 
+// Random 64-byte gather (HBM-model validation, profiles/umc_calib.md): thread t
+// reads `per_thread` 64 B lines (four 16-byte loads each) chosen by a 32-bit LCG
+// seeded with t, line = (x >> shift) & (nlines - 1) over a power-of-two number of
+// lines, and writes the sum of the floats it read.  Every lane of a wave hits a
+// different line, so each wave-load is 64 independent 64 B requests over the whole
+// buffer: the small-granularity, TLB- and row-hostile end of HBM traffic, where
+// memory-controller activity and requested bytes can part ways.  The LCG is
+// replayed in torch for the numerics check (tests/test_gpu.py).
+__global__ __launch_bounds__(kBlock) void gather64_kernel(const f32x4* __restrict__ src, uint32_t nlines_mask,
+                                                          int shift, int per_thread, uint32_t seed,
+                                                          float* __restrict__ out) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t x = seed ^ (t * 2654435761u);
+  float acc = 0.f;
+  for (int j = 0; j < per_thread; ++j) {
+    x = x * 1664525u + 1013904223u;
+    const f32x4* p = src + static_cast<size_t>((x >> shift) & nlines_mask) * 4;
+    f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+    f32x4 v = (v0 + v1) + (v2 + v3);
+    acc += (v[0] + v[1]) + (v[2] + v[3]);
+  }
+  out[t] = acc;
+}
+
+// Cache-resident re-read (HBM-model validation): `passes` sweeps over a small
+// buffer (≤ 128 MiB: MI355X's L2 is 4 MiB per XCD and the Infinity Cache / MALL
+// 256 MiB), default cache policy, thread t summing src4[t], src4[t + T], ... each
+// pass.  Requested bytes are passes × size; HBM sees the first touch (and what
+// the caches evict), so the UMC-activity model should read far below the request.
+__global__ __launch_bounds__(kBlock) void reread_kernel(const f32x4* __restrict__ src, size_t n4, int passes,
+                                                        float* __restrict__ out) {
+  const size_t T = static_cast<size_t>(gridDim.x) * kBlock;
+  const size_t t = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  float acc = 0.f;
+  for (int p = 0; p < passes; ++p) {
+    asm volatile("" ::: "memory");  // every pass reloads (no hoisting across passes)
+    f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+    for (size_t i = t; i < n4; i += T) s4 += src[i];
+    acc += (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  }
+  out[t] = acc;
+}
+
 int check(hipError_t e, const char* what) {
   if (e == hipSuccess) return 0;
   std::snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
@@ -227,6 +272,25 @@ int kgs_load_copy_f32(const float* src, float* dst, size_t n, int nblocks, void*
   hipLaunchKernelGGL(copy_f32_kernel, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
                      reinterpret_cast<const f32x4*>(src), reinterpret_cast<f32x4*>(dst), n / 4);
   return check(hipGetLastError(), "copy_f32 launch");
+}
+
+// nlines must be a power of two (64 B lines), shift = 32 - log2(nlines) ... any
+// shift in [0, 31]: the line index is (x >> shift) & (nlines - 1).  out: nblocks*256.
+int kgs_load_gather64(const float* src, uint32_t nlines, int shift, int per_thread, uint32_t seed, int nblocks,
+                      float* out, void* stream) {
+  if (nlines == 0 || (nlines & (nlines - 1)) || shift < 0 || shift > 31 || per_thread <= 0 || nblocks <= 0)
+    return check(hipErrorInvalidValue, "gather64 args");
+  hipLaunchKernelGGL(gather64_kernel, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const f32x4*>(src), nlines - 1, shift, per_thread, seed, out);
+  return check(hipGetLastError(), "gather64 launch");
+}
+
+// n must be a multiple of 4; out: nblocks*256 floats.
+int kgs_load_reread(const float* src, size_t n, int passes, int nblocks, float* out, void* stream) {
+  if ((n & 3) || passes <= 0 || nblocks <= 0) return check(hipErrorInvalidValue, "reread args");
+  hipLaunchKernelGGL(reread_kernel, dim3(nblocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const f32x4*>(src), n / 4, passes, out);
+  return check(hipGetLastError(), "reread launch");
 }
 
 int kgs_load_enable_peer(int dev, int peer) {

@@ -44,6 +44,10 @@ def lib() -> ctypes.CDLL:
         L.kgs_load_copy_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                         ctypes.c_void_p]
         L.kgs_load_enable_peer.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.kgs_load_gather64.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.kgs_load_reread.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_void_p]
         _LIB = L
     return _LIB
 
@@ -129,6 +133,43 @@ def copy_f32(src, dst, nblocks: int = 0, stream=None) -> None:
     if nblocks <= 0:
         nblocks = default_stream_blocks(n)
     _check(lib().kgs_load_copy_f32(src.data_ptr(), dst.data_ptr(), n, int(nblocks), _stream_ptr(stream)))
+
+
+def gather64(src, nlines: int, per_thread: int, seed: int, out, shift: int = 3, stream=None) -> None:
+    """out[t] = Σ of the 16 floats of each of `per_thread` random 64 B lines of `src`
+    (line = (x >> shift) & (nlines-1), x the 32-bit LCG of gather64_ref); nlines a
+    power of two, src ≥ nlines·16 floats, out = nblocks·256 floats."""
+    import torch
+
+    assert src.dtype == out.dtype == torch.float32 and src.is_contiguous() and out.is_contiguous()
+    assert nlines > 0 and nlines & (nlines - 1) == 0 and src.numel() >= nlines * 16 and src.data_ptr() % 16 == 0
+    assert out.numel() % BLOCK == 0 and 0 <= shift <= 31 and src.device == out.device
+    _check(lib().kgs_load_gather64(src.data_ptr(), nlines, shift, int(per_thread), int(seed) & 0xFFFFFFFF,
+                                   out.numel() // BLOCK, out.data_ptr(), _stream_ptr(stream)))
+
+
+def gather64_ref(src, nlines: int, per_thread: int, seed: int, threads, shift: int = 3):
+    """fp32 torch reference of gather64 for the thread ids in `threads` (int64 tensor)."""
+    import torch
+
+    M = 0xFFFFFFFF
+    x = (seed ^ ((threads * 2654435761) & M)) & M
+    lines = src.view(-1, 16)
+    acc = torch.zeros(threads.numel(), dtype=torch.float32, device=src.device)
+    for _ in range(per_thread):
+        x = (x * 1664525 + 1013904223) & M
+        acc += lines[((x >> shift) & (nlines - 1)).to(src.device)].sum(-1)
+    return acc
+
+
+def reread(src, passes: int, out, stream=None) -> None:
+    """out[t] = passes × Σ_k src4[t + k·T] (summed as float4 lanes), T = out.numel()."""
+    import torch
+
+    assert src.dtype == out.dtype == torch.float32 and src.is_contiguous() and out.is_contiguous()
+    assert src.numel() % 4 == 0 and out.numel() % BLOCK == 0 and src.data_ptr() % 16 == 0 and src.device == out.device
+    _check(lib().kgs_load_reread(src.data_ptr(), src.numel(), int(passes), out.numel() // BLOCK, out.data_ptr(),
+                                 _stream_ptr(stream)))
 
 
 def enable_peer(dev: int, peer: int) -> None:

@@ -393,6 +393,32 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     return ap
 
 
+def shared_query(window_s: float, step_s: int) -> str:
+    """GPUs that had more than one owner at the same time somewhere in the window
+    (kgs_gpu_owner: one series per (GPU, pod, container) allocation)."""
+    return (f"max_over_time((count by (kubernetes_io_hostname, gpu, uuid) (kgs_gpu_owner))"
+            f"[{int(window_s)}s:{int(step_s)}s]) > 1")
+
+
+def warn_shared_gpus(c: PromClient, end_unix: float, window_s: float, step_s: int, err=None) -> list[dict]:
+    """the default busy counter bills every tenant of a shared GPU
+    the whole GPU's busy time.  When any GPU had several owners in the window, say so
+    on stderr and name the per-pod alternative.  Best effort: a Prometheus that cannot
+    evaluate the query only costs the warning."""
+    try:
+        shared = [r["metric"] for r in result(c.query(shared_query(window_s, step_s), end_unix))]
+    except Exception as e:  # noqa: BLE001
+        L.debug("shared-GPU check skipped: %s", e)
+        return []
+    if shared:
+        gpus = ", ".join(f'{m.get("kubernetes_io_hostname", "?")}/gpu{m.get("gpu", "?")}' for m in shared[:8])
+        print(f"warning: {len(shared)} GPU(s) had more than one pod at once ({gpus}{', ...' if len(shared) > 8 else ''}); "
+              "container_gpu_busy_seconds_total bills each of them the whole GPU — "
+              "use --util-metric container_gpu_cu_seconds_total for each pod's own compute share",
+              file=err or sys.stderr)
+    return shared
+
+
 def run(a) -> int:
     c = PromClient(a.prom_url, a.proxy, a.timeout, a.retries)
     if a.compat and not a.namespace:
@@ -401,6 +427,8 @@ def run(a) -> int:
          Queries.amd(a.namespace, a.step, a.resource, a.type_label, a.util_metric))
     end = a.end if a.end else (datetime.now() if a.compat else time.time())
     rows = run_report(c, q, end, a.window, a.step, a.compat, a.mode, a.missing, show_finished=a.show_finished)
+    if not a.compat and a.util_metric == "container_gpu_busy_seconds_total":
+        warn_shared_gpus(c, end if isinstance(end, (int, float)) else end.timestamp(), a.window, a.step)
     extras: list[str] = []
     if a.mode == "pod" and not a.compat:
         if a.idle_hours:

@@ -309,3 +309,41 @@ def test_cli_group_by_namespace_end_to_end(prom, capsys):
     assert got["ml"]["GPU-h"] == 8.0 and got["ml"]["Util %"] == 50.0 and got["ml"]["Idle GPU-h"] == 4.0
     assert got["infer"]["GPU-h"] == 4.0 and got["infer"]["Busy GPU-h"] == 4.0
     assert got["TOTAL"]["Pods"] == 2 and abs(got["TOTAL"]["Util %"] - 100 * 8 / 12) < 1e-9
+
+
+def _shared_scenario(fp):
+    q = G.Queries.amd("", STEP)
+    fp.add_range(q.util, [{"metric": {"kubernetes_io_hostname": "n1", "namespace": "ml", "pod_name": p},
+                           "values": [[T_END, "90"]]} for p in ("a", "b")])
+    fp.add_instant(q.total, [{"metric": {"node": "n1", q.type_label: "MI355X"}, "value": [T_END, "8"]}])
+    fp.add_instant(q.used, [{"metric": {"node": "n1"}, "value": [T_END, "1"]}])
+    fp.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": p}, "value": [T_END, "1"]} for p in ("a", "b")])
+    fp.add_range(q.req, [{"metric": {"node": "n1", "namespace": "ml", "pod": p}, "values": [[T_END, "1"]]}
+                         for p in ("a", "b")])
+    return q
+
+
+def test_fixed_mode_warns_when_the_busy_counter_bills_a_shared_gpu_twice(prom, capsys):
+    """pods a and b share GPU 3 of n1; the default util metric
+    (container_gpu_busy_seconds_total) bills both the whole GPU, so the report says so
+    on stderr and names container_gpu_cu_seconds_total — stdout stays the table."""
+    fp, url = prom
+    _shared_scenario(fp)
+    fp.add_instant(G.shared_query(7200, STEP), [{"metric": {"kubernetes_io_hostname": "n1", "gpu": "3", "uuid": "u3"},
+                                                "value": [T_END, "2"]}])
+    G.main(["--prom-url", url, "--window", "7200", "--step", str(STEP), "--end", str(T_END), "--format", "json"])
+    cap = capsys.readouterr()
+    assert len(json.loads(cap.out)) == 2
+    assert "n1/gpu3" in cap.err and "container_gpu_cu_seconds_total" in cap.err
+    # per-pod compute share asked for: no warning; a Prometheus that cannot evaluate the check: no warning
+    G.main(["--prom-url", url, "--window", "7200", "--step", str(STEP), "--end", str(T_END), "--format", "json",
+            "--util-metric", "container_gpu_cu_seconds_total"])
+    assert "warning" not in capsys.readouterr().err
+
+
+def test_shared_gpu_check_is_best_effort(prom, capsys):
+    fp, url = prom
+    _shared_scenario(fp)  # no canned answer: the fake Prometheus rejects the subquery (400)
+    G.main(["--prom-url", url, "--window", "7200", "--step", str(STEP), "--end", str(T_END), "--format", "json"])
+    cap = capsys.readouterr()
+    assert len(json.loads(cap.out)) == 2 and "warning" not in cap.err
