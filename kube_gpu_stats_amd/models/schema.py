@@ -148,6 +148,14 @@ CATALOG: tuple[Family, ...] = (
       "∫ GPU-active share of clocks dt (per drain: ΔGRBM_SPI_BUSY / ΔGRBM_COUNT · Δt); rate() = GPU-active fraction, "
       "blind to the exporter's own counter READs (the --sm-util-source counters integral).", source="counters",
       tier="pmc"),
+    F("amdgpu_dispatch_busy_seconds_total", "counter",
+      "∫ dispatch-in-flight share dt from the counter stream (per drain: CPC_CPC_STAT_BUSY share of the clocks less "
+      "the exporter's own READ packet's CP time, never below the GRBM_SPI_BUSY share; an interval the CP was busy "
+      "for ≥ 97 % counts whole); rate() = the READ-immune 'a kernel is running' fraction behind "
+      "--sm-util-source auto.", source="counters", tier="pmc"),
+    F("kgs_pmc_read_cp_seconds", "gauge", "Command-processor busy time of one counter READ packet, learned on "
+      "intervals without waves (what amdgpu_dispatch_busy_seconds_total subtracts per READ).", source="self",
+      tier="pmc"),
     F("amdgpu_mfma_busy_seconds_total", "counter",
       "∫ MFMA-busy share of all SIMD cycles dt (per drain: ΔSQ_VALU_MFMA_BUSY_CYCLES / (SIMDs·ΔGRBM_COUNT) · Δt); "
       "rate() = matrix-core utilisation of wall time.", source="counters", tier="pmc"),

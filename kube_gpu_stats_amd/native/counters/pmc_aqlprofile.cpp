@@ -804,11 +804,15 @@ bool nonpub_barrier() {
 // Rebuild the session-layout part of kgs_pmc_info (handle's thread only; called
 // when the layout changes: open, mode switch, the first fold of an event list).
 void snap_info(Agent* a) {
+  // XCDs the result layout places results on (place_xcds), not the XCDs one fold
+  // happened to see: the first fold runs before the placement exists.
+  uint32_t placed = 0;
+  for (int x : a->res_xcd)
+    if (x >= 0 && x < kMaxXcd) placed |= 1u << x;
   std::string o = ";events=" + std::to_string(a->events.size()) + ";results=" + std::to_string(a->last_results) +
                   ";pipelined=" + std::to_string(a->pipelined ? 1 : 0) + ";lean=" + std::to_string(lean_mode()) + ":" +
                   std::to_string(a->lean_changed) + ";batch=" + std::to_string(a->batch) +
-                  ";xcd=" + std::to_string(a->xcd_seen.empty() ? 0 : __builtin_popcount(a->xcd_seen[0])) + ":" +
-                  a->xcd_from;
+                  ";xcd=" + std::to_string(__builtin_popcount(placed)) + ":" + a->xcd_from;
   if (!nonpub_barrier()) o += a->batch >= 2 ? ";nobarrier=1" : ";nobarrier=ignored(batch<2)";
   if (queue_priority() >= 0) o += ";priority=" + std::to_string(queue_priority());
   for (size_t k = 0; k < a->names.size(); ++k)

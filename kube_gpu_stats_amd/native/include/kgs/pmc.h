@@ -35,7 +35,11 @@ enum PmcIndex : int {
   kPmcGrbmActive = 1,     // GRBM_SPI_BUSY (max over XCC): clocks a shader engine had waves to run
   kPmcMfmaBusy = 2,       // SQ_VALU_MFMA_BUSY_CYCLES (sum over SIMDs)
   kPmcTaBusy = 3,         // TA_TA_BUSY (mean over TA instances): vector-memory address unit busy cycles
-  kPmcCount = 4,
+  // CPC_CPC_STAT_BUSY (max over XCC): clocks the compute command processor was busy —
+  // ≈100 % whenever a dispatch is in flight, µs kernels back to back included, plus a
+  // short fixed time per counter READ packet (Sampler's dispatch-busy integral removes it).
+  kPmcCpcBusy = 4,
+  kPmcCount = 5,
   // TD_TD_BUSY tracks TA_TA_BUSY on every load tried and doubles the drain cost
   // (288 more instances, ≈+110 µs per read), so it is not in the default set.
 };
@@ -66,7 +70,8 @@ int pmc_counter_reduce(int idx);
 // profiles/r2/immunity/.)  GRBM has two counter slots per XCC, so SPI busy
 // takes GUI-active's.  It is also the sampler's READ-immune activity test for
 // the adaptive READ rate (SamplerConfig::pmc_idle_hz).
-constexpr uint32_t kPmcSetBase = (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcMfmaBusy);
+constexpr uint32_t kPmcSetBase =
+    (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcMfmaBusy) | (1u << kPmcCpcBusy);
 constexpr uint32_t kPmcSetFull = kPmcSetBase | (1u << kPmcTaBusy);
 // "base" | "full" → mask; 0 for an unknown name.
 uint32_t pmc_set_mask(const std::string& name);
@@ -148,6 +153,7 @@ struct MockPmcConfig {
   double clock_mhz = 2100;
   double mfma_frac = 0.6;       // fraction of active time the MFMA pipes are busy
   double vmem_frac = 0.3;       // fraction of active time the TA units are busy
+  double cpc_read_us = 2.0;     // CPC_CPC_STAT_BUSY time each READ adds (the real reader's own packet)
   uint32_t mask = kPmcSetFull;  // counters the mock "reads"
   int n_xcd = 8;                // per-XCD breakdown (0 = none)
   double xcd_skew = 0.0;        // XCD x is active (1 - skew·x) of XCD 0's cycles

@@ -157,6 +157,14 @@ struct Integrals {
   // interval with one epoch and a fresh drain (Sampler::run_pmfw).
   uint64_t pmc_epoch = 0;
   int64_t pmc_last_ns = 0;
+  // ∫ dispatch-in-flight fraction dt from the counter stream: per drain, the compute
+  // command processor's busy share of the clocks (CPC_CPC_STAT_BUSY) minus the time
+  // the exporter's own READ packet kept it busy (learned on intervals with no waves),
+  // never below the SPI-busy share; an interval the CP was busy for (nearly) all of
+  // counts whole.  dispatch_drains > 0 once the counter set carries CPC busy.
+  double dispatch_seconds = 0;
+  uint64_t dispatch_drains = 0;
+  double cpc_read_us = 0;       // the READ's own CP busy time as last learned (µs)
   // ∫ busy dt that does not count the exporter's own counter READs (the default
   // --sm-util-source auto behind container_gpu_sm_util / container_gpu_busy_seconds_total):
   // per PMFW interval, the counter tier's Δactive_seconds (GRBM_SPI_BUSY) while it

@@ -132,6 +132,9 @@ constexpr double kQuietActiveFrac = 0.02;
 // worth a drop to the idle READ rate (the first READ after it would come up to one
 // idle period late, and every tick in between is a lost sample).
 constexpr int64_t kQuietHoldNs = 5000000;
+// Dispatch-busy integral: a READ interval whose CPC busy share is at least this is a
+// dispatch in flight throughout (the READ's own CP time hides under the workload's).
+constexpr double kCpcFullFrac = 0.97;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };
@@ -237,6 +240,9 @@ struct DeviceState {
     a.active_seconds = b.active_seconds;
     a.pmc_epoch = b.pmc_epoch;
     a.pmc_last_ns = b.pmc_last_ns;
+    a.dispatch_seconds = b.dispatch_seconds;
+    a.dispatch_drains = b.dispatch_drains;
+    a.cpc_read_us = b.cpc_read_us;
     return a;
   }
 };
@@ -337,6 +343,7 @@ class Sampler {
   // PMFW sample (each device's PMFW thread only; survive pause/resume).
   struct UtilPrev {
     bool have = false;
+    bool dispatch = false;  // active_s holds dispatch_seconds (else active_seconds)
     uint64_t epoch = 0;
     double active_s = 0;
   };

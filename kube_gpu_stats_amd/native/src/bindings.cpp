@@ -68,6 +68,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.hang_heals_on_reset = get<bool>(m, "hang_heals_on_reset", c.mock_pmc.hang_heals_on_reset);
     c.mock_pmc.acquire_fail_dev = get<int>(m, "acquire_fail_dev", c.mock_pmc.acquire_fail_dev);
     c.mock_pmc.batch = get<int>(m, "batch", c.mock_pmc.batch);
+    c.mock_pmc.cpc_read_us = get<double>(m, "cpc_read_us", c.mock_pmc.cpc_read_us);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -256,6 +257,9 @@ class PyExporter {
     o["mfma_busy_seconds"] = I.mfma_busy_seconds;
     o["active_seconds"] = I.active_seconds;
     o["util_seconds"] = I.util_seconds;
+    o["dispatch_seconds"] = I.dispatch_seconds;
+    o["dispatch_drains"] = I.dispatch_drains;
+    o["cpc_read_us"] = I.cpc_read_us;
     o["util_counter_seconds"] = I.util_counter_seconds;
     o["pmc_epoch"] = I.pmc_epoch;
     {

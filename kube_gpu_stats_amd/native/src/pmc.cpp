@@ -19,9 +19,9 @@ namespace kgs {
 
 namespace {
 const char* const kNames[kPmcCount] = {
-    "GRBM_COUNT", "GRBM_SPI_BUSY", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY",
+    "GRBM_COUNT", "GRBM_SPI_BUSY", "SQ_VALU_MFMA_BUSY_CYCLES", "TA_TA_BUSY", "CPC_CPC_STAT_BUSY",
 };
-const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg};
+const int kReduce[kPmcCount] = {kReduceMax, kReduceMax, kReduceSum, kReduceAvg, kReduceMax};
 
 int64_t mono_ns() {
   timespec ts;
@@ -86,6 +86,7 @@ class MockCounterSource final : public CounterSource {
  public:
   MockCounterSource(const MockConfig& b, const MockPmcConfig& c, int n_dev)
       : b_(b), c_(c), t0_(mono_ns()), restart_(static_cast<size_t>(std::max(n_dev, 1)), 0),
+        restart_reads_(static_cast<size_t>(std::max(n_dev, 1)), 0),
         delayed_(static_cast<size_t>(std::max(n_dev, 1))) {
     for (int d = 0; d < std::max(n_dev, 1); ++d) fault_.push_back(std::make_unique<Fault>());
   }
@@ -96,6 +97,7 @@ class MockCounterSource final : public CounterSource {
     if (dev == c_.acquire_fail_dev && hung(dev)) return -1;
     if (fault_[static_cast<size_t>(dev)]->stalled.load()) return -1;  // START waits behind the stall too
     restart_[static_cast<size_t>(dev)] = mono_ns();
+    restart_reads_[static_cast<size_t>(dev)] = fault_[static_cast<size_t>(dev)]->samples.load();
     delayed_[static_cast<size_t>(dev)].clear();
     return 0;
   }
@@ -142,10 +144,11 @@ class MockCounterSource final : public CounterSource {
     const int64_t r = dev >= 0 && static_cast<size_t>(dev) < restart_.size() ? restart_[static_cast<size_t>(dev)] : 0;
     int64_t t = now;
     if (c_.freeze_after_s > 0) t = std::min(now, (r > 0 ? r : t0_) + static_cast<int64_t>(c_.freeze_after_s * 1e9));
-    fill(dev, t, s);
+    const uint64_t nreads = dev >= 0 && static_cast<size_t>(dev) < fault_.size() ? fault_[static_cast<size_t>(dev)]->samples.load() : 0;
+    fill(dev, t, s, nreads);
     if (r > 0) {
       PmcSample z;
-      fill(dev, r, z);
+      fill(dev, r, z, restart_reads_[static_cast<size_t>(dev)]);
       for (int i = 0; i < kPmcCount; ++i) s.value[i] -= std::min(s.value[i], z.value[i]);
       for (uint32_t x = 0; x < s.n_xcd; ++x) {
         s.xcd_active[x] -= std::min(s.xcd_active[x], z.xcd_active[x]);
@@ -167,7 +170,7 @@ class MockCounterSource final : public CounterSource {
 
  private:
   // Cumulative counts since the source opened, at time `now`.
-  void fill(int dev, int64_t now, PmcSample& s) const {
+  void fill(int dev, int64_t now, PmcSample& s, uint64_t reads) const {
     const double t = (now - t0_) * 1e-9;
     // ∫ util/100 dt (fraction-seconds): the mock backend's load curve for this device
     const double busy_s = mock_device_util_integral(b_, dev, t) / 100.0;
@@ -177,6 +180,8 @@ class MockCounterSource final : public CounterSource {
     s.value[kPmcGrbmActive] = static_cast<uint64_t>(clk * busy_s);
     s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
     s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac);
+    // The CP is busy while the load runs, plus cpc_read_us for each READ so far.
+    s.value[kPmcCpcBusy] = static_cast<uint64_t>(clk * (busy_s + c_.cpc_read_us * 1e-6 * static_cast<double>(reads)));
     s.mask = c_.mask;
     for (int i = 0; i < kPmcCount; ++i)
       if (!(s.mask & (1u << i))) s.value[i] = 0;
@@ -219,6 +224,7 @@ class MockCounterSource final : public CounterSource {
   MockPmcConfig c_;
   int64_t t0_;
   std::vector<int64_t> restart_;  // per device: time of the last acquire (0 = never released)
+  std::vector<uint64_t> restart_reads_;  // per device: samples taken at the last acquire
   std::vector<std::deque<PmcSample>> delayed_;  // per device: samples held back (MockPmcConfig::batch)
   std::vector<std::unique_ptr<Fault>> fault_;
 };

@@ -648,6 +648,22 @@ void Exporter::render(std::string& out) {
            "Integral of the GPU-active share of clocks (GRBM_SPI_BUSY, hardware counters) over time; rate() = GPU-active "
            "fraction, blind to the exporter's own counter READs");
     for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_gpu_active_seconds_total", dev_labels_[d], nullptr, snaps[d].I.active_seconds);
+    bool any_disp = false;
+    for (int d : ids) any_disp |= snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0;
+    if (any_disp) {
+      w.head("amdgpu_dispatch_busy_seconds_total", "counter",
+             "Integral of the dispatch-in-flight share of time (CPC_CPC_STAT_BUSY less the exporter's own READ "
+             "packets, never below GRBM_SPI_BUSY); rate() = the READ-immune 'a kernel is running' fraction");
+      for (int d : ids)
+        if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
+          w.line("amdgpu_dispatch_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.dispatch_seconds);
+      w.head("kgs_pmc_read_cp_seconds", "gauge",
+             "Command-processor busy time one counter READ packet costs, as learned on intervals with no waves "
+             "(subtracted from CPC busy in amdgpu_dispatch_busy_seconds_total)");
+      for (int d : ids)
+        if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
+          w.line("kgs_pmc_read_cp_seconds", dev_labels_[d], nullptr, snaps[d].I.cpc_read_us * 1e-6);
+    }
     w.head("amdgpu_mfma_busy_seconds_total", "counter",
            "Integral of the MFMA-busy share of all SIMD cycles over time (hardware counters); rate() = matrix-core utilisation");
     for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);

@@ -380,15 +380,19 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
 // while the device's counter tier ran through the whole interval — same epoch as at
 // the previous PMFW sample, counters held and not stalled, a drain no older than
 // three of its slowest READ periods — the interval is billed the counter tier's
-// Δactive_seconds (GRBM_SPI_BUSY: waves in a shader engine, blind to the exporter's
-// own READ packets), else the PMFW GFX busy (a dispatch in flight; counts each READ
-// as ≈80 µs of work, profiles/r2/idle_busy/).  Either way the integral is exact
-// over any range covered by one source, and monotonic.
+// Δdispatch_seconds (CP busy less the exporter's own READ packets: a dispatch in
+// flight, the PMFW busy's meaning; Δactive_seconds, waves in a shader engine, for a
+// counter set without CPC busy), else the PMFW GFX busy (a dispatch in flight, but
+// counting each READ as ≈80 µs of work, profiles/r2/idle_busy/).  Either way the
+// integral is exact over any range covered by one source, and monotonic.
 void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, Integrals& I, GpuSample& s) {
   DeviceState& st = *states_[static_cast<size_t>(dev)];
   UtilPrev& up = util_prev_[static_cast<size_t>(dev)];
   Integrals pc;
   st.pmc_integ.load(pc);
+  // The counter tier's busy integral: dispatch in flight (CP busy less our READs)
+  // when the counter set has CPC busy, else waves in a shader engine (SPI busy).
+  const double cnt_busy = pc.dispatch_drains > 0 ? pc.dispatch_seconds : pc.active_seconds;
   double slow_hz = hz_.load(std::memory_order_relaxed);
   const double idle = pmc_idle_hz_.load(std::memory_order_relaxed);
   if (idle > 0) slow_hz = std::min(slow_hz, idle);
@@ -400,8 +404,9 @@ void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, In
                   now - pc.pmc_last_ns <= fresh_ns;
   double du = 0;
   if (dt_s > 0) {
-    if (ok && up.have && up.epoch == pc.pmc_epoch && pc.active_seconds >= up.active_s) {
-      du = std::min(pc.active_seconds - up.active_s, dt_s);
+    if (ok && up.have && up.epoch == pc.pmc_epoch && up.dispatch == (pc.dispatch_drains > 0) &&
+        cnt_busy >= up.active_s) {
+      du = std::min(cnt_busy - up.active_s, dt_s);
       I.util_counter_seconds += dt_s;
     } else {
       du = std::clamp(dgfx_s, 0.0, dt_s);
@@ -409,8 +414,9 @@ void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, In
   }
   I.util_seconds += du;
   up.have = ok;
+  up.dispatch = pc.dispatch_drains > 0;
   up.epoch = pc.pmc_epoch;
-  up.active_s = pc.active_seconds;
+  up.active_s = cnt_busy;
   s.cum_util_s = I.util_seconds;
   s.util_window_pct = dt_s > 0 ? static_cast<float>(100.0 * du / dt_s) : -1.0f;
 }
@@ -553,7 +559,11 @@ void Sampler::run_pmc(Worker& w) {
   int64_t next = mono_ns();
   PmcSample& pmc_base = st.pmc_base;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
-  uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0;
+  uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0, prev_ps_cpc = 0;
+  // The READ packet's own CPC busy (clock cycles), learned on intervals without waves,
+  // separately for synchronous (quiet GPU) and pipelined READs: EWMA and samples seen.
+  double read_cyc[2] = {0, 0};
+  uint64_t read_cyc_n[2] = {0, 0};
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
   int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
@@ -567,7 +577,7 @@ void Sampler::run_pmc(Worker& w) {
   // READ is then counted exactly (acquire → first READ was dropped).
   auto started_at = [&](int64_t t) {
     have_prev_ps = true;
-    prev_ps_count = prev_ps_mfma = prev_ps_active = 0;
+    prev_ps_count = prev_ps_mfma = prev_ps_active = prev_ps_cpc = 0;
     prev_ps_ns = t;
     quiet = false;
     quiet_since_ns = 0;
@@ -696,6 +706,26 @@ void Sampler::run_pmc(Worker& w) {
                               static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
           P.active_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
         }
+        // Dispatch in flight (Integrals::dispatch_seconds): the CP busy share of the
+        // interval, less the READ packet's own CP time, never below the SPI share.
+        if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcCpcBusy)) &&
+            ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcCpcBusy] >= prev_ps_cpc) {
+          const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
+          const double cpc = std::min(clk, static_cast<double>(ps.value[kPmcCpcBusy] - prev_ps_cpc));
+          const double act = (ps.mask & (1u << kPmcGrbmActive)) && ps.value[kPmcGrbmActive] >= prev_ps_active
+                                 ? static_cast<double>(ps.value[kPmcGrbmActive] - prev_ps_active)
+                                 : 0.0;
+          const int m = fresh_mode ? 1 : 0;
+          // No wave, no MFMA cycle and the CP mostly idle: the CP busy here is our READ's.
+          if (act < 0.005 * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma && cpc < 0.5 * clk) {
+            read_cyc[m] = read_cyc_n[m] ? 0.95 * read_cyc[m] + 0.05 * cpc : cpc;
+            ++read_cyc_n[m];
+            P.cpc_read_us = read_cyc[m] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
+          }
+          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(act, std::max(0.0, cpc - read_cyc[m]));
+          P.dispatch_seconds += std::min(1.0, busy / clk) * (ps.mono_ns - prev_ps_ns) * 1e-9;
+          ++P.dispatch_drains;
+        }
         // Quiet = a shader engine had waves for < kQuietActiveFrac of the clocks
         // since the previous READ, and no MFMA cycle ran.  Both counters are
         // (nearly) blind to our own READs: SPI busy reads 0.65 % with nothing but
@@ -738,6 +768,7 @@ void Sampler::run_pmc(Worker& w) {
         prev_ps_count = ps.value[kPmcGrbmCount];
         prev_ps_mfma = ps.value[kPmcMfmaBusy];
         prev_ps_active = ps.value[kPmcGrbmActive];
+        prev_ps_cpc = ps.value[kPmcCpcBusy];
         prev_ps_ns = ps.mono_ns;
         have_prev_ps = true;
         const int64_t stall = ps.mono_ns - last_plausible_ns;

@@ -337,3 +337,25 @@ def test_sm_util_pmfw_source_keeps_the_firmware_busy(mock_exporter):
     m = parse_text(ex.render())
     (_, sm), = m["container_gpu_sm_util"]
     assert sm > 98
+
+
+def test_dispatch_busy_learns_and_removes_the_reads_cp_time(mock_exporter):
+    """The dispatch-in-flight integral behind --sm-util-source auto: CPC busy counts a
+    dispatch in flight and, for a short fixed time, every counter READ packet (the
+    mock: 20 µs per READ, 4 % of the time at 2 kHz).  The sampler learns that time on
+    intervals without waves (kgs_pmc_read_cp_seconds) and subtracts it, so a 25 %-duty
+    square load integrates to 25 %, not 29-ish."""
+    ex = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", pmc_idle_hz=0, window_s=1.0,
+                       mock={"square_duty": 0.25, "util_base": 50, "util_amp": 50, "util_period_s": 0.2},
+                       mock_pmc={"cpc_read_us": 20.0})
+    time.sleep(0.5)
+    a, t0 = ex.integrals(0), time.time()
+    time.sleep(1.6)
+    b, dt = ex.integrals(0), time.time() - t0
+    assert b["dispatch_drains"] > 1000
+    assert (b["dispatch_seconds"] - a["dispatch_seconds"]) / dt == pytest.approx(0.25, abs=0.02)
+    m = parse_text(ex.render())
+    (_, cp), = m["kgs_pmc_read_cp_seconds"]
+    assert cp == pytest.approx(20e-6, rel=0.1)
+    raw = {lb["counter"]: v for lb, v in m["amdgpu_pmc_total"]}
+    assert raw["CPC_CPC_STAT_BUSY"] > raw["GRBM_SPI_BUSY"]  # the READs' own CP time is in the raw count

@@ -247,13 +247,14 @@ def test_counter_window_covers_full_window_at_high_rate(mock_exporter):
 
 
 def test_pmc_counter_sets(N, mock_exporter):
-    """base set (default): GRBM clocks + SPI busy + MFMA busy — no TA, so no vmem gauge; full adds TA."""
+    """base set (default): GRBM clocks + SPI busy + MFMA busy + CPC busy (the dispatch-in-flight
+    signal, round 4) — no TA, so no vmem gauge; full adds TA."""
     base = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0)
     full = mock_exporter(n_gpus=1, hz=500, pmc_source="mock", proc_every=0, link_every=0, pmc_set="full")
     time.sleep(0.4)
     mb, mf = parse_text(base.render()), parse_text(full.render())
     assert {lb["counter"] for lb, _ in mb["amdgpu_pmc_total"]} == {"GRBM_COUNT", "GRBM_SPI_BUSY",
-                                                                   "SQ_VALU_MFMA_BUSY_CYCLES"}
+                                                                   "SQ_VALU_MFMA_BUSY_CYCLES", "CPC_CPC_STAT_BUSY"}
     assert "TA_TA_BUSY" in {lb["counter"] for lb, _ in mf["amdgpu_pmc_total"]}
     assert "amdgpu_vmem_busy_percent" not in mb and abs(mf["amdgpu_vmem_busy_percent"][0][1] - 30) < 3
     assert abs(mb["amdgpu_mfma_util_percent"][0][1] - 60) < 3

@@ -4,6 +4,7 @@
 # abort (rc >= 124) does — nothing else touches the GPU after that.
 #   gpurun --timeout 1100 -- 'bash tools/gpu_check.sh <tag> [steps...]'
 # steps (default: probe tests smoke bench): probe probe3 tests smoke bench bench2 rocprof
+#   round 4: smprobe cpprobe graphcost testsnw wedge (the wedged-queue test last, alone)
 set -u
 TAG=${1:-r2}; shift || true
 STEPS=${*:-probe tests smoke bench}
@@ -66,6 +67,14 @@ for s in $STEPS; do
     probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
            run probe_xgmi 90 python tools/probe_xgmi.py ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider ;;
+    # round 4
+    smprobe) run sm_util_probe 300 python -u tools/sm_util_probe.py --out "$OUT/sm_util_probe.json" ;;
+    cpprobe) run cp_busy_probe 240 python -u tools/cp_busy_probe.py --out "$OUT/cp_busy_probe.json" ;;
+    graphcost) run graph_cost 400 python -u tools/graph_cost_probe.py --out "$OUT/graph_cost.json" ;;
+    testsnw) run pytest_gpu 700 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
+               -p no:cacheprovider -k "not wedged_counter_queue" ;;
+    wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+             -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" ;;
     bench2) run bench_b 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench_b.json" ;;

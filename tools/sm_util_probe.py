@@ -153,6 +153,8 @@ def measure(loads: Loads, sc, names: list[str], secs: float) -> dict:
         row = {"host_busy_pct": round(100 * busy_s / wall, 2),
                "pmfw_gfx_busy_pct": round(100 * d("amdgpu_pmfw_gfx_busy_seconds_total") / wall, 2),
                "spi_active_pct": round(100 * d("amdgpu_gpu_active_seconds_total") / wall, 2),
+               "dispatch_pct": round(100 * d("amdgpu_dispatch_busy_seconds_total") / wall, 2),
+               "read_cp_us": round(1e6 * (one(m1, "kgs_pmc_read_cp_seconds") or 0.0), 2),
                "spi_share_of_clocks_pct": round(100 * d("amdgpu_pmc_total", counter="GRBM_SPI_BUSY") / clk, 2)
                if clk > 0 else None,
                "mfma_busy_pct": round(100 * d("amdgpu_mfma_busy_seconds_total") / wall, 2),
