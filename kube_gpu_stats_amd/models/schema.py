@@ -108,8 +108,10 @@ CATALOG: tuple[Family, ...] = (
       extra=("source",), source="self"),
     F("amdgpu_umc_busy_seconds_total", "counter", "∫ UMC busy fraction dt."),
     F("amdgpu_hbm_bandwidth_bytes_per_second", "gauge",
-      "HBM read+write bandwidth, window mean, from UMC activity × the MI355X calibration (1 % = 84.1 GB/s, "
-      "±0.6 % over stream loads of 3.1–5.5 TB/s; profiles/umc_calib.md)."),
+      "Estimated HBM (DRAM) read+write bandwidth, window mean, from UMC activity × the MI355X calibration "
+      "(1 % = 84.1 GB/s): within ±2.5 % of the bytes streaming kernels move; random 64 B gathers read 2.0× their "
+      "requested bytes (each costs a 128 B DRAM access, which is real HBM traffic); cache (L2 / MALL) hits are not "
+      "counted (profiles/umc_calib.md)."),
     F("amdgpu_hbm_bytes_total", "counter",
       "HBM bytes moved (read+write), ∫ bandwidth dt from the UMC accumulators; rate() = bandwidth."),
     # ---- memory ------------------------------------------------------------------------------

@@ -484,7 +484,8 @@ void Exporter::render(std::string& out) {
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_umc_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds);
   const double full_bw = cfg_.hbm_bytes_per_s_at_full_umc;
   w.head("amdgpu_hbm_bandwidth_bytes_per_second", "gauge",
-         "HBM read+write bandwidth over the exporter window, from UMC activity (MI355X calibration: 1 % = 84.1 GB/s)");
+         "Estimated HBM (DRAM) read+write bandwidth over the exporter window, from UMC activity (MI355X calibration: "
+         "1 % = 84.1 GB/s; streams +-2.5 %, 64 B gathers count their 128 B DRAM accesses, cache hits are not counted)");
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_hbm_bandwidth_bytes_per_second", dev_labels_[d], nullptr, snaps[d].u * 0.01 * full_bw);
   w.head("amdgpu_hbm_bytes_total", "counter", "HBM bytes moved (read+write), integral of the UMC-derived bandwidth");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_hbm_bytes_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds * full_bw);
