@@ -371,20 +371,9 @@ bool poll_signals() {
   return on;
 }
 
-// Scheduling priority of the private READ queue (KGS_AQL_PRIORITY = low | normal |
-// high; unset = ROCr's default, normal).  The CP firmware arbitrates between the
-// compute queues mapped on a pipe; a low-priority READ queue should yield to a
-// dispatch-bound workload queue (profiles/launch_overhead.md).
-int queue_priority() {
-  static const int v = [] {
-    const char* e = std::getenv("KGS_AQL_PRIORITY");
-    if (!e) return -1;
-    if (std::strcmp(e, "low") == 0) return static_cast<int>(HSA_AMD_QUEUE_PRIORITY_LOW);
-    if (std::strcmp(e, "high") == 0) return static_cast<int>(HSA_AMD_QUEUE_PRIORITY_HIGH);
-    return static_cast<int>(HSA_AMD_QUEUE_PRIORITY_NORMAL);
-  }();
-  return v;
-}
+// (No READ-queue priority switch: low / normal / high changed nothing measurable
+// against a dispatch-bound stream, profiles/launch_overhead.md r2af and
+// profiles/r4/ r4c.  The cost is the CP's handling of each packet.)
 
 // KGS_AQL_PROFILE=<n>: report READ timestamps every n pipelined READs (0/unset = off).
 uint64_t profile_every() {
@@ -792,14 +781,10 @@ constexpr uint32_t kUnlanded = 0xFFFFFFFFu;
 
 bool is_publisher(const Agent* a, int k) { return a->batch < 2 || a->plan.is_publisher(k); }
 
-// KGS_AQL_NOBARRIER=1 (experiment): non-publisher READs without the AQL barrier
-// bit, so the packet processor need not wait for the previous READ's completion
-// before taking the next; the publisher keeps it (it must follow every READ of
-// its half for its writeback to cover them).
-bool nonpub_barrier() {
-  static const bool on = std::getenv("KGS_AQL_NOBARRIER") == nullptr;
-  return on;
-}
+// Every READ keeps the AQL barrier bit: dropping it on a batch's non-publisher
+// READs (the round-3 KGS_AQL_NOBARRIER experiment) cost a µs-kernel stream the same
+// 3.8 % at 8 kHz (profiles/r4/ r4c), and the publisher's writeback must follow
+// every READ of its half anyway.
 
 // Rebuild the session-layout part of kgs_pmc_info (handle's thread only; called
 // when the layout changes: open, mode switch, the first fold of an event list).
@@ -813,8 +798,6 @@ void snap_info(Agent* a) {
                   ";pipelined=" + std::to_string(a->pipelined ? 1 : 0) + ";lean=" + std::to_string(lean_mode()) + ":" +
                   std::to_string(a->lean_changed) + ";batch=" + std::to_string(a->batch) +
                   ";xcd=" + std::to_string(__builtin_popcount(placed)) + ":" + a->xcd_from;
-  if (!nonpub_barrier()) o += a->batch >= 2 ? ";nobarrier=1" : ";nobarrier=ignored(batch<2)";
-  if (queue_priority() >= 0) o += ";priority=" + std::to_string(queue_priority());
   for (size_t k = 0; k < a->names.size(); ++k)
     o += ";" + a->names[k] + "=" + std::to_string(k < a->instances.size() ? a->instances[k] : 0);
   std::lock_guard<std::mutex> g(a->info_mu);
@@ -917,7 +900,7 @@ int read_batched(Agent* a, int64_t* ts) {
   a->psubmit_ns[k] = mono_ns();
   const std::pair<int, int> none{HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_NONE};
   const bool pub = p.is_publisher(k);
-  if (enqueue(a, a->pread[k], a->psig[k], pub ? read_fences() : none, pub || nonpub_barrier()) != 0) {
+  if (enqueue(a, a->pread[k], a->psig[k], pub ? read_fences() : none) != 0) {
     if (p.last() >= 0) wait_done(a, a->psig[p.last()]);
     batch_reset(a);
     return -2;
@@ -1108,10 +1091,6 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
         return -1;
       }
       if (profile_ts()) hsa_amd_profiling_set_profiler_enabled(a->queue, 1);
-      if (queue_priority() >= 0 &&
-          hsa_amd_queue_set_priority(a->queue, static_cast<hsa_amd_queue_priority_t>(queue_priority())) !=
-              HSA_STATUS_SUCCESS)
-        KGS_DBG("hsa_amd_queue_set_priority(%d) failed\n", queue_priority());
     }
     if (!a->sig.handle && hsa_signal_create(1, 0, nullptr, &a->sig) != HSA_STATUS_SUCCESS) {  // kept across resets
       set_err(err, errlen, "hsa_signal_create failed");

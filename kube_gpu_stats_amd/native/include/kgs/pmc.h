@@ -154,6 +154,7 @@ struct MockPmcConfig {
   double mfma_frac = 0.6;       // fraction of active time the MFMA pipes are busy
   double vmem_frac = 0.3;       // fraction of active time the TA units are busy
   double cpc_read_us = 2.0;     // CPC_CPC_STAT_BUSY time each READ adds (the real reader's own packet)
+  double wave_frac = 1.0;       // share of the CP-busy time with waves in a shader engine (< 1: µs-kernel stream)
   uint32_t mask = kPmcSetFull;  // counters the mock "reads"
   int n_xcd = 8;                // per-XCD breakdown (0 = none)
   double xcd_skew = 0.0;        // XCD x is active (1 - skew·x) of XCD 0's cycles

@@ -98,8 +98,22 @@ struct SamplerConfig {
   // counters); only the time resolution of those stretches drops.  Off in
   // profiling mode (pmc_idle_hz 0) and with pmc_busy_min 0.
   double pmc_busy_min = 0.0;
-  double pmc_gap_hz = 1000.0;
+  double pmc_gap_hz = 500.0;
   double pmc_gap_hold_s = 0.001;
+  // Dispatch-bound READ rate (needs CPC busy in the counter set).  A GPU that
+  // runs nothing but µs kernels back to back keeps the command processor busy
+  // while its shader engines hold waves only part of the time (a HIP graph of
+  // 1.7 µs copies: CPC busy ≈100 %, SPI busy ≈41 %; long MFMA, GEMM or HBM
+  // kernels: the two within ≈8 points, profiles/r4/).  That stream is exactly the
+  // one each READ packet slows (+3.8 … 4.2 % at 8 kHz, +0.5 % at 1 kHz,
+  // +0.05 % at 100 Hz; profiles/r4/ r4c, r4d).  While the
+  // READ intervals of the last pmc_dispatch_hold_s had the CP dispatching with no
+  // wave in flight for at least pmc_cp_only_min of their clocks, READs drop to
+  // pmc_gap_hz; the first interval below restores every tick.  The hold keeps a
+  // few ms of small kernels inside a training step at full rate.  0 = off; off
+  // in profiling mode.
+  double pmc_cp_only_min = 0.3;
+  double pmc_dispatch_hold_s = 0.004;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
   // Counter-tier circuit breaker: consecutive failed drains that open it, and the
@@ -180,6 +194,7 @@ struct DeviceState {
   std::atomic<int> pmc_quiet{0};            // last READ interval had no wave: READs at pmc_idle_hz
   std::atomic<uint64_t> pmc_quiet_skips{0};  // ticks that skipped their READ while quiet
   std::atomic<int> pmc_gap{0};               // READ intervals below pmc_busy_min: READs at pmc_gap_hz
+  std::atomic<int> pmc_dbound{0};            // dispatch-bound (pmc_cp_only_min): READs at pmc_gap_hz too
   std::atomic<uint64_t> pmc_gap_skips{0};    // ticks that skipped their READ in a dispatch gap
   // Counter-tier fault boundary (sampler.h header comment).
   std::atomic<int> pmc_failed{0};            // breaker open: no READs until a retry succeeds
@@ -332,7 +347,7 @@ class Sampler {
   std::atomic<uint64_t> slow_passes_{0};
   std::atomic<double> pmc_idle_hz_{0.0};
   std::atomic<double> pmc_busy_min_{0.0};
-  std::atomic<double> pmc_gap_hz_{1000.0};
+  std::atomic<double> pmc_gap_hz_{500.0};
   mutable std::mutex pid_pods_mu_;
   std::shared_ptr<const std::unordered_map<uint64_t, std::string>> pid_pods_;
   std::vector<std::map<std::string, double>> pod_cu_;  // device's slow thread only

@@ -69,6 +69,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.acquire_fail_dev = get<int>(m, "acquire_fail_dev", c.mock_pmc.acquire_fail_dev);
     c.mock_pmc.batch = get<int>(m, "batch", c.mock_pmc.batch);
     c.mock_pmc.cpc_read_us = get<double>(m, "cpc_read_us", c.mock_pmc.cpc_read_us);
+    c.mock_pmc.wave_frac = get<double>(m, "wave_frac", c.mock_pmc.wave_frac);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -84,6 +85,8 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmc_busy_min = get<double>(d, "pmc_busy_min", c.sampler.pmc_busy_min);
   c.sampler.pmc_gap_hz = get<double>(d, "pmc_gap_hz", c.sampler.pmc_gap_hz);
   c.sampler.pmc_gap_hold_s = get<double>(d, "pmc_gap_hold_s", c.sampler.pmc_gap_hold_s);
+  c.sampler.pmc_cp_only_min = get<double>(d, "pmc_cp_only_min", c.sampler.pmc_cp_only_min);
+  c.sampler.pmc_dispatch_hold_s = get<double>(d, "pmc_dispatch_hold_s", c.sampler.pmc_dispatch_hold_s);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
   c.sampler.pmc_breaker_k = get<int>(d, "pmc_breaker_k", c.sampler.pmc_breaker_k);
   c.sampler.pmc_retry_s = get<double>(d, "pmc_retry_s", c.sampler.pmc_retry_s);
@@ -275,6 +278,7 @@ class PyExporter {
     o["pmc_quiet_skips"] = st.pmc_quiet_skips.load();
     o["pmc_gap"] = st.pmc_gap.load();
     o["pmc_gap_skips"] = st.pmc_gap_skips.load();
+    o["pmc_dispatch_bound"] = st.pmc_dbound.load();
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
     o["pmc_on"] = st.pmc_on.load();
@@ -522,7 +526,7 @@ PYBIND11_MODULE(_kgs_native, m) {
             if (e.sampler() && !e.sampler()->set_pmc_gap(busy_min, hz))
               throw py::value_error("busy_min must be within [0, 1] and hz within (0, 100000]");
           },
-          py::arg("busy_min"), py::arg("hz") = 1000.0,
+          py::arg("busy_min"), py::arg("hz") = 500.0,
           "Dispatch-gap READ rate: READs at hz while the SPI-busy share stays below busy_min (0 = off)")
       .def_property_readonly("pmc_busy_min",
                              [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_busy_min() : 0.0; })

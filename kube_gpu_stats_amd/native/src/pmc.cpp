@@ -177,9 +177,10 @@ class MockCounterSource final : public CounterSource {
     const double clk = c_.clock_mhz * 1e6;
     s.n = kPmcCount;
     s.value[kPmcGrbmCount] = static_cast<uint64_t>(clk * t);
-    s.value[kPmcGrbmActive] = static_cast<uint64_t>(clk * busy_s);
-    s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * busy_s * c_.mfma_frac * 1024.0);
-    s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * busy_s * c_.vmem_frac);
+    const double wave_s = busy_s * std::clamp(c_.wave_frac, 0.0, 1.0);  // waves present
+    s.value[kPmcGrbmActive] = static_cast<uint64_t>(clk * wave_s);
+    s.value[kPmcMfmaBusy] = static_cast<uint64_t>(clk * wave_s * c_.mfma_frac * 1024.0);
+    s.value[kPmcTaBusy] = static_cast<uint64_t>(clk * wave_s * c_.vmem_frac);
     // The CP is busy while the load runs, plus cpc_read_us for each READ so far.
     s.value[kPmcCpcBusy] = static_cast<uint64_t>(clk * (busy_s + c_.cpc_read_us * 1e-6 * static_cast<double>(reads)));
     s.mask = c_.mask;
@@ -192,10 +193,10 @@ class MockCounterSource final : public CounterSource {
     for (uint32_t x = 0; x < s.n_xcd; ++x) wsum += 1.0 - c_.xcd_skew * x;
     for (uint32_t x = 0; x < s.n_xcd; ++x) {
       const double w = 1.0 - c_.xcd_skew * x;
-      s.xcd_active[x] = static_cast<uint64_t>(clk * busy_s * w);
+      s.xcd_active[x] = static_cast<uint64_t>(clk * wave_s * w);
       s.xcd_mfma[x] = wsum > 0 ? static_cast<uint64_t>(s.value[kPmcMfmaBusy] * (w / wsum)) : 0;
       // TA: vmem_frac of the XCD's active cycles on each of its 32 CUs (256-CU mock)
-      s.xcd_ta[x] = (s.mask & (1u << kPmcTaBusy)) ? static_cast<uint64_t>(clk * busy_s * w * c_.vmem_frac * 32.0) : 0;
+      s.xcd_ta[x] = (s.mask & (1u << kPmcTaBusy)) ? static_cast<uint64_t>(clk * wave_s * w * c_.vmem_frac * 32.0) : 0;
     }
   }
 

@@ -802,7 +802,13 @@ void Exporter::render(std::string& out) {
            "1 while the counter READ intervals had waves for less than --pmc-busy-min of their clocks (a dispatch-bound "
            "or gappy kernel stream): READs run at --pmc-gap-hz, since each READ packet delays the workload's dispatches");
     for (int d : ids) w.line_u("kgs_pmc_gap", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_gap.load()));
-    w.head("kgs_pmc_gap_skips_total", "counter", "Sampler ticks that skipped their counter READ in a dispatch gap");
+    w.head("kgs_pmc_dispatch_bound", "gauge",
+           "1 while the command processor dispatched with no wave in flight for at least --pmc-cp-only-min of the "
+           "clocks (a stream of µs kernels, which each READ packet slows): READs run at --pmc-gap-hz");
+    for (int d : ids)
+      w.line_u("kgs_pmc_dispatch_bound", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_dbound.load()));
+    w.head("kgs_pmc_gap_skips_total", "counter",
+           "Sampler ticks that skipped their counter READ in a dispatch gap or a dispatch-bound stream");
     for (int d : ids) w.line_u("kgs_pmc_gap_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_gap_skips.load());
     w.head("kgs_pmc_failed", "gauge",
            "1 while the counter tier's circuit breaker is open: consecutive counter drains failed (a wedged command "

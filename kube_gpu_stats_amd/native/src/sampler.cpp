@@ -101,8 +101,10 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
   if (cfg_.pmc_retry_max_s < cfg_.pmc_retry_s) cfg_.pmc_retry_max_s = cfg_.pmc_retry_s;
   const double ih = cfg_.pmc_idle_hz;
   pmc_idle_hz_.store(!(ih > 0) ? 0.0 : std::clamp(ih, kMinIdleHz, kMaxHz));
-  if (!set_pmc_gap(cfg_.pmc_busy_min, cfg_.pmc_gap_hz)) set_pmc_gap(0.0, 1000.0);
+  if (!set_pmc_gap(cfg_.pmc_busy_min, cfg_.pmc_gap_hz)) set_pmc_gap(0.0, 500.0);
   if (!(cfg_.pmc_gap_hold_s >= 0)) cfg_.pmc_gap_hold_s = 0.0;
+  if (!(cfg_.pmc_cp_only_min >= 0 && cfg_.pmc_cp_only_min <= 1)) cfg_.pmc_cp_only_min = 0.0;
+  if (!(cfg_.pmc_dispatch_hold_s >= 0)) cfg_.pmc_dispatch_hold_s = 0.0;
   for (int d : dev_ids_) {
     DeviceState& st = *states_[static_cast<size_t>(d)];
     st.pmc_on.store(cfg_.pmc && pmc_ ? 1 : 0);
@@ -396,7 +398,7 @@ void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, In
   double slow_hz = hz_.load(std::memory_order_relaxed);
   const double idle = pmc_idle_hz_.load(std::memory_order_relaxed);
   if (idle > 0) slow_hz = std::min(slow_hz, idle);
-  if (pmc_busy_min_.load(std::memory_order_relaxed) > 0 && idle > 0)
+  if ((pmc_busy_min_.load(std::memory_order_relaxed) > 0 || cfg_.pmc_cp_only_min > 0) && idle > 0)
     slow_hz = std::min(slow_hz, pmc_gap_hz_.load(std::memory_order_relaxed));
   const int64_t fresh_ns = static_cast<int64_t>(3e9 / slow_hz) + 50000000LL;
   const bool ok = st.pmc_on.load(std::memory_order_relaxed) && !st.pmc_stalled.load(std::memory_order_relaxed) &&
@@ -555,7 +557,9 @@ void Sampler::run_pmc(Worker& w) {
   }
   st.pmc_quiet.store(0, std::memory_order_relaxed);
   st.pmc_gap.store(0, std::memory_order_relaxed);
+  st.pmc_dbound.store(0, std::memory_order_relaxed);
   const int64_t gap_hold_ns = static_cast<int64_t>(cfg_.pmc_gap_hold_s * 1e9);
+  const int64_t dbound_hold_ns = static_cast<int64_t>(cfg_.pmc_dispatch_hold_s * 1e9);
   int64_t next = mono_ns();
   PmcSample& pmc_base = st.pmc_base;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
@@ -569,6 +573,8 @@ void Sampler::run_pmc(Worker& w) {
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
   bool gap = false;                  // dispatch-gap READ rate (SamplerConfig::pmc_busy_min)
   int64_t gap_since_ns = 0;          // start of the current run of low-occupancy intervals (0 = none)
+  bool dbound = false;               // dispatch-bound READ rate (SamplerConfig::pmc_cp_only_min)
+  int64_t dbound_since_ns = 0;       // start of the current run of dispatch-bound intervals (0 = none)
   int64_t last_pmc_ns = 0;
   int64_t prev_ps_ns = 0;
   int64_t last_plausible_ns = mono_ns();
@@ -583,6 +589,8 @@ void Sampler::run_pmc(Worker& w) {
     quiet_since_ns = 0;
     gap = false;
     gap_since_ns = 0;
+    dbound = false;
+    dbound_since_ns = 0;
     fresh_mode = false;  // a (re)opened session reads pipelined
     last_plausible_ns = t;
     last_start_ns = t;
@@ -603,6 +611,7 @@ void Sampler::run_pmc(Worker& w) {
     st.pmc_stalled.store(0);
     st.pmc_quiet.store(0, std::memory_order_relaxed);
     st.pmc_gap.store(0, std::memory_order_relaxed);
+    st.pmc_dbound.store(0, std::memory_order_relaxed);
     st.pmc_fail_streak = 0;
     st.pmc_retry_at_ns = now + static_cast<int64_t>(st.pmc_backoff_s * 1e9);
     st.pmc_backoff_s = std::min(st.pmc_backoff_s * 2, cfg_.pmc_retry_max_s);
@@ -657,7 +666,7 @@ void Sampler::run_pmc(Worker& w) {
       }
     }
     bool pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
-    if (pmc_now && (quiet || gap)) {
+    if (pmc_now && (quiet || gap || dbound)) {
       // Quiet (no waves) READs at the idle rate, a dispatch gap at the gap rate;
       // profiling mode (idle rate 0) READs every tick.
       const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
@@ -708,6 +717,7 @@ void Sampler::run_pmc(Worker& w) {
         }
         // Dispatch in flight (Integrals::dispatch_seconds): the CP busy share of the
         // interval, less the READ packet's own CP time, never below the SPI share.
+        bool dbound_interval = false;
         if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcCpcBusy)) &&
             ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcCpcBusy] >= prev_ps_cpc) {
           const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
@@ -722,9 +732,18 @@ void Sampler::run_pmc(Worker& w) {
             ++read_cyc_n[m];
             P.cpc_read_us = read_cyc[m] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
           }
-          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(act, std::max(0.0, cpc - read_cyc[m]));
+          // The READ's own CP time lands anywhere in the interval: where the CP was busy
+          // dispatching anyway it adds nothing (busy counts once), so it adds
+          // read·(1 − busy/clk) and busy = (cpc − read) / (1 − read/clk) — exact at
+          // both ends (idle: cpc = read → 0; saturated: cpc = clk → clk).
+          const double rc = std::min(read_cyc[m], 0.5 * clk);
+          const double busy = cpc >= kCpcFullFrac * clk
+                                  ? clk
+                                  : std::max(act, std::max(0.0, (cpc - rc) / (1.0 - rc / clk)));
           P.dispatch_seconds += std::min(1.0, busy / clk) * (ps.mono_ns - prev_ps_ns) * 1e-9;
           ++P.dispatch_drains;
+          // Dispatch-bound: the CP dispatching with no wave in flight for a large share.
+          dbound_interval = cfg_.pmc_cp_only_min > 0 && busy - act >= cfg_.pmc_cp_only_min * clk;
         }
         // Quiet = a shader engine had waves for < kQuietActiveFrac of the clocks
         // since the previous READ, and no MFMA cycle ran.  Both counters are
@@ -756,6 +775,13 @@ void Sampler::run_pmc(Worker& w) {
         }
         gap = gap_interval && !quiet && ps.mono_ns - gap_since_ns >= gap_hold_ns;
         st.pmc_gap.store(gap ? 1 : 0, std::memory_order_relaxed);
+        if (!dbound_interval) {
+          dbound_since_ns = 0;
+        } else if (dbound_since_ns == 0) {
+          dbound_since_ns = prev_ps_ns;
+        }
+        dbound = dbound_interval && !quiet && ps.mono_ns - dbound_since_ns >= dbound_hold_ns;
+        st.pmc_dbound.store(dbound ? 1 : 0, std::memory_order_relaxed);
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
           const bool slow = quiet && idle_hz > 0 && idle_hz < hz;

@@ -615,6 +615,41 @@ def test_dispatch_gap_reads_drop_to_gap_rate(mock_exporter):
     assert ex.pmc_busy_min == 0.9 and ex.pmc_gap_hz == 200
 
 
+def test_dispatch_bound_reads_drop_to_gap_rate(mock_exporter):
+    """Dispatch-bound READ rate (--pmc-cp-only-min, on by default): a stream of µs
+    kernels keeps the CP busy while waves are present only part of the time (on
+    MI355X: CPC ≈100 %, SPI ≈41 %), and that stream pays each READ packet (+3.8 % at
+    8 kHz, profiles/r4/ r4c).  The mock's wave_frac 0.4 models it: after the hold,
+    READs drop to the gap rate and the dispatch integral stays exact (100 %); long
+    kernels (wave_frac 1) and --pmc-cp-only-min 0 keep every tick."""
+    def rate(ex, secs=0.6):
+        n0 = ex.integrals(0)["pmc_samples"]
+        time.sleep(secs)
+        return (ex.integrals(0)["pmc_samples"] - n0) / secs
+
+    kw = dict(n_gpus=1, hz=4000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100, window_s=1.0,
+              pmc_gap_hz=500)
+    ex = mock_exporter(mock={"util_base": 100, "util_amp": 0}, mock_pmc={"wave_frac": 0.4}, **kw)
+    time.sleep(0.3)
+    a, t0 = ex.integrals(0), time.time()
+    r = rate(ex)
+    b, dt = ex.integrals(0), time.time() - t0
+    assert 350 <= r <= 750, r                                           # ≈ the gap rate, not 4000
+    assert b["pmc_dispatch_bound"] == 1 and b["pmc_gap"] == 0 and b["pmc_quiet"] == 0, b
+    assert (b["dispatch_seconds"] - a["dispatch_seconds"]) / dt == pytest.approx(1.0, abs=0.03)
+    assert (b["active_seconds"] - a["active_seconds"]) / dt == pytest.approx(0.4, abs=0.03)
+    m = parse_text(ex.render())
+    assert m["kgs_pmc_dispatch_bound"][0][1] == 1 and m["kgs_pmc_gap_skips_total"][0][1] > 1000
+    ex.stop()
+
+    for extra in ({"mock_pmc": {"wave_frac": 1.0}}, {"mock_pmc": {"wave_frac": 0.4}, "pmc_cp_only_min": 0.0}):
+        ex = mock_exporter(mock={"util_base": 100, "util_amp": 0}, **extra, **kw)
+        time.sleep(0.3)
+        assert rate(ex) > 3000, extra
+        assert ex.integrals(0)["pmc_dispatch_bound"] == 0
+        ex.stop()
+
+
 def test_batched_counter_source_is_not_a_failure(mock_exporter):
     """--pmc-batch: a reader that publishes every B-th READ returns kPmcPending for its
     first B samples after each (re)START and then every sample B calls late.  The

@@ -899,6 +899,88 @@ def test_dispatch_gap_rate_follows_the_kernel_stream(torch_dev):
     assert k["reads_per_s"] > 7000 and k["gap_skips_per_s"] < 1000, k
 
 
+def test_dispatch_bound_rate_at_default_flags(torch_dev):
+    """--pmc-cp-only-min (default 0.3) on MI355X: a HIP graph of µs kernels keeps the CP
+    dispatching with waves present only ≈40 % of the clocks (profiles/r4/ r4b), so at
+    default flags and 8 kHz its READs drop to the gap rate (1 kHz); back-to-back MFMA
+    kernels, and a training-like step whose µs kernels last less than the 4 ms hold,
+    keep every tick."""
+    import torch
+
+    from kube_gpu_stats_amd.ops import load as L
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    dev = torch.device("cuda", 0)
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=4000, stream_bytes=1 << 30)
+    ls.run_mfma()
+    src = torch.rand(16384, device=dev)
+    dst = torch.empty_like(src)
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        L.copy_f32(src, dst, nblocks=64, stream=s)
+        s.synchronize()
+        graph = torch.cuda.CUDAGraph()                     # ≈3.5 ms of 1.7 µs copies
+        with torch.cuda.graph(graph, stream=s):
+            for _ in range(2000):
+                L.copy_f32(src, dst, nblocks=64, stream=s)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+
+    def step():                                            # ≈8 ms of MFMA, then the graph
+        ls.run_mfma()
+        graph.replay()
+
+    proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
+                             "--hz", "8000", "--pmc", "aqlprofile", "--control-stdin", "--bdfs", _bdf0(),
+                             "--proc-every", "0", "--link-every", "0", "--window", "1"],
+                            cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    one = lambda m, f: m[f][0][1] if m.get(f) else None  # noqa: E731
+    rows = {}
+    try:
+        ready = json.loads(proc.stdout.readline())
+        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
+        sc = Scraper("127.0.0.1", ready["port"])
+
+        def phase(name, run, secs=1.5):
+            m0 = parse_text(sc.get())
+            t0 = time.time()
+            seen = []
+            while time.time() - t0 < secs:
+                for _ in range(4):
+                    run()
+                seen.append(one(parse_text(sc.get()), "kgs_pmc_dispatch_bound") or 0)  # while the work is queued
+                torch.cuda.synchronize()
+            dt = time.time() - t0
+            m1 = parse_text(sc.get())
+            d = lambda f: one(m1, f) - one(m0, f)  # noqa: E731
+            rows[name] = {"reads_per_s": d("kgs_pmc_samples_total") / dt,
+                          "gap_skips_per_s": d("kgs_pmc_gap_skips_total") / dt,
+                          "dispatch_bound_share": sum(seen) / len(seen),
+                          "dispatch_pct": 100 * d("amdgpu_dispatch_busy_seconds_total") / dt,
+                          "spi_pct": 100 * d("amdgpu_gpu_active_seconds_total") / dt}
+
+        phase("tiny_graph", graph.replay)
+        phase("mfma", ls.run_mfma)
+        phase("mfma_then_graph", step)
+    finally:
+        try:
+            proc.stdin.write("quit\n")
+            proc.stdin.flush()
+            proc.communicate(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+            proc.communicate()
+    _keep("dispatch_bound.json", json.dumps(rows, indent=1))
+    print(json.dumps(rows))
+    g, k, st = rows["tiny_graph"], rows["mfma"], rows["mfma_then_graph"]
+    assert g["dispatch_bound_share"] > 0.5 and g["reads_per_s"] < 2500, g
+    assert g["dispatch_pct"] > 90, g                       # the integral is exact at the lower READ rate
+    assert k["reads_per_s"] > 7000 and k["dispatch_bound_share"] == 0, k
+    assert st["reads_per_s"] > 7000, st
+
+
 def test_sm_util_from_counters_follows_load_and_idle(torch_dev, tmp_path):
     """--sm-util-source counters on MI355X: the reference-contract gauge reads the
     counter tier's GPU-active (GRBM_SPI_BUSY) — >80 under the MFMA load, ~0 once idle

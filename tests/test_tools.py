@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -79,3 +81,47 @@ def test_soak_tool_on_the_mock(tmp_path):
     r = json.loads(out.read_text())
     assert r["fail"] == [] and len(r["windows"]) >= 2, r
     assert all(w["pmc_samples_per_s"] > 400 and w["pmfw_tables_per_s"] > 40 for w in r["windows"]), r
+
+
+def test_util_estimator_sim_scores_variants_on_a_synthetic_dump(tmp_path, capsys):
+    """tools/util_estimator_sim.py on a synthetic READ stream: 8 kHz READs that each
+    cost the CP 20 µs, an idle stretch, and a 1 ms-every-5 ms burst train whose bursts
+    run at a lower clock (1.8 GHz) than the idle stretches (2.1 GHz).  Every variant
+    reads the idle GPU as ≈0 and the train near its 20 % duty; the time split, which
+    knows the idle clock, is exact."""
+    import json
+
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import util_estimator_sim as U
+
+    def stream(busy_at, secs=1.0, hz=8000.0):
+        t, cnt, spi, cpc, out = 0.0, 0.0, 0.0, 0.0, []
+        dt = 1.0 / hz
+        step = 1e-6
+        while t < secs:
+            out.append([t, int(cnt), int(spi), int(cpc), 0])
+            s = 0.0
+            while s < dt:
+                b = busy_at(t + s)
+                f = 1.8e9 if b else 2.1e9
+                cnt += f * step
+                if b:
+                    spi += f * step
+                    cpc += f * step
+                s += step
+            cpc += 20e-6 * 2.1e9      # the READ's own CP time
+            t += dt
+        return out
+
+    burst = lambda t: (t % 0.005) < 0.001  # noqa: E731
+    loads = {"idle": {"t0": 0.0, "t1": 0.5, "duty_gpu_s": 0.0, "samples": stream(lambda t: False, 0.5)},
+             "burst_1_5": {"t0": 0.0, "t1": 0.5, "duty_gpu_s": 0.1, "samples": stream(burst, 0.5)}}
+    p = tmp_path / "dump.json"
+    p.write_text(json.dumps({"counters": [], "pipelined": 1, "rates": {"8000": loads}}))
+    assert U.main([str(p)]) == 0
+    out = json.loads(capsys.readouterr().out)["8000"]
+    assert out["read_us"] == pytest.approx(20.0, rel=0.05)
+    assert out["idle"]["subtract"] < 0.5 and out["idle"]["overlap"] < 0.5 and out["idle"]["timesplit"] < 0.5
+    b = out["burst_1_5"]
+    assert b["timesplit"] == pytest.approx(20.0, abs=0.5), b
+    assert b["subtract"] == pytest.approx(20.0, abs=3.0) and b["overlap"] == pytest.approx(20.0, abs=3.0), b

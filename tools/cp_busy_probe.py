@@ -48,7 +48,7 @@ def kfd_gpu_id() -> int:
     raise RuntimeError("no KFD GPU node")
 
 
-def child(hz: float, secs: float) -> int:
+def child(hz: float, secs: float, pipelined: bool) -> int:
     from kube_gpu_stats_amd.native import pmc_lib_path
 
     L = ctypes.CDLL(pmc_lib_path("aqlprofile"))
@@ -65,9 +65,14 @@ def child(hz: float, secs: float) -> int:
     if h < 0:
         print(json.dumps({"error": "open: " + err.value.decode()}), flush=True)
         return 1
+    if pipelined:  # the exporter's 8 kHz mode: each call returns the previous READ, stamped at its CP time
+        if L.kgs_pmc_set_pipelined(h, 1, err, 512) != 0:
+            print(json.dumps({"error": "pipelined: " + err.value.decode()}), flush=True)
+            return 1
     print(json.dumps({"ready": True}), flush=True)
     out = (ctypes.c_uint64 * n)()
     rns = ctypes.c_uint32()
+    sns = ctypes.c_int64()
     period = 1.0 / hz
     t_end = time.perf_counter() + secs
     nxt = time.perf_counter()
@@ -80,9 +85,10 @@ def child(hz: float, secs: float) -> int:
             if nxt - now > 3e-4:
                 time.sleep(nxt - now - 2e-4)
             continue
-        rc = L.kgs_pmc_sample(h, out, n, ctypes.byref(rns))
+        rc = L.kgs_pmc_sample_ts(h, out, n, ctypes.byref(rns), ctypes.byref(sns))
         if rc == 0:
-            buf.append((time.time(), list(out)))
+            # the time the CP read the values (pipelined: the previous call's READ), on the wall clock
+            buf.append((time.time() - (time.monotonic_ns() - sns.value) * 1e-9, list(out)))
         nxt += period
         if nxt < now - 10 * period:
             nxt = now
@@ -100,11 +106,15 @@ def main(argv=None) -> int:
     ap.add_argument("--rates", default="100,1000,8000")
     ap.add_argument("--secs", type=float, default=2.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--pipelined", type=int, default=0, choices=[0, 1],
+                    help="READ pipelined, as the exporter does above its idle rate")
+    ap.add_argument("--dump", default="", help="write every raw sample of the --dump-rates runs here (JSON)")
+    ap.add_argument("--dump-rates", default="8000")
     ap.add_argument("--child", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--child-secs", type=float, default=0.0, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     if a.child:
-        return child(a.child, a.child_secs)
+        return child(a.child, a.child_secs, bool(a.pipelined))
 
     import torch
 
@@ -135,11 +145,13 @@ def main(argv=None) -> int:
             return busy
         return getattr(loads, "run_" + name)(secs)
 
-    out: dict = {"counters": NAMES, "rates": {}}
+    out: dict = {"counters": NAMES, "rates": {}, "pipelined": a.pipelined}
+    dumps: dict = {}
     total = len(names) * (a.secs + 0.6) + 2.0
     for hz in [float(x) for x in a.rates.split(",")]:
         p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", str(hz), "--child-secs",
-                              str(total)], stdout=subprocess.PIPE, text=True, cwd=REPO)
+                              str(total), "--pipelined", str(a.pipelined)], stdout=subprocess.PIPE, text=True,
+                             cwd=REPO)
         first = json.loads(p.stdout.readline())
         if "error" in first:
             out["rates"][f"{hz:g}"] = first
@@ -179,11 +191,20 @@ def main(argv=None) -> int:
             res["cpc_us_per_read_idle"] = round(1e4 * r["cpc_pct"] / r["reads_per_s"], 2) if r["reads_per_s"] else None
             res["cpf_us_per_read_idle"] = round(1e4 * r["cpf_pct"] / r["reads_per_s"], 2) if r["reads_per_s"] else None
         out["rates"][f"{hz:g}"] = res
+        if a.dump and f"{hz:g}" in a.dump_rates.split(","):
+            raw = {name: {"t0": t0, "t1": t1, "duty_gpu_s": busy,
+                          "samples": [[round(ts - t0, 7)] + v for ts, v in samples if t0 - 0.01 <= ts <= t1 + 0.01]}
+                   for name, (t0, t1, busy) in marks.items()}
+            dumps[f"{hz:g}"] = raw
         print(json.dumps({f"{hz:g}": res}), flush=True)
     if a.out:
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)
+    if a.dump:
+        os.makedirs(os.path.dirname(os.path.abspath(a.dump)), exist_ok=True)
+        with open(a.dump, "w") as f:
+            json.dump({"counters": NAMES, "pipelined": a.pipelined, "rates": dumps}, f)
     return 0
 
 

@@ -4,7 +4,7 @@
 # abort (rc >= 124) does — nothing else touches the GPU after that.
 #   gpurun --timeout 1100 -- 'bash tools/gpu_check.sh <tag> [steps...]'
 # steps (default: probe tests smoke bench): probe probe3 tests smoke bench bench2 rocprof
-#   round 4: smprobe cpprobe graphcost testsnw wedge (the wedged-queue test last, alone)
+#   round 4: smprobe cpprobe graphcost testsnw testsdb wedge (the wedged-queue test last, alone)
 set -u
 TAG=${1:-r2}; shift || true
 STEPS=${*:-probe tests smoke bench}
@@ -55,7 +55,6 @@ for s in $STEPS; do
           t16k) run $s 600 "${T[@]}" --hz 16000 --pmc-batch 16 ;;
         esac ;;
     bpub*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-publish-us "${s#bpub}" --out "$OUT/$s.json" ;;
-    bnobar|bnobar2) KGS_AQL_NOBARRIER=1 run $s 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/$s.json" ;;
     b16k) run $s 600 python -u bench.py --steps 20 --warmup 5 --hz 16000 --pmc-batch 16 --out "$OUT/$s.json" ;;
     bnobatch|bnobatch2) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch 1 --out "$OUT/$s.json" ;;
     bbatch*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch "${s#bbatch}" --out "$OUT/$s.json" ;;
@@ -70,9 +69,13 @@ for s in $STEPS; do
     # round 4
     smprobe) run sm_util_probe 300 python -u tools/sm_util_probe.py --out "$OUT/sm_util_probe.json" ;;
     cpprobe) run cp_busy_probe 240 python -u tools/cp_busy_probe.py --out "$OUT/cp_busy_probe.json" ;;
+    cpdump) run cp_dump 300 python -u tools/cp_busy_probe.py --rates 8000,1000 --pipelined 1 --secs 2 \
+              --out "$OUT/cp_busy_pipelined.json" --dump "$OUT/cp_dump.json" --dump-rates 8000,1000 ;;
     graphcost) run graph_cost 400 python -u tools/graph_cost_probe.py --out "$OUT/graph_cost.json" ;;
     testsnw) run pytest_gpu 700 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
                -p no:cacheprovider -k "not wedged_counter_queue" ;;
+    testsdb) run pytest_dbound 400 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
+               -p no:cacheprovider -k "dispatch_bound or dispatch_gap or read_immune" ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;

@@ -6,11 +6,14 @@ dispatches the workload's kernels.  Long kernels hide it; a HIP graph of µs ker
 does not (bench.py's tiny_graph component: +0.3 … +1.1 % at 8 kHz in round 3).  This
 probe measures only that component, for several exporter variants on the same box:
 
-* ``default``   — the shipped reader (batched READs, barrier bit on every packet);
-* ``nobarrier`` — KGS_AQL_NOBARRIER=1: a batch's non-publisher READs without the AQL
-  barrier bit, so the packet processor need not wait for the previous READ;
-* ``prio_low``  — KGS_AQL_PRIORITY=low: the READ queue at the lowest CP priority;
-* ``batch1``    — --pmc-batch 1 (every READ writes the L2 back).
+* ``default``   — the shipped exporter: batched READs, and the dispatch-bound READ
+  rate (--pmc-cp-only-min 0.3: a GPU whose CP dispatches with no wave in flight for
+  ≥ 30 % of the clocks is READ at --pmc-gap-hz, 1 kHz);
+* ``full_rate`` — --pmc-cp-only-min 0: every tick READs, whatever the workload (the
+  round-4 r4c reader: +3.8 % at 8 kHz; the KGS_AQL_NOBARRIER and low-priority READ
+  queue variants measured the same there and were deleted);
+* ``batch1``    — --pmc-cp-only-min 0 --pmc-batch 1 (every READ writes the L2 back);
+* ``hz1000`` / ``hz100`` — the full-rate reader at 1 kHz / 100 Hz.
 
 Per variant one exporter process (--hz 8000, --control-http) and ``--rounds`` paired
 rounds of two blocks — exporter paused / sampling, order alternating (ABBA) — each
@@ -34,9 +37,10 @@ sys.path.insert(0, REPO)
 
 VARIANTS = {
     "default": ({}, []),
-    "nobarrier": ({"KGS_AQL_NOBARRIER": "1"}, []),
-    "prio_low": ({"KGS_AQL_PRIORITY": "low"}, []),
-    "batch1": ({}, ["--pmc-batch", "1"]),
+    "full_rate": ({}, ["--pmc-cp-only-min", "0"]),
+    "batch1": ({}, ["--pmc-cp-only-min", "0", "--pmc-batch", "1"]),
+    "hz1000": ({}, ["--pmc-cp-only-min", "0", "--hz", "1000"]),
+    "hz100": ({}, ["--pmc-cp-only-min", "0", "--hz", "100"]),
 }
 T975 = {5: 2.571, 7: 2.365, 11: 2.201, 15: 2.131, 23: 2.069, 31: 2.040, 47: 2.012}
 
@@ -53,7 +57,7 @@ def ci95(xs: list[float]) -> tuple[float, float]:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--variants", default="default,nobarrier,prio_low,batch1")
+    ap.add_argument("--variants", default="default,full_rate,batch1,hz1000,hz100")
     ap.add_argument("--rounds", type=int, default=24)
     ap.add_argument("--replays", type=int, default=120, help="graph replays per block (≈3.5 ms each)")
     ap.add_argument("--kernels", type=int, default=2000)
@@ -107,7 +111,7 @@ def main(argv=None) -> int:
             ready = json.loads(proc.stdout.readline())
             assert ready.get("event") == "ready" and ready.get("pmc") == "aqlprofile", ready
             sc = Scraper("127.0.0.1", ready["port"])
-            diffs, on_s, samples, t_on = [], [], 0.0, 0.0
+            diffs, on_s, samples, t_on, dbound = [], [], 0.0, 0.0, []
             for r in range(a.rounds):
                 t = {}
                 for cond in (("off", "on") if r % 2 == 0 else ("on", "off")):
@@ -119,6 +123,7 @@ def main(argv=None) -> int:
                     if cond == "on":
                         m1, w1 = parse_text(sc.get()), time.monotonic()
                         samples += m1["kgs_pmc_samples_total"][0][1] - m0["kgs_pmc_samples_total"][0][1]
+                        dbound.append(m1.get("kgs_pmc_dispatch_bound", [({}, 0)])[0][1])
                         t_on += w1 - w0
                 diffs.append(100.0 * (t["on"] / t["off"] - 1.0))
                 on_s.append(t["on"])
@@ -126,10 +131,11 @@ def main(argv=None) -> int:
             info = ready.get("pmc_info", [""])[0]
             out["variants"][name] = {"overhead_pct": round(m, 4), "overhead_ci95_pct": round(ci, 4),
                                      "samples_per_s_while_on": round(samples / t_on, 1) if t_on else None,
+                                     "dispatch_bound_share_of_scrapes": round(sum(dbound) / len(dbound), 3),
                                      "block_s_mean": round(sum(on_s) / len(on_s), 5),
                                      "kernels_per_s": round(a.kernels * a.replays / (sum(on_s) / len(on_s)), 0),
                                      "reader": ";".join(x for x in info.split(";")
-                                                        if x.split("=")[0] in ("batch", "nobarrier", "priority", "lean")),
+                                                        if x.split("=")[0] in ("batch", "lean")),
                                      "per_round_pct": [round(d, 4) for d in diffs]}
             print(json.dumps({name: {k: v for k, v in out["variants"][name].items() if k != "per_round_pct"}}),
                   flush=True)

@@ -93,8 +93,6 @@ def main() -> int:
             env["KGS_AQL_FENCE"] = opts["fence"]
         if "signal" in opts:
             env["KGS_AQL_SIGNAL"] = opts["signal"]
-        if "prio" in opts:
-            env["KGS_AQL_PRIORITY"] = opts["prio"]
         if "prof" in opts:
             env["KGS_AQL_PROFILE"] = opts["prof"]
         if "idle" in opts:
@@ -137,8 +135,7 @@ def main() -> int:
 
     # spec hz:set:reader[:lean[:key=value...]]   keys: proc=<proc-every> (0 = no per-process tier),
     # slack=<ns> (sampler timer slack), fence=sys|agent|none (AQL header fences of the
-    # reader's packets), signal=interrupt|poll (READ completion signals), prio=low|normal|high
-    # (READ queue priority), prof=<n> (CP timestamps of every READ: queueing delay and execution
+    # reader's packets), signal=interrupt|poll (READ completion signals), prof=<n> (CP timestamps of every READ: queueing delay and execution
     # time on stderr every n READs), idle=<hz> (--pmc-idle-hz; 0 = READ every tick); "off" = no exporter
     specs = sys.argv[1:] or ["100:base:aqlprofile", "1000:base:aqlprofile", "8000:base:aqlprofile",
                              "100:full:aqlprofile", "1000:full:aqlprofile", "1000:base:none"]
