@@ -54,8 +54,8 @@ int pmc_counter_reduce(int idx);
 // Counter sets (bits of PmcSample::mask).  Every READ costs the command
 // processor time that a dispatch-bound workload on the same GPU feels
 // (profiles/launch_overhead.md): the TA block alone is 512 instance reads of
-// the 560 in `full`, so the default `base` set drops it and keeps the READ to
-// 48 register reads (GRBM × 8 XCC, MFMA busy × 32 SE).
+// the 568 in `full`, so the default `base` set drops it and keeps the READ to
+// 56 register reads (GRBM count + SPI busy × 8 XCC, MFMA busy × 32 SE, CPC busy × 8).
 //
 // Activity is GRBM_SPI_BUSY, not GRBM_GUI_ACTIVE.  GUI-active — like the PMFW
 // GFX-activity accumulator behind amdgpu_gfx_busy_percent — counts the graphics

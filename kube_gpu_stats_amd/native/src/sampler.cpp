@@ -732,14 +732,10 @@ void Sampler::run_pmc(Worker& w) {
             ++read_cyc_n[m];
             P.cpc_read_us = read_cyc[m] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
           }
-          // The READ's own CP time lands anywhere in the interval: where the CP was busy
-          // dispatching anyway it adds nothing (busy counts once), so it adds
-          // read·(1 − busy/clk) and busy = (cpc − read) / (1 − read/clk) — exact at
-          // both ends (idle: cpc = read → 0; saturated: cpc = clk → clk).
-          const double rc = std::min(read_cyc[m], 0.5 * clk);
-          const double busy = cpc >= kCpcFullFrac * clk
-                                  ? clk
-                                  : std::max(act, std::max(0.0, (cpc - rc) / (1.0 - rc / clk)));
+          // (Counting the READ's CP time once where it overlaps dispatch busy —
+          // (cpc − read) / (1 − read/clk) — over-read 8 kHz burst trains by up to 4.6
+          // points on hardware, r4e; tools/util_estimator_sim.py replays the variants.)
+          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(act, std::max(0.0, cpc - read_cyc[m]));
           P.dispatch_seconds += std::min(1.0, busy / clk) * (ps.mono_ns - prev_ps_ns) * 1e-9;
           ++P.dispatch_drains;
           // Dispatch-bound: the CP dispatching with no wave in flight for a large share.

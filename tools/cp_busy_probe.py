@@ -28,6 +28,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -157,6 +158,11 @@ def main(argv=None) -> int:
             out["rates"][f"{hz:g}"] = first
             p.wait()
             continue
+        # Drain the child's stdout while the loads run: a full pipe would block its
+        # print, and with it the sampling, until the loads end.
+        lines: list[str] = []
+        reader = threading.Thread(target=lambda: lines.extend(p.stdout), daemon=True)
+        reader.start()
         time.sleep(0.5)
         marks = {}
         for name in names:
@@ -165,10 +171,11 @@ def main(argv=None) -> int:
             busy = gpu_busy(name, a.secs)
             t1 = time.time()
             marks[name] = (t0, t1, busy)
-        samples = []
-        for line in p.stdout:
-            samples.extend(json.loads(line))
         p.wait()
+        reader.join(timeout=30)
+        samples = []
+        for line in lines:
+            samples.extend(json.loads(line))
         res = {}
         for name, (t0, t1, busy) in marks.items():
             win = [s for s in samples if t0 <= s[0] <= t1]

@@ -8,10 +8,10 @@ integral the way the sampler's dispatch integral does (``sampler.cpp``, the
 ``dispatch_seconds`` block) and is scored against the kernels' own duty:
 
 * ``subtract`` — per interval: the whole interval if CPC busy ≥ 97 % of the clocks,
-  else max(SPI, CPC − learned READ cost), share × Δt (rounds r4b–r4d);
+  else max(SPI, CPC − learned READ cost), share × Δt (shipped);
 * ``overlap``  — the same, but the READ's CP time is taken to land uniformly in the
   interval, counted once where the CP was busy anyway: busy = (CPC − r) / (1 − r/clk)
-  (shipped from r4e);
+  (shipped in r4e only: phase U read 8 kHz burst trains up to 4.6 points high);
 * ``carry``    — ``subtract``, but the part of an interval's READ-cost subtraction that
   the floor at SPI cut off is carried into the next intervals (zero-mean noise in
   the READ's own CP time then cancels instead of adding up);
