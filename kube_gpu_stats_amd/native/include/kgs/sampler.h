@@ -147,8 +147,9 @@ constexpr double kQuietActiveFrac = 0.02;
 // idle period late, and every tick in between is a lost sample).
 constexpr int64_t kQuietHoldNs = 5000000;
 // Dispatch-busy integral: a READ interval whose CPC busy share is at least this is a
-// dispatch in flight throughout (the READ's own CP time hides under the workload's).
-constexpr double kCpcFullFrac = 0.97;
+// dispatch in flight throughout (the READ's own CP time hides under the workload's;
+// the CPC idles a few % of each 125 µs interval under a long kernel at 8 kHz, r4f).
+constexpr double kCpcFullFrac = 0.90;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };

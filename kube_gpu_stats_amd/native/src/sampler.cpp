@@ -567,6 +567,7 @@ void Sampler::run_pmc(Worker& w) {
   // The READ packet's own CPC busy (clock cycles), learned on intervals without waves,
   // separately for synchronous (quiet GPU) and pipelined READs: EWMA and samples seen.
   double read_cyc[2] = {0, 0};
+  double read_spi[2] = {0, 0};       // ... and its SPI-busy blip (cycles), learned alike
   uint64_t read_cyc_n[2] = {0, 0};
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
   int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
@@ -726,20 +727,31 @@ void Sampler::run_pmc(Worker& w) {
                                  ? static_cast<double>(ps.value[kPmcGrbmActive] - prev_ps_active)
                                  : 0.0;
           const int m = fresh_mode ? 1 : 0;
-          // No wave, no MFMA cycle and the CP mostly idle: the CP busy here is our READ's.
-          if (act < 0.005 * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma && cpc < 0.5 * clk) {
-            read_cyc[m] = read_cyc_n[m] ? 0.95 * read_cyc[m] + 0.05 * cpc : cpc;
+          // No wave, no MFMA cycle and the CP mostly idle: the CP busy here is our READ's,
+          // and so is the SPI blip (≈0.9 µs per READ: 0.7 % of the clocks at 8 kHz, so the
+          // test is the quiet threshold, not "no SPI at all" — r4f: a 0.5 % test kept 2 %
+          // of the 8 kHz READ-only intervals, the cheap ones, and learned 13 µs for 15.5).
+          if (act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma && cpc < 0.5 * clk) {
+            const bool first = read_cyc_n[m] == 0;
+            read_cyc[m] = first ? cpc : 0.95 * read_cyc[m] + 0.05 * cpc;
+            read_spi[m] = first ? act : 0.95 * read_spi[m] + 0.05 * act;
             ++read_cyc_n[m];
             P.cpc_read_us = read_cyc[m] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
           }
-          // (Counting the READ's CP time once where it overlaps dispatch busy —
-          // (cpc − read) / (1 − read/clk) — over-read 8 kHz burst trains by up to 4.6
-          // points on hardware, r4e; tools/util_estimator_sim.py replays the variants.)
-          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(act, std::max(0.0, cpc - read_cyc[m]));
+          // Waves of the workload: SPI busy less the READ's own blip.
+          const double wav = std::max(0.0, act - read_spi[m]);
+          // An interval the CP was busy for ≥ kCpcFullFrac counts whole: under a
+          // kernel the CPC idles a few % of each 125 µs interval at 8 kHz (r4f: MFMA and
+          // GEMM intervals 0.95-1.0), and subtracting a READ-only cost there under-read
+          // a GEMM stream by 4 points.  (Counting the READ's CP time once where it
+          // overlaps dispatch busy — (cpc − read) / (1 − read/clk) — over-read 8 kHz
+          // burst trains; tools/util_estimator_sim.py replays the variants on r4f's raw
+          // READs.)
+          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(wav, std::max(0.0, cpc - read_cyc[m]));
           P.dispatch_seconds += std::min(1.0, busy / clk) * (ps.mono_ns - prev_ps_ns) * 1e-9;
           ++P.dispatch_drains;
           // Dispatch-bound: the CP dispatching with no wave in flight for a large share.
-          dbound_interval = cfg_.pmc_cp_only_min > 0 && busy - act >= cfg_.pmc_cp_only_min * clk;
+          dbound_interval = cfg_.pmc_cp_only_min > 0 && busy - wav >= cfg_.pmc_cp_only_min * clk;
         }
         // Quiet = a shader engine had waves for < kQuietActiveFrac of the clocks
         // since the previous READ, and no MFMA cycle ran.  Both counters are

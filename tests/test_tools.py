@@ -120,8 +120,8 @@ def test_util_estimator_sim_scores_variants_on_a_synthetic_dump(tmp_path, capsys
     p.write_text(json.dumps({"counters": [], "pipelined": 1, "rates": {"8000": loads}}))
     assert U.main([str(p)]) == 0
     out = json.loads(capsys.readouterr().out)["8000"]
-    assert out["read_us"] == pytest.approx(20.0, rel=0.05)
-    assert out["idle"]["subtract"] < 0.5 and out["idle"]["overlap"] < 0.5 and out["idle"]["timesplit"] < 0.5
+    assert out["read_us_shipped"] == pytest.approx(20.0, rel=0.05)
+    assert out["idle"]["shipped"] < 0.5 and out["idle"]["overlap"] < 0.5 and out["idle"]["timesplit"] < 0.5
     b = out["burst_1_5"]
     assert b["timesplit"] == pytest.approx(20.0, abs=0.5), b
-    assert b["subtract"] == pytest.approx(20.0, abs=3.0) and b["overlap"] == pytest.approx(20.0, abs=3.0), b
+    assert b["shipped"] == pytest.approx(20.0, abs=3.0) and b["overlap"] == pytest.approx(20.0, abs=3.0), b

@@ -7,16 +7,16 @@ loads' event-timed GPU busy.  Each variant turns the READ intervals into a busy
 integral the way the sampler's dispatch integral does (``sampler.cpp``, the
 ``dispatch_seconds`` block) and is scored against the kernels' own duty:
 
-* ``subtract`` — per interval: the whole interval if CPC busy ≥ 97 % of the clocks,
-  else max(SPI, CPC − learned READ cost), share × Δt (shipped);
-* ``overlap``  — the same, but the READ's CP time is taken to land uniformly in the
-  interval, counted once where the CP was busy anyway: busy = (CPC − r) / (1 − r/clk)
-  (shipped in r4e only: phase U read 8 kHz burst trains up to 4.6 points high);
-* ``carry``    — ``subtract``, but the part of an interval's READ-cost subtraction that
-  the floor at SPI cut off is carried into the next intervals (zero-mean noise in
-  the READ's own CP time then cancels instead of adding up);
-* ``timesplit``— per interval, busy time = Δt − idle cycles / idle clock, with the
-  idle clock learned on quiet intervals (cycle shares are clock-weighted: a burst
+* ``shipped``  — the sampler from r4g: the whole interval if CPC busy ≥ 90 % of the
+  clocks, else max(SPI − the READ's SPI blip, CPC − the READ's CP cost), share × Δt;
+  both READ costs learned on every READ-only interval (SPI < 2 % of the clocks);
+* ``r4b``      — the same with a 97 % full threshold, no SPI-blip removal, and the READ
+  cost learned only where SPI < 0.5 % of the clocks (rounds r4b–r4f: at 8 kHz that kept
+  2 % of the READ-only intervals, the cheap ones);
+* ``overlap``  — ``shipped``, but the READ's CP time counted once where it overlaps
+  dispatch busy: busy = (CPC − r) / (1 − r/clk);
+* ``timesplit``— ``shipped``, but busy time = Δt − idle cycles / idle clock, with the
+  idle clock learned on READ-only intervals (cycle shares are clock-weighted: a burst
   under the power cap runs at a lower clock than the idle stretch around it).
 
 ``python tools/util_estimator_sim.py profiles/r4/r4e/cp_dump.json``
@@ -26,7 +26,7 @@ from __future__ import annotations
 import json
 import sys
 
-FULL = 0.97
+FULL = 0.90
 
 
 def intervals(samples):
@@ -38,44 +38,43 @@ def intervals(samples):
         yield dt, clk, max(0, b[2] - a[2]), max(0, b[3] - a[3])
 
 
-def learn_read(ivs) -> tuple[float, float]:
-    """READ cost in cycles (mean over intervals without waves and with the CP mostly
-    idle) and the idle clock (cycles / s over the same intervals)."""
-    cyc, clk_s, n = 0.0, 0.0, 0
+QUIET_SPI = 0.02  # the sampler's kQuietActiveFrac: a READ alone shows ≈0.9 µs of SPI busy
+
+
+def learn_read(ivs, quiet_spi: float = QUIET_SPI) -> tuple[float, float, float]:
+    """READ cost in CPC cycles and in SPI cycles (means over intervals without waves
+    and with the CP mostly idle) and the idle clock (cycles / s over the same)."""
+    cyc, spi_c, clk_s, n = 0.0, 0.0, 0.0, 0
     for dt, clk, spi, cpc in ivs:
-        if spi < 0.005 * clk and cpc < 0.5 * clk:
+        if spi < quiet_spi * clk and cpc < 0.5 * clk:
             cyc += cpc
+            spi_c += spi
             clk_s += clk / dt
             n += 1
-    return (cyc / n, clk_s / n) if n else (0.0, 0.0)
+    return (cyc / n, spi_c / n, clk_s / n) if n else (0.0, 0.0, 0.0)
 
 
-def estimate(ivs, read_cyc: float, idle_hz: float, variant: str) -> float:
-    tot, span, carry = 0.0, 0.0, 0.0
+def estimate(ivs, learned, variant: str) -> float:
+    read_cyc, read_spi, idle_hz = learned
+    full = 0.97 if variant == "r4b" else FULL
+    if variant == "r4b":
+        read_spi = 0.0
+    tot, span = 0.0, 0.0
     for dt, clk, spi, cpc in ivs:
         span += dt
-        if variant == "timesplit" and idle_hz > 0:
-            if cpc >= FULL * clk:
-                tot += dt
-                continue
-            busy_cyc = max(spi, cpc - read_cyc)
-            idle_s = max(0.0, (clk - busy_cyc) / idle_hz)
-            tot += min(dt, max(0.0, dt - idle_s))
+        wav = max(0.0, spi - read_spi)  # the READ's own SPI blip is not a wave of the workload
+        if cpc >= full * clk:
+            tot += dt
             continue
-        if cpc >= FULL * clk:
-            busy = clk
-            carry = 0.0
-        elif variant == "overlap":
+        if variant == "overlap":
             r = min(read_cyc, 0.5 * clk)
-            busy = max(spi, max(0.0, (cpc - r) / (1.0 - r / clk)))
-        elif variant == "carry":
-            raw = cpc - read_cyc + carry
-            busy = max(spi, raw)
-            carry = min(0.0, raw - spi)
-            carry = max(carry, -2 * read_cyc)  # never owe more than two READs
+            busy = max(wav, max(0.0, (cpc - r) / (1.0 - r / clk)))
         else:
-            busy = max(spi, max(0.0, cpc - read_cyc))
-        tot += min(1.0, busy / clk) * dt
+            busy = max(wav, max(0.0, cpc - read_cyc))
+        if variant == "timesplit" and idle_hz > 0:
+            tot += min(dt, max(0.0, dt - (clk - busy) / idle_hz))
+        else:
+            tot += min(1.0, busy / clk) * dt
     return 100.0 * tot / span if span else 0.0
 
 
@@ -85,9 +84,10 @@ def main(argv=None) -> int:
     out = {}
     for rate, loads in d["rates"].items():
         quiet = list(intervals(loads.get("idle", {}).get("samples", [])))
-        read_cyc, idle_hz = learn_read(quiet)
-        rows = {"read_us": round(1e6 * read_cyc / idle_hz, 2) if idle_hz else None,
-                "idle_clock_mhz": round(idle_hz / 1e6, 1)}
+        learned = {"r4b": learn_read(quiet, 0.005), "shipped": learn_read(quiet)}
+        rows = {f"read_us_{k}": round(1e6 * v[0] / v[2], 2) if v[2] else None for k, v in learned.items()}
+        rows["read_spi_us"] = round(1e6 * learned["shipped"][1] / learned["shipped"][2], 3) if learned["shipped"][2] else None
+        rows["idle_clock_mhz"] = round(learned["shipped"][2] / 1e6, 1)
         for name, L in loads.items():
             ivs = list(intervals(L["samples"]))
             if not ivs:
@@ -95,8 +95,8 @@ def main(argv=None) -> int:
             wall = L["t1"] - L["t0"]
             row = {"duty_gpu_pct": round(100 * L["duty_gpu_s"] / wall, 2),
                    "busy_clock_mhz": round(sum(c for _, c, _, _ in ivs) / sum(t for t, _, _, _ in ivs) / 1e6, 1)}
-            for v in ("subtract", "overlap", "carry", "timesplit"):
-                row[v] = round(estimate(ivs, read_cyc, idle_hz, v), 2)
+            for v in ("shipped", "r4b", "overlap", "timesplit"):
+                row[v] = round(estimate(ivs, learned["r4b" if v == "r4b" else "shipped"], v), 2)
             rows[name] = row
         out[rate] = rows
     print(json.dumps(out, indent=1))
