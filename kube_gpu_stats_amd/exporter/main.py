@@ -62,7 +62,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pmc-lean", 2, "aqlprofile READ packet: 0 as built (per-XCC CS_PARTIAL_FLUSH + full cache "
                                 "invalidate), 1 no flushes, 2 no flushes + L2 writeback only (default), 3 no cache op")
     add_flag(ap, "pmc-set", "base", "counter set: base (GRBM clocks/active + MFMA busy + CPC busy, 56 register "
-                                    "reads) | full (+ TA vector-memory busy, 568 reads: costs dispatch-bound workloads more)")
+                                    "reads) | full (+ TA vector-memory busy, 568 reads: costs dispatch-bound workloads more) | util (GRBM "
+                                    "count + SPI + CPC busy, 24 reads: the utilisation only, no MFMA / per-XCD gauges, "
+                                    "each READ cheaper for a µs-kernel stream)")
     add_flag(ap, "pmc-pipeline", True, "aqlprofile reader: overlap each counter READ's CP round trip with the "
                                        "tick sleep (the sample is stamped with the CP read time)")
     add_flag(ap, "pmc-reclaim-s", 10.0, "re-START the counters after they stalled this long (a foreign profiler "

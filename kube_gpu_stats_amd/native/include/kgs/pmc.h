@@ -73,12 +73,19 @@ int pmc_counter_reduce(int idx);
 constexpr uint32_t kPmcSetBase =
     (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcMfmaBusy) | (1u << kPmcCpcBusy);
 constexpr uint32_t kPmcSetFull = kPmcSetBase | (1u << kPmcTaBusy);
-// "base" | "full" → mask; 0 for an unknown name.
+// `util`: only what the reference-contract utilisation needs — the dispatch
+// integral (GRBM count, SPI busy, CPC busy): 24 register reads.  A READ's cost to a
+// dispatch-bound stream grows with its register reads (≈0.09 µs of a µs-kernel
+// stream's time per read, profiles/launch_overhead.md; 56 reads ≈ 5.3 µs per READ,
+// profiles/r4/ r4d), so a node that needs no MFMA or per-XCD gauges pays less.
+constexpr uint32_t kPmcSetUtil = (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcCpcBusy);
+// "base" | "full" | "util" → mask; 0 for an unknown name.
 uint32_t pmc_set_mask(const std::string& name);
 
 // Derived quantities over an interval between two cumulative samples.
 struct PmcRates {
   bool have_vmem = false;        // TA counter in the set
+  bool have_mfma = false;        // MFMA busy in the set (not in `util`)
   double gpu_active_pct = 0;     // 100 * ΔSPI_BUSY / ΔGRBM_COUNT (READ-immune)
   // 100 * ΔMFMA_BUSY / (ΔSPI_BUSY * SIMD_NUM): MFMA share of the SIMD cycles while a
   // shader engine had waves.  Not rocprofv3's MfmaUtil (that divides by

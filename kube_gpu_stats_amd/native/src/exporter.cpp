@@ -152,7 +152,7 @@ bool Exporter::init() {
     for (int d = 0; d < be_->device_count(); ++d) devs.push_back(d);
   const uint32_t pmc_mask = pmc_set_mask(cfg_.pmc_set);
   if (pmc_mask == 0) {
-    err_ = "unknown pmc_set '" + cfg_.pmc_set + "' (base | full)";
+    err_ = "unknown pmc_set '" + cfg_.pmc_set + "' (base | full | util)";
     return false;
   }
   if (cfg_.pmc_source == "mock") {

@@ -36,6 +36,7 @@ int pmc_counter_reduce(int idx) { return (idx >= 0 && idx < kPmcCount) ? kReduce
 uint32_t pmc_set_mask(const std::string& name) {
   if (name == "base" || name.empty()) return kPmcSetBase;
   if (name == "full") return kPmcSetFull;
+  if (name == "util") return kPmcSetUtil;
   return 0;
 }
 
@@ -51,11 +52,12 @@ PmcRates pmc_rates(const PmcSample& a, const PmcSample& b, int num_cu) {
   const double cu = num_cu > 0 ? num_cu : 256;
   if (cnt > 0) r.gpu_active_pct = 100.0 * act / cnt;
   r.have_vmem = (a.mask & b.mask & (1u << kPmcTaBusy)) != 0;
+  r.have_mfma = (a.mask & b.mask & (1u << kPmcMfmaBusy)) != 0;
   if (act > 0) {
     // Shares of the active (SPI-busy) cycles, capped: over a single ~125 µs drain a
     // kernel's tail can leave MFMA / TA cycles in an interval whose SPI-busy count
     // is a few hundred clocks.
-    r.mfma_util_pct = std::min(100.0, 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0));
+    if (r.have_mfma) r.mfma_util_pct = std::min(100.0, 100.0 * d(kPmcMfmaBusy) / (act * cu * 4.0));
     if (r.have_vmem) r.vmem_busy_pct = std::min(100.0, 100.0 * d(kPmcTaBusy) / act);
   }
   r.gpu_clock_mhz = cnt / dt * 1e-6;
@@ -188,7 +190,8 @@ class MockCounterSource final : public CounterSource {
       if (!(s.mask & (1u << i))) s.value[i] = 0;
     // XCD x is busy (1 - skew·x) of the time XCD 0 is (the active counter reduces by max
     // over XCDs, so XCD 0 carries the device value); MFMA cycles split likewise.
-    s.n_xcd = static_cast<uint32_t>(std::clamp(c_.n_xcd, 0, kMaxXcc));
+    // the real reader has a per-XCD fold only with the MFMA counter in the set
+    s.n_xcd = (s.mask & (1u << kPmcMfmaBusy)) ? static_cast<uint32_t>(std::clamp(c_.n_xcd, 0, kMaxXcc)) : 0;
     double wsum = 0;
     for (uint32_t x = 0; x < s.n_xcd; ++x) wsum += 1.0 - c_.xcd_skew * x;
     for (uint32_t x = 0; x < s.n_xcd; ++x) {

@@ -188,6 +188,7 @@ void Exporter::render(std::string& out) {
   // Snapshot all devices once.
   struct Snap {
     bool have = false, busy = false, pmc_have = false, pmc_rates = false;
+    bool pmc_mfma = false;  // the counter set has MFMA busy (not `util`)
     GpuSample s;
     Integrals I;
     PmcSample p;
@@ -220,6 +221,7 @@ void Exporter::render(std::string& out) {
     x.links_fresh = fresh(st.links_ok_ns, S.link_period_ns());
     x.health_fresh = fresh(st.health_ok_ns, S.link_period_ns());
     x.pmc_have = st.pmc_latest.load(x.p);
+    x.pmc_mfma = x.pmc_have && (x.p.mask & (1u << kPmcMfmaBusy));
     // Counter rates only while we hold the counters and drains keep arriving:
     // handed over (pmc_on = 0), stalled (a foreign profiler STOPped /
     // reprogrammed them) or stale → no rate gauges rather than wrong or frozen
@@ -345,14 +347,14 @@ void Exporter::render(std::string& out) {
       w.line("container_gpu_energy_joules_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
     }
     bool any_pmc_int = false;
-    for (const auto& pl : pod_lines) any_pmc_int |= snaps[static_cast<size_t>(pl.first)].pmc_have;
+    for (const auto& pl : pod_lines) any_pmc_int |= snaps[static_cast<size_t>(pl.first)].pmc_mfma;
     if (any_pmc_int) {
       w.head("container_gpu_mfma_busy_seconds_total", "counter",
              "MFMA-busy seconds (all SIMDs busy with matrix work for 1 s = 1) of the GPU allocated to the pod, counted "
              "from allocation (hardware counters)");
       for (size_t i = 0; i < pod_lines.size(); ++i) {
         const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
-        if (!x.pmc_have) continue;
+        if (!x.pmc_mfma) continue;
         const Owner* o = pod_owner[i];
         const double v = x.I.mfma_busy_seconds - (o ? o->base_mfma_s : 0.0);
         w.line("container_gpu_mfma_busy_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
@@ -367,7 +369,7 @@ void Exporter::render(std::string& out) {
         if (pod_owner[i]) w.line("kgs_gpu_owner", pod_lines[i].second, nullptr, 1);
     }
     bool any_mfma = false;
-    for (const auto& pl : pod_lines) any_mfma |= snaps[static_cast<size_t>(pl.first)].pmc_rates;
+    for (const auto& pl : pod_lines) any_mfma |= snaps[static_cast<size_t>(pl.first)].pmc_rates && snaps[static_cast<size_t>(pl.first)].r.have_mfma;
     if (any_mfma) {
       // Same labels, hardware-counter matrix-core busy: GFX busy counts a GPU busy
       // while any dispatch is in flight; this says how much of it was MFMA work.
@@ -375,7 +377,7 @@ void Exporter::render(std::string& out) {
              "Matrix-core (MFMA) busy percent of active cycles of the GPU allocated to the pod, over the exporter "
              "window (hardware counters; same labels as container_gpu_sm_util)");
       for (const auto& [d, lb] : pod_lines)
-        if (snaps[static_cast<size_t>(d)].pmc_rates)
+        if (snaps[static_cast<size_t>(d)].pmc_rates && snaps[static_cast<size_t>(d)].r.have_mfma)
           w.line("container_gpu_mfma_util", lb, nullptr, snaps[static_cast<size_t>(d)].r.mfma_util_pct);
     }
   }
@@ -667,12 +669,12 @@ void Exporter::render(std::string& out) {
     }
     w.head("amdgpu_mfma_busy_seconds_total", "counter",
            "Integral of the MFMA-busy share of all SIMD cycles over time (hardware counters); rate() = matrix-core utilisation");
-    for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);
+    for (int d : ids) if (snaps[d].pmc_mfma) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);
     w.head("amdgpu_mfma_util_percent", "gauge",
            "Matrix-core (MFMA) busy percent of the SIMD cycles while a shader engine had waves (GRBM_SPI_BUSY), over "
            "the window; not rocprofv3 MfmaUtil (GUI-active based): the wall-clock share is "
            "rate(amdgpu_mfma_busy_seconds_total)");
-    for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
+    for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_mfma) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
     w.head("amdgpu_gpu_active_percent", "gauge",
            "Percent of clocks a shader engine had waves to run (GRBM_SPI_BUSY) over the window; unlike the PMFW GFX busy "
            "it does not count the exporter's own counter READs");

@@ -884,3 +884,27 @@ def test_wake_lateness_histogram(mock_exporter):
         n = [v for lb, v in m["kgs_sampler_wake_lateness_seconds_count"] if lb["gpu"] == g][0]
         assert counts == sorted(counts) and counts[-1] == n and n > 300, (g, b, n)
         assert [v for lb, v in m["kgs_sampler_wake_lateness_seconds_sum"] if lb["gpu"] == g][0] >= 0
+
+
+def test_util_counter_set_exports_the_utilisation_only(mock_exporter):
+    """--pmc-set util: GRBM count, SPI busy and CPC busy only (24 register reads per
+    READ instead of 56), enough for the dispatch integral behind the reference-contract
+    utilisation.  No MFMA or per-XCD series are exported, rather than zeros."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", pmc_set="util", pmc_idle_hz=0, window_s=1.0,
+                       mock={"square_duty": 0.25, "util_base": 50, "util_amp": 50, "util_period_s": 0.2,
+                             "pmfw_busy_floor": 99})
+    ex.set_device_owners(0, [{"pod": "p", "namespace": "n", "container": "c"}])
+    time.sleep(0.3)
+    a, t0 = ex.integrals(0), time.time()
+    time.sleep(1.2)
+    b, dt = ex.integrals(0), time.time() - t0
+    assert (b["dispatch_seconds"] - a["dispatch_seconds"]) / dt == pytest.approx(0.25, abs=0.03)
+    assert b["mfma_busy_seconds"] == 0
+    m = parse_text(ex.render())
+    for fam in ("amdgpu_mfma_busy_seconds_total", "amdgpu_mfma_util_percent", "amdgpu_mfma_util_xcc_percent",
+                "container_gpu_mfma_util", "container_gpu_mfma_busy_seconds_total"):
+        assert not m.get(fam), fam
+    assert {lb["counter"] for lb, _ in m["amdgpu_pmc_total"]} == {"GRBM_COUNT", "GRBM_SPI_BUSY", "CPC_CPC_STAT_BUSY"}
+    (_, sm), = m["container_gpu_sm_util"]
+    assert sm == pytest.approx(25, abs=6)                     # from the counters, not the PMFW floor of 99
+    assert m["amdgpu_gpu_active_percent"][0][1] == pytest.approx(25, abs=6)
