@@ -80,7 +80,7 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                       "--pmc-gap-hz, since every READ packet delays the workload's dispatches "
                                       "(0 = off; ignored in profiling mode)")
     add_flag(ap, "pmc-gap-hz", 500.0, "counter READ rate in a dispatch gap (--pmc-busy-min) or a dispatch-bound "
-                                       "stream (--pmc-cp-only-min): a µs-kernel stream pays +0.5 % at 1 kHz, +4 % at "
+                                       "stream (--pmc-cp-only-min): a µs-kernel stream pays +0.5 %% at 1 kHz, +4 %% at "
                                        "8 kHz (profiles/r4/ r4d)")
     add_flag(ap, "pmc-gap-hold-ms", 1.0, "low-occupancy READ intervals in a row, in ms, before the gap rate applies")
     add_flag(ap, "pmc-cp-only-min", 0.3, "dispatch-bound READ rate: while the command processor dispatches with no "
@@ -97,6 +97,10 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                  "than unbatched (profiles/r3/README.md r3ab)")
     add_flag(ap, "pmc-publish-us", 1000, "longest a batched counter READ waits for its L2 writeback: a READ writes "
                                          "back early when the next tick would be later (at <= 1 kHz every READ does)")
+    add_flag(ap, "pmc-lite", False, "lite READs: a batch's non-publishing READs skip the per-SE counters (MFMA busy, "
+                                    "TA), 32 of the base set's 56 register copies, which a µs-kernel stream pays for; "
+                                    "MFMA and per-XCD values then update at the publish rate (1 kHz at 8 kHz ticks), "
+                                    "their integrals stay exact")
     add_flag(ap, "pmc-timeout-ms", 250, "bound of every wait on the command processor (counter READ, START, STOP, "
                                         "queue slot): a wedged CP costs one timeout, never a hang")
     add_flag(ap, "pmc-breaker-k", 3, "consecutive failed counter drains that open the counter tier's circuit breaker "
@@ -194,6 +198,7 @@ def config_from_args(a) -> dict:
         "pmc_timeout_ms": a.pmc_timeout_ms,
         "pmc_batch": a.pmc_batch,
         "pmc_publish_us": a.pmc_publish_us,
+        "pmc_lite": a.pmc_lite,
         "pmc_breaker_k": a.pmc_breaker_k,
         "pmc_retry_s": a.pmc_retry_s,
         "pmc_retry_max_s": a.pmc_retry_max_s,

@@ -121,6 +121,15 @@ struct Agent {
   std::vector<std::string> names;
   std::vector<int> reduce;                           // 0 sum, 1 max, 2 mean
   std::vector<char> per_cu;                          // counter's block has one instance per CU
+  std::vector<char> per_se;                          // counter read per SE (SQ, TA/TD/TCP): lite READs skip it
+  // Lite READs (kgs_pmc_configure("lite")): the batch's non-publishing READs leave
+  // the per-SE counters out; their values are the last read ones (se_*).
+  bool plite[kMaxSlots] = {};                        // slot k's READ IB is lite
+  bool se_have = false;                              // se_* hold a full READ's values since the last START
+  std::vector<double> se_vals, se_vals_xcd;
+  std::vector<uint32_t> se_seen, se_inst;
+  bool last_se_fresh = true;                         // the last returned sample read the per-SE counters
+  std::atomic<uint64_t> lite_reads{0};
   std::vector<hsa_ven_amd_aqlprofile_event_t> events;
   std::vector<int> ev_counter;                       // event index -> counter index
   hsa_ven_amd_aqlprofile_profile_t prof{};
@@ -153,6 +162,7 @@ struct Agent {
     std::vector<double> vals, vals_xcd;
     std::vector<uint32_t> xcd_seen;
     int64_t ts = 0;
+    bool se_fresh = true;
   };
   std::deque<Ready> bready;                          // folded samples not yet returned
   std::atomic<uint64_t> land_waits{0}, land_timeouts{0};  // collections that had to wait / gave up waiting
@@ -555,6 +565,12 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
   std::fprintf(stderr, "\n");
 }
 
+// SET_UCONFIG_REG offset of GRBM_GFX_INDEX, and its SE_BROADCAST_WRITES bit: the
+// READ IB selects one SE (bit clear) before copying a per-SE block's counters (SQ,
+// TA), and broadcasts again (0xe0000000) for the GRBM / CP ones
+// (profiles/r1/lean/read_packet_dump_base.txt).
+constexpr uint32_t kGrbmGfxIndex = 0x200, kSeBroadcast = 1u << 31;
+
 // Lean READ.  aqlprofile's READ IB (decoded with KGS_AQL_DUMP=1,
 // profiles/read_packet.md) brackets the per-XCC register copies with a
 // CS_PARTIAL_FLUSH on every XCC and ends with an ACQUIRE_MEM that invalidates
@@ -566,9 +582,11 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
 // 2 (default) = 1 + ACQUIRE_MEM reduced to the L2 writeback that publishes the
 // CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Cost-attribution modes
 // (KGS_AQL_LEAN only; the counter values they return are stale): 4 = 3 + no
-// COPY_DATA, 5 = every packet of the IB a NOP.  Returns packets changed.
+// COPY_DATA, 5 = every packet of the IB a NOP.  `lite` also drops the per-SE
+// copies (the MFMA busy's 32 of the base set's 56 results: the READ's CP time
+// grows with its register copies, profiles/r4/).  Returns packets changed.
 int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<volatile uint32_t*>* dsts = nullptr,
-                 const void* out = nullptr, size_t out_sz = 0) {
+                 const void* out = nullptr, size_t out_sz = 0, bool lite = false) {
   if (mode <= 0) return 0;
   uint32_t dw[4];
   std::memcpy(dw, pkt.pm4_command + 1, sizeof dw);
@@ -578,12 +596,17 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<
   uint32_t* ib = reinterpret_cast<uint32_t*>(addr);
   auto nop = [&](uint32_t at, uint32_t len) { ib[at] = (3u << 30) | ((len - 2) << 16) | (0x10u << 8); };
   int changed = 0;
+  bool se_sel = false;  // GRBM_GFX_INDEX selects one SE: the copies read a per-SE counter
   for (uint32_t i = 0; i < ndw;) {
     const uint32_t h = ib[i];
     if ((h >> 30) == 2) { ++i; continue; }
     if ((h >> 30) != 3) return -2;
     const uint32_t opc = (h >> 8) & 0xFF, len = ((h >> 16) & 0x3FFF) + 2;
-    if (mode >= 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
+    if (opc == 0x79 && len >= 3 && ib[i + 1] == kGrbmGfxIndex) se_sel = !(ib[i + 2] & kSeBroadcast);
+    if (lite && se_sel && opc == 0x40 && len == 6 && ((ib[i + 1] >> 8) & 0xF) == 5) {
+      nop(i, len);  // lite READ: no per-SE copy, and no landing check for its dwords
+      ++changed;
+    } else if (mode >= 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
       if (opc != 0x10) {
         nop(i, len);
         ++changed;
@@ -608,6 +631,7 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<
 }
 
 int g_lean = 2;  // kgs_pmc_configure("lean", m) before kgs_pmc_open; KGS_AQL_LEAN overrides
+int g_lite = 0;  // kgs_pmc_configure("lite", 1): batched non-publishing READs skip the per-SE counters
 int g_batch = 1;  // kgs_pmc_configure("batch", B) before kgs_pmc_set_pipelined; KGS_AQL_BATCH overrides
 // kgs_pmc_configure("publish_us", t): the longest a batched READ waits for its
 // publisher (aql_batch.h); 0 = only a half's B-th READ publishes.
@@ -616,6 +640,11 @@ int64_t g_publish_ns = 1000000;
 int lean_mode() {
   const char* e = std::getenv("KGS_AQL_LEAN");
   return e ? std::atoi(e) : g_lean;
+}
+
+bool lite_on() {
+  const char* e = std::getenv("KGS_AQL_LITE");
+  return e ? std::atoi(e) != 0 : g_lite != 0;
 }
 
 // Batched publication needs READs whose IB does no cache operation (lean ≥ 2 with
@@ -663,7 +692,7 @@ void place_xcds(Agent* a) {
 void snap_info(Agent* a);
 
 // Fold one completed READ's output buffer into a->vals.
-int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
+int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof, bool lite = false) {
   a->reads.fetch_add(1, std::memory_order_relaxed);
   a->vals.assign(a->names.size(), 0.0);
   a->instances.assign(a->names.size(), 0);
@@ -686,6 +715,36 @@ int fold(Agent* a, hsa_ven_amd_aqlprofile_profile_t* prof) {
   for (size_t k = 0; k < a->vals.size(); ++k)
     if (a->reduce[k] == 2 && a->instances[k] > 0)
       a->vals[k] /= (a->per_cu[k] && a->cu_count > 0) ? a->cu_count : a->instances[k];
+  // Lite READ: its per-SE dwords were not written; carry the last read values (0
+  // before the first full READ after a START: the counts restart there).  A full
+  // READ keeps its per-SE values for the lite ones after it.
+  const size_t nk = a->vals.size();
+  if (a->se_vals.size() != nk) {
+    a->se_vals.assign(nk, 0.0);
+    a->se_vals_xcd.assign(nk * kMaxXcd, 0.0);
+    a->se_seen.assign(nk, 0);
+    a->se_inst.assign(nk, 0);
+    a->se_have = false;
+  }
+  for (size_t k = 0; k < nk; ++k) {
+    if (k >= a->per_se.size() || !a->per_se[k]) continue;
+    double* vx = &a->vals_xcd[k * kMaxXcd];
+    double* sx = &a->se_vals_xcd[k * kMaxXcd];
+    if (lite) {
+      a->vals[k] = a->se_have ? a->se_vals[k] : 0.0;
+      std::copy(sx, sx + kMaxXcd, vx);
+      a->xcd_seen[k] = a->se_seen[k];
+      a->instances[k] = a->se_inst[k];
+    } else {
+      a->se_vals[k] = a->vals[k];
+      std::copy(vx, vx + kMaxXcd, sx);
+      a->se_seen[k] = a->xcd_seen[k];
+      a->se_inst[k] = a->instances[k];
+    }
+  }
+  if (lite) a->lite_reads.fetch_add(1, std::memory_order_relaxed);
+  else a->se_have = true;
+  a->last_se_fresh = !lite;
   return 0;
 }
 
@@ -848,11 +907,12 @@ void batch_collect(Agent* a, int h) {
   const int n = a->plan.slots(h, ks);
   for (int j = 0; j < n; ++j) {
     const int k = ks[j];
-    if (!wait_landed(a, k) || fold(a, &a->pprof[k]) != 0) continue;
+    if (!wait_landed(a, k) || fold(a, &a->pprof[k], a->plite[k]) != 0) continue;
     Agent::Ready r;
     r.vals = a->vals;
     r.vals_xcd = a->vals_xcd;
     r.xcd_seen = a->xcd_seen;
+    r.se_fresh = !a->plite[k];
     r.ts = a->psubmit_ns[k] + half_rtt(a);
     a->bready.push_back(std::move(r));
   }
@@ -912,6 +972,7 @@ int read_batched(Agent* a, int64_t* ts) {
   a->vals.swap(r.vals);
   a->vals_xcd.swap(r.vals_xcd);
   a->xcd_seen.swap(r.xcd_seen);
+  a->last_se_fresh = r.se_fresh;
   if (ts) *ts = r.ts;
   a->bready.pop_front();
   return 0;
@@ -963,7 +1024,8 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
     // drop the ACQUIRE_MEM (lean 3).  Every slot notes its result dwords.
     a->pdst[k].clear();
     const int mode = a->batch >= 2 && !is_publisher(a, k) ? 3 : lean_mode();
-    if (mode > 0) lean_read_ib(a->pread[k], mode, &a->pdst[k], a->pout[k], out_sz);
+    a->plite[k] = lite_on() && a->batch >= 2 && !is_publisher(a, k) && mode > 0;
+    if (mode > 0) lean_read_ib(a->pread[k], mode, &a->pdst[k], a->pout[k], out_sz, a->plite[k]);
   }
   a->pcmd_sz = std::max(a->pcmd_sz, cmd_sz);
   a->pout_sz = std::max(a->pout_sz, out_sz);
@@ -982,6 +1044,7 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
 // writeback, see read_batched), "publish_us" (0..10^6: the longest a batched READ
 // waits for its publisher, default 1000; 0 = only the B-th READ publishes).
 // "timeout_ms" (1..60000): bound of every wait on the CP (default 250).
+// "lite" (0/1): a batch's non-publishing READs skip the per-SE counters.
 // 0 = ok, -1 = unknown key / value.
 int kgs_pmc_configure(const char* key, int value) {
   if (key && std::strcmp(key, "lean") == 0 && value >= 0 && value <= 3) {
@@ -994,6 +1057,10 @@ int kgs_pmc_configure(const char* key, int value) {
   }
   if (key && std::strcmp(key, "publish_us") == 0 && value >= 0 && value <= 1000000) {
     g_publish_ns = static_cast<int64_t>(value) * 1000;
+    return 0;
+  }
+  if (key && std::strcmp(key, "lite") == 0 && (value == 0 || value == 1)) {
+    g_lite = value;
     return 0;
   }
   if (key && std::strcmp(key, "timeout_ms") == 0 && value >= 1 && value <= 60000) {
@@ -1046,6 +1113,9 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
     a->events.clear();
     a->ev_counter.clear();
     a->per_cu.assign(static_cast<size_t>(n), 0);
+    a->per_se.assign(static_cast<size_t>(n), 0);
+    a->se_have = false;  // a (re)START restarts every count
+    a->se_vals.clear();
     std::string missing;
     for (int k = 0; k < n; ++k) {
       hsa_ven_amd_aqlprofile_block_name_t block;
@@ -1056,6 +1126,7 @@ int kgs_pmc_open(uint64_t kfd_gpu_id, const char* const* names, const int* is_ma
         continue;
       }
       a->per_cu[static_cast<size_t>(k)] = bname == "TA" || bname == "TD" || bname == "TCP";
+      a->per_se[static_cast<size_t>(k)] = bname == "SQ" || a->per_cu[static_cast<size_t>(k)];
       // one event per block instance (TA per CU, SQ per SE, GRBM per XCC ...)
       hsa_ven_amd_aqlprofile_profile_t q{};
       q.agent = a->agent;
@@ -1231,6 +1302,14 @@ int kgs_pmc_sample_ts(int handle, uint64_t* out, int n, uint32_t* read_ns, int64
 // counters, sum otherwise).  Returns the number of XCDs written, 0..n-1 all
 // present, or 0 when the results carry no XCD coordinate.  Call from the thread
 // that samples the handle, after kgs_pmc_sample[_ts].
+// 1 if the last sample returned by kgs_pmc_sample[_ts] read the per-SE counters
+// (always, unless lite READs are on and it came from a non-publishing READ), 0 if
+// it carries their last read values, -1 for a bad handle.  Same thread as sample.
+int kgs_pmc_se_fresh(int handle) {
+  if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size()) return -1;
+  return g_agents[static_cast<size_t>(handle)]->last_se_fresh ? 1 : 0;
+}
+
 int kgs_pmc_sample_xcd(int handle, int counter, uint64_t* out, int max_xcd) {
   if (handle < 0 || static_cast<size_t>(handle) >= g_agents.size() || !out) return -1;
   Agent* a = g_agents[static_cast<size_t>(handle)];
@@ -1300,6 +1379,7 @@ int kgs_pmc_info(int handle, char* buf, int len) {
                   ";land_waits=" + std::to_string(a->land_waits.load()) +
                   ";land_timeouts=" + std::to_string(a->land_timeouts.load()) +
                   ";publishes=" + std::to_string(a->publishes.load()) +
+                  ";lite=" + std::to_string(lite_on() ? 1 : 0) + ":" + std::to_string(a->lite_reads.load()) +
                   ";publish_us=" + std::to_string(g_publish_ns / 1000) + ";num_xcc=" + std::to_string(a->num_xcc) +
                   ";fence=" + std::to_string(read_fences().first) + "," + std::to_string(read_fences().second) +
                   ";signal=" + (poll_signals() ? "poll" : "interrupt");

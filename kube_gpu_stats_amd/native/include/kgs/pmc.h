@@ -180,6 +180,9 @@ struct MockPmcConfig {
   // after each acquire the first `batch` samples return kPmcPending, then every
   // sample is the one taken `batch` calls earlier (1 = off).
   int batch = 1;
+  // Lite READs (--pmc-lite): only every lite_every-th sample reads the per-SE
+  // counters (MFMA, TA); the others carry the last values with se_fresh = 0 (0 = off).
+  int lite_every = 0;
 };
 // Mock counters consistent with the mock backend's utilisation curve.
 std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const MockConfig& bcfg,
@@ -196,6 +199,7 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
                                                       bool pipelined, uint32_t mask, int lean, std::string& err,
-                                                      int timeout_ms = 250, int batch = 1, int publish_us = 1000);
+                                                      int timeout_ms = 250, int batch = 1, int publish_us = 1000,
+                                                      bool lite = false);
 
 }  // namespace kgs

@@ -118,6 +118,10 @@ struct PmcSample {
   uint64_t xcd_active[kMaxXcc] = {};  // GRBM_SPI_BUSY of each XCD
   uint64_t xcd_mfma[kMaxXcc] = {};    // SQ_VALU_MFMA_BUSY_CYCLES summed over each XCD's SEs
   uint64_t xcd_ta[kMaxXcc] = {};      // TA_TA_BUSY summed over each XCD's TA instances (full set; 0 otherwise)
+  // The per-SE counters (MFMA busy, TA) were read by this drain.  With lite READs
+  // (--pmc-lite) only the publishing READs read them; the others carry the last
+  // values read, and every integral of a per-SE counter spans fresh drains only.
+  uint32_t se_fresh = 1;
 };
 static_assert(std::is_trivially_copyable<PmcSample>::value, "seqlock payload");
 

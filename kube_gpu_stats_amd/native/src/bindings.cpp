@@ -70,6 +70,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock_pmc.batch = get<int>(m, "batch", c.mock_pmc.batch);
     c.mock_pmc.cpc_read_us = get<double>(m, "cpc_read_us", c.mock_pmc.cpc_read_us);
     c.mock_pmc.wave_frac = get<double>(m, "wave_frac", c.mock_pmc.wave_frac);
+    c.mock_pmc.lite_every = get<int>(m, "lite_every", c.mock_pmc.lite_every);
   }
   c.sampler.hz = get<double>(d, "hz", c.sampler.hz);
   c.sampler.pmfw_hz = get<double>(d, "pmfw_hz", c.sampler.pmfw_hz);
@@ -101,6 +102,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.pmc_timeout_ms = get<int>(d, "pmc_timeout_ms", c.pmc_timeout_ms);
   c.pmc_batch = get<int>(d, "pmc_batch", c.pmc_batch);
   c.pmc_publish_us = get<int>(d, "pmc_publish_us", c.pmc_publish_us);
+  c.pmc_lite = get<bool>(d, "pmc_lite", c.pmc_lite);
   c.hbm_bytes_per_s_at_full_umc = get<double>(d, "hbm_bytes_per_s_at_full_umc", c.hbm_bytes_per_s_at_full_umc);
   c.listen_addr = get<std::string>(d, "listen_addr", c.listen_addr);
   c.port = get<int>(d, "port", c.port);

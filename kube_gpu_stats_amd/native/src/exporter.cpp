@@ -162,7 +162,7 @@ bool Exporter::init() {
   } else if (cfg_.pmc_source == "rocprofiler" || cfg_.pmc_source == "aqlprofile") {
     pmc_ = make_dl_counter_source(cfg_.pmc_source, cfg_.pmc_lib, *be_, devs, cfg_.pmc_pipeline, pmc_mask, cfg_.pmc_lean,
                                   pmc_err_, cfg_.pmc_timeout_ms, cfg_.pmc_batch,
-                                  cfg_.pmc_publish_us);
+                                  cfg_.pmc_publish_us, cfg_.pmc_lite);
   } else if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
     err_ = "unknown pmc_source '" + cfg_.pmc_source + "'";
     return false;

@@ -89,7 +89,9 @@ class MockCounterSource final : public CounterSource {
   MockCounterSource(const MockConfig& b, const MockPmcConfig& c, int n_dev)
       : b_(b), c_(c), t0_(mono_ns()), restart_(static_cast<size_t>(std::max(n_dev, 1)), 0),
         restart_reads_(static_cast<size_t>(std::max(n_dev, 1)), 0),
-        delayed_(static_cast<size_t>(std::max(n_dev, 1))) {
+        delayed_(static_cast<size_t>(std::max(n_dev, 1))),
+        se_last_(static_cast<size_t>(std::max(n_dev, 1))),
+        se_n_(static_cast<size_t>(std::max(n_dev, 1)), 0) {
     for (int d = 0; d < std::max(n_dev, 1); ++d) fault_.push_back(std::make_unique<Fault>());
   }
   std::string name() const override { return "mock"; }
@@ -101,6 +103,8 @@ class MockCounterSource final : public CounterSource {
     restart_[static_cast<size_t>(dev)] = mono_ns();
     restart_reads_[static_cast<size_t>(dev)] = fault_[static_cast<size_t>(dev)]->samples.load();
     delayed_[static_cast<size_t>(dev)].clear();
+    se_n_[static_cast<size_t>(dev)] = 0;
+    se_last_[static_cast<size_t>(dev)] = PmcSample{};
     return 0;
   }
   int reset(int dev) override {
@@ -160,6 +164,20 @@ class MockCounterSource final : public CounterSource {
     }
     s.mono_ns = now;
     s.read_ns = 1000;
+    s.se_fresh = 1;
+    if (c_.lite_every > 1 && dev >= 0 && static_cast<size_t>(dev) < se_last_.size()) {
+      // lite READs: only every lite_every-th one reads the per-SE counters
+      PmcSample& last = se_last_[static_cast<size_t>(dev)];
+      if (se_n_[static_cast<size_t>(dev)]++ % static_cast<uint64_t>(c_.lite_every) != 0) {
+        s.value[kPmcMfmaBusy] = last.value[kPmcMfmaBusy];
+        s.value[kPmcTaBusy] = last.value[kPmcTaBusy];
+        std::copy(last.xcd_mfma, last.xcd_mfma + kMaxXcc, s.xcd_mfma);
+        std::copy(last.xcd_ta, last.xcd_ta + kMaxXcc, s.xcd_ta);
+        s.se_fresh = 0;
+      } else {
+        last = s;
+      }
+    }
     if (c_.batch > 1 && dev >= 0 && static_cast<size_t>(dev) < delayed_.size()) {
       std::deque<PmcSample>& q = delayed_[static_cast<size_t>(dev)];  // this device's sampler thread only
       q.push_back(s);
@@ -230,6 +248,8 @@ class MockCounterSource final : public CounterSource {
   std::vector<int64_t> restart_;  // per device: time of the last acquire (0 = never released)
   std::vector<uint64_t> restart_reads_;  // per device: samples taken at the last acquire
   std::vector<std::deque<PmcSample>> delayed_;  // per device: samples held back (MockPmcConfig::batch)
+  std::vector<PmcSample> se_last_;              // per device: the last sample that read the per-SE counters
+  std::vector<uint64_t> se_n_;                  // per device: samples since the last (re)START (lite_every)
   std::vector<std::unique_ptr<Fault>> fault_;
 };
 
@@ -241,6 +261,7 @@ using sample_ts_fn = int (*)(int, uint64_t*, int, uint32_t*, int64_t*);
 using sample_xcd_fn = int (*)(int, int, uint64_t*, int);
 using pipelined_fn = int (*)(int, int, char*, int);
 using configure_fn = int (*)(const char*, int);
+using se_fresh_fn = int (*)(int);
 using close_fn = void (*)(int);
 using info_fn = int (*)(int, char*, int);
 using abort_fn = int (*)(int, int);
@@ -259,7 +280,7 @@ class DlCounterSource final : public CounterSource {
   }
 
   bool load(const std::string& path, const Backend& be, const std::vector<int>& devices, bool pipelined,
-            uint32_t mask, int lean, int timeout_ms, int batch, int publish_us, std::string& err) {
+            uint32_t mask, int lean, int timeout_ms, int batch, int publish_us, bool lite, std::string& err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!lib_) {
       err = std::string("dlopen failed: ") + dlerror();
@@ -281,6 +302,9 @@ class DlCounterSource final : public CounterSource {
     if (configure && timeout_ms > 0) configure("timeout_ms", timeout_ms);
     if (configure && batch > 1 && configure("batch", batch) != 0) err += "reader ignores batch=" + std::to_string(batch) + "; ";
     if (configure && batch > 1 && publish_us >= 0) configure("publish_us", publish_us);
+    // explicit either way: the setting is process-wide in the reader library
+    if (configure && configure("lite", lite ? 1 : 0) != 0 && lite) err += "reader ignores lite; ";
+    se_fresh_ = reinterpret_cast<se_fresh_fn>(dlsym(lib_, "kgs_pmc_se_fresh"));  // optional
     abort_ = reinterpret_cast<abort_fn>(dlsym(lib_, "kgs_pmc_abort"));  // optional (aqlprofile reader)
     reset_ = reinterpret_cast<reset_fn>(dlsym(lib_, "kgs_pmc_reset"));  // optional
     stats_ = reinterpret_cast<stats_fn>(dlsym(lib_, "kgs_pmc_stats"));  // optional
@@ -425,6 +449,7 @@ class DlCounterSource final : public CounterSource {
           sample_xcd_(handles_[dev], reader_idx_[kPmcTaBusy], s.xcd_ta, kMaxXcc) != static_cast<int>(s.n_xcd))
         std::fill(s.xcd_ta, s.xcd_ta + kMaxXcc, 0);
     }
+    s.se_fresh = se_fresh_ ? (se_fresh_(handles_[dev]) != 0 ? 1u : 0u) : 1u;
     s.mono_ns = ts > 0 ? ts : mono_ns();  // when the CP read the counters (pipelined: previous call)
     return 0;
   }
@@ -435,6 +460,7 @@ class DlCounterSource final : public CounterSource {
   sample_fn sample_ = nullptr;
   sample_ts_fn sample_ts_ = nullptr;
   sample_xcd_fn sample_xcd_ = nullptr;
+  se_fresh_fn se_fresh_ = nullptr;
   pipelined_fn set_pipe_ = nullptr;
   bool pipelined_ = false;
   const char* names_[kPmcCount] = {};
@@ -468,9 +494,9 @@ std::unique_ptr<CounterSource> make_mock_counter_source(const Backend& be, const
 std::unique_ptr<CounterSource> make_dl_counter_source(const std::string& name, const std::string& lib_path,
                                                       const Backend& be, const std::vector<int>& devices,
                                                       bool pipelined, uint32_t mask, int lean, std::string& err,
-                                                      int timeout_ms, int batch, int publish_us) {
+                                                      int timeout_ms, int batch, int publish_us, bool lite) {
   auto s = std::make_unique<DlCounterSource>(name);
-  if (!s->load(lib_path, be, devices, pipelined, mask, lean, timeout_ms, batch, publish_us, err)) return nullptr;
+  if (!s->load(lib_path, be, devices, pipelined, mask, lean, timeout_ms, batch, publish_us, lite, err)) return nullptr;
   return s;
 }
 

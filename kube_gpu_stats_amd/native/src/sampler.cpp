@@ -564,6 +564,10 @@ void Sampler::run_pmc(Worker& w) {
   PmcSample& pmc_base = st.pmc_base;
   bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
   uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0, prev_ps_cpc = 0;
+  // ... and at the previous drain that read the per-SE counters (lite READs: the publishers)
+  bool have_prev_se = false;
+  uint64_t prev_se_count = 0, prev_se_mfma = 0;
+  int64_t prev_se_ns = 0;
   // The READ packet's own CPC busy (clock cycles), learned on intervals without waves,
   // separately for synchronous (quiet GPU) and pipelined READs: EWMA and samples seen.
   double read_cyc[2] = {0, 0};
@@ -586,6 +590,9 @@ void Sampler::run_pmc(Worker& w) {
     have_prev_ps = true;
     prev_ps_count = prev_ps_mfma = prev_ps_active = prev_ps_cpc = 0;
     prev_ps_ns = t;
+    have_prev_se = true;
+    prev_se_count = prev_se_mfma = 0;
+    prev_se_ns = t;
     quiet = false;
     quiet_since_ns = 0;
     gap = false;
@@ -617,6 +624,7 @@ void Sampler::run_pmc(Worker& w) {
     st.pmc_retry_at_ns = now + static_cast<int64_t>(st.pmc_backoff_s * 1e9);
     st.pmc_backoff_s = std::min(st.pmc_backoff_s * 2, cfg_.pmc_retry_max_s);
     have_prev_ps = false;
+    have_prev_se = false;
   };
 
   while (!stop_.load(std::memory_order_relaxed)) {
@@ -702,13 +710,20 @@ void Sampler::run_pmc(Worker& w) {
           const double mhz = raw >= prev_ps_count ? (raw - prev_ps_count) * 1e3 / (ps.mono_ns - prev_ps_ns) : 0.0;
           if (mhz >= kPlausibleMhzLo && mhz <= kPlausibleMhzHi) last_plausible_ns = ps.mono_ns;
         }
-        if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcMfmaBusy)) &&
-            ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcMfmaBusy] >= prev_ps_mfma) {
-          // MFMA-busy share of all SIMD-cycles in the interval, times its length.
+        // MFMA-busy share of all SIMD-cycles since the previous drain that read the
+        // per-SE counters (every drain, unless lite READs are on), times that span.
+        if (ps.se_fresh && have_prev_se && ps.mono_ns > prev_se_ns && (ps.mask & (1u << kPmcMfmaBusy)) &&
+            ps.value[kPmcGrbmCount] > prev_se_count && ps.value[kPmcMfmaBusy] >= prev_se_mfma) {
           const double simds = (info.num_cu > 0 ? info.num_cu : 256) * 4.0;
-          const double frac = static_cast<double>(ps.value[kPmcMfmaBusy] - prev_ps_mfma) /
-                              (simds * static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count));
-          P.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
+          const double frac = static_cast<double>(ps.value[kPmcMfmaBusy] - prev_se_mfma) /
+                              (simds * static_cast<double>(ps.value[kPmcGrbmCount] - prev_se_count));
+          P.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_se_ns) * 1e-9;
+        }
+        if (ps.se_fresh) {
+          have_prev_se = true;
+          prev_se_count = ps.value[kPmcGrbmCount];
+          prev_se_mfma = ps.value[kPmcMfmaBusy];
+          prev_se_ns = ps.mono_ns;
         }
         if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcGrbmActive)) &&
             ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcGrbmActive] >= prev_ps_active) {
@@ -816,7 +831,7 @@ void Sampler::run_pmc(Worker& w) {
           }
         ps.seq = ++pmc_seq;
         st.pmc_ring.push(ps);
-        if (ps.mono_ns - last_slow_ns >= kPmcSlowNs) {
+        if (ps.se_fresh && ps.mono_ns - last_slow_ns >= kPmcSlowNs) {  // window gauges: fresh MFMA / TA
           st.pmc_slow_ring.push(ps);
           last_slow_ns = ps.mono_ns;
         }
@@ -844,6 +859,7 @@ void Sampler::run_pmc(Worker& w) {
             st.pmc_retry_at_ns = t + 1000000000LL;
             ++P.pmc_errors;
             have_prev_ps = false;
+            have_prev_se = false;
             last_plausible_ns = t;
             last_start_ns = t;
           }

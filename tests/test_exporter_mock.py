@@ -908,3 +908,25 @@ def test_util_counter_set_exports_the_utilisation_only(mock_exporter):
     (_, sm), = m["container_gpu_sm_util"]
     assert sm == pytest.approx(25, abs=6)                     # from the counters, not the PMFW floor of 99
     assert m["amdgpu_gpu_active_percent"][0][1] == pytest.approx(25, abs=6)
+
+
+def test_lite_reads_keep_the_mfma_integral_exact(mock_exporter):
+    """--pmc-lite: a batch's non-publishing READs skip the per-SE counters (MFMA busy:
+    32 of the base set's 56 register copies), so they carry the last values read.  The
+    MFMA integral spans fresh drains only and the window gauges use fresh drains, so
+    both stay what every-READ reading gives (mock: 50 % busy × mfma_frac 0.6)."""
+    kw = dict(n_gpus=1, hz=2000, pmc_source="mock", pmc_idle_hz=0, window_s=0.5, proc_every=0, link_every=0,
+              mock={"util_base": 50, "util_amp": 0})
+    rates = {}
+    for lite in (0, 8):
+        ex = mock_exporter(mock_pmc={"lite_every": lite}, **kw)
+        time.sleep(0.3)
+        a, t0 = ex.integrals(0), time.time()
+        time.sleep(1.0)
+        b, dt = ex.integrals(0), time.time() - t0
+        rates[lite] = (b["mfma_busy_seconds"] - a["mfma_busy_seconds"]) / dt
+        m = parse_text(ex.render())
+        assert m["amdgpu_mfma_util_percent"][0][1] == pytest.approx(60, abs=2), lite
+        assert (b["active_seconds"] - a["active_seconds"]) / dt == pytest.approx(0.5, abs=0.03)
+        ex.stop()
+    assert rates[0] == pytest.approx(0.3, abs=0.02) and rates[8] == pytest.approx(rates[0], abs=0.02), rates

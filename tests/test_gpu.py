@@ -1742,3 +1742,54 @@ def test_hbm_bandwidth_model_across_access_patterns(torch_dev):
     assert 0.2 < g < 5.0, rows                         # reported as the band; it moves HBM, whatever the ratio
     assert rows["reread_64MiB_mall"]["counted_over_requested"] < 0.5, rows   # cache hits are not HBM traffic
     assert rows["reread_2MiB_l2"]["counted_over_requested"] < 0.5, rows
+
+
+def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
+    """--pmc-lite on MI355X: at 8 kHz with batches of 8, seven of every eight READs leave
+    out the per-SE MFMA counters (their IB's per-SE COPY_DATA packets are NOPs).  Under
+    back-to-back MFMA kernels the MFMA busy integral and the window's MFMA util must
+    match an exporter that reads them every time, and the dispatch integral must not
+    move."""
+    import torch
+
+    from kube_gpu_stats_amd.native import pmc_lib_path
+    from kube_gpu_stats_amd.ops.load import LoadStep
+
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=8000, stream_bytes=1 << 26)
+    ls.run_mfma()
+    torch.cuda.synchronize()
+    rows = {}
+    for lite in (False, True):
+        ex = N.Exporter({"backend": "amdsmi", "hz": 8000, "port": -1, "pmc_source": "aqlprofile",
+                         "pmc_lib": pmc_lib_path("aqlprofile"), "proc_period_s": 0, "link_period_s": 0,
+                         "pmc_batch": 8, "pmc_lite": lite})
+        assert not ex.pmc_error, ex.pmc_error
+        ex.start()
+        try:
+            for _ in range(3):
+                ls.run_mfma()
+            torch.cuda.synchronize()
+            a, t0 = ex.integrals(0), time.time()
+            while time.time() - t0 < 1.5:
+                for _ in range(4):
+                    ls.run_mfma()
+                torch.cuda.synchronize()
+            b, dt = ex.integrals(0), time.time() - t0
+            w = ex.window(0, 1.0)
+            info = ex.pmc_info(0)
+        finally:
+            ex.stop()
+        lite_field = next((x for x in info.split(";") if x.startswith("lite=")), "")
+        rows["lite" if lite else "full"] = {
+            "mfma_busy_pct": 100 * (b["mfma_busy_seconds"] - a["mfma_busy_seconds"]) / dt,
+            "dispatch_pct": 100 * (b["dispatch_seconds"] - a["dispatch_seconds"]) / dt,
+            "mfma_util_pct": w["mfma_util_pct"], "reads_per_s": (b["pmc_samples"] - a["pmc_samples"]) / dt,
+            "lite": lite_field}
+    _keep("lite_reads.json", json.dumps(rows, indent=1))
+    print(json.dumps(rows))
+    f, l = rows["full"], rows["lite"]
+    assert f["lite"].startswith("lite=0") and l["lite"].startswith("lite=1:"), rows
+    assert int(l["lite"].split(":")[1]) > 1000, rows                  # lite READs did run
+    assert f["mfma_busy_pct"] > 50 and abs(l["mfma_busy_pct"] - f["mfma_busy_pct"]) < 3, rows
+    assert abs(l["mfma_util_pct"] - f["mfma_util_pct"]) < 3, rows
+    assert abs(l["dispatch_pct"] - f["dispatch_pct"]) < 2 and l["reads_per_s"] > 7000, rows

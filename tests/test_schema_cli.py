@@ -200,3 +200,14 @@ def test_amd_smi_tiers_are_floored_at_khz_tick_rates():
     assert periods("--hz", "10") == (1.0, 10.0)                     # the DaemonSet rate: as before
     assert periods("--hz", "8000", "--proc-every", "0", "--link-every", "0") == (0.0, 0.0)
     assert periods("--hz", "8000", "--proc-period", "0.02", "--link-period", "0.5") == (0.02, 0.5)  # explicit wins
+
+
+@pytest.mark.parametrize("sub", ["exporter", "who-use-gpu", "gpu-util-stats", "ps", "dmon", "record", "topo", "pmc",
+                                 "scrape"])
+def test_every_subcommand_help_renders(sub):
+    """argparse formats every help string with %: a bare % in one flag's help breaks
+    `--help` for the whole subcommand."""
+    r = subprocess.run([sys.executable, "-m", "kube_gpu_stats_amd.cli", sub, "--help"], cwd=REPO,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "usage:" in r.stdout

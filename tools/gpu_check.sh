@@ -71,7 +71,7 @@ for s in $STEPS; do
     cpprobe) run cp_busy_probe 240 python -u tools/cp_busy_probe.py --out "$OUT/cp_busy_probe.json" ;;
     cpdump) run cp_dump 300 python -u tools/cp_busy_probe.py --rates 8000,1000 --pipelined 1 --secs 2 \
               --out "$OUT/cp_busy_pipelined.json" --dump "$OUT/cp_dump.json" --dump-rates 8000,1000 ;;
-    graphutil) run graph_util 300 python -u tools/graph_cost_probe.py --variants full_rate,util_set,default \
+    graphutil) run graph_util 300 python -u tools/graph_cost_probe.py --variants full_rate,util_set,lite,default \
                  --out "$OUT/graph_util.json" ;;
     graphcost) run graph_cost 400 python -u tools/graph_cost_probe.py --out "$OUT/graph_cost.json" ;;
     testsnw) run pytest_gpu 700 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \

@@ -14,7 +14,8 @@ probe measures only that component, for several exporter variants on the same bo
   queue variants measured the same there and were deleted);
 * ``batch1``    — --pmc-cp-only-min 0 --pmc-batch 1 (every READ writes the L2 back);
 * ``hz1000`` / ``hz100`` — the full-rate reader at 1 kHz / 100 Hz;
-* ``util_set``  — full rate, --pmc-set util (24 register reads per READ instead of 56).
+* ``util_set``  — full rate, --pmc-set util (24 register reads per READ instead of 56);
+* ``lite``      — full rate, --pmc-lite (7 of 8 READs without the 32 per-SE MFMA reads).
 
 Per variant one exporter process (--hz 8000, --control-http) and ``--rounds`` paired
 rounds of two blocks — exporter paused / sampling, order alternating (ABBA) — each
@@ -43,6 +44,7 @@ VARIANTS = {
     "hz1000": ({}, ["--pmc-cp-only-min", "0", "--hz", "1000"]),
     "hz100": ({}, ["--pmc-cp-only-min", "0", "--hz", "100"]),
     "util_set": ({}, ["--pmc-cp-only-min", "0", "--pmc-set", "util"]),
+    "lite": ({}, ["--pmc-cp-only-min", "0", "--pmc-lite"]),
 }
 T975 = {5: 2.571, 7: 2.365, 11: 2.201, 15: 2.131, 23: 2.069, 31: 2.040, 47: 2.012}
 
