@@ -98,7 +98,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "pmc-publish-us", 1000, "longest a batched counter READ waits for its L2 writeback: a READ writes "
                                          "back early when the next tick would be later (at <= 1 kHz every READ does)")
     add_flag(ap, "pmc-lite", False, "lite READs: a batch's non-publishing READs skip the per-SE counters (MFMA busy, "
-                                    "TA), 32 of the base set's 56 register copies, which a µs-kernel stream pays for; "
+                                    "TA): a compacted READ without the 32 per-SE copies of the base set's 56, which "
+                                    "a µs-kernel stream pays for; "
                                     "MFMA and per-XCD values then update at the publish rate (1 kHz at 8 kHz ticks), "
                                     "their integrals stay exact")
     add_flag(ap, "pmc-timeout-ms", 250, "bound of every wait on the command processor (counter READ, START, STOP, "

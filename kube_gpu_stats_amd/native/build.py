@@ -123,6 +123,7 @@ def build_pmc_aql(force: bool = False, verbose: bool = False) -> str:
     out = pmc_aql_lib_path()
     src = os.path.join(HERE, "counters", "pmc_aqlprofile.cpp")
     deps = [src, os.path.join(HERE, "include", "kgs", "aql_ring.h"), os.path.join(HERE, "include", "kgs", "aql_batch.h"),
+            os.path.join(HERE, "include", "kgs", "aql_ib.h"),
             __file__]
     if not force and not _stale(out, deps):
         return out

@@ -66,6 +66,7 @@
 #include <vector>
 
 #include "kgs/aql_batch.h"
+#include "kgs/aql_ib.h"
 #include "kgs/aql_ring.h"
 
 namespace {
@@ -125,6 +126,9 @@ struct Agent {
   // Lite READs (kgs_pmc_configure("lite")): the batch's non-publishing READs leave
   // the per-SE counters out; their values are the last read ones (se_*).
   bool plite[kMaxSlots] = {};                        // slot k's READ IB is lite
+  void* plib[kMaxSlots] = {};                        // ... its compacted IB (kgs/aql_ib.h)
+  uint32_t plib_sz[kMaxSlots] = {};
+  std::string lite_why;                              // why a slot kept the full IB; guarded by info_mu
   bool se_have = false;                              // se_* hold a full READ's values since the last START
   std::vector<double> se_vals, se_vals_xcd;
   std::vector<uint32_t> se_seen, se_inst;
@@ -565,12 +569,6 @@ void dump_packet(const char* name, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
   std::fprintf(stderr, "\n");
 }
 
-// SET_UCONFIG_REG offset of GRBM_GFX_INDEX, and its SE_BROADCAST_WRITES bit: the
-// READ IB selects one SE (bit clear) before copying a per-SE block's counters (SQ,
-// TA), and broadcasts again (0xe0000000) for the GRBM / CP ones
-// (profiles/r1/lean/read_packet_dump_base.txt).
-constexpr uint32_t kGrbmGfxIndex = 0x200, kSeBroadcast = 1u << 31;
-
 // Lean READ.  aqlprofile's READ IB (decoded with KGS_AQL_DUMP=1,
 // profiles/read_packet.md) brackets the per-XCC register copies with a
 // CS_PARTIAL_FLUSH on every XCC and ends with an ACQUIRE_MEM that invalidates
@@ -582,11 +580,9 @@ constexpr uint32_t kGrbmGfxIndex = 0x200, kSeBroadcast = 1u << 31;
 // 2 (default) = 1 + ACQUIRE_MEM reduced to the L2 writeback that publishes the
 // CP's COPY_DATA results; 3 = 1 + no ACQUIRE_MEM.  Cost-attribution modes
 // (KGS_AQL_LEAN only; the counter values they return are stale): 4 = 3 + no
-// COPY_DATA, 5 = every packet of the IB a NOP.  `lite` also drops the per-SE
-// copies (the MFMA busy's 32 of the base set's 56 results: the READ's CP time
-// grows with its register copies, profiles/r4/).  Returns packets changed.
+// COPY_DATA, 5 = every packet of the IB a NOP.  Returns packets changed.
 int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<volatile uint32_t*>* dsts = nullptr,
-                 const void* out = nullptr, size_t out_sz = 0, bool lite = false) {
+                 const void* out = nullptr, size_t out_sz = 0) {
   if (mode <= 0) return 0;
   uint32_t dw[4];
   std::memcpy(dw, pkt.pm4_command + 1, sizeof dw);
@@ -596,17 +592,12 @@ int lean_read_ib(const hsa_ext_amd_aql_pm4_packet_t& pkt, int mode, std::vector<
   uint32_t* ib = reinterpret_cast<uint32_t*>(addr);
   auto nop = [&](uint32_t at, uint32_t len) { ib[at] = (3u << 30) | ((len - 2) << 16) | (0x10u << 8); };
   int changed = 0;
-  bool se_sel = false;  // GRBM_GFX_INDEX selects one SE: the copies read a per-SE counter
   for (uint32_t i = 0; i < ndw;) {
     const uint32_t h = ib[i];
     if ((h >> 30) == 2) { ++i; continue; }
     if ((h >> 30) != 3) return -2;
     const uint32_t opc = (h >> 8) & 0xFF, len = ((h >> 16) & 0x3FFF) + 2;
-    if (opc == 0x79 && len >= 3 && ib[i + 1] == kGrbmGfxIndex) se_sel = !(ib[i + 2] & kSeBroadcast);
-    if (lite && se_sel && opc == 0x40 && len == 6 && ((ib[i + 1] >> 8) & 0xF) == 5) {
-      nop(i, len);  // lite READ: no per-SE copy, and no landing check for its dwords
-      ++changed;
-    } else if (mode >= 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
+    if (mode >= 5 || (mode == 4 && opc == 0x40)) {  // cost attribution: NOP the packet
       if (opc != 0x10) {
         nop(i, len);
         ++changed;
@@ -987,6 +978,55 @@ bool same_events(const std::vector<hsa_ven_amd_aqlprofile_event_t>& x,
   return true;
 }
 
+// Lite READ for slot k (--pmc-lite): point its READ packet at a compacted copy of
+// its IB without the per-SE sections (kgs/aql_ib.h), and drop those results from
+// the slot's landing check.  false (the slot keeps the full IB) if the IB does not
+// compact cleanly; the reason goes to kgs_pmc_info.
+bool make_lite(Agent* a, int k, uint32_t cmd_sz) {
+  auto why = [a](const std::string& w) {
+    std::lock_guard<std::mutex> g(a->info_mu);
+    a->lite_why = w;
+    return false;
+  };
+  uint32_t dw[4];
+  std::memcpy(dw, a->pread[k].pm4_command + 1, sizeof dw);
+  if (((dw[0] >> 8) & 0xFF) != 0x3F) {
+    return why("READ packet is not an INDIRECT_BUFFER");
+  }
+  const uint64_t addr = (static_cast<uint64_t>(dw[1]) | (static_cast<uint64_t>(dw[2] & 0xFFFF) << 32)) & ~3ull;
+  const uint32_t ndw = dw[3] & 0xFFFFF;
+  std::vector<uint32_t> out;
+  const kgs::IbCompact c = kgs::compact_se_sections(reinterpret_cast<const uint32_t*>(addr), ndw, out);
+  if (!c.ok) {
+    return why(c.why);
+  }
+  if (a->plib[k] && a->plib_sz[k] < cmd_sz) {
+    hsa_amd_memory_pool_free(a->plib[k]);
+    a->plib[k] = nullptr;
+  }
+  if (!a->plib[k]) {
+    a->plib[k] = host_alloc(a, cmd_sz);
+    a->plib_sz[k] = a->plib[k] ? cmd_sz : 0;
+  }
+  if (!a->plib[k] || out.size() * 4 > cmd_sz) {
+    return why("no memory for the compacted IB");
+  }
+  std::memcpy(a->plib[k], out.data(), out.size() * 4);
+  const uint64_t na = reinterpret_cast<uint64_t>(a->plib[k]);
+  dw[1] = static_cast<uint32_t>(na) | (dw[1] & 3u);
+  dw[2] = (dw[2] & ~0xFFFFu) | static_cast<uint32_t>((na >> 32) & 0xFFFF);
+  dw[3] = (dw[3] & ~0xFFFFFu) | static_cast<uint32_t>(out.size());
+  std::memcpy(a->pread[k].pm4_command + 1, dw, sizeof dw);
+  auto& d = a->pdst[k];
+  d.erase(std::remove_if(d.begin(), d.end(),
+                         [&](volatile uint32_t* p) {
+                           const uint64_t x = reinterpret_cast<uint64_t>(p);
+                           return std::find(c.dropped_dsts.begin(), c.dropped_dsts.end(), x) != c.dropped_dsts.end();
+                         }),
+          d.end());
+  return true;
+}
+
 // Two READ slots for pipelined mode: the session's events, own buffers and
 // signals.  Only their READ packets are ever submitted (START/STOP come from the
 // main profile).  Called again when a re-open changed the event list: the slot
@@ -1024,8 +1064,8 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
     // drop the ACQUIRE_MEM (lean 3).  Every slot notes its result dwords.
     a->pdst[k].clear();
     const int mode = a->batch >= 2 && !is_publisher(a, k) ? 3 : lean_mode();
-    a->plite[k] = lite_on() && a->batch >= 2 && !is_publisher(a, k) && mode > 0;
-    if (mode > 0) lean_read_ib(a->pread[k], mode, &a->pdst[k], a->pout[k], out_sz, a->plite[k]);
+    if (mode > 0) lean_read_ib(a->pread[k], mode, &a->pdst[k], a->pout[k], out_sz);
+    a->plite[k] = lite_on() && a->batch >= 2 && !is_publisher(a, k) && mode > 0 && make_lite(a, k, cmd_sz);
   }
   a->pcmd_sz = std::max(a->pcmd_sz, cmd_sz);
   a->pout_sz = std::max(a->pout_sz, out_sz);
@@ -1386,6 +1426,7 @@ int kgs_pmc_info(int handle, char* buf, int len) {
   {
     std::lock_guard<std::mutex> g(a->info_mu);
     o += a->info_layout;
+    if (!a->lite_why.empty()) o += ";lite_full_ib=" + a->lite_why;
     if (!a->err.empty()) o += ";" + a->err;
   }
   set_err(buf, len, o);

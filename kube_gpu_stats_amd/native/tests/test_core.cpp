@@ -46,6 +46,7 @@
 #include <random>
 
 #include "kgs/aql_batch.h"
+#include "kgs/aql_ib.h"
 #include "kgs/aql_ring.h"
 #include "kgs/backend.h"
 #include "kgs/exporter.h"
@@ -802,7 +803,105 @@ static void test_batch_plan() {
   std::printf("batch plan ok\n");
 }
 
+// Lite READ IB (kgs/aql_ib.h): a synthetic READ shaped like aqlprofile's
+// (profiles/r1/lean/read_packet_dump_base.txt): a latch, one PRED_EXEC region per
+// XCC with three broadcast GRBM/CP counters and four per-SE SQ sections, lean NOPs,
+// a trailing ACQUIRE_MEM.
+namespace {
+uint32_t t3(uint32_t op, uint32_t len) { return (3u << 30) | ((len - 2) << 16) | (op << 8); }
+void put_index(std::vector<uint32_t>& ib, uint32_t v) {
+  ib.push_back(t3(kPm4SetUconfigReg, 3));
+  ib.push_back(kGrbmGfxIndexReg);
+  ib.push_back(v);
+}
+void put_copy(std::vector<uint32_t>& ib, uint32_t reg, uint64_t dst) {
+  ib.push_back(t3(kPm4CopyData, 6));
+  ib.push_back(0x500);  // src_sel register, dst_sel memory (5)
+  ib.push_back(reg);
+  ib.push_back(0);
+  ib.push_back(static_cast<uint32_t>(dst));
+  ib.push_back(static_cast<uint32_t>(dst >> 32));
+}
+std::vector<uint32_t> synthetic_read(bool odd_se_section, uint64_t* n_global) {
+  std::vector<uint32_t> ib;
+  uint64_t dst = 0x7f0000001000ull;
+  *n_global = 0;
+  ib.push_back(t3(kPm4SetUconfigReg, 3));  // CP_PERFMON_CNTL latch
+  ib.push_back(0x1808);
+  ib.push_back(0x401);
+  for (int x = 0; x < 8; ++x) {
+    const size_t pred = ib.size();
+    ib.push_back(t3(kPm4PredExec, 2));
+    ib.push_back((1u << (24 + (x % 8))) | 0);  // count patched below
+    const size_t body = ib.size();
+    ib.push_back(t3(kPm4Nop, 2));  // CS_PARTIAL_FLUSH turned NOP by the lean rewrite
+    ib.push_back(0);
+    for (uint32_t c = 0; c < 3; ++c) {  // GRBM_COUNT, GRBM_SPI_BUSY, CPC busy: LO / HI
+      put_index(ib, 0xe0000000u);
+      put_copy(ib, 0xd040 + 3 * c, dst); dst += 4;
+      put_copy(ib, 0xd041 + 3 * c, dst); dst += 4;
+      *n_global += 2;
+    }
+    for (uint32_t se = 0; se < 4; ++se) {  // SQ MFMA busy per SE
+      put_index(ib, 0x60000000u | (se << 16));
+      put_copy(ib, 0xd1c0, dst); dst += 4;
+      put_copy(ib, 0xd1c1, dst); dst += 4;
+      if (odd_se_section && x == 3 && se == 2) {  // a non-copy packet inside a per-SE section: kept whole
+        ib.push_back(t3(0x46, 2));
+        ib.push_back(0x407);
+      }
+    }
+    ib[pred + 1] |= static_cast<uint32_t>(ib.size() - body);
+  }
+  ib.push_back(t3(0x58, 7));  // ACQUIRE_MEM (L2 writeback)
+  for (int k = 0; k < 6; ++k) ib.push_back(k == 0 ? (1u << 18) : 0);
+  return ib;
+}
+}  // namespace
+
+static void test_lite_ib() {
+  uint64_t n_global = 0;
+  std::vector<uint32_t> ib = synthetic_read(false, &n_global), out;
+  std::vector<uint64_t> all;
+  CHECK(ib_copy_dsts(ib.data(), static_cast<uint32_t>(ib.size()), &all));
+  CHECK(all.size() == 8 * (6 + 8));
+  IbCompact r = compact_se_sections(ib.data(), static_cast<uint32_t>(ib.size()), out);
+  CHECK(r.ok);
+  CHECK(r.dropped_copies == 8 * 4 * 2);
+  std::vector<uint64_t> kept;
+  std::string why;
+  CHECK(ib_copy_dsts(out.data(), static_cast<uint32_t>(out.size()), &kept, &why));
+  CHECK(kept.size() == n_global);
+  // every kept packet sits under a broadcast GRBM_GFX_INDEX, and every region is closed
+  bool se = false;
+  uint32_t regions = 0;
+  for (uint32_t i = 0; i < out.size();) {
+    if (pm4_gfx_index(out.data() + i, &se)) CHECK(!se);
+    if (pm4_op(out[i]) == kPm4PredExec) ++regions;
+    CHECK(pm4_op(out[i]) != kPm4Nop);
+    i += pm4_len(out[i]);
+  }
+  CHECK(regions == 8);
+  CHECK(out.size() + r.dropped_dw == ib.size());
+  // A per-SE section with anything but copies in it stays whole (its copies too).
+  std::vector<uint32_t> ib2 = synthetic_read(true, &n_global), out2;
+  IbCompact r2 = compact_se_sections(ib2.data(), static_cast<uint32_t>(ib2.size()), out2);
+  CHECK(r2.ok && r2.dropped_copies == 8 * 4 * 2 - 2);
+  // Malformed input: a PRED_EXEC whose region ends inside a packet.
+  std::vector<uint32_t> bad = ib;
+  bad[4] += 1;  // the first region's count
+  std::vector<uint32_t> out3;
+  CHECK(!compact_se_sections(bad.data(), static_cast<uint32_t>(bad.size()), out3).ok);
+  // No per-SE section at all: nothing to gain, the caller keeps the full IB.
+  std::vector<uint32_t> flat;
+  put_index(flat, 0xe0000000u);
+  put_copy(flat, 0xd040, 0x1000);
+  CHECK(!compact_se_sections(flat.data(), static_cast<uint32_t>(flat.size()), out3).ok);
+  std::printf("lite IB ok (%zu -> %zu dwords, %u per-SE copies dropped)\n", ib.size(), out.size(), r.dropped_copies);
+}
+
 int main() {
+  test_lite_ib();
   test_batch_plan();
   test_reserve_slot();
   test_pmc_breaker();

@@ -6,6 +6,7 @@ command-processor counter reader (libkgs_pmc_aql.so: aqlprofile PM4 packets on a
 private AQL queue), mostly in its own exporter process; the rocprofiler-sdk
 device-counting reader appears only as a test-only cross-check of its numbers.
 """
+import gc
 import json
 import os
 import subprocess
@@ -979,7 +980,9 @@ def test_dispatch_bound_rate_at_default_flags(torch_dev):
     g, k, st = rows["tiny_graph"], rows["mfma"], rows["mfma_then_graph"]
     assert g["dispatch_bound_share"] > 0.5 and g["reads_per_s"] < 2500, g
     assert g["dispatch_pct"] > 90, g                       # the integral is exact at the lower READ rate
-    assert k["reads_per_s"] > 7000 and k["dispatch_bound_share"] == 0, k
+    # a few ms-long episodes around kernel boundaries were seen on one box (r4h: 3 of 350
+    # scrapes, 1 % of the ticks skipped); the rate must stay the full one
+    assert k["reads_per_s"] > 7000 and k["dispatch_bound_share"] < 0.05, k
     assert st["reads_per_s"] > 7000, st
 
 
@@ -1245,7 +1248,8 @@ print("done", flush=True)
 
 def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
     """BASELINE config 3 on hardware: two processes share the GPU — tenant A runs a
-    full-grid MFMA loop holding 8 GiB, tenant B sits idle holding 3 GiB.  The
+    full-grid MFMA loop holding 8 GiB, tenant B sits idle holding 5 GiB (not 3: a
+    failed earlier test's frames can keep ≈3.4 GiB alive in this process, r4h).  The
     node-wide slow tier's process list attributes HBM to each (to ±0.75 GiB) and
     the CU-occupancy integral gives A the compute share and B none; each process
     line carries its own pod once the PID→pod table names them.  AMD SMI reports
@@ -1258,7 +1262,7 @@ def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
     torch.cuda.empty_cache()
     env = dict(os.environ, KGS_NO_BUILD="1")
     kids = [subprocess.Popen([sys.executable, "-c", _TENANT, gib, busy, "15", REPO], stdout=subprocess.PIPE,
-                             text=True, env=env) for gib, busy in (("8", "1"), ("3", "0"))]
+                             text=True, env=env) for gib, busy in (("8", "1"), ("5", "0"))]
     ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 50, "proc_period_s": 0.1, "link_every": 0})
     ex.start()
     try:
@@ -1277,7 +1281,7 @@ def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
         p1, t1 = {p["pid"]: p for p in ex.procs(0)}, time.time()
         gib = float(1 << 30)
         a = [pid for pid, p in p1.items() if 8.0 <= p["vram_bytes"] / gib < 8.75]
-        b = [pid for pid, p in p1.items() if 3.0 <= p["vram_bytes"] / gib < 3.75]
+        b = [pid for pid, p in p1.items() if 5.0 <= p["vram_bytes"] / gib < 5.75]
         row = {"procs": {pid: {"vram_gib": round(p["vram_bytes"] / gib, 3), "cu_occupancy": p["cu_occupancy"],
                                "cu_share": round((p["cu_seconds"] - p0.get(pid, {}).get("cu_seconds", 0.0)) / (t1 - t0), 4)}
                          for pid, p in p1.items()}}
@@ -1326,7 +1330,7 @@ def test_two_tenants_per_process_hbm_and_compute_share(N, torch_dev):
     assert row["pod_busy_share"]["tenant-b"] > 0.8, row  # the whole GPU's busy, billed to the idle tenant too
     assert set(ps_rows) == {"tenant-a", "tenant-b"}, ps_rows
     assert 8.0 <= ps_rows["tenant-a"]["hbm_gib"] < 8.75 and ps_rows["tenant-a"]["cu_share_pct"] > 25, ps_rows
-    assert 3.0 <= ps_rows["tenant-b"]["hbm_gib"] < 3.75 and ps_rows["tenant-b"]["cu_share_pct"] < 2, ps_rows
+    assert 5.0 <= ps_rows["tenant-b"]["hbm_gib"] < 5.75 and ps_rows["tenant-b"]["cu_share_pct"] < 2, ps_rows
 
 
 def test_ecc_per_block_counts_on_mi355x(N):
@@ -1746,7 +1750,8 @@ def test_hbm_bandwidth_model_across_access_patterns(torch_dev):
 
 def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
     """--pmc-lite on MI355X: at 8 kHz with batches of 8, seven of every eight READs leave
-    out the per-SE MFMA counters (their IB's per-SE COPY_DATA packets are NOPs).  Under
+    out the per-SE MFMA counters (a compacted copy of their IB without the per-SE
+    sections, kgs/aql_ib.h).  Under
     back-to-back MFMA kernels the MFMA busy integral and the window's MFMA util must
     match an exporter that reads them every time, and the dispatch integral must not
     move."""
@@ -1779,17 +1784,19 @@ def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
             info = ex.pmc_info(0)
         finally:
             ex.stop()
+        del ex
+        gc.collect()  # the reader's session closes with the Exporter: the next one opens the agent again
         lite_field = next((x for x in info.split(";") if x.startswith("lite=")), "")
         rows["lite" if lite else "full"] = {
             "mfma_busy_pct": 100 * (b["mfma_busy_seconds"] - a["mfma_busy_seconds"]) / dt,
             "dispatch_pct": 100 * (b["dispatch_seconds"] - a["dispatch_seconds"]) / dt,
             "mfma_util_pct": w["mfma_util_pct"], "reads_per_s": (b["pmc_samples"] - a["pmc_samples"]) / dt,
-            "lite": lite_field}
+            "lite": lite_field, "full_ib": "lite_full_ib" in info}
     _keep("lite_reads.json", json.dumps(rows, indent=1))
     print(json.dumps(rows))
     f, l = rows["full"], rows["lite"]
     assert f["lite"].startswith("lite=0") and l["lite"].startswith("lite=1:"), rows
-    assert int(l["lite"].split(":")[1]) > 1000, rows                  # lite READs did run
+    assert int(l["lite"].split(":")[1]) > 1000 and not l["full_ib"], rows  # lite READs did run
     assert f["mfma_busy_pct"] > 50 and abs(l["mfma_busy_pct"] - f["mfma_busy_pct"]) < 3, rows
     assert abs(l["mfma_util_pct"] - f["mfma_util_pct"]) < 3, rows
     assert abs(l["dispatch_pct"] - f["dispatch_pct"]) < 2 and l["reads_per_s"] > 7000, rows
