@@ -153,6 +153,7 @@ struct Agent {
   hsa_signal_t psig[kMaxSlots]{};
   uint32_t pcmd_sz = 0, pout_sz = 0;                 // allocated sizes of the slot buffers
   std::vector<hsa_ven_amd_aqlprofile_event_t> pipe_events;  // event list the slot packets were built for
+  bool pipe_lite = false;                                    // ... and whether their non-publishers are lite
   int64_t psubmit_ns[kMaxSlots] = {};
   // Batched publication (kgs_pmc_configure("batch", B), B >= 2; see read_batched
   // and include/kgs/aql_batch.h): 2B slots in two halves of B; only a half's
@@ -1070,6 +1071,7 @@ bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err
   a->pcmd_sz = std::max(a->pcmd_sz, cmd_sz);
   a->pout_sz = std::max(a->pout_sz, out_sz);
   a->pipe_events = a->events;
+  a->pipe_lite = lite_on();
   return true;
 }
 
@@ -1374,7 +1376,8 @@ int kgs_pmc_set_pipelined(int handle, int on, char* err, int errlen) {
     a->inflight = -1;
   }
   batch_drain(a);
-  if (on && (!a->pcmd[0] || !same_events(a->pipe_events, a->events) || a->batch != batch_size())) {
+  if (on && (!a->pcmd[0] || !same_events(a->pipe_events, a->events) || a->batch != batch_size() ||
+             a->pipe_lite != lite_on())) {
     std::string e;
     if (!setup_pipeline(a, a->cmd_sz, a->out_sz, e)) {
       set_err(err, errlen, e);

@@ -78,6 +78,8 @@ for s in $STEPS; do
                -p no:cacheprovider -k "not wedged_counter_queue" ;;
     testsdb) run pytest_dbound 400 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
                -p no:cacheprovider -k "dispatch_bound or dispatch_gap or read_immune" ;;
+    testslite) run pytest_lite 300 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
+                 -p no:cacheprovider -k "lite_reads or dispatch_bound or two_tenants" ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
