@@ -87,7 +87,7 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                          "wave in flight for at least this share of the clocks (a stream of µs "
                                          "kernels, which each READ packet slows by a fixed CP cost), READ at "
                                          "--pmc-gap-hz (0 = off; ignored in profiling mode)")
-    add_flag(ap, "pmc-dispatch-hold-ms", 4.0, "dispatch-bound READ intervals in a row, in ms, before that rate applies "
+    add_flag(ap, "pmc-dispatch-hold-ms", 10.0, "dispatch-bound READ intervals in a row, in ms, before that rate applies "
                                               "(a few ms of small kernels inside a training step keep the full rate)")
     add_flag(ap, "pmc-batch", 8, choices=range(1, 17), help="counter READs per L2 writeback: a READ's results sit in the GPU's L2 until "
                                  "written back, and that writeback is half of what a READ costs a training step; "
@@ -97,7 +97,7 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                  "than unbatched (profiles/r3/README.md r3ab)")
     add_flag(ap, "pmc-publish-us", 1000, "longest a batched counter READ waits for its L2 writeback: a READ writes "
                                          "back early when the next tick would be later (at <= 1 kHz every READ does)")
-    add_flag(ap, "pmc-lite", False, "lite READs: a batch's non-publishing READs skip the per-SE counters (MFMA busy, "
+    add_flag(ap, "pmc-lite", True, "lite READs: a batch's non-publishing READs skip the per-SE counters (MFMA busy, "
                                     "TA): a compacted READ without the 32 per-SE copies of the base set's 56, which "
                                     "a µs-kernel stream pays for; "
                                     "MFMA and per-XCD values then update at the publish rate (1 kHz at 8 kHz ticks), "

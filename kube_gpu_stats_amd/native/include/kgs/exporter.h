@@ -48,7 +48,7 @@ struct ExporterConfig {
   int pmc_timeout_ms = 250;         // bound of every wait on the command processor (fault boundary)
   int pmc_batch = 8;                // counter READs per L2 writeback (aqlprofile reader; 1 = every READ)
   int pmc_publish_us = 1000;        // longest a batched READ waits for its L2 writeback (kgs/aql_batch.h)
-  bool pmc_lite = false;            // a batch's non-publishing READs skip the per-SE counters (MFMA, TA)
+  bool pmc_lite = true;             // a batch's non-publishing READs skip the per-SE counters (MFMA, TA)
   std::string listen_addr = "0.0.0.0";
   int port = 9400;                  // 0 = ephemeral, <0 = no HTTP server
   std::string node_name;

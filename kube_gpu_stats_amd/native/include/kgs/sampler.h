@@ -110,10 +110,11 @@ struct SamplerConfig {
   // READ intervals of the last pmc_dispatch_hold_s had the CP dispatching with no
   // wave in flight for at least pmc_cp_only_min of their clocks, READs drop to
   // pmc_gap_hz; the first interval below restores every tick.  The hold keeps a
-  // few ms of small kernels inside a training step at full rate.  0 = off; off
-  // in profiling mode.
+  // few ms of small kernels inside a training step at full rate (the bench step's
+  // 2000-kernel graph runs 3.5 ms, and past 4 ms on a slow host, r4j).  0 = off;
+  // off in profiling mode.
   double pmc_cp_only_min = 0.3;
-  double pmc_dispatch_hold_s = 0.004;
+  double pmc_dispatch_hold_s = 0.010;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
   // Counter-tier circuit breaker: consecutive failed drains that open it, and the
