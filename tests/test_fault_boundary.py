@@ -63,7 +63,7 @@ def test_slow_counter_reads_do_not_silence_the_gpu_or_its_neighbours(mock_export
     for g in range(8):
         assert pmfw[g] >= 45, pmfw
         if g != 2:
-            assert pmc[g] >= 0.97 * HZ, pmc  # best window; a hung neighbour would hold it far lower
+            assert pmc[g] >= 0.9 * HZ, pmc  # best window (8-CPU CI host: 0.968 seen); a hung neighbour would hold it far lower
     m = parse_text(ex.render())
     busy = {lb["gpu"]: v for lb, v in m["amdgpu_gfx_busy_percent"]}
     assert "2" in busy                              # window gauges still fresh on the slow GPU
@@ -83,7 +83,7 @@ def test_hung_counter_reads_are_isolated_and_stop_is_bounded(mock_exporter):
     assert pmc[5] == 0, pmc
     for g in range(8):
         if g != 5:
-            assert pmc[g] >= 0.97 * HZ, pmc  # best window; a hung neighbour would hold it far lower
+            assert pmc[g] >= 0.9 * HZ, pmc  # best window (8-CPU CI host: 0.968 seen); a hung neighbour would hold it far lower
     # Per-GPU hand-over: releasing the hung GPU returns at once; another GPU's
     # release takes effect on that GPU's own next tick.
     t0 = time.time()
