@@ -412,6 +412,8 @@ class TrainLoad(GpuLoad):
     workload a DaemonSet exporter shares the GPU with.  Random-init weights and
     synthetic tokens; the exporter is measured exactly as with the synthetic load."""
 
+    burst_timed = None  # no MFMA burst kernel of known length: phase U is skipped
+
     def __init__(self, a, device: int, ctx=None):
         import torch
         import torch.nn as nn

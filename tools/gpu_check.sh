@@ -40,7 +40,7 @@ for s in $STEPS; do
         #   tl3agent (lean 3 + agent release) tnop (every READ packet a NOP: the bare
         #   packet's cost; values stale) t1k (1 kHz tier) tgapNN (--pmc-busy-min 0.NN)
         T=(python -u bench.py --load train --steps 10 --warmup 2 --rounds 36 --hz-list 100 --capacity-hz ""
-           --burst-s 0 --quiet-s 0 --component-s 0 --out "$OUT/$s.json")
+           --burst-s 0 --quiet-s 0 --component-s 0 --util-s 0 --out "$OUT/$s.json")
         case $s in
           tdef|tdef2) run $s 600 "${T[@]}" ;;
           tpmfw) run $s 600 "${T[@]}" --pmc none ;;
