@@ -569,10 +569,11 @@ void Sampler::run_pmc(Worker& w) {
   uint64_t prev_se_count = 0, prev_se_mfma = 0;
   int64_t prev_se_ns = 0;
   // The READ packet's own CPC busy (clock cycles), learned on intervals without waves,
-  // separately for synchronous (quiet GPU) and pipelined READs: EWMA and samples seen.
-  double read_cyc[2] = {0, 0};
-  double read_spi[2] = {0, 0};       // ... and its SPI-busy blip (cycles), learned alike
-  uint64_t read_cyc_n[2] = {0, 0};
+  // separately for synchronous (quiet GPU) and pipelined READs, and for full and lite
+  // READs (a lite READ's compacted IB costs the CP less): EWMA and samples seen.
+  double read_cyc[2][2] = {};
+  double read_spi[2][2] = {};        // ... and its SPI-busy blip (cycles), learned alike
+  uint64_t read_cyc_n[2][2] = {};
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
   int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
@@ -742,19 +743,23 @@ void Sampler::run_pmc(Worker& w) {
                                  ? static_cast<double>(ps.value[kPmcGrbmActive] - prev_ps_active)
                                  : 0.0;
           const int m = fresh_mode ? 1 : 0;
+          const int f = ps.se_fresh ? 1 : 0;
           // No wave, no MFMA cycle and the CP mostly idle: the CP busy here is our READ's,
           // and so is the SPI blip (≈0.9 µs per READ: 0.7 % of the clocks at 8 kHz, so the
           // test is the quiet threshold, not "no SPI at all" — r4f: a 0.5 % test kept 2 %
           // of the 8 kHz READ-only intervals, the cheap ones, and learned 13 µs for 15.5).
           if (act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma && cpc < 0.5 * clk) {
-            const bool first = read_cyc_n[m] == 0;
-            read_cyc[m] = first ? cpc : 0.95 * read_cyc[m] + 0.05 * cpc;
-            read_spi[m] = first ? act : 0.95 * read_spi[m] + 0.05 * act;
-            ++read_cyc_n[m];
-            P.cpc_read_us = read_cyc[m] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
+            const bool first = read_cyc_n[m][f] == 0;
+            read_cyc[m][f] = first ? cpc : 0.95 * read_cyc[m][f] + 0.05 * cpc;
+            read_spi[m][f] = first ? act : 0.95 * read_spi[m][f] + 0.05 * act;
+            ++read_cyc_n[m][f];
+            if (f) P.cpc_read_us = read_cyc[m][f] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
           }
+          // This READ's learned cost, or the other kind's before it has its own.
+          const int k = read_cyc_n[m][f] ? f : 1 - f;
+          const double rcyc = read_cyc[m][k];
           // Waves of the workload: SPI busy less the READ's own blip.
-          const double wav = std::max(0.0, act - read_spi[m]);
+          const double wav = std::max(0.0, act - read_spi[m][k]);
           // An interval the CP was busy for ≥ kCpcFullFrac counts whole: under a
           // kernel the CPC idles a few % of each 125 µs interval at 8 kHz (r4f: MFMA and
           // GEMM intervals 0.95-1.0), and subtracting a READ-only cost there under-read
@@ -762,7 +767,7 @@ void Sampler::run_pmc(Worker& w) {
           // overlaps dispatch busy — (cpc − read) / (1 − read/clk) — over-read 8 kHz
           // burst trains; tools/util_estimator_sim.py replays the variants on r4f's raw
           // READs.)
-          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(wav, std::max(0.0, cpc - read_cyc[m]));
+          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(wav, std::max(0.0, cpc - rcyc));
           P.dispatch_seconds += std::min(1.0, busy / clk) * (ps.mono_ns - prev_ps_ns) * 1e-9;
           ++P.dispatch_drains;
           // Dispatch-bound: the CP dispatching with no wave in flight for a large share.
