@@ -151,6 +151,11 @@ constexpr int64_t kQuietHoldNs = 5000000;
 // dispatch in flight throughout (the READ's own CP time hides under the workload's;
 // the CPC idles a few % of each 125 µs interval under a long kernel at 8 kHz, r4f).
 constexpr double kCpcFullFrac = 0.90;
+// ... and a READ interval at least this long that mixes a kernel with idle is split by
+// the learned busy / idle shader clocks (at 8 kHz the edge intervals are short and the
+// split over-read 0.2 ms bursts in replay, tools/util_estimator_sim.py; at 1 kHz it
+// closes most of a 1 ms-burst train's −1.3 … −2.3 points).
+constexpr int64_t kClockSplitNs = 400000;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };

@@ -574,6 +574,10 @@ void Sampler::run_pmc(Worker& w) {
   double read_cyc[2][2] = {};
   double read_spi[2][2] = {};        // ... and its SPI-busy blip (cycles), learned alike
   uint64_t read_cyc_n[2][2] = {};
+  // Shader clock while the CP is busy throughout an interval, and in READ-only ones
+  // (EWMA, Hz; 0 = none yet): a long interval that mixes a kernel with idle weighs
+  // each part by its clock (kClockSplitNs).
+  double clk_busy_hz = 0, clk_idle_hz = 0;
   bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
   int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
@@ -754,6 +758,8 @@ void Sampler::run_pmc(Worker& w) {
             read_spi[m][f] = first ? act : 0.95 * read_spi[m][f] + 0.05 * act;
             ++read_cyc_n[m][f];
             if (f) P.cpc_read_us = read_cyc[m][f] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
+            const double hz_now = clk / ((ps.mono_ns - prev_ps_ns) * 1e-9);
+            clk_idle_hz = clk_idle_hz > 0 ? 0.95 * clk_idle_hz + 0.05 * hz_now : hz_now;
           }
           // This READ's learned cost, or the other kind's before it has its own.
           const int k = read_cyc_n[m][f] ? f : 1 - f;
@@ -768,7 +774,19 @@ void Sampler::run_pmc(Worker& w) {
           // burst trains; tools/util_estimator_sim.py replays the variants on r4f's raw
           // READs.)
           const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(wav, std::max(0.0, cpc - rcyc));
-          P.dispatch_seconds += std::min(1.0, busy / clk) * (ps.mono_ns - prev_ps_ns) * 1e-9;
+          const int64_t span_ns = ps.mono_ns - prev_ps_ns;
+          double share = std::min(1.0, busy / clk);
+          if (cpc >= kCpcFullFrac * clk) {
+            const double hz_now = clk / (span_ns * 1e-9);
+            clk_busy_hz = clk_busy_hz > 0 ? 0.95 * clk_busy_hz + 0.05 * hz_now : hz_now;
+          } else if (span_ns >= kClockSplitNs && share > 0 && clk_busy_hz > 0 && clk_idle_hz > 0) {
+            // A cycle share under-weights a kernel that ran at a lower clock than the
+            // idle rest of the interval (MFMA under the power cap: ≈2.1 GHz against
+            // ≈2.4 idle): the time share is s·r / (1 − s + s·r), r = f_idle / f_busy.
+            const double r = std::clamp(clk_idle_hz / clk_busy_hz, 0.8, 1.25);
+            share = share * r / (1.0 - share + share * r);
+          }
+          P.dispatch_seconds += share * span_ns * 1e-9;
           ++P.dispatch_drains;
           // Dispatch-bound: the CP dispatching with no wave in flight for a large share.
           dbound_interval = cfg_.pmc_cp_only_min > 0 && busy - wav >= cfg_.pmc_cp_only_min * clk;

@@ -9,7 +9,9 @@ integral the way the sampler's dispatch integral does (``sampler.cpp``, the
 
 * ``shipped``  — the sampler from r4g: the whole interval if CPC busy ≥ 90 % of the
   clocks, else max(SPI − the READ's SPI blip, CPC − the READ's CP cost), share × Δt;
-  both READ costs learned on every READ-only interval (SPI < 2 % of the clocks);
+  both READ costs learned on every READ-only interval (SPI < 2 % of the clocks); from
+  r4q a partial interval ≥ 400 µs long is split by the learned busy / idle clocks
+  (share s → s·r / (1 − s + s·r), r = f_idle / f_busy);
 * ``r4b``      — the same with a 97 % full threshold, no SPI-blip removal, and the READ
   cost learned only where SPI < 0.5 % of the clocks (rounds r4b–r4f: at 8 kHz that kept
   2 % of the READ-only intervals, the cheap ones);
@@ -60,10 +62,14 @@ def estimate(ivs, learned, variant: str) -> float:
     if variant == "r4b":
         read_spi = 0.0
     tot, span = 0.0, 0.0
+    f_busy, f_idle = 0.0, 0.0
     for dt, clk, spi, cpc in ivs:
         span += dt
         wav = max(0.0, spi - read_spi)  # the READ's own SPI blip is not a wave of the workload
+        if spi < QUIET_SPI * clk and cpc < 0.5 * clk:
+            f_idle = 0.95 * f_idle + 0.05 * clk / dt if f_idle else clk / dt
         if cpc >= full * clk:
+            f_busy = 0.95 * f_busy + 0.05 * clk / dt if f_busy else clk / dt
             tot += dt
             continue
         if variant == "overlap":
@@ -74,7 +80,11 @@ def estimate(ivs, learned, variant: str) -> float:
         if variant == "timesplit" and idle_hz > 0:
             tot += min(dt, max(0.0, dt - (clk - busy) / idle_hz))
         else:
-            tot += min(1.0, busy / clk) * dt
+            s = min(1.0, busy / clk)
+            if variant == "shipped" and dt >= 400e-6 and s > 0 and f_busy and f_idle:
+                r = min(1.25, max(0.8, f_idle / f_busy))
+                s = s * r / (1.0 - s + s * r)
+            tot += s * dt
     return 100.0 * tot / span if span else 0.0
 
 
