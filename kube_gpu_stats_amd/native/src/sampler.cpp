@@ -783,7 +783,10 @@ void Sampler::run_pmc(Worker& w) {
             // A cycle share under-weights a kernel that ran at a lower clock than the
             // idle rest of the interval (MFMA under the power cap: ≈2.1 GHz against
             // ≈2.4 idle): the time share is s·r / (1 − s + s·r), r = f_idle / f_busy.
-            const double r = std::clamp(clk_idle_hz / clk_busy_hz, 0.8, 1.25);
+            // f_busy comes from the last fully busy intervals, whose kernels need not
+            // clock like this one (a 0.2 ms burst is not power-capped like a 1 ms one):
+            // r is kept within ±10 % (r4q: ±25 % over-read a 0.2 ms train by 2 points).
+            const double r = std::clamp(clk_idle_hz / clk_busy_hz, 0.9, 1.1);
             share = share * r / (1.0 - share + share * r);
           }
           P.dispatch_seconds += share * span_ns * 1e-9;

@@ -82,7 +82,7 @@ def estimate(ivs, learned, variant: str) -> float:
         else:
             s = min(1.0, busy / clk)
             if variant == "shipped" and dt >= 400e-6 and s > 0 and f_busy and f_idle:
-                r = min(1.25, max(0.8, f_idle / f_busy))
+                r = min(1.1, max(0.9, f_idle / f_busy))
                 s = s * r / (1.0 - s + s * r)
             tot += s * dt
     return 100.0 * tot / span if span else 0.0
