@@ -758,8 +758,11 @@ void Sampler::run_pmc(Worker& w) {
             read_spi[m][f] = first ? act : 0.95 * read_spi[m][f] + 0.05 * act;
             ++read_cyc_n[m][f];
             if (f) P.cpc_read_us = read_cyc[m][f] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
-            const double hz_now = clk / ((ps.mono_ns - prev_ps_ns) * 1e-9);
-            clk_idle_hz = clk_idle_hz > 0 ? 0.95 * clk_idle_hz + 0.05 * hz_now : hz_now;
+            // the idle clock between kernels, not a quiet GPU's (its clock drops: r4r)
+            if (!fresh_mode) {
+              const double hz_now = clk / ((ps.mono_ns - prev_ps_ns) * 1e-9);
+              clk_idle_hz = clk_idle_hz > 0 ? 0.95 * clk_idle_hz + 0.05 * hz_now : hz_now;
+            }
           }
           // This READ's learned cost, or the other kind's before it has its own.
           const int k = read_cyc_n[m][f] ? f : 1 - f;
