@@ -155,8 +155,9 @@ CATALOG: tuple[Family, ...] = (
       "the exporter's own READ packet's CP time, never below the GRBM_SPI_BUSY share; an interval the CP was busy "
       "for ≥ 97 % counts whole); rate() = the READ-immune 'a kernel is running' fraction behind "
       "--sm-util-source auto.", source="counters", tier="pmc"),
-    F("kgs_pmc_read_cp_seconds", "gauge", "Command-processor busy time of one counter READ packet, learned on "
-      "intervals without waves (what amdgpu_dispatch_busy_seconds_total subtracts per READ).", source="self",
+    F("kgs_pmc_read_cp_seconds", "gauge", "Command-processor busy time of one full counter READ packet, learned on "
+      "intervals without waves (what amdgpu_dispatch_busy_seconds_total subtracts per READ; lite READs are learned "
+      "apart and cost less).", source="self",
       tier="pmc"),
     F("amdgpu_mfma_busy_seconds_total", "counter",
       "∫ MFMA-busy share of all SIMD cycles dt (per drain: ΔSQ_VALU_MFMA_BUSY_CYCLES / (SIMDs·ΔGRBM_COUNT) · Δt); "

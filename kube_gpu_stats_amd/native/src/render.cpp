@@ -661,8 +661,8 @@ void Exporter::render(std::string& out) {
         if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
           w.line("amdgpu_dispatch_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.dispatch_seconds);
       w.head("kgs_pmc_read_cp_seconds", "gauge",
-             "Command-processor busy time one counter READ packet costs, as learned on intervals with no waves "
-             "(subtracted from CPC busy in amdgpu_dispatch_busy_seconds_total)");
+             "Command-processor busy time one full counter READ packet costs, as learned on intervals with no waves "
+             "(subtracted from CPC busy in amdgpu_dispatch_busy_seconds_total; lite READs are learned apart)");
       for (int d : ids)
         if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
           w.line("kgs_pmc_read_cp_seconds", dev_labels_[d], nullptr, snaps[d].I.cpc_read_us * 1e-6);
