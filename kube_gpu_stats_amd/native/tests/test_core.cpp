@@ -897,7 +897,63 @@ static void test_lite_ib() {
   put_index(flat, 0xe0000000u);
   put_copy(flat, 0xd040, 0x1000);
   CHECK(!compact_se_sections(flat.data(), static_cast<uint32_t>(flat.size()), out3).ok);
-  std::printf("lite IB ok (%zu -> %zu dwords, %u per-SE copies dropped)\n", ib.size(), out.size(), r.dropped_copies);
+  // Fuzz: random READ shapes (XCC count, broadcast counters, SEs, stray packets, fillers).
+  // Whenever compaction succeeds its output parses, writes the input's results less the
+  // dropped ones in order, never copies under an SE-select index write, and shrinks.
+  std::mt19937 rng(1234);
+  int ok_n = 0;
+  for (int it = 0; it < 500; ++it) {
+    std::vector<uint32_t> f;
+    uint64_t dst = 0x7f0000002000ull;
+    const int nx = 1 + static_cast<int>(rng() % 8), ng = static_cast<int>(rng() % 4), ns = static_cast<int>(rng() % 5);
+    for (int x = 0; x < nx; ++x) {
+      const bool pred = rng() % 4 != 0;
+      size_t at = 0, body = 0;
+      if (pred) {
+        at = f.size();
+        f.push_back(t3(kPm4PredExec, 2));
+        f.push_back(1u << 24);
+        body = f.size();
+      }
+      if (rng() % 2) { f.push_back(t3(kPm4Nop, 2)); f.push_back(0); }
+      for (int g = 0; g < ng; ++g) { put_index(f, 0xe0000000u); put_copy(f, 0xd040, dst); dst += 4; }
+      for (int se = 0; se < ns; ++se) {
+        put_index(f, 0x60000000u | (static_cast<uint32_t>(se) << 16));
+        const int nc = static_cast<int>(rng() % 3);
+        for (int c = 0; c < nc; ++c) { put_copy(f, 0xd1c0 + c, dst); dst += 4; }
+        if (rng() % 10 == 0) { f.push_back(t3(0x46, 2)); f.push_back(0x407); }
+        if (rng() % 10 == 0) f.push_back(0x80000000u);  // type-2 filler
+      }
+      if (pred) f[at + 1] |= static_cast<uint32_t>(f.size() - body);
+    }
+    std::vector<uint64_t> in;
+    CHECK(ib_copy_dsts(f.data(), static_cast<uint32_t>(f.size()), &in));
+    std::vector<uint32_t> o;
+    IbCompact c = compact_se_sections(f.data(), static_cast<uint32_t>(f.size()), o);
+    if (!c.ok) continue;
+    ++ok_n;
+    std::vector<uint64_t> got;
+    CHECK(ib_copy_dsts(o.data(), static_cast<uint32_t>(o.size()), &got));
+    CHECK(got.size() + c.dropped_dsts.size() == in.size());
+    CHECK(o.size() < f.size());
+    // copies made under an SE-select index write: only those of the sections kept whole remain
+    auto se_copies = [](const std::vector<uint32_t>& v) {
+      uint32_t n = 0;
+      bool sel = false;
+      for (uint32_t i = 0; i < v.size();) {
+        if (pm4_type(v[i]) == 2) { ++i; continue; }
+        bool se2 = false;
+        if (pm4_gfx_index(v.data() + i, &se2)) sel = se2;
+        if (sel && pm4_copy_to_mem(v.data() + i)) ++n;
+        i += pm4_len(v[i]);
+      }
+      return n;
+    };
+    CHECK(se_copies(o) + c.dropped_copies == se_copies(f));
+  }
+  CHECK(ok_n > 100);
+  std::printf("lite IB ok (%zu -> %zu dwords, %u per-SE copies dropped; fuzz %d/500 compacted)\n", ib.size(),
+              out.size(), r.dropped_copies, ok_n);
 }
 
 int main() {
