@@ -73,7 +73,7 @@ for s in $STEPS; do
               --out "$OUT/cp_busy_pipelined.json" --dump "$OUT/cp_dump.json" --dump-rates 8000,1000 ;;
     graphutil) run graph_util 300 python -u tools/graph_cost_probe.py --variants full_rate,util_set,lite,default \
                  --out "$OUT/graph_util.json" ;;
-    graphdef) run graph_def 300 python -u tools/graph_cost_probe.py --variants default,full_rate,lite \
+    graphdef) run graph_def 300 python -u tools/graph_cost_probe.py --variants default,nolite,lite \
                 --out "$OUT/graph_def.json" ;;
     graphcost) run graph_cost 400 python -u tools/graph_cost_probe.py --out "$OUT/graph_cost.json" ;;
     testsnw) run pytest_gpu 700 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \

@@ -15,7 +15,9 @@ probe measures only that component, for several exporter variants on the same bo
 * ``batch1``    — --pmc-cp-only-min 0 --pmc-batch 1 (every READ writes the L2 back);
 * ``hz1000`` / ``hz100`` — the full-rate reader at 1 kHz / 100 Hz;
 * ``util_set``  — full rate, --pmc-set util (24 register reads per READ instead of 56);
-* ``lite``      — full rate, --pmc-lite (7 of 8 READs without the 32 per-SE MFMA reads).
+* ``lite``      — full rate, --pmc-lite (7 of 8 READs without the 32 per-SE MFMA reads;
+  the default from r4k, so ``full_rate`` is the same since);
+* ``nolite``    — full rate, --no-pmc-lite (every READ full).
 
 Per variant one exporter process (--hz 8000, --control-http) and ``--rounds`` paired
 rounds of two blocks — exporter paused / sampling, order alternating (ABBA) — each
@@ -45,6 +47,7 @@ VARIANTS = {
     "hz100": ({}, ["--pmc-cp-only-min", "0", "--hz", "100"]),
     "util_set": ({}, ["--pmc-cp-only-min", "0", "--pmc-set", "util"]),
     "lite": ({}, ["--pmc-cp-only-min", "0", "--pmc-lite"]),
+    "nolite": ({}, ["--pmc-cp-only-min", "0", "--no-pmc-lite"]),
 }
 T975 = {5: 2.571, 7: 2.365, 11: 2.201, 15: 2.131, 23: 2.069, 31: 2.040, 47: 2.012}
 
