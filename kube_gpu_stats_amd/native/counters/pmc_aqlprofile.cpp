@@ -1001,13 +1001,15 @@ bool make_lite(Agent* a, int k, uint32_t cmd_sz) {
   if (!c.ok) {
     return why(c.why);
   }
-  if (a->plib[k] && a->plib_sz[k] < cmd_sz) {
+  // the compacted IB only (≈1.5 KB for the base set), not a whole command buffer
+  const uint32_t need = static_cast<uint32_t>((out.size() * 4 + 4095) & ~size_t{4095});
+  if (a->plib[k] && a->plib_sz[k] < need) {
     hsa_amd_memory_pool_free(a->plib[k]);
     a->plib[k] = nullptr;
   }
   if (!a->plib[k]) {
-    a->plib[k] = host_alloc(a, cmd_sz);
-    a->plib_sz[k] = a->plib[k] ? cmd_sz : 0;
+    a->plib[k] = host_alloc(a, need);
+    a->plib_sz[k] = a->plib[k] ? need : 0;
   }
   if (!a->plib[k] || out.size() * 4 > cmd_sz) {
     return why("no memory for the compacted IB");
