@@ -49,17 +49,21 @@ def kfd_gpu_id() -> int:
     raise RuntimeError("no KFD GPU node")
 
 
-def child(hz: float, secs: float, pipelined: bool) -> int:
+def child(hz: float, secs: float, pipelined: bool, batch: int = 1, lite: int = 0, exporter_set: int = 0) -> int:
     from kube_gpu_stats_amd.native import pmc_lib_path
 
     L = ctypes.CDLL(pmc_lib_path("aqlprofile"))
     err = ctypes.create_string_buffer(512)
+    L.kgs_pmc_configure(b"batch", batch)  # as the exporter configures the reader (--pmc-batch, --pmc-lite)
+    L.kgs_pmc_configure(b"lite", lite)
     if L.kgs_pmc_init(err, 512) != 0:
         print(json.dumps({"error": "init: " + err.value.decode()}), flush=True)
         return 1
-    n = len(NAMES)
-    arr = (ctypes.c_char_p * n)(*[s.encode() for s in NAMES])
-    red = (ctypes.c_int * n)(*[1] * n)  # max over the XCC instances: "some XCC busy"
+    # the exporter's base set in the dump's column order (the 4th column is then MFMA busy, not CPF)
+    names = ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:25", "SQ_VALU_MFMA_BUSY_CYCLES"] if exporter_set else NAMES
+    n = len(names)
+    arr = (ctypes.c_char_p * n)(*[s.encode() for s in names])
+    red = (ctypes.c_int * n)(*([1, 1, 1, 0] if exporter_set else [1] * n))  # max over XCCs; MFMA summed
     L.kgs_pmc_open.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p,
                                ctypes.c_int]
     h = L.kgs_pmc_open(kfd_gpu_id(), arr, red, n, err, 512)
@@ -88,8 +92,9 @@ def child(hz: float, secs: float, pipelined: bool) -> int:
             continue
         rc = L.kgs_pmc_sample_ts(h, out, n, ctypes.byref(rns), ctypes.byref(sns))
         if rc == 0:
-            # the time the CP read the values (pipelined: the previous call's READ), on the wall clock
-            buf.append((time.time() - (time.monotonic_ns() - sns.value) * 1e-9, list(out)))
+            # the time the CP read the values (pipelined: the previous call's READ), on the wall clock;
+            # then whether that READ read the per-SE counters (lite READs: 0)
+            buf.append((time.time() - (time.monotonic_ns() - sns.value) * 1e-9, list(out) + [L.kgs_pmc_se_fresh(h)]))
         nxt += period
         if nxt < now - 10 * period:
             nxt = now
@@ -107,6 +112,10 @@ def main(argv=None) -> int:
     ap.add_argument("--rates", default="100,1000,8000")
     ap.add_argument("--secs", type=float, default=2.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--batch", type=int, default=1, help="reader batch (the exporter's --pmc-batch)")
+    ap.add_argument("--lite", type=int, default=0, choices=[0, 1], help="lite READs (the exporter's --pmc-lite)")
+    ap.add_argument("--exporter-set", type=int, default=0, choices=[0, 1],
+                    help="read the exporter's base set (4th column MFMA busy instead of CPF busy)")
     ap.add_argument("--pipelined", type=int, default=0, choices=[0, 1],
                     help="READ pipelined, as the exporter does above its idle rate")
     ap.add_argument("--dump", default="", help="write every raw sample of the --dump-rates runs here (JSON)")
@@ -115,7 +124,7 @@ def main(argv=None) -> int:
     ap.add_argument("--child-secs", type=float, default=0.0, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     if a.child:
-        return child(a.child, a.child_secs, bool(a.pipelined))
+        return child(a.child, a.child_secs, bool(a.pipelined), a.batch, a.lite, a.exporter_set)
 
     import torch
 
@@ -151,7 +160,8 @@ def main(argv=None) -> int:
     total = len(names) * (a.secs + 0.6) + 2.0
     for hz in [float(x) for x in a.rates.split(",")]:
         p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", str(hz), "--child-secs",
-                              str(total), "--pipelined", str(a.pipelined)], stdout=subprocess.PIPE, text=True,
+                              str(total), "--pipelined", str(a.pipelined), "--batch", str(a.batch), "--lite", str(a.lite),
+                              "--exporter-set", str(a.exporter_set)], stdout=subprocess.PIPE, text=True,
                              cwd=REPO)
         first = json.loads(p.stdout.readline())
         if "error" in first:

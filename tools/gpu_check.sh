@@ -73,6 +73,9 @@ for s in $STEPS; do
               --out "$OUT/cp_busy_pipelined.json" --dump "$OUT/cp_dump.json" --dump-rates 8000,1000 ;;
     graphutil) run graph_util 300 python -u tools/graph_cost_probe.py --variants full_rate,util_set,lite,default \
                  --out "$OUT/graph_util.json" ;;
+    cpdumplite) run cp_dump_lite 300 python -u tools/cp_busy_probe.py --rates 8000,1000 --pipelined 1 --batch 8 \
+                  --lite 1 --exporter-set 1 --secs 2 --out "$OUT/cp_busy_lite.json" --dump "$OUT/cp_dump_lite.json" \
+                  --dump-rates 8000,1000 ;;
     graphdef) run graph_def 300 python -u tools/graph_cost_probe.py --variants default,nolite,lite \
                 --out "$OUT/graph_def.json" ;;
     graphcost) run graph_cost 400 python -u tools/graph_cost_probe.py --out "$OUT/graph_cost.json" ;;
