@@ -119,7 +119,11 @@ def parse_args(argv=None):
     ap.add_argument("--xgmi-check-mib", type=int, default=2048,
                     help="phase X (N > 1): bytes of each GPU 0 → GPU k peer copy that checks the link map and unit")
     ap.add_argument("--xgmi-check-settle", type=float, default=0.5,
-                    help="phase X: seconds between a peer copy and the scrape that reads its link counters")
+                    help="phase X: seconds between a round of peer copies and the scrape that reads its link counters")
+    ap.add_argument("--xgmi-check-budget-s", type=float, default=120.0,
+                    help="phase X: start no further round of peer copies after this many seconds")
+    ap.add_argument("--mock-xgmi-swap", type=int, default=-1,
+                    help="mock: GPU whose link table reports two ports' peers swapped (phase X must flag it)")
     ap.add_argument("--xgmi-child", type=int, default=0, help=argparse.SUPPRESS)  # phase X child: exporter port
     ap.add_argument("--xgmi-bdfs", default="", help=argparse.SUPPRESS)
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
@@ -140,8 +144,9 @@ def parse_args(argv=None):
     ap.add_argument("--util-s", type=float, default=1.5,
                     help="phase U: seconds of each load (idle, two MFMA burst trains, saturating MFMA) while the "
                     "exported container_gpu_sm_util / busy counter is checked against the host-known duty (0 = off)")
-    ap.add_argument("--util-hz", default="1000",
-                    help="phase U: tick rates besides the primary --hz ('' = primary only)")
+    ap.add_argument("--util-hz", default="1000,10",
+                    help="phase U: tick rates besides the primary --hz ('' = primary only); 10 Hz is the "
+                    "DaemonSet's (deploy/daemonset.yaml), each load there runs at least 30 drain periods")
     ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
     ap.add_argument("--mock-step-ms", type=float, default=20.0, help="mock: duration of one load unit")
     ap.add_argument("--mock-latency", type=int, default=1, choices=[0, 1],
@@ -629,7 +634,8 @@ class ExporterProc(ExporterCtl):
                "--control-stdin", "--control-http", "--node-name", "bench-node", "--bdfs", ",".join(bdfs),
                "--compat-unallocated"]
         if a.mock:
-            cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock"]
+            cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock",
+                    "--mock-xgmi-swap", str(a.mock_xgmi_swap)]
             if a.mock_latency:
                 cmd += ["--mock-latency"]
         else:
@@ -1117,6 +1123,19 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
             if len(ranks) > 1:
                 by_comp[n]["per_rank_overhead_pct"] = [round(x[0], 4) for x in per_rank]
         tier["overhead_by_component"] = by_comp
+        if RELEASED in conds:
+            # The same pairing against "released" (counter session STOPped, READ queue
+            # destroyed, threads stopped): paused keeps a programmed session and its
+            # queue, which shifts a dispatch-bound stream's power state (BENCH_r04:
+            # µs-kernel graph −1.23 % at 100 Hz vs paused), so this is the neutral base
+            # for the cost of sampling.
+            vs_rel: dict = {}
+            for n in names:
+                d = [100.0 * (rd[h]["comp"][n] / rd[RELEASED]["comp"][n] - 1.0) for rd in ranks[0]
+                     if rd[RELEASED]["comp"].get(n, 0) > 0 and n in rd[h]["comp"]]
+                m_r, c_r, _ = mean_ci95(d)
+                vs_rel[n] = {"overhead_pct": m_r, "overhead_ci95_pct": c_r}
+            tier["overhead_by_component_vs_released"] = vs_rel
         # per rank: that rank's own work time, paired by round
         per_rank = []
         for k, rk in enumerate(ranks):
@@ -1299,6 +1318,12 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         D.cpu_barrier(ctx)
         time.sleep(0.3)
         per_load: dict = {}
+        # At a low counter rate the busy integral is known at the drains and billed at
+        # the PMFW samples (both at the tick rate): a window of ≥ 30 periods and a tail
+        # of two, so the last burst's drain and table land inside it (the saturating
+        # load too: its duty then counts the tail as idle).
+        secs = max(a.util_s, 30.0 / hz)
+        tail = 2.0 / hz if hz < 100 else 0.0
         for name, spec in plan:
             load.sync()
             D.cpu_barrier(ctx)  # no RCCL kernel inside the window
@@ -1306,14 +1331,14 @@ def util_accuracy(ctx, load, exp, a) -> dict:
             t0 = time.perf_counter()
             gpu_s = host_s = 0.0
             if spec is None:
-                time.sleep(a.util_s)
+                time.sleep(secs)
             elif spec == "sat":
-                gpu_s = load.saturate(a.util_s)
+                gpu_s = load.saturate(secs)
                 host_s = time.perf_counter() - t0
             else:
                 ms, period = spec
                 nxt = time.monotonic()
-                end = nxt + a.util_s
+                end = nxt + secs
                 while time.monotonic() < end:
                     h0 = time.perf_counter()
                     gpu_s += load.burst_timed(ms)
@@ -1322,6 +1347,8 @@ def util_accuracy(ctx, load, exp, a) -> dict:
                     d = nxt - time.monotonic()
                     if d > 0:
                         time.sleep(d)
+            if spec != "sat" or tail > 0:
+                time.sleep(tail)
             own = (gpu_s, host_s, time.perf_counter() - t0)
             D.cpu_barrier(ctx)
             m1, w1 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
@@ -1356,14 +1383,12 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         out["per_rate"][f"{hz:g}"] = per_load
     if exp is not None:
         exp.set_rate(a.hz)
-    # worst |error| per load over GPUs and rates (bursts and idle: exported − GPU duty;
-    # saturating: how far below 100 the export reads)
+    # worst |exported − GPU duty| per load over GPUs and rates
     worst: dict = {}
     for per_load in out["per_rate"].values():
         for name, per_gpu in per_load.items():
             for r in per_gpu.values():
-                e = abs(r["error_pts"]) if name != "mfma_saturating" else 100.0 - r["busy_counter_pct"]
-                worst[name] = round(max(worst.get(name, 0.0), e), 2)
+                worst[name] = round(max(worst.get(name, 0.0), abs(r["error_pts"])), 2)
     out["worst_error_pts"] = worst
     return out
 
@@ -1457,12 +1482,28 @@ def capacity(ctx, load, exp, a) -> dict:
     return out
 
 
+def _pair_rounds(n: int) -> list[list[tuple[int, int]]]:
+    """Every ordered pair (i, j), i != j, of n GPUs in rounds of disjoint pairs: the
+    circle method's n-1 rounds of n/2 pairs (n odd: a bye), each round once per
+    direction — 2(n-1) rounds, every GPU in at most one copy per round, so the only
+    link of each GPU that moves in a round is the one to its partner."""
+    m = n + (n % 2)
+    ring = list(range(m))
+    rounds = []
+    for _ in range(m - 1):
+        pairs = [(ring[k], ring[m - 1 - k]) for k in range(m // 2)]
+        rounds.append([(i, j) for i, j in pairs if i < n and j < n])
+        ring = [ring[0]] + [ring[-1]] + ring[1:-1]
+    return rounds + [[(j, i) for i, j in r] for r in rounds]
+
+
 def _xgmi_rank0(a, exp, bdfs: list) -> dict:
     """Phase X on local rank 0 (see xgmi_link_check)."""
     nbytes = int(a.xgmi_check_mib) << 20
     gpu_of = {d["bdf"]: int(d["gpu"]) for d in exp.json("/devices")}
     topo = exp.json("/topology")
     peer_of = {(int(x["gpu"]), int(x["link"])): x.get("peer_bdf", "") for x in topo.get("links", [])}
+    budget_s = float(getattr(a, "xgmi_check_budget_s", 120.0) or 120.0)
 
     def link_bytes(m: dict) -> dict:
         tot: dict = {}
@@ -1484,49 +1525,77 @@ def _xgmi_rank0(a, exp, bdfs: list) -> dict:
                 "bytes_counted": round(d[l_max], 1), "background_bytes": round(bg, 1),
                 "unit_ratio": round((d[l_max] - bg) / nbytes, 4)}
 
-    src_dev = 0
-    per_peer = []
-    for k in range(1, len(bdfs)):
-        g0, gk = gpu_of.get(bdfs[0]), gpu_of.get(bdfs[k])
-        if g0 is None or gk is None:
-            per_peer.append({"peer_bdf": bdfs[k], "ok": False, "reason": "GPU not sampled by the exporter"})
+    def copy_round(pairs: list[tuple[int, int]]) -> dict:
+        """The round's copies at once, each on its source GPU (in-tree copy_f32 peer
+        kernel: the source's waves store into the peer's HBM over their direct link)."""
+        if a.mock:
+            for i, j in pairs:
+                exp.json(f"/control/mock/xgmi?src={gpu_of[bdfs[i]]}&dst={gpu_of[bdfs[j]]}&bytes={nbytes}")
+            return {}
+        import torch
+
+        from kube_gpu_stats_amd.ops import load as L
+
+        bufs = []
+        for i, j in pairs:
+            src = torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", i)).fill_(1.0)
+            dst = torch.zeros(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", j))
+            L.enable_peer(i, j)
+            bufs.append((i, j, src, dst))
+        for d in {x for p in pairs for x in p}:
+            torch.cuda.synchronize(d)
+        for i, j, src, dst in bufs:
+            with torch.cuda.device(i):
+                L.copy_f32(src, dst, stream=torch.cuda.current_stream(i))
+        for i, _, _, _ in bufs:
+            torch.cuda.synchronize(i)
+        ok = {(i, j): bool((dst == 1.0).all().item()) for i, j, _, dst in bufs}  # every element arrived
+        del bufs
+        return ok
+
+    t_start = time.monotonic()
+    per_copy, skipped = [], 0
+    for pairs in _pair_rounds(len(bdfs)):
+        pairs = [(i, j) for i, j in pairs if bdfs[i] in gpu_of and bdfs[j] in gpu_of]
+        if not pairs:
+            continue
+        if time.monotonic() - t_start > budget_s:  # --xgmi-check-budget-s: report what was covered
+            skipped += len(pairs)
             continue
         m0 = parse_text(exp.sc.get())
-        copy_ok = None
-        if a.mock:
-            exp.json(f"/control/mock/xgmi?src={g0}&dst={gk}&bytes={nbytes}")
-        else:
-            # The in-tree peer-copy kernel (ops/hip/load_kernels.hip copy_f32_kernel):
-            # GPU 0's waves store straight into GPU k's HBM over their xGMI link.
-            import torch
-
-            from kube_gpu_stats_amd.ops import load as L
-
-            src = torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", src_dev)).fill_(1.0)
-            dst = torch.zeros(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", k))
-            torch.cuda.synchronize(k)
-            L.enable_peer(src_dev, k)
-            with torch.cuda.device(src_dev):
-                L.copy_f32(src, dst, stream=torch.cuda.current_stream(src_dev))
-            torch.cuda.synchronize(src_dev)
-            copy_ok = bool((dst == 1.0).all().item())  # the peer kernel copied every element
-            del src, dst
+        copied = copy_round(pairs)
         time.sleep(a.xgmi_check_settle)  # the PMFW table refreshes every ≈20 ms; the exporter reads it at 100 Hz
-        m1 = parse_text(exp.sc.get())
-        b0, b1 = link_bytes(m0), link_bytes(m1)
-        row = {"src_gpu": g0, "peer_gpu": gk, "peer_bdf": bdfs[k], "bytes": nbytes,
-               "src": moved(b0, b1, g0, bdfs[k]), "dst": moved(b0, b1, gk, bdfs[0]),
-               "copy": "in-tree copy_f32 peer kernel" if not a.mock else "mock", "copy_ok": copy_ok}
-        row["ok"] = bool(row["src"].get("ok") and row["dst"].get("ok"))
-        per_peer.append(row)
-    ratios = sorted(r[side]["unit_ratio"] for r in per_peer for side in ("src", "dst")
+        b0, b1 = link_bytes(m0), parse_text(exp.sc.get())
+        b1 = link_bytes(b1)
+        for i, j in pairs:
+            gi, gj = gpu_of[bdfs[i]], gpu_of[bdfs[j]]
+            row = {"src_gpu": gi, "peer_gpu": gj, "peer_bdf": bdfs[j], "bytes": nbytes,
+                   "src": moved(b0, b1, gi, bdfs[j]), "dst": moved(b0, b1, gj, bdfs[i]),
+                   "copy_ok": copied.get((i, j))}
+            row["ok"] = bool(row["src"].get("ok") and row["dst"].get("ok") and row["copy_ok"] is not False)
+            per_copy.append(row)
+    missing = [b for b in bdfs if b not in gpu_of]
+    ratios = sorted(r[side]["unit_ratio"] for r in per_copy for side in ("src", "dst")
                     if isinstance(r.get(side), dict) and "unit_ratio" in r[side])
     ratio = ratios[len(ratios) // 2] if ratios else None
-    out = {"bytes_per_copy": nbytes, "per_peer": per_peer,
-           "xgmi_link_map_ok": bool(per_peer) and all(r["ok"] for r in per_peer),
+    n_ok = sum(1 for r in per_copy if r["ok"])
+    total = len(bdfs) * (len(bdfs) - 1)
+    bad = [f"gpu{r['src_gpu']}->gpu{r['peer_gpu']}: " + "; ".join(
+        f"{side} gpu{r[side + '_gpu' if side == 'src' else 'peer_gpu']} link {r[side].get('link')} faces "
+        f"{r[side].get('link_peer_bdf') or '?'}" for side in ("src", "dst") if not r[side].get("ok"))
+        for r in per_copy if not r["ok"]]
+    out = {"bytes_per_copy": nbytes, "copies": "every ordered GPU pair, disjoint pairs in parallel rounds",
+           "per_copy": per_copy, "xgmi_links_ok": [n_ok, total], "bad_links": bad[:16],
+           "xgmi_link_map_ok": n_ok == total and total > 0,
            "xgmi_unit_ratio": ratio,
-           "xgmi_unit_ok": ratio is not None and 0.8 <= ratio <= 1.25}
-    if ratio is not None and not out["xgmi_unit_ok"]:
+           "xgmi_unit_ratio_min_max": [ratios[0], ratios[-1]] if ratios else None,
+           "xgmi_unit_ok": bool(ratios) and 0.8 <= ratios[0] and ratios[-1] <= 1.25,
+           "seconds": round(time.monotonic() - t_start, 2)}
+    if skipped:
+        out["skipped_over_budget"] = skipped
+    if missing:
+        out["not_sampled"] = missing
+    if ratio is not None and not 0.8 <= ratio <= 1.25:
         out["warning"] = (f"xGMI accumulator unit off by {ratio:.3g}x: set --xgmi-bytes-per-unit to "
                           f"{1024.0 * ratio:.4g}")
     return out
@@ -1534,14 +1603,17 @@ def _xgmi_rank0(a, exp, bdfs: list) -> dict:
 
 def xgmi_link_check(ctx, load, exp, a) -> dict:
     """Phase X (untimed, N > 1) — does each xGMI byte land on the link whose peer is
-    the real peer, and in which unit?  Rank 0 sees every GPU of the
-    node: for each other rank's GPU k in turn it copies ``--xgmi-check-mib`` from GPU 0
-    into GPU k (a peer copy over the one direct link), with exporter scrapes before and
-    after.  On the source and on the destination, the link whose byte counter moved
+    the real peer, and in which unit?  Rank 0 sees every GPU of
+    the node: every GPU copies ``--xgmi-check-mib`` to every peer (all N(N-1) ordered
+    pairs — 56 on 8 GPUs, each GPU's link to each peer checked as a writer and as a
+    reader), in rounds of disjoint pairs run at once, with exporter scrapes around each
+    round.  On the source and on the destination, the link whose byte counter moved
     most (read + write, minus the median of the other links as background) must be
     the one whose amdsmi peer_bdf is the other GPU; its bytes ÷ the copied bytes is the
-    accumulator-unit ratio (1.0 if --xgmi-bytes-per-unit is right).  The mock backend
-    books the copy on the right link itself (/control/mock/xgmi)."""
+    accumulator-unit ratio (1.0 if --xgmi-bytes-per-unit is right), reported per link
+    and as min / median / max.  ``xgmi_links_ok`` = [copies whose both ends are right,
+    copies]; ``bad_links`` names the wrong ones.  The mock backend books each copy on
+    the true link itself (/control/mock/xgmi); --mock-xgmi-swap G gives it a wrong map."""
     if ctx.world < 2:
         return {"skipped": "N=1: no peer GPU to copy to"}
     if a.xgmi_check_mib <= 0:
@@ -1555,11 +1627,12 @@ def xgmi_link_check(ctx, load, exp, a) -> dict:
         # rank's later timed phase (C) shares its GPU with a foreign context of rank 0
         # (VERDICT r3 weak #9).
         cmd = [sys.executable, os.path.abspath(__file__), "--xgmi-child", str(exp.port), "--xgmi-bdfs", ",".join(bdfs),
-               "--xgmi-check-mib", str(a.xgmi_check_mib), "--xgmi-check-settle", str(a.xgmi_check_settle)]
+               "--xgmi-check-mib", str(a.xgmi_check_mib), "--xgmi-check-settle", str(a.xgmi_check_settle),
+               "--xgmi-check-budget-s", str(getattr(a, "xgmi_check_budget_s", 120.0))]
         if a.mock:
             cmd.append("--mock")
         try:
-            r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+            r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=getattr(a, "xgmi_check_budget_s", 120.0) + 180)
             lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
             out = json.loads(lines[-1]) if r.returncode == 0 and lines else {
                 "error": f"phase X child rc={r.returncode}: {r.stderr[-400:]}", "xgmi_link_map_ok": False,
@@ -1760,7 +1833,9 @@ def run(a, ctx) -> dict | None:
         "xgmi_allreduce_ratio_per_gpu": allreduce_ratio(xgmi_rates(before, after, win), allreduce_GBps(load, a, n, win)),
         "xgmi_link_check": xlink,
         "xgmi_link_map_ok": xlink.get("xgmi_link_map_ok"),
+        "xgmi_links_ok": xlink.get("xgmi_links_ok"),
         "xgmi_unit_ratio": xlink.get("xgmi_unit_ratio"),
+        "xgmi_unit_ratio_min_max": xlink.get("xgmi_unit_ratio_min_max"),
         "phases_wall": PHASES,
         "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in integrals)
         / max(1, sum(i.get("pmc_samples", 0) for i in integrals)),
@@ -1772,7 +1847,7 @@ def run(a, ctx) -> dict | None:
 
 
 # ----------------------------------------------------------------------------- result line
-SUMMARY_MAX = 1500  # bytes of the summary object: the driver keeps the last ≈4 KB of stdout
+SUMMARY_MAX = 1800  # bytes of the summary object: the driver keeps the last ≈2.3 KB of stdout (BENCH_r04)
 CONTRACT_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
                  "vs_baseline", "dtype", "data")
 
@@ -1802,6 +1877,9 @@ def summarize(res: dict) -> dict:
     out["overhead_position_adjusted"] = {h: _pm(v) for h, v in pa.items() if isinstance(v, dict) and "overhead_pct" in v}
     out["overhead_by_component"] = {h: {c: _pm(v) for c, v in (t.get("overhead_by_component") or {}).items()}
                                     for h, t in tiers.items()}
+    out["overhead_by_component_vs_released"] = {h: {c: _pm(v) for c, v in
+                                                    (t.get("overhead_by_component_vs_released") or {}).items()}
+                                                for h, t in tiers.items() if t.get("overhead_by_component_vs_released")}
     out["overhead_by_rank"] = [_r(x.get("overhead_pct")) for x in (tiers.get(prim, {}).get("overhead_by_rank") or [])]
     rel = inter.get("released")
     if rel:
@@ -1822,12 +1900,15 @@ def summarize(res: dict) -> dict:
 
         short = {"burst_1ms_every_5ms": "1ms/5ms", "burst_0.2ms_every_1ms": "0.2ms/1ms", "mfma_saturating": "sat"}
         out["util_accuracy"] = {
-            "cols": "exported busy, duty, PMFW busy %",
+            "cols": "exported busy %, kernel duty %",
             **{hz: {short.get(ld, ld): [mean([r.get("busy_counter_pct") for r in pg.values()]),
-                                        mean([r.get("duty_gpu_pct") for r in pg.values()]),
-                                        mean([r.get("pmfw_gfx_busy_pct") for r in pg.values()])]
+                                        mean([r.get("duty_gpu_pct") for r in pg.values()])]
                     for ld, pg in per.items()} for hz, per in ua["per_rate"].items()},
             "worst_error_pts": {short.get(k, k): v for k, v in (ua.get("worst_error_pts") or {}).items()}}
+        # what the auto source removes: the PMFW busy of the fastest rate's 0.2 ms train
+        fast = max(ua["per_rate"], key=float)
+        pg = ua["per_rate"][fast].get("burst_0.2ms_every_1ms") or {}
+        out["util_accuracy"]["pmfw_busy_0.2ms_" + fast] = mean([r.get("pmfw_gfx_busy_pct") for r in pg.values()])
     q = res.get("quiet_gpu") or {}
     if q:
         out["quiet_gpu"] = {m: [_r(max(x.get("reads_per_s", 0) for x in v.get("per_gpu", {}).values()), 1),
@@ -1839,8 +1920,15 @@ def summarize(res: dict) -> dict:
     out["capacity_max_hz_98pct"] = (res.get("capacity") or {}).get("max_rate_hz_98pct")
     out["exporter_cpu_cores"] = res.get("exporter_cpu_cores")
     out["xgmi_link_map_ok"] = res.get("xgmi_link_map_ok")
+    out["xgmi_links_ok"] = res.get("xgmi_links_ok")
     out["xgmi_unit_ratio"] = res.get("xgmi_unit_ratio")
-    if len(json.dumps(out)) > SUMMARY_MAX and "util_accuracy" in out:  # keep the line inside the driver's window
+    out["xgmi_unit_ratio_min_max"] = res.get("xgmi_unit_ratio_min_max")
+    if (res.get("xgmi_link_check") or {}).get("bad_links"):
+        out["xgmi_bad_links"] = res["xgmi_link_check"]["bad_links"][:4]
+    # keep the summary inside the driver's window: shed the side estimates first
+    if len(json.dumps(out)) > SUMMARY_MAX:
+        out.pop("overhead_position_adjusted", None)
+    if len(json.dumps(out)) > SUMMARY_MAX and "util_accuracy" in out:
         out["util_accuracy"] = {"worst_error_pts": out["util_accuracy"].get("worst_error_pts")}
     return out
 

@@ -28,6 +28,7 @@ import os
 import threading
 import time
 
+from ..models.schema import BY_NAME
 from ..utils import log
 from .cgroup import pid_cgroup
 from .poddir import PodDirectory
@@ -157,26 +158,17 @@ class Attributor:
     def self_metrics(self) -> str:
         age = time.monotonic() - self.last_kubelet_ok if self.last_kubelet_ok else -1.0
         connected = 1 if self.client is not None else 0
-        return "\n".join([
-            "# HELP kgs_attribution_updates_total Attribution passes completed",
-            "# TYPE kgs_attribution_updates_total counter",
-            f"kgs_attribution_updates_total {self.updates}",
-            "# HELP kgs_attribution_errors_total Failed attribution passes / kubelet calls",
-            "# TYPE kgs_attribution_errors_total counter",
-            f"kgs_attribution_errors_total {self.errors}",
-            "# HELP kgs_attribution_kubelet_reconnects_total Pod-resources client re-creations",
-            "# TYPE kgs_attribution_kubelet_reconnects_total counter",
-            f"kgs_attribution_kubelet_reconnects_total {self.reconnects}",
-            "# HELP kgs_attribution_kubelet_connected 1 if a pod-resources client is open",
-            "# TYPE kgs_attribution_kubelet_connected gauge",
-            f"kgs_attribution_kubelet_connected {connected}",
-            "# HELP kgs_attribution_kubelet_age_seconds Seconds since the last good kubelet List (-1: never)",
-            "# TYPE kgs_attribution_kubelet_age_seconds gauge",
-            f"kgs_attribution_kubelet_age_seconds {age:.3f}",
-            "# HELP kgs_attribution_allocated_gpus GPUs with at least one owning container",
-            "# TYPE kgs_attribution_allocated_gpus gauge",
-            f"kgs_attribution_allocated_gpus {sum(1 for v in self.owners.values() if v)}",
-        ]) + "\n"
+        values = {"kgs_attribution_updates_total": self.updates,
+                  "kgs_attribution_errors_total": self.errors,
+                  "kgs_attribution_kubelet_reconnects_total": self.reconnects,
+                  "kgs_attribution_kubelet_connected": connected,
+                  "kgs_attribution_kubelet_age_seconds": f"{age:.3f}",
+                  "kgs_attribution_allocated_gpus": sum(1 for v in self.owners.values() if v)}
+        lines = []
+        for name, v in values.items():  # HELP / TYPE from the metric catalogue, like the native families
+            fam = BY_NAME[name]
+            lines += [f"# HELP {name} {fam.help}", f"# TYPE {name} {fam.type}", f"{name} {v}"]
+        return "\n".join(lines) + "\n"
 
     def publish(self) -> None:
         setter = getattr(self.ex, "set_extra_metrics", None)

@@ -48,6 +48,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
     add_flag(ap, "mock-latency", False, "mock provider: model AMD SMI latency as measured on MI355X (process list "
                                         "0.5 ms, link table 1 ms, RAS 0.75 ms, under one global lock; PMFW table "
                                         "read 0.125 ms, unlocked)")
+    add_flag(ap, "mock-xgmi-swap", -1, "mock provider: this GPU's link table reports its first two xGMI ports' "
+                                       "peers swapped (a wrong link map for the bench's phase X self-check)")
     add_flag(ap, "mock-partition", "SPX", "mock provider: compute partition mode (SPX | DPX | QPX | CPX)")
     add_flag(ap, "hz", 10.0, "sampler tick rate per GPU (1/10/100 Hz tiers; hardware counters every tick)")
     add_flag(ap, "pmfw-hz", 100.0, "cap on PMFW metrics-table reads/s (firmware refreshes it every ~20 ms)")
@@ -175,6 +177,7 @@ def config_from_args(a) -> dict:
     cfg = {
         "backend": a.backend,
         "mock": {"n_gpus": a.mock_gpus, "fail_rate": a.mock_fail_rate, "compute_partition": a.mock_partition,
+                 "xgmi_swap_dev": a.mock_xgmi_swap,
                  **(MOCK_LATENCY if a.mock_latency else {})},
         "hz": a.hz,
         "pmfw_hz": a.pmfw_hz,

@@ -6,12 +6,21 @@ so the reference's PromQL (gpu_util_stats.py:159) runs unchanged; the rest are t
 MI355X-native families.  ``tests/test_schema.py`` checks the renderer against this
 table, and ``docs/METRICS.md`` is generated from it (``python -m
 kube_gpu_stats_amd.models.schema``).
+
+It is also the only source of the HELP and TYPE lines: the native renderer looks them
+up in ``native/include/kgs/metric_help.h``, generated from this table (``python -m
+kube_gpu_stats_amd.models.schema --cpp-header``; the build regenerates it and
+``tests/test_schema_cli.py`` checks the committed copy and every rendered HELP line).
+A family whose meaning depends on ``--sm-util-source`` carries the non-default
+modes' text in ``variants``.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
 
 DEVICE_LABELS = ("gpu", "uuid")  # everything else about a device: amdgpu_device_info
+# the reference contract's labels (gpu_util_stats.py:45,71,159) and the pod's identity
+CONTRACT = ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid")
 
 
 @dataclass(frozen=True)
@@ -23,6 +32,11 @@ class Family:
     source: str = "pmfw"
     tier: str = "fast"
     extra: tuple[str, ...] = field(default=())
+    # (mode, help) for the non-default --sm-util-source modes ("pmfw", "counters")
+    variants: tuple[tuple[str, str], ...] = field(default=())
+
+    def help_for(self, mode: str = "") -> str:
+        return dict(self.variants).get(mode, self.help)
 
 
 F = Family
@@ -30,30 +44,45 @@ CATALOG: tuple[Family, ...] = (
     # ---- reference contract ------------------------------------------------------------
     F("container_gpu_sm_util", "gauge",
       "Busy % of the GPU allocated to the pod (mean over the exporter window), not counting the exporter's own "
-      "counter READs: with the default --sm-util-source auto, hardware-counter GPU-active (GRBM_SPI_BUSY: waves in a "
-      "shader engine) while the counter tier runs, the PMFW GFX busy otherwise (kgs_util_source_seconds_total says "
-      "which).  Reference contract: consumed by "
+      "counter READs.  Default --sm-util-source auto: while the counter tier covers the PMFW interval, the "
+      "dispatch-in-flight share from the hardware counters (CPC_CPC_STAT_BUSY less the CP time of the exporter's "
+      "own READ packets, learned on intervals without waves; never below the GRBM_SPI_BUSY share), else the PMFW "
+      "GFX busy (kgs_util_source_seconds_total says which).  Reference contract: consumed by "
       "`avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)`.",
-      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
-      "pmfw+kubelet", "fast"),
+      CONTRACT, "pmfw+kubelet", "fast",
+      variants=(("counters", "GPU-active % (GRBM_SPI_BUSY: a shader engine has waves) of the GPU allocated to the pod, "
+                             "mean over the exporter window (--sm-util-source counters).  Reference contract: consumed by "
+                             "`avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)`."),
+                ("pmfw", "GFX-engine busy % of the GPU allocated to the pod from the PMFW accumulators, mean over the "
+                         "exporter window (--sm-util-source pmfw: a dispatch in flight, each counter READ packet of the "
+                         "exporter included).  Reference contract: consumed by "
+                         "`avg(container_gpu_sm_util) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)`."))),
     F("container_gpu_mfma_util", "gauge",
       "Matrix-core (MFMA) busy % of active cycles of the GPU allocated to the pod (window), same labels as "
       "container_gpu_sm_util.  GFX busy counts a GPU busy while any dispatch is in flight; this says how much of "
       "that was matrix work.  `kgs gpu-util-stats --util-metric container_gpu_mfma_util` reports it per pod.",
-      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      CONTRACT,
       "counters+kubelet", "pmc"),
     F("container_gpu_busy_seconds_total", "counter",
-      "Busy seconds of the GPU allocated to the pod, counted from the allocation (the integral behind "
-      "container_gpu_sm_util: READ-immune under --sm-util-source auto).  "
+      "Busy seconds of the GPU allocated to the pod, counted from the allocation: the integral behind "
+      "container_gpu_sm_util.  Default --sm-util-source auto: the counter tier's dispatch-in-flight integral "
+      "(CPC_CPC_STAT_BUSY less the learned CP time of the exporter's own READs, never below GRBM_SPI_BUSY) while "
+      "that tier covers the PMFW interval, busy beyond one interval carried to the next so no rate loses time; the "
+      "PMFW GFX busy otherwise.  "
       "`100 * avg(rate(container_gpu_busy_seconds_total[1h])) by (kubernetes_io_hostname, nvidia_gpu_type, pod_name)` "
       "is the exact hourly per-pod utilisation whatever the scrape interval — the default source of "
       "`kgs gpu-util-stats` (fixed mode).  Same labels as container_gpu_sm_util.",
-      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
-      "pmfw+kubelet", "fast"),
+      CONTRACT, "pmfw+kubelet", "fast",
+      variants=(("counters", "GPU-active seconds (GRBM_SPI_BUSY) of the GPU allocated to the pod, counted from the "
+                             "allocation (--sm-util-source counters); 100 * rate() = mean busy %.  Same labels as "
+                             "container_gpu_sm_util."),
+                ("pmfw", "GFX-engine busy seconds of the GPU allocated to the pod from the PMFW accumulators, counted "
+                         "from the allocation (--sm-util-source pmfw); 100 * rate() = mean busy %.  Same labels as "
+                         "container_gpu_sm_util."))),
     F("container_gpu_mfma_busy_seconds_total", "counter",
       "MFMA-busy seconds (all SIMDs busy with matrix work for 1 s = 1) of the GPU allocated to the pod, counted from "
       "the allocation (hardware counters).  Same labels as container_gpu_sm_util.",
-      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      CONTRACT,
       "counters+kubelet", "pmc"),
     F("container_gpu_cu_seconds_total", "counter",
       "CU-occupancy seconds of the pod's own processes on the GPU (occupied CUs / all CUs, integrated by the "
@@ -61,7 +90,7 @@ CATALOG: tuple[Family, ...] = (
       "compute share: on a GPU shared by several pods each is billed its own share "
       "(`kgs gpu-util-stats --util-metric container_gpu_cu_seconds_total`), where container_gpu_busy_seconds_total "
       "bills each the whole GPU.  Same labels as container_gpu_sm_util.",
-      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      CONTRACT,
       "amdsmi-procs+cgroups+kubelet", "procs"),
     F("container_gpu_energy_joules_total", "counter",
       "Socket energy of the GPU allocated to the pod, counted from the allocation (PMFW energy accumulator).  "
@@ -69,12 +98,12 @@ CATALOG: tuple[Family, ...] = (
       "the pod's hourly energy; `kgs gpu-util-stats --energy` reports it in kWh.  A GPU shared by several pods "
       "counts in full for each; a compute partition (DPX/QPX/CPX) counts its XCCs' GFX-busy share of the socket's "
       "energy, so partitions add up to the socket.  Same labels as container_gpu_sm_util.",
-      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      CONTRACT,
       "pmfw+kubelet", "fast"),
     F("kgs_gpu_owner", "gauge",
       "1 per (GPU, pod, container) allocation reported by the kubelet: the join target that puts pod labels on any "
       "amdgpu_* series (`... * on (gpu, uuid) group_left(pod_name, namespace) kgs_gpu_owner`).",
-      ("kubernetes_io_hostname", "nvidia_gpu_type", "pod_name", "namespace", "container_name", "gpu", "uuid"),
+      CONTRACT,
       "kubelet", "attribution"),
     # ---- inventory / topology -------------------------------------------------------------
     F("amdgpu_device_info", "gauge", "Static device information (1).", extra=(
@@ -87,9 +116,11 @@ CATALOG: tuple[Family, ...] = (
       extra=("link", "peer_bdf", "link_type", "bit_rate_gbps", "max_bandwidth_gbps"), source="amdsmi", tier="slow"),
     # ---- utilisation ------------------------------------------------------------------------
     F("amdgpu_gfx_busy_percent", "gauge",
-      "GPU busy %, time-weighted mean over the window — the same source as container_gpu_sm_util (default auto: "
-      "hardware-counter GPU-active while the counter tier runs, PMFW GFX busy otherwise; never the exporter's own "
-      "counter READs)."),
+      "GPU busy %, time-weighted mean over the window — the source of container_gpu_sm_util (default auto: the "
+      "counter tier's dispatch-in-flight share — CPC busy less the learned READ cost, never below SPI busy — while "
+      "it covers the PMFW interval, PMFW GFX busy otherwise; never the exporter's own counter READs).",
+      variants=(("counters", "GFX-engine busy %, time-weighted mean over the window (PMFW accumulators)."),
+                ("pmfw", "GFX-engine busy %, time-weighted mean over the window (PMFW accumulators)."))),
     F("amdgpu_pmfw_gfx_busy_percent", "gauge",
       "Firmware (PMFW) GFX busy %, window mean from the PMFW accumulators: a dispatch in flight — and each counter "
       "READ packet of the exporter as ~80 us of work (99.7 % on an idle GPU READ at 8 kHz, profiles/r2/idle_busy/)."),
@@ -100,12 +131,23 @@ CATALOG: tuple[Family, ...] = (
       "all 8 at ~100 % even when waves run on a few; amdgpu_mfma_util_xcc_percent shows where they run.", extra=("xcc",)),
     F("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller activity %, window mean."),
     F("amdgpu_gfx_busy_seconds_total", "counter",
-      "∫ busy fraction dt of amdgpu_gfx_busy_percent's source; rate() = exact mean utilisation."),
+      "∫ busy fraction dt of amdgpu_gfx_busy_percent's source (default auto: the READ-immune integral behind "
+      "container_gpu_busy_seconds_total); rate() = exact mean utilisation.",
+      variants=(("counters", "∫ PMFW GFX busy fraction dt; rate() = exact mean utilisation."),
+                ("pmfw", "∫ PMFW GFX busy fraction dt; rate() = exact mean utilisation."))),
     F("amdgpu_pmfw_gfx_busy_seconds_total", "counter", "∫ PMFW GFX busy fraction dt (counts counter READs as work)."),
     F("kgs_util_source_seconds_total", "counter",
-      "Firmware time the READ-immune busy integral took from each source: counters (GRBM_SPI_BUSY, while the "
-      "counter tier ran through the whole PMFW interval) or pmfw (counter tier off, handed over, failed or stale).",
+      "Firmware time the READ-immune busy integral (--sm-util-source auto) billed from each source: counters (the "
+      "counter tier's dispatch integral — CPC_CPC_STAT_BUSY less the learned READ cost, never below GRBM_SPI_BUSY — "
+      "covered the PMFW interval) or pmfw (counter tier off, handed over, failed or stale).",
       extra=("source",), source="self"),
+    F("kgs_util_carry_seconds", "gauge",
+      "Counter busy the READ-immune integral has received but not billed yet (negative: billed ahead of the last "
+      "drain, run on at its share): a drain that lands after a PMFW interval's end is billed in the next one.",
+      source="self"),
+    F("kgs_util_dropped_seconds_total", "counter",
+      "Counter busy beyond the carry cap (one freshness window), never billed: a firmware clock slower than the "
+      "host's.  Should stay near 0.", source="self"),
     F("amdgpu_umc_busy_seconds_total", "counter", "∫ UMC busy fraction dt."),
     F("amdgpu_hbm_bandwidth_bytes_per_second", "gauge",
       "Estimated HBM (DRAM) read+write bandwidth, window mean, from UMC activity × the MI355X calibration "
@@ -152,9 +194,9 @@ CATALOG: tuple[Family, ...] = (
       tier="pmc"),
     F("amdgpu_dispatch_busy_seconds_total", "counter",
       "∫ dispatch-in-flight share dt from the counter stream (per drain: CPC_CPC_STAT_BUSY share of the clocks less "
-      "the exporter's own READ packet's CP time, never below the GRBM_SPI_BUSY share; an interval the CP was busy "
-      "for ≥ 97 % counts whole); rate() = the READ-immune 'a kernel is running' fraction behind "
-      "--sm-util-source auto.", source="counters", tier="pmc"),
+      "the exporter's own READ packet's CP time — counted once where it overlaps dispatch busy in intervals ≥ 400 us "
+      "— never below the GRBM_SPI_BUSY share; an interval the CP was busy for ≥ 90 % counts whole); rate() = the "
+      "READ-immune 'a kernel is running' fraction behind --sm-util-source auto.", source="counters", tier="pmc"),
     F("kgs_pmc_read_cp_seconds", "gauge", "Command-processor busy time of one full counter READ packet, learned on "
       "intervals without waves (what amdgpu_dispatch_busy_seconds_total subtracts per READ; lite READs are learned "
       "apart and cost less).", source="self",
@@ -295,6 +337,44 @@ CATALOG: tuple[Family, ...] = (
 )
 
 BY_NAME = {f.name: f for f in CATALOG}
+MODES = ("counters", "pmfw")  # --sm-util-source values with their own HELP variants (auto is the default text)
+
+
+def _c(text: str) -> str:
+    return '"' + text.replace("\\", "\\\\").replace('"', '\\"') + '"'
+
+
+def cpp_header() -> str:
+    """native/include/kgs/metric_help.h: the renderer's HELP / TYPE table."""
+    rows = []
+    for f in sorted(CATALOG, key=lambda f: f.name):
+        rows.append(f"    {{{_c(f.name)}, {_c(f.type)}, {_c('')}, {_c(f.help)}}},")
+        for mode, text in f.variants:
+            rows.append(f"    {{{_c(f.name)}, {_c(f.type)}, {_c(mode)}, {_c(text)}}},")
+    return ("// Generated by `python -m kube_gpu_stats_amd.models.schema --cpp-header` from\n"
+            "// kube_gpu_stats_amd/models/schema.py (the metric catalogue).  Do not edit.\n"
+            "#pragma once\n\n#include <cstddef>\n#include <cstring>\n\nnamespace kgs {\n\n"
+            "struct MetricDoc {\n  const char* name;\n  const char* type;\n"
+            "  const char* mode;  // \"\" = default (--sm-util-source auto); else that mode's text\n"
+            "  const char* help;\n};\n\n"
+            "inline constexpr MetricDoc kMetricDocs[] = {\n" + "\n".join(rows) + "\n};\n\n"
+            "// The family's HELP / TYPE for `mode` (falls back to the default text); nullptr if unknown.\n"
+            "// kMetricDocs is sorted by name, each default entry before its variants: a binary search.\n"
+            "inline const MetricDoc* metric_doc(const char* name, const char* mode = \"\") {\n"
+            "  size_t lo = 0, hi = sizeof kMetricDocs / sizeof kMetricDocs[0];\n"
+            "  while (lo < hi) {\n"
+            "    const size_t mid = (lo + hi) / 2;\n"
+            "    if (std::strcmp(kMetricDocs[mid].name, name) < 0) lo = mid + 1;\n"
+            "    else hi = mid;\n"
+            "  }\n"
+            "  const MetricDoc* def = nullptr;\n"
+            "  for (size_t i = lo; i < sizeof kMetricDocs / sizeof kMetricDocs[0] && "
+            "std::strcmp(kMetricDocs[i].name, name) == 0; ++i) {\n"
+            "    if (std::strcmp(kMetricDocs[i].mode, mode) == 0) return &kMetricDocs[i];\n"
+            "    if (!*kMetricDocs[i].mode) def = &kMetricDocs[i];\n"
+            "  }\n"
+            "  return def;\n"
+            "}\n\n}  // namespace kgs\n")
 
 
 def markdown() -> str:
@@ -312,4 +392,9 @@ PREAMBLE = ("# Metric catalogue\n\nGenerated by `python -m kube_gpu_stats_amd.mo
 
 
 if __name__ == "__main__":
-    print(PREAMBLE + markdown())
+    import sys
+
+    if sys.argv[1:] == ["--cpp-header"]:
+        sys.stdout.write(cpp_header())
+    else:
+        print(PREAMBLE + markdown())

@@ -77,8 +77,29 @@ def _headers() -> list[str]:
     return sorted(glob.glob(os.path.join(HERE, "include", "kgs", "*.h")))
 
 
+def metric_help_header() -> str:
+    """Regenerate include/kgs/metric_help.h (the renderer's HELP / TYPE table) from the
+    metric catalogue when the catalogue is newer; returns its path."""
+    out = os.path.join(HERE, "include", "kgs", "metric_help.h")
+    schema = os.path.join(PKG, "models", "schema.py")
+    if _stale(out, [schema]):
+        sys.path.insert(0, os.path.dirname(PKG))
+        from kube_gpu_stats_amd.models.schema import cpp_header
+
+        text = cpp_header()
+        if not os.path.exists(out) or open(out).read() != text:
+            with open(out + ".tmp", "w") as f:
+                f.write(text)
+            os.replace(out + ".tmp", out)
+        else:
+            os.utime(out)
+    return out
+
+
 def build_native(force: bool = False, verbose: bool = False) -> str:
     import pybind11
+
+    metric_help_header()
 
     out = native_module_path()
     srcs = sorted(glob.glob(os.path.join(HERE, "src", "*.cpp")))

@@ -1001,6 +1001,20 @@ bool make_lite(Agent* a, int k, uint32_t cmd_sz) {
   if (!c.ok) {
     return why(c.why);
   }
+  // fold() carries the last values over a lite READ only for the per_se counters
+  // (SQ / TA / TD / TCP): every dropped result must be one of theirs.  A
+  // session counter of another SE-indexed block (SPI, GRBMSE, ...) would have its
+  // per-SE copies dropped too and then be read from dwords the lite IB never writes.
+  // The IB has the same number of copies per event; the dropped ones must be exactly
+  // that many per event of a per_se counter.
+  size_t se_events = 0;
+  for (int ck : a->ev_counter) se_events += static_cast<size_t>(ck) < a->per_se.size() && a->per_se[ck];
+  const size_t total = c.kept_copies + c.dropped_copies, n_ev = a->events.size();
+  if (n_ev == 0 || total % n_ev != 0 || c.dropped_copies != total / n_ev * se_events) {
+    return why("dropped " + std::to_string(c.dropped_copies) + " of " + std::to_string(total) +
+               " results, not those of the " + std::to_string(se_events) + " per-SE events of " +
+               std::to_string(n_ev));
+  }
   // the compacted IB only (≈1.5 KB for the base set), not a whole command buffer
   const uint32_t need = static_cast<uint32_t>((out.size() * 4 + 4095) & ~size_t{4095});
   if (a->plib[k] && a->plib_sz[k] < need) {
@@ -1035,6 +1049,10 @@ bool make_lite(Agent* a, int k, uint32_t cmd_sz) {
 // main profile).  Called again when a re-open changed the event list: the slot
 // packets of the previous list would otherwise be folded against the new one.
 bool setup_pipeline(Agent* a, uint32_t cmd_sz, uint32_t out_sz, std::string& err) {
+  {  // a reason left by an earlier build of the slots no longer applies
+    std::lock_guard<std::mutex> g(a->info_mu);
+    a->lite_why.clear();
+  }
   a->batch = batch_size();
   a->nslots = a->batch >= 2 ? 2 * a->batch : 2;
   if (a->batch >= 2) a->plan.configure(a->batch, g_publish_ns);

@@ -100,6 +100,7 @@ struct IbCompact {
   bool ok = false;
   uint32_t dropped_copies = 0;  // per-SE COPY_DATA packets left out
   uint32_t dropped_dw = 0;      // dwords left out in all
+  uint32_t kept_copies = 0;     // COPY_DATA→memory packets the compacted IB still has
   std::vector<uint64_t> dropped_dsts;
   std::string why;              // when !ok
 };
@@ -190,6 +191,7 @@ inline IbCompact compact_se_sections(const uint32_t* ib, uint32_t ndw, std::vect
     r.why = "no per-SE section";
     return r;
   }
+  r.kept_copies = static_cast<uint32_t>(out_dsts.size());
   r.ok = true;
   return r;
 }

@@ -152,6 +152,9 @@ struct MockConfig {
   // Background xGMI traffic on every link, following the util curve (1 GB/s per
   // link at 100 %); off, only inject_xgmi() moves the link accumulators.
   bool xgmi_bg = true;
+  // A wrong link map (phase X's self-check): this GPU's link table reports the peers
+  // of its first two xGMI ports swapped, while its bytes still land on the true ports.
+  int xgmi_swap_dev = -1;
   // Slow-tier fault injection (per-device isolation test): after
   // slow_fault_after_s, calls of tier slow_fault_tier ("procs" | "links" |
   // "health") on device slow_fault_dev either hang (kind "hang": block for

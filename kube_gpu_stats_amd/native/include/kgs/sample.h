@@ -168,14 +168,20 @@ struct Integrals {
   // counts whole.  dispatch_drains > 0 once the counter set carries CPC busy.
   double dispatch_seconds = 0;
   uint64_t dispatch_drains = 0;
+  double pmc_last_share = 0;    // busy share (dispatch, else SPI) of the last drain interval
   double cpc_read_us = 0;       // the READ's own CP busy time as last learned (µs)
   // ∫ busy dt that does not count the exporter's own counter READs (the default
   // --sm-util-source auto behind container_gpu_sm_util / container_gpu_busy_seconds_total):
-  // per PMFW interval, the counter tier's Δactive_seconds (GRBM_SPI_BUSY) while it
-  // covered the whole interval, else the PMFW GFX busy.  util_counter_seconds is the
-  // time the counter source covered.
+  // per PMFW interval, the counter tier's dispatch integral (dispatch_seconds; SPI
+  // active_seconds for a set without CPC busy) while that tier covered the interval,
+  // the excess over an interval carried to the next (UtilBiller), else the PMFW GFX
+  // busy.  util_counter_seconds: the firmware time billed from the counters;
+  // util_carry_seconds: counter busy received but not yet billed;
+  // util_dropped_seconds: counter busy beyond the carry cap, never billed.
   double util_seconds = 0;
   double util_counter_seconds = 0;
+  double util_carry_seconds = 0;
+  double util_dropped_seconds = 0;
   // ∫ throttled fraction dt per reason (Δresidency / Δaccumulation_counter per
   // distinct PMFW table): seconds the GPU ran held back by each controller.
   double throttle_seconds[kThrottleReasons] = {};

@@ -51,6 +51,7 @@
 #include "kgs/pmc.h"
 #include "kgs/sample.h"
 #include "kgs/seqlock.h"
+#include "kgs/util_estimator.h"
 
 namespace kgs {
 
@@ -156,6 +157,13 @@ constexpr double kCpcFullFrac = 0.90;
 // split over-read 0.2 ms bursts in replay, tools/util_estimator_sim.py; at 1 kHz it
 // closes most of a 1 ms-burst train's −1.3 … −2.3 points).
 constexpr int64_t kClockSplitNs = 400000;
+// ... and counts the READ packet's own CP time once where it overlaps dispatch busy:
+// busy = (CPC − r) / (1 − r/clk), a READ landing at a uniformly random point of the
+// interval.  Subtracting r whole under-read the 1 kHz burst trains of r4f's raw READs
+// by 0.3 / 0.8 points (a READ during a kernel adds no CP busy); at 8 kHz the
+// intervals are shorter than this and the rule never applies (there it over-read
+// 0.2 ms trains, tools/util_estimator_sim.py).
+constexpr int64_t kReadOverlapNs = 400000;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };
@@ -264,6 +272,7 @@ struct DeviceState {
     a.pmc_last_ns = b.pmc_last_ns;
     a.dispatch_seconds = b.dispatch_seconds;
     a.dispatch_drains = b.dispatch_drains;
+    a.pmc_last_share = b.pmc_last_share;
     a.cpc_read_us = b.cpc_read_us;
     return a;
   }
@@ -361,15 +370,9 @@ class Sampler {
   // Per-device process CU-occupancy integrals (device's slow thread only; survive pause/resume).
   std::vector<std::vector<std::pair<uint32_t, double>>> cu_seconds_;
   std::vector<int64_t> last_proc_ns_;
-  // READ-immune util integral: the counter-tier state seen at the previous distinct
-  // PMFW sample (each device's PMFW thread only; survive pause/resume).
-  struct UtilPrev {
-    bool have = false;
-    bool dispatch = false;  // active_s holds dispatch_seconds (else active_seconds)
-    uint64_t epoch = 0;
-    double active_s = 0;
-  };
-  std::vector<UtilPrev> util_prev_;
+  // READ-immune util integral: the billing state carried between distinct PMFW
+  // samples (each device's PMFW thread only; survives pause/resume).
+  std::vector<UtilBiller> util_bill_;
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
   int stop_fd_ = -1;  // eventfd: readable once stop() was called; sampler threads ppoll() on it

@@ -1,0 +1,329 @@
+// The utilisation estimators behind container_gpu_sm_util / container_gpu_busy_seconds_total
+// (reference gpu_util_stats/gpu_util_stats.py:159 reads the series, :62-94 bills each
+// pod its mean) as pure, replayable units: no threads, no clocks, no device calls.
+//
+//  * DispatchEstimator — one hardware-counter drain in, the interval's integrals out.
+//    It owns everything the counter tier learns from the cumulative counts: the READ
+//    packet's own CP cost (learned on intervals without waves, per READ mode and per
+//    full / lite READ), the busy / idle shader clocks and the clock split of partial
+//    intervals, the full-interval rule, the stall (plausible-clock) watch, and the
+//    three READ-rate hysteresis machines (quiet, dispatch gap, dispatch-bound).
+//    Sampler::run_pmc feeds it every drain and only schedules and publishes.
+//  * UtilBiller — one distinct PMFW interval in, the seconds billed out.  While the
+//    counter tier covers the interval the counter integral's increment is billed;
+//    what exceeds the interval (drains land on host time, intervals are firmware
+//    time, and at 10 Hz one interval can hold two drains and the next none) is
+//    carried to the next intervals instead of being dropped — so the billed integral
+//    equals the counter integral over any window longer than a drain, at every rate.
+//
+// The pybind11 module binds both (bindings.cpp: DispatchEstimator, UtilBiller), so
+// the offline replay (tools/util_estimator_sim.py, tests/test_estimator_replay.py)
+// runs this very code on raw READ dumps recorded on MI355X.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+
+#include "kgs/pmc.h"
+
+namespace kgs {
+
+struct EstimatorParams {
+  // An interval whose SPI-busy share is below this (and with no MFMA cycle) has no
+  // waves: quiet, and its CP busy is the READ's own (sampler.h kQuietActiveFrac).
+  double quiet_active_frac = 0.02;
+  // A drain interval the CP was busy for at least this share counts whole.
+  double cpc_full_frac = 0.90;
+  // Partial intervals at least this long are split by the learned busy / idle clocks.
+  int64_t clock_split_ns = 400000;
+  double clock_ratio_lo = 0.9, clock_ratio_hi = 1.1;
+  // Partial intervals at least this long count the READ's own CP time once where it
+  // overlaps dispatch busy (0 = never).
+  int64_t read_overlap_ns = 0;
+  // Partial intervals at least this long are split in time, not cycles: idle time =
+  // idle cycles / the learned idle clock, busy time = the rest of the span — no busy
+  // clock needed, which a low READ rate may never see in a fully busy interval
+  // (0 = never; the clock-ratio split above applies instead).
+  int64_t time_split_ns = 0;
+  double ewma = 0.05;                 // weight of a new sample in every learned EWMA
+  int64_t quiet_hold_ns = 5000000;    // quiet intervals in a row before the device counts as quiet
+  double busy_min = 0.0;              // dispatch gap: SPI share below this (0 = off)
+  int64_t gap_hold_ns = 1000000;
+  double cp_only_min = 0.0;           // dispatch-bound: CP busy with no wave ≥ this share (0 = off)
+  int64_t dbound_hold_ns = 10000000;
+  double plausible_mhz_lo = 100.0, plausible_mhz_hi = 4000.0;
+  double num_simds = 1024.0;          // CUs × 4 (MFMA share of all SIMD cycles)
+};
+
+// One drain: cumulative counts since the session's START (mask bit i: value i read).
+struct Drain {
+  int64_t mono_ns = 0;
+  uint32_t mask = 0;
+  uint64_t count = 0, spi = 0, mfma = 0, cpc = 0;
+  bool se_fresh = true;   // the per-SE counters (MFMA) were read by this drain
+  bool fresh_mode = false;  // taken as a synchronous READ (quiet device), not pipelined
+};
+
+// What one drain adds, and the rate states after it.
+struct DrainStep {
+  bool interval = false;      // a previous drain existed: the increments below are real
+  double span_s = 0;
+  double active_s = 0;        // ∫ SPI-busy share dt
+  double mfma_s = 0;          // ∫ MFMA share of all SIMD cycles dt (fresh drains only)
+  bool have_dispatch = false;
+  double dispatch_s = 0;      // ∫ dispatch-in-flight share dt
+  double cp_only_share = 0;   // CP busy with no wave in flight, share of the clocks
+  bool learned = false;       // this interval taught the READ cost
+  bool quiet_interval = false, gap_interval = false, dbound_interval = false;
+  bool quiet = false, gap = false, dbound = false;  // hysteresis states after this drain
+};
+
+class DispatchEstimator {
+ public:
+  // A (re)START: every count restarts at 0 at time t, the rate states reset.
+  void restart(int64_t t) {
+    have_prev_ = have_se_ = true;
+    prev_count_ = prev_mfma_ = prev_spi_ = prev_cpc_ = 0;
+    prev_ns_ = se_ns_ = t;
+    se_count_ = se_mfma_ = 0;
+    quiet_ = gap_ = dbound_ = false;
+    quiet_since_ = gap_since_ = dbound_since_ = 0;
+    last_plausible_ns_ = t;
+  }
+  // A break with no new baseline (breaker trip, failed re-START): the next drain
+  // only re-baselines.
+  void invalidate(int64_t t) {
+    have_prev_ = have_se_ = false;
+    last_plausible_ns_ = t;
+  }
+  bool have_prev() const { return have_prev_; }
+  int64_t prev_ns() const { return prev_ns_; }
+  int64_t last_plausible_ns() const { return last_plausible_ns_; }
+  // The READ packet's own CP time, as last learned on a full (se_fresh) READ (µs).
+  double cpc_read_us() const { return cpc_read_us_; }
+  double read_cycles(bool fresh_mode, bool full) const { return read_cyc_[fresh_mode][full]; }
+  double read_spi_cycles(bool fresh_mode, bool full) const { return read_spi_[fresh_mode][full]; }
+  uint64_t read_learned(bool fresh_mode, bool full) const { return read_n_[fresh_mode][full]; }
+  double clk_busy_hz() const { return clk_busy_hz_; }
+  double clk_idle_hz() const { return clk_idle_hz_; }
+  bool quiet() const { return quiet_; }
+  bool gap() const { return gap_; }
+  bool dbound() const { return dbound_; }
+
+  DrainStep feed(const Drain& d, const EstimatorParams& p) {
+    DrainStep r;
+    const bool prev = have_prev_ && d.mono_ns > prev_ns_;
+    // Stall watch: GRBM_COUNT free-runs at the shader clock while our session is
+    // programmed; frozen or foreign counts give no plausible clock.
+    if (prev) {
+      const double mhz = d.count >= prev_count_ ? (d.count - prev_count_) * 1e3 / (d.mono_ns - prev_ns_) : 0.0;
+      if (mhz >= p.plausible_mhz_lo && mhz <= p.plausible_mhz_hi) last_plausible_ns_ = d.mono_ns;
+    }
+    // MFMA-busy share of all SIMD cycles since the previous drain that read the
+    // per-SE counters (every drain, unless lite READs are on), times that span.
+    if (d.se_fresh && have_se_ && d.mono_ns > se_ns_ && (d.mask & (1u << kPmcMfmaBusy)) && d.count > se_count_ &&
+        d.mfma >= se_mfma_) {
+      const double frac = static_cast<double>(d.mfma - se_mfma_) / (p.num_simds * static_cast<double>(d.count - se_count_));
+      r.mfma_s = std::min(frac, 1.0) * (d.mono_ns - se_ns_) * 1e-9;
+    }
+    if (d.se_fresh) {
+      have_se_ = true;
+      se_count_ = d.count;
+      se_mfma_ = d.mfma;
+      se_ns_ = d.mono_ns;
+    }
+    const bool have_act = (d.mask & (1u << kPmcGrbmActive)) != 0;
+    if (prev) {
+      r.interval = true;
+      r.span_s = (d.mono_ns - prev_ns_) * 1e-9;
+    }
+    if (prev && have_act && d.count > prev_count_ && d.spi >= prev_spi_) {
+      const double frac = static_cast<double>(d.spi - prev_spi_) / static_cast<double>(d.count - prev_count_);
+      r.active_s = std::min(frac, 1.0) * r.span_s;
+    }
+    // Dispatch in flight: the CP busy share of the interval, less the READ packet's own
+    // CP time, never below the SPI share.
+    if (prev && (d.mask & (1u << kPmcCpcBusy)) && d.count > prev_count_ && d.cpc >= prev_cpc_) {
+      const double clk = static_cast<double>(d.count - prev_count_);
+      const double cpc = std::min(clk, static_cast<double>(d.cpc - prev_cpc_));
+      const double act = have_act && d.spi >= prev_spi_ ? static_cast<double>(d.spi - prev_spi_) : 0.0;
+      const int m = d.fresh_mode ? 1 : 0;
+      const int f = d.se_fresh ? 1 : 0;
+      const int64_t span_ns = d.mono_ns - prev_ns_;
+      const double hz_now = clk / (span_ns * 1e-9);
+      // No wave, no MFMA cycle and the CP mostly idle: the CP busy here is our READ's,
+      // and so is the SPI blip (≈0.9 µs per READ: 0.7 % of the clocks at 8 kHz, so the
+      // test is the quiet threshold, not "no SPI at all" — r4f: a 0.5 % test kept 2 %
+      // of the 8 kHz READ-only intervals, the cheap ones, and learned 13 µs for 15.5).
+      if (act < p.quiet_active_frac * clk && d.mfma == prev_mfma_ && cpc < 0.5 * clk) {
+        const bool first = read_n_[m][f] == 0;
+        read_cyc_[m][f] = first ? cpc : (1 - p.ewma) * read_cyc_[m][f] + p.ewma * cpc;
+        read_spi_[m][f] = first ? act : (1 - p.ewma) * read_spi_[m][f] + p.ewma * act;
+        ++read_n_[m][f];
+        r.learned = true;
+        if (f) cpc_read_us_ = read_cyc_[m][f] / (hz_now * 1e-6);
+        // the idle clock between kernels, not a quiet GPU's (its clock drops: r4r)
+        if (!d.fresh_mode) clk_idle_hz_ = clk_idle_hz_ > 0 ? (1 - p.ewma) * clk_idle_hz_ + p.ewma * hz_now : hz_now;
+      }
+      // This READ's learned cost, or the other kind's before it has its own.
+      const int k = read_n_[m][f] ? f : 1 - f;
+      const double rcyc = read_cyc_[m][k];
+      // Waves of the workload: SPI busy less the READ's own blip.
+      const double wav = std::max(0.0, act - read_spi_[m][k]);
+      // An interval the CP was busy for ≥ cpc_full_frac counts whole: under a kernel the
+      // CPC idles a few % of each 125 µs interval at 8 kHz (r4f: MFMA and GEMM intervals
+      // 0.95-1.0), and subtracting a READ-only cost there under-read a GEMM stream by 4
+      // points.  Long partial intervals count the READ's CP time once where it overlaps
+      // dispatch busy, (cpc − read) / (1 − read/clk) (sampler.h kReadOverlapNs); at
+      // 8 kHz that over-read burst trains in replay, so short ones subtract it whole.
+      const bool full = cpc >= p.cpc_full_frac * clk;
+      const double net = p.read_overlap_ns > 0 && span_ns >= p.read_overlap_ns && rcyc < 0.5 * clk
+                             ? (cpc - rcyc) / (1.0 - rcyc / clk)
+                             : cpc - rcyc;
+      const double busy = full ? clk : std::max(wav, std::max(0.0, net));
+      double share = std::min(1.0, busy / clk);
+      if (full) {
+        clk_busy_hz_ = clk_busy_hz_ > 0 ? (1 - p.ewma) * clk_busy_hz_ + p.ewma * hz_now : hz_now;
+      } else if (p.time_split_ns > 0 && span_ns >= p.time_split_ns && share > 0 && clk_idle_hz_ > 0) {
+        // A long interval at a low READ rate: many kernels and gaps, each part at its
+        // own clock (MFMA bursts power-capped at ≈2.1 GHz, gaps at ≈2.4).  The idle
+        // part's time is its cycles at the idle clock; the busy part is the rest.
+        const double idle_s = std::max(0.0, clk - busy) / clk_idle_hz_;
+        share = std::clamp(1.0 - idle_s / (span_ns * 1e-9), 0.0, 1.0);
+      } else if (span_ns >= p.clock_split_ns && share > 0 && clk_busy_hz_ > 0 && clk_idle_hz_ > 0) {
+        // A cycle share under-weights a kernel that ran at a lower clock than the idle
+        // rest of the interval (MFMA under the power cap: ≈2.1 GHz against ≈2.4 idle):
+        // the time share is s·r / (1 − s + s·r), r = f_idle / f_busy.  f_busy comes from
+        // the last fully busy intervals, whose kernels need not clock like this one (a
+        // 0.2 ms burst is not power-capped like a 1 ms one): r is kept within ±10 %
+        // (r4q: ±25 % over-read a 0.2 ms train by 2 points).
+        const double rr = std::clamp(clk_idle_hz_ / clk_busy_hz_, p.clock_ratio_lo, p.clock_ratio_hi);
+        share = share * rr / (1.0 - share + share * rr);
+      }
+      r.have_dispatch = true;
+      r.dispatch_s = share * span_ns * 1e-9;
+      r.cp_only_share = std::max(0.0, busy - wav) / clk;
+      // Dispatch-bound: the CP dispatching with no wave in flight for a large share.
+      r.dbound_interval = p.cp_only_min > 0 && busy - wav >= p.cp_only_min * clk;
+    }
+    // Quiet = a shader engine had waves for < quiet_active_frac of the clocks since the
+    // previous READ, and no MFMA cycle ran.  Both counters are (nearly) blind to our own
+    // READs: SPI busy reads 0.65 % with nothing but 8 kHz of READs on the GPU
+    // (profiles/r2/immunity/).  Without the activity counter a device is never quiet.
+    // A dispatch gap: the same share below busy_min (quiet intervals included, so an
+    // idle stretch between short kernels does not restart the hold).
+    if (have_prev_ && have_act && d.count > prev_count_) {
+      const double act = static_cast<double>(d.spi - std::min(d.spi, prev_spi_));
+      const double clk = static_cast<double>(d.count - prev_count_);
+      r.quiet_interval = act < p.quiet_active_frac * clk && d.mfma == prev_mfma_;
+      r.gap_interval = p.busy_min > 0 && act < p.busy_min * clk;
+    }
+    quiet_ = hold(r.quiet_interval, quiet_since_, d.mono_ns, p.quiet_hold_ns);
+    gap_ = hold(r.gap_interval, gap_since_, d.mono_ns, p.gap_hold_ns) && !quiet_;
+    dbound_ = hold(r.dbound_interval, dbound_since_, d.mono_ns, p.dbound_hold_ns) && !quiet_;
+    r.quiet = quiet_;
+    r.gap = gap_;
+    r.dbound = dbound_;
+    prev_count_ = d.count;
+    prev_mfma_ = d.mfma;
+    prev_spi_ = d.spi;
+    prev_cpc_ = d.cpc;
+    prev_ns_ = d.mono_ns;
+    have_prev_ = true;
+    return r;
+  }
+
+ private:
+  // A run of qualifying intervals that began at the previous READ; true once it is
+  // at least hold_ns long.
+  bool hold(bool qualifies, int64_t& since, int64_t now, int64_t hold_ns) const {
+    if (!qualifies) {
+      since = 0;
+      return false;
+    }
+    if (since == 0) since = prev_ns_;
+    return now - since >= hold_ns;
+  }
+
+  bool have_prev_ = false, have_se_ = false;
+  uint64_t prev_count_ = 0, prev_mfma_ = 0, prev_spi_ = 0, prev_cpc_ = 0;
+  int64_t prev_ns_ = 0;
+  uint64_t se_count_ = 0, se_mfma_ = 0;
+  int64_t se_ns_ = 0;
+  // READ cost [synchronous?][full READ?]: CPC cycles, SPI-blip cycles (EWMA), samples.
+  double read_cyc_[2][2] = {};
+  double read_spi_[2][2] = {};
+  uint64_t read_n_[2][2] = {};
+  double cpc_read_us_ = 0;
+  double clk_busy_hz_ = 0, clk_idle_hz_ = 0;
+  bool quiet_ = false, gap_ = false, dbound_ = false;
+  int64_t quiet_since_ = 0, gap_since_ = 0, dbound_since_ = 0;
+  int64_t last_plausible_ns_ = 0;
+};
+
+// The counter tier as the PMFW thread sees it at one distinct PMFW sample.
+struct CounterCover {
+  bool ok = false;        // on, not stalled or failed, last drain fresh
+  uint64_t epoch = 0;     // bumped on every break of the counter integral
+  bool dispatch = false;  // busy_s is the dispatch integral (else SPI active)
+  double busy_s = 0;      // the counter tier's cumulative busy integral at its last drain
+  double share = 0;       // busy share of the last drain interval
+  double since_s = 0;     // host time from the last drain to this PMFW sample
+};
+
+class UtilBiller {
+ public:
+  struct Bill {
+    double billed_s = 0;
+    bool from_counters = false;
+  };
+  // One distinct PMFW interval: dt_s of firmware time, dgfx_s of PMFW GFX busy in it.
+  //
+  // While the counter tier held one epoch since the previous PMFW sample, the
+  // interval is billed from the counter integral: its value at the last drain, run
+  // on to this sample at the last interval's share (at 10 Hz the last drain can be
+  // 100 ms old; the next drain corrects the guess), plus what earlier intervals
+  // could not take, at most dt_s.  The rest carries on to the next intervals
+  // (negative: billed ahead of the drains, paid back first) — capped at
+  // ±max_carry_s, so a firmware clock slower than the host's cannot bank busy time
+  // that a saturated GPU then bills into a following idle stretch.  Else the PMFW
+  // busy, and the carry is dropped (its time lies in the intervals PMFW billed).
+  Bill bill(double dt_s, double dgfx_s, const CounterCover& c, double max_carry_s) {
+    Bill b;
+    const double v = c.busy_s + std::clamp(c.share, 0.0, 1.0) * std::clamp(c.since_s, 0.0, max_carry_s);
+    const bool cont = c.ok && have_ && epoch_ == c.epoch && dispatch_ == c.dispatch && c.busy_s >= last_s_;
+    if (cont) carry_s_ += v - last_v_;
+    else carry_s_ = 0;
+    if (dt_s > 0) {
+      if (cont) {
+        b.billed_s = std::clamp(carry_s_, 0.0, dt_s);
+        carry_s_ -= b.billed_s;
+        if (carry_s_ > max_carry_s) {
+          dropped_s_ += carry_s_ - max_carry_s;
+          carry_s_ = max_carry_s;
+        }
+        carry_s_ = std::max(carry_s_, -max_carry_s);
+        b.from_counters = true;
+      } else {
+        b.billed_s = std::clamp(dgfx_s, 0.0, dt_s);
+      }
+    }
+    have_ = c.ok;
+    epoch_ = c.epoch;
+    dispatch_ = c.dispatch;
+    last_s_ = c.busy_s;
+    last_v_ = v;
+    return b;
+  }
+  double carry_s() const { return carry_s_; }
+  // Counter busy beyond max_carry_s, never billed (a firmware / host clock skew, or a
+  // counter integral running ahead of firmware time).
+  double dropped_s() const { return dropped_s_; }
+
+ private:
+  bool have_ = false, dispatch_ = false;
+  uint64_t epoch_ = 0;
+  double last_s_ = 0, last_v_ = 0, carry_s_ = 0, dropped_s_ = 0;
+};
+
+}  // namespace kgs

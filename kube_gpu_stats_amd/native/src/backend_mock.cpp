@@ -309,6 +309,7 @@ class MockBackend final : public Backend {
       li.write_kb = bg / 2 + inj_[static_cast<size_t>(g)]->wr[static_cast<size_t>(li.link)].load();
       out.push_back(li);
     }
+    if (g == cfg_.xgmi_swap_dev && out.size() >= 2) std::swap(out[0].peer_bdf, out[1].peer_bdf);
     return 0;
   }
 

@@ -3,6 +3,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cmath>
+
 #include "kgs/exporter.h"
 #include "kgs/gpu_metrics.h"
 
@@ -46,6 +48,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.metrics_latency_s = get<double>(m, "metrics_latency_s", c.mock.metrics_latency_s);
     c.mock.proc_cu_share = get<std::vector<double>>(m, "proc_cu_share", c.mock.proc_cu_share);
     c.mock.xgmi_bg = get<bool>(m, "xgmi_bg", c.mock.xgmi_bg);
+    c.mock.xgmi_swap_dev = get<int>(m, "xgmi_swap_dev", c.mock.xgmi_swap_dev);
     c.mock.slow_fault_dev = get<int>(m, "slow_fault_dev", c.mock.slow_fault_dev);
     c.mock.slow_fault_tier = get<std::string>(m, "slow_fault_tier", c.mock.slow_fault_tier);
     c.mock.slow_fault_kind = get<std::string>(m, "slow_fault_kind", c.mock.slow_fault_kind);
@@ -266,6 +269,8 @@ class PyExporter {
     o["dispatch_drains"] = I.dispatch_drains;
     o["cpc_read_us"] = I.cpc_read_us;
     o["util_counter_seconds"] = I.util_counter_seconds;
+    o["util_carry_seconds"] = I.util_carry_seconds;
+    o["util_dropped_seconds"] = I.util_dropped_seconds;
     o["pmc_epoch"] = I.pmc_epoch;
     {
       py::dict t;
@@ -458,6 +463,24 @@ class PyExporter {
   Exporter ex_;
 };
 
+EstimatorParams sampler_estimator_params(int num_cu) {
+  const SamplerConfig c;
+  EstimatorParams p;
+  p.quiet_active_frac = kQuietActiveFrac;
+  p.cpc_full_frac = kCpcFullFrac;
+  p.clock_split_ns = kClockSplitNs;
+  p.read_overlap_ns = kReadOverlapNs;
+  p.quiet_hold_ns = kQuietHoldNs;
+  p.busy_min = c.pmc_busy_min;
+  p.gap_hold_ns = static_cast<int64_t>(c.pmc_gap_hold_s * 1e9);
+  p.cp_only_min = c.pmc_cp_only_min;
+  p.dbound_hold_ns = static_cast<int64_t>(c.pmc_dispatch_hold_s * 1e9);
+  p.plausible_mhz_lo = kPlausibleMhzLo;
+  p.plausible_mhz_hi = kPlausibleMhzHi;
+  p.num_simds = (num_cu > 0 ? num_cu : 256) * 4.0;
+  return p;
+}
+
 py::dict parse_metrics_blob(const py::bytes& b) {
   std::string s = b;
   GpuSample g;
@@ -535,6 +558,135 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def_property_readonly("pmc_gap_hz",
                              [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_gap_hz() : 0.0; })
       .def_property_readonly("slow_passes", &PyExporter::slow_passes);
+  // The utilisation estimators as pure units (util_estimator.h): the offline replay of
+  // raw READ dumps runs the sampler's own code.
+  py::class_<EstimatorParams>(m, "EstimatorParams")
+      .def(py::init<>())
+      .def_readwrite("quiet_active_frac", &EstimatorParams::quiet_active_frac)
+      .def_readwrite("cpc_full_frac", &EstimatorParams::cpc_full_frac)
+      .def_readwrite("clock_split_ns", &EstimatorParams::clock_split_ns)
+      .def_readwrite("clock_ratio_lo", &EstimatorParams::clock_ratio_lo)
+      .def_readwrite("clock_ratio_hi", &EstimatorParams::clock_ratio_hi)
+      .def_readwrite("read_overlap_ns", &EstimatorParams::read_overlap_ns)
+      .def_readwrite("time_split_ns", &EstimatorParams::time_split_ns)
+      .def_readwrite("ewma", &EstimatorParams::ewma)
+      .def_readwrite("quiet_hold_ns", &EstimatorParams::quiet_hold_ns)
+      .def_readwrite("busy_min", &EstimatorParams::busy_min)
+      .def_readwrite("gap_hold_ns", &EstimatorParams::gap_hold_ns)
+      .def_readwrite("cp_only_min", &EstimatorParams::cp_only_min)
+      .def_readwrite("dbound_hold_ns", &EstimatorParams::dbound_hold_ns)
+      .def_readwrite("num_simds", &EstimatorParams::num_simds);
+  m.def("sampler_estimator_params", &sampler_estimator_params, py::arg("num_cu") = 256,
+        "The EstimatorParams the sampler runs with under the default SamplerConfig");
+  py::class_<DrainStep>(m, "DrainStep")
+      .def_readonly("interval", &DrainStep::interval)
+      .def_readonly("span_s", &DrainStep::span_s)
+      .def_readonly("active_s", &DrainStep::active_s)
+      .def_readonly("mfma_s", &DrainStep::mfma_s)
+      .def_readonly("have_dispatch", &DrainStep::have_dispatch)
+      .def_readonly("dispatch_s", &DrainStep::dispatch_s)
+      .def_readonly("cp_only_share", &DrainStep::cp_only_share)
+      .def_readonly("learned", &DrainStep::learned)
+      .def_readonly("quiet_interval", &DrainStep::quiet_interval)
+      .def_readonly("gap_interval", &DrainStep::gap_interval)
+      .def_readonly("dbound_interval", &DrainStep::dbound_interval)
+      .def_readonly("quiet", &DrainStep::quiet)
+      .def_readonly("gap", &DrainStep::gap)
+      .def_readonly("dbound", &DrainStep::dbound);
+  py::class_<DispatchEstimator>(m, "DispatchEstimator")
+      .def(py::init<>())
+      .def("restart", &DispatchEstimator::restart, py::arg("mono_ns"))
+      .def("invalidate", &DispatchEstimator::invalidate, py::arg("mono_ns"))
+      .def(
+          "feed",
+          [](DispatchEstimator& e, const EstimatorParams& p, int64_t mono_ns, uint64_t count, uint64_t spi,
+             uint64_t cpc, py::object mfma, bool se_fresh, bool fresh_mode) {
+            Drain d;
+            d.mono_ns = mono_ns;
+            d.count = count;
+            d.spi = spi;
+            d.cpc = cpc;
+            d.mask = (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcCpcBusy);
+            if (!mfma.is_none()) {
+              d.mfma = mfma.cast<uint64_t>();
+              d.mask |= 1u << kPmcMfmaBusy;
+            }
+            d.se_fresh = se_fresh;
+            d.fresh_mode = fresh_mode;
+            return e.feed(d, p);
+          },
+          py::arg("params"), py::arg("mono_ns"), py::arg("count"), py::arg("spi"), py::arg("cpc"),
+          py::arg("mfma") = py::none(), py::arg("se_fresh") = true, py::arg("fresh_mode") = false,
+          "Fold one drain (cumulative counts since START); mfma=None: MFMA busy not in the set")
+      .def(
+          "replay",
+          [](DispatchEstimator& e, const EstimatorParams& p, const std::vector<std::vector<double>>& rows) {
+            // rows: [t_s, count, spi, cpc] (+ mfma, -1 = not read; + se_fresh): the integrals over the run.
+            py::dict o;
+            double disp = 0, act = 0, mfma = 0, span = 0;
+            uint64_t learned = 0, quiet = 0, dbound = 0;
+            for (const auto& r : rows) {
+              if (r.size() < 4) throw py::value_error("each row needs t_s, count, spi, cpc");
+              Drain d;
+              d.mono_ns = static_cast<int64_t>(std::llround(r[0] * 1e9));
+              d.count = static_cast<uint64_t>(r[1]);
+              d.spi = static_cast<uint64_t>(r[2]);
+              d.cpc = static_cast<uint64_t>(r[3]);
+              d.mask = (1u << kPmcGrbmCount) | (1u << kPmcGrbmActive) | (1u << kPmcCpcBusy);
+              if (r.size() > 4 && r[4] >= 0) {
+                d.mfma = static_cast<uint64_t>(r[4]);
+                d.mask |= 1u << kPmcMfmaBusy;
+              }
+              if (r.size() > 5) d.se_fresh = r[5] != 0;
+              const DrainStep s = e.feed(d, p);
+              disp += s.dispatch_s;
+              act += s.active_s;
+              mfma += s.mfma_s;
+              span += s.span_s;
+              learned += s.learned;
+              quiet += s.quiet;
+              dbound += s.dbound;
+            }
+            o["dispatch_s"] = disp;
+            o["active_s"] = act;
+            o["mfma_s"] = mfma;
+            o["span_s"] = span;
+            o["learned"] = learned;
+            o["quiet_drains"] = quiet;
+            o["dbound_drains"] = dbound;
+            return o;
+          },
+          py::arg("params"), py::arg("rows"),
+          "Fold a whole dump of drains (pipelined): rows [t_s, count, spi, cpc, mfma (-1: none), se_fresh]")
+      .def_property_readonly("cpc_read_us", &DispatchEstimator::cpc_read_us)
+      .def("read_cycles", &DispatchEstimator::read_cycles, py::arg("fresh_mode") = false, py::arg("full") = true)
+      .def("read_spi_cycles", &DispatchEstimator::read_spi_cycles, py::arg("fresh_mode") = false,
+           py::arg("full") = true)
+      .def_property_readonly("clk_busy_hz", &DispatchEstimator::clk_busy_hz)
+      .def_property_readonly("clk_idle_hz", &DispatchEstimator::clk_idle_hz)
+      .def_property_readonly("last_plausible_ns", &DispatchEstimator::last_plausible_ns);
+  py::class_<UtilBiller>(m, "UtilBiller")
+      .def(py::init<>())
+      .def(
+          "bill",
+          [](UtilBiller& b, double dt_s, double dgfx_s, bool ok, uint64_t epoch, double busy_s, double max_carry_s,
+             bool dispatch, double share, double since_s) {
+            CounterCover c;
+            c.ok = ok;
+            c.epoch = epoch;
+            c.dispatch = dispatch;
+            c.busy_s = busy_s;
+            c.share = share;
+            c.since_s = since_s;
+            const UtilBiller::Bill r = b.bill(dt_s, dgfx_s, c, max_carry_s);
+            return py::make_tuple(r.billed_s, r.from_counters);
+          },
+          py::arg("dt_s"), py::arg("dgfx_s"), py::arg("ok"), py::arg("epoch"), py::arg("busy_s"),
+          py::arg("max_carry_s") = 1.0, py::arg("dispatch") = true, py::arg("share") = 0.0,
+          py::arg("since_s") = 0.0,
+          "Bill one PMFW interval: (seconds billed, billed from the counters?)")
+      .def_property_readonly("carry_s", &UtilBiller::carry_s)
+      .def_property_readonly("dropped_s", &UtilBiller::dropped_s);
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
   m.def("pmc_counter_names", [] {

@@ -393,11 +393,16 @@ std::string Exporter::counters_json(int dev, int n, uint64_t since) {
   if (since > 0 || n > cap) n = cap;
   std::vector<PmcSample> buf;
   buf.reserve(static_cast<size_t>(n) + 1);
-  // newest first; one extra (older) entry gives the first returned sample its rates
+  // Newest first; one extra (older) entry gives the first returned sample its rates.
+  // With lite READs only the publishing drains read the per-SE counters (se_fresh):
+  // keep going, at most a batch further, until an older fresh drain is held too, so
+  // the first fresh sample's MFMA / TA rates have their base.
+  size_t extra_stale = 0;
   sampler_->state(dev).pmc_ring.visit_recent([&](const PmcSample& p) {
     buf.push_back(p);
-    if (since > 0 && p.seq <= since) return false;
-    return buf.size() < static_cast<size_t>(n) + 1;
+    const bool enough = since > 0 ? p.seq <= since : buf.size() >= static_cast<size_t>(n) + 1;
+    if (!enough) return true;
+    return p.se_fresh == 0 && ++extra_stale < 64;
   });
   const int num_cu = be_->info(dev).num_cu;
   std::string o = "{\"gpu\":" + std::to_string(dev) + ",\"counters\":[";
@@ -407,13 +412,18 @@ std::string Exporter::counters_json(int dev, int n, uint64_t since) {
   }
   o += "],\"samples\":[";
   bool first = true;
+  const PmcSample* last_fresh = nullptr;  // newest fresh drain older than the sample being written
   for (size_t i = buf.size(); i-- > 0;) {  // oldest first
     const PmcSample& p = buf[i];
-    if (since > 0 && p.seq <= since) continue;
-    if (since == 0 && i + 1 == buf.size() && buf.size() > static_cast<size_t>(n)) continue;  // rate base only
+    // the newest n (or those after `since`) are returned; older ones are rate bases
+    if (since > 0 ? p.seq <= since : i >= static_cast<size_t>(n)) {
+      if (p.se_fresh) last_fresh = &p;
+      continue;
+    }
     if (!first) o += ',';
     first = false;
-    o += "{\"seq\":" + std::to_string(p.seq) + ",\"mono_ns\":" + std::to_string(p.mono_ns) + ",\"v\":[";
+    o += "{\"seq\":" + std::to_string(p.seq) + ",\"mono_ns\":" + std::to_string(p.mono_ns) +
+         ",\"se_fresh\":" + (p.se_fresh ? "1" : "0") + ",\"v\":[";
     for (int k = 0; k < kPmcCount; ++k) {
       if (k) o += ',';
       if (p.mask & (1u << k)) o += std::to_string(p.value[k]);
@@ -421,28 +431,37 @@ std::string Exporter::counters_json(int dev, int n, uint64_t since) {
     }
     o += ']';
     if (i + 1 < buf.size()) {
+      // Device-wide counters (GRBM, CPC) are read by every drain: rates over the last interval.
       const PmcRates r = pmc_rates(buf[i + 1], p, num_cu);
       o += ",\"dt_us\":";
       jnum(o, r.dt_s * 1e6);
       o += ",\"gpu_active_pct\":";
       jnum(o, r.gpu_active_pct);
-      o += ",\"mfma_util_pct\":";
-      jnum(o, r.mfma_util_pct);
-      if (r.have_vmem) {
-        o += ",\"vmem_busy_pct\":";
-        jnum(o, r.vmem_busy_pct);
-      }
       o += ",\"gpu_clock_mhz\":";
       jnum(o, r.gpu_clock_mhz);
-      if (r.n_xcd > 0) {
-        o += ",\"xcd_mfma_util_pct\":[";
-        for (int x = 0; x < r.n_xcd; ++x) {
-          if (x) o += ',';
-          jnum(o, r.xcd_mfma_util_pct[x]);
+      // Per-SE counters (MFMA, TA) only on a fresh drain, over the span since the
+      // previous fresh one: a stale drain repeats the last values read.
+      if (p.se_fresh && last_fresh) {
+        const PmcRates f = pmc_rates(*last_fresh, p, num_cu);
+        if (f.have_mfma && f.dt_s > 0) {
+          o += ",\"mfma_util_pct\":";
+          jnum(o, f.mfma_util_pct);
         }
-        o += "]";
+        if (f.have_vmem && f.dt_s > 0) {
+          o += ",\"vmem_busy_pct\":";
+          jnum(o, f.vmem_busy_pct);
+        }
+        if (f.n_xcd > 0 && f.dt_s > 0) {
+          o += ",\"xcd_mfma_util_pct\":[";
+          for (int x = 0; x < f.n_xcd; ++x) {
+            if (x) o += ',';
+            jnum(o, f.xcd_mfma_util_pct[x]);
+          }
+          o += "]";
+        }
       }
     }
+    if (p.se_fresh) last_fresh = &p;
     o += '}';
   }
   o += "]}";

@@ -14,6 +14,7 @@
 #include <ctime>
 
 #include "kgs/exporter.h"
+#include "kgs/metric_help.h"
 
 namespace kgs {
 
@@ -94,9 +95,14 @@ struct W {
     if (end - p < 24) grow(24);
     p = std::to_chars(p, end, v).ptr;
   }
-  void head(const char* name, const char* type, const char* help) {
+  // HELP and TYPE come from the metric catalogue (models/schema.py → kgs/metric_help.h),
+  // in the text of the exporter's --sm-util-source mode.
+  const char* mode = "";
+  void head(const char* name) {
     if (!ok(name)) return;
-    put("# HELP ", 7); put(name); put(' '); put(help); put("\n# TYPE ", 8); put(name); put(' '); put(type); put('\n');
+    const MetricDoc* d = metric_doc(name, mode);
+    put("# HELP ", 7); put(name); put(' '); put(d ? d->help : "(not in the metric catalogue)");
+    put("\n# TYPE ", 8); put(name); put(' '); put(d ? d->type : "untyped"); put('\n');
   }
   // name{base,extra} value
   void labels(const char* name, const std::string& base, const char* extra) {
@@ -169,6 +175,7 @@ void Exporter::render(std::string& out) {
   const int64_t t0 = mono_ns();
   out.clear();
   W w(out, last_render_bytes_.load(std::memory_order_relaxed) + 8192, &filter_);
+  w.mode = cfg_.sm_util_source == "auto" ? "" : cfg_.sm_util_source.c_str();
   Sampler& S = *sampler_;
   const int nd = S.device_count();
   const std::vector<int>& ids = S.sampled_devices();
@@ -266,39 +273,25 @@ void Exporter::render(std::string& out) {
     const bool from_counters = cfg_.sm_util_source == "counters";
     const bool from_auto = cfg_.sm_util_source == "auto";
     if (from_auto) {
-      w.head("container_gpu_sm_util", "gauge",
-             "Busy percent of the GPU allocated to the pod over the exporter window, not counting the exporter's own "
-             "counter READs: hardware-counter GPU-active (GRBM_SPI_BUSY) while the counter tier runs, PMFW GFX busy "
-             "otherwise (reference metric contract; label nvidia_gpu_type kept for compatibility)");
+      w.head("container_gpu_sm_util");
       for (const auto& [d, lb] : pod_lines)
         if (snaps[static_cast<size_t>(d)].busy)
           w.line("container_gpu_sm_util", lb, nullptr, std::clamp(snaps[static_cast<size_t>(d)].util, 0.0, 100.0));
     } else if (from_counters) {
-      w.head("container_gpu_sm_util", "gauge",
-             "GPU-active percent (GRBM_SPI_BUSY: a shader engine has waves) of the GPU allocated to the pod, averaged "
-             "over the exporter window (reference metric contract; --sm-util-source counters)");
+      w.head("container_gpu_sm_util");
       for (const auto& [d, lb] : pod_lines) {
         const Snap& x = snaps[static_cast<size_t>(d)];
         if (x.pmc_rates) w.line("container_gpu_sm_util", lb, nullptr, x.r.gpu_active_pct);
       }
     } else {
-      w.head("container_gpu_sm_util", "gauge",
-             "GFX-engine (compute) busy percent of the GPU allocated to the pod, averaged over the exporter window "
-             "(reference metric contract; label nvidia_gpu_type kept for compatibility)");
+      w.head("container_gpu_sm_util");
       for (const auto& [d, lb] : pod_lines)
         if (snaps[static_cast<size_t>(d)].busy) w.line("container_gpu_sm_util", lb, nullptr, snaps[static_cast<size_t>(d)].g);
     }
     // Exact per-pod accounting: the GPU's busy integral since the pod was given
     // it.  rate() / increase() over any range is the exact mean utilisation,
     // whatever the scrape interval — the gauge above only sees its window.
-    w.head("container_gpu_busy_seconds_total", "counter",
-           from_auto ? "Busy seconds of the GPU allocated to the pod, counted from allocation, not counting the exporter's "
-                       "own counter READs (hardware-counter GPU-active while the counter tier runs, PMFW GFX busy "
-                       "otherwise; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)"
-           : from_counters ? "GPU-active seconds (GRBM_SPI_BUSY) of the GPU allocated to the pod, counted from allocation "
-                           "(hardware counters; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)"
-                         : "GFX-engine busy seconds of the GPU allocated to the pod, counted from allocation (PMFW "
-                           "accumulators; 100 * rate() = exact mean busy percent; same labels as container_gpu_sm_util)");
+    w.head("container_gpu_busy_seconds_total");
     for (size_t i = 0; i < pod_lines.size(); ++i) {
       const Owner* o = pod_owner[i];
       const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
@@ -315,10 +308,7 @@ void Exporter::render(std::string& out) {
     bool any_cu = false;
     for (size_t i = 0; i < pod_lines.size() && !any_cu; ++i) any_cu = pod_owner[i] != nullptr && cfg_.per_process;
     if (any_cu) {
-      w.head("container_gpu_cu_seconds_total", "counter",
-             "CU-occupancy seconds of the pod's own processes on the GPU (occupied CUs / all CUs, integrated; "
-             "processes that exited included), counted from allocation; 100 * rate() = the pod's compute share of "
-             "the GPU, exact on GPUs shared by several pods (same labels as container_gpu_sm_util)");
+      w.head("container_gpu_cu_seconds_total");
       for (size_t i = 0; i < pod_lines.size(); ++i) {
         const Owner* o = pod_owner[i];
         if (!o) continue;
@@ -336,10 +326,7 @@ void Exporter::render(std::string& out) {
     // Per-pod energy: the GPU's socket energy since the pod was given it (a GPU
     // shared by several pods counts in full for each: the pods hold it together;
     // a compute partition's energy is its share of the socket's, sampler.cpp).
-    w.head("container_gpu_energy_joules_total", "counter",
-           "Socket energy of the GPU allocated to the pod, counted from allocation (PMFW energy accumulator; a "
-           "compute partition gets its XCCs' busy share of the socket's; increase() over a window = joules the "
-           "pod's GPU drew; same labels as container_gpu_sm_util)");
+    w.head("container_gpu_energy_joules_total");
     for (size_t i = 0; i < pod_lines.size(); ++i) {
       const Owner* o = pod_owner[i];
       const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
@@ -349,9 +336,7 @@ void Exporter::render(std::string& out) {
     bool any_pmc_int = false;
     for (const auto& pl : pod_lines) any_pmc_int |= snaps[static_cast<size_t>(pl.first)].pmc_mfma;
     if (any_pmc_int) {
-      w.head("container_gpu_mfma_busy_seconds_total", "counter",
-             "MFMA-busy seconds (all SIMDs busy with matrix work for 1 s = 1) of the GPU allocated to the pod, counted "
-             "from allocation (hardware counters)");
+      w.head("container_gpu_mfma_busy_seconds_total");
       for (size_t i = 0; i < pod_lines.size(); ++i) {
         const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
         if (!x.pmc_mfma) continue;
@@ -363,8 +348,7 @@ void Exporter::render(std::string& out) {
     bool any_owner = false;
     for (const Owner* o : pod_owner) any_owner |= o != nullptr;
     if (any_owner) {
-      w.head("kgs_gpu_owner", "gauge",
-             "1 for every (GPU, pod, container) allocation the kubelet reports: join target for any amdgpu_* series");
+      w.head("kgs_gpu_owner");
       for (size_t i = 0; i < pod_lines.size(); ++i)
         if (pod_owner[i]) w.line("kgs_gpu_owner", pod_lines[i].second, nullptr, 1);
     }
@@ -373,9 +357,7 @@ void Exporter::render(std::string& out) {
     if (any_mfma) {
       // Same labels, hardware-counter matrix-core busy: GFX busy counts a GPU busy
       // while any dispatch is in flight; this says how much of it was MFMA work.
-      w.head("container_gpu_mfma_util", "gauge",
-             "Matrix-core (MFMA) busy percent of active cycles of the GPU allocated to the pod, over the exporter "
-             "window (hardware counters; same labels as container_gpu_sm_util)");
+      w.head("container_gpu_mfma_util");
       for (const auto& [d, lb] : pod_lines)
         if (snaps[static_cast<size_t>(d)].pmc_rates && snaps[static_cast<size_t>(d)].r.have_mfma)
           w.line("container_gpu_mfma_util", lb, nullptr, snaps[static_cast<size_t>(d)].r.mfma_util_pct);
@@ -393,7 +375,7 @@ void Exporter::render(std::string& out) {
   if (!sblock) {
     std::string blk;
     W b(blk, 16384, &filter_);
-    b.head("amdgpu_device_info", "gauge", "Static device information (value is always 1)");
+    b.head("amdgpu_device_info");
     for (int d : ids) {
       const DeviceInfo& in = be_->info(d);
       lb.assign(dev_labels_[static_cast<size_t>(d)]);
@@ -414,7 +396,7 @@ void Exporter::render(std::string& out) {
       b.line("amdgpu_device_info", lb, nullptr, 1);
     }
     if (!topo_.empty()) {
-      b.head("amdgpu_topology_link", "gauge", "Pairwise link between visible GPUs (1); labels carry type/hops/weight");
+      b.head("amdgpu_topology_link");
       for (const TopoEdge& e : topo_) {
         if (!sampled[static_cast<size_t>(e.src)]) continue;
         lb.assign(dev_labels_[static_cast<size_t>(e.src)]);
@@ -438,21 +420,15 @@ void Exporter::render(std::string& out) {
   // amdgpu_gfx_busy_*: the same busy signal as container_gpu_sm_util (--sm-util-source;
   // default auto: READ-immune); amdgpu_pmfw_gfx_busy_* is always the firmware's own.
   const bool util_auto = cfg_.sm_util_source == "auto";
-  w.head("amdgpu_gfx_busy_percent", "gauge",
-         util_auto ? "GPU busy percent over the exporter window, not counting the exporter's own counter READs "
-                     "(hardware-counter GPU-active while the counter tier runs, PMFW GFX busy otherwise)"
-                   : "GFX-engine busy percent, time-weighted mean over the exporter window (PMFW accumulators)");
+  w.head("amdgpu_gfx_busy_percent");
   for (int d : ids)
     if (snaps[d].busy)
       w.line("amdgpu_gfx_busy_percent", dev_labels_[d], nullptr, util_auto ? std::clamp(snaps[d].util, 0.0, 100.0) : snaps[d].g);
-  w.head("amdgpu_pmfw_gfx_busy_percent", "gauge",
-         "Firmware (PMFW) GFX busy percent over the exporter window: a dispatch in flight, and each counter READ "
-         "packet of the exporter as ~80 us of work");
+  w.head("amdgpu_pmfw_gfx_busy_percent");
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_pmfw_gfx_busy_percent", dev_labels_[d], nullptr, snaps[d].g);
-  w.head("amdgpu_gfx_busy_instant_percent", "gauge", "GFX-engine busy percent in the latest PMFW table");
+  w.head("amdgpu_gfx_busy_instant_percent");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFGfxBusy)) w.line("amdgpu_gfx_busy_instant_percent", dev_labels_[d], nullptr, snaps[d].s.gfx_busy_pct);
-  w.head("amdgpu_gfx_busy_xcc_percent", "gauge",
-         "Busy percent per XCC (accelerator complex die) over the last PMFW interval (per-XCC accumulators)");
+  w.head("amdgpu_gfx_busy_xcc_percent");
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFGfxBusyXcc)) continue;
@@ -461,45 +437,42 @@ void Exporter::render(std::string& out) {
              x.s.dt_s > 0 ? x.s.gfx_busy_xcc_window[c] : x.s.gfx_busy_xcc[c]);
     }
   }
-  w.head("amdgpu_umc_busy_percent", "gauge", "HBM memory-controller (UMC) activity percent, mean over the exporter window");
+  w.head("amdgpu_umc_busy_percent");
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_umc_busy_percent", dev_labels_[d], nullptr, snaps[d].u);
-  w.head("amdgpu_gfx_busy_seconds_total", "counter",
-         util_auto ? "Integral of the GPU busy fraction (amdgpu_gfx_busy_percent's source) over firmware time; rate() "
-                     "gives exact mean utilisation"
-                   : "Integral of GFX busy fraction over firmware time; rate() gives exact mean utilisation");
+  w.head("amdgpu_gfx_busy_seconds_total");
   for (int d : ids)
     if (snaps[d].have)
       w.line("amdgpu_gfx_busy_seconds_total", dev_labels_[d], nullptr, util_auto ? snaps[d].I.util_seconds : snaps[d].I.gfx_busy_seconds);
-  w.head("amdgpu_pmfw_gfx_busy_seconds_total", "counter",
-         "Integral of the firmware (PMFW) GFX busy fraction over firmware time (counts counter READs as work)");
+  w.head("amdgpu_pmfw_gfx_busy_seconds_total");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_pmfw_gfx_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.gfx_busy_seconds);
-  w.head("kgs_util_source_seconds_total", "counter",
-         "Firmware time the READ-immune busy integral (amdgpu_gfx_busy_seconds_total under --sm-util-source auto) "
-         "took from each source: counters (GRBM_SPI_BUSY) or pmfw (counter tier off, handed over, failed or stale)");
+  w.head("kgs_util_source_seconds_total");
   for (int d : ids) {
     if (!snaps[d].have) continue;
     w.line("kgs_util_source_seconds_total", dev_labels_[d], "source=\"counters\"", snaps[d].I.util_counter_seconds);
     w.line("kgs_util_source_seconds_total", dev_labels_[d], "source=\"pmfw\"",
            std::max(0.0, snaps[d].I.sampled_seconds - snaps[d].I.util_counter_seconds));
   }
-  w.head("amdgpu_umc_busy_seconds_total", "counter", "Integral of UMC busy fraction over firmware time");
+  w.head("kgs_util_carry_seconds");
+  for (int d : ids) if (snaps[d].have) w.line("kgs_util_carry_seconds", dev_labels_[d], nullptr, snaps[d].I.util_carry_seconds);
+  w.head("kgs_util_dropped_seconds_total");
+  for (int d : ids)
+    if (snaps[d].have) w.line("kgs_util_dropped_seconds_total", dev_labels_[d], nullptr, snaps[d].I.util_dropped_seconds);
+  w.head("amdgpu_umc_busy_seconds_total");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_umc_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds);
   const double full_bw = cfg_.hbm_bytes_per_s_at_full_umc;
-  w.head("amdgpu_hbm_bandwidth_bytes_per_second", "gauge",
-         "Estimated HBM (DRAM) read+write bandwidth over the exporter window, from UMC activity (MI355X calibration: "
-         "1 % = 84.1 GB/s; streams +-2.5 %, 64 B gathers count their 128 B DRAM accesses, cache hits are not counted)");
+  w.head("amdgpu_hbm_bandwidth_bytes_per_second");
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_hbm_bandwidth_bytes_per_second", dev_labels_[d], nullptr, snaps[d].u * 0.01 * full_bw);
-  w.head("amdgpu_hbm_bytes_total", "counter", "HBM bytes moved (read+write), integral of the UMC-derived bandwidth");
+  w.head("amdgpu_hbm_bytes_total");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_hbm_bytes_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds * full_bw);
 
   // ---- memory ------------------------------------------------------------
-  w.head("amdgpu_hbm_used_bytes", "gauge", "HBM3E bytes in use");
+  w.head("amdgpu_hbm_used_bytes");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFVram)) w.line_u("amdgpu_hbm_used_bytes", dev_labels_[d], nullptr, snaps[d].s.vram_used_bytes);
-  w.head("amdgpu_hbm_total_bytes", "gauge", "HBM3E capacity in bytes");
+  w.head("amdgpu_hbm_total_bytes");
   for (int d : ids) w.line_u("amdgpu_hbm_total_bytes", dev_labels_[d], nullptr, be_->info(d).vram_total_bytes);
 
   // ---- thermals / power / clocks ----------------------------------------
-  w.head("amdgpu_temperature_celsius", "gauge", "Temperature by sensor");
+  w.head("amdgpu_temperature_celsius");
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have) continue;
@@ -507,13 +480,11 @@ void Exporter::render(std::string& out) {
     if (x.s.valid & kFTempMem) w.line("amdgpu_temperature_celsius", dev_labels_[d], "sensor=\"hbm\"", x.s.temp_mem_c);
     if (x.s.valid & kFTempVrSoc) w.line("amdgpu_temperature_celsius", dev_labels_[d], "sensor=\"vrsoc\"", x.s.temp_vrsoc_c);
   }
-  w.head("amdgpu_power_watts", "gauge", "Socket power in watts");
+  w.head("amdgpu_power_watts");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPower)) w.line("amdgpu_power_watts", dev_labels_[d], nullptr, snaps[d].s.power_w);
-  w.head("amdgpu_energy_joules_total", "counter",
-         "Energy consumed since the exporter started (wrap-safe integration of the PMFW accumulator; a compute "
-         "partition counts its XCCs' GFX-busy share of the socket's energy, so partitions add up to the socket)");
+  w.head("amdgpu_energy_joules_total");
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_energy_joules_total", dev_labels_[d], nullptr, snaps[d].I.energy_joules);
-  w.head("amdgpu_clock_mhz", "gauge", "Current clock frequency (gfx = mean over XCCs)");
+  w.head("amdgpu_clock_mhz");
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have) continue;
@@ -527,16 +498,14 @@ void Exporter::render(std::string& out) {
     if (x.s.valid & kFUclk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"mem\"", x.s.uclk_mhz);
     if (x.s.valid & kFSocClk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"soc\"", x.s.socclk_mhz);
   }
-  w.head("amdgpu_throttle_seconds_total", "counter",
-         "Seconds the GPU ran held back by each throttler (PMFW residency accumulators: prochot, ppt = package power, "
-         "socket / vr / hbm thermal); 100 * rate() = violation percent (amdsmi PVIOL / TVIOL)");
+  w.head("amdgpu_throttle_seconds_total");
   for (int d : ids)
     if (snaps[d].have && (snaps[d].s.valid & kFThrottle))
       for (int r = 0; r < kThrottleReasons; ++r)
         w.line("amdgpu_throttle_seconds_total", dev_labels_[d], throttle_label(r), snaps[d].I.throttle_seconds[r]);
 
   // ---- interconnect ------------------------------------------------------
-  w.head("amdgpu_xgmi_read_bytes_total", "counter", "Bytes received per xGMI link (PMFW accumulator)");
+  w.head("amdgpu_xgmi_read_bytes_total");
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
@@ -546,7 +515,7 @@ void Exporter::render(std::string& out) {
              static_cast<double>(x.s.xgmi_read_kb[l]) * cfg_.xgmi_bytes_per_acc_unit);
     }
   }
-  w.head("amdgpu_xgmi_write_bytes_total", "counter", "Bytes sent per xGMI link (PMFW accumulator)");
+  w.head("amdgpu_xgmi_write_bytes_total");
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
@@ -556,7 +525,7 @@ void Exporter::render(std::string& out) {
              static_cast<double>(x.s.xgmi_write_kb[l]) * cfg_.xgmi_bytes_per_acc_unit);
     }
   }
-  w.head("amdgpu_xgmi_link_up", "gauge", "xGMI link status per port (1 up, 0 down)");
+  w.head("amdgpu_xgmi_link_up");
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
@@ -565,7 +534,7 @@ void Exporter::render(std::string& out) {
       w.line("amdgpu_xgmi_link_up", dev_labels_[d], kLinkLabels[l], x.s.xgmi_link_up[l] ? 1 : 0);
     }
   }
-  w.head("amdgpu_xgmi_link_info", "gauge", "Per-link peer and speed (slow tier, value 1)");
+  w.head("amdgpu_xgmi_link_info");
   for (int d : ids) {
     auto links = S.state(d).get_links();
     if (!links || !snaps[d].links_fresh) continue;
@@ -594,7 +563,7 @@ void Exporter::render(std::string& out) {
     }
     w.put(*lblock);
   }
-  w.head("amdgpu_ecc_errors_total", "counter", "Accumulated ECC errors by type (slow tier)");
+  w.head("amdgpu_ecc_errors_total");
   for (int d : ids) {
     auto h = S.state(d).get_health();
     if (!h || !h->ecc_valid) continue;
@@ -602,8 +571,7 @@ void Exporter::render(std::string& out) {
     w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"uncorrectable\"", h->ecc_uncorrectable);
     w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"deferred\"", h->ecc_deferred);
   }
-  w.head("amdgpu_ecc_block_errors_total", "counter",
-         "Accumulated ECC errors per RAS block (umc = HBM, gfx, xgmi_wafl, ...) and type, for the blocks with ECC enabled");
+  w.head("amdgpu_ecc_block_errors_total");
   for (int d : ids) {
     auto h = S.state(d).get_health();
     if (!h || !h->ecc_block_mask) continue;
@@ -618,76 +586,59 @@ void Exporter::render(std::string& out) {
       }
     }
   }
-  w.head("amdgpu_xgmi_error_status", "gauge", "xGMI error status: 0 none, 1 error, 2 multiple errors");
+  w.head("amdgpu_xgmi_error_status");
   for (int d : ids) {
     auto h = S.state(d).get_health();
     if (h && h->xgmi_error_status >= 0 && snaps[d].health_fresh)
       w.line("amdgpu_xgmi_error_status", dev_labels_[d], nullptr, h->xgmi_error_status);
   }
-  w.head("amdgpu_pcie_bytes_total", "counter",
-         "Bytes over the PCIe link (both directions), from the PMFW PCIe bandwidth accumulator times a MI355X "
-         "calibration (--pcie-bytes-per-unit; +-3 %); rate() = PCIe bandwidth");
+  w.head("amdgpu_pcie_bytes_total");
   for (int d : ids)
     if (snaps[d].have && (snaps[d].s.valid & kFPcie))
       w.line("amdgpu_pcie_bytes_total", dev_labels_[d], nullptr,
              static_cast<double>(snaps[d].s.pcie_bw_acc_gb) * cfg_.pcie_bytes_per_acc_unit);
-  w.head("amdgpu_pcie_bandwidth_acc_total", "counter",
-         "Raw PMFW PCIe bandwidth accumulator (amdsmi pcie_bandwidth_acc; advances once per ~100 bytes moved)");
+  w.head("amdgpu_pcie_bandwidth_acc_total");
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPcie)) w.line_u("amdgpu_pcie_bandwidth_acc_total", dev_labels_[d], nullptr, snaps[d].s.pcie_bw_acc_gb);
 
   // ---- hardware counters (PMC tier) ----------------------------------------
   bool any_pmc = false;
   for (int d : ids) any_pmc |= snaps[d].pmc_have;
   if (any_pmc) {
-    w.head("amdgpu_pmc_total", "counter",
-           "Raw hardware counter (direct command-processor reader), cumulative since exporter start");
+    w.head("amdgpu_pmc_total");
     for (int d : ids) {
       const Snap& x = snaps[d];
       if (!x.pmc_have) continue;
       for (int i = 0; i < kPmcCount; ++i)
         if (x.p.mask & (1u << i)) w.line_u("amdgpu_pmc_total", dev_labels_[d], pmc_counter_labels()[static_cast<size_t>(i)].c_str(), x.p.value[i]);
     }
-    w.head("amdgpu_gpu_active_seconds_total", "counter",
-           "Integral of the GPU-active share of clocks (GRBM_SPI_BUSY, hardware counters) over time; rate() = GPU-active "
-           "fraction, blind to the exporter's own counter READs");
+    w.head("amdgpu_gpu_active_seconds_total");
     for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_gpu_active_seconds_total", dev_labels_[d], nullptr, snaps[d].I.active_seconds);
     bool any_disp = false;
     for (int d : ids) any_disp |= snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0;
     if (any_disp) {
-      w.head("amdgpu_dispatch_busy_seconds_total", "counter",
-             "Integral of the dispatch-in-flight share of time (CPC_CPC_STAT_BUSY less the exporter's own READ "
-             "packets, never below GRBM_SPI_BUSY); rate() = the READ-immune 'a kernel is running' fraction");
+      w.head("amdgpu_dispatch_busy_seconds_total");
       for (int d : ids)
         if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
           w.line("amdgpu_dispatch_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.dispatch_seconds);
-      w.head("kgs_pmc_read_cp_seconds", "gauge",
-             "Command-processor busy time one full counter READ packet costs, as learned on intervals with no waves "
-             "(subtracted from CPC busy in amdgpu_dispatch_busy_seconds_total; lite READs are learned apart)");
+      w.head("kgs_pmc_read_cp_seconds");
       for (int d : ids)
         if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
           w.line("kgs_pmc_read_cp_seconds", dev_labels_[d], nullptr, snaps[d].I.cpc_read_us * 1e-6);
     }
-    w.head("amdgpu_mfma_busy_seconds_total", "counter",
-           "Integral of the MFMA-busy share of all SIMD cycles over time (hardware counters); rate() = matrix-core utilisation");
+    w.head("amdgpu_mfma_busy_seconds_total");
     for (int d : ids) if (snaps[d].pmc_mfma) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);
-    w.head("amdgpu_mfma_util_percent", "gauge",
-           "Matrix-core (MFMA) busy percent of the SIMD cycles while a shader engine had waves (GRBM_SPI_BUSY), over "
-           "the window; not rocprofv3 MfmaUtil (GUI-active based): the wall-clock share is "
-           "rate(amdgpu_mfma_busy_seconds_total)");
+    w.head("amdgpu_mfma_util_percent");
     for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_mfma) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
-    w.head("amdgpu_gpu_active_percent", "gauge",
-           "Percent of clocks a shader engine had waves to run (GRBM_SPI_BUSY) over the window; unlike the PMFW GFX busy "
-           "it does not count the exporter's own counter READs");
+    w.head("amdgpu_gpu_active_percent");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
-    w.head("amdgpu_vmem_busy_percent", "gauge", "Vector-memory address unit (TA) busy percent of active cycles over the window");
+    w.head("amdgpu_vmem_busy_percent");
     for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_vmem) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
-    w.head("amdgpu_gpu_clock_effective_mhz", "gauge", "Effective shader clock from GRBM_COUNT over the window");
+    w.head("amdgpu_gpu_clock_effective_mhz");
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_clock_effective_mhz", dev_labels_[d], nullptr, snaps[d].r.gpu_clock_mhz);
     bool any_xcd = false;
     for (int d : ids) any_xcd |= snaps[d].pmc_rates && snaps[d].r.n_xcd > 0;
     if (any_xcd) {
-      w.head("amdgpu_mfma_util_xcc_percent", "gauge",
-             "Matrix-core (MFMA) busy percent of one XCD's active cycles over the window (hardware counters)");
+      w.head("amdgpu_mfma_util_xcc_percent");
       for (int d : ids)
         if (snaps[d].pmc_rates)
           for (int x = 0; x < snaps[d].r.n_xcd; ++x)
@@ -695,15 +646,13 @@ void Exporter::render(std::string& out) {
       bool any_xcd_vmem = false;
       for (int d : ids) any_xcd_vmem |= snaps[d].pmc_rates && snaps[d].r.n_xcd > 0 && snaps[d].r.have_xcd_vmem;
       if (any_xcd_vmem) {
-        w.head("amdgpu_vmem_busy_xcc_percent", "gauge",
-               "Vector-memory address unit (TA) busy percent of one XCD's active cycles, mean over its CUs (full set)");
+        w.head("amdgpu_vmem_busy_xcc_percent");
         for (int d : ids)
           if (snaps[d].pmc_rates && snaps[d].r.have_xcd_vmem)
             for (int x = 0; x < snaps[d].r.n_xcd; ++x)
               w.line("amdgpu_vmem_busy_xcc_percent", dev_labels_[d], kXccLabels[x], snaps[d].r.xcd_vmem_busy_pct[x]);
       }
-      w.head("amdgpu_gpu_active_xcc_percent", "gauge",
-             "GRBM SPI-busy percent of clocks of one XCD over the window (one of its shader engines has waves to run)");
+      w.head("amdgpu_gpu_active_xcc_percent");
       for (int d : ids)
         if (snaps[d].pmc_rates)
           for (int x = 0; x < snaps[d].r.n_xcd; ++x)
@@ -713,7 +662,7 @@ void Exporter::render(std::string& out) {
 
   // ---- per-process attribution ------------------------------------------
   if (cfg_.per_process) {
-    w.head("amdgpu_process_hbm_bytes", "gauge", "HBM bytes held by a process, attributed to its pod when known");
+    w.head("amdgpu_process_hbm_bytes");
     // Labels of every process line, built once per render and shared by the
     // five per-process families.
     std::vector<std::shared_ptr<const std::vector<ProcInfo>>> procs(static_cast<size_t>(nd));
@@ -745,88 +694,71 @@ void Exporter::render(std::string& out) {
       kv(l, "pod_uid", po ? po->pod_uid : none);
     }
     for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_hbm_bytes", plabels[i], nullptr, plist[i].second->vram_bytes);
-    w.head("amdgpu_process_gtt_bytes", "gauge", "GTT (host-mapped) bytes held by a process");
+    w.head("amdgpu_process_gtt_bytes");
     for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_gtt_bytes", plabels[i], nullptr, plist[i].second->gtt_bytes);
-    w.head("amdgpu_process_cu_occupancy", "gauge", "Compute units occupied by the process' waves");
+    w.head("amdgpu_process_cu_occupancy");
     for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_cu_occupancy", plabels[i], nullptr, plist[i].second->cu_occupancy);
-    w.head("amdgpu_process_gfx_seconds_total", "counter", "GFX engine time consumed by the process (driver-reported; 0 where unsupported)");
+    w.head("amdgpu_process_gfx_seconds_total");
     for (size_t i = 0; i < plist.size(); ++i) w.line("amdgpu_process_gfx_seconds_total", plabels[i], nullptr, plist[i].second->gfx_ns * 1e-9);
-    w.head("amdgpu_process_cu_seconds_total", "counter",
-           "Integral of the process' CU-occupancy share (occupied CUs / all CUs) over time; rate() = compute share");
+    w.head("amdgpu_process_cu_seconds_total");
     for (size_t i = 0; i < plist.size(); ++i) w.line("amdgpu_process_cu_seconds_total", plabels[i], nullptr, plist[i].second->cu_seconds);
   }
 
   // ---- self metrics ------------------------------------------------------
-  w.head("kgs_up", "gauge", "1 if the device's last sampler read succeeded");
+  w.head("kgs_up");
   for (int d : ids) w.line("kgs_up", dev_labels_[d], nullptr, S.state(d).up.load());
-  w.head("kgs_last_sample_age_seconds", "gauge", "Seconds since the last successful read");
+  w.head("kgs_last_sample_age_seconds");
   for (int d : ids) {
     const int64_t t = S.state(d).last_ok_mono_ns.load();
     w.line("kgs_last_sample_age_seconds", dev_labels_[d], nullptr, t ? (now - t) * 1e-9 : -1.0);
   }
-  w.head("kgs_samples_total", "counter", "Distinct hardware samples (new PMFW firmware timestamp)");
+  w.head("kgs_samples_total");
   for (int d : ids) w.line_u("kgs_samples_total", dev_labels_[d], nullptr, snaps[d].I.distinct_samples);
-  w.head("kgs_reads_total", "counter", "Sampler reads attempted");
+  w.head("kgs_reads_total");
   for (int d : ids) w.line_u("kgs_reads_total", dev_labels_[d], nullptr, snaps[d].I.reads);
-  w.head("kgs_read_errors_total", "counter", "Sampler reads that failed");
+  w.head("kgs_read_errors_total");
   for (int d : ids) w.line_u("kgs_read_errors_total", dev_labels_[d], nullptr, snaps[d].I.read_errors);
-  w.head("kgs_sampler_overruns_total", "counter", "Ticks whose work overran the sampling period");
+  w.head("kgs_sampler_overruns_total");
   for (int d : ids) w.line_u("kgs_sampler_overruns_total", dev_labels_[d], nullptr, snaps[d].I.overruns);
-  w.head("kgs_device_recoveries_total", "counter",
-         "Device re-opens / management-library re-inits that restored reads after a failure streak");
+  w.head("kgs_device_recoveries_total");
   for (int d : ids) w.line_u("kgs_device_recoveries_total", dev_labels_[d], nullptr, snaps[d].I.recoveries);
-  w.head("kgs_pmc_samples_total", "counter", "Hardware-counter drains completed");
+  w.head("kgs_pmc_samples_total");
   for (int d : ids) w.line_u("kgs_pmc_samples_total", dev_labels_[d], nullptr, snaps[d].I.pmc_samples);
-  w.head("kgs_pmc_read_seconds_total", "counter", "Time spent draining hardware counters");
+  w.head("kgs_pmc_read_seconds_total");
   for (int d : ids) w.line("kgs_pmc_read_seconds_total", dev_labels_[d], nullptr, snaps[d].I.pmc_read_seconds);
-  w.head("kgs_pmc_errors_total", "counter", "Hardware-counter drains that failed");
+  w.head("kgs_pmc_errors_total");
   for (int d : ids) w.line_u("kgs_pmc_errors_total", dev_labels_[d], nullptr, snaps[d].I.pmc_errors);
   if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
-    w.head("kgs_pmc_enabled", "gauge",
-           "1 while the exporter holds the GPU's hardware counters, 0 after it handed them to another profiler");
+    w.head("kgs_pmc_enabled");
     for (int d : ids) w.line_u("kgs_pmc_enabled", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_on.load()));
-    w.head("kgs_pmc_releases_total", "counter", "Times the counters were handed to another profiler (SIGUSR1, /control/pmc/release)");
+    w.head("kgs_pmc_releases_total");
     for (int d : ids) w.line_u("kgs_pmc_releases_total", dev_labels_[d], nullptr, S.state(d).pmc_releases.load());
-    w.head("kgs_pmc_stalled", "gauge",
-           "1 while GRBM_COUNT shows no plausible clock (another profiler stopped or reprogrammed the counters)");
+    w.head("kgs_pmc_stalled");
     for (int d : ids) w.line_u("kgs_pmc_stalled", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_stalled.load()));
-    w.head("kgs_pmc_reclaims_total", "counter", "Automatic counter re-STARTs after a stall (--pmc-reclaim-s)");
+    w.head("kgs_pmc_reclaims_total");
     for (int d : ids) w.line_u("kgs_pmc_reclaims_total", dev_labels_[d], nullptr, S.state(d).pmc_reclaims.load());
-    w.head("kgs_pmc_refreshes_total", "counter", "Periodic counter re-STARTs that reprogram the selects (--pmc-refresh-s)");
+    w.head("kgs_pmc_refreshes_total");
     for (int d : ids) w.line_u("kgs_pmc_refreshes_total", dev_labels_[d], nullptr, S.state(d).pmc_refreshes.load());
-    w.head("kgs_pmc_quiet", "gauge",
-           "1 while the last counter READ interval saw no wave and no MFMA cycle: READs run at --pmc-idle-hz, so the "
-           "exporter's own command-processor packets do not read as GPU activity");
+    w.head("kgs_pmc_quiet");
     for (int d : ids) w.line_u("kgs_pmc_quiet", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_quiet.load()));
-    w.head("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU");
+    w.head("kgs_pmc_quiet_skips_total");
     for (int d : ids) w.line_u("kgs_pmc_quiet_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_quiet_skips.load());
-    w.head("kgs_pmc_gap", "gauge",
-           "1 while the counter READ intervals had waves for less than --pmc-busy-min of their clocks (a dispatch-bound "
-           "or gappy kernel stream): READs run at --pmc-gap-hz, since each READ packet delays the workload's dispatches");
+    w.head("kgs_pmc_gap");
     for (int d : ids) w.line_u("kgs_pmc_gap", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_gap.load()));
-    w.head("kgs_pmc_dispatch_bound", "gauge",
-           "1 while the command processor dispatched with no wave in flight for at least --pmc-cp-only-min of the "
-           "clocks (a stream of µs kernels, which each READ packet slows): READs run at --pmc-gap-hz");
+    w.head("kgs_pmc_dispatch_bound");
     for (int d : ids)
       w.line_u("kgs_pmc_dispatch_bound", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_dbound.load()));
-    w.head("kgs_pmc_gap_skips_total", "counter",
-           "Sampler ticks that skipped their counter READ in a dispatch gap or a dispatch-bound stream");
+    w.head("kgs_pmc_gap_skips_total");
     for (int d : ids) w.line_u("kgs_pmc_gap_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_gap_skips.load());
-    w.head("kgs_pmc_failed", "gauge",
-           "1 while the counter tier's circuit breaker is open: consecutive counter drains failed (a wedged command "
-           "processor); READs stop, the reader's queue is recreated and re-STARTed with exponential backoff");
+    w.head("kgs_pmc_failed");
     for (int d : ids) w.line_u("kgs_pmc_failed", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_failed.load()));
-    w.head("kgs_pmc_breaker_trips_total", "counter", "Times the counter tier's circuit breaker opened");
+    w.head("kgs_pmc_breaker_trips_total");
     for (int d : ids) w.line_u("kgs_pmc_breaker_trips_total", dev_labels_[d], nullptr, S.state(d).pmc_breaker_trips.load());
-    w.head("kgs_pmc_retries_total", "counter", "Reader resets + re-STARTs attempted while the breaker was open");
+    w.head("kgs_pmc_retries_total");
     for (int d : ids) w.line_u("kgs_pmc_retries_total", dev_labels_[d], nullptr, S.state(d).pmc_retries.load());
-    w.head("kgs_pmc_reordered_total", "counter",
-           "Counter drains dropped because their command-processor time preceded the previous drain's (the next "
-           "drain covers the interval; should stay 0)");
+    w.head("kgs_pmc_reordered_total");
     for (int d : ids) w.line_u("kgs_pmc_reordered_total", dev_labels_[d], nullptr, S.state(d).pmc_reordered.load());
-    w.head("kgs_sampler_wake_lateness_seconds", "histogram",
-           "How late the counter thread woke against each tick's absolute deadline (CPU contention, idle-state exit); "
-           "a tick later than 4 periods is skipped (kgs_sampler_overruns_total)");
+    w.head("kgs_sampler_wake_lateness_seconds");
     for (int d : ids) {
       const DeviceState& st = S.state(d);
       uint64_t cum = 0;
@@ -844,40 +776,31 @@ void Exporter::render(std::string& out) {
         if (pmc_->publish_stats(d, p)) ps.emplace_back(d, p);
       }
       if (!ps.empty()) {
-        w.head("kgs_pmc_publishes_total", "counter",
-               "Counter READs that wrote the GPU's L2 back to publish their results to the host (--pmc-batch: one per "
-               "batch of READs at high rates; every READ when unbatched)");
+        w.head("kgs_pmc_publishes_total");
         for (const auto& [d, p] : ps) w.line_u("kgs_pmc_publishes_total", dev_labels_[d], nullptr, p.publishes);
-        w.head("kgs_pmc_unlanded_total", "counter",
-               "Batched counter READs dropped because a result was not in host memory when their batch was folded "
-               "(after a 200 us wait; the next sample covers the interval; should stay near 0)");
+        w.head("kgs_pmc_unlanded_total");
         for (const auto& [d, p] : ps) w.line_u("kgs_pmc_unlanded_total", dev_labels_[d], nullptr, p.unlanded);
       }
     }
   }
-  w.head("kgs_sampler_thread_hung", "gauge",
-         "1 if a sampler thread of the device was stuck in a device call when sampling last stopped (it was "
-         "abandoned; that tier restarts once the call returns)");
+  w.head("kgs_sampler_thread_hung");
   for (int d : ids) w.line_u("kgs_sampler_thread_hung", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).thread_hung.load()));
-  w.head("kgs_slow_reads_total", "counter",
-         "Management-library reads by the node-wide slow thread (per-process list / xGMI link table + RAS)");
+  w.head("kgs_slow_reads_total");
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"procs\"", st.proc_reads.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"links\"", st.link_reads.load(std::memory_order_relaxed));
   }
-  w.head("kgs_slow_read_seconds_total", "counter", "Time the device's slow thread spent in management-library calls");
+  w.head("kgs_slow_read_seconds_total");
   for (int d : ids) w.line("kgs_slow_read_seconds_total", dev_labels_[d], nullptr, S.state(d).slow_ns_total.load(std::memory_order_relaxed) * 1e-9);
-  w.head("kgs_slow_errors_total", "counter", "Management-library reads of the device's slow thread that failed, by tier");
+  w.head("kgs_slow_errors_total");
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"procs\"", st.proc_errors.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"links\"", st.link_errors.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"health\"", st.health_errors.load(std::memory_order_relaxed));
   }
-  w.head("kgs_slow_last_ok_age_seconds", "gauge",
-         "Seconds since the tier's last good management-library read on the device (-1 = never): per-process "
-         "lines, the link table and the RAS status are dropped once this passes --stale-after");
+  w.head("kgs_slow_last_ok_age_seconds");
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     const std::atomic<int64_t>* oks[3] = {&st.procs_ok_ns, &st.links_ok_ns, &st.health_ok_ns};
@@ -890,20 +813,16 @@ void Exporter::render(std::string& out) {
       w.line("kgs_slow_last_ok_age_seconds", dev_labels_[d], tl, ok > 0 ? (now - ok) * 1e-9 : -1.0);
     }
   }
-  w.head("kgs_slow_call_seconds", "gauge",
-         "How long the device's slow thread has been inside its current management-library call (0 = none in "
-         "flight); a call that never returns keeps growing here");
+  w.head("kgs_slow_call_seconds");
   for (int d : ids) {
     const int64_t t = S.state(d).slow_call_ns.load(std::memory_order_acquire);
     w.line("kgs_slow_call_seconds", dev_labels_[d], nullptr, t > 0 && now > t ? (now - t) * 1e-9 : 0.0);
   }
-  w.head("kgs_slow_thread_hung", "gauge",
-         "1 if the device's slow thread was stuck in a management-library call when sampling last stopped (it was "
-         "abandoned; the slow tiers restart once the call returns)");
+  w.head("kgs_slow_thread_hung");
   for (int d : ids) w.line_u("kgs_slow_thread_hung", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).slow_hung.load()));
-  w.head("kgs_sampled_seconds_total", "counter", "Firmware time covered by distinct samples");
+  w.head("kgs_sampled_seconds_total");
   for (int d : ids) w.line("kgs_sampled_seconds_total", dev_labels_[d], nullptr, snaps[d].I.sampled_seconds);
-  w.head("kgs_sample_read_seconds", "histogram", "Latency of one fast-tier backend read");
+  w.head("kgs_sample_read_seconds");
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     uint64_t cum = 0;
@@ -916,19 +835,18 @@ void Exporter::render(std::string& out) {
   }
   std::string nl;
   kv(nl, "kubernetes_io_hostname", node, false);
-  w.head("kgs_scrapes_total", "counter", "Scrapes rendered");
+  w.head("kgs_scrapes_total");
   w.line_u("kgs_scrapes_total", nl, nullptr, scrapes.load() + 1);
-  w.head("kgs_scrape_render_seconds_total", "counter", "Total time spent rendering /metrics");
+  w.head("kgs_scrape_render_seconds_total");
   w.line("kgs_scrape_render_seconds_total", nl, nullptr, render_ns_total.load() * 1e-9);
-  w.head("kgs_scrape_render_last_seconds", "gauge", "Render time of the previous scrape");
+  w.head("kgs_scrape_render_last_seconds");
   w.line("kgs_scrape_render_last_seconds", nl, nullptr, render_ns_last.load() * 1e-9);
-  w.head("kgs_http_connections", "gauge", "HTTP connections held open by the exporter");
+  w.head("kgs_http_connections");
   w.line_u("kgs_http_connections", nl, nullptr, http_conns_open.load());
-  w.head("kgs_http_connections_closed_total", "counter",
-         "HTTP connections the exporter closed itself: idle past --http-idle-s, or evicted past --http-max-conns");
+  w.head("kgs_http_connections_closed_total");
   w.line_u("kgs_http_connections_closed_total", nl, "reason=\"idle\"", http_closed_idle.load());
   w.line_u("kgs_http_connections_closed_total", nl, "reason=\"limit\"", http_closed_limit.load());
-  w.head("kgs_build_info", "gauge", "Exporter build / configuration (value 1)");
+  w.head("kgs_build_info");
   {
     std::string lb = nl;
     kv(lb, "version", "0.1.0");

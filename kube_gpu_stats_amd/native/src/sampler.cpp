@@ -113,7 +113,7 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
   cu_seconds_.resize(static_cast<size_t>(n));
   pod_cu_.resize(static_cast<size_t>(n));
   last_proc_ns_.assign(static_cast<size_t>(n), 0);
-  util_prev_.resize(static_cast<size_t>(n));
+  util_bill_.resize(static_cast<size_t>(n));
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
 }
 
@@ -379,48 +379,46 @@ void Sampler::integrate(int dev, const GpuSample* prev, GpuSample& cur, Integral
 
 // ---- READ-immune busy integral (--sm-util-source auto) ------------------------
 // Per distinct PMFW interval (dt of firmware time, dgfx_s of PMFW GFX busy in it):
-// while the device's counter tier ran through the whole interval — same epoch as at
-// the previous PMFW sample, counters held and not stalled, a drain no older than
-// three of its slowest READ periods — the interval is billed the counter tier's
-// Δdispatch_seconds (CP busy less the exporter's own READ packets: a dispatch in
-// flight, the PMFW busy's meaning; Δactive_seconds, waves in a shader engine, for a
-// counter set without CPC busy), else the PMFW GFX busy (a dispatch in flight, but
-// counting each READ as ≈80 µs of work, profiles/r2/idle_busy/).  Either way the
-// integral is exact over any range covered by one source, and monotonic.
+// while the device's counter tier ran through the interval — same epoch as at the
+// previous PMFW sample, counters held and not stalled, a drain no older than three
+// of its slowest READ periods — the interval is billed from the counter tier's
+// busy integral (Δdispatch_seconds: CP busy less the exporter's own READ packets,
+// floored at SPI busy — a dispatch in flight, the PMFW busy's meaning; Δactive_seconds,
+// waves in a shader engine, for a counter set without CPC busy), else the PMFW GFX
+// busy (a dispatch in flight, but counting each READ as ≈80 µs of work,
+// profiles/r2/idle_busy/).  Drains land on host time and intervals are firmware time,
+// so an interval can receive more than dt of counter busy (two drains) and the next
+// none: UtilBiller (util_estimator.h) carries the excess forward instead of dropping
+// it (at 10 Hz dropping it billed a saturated GPU 75 %).
 void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, Integrals& I, GpuSample& s) {
   DeviceState& st = *states_[static_cast<size_t>(dev)];
-  UtilPrev& up = util_prev_[static_cast<size_t>(dev)];
   Integrals pc;
   st.pmc_integ.load(pc);
-  // The counter tier's busy integral: dispatch in flight (CP busy less our READs)
-  // when the counter set has CPC busy, else waves in a shader engine (SPI busy).
-  const double cnt_busy = pc.dispatch_drains > 0 ? pc.dispatch_seconds : pc.active_seconds;
   double slow_hz = hz_.load(std::memory_order_relaxed);
   const double idle = pmc_idle_hz_.load(std::memory_order_relaxed);
   if (idle > 0) slow_hz = std::min(slow_hz, idle);
   if ((pmc_busy_min_.load(std::memory_order_relaxed) > 0 || cfg_.pmc_cp_only_min > 0) && idle > 0)
     slow_hz = std::min(slow_hz, pmc_gap_hz_.load(std::memory_order_relaxed));
   const int64_t fresh_ns = static_cast<int64_t>(3e9 / slow_hz) + 50000000LL;
-  const bool ok = st.pmc_on.load(std::memory_order_relaxed) && !st.pmc_stalled.load(std::memory_order_relaxed) &&
-                  !st.pmc_failed.load(std::memory_order_relaxed) && pc.pmc_last_ns > 0 &&
-                  now - pc.pmc_last_ns <= fresh_ns;
-  double du = 0;
-  if (dt_s > 0) {
-    if (ok && up.have && up.epoch == pc.pmc_epoch && up.dispatch == (pc.dispatch_drains > 0) &&
-        cnt_busy >= up.active_s) {
-      du = std::min(cnt_busy - up.active_s, dt_s);
-      I.util_counter_seconds += dt_s;
-    } else {
-      du = std::clamp(dgfx_s, 0.0, dt_s);
-    }
-  }
-  I.util_seconds += du;
-  up.have = ok;
-  up.dispatch = pc.dispatch_drains > 0;
-  up.epoch = pc.pmc_epoch;
-  up.active_s = cnt_busy;
+  CounterCover c;
+  c.ok = st.pmc_on.load(std::memory_order_relaxed) && !st.pmc_stalled.load(std::memory_order_relaxed) &&
+         !st.pmc_failed.load(std::memory_order_relaxed) && pc.pmc_last_ns > 0 && now - pc.pmc_last_ns <= fresh_ns;
+  c.epoch = pc.pmc_epoch;
+  // The counter tier's busy integral: dispatch in flight (CP busy less our READs)
+  // when the counter set has CPC busy, else waves in a shader engine (SPI busy).
+  c.dispatch = pc.dispatch_drains > 0;
+  c.busy_s = c.dispatch ? pc.dispatch_seconds : pc.active_seconds;
+  c.share = pc.pmc_last_share;
+  c.since_s = (now - pc.pmc_last_ns) * 1e-9;
+  // Carry (and run the last drain on) at most one freshness window: the
+  // drain-vs-interval jitter, never a backlog.
+  const UtilBiller::Bill b = util_bill_[static_cast<size_t>(dev)].bill(dt_s, dgfx_s, c, fresh_ns * 1e-9);
+  I.util_seconds += b.billed_s;
+  if (b.from_counters) I.util_counter_seconds += dt_s;
+  I.util_carry_seconds = util_bill_[static_cast<size_t>(dev)].carry_s();
+  I.util_dropped_seconds = util_bill_[static_cast<size_t>(dev)].dropped_s();
   s.cum_util_s = I.util_seconds;
-  s.util_window_pct = dt_s > 0 ? static_cast<float>(100.0 * du / dt_s) : -1.0f;
+  s.util_window_pct = dt_s > 0 ? static_cast<float>(100.0 * b.billed_s / dt_s) : -1.0f;
 }
 
 // ---- PMFW tier: the firmware metrics table + HBM occupancy --------------------
@@ -558,54 +556,33 @@ void Sampler::run_pmc(Worker& w) {
   st.pmc_quiet.store(0, std::memory_order_relaxed);
   st.pmc_gap.store(0, std::memory_order_relaxed);
   st.pmc_dbound.store(0, std::memory_order_relaxed);
-  const int64_t gap_hold_ns = static_cast<int64_t>(cfg_.pmc_gap_hold_s * 1e9);
-  const int64_t dbound_hold_ns = static_cast<int64_t>(cfg_.pmc_dispatch_hold_s * 1e9);
+  // Everything learned from the counts (READ cost, clocks, rate hysteresis, stall
+  // watch) lives in the estimator (util_estimator.h); this thread schedules the
+  // READs and publishes.
+  EstimatorParams ep;
+  ep.quiet_active_frac = kQuietActiveFrac;
+  ep.cpc_full_frac = kCpcFullFrac;
+  ep.clock_split_ns = kClockSplitNs;
+  ep.read_overlap_ns = kReadOverlapNs;
+  ep.quiet_hold_ns = kQuietHoldNs;
+  ep.gap_hold_ns = static_cast<int64_t>(cfg_.pmc_gap_hold_s * 1e9);
+  ep.cp_only_min = cfg_.pmc_cp_only_min;
+  ep.dbound_hold_ns = static_cast<int64_t>(cfg_.pmc_dispatch_hold_s * 1e9);
+  ep.plausible_mhz_lo = kPlausibleMhzLo;
+  ep.plausible_mhz_hi = kPlausibleMhzHi;
+  ep.num_simds = (info.num_cu > 0 ? info.num_cu : 256) * 4.0;
+  DispatchEstimator est;
+  est.invalidate(mono_ns());
   int64_t next = mono_ns();
   PmcSample& pmc_base = st.pmc_base;
-  bool have_prev_ps = false;         // stall detection: previous raw GRBM_COUNT and its time
-  uint64_t prev_ps_count = 0, prev_ps_mfma = 0, prev_ps_active = 0, prev_ps_cpc = 0;
-  // ... and at the previous drain that read the per-SE counters (lite READs: the publishers)
-  bool have_prev_se = false;
-  uint64_t prev_se_count = 0, prev_se_mfma = 0;
-  int64_t prev_se_ns = 0;
-  // The READ packet's own CPC busy (clock cycles), learned on intervals without waves,
-  // separately for synchronous (quiet GPU) and pipelined READs, and for full and lite
-  // READs (a lite READ's compacted IB costs the CP less): EWMA and samples seen.
-  double read_cyc[2][2] = {};
-  double read_spi[2][2] = {};        // ... and its SPI-busy blip (cycles), learned alike
-  uint64_t read_cyc_n[2][2] = {};
-  // Shader clock while the CP is busy throughout an interval, and in READ-only ones
-  // (EWMA, Hz; 0 = none yet): a long interval that mixes a kernel with idle weighs
-  // each part by its clock (kClockSplitNs).
-  double clk_busy_hz = 0, clk_idle_hz = 0;
-  bool quiet = false;                // adaptive READ rate (SamplerConfig::pmc_idle_hz)
-  int64_t quiet_since_ns = 0;        // start of the current run of quiet READ intervals (0 = none)
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
-  bool gap = false;                  // dispatch-gap READ rate (SamplerConfig::pmc_busy_min)
-  int64_t gap_since_ns = 0;          // start of the current run of low-occupancy intervals (0 = none)
-  bool dbound = false;               // dispatch-bound READ rate (SamplerConfig::pmc_cp_only_min)
-  int64_t dbound_since_ns = 0;       // start of the current run of dispatch-bound intervals (0 = none)
   int64_t last_pmc_ns = 0;
-  int64_t prev_ps_ns = 0;
-  int64_t last_plausible_ns = mono_ns();
   int64_t last_start_ns = mono_ns();  // last (re)START of the counter session
   // A fresh START restarts every count at 0: the interval from START to the first
   // READ is then counted exactly (acquire → first READ was dropped).
   auto started_at = [&](int64_t t) {
-    have_prev_ps = true;
-    prev_ps_count = prev_ps_mfma = prev_ps_active = prev_ps_cpc = 0;
-    prev_ps_ns = t;
-    have_prev_se = true;
-    prev_se_count = prev_se_mfma = 0;
-    prev_se_ns = t;
-    quiet = false;
-    quiet_since_ns = 0;
-    gap = false;
-    gap_since_ns = 0;
-    dbound = false;
-    dbound_since_ns = 0;
+    est.restart(t);
     fresh_mode = false;  // a (re)opened session reads pipelined
-    last_plausible_ns = t;
     last_start_ns = t;
   };
   // Totals of the published stream become the base of the next session's counts.
@@ -628,8 +605,7 @@ void Sampler::run_pmc(Worker& w) {
     st.pmc_fail_streak = 0;
     st.pmc_retry_at_ns = now + static_cast<int64_t>(st.pmc_backoff_s * 1e9);
     st.pmc_backoff_s = std::min(st.pmc_backoff_s * 2, cfg_.pmc_retry_max_s);
-    have_prev_ps = false;
-    have_prev_se = false;
+    est.invalidate(now);
   };
 
   while (!stop_.load(std::memory_order_relaxed)) {
@@ -680,14 +656,14 @@ void Sampler::run_pmc(Worker& w) {
       }
     }
     bool pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
-    if (pmc_now && (quiet || gap || dbound)) {
+    if (pmc_now && (est.quiet() || est.gap() || est.dbound())) {
       // Quiet (no waves) READs at the idle rate, a dispatch gap at the gap rate;
       // profiling mode (idle rate 0) READs every tick.
       const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
-      const double slow_hz = quiet ? idle_hz : pmc_gap_hz_.load(std::memory_order_relaxed);
+      const double slow_hz = est.quiet() ? idle_hz : pmc_gap_hz_.load(std::memory_order_relaxed);
       if (idle_hz > 0 && slow_hz < hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / slow_hz)) {
         pmc_now = false;
-        (quiet ? st.pmc_quiet_skips : st.pmc_gap_skips).fetch_add(1, std::memory_order_relaxed);
+        (est.quiet() ? st.pmc_quiet_skips : st.pmc_gap_skips).fetch_add(1, std::memory_order_relaxed);
       }
     }
     if (pmc_now) {
@@ -697,7 +673,7 @@ void Sampler::run_pmc(Worker& w) {
       const int prc = src->sample(dev, ps);
       if (gone()) return;
       P.pmc_read_seconds += (mono_ns() - p0) * 1e-9;
-      if (prc == 0 && have_prev_ps && ps.mono_ns < prev_ps_ns) {
+      if (prc == 0 && est.have_prev() && ps.mono_ns < est.prev_ns()) {
         // A drain stamped before the previous one: folding it would
         // run the published totals and integrals backwards.  The counts are
         // cumulative, so the next drain covers the interval; drop this one.
@@ -708,148 +684,38 @@ void Sampler::run_pmc(Worker& w) {
           st.pmc_failed.store(0);
           st.pmc_backoff_s = cfg_.pmc_retry_s;
         }
-        // Stall detection: GRBM_COUNT free-runs at the shader clock while our
-        // session is programmed; frozen or foreign counts give no plausible clock.
-        if (have_prev_ps && ps.mono_ns > prev_ps_ns) {
-          const uint64_t raw = ps.value[kPmcGrbmCount];
-          const double mhz = raw >= prev_ps_count ? (raw - prev_ps_count) * 1e3 / (ps.mono_ns - prev_ps_ns) : 0.0;
-          if (mhz >= kPlausibleMhzLo && mhz <= kPlausibleMhzHi) last_plausible_ns = ps.mono_ns;
-        }
-        // MFMA-busy share of all SIMD-cycles since the previous drain that read the
-        // per-SE counters (every drain, unless lite READs are on), times that span.
-        if (ps.se_fresh && have_prev_se && ps.mono_ns > prev_se_ns && (ps.mask & (1u << kPmcMfmaBusy)) &&
-            ps.value[kPmcGrbmCount] > prev_se_count && ps.value[kPmcMfmaBusy] >= prev_se_mfma) {
-          const double simds = (info.num_cu > 0 ? info.num_cu : 256) * 4.0;
-          const double frac = static_cast<double>(ps.value[kPmcMfmaBusy] - prev_se_mfma) /
-                              (simds * static_cast<double>(ps.value[kPmcGrbmCount] - prev_se_count));
-          P.mfma_busy_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_se_ns) * 1e-9;
-        }
-        if (ps.se_fresh) {
-          have_prev_se = true;
-          prev_se_count = ps.value[kPmcGrbmCount];
-          prev_se_mfma = ps.value[kPmcMfmaBusy];
-          prev_se_ns = ps.mono_ns;
-        }
-        if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcGrbmActive)) &&
-            ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcGrbmActive] >= prev_ps_active) {
-          const double frac = static_cast<double>(ps.value[kPmcGrbmActive] - prev_ps_active) /
-                              static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
-          P.active_seconds += (frac > 1.0 ? 1.0 : frac) * (ps.mono_ns - prev_ps_ns) * 1e-9;
-        }
-        // Dispatch in flight (Integrals::dispatch_seconds): the CP busy share of the
-        // interval, less the READ packet's own CP time, never below the SPI share.
-        bool dbound_interval = false;
-        if (have_prev_ps && ps.mono_ns > prev_ps_ns && (ps.mask & (1u << kPmcCpcBusy)) &&
-            ps.value[kPmcGrbmCount] > prev_ps_count && ps.value[kPmcCpcBusy] >= prev_ps_cpc) {
-          const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
-          const double cpc = std::min(clk, static_cast<double>(ps.value[kPmcCpcBusy] - prev_ps_cpc));
-          const double act = (ps.mask & (1u << kPmcGrbmActive)) && ps.value[kPmcGrbmActive] >= prev_ps_active
-                                 ? static_cast<double>(ps.value[kPmcGrbmActive] - prev_ps_active)
-                                 : 0.0;
-          const int m = fresh_mode ? 1 : 0;
-          const int f = ps.se_fresh ? 1 : 0;
-          // No wave, no MFMA cycle and the CP mostly idle: the CP busy here is our READ's,
-          // and so is the SPI blip (≈0.9 µs per READ: 0.7 % of the clocks at 8 kHz, so the
-          // test is the quiet threshold, not "no SPI at all" — r4f: a 0.5 % test kept 2 %
-          // of the 8 kHz READ-only intervals, the cheap ones, and learned 13 µs for 15.5).
-          if (act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma && cpc < 0.5 * clk) {
-            const bool first = read_cyc_n[m][f] == 0;
-            read_cyc[m][f] = first ? cpc : 0.95 * read_cyc[m][f] + 0.05 * cpc;
-            read_spi[m][f] = first ? act : 0.95 * read_spi[m][f] + 0.05 * act;
-            ++read_cyc_n[m][f];
-            if (f) P.cpc_read_us = read_cyc[m][f] / (clk / ((ps.mono_ns - prev_ps_ns) * 1e-3));
-            // the idle clock between kernels, not a quiet GPU's (its clock drops: r4r)
-            if (!fresh_mode) {
-              const double hz_now = clk / ((ps.mono_ns - prev_ps_ns) * 1e-9);
-              clk_idle_hz = clk_idle_hz > 0 ? 0.95 * clk_idle_hz + 0.05 * hz_now : hz_now;
-            }
-          }
-          // This READ's learned cost, or the other kind's before it has its own.
-          const int k = read_cyc_n[m][f] ? f : 1 - f;
-          const double rcyc = read_cyc[m][k];
-          // Waves of the workload: SPI busy less the READ's own blip.
-          const double wav = std::max(0.0, act - read_spi[m][k]);
-          // An interval the CP was busy for ≥ kCpcFullFrac counts whole: under a
-          // kernel the CPC idles a few % of each 125 µs interval at 8 kHz (r4f: MFMA and
-          // GEMM intervals 0.95-1.0), and subtracting a READ-only cost there under-read
-          // a GEMM stream by 4 points.  (Counting the READ's CP time once where it
-          // overlaps dispatch busy — (cpc − read) / (1 − read/clk) — over-read 8 kHz
-          // burst trains; tools/util_estimator_sim.py replays the variants on r4f's raw
-          // READs.)
-          const double busy = cpc >= kCpcFullFrac * clk ? clk : std::max(wav, std::max(0.0, cpc - rcyc));
-          const int64_t span_ns = ps.mono_ns - prev_ps_ns;
-          double share = std::min(1.0, busy / clk);
-          if (cpc >= kCpcFullFrac * clk) {
-            const double hz_now = clk / (span_ns * 1e-9);
-            clk_busy_hz = clk_busy_hz > 0 ? 0.95 * clk_busy_hz + 0.05 * hz_now : hz_now;
-          } else if (span_ns >= kClockSplitNs && share > 0 && clk_busy_hz > 0 && clk_idle_hz > 0) {
-            // A cycle share under-weights a kernel that ran at a lower clock than the
-            // idle rest of the interval (MFMA under the power cap: ≈2.1 GHz against
-            // ≈2.4 idle): the time share is s·r / (1 − s + s·r), r = f_idle / f_busy.
-            // f_busy comes from the last fully busy intervals, whose kernels need not
-            // clock like this one (a 0.2 ms burst is not power-capped like a 1 ms one):
-            // r is kept within ±10 % (r4q: ±25 % over-read a 0.2 ms train by 2 points).
-            const double r = std::clamp(clk_idle_hz / clk_busy_hz, 0.9, 1.1);
-            share = share * r / (1.0 - share + share * r);
-          }
-          P.dispatch_seconds += share * span_ns * 1e-9;
+        ep.busy_min = pmc_busy_min_.load(std::memory_order_relaxed);
+        Drain dr;
+        dr.mono_ns = ps.mono_ns;
+        dr.mask = ps.mask;
+        dr.count = ps.value[kPmcGrbmCount];
+        dr.spi = ps.value[kPmcGrbmActive];
+        dr.mfma = ps.value[kPmcMfmaBusy];
+        dr.cpc = ps.value[kPmcCpcBusy];
+        dr.se_fresh = ps.se_fresh != 0;
+        dr.fresh_mode = fresh_mode;
+        const DrainStep r = est.feed(dr, ep);
+        P.mfma_busy_seconds += r.mfma_s;
+        P.active_seconds += r.active_s;
+        if (r.have_dispatch) {
+          P.dispatch_seconds += r.dispatch_s;
           ++P.dispatch_drains;
-          // Dispatch-bound: the CP dispatching with no wave in flight for a large share.
-          dbound_interval = cfg_.pmc_cp_only_min > 0 && busy - wav >= cfg_.pmc_cp_only_min * clk;
         }
-        // Quiet = a shader engine had waves for < kQuietActiveFrac of the clocks
-        // since the previous READ, and no MFMA cycle ran.  Both counters are
-        // (nearly) blind to our own READs: SPI busy reads 0.65 % with nothing but
-        // 8 kHz of READs on the GPU (profiles/r2/immunity/).
-        // Without the activity counter in the set a device is never quiet.
-        // A dispatch gap: the same share below pmc_busy_min (quiet intervals
-        // included, so an idle stretch between short kernels does not restart
-        // the hold).
-        bool quiet_interval = false, gap_interval = false;
-        if (have_prev_ps && (ps.mask & (1u << kPmcGrbmActive)) && ps.value[kPmcGrbmCount] > prev_ps_count) {
-          const double act = static_cast<double>(ps.value[kPmcGrbmActive] - std::min(ps.value[kPmcGrbmActive], prev_ps_active));
-          const double clk = static_cast<double>(ps.value[kPmcGrbmCount] - prev_ps_count);
-          quiet_interval = act < kQuietActiveFrac * clk && ps.value[kPmcMfmaBusy] == prev_ps_mfma;
-          const double busy_min = pmc_busy_min_.load(std::memory_order_relaxed);
-          gap_interval = busy_min > 0 && act < busy_min * clk;
-        }
-        if (!quiet_interval) {
-          quiet_since_ns = 0;
-        } else if (quiet_since_ns == 0) {
-          quiet_since_ns = prev_ps_ns;  // the interval began at the previous READ
-        }
-        quiet = quiet_interval && ps.mono_ns - quiet_since_ns >= kQuietHoldNs;
-        st.pmc_quiet.store(quiet ? 1 : 0, std::memory_order_relaxed);
-        if (!gap_interval) {
-          gap_since_ns = 0;
-        } else if (gap_since_ns == 0) {
-          gap_since_ns = prev_ps_ns;
-        }
-        gap = gap_interval && !quiet && ps.mono_ns - gap_since_ns >= gap_hold_ns;
-        st.pmc_gap.store(gap ? 1 : 0, std::memory_order_relaxed);
-        if (!dbound_interval) {
-          dbound_since_ns = 0;
-        } else if (dbound_since_ns == 0) {
-          dbound_since_ns = prev_ps_ns;
-        }
-        dbound = dbound_interval && !quiet && ps.mono_ns - dbound_since_ns >= dbound_hold_ns;
-        st.pmc_dbound.store(dbound ? 1 : 0, std::memory_order_relaxed);
+        if (r.span_s > 0) P.pmc_last_share = (r.have_dispatch ? r.dispatch_s : r.active_s) / r.span_s;
+        if (r.learned && dr.se_fresh) P.cpc_read_us = est.cpc_read_us();
+        st.pmc_quiet.store(r.quiet ? 1 : 0, std::memory_order_relaxed);
+        st.pmc_gap.store(r.gap ? 1 : 0, std::memory_order_relaxed);
+        st.pmc_dbound.store(r.dbound ? 1 : 0, std::memory_order_relaxed);
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
-          const bool slow = quiet && idle_hz > 0 && idle_hz < hz;
+          const bool slow = r.quiet && idle_hz > 0 && idle_hz < hz;
           if (slow != fresh_mode) {
             src->set_fresh(dev, slow);
             if (gone()) return;
             fresh_mode = slow;
           }
         }
-        prev_ps_count = ps.value[kPmcGrbmCount];
-        prev_ps_mfma = ps.value[kPmcMfmaBusy];
-        prev_ps_active = ps.value[kPmcGrbmActive];
-        prev_ps_cpc = ps.value[kPmcCpcBusy];
-        prev_ps_ns = ps.mono_ns;
-        have_prev_ps = true;
-        const int64_t stall = ps.mono_ns - last_plausible_ns;
+        const int64_t stall = ps.mono_ns - est.last_plausible_ns();
         st.pmc_stalled.store(stall >= kPmcStallNs ? 1 : 0, std::memory_order_relaxed);
         for (int i = 0; i < kPmcCount; ++i) ps.value[i] += pmc_base.value[i];
         if (pmc_base.n_xcd == ps.n_xcd)
@@ -887,9 +753,7 @@ void Sampler::run_pmc(Worker& w) {
             st.pmc_on.store(0);
             st.pmc_retry_at_ns = t + 1000000000LL;
             ++P.pmc_errors;
-            have_prev_ps = false;
-            have_prev_se = false;
-            last_plausible_ns = t;
+            est.invalidate(t);
             last_start_ns = t;
           }
         }

@@ -74,8 +74,9 @@ def chrome_trace(cap: dict, devices: dict | None = None) -> dict:
             ts = us(x["mono_ns"])
             ev.append({"name": "GPU active %", "ph": "C", "ts": ts, "pid": pid,
                        "args": {"active": round(x["gpu_active_pct"], 2)}})
-            ev.append({"name": "MFMA util %", "ph": "C", "ts": ts, "pid": pid,
-                       "args": {"mfma": round(x.get("mfma_util_pct", 0.0), 2)}})
+            if "mfma_util_pct" in x:  # fresh drains only (lite READs: the publishing ones)
+                ev.append({"name": "MFMA util %", "ph": "C", "ts": ts, "pid": pid,
+                           "args": {"mfma": round(x["mfma_util_pct"], 2)}})
             ev.append({"name": "shader clock MHz", "ph": "C", "ts": ts, "pid": pid,
                        "args": {"mhz": round(x.get("gpu_clock_mhz", 0.0), 1)}})
         segs, _, _ = segments(d["samples"])

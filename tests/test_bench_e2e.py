@@ -29,8 +29,8 @@ def _last_json(out: str) -> dict:
 
 
 SUMMARY_KEYS = {"value", "samples_per_sec_per_gpu", "p50_scrape_ms", "p99_scrape_ms", "scrapes", "overhead_pct",
-                "overhead_by_tier", "overhead_position_adjusted", "overhead_by_component", "overhead_by_rank",
-                "released", "delivered_by_component", "util_accuracy", "xgmi_link_map_ok", "xgmi_unit_ratio"}
+                "overhead_by_tier", "overhead_by_component", "overhead_by_component_vs_released", "overhead_by_rank",
+                "released", "delivered_by_component", "util_accuracy", "xgmi_link_map_ok", "xgmi_links_ok", "xgmi_unit_ratio"}
 
 
 def _result(out: str) -> tuple[dict, dict]:
@@ -40,7 +40,7 @@ def _result(out: str) -> tuple[dict, dict]:
     tail = out.rstrip("\n")[-3000:]
     line = json.loads(tail[tail.index("{"):]) if tail.count("\n") == 0 else _last_json(tail)
     assert len(json.dumps(line)) <= 3000, len(json.dumps(line))
-    assert list(line)[-1] == "summary" and len(json.dumps(line["summary"])) <= 1536, len(json.dumps(line["summary"]))
+    assert list(line)[-1] == "summary" and len(json.dumps(line["summary"])) <= 1800, len(json.dumps(line["summary"]))
     assert SUMMARY_KEYS <= set(line["summary"]), SUMMARY_KEYS - set(line["summary"])
     with open(os.path.join(REPO, line["full_result"])) as f:
         full = json.load(f)
@@ -60,12 +60,13 @@ def _rate_ok(v: float, hz: float) -> bool:
     return MIN_8K * hz < v <= 1.02 * hz
 
 
-FAST = ["--step-ms", "60", "--rounds", "4", "--block-steps", "1", "--settle", "0.3"]
+FAST = ["--step-ms", "60", "--rounds", "4", "--block-steps", "1", "--settle", "0.3", "--util-hz", ""]
 
 
 @pytest.mark.slow
 def test_bench_contract_single_process():
-    r = subprocess.run([sys.executable, "bench.py", "--mock", "--steps", "10", "--warmup", "1", *FAST],
+    r = subprocess.run([sys.executable, "bench.py", "--mock", "--steps", "10", "--warmup", "1", *FAST,
+                        "--util-hz", "1000,10"],
                        cwd=REPO, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     line, res = _result(r.stdout)
@@ -99,10 +100,15 @@ def test_bench_contract_single_process():
     assert set(rel) == {"paused_vs_released_pct", "paused_vs_released_ci95_pct", "100_vs_released_pct",
                         "100_vs_released_ci95_pct", "8000_vs_released_pct", "8000_vs_released_ci95_pct"}
     assert line["summary"]["released"]["paused_vs_released"][0] == pytest.approx(rel["paused_vs_released_pct"], abs=1e-3)
-    # phase U plumbing: every load at the primary rate and at 1 kHz, the
-    # exported busy counter next to the GPU-timed duty
+    # per component against "released" too
+    for hz in ("100", "8000"):
+        vr = inter["tiers"][hz]["overhead_by_component_vs_released"]
+        assert set(vr) == set(inter["tiers"][hz]["overhead_by_component"]) and line["summary"][
+            "overhead_by_component_vs_released"][hz]["mock"][0] == pytest.approx(vr["mock"]["overhead_pct"], abs=1e-3)
+    # phase U plumbing: every load at the primary rate, at 1 kHz and at
+    # the DaemonSet's 10 Hz, the exported busy counter next to the GPU-timed duty
     ua = res["util_accuracy"]
-    assert set(ua["per_rate"]) == {"8000", "1000"}
+    assert set(ua["per_rate"]) == {"8000", "1000", "10"}
     for per in ua["per_rate"].values():
         assert set(per) == {"idle", "burst_1ms_every_5ms", "burst_0.2ms_every_1ms", "mfma_saturating"}
         row = per["burst_1ms_every_5ms"]["0"]
@@ -178,8 +184,10 @@ def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads():
     x = res["xgmi_link_check"]
     assert res["xgmi_link_map_ok"] is True and x["xgmi_link_map_ok"] is True, x
     assert res["xgmi_unit_ratio"] == pytest.approx(1.0, abs=0.02) and x["xgmi_unit_ok"] is True, x
-    assert [p["peer_gpu"] for p in x["per_peer"]] == list(range(1, 8))
-    for p in x["per_peer"]:
+    assert x["xgmi_links_ok"] == [56, 56] and s["xgmi_links_ok"] == [56, 56], x["xgmi_links_ok"]
+    assert sorted((p["src_gpu"], p["peer_gpu"]) for p in x["per_copy"]) == [(i, j) for i in range(8) for j in range(8)
+                                                                            if i != j]
+    for p in x["per_copy"]:
         assert p["src"]["link_peer_bdf"] == p["peer_bdf"] and p["dst"]["ok"], p
     for hz in ("100", "2000"):
         t = res["interleaved"]["tiers"][hz]
@@ -326,6 +334,50 @@ def test_allreduce_expected_xgmi_rate():
     assert bench.allreduce_GBps(load, a, 8, 10.0) == pytest.approx(want, abs=1e-3)
     assert bench.allreduce_GBps(load, a, 1, 10.0) is None
     assert bench.allreduce_GBps(types.SimpleNamespace(reps=1), a, 8, 10.0) is None
+
+
+@pytest.mark.parametrize("swap", [-1, 5])
+def test_phase_x_checks_every_directed_link_and_names_a_wrong_one(N, swap):
+    """phase X copies between every ordered pair of an 8-GPU node (in
+    parallel rounds of disjoint pairs) and checks both ends of each copy, so all 56
+    directed link ends are validated: [56, 56] on a right map.  A mock GPU 5 whose link
+    table swaps two ports' peers fails exactly the copies over those two links, and
+    the report names GPU 5's links."""
+    import types
+
+    import bench as B
+
+    ex = N.Exporter({"backend": "mock", "mock": {"n_gpus": 8, "xgmi_swap_dev": swap}, "hz": 100, "port": 0,
+                     "node_name": "n", "pin_numa": False, "control_http": True, "link_every": 1, "proc_every": 0})
+    ex.start()
+    try:
+        time.sleep(0.5)
+        exp = B.AttachedExporter(f"127.0.0.1:{ex.port}")
+        bdfs = [d["bdf"] for d in exp.json("/devices")]
+        a = types.SimpleNamespace(xgmi_check_mib=64, mock=True, xgmi_check_settle=0.15, xgmi_check_budget_s=60)
+        out = B._xgmi_rank0(a, exp, bdfs)
+    finally:
+        ex.stop()
+    assert out["xgmi_unit_ratio_min_max"] == [1.0, 1.0]
+    if swap < 0:
+        assert out["xgmi_links_ok"] == [56, 56] and out["xgmi_link_map_ok"] and not out["bad_links"], out["bad_links"]
+    else:
+        ok, total = out["xgmi_links_ok"]
+        assert total == 56 and ok == 52 and not out["xgmi_link_map_ok"]  # 5↔peer0, 5↔peer1, both directions
+        assert all("gpu5 link 1" in b or "gpu5 link 2" in b for b in out["bad_links"]), out["bad_links"]
+        assert {(r["src_gpu"], r["peer_gpu"]) for r in out["per_copy"] if not r["ok"]} == {(0, 5), (5, 0), (1, 5), (5, 1)}
+
+
+def test_pair_rounds_cover_every_ordered_pair_once():
+    import bench as B
+
+    for n in (2, 3, 4, 7, 8):
+        rounds = B._pair_rounds(n)
+        flat = [p for r in rounds for p in r]
+        assert sorted(flat) == [(i, j) for i in range(n) for j in range(n) if i != j], n
+        for r in rounds:  # a GPU is in at most one copy per round
+            used = [g for p in r for g in p]
+            assert len(used) == len(set(used)), (n, r)
 
 
 def test_phase_x_failure_does_not_take_the_run_down(monkeypatch):

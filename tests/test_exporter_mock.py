@@ -931,3 +931,23 @@ def test_lite_reads_keep_the_mfma_integral_exact(mock_exporter):
         assert (b["active_seconds"] - a["active_seconds"]) / dt == pytest.approx(0.5, abs=0.03)
         ex.stop()
     assert rates[0] == pytest.approx(0.3, abs=0.02) and rates[8] == pytest.approx(rates[0], abs=0.02), rates
+
+
+def test_counter_stream_marks_stale_drains_and_rates_mfma_between_fresh_ones(mock_exporter):
+    """with lite READs (lite_every 8) seven of every eight drains carry
+    the last MFMA / TA values read.  /counters says which (se_fresh) and gives MFMA and
+    vmem rates only on fresh drains, measured from the previous fresh one — so their
+    per-sample mean is the load's 60 %, not a 0 / 100 sawtooth."""
+    ex = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", pmc_idle_hz=0, proc_every=0, link_every=0,
+                       mock={"util_base": 50, "util_amp": 0}, mock_pmc={"lite_every": 8})
+    time.sleep(0.4)
+    s = json.load(get(ex.port, "/counters?gpu=0&n=400"))["samples"]
+    assert len(s) == 400
+    fresh = [x for x in s if x["se_fresh"]]
+    stale = [x for x in s if not x["se_fresh"]]
+    assert 40 <= len(fresh) <= 60 and len(stale) > 300, (len(fresh), len(stale))
+    assert not any("mfma_util_pct" in x or "vmem_busy_pct" in x for x in stale)
+    assert all("gpu_active_pct" in x for x in s)  # device-wide counters: every drain
+    mf = [x["mfma_util_pct"] for x in fresh if "mfma_util_pct" in x]
+    assert len(mf) >= len(fresh) - 1  # the first one has its base: the ring is read past it
+    assert sum(mf) / len(mf) == pytest.approx(60, abs=3) and min(mf) > 40 and max(mf) < 80, mf

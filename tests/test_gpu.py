@@ -1568,6 +1568,168 @@ def test_sm_util_is_read_immune_at_khz_rates(torch_dev, tmp_path):
     assert rows["8000/burst_0.2ms_every_1ms"]["pmfw_gfx_busy_pct"] > rows["8000/burst_0.2ms_every_1ms"]["duty_gpu_pct"] + 20
 
 
+def _daemonset_exporter_args() -> list[str]:
+    """The exporter arguments of deploy/daemonset.yaml, less the deployment plumbing
+    (listen address, pod directory from the API server, pid file)."""
+    import yaml
+
+    with open(os.path.join(REPO, "deploy", "daemonset.yaml")) as f:
+        docs = [d for d in yaml.safe_load_all(f) if d]
+    ds = next(d for d in docs if d.get("kind") == "DaemonSet")
+    c = next(c for c in ds["spec"]["template"]["spec"]["containers"] if c["name"] == "exporter")
+    drop = ("--listen", "--pod-directory", "--pid-file")
+    return [a for a in c["args"] if not a.startswith(drop)]
+
+
+def _mfma_loads(ls):
+    """idle / 1 ms-every-5 ms / 0.2 ms-every-1 ms MFMA trains / saturating MFMA, each
+    returning the kernels' own event-timed GPU seconds."""
+    import torch
+
+    from kube_gpu_stats_amd.ops import load
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    load.mfma_bf16(ls.A, ls.B, ls.C, 2048, 4000)
+    e1.record()
+    torch.cuda.synchronize()
+    ms_per_iter = e0.elapsed_time(e1) / 4000
+
+    def train(secs, burst_ms, period_ms):
+        iters = max(10, int(burst_ms / ms_per_iter))
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        gpu, nxt = 0.0, time.monotonic()
+        end = nxt + secs
+        while time.monotonic() < end:
+            a.record()
+            load.mfma_bf16(ls.A, ls.B, ls.C, 2048, iters)
+            b.record()
+            b.synchronize()
+            gpu += a.elapsed_time(b) * 1e-3
+            nxt += period_ms * 1e-3
+            d = nxt - time.monotonic()
+            if d > 0:
+                time.sleep(d)
+        return gpu
+
+    def saturate(secs):
+        ev, t0 = [], time.monotonic()
+        while time.monotonic() - t0 < secs:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ls.run_mfma()
+            b.record()
+            ev.append((a, b))
+            if len(ev) >= 2:
+                ev[-2][1].synchronize()
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) * 1e-3
+
+    return {"idle": lambda s: (time.sleep(s), 0.0)[1], "burst_1ms_every_5ms": lambda s: train(s, 1.0, 5.0),
+            "burst_0.2ms_every_1ms": lambda s: train(s, 0.2, 1.0), "mfma_saturating": saturate}
+
+
+def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
+    """the configuration users get.  The exporter runs with the
+    DaemonSet's own arguments (deploy/daemonset.yaml: --hz=10 with the aqlprofile
+    counter tier) and with the same at --hz=100 (BASELINE config 4), under idle, two
+    MFMA burst trains and a saturating MFMA load.  100·rate(container_gpu_busy_seconds_total)
+    over each 6 s window — from the scrapes directly, and through a fake Prometheus fed
+    with those scrapes and `gpu-util-stats` fixed mode (the reference's per-pod mean,
+    gpu_util_stats.py:62-94 over the series of :159) — must read the kernels' event-timed
+    duty: saturated ≥ 95, idle ≤ 1, both trains within ±3 points."""
+    import threading
+
+    from fakeprom import FakeProm
+    from kube_gpu_stats_amd.ops.load import LoadStep
+    from kube_gpu_stats_amd.reports import gpu_util_stats as G
+    from kube_gpu_stats_amd.reports.promql import PromClient
+    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
+
+    shipped = _daemonset_exporter_args()
+    assert "--hz=10" in shipped and "--pmc=aqlprofile" in shipped, shipped
+    bdf = _bdf0()
+    owners = tmp_path / "owners.json"
+    owners.write_text(json.dumps({bdf: {"pod": "train-0", "namespace": "ml", "container": "main"}}))
+    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
+    ls.run_mfma()
+    loads = _mfma_loads(ls)
+    load_s, pre_s, tail_s = 6.0, 0.5, 0.5
+    rows: dict = {}
+    for tag, args in (("daemonset_10hz", shipped),
+                      ("daemonset_100hz", [a if not a.startswith("--hz=") else "--hz=100" for a in shipped])):
+        proc, ready = _exporter_proc(args + ["--node-name", "gpu-node-1", "--static-owners", str(owners),
+                                             "--pod-resources-socket", ""])
+        stop = threading.Event()
+        sc = Scraper("127.0.0.1", ready["port"])
+        sc2 = Scraper("127.0.0.1", ready["port"])
+        cur = {"fp": None}
+
+        def scraper():  # Prometheus: a scrape every 250 ms into the current load's TSDB
+            while not stop.wait(0.25):
+                f = cur["fp"]
+                if f is not None:
+                    f.ingest(parse_text(sc2.get()), time.time())
+
+        th = threading.Thread(target=scraper, daemon=True)
+        th.start()
+        try:
+            time.sleep(1.0)
+            one = lambda m, f, **kw: [v for lb, v in m.get(f, []) if all(lb.get(k) == w for k, w in kw.items())]  # noqa: E731
+            for name, run in loads.items():
+                # A saturating load is its own window (no idle around it: ≥ 95 means the
+                # whole window); idle and trains get idle edges, so the last burst's drain
+                # and PMFW table land inside the window.
+                sat = name == "mfma_saturating"
+                cur["fp"] = f = FakeProm()
+                m0, s0, w0 = parse_text(sc.get()), time.monotonic(), time.time()
+                f.ingest(m0, w0)
+                time.sleep(0.0 if sat else pre_s)
+                gpu_s = run(load_s)
+                time.sleep(0.0 if sat else tail_s)
+                m1, s1, w1 = parse_text(sc.get()), time.monotonic(), time.time()
+                cur["fp"] = None
+                f.ingest(m1, w1)
+                win = s1 - s0
+                d = lambda fam, **kw: one(m1, fam, **kw)[0] - one(m0, fam, **kw)[0]  # noqa: E731,B023
+                # the fixed report over this window: one step, rate() over it
+                furl = f.start()
+                q = G.Queries.amd("ml", int(round(win)))
+                f.add_instant(q.total, [{"metric": {"node": "gpu-node-1", q.type_label: "MI355X"}, "value": [w1, "8"]}])
+                f.add_instant(q.used, [{"metric": {"node": "gpu-node-1"}, "value": [w1, "1"]}])
+                f.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": "train-0"}, "value": [w1, "1"]}])
+                f.add_range(q.req, [{"metric": {"node": "gpu-node-1", "namespace": "ml", "pod": "train-0"},
+                                     "values": [[w1, "1"]]}])
+                rep = G.run_report(PromClient(furl), q, w1,
+                                   int(round(win)), int(round(win)), compat=False, out=open(os.devnull, "w"))
+                f.stop()
+                rows[f"{tag}/{name}"] = r = {
+                    "duty_gpu_pct": round(100 * gpu_s / win, 2),
+                    "busy_counter_pct": round(100 * d("container_gpu_busy_seconds_total") / win, 2),
+                    "report_pct": round(rep[0][4], 2) if rep else None,
+                    "pmfw_gfx_busy_pct": round(100 * d("amdgpu_pmfw_gfx_busy_seconds_total") / win, 2),
+                    "from_counters_s": round(d("kgs_util_source_seconds_total", source="counters"), 3),
+                    "dropped_s": round(one(m1, "kgs_util_dropped_seconds_total")[0], 4),
+                    "reads_per_s": round(d("kgs_pmc_samples_total") / win, 1), "window_s": round(win, 3)}
+                r["error_pts"] = round(r["busy_counter_pct"] - r["duty_gpu_pct"], 2)
+                time.sleep(0.5)
+        finally:
+            stop.set()
+            th.join(timeout=5)
+            _quit(proc)
+    _keep("shipped_config_billing.json", json.dumps({"args": shipped, "rows": rows}, indent=1))
+    print(json.dumps(rows))
+    for tag in ("daemonset_10hz", "daemonset_100hz"):
+        idle, sat = rows[f"{tag}/idle"], rows[f"{tag}/mfma_saturating"]
+        assert idle["busy_counter_pct"] <= 1.0 and idle["report_pct"] <= 1.0, idle
+        assert sat["busy_counter_pct"] >= 95.0 and sat["report_pct"] >= 95.0, sat
+        for name in ("burst_1ms_every_5ms", "burst_0.2ms_every_1ms"):
+            r = rows[f"{tag}/{name}"]
+            assert abs(r["error_pts"]) <= 3.0, (tag, name, r)
+            assert abs(r["report_pct"] - r["duty_gpu_pct"]) <= 3.0, (tag, name, r)
+            assert r["from_counters_s"] > 0.9 * r["window_s"], r
+
+
 def test_wedged_counter_queue_trips_the_breaker_and_recovers(torch_dev):
     """the counter tier's fault boundary on MI355X, once.  Under an MFMA
     load, /control/pmc/stall puts a BARRIER_AND packet that waits on a never-signalled

@@ -36,6 +36,65 @@ def test_rendered_families_match_catalog(mock_exporter):
             assert set(s.labels) <= allowed, (fam.name, set(s.labels) - allowed)
 
 
+@pytest.mark.parametrize("mode", ["auto", "counters", "pmfw"])
+def test_rendered_help_is_the_catalogue_text(N, mode):
+    """every HELP line /metrics serves is the catalogue's text for the
+    exporter's --sm-util-source mode (the renderer reads it from the header generated
+    from models/schema.py), and every family the renderer emits is in the catalogue."""
+    from kube_gpu_stats_amd.attribution.attributor import Attributor
+
+    ex = N.Exporter({"backend": "mock", "mock": {"n_gpus": 2}, "hz": 200, "port": 0, "node_name": "n",
+                     "pin_numa": False, "pmc_source": "mock", "pmc_set": "full", "proc_every": 1, "link_every": 1,
+                     "sm_util_source": mode})
+    ex.start()
+    try:
+        ex.set_device_owners(0, [{"pod": "p", "namespace": "n", "container": "c"}])
+        time.sleep(0.4)
+        Attributor(ex, socket_path=None).publish()
+        body = ex.render()
+    finally:
+        ex.stop()
+    seen = 0
+    for line in body.splitlines():
+        if line.startswith("# HELP "):
+            name, text = line[7:].split(" ", 1)
+            assert name in BY_NAME, name
+            assert text == BY_NAME[name].help_for("" if mode == "auto" else mode), name
+            seen += 1
+        elif line.startswith("# TYPE "):
+            name, typ = line[7:].split(" ", 1)
+            assert typ == BY_NAME[name].type, name
+    assert seen >= 90, seen
+
+
+def test_metric_help_header_is_generated_from_the_catalogue():
+    from kube_gpu_stats_amd.models.schema import cpp_header
+
+    path = os.path.join(REPO, "kube_gpu_stats_amd", "native", "include", "kgs", "metric_help.h")
+    assert open(path).read() == cpp_header(), "run: python -m kube_gpu_stats_amd.models.schema --cpp-header"
+    assert all("\n" not in f.help and "\\" not in f.help for f in CATALOG)
+
+
+def test_utilisation_help_names_the_shipped_estimator():
+    """The default (auto) text of the utilisation families describes what the sampler
+    computes: CP busy less the learned READ cost, floored at SPI busy, PMFW otherwise.
+    GRBM_SPI_BUSY alone is the source only of --sm-util-source counters and the
+    amdgpu_gpu_active_* families."""
+    for name in ("container_gpu_sm_util", "container_gpu_busy_seconds_total", "kgs_util_source_seconds_total",
+                 "amdgpu_dispatch_busy_seconds_total"):
+        h = BY_NAME[name].help
+        assert "CPC_CPC_STAT_BUSY" in h and "READ" in h and "GRBM_SPI_BUSY" in h, name
+    for f in CATALOG:
+        if "GRBM_SPI_BUSY" in f.help and "CPC_CPC_STAT_BUSY" not in f.help:
+            assert "active" in f.name, f.name  # amdgpu_gpu_active_*: SPI really is the source
+    for name in ("container_gpu_sm_util", "container_gpu_busy_seconds_total"):
+        assert "GRBM_SPI_BUSY" in BY_NAME[name].help_for("counters")
+        assert "PMFW" in BY_NAME[name].help_for("pmfw")
+    doc = open(os.path.join(REPO, "docs", "METRICS.md")).read()
+    from kube_gpu_stats_amd.models.schema import PREAMBLE, markdown
+    assert doc.strip() == (PREAMBLE + markdown()).strip(), "regenerate docs/METRICS.md"
+
+
 def _kgs(*args, **kw):
     return subprocess.run([sys.executable, "-m", "kube_gpu_stats_amd.cli", *args], cwd=REPO, capture_output=True,
                           text=True, timeout=120, **kw)

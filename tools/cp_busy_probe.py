@@ -35,6 +35,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 NAMES = ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:25", "CPF:23"]
+# --exporter-set 1: the exporter's base set, in this column order (4th column MFMA busy, not CPF)
+EXPORTER_NAMES = ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:25", "SQ_VALU_MFMA_BUSY_CYCLES"]
 KEYS = ["count", "spi", "cpc", "cpf"]
 
 
@@ -60,7 +62,7 @@ def child(hz: float, secs: float, pipelined: bool, batch: int = 1, lite: int = 0
         print(json.dumps({"error": "init: " + err.value.decode()}), flush=True)
         return 1
     # the exporter's base set in the dump's column order (the 4th column is then MFMA busy, not CPF)
-    names = ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:25", "SQ_VALU_MFMA_BUSY_CYCLES"] if exporter_set else NAMES
+    names = EXPORTER_NAMES if exporter_set else NAMES
     n = len(names)
     arr = (ctypes.c_char_p * n)(*[s.encode() for s in names])
     red = (ctypes.c_int * n)(*([1, 1, 1, 0] if exporter_set else [1] * n))  # max over XCCs; MFMA summed
@@ -221,7 +223,9 @@ def main(argv=None) -> int:
     if a.dump:
         os.makedirs(os.path.dirname(os.path.abspath(a.dump)), exist_ok=True)
         with open(a.dump, "w") as f:
-            json.dump({"counters": NAMES, "pipelined": a.pipelined, "rates": dumps}, f)
+            names = EXPORTER_NAMES if a.exporter_set else NAMES
+            json.dump({"counters": names, "columns": ["t_s", *names, "se_fresh"], "pipelined": a.pipelined,
+                       "batch": a.batch, "lite": a.lite, "rates": dumps}, f)
     return 0
 
 

@@ -85,6 +85,12 @@ for s in $STEPS; do
                -p no:cacheprovider -k "dispatch_bound or dispatch_gap or read_immune" ;;
     testslite) run pytest_lite 300 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
                  -p no:cacheprovider -k "lite_reads or dispatch_bound or two_tenants" ;;
+    # round 5
+    testsutil) run pytest_util 400 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread \
+                 -p no:cacheprovider -k "shipped_daemonset or read_immune or smoke_mfma or mfma_kernel" ;;
+    cpdumpall) run cp_dump_all 420 python -u tools/cp_busy_probe.py --rates 8000,1000,100,10 --pipelined 1 --batch 8 \
+                 --lite 1 --exporter-set 1 --secs 4 --out "$OUT/cp_busy_all.json" --dump "$OUT/cp_dump_all.json" \
+                 --dump-rates 8000,1000,100,10 ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;

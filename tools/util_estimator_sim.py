@@ -1,115 +1,92 @@
 #!/usr/bin/env python3
-"""Replay raw counter READs through busy-estimator variants (offline, CPU).
+"""Replay raw counter READs through the sampler's own dispatch estimator (offline, CPU).
 
 Input: ``tools/cp_busy_probe.py --dump`` output — every READ of [GRBM_COUNT,
-GRBM_SPI_BUSY, CPC busy, CPF busy] (max over XCCs) during known loads, with the
-loads' event-timed GPU busy.  Each variant turns the READ intervals into a busy
-integral the way the sampler's dispatch integral does (``sampler.cpp``, the
-``dispatch_seconds`` block) and is scored against the kernels' own duty:
+GRBM_SPI_BUSY, CPC busy, ...] (max over XCCs) during known loads, with the loads'
+event-timed GPU busy (``duty_gpu_s``).  Each load is folded READ by READ through
+``_kgs_native.DispatchEstimator`` — the C++ class ``Sampler::run_pmc`` itself runs
+(``native/include/kgs/util_estimator.h``), with the parameters of the default
+``SamplerConfig`` (``_kgs_native.sampler_estimator_params``) — after the same rate's
+idle READs have taught it the READ packet's cost, as the running sampler learns it on
+the READ-only intervals between kernels.  There is no second model of the estimator
+here: a change to the C++ class changes these numbers (tests/test_estimator_replay.py).
 
-* ``shipped``  — the sampler from r4g: the whole interval if CPC busy ≥ 90 % of the
-  clocks, else max(SPI − the READ's SPI blip, CPC − the READ's CP cost), share × Δt;
-  both READ costs learned on every READ-only interval (SPI < 2 % of the clocks); from
-  r4q a partial interval ≥ 400 µs long is split by the learned busy / idle clocks
-  (share s → s·r / (1 − s + s·r), r = f_idle / f_busy);
-* ``r4b``      — the same with a 97 % full threshold, no SPI-blip removal, and the READ
-  cost learned only where SPI < 0.5 % of the clocks (rounds r4b–r4f: at 8 kHz that kept
-  2 % of the READ-only intervals, the cheap ones);
-* ``overlap``  — ``shipped``, but the READ's CP time counted once where it overlaps
-  dispatch busy: busy = (CPC − r) / (1 − r/clk);
-* ``timesplit``— ``shipped``, but busy time = Δt − idle cycles / idle clock, with the
-  idle clock learned on READ-only intervals (cycle shares are clock-weighted: a burst
-  under the power cap runs at a lower clock than the idle stretch around it).
-
-``python tools/util_estimator_sim.py profiles/r4/r4e/cp_dump.json``
+``python tools/util_estimator_sim.py profiles/r4/r4f/cp_dump.json [--set cpc_full_frac=0.97]``
 """
 from __future__ import annotations
 
+import argparse
 import json
+import os
 import sys
 
-FULL = 0.90
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# Dump timestamps are seconds relative to each load's start (the first READs come a
+# few ms before it): shift them onto a positive clock.
+T_OFFSET_S = 10.0
 
 
-def intervals(samples):
-    for a, b in zip(samples, samples[1:]):
-        dt = b[0] - a[0]
-        clk = b[1] - a[1]
-        if dt <= 0 or clk <= 0:
+def rows_of(load: dict, mfma_col: int | None = None, fresh_col: int | None = None) -> list[list[float]]:
+    """[t_s, count, spi, cpc, mfma (-1: not in the set), se_fresh] per READ."""
+    out = []
+    for s in load["samples"]:
+        out.append([s[0] + T_OFFSET_S, s[1], s[2], s[3], s[mfma_col] if mfma_col is not None else -1,
+                    s[fresh_col] if fresh_col is not None and fresh_col < len(s) else 1])
+    return out
+
+
+def replay_rate(N, loads: dict, params, mfma_col: int | None = None, fresh_col: int | None = None) -> dict:
+    """Per load of one READ rate: the estimator's busy % of the load's wall time next to
+    the event-timed duty, warmed on that rate's idle READs."""
+    idle = rows_of(loads.get("idle", {"samples": []}), mfma_col, fresh_col)
+    out = {}
+    warm = N.DispatchEstimator()
+    if idle:
+        warm.replay(params, idle)
+    out["read_us"] = round(warm.cpc_read_us, 2)
+    out["idle_clock_mhz"] = round(warm.clk_idle_hz / 1e6, 1)
+    for name, L in loads.items():
+        rows = rows_of(L, mfma_col, fresh_col)
+        if len(rows) < 2:
             continue
-        yield dt, clk, max(0, b[2] - a[2]), max(0, b[3] - a[3])
+        est = N.DispatchEstimator()
+        if name != "idle" and idle:
+            est.replay(params, idle)         # learn the READ cost first ...
+            est.invalidate(int(rows[0][0] * 1e9))  # ... then baseline on the load's first READ
+        r = est.replay(params, rows)
+        wall = L["t1"] - L["t0"]
+        out[name] = {"duty_gpu_pct": round(100 * L["duty_gpu_s"] / wall, 2),
+                     "busy_pct": round(100 * r["dispatch_s"] / wall, 2),
+                     "err_pts": round(100 * (r["dispatch_s"] - L["duty_gpu_s"]) / wall, 2),
+                     "active_pct": round(100 * r["active_s"] / wall, 2),
+                     "reads": len(rows)}
+    return out
 
 
-QUIET_SPI = 0.02  # the sampler's kQuietActiveFrac: a READ alone shows ≈0.9 µs of SPI busy
+def replay(path: str, overrides: dict | None = None) -> dict:
+    from kube_gpu_stats_amd import load_native
 
-
-def learn_read(ivs, quiet_spi: float = QUIET_SPI) -> tuple[float, float, float]:
-    """READ cost in CPC cycles and in SPI cycles (means over intervals without waves
-    and with the CP mostly idle) and the idle clock (cycles / s over the same)."""
-    cyc, spi_c, clk_s, n = 0.0, 0.0, 0.0, 0
-    for dt, clk, spi, cpc in ivs:
-        if spi < quiet_spi * clk and cpc < 0.5 * clk:
-            cyc += cpc
-            spi_c += spi
-            clk_s += clk / dt
-            n += 1
-    return (cyc / n, spi_c / n, clk_s / n) if n else (0.0, 0.0, 0.0)
-
-
-def estimate(ivs, learned, variant: str) -> float:
-    read_cyc, read_spi, idle_hz = learned
-    full = 0.97 if variant == "r4b" else FULL
-    if variant == "r4b":
-        read_spi = 0.0
-    tot, span = 0.0, 0.0
-    f_busy, f_idle = 0.0, 0.0
-    for dt, clk, spi, cpc in ivs:
-        span += dt
-        wav = max(0.0, spi - read_spi)  # the READ's own SPI blip is not a wave of the workload
-        if spi < QUIET_SPI * clk and cpc < 0.5 * clk:
-            f_idle = 0.95 * f_idle + 0.05 * clk / dt if f_idle else clk / dt
-        if cpc >= full * clk:
-            f_busy = 0.95 * f_busy + 0.05 * clk / dt if f_busy else clk / dt
-            tot += dt
-            continue
-        if variant == "overlap":
-            r = min(read_cyc, 0.5 * clk)
-            busy = max(wav, max(0.0, (cpc - r) / (1.0 - r / clk)))
-        else:
-            busy = max(wav, max(0.0, cpc - read_cyc))
-        if variant == "timesplit" and idle_hz > 0:
-            tot += min(dt, max(0.0, dt - (clk - busy) / idle_hz))
-        else:
-            s = min(1.0, busy / clk)
-            if variant == "shipped" and dt >= 400e-6 and s > 0 and f_busy and f_idle:
-                r = min(1.1, max(0.9, f_idle / f_busy))
-                s = s * r / (1.0 - s + s * r)
-            tot += s * dt
-    return 100.0 * tot / span if span else 0.0
+    N = load_native()
+    d = json.load(open(path))
+    p = N.sampler_estimator_params()
+    for k, v in (overrides or {}).items():
+        setattr(p, k, type(getattr(p, k))(v))
+    names = d.get("counters", [])
+    mfma_col = 1 + names.index("SQ_VALU_MFMA_BUSY_CYCLES") if "SQ_VALU_MFMA_BUSY_CYCLES" in names else None
+    cols = d.get("columns") or []
+    fresh_col = cols.index("se_fresh") if "se_fresh" in cols else None
+    return {rate: replay_rate(N, loads, p, mfma_col, fresh_col) for rate, loads in d["rates"].items()}
 
 
 def main(argv=None) -> int:
-    path = (argv or sys.argv[1:])[0]
-    d = json.load(open(path))
-    out = {}
-    for rate, loads in d["rates"].items():
-        quiet = list(intervals(loads.get("idle", {}).get("samples", [])))
-        learned = {"r4b": learn_read(quiet, 0.005), "shipped": learn_read(quiet)}
-        rows = {f"read_us_{k}": round(1e6 * v[0] / v[2], 2) if v[2] else None for k, v in learned.items()}
-        rows["read_spi_us"] = round(1e6 * learned["shipped"][1] / learned["shipped"][2], 3) if learned["shipped"][2] else None
-        rows["idle_clock_mhz"] = round(learned["shipped"][2] / 1e6, 1)
-        for name, L in loads.items():
-            ivs = list(intervals(L["samples"]))
-            if not ivs:
-                continue
-            wall = L["t1"] - L["t0"]
-            row = {"duty_gpu_pct": round(100 * L["duty_gpu_s"] / wall, 2),
-                   "busy_clock_mhz": round(sum(c for _, c, _, _ in ivs) / sum(t for t, _, _, _ in ivs) / 1e6, 1)}
-            for v in ("shipped", "r4b", "overlap", "timesplit"):
-                row[v] = round(estimate(ivs, learned["r4b" if v == "r4b" else "shipped"], v), 2)
-            rows[name] = row
-        out[rate] = rows
-    print(json.dumps(out, indent=1))
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("dump")
+    ap.add_argument("--set", action="append", default=[], metavar="PARAM=VALUE",
+                    help="override one EstimatorParams field (e.g. cpc_full_frac=0.97)")
+    a = ap.parse_args(argv)
+    ov = dict(kv.split("=", 1) for kv in a.set)
+    print(json.dumps(replay(a.dump, ov), indent=1))
     return 0
 
 
