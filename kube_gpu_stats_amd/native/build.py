@@ -173,18 +173,30 @@ def build_load(force: bool = False, verbose: bool = False) -> str:
 
 def build_tsan_test(verbose: bool = False, sanitizer: str = "thread") -> str:
     """Host-only test of the seqlock / ring / sampler under a sanitizer
-    (``thread``, or ``address,undefined``)."""
+    (``thread``, or ``address,undefined``).  Objects compile in parallel."""
     tag = "tsan" if sanitizer == "thread" else "asan"
     out = os.path.join(HERE, "build", f"test_core_{tag}")
     srcs = [os.path.join(HERE, "tests", "test_core.cpp")] + [
         os.path.join(HERE, "src", f) for f in ("sampler.cpp", "backend_mock.cpp", "pmc.cpp", "gpu_metrics.cpp", "util.cpp",
                                               "exporter.cpp", "render.cpp", "http.cpp", "backend_amdsmi.cpp")]
-    os.makedirs(os.path.dirname(out), exist_ok=True)
+    objdir = os.path.join(HERE, "build", f"obj_{tag}")
+    os.makedirs(objdir, exist_ok=True)
+    metric_help_header()
+    flags = ["-std=c++17", "-O1", "-g", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-pthread"]
     if _stale(out, srcs + _headers() + [__file__]):
-        _run(["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-pthread",
-              "-I" + os.path.join(HERE, "include"), "-I" + os.path.join(ROCM, "include"), *srcs, "-o", out,
-              "-L" + os.path.join(ROCM, "lib"), "-lamd_smi", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl", "-lz"],
-             verbose)
+        def compile_one(src: str) -> str:
+            obj = os.path.join(objdir, os.path.basename(src) + ".o")
+            if _stale(obj, [src] + _headers() + [__file__]):
+                _run(["g++", *flags, "-I" + os.path.join(HERE, "include"), "-I" + os.path.join(ROCM, "include"),
+                      "-c", src, "-o", obj], verbose)
+            return obj
+
+        with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+            objs = list(ex.map(compile_one, srcs))
+        tmp = f"{out}.{os.getpid()}.tmp"
+        _run(["g++", *flags, *objs, "-o", tmp, "-L" + os.path.join(ROCM, "lib"), "-lamd_smi",
+              "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-ldl", "-lz"], verbose)
+        os.replace(tmp, out)
     return out
 
 

@@ -107,6 +107,9 @@ const BlockNameId kBlocks[] = {
     {"TCC", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC},   {"TCP", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCP},
     {"SPI", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI},   {"CPC", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPC},
     {"CPF", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_CPF},   {"GRBMSE", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBMSE},
+    // memory-side blocks, probed for a counter-tier HBM bandwidth (tools/aql_probe.py umc_* / mmea / gcea)
+    {"UMC", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_UMC},   {"MMEA", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_MMEA},
+    {"GCEA", HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GCEA},
 };
 
 constexpr int kMaxBatch = kgs::BatchPlan::kMaxBatch;
@@ -1005,15 +1008,21 @@ bool make_lite(Agent* a, int k, uint32_t cmd_sz) {
   // (SQ / TA / TD / TCP): every dropped result must be one of theirs.  A
   // session counter of another SE-indexed block (SPI, GRBMSE, ...) would have its
   // per-SE copies dropped too and then be read from dwords the lite IB never writes.
-  // The IB has the same number of copies per event; the dropped ones must be exactly
-  // that many per event of a per_se counter.
-  size_t se_events = 0;
-  for (int ck : a->ev_counter) se_events += static_cast<size_t>(ck) < a->per_se.size() && a->per_se[ck];
-  const size_t total = c.kept_copies + c.dropped_copies, n_ev = a->events.size();
-  if (n_ev == 0 || total % n_ev != 0 || c.dropped_copies != total / n_ev * se_events) {
-    return why("dropped " + std::to_string(c.dropped_copies) + " of " + std::to_string(total) +
-               " results, not those of the " + std::to_string(se_events) + " per-SE events of " +
-               std::to_string(n_ev));
+  // The output buffer holds the results in fold order, each `m` 32-bit copies (LO,
+  // HI); the open READ's fold recorded each result ordinal's counter (res_slot), so
+  // every dropped destination maps to the counter it belongs to.
+  const size_t n_res = a->res_slot.size(), copies = c.kept_copies + c.dropped_copies;
+  if (!a->res_xcd_done || n_res == 0 || copies % n_res != 0) {
+    return why("cannot map " + std::to_string(copies) + " result copies onto " + std::to_string(n_res) + " results");
+  }
+  const uint64_t base = reinterpret_cast<uint64_t>(a->pout[k]), stride = 4 * (copies / n_res);
+  for (uint64_t dst : c.dropped_dsts) {
+    const uint64_t ord = dst >= base ? (dst - base) / stride : n_res;
+    const int ck = ord < n_res ? a->res_slot[ord].first : -1;
+    if (ck < 0 || static_cast<size_t>(ck) >= a->per_se.size() || !a->per_se[static_cast<size_t>(ck)]) {
+      return why("a dropped result (ordinal " + std::to_string(ord) + ") is not a per-SE counter's" +
+                 (ck >= 0 && static_cast<size_t>(ck) < a->names.size() ? ": " + a->names[static_cast<size_t>(ck)] : ""));
+    }
   }
   // the compacted IB only (≈1.5 KB for the base set), not a whole command buffer
   const uint32_t need = static_cast<uint32_t>((out.size() * 4 + 4095) & ~size_t{4095});

@@ -164,6 +164,13 @@ constexpr int64_t kClockSplitNs = 400000;
 // intervals are shorter than this and the rule never applies (there it over-read
 // 0.2 ms trains, tools/util_estimator_sim.py).
 constexpr int64_t kReadOverlapNs = 400000;
+// ... and is split in time rather than cycles: idle time = its cycles at the learned
+// idle clock, busy time = the rest.  A cycle share under-weights power-capped kernels
+// (1 ms MFMA bursts at ≈2.1 GHz between ≈2.4 GHz gaps), and a low READ rate may never
+// see the fully busy interval the clock-ratio split needs: in the r5b raw READs (the
+// exporter's READ mode) the 1 ms / 5 ms train read −2.2 / −2.7 / −2.6 points at 1 kHz /
+// 100 Hz / 10 Hz with the clock-ratio split, −0.5 / +1.4 / +1.5 with this.
+constexpr int64_t kTimeSplitNs = 400000;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };

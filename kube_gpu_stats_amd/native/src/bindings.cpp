@@ -470,6 +470,7 @@ EstimatorParams sampler_estimator_params(int num_cu) {
   p.cpc_full_frac = kCpcFullFrac;
   p.clock_split_ns = kClockSplitNs;
   p.read_overlap_ns = kReadOverlapNs;
+  p.time_split_ns = kTimeSplitNs;
   p.quiet_hold_ns = kQuietHoldNs;
   p.busy_min = c.pmc_busy_min;
   p.gap_hold_ns = static_cast<int64_t>(c.pmc_gap_hold_s * 1e9);

@@ -564,6 +564,7 @@ void Sampler::run_pmc(Worker& w) {
   ep.cpc_full_frac = kCpcFullFrac;
   ep.clock_split_ns = kClockSplitNs;
   ep.read_overlap_ns = kReadOverlapNs;
+  ep.time_split_ns = kTimeSplitNs;
   ep.quiet_hold_ns = kQuietHoldNs;
   ep.gap_hold_ns = static_cast<int64_t>(cfg_.pmc_gap_hold_s * 1e9);
   ep.cp_only_min = cfg_.pmc_cp_only_min;

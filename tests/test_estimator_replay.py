@@ -41,13 +41,33 @@ def test_dump_replays_within_one_point_of_the_kernels_duty(shipped):
         assert rows["tiny_graph"]["active_pct"] < 50 and rows["tiny_graph"]["busy_pct"] > 99, rows["tiny_graph"]
 
 
+LOWRATE = os.path.join(REPO, "profiles", "r5", "r5b_cp_dump_lowrate.json")
+
+
 def test_one_khz_bursts_read_the_reads_cp_time_once(shipped):
     """a READ that lands inside a kernel adds no CP busy; subtracting its
-    cost whole from a 1 ms interval under-read the 1 kHz trains (−0.29 / −0.81)."""
+    cost whole from a 1 ms interval under-read the 1 kHz trains."""
     for load in ("burst_1_5", "burst_02_1"):
-        assert shipped["1000"][load]["err_pts"] > -0.6, shipped["1000"][load]
+        assert abs(shipped["1000"][load]["err_pts"]) < 0.8, shipped["1000"][load]
     old = sim.replay(DUMP, {"read_overlap_ns": 0})
     assert old["1000"]["burst_02_1"]["err_pts"] < shipped["1000"]["burst_02_1"]["err_pts"] - 0.2
+
+
+def test_low_rate_reads_in_the_exporters_read_mode_stay_within_two_points():
+    """The exporter's own READ mode (batched, lite, its counter set) recorded on MI355X at
+    1 kHz, 100 Hz and the DaemonSet's 10 Hz (r5b).  Long READ intervals mix power-capped
+    MFMA bursts (≈2.1 GHz) with faster idle gaps: a cycle share under-reads the 1 ms / 5 ms
+    train by 2.2-2.7 points, and at 10 Hz no fully busy interval ever teaches the busy
+    clock the old clock-ratio split needs.  The time split (idle cycles at the learned idle
+    clock, sampler.h kTimeSplitNs) reads every load within 2 points at every rate."""
+    now = sim.replay(LOWRATE)
+    for rate in ("1000", "100", "10"):
+        for load in ("idle", "mfma", "triad", "gemm", "tiny_graph", "burst_1_5", "burst_02_1"):
+            assert abs(now[rate][load]["err_pts"]) <= 2.0, (rate, load, now[rate][load])
+    old = sim.replay(LOWRATE, {"time_split_ns": 0})
+    for rate in ("1000", "100", "10"):
+        assert old[rate]["burst_1_5"]["err_pts"] < -2.0, (rate, old[rate]["burst_1_5"])
+        assert abs(now[rate]["burst_1_5"]["err_pts"]) < abs(old[rate]["burst_1_5"]["err_pts"]) - 0.5
 
 
 @pytest.mark.parametrize("override, load, rate", [
@@ -64,7 +84,7 @@ def test_replay_is_the_samplers_code(N):
     parameters are the sampler's."""
     p = N.sampler_estimator_params()
     assert p.cpc_full_frac == pytest.approx(0.90) and p.quiet_active_frac == pytest.approx(0.02)
-    assert p.read_overlap_ns == 400000 and p.clock_split_ns == 400000
+    assert p.read_overlap_ns == 400000 and p.clock_split_ns == 400000 and p.time_split_ns == 400000
     assert p.cp_only_min == pytest.approx(0.3) and p.num_simds == 1024
     src = open(os.path.join(REPO, "tools", "util_estimator_sim.py")).read()
     assert "DispatchEstimator" in src and "0.95 *" not in src  # no re-implemented EWMA
@@ -192,11 +212,12 @@ def test_biller_falls_back_to_pmfw_and_drops_the_carry_on_an_epoch_change(N):
 
 
 def test_committed_replay_summary_matches(shipped):
-    """profiles/r5/estimator_replay.json is this replay's output, committed: the numbers
+    """profiles/r5/estimator_replay*.json are this replay's output, committed: the numbers
     README / BASELINE cite are the current code's."""
-    path = os.path.join(REPO, "profiles", "r5", "estimator_replay.json")
-    rec = json.load(open(path))
-    for rate, rows in rec.items():
-        for load, r in rows.items():
-            if isinstance(r, dict):
-                assert shipped[rate][load]["err_pts"] == pytest.approx(r["err_pts"], abs=0.02), (rate, load)
+    for path, res in ((os.path.join(REPO, "profiles", "r5", "estimator_replay.json"), shipped),
+                      (os.path.join(REPO, "profiles", "r5", "estimator_replay_lowrate.json"), sim.replay(LOWRATE))):
+        rec = json.load(open(path))
+        for rate, rows in rec.items():
+            for load, r in rows.items():
+                if isinstance(r, dict):
+                    assert res[rate][load]["err_pts"] == pytest.approx(r["err_pts"], abs=0.02), (path, rate, load)

@@ -38,6 +38,14 @@ SETS = {
     "cpc_gd": ["GRBM_COUNT", "GRBM_SPI_BUSY", "CPC:61", "CPC:33"],
     "grbm_cp": ["GRBM:3", "GRBM:30"],
     "spi_csn": ["GRBM_COUNT", "GRBM_SPI_BUSY", "SPI:49", "SPI:52"],
+    # Round 5: a counter-tier HBM bandwidth (BASELINE config 4)?  TCC's DRAM request
+    # counters need per-dispatch perf enables other processes' kernels lack; the memory
+    # controllers' own blocks, if aqlprofile programs them on gfx950, would not.  No
+    # event list ships for them (counter_defs.yaml has none for gfx950): try the low ids.
+    "umc_a": ["GRBM_COUNT", "GRBM_SPI_BUSY", "UMC:0", "UMC:1", "UMC:2", "UMC:3"],
+    "umc_b": ["GRBM_COUNT", "GRBM_SPI_BUSY", "UMC:4", "UMC:5", "UMC:6", "UMC:7"],
+    "mmea": ["GRBM_COUNT", "GRBM_SPI_BUSY", "MMEA:0", "MMEA:1", "MMEA:2", "MMEA:3"],
+    "gcea": ["GRBM_COUNT", "GRBM_SPI_BUSY", "GCEA:0", "GCEA:1", "GCEA:2", "GCEA:3"],
 }
 
 

@@ -87,7 +87,7 @@ for s in $STEPS; do
                  -p no:cacheprovider -k "lite_reads or dispatch_bound or two_tenants" ;;
     # round 5
     testsutil) run pytest_util 400 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread \
-                 -p no:cacheprovider -k "shipped_daemonset or read_immune or smoke_mfma or mfma_kernel" ;;
+                 -p no:cacheprovider -k "shipped_daemonset or read_immune or lite_reads or mfma_kernel" ;;
     cpdumpall) run cp_dump_all 420 python -u tools/cp_busy_probe.py --rates 8000,1000,100,10 --pipelined 1 --batch 8 \
                  --lite 1 --exporter-set 1 --secs 4 --out "$OUT/cp_busy_all.json" --dump "$OUT/cp_dump_all.json" \
                  --dump-rates 8000,1000,100,10 ;;

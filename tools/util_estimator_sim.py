@@ -27,10 +27,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 T_OFFSET_S = 10.0
 
 
-def rows_of(load: dict, mfma_col: int | None = None, fresh_col: int | None = None) -> list[list[float]]:
-    """[t_s, count, spi, cpc, mfma (-1: not in the set), se_fresh] per READ."""
+def rows_of(load: dict, mfma_col: int | None = None, fresh_col: int | None = None,
+            inside: bool = False) -> list[list[float]]:
+    """[t_s, count, spi, cpc, mfma (-1: not in the set), se_fresh] per READ; ``inside``:
+    only the READs taken while the load ran (its intervals lie wholly inside it)."""
     out = []
+    wall = load.get("t1", 0.0) - load.get("t0", 0.0)
     for s in load["samples"]:
+        if inside and not 0.0 <= s[0] <= wall:
+            continue
         out.append([s[0] + T_OFFSET_S, s[1], s[2], s[3], s[mfma_col] if mfma_col is not None else -1,
                     s[fresh_col] if fresh_col is not None and fresh_col < len(s) else 1])
     return out
@@ -47,8 +52,8 @@ def replay_rate(N, loads: dict, params, mfma_col: int | None = None, fresh_col: 
     out["read_us"] = round(warm.cpc_read_us, 2)
     out["idle_clock_mhz"] = round(warm.clk_idle_hz / 1e6, 1)
     for name, L in loads.items():
-        rows = rows_of(L, mfma_col, fresh_col)
-        if len(rows) < 2:
+        rows = rows_of(L, mfma_col, fresh_col, inside=True)
+        if len(rows) < 3:
             continue
         est = N.DispatchEstimator()
         if name != "idle" and idle:
@@ -56,10 +61,12 @@ def replay_rate(N, loads: dict, params, mfma_col: int | None = None, fresh_col: 
             est.invalidate(int(rows[0][0] * 1e9))  # ... then baseline on the load's first READ
         r = est.replay(params, rows)
         wall = L["t1"] - L["t0"]
-        out[name] = {"duty_gpu_pct": round(100 * L["duty_gpu_s"] / wall, 2),
-                     "busy_pct": round(100 * r["dispatch_s"] / wall, 2),
-                     "err_pts": round(100 * (r["dispatch_s"] - L["duty_gpu_s"]) / wall, 2),
-                     "active_pct": round(100 * r["active_s"] / wall, 2),
+        # Busy as a share of the READ intervals inside the load (at 10 Hz the first and
+        # last READ sit up to a period inside it), against the kernels' duty over the load.
+        duty = 100 * L["duty_gpu_s"] / wall
+        busy = 100 * r["dispatch_s"] / r["span_s"] if r["span_s"] > 0 else 0.0
+        out[name] = {"duty_gpu_pct": round(duty, 2), "busy_pct": round(busy, 2), "err_pts": round(busy - duty, 2),
+                     "active_pct": round(100 * r["active_s"] / r["span_s"], 2) if r["span_s"] > 0 else 0.0,
                      "reads": len(rows)}
     return out
 
