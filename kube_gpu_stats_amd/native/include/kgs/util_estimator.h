@@ -45,6 +45,7 @@ struct EstimatorParams {
   // clock needed, which a low READ rate may never see in a fully busy interval
   // (0 = never; the clock-ratio split above applies instead).
   int64_t time_split_ns = 0;
+  double time_split_ratio_hi = 1.5;   // ... within f_idle / f_busy ≤ this (busy clock ≥ 0.67 × idle)
   double ewma = 0.05;                 // weight of a new sample in every learned EWMA
   int64_t quiet_hold_ns = 5000000;    // quiet intervals in a row before the device counts as quiet
   double busy_min = 0.0;              // dispatch gap: SPI share below this (0 = off)
@@ -188,8 +189,13 @@ class DispatchEstimator {
         // A long interval at a low READ rate: many kernels and gaps, each part at its
         // own clock (MFMA bursts power-capped at ≈2.1 GHz, gaps at ≈2.4).  The idle
         // part's time is its cycles at the idle clock; the busy part is the rest.
+        // Bounded to busy clocks between f_idle / time_split_ratio_hi and f_idle /
+        // clock_ratio_lo: an idle stretch that clocked below the learned idle clock
+        // (a GPU left quiet long enough to drop its clock) must not read as busy.
         const double idle_s = std::max(0.0, clk - busy) / clk_idle_hz_;
-        share = std::clamp(1.0 - idle_s / (span_ns * 1e-9), 0.0, 1.0);
+        const double t = 1.0 - idle_s / (span_ns * 1e-9);
+        auto time_share = [share](double r) { return share * r / (1.0 - share + share * r); };
+        share = std::clamp(t, time_share(p.clock_ratio_lo), time_share(p.time_split_ratio_hi));
       } else if (span_ns >= p.clock_split_ns && share > 0 && clk_busy_hz_ > 0 && clk_idle_hz_ > 0) {
         // A cycle share under-weights a kernel that ran at a lower clock than the idle
         // rest of the interval (MFMA under the power cap: ≈2.1 GHz against ≈2.4 idle):

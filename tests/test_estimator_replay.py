@@ -221,3 +221,29 @@ def test_committed_replay_summary_matches(shipped):
             for load, r in rows.items():
                 if isinstance(r, dict):
                     assert res[rate][load]["err_pts"] == pytest.approx(r["err_pts"], abs=0.02), (path, rate, load)
+
+
+def test_time_split_never_bills_a_deep_idle_stretch_as_busy(N):
+    """A 10 ms interval (the 100 Hz tier) with one 50 µs kernel, its idle rest at 1.5 GHz
+    — a GPU left quiet long enough to drop below the 2.4 GHz idle clock it learned
+    between kernels.  The time split alone would call 37 % of the interval busy (its
+    idle cycles at 2.4 GHz fill only 63 % of it); bounded to busy clocks ≥ 0.67 × the
+    idle clock it stays within 1 point of the kernel's 0.5 %."""
+    p = N.sampler_estimator_params()
+    e = N.DispatchEstimator()
+    e.restart(0)
+    t, cnt, cpc, spi = 0, 0, 0, 0
+    for _ in range(20):  # READ-only intervals between kernels teach the 2.4 GHz idle clock
+        t += 10_000_000
+        cnt += int(10_000_000 * 2.4)
+        cpc += int(16_000 * 2.4)
+        spi += 2000
+        e.feed(p, t, cnt, spi, cpc, mfma=0)
+    assert e.clk_idle_hz == pytest.approx(2.4e9, rel=0.01)
+    busy_cyc = int(50_000 * 2.1)
+    t += 10_000_000
+    cnt += busy_cyc + int((10_000_000 - 50_000) * 1.5)
+    cpc += busy_cyc + int(16_000 * 1.5)
+    spi += busy_cyc
+    s = e.feed(p, t, cnt, spi, cpc, mfma=10**6)
+    assert s.dispatch_s / 0.010 < 0.015, s.dispatch_s

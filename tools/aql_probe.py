@@ -46,6 +46,8 @@ SETS = {
     "umc_b": ["GRBM_COUNT", "GRBM_SPI_BUSY", "UMC:4", "UMC:5", "UMC:6", "UMC:7"],
     "mmea": ["GRBM_COUNT", "GRBM_SPI_BUSY", "MMEA:0", "MMEA:1", "MMEA:2", "MMEA:3"],
     "gcea": ["GRBM_COUNT", "GRBM_SPI_BUSY", "GCEA:0", "GCEA:1", "GCEA:2", "GCEA:3"],
+    # r5d: UMC and MMEA validate no event on gfx950; GCEA takes two counters per session
+    **{f"gcea{i}": ["GRBM_COUNT", "GRBM_SPI_BUSY", f"GCEA:{2 * i}", f"GCEA:{2 * i + 1}"] for i in range(8)},
 }
 
 

@@ -91,6 +91,10 @@ for s in $STEPS; do
     cpdumpall) run cp_dump_all 420 python -u tools/cp_busy_probe.py --rates 8000,1000,100,10 --pipelined 1 --batch 8 \
                  --lite 1 --exporter-set 1 --secs 4 --out "$OUT/cp_busy_all.json" --dump "$OUT/cp_dump_all.json" \
                  --dump-rates 8000,1000,100,10 ;;
+    umcprobe) KGS_AQL_PROBE_OUT="$OUT/aql_probe_mem.json" run aql_probe_mem 300 python -u tools/aql_probe.py \
+                umc_a,umc_b,mmea,gcea ;;
+    gceaprobe) KGS_AQL_PROBE_OUT="$OUT/aql_probe_gcea.json" run aql_probe_gcea 400 python -u tools/aql_probe.py \
+                gcea0,gcea1,gcea2,gcea3,gcea4,gcea5,gcea6,gcea7 ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
