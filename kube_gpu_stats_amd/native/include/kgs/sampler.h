@@ -385,6 +385,10 @@ class Sampler {
   int stop_fd_ = -1;  // eventfd: readable once stop() was called; sampler threads ppoll() on it
 };
 
+// The estimator parameters a sampler with this config runs its counter tier with (the
+// offline replay binds the same function: _kgs_native.sampler_estimator_params).
+EstimatorParams estimator_params(const SamplerConfig& cfg, int num_cu);
+
 // CPU list of a NUMA node ("0-31,64-95" parsed); empty if unknown.
 std::vector<int> numa_cpus(int node);
 

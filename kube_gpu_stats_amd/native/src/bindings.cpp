@@ -463,24 +463,7 @@ class PyExporter {
   Exporter ex_;
 };
 
-EstimatorParams sampler_estimator_params(int num_cu) {
-  const SamplerConfig c;
-  EstimatorParams p;
-  p.quiet_active_frac = kQuietActiveFrac;
-  p.cpc_full_frac = kCpcFullFrac;
-  p.clock_split_ns = kClockSplitNs;
-  p.read_overlap_ns = kReadOverlapNs;
-  p.time_split_ns = kTimeSplitNs;
-  p.quiet_hold_ns = kQuietHoldNs;
-  p.busy_min = c.pmc_busy_min;
-  p.gap_hold_ns = static_cast<int64_t>(c.pmc_gap_hold_s * 1e9);
-  p.cp_only_min = c.pmc_cp_only_min;
-  p.dbound_hold_ns = static_cast<int64_t>(c.pmc_dispatch_hold_s * 1e9);
-  p.plausible_mhz_lo = kPlausibleMhzLo;
-  p.plausible_mhz_hi = kPlausibleMhzHi;
-  p.num_simds = (num_cu > 0 ? num_cu : 256) * 4.0;
-  return p;
-}
+EstimatorParams sampler_estimator_params(int num_cu) { return estimator_params(SamplerConfig{}, num_cu); }
 
 py::dict parse_metrics_blob(const py::bytes& b) {
   std::string s = b;

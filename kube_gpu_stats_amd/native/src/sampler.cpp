@@ -56,6 +56,24 @@ struct Sampler::Worker {
   std::atomic<bool> abandoned{false};
 };
 
+EstimatorParams estimator_params(const SamplerConfig& cfg, int num_cu) {
+  EstimatorParams p;
+  p.quiet_active_frac = kQuietActiveFrac;
+  p.cpc_full_frac = kCpcFullFrac;
+  p.clock_split_ns = kClockSplitNs;
+  p.read_overlap_ns = kReadOverlapNs;
+  p.time_split_ns = kTimeSplitNs;
+  p.quiet_hold_ns = kQuietHoldNs;
+  p.busy_min = cfg.pmc_busy_min;
+  p.gap_hold_ns = static_cast<int64_t>(cfg.pmc_gap_hold_s * 1e9);
+  p.cp_only_min = cfg.pmc_cp_only_min;
+  p.dbound_hold_ns = static_cast<int64_t>(cfg.pmc_dispatch_hold_s * 1e9);
+  p.plausible_mhz_lo = kPlausibleMhzLo;
+  p.plausible_mhz_hi = kPlausibleMhzHi;
+  p.num_simds = (num_cu > 0 ? num_cu : 256) * 4.0;
+  return p;
+}
+
 std::vector<int> numa_cpus(int node) {
   std::vector<int> cpus;
   if (node < 0) return cpus;
@@ -559,19 +577,7 @@ void Sampler::run_pmc(Worker& w) {
   // Everything learned from the counts (READ cost, clocks, rate hysteresis, stall
   // watch) lives in the estimator (util_estimator.h); this thread schedules the
   // READs and publishes.
-  EstimatorParams ep;
-  ep.quiet_active_frac = kQuietActiveFrac;
-  ep.cpc_full_frac = kCpcFullFrac;
-  ep.clock_split_ns = kClockSplitNs;
-  ep.read_overlap_ns = kReadOverlapNs;
-  ep.time_split_ns = kTimeSplitNs;
-  ep.quiet_hold_ns = kQuietHoldNs;
-  ep.gap_hold_ns = static_cast<int64_t>(cfg_.pmc_gap_hold_s * 1e9);
-  ep.cp_only_min = cfg_.pmc_cp_only_min;
-  ep.dbound_hold_ns = static_cast<int64_t>(cfg_.pmc_dispatch_hold_s * 1e9);
-  ep.plausible_mhz_lo = kPlausibleMhzLo;
-  ep.plausible_mhz_hi = kPlausibleMhzHi;
-  ep.num_simds = (info.num_cu > 0 ? info.num_cu : 256) * 4.0;
+  EstimatorParams ep = estimator_params(cfg_, info.num_cu);
   DispatchEstimator est;
   est.invalidate(mono_ns());
   int64_t next = mono_ns();
