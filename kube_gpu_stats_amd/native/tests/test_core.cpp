@@ -34,6 +34,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cmath>
 #include <cerrno>
 #include <chrono>
 #include <string>
@@ -54,6 +55,7 @@
 #include "kgs/pmc.h"
 #include "kgs/sampler.h"
 #include "kgs/seqlock.h"
+#include "kgs/util_estimator.h"
 
 using namespace kgs;
 
@@ -956,7 +958,109 @@ static void test_lite_ib() {
               out.size(), r.dropped_copies, ok_n);
 }
 
+
+// DispatchEstimator on a synthetic READ stream (2.4 GHz idle, 2.1 GHz under bursts,
+// a 15 µs READ every 125 µs): the READ cost is learned on READ-only intervals, an
+// idle GPU integrates ≈0, a 1 ms-every-5 ms train its 20 % duty, and the quiet state
+// follows the hold.  Under the sanitizers: no UB in the fold, no out-of-range index.
+static void test_dispatch_estimator() {
+  const EstimatorParams p = estimator_params(SamplerConfig{}, 256);
+  DispatchEstimator e;
+  e.restart(0);
+  int64_t t = 0;
+  double cnt = 0, spi = 0, cpc = 0, mfma = 0, busy_s = 0, disp_s = 0;
+  bool quiet_seen = false;
+  auto read = [&](bool count) {
+    Drain d;
+    d.mono_ns = t;
+    d.mask = kPmcSetBase;
+    d.count = static_cast<uint64_t>(cnt);
+    d.spi = static_cast<uint64_t>(spi);
+    d.cpc = static_cast<uint64_t>(cpc);
+    d.mfma = static_cast<uint64_t>(mfma);
+    const DrainStep r = e.feed(d, p);
+    if (count) disp_s += r.dispatch_s;
+    quiet_seen |= r.quiet;
+  };
+  for (int i = 0; i < 400; ++i) {  // 50 ms idle: READs only
+    t += 125000;
+    cnt += 2.4e3 * 125;
+    cpc += 2.4e3 * 15;
+    spi += 2.4e3 * 0.9;
+    read(false);
+  }
+  CHECK(quiet_seen);
+  CHECK(std::abs(e.cpc_read_us() - 15.0) < 0.5);
+  CHECK(std::abs(e.clk_idle_hz() - 2.4e9) < 0.02e9);
+  for (int i = 0; i < 8000; ++i) {  // 1 s of a 1 ms / 5 ms train, READs every 125 µs
+    const double ph = std::fmod(t * 1e-9, 0.005);
+    const bool on = ph < 0.001;
+    const double f = on ? 2.1e3 : 2.4e3;  // cycles per µs
+    t += 125000;
+    cnt += f * 125;
+    cpc += f * 15 + (on ? f * 110 : 0.0);  // busy slice + the READ (hidden under the kernel when on)
+    spi += on ? f * 120 : 2.4e3 * 0.9;
+    mfma += on ? f * 120 * 512 : 0.0;
+    busy_s += on ? 125e-6 : 0.0;
+    read(true);
+  }
+  CHECK(std::abs(disp_s - busy_s) < 0.01 * 1.0);  // within 1 point of the 20 % duty
+  CHECK(!e.quiet());
+}
+
+// UtilBiller: drains at 10 Hz land on host time, PMFW tables on a 20 ms firmware
+// grid read at 10 Hz — an interval holds 0, 1 or 2 drains.  Carrying the excess
+// bills a saturated GPU everything but the last drain's lag; the round-4 clip
+// (cap 0) loses time; an epoch change falls back to PMFW and drops the carry.
+static void test_util_biller() {
+  auto run = [](double max_carry) {
+    UtilBiller b;
+    double billed = 0, last_fw = -1;
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<double> jit(0.0, 0.03);
+    double drain_t = 0, next_drain = 0.1 + jit(rng);
+    for (int k = 1; k <= 200; ++k) {
+      const double t = 0.1 * k + 0.004;               // PMFW thread wake-up
+      while (next_drain <= t) {
+        drain_t = next_drain;
+        next_drain += 0.1 + jit(rng) - 0.015;
+      }
+      const double fw = std::floor(t / 0.02) * 0.02;  // table time
+      const double dt = last_fw < 0 ? 0.0 : fw - last_fw;
+      last_fw = fw;
+      CounterCover c;
+      c.ok = true;
+      c.epoch = 1;
+      c.dispatch = true;
+      c.busy_s = drain_t;  // saturated: busy integral == host time at the drain
+      c.share = 1.0;
+      c.since_s = t - drain_t;
+      const UtilBiller::Bill r = b.bill(dt, 0.0, c, max_carry);
+      CHECK(r.billed_s <= dt + 1e-12);
+      billed += r.billed_s;
+    }
+    return billed;
+  };
+  const double fw_total = std::floor(20.004 / 0.02) * 0.02 - std::floor(0.104 / 0.02) * 0.02;
+  CHECK(run(0.35) > 0.99 * fw_total);
+  CHECK(run(1e-12) < 0.98 * fw_total);
+  UtilBiller b;
+  CounterCover c;
+  c.ok = true;
+  c.epoch = 1;
+  c.dispatch = true;
+  b.bill(0.02, 0.02, c, 1.0);
+  c.busy_s = 0.05;
+  CHECK(b.bill(0.02, 0.02, c, 1.0).from_counters && std::abs(b.carry_s() - 0.03) < 1e-9);
+  c.epoch = 2;
+  c.busy_s = 0.06;
+  const UtilBiller::Bill r = b.bill(0.02, 0.015, c, 1.0);
+  CHECK(!r.from_counters && std::abs(r.billed_s - 0.015) < 1e-12 && b.carry_s() == 0.0);
+}
+
 int main() {
+  test_dispatch_estimator();
+  test_util_biller();
   test_lite_ib();
   test_batch_plan();
   test_reserve_slot();
