@@ -358,22 +358,42 @@ def cpp_header() -> str:
             "  const char* mode;  // \"\" = default (--sm-util-source auto); else that mode's text\n"
             "  const char* help;\n};\n\n"
             "inline constexpr MetricDoc kMetricDocs[] = {\n" + "\n".join(rows) + "\n};\n\n"
+            "constexpr size_t kMetricDocCount = sizeof kMetricDocs / sizeof kMetricDocs[0];\n"
+            "constexpr size_t kNoMetricDoc = ~size_t{0};\n\n"
+            "constexpr bool metric_doc_streq(const char* a, const char* b) {\n"
+            "  while (*a && *a == *b) {\n"
+            "    ++a;\n"
+            "    ++b;\n"
+            "  }\n"
+            "  return *a == *b;\n"
+            "}\n\n"
+            "// Index of the family's default entry (each default entry precedes its variants);\n"
+            "// kNoMetricDoc if unknown.  Meant for constant evaluation: KGS_METRIC_DOC(\"name\").\n"
+            "constexpr size_t metric_doc_index(const char* name) {\n"
+            "  for (size_t i = 0; i < kMetricDocCount; ++i)\n"
+            "    if (!*kMetricDocs[i].mode && metric_doc_streq(kMetricDocs[i].name, name)) return i;\n"
+            "  return kNoMetricDoc;\n"
+            "}\n\n"
+            "// The entry at `i` in the text of `mode` (\"\" = default): the variants follow it.\n"
+            "inline const MetricDoc& metric_doc_at(size_t i, const char* mode) {\n"
+            "  if (*mode)\n"
+            "    for (size_t j = i + 1; j < kMetricDocCount && std::strcmp(kMetricDocs[j].name, kMetricDocs[i].name) == 0; ++j)\n"
+            "      if (std::strcmp(kMetricDocs[j].mode, mode) == 0) return kMetricDocs[j];\n"
+            "  return kMetricDocs[i];\n"
+            "}\n\n"
+            "// A family's entry index, resolved at compile time; a name missing from the\n"
+            "// catalogue does not compile.\n"
+            "#define KGS_METRIC_DOC(name)                                                         \\\n"
+            "  ([]() {                                                                           \\\n"
+            "    constexpr size_t kgs_doc_i = ::kgs::metric_doc_index(name);                     \\\n"
+            "    static_assert(kgs_doc_i != ::kgs::kNoMetricDoc, \"not in models/schema.py: \" name); \\\n"
+            "    return kgs_doc_i;                                                               \\\n"
+            "  }())\n\n"
             "// The family's HELP / TYPE for `mode` (falls back to the default text); nullptr if unknown.\n"
-            "// kMetricDocs is sorted by name, each default entry before its variants: a binary search.\n"
             "inline const MetricDoc* metric_doc(const char* name, const char* mode = \"\") {\n"
-            "  size_t lo = 0, hi = sizeof kMetricDocs / sizeof kMetricDocs[0];\n"
-            "  while (lo < hi) {\n"
-            "    const size_t mid = (lo + hi) / 2;\n"
-            "    if (std::strcmp(kMetricDocs[mid].name, name) < 0) lo = mid + 1;\n"
-            "    else hi = mid;\n"
-            "  }\n"
-            "  const MetricDoc* def = nullptr;\n"
-            "  for (size_t i = lo; i < sizeof kMetricDocs / sizeof kMetricDocs[0] && "
-            "std::strcmp(kMetricDocs[i].name, name) == 0; ++i) {\n"
-            "    if (std::strcmp(kMetricDocs[i].mode, mode) == 0) return &kMetricDocs[i];\n"
-            "    if (!*kMetricDocs[i].mode) def = &kMetricDocs[i];\n"
-            "  }\n"
-            "  return def;\n"
+            "  for (size_t i = 0; i < kMetricDocCount; ++i)\n"
+            "    if (!*kMetricDocs[i].mode && std::strcmp(kMetricDocs[i].name, name) == 0) return &metric_doc_at(i, mode);\n"
+            "  return nullptr;\n"
             "}\n\n}  // namespace kgs\n")
 
 

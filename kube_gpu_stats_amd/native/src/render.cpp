@@ -96,13 +96,14 @@ struct W {
     p = std::to_chars(p, end, v).ptr;
   }
   // HELP and TYPE come from the metric catalogue (models/schema.py → kgs/metric_help.h),
-  // in the text of the exporter's --sm-util-source mode.
+  // in the text of the exporter's --sm-util-source mode; `doc` is resolved at compile
+  // time (KGS_METRIC_DOC), so a family the catalogue lacks does not build.
   const char* mode = "";
-  void head(const char* name) {
-    if (!ok(name)) return;
-    const MetricDoc* d = metric_doc(name, mode);
-    put("# HELP ", 7); put(name); put(' '); put(d ? d->help : "(not in the metric catalogue)");
-    put("\n# TYPE ", 8); put(name); put(' '); put(d ? d->type : "untyped"); put('\n');
+  void head(size_t doc) {
+    const MetricDoc& d = metric_doc_at(doc, mode);
+    if (!ok(d.name)) return;
+    put("# HELP ", 7); put(d.name); put(' '); put(d.help);
+    put("\n# TYPE ", 8); put(d.name); put(' '); put(d.type); put('\n');
   }
   // name{base,extra} value
   void labels(const char* name, const std::string& base, const char* extra) {
@@ -273,25 +274,25 @@ void Exporter::render(std::string& out) {
     const bool from_counters = cfg_.sm_util_source == "counters";
     const bool from_auto = cfg_.sm_util_source == "auto";
     if (from_auto) {
-      w.head("container_gpu_sm_util");
+      w.head(KGS_METRIC_DOC("container_gpu_sm_util"));
       for (const auto& [d, lb] : pod_lines)
         if (snaps[static_cast<size_t>(d)].busy)
           w.line("container_gpu_sm_util", lb, nullptr, std::clamp(snaps[static_cast<size_t>(d)].util, 0.0, 100.0));
     } else if (from_counters) {
-      w.head("container_gpu_sm_util");
+      w.head(KGS_METRIC_DOC("container_gpu_sm_util"));
       for (const auto& [d, lb] : pod_lines) {
         const Snap& x = snaps[static_cast<size_t>(d)];
         if (x.pmc_rates) w.line("container_gpu_sm_util", lb, nullptr, x.r.gpu_active_pct);
       }
     } else {
-      w.head("container_gpu_sm_util");
+      w.head(KGS_METRIC_DOC("container_gpu_sm_util"));
       for (const auto& [d, lb] : pod_lines)
         if (snaps[static_cast<size_t>(d)].busy) w.line("container_gpu_sm_util", lb, nullptr, snaps[static_cast<size_t>(d)].g);
     }
     // Exact per-pod accounting: the GPU's busy integral since the pod was given
     // it.  rate() / increase() over any range is the exact mean utilisation,
     // whatever the scrape interval — the gauge above only sees its window.
-    w.head("container_gpu_busy_seconds_total");
+    w.head(KGS_METRIC_DOC("container_gpu_busy_seconds_total"));
     for (size_t i = 0; i < pod_lines.size(); ++i) {
       const Owner* o = pod_owner[i];
       const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
@@ -308,7 +309,7 @@ void Exporter::render(std::string& out) {
     bool any_cu = false;
     for (size_t i = 0; i < pod_lines.size() && !any_cu; ++i) any_cu = pod_owner[i] != nullptr && cfg_.per_process;
     if (any_cu) {
-      w.head("container_gpu_cu_seconds_total");
+      w.head(KGS_METRIC_DOC("container_gpu_cu_seconds_total"));
       for (size_t i = 0; i < pod_lines.size(); ++i) {
         const Owner* o = pod_owner[i];
         if (!o) continue;
@@ -326,7 +327,7 @@ void Exporter::render(std::string& out) {
     // Per-pod energy: the GPU's socket energy since the pod was given it (a GPU
     // shared by several pods counts in full for each: the pods hold it together;
     // a compute partition's energy is its share of the socket's, sampler.cpp).
-    w.head("container_gpu_energy_joules_total");
+    w.head(KGS_METRIC_DOC("container_gpu_energy_joules_total"));
     for (size_t i = 0; i < pod_lines.size(); ++i) {
       const Owner* o = pod_owner[i];
       const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
@@ -336,7 +337,7 @@ void Exporter::render(std::string& out) {
     bool any_pmc_int = false;
     for (const auto& pl : pod_lines) any_pmc_int |= snaps[static_cast<size_t>(pl.first)].pmc_mfma;
     if (any_pmc_int) {
-      w.head("container_gpu_mfma_busy_seconds_total");
+      w.head(KGS_METRIC_DOC("container_gpu_mfma_busy_seconds_total"));
       for (size_t i = 0; i < pod_lines.size(); ++i) {
         const Snap& x = snaps[static_cast<size_t>(pod_lines[i].first)];
         if (!x.pmc_mfma) continue;
@@ -348,7 +349,7 @@ void Exporter::render(std::string& out) {
     bool any_owner = false;
     for (const Owner* o : pod_owner) any_owner |= o != nullptr;
     if (any_owner) {
-      w.head("kgs_gpu_owner");
+      w.head(KGS_METRIC_DOC("kgs_gpu_owner"));
       for (size_t i = 0; i < pod_lines.size(); ++i)
         if (pod_owner[i]) w.line("kgs_gpu_owner", pod_lines[i].second, nullptr, 1);
     }
@@ -357,7 +358,7 @@ void Exporter::render(std::string& out) {
     if (any_mfma) {
       // Same labels, hardware-counter matrix-core busy: GFX busy counts a GPU busy
       // while any dispatch is in flight; this says how much of it was MFMA work.
-      w.head("container_gpu_mfma_util");
+      w.head(KGS_METRIC_DOC("container_gpu_mfma_util"));
       for (const auto& [d, lb] : pod_lines)
         if (snaps[static_cast<size_t>(d)].pmc_rates && snaps[static_cast<size_t>(d)].r.have_mfma)
           w.line("container_gpu_mfma_util", lb, nullptr, snaps[static_cast<size_t>(d)].r.mfma_util_pct);
@@ -375,7 +376,7 @@ void Exporter::render(std::string& out) {
   if (!sblock) {
     std::string blk;
     W b(blk, 16384, &filter_);
-    b.head("amdgpu_device_info");
+    b.head(KGS_METRIC_DOC("amdgpu_device_info"));
     for (int d : ids) {
       const DeviceInfo& in = be_->info(d);
       lb.assign(dev_labels_[static_cast<size_t>(d)]);
@@ -396,7 +397,7 @@ void Exporter::render(std::string& out) {
       b.line("amdgpu_device_info", lb, nullptr, 1);
     }
     if (!topo_.empty()) {
-      b.head("amdgpu_topology_link");
+      b.head(KGS_METRIC_DOC("amdgpu_topology_link"));
       for (const TopoEdge& e : topo_) {
         if (!sampled[static_cast<size_t>(e.src)]) continue;
         lb.assign(dev_labels_[static_cast<size_t>(e.src)]);
@@ -420,15 +421,15 @@ void Exporter::render(std::string& out) {
   // amdgpu_gfx_busy_*: the same busy signal as container_gpu_sm_util (--sm-util-source;
   // default auto: READ-immune); amdgpu_pmfw_gfx_busy_* is always the firmware's own.
   const bool util_auto = cfg_.sm_util_source == "auto";
-  w.head("amdgpu_gfx_busy_percent");
+  w.head(KGS_METRIC_DOC("amdgpu_gfx_busy_percent"));
   for (int d : ids)
     if (snaps[d].busy)
       w.line("amdgpu_gfx_busy_percent", dev_labels_[d], nullptr, util_auto ? std::clamp(snaps[d].util, 0.0, 100.0) : snaps[d].g);
-  w.head("amdgpu_pmfw_gfx_busy_percent");
+  w.head(KGS_METRIC_DOC("amdgpu_pmfw_gfx_busy_percent"));
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_pmfw_gfx_busy_percent", dev_labels_[d], nullptr, snaps[d].g);
-  w.head("amdgpu_gfx_busy_instant_percent");
+  w.head(KGS_METRIC_DOC("amdgpu_gfx_busy_instant_percent"));
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFGfxBusy)) w.line("amdgpu_gfx_busy_instant_percent", dev_labels_[d], nullptr, snaps[d].s.gfx_busy_pct);
-  w.head("amdgpu_gfx_busy_xcc_percent");
+  w.head(KGS_METRIC_DOC("amdgpu_gfx_busy_xcc_percent"));
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFGfxBusyXcc)) continue;
@@ -437,42 +438,42 @@ void Exporter::render(std::string& out) {
              x.s.dt_s > 0 ? x.s.gfx_busy_xcc_window[c] : x.s.gfx_busy_xcc[c]);
     }
   }
-  w.head("amdgpu_umc_busy_percent");
+  w.head(KGS_METRIC_DOC("amdgpu_umc_busy_percent"));
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_umc_busy_percent", dev_labels_[d], nullptr, snaps[d].u);
-  w.head("amdgpu_gfx_busy_seconds_total");
+  w.head(KGS_METRIC_DOC("amdgpu_gfx_busy_seconds_total"));
   for (int d : ids)
     if (snaps[d].have)
       w.line("amdgpu_gfx_busy_seconds_total", dev_labels_[d], nullptr, util_auto ? snaps[d].I.util_seconds : snaps[d].I.gfx_busy_seconds);
-  w.head("amdgpu_pmfw_gfx_busy_seconds_total");
+  w.head(KGS_METRIC_DOC("amdgpu_pmfw_gfx_busy_seconds_total"));
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_pmfw_gfx_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.gfx_busy_seconds);
-  w.head("kgs_util_source_seconds_total");
+  w.head(KGS_METRIC_DOC("kgs_util_source_seconds_total"));
   for (int d : ids) {
     if (!snaps[d].have) continue;
     w.line("kgs_util_source_seconds_total", dev_labels_[d], "source=\"counters\"", snaps[d].I.util_counter_seconds);
     w.line("kgs_util_source_seconds_total", dev_labels_[d], "source=\"pmfw\"",
            std::max(0.0, snaps[d].I.sampled_seconds - snaps[d].I.util_counter_seconds));
   }
-  w.head("kgs_util_carry_seconds");
+  w.head(KGS_METRIC_DOC("kgs_util_carry_seconds"));
   for (int d : ids) if (snaps[d].have) w.line("kgs_util_carry_seconds", dev_labels_[d], nullptr, snaps[d].I.util_carry_seconds);
-  w.head("kgs_util_dropped_seconds_total");
+  w.head(KGS_METRIC_DOC("kgs_util_dropped_seconds_total"));
   for (int d : ids)
     if (snaps[d].have) w.line("kgs_util_dropped_seconds_total", dev_labels_[d], nullptr, snaps[d].I.util_dropped_seconds);
-  w.head("amdgpu_umc_busy_seconds_total");
+  w.head(KGS_METRIC_DOC("amdgpu_umc_busy_seconds_total"));
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_umc_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds);
   const double full_bw = cfg_.hbm_bytes_per_s_at_full_umc;
-  w.head("amdgpu_hbm_bandwidth_bytes_per_second");
+  w.head(KGS_METRIC_DOC("amdgpu_hbm_bandwidth_bytes_per_second"));
   for (int d : ids) if (snaps[d].busy) w.line("amdgpu_hbm_bandwidth_bytes_per_second", dev_labels_[d], nullptr, snaps[d].u * 0.01 * full_bw);
-  w.head("amdgpu_hbm_bytes_total");
+  w.head(KGS_METRIC_DOC("amdgpu_hbm_bytes_total"));
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_hbm_bytes_total", dev_labels_[d], nullptr, snaps[d].I.umc_busy_seconds * full_bw);
 
   // ---- memory ------------------------------------------------------------
-  w.head("amdgpu_hbm_used_bytes");
+  w.head(KGS_METRIC_DOC("amdgpu_hbm_used_bytes"));
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFVram)) w.line_u("amdgpu_hbm_used_bytes", dev_labels_[d], nullptr, snaps[d].s.vram_used_bytes);
-  w.head("amdgpu_hbm_total_bytes");
+  w.head(KGS_METRIC_DOC("amdgpu_hbm_total_bytes"));
   for (int d : ids) w.line_u("amdgpu_hbm_total_bytes", dev_labels_[d], nullptr, be_->info(d).vram_total_bytes);
 
   // ---- thermals / power / clocks ----------------------------------------
-  w.head("amdgpu_temperature_celsius");
+  w.head(KGS_METRIC_DOC("amdgpu_temperature_celsius"));
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have) continue;
@@ -480,11 +481,11 @@ void Exporter::render(std::string& out) {
     if (x.s.valid & kFTempMem) w.line("amdgpu_temperature_celsius", dev_labels_[d], "sensor=\"hbm\"", x.s.temp_mem_c);
     if (x.s.valid & kFTempVrSoc) w.line("amdgpu_temperature_celsius", dev_labels_[d], "sensor=\"vrsoc\"", x.s.temp_vrsoc_c);
   }
-  w.head("amdgpu_power_watts");
+  w.head(KGS_METRIC_DOC("amdgpu_power_watts"));
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPower)) w.line("amdgpu_power_watts", dev_labels_[d], nullptr, snaps[d].s.power_w);
-  w.head("amdgpu_energy_joules_total");
+  w.head(KGS_METRIC_DOC("amdgpu_energy_joules_total"));
   for (int d : ids) if (snaps[d].have) w.line("amdgpu_energy_joules_total", dev_labels_[d], nullptr, snaps[d].I.energy_joules);
-  w.head("amdgpu_clock_mhz");
+  w.head(KGS_METRIC_DOC("amdgpu_clock_mhz"));
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have) continue;
@@ -498,14 +499,14 @@ void Exporter::render(std::string& out) {
     if (x.s.valid & kFUclk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"mem\"", x.s.uclk_mhz);
     if (x.s.valid & kFSocClk) w.line("amdgpu_clock_mhz", dev_labels_[d], "clock=\"soc\"", x.s.socclk_mhz);
   }
-  w.head("amdgpu_throttle_seconds_total");
+  w.head(KGS_METRIC_DOC("amdgpu_throttle_seconds_total"));
   for (int d : ids)
     if (snaps[d].have && (snaps[d].s.valid & kFThrottle))
       for (int r = 0; r < kThrottleReasons; ++r)
         w.line("amdgpu_throttle_seconds_total", dev_labels_[d], throttle_label(r), snaps[d].I.throttle_seconds[r]);
 
   // ---- interconnect ------------------------------------------------------
-  w.head("amdgpu_xgmi_read_bytes_total");
+  w.head(KGS_METRIC_DOC("amdgpu_xgmi_read_bytes_total"));
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
@@ -515,7 +516,7 @@ void Exporter::render(std::string& out) {
              static_cast<double>(x.s.xgmi_read_kb[l]) * cfg_.xgmi_bytes_per_acc_unit);
     }
   }
-  w.head("amdgpu_xgmi_write_bytes_total");
+  w.head(KGS_METRIC_DOC("amdgpu_xgmi_write_bytes_total"));
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
@@ -525,7 +526,7 @@ void Exporter::render(std::string& out) {
              static_cast<double>(x.s.xgmi_write_kb[l]) * cfg_.xgmi_bytes_per_acc_unit);
     }
   }
-  w.head("amdgpu_xgmi_link_up");
+  w.head(KGS_METRIC_DOC("amdgpu_xgmi_link_up"));
   for (int d : ids) {
     const Snap& x = snaps[d];
     if (!x.have || !(x.s.valid & kFXgmi)) continue;
@@ -534,7 +535,7 @@ void Exporter::render(std::string& out) {
       w.line("amdgpu_xgmi_link_up", dev_labels_[d], kLinkLabels[l], x.s.xgmi_link_up[l] ? 1 : 0);
     }
   }
-  w.head("amdgpu_xgmi_link_info");
+  w.head(KGS_METRIC_DOC("amdgpu_xgmi_link_info"));
   for (int d : ids) {
     auto links = S.state(d).get_links();
     if (!links || !snaps[d].links_fresh) continue;
@@ -563,7 +564,7 @@ void Exporter::render(std::string& out) {
     }
     w.put(*lblock);
   }
-  w.head("amdgpu_ecc_errors_total");
+  w.head(KGS_METRIC_DOC("amdgpu_ecc_errors_total"));
   for (int d : ids) {
     auto h = S.state(d).get_health();
     if (!h || !h->ecc_valid) continue;
@@ -571,7 +572,7 @@ void Exporter::render(std::string& out) {
     w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"uncorrectable\"", h->ecc_uncorrectable);
     w.line_u("amdgpu_ecc_errors_total", dev_labels_[d], "type=\"deferred\"", h->ecc_deferred);
   }
-  w.head("amdgpu_ecc_block_errors_total");
+  w.head(KGS_METRIC_DOC("amdgpu_ecc_block_errors_total"));
   for (int d : ids) {
     auto h = S.state(d).get_health();
     if (!h || !h->ecc_block_mask) continue;
@@ -586,59 +587,59 @@ void Exporter::render(std::string& out) {
       }
     }
   }
-  w.head("amdgpu_xgmi_error_status");
+  w.head(KGS_METRIC_DOC("amdgpu_xgmi_error_status"));
   for (int d : ids) {
     auto h = S.state(d).get_health();
     if (h && h->xgmi_error_status >= 0 && snaps[d].health_fresh)
       w.line("amdgpu_xgmi_error_status", dev_labels_[d], nullptr, h->xgmi_error_status);
   }
-  w.head("amdgpu_pcie_bytes_total");
+  w.head(KGS_METRIC_DOC("amdgpu_pcie_bytes_total"));
   for (int d : ids)
     if (snaps[d].have && (snaps[d].s.valid & kFPcie))
       w.line("amdgpu_pcie_bytes_total", dev_labels_[d], nullptr,
              static_cast<double>(snaps[d].s.pcie_bw_acc_gb) * cfg_.pcie_bytes_per_acc_unit);
-  w.head("amdgpu_pcie_bandwidth_acc_total");
+  w.head(KGS_METRIC_DOC("amdgpu_pcie_bandwidth_acc_total"));
   for (int d : ids) if (snaps[d].have && (snaps[d].s.valid & kFPcie)) w.line_u("amdgpu_pcie_bandwidth_acc_total", dev_labels_[d], nullptr, snaps[d].s.pcie_bw_acc_gb);
 
   // ---- hardware counters (PMC tier) ----------------------------------------
   bool any_pmc = false;
   for (int d : ids) any_pmc |= snaps[d].pmc_have;
   if (any_pmc) {
-    w.head("amdgpu_pmc_total");
+    w.head(KGS_METRIC_DOC("amdgpu_pmc_total"));
     for (int d : ids) {
       const Snap& x = snaps[d];
       if (!x.pmc_have) continue;
       for (int i = 0; i < kPmcCount; ++i)
         if (x.p.mask & (1u << i)) w.line_u("amdgpu_pmc_total", dev_labels_[d], pmc_counter_labels()[static_cast<size_t>(i)].c_str(), x.p.value[i]);
     }
-    w.head("amdgpu_gpu_active_seconds_total");
+    w.head(KGS_METRIC_DOC("amdgpu_gpu_active_seconds_total"));
     for (int d : ids) if (snaps[d].pmc_have) w.line("amdgpu_gpu_active_seconds_total", dev_labels_[d], nullptr, snaps[d].I.active_seconds);
     bool any_disp = false;
     for (int d : ids) any_disp |= snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0;
     if (any_disp) {
-      w.head("amdgpu_dispatch_busy_seconds_total");
+      w.head(KGS_METRIC_DOC("amdgpu_dispatch_busy_seconds_total"));
       for (int d : ids)
         if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
           w.line("amdgpu_dispatch_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.dispatch_seconds);
-      w.head("kgs_pmc_read_cp_seconds");
+      w.head(KGS_METRIC_DOC("kgs_pmc_read_cp_seconds"));
       for (int d : ids)
         if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
           w.line("kgs_pmc_read_cp_seconds", dev_labels_[d], nullptr, snaps[d].I.cpc_read_us * 1e-6);
     }
-    w.head("amdgpu_mfma_busy_seconds_total");
+    w.head(KGS_METRIC_DOC("amdgpu_mfma_busy_seconds_total"));
     for (int d : ids) if (snaps[d].pmc_mfma) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);
-    w.head("amdgpu_mfma_util_percent");
+    w.head(KGS_METRIC_DOC("amdgpu_mfma_util_percent"));
     for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_mfma) w.line("amdgpu_mfma_util_percent", dev_labels_[d], nullptr, snaps[d].r.mfma_util_pct);
-    w.head("amdgpu_gpu_active_percent");
+    w.head(KGS_METRIC_DOC("amdgpu_gpu_active_percent"));
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_active_percent", dev_labels_[d], nullptr, snaps[d].r.gpu_active_pct);
-    w.head("amdgpu_vmem_busy_percent");
+    w.head(KGS_METRIC_DOC("amdgpu_vmem_busy_percent"));
     for (int d : ids) if (snaps[d].pmc_rates && snaps[d].r.have_vmem) w.line("amdgpu_vmem_busy_percent", dev_labels_[d], nullptr, snaps[d].r.vmem_busy_pct);
-    w.head("amdgpu_gpu_clock_effective_mhz");
+    w.head(KGS_METRIC_DOC("amdgpu_gpu_clock_effective_mhz"));
     for (int d : ids) if (snaps[d].pmc_rates) w.line("amdgpu_gpu_clock_effective_mhz", dev_labels_[d], nullptr, snaps[d].r.gpu_clock_mhz);
     bool any_xcd = false;
     for (int d : ids) any_xcd |= snaps[d].pmc_rates && snaps[d].r.n_xcd > 0;
     if (any_xcd) {
-      w.head("amdgpu_mfma_util_xcc_percent");
+      w.head(KGS_METRIC_DOC("amdgpu_mfma_util_xcc_percent"));
       for (int d : ids)
         if (snaps[d].pmc_rates)
           for (int x = 0; x < snaps[d].r.n_xcd; ++x)
@@ -646,13 +647,13 @@ void Exporter::render(std::string& out) {
       bool any_xcd_vmem = false;
       for (int d : ids) any_xcd_vmem |= snaps[d].pmc_rates && snaps[d].r.n_xcd > 0 && snaps[d].r.have_xcd_vmem;
       if (any_xcd_vmem) {
-        w.head("amdgpu_vmem_busy_xcc_percent");
+        w.head(KGS_METRIC_DOC("amdgpu_vmem_busy_xcc_percent"));
         for (int d : ids)
           if (snaps[d].pmc_rates && snaps[d].r.have_xcd_vmem)
             for (int x = 0; x < snaps[d].r.n_xcd; ++x)
               w.line("amdgpu_vmem_busy_xcc_percent", dev_labels_[d], kXccLabels[x], snaps[d].r.xcd_vmem_busy_pct[x]);
       }
-      w.head("amdgpu_gpu_active_xcc_percent");
+      w.head(KGS_METRIC_DOC("amdgpu_gpu_active_xcc_percent"));
       for (int d : ids)
         if (snaps[d].pmc_rates)
           for (int x = 0; x < snaps[d].r.n_xcd; ++x)
@@ -662,7 +663,7 @@ void Exporter::render(std::string& out) {
 
   // ---- per-process attribution ------------------------------------------
   if (cfg_.per_process) {
-    w.head("amdgpu_process_hbm_bytes");
+    w.head(KGS_METRIC_DOC("amdgpu_process_hbm_bytes"));
     // Labels of every process line, built once per render and shared by the
     // five per-process families.
     std::vector<std::shared_ptr<const std::vector<ProcInfo>>> procs(static_cast<size_t>(nd));
@@ -694,71 +695,71 @@ void Exporter::render(std::string& out) {
       kv(l, "pod_uid", po ? po->pod_uid : none);
     }
     for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_hbm_bytes", plabels[i], nullptr, plist[i].second->vram_bytes);
-    w.head("amdgpu_process_gtt_bytes");
+    w.head(KGS_METRIC_DOC("amdgpu_process_gtt_bytes"));
     for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_gtt_bytes", plabels[i], nullptr, plist[i].second->gtt_bytes);
-    w.head("amdgpu_process_cu_occupancy");
+    w.head(KGS_METRIC_DOC("amdgpu_process_cu_occupancy"));
     for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_cu_occupancy", plabels[i], nullptr, plist[i].second->cu_occupancy);
-    w.head("amdgpu_process_gfx_seconds_total");
+    w.head(KGS_METRIC_DOC("amdgpu_process_gfx_seconds_total"));
     for (size_t i = 0; i < plist.size(); ++i) w.line("amdgpu_process_gfx_seconds_total", plabels[i], nullptr, plist[i].second->gfx_ns * 1e-9);
-    w.head("amdgpu_process_cu_seconds_total");
+    w.head(KGS_METRIC_DOC("amdgpu_process_cu_seconds_total"));
     for (size_t i = 0; i < plist.size(); ++i) w.line("amdgpu_process_cu_seconds_total", plabels[i], nullptr, plist[i].second->cu_seconds);
   }
 
   // ---- self metrics ------------------------------------------------------
-  w.head("kgs_up");
+  w.head(KGS_METRIC_DOC("kgs_up"));
   for (int d : ids) w.line("kgs_up", dev_labels_[d], nullptr, S.state(d).up.load());
-  w.head("kgs_last_sample_age_seconds");
+  w.head(KGS_METRIC_DOC("kgs_last_sample_age_seconds"));
   for (int d : ids) {
     const int64_t t = S.state(d).last_ok_mono_ns.load();
     w.line("kgs_last_sample_age_seconds", dev_labels_[d], nullptr, t ? (now - t) * 1e-9 : -1.0);
   }
-  w.head("kgs_samples_total");
+  w.head(KGS_METRIC_DOC("kgs_samples_total"));
   for (int d : ids) w.line_u("kgs_samples_total", dev_labels_[d], nullptr, snaps[d].I.distinct_samples);
-  w.head("kgs_reads_total");
+  w.head(KGS_METRIC_DOC("kgs_reads_total"));
   for (int d : ids) w.line_u("kgs_reads_total", dev_labels_[d], nullptr, snaps[d].I.reads);
-  w.head("kgs_read_errors_total");
+  w.head(KGS_METRIC_DOC("kgs_read_errors_total"));
   for (int d : ids) w.line_u("kgs_read_errors_total", dev_labels_[d], nullptr, snaps[d].I.read_errors);
-  w.head("kgs_sampler_overruns_total");
+  w.head(KGS_METRIC_DOC("kgs_sampler_overruns_total"));
   for (int d : ids) w.line_u("kgs_sampler_overruns_total", dev_labels_[d], nullptr, snaps[d].I.overruns);
-  w.head("kgs_device_recoveries_total");
+  w.head(KGS_METRIC_DOC("kgs_device_recoveries_total"));
   for (int d : ids) w.line_u("kgs_device_recoveries_total", dev_labels_[d], nullptr, snaps[d].I.recoveries);
-  w.head("kgs_pmc_samples_total");
+  w.head(KGS_METRIC_DOC("kgs_pmc_samples_total"));
   for (int d : ids) w.line_u("kgs_pmc_samples_total", dev_labels_[d], nullptr, snaps[d].I.pmc_samples);
-  w.head("kgs_pmc_read_seconds_total");
+  w.head(KGS_METRIC_DOC("kgs_pmc_read_seconds_total"));
   for (int d : ids) w.line("kgs_pmc_read_seconds_total", dev_labels_[d], nullptr, snaps[d].I.pmc_read_seconds);
-  w.head("kgs_pmc_errors_total");
+  w.head(KGS_METRIC_DOC("kgs_pmc_errors_total"));
   for (int d : ids) w.line_u("kgs_pmc_errors_total", dev_labels_[d], nullptr, snaps[d].I.pmc_errors);
   if (cfg_.pmc_source != "none" && !cfg_.pmc_source.empty()) {
-    w.head("kgs_pmc_enabled");
+    w.head(KGS_METRIC_DOC("kgs_pmc_enabled"));
     for (int d : ids) w.line_u("kgs_pmc_enabled", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_on.load()));
-    w.head("kgs_pmc_releases_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_releases_total"));
     for (int d : ids) w.line_u("kgs_pmc_releases_total", dev_labels_[d], nullptr, S.state(d).pmc_releases.load());
-    w.head("kgs_pmc_stalled");
+    w.head(KGS_METRIC_DOC("kgs_pmc_stalled"));
     for (int d : ids) w.line_u("kgs_pmc_stalled", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_stalled.load()));
-    w.head("kgs_pmc_reclaims_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_reclaims_total"));
     for (int d : ids) w.line_u("kgs_pmc_reclaims_total", dev_labels_[d], nullptr, S.state(d).pmc_reclaims.load());
-    w.head("kgs_pmc_refreshes_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_refreshes_total"));
     for (int d : ids) w.line_u("kgs_pmc_refreshes_total", dev_labels_[d], nullptr, S.state(d).pmc_refreshes.load());
-    w.head("kgs_pmc_quiet");
+    w.head(KGS_METRIC_DOC("kgs_pmc_quiet"));
     for (int d : ids) w.line_u("kgs_pmc_quiet", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_quiet.load()));
-    w.head("kgs_pmc_quiet_skips_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_quiet_skips_total"));
     for (int d : ids) w.line_u("kgs_pmc_quiet_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_quiet_skips.load());
-    w.head("kgs_pmc_gap");
+    w.head(KGS_METRIC_DOC("kgs_pmc_gap"));
     for (int d : ids) w.line_u("kgs_pmc_gap", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_gap.load()));
-    w.head("kgs_pmc_dispatch_bound");
+    w.head(KGS_METRIC_DOC("kgs_pmc_dispatch_bound"));
     for (int d : ids)
       w.line_u("kgs_pmc_dispatch_bound", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_dbound.load()));
-    w.head("kgs_pmc_gap_skips_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_gap_skips_total"));
     for (int d : ids) w.line_u("kgs_pmc_gap_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_gap_skips.load());
-    w.head("kgs_pmc_failed");
+    w.head(KGS_METRIC_DOC("kgs_pmc_failed"));
     for (int d : ids) w.line_u("kgs_pmc_failed", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_failed.load()));
-    w.head("kgs_pmc_breaker_trips_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_breaker_trips_total"));
     for (int d : ids) w.line_u("kgs_pmc_breaker_trips_total", dev_labels_[d], nullptr, S.state(d).pmc_breaker_trips.load());
-    w.head("kgs_pmc_retries_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_retries_total"));
     for (int d : ids) w.line_u("kgs_pmc_retries_total", dev_labels_[d], nullptr, S.state(d).pmc_retries.load());
-    w.head("kgs_pmc_reordered_total");
+    w.head(KGS_METRIC_DOC("kgs_pmc_reordered_total"));
     for (int d : ids) w.line_u("kgs_pmc_reordered_total", dev_labels_[d], nullptr, S.state(d).pmc_reordered.load());
-    w.head("kgs_sampler_wake_lateness_seconds");
+    w.head(KGS_METRIC_DOC("kgs_sampler_wake_lateness_seconds"));
     for (int d : ids) {
       const DeviceState& st = S.state(d);
       uint64_t cum = 0;
@@ -776,31 +777,31 @@ void Exporter::render(std::string& out) {
         if (pmc_->publish_stats(d, p)) ps.emplace_back(d, p);
       }
       if (!ps.empty()) {
-        w.head("kgs_pmc_publishes_total");
+        w.head(KGS_METRIC_DOC("kgs_pmc_publishes_total"));
         for (const auto& [d, p] : ps) w.line_u("kgs_pmc_publishes_total", dev_labels_[d], nullptr, p.publishes);
-        w.head("kgs_pmc_unlanded_total");
+        w.head(KGS_METRIC_DOC("kgs_pmc_unlanded_total"));
         for (const auto& [d, p] : ps) w.line_u("kgs_pmc_unlanded_total", dev_labels_[d], nullptr, p.unlanded);
       }
     }
   }
-  w.head("kgs_sampler_thread_hung");
+  w.head(KGS_METRIC_DOC("kgs_sampler_thread_hung"));
   for (int d : ids) w.line_u("kgs_sampler_thread_hung", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).thread_hung.load()));
-  w.head("kgs_slow_reads_total");
+  w.head(KGS_METRIC_DOC("kgs_slow_reads_total"));
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"procs\"", st.proc_reads.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_reads_total", dev_labels_[d], "tier=\"links\"", st.link_reads.load(std::memory_order_relaxed));
   }
-  w.head("kgs_slow_read_seconds_total");
+  w.head(KGS_METRIC_DOC("kgs_slow_read_seconds_total"));
   for (int d : ids) w.line("kgs_slow_read_seconds_total", dev_labels_[d], nullptr, S.state(d).slow_ns_total.load(std::memory_order_relaxed) * 1e-9);
-  w.head("kgs_slow_errors_total");
+  w.head(KGS_METRIC_DOC("kgs_slow_errors_total"));
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"procs\"", st.proc_errors.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"links\"", st.link_errors.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"health\"", st.health_errors.load(std::memory_order_relaxed));
   }
-  w.head("kgs_slow_last_ok_age_seconds");
+  w.head(KGS_METRIC_DOC("kgs_slow_last_ok_age_seconds"));
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     const std::atomic<int64_t>* oks[3] = {&st.procs_ok_ns, &st.links_ok_ns, &st.health_ok_ns};
@@ -813,16 +814,16 @@ void Exporter::render(std::string& out) {
       w.line("kgs_slow_last_ok_age_seconds", dev_labels_[d], tl, ok > 0 ? (now - ok) * 1e-9 : -1.0);
     }
   }
-  w.head("kgs_slow_call_seconds");
+  w.head(KGS_METRIC_DOC("kgs_slow_call_seconds"));
   for (int d : ids) {
     const int64_t t = S.state(d).slow_call_ns.load(std::memory_order_acquire);
     w.line("kgs_slow_call_seconds", dev_labels_[d], nullptr, t > 0 && now > t ? (now - t) * 1e-9 : 0.0);
   }
-  w.head("kgs_slow_thread_hung");
+  w.head(KGS_METRIC_DOC("kgs_slow_thread_hung"));
   for (int d : ids) w.line_u("kgs_slow_thread_hung", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).slow_hung.load()));
-  w.head("kgs_sampled_seconds_total");
+  w.head(KGS_METRIC_DOC("kgs_sampled_seconds_total"));
   for (int d : ids) w.line("kgs_sampled_seconds_total", dev_labels_[d], nullptr, snaps[d].I.sampled_seconds);
-  w.head("kgs_sample_read_seconds");
+  w.head(KGS_METRIC_DOC("kgs_sample_read_seconds"));
   for (int d : ids) {
     const DeviceState& st = S.state(d);
     uint64_t cum = 0;
@@ -835,18 +836,18 @@ void Exporter::render(std::string& out) {
   }
   std::string nl;
   kv(nl, "kubernetes_io_hostname", node, false);
-  w.head("kgs_scrapes_total");
+  w.head(KGS_METRIC_DOC("kgs_scrapes_total"));
   w.line_u("kgs_scrapes_total", nl, nullptr, scrapes.load() + 1);
-  w.head("kgs_scrape_render_seconds_total");
+  w.head(KGS_METRIC_DOC("kgs_scrape_render_seconds_total"));
   w.line("kgs_scrape_render_seconds_total", nl, nullptr, render_ns_total.load() * 1e-9);
-  w.head("kgs_scrape_render_last_seconds");
+  w.head(KGS_METRIC_DOC("kgs_scrape_render_last_seconds"));
   w.line("kgs_scrape_render_last_seconds", nl, nullptr, render_ns_last.load() * 1e-9);
-  w.head("kgs_http_connections");
+  w.head(KGS_METRIC_DOC("kgs_http_connections"));
   w.line_u("kgs_http_connections", nl, nullptr, http_conns_open.load());
-  w.head("kgs_http_connections_closed_total");
+  w.head(KGS_METRIC_DOC("kgs_http_connections_closed_total"));
   w.line_u("kgs_http_connections_closed_total", nl, "reason=\"idle\"", http_closed_idle.load());
   w.line_u("kgs_http_connections_closed_total", nl, "reason=\"limit\"", http_closed_limit.load());
-  w.head("kgs_build_info");
+  w.head(KGS_METRIC_DOC("kgs_build_info"));
   {
     std::string lb = nl;
     kv(lb, "version", "0.1.0");

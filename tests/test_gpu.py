@@ -1633,12 +1633,13 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
     """the configuration users get.  The exporter runs with the
     DaemonSet's own arguments (deploy/daemonset.yaml: --hz=10 with the aqlprofile
     counter tier) and with the same at --hz=100 (BASELINE config 4), under idle, two
-    MFMA burst trains and a saturating MFMA load.  100·rate(container_gpu_busy_seconds_total)
-    over each 6 s window — from the scrapes directly, and through a fake Prometheus fed
-    with those scrapes and `gpu-util-stats` fixed mode (the reference's per-pod mean,
-    gpu_util_stats.py:62-94 over the series of :159) — must read the kernels' event-timed
-    duty: saturated ≥ 95 over the load alone and within ±3 of its duty with idle edges,
-    idle ≤ 1, both trains within ±3 points."""
+    MFMA burst trains and a saturating MFMA load (6 s each, with 0.5 s idle edges).
+    100·rate(container_gpu_busy_seconds_total) from the scrapes must read the kernels'
+    event-timed duty — saturated ≥ 95 over the load alone and within ±3 of its duty with
+    the edges, idle ≤ 1, both trains within ±3 points — and a fake Prometheus fed with
+    scrapes every 100 ms, through `gpu-util-stats` fixed mode (the reference's per-pod
+    mean, gpu_util_stats.py:62-94 over the series of :159), within ±4 (its extrapolated
+    rate() over a 7 s range)."""
     import threading
 
     from fakeprom import FakeProm
@@ -1666,8 +1667,8 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
         sc2 = Scraper("127.0.0.1", ready["port"])
         cur = {"fp": None}
 
-        def scraper():  # Prometheus: a scrape every 250 ms into the current load's TSDB
-            while not stop.wait(0.25):
+        def scraper():  # Prometheus: a scrape every 100 ms into the current load's TSDB
+            while not stop.wait(0.1):
                 f = cur["fp"]
                 if f is not None:
                     f.ingest(parse_text(sc2.get()), time.time())
@@ -1728,11 +1729,13 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
         idle, sat = rows[f"{tag}/idle"], rows[f"{tag}/mfma_saturating"]
         assert idle["busy_counter_pct"] <= 1.0 and idle["report_pct"] <= 1.0, idle
         assert sat["load_only_busy_pct"] >= 95.0, sat
-        assert abs(sat["error_pts"]) <= 3.0 and abs(sat["report_pct"] - sat["duty_gpu_pct"]) <= 3.0, sat
+        # the report is Prometheus' extrapolated rate() over a 7 s range of a counter that
+        # advances in 100 ms PMFW steps at 10 Hz: held to ±4, the exact counter to ±3
+        assert abs(sat["error_pts"]) <= 3.0 and abs(sat["report_pct"] - sat["duty_gpu_pct"]) <= 4.0, sat
         for name in ("burst_1ms_every_5ms", "burst_0.2ms_every_1ms"):
             r = rows[f"{tag}/{name}"]
             assert abs(r["error_pts"]) <= 3.0, (tag, name, r)
-            assert abs(r["report_pct"] - r["duty_gpu_pct"]) <= 3.0, (tag, name, r)
+            assert abs(r["report_pct"] - r["duty_gpu_pct"]) <= 4.0, (tag, name, r)
             assert r["from_counters_s"] > 0.9 * r["window_s"], r
 
 
@@ -1922,8 +1925,8 @@ def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
     out the per-SE MFMA counters (a compacted copy of their IB without the per-SE
     sections, kgs/aql_ib.h).  Under
     back-to-back MFMA kernels the MFMA busy integral and the window's MFMA util must
-    match an exporter that reads them every time, and the dispatch integral must not
-    move."""
+    match an exporter that reads them every time, and in both modes the dispatch integral
+    must read the kernels' event-timed duty within 2 points."""
     import torch
 
     from kube_gpu_stats_amd.native import pmc_lib_path
@@ -1944,10 +1947,15 @@ def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
                 ls.run_mfma()
             torch.cuda.synchronize()
             a, t0 = ex.integrals(0), time.time()
+            gpu_s = 0.0
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             while time.time() - t0 < 1.5:
+                e0.record()
                 for _ in range(4):
                     ls.run_mfma()
+                e1.record()
                 torch.cuda.synchronize()
+                gpu_s += e0.elapsed_time(e1) * 1e-3
             b, dt = ex.integrals(0), time.time() - t0
             w = ex.window(0, 1.0)
             info = ex.pmc_info(0)
@@ -1959,6 +1967,7 @@ def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
         rows["lite" if lite else "full"] = {
             "mfma_busy_pct": 100 * (b["mfma_busy_seconds"] - a["mfma_busy_seconds"]) / dt,
             "dispatch_pct": 100 * (b["dispatch_seconds"] - a["dispatch_seconds"]) / dt,
+            "duty_gpu_pct": 100 * gpu_s / dt,
             "mfma_util_pct": w["mfma_util_pct"], "reads_per_s": (b["pmc_samples"] - a["pmc_samples"]) / dt,
             "lite": lite_field, "full_ib": "lite_full_ib" in info}
     _keep("lite_reads.json", json.dumps(rows, indent=1))
@@ -1968,4 +1977,8 @@ def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
     assert int(l["lite"].split(":")[1]) > 1000 and not l["full_ib"], rows  # lite READs did run
     assert f["mfma_busy_pct"] > 50 and abs(l["mfma_busy_pct"] - f["mfma_busy_pct"]) < 3, rows
     assert abs(l["mfma_util_pct"] - f["mfma_util_pct"]) < 3, rows
-    assert abs(l["dispatch_pct"] - f["dispatch_pct"]) < 2 and l["reads_per_s"] > 7000, rows
+    # each mode's dispatch integral against its own run's event-timed kernel duty (the two
+    # runs' duty differs by the host syncs between groups of kernels)
+    for r in (f, l):
+        assert abs(r["dispatch_pct"] - r["duty_gpu_pct"]) < 2, rows
+    assert l["reads_per_s"] > 7000, rows
