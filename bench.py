@@ -1104,7 +1104,12 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
     for h in hzs:
         diffs = [100.0 * (row[h] / row[0.0] - 1.0) for row in rows]
         m, ci, sd = mean_ci95(diffs)
+        srt = sorted(diffs)
+        med = (srt[(len(srt) - 1) // 2] + srt[len(srt) // 2]) / 2 if srt else float("nan")
         tier = {"overhead_pct": m, "overhead_ci95_pct": ci, "overhead_sd_pct": sd,
+                # robustness next to the mean: a few disturbed rounds (another tenant of the
+                # box, a clock event) move the mean and its CI, not the median
+                "overhead_median_pct": med,
                 "overhead_per_round_pct": [round(d, 4) for d in diffs],
                 "_rates": rates[h], "_lat": lat[h]}
         # per component (rank 0's GPU, and the mean of every rank's own estimate)
@@ -1874,6 +1879,7 @@ def summarize(res: dict) -> dict:
                  "p50_scrape_ms": _r(res.get("p50_scrape_ms")), "p99_scrape_ms": _r(res.get("p99_scrape_ms")),
                  "scrapes": res.get("scrapes"), "overhead_pct": _pm(res)}
     out["overhead_by_tier"] = {h: _pm(t) for h, t in tiers.items()}
+    out["overhead_median_by_tier"] = {h: _r(t.get("overhead_median_pct")) for h, t in tiers.items()}
     out["overhead_position_adjusted"] = {h: _pm(v) for h, v in pa.items() if isinstance(v, dict) and "overhead_pct" in v}
     out["overhead_by_component"] = {h: {c: _pm(v) for c, v in (t.get("overhead_by_component") or {}).items()}
                                     for h, t in tiers.items()}

@@ -29,7 +29,8 @@ def _last_json(out: str) -> dict:
 
 
 SUMMARY_KEYS = {"value", "samples_per_sec_per_gpu", "p50_scrape_ms", "p99_scrape_ms", "scrapes", "overhead_pct",
-                "overhead_by_tier", "overhead_by_component", "overhead_by_component_vs_released", "overhead_by_rank",
+                "overhead_by_tier", "overhead_median_by_tier", "overhead_by_component", "overhead_by_component_vs_released",
+                "overhead_by_rank",
                 "released", "delivered_by_component", "util_accuracy", "xgmi_link_map_ok", "xgmi_links_ok", "xgmi_unit_ratio"}
 
 
