@@ -1881,11 +1881,14 @@ def summarize(res: dict) -> dict:
     out["overhead_by_tier"] = {h: _pm(t) for h, t in tiers.items()}
     out["overhead_median_by_tier"] = {h: _r(t.get("overhead_median_pct")) for h, t in tiers.items()}
     out["overhead_position_adjusted"] = {h: _pm(v) for h, v in pa.items() if isinstance(v, dict) and "overhead_pct" in v}
-    out["overhead_by_component"] = {h: {c: _pm(v) for c, v in (t.get("overhead_by_component") or {}).items()}
-                                    for h, t in tiers.items()}
-    out["overhead_by_component_vs_released"] = {h: {c: _pm(v) for c, v in
-                                                    (t.get("overhead_by_component_vs_released") or {}).items()}
-                                                for h, t in tiers.items() if t.get("overhead_by_component_vs_released")}
+    # per tier and component: [vs paused, ± 95 %, vs released, ± 95 %] (the last two when
+    # the run had the released condition)
+    def comp(t: dict) -> dict:
+        rel = t.get("overhead_by_component_vs_released") or {}
+        return {c: (_pm(v) or [None, None]) + (_pm(rel.get(c)) or []) for c, v in
+                (t.get("overhead_by_component") or {}).items()}
+
+    out["overhead_by_component"] = {h: comp(t) for h, t in tiers.items()}
     out["overhead_by_rank"] = [_r(x.get("overhead_pct")) for x in (tiers.get(prim, {}).get("overhead_by_rank") or [])]
     rel = inter.get("released")
     if rel:

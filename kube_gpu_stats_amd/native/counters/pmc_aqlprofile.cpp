@@ -1008,14 +1008,14 @@ bool make_lite(Agent* a, int k, uint32_t cmd_sz) {
   // (SQ / TA / TD / TCP): every dropped result must be one of theirs.  A
   // session counter of another SE-indexed block (SPI, GRBMSE, ...) would have its
   // per-SE copies dropped too and then be read from dwords the lite IB never writes.
-  // The output buffer holds the results in fold order, each `m` 32-bit copies (LO,
-  // HI); the open READ's fold recorded each result ordinal's counter (res_slot), so
-  // every dropped destination maps to the counter it belongs to.
+  // The output buffer holds the results in fold order, each `m` copies of one size
+  // (gfx950: two 32-bit copies, LO and HI); the open READ's fold recorded each result
+  // ordinal's counter (res_slot), so every dropped destination maps to its counter.
   const size_t n_res = a->res_slot.size(), copies = c.kept_copies + c.dropped_copies;
-  if (!a->res_xcd_done || n_res == 0 || copies % n_res != 0) {
+  if (!a->res_xcd_done || n_res == 0 || copies % n_res != 0 || c.copy_bytes == 0) {
     return why("cannot map " + std::to_string(copies) + " result copies onto " + std::to_string(n_res) + " results");
   }
-  const uint64_t base = reinterpret_cast<uint64_t>(a->pout[k]), stride = 4 * (copies / n_res);
+  const uint64_t base = reinterpret_cast<uint64_t>(a->pout[k]), stride = c.copy_bytes * (copies / n_res);
   for (uint64_t dst : c.dropped_dsts) {
     const uint64_t ord = dst >= base ? (dst - base) / stride : n_res;
     const int ck = ord < n_res ? a->res_slot[ord].first : -1;

@@ -42,6 +42,8 @@ inline uint32_t pm4_len(uint32_t h) { return ((h >> 16) & 0x3FFF) + 2; }  // dwo
 inline bool pm4_copy_to_mem(const uint32_t* p) {
   return pm4_op(p[0]) == kPm4CopyData && pm4_len(p[0]) == 6 && ((p[1] >> 8) & 0xF) == 5;
 }
+// Bytes one COPY_DATA writes: COUNT_SEL (control bit 16) selects 64 bits, else 32.
+inline uint32_t pm4_copy_bytes(const uint32_t* p) { return (p[1] >> 16) & 1u ? 8u : 4u; }
 inline uint64_t pm4_copy_dst(const uint32_t* p) {
   return (static_cast<uint64_t>(p[4]) | (static_cast<uint64_t>(p[5]) << 32)) & ~3ull;
 }
@@ -101,6 +103,7 @@ struct IbCompact {
   uint32_t dropped_copies = 0;  // per-SE COPY_DATA packets left out
   uint32_t dropped_dw = 0;      // dwords left out in all
   uint32_t kept_copies = 0;     // COPY_DATA→memory packets the compacted IB still has
+  uint32_t copy_bytes = 0;      // bytes each copy writes (0: the copies differ in size)
   std::vector<uint64_t> dropped_dsts;
   std::string why;              // when !ok
 };
@@ -192,6 +195,15 @@ inline IbCompact compact_se_sections(const uint32_t* ib, uint32_t ndw, std::vect
     return r;
   }
   r.kept_copies = static_cast<uint32_t>(out_dsts.size());
+  for (uint32_t i = 0; i < ndw;) {  // one copy size for every result copy, or 0
+    if (pm4_type(ib[i]) == 2) { ++i; continue; }
+    if (pm4_copy_to_mem(ib + i)) {
+      const uint32_t b = pm4_copy_bytes(ib + i);
+      if (r.copy_bytes == 0) r.copy_bytes = b;
+      else if (r.copy_bytes != b) { r.copy_bytes = 0; break; }
+    }
+    i += pm4_len(ib[i]);
+  }
   r.ok = true;
   return r;
 }

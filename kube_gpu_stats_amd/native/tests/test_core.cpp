@@ -870,6 +870,10 @@ static void test_lite_ib() {
   IbCompact r = compact_se_sections(ib.data(), static_cast<uint32_t>(ib.size()), out);
   CHECK(r.ok);
   CHECK(r.dropped_copies == 8 * 4 * 2);
+  CHECK(r.kept_copies + r.dropped_copies == all.size() && r.copy_bytes == 4);  // 32-bit LO / HI copies
+  // the dropped results are the SQ ones: with 2 copies of 4 B per result in IB order,
+  // ordinal = offset / 8 lands on the 4 SE results after each XCC's 3 global ones
+  for (uint64_t d : r.dropped_dsts) CHECK((d - 0x7f0000001000ull) / 8 % 7 >= 3);
   std::vector<uint64_t> kept;
   std::string why;
   CHECK(ib_copy_dsts(out.data(), static_cast<uint32_t>(out.size()), &kept, &why));
