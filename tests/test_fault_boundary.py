@@ -13,6 +13,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 import urllib.error
 import urllib.request
@@ -261,15 +262,24 @@ def test_injected_queue_stall_trips_the_breaker_and_a_fresh_queue_recovers(mock_
     assert body == {"gpu": 1, "stall": True}
     t0 = time.time()
     seen_failed, totals = None, [g0(before)]
+    done = threading.Event()
+
+    def watch():  # the breaker may open and close again while the rates below are measured
+        nonlocal seen_failed
+        while not done.is_set() and time.time() - t0 < 3.0:
+            m = parse_text(ex.render())
+            totals.append(g0(m))
+            if seen_failed is None and {lb["gpu"]: v for lb, v in m["kgs_pmc_failed"]}["1"] == 1:
+                seen_failed = time.time() - t0
+            if seen_failed is not None and ex.integrals(1)["pmc_failed"] == 0:
+                break
+            time.sleep(0.01)
+
+    th = threading.Thread(target=watch)
+    th.start()
     pmfw, pmc = rates_once(ex, [0, 1], 0.6)                # while wedged / tripping
-    while time.time() - t0 < 3.0:
-        m = parse_text(ex.render())
-        totals.append(g0(m))
-        if seen_failed is None and {lb["gpu"]: v for lb, v in m["kgs_pmc_failed"]}["1"] == 1:
-            seen_failed = time.time() - t0
-        if seen_failed is not None and ex.integrals(1)["pmc_failed"] == 0:
-            break
-        time.sleep(0.02)
+    th.join(timeout=5)
+    done.set()
     i = ex.integrals(1)
     assert i["pmc_stalls_injected"] == 1 and i["pmc_breaker_trips"] == 1 and i["pmc_resets"] >= 1, i
     assert seen_failed is not None and seen_failed < 3 * 0.1 + 0.5, seen_failed  # K x timeout + slack
