@@ -1384,6 +1384,10 @@ def util_accuracy(ctx, load, exp, a) -> dict:
                 per_gpu[g]["from_counters_pct"] = (round(100 * (src.get("counters", 0.0) - src0.get("counters", 0.0))
                                                          / tot, 1) if tot > 0 else None)
                 per_gpu[g]["error_pts"] = round(per_gpu[g]["busy_counter_pct"] - per_gpu[g]["duty_gpu_pct"], 2)
+                # the clocks the time split priced this window's idle cycles at (diagnostic)
+                clk = {lb.get("kind"): v for lb, v in m1.get("kgs_pmc_shader_clock_hz", []) if lb["gpu"] == g}
+                if clk:
+                    per_gpu[g]["clock_mhz"] = {k: round(v / 1e6, 1) for k, v in sorted(clk.items())}
             per_load[name] = per_gpu
         out["per_rate"][f"{hz:g}"] = per_load
     if exp is not None:

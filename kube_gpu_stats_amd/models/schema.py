@@ -201,6 +201,11 @@ CATALOG: tuple[Family, ...] = (
       "intervals without waves (what amdgpu_dispatch_busy_seconds_total subtracts per READ; lite READs are learned "
       "apart and cost less).", source="self",
       tier="pmc"),
+    F("kgs_pmc_shader_clock_hz", "gauge",
+      "Shader clock the dispatch estimator learned from GRBM_COUNT: kind=idle on intervals without waves, kind=busy "
+      "on intervals the CP was busy for all of.  A long partial interval (low READ rate) prices its idle cycles at "
+      "the idle clock (the time split behind amdgpu_dispatch_busy_seconds_total).", extra=("kind",), source="self",
+      tier="pmc"),
     F("amdgpu_mfma_busy_seconds_total", "counter",
       "∫ MFMA-busy share of all SIMD cycles dt (per drain: ΔSQ_VALU_MFMA_BUSY_CYCLES / (SIMDs·ΔGRBM_COUNT) · Δt); "
       "rate() = matrix-core utilisation of wall time.", source="counters", tier="pmc"),

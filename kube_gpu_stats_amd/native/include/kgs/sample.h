@@ -170,6 +170,11 @@ struct Integrals {
   uint64_t dispatch_drains = 0;
   double pmc_last_share = 0;    // busy share (dispatch, else SPI) of the last drain interval
   double cpc_read_us = 0;       // the READ's own CP busy time as last learned (µs)
+  // The shader clocks the estimator learned (DispatchEstimator): on READ-only intervals
+  // (idle) and on fully busy ones (busy); 0 until seen.  The time split of long partial
+  // intervals prices idle cycles at the idle clock.
+  double pmc_clk_idle_hz = 0;
+  double pmc_clk_busy_hz = 0;
   // ∫ busy dt that does not count the exporter's own counter READs (the default
   // --sm-util-source auto behind container_gpu_sm_util / container_gpu_busy_seconds_total):
   // per PMFW interval, the counter tier's dispatch integral (dispatch_seconds; SPI

@@ -281,6 +281,8 @@ struct DeviceState {
     a.dispatch_drains = b.dispatch_drains;
     a.pmc_last_share = b.pmc_last_share;
     a.cpc_read_us = b.cpc_read_us;
+    a.pmc_clk_idle_hz = b.pmc_clk_idle_hz;
+    a.pmc_clk_busy_hz = b.pmc_clk_busy_hz;
     return a;
   }
 };

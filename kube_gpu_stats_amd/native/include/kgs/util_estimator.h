@@ -275,6 +275,7 @@ struct CounterCover {
   double busy_s = 0;      // the counter tier's cumulative busy integral at its last drain
   double share = 0;       // busy share of the last drain interval
   double since_s = 0;     // host time from the last drain to this PMFW sample
+  uint64_t drains = 0;    // drains folded so far (a new one restarts the run-on guess)
 };
 
 class UtilBiller {
@@ -287,16 +288,26 @@ class UtilBiller {
   //
   // While the counter tier held one epoch since the previous PMFW sample, the
   // interval is billed from the counter integral: its value at the last drain, run
-  // on to this sample at the last interval's share (at 10 Hz the last drain can be
-  // 100 ms old; the next drain corrects the guess), plus what earlier intervals
-  // could not take, at most dt_s.  The rest carries on to the next intervals
-  // (negative: billed ahead of the drains, paid back first) — capped at
-  // ±max_carry_s, so a firmware clock slower than the host's cannot bank busy time
-  // that a saturated GPU then bills into a following idle stretch.  Else the PMFW
-  // busy, and the carry is dropped (its time lies in the intervals PMFW billed).
+  // on to this sample (at 10 Hz the last drain can be 100 ms old; the next drain
+  // corrects the guess), plus what earlier intervals could not take, at most dt_s.
+  // The run-on guesses each PMFW interval after the drain at the last drain's share,
+  // never above the PMFW GFX busy share of that interval: a guess past the end of a
+  // load cannot be taken back from a counter, and the PMFW — whatever else it counts
+  // (our READs: ≈80 µs each) — sees the GPU stop at once (r5j: 10 Hz, a saturated
+  // 3 s load billed 0.042 s past its end without this bound).  The rest carries on
+  // to the next intervals (negative: billed ahead of the drains, paid back first) —
+  // capped at ±max_carry_s, so a firmware clock slower than the host's cannot bank
+  // busy time that a saturated GPU then bills into a following idle stretch.  Else
+  // the PMFW busy, and the carry is dropped (its time lies in the intervals PMFW billed).
   Bill bill(double dt_s, double dgfx_s, const CounterCover& c, double max_carry_s) {
     Bill b;
-    const double v = c.busy_s + std::clamp(c.share, 0.0, 1.0) * std::clamp(c.since_s, 0.0, max_carry_s);
+    const double share = std::clamp(c.share, 0.0, 1.0);
+    const double since = std::clamp(c.since_s, 0.0, max_carry_s);
+    const double rate = dt_s > 0 ? std::min(share, std::clamp(dgfx_s / dt_s, 0.0, 1.0)) : 0.0;
+    if (c.drains != drains_ || !have_) guess_s_ = rate * std::min(since, std::max(dt_s, 0.0));
+    else guess_s_ = std::min(guess_s_ + rate * std::max(dt_s, 0.0), share * since);
+    drains_ = c.drains;
+    const double v = c.busy_s + guess_s_;
     const bool cont = c.ok && have_ && epoch_ == c.epoch && dispatch_ == c.dispatch && c.busy_s >= last_s_;
     if (cont) carry_s_ += v - last_v_;
     else carry_s_ = 0;
@@ -328,8 +339,8 @@ class UtilBiller {
 
  private:
   bool have_ = false, dispatch_ = false;
-  uint64_t epoch_ = 0;
-  double last_s_ = 0, last_v_ = 0, carry_s_ = 0, dropped_s_ = 0;
+  uint64_t epoch_ = 0, drains_ = 0;
+  double last_s_ = 0, last_v_ = 0, carry_s_ = 0, dropped_s_ = 0, guess_s_ = 0;
 };
 
 }  // namespace kgs

@@ -268,6 +268,8 @@ class PyExporter {
     o["dispatch_seconds"] = I.dispatch_seconds;
     o["dispatch_drains"] = I.dispatch_drains;
     o["cpc_read_us"] = I.cpc_read_us;
+    o["pmc_clk_idle_hz"] = I.pmc_clk_idle_hz;
+    o["pmc_clk_busy_hz"] = I.pmc_clk_busy_hz;
     o["util_counter_seconds"] = I.util_counter_seconds;
     o["util_carry_seconds"] = I.util_carry_seconds;
     o["util_dropped_seconds"] = I.util_dropped_seconds;
@@ -655,7 +657,7 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def(
           "bill",
           [](UtilBiller& b, double dt_s, double dgfx_s, bool ok, uint64_t epoch, double busy_s, double max_carry_s,
-             bool dispatch, double share, double since_s) {
+             bool dispatch, double share, double since_s, uint64_t drains) {
             CounterCover c;
             c.ok = ok;
             c.epoch = epoch;
@@ -663,13 +665,15 @@ PYBIND11_MODULE(_kgs_native, m) {
             c.busy_s = busy_s;
             c.share = share;
             c.since_s = since_s;
+            c.drains = drains;
             const UtilBiller::Bill r = b.bill(dt_s, dgfx_s, c, max_carry_s);
             return py::make_tuple(r.billed_s, r.from_counters);
           },
           py::arg("dt_s"), py::arg("dgfx_s"), py::arg("ok"), py::arg("epoch"), py::arg("busy_s"),
           py::arg("max_carry_s") = 1.0, py::arg("dispatch") = true, py::arg("share") = 0.0,
-          py::arg("since_s") = 0.0,
-          "Bill one PMFW interval: (seconds billed, billed from the counters?)")
+          py::arg("since_s") = 0.0, py::arg("drains") = 0,
+          "Bill one PMFW interval: (seconds billed, billed from the counters?).  drains: the count of "
+          "drains folded so far (a new drain restarts the run-on guess)")
       .def_property_readonly("carry_s", &UtilBiller::carry_s)
       .def_property_readonly("dropped_s", &UtilBiller::dropped_s);
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");

@@ -625,6 +625,14 @@ void Exporter::render(std::string& out) {
       for (int d : ids)
         if (snaps[d].pmc_have && snaps[d].I.dispatch_drains > 0)
           w.line("kgs_pmc_read_cp_seconds", dev_labels_[d], nullptr, snaps[d].I.cpc_read_us * 1e-6);
+      w.head(KGS_METRIC_DOC("kgs_pmc_shader_clock_hz"));
+      for (int d : ids) {
+        if (!snaps[d].pmc_have || snaps[d].I.dispatch_drains == 0) continue;
+        if (snaps[d].I.pmc_clk_idle_hz > 0)
+          w.line("kgs_pmc_shader_clock_hz", dev_labels_[d], "kind=\"idle\"", snaps[d].I.pmc_clk_idle_hz);
+        if (snaps[d].I.pmc_clk_busy_hz > 0)
+          w.line("kgs_pmc_shader_clock_hz", dev_labels_[d], "kind=\"busy\"", snaps[d].I.pmc_clk_busy_hz);
+      }
     }
     w.head(KGS_METRIC_DOC("amdgpu_mfma_busy_seconds_total"));
     for (int d : ids) if (snaps[d].pmc_mfma) w.line("amdgpu_mfma_busy_seconds_total", dev_labels_[d], nullptr, snaps[d].I.mfma_busy_seconds);

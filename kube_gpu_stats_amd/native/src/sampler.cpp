@@ -428,6 +428,7 @@ void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, In
   c.busy_s = c.dispatch ? pc.dispatch_seconds : pc.active_seconds;
   c.share = pc.pmc_last_share;
   c.since_s = (now - pc.pmc_last_ns) * 1e-9;
+  c.drains = pc.pmc_samples;
   // Carry (and run the last drain on) at most one freshness window: the
   // drain-vs-interval jitter, never a backlog.
   const UtilBiller::Bill b = util_bill_[static_cast<size_t>(dev)].bill(dt_s, dgfx_s, c, fresh_ns * 1e-9);
@@ -710,6 +711,8 @@ void Sampler::run_pmc(Worker& w) {
         }
         if (r.span_s > 0) P.pmc_last_share = (r.have_dispatch ? r.dispatch_s : r.active_s) / r.span_s;
         if (r.learned && dr.se_fresh) P.cpc_read_us = est.cpc_read_us();
+        P.pmc_clk_idle_hz = est.clk_idle_hz();
+        P.pmc_clk_busy_hz = est.clk_busy_hz();
         st.pmc_quiet.store(r.quiet ? 1 : 0, std::memory_order_relaxed);
         st.pmc_gap.store(r.gap ? 1 : 0, std::memory_order_relaxed);
         st.pmc_dbound.store(r.dbound ? 1 : 0, std::memory_order_relaxed);

@@ -131,7 +131,7 @@ def _simulate(N, hz, busy_of_t, secs=20.0, fw_period=0.020, drain_jitter=0.3, se
     b = N.UtilBiller()
     fresh = 3.0 / min(hz, 100.0) + 0.05
     billed, trace, last_fw, k = 0.0, [], None, 0
-    t = 0.0
+    t = last_t = 0.0
     while t < secs:
         t += 1.0 / pmfw_rate
         while k + 1 < len(drain_t) and drain_t[k + 1] <= t:
@@ -144,7 +144,10 @@ def _simulate(N, hz, busy_of_t, secs=20.0, fw_period=0.020, drain_jitter=0.3, se
         share = 0.0
         if extrapolate and k > 0:
             share = (busy_of_t(drain_t[k]) - busy_of_t(drain_t[k - 1])) / (drain_t[k] - drain_t[k - 1])
-        got, from_c = b.bill(dt, 0.0, True, 1, busy_of_t(drain_t[k]), max_carry or fresh, True, share, t - drain_t[k])
+        dgfx = min(dt, busy_of_t(t) - busy_of_t(last_t))  # the PMFW's busy of the interval
+        last_t = t
+        got, from_c = b.bill(dt, dgfx, True, 1, busy_of_t(drain_t[k]), max_carry or fresh, True, share,
+                             t - drain_t[k], k)
         if dt > 0:
             assert from_c and got <= dt + 1e-12
             billed += got
@@ -180,6 +183,22 @@ def test_biller_is_lossless_when_drains_alias_with_pmfw_intervals(N, hz):
     # A 5 s window's edges each sit within one drain period of the integral's last known
     # point: a load that flips every 185 ms is billed within that, and 50 ± 1 from 50 Hz.
     assert _worst_window(trace, SQ) < 2 / (5 * hz) + 0.005
+
+
+@pytest.mark.parametrize("hz", [10, 100])
+def test_run_on_guess_stops_with_the_load(N, hz):
+    """A saturated 3 s load, then idle: the guess that runs the last drain on to each
+    PMFW sample is bounded by that interval's PMFW busy, so nothing is billed past the
+    load's end (r5j, 10 Hz: the unbounded guess billed 3 s of load as 3.04 s, for good —
+    a counter cannot take it back)."""
+    busy = lambda t: min(max(t - 1.0, 0.0), 3.0)  # noqa: E731
+    billed, b, trace = _simulate(N, hz, busy, secs=8.0, drain_jitter=0.0)
+    assert billed == pytest.approx(3.0, abs=0.005), billed
+    assert b.carry_s == pytest.approx(0.0, abs=1e-6)
+    # and the guess still keeps the billed integral current while the load runs
+    mid = [bl for fw, bl in trace if 2.0 <= fw <= 3.5]
+    fws = [fw for fw, bl in trace if 2.0 <= fw <= 3.5]
+    assert max(abs(bl - busy(fw)) for fw, bl in zip(fws, mid)) < 1.5 / hz + 0.02
 
 
 def test_clipping_each_interval_loses_busy_time(N):

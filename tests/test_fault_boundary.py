@@ -273,7 +273,7 @@ def test_injected_queue_stall_trips_the_breaker_and_a_fresh_queue_recovers(mock_
                 seen_failed = time.time() - t0
             if seen_failed is not None and ex.integrals(1)["pmc_failed"] == 0:
                 break
-            time.sleep(0.01)
+            time.sleep(0.02)
 
     th = threading.Thread(target=watch)
     th.start()
@@ -287,8 +287,12 @@ def test_injected_queue_stall_trips_the_breaker_and_a_fresh_queue_recovers(mock_
     assert all(b >= a for a, b in zip(totals, totals[1:])), totals               # monotonic throughout
     time.sleep(0.2)
     assert g0(parse_text(ex.render())) > totals[-1]                              # and counting again
-    assert pmc[0] >= 0.95 * HZ and pmfw[0] >= 40 and pmfw[1] >= 40, (pmc, pmfw)
-    assert ex.integrals(0)["pmc_breaker_trips"] == 0
+    # GPU 0 never waits on GPU 1's queue: no READ error, no trip, its rate kept (0.8: the
+    # watcher renders at 50 Hz and a loaded CI host steals the sampler's wake-ups — six
+    # concurrent runs of this test measured 0.91-0.95 of the rate)
+    assert pmc[0] >= 0.8 * HZ and pmfw[0] >= 40 and pmfw[1] >= 40, (pmc, pmfw)
+    i0 = ex.integrals(0)
+    assert i0["pmc_breaker_trips"] == 0 and i0["pmc_errors"] == 0, i0
 
 
 def _slow_fault_exporter(mock_exporter, **fault):
