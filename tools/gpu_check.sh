@@ -95,6 +95,12 @@ for s in $STEPS; do
                 umc_a,umc_b,mmea,gcea ;;
     gceaprobe) KGS_AQL_PROBE_OUT="$OUT/aql_probe_gcea.json" run aql_probe_gcea 400 python -u tools/aql_probe.py \
                 gcea0,gcea1,gcea2,gcea3,gcea4,gcea5,gcea6,gcea7 ;;
+    utilonly*) run $s 300 python -u bench.py --steps 5 --warmup 2 --rounds 2 --burst-s 0 --capacity-hz "" \
+                 --quiet-s 0 --component-s 0 --util-s 3 --out "$OUT/$s.json" ;;  # phase U, 8 kHz / 1 kHz / 10 Hz
+    lowrate) run lowrate_10 90 python -u tools/lowrate_probe.py --hz 10 --out "$OUT/lr_10.json"
+             run lowrate_10_sat 60 python -u tools/lowrate_probe.py --hz 10 --burst-ms 3000 --period-ms 3000 \
+               --load-s 3 --out "$OUT/lr_10_sat.json"
+             run lowrate_100 60 python -u tools/lowrate_probe.py --hz 100 --out "$OUT/lr_100.json" ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
