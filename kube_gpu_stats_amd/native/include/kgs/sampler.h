@@ -171,6 +171,14 @@ constexpr int64_t kReadOverlapNs = 400000;
 // exporter's READ mode) the 1 ms / 5 ms train read −2.2 / −2.7 / −2.6 points at 1 kHz /
 // 100 Hz / 10 Hz with the clock-ratio split, −0.5 / +1.4 / +1.5 with this.
 constexpr int64_t kTimeSplitNs = 400000;
+// ... and blended with the cycle share: the gaps between kernels clock between the
+// kernels' clock (the cycle share's assumption) and the learned idle clock (the time
+// split's), so the truth lies between the two.  Replayed on the r4f, r5b and r5l raw
+// READs (1 kHz / 100 Hz / 10 Hz, 1 ms / 5 ms and 0.2 ms / 1 ms trains), the worst error
+// is 2.7 points with the cycle share, 2.0 with the time split alone, 1.5 / 1.4 / 1.3 /
+// 1.5 at weights 0.5 / 0.6 / 0.7 / 0.8; 0.6 keeps the DaemonSet's 10 Hz and config 4's
+// 100 Hz within 0.3 (tests/test_estimator_replay.py).
+constexpr double kTimeSplitWeight = 0.6;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };

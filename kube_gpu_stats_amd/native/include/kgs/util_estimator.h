@@ -46,6 +46,10 @@ struct EstimatorParams {
   // (0 = never; the clock-ratio split above applies instead).
   int64_t time_split_ns = 0;
   double time_split_ratio_hi = 1.5;   // ... within f_idle / f_busy ≤ this (busy clock ≥ 0.67 × idle)
+  // ... and taken this far from the cycle share: the cycle share assumes the gaps ran
+  // at the kernels' clock, the time split that they ran at the learned idle clock; the
+  // truth lies between (1 = the time split alone).
+  double time_split_weight = 1.0;
   double ewma = 0.05;                 // weight of a new sample in every learned EWMA
   int64_t quiet_hold_ns = 5000000;    // quiet intervals in a row before the device counts as quiet
   double busy_min = 0.0;              // dispatch gap: SPI share below this (0 = off)
@@ -187,15 +191,20 @@ class DispatchEstimator {
         clk_busy_hz_ = clk_busy_hz_ > 0 ? (1 - p.ewma) * clk_busy_hz_ + p.ewma * hz_now : hz_now;
       } else if (p.time_split_ns > 0 && span_ns >= p.time_split_ns && share > 0 && clk_idle_hz_ > 0) {
         // A long interval at a low READ rate: many kernels and gaps, each part at its
-        // own clock (MFMA bursts power-capped at ≈2.1 GHz, gaps at ≈2.4).  The idle
-        // part's time is its cycles at the idle clock; the busy part is the rest.
-        // Bounded to busy clocks between f_idle / time_split_ratio_hi and f_idle /
-        // clock_ratio_lo: an idle stretch that clocked below the learned idle clock
-        // (a GPU left quiet long enough to drop its clock) must not read as busy.
+        // own clock (MFMA bursts power-capped at ≈2.1 GHz, gaps up to ≈2.4).  With the
+        // gaps at the learned idle clock, the idle part's time is its cycles at that
+        // clock and the busy part is the rest; bounded to busy clocks between f_idle /
+        // time_split_ratio_hi and f_idle / clock_ratio_lo, so an idle stretch that
+        // clocked below the learned idle clock (a GPU left quiet long enough to drop its
+        // clock) must not read as busy.  But gaps between kernels clock between the two
+        // (r5b, r5l dumps: 1 ms / 5 ms trains clock 2.28-2.32 GHz on average, 0.2 ms /
+        // 1 ms trains 2.34-2.37, against 2.41 idle), so the cycle share reads low and the
+        // time split high, by up to 2.2 and 2.0 points: time_split_weight blends them.
         const double idle_s = std::max(0.0, clk - busy) / clk_idle_hz_;
         const double t = 1.0 - idle_s / (span_ns * 1e-9);
         auto time_share = [share](double r) { return share * r / (1.0 - share + share * r); };
-        share = std::clamp(t, time_share(p.clock_ratio_lo), time_share(p.time_split_ratio_hi));
+        const double ts = std::clamp(t, time_share(p.clock_ratio_lo), time_share(p.time_split_ratio_hi));
+        share += p.time_split_weight * (ts - share);
       } else if (span_ns >= p.clock_split_ns && share > 0 && clk_busy_hz_ > 0 && clk_idle_hz_ > 0) {
         // A cycle share under-weights a kernel that ran at a lower clock than the idle
         // rest of the interval (MFMA under the power cap: ≈2.1 GHz against ≈2.4 idle):
