@@ -1633,13 +1633,13 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
     """the configuration users get.  The exporter runs with the
     DaemonSet's own arguments (deploy/daemonset.yaml: --hz=10 with the aqlprofile
     counter tier) and with the same at --hz=100 (BASELINE config 4), under idle, two
-    MFMA burst trains and a saturating MFMA load (6 s each, with 0.5 s idle edges).
+    MFMA burst trains and a saturating MFMA load (6 s each, with idle edges to 8 s).
     100·rate(container_gpu_busy_seconds_total) from the scrapes must read the kernels'
     event-timed duty — saturated ≥ 95 over the load alone and within ±3 of its duty with
     the edges, idle ≤ 1, both trains within ±3 points — and a fake Prometheus fed with
     scrapes every 100 ms, through `gpu-util-stats` fixed mode (the reference's per-pod
     mean, gpu_util_stats.py:62-94 over the series of :159), within ±4 (its extrapolated
-    rate() over a 7 s range)."""
+    rate() over an 8 s range)."""
     import threading
 
     from fakeprom import FakeProm
@@ -1656,7 +1656,7 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
     ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
     ls.run_mfma()
     loads = _mfma_loads(ls)
-    load_s, pre_s, tail_s = 6.0, 0.5, 0.5
+    load_s, pre_s, tail_s, range_s = 6.0, 0.5, 0.5, 8
     rows: dict = {}
     for tag, args in (("daemonset_10hz", shipped),
                       ("daemonset_100hz", [a if not a.startswith("--hz=") else "--hz=100" for a in shipped])):
@@ -1667,11 +1667,12 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
         sc2 = Scraper("127.0.0.1", ready["port"])
         cur = {"fp": None}
 
-        def scraper():  # Prometheus: a scrape every 100 ms into the current load's TSDB
-            while not stop.wait(0.1):
+        def scraper():  # Prometheus: a scrape every 100 ms into the current load's TSDB,
+            while not stop.wait(0.1):  # stamped with the scrape's start time, as Prometheus does
                 f = cur["fp"]
                 if f is not None:
-                    f.ingest(parse_text(sc2.get()), time.time())
+                    ts = time.time()
+                    f.ingest(parse_text(sc2.get()), ts)
 
         th = threading.Thread(target=scraper, daemon=True)
         th.start()
@@ -1682,29 +1683,36 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
                 # Every load has idle edges (its last burst's drain and PMFW table land
                 # inside the window, which the report's rate() covers); a saturating load
                 # is also read over the load alone, where ≥ 95 means the whole window.
+                # The window is just under the report's range, so its first scrape sits
+                # inside the range and rate() extrapolates over nothing but 20 ms: an
+                # edge scrape that misses the range makes rate() extrapolate only half a
+                # scrape interval there (r5n: −6 points on a saturated window whose exact
+                # counter read −0.04).
                 cur["fp"] = f = FakeProm()
-                m0, s0, w0 = parse_text(sc.get()), time.monotonic(), time.time()
+                s0, w0 = time.monotonic(), time.time()
+                m0 = parse_text(sc.get())
                 f.ingest(m0, w0)
                 time.sleep(pre_s)
                 ma, sa = parse_text(sc.get()), time.monotonic()
                 gpu_s = run(load_s)
                 mb, sb = parse_text(sc.get()), time.monotonic()
-                time.sleep(tail_s)
-                m1, s1, w1 = parse_text(sc.get()), time.monotonic(), time.time()
+                time.sleep(max(tail_s, s0 + range_s - 0.02 - time.monotonic()))
                 cur["fp"] = None
+                s1, w1 = time.monotonic(), time.time()
+                m1 = parse_text(sc.get())
                 f.ingest(m1, w1)
                 win = s1 - s0
+                assert win < range_s, win
                 d = lambda fam, **kw: one(m1, fam, **kw)[0] - one(m0, fam, **kw)[0]  # noqa: E731,B023
                 # the fixed report over this window: one step, rate() over it
                 furl = f.start()
-                q = G.Queries.amd("ml", int(round(win)))
+                q = G.Queries.amd("ml", range_s)
                 f.add_instant(q.total, [{"metric": {"node": "gpu-node-1", q.type_label: "MI355X"}, "value": [w1, "8"]}])
                 f.add_instant(q.used, [{"metric": {"node": "gpu-node-1"}, "value": [w1, "1"]}])
                 f.add_instant(q.live, [{"metric": {"namespace": "ml", "pod": "train-0"}, "value": [w1, "1"]}])
                 f.add_range(q.req, [{"metric": {"node": "gpu-node-1", "namespace": "ml", "pod": "train-0"},
                                      "values": [[w1, "1"]]}])
-                rep = G.run_report(PromClient(furl), q, w1,
-                                   int(round(win)), int(round(win)), compat=False, out=open(os.devnull, "w"))
+                rep = G.run_report(PromClient(furl), q, w1, range_s, range_s, compat=False, out=open(os.devnull, "w"))
                 f.stop()
                 busy_load = one(mb, "container_gpu_busy_seconds_total")[0] - one(ma, "container_gpu_busy_seconds_total")[0]
                 rows[f"{tag}/{name}"] = r = {
@@ -1729,7 +1737,7 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
         idle, sat = rows[f"{tag}/idle"], rows[f"{tag}/mfma_saturating"]
         assert idle["busy_counter_pct"] <= 1.0 and idle["report_pct"] <= 1.0, idle
         assert sat["load_only_busy_pct"] >= 95.0, sat
-        # the report is Prometheus' extrapolated rate() over a 7 s range of a counter that
+        # the report is Prometheus' extrapolated rate() over an 8 s range of a counter that
         # advances in 100 ms PMFW steps at 10 Hz: held to ±4, the exact counter to ±3
         assert abs(sat["error_pts"]) <= 3.0 and abs(sat["report_pct"] - sat["duty_gpu_pct"]) <= 4.0, sat
         for name in ("burst_1ms_every_5ms", "burst_0.2ms_every_1ms"):
