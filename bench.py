@@ -73,9 +73,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--hz", type=float, default=8000.0,
+    ap.add_argument("--hz", type=float, default=16000.0,
                     help="primary sampler tick rate per GPU (phase B): one hardware-counter drain per tick "
-                    "(PMFW table ≤ 100 Hz); 8 kHz costs ≈0.05 exporter cores/GPU (profiles/r1/pipelined)")
+                    "(PMFW table ≤ 100 Hz); 16 kHz costs ≈0.07 exporter cores/GPU and no GPU time against the "
+                    "released baseline (profiles/r5/r5i), 8 kHz ≈0.05")
     ap.add_argument("--hz-list", default="100",
                     help="further tick rates measured in the interleaved rounds (BASELINE config 4 = 100 Hz); "
                     "'' = primary only")
@@ -89,7 +90,8 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-busy-min", type=float, default=0.0,
                     help="exporter --pmc-busy-min: READ at --pmc-gap-hz while the SPI-busy share is below this")
     ap.add_argument("--pmc-gap-hz", type=float, default=1000.0, help="exporter --pmc-gap-hz")
-    ap.add_argument("--pmc-batch", type=int, default=8, help="exporter --pmc-batch: counter READs per L2 writeback")
+    ap.add_argument("--pmc-batch", type=int, default=16,
+                    help="exporter --pmc-batch: counter READs per L2 writeback (16 at 16 kHz: one per ms)")
     ap.add_argument("--pmc-publish-us", type=int, default=1000, help="exporter --pmc-publish-us")
     ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
@@ -128,8 +130,8 @@ def parse_args(argv=None):
     ap.add_argument("--xgmi-bdfs", default="", help=argparse.SUPPRESS)
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--burst-s", type=float, default=0.6,
-                    help="phase R: length of the MFMA burst train read back from /counters (0 = off; the "
-                    "full-rate ring holds ≈1 s at 8 kHz)")
+                    help="phase R: length of the MFMA burst train read back from /counters (0 = off; cut to "
+                    "what the full-rate ring holds: ≈0.5 s at 16 kHz)")
     ap.add_argument("--burst-ms", type=float, default=1.0, help="phase R: length of one burst")
     ap.add_argument("--burst-period-ms", type=float, default=5.0, help="phase R: burst period")
     ap.add_argument("--capacity-hz", default="16000,24000,32000",
@@ -1200,6 +1202,9 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
     return out
 
 
+RING = 8190  # drains /counters returns at most (native kPmcRing 8192, less the write slot)
+
+
 def burst_train(ctx, load, exp, a) -> dict:
     """Phase R — what the primary rate resolves ("the headline value is a
     dial").  Every rank fires a train of ≈``--burst-ms`` MFMA kernels, one every
@@ -1215,9 +1220,12 @@ def burst_train(ctx, load, exp, a) -> dict:
         exp.set_idle_hz(0)  # profiling mode: READ every tick
     D.barrier(ctx)
     period = a.burst_period_ms * 1e-3
+    # /counters keeps the last RING drains: the train must fit in them (8190 drains are
+    # 1.0 s at 8 kHz, 0.51 s at 16 kHz — r5i resolved 102 of 120 bursts of a 0.6 s train)
+    train_s = min(a.burst_s, 0.8 * RING / a.hz) if a.hz > 0 else a.burst_s
     bursts: list[tuple[int, int]] = []
     nxt = time.monotonic()
-    t_end = nxt + a.burst_s
+    t_end = nxt + train_s
     while time.monotonic() < t_end:
         t0 = time.monotonic_ns()
         load.burst(a.burst_ms)
@@ -1241,7 +1249,7 @@ def burst_train(ctx, load, exp, a) -> dict:
         g = gpu_of.get(bdf)
         if g is None or not bs:
             continue
-        body = json.load(urllib.request.urlopen(f"{base}/counters?gpu={g}&n=8190", timeout=10))
+        body = json.load(urllib.request.urlopen(f"{base}/counters?gpu={g}&n={RING}", timeout=10))
         lo, hi = bs[0][0] - 2_000_000, bs[-1][1] + 2_000_000
         win = [x for x in body.get("samples", []) if lo <= x["mono_ns"] <= hi]
         segs, busy, span = segments(win)
@@ -1253,7 +1261,7 @@ def burst_train(ctx, load, exp, a) -> dict:
                   "median_segment_ms": med([e - s for s, e in segs]),
                   "duty_host": round(sum(e - s for s, e in bs) * 1e-9 / span, 4) if span else None,
                   "duty_counters": round(busy / span, 4) if span else None}
-    return {"burst_ms": a.burst_ms, "period_ms": a.burst_period_ms, "train_s": a.burst_s,
+    return {"burst_ms": a.burst_ms, "period_ms": a.burst_period_ms, "train_s": round(train_s, 3),
             "mode": "profiling (--pmc-idle-hz 0: every tick READs)", "mock": bool(a.mock), "per_gpu": per}
 
 
@@ -1457,7 +1465,7 @@ def capacity(ctx, load, exp, a) -> dict:
     idle_hz = exp.set_idle_hz(-1) if exp is not None else 0.0
     if exp is not None:
         exp.set_idle_hz(0)
-    for hz in [a.hz] + rates:
+    for hz in [a.hz] + [r for r in rates if r != a.hz]:
         w0 = 0.0
         before: dict = {}
         if exp is not None:
