@@ -73,10 +73,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--hz", type=float, default=16000.0,
+    ap.add_argument("--hz", type=float, default=8000.0,
                     help="primary sampler tick rate per GPU (phase B): one hardware-counter drain per tick "
-                    "(PMFW table ≤ 100 Hz); 16 kHz costs ≈0.07 exporter cores/GPU and no GPU time against the "
-                    "released baseline (profiles/r5/r5i), 8 kHz ≈0.05")
+                    "(PMFW table ≤ 100 Hz); 8 kHz costs ≈0.05 exporter cores/GPU; 16 kHz (with --pmc-batch 16) "
+                    "≈0.07 and +0.1 %% GPU time vs paused, +0.01 %% vs released (profiles/r5/r5o)")
     ap.add_argument("--hz-list", default="100",
                     help="further tick rates measured in the interleaved rounds (BASELINE config 4 = 100 Hz); "
                     "'' = primary only")
@@ -90,8 +90,8 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-busy-min", type=float, default=0.0,
                     help="exporter --pmc-busy-min: READ at --pmc-gap-hz while the SPI-busy share is below this")
     ap.add_argument("--pmc-gap-hz", type=float, default=1000.0, help="exporter --pmc-gap-hz")
-    ap.add_argument("--pmc-batch", type=int, default=16,
-                    help="exporter --pmc-batch: counter READs per L2 writeback (16 at 16 kHz: one per ms)")
+    ap.add_argument("--pmc-batch", type=int, default=8,
+                    help="exporter --pmc-batch: counter READs per L2 writeback (8 at 8 kHz: one per ms)")
     ap.add_argument("--pmc-publish-us", type=int, default=1000, help="exporter --pmc-publish-us")
     ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
                     help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
@@ -131,7 +131,7 @@ def parse_args(argv=None):
     ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
     ap.add_argument("--burst-s", type=float, default=0.6,
                     help="phase R: length of the MFMA burst train read back from /counters (0 = off; cut to "
-                    "what the full-rate ring holds: ≈0.5 s at 16 kHz)")
+                    "what the full-rate ring holds: ≈1 s at 8 kHz, 0.5 s at 16 kHz)")
     ap.add_argument("--burst-ms", type=float, default=1.0, help="phase R: length of one burst")
     ap.add_argument("--burst-period-ms", type=float, default=5.0, help="phase R: burst period")
     ap.add_argument("--capacity-hz", default="16000,24000,32000",

@@ -60,8 +60,8 @@ def _rate_ok(v: float, hz: float) -> bool:
     return MIN_8K * hz < v <= 1.02 * hz
 
 
-# The mock runs at 8 kHz (bench.py's default primary rate is 16 kHz, with 16 READs per
-# batch): this 8-CPU VM cannot hold 16 kHz for several mock GPUs at once.
+# The mock runs at bench.py's default 8 kHz, stated here so that the tests do not follow a
+# change of the default: this 8-CPU VM cannot hold 16 kHz for several mock GPUs at once.
 FAST = ["--hz", "8000", "--pmc-batch", "8", "--step-ms", "60", "--rounds", "4", "--block-steps", "1", "--settle",
         "0.3", "--util-hz", ""]
 
