@@ -574,6 +574,25 @@ def test_quiet_gpu_counter_reads_drop_to_idle_rate(mock_exporter):
     assert w["gpu_active_pct"] == pytest.approx(25, abs=4), w      # the integral is exact at any READ rate
 
 
+def test_learned_shader_clocks_are_exported(mock_exporter):
+    """kgs_pmc_shader_clock_hz: the clocks the dispatch estimator learned (idle on READ-only
+    intervals, busy on fully busy ones) — what the time split of long intervals prices idle
+    cycles at.  The mock counts GRBM_COUNT at its 2100 MHz throughout."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0,
+                       mock={"square_duty": 0.5, "util_period_s": 0.2, "util_base": 50, "util_amp": 50})
+    time.sleep(1.0)
+    m = parse_text(ex.render())
+    clk = {lb["kind"]: v for lb, v in m["kgs_pmc_shader_clock_hz"]}
+    assert set(clk) == {"idle", "busy"}, clk
+    assert clk["idle"] == pytest.approx(2.1e9, rel=0.02) and clk["busy"] == pytest.approx(2.1e9, rel=0.02), clk
+    i = ex.integrals(0)
+    assert i["pmc_clk_idle_hz"] == pytest.approx(clk["idle"], rel=0.05)
+    # one clock everywhere: the time split, the cycle share and their blend agree, so the
+    # square wave bills its duty
+    w = ex.window(0, 0.8)
+    assert w["util_pct"] == pytest.approx(50, abs=6), w
+
+
 def test_dispatch_gap_reads_drop_to_gap_rate(mock_exporter):
     """Dispatch-gap READ rate (--pmc-busy-min): each READ packet delays the workload's
     dispatches, and a READ whose IB is all NOPs costs a training step as much as a
