@@ -202,7 +202,7 @@ class DispatchEstimator {
         // time split high, by up to 2.2 and 2.0 points: time_split_weight blends them.
         const double idle_s = std::max(0.0, clk - busy) / clk_idle_hz_;
         const double t = 1.0 - idle_s / (span_ns * 1e-9);
-        auto time_share = [share](double r) { return share * r / (1.0 - share + share * r); };
+        auto time_share = [share](double ratio) { return share * ratio / (1.0 - share + share * ratio); };
         const double ts = std::clamp(t, time_share(p.clock_ratio_lo), time_share(p.time_split_ratio_hi));
         share += p.time_split_weight * (ts - share);
       } else if (span_ns >= p.clock_split_ns && share > 0 && clk_busy_hz_ > 0 && clk_idle_hz_ > 0) {
