@@ -1337,9 +1337,13 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         # the carry a saturated load holds (≤ one interval's worth, billed ≤ dt per
         # interval) land inside it — r5k: a tail of two read a saturated 10 Hz window
         # 2.7 points low where the same load over a long window bills to 0.1 %
-        # (profiles/r5/r5k/lr_10_sat.json).  The duty counts the tail as idle.
+        # (profiles/r5/r5k/lr_10_sat.json).  At any rate the billing runs on the PMFW
+        # thread (≤ 100 Hz, tables every ≈20 ms), so the integral a scrape sees lags the
+        # drains by up to a few tens of ms: 50 ms of tail at least, or a saturated 1.5 s
+        # window reads that lag as 0.5-0.9 points of missing busy.  The duty counts the
+        # tail as idle.
         secs = max(a.util_s, 30.0 / hz)
-        tail = 5.0 / hz if hz < 100 else 0.0
+        tail = max(5.0 / hz, 0.05)
         for name, spec in plan:
             load.sync()
             D.cpu_barrier(ctx)  # no RCCL kernel inside the window
@@ -1363,8 +1367,7 @@ def util_accuracy(ctx, load, exp, a) -> dict:
                     d = nxt - time.monotonic()
                     if d > 0:
                         time.sleep(d)
-            if spec != "sat" or tail > 0:
-                time.sleep(tail)
+            time.sleep(tail)
             own = (gpu_s, host_s, time.perf_counter() - t0)
             D.cpu_barrier(ctx)
             m1, w1 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
