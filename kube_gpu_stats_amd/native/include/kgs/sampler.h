@@ -179,6 +179,12 @@ constexpr int64_t kTimeSplitNs = 400000;
 // 1.5 at weights 0.5 / 0.6 / 0.7 / 0.8; 0.6 keeps the DaemonSet's 10 Hz and config 4's
 // 100 Hz within 0.3 (tests/test_estimator_replay.py).
 constexpr double kTimeSplitWeight = 0.6;
+// ... unless READ-only intervals taught the idle clock within this long before the
+// interval: READ-only intervals among the kernels (a 1 ms train at 1 kHz: 3-4 of every 5
+// intervals) measure the gaps' own clock, and the time split alone is right there (the
+// three dumps' 1 kHz 1 ms trains: −0.55 / −1.41 / −0.17 points blended, +0.02 / −0.90 /
+// +0.02 with this; at 100 Hz and 10 Hz no READ-only interval falls inside a train).
+constexpr int64_t kGapClockFreshNs = 10000000;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };

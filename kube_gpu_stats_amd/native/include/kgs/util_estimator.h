@@ -50,6 +50,10 @@ struct EstimatorParams {
   // at the kernels' clock, the time split that they ran at the learned idle clock; the
   // truth lies between (1 = the time split alone).
   double time_split_weight = 1.0;
+  // ... unless the idle clock was learned this recently before the interval (0 = never):
+  // READ-only intervals among the kernels measure the clock of the gaps themselves
+  // (1 ms bursts every 5 ms at 1 kHz), and the time split alone is then right.
+  int64_t gap_clock_fresh_ns = 0;
   double ewma = 0.05;                 // weight of a new sample in every learned EWMA
   int64_t quiet_hold_ns = 5000000;    // quiet intervals in a row before the device counts as quiet
   double busy_min = 0.0;              // dispatch gap: SPI share below this (0 = off)
@@ -168,7 +172,10 @@ class DispatchEstimator {
         r.learned = true;
         if (f) cpc_read_us_ = read_cyc_[m][f] / (hz_now * 1e-6);
         // the idle clock between kernels, not a quiet GPU's (its clock drops: r4r)
-        if (!d.fresh_mode) clk_idle_hz_ = clk_idle_hz_ > 0 ? (1 - p.ewma) * clk_idle_hz_ + p.ewma * hz_now : hz_now;
+        if (!d.fresh_mode) {
+          clk_idle_hz_ = clk_idle_hz_ > 0 ? (1 - p.ewma) * clk_idle_hz_ + p.ewma * hz_now : hz_now;
+          idle_learned_ns_ = d.mono_ns;
+        }
       }
       // This READ's learned cost, or the other kind's before it has its own.
       const int k = read_n_[m][f] ? f : 1 - f;
@@ -199,12 +206,16 @@ class DispatchEstimator {
         // clock) must not read as busy.  But gaps between kernels clock between the two
         // (r5b, r5l dumps: 1 ms / 5 ms trains clock 2.28-2.32 GHz on average, 0.2 ms /
         // 1 ms trains 2.34-2.37, against 2.41 idle), so the cycle share reads low and the
-        // time split high, by up to 2.2 and 2.0 points: time_split_weight blends them.
+        // time split high, by up to 2.2 and 2.0 points: time_split_weight blends them —
+        // unless READ-only intervals among these kernels taught the idle clock just now
+        // (gap_clock_fresh_ns): then it is the gaps' own clock.
         const double idle_s = std::max(0.0, clk - busy) / clk_idle_hz_;
         const double t = 1.0 - idle_s / (span_ns * 1e-9);
         auto time_share = [share](double ratio) { return share * ratio / (1.0 - share + share * ratio); };
         const double ts = std::clamp(t, time_share(p.clock_ratio_lo), time_share(p.time_split_ratio_hi));
-        share += p.time_split_weight * (ts - share);
+        const bool gap_clock = p.gap_clock_fresh_ns > 0 && idle_learned_ns_ > 0 && prev_ns_ >= idle_learned_ns_ &&
+                               prev_ns_ - idle_learned_ns_ <= p.gap_clock_fresh_ns;
+        share += (gap_clock ? 1.0 : p.time_split_weight) * (ts - share);
       } else if (span_ns >= p.clock_split_ns && share > 0 && clk_busy_hz_ > 0 && clk_idle_hz_ > 0) {
         // A cycle share under-weights a kernel that ran at a lower clock than the idle
         // rest of the interval (MFMA under the power cap: ≈2.1 GHz against ≈2.4 idle):
@@ -271,6 +282,7 @@ class DispatchEstimator {
   uint64_t read_n_[2][2] = {};
   double cpc_read_us_ = 0;
   double clk_busy_hz_ = 0, clk_idle_hz_ = 0;
+  int64_t idle_learned_ns_ = 0;  // the drain that last taught clk_idle_hz_
   bool quiet_ = false, gap_ = false, dbound_ = false;
   int64_t quiet_since_ = 0, gap_since_ = 0, dbound_since_ = 0;
   int64_t last_plausible_ns_ = 0;

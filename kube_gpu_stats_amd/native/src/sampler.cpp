@@ -64,6 +64,7 @@ EstimatorParams estimator_params(const SamplerConfig& cfg, int num_cu) {
   p.read_overlap_ns = kReadOverlapNs;
   p.time_split_ns = kTimeSplitNs;
   p.time_split_weight = kTimeSplitWeight;
+  p.gap_clock_fresh_ns = kGapClockFreshNs;
   p.quiet_hold_ns = kQuietHoldNs;
   p.busy_min = cfg.pmc_busy_min;
   p.gap_hold_ns = static_cast<int64_t>(cfg.pmc_gap_hold_s * 1e9);

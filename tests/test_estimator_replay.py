@@ -90,6 +90,12 @@ def test_low_rate_reads_in_the_exporters_read_mode_stay_within_two_points():
         assert abs(now[rate]["burst_1_5"]["err_pts"]) < abs(old[rate]["burst_1_5"]["err_pts"]) - 0.5
     # the time split alone: the r5l 0.2 ms train reads ≈ 2 points high
     assert _worst_train_error({"time_split_weight": 1.0}) > worst + 0.5
+    # the blend where READ-only intervals among the kernels just measured the gaps' clock:
+    # the 1 kHz 1 ms trains read up to 0.5 points lower
+    fresh, stale = sim.replay(LOWRATE), sim.replay(LOWRATE, {"gap_clock_fresh_ns": 0})
+    assert fresh["1000"]["burst_1_5"]["err_pts"] > stale["1000"]["burst_1_5"]["err_pts"] + 0.3, (fresh, stale)
+    for rate in ("100", "10"):  # no READ-only interval inside a train at these rates
+        assert fresh[rate]["burst_1_5"]["err_pts"] == stale[rate]["burst_1_5"]["err_pts"]
 
 
 @pytest.mark.parametrize("override, load, rate", [
@@ -107,7 +113,7 @@ def test_replay_is_the_samplers_code(N):
     p = N.sampler_estimator_params()
     assert p.cpc_full_frac == pytest.approx(0.90) and p.quiet_active_frac == pytest.approx(0.02)
     assert p.read_overlap_ns == 400000 and p.clock_split_ns == 400000 and p.time_split_ns == 400000
-    assert p.time_split_weight == pytest.approx(0.6)
+    assert p.time_split_weight == pytest.approx(0.6) and p.gap_clock_fresh_ns == 10_000_000
     assert p.cp_only_min == pytest.approx(0.3) and p.num_simds == 1024
     src = open(os.path.join(REPO, "tools", "util_estimator_sim.py")).read()
     assert "DispatchEstimator" in src and "0.95 *" not in src  # no re-implemented EWMA
