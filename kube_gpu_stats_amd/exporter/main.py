@@ -110,6 +110,9 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                      "(kgs_pmc_failed = 1: READs stop, the reader's queue is recreated)")
     add_flag(ap, "pmc-retry-s", 1.0, "first retry (reset + re-START) after the breaker opened; doubles per failed retry")
     add_flag(ap, "pmc-retry-max-s", 60.0, "longest retry interval of the counter tier's breaker")
+    add_flag(ap, "tick-dither", 0.25, "counter-tick dither: each READ deadline random-walks off the fixed grid by up "
+                                     "to this share of a period per tick (within half a period), so the READ phase "
+                                     "does not lock onto a periodic workload; the rate stays exact (0 = fixed grid)")
     add_flag(ap, "stop-timeout", 1.0, "shutdown waits this long for the sampler threads, then abandons any stuck in a "
                                       "device call (the exporter still exits on SIGTERM during a GPU hang)")
     add_flag(ap, "listen", "0.0.0.0:9400", "HTTP listen address (port 0 = ephemeral)")
@@ -207,6 +210,7 @@ def config_from_args(a) -> dict:
         "pmc_retry_s": a.pmc_retry_s,
         "pmc_retry_max_s": a.pmc_retry_max_s,
         "stop_timeout_s": a.stop_timeout,
+        "tick_dither": a.tick_dither,
         "listen_addr": host or "0.0.0.0",
         "port": int(port),
         "node_name": a.node_name,

@@ -37,6 +37,7 @@
 // scrape path never calls into the driver.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <map>
@@ -124,10 +125,45 @@ struct SamplerConfig {
   double pmc_retry_s = 1.0, pmc_retry_max_s = 60.0;
   // stop() waits this long for the sampler threads, then abandons the stuck ones.
   double stop_timeout_s = 1.0;
+  // Counter-tick dither: each tick's deadline sits off the fixed grid by an offset
+  // that random-walks (± tick_dither of a period per tick, reflected at ± half a
+  // period), so the READ phase does not lock onto a periodic workload (a kernel
+  // every 1 ms against a 125 µs tick keeps one phase for seconds, and the per-interval
+  // rules then err the same way on every kernel).  The grid keeps the long-run rate
+  // exact.  0 = a fixed grid.
+  double tick_dither = 0.25;
 };
 
 constexpr double kMaxHz = 100000.0;     // tick-rate ceiling accepted at run time (set_hz)
 constexpr double kMinIdleHz = 0.01;     // pmc_idle_hz: 0 (off) or at least this
+
+// The counter tick's dithered offset from its fixed grid (SamplerConfig::tick_dither): a
+// random walk of at most `dither` of a period per tick, reflected into ± half a period.
+class TickDither {
+ public:
+  explicit TickDither(uint64_t seed) : rng_(seed ? seed : 0x9E3779B97F4A7C15ull) {}
+  // The next tick's offset (ns) for a grid period of period_ns.
+  double step(int64_t period_ns, double dither) {
+    if (!(dither > 0)) return off_ = 0;
+    const double half = 0.5 * static_cast<double>(period_ns);
+    off_ += uniform() * std::min(dither, 0.5) * static_cast<double>(period_ns);
+    if (off_ > half) off_ = 2 * half - off_;
+    if (off_ < -half) off_ = -2 * half - off_;
+    return off_;
+  }
+  void reset() { off_ = 0; }
+  double offset() const { return off_; }
+
+ private:
+  double uniform() {  // xorshift64*: [-1, 1)
+    rng_ ^= rng_ >> 12;
+    rng_ ^= rng_ << 25;
+    rng_ ^= rng_ >> 27;
+    return static_cast<double>((rng_ * 0x2545F4914F6CDD1Dull) >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+  }
+  uint64_t rng_;
+  double off_ = 0;
+};
 
 constexpr size_t kRing = 1024;          // ≥10 s of history at 100 Hz
 // Counter samples decimated to one per kPmcSlowNs feed the window gauges, so a

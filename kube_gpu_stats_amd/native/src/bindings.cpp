@@ -96,6 +96,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmc_retry_s = get<double>(d, "pmc_retry_s", c.sampler.pmc_retry_s);
   c.sampler.pmc_retry_max_s = get<double>(d, "pmc_retry_max_s", c.sampler.pmc_retry_max_s);
   c.sampler.stop_timeout_s = get<double>(d, "stop_timeout_s", c.sampler.stop_timeout_s);
+  c.sampler.tick_dither = get<double>(d, "tick_dither", c.sampler.tick_dither);
   c.bdfs = get<std::vector<std::string>>(d, "bdfs", c.bdfs);
   c.pmc_source = get<std::string>(d, "pmc_source", c.pmc_source);
   c.pmc_lib = get<std::string>(d, "pmc_lib", c.pmc_lib);

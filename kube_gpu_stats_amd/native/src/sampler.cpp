@@ -583,7 +583,9 @@ void Sampler::run_pmc(Worker& w) {
   EstimatorParams ep = estimator_params(cfg_, info.num_cu);
   DispatchEstimator est;
   est.invalidate(mono_ns());
-  int64_t next = mono_ns();
+  int64_t grid = mono_ns();  // the fixed tick grid; next = grid + the dithered offset
+  int64_t next = grid;
+  TickDither dither(0x9E3779B97F4A7C15ull ^ (static_cast<uint64_t>(dev) << 32) ^ static_cast<uint64_t>(grid));
   PmcSample& pmc_base = st.pmc_base;
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
   int64_t last_pmc_ns = 0;
@@ -787,7 +789,8 @@ void Sampler::run_pmc(Worker& w) {
     // Nothing to READ (handed over / breaker open): poll the hand-over flag and the
     // retry deadline at ≤ 100 Hz instead of every tick.
     if (!st.pmc_on.load(std::memory_order_relaxed)) step = std::max<int64_t>(period_ns, 10000000LL);
-    next += step;
+    grid += step;
+    next = grid + static_cast<int64_t>(dither.step(period_ns, cfg_.tick_dither));
     const int64_t now = mono_ns();
     if (next <= now) {
       ++P.overruns;
@@ -795,7 +798,10 @@ void Sampler::run_pmc(Worker& w) {
       // absolute schedule, so the missed ticks run at once and the delivered rate
       // stays the configured one.  Further behind, the rate is beyond the work (or
       // the host stalled): re-anchor and sleep a quarter period instead of bursting.
-      if (now - next > kCatchUpPeriods * step) next = now + period_ns / 4;
+      if (now - next > kCatchUpPeriods * step) {
+        grid = next = now + period_ns / 4;
+        dither.reset();
+      }
     }
     st.pmc_integ.store(P);
     // Sleep until the absolute deadline or until stop() signals the eventfd.

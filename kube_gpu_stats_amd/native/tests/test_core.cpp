@@ -1062,9 +1062,32 @@ static void test_util_biller() {
   CHECK(!r.from_counters && std::abs(r.billed_s - 0.015) < 1e-12 && b.carry_s() == 0.0);
 }
 
+// TickDither: the offset stays within half a period, moves at most `dither` of a period
+// per tick, spreads over the whole period (the READ phase cannot lock onto a periodic
+// load) and averages out (the grid keeps the rate); dither 0 is the fixed grid.
+static void test_tick_dither() {
+  TickDither d(42);
+  const int64_t period = 125000;
+  double prev = 0, sum = 0;
+  int bins[8] = {};
+  const int n = 200000;
+  for (int i = 0; i < n; ++i) {
+    const double o = d.step(period, 0.25);
+    CHECK(std::abs(o) <= 0.5 * period + 1e-6);
+    CHECK(std::abs(o - prev) <= 0.25 * period + 1e-6);
+    prev = o;
+    sum += o;
+    ++bins[std::min(7, static_cast<int>((o + 0.5 * period) / period * 8))];
+  }
+  CHECK(std::abs(sum / n) < 0.05 * period);
+  for (int b : bins) CHECK(b > n / 8 / 2);  // every eighth of the period visited often
+  CHECK(d.step(period, 0.0) == 0.0 && d.offset() == 0.0);
+}
+
 int main() {
   test_dispatch_estimator();
   test_util_biller();
+  test_tick_dither();
   test_lite_ib();
   test_batch_plan();
   test_reserve_slot();

@@ -593,6 +593,23 @@ def test_learned_shader_clocks_are_exported(mock_exporter):
     assert w["util_pct"] == pytest.approx(50, abs=6), w
 
 
+def test_counter_tick_dither_keeps_the_rate(mock_exporter):
+    """--tick-dither: each counter tick's deadline random-walks off the fixed grid (≤ a
+    quarter period per tick, within half a period; native TickDither, test_core.cpp), so
+    the READ phase does not lock onto a periodic workload (tools/phase_probe.py, r5t: the
+    window-to-window spread of a 0.2 ms / 1 ms train at 8 kHz fell from 0.60 to 0.08
+    points); the grid keeps the delivered rate the configured one."""
+    for dither in (0.25, 0.0):
+        ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=0,
+                           tick_dither=dither, mock={"util_base": 50, "util_amp": 0})
+        time.sleep(0.3)
+        n0, t0 = ex.integrals(0)["pmc_samples"], time.monotonic()
+        time.sleep(1.5)
+        rate = (ex.integrals(0)["pmc_samples"] - n0) / (time.monotonic() - t0)
+        ex.stop()
+        assert 0.9 * 1000 <= rate <= 1.01 * 1000, (dither, rate)
+
+
 def test_dispatch_gap_reads_drop_to_gap_rate(mock_exporter):
     """Dispatch-gap READ rate (--pmc-busy-min): each READ packet delays the workload's
     dispatches, and a READ whose IB is all NOPs costs a training step as much as a

@@ -97,6 +97,8 @@ for s in $STEPS; do
                 gcea0,gcea1,gcea2,gcea3,gcea4,gcea5,gcea6,gcea7 ;;
     utilonly*) run $s 300 python -u bench.py --steps 5 --warmup 2 --rounds 2 --burst-s 0 --capacity-hz "" \
                  --quiet-s 0 --component-s 0 --util-s 3 --out "$OUT/$s.json" ;;  # phase U, 8 kHz / 1 kHz / 10 Hz
+    phase) run phase_8k 200 python -u tools/phase_probe.py --out "$OUT/phase_8k.json"
+           run phase_8k_1ms 200 python -u tools/phase_probe.py --burst-ms 1 --period-ms 5 --out "$OUT/phase_8k_1ms.json" ;;
     lowrate) run lowrate_10 90 python -u tools/lowrate_probe.py --hz 10 --out "$OUT/lr_10.json"
              run lowrate_10_sat 60 python -u tools/lowrate_probe.py --hz 10 --burst-ms 3000 --period-ms 3000 \
                --load-s 3 --out "$OUT/lr_10_sat.json"
