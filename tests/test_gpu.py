@@ -1635,8 +1635,9 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
     counter tier) and with the same at --hz=100 (BASELINE config 4), under idle, two
     MFMA burst trains and a saturating MFMA load (6 s each, with idle edges to 8 s).
     100·rate(container_gpu_busy_seconds_total) from the scrapes must read the kernels'
-    event-timed duty — saturated ≥ 95 of the load's duration (the window's busy, idle edges included) and within ±3 of its duty with
-    the edges, idle ≤ 1, both trains within ±3 points — and a fake Prometheus fed with
+    event-timed duty — saturated ≥ 95 of the load's duration (the window's busy, idle
+    edges included) and within ±3 of its duty over the window, idle ≤ 1, both trains
+    within ±3 points — and a fake Prometheus fed with
     scrapes every 100 ms, through `gpu-util-stats` fixed mode (the reference's per-pod
     mean, gpu_util_stats.py:62-94 over the series of :159), within ±4 (its extrapolated
     rate() over an 8 s range)."""
