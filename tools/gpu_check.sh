@@ -99,6 +99,9 @@ for s in $STEPS; do
                  --quiet-s 0 --component-s 0 --util-s 3 --out "$OUT/$s.json" ;;  # phase U, 8 kHz / 1 kHz / 10 Hz
     phase) run phase_8k 200 python -u tools/phase_probe.py --out "$OUT/phase_8k.json"
            run phase_8k_1ms 200 python -u tools/phase_probe.py --burst-ms 1 --period-ms 5 --out "$OUT/phase_8k_1ms.json" ;;
+    phaselow) run phase_1k 200 python -u tools/phase_probe.py --hz 1000 --out "$OUT/phase_1k.json"
+              run phase_100 300 python -u tools/phase_probe.py --hz 100 --burst-ms 1 --period-ms 5 --window-s 2 \
+                --windows 10 --out "$OUT/phase_100.json" ;;
     lowrate) run lowrate_10 90 python -u tools/lowrate_probe.py --hz 10 --out "$OUT/lr_10.json"
              run lowrate_10_sat 60 python -u tools/lowrate_probe.py --hz 10 --burst-ms 3000 --period-ms 3000 \
                --load-s 3 --out "$OUT/lr_10_sat.json"
