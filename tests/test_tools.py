@@ -124,3 +124,12 @@ def test_util_estimator_sim_replays_a_synthetic_dump(tmp_path, capsys):
     assert out["idle"]["busy_pct"] < 0.5
     b = out["burst_1_5"]
     assert b["busy_pct"] == pytest.approx(20.0, abs=0.5), b
+
+
+@pytest.mark.parametrize("tool", ["lowrate_probe.py", "phase_probe.py", "util_estimator_sim.py", "cp_busy_probe.py"])
+def test_round5_probes_parse_their_arguments_before_touching_a_gpu(tool):
+    """The GPU probes of round 5 answer --help on a machine without a GPU (argparse before
+    any torch / HIP import)."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", tool), "--help"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0 and "usage" in r.stdout.lower(), r.stderr[-500:]
