@@ -126,10 +126,10 @@ def test_util_estimator_sim_replays_a_synthetic_dump(tmp_path, capsys):
     assert b["busy_pct"] == pytest.approx(20.0, abs=0.5), b
 
 
-@pytest.mark.parametrize("tool", ["lowrate_probe.py", "phase_probe.py", "util_estimator_sim.py", "cp_busy_probe.py"])
-def test_round5_probes_parse_their_arguments_before_touching_a_gpu(tool):
-    """The GPU probes of round 5 answer --help on a machine without a GPU (argparse before
-    any torch / HIP import)."""
+@pytest.mark.parametrize("tool", sorted(f for f in os.listdir(os.path.join(REPO, "tools")) if f.endswith(".py")))
+def test_every_tool_answers_help_without_a_gpu(tool):
+    """Every evidence tool answers --help on a machine without a GPU (argparse, or the
+    docstring of a one-off probe, before any torch / HIP call)."""
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", tool), "--help"], capture_output=True, text=True,
                        timeout=60)
     assert r.returncode == 0 and "usage" in r.stdout.lower(), r.stderr[-500:]

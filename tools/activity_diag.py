@@ -5,6 +5,12 @@ process' load; prints the per-phase mean GPU-active and MFMA util from /counters
 
     python tools/activity_diag.py
 """
+
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
 import json, os, subprocess, sys, time, urllib.request
 sys.path.insert(0, ".")
 import torch

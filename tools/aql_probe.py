@@ -11,6 +11,12 @@ be checked against them (64 B / 128 B requests).
 """
 from __future__ import annotations
 
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
+
 import ctypes
 import glob
 import json

@@ -1,5 +1,11 @@
 """Probe: the aqlprofile counter reader inside a process that already runs HIP
 (torch) — what smoke() needs to exercise the counter tier in-process."""
+
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
 import json
 import os
 import sys

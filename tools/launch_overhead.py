@@ -9,6 +9,12 @@ off again.  Writes gpurun_out/launch_overhead.json.
 """
 from __future__ import annotations
 
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
+
 import json
 import os
 import subprocess

@@ -1,6 +1,12 @@
 """GPU diagnostic: raw rocprofiler counter deltas per synthetic-load phase, and
 stream-kernel variants (nt vs default loads, grid sizes).  Writes
 gpurun_out/pmc_debug.json."""
+
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
 import json
 import os
 import subprocess

@@ -2,6 +2,12 @@
 read costs.  Launches native pmc_probe (its own HSA process) over candidate
 counter sets, runs idle / MFMA / triad / copy phases here, and attributes each
 probe interval to a phase.  Writes gpurun_out/pmc_probe.json."""
+
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
 import json
 import os
 import subprocess

@@ -5,6 +5,12 @@ of the PMFW table pread of the fast tier, so the mock's latency model
 
     python tools/probe_amdsmi_latency.py > gpurun_out/r2/amdsmi_latency.json
 """
+
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
 import json
 import os
 import statistics

@@ -15,6 +15,12 @@ Writes ``gpurun_out/probe.json``.
 """
 from __future__ import annotations
 
+import sys as _sys
+
+if __name__ == "__main__" and {"-h", "--help"} & set(_sys.argv[1:]):
+    print(__doc__)  # a one-off GPU probe: no flags beyond this
+    _sys.exit(0)
+
 import glob
 import json
 import os
