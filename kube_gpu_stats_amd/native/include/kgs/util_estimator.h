@@ -38,8 +38,8 @@ struct EstimatorParams {
   int64_t clock_split_ns = 400000;
   double clock_ratio_lo = 0.9, clock_ratio_hi = 1.1;
   // Partial intervals at least this long count the READ's own CP time once where it
-  // overlaps dispatch busy (0 = never).
-  int64_t read_overlap_ns = 0;
+  // overlaps dispatch busy (0 = every interval, < 0 = never).
+  int64_t read_overlap_ns = -1;
   // Partial intervals at least this long are split in time, not cycles: idle time =
   // idle cycles / the learned idle clock, busy time = the rest of the span — no busy
   // clock needed, which a low READ rate may never see in a fully busy interval
@@ -54,6 +54,9 @@ struct EstimatorParams {
   // READ-only intervals among the kernels measure the clock of the gaps themselves
   // (1 ms bursts every 5 ms at 1 kHz), and the time split alone is then right.
   int64_t gap_clock_fresh_ns = 0;
+  // A READ-only interval (the READ-cost learning rule's) bills no dispatch (false: its CP
+  // busy less the learned READ cost, floored at 0).
+  bool read_only_bills_zero = false;
   double ewma = 0.05;                 // weight of a new sample in every learned EWMA
   int64_t quiet_hold_ns = 5000000;    // quiet intervals in a row before the device counts as quiet
   double busy_min = 0.0;              // dispatch gap: SPI share below this (0 = off)
@@ -164,7 +167,8 @@ class DispatchEstimator {
       // and so is the SPI blip (≈0.9 µs per READ: 0.7 % of the clocks at 8 kHz, so the
       // test is the quiet threshold, not "no SPI at all" — r4f: a 0.5 % test kept 2 %
       // of the 8 kHz READ-only intervals, the cheap ones, and learned 13 µs for 15.5).
-      if (act < p.quiet_active_frac * clk && d.mfma == prev_mfma_ && cpc < 0.5 * clk) {
+      const bool read_only = act < p.quiet_active_frac * clk && d.mfma == prev_mfma_ && cpc < 0.5 * clk;
+      if (read_only) {
         const bool first = read_n_[m][f] == 0;
         read_cyc_[m][f] = first ? cpc : (1 - p.ewma) * read_cyc_[m][f] + p.ewma * cpc;
         read_spi_[m][f] = first ? act : (1 - p.ewma) * read_spi_[m][f] + p.ewma * act;
@@ -185,14 +189,18 @@ class DispatchEstimator {
       // An interval the CP was busy for ≥ cpc_full_frac counts whole: under a kernel the
       // CPC idles a few % of each 125 µs interval at 8 kHz (r4f: MFMA and GEMM intervals
       // 0.95-1.0), and subtracting a READ-only cost there under-read a GEMM stream by 4
-      // points.  Long partial intervals count the READ's CP time once where it overlaps
-      // dispatch busy, (cpc − read) / (1 − read/clk) (sampler.h kReadOverlapNs); at
-      // 8 kHz that over-read burst trains in replay, so short ones subtract it whole.
+      // points.  Partial intervals count the READ's CP time once where it overlaps
+      // dispatch busy, (cpc − read) / (1 − read/clk) (sampler.h kReadOverlapNs).
       const bool full = cpc >= p.cpc_full_frac * clk;
-      const double net = p.read_overlap_ns > 0 && span_ns >= p.read_overlap_ns && rcyc < 0.5 * clk
+      const double net = p.read_overlap_ns >= 0 && span_ns >= p.read_overlap_ns && rcyc < 0.5 * clk
                              ? (cpc - rcyc) / (1.0 - rcyc / clk)
                              : cpc - rcyc;
-      const double busy = full ? clk : std::max(wav, std::max(0.0, net));
+      // A READ-only interval (the learning rule's: no waves, no MFMA cycle, the CP mostly
+      // idle) bills nothing: its CP busy less the learned mean READ cost is that READ's
+      // own scatter, and keeping the positive half of it (max 0) billed ≈2 µs per READ-only
+      // interval — 0.6 points on a 1 ms / 5 ms train at 8 kHz, whose gaps are all READ-only
+      // intervals (r5l dump: full intervals alone sum to the kernels' duty).
+      const double busy = full ? clk : (read_only && p.read_only_bills_zero) ? 0.0 : std::max(wav, std::max(0.0, net));
       double share = std::min(1.0, busy / clk);
       if (full) {
         clk_busy_hz_ = clk_busy_hz_ > 0 ? (1 - p.ewma) * clk_busy_hz_ + p.ewma * hz_now : hz_now;

@@ -559,6 +559,7 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def_readwrite("time_split_ratio_hi", &EstimatorParams::time_split_ratio_hi)
       .def_readwrite("time_split_weight", &EstimatorParams::time_split_weight)
       .def_readwrite("gap_clock_fresh_ns", &EstimatorParams::gap_clock_fresh_ns)
+      .def_readwrite("read_only_bills_zero", &EstimatorParams::read_only_bills_zero)
       .def_readwrite("ewma", &EstimatorParams::ewma)
       .def_readwrite("quiet_hold_ns", &EstimatorParams::quiet_hold_ns)
       .def_readwrite("busy_min", &EstimatorParams::busy_min)

@@ -62,6 +62,7 @@ EstimatorParams estimator_params(const SamplerConfig& cfg, int num_cu) {
   p.cpc_full_frac = kCpcFullFrac;
   p.clock_split_ns = kClockSplitNs;
   p.read_overlap_ns = kReadOverlapNs;
+  p.read_only_bills_zero = kReadOnlyBillsZero;
   p.time_split_ns = kTimeSplitNs;
   p.time_split_weight = kTimeSplitWeight;
   p.gap_clock_fresh_ns = kGapClockFreshNs;

@@ -44,12 +44,21 @@ def test_dump_replays_within_one_point_of_the_kernels_duty(shipped):
 LOWRATE = os.path.join(REPO, "profiles", "r5", "r5b_cp_dump_lowrate.json")
 
 
+def test_read_only_intervals_bill_nothing(shipped):
+    """A READ-only interval's CP busy less the learned mean READ cost is the READ's own
+    scatter: keeping its positive half billed an idle GPU 0.14 % at 8 kHz and the gaps of a
+    burst train with it (sampler.h kReadOnlyBillsZero)."""
+    assert abs(shipped["8000"]["idle"]["err_pts"]) <= 0.05 and abs(shipped["1000"]["idle"]["err_pts"]) <= 0.05
+    old = sim.replay(DUMP, {"read_only_bills_zero": "false"})
+    assert old["8000"]["idle"]["err_pts"] > 0.1, old["8000"]["idle"]
+
+
 def test_one_khz_bursts_read_the_reads_cp_time_once(shipped):
     """a READ that lands inside a kernel adds no CP busy; subtracting its
     cost whole from a 1 ms interval under-read the 1 kHz trains."""
     for load in ("burst_1_5", "burst_02_1"):
         assert abs(shipped["1000"][load]["err_pts"]) < 0.8, shipped["1000"][load]
-    old = sim.replay(DUMP, {"read_overlap_ns": 0})
+    old = sim.replay(DUMP, {"read_overlap_ns": -1})
     assert old["1000"]["burst_02_1"]["err_pts"] < shipped["1000"]["burst_02_1"]["err_pts"] - 0.2
 
 
@@ -112,7 +121,8 @@ def test_replay_is_the_samplers_code(N):
     parameters are the sampler's."""
     p = N.sampler_estimator_params()
     assert p.cpc_full_frac == pytest.approx(0.90) and p.quiet_active_frac == pytest.approx(0.02)
-    assert p.read_overlap_ns == 400000 and p.clock_split_ns == 400000 and p.time_split_ns == 400000
+    assert p.read_overlap_ns == 0 and p.clock_split_ns == 400000 and p.time_split_ns == 400000
+    assert p.read_only_bills_zero is True
     assert p.time_split_weight == pytest.approx(0.6) and p.gap_clock_fresh_ns == 10_000_000
     assert p.cp_only_min == pytest.approx(0.3) and p.num_simds == 1024
     src = open(os.path.join(REPO, "tools", "util_estimator_sim.py")).read()

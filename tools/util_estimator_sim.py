@@ -78,7 +78,8 @@ def replay(path: str, overrides: dict | None = None) -> dict:
     d = json.load(open(path))
     p = N.sampler_estimator_params()
     for k, v in (overrides or {}).items():
-        setattr(p, k, type(getattr(p, k))(v))
+        t = type(getattr(p, k))
+        setattr(p, k, str(v).lower() in ("1", "true", "yes") if t is bool else t(v))
     names = d.get("counters", [])
     mfma_col = 1 + names.index("SQ_VALU_MFMA_BUSY_CYCLES") if "SQ_VALU_MFMA_BUSY_CYCLES" in names else None
     cols = d.get("columns") or []
