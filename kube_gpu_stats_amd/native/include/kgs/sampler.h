@@ -193,21 +193,14 @@ constexpr double kCpcFullFrac = 0.90;
 // split over-read 0.2 ms bursts in replay, tools/util_estimator_sim.py; at 1 kHz it
 // closes most of a 1 ms-burst train's −1.3 … −2.3 points).
 constexpr int64_t kClockSplitNs = 400000;
-// A partial READ interval counts the READ packet's own CP time once where it overlaps
-// dispatch busy: busy = (CPC − r) / (1 − r/clk), a READ landing at a uniformly random
-// point of the interval.  Subtracting r whole under-read the 1 kHz burst trains of
-// r4f's raw READs by 0.3 / 0.8 points and the 8 kHz 0.2 ms trains by 0.5-0.8 (a READ
-// during a kernel adds no CP busy).  Round 4 kept it to intervals ≥ 400 µs because at
-// 8 kHz it over-read burst trains in replay — but that was the READ-only intervals'
-// rectified scatter below, not this rule (0 = every interval).
-constexpr int64_t kReadOverlapNs = 0;
-// A READ-only interval (no waves, no MFMA cycle, the CP mostly idle: the intervals that
-// teach the READ cost) bills no dispatch.  Its CP busy less the learned mean READ cost
-// is that READ's scatter, and keeping the positive half (max 0) billed an idle GPU 0.1-
-// 0.2 % at 8 kHz and a 1 ms / 5 ms train +0.6 points (r5l dump: its full intervals alone
-// sum to the kernels' duty).  With both rules the 8 kHz trains of the r4f and r5l dumps
-// replay within 0.53 points (before: 0.60 and −0.49, idle 0.23).
-constexpr bool kReadOnlyBillsZero = true;
+// ... and counts the READ packet's own CP time once where it overlaps dispatch busy:
+// busy = (CPC − r) / (1 − r/clk), a READ landing at a uniformly random point of the
+// interval.  Subtracting r whole under-read the 1 kHz burst trains of r4f's raw READs
+// by 0.3 / 0.8 points (a READ during a kernel adds no CP busy).  At 8 kHz the rule
+// over-reads 0.2 ms / 1 ms trains on MI355X (r6a: +1.39 points with it at every
+// interval length, though the r4f / r5l dumps replay it at +0.04 / +0.53), so it stays
+// with the long intervals.
+constexpr int64_t kReadOverlapNs = 400000;
 // ... and is split in time rather than cycles: idle time = its cycles at the learned
 // idle clock, busy time = the rest.  A cycle share under-weights power-capped kernels
 // (1 ms MFMA bursts at ≈2.1 GHz between ≈2.4 GHz gaps), and a low READ rate may never
@@ -230,6 +223,12 @@ constexpr double kTimeSplitWeight = 0.6;
 // three dumps' 1 kHz 1 ms trains: −0.55 / −1.41 / −0.17 points blended, +0.02 / −0.90 /
 // +0.02 with this; at 100 Hz and 10 Hz no READ-only interval falls inside a train).
 constexpr int64_t kGapClockFreshNs = 10000000;
+// A READ-only interval (no waves, no MFMA cycle, the CP mostly idle: the intervals that
+// teach the READ cost) bills no dispatch.  Its CP busy less the learned mean READ cost
+// is that READ's scatter, and keeping the positive half (max 0) billed an idle GPU 0.1-
+// 0.2 % at 8 kHz and a 1 ms / 5 ms train +0.6 points (r5l dump: its full intervals alone
+// sum to the kernels' duty; r6a on MI355X: the 8 kHz 1 ms train +0.53 → +0.04 points).
+constexpr bool kReadOnlyBillsZero = true;
 extern const double kReadHistBoundsUs[kReadHistBuckets];
 // Slow tiers (DeviceState::slow_call_tier, kgs_slow_* labels).
 enum SlowTier : int { kSlowProcs = 0, kSlowLinks = 1, kSlowHealth = 2 };

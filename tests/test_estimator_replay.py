@@ -121,7 +121,7 @@ def test_replay_is_the_samplers_code(N):
     parameters are the sampler's."""
     p = N.sampler_estimator_params()
     assert p.cpc_full_frac == pytest.approx(0.90) and p.quiet_active_frac == pytest.approx(0.02)
-    assert p.read_overlap_ns == 0 and p.clock_split_ns == 400000 and p.time_split_ns == 400000
+    assert p.read_overlap_ns == 400000 and p.clock_split_ns == 400000 and p.time_split_ns == 400000
     assert p.read_only_bills_zero is True
     assert p.time_split_weight == pytest.approx(0.6) and p.gap_clock_fresh_ns == 10_000_000
     assert p.cp_only_min == pytest.approx(0.3) and p.num_simds == 1024
