@@ -195,7 +195,8 @@ CATALOG: tuple[Family, ...] = (
     F("amdgpu_dispatch_busy_seconds_total", "counter",
       "∫ dispatch-in-flight share dt from the counter stream (per drain: CPC_CPC_STAT_BUSY share of the clocks less "
       "the exporter's own READ packet's CP time — counted once where it overlaps dispatch busy in intervals ≥ 400 us "
-      "— never below the GRBM_SPI_BUSY share; an interval the CP was busy for ≥ 90 % counts whole; intervals ≥ 400 us "
+      "— never below the GRBM_SPI_BUSY share; an interval the CP was busy for ≥ 90 % counts whole, a READ-only one "
+      "(no waves, no MFMA cycle) as nothing; intervals ≥ 400 us "
       "split busy from idle part in time — idle cycles at the learned idle clock, kgs_pmc_shader_clock_hz — blended "
       "0.6 with the cycle share unless READ-only intervals among the kernels just measured the gaps' clock); rate() = "
       "the READ-immune 'a kernel is running' fraction behind --sm-util-source auto.", source="counters", tier="pmc"),
