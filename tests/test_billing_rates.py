@@ -54,12 +54,20 @@ def _sweep(N, mock: dict) -> dict:
             ex.stop()
 
 
+def _edge(hz: float) -> float:
+    """Share of the window by which the dispatch integral's increment can be off: its
+    last drain before each edge is up to 1.25 ticks old (dithered ticks)."""
+    return max(0.01, 2 * 1.25 / (hz * WINDOW_S))
+
+
 @pytest.mark.slow
 def test_saturated_gpu_bills_at_least_99_percent_at_every_rate(N):
     r = _sweep(N, {"util_base": 100, "util_amp": 0})
     for hz, x in r.items():
         assert x["billed"] >= 0.99 and x["metric"] >= 0.99, (hz, x)
-        assert x["billed"] == pytest.approx(x["dispatch"], abs=0.01), (hz, x)  # the counter integral, all of it
+        # the counter integral, all of it (its increment over the window is known at the
+        # drains: up to a dithered tick, 125 ms at 10 Hz, at either edge)
+        assert x["billed"] == pytest.approx(x["dispatch"], abs=_edge(hz)), (hz, x)
         assert x["from_counters"] > 0.99 and x["dropped"] < 0.05, (hz, x)
 
 
@@ -70,4 +78,4 @@ def test_half_duty_square_bills_fifty_at_every_rate(N):
     for hz, x in r.items():
         assert 100 * x["billed"] == pytest.approx(50, abs=1), (hz, x)
         assert 100 * x["metric"] == pytest.approx(50, abs=1), (hz, x)
-        assert x["billed"] == pytest.approx(x["dispatch"], abs=0.01), (hz, x)
+        assert x["billed"] == pytest.approx(x["dispatch"], abs=_edge(hz)), (hz, x)
