@@ -1332,7 +1332,7 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         time.sleep(0.3)
         per_load: dict = {}
         # At a low counter rate the busy integral is known at the drains and billed at
-        # the PMFW samples (both at the tick rate): a window of ≥ 30 periods and a tail
+        # the PMFW samples (both at the tick rate): a window of ≥ 60 periods and a tail
         # of five, so the last burst's drain (pipelined: one tick late), its table and
         # the carry a saturated load holds (≤ one interval's worth, billed ≤ dt per
         # interval) land inside it — r5k: a tail of two read a saturated 10 Hz window
@@ -1342,7 +1342,7 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         # drains by up to a few tens of ms: 50 ms of tail at least, or a saturated 1.5 s
         # window reads that lag as 0.5-0.9 points of missing busy.  The duty counts the
         # tail as idle.
-        secs = max(a.util_s, 30.0 / hz)
+        secs = max(a.util_s, 60.0 / hz)
         tail = max(5.0 / hz, 0.05)
         for name, spec in plan:
             load.sync()
