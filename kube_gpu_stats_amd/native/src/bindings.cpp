@@ -275,6 +275,7 @@ class PyExporter {
     o["util_carry_seconds"] = I.util_carry_seconds;
     o["util_dropped_seconds"] = I.util_dropped_seconds;
     o["pmc_epoch"] = I.pmc_epoch;
+    o["pmc_last_ns"] = I.pmc_last_ns;
     {
       py::dict t;
       for (int r = 0; r < kThrottleReasons; ++r) t[throttle_reason_name(r)] = I.throttle_seconds[r];
