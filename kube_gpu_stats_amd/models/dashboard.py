@@ -154,6 +154,13 @@ def build() -> dict:
                [(_dev("histogram_quantile(0.99, rate(kgs_sampler_wake_lateness_seconds_bucket[5m]))"),
                  "p99 late s gpu{{gpu}}"),
                 (_dev("rate(kgs_sampler_overruns_total[5m])"), "overruns/s gpu{{gpu}}")], 8, y, w=8))
+    # the READ-immune utilisation's health: the share of firmware time billed from the
+    # counter tier (< 1: hand-over, breaker or stale drains billed from PMFW), the counter
+    # busy not yet billed, and the clocks the dispatch estimator prices idle cycles at
+    add(_panel(0, "Utilisation from counters (share), billing carry, learned shader clocks",
+               [(_dev('rate(kgs_util_source_seconds_total{source="counters"}[5m])'), "counters share gpu{{gpu}}"),
+                (_dev("kgs_util_carry_seconds"), "carry s gpu{{gpu}}"),
+                (_dev("kgs_pmc_shader_clock_hz / 1e9"), "{{kind}} clock GHz gpu{{gpu}}")], 16, y, w=8))
 
     return {
         "title": "MI355X GPU stats (kube_gpu_stats_amd)",
