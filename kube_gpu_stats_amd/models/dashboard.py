@@ -160,7 +160,7 @@ def build() -> dict:
     add(_panel(0, "Utilisation from counters (share), billing carry, learned shader clocks",
                [(_dev('rate(kgs_util_source_seconds_total{source="counters"}[5m])'), "counters share gpu{{gpu}}"),
                 (_dev("kgs_util_carry_seconds"), "carry s gpu{{gpu}}"),
-                (_dev("kgs_pmc_shader_clock_hz / 1e9"), "{{kind}} clock GHz gpu{{gpu}}")], 16, y, w=8))
+                (_dev("kgs_pmc_shader_clock_hz / 1000000000"), "{{kind}} clock GHz gpu{{gpu}}")], 16, y, w=8))
 
     return {
         "title": "MI355X GPU stats (kube_gpu_stats_amd)",
