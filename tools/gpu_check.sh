@@ -56,6 +56,9 @@ for s in $STEPS; do
         esac ;;
     bpub*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-publish-us "${s#bpub}" --out "$OUT/$s.json" ;;
     b16k) run $s 600 python -u bench.py --steps 20 --warmup 5 --hz 16000 --pmc-batch 16 --out "$OUT/$s.json" ;;
+    b16knd) KGS_TICK_DITHER=0 run $s 600 python -u bench.py --steps 20 --warmup 5 --hz 16000 --pmc-batch 16 \
+              --out "$OUT/$s.json" ;;  # the 16 kHz tier on a fixed tick grid
+    bnd) KGS_TICK_DITHER=0 run $s 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/$s.json" ;;
     bnobatch|bnobatch2) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch 1 --out "$OUT/$s.json" ;;
     bbatch*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch "${s#bbatch}" --out "$OUT/$s.json" ;;
     bgap*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-busy-min "0.${s#bgap}" --out "$OUT/$s.json" ;;
