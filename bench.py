@@ -367,6 +367,31 @@ class GpuLoad(Load):
         e1.synchronize()
         return e0.elapsed_time(e1) * 1e-3
 
+    def triad_burst_timed(self, ms: float) -> float:
+        """One HBM triad of ≈``ms`` milliseconds (a slice of the stream buffers), waited for:
+        its own GPU time (HIP events), seconds (phase U: a memory-bound kernel, which runs
+        at the full shader clock where an MFMA burst is power-capped)."""
+        from kube_gpu_stats_amd.ops import load as L
+
+        torch = self.torch
+        if not hasattr(self, "_bev"):
+            self._bev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        e0, e1 = self._bev
+        a, b, c = self.ls.a, self.ls.b, self.ls.c
+        if not hasattr(self, "_triad_per_ms"):  # elements per ms, from one 1/8-buffer triad
+            n = a.numel() // 8
+            e0.record()
+            L.triad_f32(a[:n], b[:n], c[:n], 1.5)
+            e1.record()
+            e1.synchronize()
+            self._triad_per_ms = n / max(e0.elapsed_time(e1), 1e-3)
+        n = min(a.numel(), max(1 << 20, int(self._triad_per_ms * ms)))
+        e0.record()
+        L.triad_f32(a[:n], b[:n], c[:n], 1.5)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e-3
+
     def saturate(self, secs: float) -> float:
         """MFMA kernels back to back (two in flight) for ``secs``: Σ their GPU time (phase U)."""
         torch = self.torch
@@ -542,6 +567,8 @@ class MockLoad(Load):
     def burst_timed(self, ms: float) -> float:
         self.burst(ms)
         return ms * 1e-3
+
+    triad_burst_timed = burst_timed
 
     def saturate(self, secs: float) -> float:
         time.sleep(secs)
@@ -1313,8 +1340,8 @@ def util_accuracy(ctx, load, exp, a) -> dict:
     GPU used to read ≈100 % busy.  At the primary rate and each --util-hz rate, with
     the exporter's default flags (adaptive idle rate, batched READs, --sm-util-source
     auto), every rank runs the same load for --util-s — idle, a train of 1 ms MFMA
-    kernels every 5 ms, a train of 0.2 ms kernels every 1 ms, MFMA kernels back to
-    back — and rank 0 reads, per GPU, 100·rate(container_gpu_busy_seconds_total)
+    kernels every 5 ms, a train of 0.2 ms kernels every 1 ms, a train of 1 ms HBM triads
+    every 5 ms (memory-bound: full shader clock), MFMA kernels back to back — and rank 0 reads, per GPU, 100·rate(container_gpu_busy_seconds_total)
     (exact over the window), the container_gpu_sm_util gauge and the raw PMFW GFX busy,
     next to the duty the rank measured: its kernels' own GPU time (HIP events) over
     the window (``duty_gpu_pct``, the truth "a kernel is running" means) and the
@@ -1323,6 +1350,7 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         return {}
     rates = [a.hz] + [float(x) for x in str(a.util_hz).split(",") if x.strip() and float(x) != a.hz]
     plan = [("idle", None), ("burst_1ms_every_5ms", (1.0, 5.0)), ("burst_0.2ms_every_1ms", (0.2, 1.0)),
+            ("triad_1ms_every_5ms", (1.0, 5.0, "triad")),
             ("mfma_saturating", "sat")]
     out: dict = {"secs_per_load": a.util_s, "per_rate": {}}
     for hz in rates:
@@ -1356,12 +1384,13 @@ def util_accuracy(ctx, load, exp, a) -> dict:
                 gpu_s = load.saturate(secs)
                 host_s = time.perf_counter() - t0
             else:
-                ms, period = spec
+                ms, period = spec[0], spec[1]
+                burst = load.triad_burst_timed if spec[2:] == ("triad",) else load.burst_timed
                 nxt = time.monotonic()
                 end = nxt + secs
                 while time.monotonic() < end:
                     h0 = time.perf_counter()
-                    gpu_s += load.burst_timed(ms)
+                    gpu_s += burst(ms)
                     host_s += time.perf_counter() - h0
                     nxt += period * 1e-3
                     d = nxt - time.monotonic()
@@ -1925,7 +1954,8 @@ def summarize(res: dict) -> dict:
             xs = [x for x in xs if x is not None]
             return _r(sum(xs) / len(xs), 1) if xs else None
 
-        short = {"burst_1ms_every_5ms": "1ms/5ms", "burst_0.2ms_every_1ms": "0.2ms/1ms", "mfma_saturating": "sat"}
+        short = {"burst_1ms_every_5ms": "1ms/5ms", "burst_0.2ms_every_1ms": "0.2ms/1ms",
+                 "triad_1ms_every_5ms": "triad1ms/5ms", "mfma_saturating": "sat"}
         out["util_accuracy"] = {
             "cols": "exported busy %, kernel duty %",
             **{hz: {short.get(ld, ld): [mean([r.get("busy_counter_pct") for r in pg.values()]),
