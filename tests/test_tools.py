@@ -124,6 +124,13 @@ def test_util_estimator_sim_replays_a_synthetic_dump(tmp_path, capsys):
     assert out["idle"]["busy_pct"] < 0.5
     b = out["burst_1_5"]
     assert b["busy_pct"] == pytest.approx(20.0, abs=0.5), b
+    # --classes: the train's busy comes from the full intervals (≈ 7 of every 8 burst
+    # intervals) plus its edges; the READ-only intervals between bursts add nothing
+    assert U.main([str(p), "--classes"]) == 0
+    c = json.loads(capsys.readouterr().out)["8000"]["burst_1_5"]
+    assert c["read_only"]["intervals"] > 1000 and c["read_only"]["busy_us_per_s"] == 0.0, c
+    total = sum(c[k]["busy_us_per_s"] for k in ("full", "partial", "read_only"))
+    assert total == pytest.approx(c["duty_us_per_s"], rel=0.03) and c["full"]["busy_us_per_s"] > 0.8 * total, c
 
 
 @pytest.mark.parametrize("tool", sorted(f for f in os.listdir(os.path.join(REPO, "tools")) if f.endswith(".py")))

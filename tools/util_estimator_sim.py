@@ -71,7 +71,41 @@ def replay_rate(N, loads: dict, params, mfma_col: int | None = None, fresh_col: 
     return out
 
 
-def replay(path: str, overrides: dict | None = None) -> dict:
+def interval_classes(N, loads: dict, params, mfma_col: int | None = None, fresh_col: int | None = None) -> dict:
+    """Per load: where the estimate comes from — READ intervals the CP was busy for ≥
+    cpc_full_frac (counted whole), partial ones, and READ-only ones — as µs per second of
+    load, with the kernels' duty for comparison (how r5aa / r5ab found the READ-only
+    intervals' rectified scatter)."""
+    idle = rows_of(loads.get("idle", {"samples": []}), mfma_col, fresh_col)
+    out = {}
+    for name, L in loads.items():
+        rows = rows_of(L, mfma_col, fresh_col, inside=True)
+        if name == "idle" or len(rows) < 3:
+            continue
+        est = N.DispatchEstimator()
+        if idle:
+            est.replay(params, idle)
+        est.invalidate(int(rows[0][0] * 1e9))
+        cls = {"full": [0, 0.0], "partial": [0, 0.0], "read_only": [0, 0.0]}
+        prev, span = None, 0.0
+        for r in rows:
+            s = est.feed(params, int(r[0] * 1e9), int(r[1]), int(r[2]), int(r[3]), None if r[4] < 0 else int(r[4]),
+                         bool(r[5]), False)
+            if prev is not None and s.have_dispatch and r[1] > prev[1]:
+                cpc = (r[3] - prev[3]) / (r[1] - prev[1])
+                k = "full" if cpc >= params.cpc_full_frac else ("read_only" if s.learned else "partial")
+                cls[k][0] += 1
+                cls[k][1] += s.dispatch_s
+                span += s.span_s
+            prev = r
+        if span <= 0:
+            continue
+        out[name] = {"duty_us_per_s": round(1e6 * L["duty_gpu_s"] / (L["t1"] - L["t0"]), 1),
+                     **{k: {"intervals": n, "busy_us_per_s": round(1e6 * v / span, 1)} for k, (n, v) in cls.items()}}
+    return out
+
+
+def replay(path: str, overrides: dict | None = None, classes: bool = False) -> dict:
     from kube_gpu_stats_amd import load_native
 
     N = load_native()
@@ -84,6 +118,8 @@ def replay(path: str, overrides: dict | None = None) -> dict:
     mfma_col = 1 + names.index("SQ_VALU_MFMA_BUSY_CYCLES") if "SQ_VALU_MFMA_BUSY_CYCLES" in names else None
     cols = d.get("columns") or []
     fresh_col = cols.index("se_fresh") if "se_fresh" in cols else None
+    if classes:
+        return {rate: interval_classes(N, loads, p, mfma_col, fresh_col) for rate, loads in d["rates"].items()}
     return {rate: replay_rate(N, loads, p, mfma_col, fresh_col) for rate, loads in d["rates"].items()}
 
 
@@ -92,9 +128,11 @@ def main(argv=None) -> int:
     ap.add_argument("dump")
     ap.add_argument("--set", action="append", default=[], metavar="PARAM=VALUE",
                     help="override one EstimatorParams field (e.g. cpc_full_frac=0.97)")
+    ap.add_argument("--classes", action="store_true",
+                    help="instead: each load's estimate split by READ-interval class (full / partial / READ-only)")
     a = ap.parse_args(argv)
     ov = dict(kv.split("=", 1) for kv in a.set)
-    print(json.dumps(replay(a.dump, ov), indent=1))
+    print(json.dumps(replay(a.dump, ov, classes=a.classes), indent=1))
     return 0
 
 
