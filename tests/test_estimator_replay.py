@@ -306,3 +306,54 @@ def test_time_split_never_bills_a_deep_idle_stretch_as_busy(N):
     spi += busy_cyc
     s = e.feed(p, t, cnt, spi, cpc, mfma=10**6)
     assert s.dispatch_s / 0.010 < 0.015, s.dispatch_s
+
+
+# ---- UtilBiller properties (hypothesis) ------------------------------------------
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=60, deadline=None)
+@given(hz=st.sampled_from([10.0, 25.0, 50.0, 100.0, 1000.0]),
+       jitter=st.floats(min_value=0.0, max_value=0.9),
+       duty=st.floats(min_value=0.0, max_value=1.0),
+       period=st.floats(min_value=0.01, max_value=0.5),
+       fw_period=st.sampled_from([0.01, 0.02]),
+       seed=st.integers(0, 10_000))
+def test_biller_properties(N, hz, jitter, duty, period, fw_period, seed):
+    """For any drain rate and jitter, square-wave load and firmware cadence: every PMFW
+    interval bills within [0, dt]; the carry stays within ± the cap; and over the run the
+    billed total equals the counter integral at the last drain, give or take the carry
+    and the run-on guess (never more than one freshness window)."""
+    busy = lambda t: math.floor(t / period) * period * duty + min(max(t - math.floor(t / period) * period, 0.0),  # noqa: E731
+                                                                   period * duty)
+    rnd = random.Random(seed)
+    secs = 6.0
+    drain_t, t = [], 0.0
+    while t < secs + 1:
+        drain_t.append(t + rnd.uniform(0, jitter / hz))
+        t += 1.0 / hz
+    b = N.UtilBiller()
+    cap = 3.0 / min(hz, 100.0) + 0.05
+    pmfw_rate = min(hz, 100.0)
+    billed, last_fw, last_t, k, t = 0.0, None, 0.0, 0, 0.0
+    while t < secs:
+        t += 1.0 / pmfw_rate
+        while k + 1 < len(drain_t) and drain_t[k + 1] <= t:
+            k += 1
+        fw = math.floor(t / fw_period) * fw_period
+        dt = fw - last_fw if last_fw is not None else 0.0
+        if last_fw is not None and dt <= 0:
+            continue
+        last_fw = fw
+        share = (busy(drain_t[k]) - busy(drain_t[k - 1])) / (drain_t[k] - drain_t[k - 1]) if k > 0 else 0.0
+        dgfx = min(dt, busy(t) - busy(last_t))
+        last_t = t
+        got, _ = b.bill(dt, dgfx, True, 1, busy(drain_t[k]), cap, True, share, t - drain_t[k], k)
+        assert -1e-12 <= got <= dt + 1e-12
+        assert abs(b.carry_s) <= cap + 1e-9
+        billed += got
+    truth = busy(drain_t[k])
+    assert b.dropped_s == pytest.approx(0.0, abs=1e-9)
+    assert abs(billed - truth) <= cap + 1e-9, (billed, truth, b.carry_s)
