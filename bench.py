@@ -87,9 +87,8 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-set", default="base", choices=["base", "full"],
                     help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register "
                     "reads)")
-    ap.add_argument("--pmc-busy-min", type=float, default=0.0,
-                    help="exporter --pmc-busy-min: READ at --pmc-gap-hz while the SPI-busy share is below this")
-    ap.add_argument("--pmc-gap-hz", type=float, default=1000.0, help="exporter --pmc-gap-hz")
+    ap.add_argument("--pmc-dispatch-hz", type=float, default=1000.0,
+                    help="exporter --pmc-dispatch-hz: READ rate while the CP dispatches with no wave in flight")
     ap.add_argument("--pmc-batch", type=int, default=8,
                     help="exporter --pmc-batch: counter READs per L2 writeback (8 at 8 kHz: one per ms)")
     ap.add_argument("--pmc-publish-us", type=int, default=1000, help="exporter --pmc-publish-us")
@@ -153,7 +152,8 @@ def parse_args(argv=None):
     ap.add_argument("--mock-step-ms", type=float, default=20.0, help="mock: duration of one load unit")
     ap.add_argument("--mock-latency", type=int, default=1, choices=[0, 1],
                     help="mock: model AMD SMI call latency under one global lock (profiles/r2/mock_scaling.md)")
-    ap.add_argument("--out", default="", help="write the full result JSON here (default gpurun_out/bench_result_n<N>.json)")
+    ap.add_argument("--out", default="", help="write the full result JSON here (default gpurun_out/bench_result_n<N>.json); the "
+                    "exporter log goes next to it")
     ap.add_argument("--attach", default="", help="host:port of an exporter started with --control-http; it is "
                     "paused for phases A/C instead of being spawned (lets rocprofv3 trace the bench alone)")
     return ap.parse_args(argv)
@@ -672,7 +672,7 @@ class ExporterProc(ExporterCtl):
             pmc = PMC_READER if a.pmc == "auto" else a.pmc
             cmd += ["--pmc", pmc, "--pmc-pipeline" if a.pmc_pipeline else "--no-pmc-pipeline", "--pmc-set", a.pmc_set,
                     "--pmc-lean", str(a.pmc_lean)]
-        cmd += ["--pmc-busy-min", f"{a.pmc_busy_min:g}", "--pmc-gap-hz", f"{a.pmc_gap_hz:g}"]
+        cmd += ["--pmc-dispatch-hz", f"{a.pmc_dispatch_hz:g}"]
         if not a.mock:
             cmd += ["--pmc-batch", str(a.pmc_batch), "--pmc-publish-us", str(a.pmc_publish_us)]
         env = dict(os.environ)
@@ -1746,14 +1746,15 @@ def run(a, ctx) -> dict | None:
     exp = None
     err = ""
     if ctx.local_rank == 0:
-        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        logdir = os.path.dirname(os.path.abspath(a.out)) if a.out else os.path.join(REPO, "gpurun_out")
+        os.makedirs(logdir, exist_ok=True)
         try:
             if attached is not None:
                 attached.set_rate(a.hz)
                 attached.resume()
                 exp = attached
             else:
-                exp = ExporterProc(a, bdfs, os.path.join(REPO, "gpurun_out", f"bench_exporter_r{ctx.rank}.log"))
+                exp = ExporterProc(a, bdfs, os.path.join(logdir, f"bench_exporter_r{ctx.rank}.log"))
         except Exception as e:  # noqa: BLE001
             err = str(e)
     err = D.broadcast_object(ctx, err)
@@ -1840,7 +1841,7 @@ def run(a, ctx) -> dict | None:
                    "batch_meaning": "GPUs sampled per tick (one counter drain each)",
                    "seq_len_meaning": "sampler ticks per GPU per timed step",
                    "hz": a.hz, "hz_tiers": hzs, "sample_source": source,
-                   "pmc_gap": {"busy_min": a.pmc_busy_min, "hz": a.pmc_gap_hz} if a.pmc_busy_min > 0 else None,
+                   "pmc_dispatch_hz": a.pmc_dispatch_hz,
                    "pmc_batch": a.pmc_batch, "pmc_publish_us": a.pmc_publish_us,
                    "exporter": "attached" if a.attach else "spawned", "load": "mock" if a.mock else a.load,
                    "units_per_step": load.reps, "unit_ms": unit_s * 1e3},

@@ -77,18 +77,12 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                        "command-processor packet that GFX busy / GUI-active count as work (≈80 / "
                                        "190 µs each), so a quiet GPU is read at this rate and a busy one every tick "
                                        "(0 = every tick: profiling mode)")
-    add_flag(ap, "pmc-busy-min", 0.0, "dispatch-gap READ rate: while the counter READ intervals have waves for less "
-                                      "than this share of their clocks (short kernels with dispatch gaps), READ at "
-                                      "--pmc-gap-hz, since every READ packet delays the workload's dispatches "
-                                      "(0 = off; ignored in profiling mode)")
-    add_flag(ap, "pmc-gap-hz", 500.0, "counter READ rate in a dispatch gap (--pmc-busy-min) or a dispatch-bound "
-                                       "stream (--pmc-cp-only-min): a µs-kernel stream pays +0.5 %% at 1 kHz, +4 %% at "
-                                       "8 kHz (profiles/r4/ r4d)")
-    add_flag(ap, "pmc-gap-hold-ms", 1.0, "low-occupancy READ intervals in a row, in ms, before the gap rate applies")
+    add_flag(ap, "pmc-dispatch-hz", 500.0, "counter READ rate in a dispatch-bound stream (--pmc-cp-only-min): a "
+                                            "µs-kernel stream pays +0.5 %% at 1 kHz, +4 %% at 8 kHz (profiles/r4/ r4d)")
     add_flag(ap, "pmc-cp-only-min", 0.3, "dispatch-bound READ rate: while the command processor dispatches with no "
                                          "wave in flight for at least this share of the clocks (a stream of µs "
                                          "kernels, which each READ packet slows by a fixed CP cost), READ at "
-                                         "--pmc-gap-hz (0 = off; ignored in profiling mode)")
+                                         "--pmc-dispatch-hz (0 = off; ignored in profiling mode)")
     add_flag(ap, "pmc-dispatch-hold-ms", 10.0, "dispatch-bound READ intervals in a row, in ms, before that rate applies "
                                               "(a few ms of small kernels inside a training step keep the full rate)")
     add_flag(ap, "pmc-batch", 8, choices=range(1, 17), help="counter READs per L2 writeback: a READ's results sit in the GPU's L2 until "
@@ -197,9 +191,7 @@ def config_from_args(a) -> dict:
         "pmc_reclaim_s": a.pmc_reclaim_s,
         "pmc_refresh_s": a.pmc_refresh_s,
         "pmc_idle_hz": a.pmc_idle_hz,
-        "pmc_busy_min": a.pmc_busy_min,
-        "pmc_gap_hz": a.pmc_gap_hz,
-        "pmc_gap_hold_s": a.pmc_gap_hold_ms * 1e-3,
+        "pmc_dispatch_hz": a.pmc_dispatch_hz,
         "pmc_cp_only_min": a.pmc_cp_only_min,
         "pmc_dispatch_hold_s": a.pmc_dispatch_hold_ms * 1e-3,
         "pmc_timeout_ms": a.pmc_timeout_ms,

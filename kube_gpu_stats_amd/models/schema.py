@@ -265,14 +265,11 @@ CATALOG: tuple[Family, ...] = (
       "--pmc-idle-hz so the exporter's own packets do not read as GPU activity.", source="self"),
     F("kgs_pmc_quiet_skips_total", "counter", "Sampler ticks that skipped their counter READ on a quiet GPU.",
       source="self"),
-    F("kgs_pmc_gap", "gauge", "1 while the counter READ intervals had waves for less than --pmc-busy-min of their "
-      "clocks (short kernels with dispatch gaps): READs drop to --pmc-gap-hz, since each READ packet delays the "
-      "workload's dispatches.", source="self"),
     F("kgs_pmc_dispatch_bound", "gauge", "1 while the command processor dispatched with no wave in flight for at "
       "least --pmc-cp-only-min of the clocks for --pmc-dispatch-hold-ms (a stream of µs kernels, which each READ "
-      "packet slows): READs drop to --pmc-gap-hz.", source="self"),
-    F("kgs_pmc_gap_skips_total", "counter", "Sampler ticks that skipped their counter READ in a dispatch gap or a "
-      "dispatch-bound stream.", source="self"),
+      "packet slows): READs drop to --pmc-dispatch-hz.", source="self"),
+    F("kgs_pmc_dispatch_skips_total", "counter", "Sampler ticks that skipped their counter READ in a dispatch-bound "
+      "stream.", source="self"),
     F("kgs_pmc_failed", "gauge", "1 while the counter tier's circuit breaker is open: --pmc-breaker-k consecutive "
       "counter drains failed (a wedged command processor).  READs stop; after --pmc-retry-s (doubling to "
       "--pmc-retry-max-s) the reader's AQL queue is recreated and the counters re-STARTed.  The PMFW tier of the "

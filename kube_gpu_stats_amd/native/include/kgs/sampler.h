@@ -88,20 +88,6 @@ struct SamplerConfig {
   // idle stretches drops.  0 = READ every tick (profiling mode: full resolution,
   // and the PMFW GFX busy reads the READs as work).
   double pmc_idle_hz = 100.0;
-  // Dispatch-gap READ rate.  Every READ is one more AQL packet for the command
-  // processor that also dispatches the workload's kernels, and a READ whose
-  // indirect buffer is all NOPs costs a bf16 training step as much as a real one
-  // (profiles/r3/README.md, r3e): the cost is per packet.  Long kernels hide it
-  // (SPI busy ≈97 % of the clocks, nothing to dispatch); a stream of short
-  // kernels with dispatch gaps between them does not.  While the READ intervals
-  // of the last pmc_gap_hold_s had waves for less than pmc_busy_min of their
-  // clocks, READs drop to pmc_gap_hz; the first interval at or above
-  // pmc_busy_min restores every tick.  Integrals stay exact (cumulative
-  // counters); only the time resolution of those stretches drops.  Off in
-  // profiling mode (pmc_idle_hz 0) and with pmc_busy_min 0.
-  double pmc_busy_min = 0.0;
-  double pmc_gap_hz = 500.0;
-  double pmc_gap_hold_s = 0.001;
   // Dispatch-bound READ rate (needs CPC busy in the counter set).  A GPU that
   // runs nothing but µs kernels back to back keeps the command processor busy
   // while its shader engines hold waves only part of the time (a HIP graph of
@@ -111,12 +97,17 @@ struct SamplerConfig {
   // +0.05 % at 100 Hz; profiles/r4/ r4c, r4d).  While the
   // READ intervals of the last pmc_dispatch_hold_s had the CP dispatching with no
   // wave in flight for at least pmc_cp_only_min of their clocks, READs drop to
-  // pmc_gap_hz; the first interval below restores every tick.  The hold keeps a
+  // pmc_dispatch_hz; the first interval below restores every tick.  The hold keeps a
   // few ms of small kernels inside a training step at full rate (the bench step's
   // 2000-kernel graph runs 3.5 ms, and past 4 ms on a slow host, r4j).  0 = off;
-  // off in profiling mode.
+  // off in profiling mode.  Integrals stay exact (cumulative counters); only the
+  // time resolution of those stretches drops.  (Round 5's SPI-keyed "dispatch gap"
+  // rate is gone: a saturated MFMA stream's SPI share wanders 89-95 % from box to
+  // box, so no fixed SPI threshold separates it from a gapped stream; the CP-only
+  // share does, and this rate already covers the µs-kernel case.)
   double pmc_cp_only_min = 0.3;
   double pmc_dispatch_hold_s = 0.010;
+  double pmc_dispatch_hz = 500.0;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
   // Counter-tier circuit breaker: consecutive failed drains that open it, and the
@@ -273,9 +264,8 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_refreshes{0};   // periodic re-STARTs (pmc_refresh_s)
   std::atomic<int> pmc_quiet{0};            // last READ interval had no wave: READs at pmc_idle_hz
   std::atomic<uint64_t> pmc_quiet_skips{0};  // ticks that skipped their READ while quiet
-  std::atomic<int> pmc_gap{0};               // READ intervals below pmc_busy_min: READs at pmc_gap_hz
-  std::atomic<int> pmc_dbound{0};            // dispatch-bound (pmc_cp_only_min): READs at pmc_gap_hz too
-  std::atomic<uint64_t> pmc_gap_skips{0};    // ticks that skipped their READ in a dispatch gap
+  std::atomic<int> pmc_dbound{0};            // dispatch-bound (pmc_cp_only_min): READs at pmc_dispatch_hz
+  std::atomic<uint64_t> pmc_dbound_skips{0};  // ticks that skipped their READ while dispatch-bound
   // Counter-tier fault boundary (sampler.h header comment).
   std::atomic<int> pmc_failed{0};            // breaker open: no READs until a retry succeeds
   std::atomic<uint64_t> pmc_breaker_trips{0};
@@ -381,11 +371,10 @@ class Sampler {
   // (unchanged) unless hz == 0 or kMinIdleHz <= hz <= kMaxHz.
   bool set_pmc_idle_hz(double hz);
   double pmc_idle_hz() const { return pmc_idle_hz_.load(std::memory_order_relaxed); }
-  // Dispatch-gap rate (SamplerConfig::pmc_busy_min): false (unchanged) unless
-  // 0 <= busy_min <= 1 and 0 < hz <= kMaxHz.
-  bool set_pmc_gap(double busy_min, double hz);
-  double pmc_busy_min() const { return pmc_busy_min_.load(std::memory_order_relaxed); }
-  double pmc_gap_hz() const { return pmc_gap_hz_.load(std::memory_order_relaxed); }
+  // Dispatch-bound READ rate (SamplerConfig::pmc_dispatch_hz), in place; false
+  // (unchanged) unless 0 < hz <= kMaxHz.
+  bool set_pmc_dispatch_hz(double hz);
+  double pmc_dispatch_hz() const { return pmc_dispatch_hz_.load(std::memory_order_relaxed); }
   // Slow-tier passes completed (all devices).
   uint64_t slow_passes() const { return slow_passes_.load(); }
   // Test hook: the device's counter thread wedges its reader's queue
@@ -429,8 +418,7 @@ class Sampler {
   std::atomic<double> hz_{10.0};
   std::atomic<uint64_t> slow_passes_{0};
   std::atomic<double> pmc_idle_hz_{0.0};
-  std::atomic<double> pmc_busy_min_{0.0};
-  std::atomic<double> pmc_gap_hz_{500.0};
+  std::atomic<double> pmc_dispatch_hz_{500.0};
   mutable std::mutex pid_pods_mu_;
   std::shared_ptr<const std::unordered_map<uint64_t, std::string>> pid_pods_;
   std::vector<std::map<std::string, double>> pod_cu_;  // device's slow thread only

@@ -7,7 +7,7 @@
 //    packet's own CP cost (learned on intervals without waves, per READ mode and per
 //    full / lite READ), the busy / idle shader clocks and the clock split of partial
 //    intervals, the full-interval rule, the stall (plausible-clock) watch, and the
-//    three READ-rate hysteresis machines (quiet, dispatch gap, dispatch-bound).
+//    two READ-rate hysteresis machines (quiet, dispatch-bound).
 //    Sampler::run_pmc feeds it every drain and only schedules and publishes.
 //  * UtilBiller — one distinct PMFW interval in, the seconds billed out.  While the
 //    counter tier covers the interval the counter integral's increment is billed;
@@ -59,8 +59,6 @@ struct EstimatorParams {
   bool read_only_bills_zero = false;
   double ewma = 0.05;                 // weight of a new sample in every learned EWMA
   int64_t quiet_hold_ns = 5000000;    // quiet intervals in a row before the device counts as quiet
-  double busy_min = 0.0;              // dispatch gap: SPI share below this (0 = off)
-  int64_t gap_hold_ns = 1000000;
   double cp_only_min = 0.0;           // dispatch-bound: CP busy with no wave ≥ this share (0 = off)
   int64_t dbound_hold_ns = 10000000;
   double plausible_mhz_lo = 100.0, plausible_mhz_hi = 4000.0;
@@ -86,8 +84,8 @@ struct DrainStep {
   double dispatch_s = 0;      // ∫ dispatch-in-flight share dt
   double cp_only_share = 0;   // CP busy with no wave in flight, share of the clocks
   bool learned = false;       // this interval taught the READ cost
-  bool quiet_interval = false, gap_interval = false, dbound_interval = false;
-  bool quiet = false, gap = false, dbound = false;  // hysteresis states after this drain
+  bool quiet_interval = false, dbound_interval = false;
+  bool quiet = false, dbound = false;  // hysteresis states after this drain
 };
 
 class DispatchEstimator {
@@ -98,8 +96,8 @@ class DispatchEstimator {
     prev_count_ = prev_mfma_ = prev_spi_ = prev_cpc_ = 0;
     prev_ns_ = se_ns_ = t;
     se_count_ = se_mfma_ = 0;
-    quiet_ = gap_ = dbound_ = false;
-    quiet_since_ = gap_since_ = dbound_since_ = 0;
+    quiet_ = dbound_ = false;
+    quiet_since_ = dbound_since_ = 0;
     last_plausible_ns_ = t;
   }
   // A break with no new baseline (breaker trip, failed re-START): the next drain
@@ -119,7 +117,6 @@ class DispatchEstimator {
   double clk_busy_hz() const { return clk_busy_hz_; }
   double clk_idle_hz() const { return clk_idle_hz_; }
   bool quiet() const { return quiet_; }
-  bool gap() const { return gap_; }
   bool dbound() const { return dbound_; }
 
   DrainStep feed(const Drain& d, const EstimatorParams& p) {
@@ -244,19 +241,14 @@ class DispatchEstimator {
     // previous READ, and no MFMA cycle ran.  Both counters are (nearly) blind to our own
     // READs: SPI busy reads 0.65 % with nothing but 8 kHz of READs on the GPU
     // (profiles/r2/immunity/).  Without the activity counter a device is never quiet.
-    // A dispatch gap: the same share below busy_min (quiet intervals included, so an
-    // idle stretch between short kernels does not restart the hold).
     if (have_prev_ && have_act && d.count > prev_count_) {
       const double act = static_cast<double>(d.spi - std::min(d.spi, prev_spi_));
       const double clk = static_cast<double>(d.count - prev_count_);
       r.quiet_interval = act < p.quiet_active_frac * clk && d.mfma == prev_mfma_;
-      r.gap_interval = p.busy_min > 0 && act < p.busy_min * clk;
     }
     quiet_ = hold(r.quiet_interval, quiet_since_, d.mono_ns, p.quiet_hold_ns);
-    gap_ = hold(r.gap_interval, gap_since_, d.mono_ns, p.gap_hold_ns) && !quiet_;
     dbound_ = hold(r.dbound_interval, dbound_since_, d.mono_ns, p.dbound_hold_ns) && !quiet_;
     r.quiet = quiet_;
-    r.gap = gap_;
     r.dbound = dbound_;
     prev_count_ = d.count;
     prev_mfma_ = d.mfma;
@@ -291,8 +283,8 @@ class DispatchEstimator {
   double cpc_read_us_ = 0;
   double clk_busy_hz_ = 0, clk_idle_hz_ = 0;
   int64_t idle_learned_ns_ = 0;  // the drain that last taught clk_idle_hz_
-  bool quiet_ = false, gap_ = false, dbound_ = false;
-  int64_t quiet_since_ = 0, gap_since_ = 0, dbound_since_ = 0;
+  bool quiet_ = false, dbound_ = false;
+  int64_t quiet_since_ = 0, dbound_since_ = 0;
   int64_t last_plausible_ns_ = 0;
 };
 

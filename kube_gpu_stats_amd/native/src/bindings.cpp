@@ -86,9 +86,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmc_reclaim_s = get<double>(d, "pmc_reclaim_s", c.sampler.pmc_reclaim_s);
   c.sampler.pmc_refresh_s = get<double>(d, "pmc_refresh_s", c.sampler.pmc_refresh_s);
   c.sampler.pmc_idle_hz = get<double>(d, "pmc_idle_hz", c.sampler.pmc_idle_hz);
-  c.sampler.pmc_busy_min = get<double>(d, "pmc_busy_min", c.sampler.pmc_busy_min);
-  c.sampler.pmc_gap_hz = get<double>(d, "pmc_gap_hz", c.sampler.pmc_gap_hz);
-  c.sampler.pmc_gap_hold_s = get<double>(d, "pmc_gap_hold_s", c.sampler.pmc_gap_hold_s);
+  c.sampler.pmc_dispatch_hz = get<double>(d, "pmc_dispatch_hz", c.sampler.pmc_dispatch_hz);
   c.sampler.pmc_cp_only_min = get<double>(d, "pmc_cp_only_min", c.sampler.pmc_cp_only_min);
   c.sampler.pmc_dispatch_hold_s = get<double>(d, "pmc_dispatch_hold_s", c.sampler.pmc_dispatch_hold_s);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
@@ -287,8 +285,7 @@ class PyExporter {
     o["slow_read_seconds"] = st.slow_ns_total.load() * 1e-9;
     o["pmc_quiet"] = st.pmc_quiet.load();
     o["pmc_quiet_skips"] = st.pmc_quiet_skips.load();
-    o["pmc_gap"] = st.pmc_gap.load();
-    o["pmc_gap_skips"] = st.pmc_gap_skips.load();
+    o["pmc_dispatch_skips"] = st.pmc_dbound_skips.load();
     o["pmc_dispatch_bound"] = st.pmc_dbound.load();
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
@@ -533,18 +530,13 @@ PYBIND11_MODULE(_kgs_native, m) {
               throw py::value_error("pmc_idle_hz must be 0 or within [0.01, 100000]");
           },
           "Counter READ rate while the GPU has no wave (adaptive; 0 = every tick)")
-      .def(
-          "set_pmc_gap",
-          [](PyExporter& e, double busy_min, double hz) {
-            if (e.sampler() && !e.sampler()->set_pmc_gap(busy_min, hz))
-              throw py::value_error("busy_min must be within [0, 1] and hz within (0, 100000]");
+      .def_property(
+          "pmc_dispatch_hz", [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_dispatch_hz() : 0.0; },
+          [](PyExporter& e, double hz) {
+            if (e.sampler() && !e.sampler()->set_pmc_dispatch_hz(hz))
+              throw py::value_error("pmc_dispatch_hz must be within (0, 100000]");
           },
-          py::arg("busy_min"), py::arg("hz") = 500.0,
-          "Dispatch-gap READ rate: READs at hz while the SPI-busy share stays below busy_min (0 = off)")
-      .def_property_readonly("pmc_busy_min",
-                             [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_busy_min() : 0.0; })
-      .def_property_readonly("pmc_gap_hz",
-                             [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_gap_hz() : 0.0; })
+          "Counter READ rate while the CP dispatches with no wave in flight (--pmc-cp-only-min)")
       .def_property_readonly("slow_passes", &PyExporter::slow_passes);
   // The utilisation estimators as pure units (util_estimator.h): the offline replay of
   // raw READ dumps runs the sampler's own code.
@@ -563,8 +555,6 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def_readwrite("read_only_bills_zero", &EstimatorParams::read_only_bills_zero)
       .def_readwrite("ewma", &EstimatorParams::ewma)
       .def_readwrite("quiet_hold_ns", &EstimatorParams::quiet_hold_ns)
-      .def_readwrite("busy_min", &EstimatorParams::busy_min)
-      .def_readwrite("gap_hold_ns", &EstimatorParams::gap_hold_ns)
       .def_readwrite("cp_only_min", &EstimatorParams::cp_only_min)
       .def_readwrite("dbound_hold_ns", &EstimatorParams::dbound_hold_ns)
       .def_readwrite("num_simds", &EstimatorParams::num_simds);
@@ -580,10 +570,8 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def_readonly("cp_only_share", &DrainStep::cp_only_share)
       .def_readonly("learned", &DrainStep::learned)
       .def_readonly("quiet_interval", &DrainStep::quiet_interval)
-      .def_readonly("gap_interval", &DrainStep::gap_interval)
       .def_readonly("dbound_interval", &DrainStep::dbound_interval)
       .def_readonly("quiet", &DrainStep::quiet)
-      .def_readonly("gap", &DrainStep::gap)
       .def_readonly("dbound", &DrainStep::dbound);
   py::class_<DispatchEstimator>(m, "DispatchEstimator")
       .def(py::init<>())

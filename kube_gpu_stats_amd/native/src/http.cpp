@@ -350,18 +350,16 @@ void HttpServer::loop() {
             respond(c, 200, "OK", "application/json",
                     "{\"pmc_idle_hz\":" + std::to_string(s ? s->pmc_idle_hz() : 0.0) + "}");
           }
-        } else if (target == "/control/pmc/gap") {
-          // Dispatch-gap READ rate (--pmc-busy-min, --pmc-gap-hz); min=0 turns it off;
-          // no min only reads the setting.  Out of range → 400.
+        } else if (target == "/control/pmc/dispatch") {
+          // Dispatch-bound READ rate (--pmc-dispatch-hz); no hz only reads the setting.
+          // Out of range → 400.
           Sampler* s = ex_->sampler();
-          const double mn = query_double(query, "min", -1.0);
-          const double hz = query_double(query, "hz", s ? s->pmc_gap_hz() : 1000.0);
-          if (s && mn != -1.0 && !s->set_pmc_gap(mn, hz)) {
-            respond(c, 400, "Bad Request", "text/plain", "min must be within [0, 1] and hz within (0, 100000]\n");
+          const double hz = query_double(query, "hz", -1.0);
+          if (s && hz != -1.0 && !s->set_pmc_dispatch_hz(hz)) {
+            respond(c, 400, "Bad Request", "text/plain", "hz must be within (0, 100000]\n");
           } else {
             respond(c, 200, "OK", "application/json",
-                    "{\"pmc_busy_min\":" + std::to_string(s ? s->pmc_busy_min() : 0.0) +
-                        ",\"pmc_gap_hz\":" + std::to_string(s ? s->pmc_gap_hz() : 0.0) + "}");
+                    "{\"pmc_dispatch_hz\":" + std::to_string(s ? s->pmc_dispatch_hz() : 0.0) + "}");
           }
         } else if (ex_->config().control_http && (target == "/control/pause" || target == "/control/resume")) {
           if (target == "/control/pause") ex_->pause_sampling();

@@ -752,13 +752,11 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_quiet", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_quiet.load()));
     w.head(KGS_METRIC_DOC("kgs_pmc_quiet_skips_total"));
     for (int d : ids) w.line_u("kgs_pmc_quiet_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_quiet_skips.load());
-    w.head(KGS_METRIC_DOC("kgs_pmc_gap"));
-    for (int d : ids) w.line_u("kgs_pmc_gap", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_gap.load()));
     w.head(KGS_METRIC_DOC("kgs_pmc_dispatch_bound"));
     for (int d : ids)
       w.line_u("kgs_pmc_dispatch_bound", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_dbound.load()));
-    w.head(KGS_METRIC_DOC("kgs_pmc_gap_skips_total"));
-    for (int d : ids) w.line_u("kgs_pmc_gap_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_gap_skips.load());
+    w.head(KGS_METRIC_DOC("kgs_pmc_dispatch_skips_total"));
+    for (int d : ids) w.line_u("kgs_pmc_dispatch_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_dbound_skips.load());
     w.head(KGS_METRIC_DOC("kgs_pmc_failed"));
     for (int d : ids) w.line_u("kgs_pmc_failed", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_failed.load()));
     w.head(KGS_METRIC_DOC("kgs_pmc_breaker_trips_total"));

@@ -67,8 +67,6 @@ EstimatorParams estimator_params(const SamplerConfig& cfg, int num_cu) {
   p.time_split_weight = kTimeSplitWeight;
   p.gap_clock_fresh_ns = kGapClockFreshNs;
   p.quiet_hold_ns = kQuietHoldNs;
-  p.busy_min = cfg.pmc_busy_min;
-  p.gap_hold_ns = static_cast<int64_t>(cfg.pmc_gap_hold_s * 1e9);
   p.cp_only_min = cfg.pmc_cp_only_min;
   p.dbound_hold_ns = static_cast<int64_t>(cfg.pmc_dispatch_hold_s * 1e9);
   p.plausible_mhz_lo = kPlausibleMhzLo;
@@ -122,8 +120,7 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
   if (cfg_.pmc_retry_max_s < cfg_.pmc_retry_s) cfg_.pmc_retry_max_s = cfg_.pmc_retry_s;
   const double ih = cfg_.pmc_idle_hz;
   pmc_idle_hz_.store(!(ih > 0) ? 0.0 : std::clamp(ih, kMinIdleHz, kMaxHz));
-  if (!set_pmc_gap(cfg_.pmc_busy_min, cfg_.pmc_gap_hz)) set_pmc_gap(0.0, 500.0);
-  if (!(cfg_.pmc_gap_hold_s >= 0)) cfg_.pmc_gap_hold_s = 0.0;
+  if (!set_pmc_dispatch_hz(cfg_.pmc_dispatch_hz)) set_pmc_dispatch_hz(500.0);
   if (!(cfg_.pmc_cp_only_min >= 0 && cfg_.pmc_cp_only_min <= 1)) cfg_.pmc_cp_only_min = 0.0;
   if (!(cfg_.pmc_dispatch_hold_s >= 0)) cfg_.pmc_dispatch_hold_s = 0.0;
   for (int d : dev_ids_) {
@@ -174,10 +171,9 @@ bool Sampler::set_pmc_idle_hz(double hz) {
   return true;
 }
 
-bool Sampler::set_pmc_gap(double busy_min, double hz) {
-  if (!(busy_min >= 0 && busy_min <= 1 && hz > 0 && hz <= kMaxHz)) return false;
-  pmc_busy_min_.store(busy_min, std::memory_order_relaxed);
-  pmc_gap_hz_.store(hz, std::memory_order_relaxed);
+bool Sampler::set_pmc_dispatch_hz(double hz) {
+  if (!(hz > 0 && hz <= kMaxHz)) return false;
+  pmc_dispatch_hz_.store(hz, std::memory_order_relaxed);
   return true;
 }
 
@@ -418,8 +414,8 @@ void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, In
   double slow_hz = hz_.load(std::memory_order_relaxed);
   const double idle = pmc_idle_hz_.load(std::memory_order_relaxed);
   if (idle > 0) slow_hz = std::min(slow_hz, idle);
-  if ((pmc_busy_min_.load(std::memory_order_relaxed) > 0 || cfg_.pmc_cp_only_min > 0) && idle > 0)
-    slow_hz = std::min(slow_hz, pmc_gap_hz_.load(std::memory_order_relaxed));
+  if (cfg_.pmc_cp_only_min > 0 && idle > 0)
+    slow_hz = std::min(slow_hz, pmc_dispatch_hz_.load(std::memory_order_relaxed));
   const int64_t fresh_ns = static_cast<int64_t>(3e9 / slow_hz) + 50000000LL;
   CounterCover c;
   c.ok = st.pmc_on.load(std::memory_order_relaxed) && !st.pmc_stalled.load(std::memory_order_relaxed) &&
@@ -576,7 +572,6 @@ void Sampler::run_pmc(Worker& w) {
     if (gone()) return;
   }
   st.pmc_quiet.store(0, std::memory_order_relaxed);
-  st.pmc_gap.store(0, std::memory_order_relaxed);
   st.pmc_dbound.store(0, std::memory_order_relaxed);
   // Everything learned from the counts (READ cost, clocks, rate hysteresis, stall
   // watch) lives in the estimator (util_estimator.h); this thread schedules the
@@ -613,7 +608,6 @@ void Sampler::run_pmc(Worker& w) {
     st.pmc_on.store(0);
     st.pmc_stalled.store(0);
     st.pmc_quiet.store(0, std::memory_order_relaxed);
-    st.pmc_gap.store(0, std::memory_order_relaxed);
     st.pmc_dbound.store(0, std::memory_order_relaxed);
     st.pmc_fail_streak = 0;
     st.pmc_retry_at_ns = now + static_cast<int64_t>(st.pmc_backoff_s * 1e9);
@@ -669,14 +663,14 @@ void Sampler::run_pmc(Worker& w) {
       }
     }
     bool pmc_now = st.pmc_on.load(std::memory_order_relaxed) != 0;
-    if (pmc_now && (est.quiet() || est.gap() || est.dbound())) {
-      // Quiet (no waves) READs at the idle rate, a dispatch gap at the gap rate;
-      // profiling mode (idle rate 0) READs every tick.
+    if (pmc_now && (est.quiet() || est.dbound())) {
+      // Quiet (no waves) READs at the idle rate, a dispatch-bound stream at the
+      // dispatch rate; profiling mode (idle rate 0) READs every tick.
       const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
-      const double slow_hz = est.quiet() ? idle_hz : pmc_gap_hz_.load(std::memory_order_relaxed);
+      const double slow_hz = est.quiet() ? idle_hz : pmc_dispatch_hz_.load(std::memory_order_relaxed);
       if (idle_hz > 0 && slow_hz < hz && mono_ns() - last_pmc_ns < static_cast<int64_t>(1e9 / slow_hz)) {
         pmc_now = false;
-        (est.quiet() ? st.pmc_quiet_skips : st.pmc_gap_skips).fetch_add(1, std::memory_order_relaxed);
+        (est.quiet() ? st.pmc_quiet_skips : st.pmc_dbound_skips).fetch_add(1, std::memory_order_relaxed);
       }
     }
     if (pmc_now) {
@@ -697,7 +691,6 @@ void Sampler::run_pmc(Worker& w) {
           st.pmc_failed.store(0);
           st.pmc_backoff_s = cfg_.pmc_retry_s;
         }
-        ep.busy_min = pmc_busy_min_.load(std::memory_order_relaxed);
         Drain dr;
         dr.mono_ns = ps.mono_ns;
         dr.mask = ps.mask;
@@ -719,7 +712,6 @@ void Sampler::run_pmc(Worker& w) {
         P.pmc_clk_idle_hz = est.clk_idle_hz();
         P.pmc_clk_busy_hz = est.clk_busy_hz();
         st.pmc_quiet.store(r.quiet ? 1 : 0, std::memory_order_relaxed);
-        st.pmc_gap.store(r.gap ? 1 : 0, std::memory_order_relaxed);
         st.pmc_dbound.store(r.dbound ? 1 : 0, std::memory_order_relaxed);
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);

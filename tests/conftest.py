@@ -7,6 +7,28 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def gpurun_out_digest() -> str:
+    """sha256 over every file under gpurun_out/ (path, size, bytes)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    root = os.path.join(REPO, "gpurun_out")
+    for d, dirs, files in sorted(os.walk(root)):
+        dirs.sort()
+        for f in sorted(files):
+            p = os.path.join(d, f)
+            h.update(os.path.relpath(p, root).encode())
+            try:
+                with open(p, "rb") as fh:
+                    h.update(fh.read())
+            except OSError:
+                h.update(b"<unreadable>")
+    return h.hexdigest()
+
+
+GPURUN_OUT_AT_START = gpurun_out_digest()
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on a GPU box)")
     config.addinivalue_line("markers", "slow: takes more than a few seconds")

@@ -67,9 +67,9 @@ FAST = ["--hz", "8000", "--pmc-batch", "8", "--step-ms", "60", "--rounds", "4", 
 
 
 @pytest.mark.slow
-def test_bench_contract_single_process():
+def test_bench_contract_single_process(tmp_path):
     r = subprocess.run([sys.executable, "bench.py", "--mock", "--steps", "10", "--warmup", "1", *FAST,
-                        "--util-hz", "1000,10"],
+                        "--util-hz", "1000,10", "--out", str(tmp_path / "bench.json")],
                        cwd=REPO, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     line, res = _result(r.stdout)
@@ -158,10 +158,10 @@ def test_bench_contract_single_process():
 
 
 @pytest.mark.slow
-def test_bench_contract_torchrun_gloo_world2():
+def test_bench_contract_torchrun_gloo_world2(tmp_path):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2", "--mock",
-                        "--steps", "6", "--warmup", "1", *FAST],
+                        "--steps", "6", "--warmup", "1", *FAST, "--out", str(tmp_path / "bench.json")],
                        cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     _, res = _result(r.stdout)
@@ -172,14 +172,15 @@ def test_bench_contract_torchrun_gloo_world2():
 
 
 @pytest.mark.slow
-def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads():
+def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads(tmp_path):
     """The 8-GPU driver run must validate itself unattended: phase X
     books a GPU 0 → GPU k peer copy per peer (the mock backend puts it on the link to
     k) and finds each copy on the link whose peer_bdf is k's, at unit ratio 1; the
     interleaved overheads come per rank and per component, power per rank."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "bench.py", "--mock", "--gpus", "8", "--steps", "4", "--warmup", "1",
-                        *FAST, "--hz", "2000", "--capacity-hz", "", "--burst-s", "0", "--quiet-s", "0"],
+                        *FAST, "--hz", "2000", "--capacity-hz", "", "--burst-s", "0", "--quiet-s", "0",
+                        "--out", str(tmp_path / "bench.json")],
                        cwd=REPO, capture_output=True, text=True, timeout=420, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     line, res = _result(r.stdout)
@@ -202,11 +203,12 @@ def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads():
 
 
 @pytest.mark.slow
-def test_bench_self_spawns_ranks_without_torchrun():
+def test_bench_self_spawns_ranks_without_torchrun(tmp_path):
     """`python bench.py --gpus 4` (no torchrun env) launches 4 ranks itself, so a plain
     invocation — the driver's scaling runs included — measures N GPUs, not 1."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run([sys.executable, "bench.py", "--mock", "--gpus", "4", "--steps", "6", "--warmup", "1", *FAST],
+    r = subprocess.run([sys.executable, "bench.py", "--mock", "--gpus", "4", "--steps", "6", "--warmup", "1", *FAST,
+                        "--out", str(tmp_path / "bench.json")],
                        cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     _, res = _result(r.stdout)

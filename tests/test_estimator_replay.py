@@ -396,3 +396,62 @@ def test_dispatch_estimator_reads_a_square_wave_at_one_clock(N, hz, period, duty
     truth = sum(min(max(rows[-1][0] - 10.0 - k * period, 0.0), duty * period)
                 for k in range(int((rows[-1][0] - 10.0) / period) + 2)) / (rows[-1][0] - 10.0)
     assert 100 * r["dispatch_s"] / r["span_s"] == pytest.approx(100 * truth, abs=1.5), (r, truth)
+
+
+@settings(max_examples=25, deadline=None)
+@given(hz=st.sampled_from([8000.0, 1000.0, 100.0]),
+       lo=st.floats(min_value=0.86, max_value=0.90),
+       hi=st.floats(min_value=0.90, max_value=0.95),
+       seed=st.integers(0, 10_000))
+def test_a_saturated_stream_never_leaves_the_full_read_rate(N, hz, lo, hi, seed):
+    """back-to-back MFMA kernels keep the CP busy every interval while
+    their SPI share wanders 89.6-94.8 % from box to box (r3h, r3j, r4d, r5, GPUTEST_r05).
+    Round 5's SPI-keyed gap rate put 28 % of such a stream on a slower READ rate at a 0.9
+    threshold; the only rate machines left key on "no wave at all" (quiet) and on CP busy
+    without waves (dispatch-bound, cp_only_min 0.3), so wherever the per-interval SPI share
+    wanders in [0.86, 0.95] the stream keeps every tick and bills whole."""
+    p = N.sampler_estimator_params()
+    e = N.DispatchEstimator()
+    e.restart(0)
+    rnd = random.Random(seed)
+    f, t, cnt, spi, cpc, mfma = 2.1, 0, 0, 0, 0, 0
+    period = int(1e9 / hz)
+    busy = span = 0.0
+    for _ in range(int(min(hz, 1000) * 2)):  # 2 s at ≤ 1 kHz, 0.25 s at 8 kHz
+        t += period
+        clk = int(period * f)
+        cnt += clk
+        cpc += int(clk * rnd.uniform(0.97, 1.0))
+        spi += int(clk * rnd.uniform(lo, hi))
+        mfma += int(clk * 1024 * 0.8)
+        s = e.feed(p, t, cnt, spi, cpc, mfma=mfma)
+        assert not (s.quiet or s.dbound or s.quiet_interval or s.dbound_interval), (lo, hi, s.cp_only_share)
+        busy += s.dispatch_s
+        span += s.span_s
+    assert busy / span == pytest.approx(1.0, abs=0.02)
+    assert not hasattr(s, "gap") and not hasattr(p, "busy_min")
+
+
+def test_a_microsecond_kernel_stream_is_dispatch_bound_after_the_hold(N):
+    """The rate machine that replaced it: CP busy ≈100 % with waves ≈41 % of the clocks (a
+    HIP graph of 1.7 µs copies on MI355X, profiles/r4/ r4b) turns dispatch-bound once the
+    10 ms hold has passed, and a long kernel ends it on its first interval."""
+    p = N.sampler_estimator_params()
+    e = N.DispatchEstimator()
+    e.restart(0)
+    t = cnt = spi = cpc = 0
+    period, f = 125_000, 2.4
+    states = []
+    for i in range(160):  # 20 ms at 8 kHz
+        t += period
+        clk = int(period * f)
+        cnt += clk
+        cpc += clk
+        spi += int(0.41 * clk)
+        states.append(e.feed(p, t, cnt, spi, cpc, mfma=0).dbound)
+    assert not any(states[:79]) and all(states[81:]), states.index(True)
+    t += period
+    cnt += int(period * f)
+    cpc += int(period * f)
+    spi += int(0.95 * period * f)
+    assert not e.feed(p, t, cnt, spi, cpc, mfma=10**9).dbound

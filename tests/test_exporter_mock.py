@@ -610,73 +610,47 @@ def test_counter_tick_dither_keeps_the_rate(mock_exporter):
         assert 0.9 * 1000 <= rate <= 1.01 * 1000, (dither, rate)
 
 
-def test_dispatch_gap_reads_drop_to_gap_rate(mock_exporter):
-    """Dispatch-gap READ rate (--pmc-busy-min): each READ packet delays the workload's
-    dispatches, and a READ whose IB is all NOPs costs a training step as much as a
-    real one (profiles/r3/README.md, r3e).  While the READ intervals show waves for
-    less than busy_min of the clocks, READs drop to the gap rate; a share at or
-    above busy_min, or profiling mode, READs every tick.  Integrals stay exact."""
-    def rate(ex, secs=1.0):
-        n0 = ex.integrals(0)["pmc_samples"]
-        time.sleep(secs)
-        return (ex.integrals(0)["pmc_samples"] - n0) / secs
-
-    ex = mock_exporter(n_gpus=1, hz=2000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=50,
-                       window_s=1.0, mock={"util_base": 50, "util_amp": 0})   # 50 % SPI-busy share
-    time.sleep(0.2)
-    assert ex.pmc_busy_min == 0 and rate(ex, 0.5) > 1400                  # off by default: every tick
-    ex.set_pmc_gap(0.9, 200)
-    time.sleep(0.05)
-    r_gap = rate(ex)
-    assert 150 <= r_gap <= 260, r_gap                                   # ≈ the gap rate, not 2000
-    m = parse_text(ex.render())
-    assert m["kgs_pmc_gap"][0][1] == 1 and m["kgs_pmc_gap_skips_total"][0][1] > 1000
-    assert m["kgs_pmc_quiet"][0][1] == 0
-    w = ex.window(0, 1.0)
-    assert w["gpu_active_pct"] == pytest.approx(50, abs=4), w             # exact at any READ rate
-    ex.set_pmc_gap(0.3, 200)                                            # 50 % ≥ 30 %: every tick again
-    time.sleep(0.05)
-    assert rate(ex, 0.5) > 1400
-    assert ex.integrals(0)["pmc_gap"] == 0
-    with urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/gap?min=0.9&hz=200", timeout=5) as r:
-        assert json.load(r) == {"pmc_busy_min": 0.9, "pmc_gap_hz": 200.0}
-    ex.pmc_idle_hz = 0                                                  # profiling mode overrides it
-    time.sleep(0.05)
-    assert rate(ex, 0.5) > 1400
-    for bad in ("min=1.5", "min=-0.5", "min=0.5&hz=0"):
-        with pytest.raises(urllib.error.HTTPError) as e:
-            urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/gap?{bad}", timeout=5)
-        assert e.value.code == 400, bad
-    with pytest.raises(ValueError):
-        ex.set_pmc_gap(2.0)
-    assert ex.pmc_busy_min == 0.9 and ex.pmc_gap_hz == 200
-
-
-def test_dispatch_bound_reads_drop_to_gap_rate(mock_exporter):
+def test_dispatch_bound_reads_drop_to_dispatch_rate(mock_exporter):
     """Dispatch-bound READ rate (--pmc-cp-only-min, on by default): a stream of µs
     kernels keeps the CP busy while waves are present only part of the time (on
     MI355X: CPC ≈100 %, SPI ≈41 %), and that stream pays each READ packet (+3.8 % at
     8 kHz, profiles/r4/ r4c).  The mock's wave_frac 0.4 models it: after the hold,
-    READs drop to the gap rate and the dispatch integral stays exact (100 %); long
-    kernels (wave_frac 1) and --pmc-cp-only-min 0 keep every tick."""
+    READs drop to the dispatch rate and the dispatch integral stays exact (100 %); long
+    kernels (wave_frac 1) and --pmc-cp-only-min 0 keep every tick.  The rate is
+    settable in place (Python property, loopback /control/pmc/dispatch)."""
     def rate(ex, secs=0.6):
         n0 = ex.integrals(0)["pmc_samples"]
         time.sleep(secs)
         return (ex.integrals(0)["pmc_samples"] - n0) / secs
 
     kw = dict(n_gpus=1, hz=4000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100, window_s=1.0,
-              pmc_gap_hz=500)
+              pmc_dispatch_hz=500)
     ex = mock_exporter(mock={"util_base": 100, "util_amp": 0}, mock_pmc={"wave_frac": 0.4}, **kw)
     time.sleep(0.3)
     a, t0 = ex.integrals(0), time.time()
     r = rate(ex)
     b, dt = ex.integrals(0), time.time() - t0
-    assert 350 <= r <= 750, r                                           # ≈ the gap rate, not 4000
-    assert b["pmc_dispatch_bound"] == 1 and b["pmc_gap"] == 0 and b["pmc_quiet"] == 0, b
+    assert 350 <= r <= 750, r                                           # ≈ the dispatch rate, not 4000
+    assert b["pmc_dispatch_bound"] == 1 and b["pmc_quiet"] == 0 and "pmc_gap" not in b, b
     assert (b["dispatch_seconds"] - a["dispatch_seconds"]) / dt == pytest.approx(1.0, abs=0.03)
     assert (b["active_seconds"] - a["active_seconds"]) / dt == pytest.approx(0.4, abs=0.03)
     m = parse_text(ex.render())
-    assert m["kgs_pmc_dispatch_bound"][0][1] == 1 and m["kgs_pmc_gap_skips_total"][0][1] > 1000
+    assert m["kgs_pmc_dispatch_bound"][0][1] == 1 and m["kgs_pmc_dispatch_skips_total"][0][1] > 1000
+    assert "kgs_pmc_gap" not in m and "kgs_pmc_gap_skips_total" not in m
+    ex.pmc_dispatch_hz = 200
+    time.sleep(0.05)
+    assert 150 <= rate(ex) <= 300
+    with urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/dispatch?hz=1000", timeout=5) as resp:
+        assert json.load(resp) == {"pmc_dispatch_hz": 1000.0}
+    time.sleep(0.05)
+    assert 700 <= rate(ex) <= 1300
+    for bad in ("hz=0", "hz=-5", "hz=200000"):
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/dispatch?{bad}", timeout=5)
+        assert e.value.code == 400, bad
+    with pytest.raises(ValueError):
+        ex.pmc_dispatch_hz = 0
+    assert ex.pmc_dispatch_hz == 1000
     ex.stop()
 
     for extra in ({"mock_pmc": {"wave_frac": 1.0}}, {"mock_pmc": {"wave_frac": 0.4}, "pmc_cp_only_min": 0.0}):

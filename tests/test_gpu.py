@@ -830,80 +830,10 @@ def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
     assert a["publishes_per_s"] >= 0.9 * a["reads_per_s"], a
 
 
-def test_dispatch_gap_rate_follows_the_kernel_stream(torch_dev):
-    """--pmc-busy-min on MI355X (profiles/r3/README.md r3e/r3f): every READ is an AQL
-    packet the command processor handles between the workload's dispatches.  While a
-    HIP graph of µs kernels runs (waves in flight for well under 90 % of the clocks)
-    the sampler READs at --pmc-gap-hz; the long MFMA kernel (SPI busy ≈96 %) keeps
-    every tick."""
-    import torch
-
-    from kube_gpu_stats_amd.ops.load import LoadStep
-    from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
-
-    dev = torch.device("cuda", 0)
-    ls = LoadStep(device=0, mfma_blocks=2048, mfma_iters=20000, stream_bytes=1 << 30)
-    ls.run_mfma()
-    x = torch.zeros(16384, device=dev)
-    side = torch.cuda.Stream(device=dev)
-    with torch.cuda.stream(side):
-        for _ in range(3):
-            x.add_(1.0)
-    torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        for _ in range(2000):
-            x.add_(1.0)
-    graph.replay()
-    torch.cuda.synchronize()
-    proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
-                             "--hz", "8000", "--pmc", "aqlprofile", "--pmc-busy-min", "0.9", "--pmc-gap-hz", "1000",
-                             "--control-stdin", "--bdfs", _bdf0(), "--proc-every", "0", "--link-every", "0",
-                             "--window", "1"],
-                            cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    one = lambda m, f: m[f][0][1] if m.get(f) else None  # noqa: E731
-    rows = {}
-    try:
-        ready = json.loads(proc.stdout.readline())
-        assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
-        sc = Scraper("127.0.0.1", ready["port"])
-
-        def phase(name, run, secs=1.5):
-            m0 = parse_text(sc.get())
-            t0 = time.time()
-            gap_seen = 0
-            while time.time() - t0 < secs:
-                run()
-                run()
-                gap_seen = max(gap_seen, one(parse_text(sc.get()), "kgs_pmc_gap") or 0)  # while the work is queued
-                torch.cuda.synchronize()
-            dt = time.time() - t0
-            m1 = parse_text(sc.get())
-            d = lambda f: one(m1, f) - one(m0, f)  # noqa: E731
-            rows[name] = {"reads_per_s": d("kgs_pmc_samples_total") / dt, "gap_skips_per_s": d("kgs_pmc_gap_skips_total") / dt,
-                          "gap_seen": gap_seen, "gpu_active_pct": one(m1, "amdgpu_gpu_active_percent")}
-
-        phase("tiny_graph", graph.replay)
-        phase("mfma", ls.run_mfma)
-    finally:
-        try:
-            proc.stdin.write("quit\n")
-            proc.stdin.flush()
-            proc.communicate(timeout=30)
-        except Exception:  # noqa: BLE001
-            proc.kill()
-            proc.communicate()
-    _keep("dispatch_gap.json", json.dumps(rows, indent=1))
-    print(json.dumps(rows))
-    g, k = rows["tiny_graph"], rows["mfma"]
-    assert g["gap_seen"] == 1 and g["reads_per_s"] < 3000 and g["gap_skips_per_s"] > 4000, g
-    assert k["reads_per_s"] > 7000 and k["gap_skips_per_s"] < 1000, k
-
-
 def test_dispatch_bound_rate_at_default_flags(torch_dev):
     """--pmc-cp-only-min (default 0.3) on MI355X: a HIP graph of µs kernels keeps the CP
     dispatching with waves present only ≈40 % of the clocks (profiles/r4/ r4b), so at
-    default flags and 8 kHz its READs drop to the gap rate (1 kHz); back-to-back MFMA
+    default flags and 8 kHz its READs drop to the dispatch rate (500 Hz); back-to-back MFMA
     kernels, and a training-like step whose µs kernels last less than the 10 ms hold,
     keep every tick."""
     import torch
@@ -957,9 +887,9 @@ def test_dispatch_bound_rate_at_default_flags(torch_dev):
             m1 = parse_text(sc.get())
             d = lambda f: one(m1, f) - one(m0, f)  # noqa: E731
             rows[name] = {"reads_per_s": d("kgs_pmc_samples_total") / dt,
-                          "gap_skips_per_s": d("kgs_pmc_gap_skips_total") / dt,
+                          "dispatch_skips_per_s": d("kgs_pmc_dispatch_skips_total") / dt,
                           # the first scrape can still show the previous phase's state: the
-                          # gap-rate READ that clears it is up to 2 ms away
+                          # dispatch-rate READ that clears it is up to 2 ms away
                           "dispatch_bound_share": sum(seen[1:]) / max(1, len(seen) - 1),
                           "dispatch_pct": 100 * d("amdgpu_dispatch_busy_seconds_total") / dt,
                           "spi_pct": 100 * d("amdgpu_gpu_active_seconds_total") / dt}

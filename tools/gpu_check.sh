@@ -34,11 +34,11 @@ for s in $STEPS; do
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc none --out "$OUT/trainpmfw.json" ;;
     train2) run train2 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 2 --out "$OUT/train2.json" ;;
-    tdef|tdef2|tpmfw|tagent|tl3agent|tnop|t1k|tgap*|tbatch*|tpub*|tnobatch|tnobatch2|t16k)
+    tdef|tdef2|tpmfw|tagent|tl3agent|tnop|t1k|tbatch*|tpub*|tnobatch|tnobatch2|t16k)
         # training-step side runs, 36 rounds = every block order 6 times:
         #   tdef (defaults) tpmfw (no READs) tagent (release fence at agent scope)
         #   tl3agent (lean 3 + agent release) tnop (every READ packet a NOP: the bare
-        #   packet's cost; values stale) t1k (1 kHz tier) tgapNN (--pmc-busy-min 0.NN)
+        #   packet's cost; values stale) t1k (1 kHz tier)
         T=(python -u bench.py --load train --steps 10 --warmup 2 --rounds 36 --hz-list 100 --capacity-hz ""
            --burst-s 0 --quiet-s 0 --component-s 0 --util-s 0 --out "$OUT/$s.json")
         case $s in
@@ -48,7 +48,6 @@ for s in $STEPS; do
           tl3agent) KGS_AQL_FENCE=none,agent KGS_AQL_LEAN=3 run $s 600 "${T[@]}" ;;
           tnop) KGS_AQL_LEAN=5 run $s 600 "${T[@]}" ;;
           t1k) run $s 600 "${T[@]}" --hz 1000 ;;
-          tgap*) run $s 600 "${T[@]}" --pmc-busy-min "0.${s#tgap}" ;;  # tgap90: --pmc-busy-min 0.90
           tbatch*) run $s 600 "${T[@]}" --pmc-batch "${s#tbatch}" ;;      # tbatch8: --pmc-batch 8
           tpub*) run $s 600 "${T[@]}" --pmc-publish-us "${s#tpub}" ;;     # tpub0: count-only batches
           tnobatch|tnobatch2) run $s 600 "${T[@]}" --pmc-batch 1 ;;
@@ -61,7 +60,6 @@ for s in $STEPS; do
     bnd) KGS_TICK_DITHER=0 run $s 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/$s.json" ;;
     bnobatch|bnobatch2) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch 1 --out "$OUT/$s.json" ;;
     bbatch*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-batch "${s#bbatch}" --out "$OUT/$s.json" ;;
-    bgap*) run $s 600 python -u bench.py --steps 20 --warmup 5 --pmc-busy-min "0.${s#bgap}" --out "$OUT/$s.json" ;;
     soak) run soak 420 python -u tools/soak.py --seconds 240 --out "$OUT/soak.json" ;;
     rss) run rss 180 python -u tools/rss_probe.py --out "$OUT/rss_probe.json" ;;
     hsarss) run hsarss 300 python -u tools/hsa_rss_probe.py --out "$OUT/hsa_rss.json" ;;
@@ -85,7 +83,7 @@ for s in $STEPS; do
     testsnw) run pytest_gpu 700 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
                -p no:cacheprovider -k "not wedged_counter_queue" ;;
     testsdb) run pytest_dbound 400 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
-               -p no:cacheprovider -k "dispatch_bound or dispatch_gap or read_immune" ;;
+               -p no:cacheprovider -k "dispatch_bound or read_immune" ;;
     testslite) run pytest_lite 300 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
                  -p no:cacheprovider -k "lite_reads or dispatch_bound or two_tenants" ;;
     # round 5
@@ -109,6 +107,11 @@ for s in $STEPS; do
              run lowrate_10_sat 60 python -u tools/lowrate_probe.py --hz 10 --burst-ms 3000 --period-ms 3000 \
                --load-s 3 --out "$OUT/lr_10_sat.json"
              run lowrate_100 60 python -u tools/lowrate_probe.py --hz 100 --out "$OUT/lr_100.json" ;;
+    # round 6: the driver's own invocation (one process, -x), and the same without -x
+    testsx) run pytest_gpu_x 900 python -u -m pytest tests -x -q -m gpu --timeout 150 --timeout-method thread \
+              -p no:cacheprovider -rA ;;
+    testsall) run pytest_gpu_all 900 python -u -m pytest tests -q -m gpu -v --timeout 150 --timeout-method thread \
+                -p no:cacheprovider -rA ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;

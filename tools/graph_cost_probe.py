@@ -8,7 +8,7 @@ probe measures only that component, for several exporter variants on the same bo
 
 * ``default``   — the shipped exporter: batched READs, and the dispatch-bound READ
   rate (--pmc-cp-only-min 0.3: a GPU whose CP dispatches with no wave in flight for
-  ≥ 30 % of the clocks is READ at --pmc-gap-hz, 1 kHz);
+  ≥ 30 % of the clocks is READ at --pmc-dispatch-hz, 1 kHz);
 * ``full_rate`` — --pmc-cp-only-min 0: every tick READs, whatever the workload (the
   round-4 r4c reader: +3.8 % at 8 kHz; the KGS_AQL_NOBARRIER and low-priority READ
   queue variants measured the same there and were deleted);
