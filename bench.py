@@ -1,2045 +1,18 @@
 #!/usr/bin/env python3
-"""Headline benchmark: counter samples/s per GPU, p50 /metrics scrape latency and
-GPU-time overhead %, under synthetic gfx950 load (BASELINE.json "metric").
+"""Headline benchmark entry point (the driver's contract):
 
     python bench.py --gpus N --steps K --warmup W
 
-With N > 1 and no torchrun environment, bench.py starts N rank processes itself
-(``torch.distributed.run``, 127.0.0.1) before anything touches a GPU, and exits
-with their status; under torchrun it is one of those ranks.  One rank per GPU;
-rank 0 prints the result line.
-
-A *step* is a fixed block of synthetic load on every GPU: a *unit* (an MFMA-bound
-bf16 kernel + HBM triads, ops/hip/load_kernels.hip, + a HIP graph of 2000 tiny
-copies — the dispatch-bound part, where the counter reader's command-processor
-packets would cost the workload time) repeated until the step lasts ≥ --step-ms
-(default 500 ms), so every timed region is long against timer and DVFS noise.
-
-  A  K steps, no exporter process                       (baseline)
-  B  K steps, node exporter sampling every GPU at --hz (PMFW table, HBM, per-process
-     list, xGMI, hardware counters) and scraped at --scrape-hz      (THE timed region)
-  R  untimed: a train of ~1 ms MFMA bursts every 5 ms on every GPU, read back from the
-     exporter's full-rate /counters stream — how many bursts the primary rate resolves
-     (``burst_resolution``)
-  Q  untimed: every GPU idle; the exporter's READ rate, the PMFW GFX busy and the
-     SPI-busy share it reports, in the default adaptive mode and in profiling mode
-     (``quiet_gpu``) — the cost of sampling that GPU-time overhead cannot show
-  I  --rounds rounds of one block per condition — exporter paused, then each rate of
-     --hz-list — in alternating order (off,100,8k | 8k,100,off | ...), --block-steps
-     steps per block, scraped while sampling.  Per round, overhead = t_on/t_off − 1;
-     the result is the mean over rounds ± a 95 % t-interval.  Adjacent blocks share
-     thermal and power state, so slow drift cancels (A/B/C cannot do that).  The bench
-     reads the PMFW table itself at every block edge: power and package-power throttle
-     residency per condition (``interleaved.power``; profiles/r2/r2aq).
-  S  untimed: one block at each --capacity-hz rate in profiling mode — delivered drains,
-     overruns, host µs per drain (``capacity``)
-  C  K steps, exporter stopped                           (second baseline)
-
-``value`` = counter samples/s summed over the N GPUs (the driver's contract: the
-whole-job aggregate; weak scaling, per-GPU rate fixed).  ``samples_per_sec_per_gpu``
-is the per-GPU figure the metric name refers to.  A counter sample is one hardware-
-counter drain (values advance on every drain), or one distinct PMFW table where
-the counter tier is unavailable.  Scrape latency is request → last body byte on a
-keep-alive connection, as a Prometheus server sees it (utils/scrape.py).
-
-The exporter runs as its own process (as in production: DaemonSet vs workload),
-launched by local rank 0 over the PCI addresses of every local rank's GPU.
-``--mock`` runs the same flow on CPU with the mock provider (tests only).
+The phases live in the ``bench/`` package (bench/__init__.py describes them); this
+file only puts the repository on sys.path and runs ``bench.cli.main``.  With N > 1
+and no torchrun environment it starts N ranks itself (bench/cli.py spawn_ranks).
 """
-from __future__ import annotations
-
-import argparse
-import json
-import math
 import os
-import select
-import socket
-import subprocess
 import sys
-import time
 
-REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from kube_gpu_stats_amd.parallel import dist as D  # noqa: E402
-from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text  # noqa: E402
-
-METRIC = "counter samples/sec/GPU + p50 scrape latency at 8×MI355X; GPU-time overhead %"
-PMC_READER = "aqlprofile"  # direct CP reads (native/counters/pmc_aqlprofile.cpp)
-
-
-def parse_args(argv=None):
-    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--hz", type=float, default=8000.0,
-                    help="primary sampler tick rate per GPU (phase B): one hardware-counter drain per tick "
-                    "(PMFW table ≤ 100 Hz); 8 kHz costs ≈0.05 exporter cores/GPU; 16 kHz (with --pmc-batch 16) "
-                    "≈0.07 and +0.1 %% GPU time vs paused, +0.01 %% vs released (profiles/r5/r5o)")
-    ap.add_argument("--hz-list", default="100",
-                    help="further tick rates measured in the interleaved rounds (BASELINE config 4 = 100 Hz); "
-                    "'' = primary only")
-    ap.add_argument("--pmc", default="auto", choices=["auto", "aqlprofile", "none"],
-                    help="counter reader (auto = %s)" % PMC_READER)
-    ap.add_argument("--pmc-pipeline", type=int, default=1, choices=[0, 1],
-                    help="aqlprofile reader: pipelined READs (1) or submit-and-wait per sample (0)")
-    ap.add_argument("--pmc-set", default="base", choices=["base", "full"],
-                    help="counter set: base (GRBM clocks + SPI busy + MFMA busy) or full (+ TA busy, 10x the CP register "
-                    "reads)")
-    ap.add_argument("--pmc-dispatch-hz", type=float, default=1000.0,
-                    help="exporter --pmc-dispatch-hz: READ rate while the CP dispatches with no wave in flight")
-    ap.add_argument("--pmc-batch", type=int, default=8,
-                    help="exporter --pmc-batch: counter READs per L2 writeback (8 at 8 kHz: one per ms)")
-    ap.add_argument("--pmc-publish-us", type=int, default=1000, help="exporter --pmc-publish-us")
-    ap.add_argument("--pmc-lean", type=int, default=2, choices=[0, 1, 2, 3],
-                    help="aqlprofile READ packet mode (exporter --pmc-lean; 0 = as aqlprofile builds it)")
-    ap.add_argument("--scrape-hz", type=float, default=20.0)
-    ap.add_argument("--step-ms", type=float, default=500.0,
-                    help="each step repeats the load unit until it lasts at least this long")
-    ap.add_argument("--rounds", type=int, default=48,
-                    help="interleaved rounds (0 = off); 48 x 3 blocks of ~1 s put the 95 %% CI of the "
-                         "overhead under 0.1 %% on a power-capped MI355X (per-round sd 0.18-0.28 %%: r2ag, r2aj)")
-    ap.add_argument("--block-steps", type=int, default=2, help="steps per interleaved block")
-    ap.add_argument("--mfma-iters", type=int, default=150000, help="≈40 ms of MFMA work per unit on MI355X")
-    ap.add_argument("--mfma-blocks", type=int, default=2048)
-    ap.add_argument("--stream-gib", type=float, default=6.0)
-    ap.add_argument("--triads", type=int, default=2)
-    ap.add_argument("--tiny-kernels", type=int, default=2000,
-                    help="dispatch-bound part of each unit: a HIP graph of this many 64 KiB copies (≈1.7 µs each); "
-                    "it is where counter READs on the command processor would show up (0 = off)")
-    ap.add_argument("--load", default="synthetic", choices=["synthetic", "train"],
-                    help="GPU work per unit: the synthetic gfx950 kernels (default) or a PyTorch bf16 "
-                    "decoder training step (forward + backward + AdamW, DDP when N > 1)")
-    ap.add_argument("--train-dim", type=int, default=4096)
-    ap.add_argument("--train-layers", type=int, default=4)
-    ap.add_argument("--train-batch", type=int, default=4)
-    ap.add_argument("--train-seq", type=int, default=2048)
-    ap.add_argument("--train-vocab", type=int, default=32768)
-    ap.add_argument("--xgmi-mib", type=int, default=256, help="RCCL all-reduce size per unit when N > 1 (0 = off)")
-    ap.add_argument("--xgmi-check-mib", type=int, default=2048,
-                    help="phase X (N > 1): bytes of each GPU 0 → GPU k peer copy that checks the link map and unit")
-    ap.add_argument("--xgmi-check-settle", type=float, default=0.5,
-                    help="phase X: seconds between a round of peer copies and the scrape that reads its link counters")
-    ap.add_argument("--xgmi-check-budget-s", type=float, default=120.0,
-                    help="phase X: start no further round of peer copies after this many seconds")
-    ap.add_argument("--mock-xgmi-swap", type=int, default=-1,
-                    help="mock: GPU whose link table reports two ports' peers swapped (phase X must flag it)")
-    ap.add_argument("--xgmi-child", type=int, default=0, help=argparse.SUPPRESS)  # phase X child: exporter port
-    ap.add_argument("--xgmi-bdfs", default="", help=argparse.SUPPRESS)
-    ap.add_argument("--settle", type=float, default=1.0, help="seconds between exporter start and phase B")
-    ap.add_argument("--burst-s", type=float, default=0.6,
-                    help="phase R: length of the MFMA burst train read back from /counters (0 = off; cut to "
-                    "what the full-rate ring holds: ≈1 s at 8 kHz, 0.5 s at 16 kHz)")
-    ap.add_argument("--burst-ms", type=float, default=1.0, help="phase R: length of one burst")
-    ap.add_argument("--burst-period-ms", type=float, default=5.0, help="phase R: burst period")
-    ap.add_argument("--capacity-hz", default="16000,24000,32000",
-                    help="phase S: tick rates above --hz to try under the load, one block each ('' = off)")
-    ap.add_argument("--quiet-s", type=float, default=1.5,
-                    help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
-    ap.add_argument("--component-s", type=float, default=1.0,
-                    help="phase K: seconds each load component runs alone while the exporter samples (0 = off)")
-    ap.add_argument("--released", type=int, default=1, choices=[0, 1],
-                    help="phase I: a fourth interleaved condition, 'released' — counter session STOPped and the "
-                    "reader's READ queue destroyed for the block (1 = on)")
-    ap.add_argument("--util-s", type=float, default=1.5,
-                    help="phase U: seconds of each load (idle, two MFMA burst trains, saturating MFMA) while the "
-                    "exported container_gpu_sm_util / busy counter is checked against the host-known duty (0 = off)")
-    ap.add_argument("--util-hz", default="1000,10",
-                    help="phase U: tick rates besides the primary --hz ('' = primary only); 10 Hz is the "
-                    "DaemonSet's (deploy/daemonset.yaml), each load there runs at least 30 drain periods")
-    ap.add_argument("--mock", action="store_true", help="CPU plumbing run with the mock provider")
-    ap.add_argument("--mock-step-ms", type=float, default=20.0, help="mock: duration of one load unit")
-    ap.add_argument("--mock-latency", type=int, default=1, choices=[0, 1],
-                    help="mock: model AMD SMI call latency under one global lock (profiles/r2/mock_scaling.md)")
-    ap.add_argument("--out", default="", help="write the full result JSON here (default gpurun_out/bench_result_n<N>.json); the "
-                    "exporter log goes next to it")
-    ap.add_argument("--attach", default="", help="host:port of an exporter started with --control-http; it is "
-                    "paused for phases A/C instead of being spawned (lets rocprofv3 trace the bench alone)")
-    return ap.parse_args(argv)
-
-
-def tiers(a) -> list[float]:
-    """Every tick rate measured: the primary --hz plus --hz-list, ascending."""
-    extra = [float(x) for x in str(a.hz_list).split(",") if x.strip()]
-    return sorted({float(a.hz), *extra})
-
-
-# ----------------------------------------------------------------------------- rank launch
-def free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def spawn_ranks(a, argv: list[str]) -> int:
-    """``--gpus N`` without a torchrun environment: start N ranks (one per GPU) with
-    torch.distributed.run as a child process and return its exit status.  This
-    process never initialises a GPU (no HIP call happens before the children run),
-    so nothing here is replaced by exec and no device is held twice."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
-    env = dict(os.environ)
-    env.setdefault("OMP_NUM_THREADS", "4")
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, cwd=REPO, env=env)
-
-
-# ----------------------------------------------------------------------------- statistics
-T975 = {1: 12.706, 2: 4.303, 3: 3.182, 4: 2.776, 5: 2.571, 6: 2.447, 7: 2.365, 8: 2.306, 9: 2.262, 10: 2.228,
-        11: 2.201, 12: 2.179, 13: 2.160, 14: 2.145, 15: 2.131, 16: 2.120, 17: 2.110, 18: 2.101, 19: 2.093,
-        20: 2.086, 24: 2.064, 29: 2.045, 39: 2.023, 59: 2.001}
-
-
-def t975(df: int) -> float:
-    """Two-sided 95 % Student-t quantile (table; 1.96 beyond 60 degrees of freedom)."""
-    if df <= 0:
-        return float("nan")
-    for k in sorted(T975):
-        if df <= k:
-            return T975[k]
-    return 1.96
-
-
-def mean_ci95(xs: list[float]) -> tuple[float, float, float]:
-    """(mean, 95 % half-width, sample SD) of paired differences."""
-    n = len(xs)
-    if n == 0:
-        return float("nan"), float("nan"), float("nan")
-    m = sum(xs) / n
-    if n == 1:
-        return m, float("nan"), float("nan")
-    sd = math.sqrt(sum((x - m) ** 2 for x in xs) / (n - 1))
-    return m, t975(n - 1) * sd / math.sqrt(n), sd
-
-
-# ----------------------------------------------------------------------------- load
-class Load:
-    """A step = ``reps`` back-to-back units (set by calibrate_reps)."""
-
-    reps = 1
-    timing = False  # per-component event timing (interleaved blocks)
-
-    def step(self):
-        for _ in range(self.reps):
-            self.unit()
-
-    def components_start(self) -> None:
-        self.timing = True
-
-    def components_end(self) -> dict:
-        """Seconds of GPU time per load component since components_start (synced)."""
-        self.timing = False
-        return {}
-
-
-class EventTimer:
-    """HIP events bracketing each load component inside a timed block: a component's
-    GPU time per block, so the paired overheads can be split by what the exporter
-    could slow down — a long MFMA kernel, HBM streams, or the dispatch-bound graph of
-    tiny kernels.  Events are recorded in every condition alike."""
-
-    def __init__(self, torch):
-        self.torch = torch
-        self.pool: list = []
-        self.used: list[tuple[str, int]] = []
-
-    def mark(self, name: str) -> None:
-        """Record the event that opens (or closes) ``name``; components alternate open/close."""
-        i = len(self.used)
-        if i >= len(self.pool):
-            self.pool.append(self.torch.cuda.Event(enable_timing=True))
-        self.pool[i].record()
-        self.used.append((name, i))
-
-    def collect(self) -> dict:
-        self.torch.cuda.synchronize()
-        out: dict[str, float] = {}
-        for (name, a), (_, b) in zip(self.used[0::2], self.used[1::2]):
-            out[name] = out.get(name, 0.0) + self.pool[a].elapsed_time(self.pool[b]) * 1e-3
-        self.used.clear()
-        return out
-
-
-class GpuLoad(Load):
-    def __init__(self, a, device: int, ctx=None):
-        import torch
-
-        from kube_gpu_stats_amd.ops.load import LoadStep
-
-        self.torch = torch
-        self.ls = LoadStep(device=device, mfma_blocks=a.mfma_blocks, mfma_iters=a.mfma_iters,
-                           stream_bytes=int(a.stream_gib * (1 << 30)))
-        self.triads = a.triads
-        # Dispatch-bound component: back-to-back tiny kernels replayed from a HIP
-        # graph.  Long kernels hide command-processor contention; these expose it.
-        self.graph = None
-        self.tiny = int(a.tiny_kernels)
-        if self.tiny > 0:
-            from kube_gpu_stats_amd.ops import load as L
-
-            self.tsrc = torch.rand(16384, device=torch.device("cuda", device))
-            self.tdst = torch.empty_like(self.tsrc)
-            s = torch.cuda.Stream(device=device)
-            s.wait_stream(torch.cuda.current_stream(device))
-            with torch.cuda.stream(s):
-                L.copy_f32(self.tsrc, self.tdst, nblocks=64, stream=s)
-                s.synchronize()
-                self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph, stream=s):
-                    for _ in range(self.tiny):
-                        L.copy_f32(self.tsrc, self.tdst, nblocks=64, stream=s)
-            torch.cuda.current_stream(device).wait_stream(s)
-        # xGMI traffic for N > 1: one RCCL all-reduce per step over the
-        # point-to-point xGMI mesh, so the exporter's per-link counters move.
-        self.ar = None
-        if ctx is not None and ctx.is_dist and a.xgmi_mib > 0:
-            self.ar = torch.ones(int(a.xgmi_mib) << 18, dtype=torch.float32, device=torch.device("cuda", device))
-        self.ev = EventTimer(torch)
-
-    def unit(self):
-        t = self.timing
-        if t:
-            self.ev.mark("mfma")
-        self.ls.run_mfma()
-        if t:
-            self.ev.mark("mfma")
-            self.ev.mark("triad")
-        for _ in range(self.triads):
-            self.ls.run_stream()
-        if t:
-            self.ev.mark("triad")
-        if self.graph is not None:
-            if t:
-                self.ev.mark("tiny_graph")
-            self.graph.replay()
-            if t:
-                self.ev.mark("tiny_graph")
-        if self.ar is not None:
-            import torch.distributed as dist
-
-            if t:
-                self.ev.mark("allreduce")
-            dist.all_reduce(self.ar)
-            self.ar.mul_(0.5)  # keep values bounded across steps
-            if t:
-                self.ev.mark("allreduce")
-
-    def components_end(self) -> dict:
-        self.timing = False
-        return self.ev.collect()
-
-    def component_names(self) -> list[str]:
-        return ["mfma", "triad"] + (["tiny_graph"] if self.graph is not None else [])
-
-    def run_component(self, name: str) -> None:
-        """One launch of a single load component (phase K)."""
-        if name == "mfma":
-            self.ls.run_mfma()
-        elif name == "triad":
-            self.ls.run_stream()
-        elif name == "tiny_graph":
-            self.graph.replay()
-
-    def sync(self):
-        self.torch.cuda.synchronize()
-
-    def burst(self, ms: float) -> None:
-        """One MFMA kernel of ≈``ms`` milliseconds, waited for (phase R)."""
-        from kube_gpu_stats_amd.ops import load as L
-
-        iters = max(50, int(self.ls.mfma_iters * ms / max(self.mfma_ms, 1e-3)))
-        L.mfma_bf16(self.ls.A, self.ls.B, self.ls.C, self.ls.mfma_blocks, iters)
-        self.torch.cuda.synchronize()
-
-    def burst_timed(self, ms: float) -> float:
-        """burst(), returning the kernel's own GPU time (HIP events), seconds (phase U)."""
-        from kube_gpu_stats_amd.ops import load as L
-
-        torch = self.torch
-        if not hasattr(self, "_bev"):
-            self._bev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        e0, e1 = self._bev
-        iters = max(10, int(self.ls.mfma_iters * ms / max(self.mfma_ms, 1e-3)))
-        e0.record()
-        L.mfma_bf16(self.ls.A, self.ls.B, self.ls.C, self.ls.mfma_blocks, iters)
-        e1.record()
-        e1.synchronize()
-        return e0.elapsed_time(e1) * 1e-3
-
-    def triad_burst_timed(self, ms: float) -> float:
-        """One HBM triad of ≈``ms`` milliseconds (a slice of the stream buffers), waited for:
-        its own GPU time (HIP events), seconds (phase U: a memory-bound kernel, which runs
-        at the full shader clock where an MFMA burst is power-capped)."""
-        from kube_gpu_stats_amd.ops import load as L
-
-        torch = self.torch
-        if not hasattr(self, "_bev"):
-            self._bev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        e0, e1 = self._bev
-        a, b, c = self.ls.a, self.ls.b, self.ls.c
-        if not hasattr(self, "_triad_per_ms"):  # elements per ms, from a warm 1/8-buffer triad
-            n = a.numel() // 32 * 4
-            for _ in range(2):  # the first pass pays first-touch and TLB misses
-                e0.record()
-                L.triad_f32(a[:n], b[:n], c[:n], 1.5)
-                e1.record()
-                e1.synchronize()
-            self._triad_per_ms = n / max(e0.elapsed_time(e1), 1e-3)
-        n = min(a.numel(), max(1 << 20, int(self._triad_per_ms * ms))) // 4 * 4  # float4 accesses
-        e0.record()
-        L.triad_f32(a[:n], b[:n], c[:n], 1.5)
-        e1.record()
-        e1.synchronize()
-        return e0.elapsed_time(e1) * 1e-3
-
-    def saturate(self, secs: float) -> float:
-        """MFMA kernels back to back (two in flight) for ``secs``: Σ their GPU time (phase U)."""
-        torch = self.torch
-        ev = []
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < secs:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            self.ls.run_mfma()
-            e1.record()
-            ev.append((e0, e1))
-            if len(ev) >= 2:
-                ev[-2][1].synchronize()
-        torch.cuda.synchronize()
-        return sum(x.elapsed_time(y) for x, y in ev) * 1e-3
-
-    def calibrate(self) -> dict:
-        """Per-kernel throughput (events), outside every timed region."""
-        torch = self.torch
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        e[0].record()
-        self.ls.run_mfma()
-        e[1].record()
-        self.ls.run_stream()
-        e[2].record()
-        if self.graph is not None:
-            self.graph.replay()
-        e[3].record()
-        torch.cuda.synchronize()
-        mfma_s = e[0].elapsed_time(e[1]) * 1e-3
-        self.mfma_ms = mfma_s * 1e3
-        tri_s = e[1].elapsed_time(e[2]) * 1e-3
-        out = {"mfma_ms": mfma_s * 1e3, "mfma_tflops": self.ls.flops / mfma_s / 1e12,
-               "triad_ms": tri_s * 1e3, "triad_tbps": self.ls.bytes / tri_s / 1e12}
-        if self.graph is not None:
-            g_s = e[2].elapsed_time(e[3]) * 1e-3
-            out.update({"tiny_graph_ms": g_s * 1e3, "tiny_kernels_per_s": self.tiny / g_s})
-        return out
-
-    def pci_bdf(self, device: int) -> str:
-        p = self.torch.cuda.get_device_properties(device)
-        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
-
-
-class TrainLoad(GpuLoad):
-    """``--load train``: one PyTorch bf16 training step per bench step instead of the
-    synthetic kernels: a decoder stack (RMSNorm, causal SDPA, SwiGLU MLP) forward +
-    backward + AdamW, DDP over RCCL when N > 1.  Hundreds of library kernels
-    (hipBLASLt GEMMs, flash attention, elementwise) per step, which is the kind of
-    workload a DaemonSet exporter shares the GPU with.  Random-init weights and
-    synthetic tokens; the exporter is measured exactly as with the synthetic load."""
-
-    burst_timed = None  # no MFMA burst kernel of known length: phase U is skipped
-
-    def __init__(self, a, device: int, ctx=None):
-        import torch
-        import torch.nn as nn
-        import torch.nn.functional as F
-
-        self.torch = torch
-        dev = torch.device("cuda", device) if device >= 0 else torch.device("cpu")  # cpu: tests only
-        d, h, L, ff = a.train_dim, a.train_dim // 128, a.train_layers, int(a.train_dim * 8 / 3 / 256 + 0.5) * 256
-        self.batch, self.seq, self.vocab = a.train_batch, a.train_seq, a.train_vocab
-
-        class Block(nn.Module):
-            def __init__(self):
-                super().__init__()
-                self.n1 = nn.RMSNorm(d)
-                self.qkv = nn.Linear(d, 3 * d, bias=False)
-                self.o = nn.Linear(d, d, bias=False)
-                self.n2 = nn.RMSNorm(d)
-                self.up = nn.Linear(d, 2 * ff, bias=False)
-                self.down = nn.Linear(ff, d, bias=False)
-
-            def forward(self, x):
-                B, S, _ = x.shape
-                q, k, v = self.qkv(self.n1(x)).view(B, S, 3, h, d // h).permute(2, 0, 3, 1, 4)
-                y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-                x = x + self.o(y.transpose(1, 2).reshape(B, S, d))
-                g, u = self.up(self.n2(x)).chunk(2, dim=-1)
-                return x + self.down(F.silu(g) * u)
-
-        class Model(nn.Module):
-            def __init__(self, vocab):
-                super().__init__()
-                self.emb = nn.Embedding(vocab, d)
-                self.blocks = nn.ModuleList(Block() for _ in range(L))
-                self.norm = nn.RMSNorm(d)
-                self.head = nn.Linear(d, vocab, bias=False)
-
-            def forward(self, t):
-                x = self.emb(t)
-                for b in self.blocks:
-                    x = b(x)
-                return self.head(self.norm(x))
-
-        torch.manual_seed(1234)
-        model = Model(self.vocab).to(device=dev, dtype=torch.bfloat16)
-        self.params = sum(p.numel() for p in model.parameters())
-        if ctx is not None and ctx.is_dist:
-            from torch.nn.parallel import DistributedDataParallel
-
-            model = DistributedDataParallel(model, device_ids=[device], bucket_cap_mb=256)
-        self.model = model
-        self.opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=dev.type == "cuda")
-        g = torch.Generator(device=dev).manual_seed(1234 + (ctx.rank if ctx is not None else 0))
-        self.tok = torch.randint(0, self.vocab, (self.batch, self.seq + 1), device=dev, generator=g)
-        self.F = F
-
-        self.ev = EventTimer(torch) if dev.type == "cuda" else None
-
-    burst = None  # phase R runs on the synthetic load only
-
-    def component_names(self) -> list[str]:
-        return []  # one component (the whole step): phase K has nothing to split
-
-    def unit(self):
-        t = self.timing and self.ev is not None
-        if t:
-            self.ev.mark("train_step")
-        logits = self.model(self.tok[:, :-1])
-        loss = self.F.cross_entropy(logits.float().view(-1, self.vocab), self.tok[:, 1:].reshape(-1))
-        loss.backward()
-        self.opt.step()
-        self.opt.zero_grad(set_to_none=True)
-        if t:
-            self.ev.mark("train_step")
-
-    def components_end(self) -> dict:
-        self.timing = False
-        return self.ev.collect() if self.ev is not None else {}
-
-    def calibrate(self) -> dict:
-        torch = self.torch
-        self.unit()  # first step: allocator growth, kernel selection; not representative
-        torch.cuda.synchronize()
-        ts = []
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            self.unit()
-            e1.record()
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1e-3)
-        s = sorted(ts)[1]
-        toks = self.batch * self.seq
-        # 6·N·T for the dense weights + causal attention (fwd 2·S·d per token per layer, x3 with bwd)
-        return {"train_step_ms": s * 1e3, "train_tokens_per_s": toks / s, "train_params": self.params,
-                "train_tflops": 6.0 * self.params * toks / s / 1e12}
-
-
-class MockLoad(Load):
-    def __init__(self, a, device: int):
-        self.dt = a.mock_step_ms * 1e-3
-
-    def unit(self):
-        t0 = time.perf_counter()
-        time.sleep(self.dt)  # releases the GIL like a GPU sync would
-        if self.timing:
-            self.comp["mock"] = self.comp.get("mock", 0.0) + time.perf_counter() - t0
-
-    def components_start(self) -> None:
-        self.timing = True
-        self.comp: dict[str, float] = {}
-
-    def components_end(self) -> dict:
-        self.timing = False
-        return dict(self.comp)
-
-    def burst(self, ms: float) -> None:
-        time.sleep(ms * 1e-3)  # plumbing only: the mock counters do not follow the host
-
-    def burst_timed(self, ms: float) -> float:
-        self.burst(ms)
-        return ms * 1e-3
-
-    triad_burst_timed = burst_timed
-
-    def saturate(self, secs: float) -> float:
-        time.sleep(secs)
-        return secs
-
-    def sync(self):
-        pass
-
-    def calibrate(self) -> dict:
-        return {"mock_unit_ms": self.dt * 1e3}
-
-    def pci_bdf(self, device: int) -> str:
-        return f"0000:{0x11 + 0x10 * device:02x}:00.0"  # mock provider's BDF scheme
-
-
-# ----------------------------------------------------------------------------- exporter
-class ExporterCtl:
-    """Control calls shared by the spawned and the attached exporter (``self.sc``)."""
-
-    def pmc_enabled(self) -> dict:
-        m = parse_text(self.sc.get())
-        return {lb["gpu"]: v for lb, v in m.get("kgs_pmc_enabled", [])}
-
-    def _wait_pmc(self, on: bool, timeout: float = 10.0) -> bool:
-        end = time.time() + timeout
-        while time.time() < end:
-            st = self.pmc_enabled()
-            if st and all((v == 1) == on for v in st.values()):
-                return True
-            time.sleep(0.01)
-        return False
-
-    def release(self, drop_queue: bool = True) -> bool:
-        """Counter sessions STOPped on every GPU (and, with drop_queue, the reader's READ
-        queues destroyed): the "released" condition.  Needs running sampler threads —
-        each GPU's own counter thread acts — and waits until all have."""
-        self.sc.get("/control/pmc/release" + ("?drop_queue=1" if drop_queue else ""))
-        return self._wait_pmc(False)
-
-    def acquire(self) -> bool:
-        self.sc.get("/control/pmc/acquire")
-        return self._wait_pmc(True)
-
-
-class AttachedExporter(ExporterCtl):
-    """An already-running exporter (``--control-http``) driven over HTTP."""
-
-    def __init__(self, hostport: str):
-        host, _, port = hostport.rpartition(":")
-        self.port = int(port)
-        self.sc = Scraper(host or "127.0.0.1", self.port)
-        m = parse_text(self.sc.get())
-        info = m.get("kgs_build_info", [({}, 0)])[0][0]
-        self.ready = {"pmc": info.get("pmc_source", "none"), "pmc_error": "",
-                      "hz": float(info.get("sample_hz", "0") or 0)}
-
-    def pause(self):
-        self.sc.get("/control/pause")
-
-    def resume(self):
-        self.sc.get("/control/resume")
-
-    def set_rate(self, hz: float):
-        self.sc.get(f"/control/rate?hz={hz:g}")
-
-    def set_idle_hz(self, hz: float) -> float:
-        return json.loads(self.sc.get(f"/control/pmc/idle?hz={hz:g}")).get("pmc_idle_hz", 0.0)
-
-    def json(self, path: str):
-        return json.loads(self.sc.get(path))
-
-    def stop(self) -> dict:
-        self.pause()
-        m = parse_text(self.sc.get())
-        fam = lambda n: {lb["gpu"]: v for lb, v in m.get(n, [])}  # noqa: E731
-        reads, rs, pmc, prs = (fam("kgs_reads_total"), fam("kgs_read_seconds_total"),
-                               fam("kgs_pmc_samples_total"), fam("kgs_pmc_read_seconds_total"))
-        hist = fam("kgs_sample_read_seconds_sum")
-        return {"integrals": [{"gpu": g, "reads": reads[g], "read_seconds": hist.get(g, rs.get(g, 0.0)),
-                               "pmc_samples": pmc.get(g, 0), "pmc_read_seconds": prs.get(g, 0.0),
-                               "overruns": fam("kgs_sampler_overruns_total").get(g, 0)} for g in sorted(reads)]}
-
-
-class ExporterProc(ExporterCtl):
-    def __init__(self, a, bdfs: list[str], log_path: str):
-        # Production tiers: per-process list at 10 Hz, xGMI links + RAS at 1 Hz (node-wide
-        # slow thread), gauges over a 2 s window (phase B is ~10 s).
-        # --compat-unallocated: the reference-contract series (container_gpu_sm_util,
-        # container_gpu_busy_seconds_total) for every GPU, pod_name="" (phase U reads them).
-        cmd = [sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
-               "--hz", str(a.hz), "--proc-period", "0.1", "--link-period", "1.0", "--window", "2",
-               "--control-stdin", "--control-http", "--node-name", "bench-node", "--bdfs", ",".join(bdfs),
-               "--compat-unallocated"]
-        if a.mock:
-            cmd += ["--backend", "mock", "--mock-gpus", str(max(8, len(bdfs))), "--pmc", "mock",
-                    "--mock-xgmi-swap", str(a.mock_xgmi_swap)]
-            if a.mock_latency:
-                cmd += ["--mock-latency"]
-        else:
-            pmc = PMC_READER if a.pmc == "auto" else a.pmc
-            cmd += ["--pmc", pmc, "--pmc-pipeline" if a.pmc_pipeline else "--no-pmc-pipeline", "--pmc-set", a.pmc_set,
-                    "--pmc-lean", str(a.pmc_lean)]
-        cmd += ["--pmc-dispatch-hz", f"{a.pmc_dispatch_hz:g}"]
-        if not a.mock:
-            cmd += ["--pmc-batch", str(a.pmc_batch), "--pmc-publish-us", str(a.pmc_publish_us)]
-        env = dict(os.environ)
-        env.setdefault("KGS_NO_BUILD", "1")
-        env.setdefault("PYTHONFAULTHANDLER", "1")  # a native fault leaves a trace in the exporter log
-        self.log = open(log_path, "w")
-        self.p = subprocess.Popen(cmd, cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.log,
-                                  text=True, env=env)
-        self.ready = self._wait_ready(120.0)
-        self.port = int(self.ready["port"])
-        self.sc = Scraper("127.0.0.1", self.port)
-
-    def pause(self):
-        self.sc.get("/control/pause")
-
-    def resume(self):
-        self.sc.get("/control/resume")
-
-    def set_rate(self, hz: float):
-        self.sc.get(f"/control/rate?hz={hz:g}")
-
-    def set_idle_hz(self, hz: float) -> float:
-        return json.loads(self.sc.get(f"/control/pmc/idle?hz={hz:g}")).get("pmc_idle_hz", 0.0)
-
-    def json(self, path: str):
-        return json.loads(self.sc.get(path))
-
-    def _wait_ready(self, timeout: float) -> dict:
-        end = time.time() + timeout
-        while time.time() < end:
-            r, _, _ = select.select([self.p.stdout], [], [], 1.0)
-            if r:
-                line = self.p.stdout.readline()
-                if not line:
-                    break
-                try:
-                    msg = json.loads(line)
-                except ValueError:
-                    continue
-                if msg.get("event") == "ready":
-                    return msg
-                if msg.get("event") == "error":
-                    raise RuntimeError("exporter failed: " + msg.get("error", ""))
-            if self.p.poll() is not None:
-                break
-        raise RuntimeError(f"exporter did not become ready (rc={self.p.poll()}); see {self.log.name}")
-
-    def stop(self) -> dict:
-        try:
-            self.p.stdin.write("quit\n")
-            self.p.stdin.flush()
-        except OSError:
-            pass
-        try:
-            out, _ = self.p.communicate(timeout=30)
-        except subprocess.TimeoutExpired:
-            self.p.kill()
-            out, _ = self.p.communicate()
-        self.log.close()
-        for line in out.splitlines():
-            try:
-                msg = json.loads(line)
-                if msg.get("event") == "stopped":
-                    return msg
-            except ValueError:
-                pass
-        return {}
-
-
-def proc_cpu_seconds(pid: int) -> float:
-    """utime + stime of a process (all threads), seconds; 0 if unreadable."""
-    try:
-        with open(f"/proc/{pid}/stat") as f:
-            fields = f.read().rsplit(")", 1)[1].split()
-        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
-    except (OSError, IndexError, ValueError):
-        return 0.0
-
-
-def thread_cpu_seconds(pid: int) -> dict:
-    """Per-thread utime + stime, keyed ``<comm>/<tid>`` (finds spinning helper threads)."""
-    out = {}
-    tck = os.sysconf("SC_CLK_TCK")
-    try:
-        tids = os.listdir(f"/proc/{pid}/task")
-    except OSError:
-        return out
-    for tid in tids:
-        try:
-            with open(f"/proc/{pid}/task/{tid}/stat") as f:
-                raw = f.read()
-            comm = raw[raw.index("(") + 1:raw.rindex(")")]
-            fields = raw.rsplit(")", 1)[1].split()
-            out[f"{comm}/{tid}"] = (int(fields[11]) + int(fields[12])) / tck
-        except (OSError, ValueError, IndexError):
-            continue
-    return out
-
-
-def sample_counts(m: dict) -> tuple[dict, dict]:
-    pmfw = {lb["gpu"]: v for lb, v in m.get("kgs_samples_total", [])}
-    pmc = {lb["gpu"]: v for lb, v in m.get("kgs_pmc_samples_total", [])}
-    return pmfw, pmc
-
-
-def xgmi_rates(before: dict, after: dict, win: float) -> dict:
-    """xGMI bytes/s per GPU (all links, read + write) over the timed window, from the
-    exporter's PMFW per-link accumulators."""
-    def tot(m):
-        out: dict = {}
-        for fam in ("amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total"):
-            for lb, v in m.get(fam, []):
-                out[lb["gpu"]] = out.get(lb["gpu"], 0.0) + v
-        return out
-    b, a_ = tot(before), tot(after)
-    return {g: round((a_[g] - b.get(g, 0.0)) / win / 1e9, 3) for g in a_} if win > 0 else {}
-
-
-def allreduce_GBps(load, a, n: int, win: float):
-    """xGMI bytes/s per GPU that phase B's all-reduces imply (None without them)."""
-    if getattr(load, "ar", None) is None or n < 2 or win <= 0:
-        return None
-    size = load.ar.numel() * load.ar.element_size()
-    return round(2 * 2 * (n - 1) / n * size * a.steps * load.reps / win / 1e9, 3)
-
-
-def allreduce_ratio(measured: dict, expected) -> dict | None:
-    """Per GPU, the xGMI bytes its link counters saw during phase B ÷ the bytes its
-    all-reduces must have moved (None without all-reduces)."""
-    if not expected:
-        return None
-    return {g: round(v / expected, 4) for g, v in measured.items()}
-
-
-def observed(m: dict) -> dict:
-    """What the exporter saw of the load (window gauges of the last scrape), per GPU."""
-    out: dict = {}
-    for fam, key in (("amdgpu_gfx_busy_percent", "gfx_busy_pct"), ("amdgpu_umc_busy_percent", "umc_busy_pct"),
-                     ("amdgpu_mfma_util_percent", "mfma_util_pct"), ("amdgpu_vmem_busy_percent", "vmem_busy_pct"),
-                     ("amdgpu_power_watts", "power_w"), ("amdgpu_gpu_clock_effective_mhz", "clock_mhz")):
-        for lb, v in m.get(fam, []):
-            out.setdefault(lb["gpu"], {})[key] = round(v, 2)
-    for lb, v in m.get("amdgpu_mfma_util_xcc_percent", []):  # XCD order 0..7
-        out.setdefault(lb["gpu"], {}).setdefault("mfma_util_xcd_pct", []).append(round(v, 1))
-    return out
-
-
-def throttled(before: dict, after: dict, win: float) -> dict:
-    """Per GPU and throttler, % of the timed window the GPU ran held back
-    (amdgpu_throttle_seconds_total deltas; reason="ppt" is the package-power cap)."""
-    out: dict = {}
-    if win <= 0:
-        return out
-    b = {(lb["gpu"], lb["reason"]): v for lb, v in before.get("amdgpu_throttle_seconds_total", [])}
-    for lb, v in after.get("amdgpu_throttle_seconds_total", []):
-        d = v - b.get((lb["gpu"], lb["reason"]), v)
-        if d > 0:
-            out.setdefault(lb["gpu"], {})[lb["reason"]] = round(100.0 * d / win, 2)
-    return out
-
-
-def wake_lateness(before: dict, after: dict) -> dict:
-    """Per GPU, how late the counter thread woke against its tick deadlines during
-    phase B (kgs_sampler_wake_lateness_seconds deltas): the box's CPU contention,
-    which is what makes phase B fall short of the nominal rate on some boxes."""
-    out: dict = {}
-    fam = "kgs_sampler_wake_lateness_seconds"
-    b = {(lb["gpu"], lb["le"]): v for lb, v in before.get(fam + "_bucket", [])}
-    buckets: dict = {}
-    for lb, v in after.get(fam + "_bucket", []):
-        le = float("inf") if lb["le"] == "+Inf" else float(lb["le"])
-        buckets.setdefault(lb["gpu"], []).append((le, v - b.get((lb["gpu"], lb["le"]), 0.0)))
-    sums = {lb["gpu"]: v for lb, v in after.get(fam + "_sum", [])}
-    sums0 = {lb["gpu"]: v for lb, v in before.get(fam + "_sum", [])}
-    for g, bl in buckets.items():
-        bl.sort()
-        n = bl[-1][1] if bl else 0
-        if n <= 0:
-            continue
-        le = lambda t: max((c for x, c in bl if x <= t + 1e-12), default=0.0)  # noqa: E731  cumulative ≤ t
-        out[g] = {"ticks": int(n), "share_within_10us": round(le(10e-6) / n, 4),
-                  "share_within_100us": round(le(100e-6) / n, 4), "share_over_500us": round(1 - le(500e-6) / n, 5),
-                  "share_over_2500us": round(1 - le(2500e-6) / n, 5),
-                  "mean_us": round(1e6 * (sums.get(g, 0.0) - sums0.get(g, 0.0)) / n, 2)}
-    return out
-
-
-# ----------------------------------------------------------------------------- phases
-PHASES: dict[str, list[float]] = {}
-
-
-def timed(ctx, load, k: int, name: str = "") -> float:
-    """Barrier + sync on both sides; returns the MAX over ranks of the wall time.
-
-    The wall-clock (epoch) bounds of each named phase are kept in PHASES so a
-    rocprofv3 kernel trace of the run can be split into exporter-off / -on
-    phases (tools/rocprof_overhead.py)."""
-    D.barrier(ctx)
-    load.sync()
-    w0 = time.time()
-    t0 = time.perf_counter()
-    for _ in range(k):
-        load.step()
-    load.sync()
-    D.barrier(ctx)
-    dt = time.perf_counter() - t0
-    if name:
-        PHASES[name] = [w0, time.time()]
-    return D.all_reduce(ctx, [dt], "max")[0]
-
-
-def calibrate_reps(ctx, load, step_ms: float) -> tuple[int, float]:
-    """Units per step so one step lasts ≥ step_ms on the slowest rank."""
-    load.unit()
-    load.sync()
-    D.barrier(ctx)
-    t0 = time.perf_counter()
-    load.unit()
-    load.sync()
-    unit_s = D.all_reduce(ctx, [time.perf_counter() - t0], "max")[0]
-    return max(1, math.ceil(step_ms * 1e-3 / max(unit_s, 1e-6))), unit_s
-
-
-class Rates:
-    """Per-GPU sample counts over a set of windows, from /metrics counter deltas."""
-
-    def __init__(self):
-        self.pmc: dict[str, float] = {}
-        self.pmfw: dict[str, float] = {}
-        self.secs = 0.0
-
-    def add(self, before: dict, after: dict, secs: float) -> None:
-        bp, bc = sample_counts(before)
-        ap_, ac = sample_counts(after)
-        for g in ap_:
-            self.pmfw[g] = self.pmfw.get(g, 0.0) + ap_[g] - bp.get(g, 0.0)
-            self.pmc[g] = self.pmc.get(g, 0.0) + ac.get(g, 0.0) - bc.get(g, 0.0)
-        self.secs += secs
-
-    def per_gpu(self, pmc_on: bool) -> tuple[dict, str]:
-        """Per GPU: its counter stream if it delivered one, else its PMFW table rate,
-        so one device whose counter tier failed lowers the total by its own share only."""
-        if self.secs <= 0:
-            return {}, "none"
-        gpus = sorted(self.pmfw, key=int)
-        out, n_pmc = {}, 0
-        for g in gpus:
-            if pmc_on and self.pmc.get(g, 0) > 0:
-                out[g] = self.pmc[g] / self.secs
-                n_pmc += 1
-            else:
-                out[g] = self.pmfw[g] / self.secs
-        src = "pmc" if n_pmc == len(gpus) else ("pmfw" if n_pmc == 0 else f"pmc on {n_pmc}/{len(gpus)} GPUs")
-        return out, src
-
-
-class PmfwProbe:
-    """Rank-local PMFW table reads at interleaved-block edges (one ≈46 µs sysfs pread
-    each), independent of the exporter — which is paused in the "off" blocks: the
-    block's average socket power and package-power throttle residency, from the
-    table's own energy / PPT-residency accumulators and firmware clock.  Shows
-    whether a sampling rate changes the GPU's power state (profiles/r2/r2aq)."""
-
-    def __init__(self, bdf: str):
-        self.path = f"/sys/bus/pci/devices/{bdf}/gpu_metrics"
-        try:
-            from kube_gpu_stats_amd.native import load
-
-            self.N = load(rebuild=False)  # built by local rank 0 long before the rounds
-            self.read()
-        except Exception:  # noqa: BLE001 - mock runs, other table revisions: no probe
-            self.N = None
-
-    def read(self) -> dict | None:
-        if self.N is None:
-            return None
-        with open(self.path, "rb") as f:
-            return self.N.parse_gpu_metrics_v1_8(f.read())
-
-    @staticmethod
-    def delta(a: dict | None, b: dict | None) -> dict | None:
-        if not a or not b or b["fw_ts"] <= a["fw_ts"]:
-            return None
-        dt = (b["fw_ts"] - a["fw_ts"]) * 1e-8  # firmware clock: 10 ns
-        out = {"power_w": (b["energy_acc"] - a["energy_acc"]) / 65536.0 / dt}  # 2^-16 J units
-        dc = b["accumulation_counter"] - a["accumulation_counter"]
-        if dc > 0 and b["ppt_residency_acc"] >= a["ppt_residency_acc"]:
-            out["ppt_pct"] = 100.0 * (b["ppt_residency_acc"] - a["ppt_residency_acc"]) / dc
-        return out
-
-
-def scrape_at(sc) -> tuple[dict, float]:
-    """One /metrics scrape and the time it was rendered (the request is sent at ``t``;
-    the exporter renders within ~0.1 ms).  Count deltas between two scrapes cover
-    exactly the interval between their ``t``s — timing after the parse instead would
-    move the window by the parse time of the page (≈10 ms per GPU's worth of series)."""
-    t = time.perf_counter()
-    body = sc.get()
-    return parse_text(body), t
-
-
-def pct(xs: list[float], q: float) -> float | None:
-    if not xs:
-        return None
-    s = sorted(xs)
-    return s[min(len(s) - 1, int(q * len(s)))]
-
-
-def timed_block(ctx, load, k: int) -> tuple[float, float]:
-    """One interleaved block: (this rank's own time to finish its k steps, the time
-    until every rank has — the MAX-over-ranks wall time the headline uses)."""
-    D.barrier(ctx)
-    load.sync()
-    t0 = time.perf_counter()
-    for _ in range(k):
-        load.step()
-    load.sync()
-    own = time.perf_counter() - t0
-    D.barrier(ctx)
-    return own, time.perf_counter() - t0
-
-
-RELEASED = -1.0  # interleaved condition: counter session STOPped, READ queue destroyed, sampler paused
-
-
-def cond_label(c: float) -> str:
-    return "released" if c < 0 else f"{c:g}"
-
-
-def order_design(conds: list[float], rounds: int) -> list[tuple]:
-    """Every permutation of the conditions in turn (3 conditions: all 6 orders), so
-    each condition sits in each block position equally often and a block-position
-    effect cannot pose as a sampling cost."""
-    import itertools
-
-    perms = list(itertools.permutations(conds))
-    return [perms[r % len(perms)] for r in range(rounds)]
-
-
-def position_adjusted(rows: list[dict], conds: list[float], orders: list[tuple]) -> dict:
-    """Least squares on log(block seconds) = round + condition + position effects;
-    the condition effects are the position-adjusted overheads (exp(b) − 1, with a
-    95 % interval from the residual variance)."""
-    import numpy as np
-
-    R, C = len(rows), len(conds)
-    P = C
-    y, X = [], []
-    for r, (row, order) in enumerate(zip(rows, orders)):
-        for pos, c in enumerate(order):
-            x = np.zeros(R + (C - 1) + (P - 1))
-            x[r] = 1.0
-            ci = conds.index(c)
-            if ci > 0:
-                x[R + ci - 1] = 1.0
-            if pos > 0:
-                x[R + C - 1 + pos - 1] = 1.0
-            X.append(x)
-            y.append(math.log(row[c]))
-    X, y = np.array(X), np.array(y)
-    beta, *_ = np.linalg.lstsq(X, y, rcond=None)
-    resid = y - X @ beta
-    dof = len(y) - np.linalg.matrix_rank(X)
-    out: dict = {"model": "log t = round + condition + position", "dof": int(dof)}
-    if dof <= 0:
-        return out
-    s2 = float(resid @ resid) / dof
-    cov = s2 * np.linalg.pinv(X.T @ X)
-    for ci in range(1, C):
-        k = R + ci - 1
-        b, se = float(beta[k]), math.sqrt(max(0.0, float(cov[k, k])))
-        out[cond_label(conds[ci])] = {"overhead_pct": 100 * (math.exp(b) - 1),
-                                 "overhead_ci95_pct": 100 * math.exp(b) * t975(dof) * se}
-    out["position_effect_pct"] = {str(p): 100 * (math.exp(float(beta[R + C - 1 + p - 1])) - 1) for p in range(1, P)}
-    return out
-
-
-def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
-    """Rounds of blocks: exporter paused (0), released (--released: also the counter
-    session STOPped and the reader's READ queue destroyed, re-acquired after the
-    block) and sampling at each rate in ``hzs``, the block order cycling through every
-    permutation of the conditions (order_design).  Paused means the sampler threads
-    are stopped — no PMFW read, no counter READ, no scrape — while the process and its
-    counter session stay up, so the paired difference is the cost of sampling +
-    scraping; released vs paused is the cost of a programmed perfmon session and a
-    mapped READ queue alone, with CIs like every tier.
-
-    Per block and rank: its own GPU-work time, the all-rank (MAX) time, the GPU time
-    of each load component (HIP events: MFMA kernel, triads, tiny-kernel graph,
-    all-reduce) and the block's power from the rank's own PMFW table.  The headline
-    overhead is the paired MAX-time ratio; per rank and per component the same pairing
-    on that rank's / component's own times."""
-    if a.rounds <= 0:
-        return {}
-    conds = [0.0] + ([RELEASED] if a.released else []) + list(hzs)  # the same on every rank
-    orders = order_design(conds, a.rounds)
-    released_now = False
-    probe = None if a.mock else PmfwProbe(load.pci_bdf(ctx.local_rank))
-    rates = {h: Rates() for h in hzs}
-    lat: dict[float, list[float]] = {h: [] for h in hzs}
-    paused_reads = 0.0
-    local: list[dict] = []  # per round: {cond: {"own", "all", "comp", "power"}}
-    for order in orders:
-        blk: dict = {}
-        for c in order:
-            sc = None
-            before: dict = {}
-            w0 = 0.0
-            if exp is not None:
-                if released_now and c != RELEASED:  # leave "released": threads up, counters re-acquired
-                    exp.resume()
-                    exp.acquire()
-                    released_now = False
-                if c == 0:
-                    exp.pause()
-                elif c == RELEASED:
-                    exp.resume()
-                    if not released_now:
-                        exp.release(drop_queue=True)
-                        released_now = True
-                    exp.pause()
-                else:
-                    exp.set_rate(c)
-                    exp.resume()
-                if c > 0:
-                    sc = Scraper("127.0.0.1", exp.port).start(a.scrape_hz)
-                before, w0 = scrape_at(exp.sc)
-            p0 = probe.read() if probe is not None else None
-            load.components_start()
-            own, dt = timed_block(ctx, load, a.block_steps)
-            comp = load.components_end()
-            pw = PmfwProbe.delta(p0, probe.read() if probe is not None else None)
-            if exp is not None:
-                if sc is not None:
-                    sc.stop()
-                after, w1 = scrape_at(exp.sc)
-                win = w1 - w0
-                if c > 0:
-                    rates[c].add(before, after, win)
-                    lat[c].extend(sc.latencies_s)
-                elif c == 0:  # paused really means no reads
-                    rb = {lb["gpu"]: v for lb, v in before.get("kgs_reads_total", [])}
-                    paused_reads += sum(v - rb.get(g, 0.0) for g, v in
-                                        ((lb["gpu"], v) for lb, v in after.get("kgs_reads_total", [])))
-            blk[c] = {"own": own, "all": dt, "comp": comp, "power": pw}
-        local.append(blk)
-    if exp is not None:
-        exp.resume()
-        if released_now:
-            exp.acquire()
-        exp.set_rate(a.hz)
-    ranks = D.all_gather_object(ctx, local)  # [rank][round][cond]
-    rows = [{c: max(rk[r][c]["all"] for rk in ranks) for c in conds} for r in range(a.rounds)]
-    out: dict = {"rounds": a.rounds, "block_steps": a.block_steps,
-                 "order_design": {"kind": "all permutations in turn", "orders": [[cond_label(c) for c in o]
-                                                                                for o in dict.fromkeys(orders)],
-                                  "balanced": a.rounds % len(dict.fromkeys(orders)) == 0},
-                 "paused_reads": paused_reads, "tiers": {}}
-    for h in hzs:
-        diffs = [100.0 * (row[h] / row[0.0] - 1.0) for row in rows]
-        m, ci, sd = mean_ci95(diffs)
-        srt = sorted(diffs)
-        med = (srt[(len(srt) - 1) // 2] + srt[len(srt) // 2]) / 2 if srt else float("nan")
-        tier = {"overhead_pct": m, "overhead_ci95_pct": ci, "overhead_sd_pct": sd,
-                # robustness next to the mean: a few disturbed rounds (another tenant of the
-                # box, a clock event) move the mean and its CI, not the median
-                "overhead_median_pct": med,
-                "overhead_per_round_pct": [round(d, 4) for d in diffs],
-                "_rates": rates[h], "_lat": lat[h]}
-        # per component (rank 0's GPU, and the mean of every rank's own estimate)
-        names = sorted({n for rk in ranks for rd in rk for n in rd[h]["comp"]})
-        by_comp: dict = {}
-        for n in names:
-            per_rank = []
-            for rk in ranks:
-                d = [100.0 * (rd[h]["comp"][n] / rd[0.0]["comp"][n] - 1.0) for rd in rk
-                     if rd[0.0]["comp"].get(n, 0) > 0 and n in rd[h]["comp"]]
-                per_rank.append(mean_ci95(d))
-            m0, c0, _ = per_rank[0]
-            share = sum(rd[0.0]["comp"].get(n, 0.0) for rd in ranks[0]) / max(
-                1e-12, sum(rd[0.0]["own"] for rd in ranks[0]))
-            by_comp[n] = {"overhead_pct": m0, "overhead_ci95_pct": c0, "share_of_block_time": round(share, 4)}
-            if len(ranks) > 1:
-                by_comp[n]["per_rank_overhead_pct"] = [round(x[0], 4) for x in per_rank]
-        tier["overhead_by_component"] = by_comp
-        if RELEASED in conds:
-            # The same pairing against "released" (counter session STOPped, READ queue
-            # destroyed, threads stopped): paused keeps a programmed session and its
-            # queue, which shifts a dispatch-bound stream's power state (BENCH_r04:
-            # µs-kernel graph −1.23 % at 100 Hz vs paused), so this is the neutral base
-            # for the cost of sampling.
-            vs_rel: dict = {}
-            for n in names:
-                d = [100.0 * (rd[h]["comp"][n] / rd[RELEASED]["comp"][n] - 1.0) for rd in ranks[0]
-                     if rd[RELEASED]["comp"].get(n, 0) > 0 and n in rd[h]["comp"]]
-                m_r, c_r, _ = mean_ci95(d)
-                vs_rel[n] = {"overhead_pct": m_r, "overhead_ci95_pct": c_r}
-            tier["overhead_by_component_vs_released"] = vs_rel
-        # per rank: that rank's own work time, paired by round
-        per_rank = []
-        for k, rk in enumerate(ranks):
-            m_k, c_k, _ = mean_ci95([100.0 * (rd[h]["own"] / rd[0.0]["own"] - 1.0) for rd in rk])
-            per_rank.append({"rank": k, "overhead_pct": round(m_k, 4), "overhead_ci95_pct": round(c_k, 4)})
-        tier["overhead_by_rank"] = per_rank
-        out["tiers"][f"{h:g}"] = tier
-    if RELEASED in conds:
-        # Released vs paused: the cost of a STARTed perfmon session + a mapped READ
-        # queue with nothing sampling; each rate vs released: everything the
-        # counter tier costs, session and queue included.
-        rel: dict = {}
-        m, ci, _ = mean_ci95([100.0 * (row[0.0] / row[RELEASED] - 1.0) for row in rows])
-        rel["paused_vs_released_pct"], rel["paused_vs_released_ci95_pct"] = m, ci
-        for h in hzs:
-            m, ci, _ = mean_ci95([100.0 * (row[h] / row[RELEASED] - 1.0) for row in rows])
-            rel[f"{h:g}_vs_released_pct"], rel[f"{h:g}_vs_released_ci95_pct"] = m, ci
-        out["released"] = rel
-    out["block_seconds"] = [[cond_label(c), round(rows[r][c], 6)] for r, o in enumerate(orders) for c in o]
-    # Block-position means (every condition pooled, and per condition): with the
-    # permutation design each condition's mean covers every position equally.
-    pos_all: dict[int, list[float]] = {}
-    pos_c: dict[str, dict[int, list[float]]] = {}
-    for r, o in enumerate(orders):
-        for p, c in enumerate(o):
-            pos_all.setdefault(p, []).append(rows[r][c])
-            pos_c.setdefault(cond_label(c), {}).setdefault(p, []).append(rows[r][c])
-    out["position_means"] = {"all": {str(p): round(sum(v) / len(v), 6) for p, v in sorted(pos_all.items())},
-                             "by_condition": {c: {str(p): round(sum(v) / len(v), 6) for p, v in sorted(d.items())}
-                                              for c, d in pos_c.items()}}
-    try:
-        out["position_adjusted"] = position_adjusted(rows, conds, orders)
-    except Exception as e:  # noqa: BLE001 - report, never fail the bench on the side estimate
-        out["position_adjusted"] = {"error": repr(e)}
-    # Power state per condition of every rank's GPU (PMFW energy / PPT accumulators).
-    power_by_rank = []
-    for k, rk in enumerate(ranks):
-        power: dict = {}
-        for c in conds:
-            pw = [rd[c]["power"] for rd in rk if rd[c]["power"]]
-            if not pw:
-                continue
-            ws = [d["power_w"] for d in pw]
-            ps = [d["ppt_pct"] for d in pw if "ppt_pct" in d]
-            power[cond_label(c)] = {"blocks": len(ws), "power_w_mean": round(sum(ws) / len(ws), 2),
-                                    "ppt_pct_mean": round(sum(ps) / len(ps), 3) if ps else None}
-            paired = [(rd[c]["power"], rd[0.0]["power"]) for rd in rk if rd[c]["power"] and rd[0.0]["power"]]
-            if c != 0 and paired:
-                m, ci, _ = mean_ci95([x["power_w"] - y["power_w"] for x, y in paired])
-                power[cond_label(c)]["power_w_vs_paused"] = round(m, 2)
-                power[cond_label(c)]["power_w_vs_paused_ci95"] = round(ci, 2)
-        power_by_rank.append(power)
-    if any(power_by_rank):
-        out["power"] = {"by_condition": power_by_rank[0], "by_rank": power_by_rank,
-                        "note": "PMFW energy / PPT-residency accumulators read by each rank at its own GPU's block "
-                                "edges ('0' = exporter paused)"}
-    return out
-
-
-RING = 8190  # drains /counters returns at most (native kPmcRing 8192, less the write slot)
-
-
-def burst_train(ctx, load, exp, a) -> dict:
-    """Phase R — what the primary rate resolves ("the headline value is a
-    dial").  Every rank fires a train of ≈``--burst-ms`` MFMA kernels, one every
-    ``--burst-period-ms``, for ``--burst-s``; the node exporter keeps sampling at the
-    primary rate.  Rank 0 then reads each GPU's full-rate ``/counters`` stream and
-    counts busy segments (reports/dmon.py ``segments``): at 8 kHz every launched
-    burst is its own segment and the busy integral matches the host's duty cycle,
-    where the ≈50 Hz PMFW table only sees the average.  Untimed; not in any overhead."""
-    if a.burst_s <= 0 or getattr(load, "burst", None) is None:
-        return {}
-    idle_hz = exp.set_idle_hz(-1) if exp is not None else 0.0  # hz < 0 only reads the setting
-    if exp is not None:
-        exp.set_idle_hz(0)  # profiling mode: READ every tick
-    D.barrier(ctx)
-    period = a.burst_period_ms * 1e-3
-    # /counters keeps the last RING drains: the train must fit in them (8190 drains are
-    # 1.0 s at 8 kHz, 0.51 s at 16 kHz — r5i resolved 102 of 120 bursts of a 0.6 s train)
-    train_s = min(a.burst_s, 0.8 * RING / a.hz) if a.hz > 0 else a.burst_s
-    bursts: list[tuple[int, int]] = []
-    nxt = time.monotonic()
-    t_end = nxt + train_s
-    while time.monotonic() < t_end:
-        t0 = time.monotonic_ns()
-        load.burst(a.burst_ms)
-        bursts.append((t0, time.monotonic_ns()))
-        nxt += period
-        d = nxt - time.monotonic()
-        if d > 0:
-            time.sleep(d)
-    everyone = D.all_gather_object(ctx, (load.pci_bdf(ctx.local_rank), bursts))
-    if exp is None:
-        return {}
-    exp.set_idle_hz(idle_hz)
-    import urllib.request
-
-    from kube_gpu_stats_amd.reports.dmon import segments
-
-    base = f"http://127.0.0.1:{exp.port}"
-    gpu_of = {d["bdf"]: str(d["gpu"]) for d in json.load(urllib.request.urlopen(base + "/devices", timeout=10))}
-    per: dict[str, dict] = {}
-    for bdf, bs in everyone:
-        g = gpu_of.get(bdf)
-        if g is None or not bs:
-            continue
-        body = json.load(urllib.request.urlopen(f"{base}/counters?gpu={g}&n={RING}", timeout=10))
-        lo, hi = bs[0][0] - 2_000_000, bs[-1][1] + 2_000_000
-        win = [x for x in body.get("samples", []) if lo <= x["mono_ns"] <= hi]
-        segs, busy, span = segments(win)
-        med = lambda xs: sorted(xs)[len(xs) // 2] * 1e-6 if xs else None  # noqa: E731
-        per[g] = {"launched": len(bs), "segments": len(segs), "drains": len(win),
-                  "drains_per_s": round(len(win) / span, 1) if span else None,
-                  "covered_s": round(span, 4),
-                  "median_burst_ms_host": med([e - s for s, e in bs]),
-                  "median_segment_ms": med([e - s for s, e in segs]),
-                  "duty_host": round(sum(e - s for s, e in bs) * 1e-9 / span, 4) if span else None,
-                  "duty_counters": round(busy / span, 4) if span else None}
-    return {"burst_ms": a.burst_ms, "period_ms": a.burst_period_ms, "train_s": round(train_s, 3),
-            "mode": "profiling (--pmc-idle-hz 0: every tick READs)", "mock": bool(a.mock), "per_gpu": per}
-
-
-def quiet_gpu(ctx, load, exp, a) -> dict:
-    """Phase Q — what the exporter does to an idle GPU (untimed).  Every counter READ
-    is a command-processor packet that the PMFW GFX busy — the source of
-    container_gpu_sm_util — counts as ≈80 µs of work, so a GPU READ every tick at
-    8 kHz reads ~99 % busy while idle.  With the GPU idle on every rank, rank 0
-    reads from the exporter's own counters, per GPU: the READ rate, the PMFW GFX
-    busy (exact, from amdgpu_gfx_busy_seconds_total) and the SPI-busy share of
-    clocks, first in the default adaptive mode (a quiet GPU is READ at
-    --pmc-idle-hz) and then in profiling mode (every tick) for contrast."""
-    if a.quiet_s <= 0:
-        return {}
-    D.barrier(ctx)
-    load.sync()  # the barrier's own kernel is done: every GPU is idle from here
-    out: dict = {}
-    if exp is not None:
-        default_idle = exp.set_idle_hz(-1)  # hz < 0 only reads the setting
-        for mode, hz in (("adaptive", default_idle), ("profiling", 0.0)):
-            exp.set_idle_hz(hz)
-            time.sleep(0.2)
-            m0, t0 = scrape_at(exp.sc)
-            time.sleep(a.quiet_s)
-            m1, t1 = scrape_at(exp.sc)
-            dt = t1 - t0
-            fam = lambda m, n, **kw: {lb["gpu"]: v for lb, v in m.get(n, [])  # noqa: E731
-                                      if all(lb.get(k) == w for k, w in kw.items())}
-            r0, r1 = fam(m0, "kgs_pmc_samples_total"), fam(m1, "kgs_pmc_samples_total")
-            g0, g1 = fam(m0, "amdgpu_gfx_busy_seconds_total"), fam(m1, "amdgpu_gfx_busy_seconds_total")
-            c0, c1 = fam(m0, "amdgpu_pmc_total", counter="GRBM_COUNT"), fam(m1, "amdgpu_pmc_total", counter="GRBM_COUNT")
-            s0, s1 = (fam(m0, "amdgpu_pmc_total", counter="GRBM_SPI_BUSY"),
-                      fam(m1, "amdgpu_pmc_total", counter="GRBM_SPI_BUSY"))
-            out[mode] = {"pmc_idle_hz": hz, "per_gpu": {
-                g: {"reads_per_s": round((r1[g] - r0.get(g, 0)) / dt, 1),
-                    "pmfw_gfx_busy_pct": round(100 * (g1.get(g, 0) - g0.get(g, 0)) / dt, 3),
-                    "gpu_active_pct": (round(100 * (s1[g] - s0.get(g, 0)) / (c1[g] - c0.get(g, 0)), 3)
-                                       if g in s1 and g in c1 and c1[g] > c0.get(g, 0) else None)}
-                for g in sorted(r1, key=int)}}
-        exp.set_idle_hz(default_idle)
-    D.cpu_barrier(ctx)  # the other ranks wait here without a spinning RCCL kernel on their GPUs
-    return out
-
-
-def util_accuracy(ctx, load, exp, a) -> dict:
-    """Phase U (untimed) — does the reference-contract utilisation count the exporter's
-    own counter READs?  (VERDICT r3 #1.)  Every counter READ is a command-processor
-    packet the PMFW GFX busy counts as ≈80 µs of work, so at kHz tick rates a bursty
-    GPU used to read ≈100 % busy.  At the primary rate and each --util-hz rate, with
-    the exporter's default flags (adaptive idle rate, batched READs, --sm-util-source
-    auto), every rank runs the same load for --util-s — idle, a train of 1 ms MFMA
-    kernels every 5 ms, a train of 0.2 ms kernels every 1 ms, a train of 1 ms HBM triads
-    every 5 ms (memory-bound: full shader clock), MFMA kernels back to back — and rank 0 reads, per GPU, 100·rate(container_gpu_busy_seconds_total)
-    (exact over the window), the container_gpu_sm_util gauge and the raw PMFW GFX busy,
-    next to the duty the rank measured: its kernels' own GPU time (HIP events) over
-    the window (``duty_gpu_pct``, the truth "a kernel is running" means) and the
-    host-timed launch-to-sync time (``duty_host_pct``)."""
-    if a.util_s <= 0 or getattr(load, "burst_timed", None) is None:
-        return {}
-    rates = [a.hz] + [float(x) for x in str(a.util_hz).split(",") if x.strip() and float(x) != a.hz]
-    plan = [("idle", None), ("burst_1ms_every_5ms", (1.0, 5.0)), ("burst_0.2ms_every_1ms", (0.2, 1.0)),
-            ("triad_1ms_every_5ms", (1.0, 5.0, "triad")),
-            ("mfma_saturating", "sat")]
-    out: dict = {"secs_per_load": a.util_s, "per_rate": {}}
-    for hz in rates:
-        if exp is not None:
-            exp.set_rate(hz)
-        D.cpu_barrier(ctx)
-        time.sleep(0.3)
-        per_load: dict = {}
-        # At a low counter rate the busy integral is known at the drains and billed at
-        # the PMFW samples (both at the tick rate): a window of ≥ 60 periods and a tail
-        # of five, so the last burst's drain (pipelined: one tick late), its table and
-        # the carry a saturated load holds (≤ one interval's worth, billed ≤ dt per
-        # interval) land inside it — r5k: a tail of two read a saturated 10 Hz window
-        # 2.7 points low where the same load over a long window bills to 0.1 %
-        # (profiles/r5/r5k/lr_10_sat.json).  At any rate the billing runs on the PMFW
-        # thread (≤ 100 Hz, tables every ≈20 ms), so the integral a scrape sees lags the
-        # drains by up to a few tens of ms: 50 ms of tail at least, or a saturated 1.5 s
-        # window reads that lag as 0.5-0.9 points of missing busy.  The duty counts the
-        # tail as idle.
-        secs = max(a.util_s, 60.0 / hz)
-        tail = max(5.0 / hz, 0.05)
-        for name, spec in plan:
-            load.sync()
-            D.cpu_barrier(ctx)  # no RCCL kernel inside the window
-            m0, w0 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
-            t0 = time.perf_counter()
-            gpu_s = host_s = 0.0
-            if spec is None:
-                time.sleep(secs)
-            elif spec == "sat":
-                gpu_s = load.saturate(secs)
-                host_s = time.perf_counter() - t0
-            else:
-                ms, period = spec[0], spec[1]
-                burst = load.triad_burst_timed if spec[2:] == ("triad",) else load.burst_timed
-                nxt = time.monotonic()
-                end = nxt + secs
-                while time.monotonic() < end:
-                    h0 = time.perf_counter()
-                    gpu_s += burst(ms)
-                    host_s += time.perf_counter() - h0
-                    nxt += period * 1e-3
-                    d = nxt - time.monotonic()
-                    if d > 0:
-                        time.sleep(d)
-            time.sleep(tail)
-            own = (gpu_s, host_s, time.perf_counter() - t0)
-            D.cpu_barrier(ctx)
-            m1, w1 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
-            everyone = D.all_gather_object(ctx, (load.pci_bdf(ctx.local_rank), own))
-            if exp is None:
-                continue
-            win = w1 - w0
-            gpu_of = {d["bdf"]: str(d["gpu"]) for d in exp.json("/devices")}
-
-            def delta(fam, g):
-                b = {lb["gpu"]: v for lb, v in m0.get(fam, [])}
-                return sum(v for lb, v in m1.get(fam, []) if lb["gpu"] == g) - b.get(g, 0.0)
-
-            per_gpu: dict = {}
-            for bdf, (g_s, h_s, _) in everyone:
-                g = gpu_of.get(bdf)
-                if g is None or win <= 0:
-                    continue
-                sm = [v for lb, v in m1.get("container_gpu_sm_util", []) if lb["gpu"] == g]
-                per_gpu[g] = {"duty_gpu_pct": round(100 * g_s / win, 2), "duty_host_pct": round(100 * h_s / win, 2),
-                              "busy_counter_pct": round(100 * delta("container_gpu_busy_seconds_total", g) / win, 2),
-                              "sm_util_gauge": round(sm[0], 2) if sm else None,
-                              "pmfw_gfx_busy_pct": round(100 * delta("amdgpu_pmfw_gfx_busy_seconds_total", g) / win, 2),
-                              "reads_per_s": round(delta("kgs_pmc_samples_total", g) / win, 1)}
-                src = {lb["source"]: v for lb, v in m1.get("kgs_util_source_seconds_total", []) if lb["gpu"] == g}
-                src0 = {lb["source"]: v for lb, v in m0.get("kgs_util_source_seconds_total", []) if lb["gpu"] == g}
-                tot = sum(src.get(k, 0.0) - src0.get(k, 0.0) for k in src)
-                per_gpu[g]["from_counters_pct"] = (round(100 * (src.get("counters", 0.0) - src0.get("counters", 0.0))
-                                                         / tot, 1) if tot > 0 else None)
-                per_gpu[g]["error_pts"] = round(per_gpu[g]["busy_counter_pct"] - per_gpu[g]["duty_gpu_pct"], 2)
-                # the clocks the time split priced this window's idle cycles at (diagnostic)
-                clk = {lb.get("kind"): v for lb, v in m1.get("kgs_pmc_shader_clock_hz", []) if lb["gpu"] == g}
-                if clk:
-                    per_gpu[g]["clock_mhz"] = {k: round(v / 1e6, 1) for k, v in sorted(clk.items())}
-            per_load[name] = per_gpu
-        out["per_rate"][f"{hz:g}"] = per_load
-    if exp is not None:
-        exp.set_rate(a.hz)
-    # worst |exported − GPU duty| per load over GPUs and rates
-    worst: dict = {}
-    for per_load in out["per_rate"].values():
-        for name, per_gpu in per_load.items():
-            for r in per_gpu.values():
-                worst[name] = round(max(worst.get(name, 0.0), abs(r["error_pts"])), 2)
-    out["worst_error_pts"] = worst
-    return out
-
-
-def component_rates(ctx, load, exp, a) -> dict:
-    """Phase K (untimed) — samples/s the exporter delivers at the primary rate while
-    each load component runs alone for --component-s: the long MFMA kernel, the HBM
-    triads, the dispatch-bound tiny-kernel graph (the headline's blend, split)."""
-    if a.component_s <= 0:
-        return {}
-    names = getattr(load, "component_names", lambda: [])()
-    if not names:
-        return {}
-    out: dict = {}
-    for name in names:
-        D.barrier(ctx)
-        load.sync()
-        before, w0 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
-        t0 = time.perf_counter()
-        k = 0
-        while time.perf_counter() - t0 < a.component_s:
-            load.run_component(name)
-            k += 1
-            if k % 4 == 0:
-                load.sync()
-        load.sync()
-        D.barrier(ctx)
-        if exp is None:
-            continue
-        after, w1 = scrape_at(exp.sc)
-        r = Rates()
-        r.add(before, after, w1 - w0)
-        pg, src = r.per_gpu(exp.ready.get("pmc", "none") != "none")
-        out[name] = {"samples_per_sec_per_gpu": {g: round(v, 1) for g, v in pg.items()}, "sample_source": src,
-                     "launches": k, "seconds": round(w1 - w0, 3)}
-    return out
-
-
-def capacity(ctx, load, exp, a) -> dict:
-    """Phase S — how far the counter tier goes past the primary rate (untimed).  Under the
-    same load, one ``--block-steps`` block at each ``--capacity-hz`` rate: delivered
-    counter drains per GPU, the worst GPU's share of nominal, overruns per second and
-    host µs per drain.  ``max_rate_hz_98pct`` is the highest rate tried (the primary one
-    included) at which every GPU delivered ≥ 98 %: the headroom behind the headline
-    number, which is the configured tick rate delivered."""
-    rates = [float(x) for x in str(a.capacity_hz).split(",") if x.strip()]
-    if not rates:
-        return {}
-    out: dict = {"block_steps": a.block_steps, "mode": "profiling (--pmc-idle-hz 0: every tick READs)",
-                 "rates": {}}
-    best = None
-    # Profiling mode: a GPU idle at a block edge would otherwise be READ at the idle
-    # rate until its first busy READ, which is the adaptive rate at work, not capacity.
-    idle_hz = exp.set_idle_hz(-1) if exp is not None else 0.0
-    if exp is not None:
-        exp.set_idle_hz(0)
-    for hz in [a.hz] + [r for r in rates if r != a.hz]:
-        w0 = 0.0
-        before: dict = {}
-        if exp is not None:
-            exp.set_rate(hz)
-            time.sleep(0.05)
-            before, w0 = scrape_at(exp.sc)
-        dt = timed(ctx, load, a.block_steps)
-        if exp is None:
-            continue
-        after, w1 = scrape_at(exp.sc)
-        win = w1 - w0
-        r = Rates()
-        r.add(before, after, win)
-        pg, src = r.per_gpu(exp.ready.get("pmc", "none") != "none")
-
-        def delta(fam):
-            b = {lb["gpu"]: v for lb, v in before.get(fam, [])}
-            return {lb["gpu"]: v - b.get(lb["gpu"], 0.0) for lb, v in after.get(fam, [])}
-
-        ov, rs = delta("kgs_sampler_overruns_total"), delta("kgs_pmc_read_seconds_total")
-        worst = min(pg.values()) / hz if pg else 0.0
-        out["rates"][f"{hz:g}"] = {
-            "samples_per_sec_per_gpu": {g: round(v, 1) for g, v in pg.items()}, "sample_source": src,
-            "worst_gpu_pct_of_nominal": round(100 * worst, 2),
-            "overruns_per_s_per_gpu": round(sum(ov.values()) / max(1, len(ov)) / win, 1) if win > 0 else None,
-            "host_us_per_drain": round(1e6 * sum(rs.values()) / max(1.0, sum(r.pmc.values())), 2),
-            "block_s": round(dt, 4)}
-        if worst >= 0.98:
-            best = hz if best is None else max(best, hz)
-    if exp is not None:
-        exp.set_rate(a.hz)
-        exp.set_idle_hz(idle_hz)
-    out["max_rate_hz_98pct"] = best
-    return out
-
-
-def _pair_rounds(n: int) -> list[list[tuple[int, int]]]:
-    """Every ordered pair (i, j), i != j, of n GPUs in rounds of disjoint pairs: the
-    circle method's n-1 rounds of n/2 pairs (n odd: a bye), each round once per
-    direction — 2(n-1) rounds, every GPU in at most one copy per round, so the only
-    link of each GPU that moves in a round is the one to its partner."""
-    m = n + (n % 2)
-    ring = list(range(m))
-    rounds = []
-    for _ in range(m - 1):
-        pairs = [(ring[k], ring[m - 1 - k]) for k in range(m // 2)]
-        rounds.append([(i, j) for i, j in pairs if i < n and j < n])
-        ring = [ring[0]] + [ring[-1]] + ring[1:-1]
-    return rounds + [[(j, i) for i, j in r] for r in rounds]
-
-
-def _xgmi_rank0(a, exp, bdfs: list) -> dict:
-    """Phase X on local rank 0 (see xgmi_link_check)."""
-    nbytes = int(a.xgmi_check_mib) << 20
-    gpu_of = {d["bdf"]: int(d["gpu"]) for d in exp.json("/devices")}
-    topo = exp.json("/topology")
-    peer_of = {(int(x["gpu"]), int(x["link"])): x.get("peer_bdf", "") for x in topo.get("links", [])}
-    budget_s = float(getattr(a, "xgmi_check_budget_s", 120.0) or 120.0)
-
-    def link_bytes(m: dict) -> dict:
-        tot: dict = {}
-        for fam in ("amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total"):
-            for lb, v in m.get(fam, []):
-                key = (int(lb["gpu"]), int(lb["link"]))
-                tot[key] = tot.get(key, 0.0) + v
-        return tot
-
-    def moved(before: dict, after: dict, gpu: int, want_bdf: str) -> dict:
-        d = {l: after[(g, l)] - before.get((g, l), 0.0) for (g, l) in after if g == gpu}
-        if not d:
-            return {"ok": False, "reason": "no xGMI byte counters for this GPU"}
-        l_max = max(d, key=d.get)
-        rest = sorted(v for l, v in d.items() if l != l_max)
-        bg = rest[len(rest) // 2] if rest else 0.0
-        peer = peer_of.get((gpu, l_max), "")
-        return {"link": l_max, "link_peer_bdf": peer, "ok": peer == want_bdf and d[l_max] - bg > 0,
-                "bytes_counted": round(d[l_max], 1), "background_bytes": round(bg, 1),
-                "unit_ratio": round((d[l_max] - bg) / nbytes, 4)}
-
-    def copy_round(pairs: list[tuple[int, int]]) -> dict:
-        """The round's copies at once, each on its source GPU (in-tree copy_f32 peer
-        kernel: the source's waves store into the peer's HBM over their direct link)."""
-        if a.mock:
-            for i, j in pairs:
-                exp.json(f"/control/mock/xgmi?src={gpu_of[bdfs[i]]}&dst={gpu_of[bdfs[j]]}&bytes={nbytes}")
-            return {}
-        import torch
-
-        from kube_gpu_stats_amd.ops import load as L
-
-        bufs = []
-        for i, j in pairs:
-            src = torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", i)).fill_(1.0)
-            dst = torch.zeros(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", j))
-            L.enable_peer(i, j)
-            bufs.append((i, j, src, dst))
-        for d in {x for p in pairs for x in p}:
-            torch.cuda.synchronize(d)
-        for i, j, src, dst in bufs:
-            with torch.cuda.device(i):
-                L.copy_f32(src, dst, stream=torch.cuda.current_stream(i))
-        for i, _, _, _ in bufs:
-            torch.cuda.synchronize(i)
-        ok = {(i, j): bool((dst == 1.0).all().item()) for i, j, _, dst in bufs}  # every element arrived
-        del bufs
-        return ok
-
-    t_start = time.monotonic()
-    per_copy, skipped = [], 0
-    for pairs in _pair_rounds(len(bdfs)):
-        pairs = [(i, j) for i, j in pairs if bdfs[i] in gpu_of and bdfs[j] in gpu_of]
-        if not pairs:
-            continue
-        if time.monotonic() - t_start > budget_s:  # --xgmi-check-budget-s: report what was covered
-            skipped += len(pairs)
-            continue
-        m0 = parse_text(exp.sc.get())
-        copied = copy_round(pairs)
-        time.sleep(a.xgmi_check_settle)  # the PMFW table refreshes every ≈20 ms; the exporter reads it at 100 Hz
-        b0, b1 = link_bytes(m0), parse_text(exp.sc.get())
-        b1 = link_bytes(b1)
-        for i, j in pairs:
-            gi, gj = gpu_of[bdfs[i]], gpu_of[bdfs[j]]
-            row = {"src_gpu": gi, "peer_gpu": gj, "peer_bdf": bdfs[j], "bytes": nbytes,
-                   "src": moved(b0, b1, gi, bdfs[j]), "dst": moved(b0, b1, gj, bdfs[i]),
-                   "copy_ok": copied.get((i, j))}
-            row["ok"] = bool(row["src"].get("ok") and row["dst"].get("ok") and row["copy_ok"] is not False)
-            per_copy.append(row)
-    missing = [b for b in bdfs if b not in gpu_of]
-    ratios = sorted(r[side]["unit_ratio"] for r in per_copy for side in ("src", "dst")
-                    if isinstance(r.get(side), dict) and "unit_ratio" in r[side])
-    ratio = ratios[len(ratios) // 2] if ratios else None
-    n_ok = sum(1 for r in per_copy if r["ok"])
-    total = len(bdfs) * (len(bdfs) - 1)
-    bad = [f"gpu{r['src_gpu']}->gpu{r['peer_gpu']}: " + "; ".join(
-        f"{side} gpu{r[side + '_gpu' if side == 'src' else 'peer_gpu']} link {r[side].get('link')} faces "
-        f"{r[side].get('link_peer_bdf') or '?'}" for side in ("src", "dst") if not r[side].get("ok"))
-        for r in per_copy if not r["ok"]]
-    out = {"bytes_per_copy": nbytes, "copies": "every ordered GPU pair, disjoint pairs in parallel rounds",
-           "per_copy": per_copy, "xgmi_links_ok": [n_ok, total], "bad_links": bad[:16],
-           "xgmi_link_map_ok": n_ok == total and total > 0,
-           "xgmi_unit_ratio": ratio,
-           "xgmi_unit_ratio_min_max": [ratios[0], ratios[-1]] if ratios else None,
-           "xgmi_unit_ok": bool(ratios) and 0.8 <= ratios[0] and ratios[-1] <= 1.25,
-           "seconds": round(time.monotonic() - t_start, 2)}
-    if skipped:
-        out["skipped_over_budget"] = skipped
-    if missing:
-        out["not_sampled"] = missing
-    if ratio is not None and not 0.8 <= ratio <= 1.25:
-        out["warning"] = (f"xGMI accumulator unit off by {ratio:.3g}x: set --xgmi-bytes-per-unit to "
-                          f"{1024.0 * ratio:.4g}")
-    return out
-
-
-def xgmi_link_check(ctx, load, exp, a) -> dict:
-    """Phase X (untimed, N > 1) — does each xGMI byte land on the link whose peer is
-    the real peer, and in which unit?  Rank 0 sees every GPU of
-    the node: every GPU copies ``--xgmi-check-mib`` to every peer (all N(N-1) ordered
-    pairs — 56 on 8 GPUs, each GPU's link to each peer checked as a writer and as a
-    reader), in rounds of disjoint pairs run at once, with exporter scrapes around each
-    round.  On the source and on the destination, the link whose byte counter moved
-    most (read + write, minus the median of the other links as background) must be
-    the one whose amdsmi peer_bdf is the other GPU; its bytes ÷ the copied bytes is the
-    accumulator-unit ratio (1.0 if --xgmi-bytes-per-unit is right), reported per link
-    and as min / median / max.  ``xgmi_links_ok`` = [copies whose both ends are right,
-    copies]; ``bad_links`` names the wrong ones.  The mock backend books each copy on
-    the true link itself (/control/mock/xgmi); --mock-xgmi-swap G gives it a wrong map."""
-    if ctx.world < 2:
-        return {"skipped": "N=1: no peer GPU to copy to"}
-    if a.xgmi_check_mib <= 0:
-        return {"skipped": "--xgmi-check-mib 0"}
-    D.cpu_barrier(ctx)
-    out: dict = {}
-    # every rank's GPU, in local-rank order (a collective: every rank calls it)
-    bdfs = [b for _, b in sorted(set(D.all_gather_object(ctx, (ctx.local_rank, load.pci_bdf(ctx.local_rank)))))]
-    if ctx.local_rank == 0 and exp is not None:
-        # In a child process: its HIP contexts on every peer GPU end with it, so no
-        # rank's later timed phase (C) shares its GPU with a foreign context of rank 0
-        # (VERDICT r3 weak #9).
-        cmd = [sys.executable, os.path.abspath(__file__), "--xgmi-child", str(exp.port), "--xgmi-bdfs", ",".join(bdfs),
-               "--xgmi-check-mib", str(a.xgmi_check_mib), "--xgmi-check-settle", str(a.xgmi_check_settle),
-               "--xgmi-check-budget-s", str(getattr(a, "xgmi_check_budget_s", 120.0))]
-        if a.mock:
-            cmd.append("--mock")
-        try:
-            r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=getattr(a, "xgmi_check_budget_s", 120.0) + 180)
-            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-            out = json.loads(lines[-1]) if r.returncode == 0 and lines else {
-                "error": f"phase X child rc={r.returncode}: {r.stderr[-400:]}", "xgmi_link_map_ok": False,
-                "xgmi_unit_ratio": None}
-        except Exception as e:  # noqa: BLE001  a failed self-check must not take the run (and the other ranks) down
-            out = {"error": f"{type(e).__name__}: {e}", "xgmi_link_map_ok": False, "xgmi_unit_ratio": None}
-    D.cpu_barrier(ctx)
-    return out
-
-
-def xgmi_child(a) -> int:
-    """``--xgmi-child PORT``: phase X's peer copies in a process of their own (rank 0
-    starts it; it never joins the rank group)."""
-    try:
-        exp = AttachedExporter(f"127.0.0.1:{a.xgmi_child}")
-        out = _xgmi_rank0(a, exp, [b for b in a.xgmi_bdfs.split(",") if b])
-    except Exception as e:  # noqa: BLE001
-        out = {"error": f"{type(e).__name__}: {e}", "xgmi_link_map_ok": False, "xgmi_unit_ratio": None}
-    print(json.dumps(out), flush=True)
-    return 0
-
-
-def run(a, ctx) -> dict | None:
-    n = ctx.world
-    hzs = tiers(a)
-    a.hz = hzs[-1]  # the fastest tier is the primary (phase B)
-    if ctx.local_rank == 0 and not a.attach:
-        # The exporter child runs with KGS_NO_BUILD=1: make sure its artefacts exist
-        # (incremental no-op when the in-tree .so files are current).
-        from kube_gpu_stats_amd.native import build as B
-
-        B.build_native()
-        if not a.mock:
-            B.build_pmc_aql()
-    if a.mock:
-        load = MockLoad(a, ctx.local_rank)
-    elif a.load == "train":
-        load = TrainLoad(a, ctx.local_rank, ctx)
-    else:
-        load = GpuLoad(a, ctx.local_rank, ctx)
-
-    calib = load.calibrate()
-    load.reps, unit_s = calibrate_reps(ctx, load, a.step_ms)
-    for _ in range(a.warmup):
-        load.step()
-    load.sync()
-
-    # phase A: no exporter (an attached exporter is paused: process up, no reads)
-    attached = None
-    if a.attach and ctx.local_rank == 0:
-        attached = AttachedExporter(a.attach)
-        attached.pause()
-    t_a = timed(ctx, load, a.steps, "A_off")
-
-    # start the node exporter over every local rank's GPU
-    bdfs = D.all_gather_object(ctx, (ctx.local_rank, load.pci_bdf(ctx.local_rank)))
-    bdfs = [b for _, b in sorted(set(bdfs))]
-    exp = None
-    err = ""
-    if ctx.local_rank == 0:
-        logdir = os.path.dirname(os.path.abspath(a.out)) if a.out else os.path.join(REPO, "gpurun_out")
-        os.makedirs(logdir, exist_ok=True)
-        try:
-            if attached is not None:
-                attached.set_rate(a.hz)
-                attached.resume()
-                exp = attached
-            else:
-                exp = ExporterProc(a, bdfs, os.path.join(logdir, f"bench_exporter_r{ctx.rank}.log"))
-        except Exception as e:  # noqa: BLE001
-            err = str(e)
-    err = D.broadcast_object(ctx, err)
-    if err:
-        return {"metric": METRIC, "value": None, "error": err}
-    time.sleep(a.settle)
-
-    # phase B: exporter on at the primary rate, scraped (THE timed region)
-    sc_b = None
-    before = after = {}
-    win = 0.0
-    exp_pid = int(exp.ready.get("pid", 0) or 0) if exp is not None else 0
-    cpu0 = cpu1 = 0.0
-    cpu_win = 0.0
-    thr0: dict = {}
-    thr1: dict = {}
-    if exp is not None:
-        sc_b = Scraper("127.0.0.1", exp.port)
-        cpu0, thr0, c_t0 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid), time.perf_counter()
-        before, w0 = scrape_at(sc_b)  # counts as of the render, timed at the request
-        sc_b.start(a.scrape_hz)
-    t_b = timed(ctx, load, a.steps, "B_on")
-    if exp is not None:
-        sc_b.stop()
-        after, w1 = scrape_at(sc_b)
-        win = w1 - w0
-        cpu1, thr1 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
-        cpu_win = time.perf_counter() - c_t0
-
-    resolution = burst_train(ctx, load, exp, a)
-    quiet = quiet_gpu(ctx, load, exp, a)
-    util = util_accuracy(ctx, load, exp, a)
-    inter = interleaved(ctx, load, exp, a, hzs)
-    cap = capacity(ctx, load, exp, a)
-    comp_rates = component_rates(ctx, load, exp, a)
-    xlink = xgmi_link_check(ctx, load, exp, a)
-    stopped = exp.stop() if exp is not None else {}
-
-    # phase C: exporter off again
-    t_c = timed(ctx, load, a.steps, "C_off")
-    if exp is None:
-        return None
-
-    pmc_on = exp.ready.get("pmc", "none") != "none"
-    rb = Rates()
-    rb.add(before, after, win)
-    per_gpu, source = rb.per_gpu(pmc_on)
-    total = sum(per_gpu.values())
-    lat_primary = list(sc_b.latencies_s)
-    tier_out = {}
-    for h, t in inter.get("tiers", {}).items():
-        r: Rates = t.pop("_rates")
-        lat: list = t.pop("_lat")
-        pg, src = r.per_gpu(pmc_on)
-        if float(h) == a.hz:
-            lat_primary += lat
-        tier_out[h] = {"samples_per_sec_per_gpu": {g: round(v, 2) for g, v in pg.items()},
-                       "aggregate_samples_per_sec": round(sum(pg.values()), 2), "sample_source": src,
-                       "p50_scrape_ms": (pct(lat, 0.5) or 0) * 1e3, "p99_scrape_ms": (pct(lat, 0.99) or 0) * 1e3,
-                       "scrapes": len(lat), **{k: v for k, v in t.items()}}
-    inter["tiers"] = tier_out
-    prim = tier_out.get(f"{a.hz:g}", {})
-    step_s = t_b / a.steps
-    integrals = stopped.get("integrals") or []
-    return {
-        "metric": METRIC,
-        "value": total,
-        "unit": f"samples/s (sum over the {n} GPU{'s' if n > 1 else ''})",
-        "n_gpus": n,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": step_s * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16",
-        "data": ("synthetic mock provider (CPU plumbing)" if a.mock
-                 else f"synthetic tokens, random-init {a.train_layers}-layer d={a.train_dim} bf16 decoder "
-                 "training step (fwd + bwd + AdamW) as the GPU load" if a.load == "train"
-                 else "synthetic (gfx950 MFMA bf16 + HBM triad + HIP-graph tiny-kernel load; random-init operands)"),
-        "config": {"model": "node exporter: PMFW table + HBM + per-PID + xGMI + hardware counters "
-                            f"({exp.ready.get('pmc')}), {a.hz:g} Hz/GPU, /metrics scraped at {a.scrape_hz:g} Hz",
-                   "global_batch": n, "seq_len": int(round(a.hz * step_s)), "parallelism": f"dp{n}",
-                   "batch_meaning": "GPUs sampled per tick (one counter drain each)",
-                   "seq_len_meaning": "sampler ticks per GPU per timed step",
-                   "hz": a.hz, "hz_tiers": hzs, "sample_source": source,
-                   "pmc_dispatch_hz": a.pmc_dispatch_hz,
-                   "pmc_batch": a.pmc_batch, "pmc_publish_us": a.pmc_publish_us,
-                   "exporter": "attached" if a.attach else "spawned", "load": "mock" if a.mock else a.load,
-                   "units_per_step": load.reps, "unit_ms": unit_s * 1e3},
-        "value_semantics": "aggregate over all GPUs (driver contract); per-GPU in samples_per_sec_per_gpu",
-        "samples_per_sec_per_gpu": total / max(1, len(per_gpu)),
-        "aggregate_samples_per_sec": total,
-        "pmc_samples_per_sec_per_gpu": {g: round((rb.pmc.get(g, 0) / win) if win > 0 else 0, 2) for g in per_gpu},
-        "pmfw_distinct_samples_per_sec_per_gpu": {g: round((rb.pmfw.get(g, 0) / win) if win > 0 else 0, 2)
-                                                  for g in per_gpu},
-        "p50_scrape_ms": (pct(lat_primary, 0.5) or 0) * 1e3,
-        "p99_scrape_ms": (pct(lat_primary, 0.99) or 0) * 1e3,
-        "scrapes": len(lat_primary),
-        "scrape_errors": sc_b.errors,
-        "scrape_bytes_avg": sc_b.bytes / max(1, len(sc_b.latencies_s)),
-        # headline overhead: paired interleaved rounds at the primary rate (mean ± 95 % CI)
-        "overhead_pct": prim.get("overhead_pct"),
-        "overhead_ci95_pct": prim.get("overhead_ci95_pct"),
-        "overhead_abc_pct": 100.0 * (t_b / (0.5 * (t_a + t_c)) - 1.0),
-        "t_off_a_s": t_a,
-        "t_on_s": t_b,
-        "t_off_c_s": t_c,
-        "interleaved": inter,
-        "burst_resolution": resolution,
-        "quiet_gpu": quiet,
-        "util_accuracy": util,
-        "capacity": cap,
-        "delivered_by_component": comp_rates,
-        "exporter_cpu_cores": round((cpu1 - cpu0) / cpu_win, 4) if cpu_win > 0 and exp_pid else None,
-        "exporter_cpu_cores_by_thread": {k: round((v - thr0.get(k, 0.0)) / cpu_win, 4) for k, v in thr1.items()
-                                         if cpu_win > 0 and v - thr0.get(k, 0.0) > 0.005 * cpu_win},
-        "pmc_source": exp.ready.get("pmc"),
-        "pmc_error": exp.ready.get("pmc_error"),
-        "load": calib,
-        "observed_during_load": observed(after),
-        "sampler_wake_lateness": wake_lateness(before, after),
-        "throttled_pct_during_load": throttled(before, after, win),
-        "xgmi_GBps_per_gpu": xgmi_rates(before, after, win),
-        # what the phase-B all-reduces must have moved per GPU (read + write, bandwidth-optimal
-        # 2(N-1)/N each way): the measured / expected ratio pins the PMFW xGMI accumulator unit
-        "xgmi_allreduce_GBps_per_gpu_expected": allreduce_GBps(load, a, n, win),
-        # measured ÷ expected per GPU: 1.0 if the link counters' unit is right and the
-        # all-reduces ran on xGMI (phase X pins the unit link by link)
-        "xgmi_allreduce_ratio_per_gpu": allreduce_ratio(xgmi_rates(before, after, win), allreduce_GBps(load, a, n, win)),
-        "xgmi_link_check": xlink,
-        "xgmi_link_map_ok": xlink.get("xgmi_link_map_ok"),
-        "xgmi_links_ok": xlink.get("xgmi_links_ok"),
-        "xgmi_unit_ratio": xlink.get("xgmi_unit_ratio"),
-        "xgmi_unit_ratio_min_max": xlink.get("xgmi_unit_ratio_min_max"),
-        "phases_wall": PHASES,
-        "pmc_read_us_mean": 1e6 * sum(i.get("pmc_read_seconds", 0) for i in integrals)
-        / max(1, sum(i.get("pmc_samples", 0) for i in integrals)),
-        "pmfw_read_us_mean": 1e6 * sum(i.get("read_seconds", 0) for i in integrals)
-        / max(1, sum(i.get("reads", 0) for i in integrals)),
-        "exporter_integrals": integrals,
-        "pmc_reader_info": stopped.get("pmc_info") if isinstance(stopped, dict) else None,
-    }
-
-
-# ----------------------------------------------------------------------------- result line
-SUMMARY_MAX = 1800  # bytes of the summary object: the driver keeps the last ≈2.3 KB of stdout (BENCH_r04)
-CONTRACT_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-                 "vs_baseline", "dtype", "data")
-
-
-def _r(x, nd=3):
-    return None if x is None else round(float(x), nd)
-
-
-def _pm(d: dict | None, k="overhead_pct", c="overhead_ci95_pct") -> list | None:
-    return [_r(d.get(k)), _r(d.get(c))] if isinstance(d, dict) and d.get(k) is not None else None
-
-
-def summarize(res: dict) -> dict:
-    """The headline numbers in ≤ 1.5 KB: what a reader of the last few
-    KB of stdout needs — value, scrape latency, overhead ± CI per tier (paired and
-    position-adjusted), per load component and per rank, released vs paused, what the
-    exporter delivered per component, phase U's utilisation accuracy and phase X's
-    xGMI verdict."""
-    inter = res.get("interleaved") or {}
-    tiers = inter.get("tiers") or {}
-    prim = f"{res.get('config', {}).get('hz', 0):g}"
-    pa = inter.get("position_adjusted") or {}
-    out: dict = {"value": _r(res.get("value"), 1), "samples_per_sec_per_gpu": _r(res.get("samples_per_sec_per_gpu"), 1),
-                 "p50_scrape_ms": _r(res.get("p50_scrape_ms")), "p99_scrape_ms": _r(res.get("p99_scrape_ms")),
-                 "scrapes": res.get("scrapes"), "overhead_pct": _pm(res)}
-    out["overhead_by_tier"] = {h: _pm(t) for h, t in tiers.items()}
-    out["overhead_median_by_tier"] = {h: _r(t.get("overhead_median_pct")) for h, t in tiers.items()}
-    out["overhead_position_adjusted"] = {h: _pm(v) for h, v in pa.items() if isinstance(v, dict) and "overhead_pct" in v}
-    # per tier and component: [vs paused, ± 95 %, vs released, ± 95 %] (the last two when
-    # the run had the released condition)
-    def comp(t: dict) -> dict:
-        rel = t.get("overhead_by_component_vs_released") or {}
-        return {c: (_pm(v) or [None, None]) + (_pm(rel.get(c)) or []) for c, v in
-                (t.get("overhead_by_component") or {}).items()}
-
-    out["overhead_by_component"] = {h: comp(t) for h, t in tiers.items()}
-    out["overhead_by_rank"] = [_r(x.get("overhead_pct")) for x in (tiers.get(prim, {}).get("overhead_by_rank") or [])]
-    rel = inter.get("released")
-    if rel:
-        pw = ((inter.get("power") or {}).get("by_condition") or {}).get("released", {})
-        out["released"] = {"paused_vs_released": _pm(rel, "paused_vs_released_pct", "paused_vs_released_ci95_pct"),
-                           **{k[:-len("_vs_released_pct")] + "_vs_released":
-                              _pm(rel, k, k.replace("_pct", "_ci95_pct"))
-                              for k in rel if k.endswith("_vs_released_pct") and not k.startswith("paused")},
-                           "power_w_vs_paused": pw.get("power_w_vs_paused")}
-    dbc = res.get("delivered_by_component") or {}
-    out["delivered_by_component"] = {c: _r(min((v.get("samples_per_sec_per_gpu") or {"x": 0}).values()), 1)
-                                     for c, v in dbc.items()}
-    ua = res.get("util_accuracy") or {}
-    if ua.get("per_rate"):
-        def mean(xs):
-            xs = [x for x in xs if x is not None]
-            return _r(sum(xs) / len(xs), 1) if xs else None
-
-        short = {"burst_1ms_every_5ms": "1ms/5ms", "burst_0.2ms_every_1ms": "0.2ms/1ms",
-                 "triad_1ms_every_5ms": "triad1ms/5ms", "mfma_saturating": "sat"}
-        out["util_accuracy"] = {
-            "cols": "exported busy %, kernel duty %",
-            **{hz: {short.get(ld, ld): [mean([r.get("busy_counter_pct") for r in pg.values()]),
-                                        mean([r.get("duty_gpu_pct") for r in pg.values()])]
-                    for ld, pg in per.items()} for hz, per in ua["per_rate"].items()},
-            "worst_error_pts": {short.get(k, k): v for k, v in (ua.get("worst_error_pts") or {}).items()}}
-        # what the auto source removes: the PMFW busy of the fastest rate's 0.2 ms train
-        fast = max(ua["per_rate"], key=float)
-        pg = ua["per_rate"][fast].get("burst_0.2ms_every_1ms") or {}
-        out["util_accuracy"]["pmfw_busy_0.2ms_" + fast] = mean([r.get("pmfw_gfx_busy_pct") for r in pg.values()])
-    q = res.get("quiet_gpu") or {}
-    if q:
-        out["quiet_gpu"] = {m: [_r(max(x.get("reads_per_s", 0) for x in v.get("per_gpu", {}).values()), 1),
-                                _r(max(x.get("pmfw_gfx_busy_pct", 0) for x in v.get("per_gpu", {}).values()), 2)]
-                            for m, v in q.items() if v.get("per_gpu")}
-    br = (res.get("burst_resolution") or {}).get("per_gpu") or {}
-    if br:
-        out["bursts_resolved"] = [sum(v.get("segments", 0) for v in br.values()), sum(v.get("launched", 0) for v in br.values())]
-    out["capacity_max_hz_98pct"] = (res.get("capacity") or {}).get("max_rate_hz_98pct")
-    out["exporter_cpu_cores"] = res.get("exporter_cpu_cores")
-    out["xgmi_link_map_ok"] = res.get("xgmi_link_map_ok")
-    out["xgmi_links_ok"] = res.get("xgmi_links_ok")
-    out["xgmi_unit_ratio"] = res.get("xgmi_unit_ratio")
-    out["xgmi_unit_ratio_min_max"] = res.get("xgmi_unit_ratio_min_max")
-    if (res.get("xgmi_link_check") or {}).get("bad_links"):
-        out["xgmi_bad_links"] = res["xgmi_link_check"]["bad_links"][:4]
-    # keep the summary inside the driver's window: shed the side estimates first
-    if len(json.dumps(out)) > SUMMARY_MAX:
-        out.pop("overhead_position_adjusted", None)
-    if len(json.dumps(out)) > SUMMARY_MAX and "util_accuracy" in out:
-        out["util_accuracy"] = {"worst_error_pts": out["util_accuracy"].get("worst_error_pts")}
-    return out
-
-
-def compact(res: dict, full_path: str) -> dict:
-    """The stdout line: the driver's contract keys, the config, where the full result
-    is, and ``summary`` last."""
-    line = {k: res.get(k) for k in CONTRACT_KEYS if k in res}
-    if "error" in res:
-        line["error"] = res["error"]
-    cfg = res.get("config") or {}
-    line["config"] = {k: cfg[k] for k in ("model", "global_batch", "seq_len", "parallelism", "hz", "hz_tiers",
-                                         "sample_source", "pmc_batch", "load") if k in cfg}
-    line["full_result"] = full_path
-    if res.get("value") is not None:
-        line["summary"] = summarize(res)
-    return line
-
-
-# ----------------------------------------------------------------------------- main
-def main(argv=None) -> int:
-    import faulthandler
-    import signal
-
-    # `kill -USR1 <rank pid>` dumps every thread's stack to stderr (a hung rank says where)
-    faulthandler.register(signal.SIGUSR1, all_threads=True)
-    argv = list(sys.argv[1:] if argv is None else argv)
-    a = parse_args(argv)
-    if a.xgmi_child:
-        return xgmi_child(a)
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return spawn_ranks(a, argv)
-    ctx = D.init_from_env(not a.mock)
-    if ctx.world != a.gpus and ctx.rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {ctx.world}; measuring {ctx.world} rank(s)", file=sys.stderr)
-    result = run(a, ctx)
-    # make the result visible to rank 0 if the exporter lived elsewhere (single node: it is rank 0)
-    result = D.broadcast_object(ctx, result)
-    rc = 0
-    if ctx.rank == 0 and result is not None:
-        # The full result (per-round blocks, per-GPU tables, ...) goes to a side file;
-        # stdout gets one compact line whose last key is ``summary``, so the part a
-        # driver keeps of stdout (its last few KB) holds every headline number.
-        full = a.out or os.path.join(REPO, "gpurun_out", f"bench_result_n{ctx.world}.json")
-        os.makedirs(os.path.dirname(os.path.abspath(full)), exist_ok=True)
-        with open(full, "w") as f:
-            f.write(json.dumps(result) + "\n")
-        print(json.dumps(compact(result, os.path.relpath(full, REPO))), flush=True)
-        rc = 1 if result.get("value") is None else 0
-    D.destroy(ctx)
-    return rc
-
+from bench.cli import main  # noqa: E402
 
 if __name__ == "__main__":
     sys.exit(main())

@@ -392,12 +392,9 @@ def test_phase_x_failure_does_not_take_the_run_down(monkeypatch):
     """Phase X runs on local rank 0 between two collectives: an exception there (a
     failed peer copy, an exporter endpoint error) must end in the result, not in a
     crashed rank 0 that leaves the other ranks waiting at the barrier."""
-    import importlib.util
     import types
 
-    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
-    b = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(b)
+    import bench as b
     calls = []
     monkeypatch.setattr(b.D, "cpu_barrier", lambda ctx: calls.append("barrier"))
     monkeypatch.setattr(b.D, "all_gather_object", lambda ctx, obj: [(0, "0000:01:00.0"), (1, "0000:02:00.0")])

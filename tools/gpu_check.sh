@@ -112,6 +112,7 @@ for s in $STEPS; do
               -p no:cacheprovider -rA ;;
     testsall) run pytest_gpu_all 900 python -u -m pytest tests -q -m gpu -v --timeout 150 --timeout-method thread \
                 -p no:cacheprovider -rA ;;
+    kfdprobe) run kfd_proc 120 python -u tools/kfd_proc_probe.py --out "$OUT/kfd_proc.json" ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
