@@ -84,6 +84,10 @@ def parse_args(argv=None):
                     help="phase S: tick rates above --hz to try under the load, one block each ('' = off)")
     ap.add_argument("--quiet-s", type=float, default=1.5,
                     help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
+    ap.add_argument("--idle-power-s", type=float, default=60.0,
+                    help="phase P: seconds per condition of an idle GPU with the counter session programmed vs "
+                    "released, paired in --idle-power-rounds ABBA rounds (0 = off)")
+    ap.add_argument("--idle-power-rounds", type=int, default=6)
     ap.add_argument("--component-s", type=float, default=1.0,
                     help="phase K: seconds each load component runs alone while the exporter samples (0 = off)")
     ap.add_argument("--released", type=int, default=1, choices=[0, 1],
@@ -92,6 +96,10 @@ def parse_args(argv=None):
     ap.add_argument("--util-s", type=float, default=1.5,
                     help="phase U: seconds of each load (idle, two MFMA burst trains, saturating MFMA) while the "
                     "exported container_gpu_sm_util / busy counter is checked against the host-known duty (0 = off)")
+    ap.add_argument("--util-irregular", type=int, default=1, choices=[0, 1],
+                    help="phase U: also the out-of-sample loads — seeded random 5 µs-20 ms kernels and gaps on one and "
+                    "on two streams, and a bf16 training step (VERDICT r5 #3)")
+    ap.add_argument("--util-seed", type=int, default=6, help="phase U: seed of the random kernel schedules")
     ap.add_argument("--util-hz", default="1000,10",
                     help="phase U: tick rates besides the primary --hz ('' = primary only); 10 Hz is the "
                     "DaemonSet's (deploy/daemonset.yaml), each load there runs at least 30 drain periods")

@@ -60,6 +60,7 @@ class GpuLoad(Load):
         from kube_gpu_stats_amd.ops.load import LoadStep
 
         self.torch = torch
+        self.a, self.device = a, device
         self.ls = LoadStep(device=device, mfma_blocks=a.mfma_blocks, mfma_iters=a.mfma_iters,
                            stream_bytes=int(a.stream_gib * (1 << 30)))
         self.triads = a.triads
@@ -200,6 +201,35 @@ class GpuLoad(Load):
                 ev[-2][1].synchronize()
         torch.cuda.synchronize()
         return sum(x.elapsed_time(y) for x, y in ev) * 1e-3
+
+    def irregular(self, secs: float, seed: int, streams: int = 1) -> float:
+        """Seeded random MFMA kernels (5 µs - 20 ms) and gaps on ``streams`` streams for
+        ``secs``: the union of the kernels' event-timed intervals, seconds (phase U)."""
+        from kube_gpu_stats_amd.ops.irregular import IrregularLoad, mfma_launcher
+
+        if not hasattr(self, "_irr"):
+            per_iter = self.mfma_ms / max(1, self.ls.mfma_iters)
+            self._irr = IrregularLoad(self.torch, mfma_launcher(self.torch, self.ls, per_iter), self.device)
+        r = self._irr.run(secs, seed, streams)
+        self.last_irregular = r
+        return r["busy_s"]
+
+    def prepare_train(self) -> None:
+        if not hasattr(self, "_train"):
+            self._train = TrainLoad(self.a, self.device, None)
+            self._train.unit()  # allocator growth, kernel selection
+            self._train.unit()
+            self.torch.cuda.synchronize()
+
+    def train_timed(self, secs: float) -> float:
+        """bf16 decoder training steps (TrainLoad, no DDP) for ``secs``: the union of the
+        step kernels' execution intervals from the PyTorch profiler, seconds (phase U)."""
+        from kube_gpu_stats_amd.ops.irregular import profiled_busy
+
+        self.prepare_train()
+        busy, steps, kernels = profiled_busy(self.torch, self._train.unit, secs)
+        self.last_train = {"steps": steps, "kernels": kernels}
+        return busy
 
     def calibrate(self) -> dict:
         """Per-kernel throughput (events), outside every timed region."""
@@ -366,6 +396,14 @@ class MockLoad(Load):
     def saturate(self, secs: float) -> float:
         time.sleep(secs)
         return secs
+
+    def irregular(self, secs: float, seed: int, streams: int = 1) -> float:
+        time.sleep(secs)  # plumbing only: the mock counters do not follow the host
+        return 0.5 * secs
+
+    def train_timed(self, secs: float) -> float:
+        time.sleep(secs)
+        return 0.9 * secs
 
     def sync(self):
         pass

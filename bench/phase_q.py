@@ -1,11 +1,13 @@
-"""Phase Q — what the exporter does to an idle GPU (READ rate, PMFW busy, SPI share)."""
+"""Phase Q — what the exporter does to an idle GPU (READ rate, PMFW busy, SPI share), and
+phase P — what its counter session costs that GPU in socket power."""
 from __future__ import annotations
 
 import time
 
 from kube_gpu_stats_amd.parallel import dist as D
 
-from .common import scrape_at
+from .common import mean_ci95, scrape_at
+from .exporter import PmfwProbe
 
 
 def quiet_gpu(ctx, load, exp, a) -> dict:
@@ -46,4 +48,67 @@ def quiet_gpu(ctx, load, exp, a) -> dict:
                 for g in sorted(r1, key=int)}}
         exp.set_idle_hz(default_idle)
     D.cpu_barrier(ctx)  # the other ranks wait here without a spinning RCCL kernel on their GPUs
+    return out
+
+
+def idle_power(ctx, load, exp, a) -> dict:
+    """Phase P (untimed) — what the counter session costs an idle GPU in power (VERDICT
+    r5 #5).  With every rank's GPU idle, --idle-power-s of blocks with the exporter
+    running at its defaults (the quiet GPU READ at --pmc-idle-hz, the perfmon session
+    programmed, the READ queue mapped) alternate (ABBA) with blocks where the counter
+    session is released and the READ queue destroyed while the PMFW and slow tiers keep
+    sampling — what an exporter that dropped its session on a quiet GPU would leave.
+    Each rank reads its own GPU's socket power from the PMFW energy accumulator at the
+    block edges (PmfwProbe, not the exporter); the paired difference per round is the
+    session's idle cost, mean ± 95 % CI (``summary.quiet_gpu.power_w_session``)."""
+    secs = float(getattr(a, "idle_power_s", 0.0) or 0.0)
+    rounds = int(getattr(a, "idle_power_rounds", 6) or 0)
+    if secs <= 0 or rounds <= 0 or a.mock:
+        return {}
+    block = secs / rounds
+    probe = PmfwProbe(load.pci_bdf(ctx.local_rank))
+    if probe.N is None:
+        return {"skipped": "no PMFW table probe"}
+    D.cpu_barrier(ctx)
+    load.sync()
+    local: list[dict] = []
+    for r in range(rounds):
+        order = ("session", "released") if r % 2 == 0 else ("released", "session")
+        row: dict = {}
+        for cond in order:
+            if ctx.local_rank == 0 and exp is not None:
+                if cond == "released":
+                    exp.release(drop_queue=True)
+                else:
+                    exp.acquire()
+            D.cpu_barrier(ctx)
+            time.sleep(min(1.0, 0.2 * block))  # settle: the power-state change after the switch
+            p0 = probe.read()
+            time.sleep(block)
+            row[cond] = PmfwProbe.delta(p0, probe.read())
+            D.cpu_barrier(ctx)
+        local.append(row)
+    if ctx.local_rank == 0 and exp is not None:
+        exp.acquire()
+    ranks = D.all_gather_object(ctx, local)
+    per_rank = []
+    for rk in ranks:
+        pairs = [(rd["session"]["power_w"], rd["released"]["power_w"]) for rd in rk
+                 if rd.get("session") and rd.get("released")]
+        if not pairs:
+            per_rank.append(None)
+            continue
+        m, ci, sd = mean_ci95([s - r for s, r in pairs])
+        per_rank.append({"session_w": round(sum(s for s, _ in pairs) / len(pairs), 2),
+                         "released_w": round(sum(r for _, r in pairs) / len(pairs), 2),
+                         "session_minus_released_w": round(m, 3), "ci95_w": round(ci, 3), "sd_w": round(sd, 3),
+                         "rounds": len(pairs)})
+    ok = [p for p in per_rank if p]
+    out = {"secs_per_condition": secs, "rounds": rounds, "block_s": round(block, 2),
+           "conditions": {"session": "exporter defaults: quiet GPU READ at --pmc-idle-hz, session programmed",
+                          "released": "counter session STOPped and READ queue destroyed; PMFW / slow tiers sampling"},
+           "per_rank": per_rank}
+    if ok:
+        out["session_minus_released_w"] = round(sum(p["session_minus_released_w"] for p in ok) / len(ok), 3)
+        out["ci95_w"] = round(max(p["ci95_w"] for p in ok), 3)
     return out

@@ -16,7 +16,12 @@ def util_accuracy(ctx, load, exp, a) -> dict:
     the exporter's default flags (adaptive idle rate, batched READs, --sm-util-source
     auto), every rank runs the same load for --util-s — idle, a train of 1 ms MFMA
     kernels every 5 ms, a train of 0.2 ms kernels every 1 ms, a train of 1 ms HBM triads
-    every 5 ms (memory-bound: full shader clock), MFMA kernels back to back — and rank 0 reads, per GPU, 100·rate(container_gpu_busy_seconds_total)
+    every 5 ms (memory-bound: full shader clock), MFMA kernels back to back, and (with
+    --util-irregular) the out-of-sample loads of ops/irregular.py:
+    seeded random MFMA kernels of 5 µs – 20 ms with random 5 µs – 20 ms gaps on one
+    stream and on two streams at once (duty = the union of the kernels' event-timed
+    intervals), and a bf16 decoder training step (duty = the union of its kernels'
+    intervals from the PyTorch profiler) — and rank 0 reads, per GPU, 100·rate(container_gpu_busy_seconds_total)
     (exact over the window), the container_gpu_sm_util gauge and the raw PMFW GFX busy,
     next to the duty the rank measured: its kernels' own GPU time (HIP events) over
     the window (``duty_gpu_pct``, the truth "a kernel is running" means) and the
@@ -27,7 +32,16 @@ def util_accuracy(ctx, load, exp, a) -> dict:
     plan = [("idle", None), ("burst_1ms_every_5ms", (1.0, 5.0)), ("burst_0.2ms_every_1ms", (0.2, 1.0)),
             ("triad_1ms_every_5ms", (1.0, 5.0, "triad")),
             ("mfma_saturating", "sat")]
+    if getattr(a, "util_irregular", 0):
+        plan += [("random_kernels", ("irregular", 1)), ("two_stream_random", ("irregular", 2)),
+                 ("train_step", "train")]
     out: dict = {"secs_per_load": a.util_s, "per_rate": {}}
+    errors: dict = {}
+    if any(spec == "train" for _, spec in plan) and hasattr(load, "prepare_train"):
+        try:  # build and warm the training step outside every window
+            load.prepare_train()
+        except Exception as e:  # noqa: BLE001 - report the load as failed, keep the phase
+            errors["train_step"] = f"{type(e).__name__}: {e}"[:300]
     for hz in rates:
         if exp is not None:
             exp.set_rate(hz)
@@ -47,16 +61,30 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         # tail as idle.
         secs = max(a.util_s, 60.0 / hz)
         tail = max(5.0 / hz, 0.05)
-        for name, spec in plan:
+        for li, (name, spec) in enumerate(plan):
             load.sync()
             D.cpu_barrier(ctx)  # no RCCL kernel inside the window
             m0, w0 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
             t0 = time.perf_counter()
             gpu_s = host_s = 0.0
-            if spec is None:
+            err = errors.get(name)
+            if err:
+                pass
+            elif spec is None:
                 time.sleep(secs)
             elif spec == "sat":
                 gpu_s = load.saturate(secs)
+                host_s = time.perf_counter() - t0
+            elif spec == "train" or spec[0] == "irregular":
+                try:
+                    if spec == "train":
+                        gpu_s = load.train_timed(secs)
+                    else:  # one seed per (rate, load): the same schedule on every rank and every run
+                        gpu_s = load.irregular(secs, seed=int(getattr(a, "util_seed", 6)) * 100 + 10 * rates.index(hz)
+                                               + li, streams=spec[1])
+                except Exception as e:  # noqa: BLE001
+                    err = errors[name] = f"{type(e).__name__}: {e}"[:300]
+                    load.sync()
                 host_s = time.perf_counter() - t0
             else:
                 ms, period = spec[0], spec[1]
@@ -72,7 +100,7 @@ def util_accuracy(ctx, load, exp, a) -> dict:
                     if d > 0:
                         time.sleep(d)
             time.sleep(tail)
-            own = (gpu_s, host_s, time.perf_counter() - t0)
+            own = (gpu_s, host_s, time.perf_counter() - t0, err)
             D.cpu_barrier(ctx)
             m1, w1 = scrape_at(exp.sc) if exp is not None else ({}, 0.0)
             everyone = D.all_gather_object(ctx, (load.pci_bdf(ctx.local_rank), own))
@@ -86,9 +114,12 @@ def util_accuracy(ctx, load, exp, a) -> dict:
                 return sum(v for lb, v in m1.get(fam, []) if lb["gpu"] == g) - b.get(g, 0.0)
 
             per_gpu: dict = {}
-            for bdf, (g_s, h_s, _) in everyone:
+            for bdf, (g_s, h_s, _, e_r) in everyone:
                 g = gpu_of.get(bdf)
                 if g is None or win <= 0:
+                    continue
+                if e_r:
+                    per_gpu[g] = {"error": e_r}
                     continue
                 sm = [v for lb, v in m1.get("container_gpu_sm_util", []) if lb["gpu"] == g]
                 per_gpu[g] = {"duty_gpu_pct": round(100 * g_s / win, 2), "duty_host_pct": round(100 * h_s / win, 2),
@@ -115,6 +146,8 @@ def util_accuracy(ctx, load, exp, a) -> dict:
     for per_load in out["per_rate"].values():
         for name, per_gpu in per_load.items():
             for r in per_gpu.values():
+                if "error_pts" not in r:
+                    continue
                 worst[name] = round(max(worst.get(name, 0.0), abs(r["error_pts"])), 2)
     out["worst_error_pts"] = worst
     return out

@@ -13,7 +13,7 @@ from .loads import GpuLoad, MockLoad, TrainLoad
 from .observe import allreduce_GBps, allreduce_ratio, observed, throttled, wake_lateness, xgmi_rates
 from .phase_i import interleaved
 from .phase_k import component_rates
-from .phase_q import quiet_gpu
+from .phase_q import idle_power, quiet_gpu
 from .phase_r import burst_train
 from .phase_s import capacity
 from .phase_u import util_accuracy
@@ -98,6 +98,10 @@ def run(a, ctx) -> dict | None:
 
     resolution = burst_train(ctx, load, exp, a)
     quiet = quiet_gpu(ctx, load, exp, a)
+    if quiet is not None:
+        power = idle_power(ctx, load, exp, a)
+        if power:
+            quiet["idle_power"] = power
     util = util_accuracy(ctx, load, exp, a)
     inter = interleaved(ctx, load, exp, a, hzs)
     cap = capacity(ctx, load, exp, a)

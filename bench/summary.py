@@ -56,7 +56,8 @@ def summarize(res: dict) -> dict:
             return _r(sum(xs) / len(xs), 1) if xs else None
 
         short = {"burst_1ms_every_5ms": "1ms/5ms", "burst_0.2ms_every_1ms": "0.2ms/1ms",
-                 "triad_1ms_every_5ms": "triad1ms/5ms", "mfma_saturating": "sat"}
+                 "triad_1ms_every_5ms": "triad1ms/5ms", "mfma_saturating": "sat", "random_kernels": "rand",
+                 "two_stream_random": "rand2s", "train_step": "train"}
         out["util_accuracy"] = {
             "cols": "exported busy %, kernel duty %",
             **{hz: {short.get(ld, ld): [mean([r.get("busy_counter_pct") for r in pg.values()]),
@@ -72,6 +73,10 @@ def summarize(res: dict) -> dict:
         out["quiet_gpu"] = {m: [_r(max(x.get("reads_per_s", 0) for x in v.get("per_gpu", {}).values()), 1),
                                 _r(max(x.get("pmfw_gfx_busy_pct", 0) for x in v.get("per_gpu", {}).values()), 2)]
                             for m, v in q.items() if v.get("per_gpu")}
+        ip = q.get("idle_power") or {}
+        if "session_minus_released_w" in ip:  # phase P: [session − released W, ± 95 %, released W]
+            out["quiet_gpu"]["power_w_session"] = [ip["session_minus_released_w"], ip.get("ci95_w"),
+                                                   (ip["per_rank"][0] or {}).get("released_w")]
     br = (res.get("burst_resolution") or {}).get("per_gpu") or {}
     if br:
         out["bursts_resolved"] = [sum(v.get("segments", 0) for v in br.values()), sum(v.get("launched", 0) for v in br.values())]

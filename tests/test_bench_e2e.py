@@ -115,13 +115,13 @@ def test_bench_contract_single_process(tmp_path):
     assert set(ua["per_rate"]) == {"8000", "1000", "10"}
     for per in ua["per_rate"].values():
         assert set(per) == {"idle", "burst_1ms_every_5ms", "burst_0.2ms_every_1ms", "triad_1ms_every_5ms",
-                            "mfma_saturating"}
+                            "mfma_saturating", "random_kernels", "two_stream_random", "train_step"}
         row = per["burst_1ms_every_5ms"]["0"]
         assert set(row) >= {"duty_gpu_pct", "duty_host_pct", "busy_counter_pct", "sm_util_gauge", "pmfw_gfx_busy_pct",
                             "from_counters_pct", "error_pts"}
         assert 10 < row["duty_gpu_pct"] < 30 and row["from_counters_pct"] > 90, row  # mock bursts: sleeps
     assert set(ua["worst_error_pts"]) == {"idle", "burst_1ms_every_5ms", "burst_0.2ms_every_1ms", "triad_1ms_every_5ms",
-                                          "mfma_saturating"}
+                                          "mfma_saturating", "random_kernels", "two_stream_random", "train_step"}
     assert inter["paused_reads"] == 0
     assert res["xgmi_link_check"] == {"skipped": "N=1: no peer GPU to copy to"} and res["xgmi_link_map_ok"] is None
     for hz in ("100", "8000"):

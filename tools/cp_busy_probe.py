@@ -122,6 +122,11 @@ def main(argv=None) -> int:
                     help="READ pipelined, as the exporter does above its idle rate")
     ap.add_argument("--dump", default="", help="write every raw sample of the --dump-rates runs here (JSON)")
     ap.add_argument("--dump-rates", default="8000")
+    ap.add_argument("--irregular", type=int, default=0, choices=[0, 1],
+                    help="also the out-of-sample loads of ops/irregular.py (VERDICT r5 #3): seeded random MFMA "
+                    "kernels and gaps on one and two streams, and a bf16 training step (profiler-timed)")
+    ap.add_argument("--only-irregular", type=int, default=0, choices=[0, 1],
+                    help="with --irregular: idle + the irregular loads only (the held-out dumps)")
     ap.add_argument("--child", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--child-secs", type=float, default=0.0, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
@@ -135,6 +140,20 @@ def main(argv=None) -> int:
 
     loads = Loads(torch)
     names = ["idle", "mfma", "triad", "gemm", "tiny_graph", "burst_1_5", "burst_02_1"]
+    irr = train = None
+    if a.irregular:
+        from kube_gpu_stats_amd.ops.irregular import IrregularLoad, mfma_launcher, profiled_busy
+
+        irr = IrregularLoad(torch, mfma_launcher(torch, loads.ls, loads.ms_per_iter))
+        import bench
+
+        ta = bench.parse_args(["--train-dim", "2048", "--train-layers", "4", "--train-batch", "4", "--train-seq", "1024"])
+        train = bench.TrainLoad(ta, 0, None)
+        for _ in range(2):
+            train.unit()
+        torch.cuda.synchronize()
+        names = (["idle"] if a.only_irregular else names) + ["random_kernels", "two_stream_random", "train_step"]
+    seeds = {"random_kernels": (71, 1), "two_stream_random": (72, 2)}
 
     def gpu_busy(name: str, secs: float) -> float:
         """Event-timed kernel seconds (bursts: event-timed too, not host-timed)."""
@@ -155,6 +174,10 @@ def main(argv=None) -> int:
                 if d > 0:
                     time.sleep(d)
             return busy
+        if name in seeds:
+            return irr.run(secs, seeds[name][0], seeds[name][1])["busy_s"]
+        if name == "train_step":
+            return profiled_busy(torch, train.unit, secs)[0]
         return getattr(loads, "run_" + name)(secs)
 
     out: dict = {"counters": NAMES, "rates": {}, "pipelined": a.pipelined}

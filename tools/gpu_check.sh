@@ -112,6 +112,11 @@ for s in $STEPS; do
               -p no:cacheprovider -rA ;;
     testsall) run pytest_gpu_all 900 python -u -m pytest tests -q -m gpu -v --timeout 150 --timeout-method thread \
                 -p no:cacheprovider -rA ;;
+    cpdumpirr) run cp_dump_irregular 420 python -u tools/cp_busy_probe.py --rates 8000,1000,100,10 --pipelined 1 \
+                 --batch 8 --lite 1 --exporter-set 1 --secs 4 --irregular 1 --only-irregular 1 \
+                 --out "$OUT/cp_busy_irregular.json" --dump "$OUT/cp_dump_irregular.json" --dump-rates 8000,1000,100,10 ;;
+    testsirr) run pytest_irregular 300 python -u -m pytest tests -m gpu -v --timeout 250 --timeout-method thread \
+                -p no:cacheprovider -rA -k "irregular" ;;
     kfdprobe) run kfd_proc 120 python -u tools/kfd_proc_probe.py --out "$OUT/kfd_proc.json" ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
