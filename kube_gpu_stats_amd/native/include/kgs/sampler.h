@@ -127,6 +127,10 @@ struct SamplerConfig {
 
 constexpr double kMaxHz = 100000.0;     // tick-rate ceiling accepted at run time (set_hz)
 constexpr double kMinIdleHz = 0.01;     // pmc_idle_hz: 0 (off) or at least this
+// UtilBiller's carry (and run-on guess) never exceeds this, whatever the freshness
+// window: at --pmc-idle-hz 0.01 that window is 300 s, and busy carried that long would
+// be billed into a later idle stretch — or a later pod.
+constexpr double kMaxUtilCarryS = 1.0;
 
 // The counter tick's dithered offset from its fixed grid (SamplerConfig::tick_dither): a
 // random walk of at most `dither` of a period per tick, reflected into ± half a period.
@@ -272,6 +276,7 @@ struct DeviceState {
   std::atomic<uint64_t> pmc_retries{0};      // reset + acquire attempts while the breaker is open
   std::atomic<int> thread_hung{0};           // a sampler thread of this device was abandoned by stop()
   std::atomic<uint64_t> pmc_reordered{0};    // drains dropped: CP time earlier than the previous drain's
+  std::atomic<int> util_carry_drop{0};       // owners changed: the PMFW thread drops the billing carry
   // Test hook (Sampler::inject_pmc_stall, /control/pmc/stall with --control-http):
   // the device's own counter thread asks the source to wedge its READ queue.
   std::atomic<int> pmc_stall_req{0};
@@ -391,6 +396,9 @@ class Sampler {
   // (GPU, PID) → "namespace/pod" of the processes' pods, for the per-pod CU
   // integrals (slow tier; the exporter pushes it with its PID → pod table).
   void set_pid_pods(std::shared_ptr<const std::unordered_map<uint64_t, std::string>> m);
+  // The GPU's owner set changed: its PMFW thread drops the billing carry at its next
+  // distinct sample (UtilBiller::drop_carry).
+  void drop_util_carry(int dev);
   // ∫ CU-occupancy share dt of the pod `ns_pod` ("namespace/pod") on `dev`, 0 if none.
   double pod_cu_seconds(int dev, const std::string& ns_pod) const;
 

@@ -164,7 +164,12 @@ class DispatchEstimator {
       // and so is the SPI blip (≈0.9 µs per READ: 0.7 % of the clocks at 8 kHz, so the
       // test is the quiet threshold, not "no SPI at all" — r4f: a 0.5 % test kept 2 %
       // of the 8 kHz READ-only intervals, the cheap ones, and learned 13 µs for 15.5).
-      const bool read_only = act < p.quiet_active_frac * clk && d.mfma == prev_mfma_ && cpc < 0.5 * clk;
+      const bool read_only_shape = act < p.quiet_active_frac * clk && d.mfma == prev_mfma_ && cpc < 0.5 * clk;
+      // ... and, once this READ kind's cost is known, CP busy within 2 × that cost: the
+      // shape alone also fits CP-only work (a stream of wave-less dispatches at 30-50 % of
+      // the clocks), which must neither teach the READ cost nor bill zero.
+      const double known = read_n_[m][f] ? read_cyc_[m][f] : 0.0;
+      const bool read_only = read_only_shape && (known <= 0 || cpc <= 2.0 * known);
       if (read_only) {
         const bool first = read_n_[m][f] == 0;
         read_cyc_[m][f] = first ? cpc : (1 - p.ewma) * read_cyc_[m][f] + p.ewma * cpc;
@@ -354,6 +359,13 @@ class UtilBiller {
     return b;
   }
   double carry_s() const { return carry_s_; }
+  // The GPU changed hands (a pod's allocation ended or began): busy still carried is the
+  // previous owner's, and container_gpu_busy_seconds_total counts per allocation — drop
+  // it (into dropped_s) rather than bill it to the next pod.
+  void drop_carry() {
+    dropped_s_ += std::max(carry_s_, 0.0);
+    carry_s_ = 0;
+  }
   // Counter busy beyond max_carry_s, never billed (a firmware / host clock skew, or a
   // counter integral running ahead of firmware time).
   double dropped_s() const { return dropped_s_; }

@@ -668,7 +668,9 @@ PYBIND11_MODULE(_kgs_native, m) {
           "Bill one PMFW interval: (seconds billed, billed from the counters?).  drains: the count of "
           "drains folded so far (a new drain restarts the run-on guess)")
       .def_property_readonly("carry_s", &UtilBiller::carry_s)
-      .def_property_readonly("dropped_s", &UtilBiller::dropped_s);
+      .def_property_readonly("dropped_s", &UtilBiller::dropped_s)
+      .def("drop_carry", &UtilBiller::drop_carry, "The GPU changed hands: drop the busy still carried");
+  m.attr("MAX_UTIL_CARRY_S") = kMaxUtilCarryS;
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
   m.def("pmc_counter_names", [] {

@@ -231,12 +231,14 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
   auto m = owners_ ? std::make_shared<std::map<int, std::vector<Owner>>>(*owners_)
                    : std::make_shared<std::map<int, std::vector<Owner>>>();
   const auto prev = m->find(dev);
+  size_t kept_n = 0;
   for (Owner& x : o) {
     // An owner already on this GPU keeps its base; a new one starts counting now.
     const Owner* kept = nullptr;
     if (prev != m->end())
       for (const Owner& y : prev->second)
         if (y.same(x)) kept = &y;
+    kept_n += kept != nullptr;
     x.base_busy_s = kept ? kept->base_busy_s : I.gfx_busy_seconds;
     x.base_mfma_s = kept ? kept->base_mfma_s : I.mfma_busy_seconds;
     x.base_active_s = kept ? kept->base_active_s : I.active_seconds;
@@ -244,9 +246,12 @@ void Exporter::set_device_owners(int dev, std::vector<Owner> o) {
     x.base_energy_j = kept ? kept->base_energy_j : I.energy_joules;
     x.base_cu_s = kept ? kept->base_cu_s : (sampler_ ? sampler_->pod_cu_seconds(dev, x.ns + "/" + x.pod) : 0.0);
   }
+  const size_t prev_n = prev != m->end() ? prev->second.size() : 0;
+  const bool changed = kept_n != o.size() || kept_n != prev_n;
   if (o.empty()) m->erase(dev);
   else (*m)[dev] = std::move(o);
   owners_ = std::move(m);
+  if (changed && sampler_) sampler_->drop_util_carry(dev);  // the old owner's carried busy is not the new one's
 }
 
 void Exporter::set_pid_owners(std::unordered_map<uint64_t, PidOwner> m) {

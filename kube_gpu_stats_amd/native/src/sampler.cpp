@@ -186,6 +186,10 @@ void Sampler::set_pmc_wanted(bool on, int dev, bool drop_queue) {
     }
 }
 
+void Sampler::drop_util_carry(int dev) {
+  if (dev >= 0 && dev < device_count()) states_[static_cast<size_t>(dev)]->util_carry_drop.store(1);
+}
+
 void Sampler::set_pid_pods(std::shared_ptr<const std::unordered_map<uint64_t, std::string>> m) {
   std::lock_guard<std::mutex> g(pid_pods_mu_);
   pid_pods_ = std::move(m);
@@ -428,9 +432,11 @@ void Sampler::run_pmfw_util(int dev, int64_t now, double dgfx_s, double dt_s, In
   c.share = pc.pmc_last_share;
   c.since_s = (now - pc.pmc_last_ns) * 1e-9;
   c.drains = pc.pmc_samples;
-  // Carry (and run the last drain on) at most one freshness window: the
-  // drain-vs-interval jitter, never a backlog.
-  const UtilBiller::Bill b = util_bill_[static_cast<size_t>(dev)].bill(dt_s, dgfx_s, c, fresh_ns * 1e-9);
+  // Carry (and run the last drain on) at most one freshness window, and never more
+  // than kMaxUtilCarryS: the drain-vs-interval jitter, never a backlog.
+  if (st.util_carry_drop.exchange(0, std::memory_order_relaxed)) util_bill_[static_cast<size_t>(dev)].drop_carry();
+  const UtilBiller::Bill b =
+      util_bill_[static_cast<size_t>(dev)].bill(dt_s, dgfx_s, c, std::min(fresh_ns * 1e-9, kMaxUtilCarryS));
   I.util_seconds += b.billed_s;
   if (b.from_counters) I.util_counter_seconds += dt_s;
   I.util_carry_seconds = util_bill_[static_cast<size_t>(dev)].carry_s();

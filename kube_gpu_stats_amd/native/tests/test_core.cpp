@@ -1012,6 +1012,58 @@ static void test_dispatch_estimator() {
   CHECK(!e.quiet());
 }
 
+// an interval with no wave, no MFMA cycle and the CP busy ≈48 % of the clocks
+// has the READ-learning rule's shape, but its CP time is four READs' worth: it bills that
+// time (less one READ) and classifies as dispatch-bound — only intervals within
+// 2 × the learned READ cost bill zero.
+static void test_cp_only_work_is_not_read_only() {
+  const EstimatorParams p = estimator_params(SamplerConfig{}, 256);
+  DispatchEstimator e;
+  e.restart(0);
+  int64_t t = 0;
+  double cnt = 0, spi = 0, cpc = 0;
+  auto read = [&]() {
+    Drain d;
+    d.mono_ns = t;
+    d.mask = kPmcSetBase;
+    d.count = static_cast<uint64_t>(cnt);
+    d.spi = static_cast<uint64_t>(spi);
+    d.cpc = static_cast<uint64_t>(cpc);
+    return e.feed(d, p);
+  };
+  for (int i = 0; i < 100; ++i) {  // idle READs teach the 15 µs READ cost
+    t += 125000;
+    cnt += 2.4e3 * 125;
+    cpc += 2.4e3 * 15;
+    spi += 2.4e3 * 0.9;
+    read();
+  }
+  double disp = 0;
+  bool dbound = false;
+  for (int i = 0; i < 120; ++i) {  // 15 ms of CP-only work at 48 % of the clocks, SPI < 2 %
+    t += 125000;
+    cnt += 2.4e3 * 125;
+    cpc += 2.4e3 * 60;
+    spi += 2.4e3 * 0.9;
+    const DrainStep r = read();
+    disp += r.dispatch_s;
+    CHECK(r.dispatch_s > 40e-6);  // 60 µs of CP time less the READ's 15
+    dbound |= r.dbound_interval;
+  }
+  CHECK(std::abs(disp - 120 * 45e-6) < 120 * 3e-6);
+  // each interval is CP-busy without waves for ≥ 0.3 of the clocks; the READ rate still
+  // drops to the idle rate rather than the dispatch rate, since no wave ran (quiet wins)
+  CHECK(dbound);
+  CHECK(e.quiet() && !e.dbound());
+  // a READ-only interval within the learned cost still bills nothing
+  t += 125000;
+  cnt += 2.4e3 * 125;
+  cpc += 2.4e3 * 16;
+  spi += 2.4e3 * 0.9;
+  CHECK(read().dispatch_s == 0.0);
+  std::printf("cp-only work billed ok (%.1f µs per interval, dispatch-bound %d)\n", disp / 120 * 1e6, dbound);
+}
+
 // UtilBiller: drains at 10 Hz land on host time, PMFW tables on a 20 ms firmware
 // grid read at 10 Hz — an interval holds 0, 1 or 2 drains.  Carrying the excess
 // bills a saturated GPU everything but the last drain's lag; the round-4 clip
@@ -1086,6 +1138,7 @@ static void test_tick_dither() {
 
 int main() {
   test_dispatch_estimator();
+  test_cp_only_work_is_not_read_only();
   test_util_biller();
   test_tick_dither();
   test_lite_ib();

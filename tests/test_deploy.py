@@ -76,6 +76,32 @@ def test_monitoring_rules_reference_exported_families():
     assert not unknown_series(exprs)
 
 
+def _alert_not_from_counters(pmfw_rate: float, enabled: int, failed: int) -> bool:
+    """KgsUtilisationNotFromCounters for one (instance, gpu), evaluated by hand on the
+    exact expression shape the rule uses: ``A > 0.5 and on (instance, gpu) (B == 1 or
+    C == 1)`` (PromQL ``and`` keeps the left sample where the right side has a series)."""
+    right = enabled == 1 or failed == 1
+    return pmfw_rate > 0.5 and right
+
+
+def test_pmfw_billing_alert_fires_while_the_breaker_is_open():
+    """trip() sets kgs_pmc_enabled 0 while the counter tier's breaker is open,
+    so a rule gated on kgs_pmc_enabled == 1 alone never fired for the case it names.
+    Gated on the exporter *wanting* the counters: an open breaker (enabled 0, failed 1)
+    and stale drains (enabled 1) fire; a hand-over to another profiler (enabled 0,
+    failed 0) does not."""
+    docs = load("monitoring.yaml")
+    rule = next(d for d in docs if d["kind"] == "PrometheusRule")
+    r = next(r for g in rule["spec"]["groups"] for r in g["rules"] if r.get("alert") == "KgsUtilisationNotFromCounters")
+    expr = " ".join(r["expr"].split())
+    assert expr.endswith("and on (instance, gpu) (kgs_pmc_enabled == 1 or kgs_pmc_failed == 1)"), expr
+    assert expr.startswith('rate(kgs_util_source_seconds_total{source="pmfw"}[15m]) > 0.5'), expr
+    assert _alert_not_from_counters(1.0, enabled=0, failed=1)       # breaker open between retries
+    assert _alert_not_from_counters(1.0, enabled=1, failed=0)       # counters held, drains stale
+    assert not _alert_not_from_counters(1.0, enabled=0, failed=0)   # handed over (SIGUSR1): expected
+    assert not _alert_not_from_counters(0.1, enabled=0, failed=1)   # mostly billed from counters
+
+
 def test_report_cronjob_has_rbac():
     docs = load("reports-cronjob.yaml")
     kinds = {d["kind"] for d in docs}

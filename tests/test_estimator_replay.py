@@ -270,11 +270,12 @@ def test_biller_falls_back_to_pmfw_and_drops_the_carry_on_an_epoch_change(N):
 
 
 def test_committed_replay_summary_matches(shipped):
-    """profiles/r5/estimator_replay*.json are this replay's output, committed: the numbers
-    README / BASELINE cite are the current code's."""
-    for path, res in ((os.path.join(REPO, "profiles", "r5", "estimator_replay.json"), shipped),
-                      (os.path.join(REPO, "profiles", "r5", "estimator_replay_lowrate.json"), sim.replay(LOWRATE)),
-                      (os.path.join(REPO, "profiles", "r5", "estimator_replay_r5l.json"), sim.replay(LOWRATE_R5L))):
+    """profiles/r6/estimator_replay*.json are this replay's output, committed: the numbers
+    README / BASELINE cite are the current code's (r6: READ-cost learning gated at 2 × the
+    learned cost moved one row, r4f 1 kHz 1 ms / 5 ms, from −0.23 to +0.08)."""
+    for path, res in ((os.path.join(REPO, "profiles", "r6", "estimator_replay.json"), shipped),
+                      (os.path.join(REPO, "profiles", "r6", "estimator_replay_lowrate.json"), sim.replay(LOWRATE)),
+                      (os.path.join(REPO, "profiles", "r6", "estimator_replay_r5l.json"), sim.replay(LOWRATE_R5L))):
         rec = json.load(open(path))
         for rate, rows in rec.items():
             for load, r in rows.items():
@@ -455,3 +456,45 @@ def test_a_microsecond_kernel_stream_is_dispatch_bound_after_the_hold(N):
     cpc += int(period * f)
     spi += int(0.95 * period * f)
     assert not e.feed(p, t, cnt, spi, cpc, mfma=10**9).dbound
+
+
+def test_carry_is_dropped_when_the_gpu_changes_hands(N):
+    """container_gpu_busy_seconds_total counts per allocation, so busy still
+    carried when a pod's allocation ends belongs to that pod, not the next one.  The
+    exporter drops it when the owner set changes (Exporter::set_device_owners →
+    Sampler::drop_util_carry), and the carry is capped at MAX_UTIL_CARRY_S whatever the
+    freshness window (pmc_idle_hz 0.01 makes that window 300 s)."""
+    b = N.UtilBiller()
+    b.bill(0.02, 0.02, True, 1, 0.0, 1.0)
+    b.bill(0.02, 0.02, True, 1, 0.05, 1.0)            # two drains' worth in one interval: 0.03 carried
+    assert b.carry_s == pytest.approx(0.03)
+    b.drop_carry()
+    assert b.carry_s == 0 and b.dropped_s == pytest.approx(0.03)
+    got, from_c = b.bill(0.02, 0.0, True, 1, 0.05, 1.0)  # the new owner's idle interval bills nothing
+    assert from_c and got == 0.0
+    assert N.MAX_UTIL_CARRY_S == pytest.approx(1.0)
+
+
+def test_reallocation_starts_the_new_pods_counter_at_zero(mock_exporter):
+    """A saturated mock GPU handed from pod a to pod b: b's container_gpu_busy_seconds_total
+    starts at 0 and never bills more than the time since its allocation (the old owner's
+    carry is dropped, not billed to b)."""
+    from kube_gpu_stats_amd.utils.scrape import parse_text
+
+    ex = mock_exporter(n_gpus=1, hz=10, pmc_source="mock", proc_every=0, link_every=0,
+                       mock={"util_base": 100, "util_amp": 0})
+    ex.set_device_owners(0, [{"pod": "a", "namespace": "ns", "container": "c"}])
+    import time as _t
+
+    _t.sleep(1.2)
+    d0 = ex.integrals(0)["util_dropped_seconds"]
+    ex.set_device_owners(0, [{"pod": "a", "namespace": "ns", "container": "c"}])  # same owner: nothing dropped
+    _t.sleep(0.3)
+    t0 = _t.monotonic()
+    ex.set_device_owners(0, [{"pod": "b", "namespace": "ns", "container": "c"}])
+    _t.sleep(1.0)
+    m = parse_text(ex.render())
+    el = _t.monotonic() - t0
+    busy = {lb["pod_name"]: v for lb, v in m["container_gpu_busy_seconds_total"]}
+    assert set(busy) == {"b"} and 0.5 < busy["b"] <= el + 0.02, (busy, el)
+    assert ex.integrals(0)["util_dropped_seconds"] >= d0

@@ -265,13 +265,15 @@ def test_injected_queue_stall_trips_the_breaker_and_a_fresh_queue_recovers(mock_
     done = threading.Event()
 
     def watch():  # the breaker may open and close again while the rates below are measured
+        # Light: GPU 1's latest drain and its breaker flag, not a full render of both GPUs'
+        # pages (a 50 Hz render stole GPU 0's wake-ups on a loaded CI host).
         nonlocal seen_failed
         while not done.is_set() and time.time() - t0 < 3.0:
-            m = parse_text(ex.render())
-            totals.append(g0(m))
-            if seen_failed is None and {lb["gpu"]: v for lb, v in m["kgs_pmc_failed"]}["1"] == 1:
+            totals.append(ex.pmc(1)["values"]["GRBM_COUNT"])
+            failed = ex.integrals(1)["pmc_failed"]
+            if seen_failed is None and failed == 1:
                 seen_failed = time.time() - t0
-            if seen_failed is not None and ex.integrals(1)["pmc_failed"] == 0:
+            if seen_failed is not None and failed == 0:
                 break
             time.sleep(0.02)
 
@@ -287,12 +289,20 @@ def test_injected_queue_stall_trips_the_breaker_and_a_fresh_queue_recovers(mock_
     assert all(b >= a for a, b in zip(totals, totals[1:])), totals               # monotonic throughout
     time.sleep(0.2)
     assert g0(parse_text(ex.render())) > totals[-1]                              # and counting again
-    # GPU 0 never waits on GPU 1's queue: no READ error, no trip, its rate kept (0.8: the
-    # watcher renders at 50 Hz and a loaded CI host steals the sampler's wake-ups — six
-    # concurrent runs of this test measured 0.91-0.95 of the rate)
-    assert pmc[0] >= 0.8 * HZ and pmfw[0] >= 40 and pmfw[1] >= 40, (pmc, pmfw)
+    # GPU 0 never waits on GPU 1's queue: no READ error, no trip, its rate kept — to
+    # 0.95 of the tick rate, so a partial cross-GPU stall (GPU 0 slowed ≈15 % by GPU 1's
+    # wedge) fails here
+    assert pmc[0] >= 0.95 * HZ and pmfw[0] >= 40 and pmfw[1] >= 40, (pmc, pmfw)
+    assert m_render_failed_seen(ex, seen_failed)
     i0 = ex.integrals(0)
     assert i0["pmc_breaker_trips"] == 0 and i0["pmc_errors"] == 0, i0
+
+
+def m_render_failed_seen(ex, seen_failed) -> bool:
+    """The breaker's state reached the scrape too: kgs_pmc_breaker_trips_total counts the
+    trip the watcher saw through integrals()."""
+    m = parse_text(ex.render())
+    return seen_failed is not None and {lb["gpu"]: v for lb, v in m["kgs_pmc_breaker_trips_total"]}["1"] == 1
 
 
 def _slow_fault_exporter(mock_exporter, **fault):
