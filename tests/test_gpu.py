@@ -18,6 +18,24 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MARGINS = os.path.join(REPO, "gpurun_out", "gpu_tests", "margins.jsonl")
+
+
+def bound(quantity: str, value, lo=None, hi=None, ctx=None) -> None:
+    """``assert lo <= value <= hi`` (either side optional) that also appends the
+    observation to gpurun_out/gpu_tests/margins.jsonl: tools/gpu_margins.py tabulates
+    every bound against what every kept run measured (profiles/gpu_test_margins.md;
+    VERDICT r5 #2: one thin-margin assertion cost the driver 16 other tests)."""
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0].split("::")[-1]
+    try:
+        os.makedirs(os.path.dirname(MARGINS), exist_ok=True)
+        with open(MARGINS, "a") as f:
+            f.write(json.dumps({"test": test, "q": quantity, "value": value, "lo": lo, "hi": hi,
+                                "t": round(time.time(), 1)}) + "\n")
+    except OSError:
+        pass
+    ok = value is not None and (lo is None or value >= lo) and (hi is None or value <= hi)
+    assert ok, (quantity, value, {"lo": lo, "hi": hi}, ctx)
 
 
 @pytest.fixture(scope="module")
@@ -146,8 +164,8 @@ def test_load_throughput_and_util_accumulators(N, torch_dev):
     tflops = ls.flops / (e0.elapsed_time(e1) * 1e-3) / 1e12
     tbps = ls.bytes / (e1.elapsed_time(e2) * 1e-3) / 1e12
     print(json.dumps({"mfma_tflops": tflops, "triad_tbps": tbps}))
-    assert tflops > 500, tflops      # dense bf16 MFMA peak ≈2500
-    assert tbps > 3.0, tbps          # HBM3E ≈6.3 measured achievable
+    bound("mfma_tflops", tflops, lo=500)      # dense bf16 MFMA peak ≈2500
+    bound("triad_tbps", tbps, lo=3.0)         # HBM3E ≈6.3 measured achievable
 
     ex = N.Exporter({"backend": "amdsmi", "port": -1, "hz": 100})
     ex.start()
@@ -165,13 +183,14 @@ def test_load_throughput_and_util_accumulators(N, torch_dev):
     # this process' waves occupy CUs; the occupancy integral grows (PIDs are host-namespace).
     # The instantaneous cu_occupancy of the last list can already be 0 (the loop ended
     # with a synchronize), so the integral is the check.
-    assert any(p["cu_seconds"] > 0.2 for p in procs), procs
+    bound("max_proc_cu_seconds", max((p["cu_seconds"] for p in procs), default=0.0), lo=0.2, ctx=procs)
     # per-XCC accumulators: every one of the 8 dies is busy under a full-grid MFMA load
-    assert len(snap["gfx_busy_xcc_window"]) == 8 and min(snap["gfx_busy_xcc_window"]) > 90, snap
+    assert len(snap["gfx_busy_xcc_window"]) == 8, snap
+    bound("min_xcc_gfx_busy_pct", min(snap["gfx_busy_xcc_window"]), lo=90, ctx=snap)
     print(json.dumps({"window": w, "integrals": integ, "wall_s": wall}))
-    assert w["gfx_busy_pct"] > 90, w
+    bound("window_gfx_busy_pct", w["gfx_busy_pct"], lo=90, ctx=w)
     # PMFW cadence ≈ 50 Hz of distinct tables
-    assert 30 <= integ["distinct_samples"] / wall <= 120, integ
+    bound("pmfw_tables_per_s", integ["distinct_samples"] / wall, lo=30, hi=120, ctx=integ)
 
 
 def _proc_cpu_seconds(pid: int) -> float:
@@ -231,15 +250,15 @@ def test_counter_reader_exporter_process(torch_dev, mode):
         cores = (_proc_cpu_seconds(proc.pid) - cpu0) / (time.time() - w0)
         print(json.dumps({"mode": mode, "mfma_util": mfma, "vmem_busy": vmem, "clock_mhz": clk,
                           "pmc_samples": pmc_n, "exporter_cpu_cores": cores, "pmc_info": ready.get("pmc_info")}))
-        assert mfma[0] > 50, mfma
+        bound(f"mfma_util_pct[{mode}]", mfma[0], lo=50)
         if full:
-            assert vmem[0] > 30, vmem     # triad keeps the TA units busy
+            bound(f"vmem_busy_pct[{mode}]", vmem[0], lo=30)     # triad keeps the TA units busy
         else:
             assert not vmem, vmem         # base set: no TA block read
-        assert 1000 < clk[0] < 2600, clk
-        assert pmc_n[0] > 200
+        bound(f"clock_mhz[{mode}]", clk[0], lo=1000, hi=2600)
+        bound(f"pmc_samples_4s_100hz[{mode}]", pmc_n[0], lo=200)
         if reader == "aqlprofile":
-            assert cores < 0.5, cores  # no spinning helper thread (rocprofiler path: ≈1.0)
+            bound(f"exporter_cpu_cores[{mode}]", cores, hi=0.5)  # no spinning helper thread (rocprofiler path: ≈1.0)
             want = "pipelined=0" if mode.endswith("-sync") else "pipelined=1"
             assert want in ready["pmc_info"][0], ready["pmc_info"]
     finally:
