@@ -84,9 +84,9 @@ def parse_args(argv=None):
                     help="phase S: tick rates above --hz to try under the load, one block each ('' = off)")
     ap.add_argument("--quiet-s", type=float, default=1.5,
                     help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
-    ap.add_argument("--idle-power-s", type=float, default=60.0,
-                    help="phase P: seconds per condition of an idle GPU with the counter session programmed vs "
-                    "released, paired in --idle-power-rounds ABBA rounds (0 = off)")
+    ap.add_argument("--idle-power-s", type=float, default=48.0,
+                    help="phase P: seconds per condition (session programmed / released / parked by the quiet "
+                    "release) of an idle GPU, in --idle-power-rounds rounds of every order (0 = off)")
     ap.add_argument("--idle-power-rounds", type=int, default=6)
     ap.add_argument("--component-s", type=float, default=1.0,
                     help="phase K: seconds each load component runs alone while the exporter samples (0 = off)")

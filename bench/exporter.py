@@ -41,6 +41,21 @@ class ExporterCtl:
         self.sc.get("/control/pmc/acquire")
         return self._wait_pmc(True)
 
+    def set_quiet_release(self, secs: float) -> float:
+        """--pmc-quiet-release-s in place (secs < 0 only reads it)."""
+        q = f"?s={secs:g}" if secs >= 0 else ""
+        return json.loads(self.sc.get("/control/pmc/quiet_release" + q)).get("pmc_quiet_release_s", 0.0)
+
+    def wait_parked(self, timeout: float = 10.0) -> bool:
+        """Every GPU's counter session released for quiet (kgs_pmc_parked 1)."""
+        end = time.time() + timeout
+        while time.time() < end:
+            st = {lb["gpu"]: v for lb, v in parse_text(self.sc.get()).get("kgs_pmc_parked", [])}
+            if st and all(v == 1 for v in st.values()):
+                return True
+            time.sleep(0.05)
+        return False
+
 
 class AttachedExporter(ExporterCtl):
     """An already-running exporter (``--control-http``) driven over HTTP."""

@@ -52,35 +52,52 @@ def quiet_gpu(ctx, load, exp, a) -> dict:
 
 
 def idle_power(ctx, load, exp, a) -> dict:
-    """Phase P (untimed) — what the counter session costs an idle GPU in power (VERDICT
-    r5 #5).  With every rank's GPU idle, --idle-power-s of blocks with the exporter
-    running at its defaults (the quiet GPU READ at --pmc-idle-hz, the perfmon session
-    programmed, the READ queue mapped) alternate (ABBA) with blocks where the counter
-    session is released and the READ queue destroyed while the PMFW and slow tiers keep
-    sampling — what an exporter that dropped its session on a quiet GPU would leave.
+    """Phase P (untimed) — what the counter session costs an idle GPU in power, and what
+    the quiet release saves.  With every rank's GPU idle, three
+    conditions in blocks of --idle-power-s / --idle-power-rounds each, the block order
+    cycling through every permutation:
+
+    * ``session``  — the counter session programmed and the quiet GPU READ at
+      --pmc-idle-hz (the exporter as rounds 1-5 shipped it: quiet release off);
+    * ``released`` — the session STOPped and the READ queue destroyed while the PMFW and
+      slow tiers keep sampling (the neutral base);
+    * ``parked``   — the exporter's quiet release (--pmc-quiet-release-s, here 1 s)
+      having released the session by itself.
+
     Each rank reads its own GPU's socket power from the PMFW energy accumulator at the
-    block edges (PmfwProbe, not the exporter); the paired difference per round is the
-    session's idle cost, mean ± 95 % CI (``summary.quiet_gpu.power_w_session``)."""
+    block edges (PmfwProbe, not the exporter); per round, each condition is paired with
+    that round's ``released`` block: mean ± 95 % CI (``summary.quiet_gpu.power_w``)."""
     secs = float(getattr(a, "idle_power_s", 0.0) or 0.0)
     rounds = int(getattr(a, "idle_power_rounds", 6) or 0)
     if secs <= 0 or rounds <= 0 or a.mock:
         return {}
+    import itertools
+
     block = secs / rounds
     probe = PmfwProbe(load.pci_bdf(ctx.local_rank))
     if probe.N is None:
         return {"skipped": "no PMFW table probe"}
+    conds = ("session", "released", "parked")
+    perms = list(itertools.permutations(conds))
     D.cpu_barrier(ctx)
     load.sync()
+    default_qr = exp.set_quiet_release(-1) if ctx.local_rank == 0 and exp is not None else 0.0
     local: list[dict] = []
+    parked_ok = True
     for r in range(rounds):
-        order = ("session", "released") if r % 2 == 0 else ("released", "session")
         row: dict = {}
-        for cond in order:
+        for cond in perms[r % len(perms)]:
             if ctx.local_rank == 0 and exp is not None:
                 if cond == "released":
+                    exp.set_quiet_release(0)
                     exp.release(drop_queue=True)
-                else:
+                elif cond == "session":
+                    exp.set_quiet_release(0)
                     exp.acquire()
+                else:
+                    exp.set_quiet_release(1.0)
+                    exp.acquire()
+                    parked_ok &= exp.wait_parked(10.0)
             D.cpu_barrier(ctx)
             time.sleep(min(1.0, 0.2 * block))  # settle: the power-state change after the switch
             p0 = probe.read()
@@ -89,26 +106,30 @@ def idle_power(ctx, load, exp, a) -> dict:
             D.cpu_barrier(ctx)
         local.append(row)
     if ctx.local_rank == 0 and exp is not None:
+        exp.set_quiet_release(default_qr)
         exp.acquire()
     ranks = D.all_gather_object(ctx, local)
     per_rank = []
     for rk in ranks:
-        pairs = [(rd["session"]["power_w"], rd["released"]["power_w"]) for rd in rk
-                 if rd.get("session") and rd.get("released")]
-        if not pairs:
-            per_rank.append(None)
-            continue
-        m, ci, sd = mean_ci95([s - r for s, r in pairs])
-        per_rank.append({"session_w": round(sum(s for s, _ in pairs) / len(pairs), 2),
-                         "released_w": round(sum(r for _, r in pairs) / len(pairs), 2),
-                         "session_minus_released_w": round(m, 3), "ci95_w": round(ci, 3), "sd_w": round(sd, 3),
-                         "rounds": len(pairs)})
-    ok = [p for p in per_rank if p]
-    out = {"secs_per_condition": secs, "rounds": rounds, "block_s": round(block, 2),
-           "conditions": {"session": "exporter defaults: quiet GPU READ at --pmc-idle-hz, session programmed",
-                          "released": "counter session STOPped and READ queue destroyed; PMFW / slow tiers sampling"},
+        one: dict = {}
+        for cond in conds:
+            ws = [rd[cond]["power_w"] for rd in rk if rd.get(cond)]
+            if ws:
+                one[f"{cond}_w"] = round(sum(ws) / len(ws), 2)
+        for cond in ("session", "parked"):
+            d = [rd[cond]["power_w"] - rd["released"]["power_w"] for rd in rk if rd.get(cond) and rd.get("released")]
+            if d:
+                m, ci, sd = mean_ci95(d)
+                one[f"{cond}_minus_released_w"] = [round(m, 3), round(ci, 3)]
+        per_rank.append(one)
+    out = {"secs_per_condition": secs, "rounds": rounds, "block_s": round(block, 2), "parked_reached": parked_ok,
+           "conditions": {"session": "counter session programmed, quiet GPU READ at --pmc-idle-hz, no quiet release",
+                          "released": "session STOPped and READ queue destroyed; PMFW / slow tiers sampling",
+                          "parked": "the exporter's quiet release (1 s here) released the session by itself"},
            "per_rank": per_rank}
-    if ok:
-        out["session_minus_released_w"] = round(sum(p["session_minus_released_w"] for p in ok) / len(ok), 3)
-        out["ci95_w"] = round(max(p["ci95_w"] for p in ok), 3)
+    for cond in ("session", "parked"):
+        k = f"{cond}_minus_released_w"
+        vals = [p[k] for p in per_rank if k in p]
+        if vals:
+            out[k] = [round(sum(v[0] for v in vals) / len(vals), 3), round(max(v[1] for v in vals), 3)]
     return out

@@ -74,9 +74,10 @@ def summarize(res: dict) -> dict:
                                 _r(max(x.get("pmfw_gfx_busy_pct", 0) for x in v.get("per_gpu", {}).values()), 2)]
                             for m, v in q.items() if v.get("per_gpu")}
         ip = q.get("idle_power") or {}
-        if "session_minus_released_w" in ip:  # phase P: [session − released W, ± 95 %, released W]
-            out["quiet_gpu"]["power_w_session"] = [ip["session_minus_released_w"], ip.get("ci95_w"),
-                                                   (ip["per_rank"][0] or {}).get("released_w")]
+        if "session_minus_released_w" in ip:  # phase P: W above released (± 95 %), and the released W
+            out["quiet_gpu"]["power_w"] = {"session": ip["session_minus_released_w"],
+                                           "parked": ip.get("parked_minus_released_w"),
+                                           "released": (ip["per_rank"][0] or {}).get("released_w")}
     br = (res.get("burst_resolution") or {}).get("per_gpu") or {}
     if br:
         out["bursts_resolved"] = [sum(v.get("segments", 0) for v in br.values()), sum(v.get("launched", 0) for v in br.values())]

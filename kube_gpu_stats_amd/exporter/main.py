@@ -79,6 +79,11 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                        "(0 = every tick: profiling mode)")
     add_flag(ap, "pmc-dispatch-hz", 500.0, "counter READ rate in a dispatch-bound stream (--pmc-cp-only-min): a "
                                             "µs-kernel stream pays +0.5 %% at 1 kHz, +4 %% at 8 kHz (profiles/r4/ r4d)")
+    add_flag(ap, "pmc-quiet-release-s", 30.0, "release the counter session (STOP, READ queue destroyed) after the "
+                                               "GPU has been quiet this long, and bill it from the PMFW until the PMFW "
+                                               "shows GFX busy again: the session costs an idle MI355X ≈23 W "
+                                               "(bench phase P, r6b).  0 = never; ignored with --sm-util-source "
+                                               "counters and in profiling mode")
     add_flag(ap, "pmc-cp-only-min", 0.3, "dispatch-bound READ rate: while the command processor dispatches with no "
                                          "wave in flight for at least this share of the clocks (a stream of µs "
                                          "kernels, which each READ packet slows by a fixed CP cost), READ at "
@@ -192,6 +197,7 @@ def config_from_args(a) -> dict:
         "pmc_refresh_s": a.pmc_refresh_s,
         "pmc_idle_hz": a.pmc_idle_hz,
         "pmc_dispatch_hz": a.pmc_dispatch_hz,
+        "pmc_quiet_release_s": 0.0 if a.sm_util_source == "counters" else a.pmc_quiet_release_s,
         "pmc_cp_only_min": a.pmc_cp_only_min,
         "pmc_dispatch_hold_s": a.pmc_dispatch_hold_ms * 1e-3,
         "pmc_timeout_ms": a.pmc_timeout_ms,

@@ -268,6 +268,12 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_dispatch_bound", "gauge", "1 while the command processor dispatched with no wave in flight for at "
       "least --pmc-cp-only-min of the clocks for --pmc-dispatch-hold-ms (a stream of µs kernels, which each READ "
       "packet slows): READs drop to --pmc-dispatch-hz.", source="self"),
+    F("kgs_pmc_parked", "gauge", "1 while the counter session is released because the GPU has been quiet for "
+      "--pmc-quiet-release-s (no wave, no MFMA cycle): a programmed session and its READ queue keep an idle MI355X "
+      "out of its low-power state (+22.7 W per idle GPU, bench phase P).  Utilisation is billed from the PMFW GFX "
+      "busy meanwhile (no READ inflates it), and the counter-tier gauges are withheld; the session is re-acquired "
+      "as soon as one PMFW interval shows GFX busy.", source="self"),
+    F("kgs_pmc_parks_total", "counter", "Quiet releases of the counter session (kgs_pmc_parked).", source="self"),
     F("kgs_pmc_dispatch_skips_total", "counter", "Sampler ticks that skipped their counter READ in a dispatch-bound "
       "stream.", source="self"),
     F("kgs_pmc_failed", "gauge", "1 while the counter tier's circuit breaker is open: --pmc-breaker-k consecutive "

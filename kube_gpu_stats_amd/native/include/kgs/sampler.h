@@ -108,6 +108,16 @@ struct SamplerConfig {
   double pmc_cp_only_min = 0.3;
   double pmc_dispatch_hold_s = 0.010;
   double pmc_dispatch_hz = 500.0;
+  // Quiet release ("parking").  A programmed perfmon session and a mapped READ queue
+  // keep an idle MI355X out of its low-power state: +22.7 ± 11.1 W per idle GPU with
+  // the session and its 100 Hz quiet READs against the session released (r6b, bench
+  // phase P).  After the device has been quiet (no wave, no MFMA cycle) for this long,
+  // its counter thread STOPs the session and destroys the READ queue; it re-acquires
+  // when the PMFW table shows GFX busy again (≥ kUnparkBusyPct over one distinct
+  // PMFW interval), on a control-plane acquire, or on a refresh.  In between the
+  // READ-immune utilisation is billed from the PMFW GFX busy — which no READ inflates
+  // while parked.  0 = never (profiling mode never parks either).
+  double pmc_quiet_release_s = 0.0;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
   // Counter-tier circuit breaker: consecutive failed drains that open it, and the
@@ -131,6 +141,11 @@ constexpr double kMinIdleHz = 0.01;     // pmc_idle_hz: 0 (off) or at least this
 // window: at --pmc-idle-hz 0.01 that window is 300 s, and busy carried that long would
 // be billed into a later idle stretch — or a later pod.
 constexpr double kMaxUtilCarryS = 1.0;
+// A parked counter tier (SamplerConfig::pmc_quiet_release_s) re-acquires once one
+// distinct PMFW interval shows at least this GFX busy: an idle MI355X with nothing
+// READing it shows 0.07 % (r6b phase U, 10 Hz idle row); a 0.2 ms kernel in a 20 ms
+// table shows 1 %.
+constexpr double kUnparkBusyPct = 1.0;
 
 // The counter tick's dithered offset from its fixed grid (SamplerConfig::tick_dither): a
 // random walk of at most `dither` of a period per tick, reflected into ± half a period.
@@ -269,6 +284,10 @@ struct DeviceState {
   std::atomic<int> pmc_quiet{0};            // last READ interval had no wave: READs at pmc_idle_hz
   std::atomic<uint64_t> pmc_quiet_skips{0};  // ticks that skipped their READ while quiet
   std::atomic<int> pmc_dbound{0};            // dispatch-bound (pmc_cp_only_min): READs at pmc_dispatch_hz
+  std::atomic<int> pmc_parked{0};            // session released after pmc_quiet_release_s of quiet
+  std::atomic<uint64_t> pmc_parks{0};        // quiet releases
+  std::atomic<int> pmc_unpark_req{0};        // control plane: re-acquire a parked device now
+  std::atomic<int64_t> pmc_unpark_lag_ns{-1};  // last re-acquire: mono time since the PMFW sample that showed busy
   std::atomic<uint64_t> pmc_dbound_skips{0};  // ticks that skipped their READ while dispatch-bound
   // Counter-tier fault boundary (sampler.h header comment).
   std::atomic<int> pmc_failed{0};            // breaker open: no READs until a retry succeeds
@@ -380,6 +399,10 @@ class Sampler {
   // (unchanged) unless 0 < hz <= kMaxHz.
   bool set_pmc_dispatch_hz(double hz);
   double pmc_dispatch_hz() const { return pmc_dispatch_hz_.load(std::memory_order_relaxed); }
+  // Quiet-release delay (SamplerConfig::pmc_quiet_release_s), in place; 0 = never park.
+  // false (unchanged) unless 0 <= s <= 86400.
+  bool set_pmc_quiet_release_s(double s);
+  double pmc_quiet_release_s() const { return pmc_quiet_release_s_.load(std::memory_order_relaxed); }
   // Slow-tier passes completed (all devices).
   uint64_t slow_passes() const { return slow_passes_.load(); }
   // Test hook: the device's counter thread wedges its reader's queue
@@ -427,6 +450,7 @@ class Sampler {
   std::atomic<uint64_t> slow_passes_{0};
   std::atomic<double> pmc_idle_hz_{0.0};
   std::atomic<double> pmc_dispatch_hz_{500.0};
+  std::atomic<double> pmc_quiet_release_s_{0.0};
   mutable std::mutex pid_pods_mu_;
   std::shared_ptr<const std::unordered_map<uint64_t, std::string>> pid_pods_;
   std::vector<std::map<std::string, double>> pod_cu_;  // device's slow thread only

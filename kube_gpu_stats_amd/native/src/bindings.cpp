@@ -87,6 +87,7 @@ ExporterConfig parse_config(const py::dict& d) {
   c.sampler.pmc_refresh_s = get<double>(d, "pmc_refresh_s", c.sampler.pmc_refresh_s);
   c.sampler.pmc_idle_hz = get<double>(d, "pmc_idle_hz", c.sampler.pmc_idle_hz);
   c.sampler.pmc_dispatch_hz = get<double>(d, "pmc_dispatch_hz", c.sampler.pmc_dispatch_hz);
+  c.sampler.pmc_quiet_release_s = get<double>(d, "pmc_quiet_release_s", c.sampler.pmc_quiet_release_s);
   c.sampler.pmc_cp_only_min = get<double>(d, "pmc_cp_only_min", c.sampler.pmc_cp_only_min);
   c.sampler.pmc_dispatch_hold_s = get<double>(d, "pmc_dispatch_hold_s", c.sampler.pmc_dispatch_hold_s);
   c.sampler.devices = get<std::vector<int>>(d, "devices", c.sampler.devices);
@@ -286,6 +287,12 @@ class PyExporter {
     o["pmc_quiet"] = st.pmc_quiet.load();
     o["pmc_quiet_skips"] = st.pmc_quiet_skips.load();
     o["pmc_dispatch_skips"] = st.pmc_dbound_skips.load();
+    o["pmc_parked"] = st.pmc_parked.load();
+    o["pmc_parks"] = st.pmc_parks.load();
+    {
+      const int64_t lag = st.pmc_unpark_lag_ns.load();
+      o["pmc_unpark_lag_s"] = lag >= 0 ? py::cast(lag * 1e-9) : py::none();
+    }
     o["pmc_dispatch_bound"] = st.pmc_dbound.load();
     o["up"] = ex_.sampler()->state(d).up.load();
     o["cpu_pinned"] = ex_.sampler()->state(d).cpu_pinned.load();
@@ -537,6 +544,14 @@ PYBIND11_MODULE(_kgs_native, m) {
               throw py::value_error("pmc_dispatch_hz must be within (0, 100000]");
           },
           "Counter READ rate while the CP dispatches with no wave in flight (--pmc-cp-only-min)")
+      .def_property(
+          "pmc_quiet_release_s",
+          [](const PyExporter& e) { return e.sampler() ? e.sampler()->pmc_quiet_release_s() : 0.0; },
+          [](PyExporter& e, double v) {
+            if (e.sampler() && !e.sampler()->set_pmc_quiet_release_s(v))
+              throw py::value_error("pmc_quiet_release_s must be within [0, 86400]");
+          },
+          "Seconds of quiet before the counter session is released (parked); 0 = never")
       .def_property_readonly("slow_passes", &PyExporter::slow_passes);
   // The utilisation estimators as pure units (util_estimator.h): the offline replay of
   // raw READ dumps runs the sampler's own code.

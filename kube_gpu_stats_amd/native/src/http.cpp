@@ -361,6 +361,16 @@ void HttpServer::loop() {
             respond(c, 200, "OK", "application/json",
                     "{\"pmc_dispatch_hz\":" + std::to_string(s ? s->pmc_dispatch_hz() : 0.0) + "}");
           }
+        } else if (target == "/control/pmc/quiet_release") {
+          // Quiet-release delay (--pmc-quiet-release-s); s=0 never parks; no s only reads it.
+          Sampler* s = ex_->sampler();
+          const double v = query_double(query, "s", -1.0);
+          if (s && v != -1.0 && !s->set_pmc_quiet_release_s(v)) {
+            respond(c, 400, "Bad Request", "text/plain", "s must be within [0, 86400]\n");
+          } else {
+            respond(c, 200, "OK", "application/json",
+                    "{\"pmc_quiet_release_s\":" + std::to_string(s ? s->pmc_quiet_release_s() : 0.0) + "}");
+          }
         } else if (ex_->config().control_http && (target == "/control/pause" || target == "/control/resume")) {
           if (target == "/control/pause") ex_->pause_sampling();
           else ex_->resume_sampling();

@@ -755,6 +755,10 @@ void Exporter::render(std::string& out) {
     w.head(KGS_METRIC_DOC("kgs_pmc_dispatch_bound"));
     for (int d : ids)
       w.line_u("kgs_pmc_dispatch_bound", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_dbound.load()));
+    w.head(KGS_METRIC_DOC("kgs_pmc_parked"));
+    for (int d : ids) w.line_u("kgs_pmc_parked", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_parked.load()));
+    w.head(KGS_METRIC_DOC("kgs_pmc_parks_total"));
+    for (int d : ids) w.line_u("kgs_pmc_parks_total", dev_labels_[d], nullptr, S.state(d).pmc_parks.load());
     w.head(KGS_METRIC_DOC("kgs_pmc_dispatch_skips_total"));
     for (int d : ids) w.line_u("kgs_pmc_dispatch_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_dbound_skips.load());
     w.head(KGS_METRIC_DOC("kgs_pmc_failed"));

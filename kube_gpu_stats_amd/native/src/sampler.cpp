@@ -121,6 +121,7 @@ Sampler::Sampler(Backend* be, CounterSource* pmc, SamplerConfig cfg) : be_(be), 
   const double ih = cfg_.pmc_idle_hz;
   pmc_idle_hz_.store(!(ih > 0) ? 0.0 : std::clamp(ih, kMinIdleHz, kMaxHz));
   if (!set_pmc_dispatch_hz(cfg_.pmc_dispatch_hz)) set_pmc_dispatch_hz(500.0);
+  if (!set_pmc_quiet_release_s(cfg_.pmc_quiet_release_s)) set_pmc_quiet_release_s(0.0);
   if (!(cfg_.pmc_cp_only_min >= 0 && cfg_.pmc_cp_only_min <= 1)) cfg_.pmc_cp_only_min = 0.0;
   if (!(cfg_.pmc_dispatch_hold_s >= 0)) cfg_.pmc_dispatch_hold_s = 0.0;
   for (int d : dev_ids_) {
@@ -177,11 +178,18 @@ bool Sampler::set_pmc_dispatch_hz(double hz) {
   return true;
 }
 
+bool Sampler::set_pmc_quiet_release_s(double v) {
+  if (!(v >= 0 && v <= 86400)) return false;
+  pmc_quiet_release_s_.store(v, std::memory_order_relaxed);
+  return true;
+}
+
 void Sampler::set_pmc_wanted(bool on, int dev, bool drop_queue) {
   for (int d : dev_ids_)
     if (dev < 0 || d == dev) {
       DeviceState& st = *states_[static_cast<size_t>(d)];
       if (!on && drop_queue) st.pmc_drop_queue.store(1);
+      if (on) st.pmc_unpark_req.store(1);  // an explicit acquire also ends a quiet release
       st.pmc_want.store(on ? 1 : 0);
     }
 }
@@ -592,6 +600,9 @@ void Sampler::run_pmc(Worker& w) {
   bool fresh_mode = false;           // reader switched to synchronous READs (quiet at the idle rate)
   int64_t last_pmc_ns = 0;
   int64_t last_start_ns = mono_ns();  // last (re)START of the counter session
+  int64_t quiet_run_ns = 0;          // start of the current run of quiet drains (quiet release)
+  int64_t park_ns = 0;               // when the session was last released for quiet
+  int64_t unpark_retry_at_ns = 0;    // after a failed re-acquire of a parked device
   // A fresh START restarts every count at 0: the interval from START to the first
   // READ is then counted exactly (acquire → first READ was dropped).
   auto started_at = [&](int64_t t) {
@@ -639,12 +650,48 @@ void Sampler::run_pmc(Worker& w) {
       // as a base so the exported counters stay monotonic.
       carry_base();
     }
+    if (!want && st.pmc_parked.load(std::memory_order_relaxed)) {
+      st.pmc_parked.store(0);  // handed over while parked: nothing is held, the hand-over stands
+      st.pmc_releases.fetch_add(1, std::memory_order_relaxed);
+    }
     if (!want && st.pmc_drop_queue.exchange(0)) {  // "released": no queue left mapped either
       src->reset(dev);
       if (gone()) return;
     }
+    // ---- quiet release ended: PMFW busy again, or the control plane asked -----
+    if (want && st.pmc_parked.load(std::memory_order_relaxed) && mono_ns() >= unpark_retry_at_ns) {
+      bool wake = st.pmc_unpark_req.exchange(0, std::memory_order_relaxed) != 0;
+      int64_t busy_ns = 0;
+      GpuSample g;
+      // A distinct PMFW interval read after the release settled (the STOP and the queue
+      // teardown are CP work of their own) that shows GFX busy.
+      if (!wake && st.latest.load(g) && g.mono_ns > park_ns + 50000000LL && g.gfx_busy_window_pct >= kUnparkBusyPct) {
+        wake = true;
+        busy_ns = g.mono_ns;
+      }
+      if (wake) {
+        const int rc = src->acquire(dev);
+        if (gone()) return;
+        const int64_t now_c = mono_ns();
+        if (rc == 0) {
+          ++P.pmc_epoch;
+          st.pmc_on.store(1);
+          st.pmc_parked.store(0);
+          started_at(now_c);
+          src->set_fresh(dev, false);  // the released session was READ synchronously (quiet)
+          if (gone()) return;
+          quiet_run_ns = 0;
+          if (busy_ns) st.pmc_unpark_lag_ns.store(now_c - busy_ns, std::memory_order_relaxed);
+        } else {
+          ++P.pmc_errors;
+          unpark_retry_at_ns = now_c + 1000000000LL;  // stays parked (PMFW billing); retry ≤ 1/s
+        }
+      }
+    }
+    st.pmc_unpark_req.store(0, std::memory_order_relaxed);  // only meaningful while parked
     // ---- (re)acquire: after a hand-over, or a retry of an open breaker --------
-    if (want && !st.pmc_on.load(std::memory_order_relaxed) && mono_ns() >= st.pmc_retry_at_ns) {
+    if (want && !st.pmc_on.load(std::memory_order_relaxed) && !st.pmc_parked.load(std::memory_order_relaxed) &&
+        mono_ns() >= st.pmc_retry_at_ns) {
       const bool failed = st.pmc_failed.load() != 0;
       if (failed) {  // wedged before: drop the old queue, then START on a fresh one
         st.pmc_retries.fetch_add(1, std::memory_order_relaxed);
@@ -719,6 +766,14 @@ void Sampler::run_pmc(Worker& w) {
         P.pmc_clk_busy_hz = est.clk_busy_hz();
         st.pmc_quiet.store(r.quiet ? 1 : 0, std::memory_order_relaxed);
         st.pmc_dbound.store(r.dbound ? 1 : 0, std::memory_order_relaxed);
+        {  // quiet release: how long the device has been quiet, READ at the idle rate
+          const double qr = pmc_quiet_release_s_.load(std::memory_order_relaxed);
+          if (r.quiet && qr > 0 && pmc_idle_hz_.load(std::memory_order_relaxed) > 0) {
+            if (quiet_run_ns == 0) quiet_run_ns = ps.mono_ns;
+          } else {
+            quiet_run_ns = 0;
+          }
+        }
         {
           const double idle_hz = pmc_idle_hz_.load(std::memory_order_relaxed);
           const bool slow = r.quiet && idle_hz > 0 && idle_hz < hz;
@@ -769,6 +824,29 @@ void Sampler::run_pmc(Worker& w) {
             est.invalidate(t);
             last_start_ns = t;
           }
+        }
+        const double qr = pmc_quiet_release_s_.load(std::memory_order_relaxed);
+        if (quiet_run_ns && qr > 0 && st.pmc_on.load(std::memory_order_relaxed) &&
+            st.pmc_want.load(std::memory_order_relaxed) && ps.mono_ns - quiet_run_ns >= static_cast<int64_t>(qr * 1e9)) {
+          // Park: STOP the session and destroy the READ queue (nothing of the counter
+          // tier left on the GPU); totals carry over like a hand-over, and the billing
+          // falls back to the PMFW at the epoch change.
+          ++P.pmc_epoch;
+          carry_base();
+          src->release(dev);
+          if (gone()) return;
+          src->reset(dev);
+          if (gone()) return;
+          park_ns = mono_ns();
+          st.pmc_on.store(0);
+          st.pmc_parked.store(1);
+          st.pmc_parks.fetch_add(1, std::memory_order_relaxed);
+          st.pmc_quiet.store(0, std::memory_order_relaxed);
+          st.pmc_dbound.store(0, std::memory_order_relaxed);
+          st.pmc_unpark_req.store(0, std::memory_order_relaxed);
+          quiet_run_ns = 0;
+          fresh_mode = false;
+          est.invalidate(park_ns);
         }
       } else if (prc == kPmcPending) {
         // A batched reader's first READs are not published yet: nothing to fold.

@@ -961,3 +961,47 @@ def test_counter_stream_marks_stale_drains_and_rates_mfma_between_fresh_ones(moc
     mf = [x["mfma_util_pct"] for x in fresh if "mfma_util_pct" in x]
     assert len(mf) >= len(fresh) - 1  # the first one has its base: the ring is read past it
     assert sum(mf) / len(mf) == pytest.approx(60, abs=3) and min(mf) > 40 and max(mf) < 80, mf
+
+
+def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
+    """a programmed counter session keeps an idle MI355X ≈23 W above its
+    released state (bench phase P, profiles/r6/r6b).  With --pmc-quiet-release-s the
+    counter thread releases the session (STOP + READ queue destroyed) once the GPU has
+    been quiet that long, bills from the PMFW meanwhile, and re-acquires within one PMFW
+    interval of the PMFW showing GFX busy.  A 50 % square wave (1.5 s at 100 %, 1.5 s
+    idle): every idle half parks, every busy half unparks, and the billed integral over
+    whole periods is the wave's 50 % — as without parking."""
+    import urllib.request
+
+    kw = dict(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100,
+              mock={"util_base": 50, "util_amp": 50, "square_duty": 0.5, "util_period_s": 3.0, "fw_period_s": 0.02})
+    ex = mock_exporter(pmc_quiet_release_s=0.3, **kw)
+    ref = mock_exporter(pmc_quiet_release_s=0.0, **kw)
+    time.sleep(0.5)
+    a, r0, t0 = ex.integrals(0), ref.integrals(0), time.monotonic()
+    parked_seen = on_seen = 0
+    while time.monotonic() - t0 < 6.0:
+        i = ex.integrals(0)
+        parked_seen |= i["pmc_parked"]
+        on_seen |= i["pmc_on"] and not i["pmc_parked"]
+        time.sleep(0.05)
+    b, r1 = ex.integrals(0), ref.integrals(0)
+    assert parked_seen and on_seen
+    assert b["pmc_parks"] - a["pmc_parks"] >= 2, b          # one per idle half
+    assert b["pmc_unpark_lag_s"] is not None and b["pmc_unpark_lag_s"] < 0.05, b  # ≤ one 20 ms table + a poll
+    billed = (b["util_seconds"] - a["util_seconds"]) / (b["sampled_seconds"] - a["sampled_seconds"])
+    billed_ref = (r1["util_seconds"] - r0["util_seconds"]) / (r1["sampled_seconds"] - r0["sampled_seconds"])
+    assert billed == pytest.approx(billed_ref, abs=0.02) and billed == pytest.approx(0.5, abs=0.05), (billed, billed_ref)
+    assert ref.integrals(0)["pmc_parks"] == 0
+    m = parse_text(ex.render())
+    assert m["kgs_pmc_parks_total"][0][1] >= 2 and "kgs_pmc_parked" in m
+    # the control plane: read / set the delay; an acquire ends a park at once
+    with urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/quiet_release?s=0.1", timeout=5) as resp:
+        assert json.load(resp) == {"pmc_quiet_release_s": 0.1}
+    for bad in ("s=-5", "s=1e9"):
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/control/pmc/quiet_release?{bad}", timeout=5)
+        assert e.value.code == 400, bad
+    with pytest.raises(ValueError):
+        ex.pmc_quiet_release_s = -2
+    assert ex.pmc_quiet_release_s == pytest.approx(0.1)
