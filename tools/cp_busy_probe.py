@@ -182,7 +182,10 @@ def main(argv=None) -> int:
 
     out: dict = {"counters": NAMES, "rates": {}, "pipelined": a.pipelined}
     dumps: dict = {}
-    total = len(names) * (a.secs + 0.6) + 2.0
+    # the profiler-timed training step returns seconds after its last kernel (trace
+    # post-processing): the reader must outlive every load's window, or the replay
+    # compares busy over a short READ span with the duty over the whole window
+    total = len(names) * (a.secs + 0.6) + 2.0 + (30.0 if a.irregular else 0.0)
     for hz in [float(x) for x in a.rates.split(",")]:
         p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", str(hz), "--child-secs",
                               str(total), "--pipelined", str(a.pipelined), "--batch", str(a.batch), "--lite", str(a.lite),

@@ -121,7 +121,7 @@ for s in $STEPS; do
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke ;;
-    bench) run bench 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" ;;
+    bench) run bench 900 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" ;;
     bench2) run bench_b 600 python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench_b.json" ;;
     rocprof) run rocprof 1000 bash tools/gpu_rocprof.sh "$OUT/rocprof" ;;
   esac
