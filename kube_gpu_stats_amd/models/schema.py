@@ -268,6 +268,10 @@ CATALOG: tuple[Family, ...] = (
     F("kgs_pmc_dispatch_bound", "gauge", "1 while the command processor dispatched with no wave in flight for at "
       "least --pmc-cp-only-min of the clocks for --pmc-dispatch-hold-ms (a stream of µs kernels, which each READ "
       "packet slows): READs drop to --pmc-dispatch-hz.", source="self"),
+    F("kgs_process_cu_unavailable", "gauge", "Processes on the GPU whose CU occupancy could not be read in the last "
+      "per-process pass (their KFD stats are gone: a process tearing down).  Their amdgpu_process_cu_occupancy line "
+      "is withheld and nothing is integrated for them; a pod whose CU-seconds are all unknown gets no "
+      "container_gpu_cu_seconds_total line rather than 0.", source="self"),
     F("kgs_pmc_parked", "gauge", "1 while the counter session is released because the GPU has been quiet for "
       "--pmc-quiet-release-s (no wave, no MFMA cycle): a programmed session and its READ queue keep an idle MI355X "
       "out of its low-power state (+22.7 W per idle GPU, bench phase P).  Utilisation is billed from the PMFW GFX "

@@ -178,7 +178,8 @@ def build_tsan_test(verbose: bool = False, sanitizer: str = "thread") -> str:
     out = os.path.join(HERE, "build", f"test_core_{tag}")
     srcs = [os.path.join(HERE, "tests", "test_core.cpp")] + [
         os.path.join(HERE, "src", f) for f in ("sampler.cpp", "backend_mock.cpp", "pmc.cpp", "gpu_metrics.cpp", "util.cpp",
-                                              "exporter.cpp", "render.cpp", "http.cpp", "backend_amdsmi.cpp")]
+                                              "exporter.cpp", "render.cpp", "http.cpp", "backend_amdsmi.cpp",
+                                              "kfd_procs.cpp")]
     objdir = os.path.join(HERE, "build", f"obj_{tag}")
     os.makedirs(objdir, exist_ok=True)
     metric_help_header()

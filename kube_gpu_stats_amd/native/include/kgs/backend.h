@@ -47,6 +47,9 @@ struct ProcInfo {
   uint64_t vram_bytes = 0, gtt_bytes = 0, cpu_bytes = 0;
   uint64_t gfx_ns = 0;         // cumulative engine time (if the driver reports it)
   uint32_t cu_occupancy = 0;   // CUs in use by the process' waves
+  // cu_occupancy was read (false: its KFD stats are unreadable — a process tearing down;
+  // the sampler neither integrates nor exports it, kgs_process_cu_unavailable counts it)
+  bool cu_valid = true;
   uint32_t evicted_ms = 0;
   // ∫ cu_occupancy / num_cu dt, integrated by the sampler across reads: ROCm compute
   // runs on user-mode queues the driver does not time (gfx_ns reads 0 on MI355X), so
@@ -149,6 +152,9 @@ struct MockConfig {
   // (empty: 1 + dev % 2 processes at half the CUs each).  Two tenants sharing one
   // GPU with shares {0.6, 0.0} is the shared-GPU billing test.
   std::vector<double> proc_cu_share;
+  // Process k of every device whose CU occupancy cannot be read (ProcInfo::cu_valid
+  // false), as for a process tearing down; -1 = none.
+  int proc_cu_fail = -1;
   // Background xGMI traffic on every link, following the util curve (1 GB/s per
   // link at 100 %); off, only inject_xgmi() moves the link accumulators.
   bool xgmi_bg = true;

@@ -42,6 +42,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <set>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -260,6 +261,9 @@ struct DeviceState {
   // Per-pod CU-occupancy seconds on this GPU ("namespace/pod" → ∫ Σ share dt of the
   // pod's processes), processes that exited included (slow tier).
   std::shared_ptr<const std::map<std::string, double>> pod_cu;
+  // Pods ("namespace/pod") with a process whose CU occupancy could not be read in the
+  // last per-process pass (ProcInfo::cu_valid false): their CU-seconds are unknown.
+  std::shared_ptr<const std::set<std::string>> pod_cu_unknown;
   int64_t procs_mono_ns = 0;
 
   std::atomic<int> up{0};
@@ -318,6 +322,7 @@ struct DeviceState {
   bool have_pmfw_prev = false;
   // Slow-thread self metrics: completed passes and their latency per tier.
   std::atomic<uint64_t> proc_reads{0}, proc_errors{0}, link_reads{0};
+  std::atomic<int> procs_cu_unavailable{0};  // processes of the last pass whose CU occupancy was unreadable
   std::atomic<uint64_t> slow_ns_total{0};
 
   std::shared_ptr<const std::vector<ProcInfo>> get_procs() const {
@@ -335,6 +340,10 @@ struct DeviceState {
   std::shared_ptr<const std::map<std::string, double>> get_pod_cu() const {
     std::lock_guard<std::mutex> g(slow_mu);
     return pod_cu;
+  }
+  std::shared_ptr<const std::set<std::string>> get_pod_cu_unknown() const {
+    std::lock_guard<std::mutex> g(slow_mu);
+    return pod_cu_unknown;
   }
   // Both tiers' integrals in one view (overruns: both threads').
   Integrals integrals() const {

@@ -17,6 +17,7 @@
 
 #include "kgs/backend.h"
 #include "kgs/gpu_metrics.h"
+#include "kgs/kfd_procs.h"
 
 namespace kgs {
 
@@ -150,6 +151,11 @@ class AmdSmiBackend final : public Backend {
 
   int read_procs(int d, std::vector<ProcInfo>& out) override {
     out.clear();
+    // The KFD's own per-process files first: no queue walk, no stdout message, no AMD
+    // SMI lock, and a per-process flag when the CU occupancy cannot be read
+    // (kgs/kfd_procs.h).  AMD SMI only where the KFD sysfs cannot be listed.
+    const DeviceInfo& in = devs_[d]->info;
+    if (in.kfd_gpu_id && read_kfd_procs(kKfdProcRoot, "/proc", in.kfd_gpu_id, in.bdf, out) == 0) return 0;
     std::vector<amdsmi_proc_info_t> list;
     uint32_t cap = 0;
     {
@@ -176,6 +182,13 @@ class AmdSmiBackend final : public Backend {
       pi.cpu_bytes = p.memory_usage.cpu_mem;
       pi.gfx_ns = p.engine_usage.gfx;
       pi.cu_occupancy = p.cu_occupancy;
+      {  // AMD SMI reads a process's CU occupancy through its KFD queues directory and
+         // reports 0 when that is gone: unknown, not idle
+        char qp[96];
+        std::snprintf(qp, sizeof qp, "%s/%u/queues", kKfdProcRoot, p.pid);
+        pi.cu_valid = access(qp, R_OK | X_OK) == 0;
+        if (!pi.cu_valid) pi.cu_occupancy = 0;
+      }
       pi.evicted_ms = p.evicted_time;
       out.push_back(std::move(pi));
     }

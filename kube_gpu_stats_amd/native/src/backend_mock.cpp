@@ -283,6 +283,10 @@ class MockBackend final : public Backend {
       p.cu_occupancy = shares ? static_cast<uint32_t>(std::lround(cfg_.proc_cu_share[static_cast<size_t>(k)] *
                                                                   infos_[static_cast<size_t>(d)].num_cu))
                               : 128;
+      if (k == cfg_.proc_cu_fail) {  // its KFD stats unreadable (a process tearing down)
+        p.cu_valid = false;
+        p.cu_occupancy = 0;
+      }
       out.push_back(p);
     }
     return 0;

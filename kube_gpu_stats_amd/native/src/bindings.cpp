@@ -7,6 +7,7 @@
 
 #include "kgs/exporter.h"
 #include "kgs/gpu_metrics.h"
+#include "kgs/kfd_procs.h"
 
 namespace py = pybind11;
 using namespace kgs;
@@ -47,6 +48,7 @@ ExporterConfig parse_config(const py::dict& d) {
     c.mock.health_latency_s = get<double>(m, "health_latency_s", c.mock.health_latency_s);
     c.mock.metrics_latency_s = get<double>(m, "metrics_latency_s", c.mock.metrics_latency_s);
     c.mock.proc_cu_share = get<std::vector<double>>(m, "proc_cu_share", c.mock.proc_cu_share);
+    c.mock.proc_cu_fail = get<int>(m, "proc_cu_fail", c.mock.proc_cu_fail);
     c.mock.xgmi_bg = get<bool>(m, "xgmi_bg", c.mock.xgmi_bg);
     c.mock.xgmi_swap_dev = get<int>(m, "xgmi_swap_dev", c.mock.xgmi_swap_dev);
     c.mock.slow_fault_dev = get<int>(m, "slow_fault_dev", c.mock.slow_fault_dev);
@@ -368,6 +370,7 @@ class PyExporter {
       o["cpu_bytes"] = x.cpu_bytes;
       o["gfx_ns"] = x.gfx_ns;
       o["cu_occupancy"] = x.cu_occupancy;
+      o["cu_valid"] = x.cu_valid;
       o["cu_seconds"] = x.cu_seconds;
       o["evicted_ms"] = x.evicted_ms;
       l.append(o);
@@ -687,6 +690,29 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("drop_carry", &UtilBiller::drop_carry, "The GPU changed hands: drop the busy still carried");
   m.attr("MAX_UTIL_CARRY_S") = kMaxUtilCarryS;
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
+  m.def(
+      "read_kfd_procs",
+      [](const std::string& kfd_root, const std::string& proc_root, uint64_t gpu_id, const std::string& bdf) {
+        std::vector<ProcInfo> v;
+        if (read_kfd_procs(kfd_root, proc_root, gpu_id, bdf, v) != 0) return py::object(py::none());
+        py::list l;
+        for (const ProcInfo& x : v) {
+          py::dict o;
+          o["pid"] = x.pid;
+          o["name"] = x.name;
+          o["vram_bytes"] = x.vram_bytes;
+          o["gtt_bytes"] = x.gtt_bytes;
+          o["cpu_bytes"] = x.cpu_bytes;
+          o["gfx_ns"] = x.gfx_ns;
+          o["cu_occupancy"] = x.cu_occupancy;
+          o["cu_valid"] = x.cu_valid;
+          o["evicted_ms"] = x.evicted_ms;
+          l.append(o);
+        }
+        return py::object(l);
+      },
+      py::arg("kfd_root"), py::arg("proc_root"), py::arg("gpu_id"), py::arg("bdf"),
+      "The processes with a KFD context on gpu_id, from the KFD sysfs + DRM fdinfo (None: no KFD root)");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
   m.def("pmc_counter_names", [] {
     std::vector<std::string> v;

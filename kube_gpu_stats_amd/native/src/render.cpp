@@ -315,10 +315,21 @@ void Exporter::render(std::string& out) {
         if (!o) continue;
         const int d = pod_lines[i].first;
         auto pc = S.state(d).get_pod_cu();
+        const std::string key = o->ns + "/" + o->pod;
         double v = 0;
+        bool have = false;
         if (pc) {
-          auto it = pc->find(o->ns + "/" + o->pod);
-          if (it != pc->end()) v = it->second;
+          auto it = pc->find(key);
+          if (it != pc->end()) {
+            v = it->second;
+            have = true;
+          }
+        }
+        // A pod whose processes' CU occupancy could not be read has no CU-seconds yet:
+        // its line is withheld rather than billed 0 (kgs_process_cu_unavailable says why).
+        if (!have) {
+          auto uk = S.state(d).get_pod_cu_unknown();
+          if (uk && uk->count(key)) continue;
         }
         v -= o->base_cu_s;
         w.line("container_gpu_cu_seconds_total", pod_lines[i].second, nullptr, v > 0 ? v : 0.0);
@@ -706,7 +717,9 @@ void Exporter::render(std::string& out) {
     w.head(KGS_METRIC_DOC("amdgpu_process_gtt_bytes"));
     for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_gtt_bytes", plabels[i], nullptr, plist[i].second->gtt_bytes);
     w.head(KGS_METRIC_DOC("amdgpu_process_cu_occupancy"));
-    for (size_t i = 0; i < plist.size(); ++i) w.line_u("amdgpu_process_cu_occupancy", plabels[i], nullptr, plist[i].second->cu_occupancy);
+    for (size_t i = 0; i < plist.size(); ++i)  // an unreadable occupancy is unknown: no line, not 0
+      if (plist[i].second->cu_valid)
+        w.line_u("amdgpu_process_cu_occupancy", plabels[i], nullptr, plist[i].second->cu_occupancy);
     w.head(KGS_METRIC_DOC("amdgpu_process_gfx_seconds_total"));
     for (size_t i = 0; i < plist.size(); ++i) w.line("amdgpu_process_gfx_seconds_total", plabels[i], nullptr, plist[i].second->gfx_ns * 1e-9);
     w.head(KGS_METRIC_DOC("amdgpu_process_cu_seconds_total"));
@@ -810,6 +823,12 @@ void Exporter::render(std::string& out) {
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"procs\"", st.proc_errors.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"links\"", st.link_errors.load(std::memory_order_relaxed));
     w.line_u("kgs_slow_errors_total", dev_labels_[d], "tier=\"health\"", st.health_errors.load(std::memory_order_relaxed));
+  }
+  if (cfg_.per_process) {
+    w.head(KGS_METRIC_DOC("kgs_process_cu_unavailable"));
+    for (int d : ids)
+      w.line_u("kgs_process_cu_unavailable", dev_labels_[d], nullptr,
+               static_cast<uint64_t>(S.state(d).procs_cu_unavailable.load(std::memory_order_relaxed)));
   }
   w.head(KGS_METRIC_DOC("kgs_slow_last_ok_age_seconds"));
   for (int d : ids) {

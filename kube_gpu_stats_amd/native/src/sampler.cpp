@@ -951,10 +951,15 @@ void Sampler::run_slow(Worker& w) {
         bool pods_changed = false;
         std::vector<std::pair<uint32_t, double>> next_cs;
         next_cs.reserve(procs.size());
+        int unavailable = 0;
+        std::set<std::string> unknown_pods;
         for (ProcInfo& p : procs) {
           auto it = std::lower_bound(cs.begin(), cs.end(), std::make_pair(p.pid, -1.0));
           const bool known = it != cs.end() && it->first == p.pid;
-          const double inc = known ? p.cu_occupancy / ncu * dt : 0.0;
+          // An unreadable CU occupancy adds nothing, not 0 % of the interval: the
+          // process's integral stands still, and its pod is flagged.
+          const double inc = known && p.cu_valid ? p.cu_occupancy / ncu * dt : 0.0;
+          unavailable += !p.cu_valid;
           p.cu_seconds = known ? it->second + inc : 0.0;
           next_cs.emplace_back(p.pid, p.cu_seconds);
           // The pod's integral keeps what its processes ran after they exit: the
@@ -962,9 +967,13 @@ void Sampler::run_slow(Worker& w) {
           if (pid_pods) {
             auto po = pid_pods->find((static_cast<uint64_t>(static_cast<uint32_t>(dev)) << 32) | p.pid);
             if (po != pid_pods->end()) {
-              double& v = pods[po->second];
-              if (inc > 0 || v == 0) pods_changed = true;
-              v += inc;
+              if (!p.cu_valid) {
+                unknown_pods.insert(po->second);
+              } else {
+                auto [pv, fresh] = pods.try_emplace(po->second, 0.0);
+                if (inc > 0 || fresh) pods_changed = true;
+                pv->second += inc;
+              }
             }
           }
         }
@@ -974,12 +983,15 @@ void Sampler::run_slow(Worker& w) {
         auto sp = std::make_shared<const std::vector<ProcInfo>>(procs);
         std::shared_ptr<const std::map<std::string, double>> pc;
         if (pods_changed) pc = std::make_shared<const std::map<std::string, double>>(pods);
+        auto uk = std::make_shared<const std::set<std::string>>(std::move(unknown_pods));
         {
           std::lock_guard<std::mutex> g(st.slow_mu);
           st.procs = std::move(sp);
           st.procs_mono_ns = now_p;
           if (pc) st.pod_cu = std::move(pc);
+          st.pod_cu_unknown = std::move(uk);
         }
+        st.procs_cu_unavailable.store(unavailable, std::memory_order_relaxed);
         st.procs_ok_ns.store(now_p, std::memory_order_release);
         st.proc_reads.fetch_add(1, std::memory_order_relaxed);
       } else {

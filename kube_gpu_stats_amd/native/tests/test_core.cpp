@@ -31,6 +31,7 @@
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -52,6 +53,7 @@
 #include "kgs/backend.h"
 #include "kgs/exporter.h"
 #include "kgs/gpu_metrics.h"
+#include "kgs/kfd_procs.h"
 #include "kgs/pmc.h"
 #include "kgs/sampler.h"
 #include "kgs/seqlock.h"
@@ -1136,7 +1138,65 @@ static void test_tick_dither() {
   CHECK(d.step(period, 0.0) == 0.0 && d.offset() == 0.0);
 }
 
+// read_kfd_procs from one slow thread per GPU at once (the fdinfo parse must not share
+// tokenizer state: strtok_r), on a fake KFD + /proc tree under /tmp.
+static void test_kfd_procs_concurrent() {
+  char tmpl[] = "/tmp/kgs_kfd_XXXXXX";
+  const char* root = mkdtemp(tmpl);
+  CHECK(root != nullptr);
+  const std::string r(root), kfd = r + "/kfd", proc = r + "/proc";
+  auto mk = [](const std::string& d) { mkdir(d.c_str(), 0755); };
+  auto put = [](const std::string& f, const std::string& v) {
+    FILE* fp = std::fopen(f.c_str(), "w");
+    std::fputs(v.c_str(), fp);
+    std::fclose(fp);
+  };
+  mk(kfd);
+  mk(proc);
+  for (int pid = 100; pid < 108; ++pid) {
+    const std::string kd = kfd + "/" + std::to_string(pid), pd = proc + "/" + std::to_string(pid);
+    mk(kd);
+    for (int g = 1; g <= 4; ++g) {
+      put(kd + "/vram_" + std::to_string(g), std::to_string(g << 20) + "\n");
+      mk(kd + "/stats_" + std::to_string(g));
+      put(kd + "/stats_" + std::to_string(g) + "/cu_occupancy", std::to_string(pid % 7) + "\n");
+    }
+    mk(pd);
+    mk(pd + "/fd");
+    mk(pd + "/fdinfo");
+    put(pd + "/comm", "proc" + std::to_string(pid) + "\n");
+    for (int g = 1; g <= 4; ++g) {
+      const std::string fd = std::to_string(10 + g);
+      CHECK(symlink("/dev/dri/renderD128", (pd + "/fd/" + fd).c_str()) == 0);
+      char bdf[32];
+      std::snprintf(bdf, sizeof bdf, "0000:%02x:00.0", g);
+      put(pd + "/fdinfo/" + fd, std::string("drm-client-id:\t") + fd + "\ndrm-pdev:\t" + bdf +
+                                    "\ndrm-memory-gtt:\t4 KiB\ndrm-engine-gfx:\t100 ns\n");
+    }
+  }
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int g = 1; g <= 4; ++g)
+    th.emplace_back([&, g] {
+      char bdf[32];
+      std::snprintf(bdf, sizeof bdf, "0000:%02x:00.0", g);
+      for (int it = 0; it < 50; ++it) {
+        std::vector<ProcInfo> v;
+        if (read_kfd_procs(kfd, proc, static_cast<uint64_t>(g), bdf, v) != 0 || v.size() != 8) ++bad;
+        for (const ProcInfo& p : v)
+          if (p.vram_bytes != (static_cast<uint64_t>(g) << 20) || p.gtt_bytes != 4096 || p.gfx_ns != 100 || !p.cu_valid)
+            ++bad;
+      }
+    });
+  for (auto& t : th) t.join();
+  CHECK(bad.load() == 0);
+  std::string cmd = "rm -rf " + r;
+  CHECK(std::system(cmd.c_str()) == 0);
+  std::printf("kfd procs concurrent ok\n");
+}
+
 int main() {
+  test_kfd_procs_concurrent();
   test_dispatch_estimator();
   test_cp_only_work_is_not_read_only();
   test_util_biller();

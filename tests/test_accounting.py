@@ -359,3 +359,74 @@ def test_dispatch_busy_learns_and_removes_the_reads_cp_time(mock_exporter):
     assert cp == pytest.approx(20e-6, rel=0.1)
     raw = {lb["counter"]: v for lb, v in m["amdgpu_pmc_total"]}
     assert raw["CPC_CPC_STAT_BUSY"] > raw["GRBM_SPI_BUSY"]  # the READs' own CP time is in the raw count
+
+
+def test_unreadable_cu_occupancy_is_withheld_not_billed_zero(mock_exporter):
+    """a process whose CU occupancy cannot be read (its KFD stats gone —
+    AMD SMI printed "Unable to open queues directory" and reported 0) used to bill its
+    pod 0 CU-seconds, indistinguishable from "no compute".  Now: nothing is integrated
+    for it, its amdgpu_process_cu_occupancy line is withheld, kgs_process_cu_unavailable
+    counts it, and a pod whose processes are all unreadable gets no
+    container_gpu_cu_seconds_total line (the other pod on the GPU keeps its own)."""
+    ex = mock_exporter(n_gpus=1, hz=100, proc_period_s=0.05, link_every=0,
+                       mock={"util_base": 70, "util_amp": 1e-4, "proc_cu_share": [0.6, 0.3], "proc_cu_fail": 0})
+    ex.set_device_owners(0, [{"pod": "lost", "namespace": "ml", "container": "c"},
+                             {"pod": "seen", "namespace": "dev", "container": "c"}])
+    ex.set_pid_owners({(0, 100000): {"pod": "lost", "namespace": "ml", "container": "c"},
+                       (0, 100001): {"pod": "seen", "namespace": "dev", "container": "c"}})
+    time.sleep(0.6)
+    m = parse_text(ex.render())
+    cu = {lb["pod_name"]: v for lb, v in m["container_gpu_cu_seconds_total"]}
+    assert "lost" not in cu and cu["seen"] > 0.05, cu
+    occ = {lb["pid"]: v for lb, v in m["amdgpu_process_cu_occupancy"]}
+    assert occ == {"100001": pytest.approx(0.3 * 256, abs=1)}, occ
+    assert [v for lb, v in m["kgs_process_cu_unavailable"]] == [1.0]
+    procs = {p["pid"]: p for p in ex.procs(0)}
+    assert procs[100000]["cu_valid"] is False and procs[100000]["cu_seconds"] == 0.0
+    assert procs[100001]["cu_valid"] is True and procs[100001]["cu_seconds"] > 0.05
+
+
+def test_kfd_sysfs_process_reader(N, tmp_path):
+    """The KFD-sysfs process reader (native/src/kfd_procs.cpp) on a fake tree laid out as
+    MI355X's (profiles/r6/r6b/kfd_proc.json): processes on this GPU only (vram_<gpu_id>),
+    CU occupancy from stats_<gpu_id>/ (unreadable → cu_valid False, not 0), the name from
+    /proc/<pid>/comm, GTT / CPU bytes and gfx ns from the fdinfo of this GPU's DRM client
+    (dup'd fds counted once)."""
+    import os as _os
+
+    kfd, proc = tmp_path / "kfd", tmp_path / "proc"
+    gid, other = 36622, 23660
+
+    def kproc(pid, gpu, vram, cu=None, evicted=0):
+        d = kfd / str(pid)
+        d.mkdir(parents=True, exist_ok=True)
+        (d / f"vram_{gpu}").write_text(f"{vram}\n")
+        if cu is not None:
+            (d / f"stats_{gpu}").mkdir()
+            (d / f"stats_{gpu}" / "cu_occupancy").write_text(f"{cu}\n")
+            (d / f"stats_{gpu}" / "evicted_ms").write_text(f"{evicted}\n")
+
+    kproc(101, gid, 534769664, cu=128, evicted=7)   # a tenant on our GPU
+    kproc(102, gid, 0, cu=None)                      # tearing down: stats gone
+    kproc(103, other, 1 << 30, cu=64)                # another GPU's tenant
+    (kfd / "not-a-pid").mkdir()
+    p101 = proc / "101"
+    (p101 / "fd").mkdir(parents=True)
+    (p101 / "fdinfo").mkdir()
+    (p101 / "comm").write_text("python3\n")
+    for fd in ("5", "9"):  # a dup'd render-node fd: one DRM client
+        _os.symlink("/dev/dri/renderD128", p101 / "fd" / fd)
+        (p101 / "fdinfo" / fd).write_text("pos:\t0\ndrm-driver:\tamdgpu\ndrm-client-id:\t9\ndrm-pdev:\t0000:75:00.0\n"
+                                          "drm-memory-vram:\t1464 KiB\ndrm-memory-gtt: \t6896 KiB\n"
+                                          "drm-memory-cpu: \t2 MiB\ndrm-engine-gfx:\t15483 ns\n")
+    _os.symlink("/dev/dri/renderD136", p101 / "fd" / "11")  # another GPU's render node
+    (p101 / "fdinfo" / "11").write_text("drm-client-id:\t12\ndrm-pdev:\t0000:05:00.0\ndrm-memory-gtt:\t99 KiB\n")
+    _os.symlink("/tmp/log.txt", p101 / "fd" / "1")
+    got = {p["pid"]: p for p in N.read_kfd_procs(str(kfd), str(proc), gid, "0000:75:00.0")}
+    assert set(got) == {101, 102}
+    a, b = got[101], got[102]
+    assert a["vram_bytes"] == 534769664 and a["cu_occupancy"] == 128 and a["cu_valid"] and a["evicted_ms"] == 7
+    assert a["name"] == "python3" and a["gtt_bytes"] == 6896 << 10 and a["cpu_bytes"] == 2 << 20
+    assert a["gfx_ns"] == 15483
+    assert b["cu_valid"] is False and b["cu_occupancy"] == 0 and b["name"] == "" and b["gtt_bytes"] == 0
+    assert N.read_kfd_procs(str(tmp_path / "absent"), str(proc), gid, "0000:75:00.0") is None
