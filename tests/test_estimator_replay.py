@@ -498,3 +498,30 @@ def test_reallocation_starts_the_new_pods_counter_at_zero(mock_exporter):
     busy = {lb["pod_name"]: v for lb, v in m["container_gpu_busy_seconds_total"]}
     assert set(busy) == {"b"} and 0.5 < busy["b"] <= el + 0.02, (busy, el)
     assert ex.integrals(0)["util_dropped_seconds"] >= d0
+
+
+HELDOUT = os.path.join(REPO, "profiles", "r6", "r6c", "cp_dump_irregular.json.gz")
+
+
+def test_held_out_irregular_loads_replay_within_one_and_a_half_points():
+    """out of sample.  Every constant of the estimator was fitted on the
+    r4f / r5b / r5l dumps of strictly periodic single-stream trains.  The r6c dump
+    (recorded on MI355X in the exporter's READ mode at 8 kHz, 1 kHz, 100 Hz and 10 Hz)
+    holds loads none of them saw — seeded random 5 µs - 20 ms MFMA kernels with random
+    gaps on one and on two streams, and a bf16 decoder training step (duty: the union of
+    its kernels' intervals, PyTorch profiler) — and replays within ±1.5 points of the
+    duty at every rate with the shipped parameters, which test_replay_is_the_samplers_code
+    pins, so nothing here was retuned to fit it."""
+    res = sim.replay(HELDOUT)
+    assert set(res) == {"8000", "1000", "100", "10"}
+    for rate, rows in res.items():
+        assert abs(rows["idle"]["err_pts"]) <= 0.05, (rate, rows["idle"])
+        for load in ("random_kernels", "two_stream_random", "train_step"):
+            r = rows[load]
+            assert 20 < r["duty_gpu_pct"] < 90, (rate, load, r)
+            assert abs(r["err_pts"]) <= 1.5, (rate, load, r)
+    rec = json.load(open(os.path.join(REPO, "profiles", "r6", "estimator_replay_irregular_heldout.json")))
+    for rate, rows in rec.items():
+        for load, r in rows.items():
+            if isinstance(r, dict):
+                assert res[rate][load]["err_pts"] == pytest.approx(r["err_pts"], abs=0.02), (rate, load)

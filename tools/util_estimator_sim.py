@@ -109,7 +109,13 @@ def replay(path: str, overrides: dict | None = None, classes: bool = False) -> d
     from kube_gpu_stats_amd import load_native
 
     N = load_native()
-    d = json.load(open(path))
+    if path.endswith(".gz"):  # held-out dumps are committed compressed (profiles/r6/r6c)
+        import gzip
+
+        with gzip.open(path, "rt") as f:
+            d = json.load(f)
+    else:
+        d = json.load(open(path))
     p = N.sampler_estimator_params()
     for k, v in (overrides or {}).items():
         t = type(getattr(p, k))
