@@ -140,3 +140,14 @@ def test_every_tool_answers_help_without_a_gpu(tool):
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", tool), "--help"], capture_output=True, text=True,
                        timeout=60)
     assert r.returncode == 0 and len(r.stdout.strip()) > 40, (r.stdout[-300:], r.stderr[-500:])
+
+
+def test_tools_readme_lists_every_remaining_file():
+    """tools/ holds the probes its README cites as evidence, and the README
+    lists every file that remains."""
+    here = os.path.join(REPO, "tools")
+    text = open(os.path.join(here, "README.md")).read()
+    files = [f for f in os.listdir(here) if os.path.isfile(os.path.join(here, f)) and f != "README.md"
+             and not f.endswith(".pyc")]
+    missing = [f for f in files if f"`{f}`" not in text and f"`{f} " not in text]
+    assert not missing, missing

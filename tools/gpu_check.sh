@@ -3,11 +3,11 @@
 # time limit; a test failure (rc 1) does not stop the script, a timeout / signal /
 # abort (rc >= 124) does — nothing else touches the GPU after that.
 #   gpurun --timeout 1100 -- 'bash tools/gpu_check.sh <tag> [steps...]'
-# steps (default: probe tests smoke bench): probe probe3 tests smoke bench bench2 rocprof
+# steps (default: tests smoke bench): tests testsall testsx smoke bench bench2 rocprof
 #   round 4: smprobe cpprobe graphcost testsnw testsdb wedge (the wedged-queue test last, alone)
 set -u
 TAG=${1:-r2}; shift || true
-STEPS=${*:-probe tests smoke bench}
+STEPS=${*:-testsall smoke bench}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -23,10 +23,6 @@ run() {  # name limit cmd...
 }
 for s in $STEPS; do
   case $s in
-    probe3) run event_source 30 ls -la /sys/bus/event_source/devices/
-            run perf_pmu 90 python tools/perf_pmu_probe.py --out "$OUT/perf_pmu.json"
-            KGS_AQL_PROBE_OUT="$OUT/aql_probe_cp.json" run aql_probe_cp 400 python -u tools/aql_probe.py \
-              cpc_dispatch,cpc_busy,cpc_gd,grbm_cp,spi_csn ;;
     bench3) run bench3 600 python -u bench.py --steps 20 --warmup 5 --pmc-lean 3 --out "$OUT/bench3.json" ;;
     train3) run train3 600 python -u bench.py --load train --steps 10 --warmup 2 --rounds 32 --hz-list 100 \
               --capacity-hz "" --burst-s 0 --quiet-s 0 --component-s 0 --pmc-lean 3 --out "$OUT/train3.json" ;;
@@ -64,8 +60,6 @@ for s in $STEPS; do
     rss) run rss 180 python -u tools/rss_probe.py --out "$OUT/rss_probe.json" ;;
     hsarss) run hsarss 300 python -u tools/hsa_rss_probe.py --out "$OUT/hsa_rss.json" ;;
     soak90) run soak90 240 python -u tools/soak.py --seconds 90 --out "$OUT/soak90.json" ;;
-    probe) run probe_latency 90 python tools/probe_amdsmi_latency.py
-           run probe_xgmi 90 python tools/probe_xgmi.py ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider ;;
     # round 4
     smprobe) run sm_util_probe 300 python -u tools/sm_util_probe.py --out "$OUT/sm_util_probe.json" ;;
