@@ -86,6 +86,8 @@ class IrregularLoad:
         rnds = [random.Random(seed * 1000 + k) for k in range(streams)]
         ref = torch.cuda.Event(enable_timing=True)
         ref.record(ss[0])
+        ref.synchronize()
+        t_ref_ns = time.monotonic_ns()  # host CLOCK_MONOTONIC at the reference stamp (± µs)
         for s in ss[1:]:
             s.wait_event(ref)  # no kernel of stream k starts before the reference stamp
         events: list[tuple] = []
@@ -128,7 +130,7 @@ class IrregularLoad:
         wall = time.perf_counter() - t0
         iv = [(ref.elapsed_time(a) * 1e-3, ref.elapsed_time(b) * 1e-3) for a, b in events]
         return {"busy_s": union_seconds(iv), "sum_s": sum(b - a for a, b in iv), "kernels": len(iv),
-                "wall_s": wall, "streams": streams, "seed": seed}
+                "wall_s": wall, "streams": streams, "seed": seed, "t_ref_mono_ns": t_ref_ns, "intervals": iv}
 
 
 def mfma_launcher(torch, ls, ms_per_iter: float, blocks: int = 2048):

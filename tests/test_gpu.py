@@ -1756,14 +1756,23 @@ def test_irregular_loads_bill_their_duty(torch_dev, tmp_path):
     for _ in range(2):
         tl.unit()
     torch.cuda.synchronize()
-    loads = {"random_kernels": lambda secs: irr.run(secs, 81, 1)["busy_s"],
-             "two_stream_random": lambda secs: irr.run(secs, 82, 2)["busy_s"],
+    last: dict = {}
+
+    def irregular(secs, seed, streams):
+        r = irr.run(secs, seed, streams)
+        last.clear()
+        last.update(r)
+        return r["busy_s"]
+
+    loads = {"random_kernels": lambda secs: irregular(secs, 81, 1),
+             "two_stream_random": lambda secs: irregular(secs, 82, 2),
              "train_step": lambda secs: profiled_busy(torch, tl.unit, secs)[0]}
     shipped = _daemonset_exporter_args()
     bdf = _bdf0()
     owners = tmp_path / "owners.json"
     owners.write_text(json.dumps({bdf: {"pod": "train-0", "namespace": "ml", "container": "main"}}))
     rows: dict = {}
+    raw: dict = {}
     for hz in (10, 1000, 8000):
         args = [x if not x.startswith("--hz=") else f"--hz={hz}" for x in shipped]
         proc, ready = _exporter_proc(args + ["--node-name", "gpu-node-1", "--static-owners", str(owners),
@@ -1791,9 +1800,18 @@ def test_irregular_loads_bill_their_duty(torch_dev, tmp_path):
                     "from_counters_s": round(d("kgs_util_source_seconds_total", source="counters"), 3),
                     "reads_per_s": round(d("kgs_pmc_samples_total") / win, 1), "window_s": round(win, 3)}
                 r["error_pts"] = round(r["busy_counter_pct"] - r["duty_gpu_pct"], 2)
+                if hz == 10 and name != "train_step":
+                    # every drain and PMFW sample of the window, and the kernels' intervals on
+                    # the same clock, for an offline replay (tools/util_estimator_sim.py)
+                    raw[f"{hz}/{name}"] = {
+                        "t_ref_mono_ns": last["t_ref_mono_ns"], "kernels_s": [[round(a, 6), round(b, 6)]
+                                                                              for a, b in last["intervals"]],
+                        "counters": json.loads(sc.get("/counters?gpu=0&n=400")),
+                        "pmfw": json.loads(sc.get("/samples?gpu=0&n=400"))}
                 time.sleep(0.3)
         finally:
             _quit(proc)
+    _keep("irregular_raw_10hz.json", json.dumps(raw))
     _keep("irregular_billing.json", json.dumps({"args": shipped, "rows": rows}, indent=1))
     print(json.dumps(rows))
     for key, r in rows.items():
