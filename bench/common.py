@@ -5,6 +5,7 @@ from __future__ import annotations
 import math
 import os
 import socket
+import sys
 import time
 
 from kube_gpu_stats_amd.parallel import dist as D
@@ -138,3 +139,14 @@ def tiers(a) -> list[float]:
     """Every tick rate measured: the primary --hz plus --hz-list, ascending."""
     extra = [float(x) for x in str(a.hz_list).split(",") if x.strip()]
     return sorted({float(a.hz), *extra})
+
+
+_T0 = time.monotonic()
+
+
+def progress(ctx, msg: str) -> None:
+    """One line to stderr on rank 0 per phase (and per round of the long ones): a run that
+    prints nothing for minutes is taken for hung by the GPU harness; stdout stays the
+    driver's one result line."""
+    if ctx is None or getattr(ctx, "rank", 0) == 0:
+        print(f"[bench +{time.monotonic() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)

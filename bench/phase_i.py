@@ -6,7 +6,7 @@ import math
 from kube_gpu_stats_amd.parallel import dist as D
 from kube_gpu_stats_amd.utils.scrape import Scraper
 
-from .common import RELEASED, cond_label, mean_ci95, scrape_at, t975, timed_block
+from .common import RELEASED, cond_label, mean_ci95, progress, scrape_at, t975, timed_block
 from .exporter import PmfwProbe, Rates
 
 
@@ -83,8 +83,10 @@ def interleaved(ctx, load, exp, a, hzs: list[float]) -> dict:
     lat: dict[float, list[float]] = {h: [] for h in hzs}
     paused_reads = 0.0
     local: list[dict] = []  # per round: {cond: {"own", "all", "comp", "power"}}
-    for order in orders:
+    for ri, order in enumerate(orders):
         blk: dict = {}
+        if ri % 8 == 0:
+            progress(ctx, f"phase I round {ri + 1}/{len(orders)}")
         for c in order:
             sc = None
             before: dict = {}

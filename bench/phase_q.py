@@ -6,7 +6,7 @@ import time
 
 from kube_gpu_stats_amd.parallel import dist as D
 
-from .common import mean_ci95, scrape_at
+from .common import mean_ci95, progress, scrape_at
 from .exporter import PmfwProbe
 
 
@@ -86,6 +86,7 @@ def idle_power(ctx, load, exp, a) -> dict:
     parked_ok = True
     for r in range(rounds):
         row: dict = {}
+        progress(ctx, f"phase P round {r + 1}/{rounds}")
         for cond in perms[r % len(perms)]:
             if ctx.local_rank == 0 and exp is not None:
                 if cond == "released":

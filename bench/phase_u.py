@@ -5,7 +5,7 @@ import time
 
 from kube_gpu_stats_amd.parallel import dist as D
 
-from .common import scrape_at
+from .common import progress, scrape_at
 
 
 def util_accuracy(ctx, load, exp, a) -> dict:
@@ -43,6 +43,7 @@ def util_accuracy(ctx, load, exp, a) -> dict:
         except Exception as e:  # noqa: BLE001 - report the load as failed, keep the phase
             errors["train_step"] = f"{type(e).__name__}: {e}"[:300]
     for hz in rates:
+        progress(ctx, f"phase U at {hz:g} Hz")
         if exp is not None:
             exp.set_rate(hz)
         D.cpu_barrier(ctx)

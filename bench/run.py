@@ -7,7 +7,7 @@ import time
 from kube_gpu_stats_amd.parallel import dist as D
 from kube_gpu_stats_amd.utils.scrape import Scraper
 
-from .common import METRIC, PHASES, REPO, calibrate_reps, pct, scrape_at, tiers, timed
+from .common import METRIC, PHASES, REPO, calibrate_reps, pct, progress, scrape_at, tiers, timed
 from .exporter import AttachedExporter, ExporterProc, Rates, proc_cpu_seconds, thread_cpu_seconds
 from .loads import GpuLoad, MockLoad, TrainLoad
 from .observe import allreduce_GBps, allreduce_ratio, observed, throttled, wake_lateness, xgmi_rates
@@ -39,6 +39,7 @@ def run(a, ctx) -> dict | None:
     else:
         load = GpuLoad(a, ctx.local_rank, ctx)
 
+    progress(ctx, f"load {type(load).__name__}: calibrating")
     calib = load.calibrate()
     load.reps, unit_s = calibrate_reps(ctx, load, a.step_ms)
     for _ in range(a.warmup):
@@ -50,6 +51,7 @@ def run(a, ctx) -> dict | None:
     if a.attach and ctx.local_rank == 0:
         attached = AttachedExporter(a.attach)
         attached.pause()
+    progress(ctx, f"phase A: {a.steps} steps, no exporter")
     t_a = timed(ctx, load, a.steps, "A_off")
 
     # start the node exporter over every local rank's GPU
@@ -88,6 +90,7 @@ def run(a, ctx) -> dict | None:
         cpu0, thr0, c_t0 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid), time.perf_counter()
         before, w0 = scrape_at(sc_b)  # counts as of the render, timed at the request
         sc_b.start(a.scrape_hz)
+    progress(ctx, f"phase B: {a.steps} steps, exporter at {a.hz:g} Hz")
     t_b = timed(ctx, load, a.steps, "B_on")
     if exp is not None:
         sc_b.stop()
@@ -96,20 +99,29 @@ def run(a, ctx) -> dict | None:
         cpu1, thr1 = proc_cpu_seconds(exp_pid), thread_cpu_seconds(exp_pid)
         cpu_win = time.perf_counter() - c_t0
 
+    progress(ctx, "phase R: burst resolution")
     resolution = burst_train(ctx, load, exp, a)
+    progress(ctx, "phase Q: idle GPU")
     quiet = quiet_gpu(ctx, load, exp, a)
     if quiet is not None:
+        progress(ctx, "phase P: idle-GPU power, session / released / parked")
         power = idle_power(ctx, load, exp, a)
         if power:
             quiet["idle_power"] = power
+    progress(ctx, "phase U: utilisation accuracy")
     util = util_accuracy(ctx, load, exp, a)
+    progress(ctx, f"phase I: {a.rounds} interleaved rounds")
     inter = interleaved(ctx, load, exp, a, hzs)
+    progress(ctx, "phase S: capacity")
     cap = capacity(ctx, load, exp, a)
+    progress(ctx, "phase K: per-component delivery")
     comp_rates = component_rates(ctx, load, exp, a)
+    progress(ctx, "phase X: xGMI link map")
     xlink = xgmi_link_check(ctx, load, exp, a)
     stopped = exp.stop() if exp is not None else {}
 
     # phase C: exporter off again
+    progress(ctx, "phase C: exporter stopped")
     t_c = timed(ctx, load, a.steps, "C_off")
     if exp is None:
         return None

@@ -1051,7 +1051,8 @@ def test_pcie_bytes_counter_tracks_host_copies(N, torch_dev):
     for name, r in out.items():
         # one factor for both directions (±3 %, profiles/r2/pcie/) + table granularity; the
         # check is the unit (round 1 exported the accumulator ×10⁹), not the last percent
-        bound(f"pcie_counted_over_moved[{name}]", r["counted"] / r["moved"], lo=0.90, hi=1.10, ctx=r)
+        # H2D reads 1.03-1.06 (PMFW counts link-level overhead): hi re-based 1.10 → 1.15
+        bound(f"pcie_counted_over_moved[{name}]", r["counted"] / r["moved"], lo=0.90, hi=1.15, ctx=r)
 
 
 def test_energy_counter_matches_socket_power(N, torch_dev):
@@ -1817,7 +1818,8 @@ def test_irregular_loads_bill_their_duty(torch_dev, tmp_path):
     for key, r in rows.items():
         assert 5 < r["duty_gpu_pct"] < 100, (key, r)   # the loads are neither idle nor saturating
         assert r["from_counters_s"] > 0.9 * r["window_s"], (key, r)
-        bound(f"irregular_abs_err_pts[{key}]", abs(r["error_pts"]), hi=IRREGULAR_BOUND_PTS, ctx=r)
+        bound(f"irregular_abs_err_pts[{key}]", abs(r["error_pts"]),
+              hi=IRREGULAR_BOUND_PTS.get(key.split("/", 1)[1], 4.0), ctx=r)
 
 
 def test_quiet_release_parks_and_wakes_on_hardware(torch_dev):
@@ -1876,9 +1878,12 @@ def test_quiet_release_parks_and_wakes_on_hardware(torch_dev):
     bound("quiet_release_error_pts", abs(row["error_pts"]), hi=3.0, ctx=row)
 
 
-# Held for the first hardware runs of the irregular loads (profiles/gpu_test_margins.md
-# records what they read and re-bases this at ≥ 2× the spread seen across boxes).
-IRREGULAR_BOUND_PTS = 4.0
+# Bounds at ≥ 2× the spread seen across boxes (profiles/gpu_test_margins.md): the random
+# loads read within 1.7 points everywhere (10 Hz: −1.4 … −1.7 on three boxes); the 8 kHz
+# training step read 0.0 / +0.03 on two boxes and −2.19 on r6b, where the counters fell
+# 2.2 points below both the duty and the PMFW busy, once — unexplained, so its bound is
+# 2.19 + 2 × 2.19.
+IRREGULAR_BOUND_PTS = {"train_step": 6.6}
 
 
 def test_wedged_counter_queue_trips_the_breaker_and_recovers(torch_dev):
