@@ -129,15 +129,71 @@ def replay(path: str, overrides: dict | None = None, classes: bool = False) -> d
     return {rate: replay_rate(N, loads, p, mfma_col, fresh_col) for rate, loads in d["rates"].items()}
 
 
+def replay_exporter_raw(path: str, overrides: dict | None = None) -> dict:
+    """The irregular GPU test's raw 10 Hz capture (``irregular_raw_10hz.json``: the
+    exporter's own drains from ``/counters`` and the kernels' event-timed intervals on the
+    host monotonic clock) folded through the estimator drain by drain, warmed on the
+    drains before the load: per load the dispatch integral against the kernels' union over
+    the same drain intervals, and the intervals that err most."""
+    from kube_gpu_stats_amd import load_native
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from kube_gpu_stats_amd.ops.irregular import union_seconds
+
+    N = load_native()
+    p = N.sampler_estimator_params()
+    for k, v in (overrides or {}).items():
+        t = type(getattr(p, k))
+        setattr(p, k, str(v).lower() in ("1", "true", "yes") if t is bool else t(v))
+    d = json.load(open(path))
+    out = {}
+    for name, rec in d.items():
+        names = rec["counters"]["counters"]
+        ix = {n: i for i, n in enumerate(names)}
+        t_ref = rec["t_ref_mono_ns"] * 1e-9
+        kern = [(t_ref + a, t_ref + b) for a, b in rec["kernels_s"]]
+        k0, k1 = min(a for a, _ in kern), max(b for _, b in kern)
+        est = N.DispatchEstimator()
+        prev_t = None
+        busy = truth = span = 0.0
+        worst = []
+        for smp in rec["counters"]["samples"]:
+            v = smp["v"]
+            t = smp["mono_ns"] * 1e-9
+            mf = v[ix["SQ_VALU_MFMA_BUSY_CYCLES"]] if v[ix["SQ_VALU_MFMA_BUSY_CYCLES"]] is not None else None
+            s = est.feed(p, smp["mono_ns"], int(v[ix["GRBM_COUNT"]]), int(v[ix["GRBM_SPI_BUSY"]]),
+                         int(v[ix["CPC_CPC_STAT_BUSY"]]), None if mf is None else int(mf), bool(smp["se_fresh"]), False)
+            if prev_t is not None and prev_t >= k0 - 0.2 and t <= k1 + 0.4:
+                tr = union_seconds([(max(a, prev_t), min(b, t)) for a, b in kern if b > prev_t and a < t])
+                busy += s.dispatch_s
+                truth += tr
+                span += t - prev_t
+                worst.append((round(s.dispatch_s - tr, 5), round(prev_t - k0, 3), round(t - prev_t, 4),
+                              round(tr / (t - prev_t), 3)))
+            prev_t = t
+        worst.sort(key=lambda x: abs(x[0]), reverse=True)
+        out[name] = {"span_s": round(span, 3), "busy_pct": round(100 * busy / span, 2) if span else None,
+                     "truth_pct": round(100 * truth / span, 2) if span else None,
+                     "err_pts": round(100 * (busy - truth) / span, 2) if span else None,
+                     "intervals": len(worst), "worst": worst[:8],
+                     "idle_clock_mhz": round(est.clk_idle_hz / 1e6, 1), "busy_clock_mhz": round(est.clk_busy_hz / 1e6, 1)}
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("dump")
+    ap.add_argument("--exporter-raw", action="store_true",
+                    help="the dump is an irregular_raw_10hz.json capture of the exporter's own drains")
     ap.add_argument("--set", action="append", default=[], metavar="PARAM=VALUE",
                     help="override one EstimatorParams field (e.g. cpc_full_frac=0.97)")
     ap.add_argument("--classes", action="store_true",
                     help="instead: each load's estimate split by READ-interval class (full / partial / READ-only)")
     a = ap.parse_args(argv)
     ov = dict(kv.split("=", 1) for kv in a.set)
+    if a.exporter_raw:
+        print(json.dumps(replay_exporter_raw(a.dump, ov), indent=1))
+        return 0
     print(json.dumps(replay(a.dump, ov, classes=a.classes), indent=1))
     return 0
 
