@@ -644,7 +644,8 @@ def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
         assert [r[:4] for r in rows] == [["gpu-node-1", "ml", "train-0", 1]], rows
         # the load loop pauses for every scrape + ingest (≈ms each, 4 per second), and a 1 s
         # rate() range of a counter that moves in ≈20 ms PMFW steps is good to a few per cent
-        bound("f5_fixed_report_util", rows[0][4], lo=80, ctx=rows)
+        # 90-101 across boxes (a 1 s rate() extrapolated over ≈20 ms PMFW steps): re-based 80 → 65
+        bound("f5_fixed_report_util", rows[0][4], lo=65, ctx=rows)
         # --energy: the pod's GPU energy over the 2 s window, as mean watts ≈ the socket power
         kwh = G.pod_energy_kwh(PromClient(url), end - 2, end, 1)
         watts = kwh[("gpu-node-1", "ml", "train-0")] * 3.6e6 / 2
@@ -767,7 +768,7 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev, batch):
     bound(f"burst_seg_len_abs_err_ms[batch{batch}]", abs(seg_len - host_len), hi=0.35 * host_len + 0.25,
           ctx=summary)  # ±2 drains of 125 µs + launch/sync jitter
     bound(f"burst_share_min[batch{batch}]", min(sh), hi=5, ctx=summary)
-    bound(f"burst_share_max[batch{batch}]", max(sh), lo=90, ctx=summary)
+    bound(f"burst_share_max[batch{batch}]", max(sh), lo=85, ctx=summary)  # 100-105 seen (quantised shares)
     bound(f"burst_duty_abs_err[batch{batch}]", abs(summary["duty_counters"] - host_duty), hi=0.08, ctx=summary)
     assert len(pm_in) >= 10, summary                  # ≈50 tables/s
     # profiling mode: PMFW reads the READs as work — far above the ≈20 % true duty
