@@ -83,6 +83,7 @@ def idle_power(ctx, load, exp, a) -> dict:
     load.sync()
     default_qr = exp.set_quiet_release(-1) if ctx.local_rank == 0 and exp is not None else 0.0
     local: list[dict] = []
+    blocks: list[dict] = []  # rank 0: the exporter's side of each block
     parked_ok = True
     for r in range(rounds):
         row: dict = {}
@@ -101,9 +102,18 @@ def idle_power(ctx, load, exp, a) -> dict:
                     parked_ok &= exp.wait_parked(10.0)
             D.cpu_barrier(ctx)
             time.sleep(min(1.0, 0.2 * block))  # settle: the power-state change after the switch
+            m0 = scrape_at(exp.sc)[0] if ctx.local_rank == 0 and exp is not None else None
             p0 = probe.read()
             time.sleep(block)
             row[cond] = PmfwProbe.delta(p0, probe.read())
+            if m0 is not None:  # what the exporter did in the block: parks, READs, PMFW busy
+                m1 = scrape_at(exp.sc)[0]
+                tot = lambda m, f: sum(v for _, v in m.get(f, []))  # noqa: E731
+                blocks.append({"round": r, "cond": cond, "parks": tot(m1, "kgs_pmc_parks_total") - tot(m0, "kgs_pmc_parks_total"),
+                               "reads_per_s": round((tot(m1, "kgs_pmc_samples_total") - tot(m0, "kgs_pmc_samples_total")) / block, 1),
+                               "pmfw_busy_pct": round(100 * (tot(m1, "amdgpu_pmfw_gfx_busy_seconds_total")
+                                                              - tot(m0, "amdgpu_pmfw_gfx_busy_seconds_total")) / block, 3),
+                               "parked_at_end": tot(m1, "kgs_pmc_parked")})
             D.cpu_barrier(ctx)
         local.append(row)
     if ctx.local_rank == 0 and exp is not None:
@@ -127,7 +137,14 @@ def idle_power(ctx, load, exp, a) -> dict:
            "conditions": {"session": "counter session programmed, quiet GPU READ at --pmc-idle-hz, no quiet release",
                           "released": "session STOPped and READ queue destroyed; PMFW / slow tiers sampling",
                           "parked": "the exporter's quiet release (1 s here) released the session by itself"},
-           "per_rank": per_rank}
+           "per_rank": per_rank, "blocks": blocks}
+    for cond in conds:
+        bl = [b for b in blocks if b["cond"] == cond]
+        if bl:
+            out.setdefault("exporter_by_condition", {})[cond] = {
+                "parks_per_block": round(sum(b["parks"] for b in bl) / len(bl), 2),
+                "reads_per_s": round(sum(b["reads_per_s"] for b in bl) / len(bl), 1),
+                "pmfw_busy_pct": round(sum(b["pmfw_busy_pct"] for b in bl) / len(bl), 3)}
     for cond in ("session", "parked"):
         k = f"{cond}_minus_released_w"
         vals = [p[k] for p in per_rank if k in p]
