@@ -15,7 +15,7 @@ EXP=$!
 for i in $(seq 60); do grep -q '"event": "ready"' "$OUT/exporter.out" 2>/dev/null && break; sleep 1; done
 if ! grep -q '"event": "ready"' "$OUT/exporter.out"; then echo "exporter not ready"; kill $EXP; exit 1; fi
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 bench.py --steps 6 --warmup 2 \
-  --step-ms ${KGS_ROCPROF_STEP_MS:-450} --rounds 24 --util-s 0 --released 0 --attach 127.0.0.1:19400 --out "$OUT/bench_rocprof.json" > "$OUT/bench.log" 2>&1
+  --step-ms ${KGS_ROCPROF_STEP_MS:-450} --rounds 24 --util-s 0 --idle-power-s 0 --released 0 --attach 127.0.0.1:19400 --out "$OUT/bench_rocprof.json" > "$OUT/bench.log" 2>&1
 RC=$?
 kill $EXP; wait $EXP 2>/dev/null
 echo "rocprof rc=$RC"
