@@ -117,7 +117,7 @@ def pmc_control(a) -> int:
     body = urllib.request.urlopen(f"http://{a.exporter}/metrics", timeout=10).read().decode()
     print("\n".join(ln for ln in body.splitlines()
                     if ln.startswith(("kgs_pmc_enabled", "kgs_pmc_stalled", "kgs_pmc_failed", "kgs_pmc_quiet ",
-                                       "kgs_pmc_quiet{", "kgs_pmc_dispatch_bound", "kgs_sampler_thread_hung",
+                                       "kgs_pmc_quiet{", "kgs_pmc_dispatch_bound", "kgs_pmc_parked", "kgs_sampler_thread_hung",
                                        "kgs_pmc_publishes_total", "kgs_pmc_unlanded_total"))
                     and (a.gpu < 0 or f'gpu="{a.gpu}"' in ln)))
     return 0
