@@ -51,6 +51,17 @@ def quiet_gpu(ctx, load, exp, a) -> dict:
     return out
 
 
+class MockPowerProbe:
+    """PmfwProbe's interface for --mock runs: a 250 W idle socket on the host clock."""
+
+    N = True
+
+    def read(self) -> dict:
+        t = time.monotonic()
+        return {"fw_ts": int(t * 1e8), "energy_acc": int(250.0 * t * 65536.0), "accumulation_counter": int(t * 1e3),
+                "ppt_residency_acc": 0}
+
+
 def idle_power(ctx, load, exp, a) -> dict:
     """Phase P (untimed) — what the counter session costs an idle GPU in power, and what
     the quiet release saves.  With every rank's GPU idle, three
@@ -69,12 +80,14 @@ def idle_power(ctx, load, exp, a) -> dict:
     that round's ``released`` block: mean ± 95 % CI (``summary.quiet_gpu.power_w``)."""
     secs = float(getattr(a, "idle_power_s", 0.0) or 0.0)
     rounds = int(getattr(a, "idle_power_rounds", 6) or 0)
-    if secs <= 0 or rounds <= 0 or a.mock:
+    if secs <= 0 or rounds <= 0:
         return {}
     import itertools
 
     block = secs / rounds
-    probe = PmfwProbe(load.pci_bdf(ctx.local_rank))
+    # --mock: the orchestration on CPU (every rank, every barrier), against a constant
+    # synthetic socket power — no power number of a mock run means anything
+    probe = MockPowerProbe() if a.mock else PmfwProbe(load.pci_bdf(ctx.local_rank))
     if probe.N is None:
         return {"skipped": "no PMFW table probe"}
     conds = ("session", "released", "parked")
@@ -99,7 +112,7 @@ def idle_power(ctx, load, exp, a) -> dict:
                 else:
                     exp.set_quiet_release(1.0)
                     exp.acquire()
-                    parked_ok &= exp.wait_parked(10.0)
+                    parked_ok &= exp.wait_parked(1.0 if a.mock else 10.0)
             D.cpu_barrier(ctx)
             time.sleep(min(1.0, 0.2 * block))  # settle: the power-state change after the switch
             m0 = scrape_at(exp.sc)[0] if ctx.local_rank == 0 and exp is not None else None

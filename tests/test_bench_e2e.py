@@ -63,13 +63,15 @@ def _rate_ok(v: float, hz: float) -> bool:
 # The mock runs at bench.py's default 8 kHz, stated here so that the tests do not follow a
 # change of the default: this 8-CPU VM cannot hold 16 kHz for several mock GPUs at once.
 FAST = ["--hz", "8000", "--pmc-batch", "8", "--step-ms", "60", "--rounds", "4", "--block-steps", "1", "--settle",
-        "0.3", "--util-hz", ""]
+        "0.3", "--util-hz", "", "--idle-power-s", "0"]
+# phase P's orchestration on the mock (constant synthetic power: the plumbing, not a number)
+POWER = ["--idle-power-s", "1.2", "--idle-power-rounds", "2"]
 
 
 @pytest.mark.slow
 def test_bench_contract_single_process(tmp_path):
     r = subprocess.run([sys.executable, "bench.py", "--mock", "--steps", "10", "--warmup", "1", *FAST,
-                        "--util-hz", "1000,10", "--out", str(tmp_path / "bench.json")],
+                        "--util-hz", "1000,10", *POWER, "--out", str(tmp_path / "bench.json")],
                        cwd=REPO, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     line, res = _result(r.stdout)
@@ -147,6 +149,11 @@ def test_bench_contract_single_process(tmp_path):
     # phase Q plumbing: both exporter modes measured, the default idle rate restored after
     q = res["quiet_gpu"]
     assert q["adaptive"]["pmc_idle_hz"] == 100 and q["profiling"]["pmc_idle_hz"] == 0
+    ip = q["idle_power"]  # phase P ran every condition on the mock, in rounds of every order
+    assert ip["rounds"] == 2 and [b["cond"] for b in ip["blocks"]][:3] == ["session", "released", "parked"], ip
+    assert ip["per_rank"][0]["session_minus_released_w"][0] == pytest.approx(0.0, abs=1.0), ip
+    assert set(ip["exporter_by_condition"]) == {"session", "released", "parked"}
+    assert ip["exporter_by_condition"]["released"]["reads_per_s"] == 0, ip
     assert set(q["adaptive"]["per_gpu"]["0"]) == {"reads_per_s", "pmfw_gfx_busy_pct", "gpu_active_pct"}
     # phase S plumbing: the primary rate and each capacity rate got a block, rate restored after
     cap = res["capacity"]
@@ -179,7 +186,7 @@ def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads(tmp_path):
     interleaved overheads come per rank and per component, power per rank."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "bench.py", "--mock", "--gpus", "8", "--steps", "4", "--warmup", "1",
-                        *FAST, "--hz", "2000", "--capacity-hz", "", "--burst-s", "0", "--quiet-s", "0",
+                        *FAST, "--hz", "2000", "--capacity-hz", "", "--burst-s", "0", "--quiet-s", "0", *POWER,
                         "--out", str(tmp_path / "bench.json")],
                        cwd=REPO, capture_output=True, text=True, timeout=420, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
@@ -196,6 +203,7 @@ def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads(tmp_path):
                                                                             if i != j]
     for p in x["per_copy"]:
         assert p["src"]["link_peer_bdf"] == p["peer_bdf"] and p["dst"]["ok"], p
+    assert len(res["quiet_gpu"]["idle_power"]["per_rank"]) == 8  # phase P: every rank's own probe
     for hz in ("100", "2000"):
         t = res["interleaved"]["tiers"][hz]
         assert [q["rank"] for q in t["overhead_by_rank"]] == list(range(8))
