@@ -1005,3 +1005,28 @@ def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
     with pytest.raises(ValueError):
         ex.pmc_quiet_release_s = -2
     assert ex.pmc_quiet_release_s == pytest.approx(0.1)
+
+
+def test_hand_over_while_parked_and_back(mock_exporter):
+    """A device parked by the quiet release can be handed over (kgs pmc release: nothing is
+    held, the hand-over stands) and acquired back at once by the control plane, whatever
+    the load (an explicit acquire ends a park without waiting for PMFW busy)."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100,
+                       pmc_quiet_release_s=0.2, mock={"util_base": 0, "util_amp": 0})
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 3 and not ex.integrals(0)["pmc_parked"]:
+        time.sleep(0.02)
+    i = ex.integrals(0)
+    assert i["pmc_parked"] == 1 and i["pmc_on"] == 0, i
+    ex.set_pmc_enabled(False)
+    time.sleep(0.1)
+    i = ex.integrals(0)
+    assert i["pmc_parked"] == 0 and i["pmc_on"] == 0 and not ex.pmc_enabled, i
+    ex.pmc_quiet_release_s = 0          # stay acquired on the idle mock GPU this time
+    ex.set_pmc_enabled(True)
+    time.sleep(0.2)
+    i = ex.integrals(0)
+    assert i["pmc_on"] == 1 and i["pmc_parked"] == 0, i
+    n = i["pmc_samples"]
+    time.sleep(0.3)
+    assert ex.integrals(0)["pmc_samples"] > n  # drains again (at the idle rate)
