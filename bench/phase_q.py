@@ -117,8 +117,13 @@ def idle_power(ctx, load, exp, a) -> dict:
             time.sleep(min(1.0, 0.2 * block))  # settle: the power-state change after the switch
             m0 = scrape_at(exp.sc)[0] if ctx.local_rank == 0 and exp is not None else None
             p0 = probe.read()
-            time.sleep(block)
-            row[cond] = PmfwProbe.delta(p0, probe.read())
+            time.sleep(0.5 * block)
+            pm = probe.read()
+            time.sleep(0.5 * block)
+            p1 = probe.read()
+            row[cond] = PmfwProbe.delta(p0, p1)
+            # the block's halves: a power state still settling after the switch shows here
+            halves = [(PmfwProbe.delta(p0, pm) or {}).get("power_w"), (PmfwProbe.delta(pm, p1) or {}).get("power_w")]
             if m0 is not None:  # what the exporter did in the block: parks, READs, PMFW busy
                 m1 = scrape_at(exp.sc)[0]
                 tot = lambda m, f: sum(v for _, v in m.get(f, []))  # noqa: E731
@@ -126,7 +131,8 @@ def idle_power(ctx, load, exp, a) -> dict:
                                "reads_per_s": round((tot(m1, "kgs_pmc_samples_total") - tot(m0, "kgs_pmc_samples_total")) / block, 1),
                                "pmfw_busy_pct": round(100 * (tot(m1, "amdgpu_pmfw_gfx_busy_seconds_total")
                                                               - tot(m0, "amdgpu_pmfw_gfx_busy_seconds_total")) / block, 3),
-                               "parked_at_end": tot(m1, "kgs_pmc_parked")})
+                               "parked_at_end": tot(m1, "kgs_pmc_parked"),
+                               "power_w": [None if w is None else round(w, 2) for w in halves]})
             D.cpu_barrier(ctx)
         local.append(row)
     if ctx.local_rank == 0 and exp is not None:

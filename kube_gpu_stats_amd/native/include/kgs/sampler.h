@@ -114,8 +114,8 @@ struct SamplerConfig {
   // the session and its 100 Hz quiet READs against the session released (r6b, bench
   // phase P).  After the device has been quiet (no wave, no MFMA cycle) for this long,
   // its counter thread STOPs the session and destroys the READ queue; it re-acquires
-  // when the PMFW table shows GFX busy again (≥ kUnparkBusyPct over one distinct
-  // PMFW interval), on a control-plane acquire, or on a refresh.  In between the
+  // when the PMFW table shows GFX busy again (≥ kUnparkBusyPct over kUnparkWindowS of
+  // table time), on a control-plane acquire, or on a refresh.  In between the
   // READ-immune utilisation is billed from the PMFW GFX busy — which no READ inflates
   // while parked.  0 = never (profiling mode never parks either).
   double pmc_quiet_release_s = 0.0;
@@ -142,11 +142,15 @@ constexpr double kMinIdleHz = 0.01;     // pmc_idle_hz: 0 (off) or at least this
 // window: at --pmc-idle-hz 0.01 that window is 300 s, and busy carried that long would
 // be billed into a later idle stretch — or a later pod.
 constexpr double kMaxUtilCarryS = 1.0;
-// A parked counter tier (SamplerConfig::pmc_quiet_release_s) re-acquires once one
-// distinct PMFW interval shows at least this GFX busy: an idle MI355X with nothing
-// READing it shows 0.07 % (r6b phase U, 10 Hz idle row); a 0.2 ms kernel in a 20 ms
-// table shows 1 %.
+// A parked counter tier (SamplerConfig::pmc_quiet_release_s) re-acquires once the PMFW
+// GFX busy over kUnparkWindowS of table time since the park settled reaches this: an
+// idle MI355X with nothing READing it shows 0.07 % (r6b phase U, 10 Hz idle row); 1 ms
+// of kernels in 100 ms shows 1 %.  Round 6's first rule, one distinct PMFW interval
+// ≥ 1 %, woke on stray blips (a 0.2 ms packet in a 20 ms table): r6g phase P un- and
+// re-parked in 2 of 6 parked blocks.  Whatever runs meanwhile is billed from the PMFW
+// busy, which nothing inflates while no READ runs.
 constexpr double kUnparkBusyPct = 1.0;
+constexpr double kUnparkWindowS = 0.1;
 
 // The counter tick's dithered offset from its fixed grid (SamplerConfig::tick_dither): a
 // random walk of at most `dither` of a period per tick, reflected into ± half a period.

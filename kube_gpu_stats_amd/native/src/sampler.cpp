@@ -603,6 +603,7 @@ void Sampler::run_pmc(Worker& w) {
   int64_t quiet_run_ns = 0;          // start of the current run of quiet drains (quiet release)
   int64_t park_ns = 0;               // when the session was last released for quiet
   int64_t unpark_retry_at_ns = 0;    // after a failed re-acquire of a parked device
+  double unpark_base_dt = -1, unpark_base_gfx = 0;  // start of the parked busy window
   // A fresh START restarts every count at 0: the interval from START to the first
   // READ is then counted exactly (acquire → first READ was dropped).
   auto started_at = [&](int64_t t) {
@@ -663,11 +664,21 @@ void Sampler::run_pmc(Worker& w) {
       bool wake = st.pmc_unpark_req.exchange(0, std::memory_order_relaxed) != 0;
       int64_t busy_ns = 0;
       GpuSample g;
-      // A distinct PMFW interval read after the release settled (the STOP and the queue
-      // teardown are CP work of their own) that shows GFX busy.
-      if (!wake && st.latest.load(g) && g.mono_ns > park_ns + 50000000LL && g.gfx_busy_window_pct >= kUnparkBusyPct) {
-        wake = true;
-        busy_ns = g.mono_ns;
+      // PMFW busy over a tumbling window of table time, from the first table read after
+      // the release settled (the STOP and the queue teardown are CP work of their own).
+      if (!wake && st.latest.load(g) && g.mono_ns > park_ns + 50000000LL && g.cum_dt_s > 0) {
+        if (unpark_base_dt < 0 || g.cum_dt_s < unpark_base_dt) {
+          unpark_base_dt = g.cum_dt_s;
+          unpark_base_gfx = g.cum_gfx_s;
+        } else if (g.cum_dt_s - unpark_base_dt >= kUnparkWindowS) {
+          const double pct = 100.0 * (g.cum_gfx_s - unpark_base_gfx) / (g.cum_dt_s - unpark_base_dt);
+          if (pct >= kUnparkBusyPct) {
+            wake = true;
+            busy_ns = g.mono_ns;
+          }
+          unpark_base_dt = g.cum_dt_s;
+          unpark_base_gfx = g.cum_gfx_s;
+        }
       }
       if (wake) {
         const int rc = src->acquire(dev);
@@ -838,6 +849,7 @@ void Sampler::run_pmc(Worker& w) {
           src->reset(dev);
           if (gone()) return;
           park_ns = mono_ns();
+          unpark_base_dt = -1;
           st.pmc_on.store(0);
           st.pmc_parked.store(1);
           st.pmc_parks.fetch_add(1, std::memory_order_relaxed);

@@ -967,8 +967,8 @@ def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
     """a programmed counter session keeps an idle MI355X ≈23 W above its
     released state (bench phase P, profiles/r6/r6b).  With --pmc-quiet-release-s the
     counter thread releases the session (STOP + READ queue destroyed) once the GPU has
-    been quiet that long, bills from the PMFW meanwhile, and re-acquires within one PMFW
-    interval of the PMFW showing GFX busy.  A 50 % square wave (1.5 s at 100 %, 1.5 s
+    been quiet that long, bills from the PMFW meanwhile, and re-acquires once the PMFW
+    shows GFX busy (≥ 1 % over 100 ms of table time).  A 50 % square wave (1.5 s at 100 %, 1.5 s
     idle): every idle half parks, every busy half unparks, and the billed integral over
     whole periods is the wave's 50 % — as without parking."""
     import urllib.request
@@ -1005,6 +1005,24 @@ def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
     with pytest.raises(ValueError):
         ex.pmc_quiet_release_s = -2
     assert ex.pmc_quiet_release_s == pytest.approx(0.1)
+
+
+def test_a_stray_blip_does_not_unpark(mock_exporter):
+    """r6g phase P: a parked GPU un- and re-parked in 2 of 6 idle blocks — one 20 ms PMFW
+    table ≥ 1 % busy (a 0.2 ms packet) was enough to re-acquire.  The wake-up now needs
+    ≥ 1 % over 100 ms of table time: 0.2 ms blips every 0.5 s leave the device parked."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100,
+                       pmc_quiet_release_s=0.2,
+                       mock={"util_base": 50, "util_amp": 50, "square_duty": 0.0004, "util_period_s": 0.5,
+                             "fw_period_s": 0.02})
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 3 and not ex.integrals(0)["pmc_parked"]:
+        time.sleep(0.02)
+    a = ex.integrals(0)
+    assert a["pmc_parked"] == 1, a
+    time.sleep(2.5)  # five blips
+    b = ex.integrals(0)
+    assert b["pmc_parked"] == 1 and b["pmc_parks"] == a["pmc_parks"], (a, b)
 
 
 def test_hand_over_while_parked_and_back(mock_exporter):
