@@ -114,8 +114,9 @@ struct SamplerConfig {
   // the session and its 100 Hz quiet READs against the session released (r6b, bench
   // phase P).  After the device has been quiet (no wave, no MFMA cycle) for this long,
   // its counter thread STOPs the session and destroys the READ queue; it re-acquires
-  // when the PMFW table shows GFX busy again (≥ kUnparkBusyPct over kUnparkWindowS of
-  // table time), on a control-plane acquire, or on a refresh.  In between the
+  // when the PMFW table shows GFX busy again (kUnparkTablePct in one interval, or
+  // kUnparkBusyPct over kUnparkWindowS of table time), on a control-plane acquire, or
+  // on a refresh.  In between the
   // READ-immune utilisation is billed from the PMFW GFX busy — which no READ inflates
   // while parked.  0 = never (profiling mode never parks either).
   double pmc_quiet_release_s = 0.0;
@@ -142,13 +143,15 @@ constexpr double kMinIdleHz = 0.01;     // pmc_idle_hz: 0 (off) or at least this
 // window: at --pmc-idle-hz 0.01 that window is 300 s, and busy carried that long would
 // be billed into a later idle stretch — or a later pod.
 constexpr double kMaxUtilCarryS = 1.0;
-// A parked counter tier (SamplerConfig::pmc_quiet_release_s) re-acquires once the PMFW
-// GFX busy over kUnparkWindowS of table time since the park settled reaches this: an
-// idle MI355X with nothing READing it shows 0.07 % (r6b phase U, 10 Hz idle row); 1 ms
-// of kernels in 100 ms shows 1 %.  Round 6's first rule, one distinct PMFW interval
-// ≥ 1 %, woke on stray blips (a 0.2 ms packet in a 20 ms table): r6g phase P un- and
-// re-parked in 2 of 6 parked blocks.  Whatever runs meanwhile is billed from the PMFW
-// busy, which nothing inflates while no READ runs.
+// A parked counter tier (SamplerConfig::pmc_quiet_release_s) re-acquires once one
+// distinct PMFW interval shows kUnparkTablePct GFX busy (a load starting: ≥ 2 ms of
+// kernels in a 20 ms table), or the busy over kUnparkWindowS of table time since the
+// park settled reaches kUnparkBusyPct (a trickle of work: an idle MI355X with nothing
+// READing it shows 0.07 %, r6b phase U 10 Hz idle row; 1 ms of kernels in 100 ms shows
+// 1 %).  Round 6's first rule, one interval ≥ 1 %, woke on stray blips (a 0.2 ms packet
+// in a 20 ms table): r6g phase P un- and re-parked in 2 of 6 parked blocks.  Whatever
+// runs meanwhile is billed from the PMFW busy, which nothing inflates while no READ runs.
+constexpr double kUnparkTablePct = 10.0;
 constexpr double kUnparkBusyPct = 1.0;
 constexpr double kUnparkWindowS = 0.1;
 

@@ -664,10 +664,14 @@ void Sampler::run_pmc(Worker& w) {
       bool wake = st.pmc_unpark_req.exchange(0, std::memory_order_relaxed) != 0;
       int64_t busy_ns = 0;
       GpuSample g;
-      // PMFW busy over a tumbling window of table time, from the first table read after
-      // the release settled (the STOP and the queue teardown are CP work of their own).
+      // PMFW busy in one interval, or over a tumbling window of table time, from the first
+      // table read after the release settled (the STOP and the queue teardown are CP work
+      // of their own).
       if (!wake && st.latest.load(g) && g.mono_ns > park_ns + 50000000LL && g.cum_dt_s > 0) {
-        if (unpark_base_dt < 0 || g.cum_dt_s < unpark_base_dt) {
+        if (g.gfx_busy_window_pct >= kUnparkTablePct) {
+          wake = true;
+          busy_ns = g.mono_ns;
+        } else if (unpark_base_dt < 0 || g.cum_dt_s < unpark_base_dt) {
           unpark_base_dt = g.cum_dt_s;
           unpark_base_gfx = g.cum_gfx_s;
         } else if (g.cum_dt_s - unpark_base_dt >= kUnparkWindowS) {

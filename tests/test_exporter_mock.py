@@ -968,7 +968,7 @@ def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
     released state (bench phase P, profiles/r6/r6b).  With --pmc-quiet-release-s the
     counter thread releases the session (STOP + READ queue destroyed) once the GPU has
     been quiet that long, bills from the PMFW meanwhile, and re-acquires once the PMFW
-    shows GFX busy (≥ 1 % over 100 ms of table time).  A 50 % square wave (1.5 s at 100 %, 1.5 s
+    shows a load starting (one table ≥ 10 % busy).  A 50 % square wave (1.5 s at 100 %, 1.5 s
     idle): every idle half parks, every busy half unparks, and the billed integral over
     whole periods is the wave's 50 % — as without parking."""
     import urllib.request
@@ -1010,7 +1010,8 @@ def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
 def test_a_stray_blip_does_not_unpark(mock_exporter):
     """r6g phase P: a parked GPU un- and re-parked in 2 of 6 idle blocks — one 20 ms PMFW
     table ≥ 1 % busy (a 0.2 ms packet) was enough to re-acquire.  The wake-up now needs
-    ≥ 1 % over 100 ms of table time: 0.2 ms blips every 0.5 s leave the device parked."""
+    ≥ 10 % in one table (a load starting) or ≥ 1 % over 100 ms of table time (a trickle):
+    0.2 ms blips every 0.5 s leave the device parked."""
     ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100,
                        pmc_quiet_release_s=0.2,
                        mock={"util_base": 50, "util_amp": 50, "square_duty": 0.0004, "util_period_s": 0.5,
