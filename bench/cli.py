@@ -84,10 +84,13 @@ def parse_args(argv=None):
                     help="phase S: tick rates above --hz to try under the load, one block each ('' = off)")
     ap.add_argument("--quiet-s", type=float, default=1.5,
                     help="phase Q: seconds of idle GPU per exporter mode (adaptive / profiling; 0 = off)")
-    ap.add_argument("--idle-power-s", type=float, default=48.0,
+    ap.add_argument("--idle-power-s", type=float, default=36.0,
                     help="phase P: seconds per condition (session programmed / released / parked by the quiet "
                     "release) of an idle GPU, in --idle-power-rounds rounds of every order (0 = off)")
     ap.add_argument("--idle-power-rounds", type=int, default=6)
+    ap.add_argument("--idle-power-settle-s", type=float, default=6.0,
+                    help="phase P: wait after each switch before measuring — an idle MI355X drops to its "
+                    "low-power state ≈5 s after its last GPU work (r6h)")
     ap.add_argument("--component-s", type=float, default=1.0,
                     help="phase K: seconds each load component runs alone while the exporter samples (0 = off)")
     ap.add_argument("--released", type=int, default=1, choices=[0, 1],

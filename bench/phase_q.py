@@ -76,8 +76,13 @@ def idle_power(ctx, load, exp, a) -> dict:
       having released the session by itself.
 
     Each rank reads its own GPU's socket power from the PMFW energy accumulator at the
-    block edges (PmfwProbe, not the exporter); per round, each condition is paired with
-    that round's ``released`` block: mean ± 95 % CI (``summary.quiet_gpu.power_w``)."""
+    block edges and halfway (PmfwProbe, not the exporter); per round, each condition is
+    paired with that round's ``released`` block: mean ± 95 % CI
+    (``summary.quiet_gpu.power_w``), and the same over the blocks' second halves
+    (``late``).  An idle MI355X sits at one of two levels, ≈291 W or ≈257 W (r6h), and
+    drops to the low one only ≈5 s after its last GPU work: measuring 1 s after the
+    switch (r6b-r6g) billed that lag to whichever condition followed the session, so
+    each block now starts --idle-power-settle-s after the switch."""
     secs = float(getattr(a, "idle_power_s", 0.0) or 0.0)
     rounds = int(getattr(a, "idle_power_rounds", 6) or 0)
     if secs <= 0 or rounds <= 0:
@@ -85,6 +90,8 @@ def idle_power(ctx, load, exp, a) -> dict:
     import itertools
 
     block = secs / rounds
+    # --mock: no power level to wait for
+    settle = min(1.0, 0.2 * block) if a.mock else float(getattr(a, "idle_power_settle_s", 6.0))
     # --mock: the orchestration on CPU (every rank, every barrier), against a constant
     # synthetic socket power — no power number of a mock run means anything
     probe = MockPowerProbe() if a.mock else PmfwProbe(load.pci_bdf(ctx.local_rank))
@@ -114,7 +121,7 @@ def idle_power(ctx, load, exp, a) -> dict:
                     exp.acquire()
                     parked_ok &= exp.wait_parked(1.0 if a.mock else 10.0)
             D.cpu_barrier(ctx)
-            time.sleep(min(1.0, 0.2 * block))  # settle: the power-state change after the switch
+            time.sleep(settle)  # the power-state change after the switch
             m0 = scrape_at(exp.sc)[0] if ctx.local_rank == 0 and exp is not None else None
             p0 = probe.read()
             time.sleep(0.5 * block)
@@ -124,6 +131,8 @@ def idle_power(ctx, load, exp, a) -> dict:
             row[cond] = PmfwProbe.delta(p0, p1)
             # the block's halves: a power state still settling after the switch shows here
             halves = [(PmfwProbe.delta(p0, pm) or {}).get("power_w"), (PmfwProbe.delta(pm, p1) or {}).get("power_w")]
+            if row[cond] is not None:
+                row[cond]["late_w"] = halves[1]
             if m0 is not None:  # what the exporter did in the block: parks, READs, PMFW busy
                 m1 = scrape_at(exp.sc)[0]
                 tot = lambda m, f: sum(v for _, v in m.get(f, []))  # noqa: E731
@@ -147,12 +156,16 @@ def idle_power(ctx, load, exp, a) -> dict:
             if ws:
                 one[f"{cond}_w"] = round(sum(ws) / len(ws), 2)
         for cond in ("session", "parked"):
-            d = [rd[cond]["power_w"] - rd["released"]["power_w"] for rd in rk if rd.get(cond) and rd.get("released")]
-            if d:
-                m, ci, sd = mean_ci95(d)
-                one[f"{cond}_minus_released_w"] = [round(m, 3), round(ci, 3)]
+            for key, tag in (("power_w", ""), ("late_w", "late_")):
+                d = [rd[cond][key] - rd["released"][key] for rd in rk
+                     if rd.get(cond) and rd.get("released") and rd[cond].get(key) is not None
+                     and rd["released"].get(key) is not None]
+                if d:
+                    m, ci, sd = mean_ci95(d)
+                    one[f"{cond}_minus_released_{tag}w"] = [round(m, 3), round(ci, 3)]
         per_rank.append(one)
-    out = {"secs_per_condition": secs, "rounds": rounds, "block_s": round(block, 2), "parked_reached": parked_ok,
+    out = {"secs_per_condition": secs, "rounds": rounds, "block_s": round(block, 2), "settle_s": settle,
+           "parked_reached": parked_ok,
            "conditions": {"session": "counter session programmed, quiet GPU READ at --pmc-idle-hz, no quiet release",
                           "released": "session STOPped and READ queue destroyed; PMFW / slow tiers sampling",
                           "parked": "the exporter's quiet release (1 s here) released the session by itself"},
@@ -165,8 +178,8 @@ def idle_power(ctx, load, exp, a) -> dict:
                 "reads_per_s": round(sum(b["reads_per_s"] for b in bl) / len(bl), 1),
                 "pmfw_busy_pct": round(sum(b["pmfw_busy_pct"] for b in bl) / len(bl), 3)}
     for cond in ("session", "parked"):
-        k = f"{cond}_minus_released_w"
-        vals = [p[k] for p in per_rank if k in p]
-        if vals:
-            out[k] = [round(sum(v[0] for v in vals) / len(vals), 3), round(max(v[1] for v in vals), 3)]
+        for k in (f"{cond}_minus_released_w", f"{cond}_minus_released_late_w"):
+            vals = [p[k] for p in per_rank if k in p]
+            if vals:
+                out[k] = [round(sum(v[0] for v in vals) / len(vals), 3), round(max(v[1] for v in vals), 3)]
     return out

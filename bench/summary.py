@@ -77,7 +77,9 @@ def summarize(res: dict) -> dict:
         if "session_minus_released_w" in ip:  # phase P: W above released (± 95 %), and the released W
             out["quiet_gpu"]["power_w"] = {"session": ip["session_minus_released_w"],
                                            "parked": ip.get("parked_minus_released_w"),
-                                           "released": (ip["per_rank"][0] or {}).get("released_w")}
+                                           "released": (ip["per_rank"][0] or {}).get("released_w"),
+                                           "late": [(ip.get("session_minus_released_late_w") or [None])[0],
+                                                    (ip.get("parked_minus_released_late_w") or [None])[0]]}
     br = (res.get("burst_resolution") or {}).get("per_gpu") or {}
     if br:
         out["bursts_resolved"] = [sum(v.get("segments", 0) for v in br.values()), sum(v.get("launched", 0) for v in br.values())]
