@@ -2,6 +2,7 @@
 phase P — what its counter session costs that GPU in socket power."""
 from __future__ import annotations
 
+import statistics
 import time
 
 from kube_gpu_stats_amd.parallel import dist as D
@@ -82,7 +83,10 @@ def idle_power(ctx, load, exp, a) -> dict:
     (``late``).  An idle MI355X sits at one of two levels, ≈291 W or ≈257 W (r6h), and
     drops to the low one only ≈5 s after its last GPU work: measuring 1 s after the
     switch (r6b-r6g) billed that lag to whichever condition followed the session, so
-    each block now starts --idle-power-settle-s after the switch."""
+    each block now starts --idle-power-settle-s after the switch.  A released GPU also
+    leaves the low level by itself now and then (r6i: 2 of 12 blocks, each with a
+    0.005 % PMFW busy blip that is not the exporter's), so the level difference is the
+    median of the paired second halves (``*_minus_released_median_w``)."""
     secs = float(getattr(a, "idle_power_s", 0.0) or 0.0)
     rounds = int(getattr(a, "idle_power_rounds", 6) or 0)
     if secs <= 0 or rounds <= 0:
@@ -163,6 +167,8 @@ def idle_power(ctx, load, exp, a) -> dict:
                 if d:
                     m, ci, sd = mean_ci95(d)
                     one[f"{cond}_minus_released_{tag}w"] = [round(m, 3), round(ci, 3)]
+                    if tag:  # the level: robust to a block caught in a stray excursion (r6i)
+                        one[f"{cond}_minus_released_median_w"] = round(statistics.median(d), 3)
         per_rank.append(one)
     out = {"secs_per_condition": secs, "rounds": rounds, "block_s": round(block, 2), "settle_s": settle,
            "parked_reached": parked_ok,
@@ -182,4 +188,8 @@ def idle_power(ctx, load, exp, a) -> dict:
             vals = [p[k] for p in per_rank if k in p]
             if vals:
                 out[k] = [round(sum(v[0] for v in vals) / len(vals), 3), round(max(v[1] for v in vals), 3)]
+        k = f"{cond}_minus_released_median_w"
+        vals = [p[k] for p in per_rank if k in p]
+        if vals:
+            out[k] = round(statistics.median(vals), 3)
     return out

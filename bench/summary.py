@@ -78,8 +78,8 @@ def summarize(res: dict) -> dict:
             out["quiet_gpu"]["power_w"] = {"session": ip["session_minus_released_w"],
                                            "parked": ip.get("parked_minus_released_w"),
                                            "released": (ip["per_rank"][0] or {}).get("released_w"),
-                                           "late": [(ip.get("session_minus_released_late_w") or [None])[0],
-                                                    (ip.get("parked_minus_released_late_w") or [None])[0]]}
+                                           "median": [ip.get("session_minus_released_median_w"),
+                                                      ip.get("parked_minus_released_median_w")]}
     br = (res.get("burst_resolution") or {}).get("per_gpu") or {}
     if br:
         out["bursts_resolved"] = [sum(v.get("segments", 0) for v in br.values()), sum(v.get("launched", 0) for v in br.values())]

@@ -81,8 +81,8 @@ def build_parser(ap: argparse.ArgumentParser | None = None) -> argparse.Argument
                                             "µs-kernel stream pays +0.5 %% at 1 kHz, +4 %% at 8 kHz (profiles/r4/ r4d)")
     add_flag(ap, "pmc-quiet-release-s", 30.0, "release the counter session (STOP, READ queue destroyed) after the "
                                                "GPU has been quiet this long, and bill it from the PMFW until the PMFW "
-                                               "shows GFX busy again: the session costs an idle MI355X ≈23 W "
-                                               "(bench phase P, r6b).  0 = never; ignored with --sm-util-source "
+                                               "shows GFX busy again: the session costs an idle MI355X ≈32 W "
+                                               "(bench phase P, r6h / r6i).  0 = never; ignored with --sm-util-source "
                                                "counters and in profiling mode")
     add_flag(ap, "pmc-cp-only-min", 0.3, "dispatch-bound READ rate: while the command processor dispatches with no "
                                          "wave in flight for at least this share of the clocks (a stream of µs "

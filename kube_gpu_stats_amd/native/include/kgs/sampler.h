@@ -110,9 +110,9 @@ struct SamplerConfig {
   double pmc_dispatch_hold_s = 0.010;
   double pmc_dispatch_hz = 500.0;
   // Quiet release ("parking").  A programmed perfmon session and a mapped READ queue
-  // keep an idle MI355X out of its low-power state: +22.7 ± 11.1 W per idle GPU with
-  // the session and its 100 Hz quiet READs against the session released (r6b, bench
-  // phase P).  After the device has been quiet (no wave, no MFMA cycle) for this long,
+  // keep an idle MI355X out of its low-power state: ≈291 W against ≈258 W, +32 … +35 W
+  // per idle GPU with the session and its 100 Hz quiet READs against the session
+  // released (bench phase P, r6h / r6i; the level drops ≈5 s after the last GPU work).  After the device has been quiet (no wave, no MFMA cycle) for this long,
   // its counter thread STOPs the session and destroys the READ queue; it re-acquires
   // when the PMFW table shows GFX busy again (kUnparkTablePct in one interval, or
   // kUnparkBusyPct over kUnparkWindowS of table time), on a control-plane acquire, or

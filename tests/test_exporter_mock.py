@@ -964,7 +964,7 @@ def test_counter_stream_marks_stale_drains_and_rates_mfma_between_fresh_ones(moc
 
 
 def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
-    """a programmed counter session keeps an idle MI355X ≈23 W above its
+    """a programmed counter session keeps an idle MI355X ≈32 W above its
     released state (bench phase P, profiles/r6/r6b).  With --pmc-quiet-release-s the
     counter thread releases the session (STOP + READ queue destroyed) once the GPU has
     been quiet that long, bills from the PMFW meanwhile, and re-acquires once the PMFW
