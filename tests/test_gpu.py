@@ -1531,7 +1531,9 @@ def test_sm_util_is_read_immune_at_khz_rates(torch_dev, tmp_path):
     for hz in (8000, 1000):
         idle, sat = rows[f"{hz}/idle"], rows[f"{hz}/mfma_saturating"]
         bound(f"read_immune_idle_busy_pct[{hz}]", idle["busy_counter_pct"], hi=1.0, ctx=idle)
-        bound(f"read_immune_saturated_busy_pct[{hz}]", sat["busy_counter_pct"], lo=95.0, ctx=sat)
+        # a saturated GPU read 97.75-99.45 % over six boxes (profiles/gpu_test_margins.md):
+        # 93 keeps twice that spread between the bound and the lowest
+        bound(f"read_immune_saturated_busy_pct[{hz}]", sat["busy_counter_pct"], lo=93.0, ctx=sat)
         for name in ("burst_1ms_every_5ms", "burst_0.2ms_every_1ms"):
             r = rows[f"{hz}/{name}"]
             bound(f"read_immune_abs_err_pts[{hz}/{name}]", abs(r["error_pts"]), hi=3.0, ctx=r)
