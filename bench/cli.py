@@ -88,6 +88,9 @@ def parse_args(argv=None):
                     help="phase P: seconds per condition (session programmed / released / parked by the quiet "
                     "release) of an idle GPU, in --idle-power-rounds rounds of every order (0 = off)")
     ap.add_argument("--idle-power-rounds", type=int, default=6)
+    ap.add_argument("--idle-power-absent", type=int, default=0, choices=[0, 1],
+                    help="phase P: a fourth condition, 'absent' — session released and every sampling tier "
+                    "paused, so nothing of the exporter touches the GPU")
     ap.add_argument("--idle-power-settle-s", type=float, default=6.0,
                     help="phase P: wait after each switch before measuring — an idle MI355X drops to its "
                     "low-power state ≈5 s after its last GPU work (r6h)")

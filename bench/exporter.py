@@ -286,4 +286,6 @@ class PmfwProbe:
         dc = b["accumulation_counter"] - a["accumulation_counter"]
         if dc > 0 and b["ppt_residency_acc"] >= a["ppt_residency_acc"]:
             out["ppt_pct"] = 100.0 * (b["ppt_residency_acc"] - a["ppt_residency_acc"]) / dc
+        if dc > 0 and b.get("gfx_activity_acc", -1) >= a.get("gfx_activity_acc", 0) >= 0:
+            out["gfx_busy_pct"] = (b["gfx_activity_acc"] - a["gfx_activity_acc"]) / dc  # % per tick
         return out

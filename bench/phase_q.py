@@ -74,7 +74,10 @@ def idle_power(ctx, load, exp, a) -> dict:
     * ``released`` — the session STOPped and the READ queue destroyed while the PMFW and
       slow tiers keep sampling (the neutral base);
     * ``parked``   — the exporter's quiet release (--pmc-quiet-release-s, here 1 s)
-      having released the session by itself.
+      having released the session by itself;
+    * ``absent``   — (--idle-power-absent 1) released and every sampling tier paused:
+      nothing of the exporter touches the GPU.  Four conditions run in a Williams
+      square (each order of neighbours once per four rounds).
 
     Each rank reads its own GPU's socket power from the PMFW energy accumulator at the
     block edges and halfway (PmfwProbe, not the exporter); per round, each condition is
@@ -101,8 +104,14 @@ def idle_power(ctx, load, exp, a) -> dict:
     probe = MockPowerProbe() if a.mock else PmfwProbe(load.pci_bdf(ctx.local_rank))
     if probe.N is None:
         return {"skipped": "no PMFW table probe"}
-    conds = ("session", "released", "parked")
-    perms = list(itertools.permutations(conds))
+    if int(getattr(a, "idle_power_absent", 0) or 0):
+        conds: tuple = ("session", "released", "parked", "absent")
+        perms = [("session", "released", "absent", "parked"), ("released", "parked", "session", "absent"),
+                 ("parked", "absent", "released", "session"), ("absent", "session", "parked", "released")]
+    else:
+        conds = ("session", "released", "parked")
+        perms = list(itertools.permutations(conds))
+    paused = False
     D.cpu_barrier(ctx)
     load.sync()
     default_qr = exp.set_quiet_release(-1) if ctx.local_rank == 0 and exp is not None else 0.0
@@ -114,9 +123,15 @@ def idle_power(ctx, load, exp, a) -> dict:
         progress(ctx, f"phase P round {r + 1}/{rounds}")
         for cond in perms[r % len(perms)]:
             if ctx.local_rank == 0 and exp is not None:
-                if cond == "released":
+                if paused:
+                    exp.resume()
+                    paused = False
+                if cond in ("released", "absent"):
                     exp.set_quiet_release(0)
                     exp.release(drop_queue=True)
+                    if cond == "absent":
+                        exp.pause()
+                        paused = True
                 elif cond == "session":
                     exp.set_quiet_release(0)
                     exp.acquire()
@@ -145,10 +160,14 @@ def idle_power(ctx, load, exp, a) -> dict:
                                "pmfw_busy_pct": round(100 * (tot(m1, "amdgpu_pmfw_gfx_busy_seconds_total")
                                                               - tot(m0, "amdgpu_pmfw_gfx_busy_seconds_total")) / block, 3),
                                "parked_at_end": tot(m1, "kgs_pmc_parked"),
-                               "power_w": [None if w is None else round(w, 2) for w in halves]})
+                               "power_w": [None if w is None else round(w, 2) for w in halves],
+                               "probe_gfx_busy_pct": (None if row[cond] is None or "gfx_busy_pct" not in row[cond]
+                                                      else round(row[cond]["gfx_busy_pct"], 4))})
             D.cpu_barrier(ctx)
         local.append(row)
     if ctx.local_rank == 0 and exp is not None:
+        if paused:
+            exp.resume()
         exp.set_quiet_release(default_qr)
         exp.acquire()
     ranks = D.all_gather_object(ctx, local)
@@ -159,7 +178,7 @@ def idle_power(ctx, load, exp, a) -> dict:
             ws = [rd[cond]["power_w"] for rd in rk if rd.get(cond)]
             if ws:
                 one[f"{cond}_w"] = round(sum(ws) / len(ws), 2)
-        for cond in ("session", "parked"):
+        for cond in (c for c in conds if c != "released"):
             for key, tag in (("power_w", ""), ("late_w", "late_")):
                 d = [rd[cond][key] - rd["released"][key] for rd in rk
                      if rd.get(cond) and rd.get("released") and rd[cond].get(key) is not None
@@ -174,7 +193,8 @@ def idle_power(ctx, load, exp, a) -> dict:
            "parked_reached": parked_ok,
            "conditions": {"session": "counter session programmed, quiet GPU READ at --pmc-idle-hz, no quiet release",
                           "released": "session STOPped and READ queue destroyed; PMFW / slow tiers sampling",
-                          "parked": "the exporter's quiet release (1 s here) released the session by itself"},
+                          "parked": "the exporter's quiet release (1 s here) released the session by itself",
+                          "absent": "released, and every sampling tier paused"},
            "per_rank": per_rank, "blocks": blocks}
     for cond in conds:
         bl = [b for b in blocks if b["cond"] == cond]
@@ -183,7 +203,7 @@ def idle_power(ctx, load, exp, a) -> dict:
                 "parks_per_block": round(sum(b["parks"] for b in bl) / len(bl), 2),
                 "reads_per_s": round(sum(b["reads_per_s"] for b in bl) / len(bl), 1),
                 "pmfw_busy_pct": round(sum(b["pmfw_busy_pct"] for b in bl) / len(bl), 3)}
-    for cond in ("session", "parked"):
+    for cond in (c for c in conds if c != "released"):
         for k in (f"{cond}_minus_released_w", f"{cond}_minus_released_late_w"):
             vals = [p[k] for p in per_rank if k in p]
             if vals:

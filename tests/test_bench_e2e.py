@@ -187,7 +187,7 @@ def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads(tmp_path):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "bench.py", "--mock", "--gpus", "8", "--steps", "4", "--warmup", "1",
                         *FAST, "--hz", "2000", "--capacity-hz", "", "--burst-s", "0", "--quiet-s", "0", *POWER,
-                        "--out", str(tmp_path / "bench.json")],
+                        "--idle-power-absent", "1", "--out", str(tmp_path / "bench.json")],
                        cwd=REPO, capture_output=True, text=True, timeout=420, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     line, res = _result(r.stdout)
@@ -203,7 +203,12 @@ def test_bench_8_ranks_xgmi_link_map_and_per_rank_overheads(tmp_path):
                                                                             if i != j]
     for p in x["per_copy"]:
         assert p["src"]["link_peer_bdf"] == p["peer_bdf"] and p["dst"]["ok"], p
-    assert len(res["quiet_gpu"]["idle_power"]["per_rank"]) == 8  # phase P: every rank's own probe
+    ip = res["quiet_gpu"]["idle_power"]
+    assert len(ip["per_rank"]) == 8  # phase P: every rank's own probe
+    # the fourth condition, "absent" (every tier paused), in a Williams square
+    assert [b["cond"] for b in ip["blocks"]] == ["session", "released", "absent", "parked",
+                                                 "released", "parked", "session", "absent"], ip["blocks"]
+    assert ip["exporter_by_condition"]["absent"]["reads_per_s"] == 0 and "absent_minus_released_w" in ip
     for hz in ("100", "2000"):
         t = res["interleaved"]["tiers"][hz]
         assert [q["rank"] for q in t["overhead_by_rank"]] == list(range(8))
