@@ -118,6 +118,7 @@ for s in $STEPS; do
     powerabs) run powerabs 720 python -u bench.py --steps 5 --warmup 2 --rounds 0 --burst-s 0 --capacity-hz "" \
                 --quiet-s 0 --component-s 0 --util-s 0 --idle-power-s 64 --idle-power-rounds 8 --idle-power-absent 1 \
                 --out "$OUT/powerabs.json" ;;
+    tierprobe) run idle_tier 600 python -u tools/idle_tier_probe.py --out "$OUT/idle_tier_probe.json" ;;
     kfdprobe) run kfd_proc 120 python -u tools/kfd_proc_probe.py --out "$OUT/kfd_proc.json" ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
