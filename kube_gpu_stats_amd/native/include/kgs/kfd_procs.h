@@ -23,6 +23,7 @@
 
 #include <cstdint>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "kgs/backend.h"
@@ -31,10 +32,28 @@ namespace kgs {
 
 constexpr const char* kKfdProcRoot = "/sys/class/kfd/kfd/proc";
 
+// The DRM fds each process held at its last full /proc/<pid>/fd walk.  The walk is one
+// readlink per fd — 5.6 ms for a process holding 2000 (data loaders, sockets, shards) —
+// so it repeats at most every kDrmRescanNs per process; in between only the remembered
+// fds are checked (still a /dev/dri link) and their fdinfo read, and any that is not
+// forces a new walk.  A DRM fd opened after the walk counts from the next one.  One
+// cache per calling thread (the per-GPU slow thread); pids gone are dropped.
+struct DrmFdCache {
+  struct Ent {
+    std::vector<std::string> fds;
+    int64_t scan_ns = 0;
+  };
+  std::unordered_map<uint32_t, Ent> by_pid;
+  uint64_t walks = 0;  // full fd-directory walks (tests)
+};
+constexpr int64_t kDrmRescanNs = 10000000000LL;
+
 // Every process with a KFD context on GPU `gpu_id` (KFD topology gpu_id): 0 with `out`
 // filled, or -1 if kfd_root cannot be listed (no KFD sysfs: the caller falls back).
-// `bdf` ("0000:75:00.0") selects the fdinfo entries of this GPU's render node.
+// `bdf` ("0000:75:00.0") selects the fdinfo entries of this GPU's render node; `cache`
+// (optional, with the caller's monotonic `now_ns`) spares the fd walks.
 int read_kfd_procs(const std::string& kfd_root, const std::string& proc_root, uint64_t gpu_id,
-                   const std::string& bdf, std::vector<ProcInfo>& out);
+                   const std::string& bdf, std::vector<ProcInfo>& out, DrmFdCache* cache = nullptr,
+                   int64_t now_ns = 0);
 
 }  // namespace kgs

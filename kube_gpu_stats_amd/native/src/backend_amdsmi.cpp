@@ -57,6 +57,7 @@ struct Dev {
   bool partitioned = false;  // a DPX/QPX/CPX partition: restrict the table to its XCCs
   uint64_t ecc_mask = 0;     // blocks with ECC enabled (read once, slow thread only)
   bool ecc_mask_read = false;
+  DrmFdCache fd_cache;       // per-process DRM fds (slow thread only)
   alignas(64) uint8_t buf[4096];
 };
 
@@ -155,7 +156,9 @@ class AmdSmiBackend final : public Backend {
     // SMI lock, and a per-process flag when the CU occupancy cannot be read
     // (kgs/kfd_procs.h).  AMD SMI only where the KFD sysfs cannot be listed.
     const DeviceInfo& in = devs_[d]->info;
-    if (in.kfd_gpu_id && read_kfd_procs(kKfdProcRoot, "/proc", in.kfd_gpu_id, in.bdf, out) == 0) return 0;
+    if (in.kfd_gpu_id &&
+        read_kfd_procs(kKfdProcRoot, "/proc", in.kfd_gpu_id, in.bdf, out, &devs_[d]->fd_cache, now_ns(CLOCK_MONOTONIC)) == 0)
+      return 0;
     std::vector<amdsmi_proc_info_t> list;
     uint32_t cap = 0;
     {

@@ -690,11 +690,18 @@ PYBIND11_MODULE(_kgs_native, m) {
       .def("drop_carry", &UtilBiller::drop_carry, "The GPU changed hands: drop the busy still carried");
   m.attr("MAX_UTIL_CARRY_S") = kMaxUtilCarryS;
   m.def("parse_gpu_metrics_v1_8", &parse_metrics_blob, "Parse a raw PMFW gpu_metrics v1.8 table");
+  py::class_<DrmFdCache>(m, "DrmFdCache", "Per-process DRM fds between /proc/<pid>/fd walks (kgs/kfd_procs.h)")
+      .def(py::init<>())
+      .def_readonly("walks", &DrmFdCache::walks)
+      .def_property_readonly("pids", [](const DrmFdCache& c) { return c.by_pid.size(); });
+  m.attr("DRM_RESCAN_S") = kDrmRescanNs * 1e-9;
   m.def(
       "read_kfd_procs",
-      [](const std::string& kfd_root, const std::string& proc_root, uint64_t gpu_id, const std::string& bdf) {
+      [](const std::string& kfd_root, const std::string& proc_root, uint64_t gpu_id, const std::string& bdf,
+         DrmFdCache* cache, double now_s) {
         std::vector<ProcInfo> v;
-        if (read_kfd_procs(kfd_root, proc_root, gpu_id, bdf, v) != 0) return py::object(py::none());
+        if (read_kfd_procs(kfd_root, proc_root, gpu_id, bdf, v, cache, static_cast<int64_t>(now_s * 1e9)) != 0)
+          return py::object(py::none());
         py::list l;
         for (const ProcInfo& x : v) {
           py::dict o;
@@ -711,8 +718,10 @@ PYBIND11_MODULE(_kgs_native, m) {
         }
         return py::object(l);
       },
-      py::arg("kfd_root"), py::arg("proc_root"), py::arg("gpu_id"), py::arg("bdf"),
-      "The processes with a KFD context on gpu_id, from the KFD sysfs + DRM fdinfo (None: no KFD root)");
+      py::arg("kfd_root"), py::arg("proc_root"), py::arg("gpu_id"), py::arg("bdf"), py::arg("cache") = nullptr,
+      py::arg("now_s") = 0.0,
+      "The processes with a KFD context on gpu_id, from the KFD sysfs + DRM fdinfo (None: no KFD root); with a "
+      "DrmFdCache, a process's fd directory is walked at most every DRM_RESCAN_S of now_s");
   m.def("gpu_type_from_market_name", &gpu_type_from_market_name);
   m.def("pmc_counter_names", [] {
     std::vector<std::string> v;

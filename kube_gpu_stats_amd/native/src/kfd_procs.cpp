@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
 #include <set>
 
 namespace kgs {
@@ -59,23 +60,47 @@ uint64_t scaled(const char* v) {
   return x;
 }
 
+bool is_drm_fd(const std::string& fd_path) {
+  char link[256];
+  const ssize_t n = readlink(fd_path.c_str(), link, sizeof link - 1);
+  if (n <= 0) return false;
+  link[n] = 0;
+  return std::strncmp(link, "/dev/dri/", 9) == 0;
+}
+
+// The DRM fds of `pid` (names under /proc/<pid>/fd): the cached list while it is fresh
+// and every fd in it still a DRM link, else a full walk (kgs/kfd_procs.h DrmFdCache).
+std::vector<std::string> drm_fds(const std::string& fd_dir, uint32_t pid, DrmFdCache* cache, int64_t now_ns) {
+  if (cache) {
+    auto it = cache->by_pid.find(pid);
+    if (it != cache->by_pid.end() && now_ns - it->second.scan_ns < kDrmRescanNs) {
+      bool ok = true;
+      for (const std::string& fd : it->second.fds) ok = ok && is_drm_fd(fd_dir + "/" + fd);
+      if (ok) return it->second.fds;
+    }
+  }
+  std::vector<std::string> fds;
+  DIR* d = opendir(fd_dir.c_str());
+  if (!d) return fds;
+  while (dirent* e = readdir(d))
+    if (all_digits(e->d_name) && is_drm_fd(fd_dir + "/" + e->d_name)) fds.emplace_back(e->d_name);
+  closedir(d);
+  if (cache) {
+    ++cache->walks;
+    cache->by_pid[pid] = DrmFdCache::Ent{fds, now_ns};
+  }
+  return fds;
+}
+
 // The DRM clients of `pid` on the render node at `bdf`: Σ GTT / CPU bytes and gfx
 // engine ns over distinct drm-client-ids (dup'd fds share one client).
-void drm_fdinfo(const std::string& proc_root, uint32_t pid, const std::string& bdf, ProcInfo& p) {
-  const std::string fd_dir = proc_root + "/" + std::to_string(pid) + "/fd";
-  DIR* d = opendir(fd_dir.c_str());
-  if (!d) return;
+void drm_fdinfo(const std::string& proc_root, uint32_t pid, const std::string& bdf, ProcInfo& p, DrmFdCache* cache,
+                int64_t now_ns) {
+  const std::string pid_dir = proc_root + "/" + std::to_string(pid);
   std::set<uint64_t> seen;
-  char link[256];
   char buf[4096];
-  while (dirent* e = readdir(d)) {
-    if (!all_digits(e->d_name)) continue;
-    const std::string fd_path = fd_dir + "/" + e->d_name;
-    const ssize_t n = readlink(fd_path.c_str(), link, sizeof link - 1);
-    if (n <= 0) continue;
-    link[n] = 0;
-    if (std::strncmp(link, "/dev/dri/", 9) != 0) continue;
-    if (!slurp(proc_root + "/" + std::to_string(pid) + "/fdinfo/" + e->d_name, buf, sizeof buf)) continue;
+  for (const std::string& fd : drm_fds(pid_dir + "/fd", pid, cache, now_ns)) {
+    if (!slurp(pid_dir + "/fdinfo/" + fd, buf, sizeof buf)) continue;
     bool ours = false;
     uint64_t client = ~0ull, gtt = 0, cpu = 0, gfx = 0;
     char* save = nullptr;  // strtok_r: one slow thread per GPU runs this at once
@@ -97,13 +122,12 @@ void drm_fdinfo(const std::string& proc_root, uint32_t pid, const std::string& b
     p.cpu_bytes += cpu;
     p.gfx_ns += gfx;
   }
-  closedir(d);
 }
 
 }  // namespace
 
 int read_kfd_procs(const std::string& kfd_root, const std::string& proc_root, uint64_t gpu_id,
-                   const std::string& bdf, std::vector<ProcInfo>& out) {
+                   const std::string& bdf, std::vector<ProcInfo>& out, DrmFdCache* cache, int64_t now_ns) {
   out.clear();
   DIR* d = opendir(kfd_root.c_str());
   if (!d) return -1;
@@ -131,9 +155,15 @@ int read_kfd_procs(const std::string& kfd_root, const std::string& proc_root, ui
       while (n > 0 && (comm[n - 1] == '\n' || comm[n - 1] == 0)) --n;
       p.name.assign(comm, n);
     }
-    drm_fdinfo(proc_root, pid, bdf, p);
+    drm_fdinfo(proc_root, pid, bdf, p, cache, now_ns);
     out.push_back(std::move(p));
   }
+  if (cache)  // forget the processes that left this GPU
+    for (auto it = cache->by_pid.begin(); it != cache->by_pid.end();) {
+      bool here = false;
+      for (const ProcInfo& q : out) here = here || q.pid == it->first;
+      it = here ? std::next(it) : cache->by_pid.erase(it);
+    }
   return 0;
 }
 

@@ -1180,9 +1180,12 @@ static void test_kfd_procs_concurrent() {
     th.emplace_back([&, g] {
       char bdf[32];
       std::snprintf(bdf, sizeof bdf, "0000:%02x:00.0", g);
+      DrmFdCache cache;  // one per thread, as one per GPU slow thread
       for (int it = 0; it < 50; ++it) {
         std::vector<ProcInfo> v;
-        if (read_kfd_procs(kfd, proc, static_cast<uint64_t>(g), bdf, v) != 0 || v.size() != 8) ++bad;
+        if (read_kfd_procs(kfd, proc, static_cast<uint64_t>(g), bdf, v, it % 2 ? &cache : nullptr, it * 1000000LL) != 0 ||
+            v.size() != 8)
+          ++bad;
         for (const ProcInfo& p : v)
           if (p.vram_bytes != (static_cast<uint64_t>(g) << 20) || p.gtt_bytes != 4096 || p.gfx_ns != 100 || !p.cu_valid)
             ++bad;

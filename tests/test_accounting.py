@@ -430,3 +430,41 @@ def test_kfd_sysfs_process_reader(N, tmp_path):
     assert a["gfx_ns"] == 15483
     assert b["cu_valid"] is False and b["cu_occupancy"] == 0 and b["name"] == "" and b["gtt_bytes"] == 0
     assert N.read_kfd_procs(str(tmp_path / "absent"), str(proc), gid, "0000:75:00.0") is None
+
+
+def test_kfd_reader_walks_a_process_fd_directory_at_most_every_10s(N, tmp_path):
+    """A process holding thousands of fds cost the per-process tier one readlink each per
+    poll (5.6 ms at 2000 fds).  With the slow thread's DrmFdCache the /proc/<pid>/fd walk
+    repeats only every DRM_RESCAN_S; in between the remembered DRM fds' fdinfo are read
+    (values still current), a remembered fd that stopped being a DRM link forces a walk,
+    and a process that left the GPU is forgotten."""
+    import os as _os
+
+    kfd, proc = tmp_path / "kfd", tmp_path / "proc"
+    gid = 7
+    (kfd / "201").mkdir(parents=True)
+    (kfd / "201" / f"vram_{gid}").write_text("4096\n")
+    p = proc / "201"
+    (p / "fd").mkdir(parents=True)
+    (p / "fdinfo").mkdir()
+    for i in range(50):
+        _os.symlink("/tmp/data.bin", p / "fd" / str(100 + i))
+    _os.symlink("/dev/dri/renderD128", p / "fd" / "5")
+
+    def info(ns):
+        (p / "fdinfo" / "5").write_text(f"drm-client-id:\t3\ndrm-pdev:\t0000:75:00.0\ndrm-engine-gfx:\t{ns} ns\n")
+
+    info(100)
+    c = N.DrmFdCache()
+    read = lambda t: N.read_kfd_procs(str(kfd), str(proc), gid, "0000:75:00.0", c, t)[0]  # noqa: E731
+    assert read(1.0)["gfx_ns"] == 100 and c.walks == 1
+    info(250)
+    assert read(2.0)["gfx_ns"] == 250 and c.walks == 1          # fdinfo re-read, no walk
+    assert read(1.0 + N.DRM_RESCAN_S)["gfx_ns"] == 250 and c.walks == 2  # the periodic walk
+    (p / "fd" / "5").unlink()                                     # fd 5 closed and reused for a file
+    _os.symlink("/tmp/other.bin", p / "fd" / "5")
+    _os.symlink("/dev/dri/renderD128", p / "fd" / "7")
+    (p / "fdinfo" / "7").write_text("drm-client-id:\t4\ndrm-pdev:\t0000:75:00.0\ndrm-engine-gfx:\t9 ns\n")
+    assert read(12.0)["gfx_ns"] == 9 and c.walks == 3              # stale entry: walked again at once
+    (kfd / "201" / f"vram_{gid}").unlink()                         # the process left this GPU
+    assert N.read_kfd_procs(str(kfd), str(proc), gid, "0000:75:00.0", c, 13.0) == [] and c.pids == 0
