@@ -661,7 +661,11 @@ void Sampler::run_pmc(Worker& w) {
     }
     // ---- quiet release ended: PMFW busy again, or the control plane asked -----
     if (want && st.pmc_parked.load(std::memory_order_relaxed) && mono_ns() >= unpark_retry_at_ns) {
-      bool wake = st.pmc_unpark_req.exchange(0, std::memory_order_relaxed) != 0;
+      // ... or parking is off now: the quiet release set to 0, or profiling mode (every
+      // tick READ) switched on while parked.
+      bool wake = st.pmc_unpark_req.exchange(0, std::memory_order_relaxed) != 0 ||
+                  !(pmc_quiet_release_s_.load(std::memory_order_relaxed) > 0) ||
+                  !(pmc_idle_hz_.load(std::memory_order_relaxed) > 0);
       int64_t busy_ns = 0;
       GpuSample g;
       // PMFW busy in one interval, or over a tumbling window of table time, from the first

@@ -1029,7 +1029,8 @@ def test_a_stray_blip_does_not_unpark(mock_exporter):
 def test_hand_over_while_parked_and_back(mock_exporter):
     """A device parked by the quiet release can be handed over (kgs pmc release: nothing is
     held, the hand-over stands) and acquired back at once by the control plane, whatever
-    the load (an explicit acquire ends a park without waiting for PMFW busy)."""
+    the load (an explicit acquire ends a park without waiting for PMFW busy); switching
+    parking off while parked (quiet release 0, or profiling mode) re-acquires too."""
     ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100,
                        pmc_quiet_release_s=0.2, mock={"util_base": 0, "util_amp": 0})
     t0 = time.monotonic()
@@ -1049,3 +1050,16 @@ def test_hand_over_while_parked_and_back(mock_exporter):
     n = i["pmc_samples"]
     time.sleep(0.3)
     assert ex.integrals(0)["pmc_samples"] > n  # drains again (at the idle rate)
+    # parking switched off while parked — the quiet release set to 0, or profiling mode
+    # on — re-acquires at once, whatever the load
+    for switch_off in (lambda: setattr(ex, "pmc_quiet_release_s", 0), lambda: setattr(ex, "pmc_idle_hz", 0)):
+        ex.pmc_idle_hz = 100
+        ex.pmc_quiet_release_s = 0.2
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < 3 and not ex.integrals(0)["pmc_parked"]:
+            time.sleep(0.02)
+        assert ex.integrals(0)["pmc_parked"] == 1
+        switch_off()
+        time.sleep(0.2)
+        i = ex.integrals(0)
+        assert i["pmc_parked"] == 0 and i["pmc_on"] == 1, i
