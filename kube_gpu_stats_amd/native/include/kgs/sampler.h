@@ -112,13 +112,14 @@ struct SamplerConfig {
   // Quiet release ("parking").  A programmed perfmon session and a mapped READ queue
   // keep an idle MI355X out of its low-power state: ≈291 W against ≈258 W, +32 … +35 W
   // per idle GPU with the session and its 100 Hz quiet READs against the session
-  // released (bench phase P, r6h / r6i; the level drops ≈5 s after the last GPU work).  After the device has been quiet (no wave, no MFMA cycle) for this long,
-  // its counter thread STOPs the session and destroys the READ queue; it re-acquires
-  // when the PMFW table shows GFX busy again (kUnparkTablePct in one interval, or
-  // kUnparkBusyPct over kUnparkWindowS of table time), on a control-plane acquire, or
-  // on a refresh.  In between the
-  // READ-immune utilisation is billed from the PMFW GFX busy — which no READ inflates
-  // while parked.  0 = never (profiling mode never parks either).
+  // released (bench phase P, r6h / r6i; the level drops ≈5 s after the last GPU work).
+  // After the device has been quiet (no wave, no MFMA cycle) for this long, its counter
+  // thread STOPs the session and destroys the READ queue; it re-acquires when the PMFW
+  // table shows GFX busy again (kUnparkTablePct in one interval, or kUnparkBusyPct over
+  // kUnparkWindowS of table time), on a control-plane acquire, or when parking is
+  // switched off (this set to 0, or profiling mode).  In between the READ-immune
+  // utilisation is billed from the PMFW GFX busy — which no READ inflates while parked.
+  // 0 = never (profiling mode never parks either).
   double pmc_quiet_release_s = 0.0;
   int max_backoff_ms = 1000;   // while a device keeps failing
   std::vector<int> devices;    // subset to sample (empty = all)
