@@ -119,6 +119,10 @@ for s in $STEPS; do
                 --quiet-s 0 --component-s 0 --util-s 0 --idle-power-s 64 --idle-power-rounds 8 --idle-power-absent 1 \
                 --out "$OUT/powerabs.json" ;;
     tierprobe) run idle_tier 600 python -u tools/idle_tier_probe.py --out "$OUT/idle_tier_probe.json" ;;
+    useeds) for s in 1 2 3 4 5 6 7 8; do
+              run useed_$s 240 python -u bench.py --steps 3 --warmup 1 --rounds 0 --burst-s 0 --capacity-hz "" \
+                --quiet-s 0 --component-s 0 --idle-power-s 0 --util-hz 10 --util-seed $s --out "$OUT/useed_$s.json" || break
+            done ;;
     kfdprobe) run kfd_proc 120 python -u tools/kfd_proc_probe.py --out "$OUT/kfd_proc.json" ;;
     wedge) run pytest_wedge 150 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              -p no:cacheprovider -k wedged_counter_queue ;;
