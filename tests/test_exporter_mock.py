@@ -1026,6 +1026,29 @@ def test_a_stray_blip_does_not_unpark(mock_exporter):
     assert b["pmc_parked"] == 1 and b["pmc_parks"] == a["pmc_parks"], (a, b)
 
 
+@pytest.mark.parametrize("floor,wakes", [(2.0, True), (0.5, False)])
+def test_a_trickle_unparks_over_100ms(mock_exporter, floor, wakes):
+    """The parked tier's slow wake-up path: no PMFW table reaches 10 %, but a steady
+    trickle of GFX busy (the mock PMFW reads `floor` % while the counters see no wave)
+    re-acquires once 100 ms of table time average ≥ 1 % — and the GPU, still quiet to the
+    counters, parks again; below 1 % it stays parked."""
+    ex = mock_exporter(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100,
+                       pmc_quiet_release_s=0.2,
+                       mock={"util_base": 0, "util_amp": 0, "square_duty": 0.5, "util_period_s": 1.0,
+                             "pmfw_busy_floor": floor, "fw_period_s": 0.02})
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 3 and not ex.integrals(0)["pmc_parks"]:
+        time.sleep(0.02)
+    a = ex.integrals(0)
+    assert a["pmc_parks"] >= 1, a
+    time.sleep(1.5)
+    b = ex.integrals(0)
+    if wakes:
+        assert b["pmc_parks"] - a["pmc_parks"] >= 2, (a, b)  # woke (≈0.1 s) and parked again (0.2 s quiet), repeatedly
+    else:
+        assert b["pmc_parks"] == a["pmc_parks"] and b["pmc_parked"] == 1, (a, b)
+
+
 def test_hand_over_while_parked_and_back(mock_exporter):
     """A device parked by the quiet release can be handed over (kgs pmc release: nothing is
     held, the hand-over stands) and acquired back at once by the control plane, whatever
