@@ -102,8 +102,9 @@ def idle_power(ctx, load, exp, a) -> dict:
     # --mock: the orchestration on CPU (every rank, every barrier), against a constant
     # synthetic socket power — no power number of a mock run means anything
     probe = MockPowerProbe() if a.mock else PmfwProbe(load.pci_bdf(ctx.local_rank))
-    if probe.N is None:
-        return {"skipped": "no PMFW table probe"}
+    # every rank skips or none does: a rank leaving early would strand the others in a barrier
+    if not all(D.all_gather_object(ctx, probe.N is not None)):
+        return {"skipped": "no PMFW table probe on some rank"}
     if int(getattr(a, "idle_power_absent", 0) or 0):
         conds: tuple = ("session", "released", "parked", "absent")
         perms = [("session", "released", "absent", "parked"), ("released", "parked", "session", "absent"),
