@@ -274,10 +274,13 @@ CATALOG: tuple[Family, ...] = (
       "container_gpu_cu_seconds_total line rather than 0.", source="self"),
     F("kgs_pmc_parked", "gauge", "1 while the counter session is released because the GPU has been quiet for "
       "--pmc-quiet-release-s (no wave, no MFMA cycle): a programmed session and its READ queue keep an idle MI355X "
-      "out of its low-power state (+22.7 W per idle GPU, bench phase P).  Utilisation is billed from the PMFW GFX "
-      "busy meanwhile (no READ inflates it), and the counter-tier gauges are withheld; the session is re-acquired "
-      "as soon as one PMFW interval shows GFX busy.", source="self"),
+      "out of its low-power state (≈291 W against ≈258 W: +32 W per idle GPU, bench phase P).  Utilisation is "
+      "billed from the PMFW GFX busy meanwhile (no READ inflates it), and the counter-tier gauges are withheld; the "
+      "session is re-acquired as soon as one PMFW interval shows ≥ 10 % GFX busy or 100 ms of them ≥ 1 %.",
+      source="self"),
     F("kgs_pmc_parks_total", "counter", "Quiet releases of the counter session (kgs_pmc_parked).", source="self"),
+    F("kgs_pmc_parked_seconds_total", "counter", "Seconds the counter session has spent released by the quiet "
+      "release (kgs_pmc_parked): × ≈32 W is the energy the release saved an idle MI355X.", source="self"),
     F("kgs_pmc_dispatch_skips_total", "counter", "Sampler ticks that skipped their counter READ in a dispatch-bound "
       "stream.", source="self"),
     F("kgs_pmc_failed", "gauge", "1 while the counter tier's circuit breaker is open: --pmc-breaker-k consecutive "

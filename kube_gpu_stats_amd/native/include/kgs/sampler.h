@@ -303,6 +303,14 @@ struct DeviceState {
   std::atomic<int> pmc_dbound{0};            // dispatch-bound (pmc_cp_only_min): READs at pmc_dispatch_hz
   std::atomic<int> pmc_parked{0};            // session released after pmc_quiet_release_s of quiet
   std::atomic<uint64_t> pmc_parks{0};        // quiet releases
+  // Parked time (kgs_pmc_parked_seconds_total): the parks that ended, and the start of
+  // the current one (0: not parked) — one seqlocked pair, so a scrape never sees a park
+  // counted twice or not at all while it ends (writer: kgs-gpu<N>).
+  struct ParkTime {
+    int64_t ended_ns = 0;
+    int64_t since_ns = 0;
+  };
+  Seqlock<ParkTime> park_time;
   std::atomic<int> pmc_unpark_req{0};        // control plane: re-acquire a parked device now
   std::atomic<int64_t> pmc_unpark_lag_ns{-1};  // last re-acquire: mono time since the PMFW sample that showed busy
   std::atomic<uint64_t> pmc_dbound_skips{0};  // ticks that skipped their READ while dispatch-bound

@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include <cmath>
+#include <ctime>
 
 #include "kgs/exporter.h"
 #include "kgs/gpu_metrics.h"
@@ -13,6 +14,12 @@ namespace py = pybind11;
 using namespace kgs;
 
 namespace {
+
+int64_t mono_ns_now() {
+  timespec ts{};
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
 
 template <class T>
 T get(const py::dict& d, const char* k, T dflt) {
@@ -291,6 +298,12 @@ class PyExporter {
     o["pmc_dispatch_skips"] = st.pmc_dbound_skips.load();
     o["pmc_parked"] = st.pmc_parked.load();
     o["pmc_parks"] = st.pmc_parks.load();
+    {
+      DeviceState::ParkTime pt;
+      st.park_time.load(pt);
+      const int64_t cur = pt.since_ns > 0 ? std::max<int64_t>(0, mono_ns_now() - pt.since_ns) : 0;
+      o["pmc_parked_s"] = (pt.ended_ns + cur) * 1e-9;
+    }
     {
       const int64_t lag = st.pmc_unpark_lag_ns.load();
       o["pmc_unpark_lag_s"] = lag >= 0 ? py::cast(lag * 1e-9) : py::none();

@@ -772,6 +772,13 @@ void Exporter::render(std::string& out) {
     for (int d : ids) w.line_u("kgs_pmc_parked", dev_labels_[d], nullptr, static_cast<uint64_t>(S.state(d).pmc_parked.load()));
     w.head(KGS_METRIC_DOC("kgs_pmc_parks_total"));
     for (int d : ids) w.line_u("kgs_pmc_parks_total", dev_labels_[d], nullptr, S.state(d).pmc_parks.load());
+    w.head(KGS_METRIC_DOC("kgs_pmc_parked_seconds_total"));
+    for (int d : ids) {
+      DeviceState::ParkTime pt;  // never written: never parked
+      S.state(d).park_time.load(pt);
+      const int64_t cur = pt.since_ns > 0 ? std::max<int64_t>(0, mono_ns() - pt.since_ns) : 0;
+      w.line("kgs_pmc_parked_seconds_total", dev_labels_[d], nullptr, (pt.ended_ns + cur) * 1e-9);
+    }
     w.head(KGS_METRIC_DOC("kgs_pmc_dispatch_skips_total"));
     for (int d : ids) w.line_u("kgs_pmc_dispatch_skips_total", dev_labels_[d], nullptr, S.state(d).pmc_dbound_skips.load());
     w.head(KGS_METRIC_DOC("kgs_pmc_failed"));

@@ -616,6 +616,16 @@ void Sampler::run_pmc(Worker& w) {
     PmcSample last;
     if (st.pmc_latest.load(last)) pmc_base = last;
   };
+  // A park ended: its time joins the total (kgs_pmc_parked_seconds_total).
+  DeviceState::ParkTime pt;  // this thread's copy of st.park_time (carried over a pause / resume)
+  st.park_time.load(pt);
+  auto end_park = [&] {
+    if (pt.since_ns > 0) {
+      pt.ended_ns += mono_ns() - pt.since_ns;
+      pt.since_ns = 0;
+      st.park_time.store(pt);
+    }
+  };
   // Open the breaker: stop READing this device, retry after the backoff.
   auto trip = [&](int64_t now) {
     ++P.pmc_epoch;  // the counter integral stops here: the READ-immune util falls back to PMFW
@@ -652,6 +662,7 @@ void Sampler::run_pmc(Worker& w) {
       carry_base();
     }
     if (!want && st.pmc_parked.load(std::memory_order_relaxed)) {
+      end_park();
       st.pmc_parked.store(0);  // handed over while parked: nothing is held, the hand-over stands
       st.pmc_releases.fetch_add(1, std::memory_order_relaxed);
     }
@@ -695,6 +706,7 @@ void Sampler::run_pmc(Worker& w) {
         if (rc == 0) {
           ++P.pmc_epoch;
           st.pmc_on.store(1);
+          end_park();
           st.pmc_parked.store(0);
           started_at(now_c);
           src->set_fresh(dev, false);  // the released session was READ synchronously (quiet)
@@ -859,6 +871,8 @@ void Sampler::run_pmc(Worker& w) {
           park_ns = mono_ns();
           unpark_base_dt = -1;
           st.pmc_on.store(0);
+          pt.since_ns = park_ns;
+          st.park_time.store(pt);
           st.pmc_parked.store(1);
           st.pmc_parks.fetch_add(1, std::memory_order_relaxed);
           st.pmc_quiet.store(0, std::memory_order_relaxed);

@@ -980,11 +980,15 @@ def test_quiet_release_parks_the_session_and_bills_continuously(mock_exporter):
     time.sleep(0.5)
     a, r0, t0 = ex.integrals(0), ref.integrals(0), time.monotonic()
     parked_seen = on_seen = 0
+    parked_s = []  # kgs_pmc_parked_seconds_total as scraped: monotonic through every park / unpark
     while time.monotonic() - t0 < 6.0:
         i = ex.integrals(0)
         parked_seen |= i["pmc_parked"]
         on_seen |= i["pmc_on"] and not i["pmc_parked"]
+        parked_s.append(parse_text(ex.render())["kgs_pmc_parked_seconds_total"][0][1])
         time.sleep(0.05)
+    assert all(y >= x for x, y in zip(parked_s, parked_s[1:])), parked_s
+    assert 1.5 < parked_s[-1] - parked_s[0] < 4.5, parked_s  # most of each 1.5 s idle half
     b, r1 = ex.integrals(0), ref.integrals(0)
     assert parked_seen and on_seen
     assert b["pmc_parks"] - a["pmc_parks"] >= 2, b          # one per idle half
@@ -1024,6 +1028,7 @@ def test_a_stray_blip_does_not_unpark(mock_exporter):
     time.sleep(2.5)  # five blips
     b = ex.integrals(0)
     assert b["pmc_parked"] == 1 and b["pmc_parks"] == a["pmc_parks"], (a, b)
+    assert b["pmc_parked_s"] - a["pmc_parked_s"] == pytest.approx(2.5, abs=0.2), (a, b)  # kgs_pmc_parked_seconds_total
 
 
 @pytest.mark.parametrize("floor,wakes", [(2.0, True), (0.5, False)])
