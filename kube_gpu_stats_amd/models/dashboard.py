@@ -133,7 +133,8 @@ def build() -> dict:
                 (_dev("rate(kgs_pmc_samples_total[1m])"), "pmc gpu{{gpu}}"),
                 (_dev("kgs_pmc_quiet"), "quiet (idle READ rate) gpu{{gpu}}"),
                 (_dev("kgs_pmc_dispatch_bound"), "dispatch-bound (dispatch READ rate) gpu{{gpu}}"),
-                (_dev("kgs_pmc_parked"), "parked (session released while quiet) gpu{{gpu}}")], 0, y, w=8))
+                (_dev("kgs_pmc_parked"), "parked (session released while quiet) gpu{{gpu}}"),
+                (_dev("rate(kgs_pmc_parked_seconds_total[1h])"), "parked share, last hour gpu{{gpu}}")], 0, y, w=8))
     add(_panel(0, "Scrape render time / HTTP connections",
                [("kgs_scrape_render_last_seconds", "render s {{instance}}"),
                 ("kgs_http_connections", "connections {{instance}}"),
