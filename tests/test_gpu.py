@@ -1871,6 +1871,7 @@ def test_quiet_release_parks_and_wakes_on_hardware(torch_dev):
     d = lambda f: one(m1, f) - one(m0, f)  # noqa: E731
     row = {"parked_before_load": parked, "parks": one(m1, "kgs_pmc_parks_total"),
            "enabled_after_load": one(m1, "kgs_pmc_enabled"), "parked_after_load": one(m1, "kgs_pmc_parked"),
+           "parked_s": one(m1, "kgs_pmc_parked_seconds_total"),
            "duty_gpu_pct": round(100 * gpu_s / win, 2),
            "busy_counter_pct": round(100 * d("container_gpu_busy_seconds_total") / win, 2)}
     row["error_pts"] = round(row["busy_counter_pct"] - row["duty_gpu_pct"], 2)
@@ -1878,6 +1879,7 @@ def test_quiet_release_parks_and_wakes_on_hardware(torch_dev):
     print(json.dumps(row))
     assert parked == 1 and row["parks"] >= 1, row
     assert row["enabled_after_load"] == 1 and row["parked_after_load"] == 0, row   # re-acquired under the load
+    assert row["parked_s"] is not None and row["parked_s"] > 0, row               # the park's time, counted
     bound("quiet_release_error_pts", abs(row["error_pts"]), hi=3.0, ctx=row)
 
 
