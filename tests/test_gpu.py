@@ -644,8 +644,10 @@ def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
         assert [r[:4] for r in rows] == [["gpu-node-1", "ml", "train-0", 1]], rows
         # the load loop pauses for every scrape + ingest (≈ms each, 4 per second), and a 1 s
         # rate() range of a counter that moves in ≈20 ms PMFW steps is good to a few per cent
-        # 90-101 across boxes (a 1 s rate() extrapolated over ≈20 ms PMFW steps): re-based 80 → 65
-        bound("f5_fixed_report_util", rows[0][4], lo=65, ctx=rows)
+        # 82.7-101 across seven boxes (a 1 s rate() extrapolated over ≈20 ms PMFW steps, the
+        # load paused for each scrape): re-based 80 → 65 → 45, twice that spread below the
+        # lowest — still far from an idle GPU's 0
+        bound("f5_fixed_report_util", rows[0][4], lo=45, ctx=rows)
         # --energy: the pod's GPU energy over the 2 s window, as mean watts ≈ the socket power
         kwh = G.pod_energy_kwh(PromClient(url), end - 2, end, 1)
         watts = kwh[("gpu-node-1", "ml", "train-0")] * 3.6e6 / 2
@@ -1720,12 +1722,14 @@ def test_shipped_daemonset_config_bills_the_kernels_duty(torch_dev, tmp_path):
         # re-based 95 → 93 (profiles/gpu_test_margins.md: 97.98-99.93 over the current tree's runs)
         bound(f"shipped_saturated_load_only_busy_pct[{tag}]", sat["load_only_busy_pct"], lo=93.0, ctx=sat)
         # the report is Prometheus' extrapolated rate() over an 8 s range of a counter that
-        # advances in 100 ms PMFW steps at 10 Hz: held to ±4, the exact counter to ±3
+        # advances in 100 ms PMFW steps at 10 Hz: held to ±4.5 (0.12-1.47 over eleven runs,
+        # re-based from 4 for twice that spread), the exact counter to ±3
         bound(f"shipped_saturated_abs_err_pts[{tag}]", abs(sat["error_pts"]), hi=3.0, ctx=sat)
-        bound(f"shipped_saturated_report_abs_err_pts[{tag}]", abs(sat["report_pct"] - sat["duty_gpu_pct"]), hi=4.0, ctx=sat)
+        bound(f"shipped_saturated_report_abs_err_pts[{tag}]", abs(sat["report_pct"] - sat["duty_gpu_pct"]), hi=4.5, ctx=sat)
         for name in ("burst_1ms_every_5ms", "burst_0.2ms_every_1ms"):
             r = rows[f"{tag}/{name}"]
-            bound(f"shipped_abs_err_pts[{tag}/{name}]", abs(r["error_pts"]), hi=3.0, ctx=r)
+            # 0.00-1.12 points over eleven runs: 3.5 keeps twice that spread clear (was 3)
+            bound(f"shipped_abs_err_pts[{tag}/{name}]", abs(r["error_pts"]), hi=3.5, ctx=r)
             bound(f"shipped_report_abs_err_pts[{tag}/{name}]", abs(r["report_pct"] - r["duty_gpu_pct"]), hi=4.0, ctx=r)
             assert r["from_counters_s"] > 0.9 * r["window_s"], r
 
