@@ -116,8 +116,9 @@ struct SamplerConfig {
   // After the device has been quiet (no wave, no MFMA cycle) for this long, its counter
   // thread STOPs the session and destroys the READ queue; it re-acquires when the PMFW
   // table shows GFX busy again (kUnparkTablePct in one interval, or kUnparkBusyPct over
-  // kUnparkWindowS of table time), on a control-plane acquire, or when parking is
-  // switched off (this set to 0, or profiling mode).  In between the READ-immune
+  // kUnparkWindowS of table time), on a control-plane acquire, when parking is
+  // switched off (this set to 0, or profiling mode), or when no PMFW table has come for
+  // 1 s (nothing else would bill the GPU).  In between the READ-immune
   // utilisation is billed from the PMFW GFX busy — which no READ inflates while parked.
   // 0 = never (profiling mode never parks either).
   double pmc_quiet_release_s = 0.0;

@@ -679,10 +679,15 @@ void Sampler::run_pmc(Worker& w) {
                   !(pmc_idle_hz_.load(std::memory_order_relaxed) > 0);
       int64_t busy_ns = 0;
       GpuSample g;
+      // ... or the PMFW tier has gone silent (no table for 1 s): nothing would bill the GPU
+      // while parked, so the counters take over again.
+      const int64_t now_w = mono_ns();
+      const bool have_g = st.latest.load(g);
+      if (!wake && now_w - park_ns > 1000000000LL && (!have_g || now_w - g.mono_ns > 1000000000LL)) wake = true;
       // PMFW busy in one interval, or over a tumbling window of table time, from the first
       // table read after the release settled (the STOP and the queue teardown are CP work
       // of their own).
-      if (!wake && st.latest.load(g) && g.mono_ns > park_ns + 50000000LL && g.cum_dt_s > 0) {
+      if (!wake && have_g && g.mono_ns > park_ns + 50000000LL && g.cum_dt_s > 0) {
         if (g.gfx_busy_window_pct >= kUnparkTablePct) {
           wake = true;
           busy_ns = g.mono_ns;

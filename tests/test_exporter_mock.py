@@ -1054,6 +1054,19 @@ def test_a_trickle_unparks_over_100ms(mock_exporter, floor, wakes):
         assert b["pmc_parks"] == a["pmc_parks"] and b["pmc_parked"] == 1, (a, b)
 
 
+def test_a_parked_tier_wakes_when_the_pmfw_goes_silent(mock_exporter):
+    """While parked only the PMFW bills the GPU: with no PMFW table for 1 s (every read
+    failing here) the counter tier re-acquires rather than leave the GPU unbilled — and,
+    the mock GPU still quiet, parks again; with the PMFW reading, one park holds."""
+    kw = dict(n_gpus=1, hz=1000, pmc_source="mock", proc_every=0, link_every=0, pmc_idle_hz=100,
+              pmc_quiet_release_s=0.2)
+    silent = mock_exporter(mock={"util_base": 0, "util_amp": 0, "fail_rate": 1.0}, **kw)
+    ok = mock_exporter(mock={"util_base": 0, "util_amp": 0}, **kw)
+    time.sleep(3.5)
+    assert silent.integrals(0)["pmc_parks"] >= 2, silent.integrals(0)
+    assert ok.integrals(0)["pmc_parks"] == 1, ok.integrals(0)
+
+
 def test_hand_over_while_parked_and_back(mock_exporter):
     """A device parked by the quiet release can be handed over (kgs pmc release: nothing is
     held, the hand-over stands) and acquired back at once by the control plane, whatever
