@@ -570,6 +570,9 @@ void Sampler::run_pmc(Worker& w) {
   pin(dev, "kgs-gpu%d");
   const double hz = hz_.load();
   const int64_t period_ns = static_cast<int64_t>(1e9 / hz);
+  // A PMFW tier silent this long wakes a parked device: three of its periods, ≥ 1 s.
+  const double pmfw_rate = cfg_.pmfw_hz > 0 && cfg_.pmfw_hz < hz ? cfg_.pmfw_hz : hz;
+  const int64_t pmfw_silent_ns = std::max<int64_t>(1000000000LL, static_cast<int64_t>(3e9 / pmfw_rate));
   auto gone = [&w] { return w.abandoned.load(std::memory_order_acquire); };
   Integrals P;
   uint64_t pmc_seq = 0;
@@ -679,11 +682,11 @@ void Sampler::run_pmc(Worker& w) {
                   !(pmc_idle_hz_.load(std::memory_order_relaxed) > 0);
       int64_t busy_ns = 0;
       GpuSample g;
-      // ... or the PMFW tier has gone silent (no table for 1 s): nothing would bill the GPU
-      // while parked, so the counters take over again.
+      // ... or the PMFW tier has gone silent (no table for three of its periods, ≥ 1 s):
+      // nothing would bill the GPU while parked, so the counters take over again.
       const int64_t now_w = mono_ns();
       const bool have_g = st.latest.load(g);
-      if (!wake && now_w - park_ns > 1000000000LL && (!have_g || now_w - g.mono_ns > 1000000000LL)) wake = true;
+      if (!wake && now_w - park_ns > pmfw_silent_ns && (!have_g || now_w - g.mono_ns > pmfw_silent_ns)) wake = true;
       // PMFW busy in one interval, or over a tumbling window of table time, from the first
       // table read after the release settled (the STOP and the queue teardown are CP work
       // of their own).
