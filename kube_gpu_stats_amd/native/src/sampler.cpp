@@ -1,5 +1,6 @@
 // Per-GPU sampler threads.  See sampler.h.
 #include "kgs/sampler.h"
+#include "kgs/unpark.h"
 
 #include <poll.h>
 #include <pthread.h>
@@ -606,7 +607,7 @@ void Sampler::run_pmc(Worker& w) {
   int64_t quiet_run_ns = 0;          // start of the current run of quiet drains (quiet release)
   int64_t park_ns = 0;               // when the session was last released for quiet
   int64_t unpark_retry_at_ns = 0;    // after a failed re-acquire of a parked device
-  double unpark_base_dt = -1, unpark_base_gfx = 0;  // start of the parked busy window
+  UnparkDetector unpark(kUnparkTablePct, kUnparkBusyPct, kUnparkWindowS);  // kgs/unpark.h
   // A fresh START restarts every count at 0: the interval from START to the first
   // READ is then counted exactly (acquire → first READ was dropped).
   auto started_at = [&](int64_t t) {
@@ -680,33 +681,12 @@ void Sampler::run_pmc(Worker& w) {
       bool wake = st.pmc_unpark_req.exchange(0, std::memory_order_relaxed) != 0 ||
                   !(pmc_quiet_release_s_.load(std::memory_order_relaxed) > 0) ||
                   !(pmc_idle_hz_.load(std::memory_order_relaxed) > 0);
+      // ... or the PMFW shows work again, or has gone silent for three of its periods
+      // (≥ 1 s: nothing would bill the GPU while parked) — kgs/unpark.h.
       int64_t busy_ns = 0;
       GpuSample g;
-      // ... or the PMFW tier has gone silent (no table for three of its periods, ≥ 1 s):
-      // nothing would bill the GPU while parked, so the counters take over again.
-      const int64_t now_w = mono_ns();
       const bool have_g = st.latest.load(g);
-      if (!wake && now_w - park_ns > pmfw_silent_ns && (!have_g || now_w - g.mono_ns > pmfw_silent_ns)) wake = true;
-      // PMFW busy in one interval, or over a tumbling window of table time, from the first
-      // table read after the release settled (the STOP and the queue teardown are CP work
-      // of their own).
-      if (!wake && have_g && g.mono_ns > park_ns + 50000000LL && g.cum_dt_s > 0) {
-        if (g.gfx_busy_window_pct >= kUnparkTablePct) {
-          wake = true;
-          busy_ns = g.mono_ns;
-        } else if (unpark_base_dt < 0 || g.cum_dt_s < unpark_base_dt) {
-          unpark_base_dt = g.cum_dt_s;
-          unpark_base_gfx = g.cum_gfx_s;
-        } else if (g.cum_dt_s - unpark_base_dt >= kUnparkWindowS) {
-          const double pct = 100.0 * (g.cum_gfx_s - unpark_base_gfx) / (g.cum_dt_s - unpark_base_dt);
-          if (pct >= kUnparkBusyPct) {
-            wake = true;
-            busy_ns = g.mono_ns;
-          }
-          unpark_base_dt = g.cum_dt_s;
-          unpark_base_gfx = g.cum_gfx_s;
-        }
-      }
+      if (!wake) wake = unpark.poll(mono_ns(), have_g ? &g : nullptr, pmfw_silent_ns, &busy_ns);
       if (wake) {
         const int rc = src->acquire(dev);
         if (gone()) return;
@@ -877,7 +857,7 @@ void Sampler::run_pmc(Worker& w) {
           src->reset(dev);
           if (gone()) return;
           park_ns = mono_ns();
-          unpark_base_dt = -1;
+          unpark.parked(park_ns);
           st.pmc_on.store(0);
           pt.since_ns = park_ns;
           st.park_time.store(pt);

@@ -57,6 +57,7 @@
 #include "kgs/pmc.h"
 #include "kgs/sampler.h"
 #include "kgs/seqlock.h"
+#include "kgs/unpark.h"
 #include "kgs/util_estimator.h"
 
 using namespace kgs;
@@ -1198,7 +1199,58 @@ static void test_kfd_procs_concurrent() {
   std::printf("kfd procs concurrent ok\n");
 }
 
+// The parked tier's wake-up (kgs/unpark.h) on synthetic PMFW tables every 20 ms: a stray
+// 0.2 ms blip (one table at 1 %) does not wake it, a table at ≥ 10 % does at once, a
+// trickle of 2 % does within one 100 ms window, 0.5 % never, tables read during the
+// 50 ms settle are skipped, and a PMFW that stops wakes it after `silent`.
+static void test_unpark_detector() {
+  const int64_t ms = 1000000;
+  const int64_t silent = 1000 * ms;
+  auto run = [&](auto pct_at, int64_t stop_at_ms, int64_t* woke_at_ms) {
+    UnparkDetector u(kUnparkTablePct, kUnparkBusyPct, kUnparkWindowS);
+    const int64_t park = 1000 * ms;
+    u.parked(park);
+    GpuSample g;
+    double cum_gfx = 0, cum_dt = 10.0;
+    bool have = false;
+    for (int64_t t = park; t < park + 3000 * ms; t += 5 * ms) {
+      const int64_t rel = (t - park) / ms;
+      if (rel % 20 == 0 && rel < stop_at_ms) {  // a new table every 20 ms
+        const double pct = pct_at(rel);
+        cum_gfx += pct * 0.01 * 0.02;
+        cum_dt += 0.02;
+        g.mono_ns = t;
+        g.gfx_busy_window_pct = static_cast<float>(pct);
+        g.cum_gfx_s = cum_gfx;
+        g.cum_dt_s = cum_dt;
+        have = true;
+      }
+      int64_t busy = 0;
+      if (u.poll(t, have ? &g : nullptr, silent, &busy)) {
+        *woke_at_ms = rel;
+        return busy;
+      }
+    }
+    *woke_at_ms = -1;
+    return int64_t{0};
+  };
+  int64_t at = 0;
+  run([](int64_t r) { return r == 500 ? 1.0 : 0.0; }, 1 << 30, &at);
+  CHECK(at == -1);                                       // one blip: stays parked
+  const int64_t busy = run([](int64_t r) { return r >= 400 ? 60.0 : 0.0; }, 1 << 30, &at);
+  CHECK(at == 400 && busy > 0);                          // a load: the first table wakes it
+  run([](int64_t r) { return r >= 20 ? 2.0 : 0.0; }, 1 << 30, &at);
+  CHECK(at > 0 && at <= 200);                            // a trickle: within a window or two
+  run([](int64_t) { return 0.5; }, 1 << 30, &at);
+  CHECK(at == -1);                                       // below 1 %: never
+  run([](int64_t r) { return r < 50 ? 80.0 : 0.0; }, 1 << 30, &at);
+  CHECK(at == -1);                                       // the park's own CP work: skipped
+  run([](int64_t) { return 0.0; }, 500, &at);
+  CHECK(at > 1480 && at <= 1490);                        // last table at 480 ms: silent 1 s later
+}
+
 int main() {
+  test_unpark_detector();
   test_kfd_procs_concurrent();
   test_dispatch_estimator();
   test_cp_only_work_is_not_read_only();
