@@ -59,6 +59,8 @@ for s in $STEPS; do
     soak) run soak 420 python -u tools/soak.py --seconds 240 --out "$OUT/soak.json" ;;
     rss) run rss 180 python -u tools/rss_probe.py --out "$OUT/rss_probe.json" ;;
     hsarss) run hsarss 300 python -u tools/hsa_rss_probe.py --out "$OUT/hsa_rss.json" ;;
+    soakpark) run soakpark 360 python -u tools/soak.py --seconds 180 --idle-s 4 --quiet-release-s 2 \
+                --out "$OUT/soakpark.json" ;;
     soak90) run soak90 240 python -u tools/soak.py --seconds 90 --out "$OUT/soak90.json" ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider ;;
     # round 4

@@ -12,6 +12,10 @@ READs, counter errors, breaker trips, sampler overruns, exporter RSS and CPU, re
 The run fails (exit 1) on any counter error, dropped READ, breaker trip or hung thread,
 or an RSS that grows by more than 8 MiB after the first minute.
 
+With ``--idle-s 4 --quiet-release-s 2`` every cycle's idle stretch parks the counter tier
+(the quiet release) and the next busy phase takes it back, under the same re-STARTs and
+hand-overs; the run then also fails unless it parked and woke every cycle or so.
+
     python tools/soak.py --seconds 240 --out gpurun_out/soak.json
 """
 from __future__ import annotations
@@ -68,6 +72,9 @@ def main() -> int:
     ap.add_argument("--window", type=float, default=10.0)
     ap.add_argument("--out", default="gpurun_out/soak.json")
     ap.add_argument("--mock", action="store_true", help="mock GPU and counters, no load (CPU rehearsal of the script)")
+    ap.add_argument("--idle-s", type=float, default=1.0, help="idle stretch of each load cycle")
+    ap.add_argument("--quiet-release-s", type=float, default=None,
+                    help="the exporter's --pmc-quiet-release-s (default: the exporter's own)")
     a = ap.parse_args()
 
     from kube_gpu_stats_amd.utils.scrape import Scraper, parse_text
@@ -94,7 +101,8 @@ def main() -> int:
     err = open(os.path.splitext(a.out)[0] + "_exporter.err", "w")  # a pipe nobody drains could block the exporter
     proc = subprocess.Popen([sys.executable, "-m", "kube_gpu_stats_amd.cli", "exporter", "--listen", "127.0.0.1:0",
                              "--hz", f"{a.hz:g}", *src, "--control-stdin", "--control-http",
-                             "--pmc-refresh-s", "20", "--window", "1"],
+                             "--pmc-refresh-s", "20", "--window", "1",
+                             *([] if a.quiet_release_s is None else ["--pmc-quiet-release-s", f"{a.quiet_release_s:g}"])],
                             cwd=REPO, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=err, text=True)
     windows: list[dict] = []
     fail: list[str] = []
@@ -107,7 +115,8 @@ def main() -> int:
         fams = ("kgs_pmc_samples_total", "kgs_samples_total", "kgs_pmc_publishes_total", "kgs_pmc_unlanded_total",
                 "kgs_pmc_errors_total", "kgs_pmc_breaker_trips_total", "kgs_sampler_overruns_total",
                 "kgs_pmc_refreshes_total", "kgs_pmc_releases_total", "kgs_scrape_render_seconds_total",
-                "kgs_scrapes_total", "kgs_sampler_thread_hung", "amdgpu_gpu_active_seconds_total")
+                "kgs_scrapes_total", "kgs_sampler_thread_hung", "amdgpu_gpu_active_seconds_total",
+                "kgs_pmc_parks_total", "kgs_pmc_parked_seconds_total")
         snap = lambda: {f: one(parse_text(sc.get()), f) for f in fams}  # noqa: E731
         t_start = time.time()
         w_t0, w_m0, w_cpu0, w_thr0 = t_start, snap(), cpu_s(proc.pid), thread_cpu(proc.pid)
@@ -117,7 +126,7 @@ def main() -> int:
         phase_t0, phase = t_start, 0
         while time.time() - t_start < a.seconds:
             now = time.time()
-            # load cycle: 2 s continuous, 2 s bursts with 20 ms gaps, 1 s idle
+            # load cycle: 2 s continuous, 2 s bursts with 20 ms gaps, --idle-s idle
             if phase == 0:
                 ls()
                 sync()
@@ -132,7 +141,7 @@ def main() -> int:
                     phase, phase_t0 = 2, time.time()
             else:
                 time.sleep(0.05)
-                if time.time() - phase_t0 >= 1.0:
+                if time.time() - phase_t0 >= a.idle_s:
                     phase, phase_t0 = 0, time.time()
             if now >= next_scrape:
                 sc.get()
@@ -154,6 +163,7 @@ def main() -> int:
                      "dropped": d["kgs_pmc_unlanded_total"], "pmc_errors": d["kgs_pmc_errors_total"],
                      "breaker_trips": d["kgs_pmc_breaker_trips_total"], "overruns": d["kgs_sampler_overruns_total"],
                      "refreshes": d["kgs_pmc_refreshes_total"], "handovers": d["kgs_pmc_releases_total"],
+                     "parks": d["kgs_pmc_parks_total"], "parked_share": round(d["kgs_pmc_parked_seconds_total"] / dt, 3),
                      "render_ms": round(1e3 * d["kgs_scrape_render_seconds_total"] / max(d["kgs_scrapes_total"], 1), 3),
                      "rss_mib": round(rss_mib(proc.pid), 1), "cpu_cores": round((c1 - w_cpu0) / dt, 4),
                      "thread_hung": m1["kgs_sampler_thread_hung"],
@@ -178,6 +188,12 @@ def main() -> int:
         for k in ("dropped", "pmc_errors", "breaker_trips", "thread_hung"):
             if w[k]:
                 fail.append(f"t={w['t']}: {k}={w[k]}")
+    # a park per cycle expected (not on --mock: its GPU never goes quiet)
+    if a.quiet_release_s and a.idle_s > a.quiet_release_s + 0.5 and not a.mock:
+        cycles = a.seconds / (4.0 + a.idle_s)
+        parks = sum(w["parks"] for w in windows)
+        if parks < 0.5 * cycles:
+            fail.append(f"{parks:g} parks in {cycles:.0f} cycles whose idle stretch outlasts the quiet release")
     after = [w["rss_mib"] for w in windows if w["t"] >= 60]
     if after and max(after) - after[0] > 8.0:
         fail.append(f"RSS grew {max(after) - after[0]:.1f} MiB after the first minute")
@@ -188,6 +204,7 @@ def main() -> int:
            "pmc_samples_per_s_min_max": [min(w["pmc_samples_per_s"] for w in full),
                                          max(w["pmc_samples_per_s"] for w in full)] if full else None,
            "refreshes": sum(w["refreshes"] for w in windows), "handovers": sum(w["handovers"] for w in windows),
+           "parks": sum(w["parks"] for w in windows),
            "cpu_cores_mean": round(sum(w["cpu_cores"] for w in windows) / len(windows), 4) if windows else None}
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
