@@ -121,6 +121,7 @@ for s in $STEPS; do
                 --quiet-s 0 --component-s 0 --util-s 0 --idle-power-s 64 --idle-power-rounds 8 --idle-power-absent 1 \
                 --out "$OUT/powerabs.json" ;;
     tierprobe) run idle_tier 600 python -u tools/idle_tier_probe.py --out "$OUT/idle_tier_probe.json" ;;
+    tierprobe60) run idle_tier60 840 python -u tools/idle_tier_probe.py --secs 60 --out "$OUT/idle_tier_probe60.json" ;;
     useeds) for s in 1 2 3 4 5 6 7 8; do
               run useed_$s 240 python -u bench.py --steps 3 --warmup 1 --rounds 0 --burst-s 0 --capacity-hz "" \
                 --quiet-s 0 --component-s 0 --idle-power-s 0 --util-hz 10 --util-seed $s --out "$OUT/useed_$s.json" || break
