@@ -25,7 +25,7 @@ from ..utils.scrape import Scraper, parse_text
 COLS = [("gpu", "GPU", 3), ("pod", "POD", 18), ("gfx", "GFX%", 5), ("mfma", "MFMA%", 5), ("vmem", "VMEM%", 5),
         ("umc", "UMC%", 5), ("hbm_gb", "HBM_GB", 7), ("hbm_pct", "HBM%", 5), ("power_w", "PWR_W", 6),
         ("energy_w", "AVG_W", 6), ("temp_c", "TEMP", 4), ("clk_mhz", "MHZ", 5), ("xgmi_gbps", "XGMI_GB/s", 9),
-        ("pcie_gbps", "PCIE_GB/s", 9), ("ppt_pct", "PVIOL%", 6), ("xcd_mfma", "MFMA%_PER_XCD", 31)]
+        ("pcie_gbps", "PCIE_GB/s", 9), ("ppt_pct", "PVIOL%", 6), ("pmc", "PMC", 5), ("xcd_mfma", "MFMA%_PER_XCD", 31)]
 BURST_COLS = [("mfma_min", "MFMA_MIN", 8), ("mfma_max", "MFMA_MAX", 8), ("bursts", "BURSTS", 6),
               ("duty", "DUTY%", 5), ("drains", "DRAINS", 6)]
 
@@ -100,6 +100,27 @@ def _xcd_split(m: dict, fam: str) -> dict[str, str]:
     return {g: "/".join(f"{x[k]:.0f}" for k in sorted(x)) for g, x in per.items()}
 
 
+def pmc_state(m: dict) -> dict[str, str]:
+    """The counter tier per GPU, as one word: ``fail`` (breaker open), ``park`` (released
+    by the quiet release), ``off`` (handed over / not configured), ``quiet`` (no wave:
+    READ at the idle rate), ``dbnd`` (dispatch-bound: READ at the dispatch rate), ``on``."""
+    out = {}
+    for g, on in _by_gpu(m, "kgs_pmc_enabled").items():
+        if _by_gpu(m, "kgs_pmc_failed").get(g):
+            out[g] = "fail"
+        elif _by_gpu(m, "kgs_pmc_parked").get(g):
+            out[g] = "park"
+        elif not on:
+            out[g] = "off"
+        elif _by_gpu(m, "kgs_pmc_quiet").get(g):
+            out[g] = "quiet"
+        elif _by_gpu(m, "kgs_pmc_dispatch_bound").get(g):
+            out[g] = "dbnd"
+        else:
+            out[g] = "on"
+    return out
+
+
 def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
     """One row per GPU from a scrape (and the previous one, for rates)."""
     gfx = _by_gpu(cur, "amdgpu_gfx_busy_percent")
@@ -121,6 +142,7 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
     pxgmi = _sum_by_gpu(prev, "amdgpu_xgmi_read_bytes_total", "amdgpu_xgmi_write_bytes_total") if prev else {}
     pods = _pods(cur)
     xcd = _xcd_split(cur, "amdgpu_mfma_util_xcc_percent")
+    pmc = pmc_state(cur)
     gpus = sorted(set(gfx) | set(used) | set(power), key=lambda g: int(g) if g.isdigit() else 0)
     rows = []
     for g in gpus:
@@ -128,7 +150,7 @@ def rows_from(prev: dict | None, cur: dict, dt: float) -> list[dict]:
              "umc": umc.get(g), "hbm_gb": used[g] / 1e9 if g in used else None,
              "hbm_pct": 100.0 * used[g] / total[g] if total.get(g) and g in used else None,
              "power_w": power.get(g), "temp_c": temp.get(g), "clk_mhz": clk.get(g), "energy_w": None,
-             "xgmi_gbps": None, "pcie_gbps": None, "ppt_pct": None, "xcd_mfma": xcd.get(g)}
+             "xgmi_gbps": None, "pcie_gbps": None, "ppt_pct": None, "pmc": pmc.get(g, "-"), "xcd_mfma": xcd.get(g)}
         if dt > 0 and g in penergy and g in energy and energy[g] >= penergy[g]:
             r["energy_w"] = (energy[g] - penergy[g]) / dt
         if dt > 0 and g in pxgmi and g in xgmi and xgmi[g] >= pxgmi[g]:

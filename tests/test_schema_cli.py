@@ -206,6 +206,7 @@ def test_cli_dmon_rows_and_counter_bursts(mock_exporter):
         assert 55 <= r["mfma_min"] <= r["mfma_max"] <= 65             # mock: MFMA busy 60 % of active cycles
         assert [55 <= float(x) <= 65 for x in r["xcd_mfma"].split("/")] == [True] * 8  # per-XCD split
         assert 15 <= r["duty"] <= 85 and r["bursts"] is not None     # mock GPU active 50 ± 30 %
+        assert r["pmc"] == "on"                                      # the counter tier, one word
     buf = io.StringIO()
     a = dmon.build_parser().parse_args([f"http://127.0.0.1:{ex.port}", "--interval", "0.1", "--count", "2"])
     dmon.run(a, out=buf)
@@ -270,3 +271,17 @@ def test_every_subcommand_help_renders(sub):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "usage:" in r.stdout
+
+
+def test_dmon_pmc_state_word():
+    """`kgs dmon`'s PMC column: the counter tier per GPU in one word, the breaker first."""
+    from kube_gpu_stats_amd.reports.dmon import pmc_state
+
+    def fam(*vals):
+        return [({"gpu": str(i)}, v) for i, v in enumerate(vals)]
+
+    m = {"kgs_pmc_enabled": fam(1, 1, 1, 0, 0, 0), "kgs_pmc_quiet": fam(0, 1, 0, 0, 0, 0),
+         "kgs_pmc_dispatch_bound": fam(0, 0, 1, 0, 0, 0), "kgs_pmc_parked": fam(0, 0, 0, 1, 0, 0),
+         "kgs_pmc_failed": fam(0, 0, 0, 0, 0, 1)}
+    assert pmc_state(m) == {"0": "on", "1": "quiet", "2": "dbnd", "3": "park", "4": "off", "5": "fail"}
+    assert pmc_state({}) == {}
