@@ -2132,7 +2132,8 @@ def test_lite_reads_match_full_reads_on_hardware(N, torch_dev):
     assert f["lite"].startswith("lite=0") and l["lite"].startswith("lite=1:"), rows
     assert int(l["lite"].split(":")[1]) > 1000 and not l["full_ib"], rows  # lite READs did run
     bound("lite_full_mfma_busy_pct", f["mfma_busy_pct"], lo=50, ctx=rows)
-    bound("lite_vs_full_mfma_busy_pts", abs(l["mfma_busy_pct"] - f["mfma_busy_pct"]), hi=3, ctx=rows)
+    # 0.01-1.05 points over eleven runs (r6v the widest): 3.5 keeps twice that spread clear (was 3)
+    bound("lite_vs_full_mfma_busy_pts", abs(l["mfma_busy_pct"] - f["mfma_busy_pct"]), hi=3.5, ctx=rows)
     bound("lite_vs_full_mfma_util_pts", abs(l["mfma_util_pct"] - f["mfma_util_pct"]), hi=3, ctx=rows)
     # each mode's dispatch integral against its own run's event-timed kernel duty (the two
     # runs' duty differs by the host syncs between groups of kernels)
