@@ -89,7 +89,8 @@ def idle_power(ctx, load, exp, a) -> dict:
     each block now starts --idle-power-settle-s after the switch.  A released GPU also
     leaves the low level by itself now and then (r6i: 2 of 12 blocks, each with a
     0.005 % PMFW busy blip that is not the exporter's), so the level difference is the
-    median of the paired second halves (``*_minus_released_median_w``)."""
+    median of the paired second halves (``*_minus_released_median_w``), and the floor —
+    each condition's lowest settled block — against released's (``*_floor_w``)."""
     secs = float(getattr(a, "idle_power_s", 0.0) or 0.0)
     rounds = int(getattr(a, "idle_power_rounds", 6) or 0)
     if secs <= 0 or rounds <= 0:
@@ -189,6 +190,15 @@ def idle_power(ctx, load, exp, a) -> dict:
                     one[f"{cond}_minus_released_{tag}w"] = [round(m, 3), round(ci, 3)]
                     if tag:  # the level: robust to a block caught in a stray excursion (r6i)
                         one[f"{cond}_minus_released_median_w"] = round(statistics.median(d), 3)
+        # ... and the floor: each condition's lowest settled block.  The platform's own
+        # excursions (≈ once per 30 s, r6l / r6t) only ever raise a block, and caught half
+        # the parked blocks in r6x, where even the median moved; the floor is the level a
+        # condition holds when nothing else wakes the GPU.
+        floor = {c: min((rd[c]["late_w"] for rd in rk if rd.get(c) and rd[c].get("late_w") is not None),
+                        default=None) for c in conds}
+        for cond in (c for c in conds if c != "released"):
+            if floor.get(cond) is not None and floor.get("released") is not None:
+                one[f"{cond}_minus_released_floor_w"] = round(floor[cond] - floor["released"], 3)
         per_rank.append(one)
     out = {"secs_per_condition": secs, "rounds": rounds, "block_s": round(block, 2), "settle_s": settle,
            "parked_reached": parked_ok,
@@ -209,8 +219,8 @@ def idle_power(ctx, load, exp, a) -> dict:
             vals = [p[k] for p in per_rank if k in p]
             if vals:
                 out[k] = [round(sum(v[0] for v in vals) / len(vals), 3), round(max(v[1] for v in vals), 3)]
-        k = f"{cond}_minus_released_median_w"
-        vals = [p[k] for p in per_rank if k in p]
-        if vals:
-            out[k] = round(statistics.median(vals), 3)
+        for k in (f"{cond}_minus_released_median_w", f"{cond}_minus_released_floor_w"):
+            vals = [p[k] for p in per_rank if k in p]
+            if vals:
+                out[k] = round(statistics.median(vals), 3)
     return out

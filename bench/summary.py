@@ -79,7 +79,9 @@ def summarize(res: dict) -> dict:
                                            "parked": ip.get("parked_minus_released_w"),
                                            "released": (ip["per_rank"][0] or {}).get("released_w"),
                                            "median": [ip.get("session_minus_released_median_w"),
-                                                      ip.get("parked_minus_released_median_w")]}
+                                                      ip.get("parked_minus_released_median_w")],
+                                           "floor": [ip.get("session_minus_released_floor_w"),
+                                                     ip.get("parked_minus_released_floor_w")]}
     br = (res.get("burst_resolution") or {}).get("per_gpu") or {}
     if br:
         out["bursts_resolved"] = [sum(v.get("segments", 0) for v in br.values()), sum(v.get("launched", 0) for v in br.values())]
