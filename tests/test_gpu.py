@@ -904,6 +904,16 @@ def test_dispatch_bound_rate_at_default_flags(torch_dev):
         ready = json.loads(proc.stdout.readline())
         assert ready["event"] == "ready" and ready["pmc"] == "aqlprofile", ready
         sc = Scraper("127.0.0.1", ready["port"])
+        # "ready" can come before the counter tier's first drains: the first phase's base
+        # scrape needs every family it subtracts (r6y: one box scraped before they existed)
+        fams = ("kgs_pmc_samples_total", "kgs_pmc_dispatch_skips_total", "amdgpu_dispatch_busy_seconds_total",
+                "amdgpu_gpu_active_seconds_total")
+        t_wait = time.time()
+        while time.time() - t_wait < 15:
+            m = parse_text(sc.get())
+            if all(one(m, f) is not None for f in fams) and one(m, "kgs_pmc_samples_total") > 0:
+                break
+            time.sleep(0.05)
 
         def phase(name, run, secs=1.5):
             m0 = parse_text(sc.get())
