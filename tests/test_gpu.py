@@ -652,7 +652,9 @@ def test_f5_slice_static_owner_to_report(torch_dev, tmp_path):
         kwh = G.pod_energy_kwh(PromClient(url), end - 2, end, 1)
         watts = kwh[("gpu-node-1", "ml", "train-0")] * 3.6e6 / 2
         pw = m["amdgpu_power_watts"][0][1]
-        bound("f5_pod_watts", watts, lo=300, hi=1600, ctx=pw)
+        # 1217-1396 W over thirteen runs (a 2 s energy rate() under the MFMA load): the upper
+        # bound 1600 → 1800 keeps twice that spread clear; it is a units check, not a power cap
+        bound("f5_pod_watts", watts, lo=300, hi=1800, ctx=pw)
         bound("f5_pod_watts_over_power", watts / pw, lo=0.75, hi=1.25, ctx=(watts, pw))
         import io
 
