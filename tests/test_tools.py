@@ -151,3 +151,15 @@ def test_tools_readme_lists_every_remaining_file():
              and not f.endswith(".pyc")]
     missing = [f for f in files if f"`{f}`" not in text and f"`{f} " not in text]
     assert not missing, missing
+
+
+def test_gpu_margins_reads_runs_in_the_order_they_were_taken():
+    """The bounds in force come from the last margins.jsonl read: run tags go r6y, r6z,
+    r6aa, r6ab (spreadsheet columns), rounds in order."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import gpu_margins as G
+
+    paths = [os.path.join(G.PROFILES, *p.split("/"), "margins.jsonl")
+             for p in ("r6/r6ab", "r6/r6z", "r5/r5an", "r6/r6aa", "r6/r6b", "r6/r6y")]
+    got = [G.run_dir(p) for p in sorted(paths, key=G.run_order)]
+    assert got == ["r5/r5an", "r6/r6b", "r6/r6y", "r6/r6z", "r6/r6aa", "r6/r6ab"], got

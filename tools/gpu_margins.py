@@ -159,13 +159,23 @@ def run_dir(path: str) -> str:
     return "/".join(rel[:2]) if len(rel) > 2 else rel[0]
 
 
+def run_order(path: str) -> tuple:
+    """Runs in the order they were taken: rN, then the tag as a spreadsheet column
+    (r6z before r6aa), so the last margins.jsonl read holds the newest bounds."""
+    parts = run_dir(path).split("/")
+    rnd = parts[0][1:] if parts[0][:1] == "r" else ""
+    tag = parts[1] if len(parts) > 1 else ""
+    suffix = tag[len(parts[0]):] if tag.startswith(parts[0]) else tag
+    return (int(rnd) if rnd.isdigit() else 0, len(suffix), suffix, path)
+
+
 def collect(root: str = PROFILES) -> tuple[dict, dict]:
     """({(test, q): {run: value}}, {(test, q): (lo, hi)} — the newest bound)."""
     obs: dict = {}
     bounds: dict = {}
     test_of: dict = {}
     with_margins = set()
-    for path in sorted(glob.glob(os.path.join(root, "**", "margins.jsonl"), recursive=True)):
+    for path in sorted(glob.glob(os.path.join(root, "**", "margins.jsonl"), recursive=True), key=run_order):
         run = run_dir(path)
         if not current(run):
             continue
