@@ -854,7 +854,9 @@ def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
     bound("idle_profiling_pmfw_busy_pct", p["pmfw_gfx_busy_pct"], lo=80, ctx=p)   # the effect the idle rate removes
     bound("idle_profiling_active_pct", p["gpu_active_pct"], hi=2, ctx=p)          # ... which SPI busy does not see
     bound("loaded_reads_per_s", ld["reads_per_s"], lo=7000, ctx=ld)  # a loaded GPU gets every tick
-    bound("loaded_active_pct", ld["gpu_active_pct"], lo=80, ctx=ld)
+    # 91.0-96.6 % over seventeen runs (the MFMA load's SPI share varies by box): 78 keeps
+    # twice that spread below the lowest (was 80)
+    bound("loaded_active_pct", ld["gpu_active_pct"], lo=78, ctx=ld)
     bound("loaded_mfma_util_pct", ld["mfma_util_pct"], lo=50, ctx=ld)
     # batched publication (--pmc-batch 8, ≤ 1 ms): at 8 kHz about one READ in 8 writes the
     # L2 back; the quiet GPU's synchronous 100 Hz READs each do
