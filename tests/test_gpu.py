@@ -767,8 +767,9 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev, batch):
     _keep("burst_resolution.json" if batch == 1 else f"burst_resolution_batch{batch}.json", json.dumps(summary, indent=1))
     print(json.dumps({k: v for k, v in summary.items() if k != "first_50ms"}))
     bound(f"burst_drain_rate_hz[batch{batch}]", summary["drain_rate_hz"], lo=7000, ctx=summary)
+    # 0-3 over seventeen runs (r6ae the first above 0): max(9, 7 %) keeps twice that clear
     bound(f"burst_segments_minus_launched[batch{batch}]", abs(len(segs) - len(bursts)),
-          hi=max(3, 0.05 * len(bursts)), ctx=summary)
+          hi=max(9, 0.07 * len(bursts)), ctx=summary)
     bound(f"burst_seg_len_abs_err_ms[batch{batch}]", abs(seg_len - host_len), hi=0.35 * host_len + 0.25,
           ctx=summary)  # ±2 drains of 125 µs + launch/sync jitter
     bound(f"burst_share_min[batch{batch}]", min(sh), hi=5, ctx=summary)
@@ -776,8 +777,9 @@ def test_counter_stream_resolves_sub_pmfw_bursts(torch_dev, batch):
     bound(f"burst_duty_abs_err[batch{batch}]", abs(summary["duty_counters"] - host_duty), hi=0.08, ctx=summary)
     assert len(pm_in) >= 10, summary                  # ≈50 tables/s
     # profiling mode: PMFW reads the READs as work — far above the ≈20 % true duty
-    # (r2q: 99.6-100; r2at: min 69.5 on a box draining at 7.65 kHz)
-    bound(f"burst_pmfw_busy_min_profiling[batch{batch}]", min(pm_in), lo=50, ctx=summary)
+    # (r2q: 99.6-100; r2at: min 69.5 on a box draining at 7.65 kHz; r6ae 78.05 among
+    # seventeen runs of 98-100): 30, twice that spread below, still above the duty
+    bound(f"burst_pmfw_busy_min_profiling[batch{batch}]", min(pm_in), lo=30, ctx=summary)
 
 
 def test_exporter_does_not_make_an_idle_gpu_look_busy(torch_dev):
